@@ -1,0 +1,359 @@
+"""Python view of the native device/topology library (N3/N4/N6).
+
+``libamdgpu_topo.so`` (``native/topology``) enumerates MI355X GPUs from KFD /
+PCI / DRM sysfs, collects amd-smi metrics and watches health events.  This
+module turns its C structs into dataclasses for the control plane.  Every
+function takes ``root`` so it runs unchanged against captured or synthetic
+sysfs trees (``tests/fakesys.py``) - the MI355X counterpart of the NVML
+queries behind ``nvidia-smi`` (/root/reference/README.md:152,158-167).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import asdict, dataclass, field
+
+from .. import native
+
+LIB = "libamdgpu_topo.so"
+LINK_PCIE = 2
+LINK_XGMI = 11
+
+
+class _Gpu(ctypes.Structure):
+    _fields_ = [
+        ("kfd_node", ctypes.c_int32),
+        ("gpu_id", ctypes.c_uint32),
+        ("gfx_target_version", ctypes.c_uint32),
+        ("arch", ctypes.c_char * 16),
+        ("simd_count", ctypes.c_uint32),
+        ("simd_per_cu", ctypes.c_uint32),
+        ("cu_count", ctypes.c_uint32),
+        ("num_xcc", ctypes.c_uint32),
+        ("max_waves_per_simd", ctypes.c_uint32),
+        ("wave_front_size", ctypes.c_uint32),
+        ("lds_size_kib", ctypes.c_uint32),
+        ("max_engine_clk_mhz", ctypes.c_uint32),
+        ("vram_bytes", ctypes.c_uint64),
+        ("drm_render_minor", ctypes.c_uint32),
+        ("domain", ctypes.c_uint32),
+        ("location_id", ctypes.c_uint32),
+        ("bdf", ctypes.c_char * 16),
+        ("vendor_id", ctypes.c_uint32),
+        ("device_id", ctypes.c_uint32),
+        ("unique_id", ctypes.c_uint64),
+        ("hive_id", ctypes.c_uint64),
+        ("num_xgmi_links", ctypes.c_uint32),
+        ("numa_node", ctypes.c_int32),
+        ("physical_index", ctypes.c_int32),
+        ("partition_index", ctypes.c_int32),
+        ("partition_count", ctypes.c_int32),
+        ("compute_partition", ctypes.c_char * 8),
+        ("memory_partition", ctypes.c_char * 8),
+    ]
+
+
+class _Link(ctypes.Structure):
+    _fields_ = [
+        ("from_gpu", ctypes.c_int32),
+        ("to_gpu", ctypes.c_int32),
+        ("type", ctypes.c_uint32),
+        ("weight", ctypes.c_uint32),
+        ("min_bandwidth_mbps", ctypes.c_uint32),
+        ("max_bandwidth_mbps", ctypes.c_uint32),
+    ]
+
+
+class _Metrics(ctypes.Structure):
+    _fields_ = [
+        ("index", ctypes.c_int32),
+        ("bdf", ctypes.c_char * 16),
+        ("uuid", ctypes.c_char * 64),
+        ("market_name", ctypes.c_char * 64),
+        ("vram_total_bytes", ctypes.c_uint64),
+        ("vram_used_bytes", ctypes.c_uint64),
+        ("gfx_activity_pct", ctypes.c_uint32),
+        ("umc_activity_pct", ctypes.c_uint32),
+        ("mm_activity_pct", ctypes.c_uint32),
+        ("socket_power_w", ctypes.c_double),
+        ("power_limit_w", ctypes.c_double),
+        ("temp_hotspot_c", ctypes.c_double),
+        ("temp_mem_c", ctypes.c_double),
+        ("temp_edge_c", ctypes.c_double),
+        ("gfx_clk_mhz", ctypes.c_uint32),
+        ("mem_clk_mhz", ctypes.c_uint32),
+        ("energy_j", ctypes.c_double),
+        ("ecc_correctable", ctypes.c_uint64),
+        ("ecc_uncorrectable", ctypes.c_uint64),
+        ("ecc_deferred", ctypes.c_uint64),
+        ("xgmi_links_total", ctypes.c_uint32),
+        ("xgmi_links_up", ctypes.c_uint32),
+        ("xgmi_links_error", ctypes.c_uint32),
+        ("bad_pages", ctypes.c_uint32),
+        ("num_processes", ctypes.c_uint32),
+        ("valid_mask", ctypes.c_uint32),
+    ]
+
+
+class _Event(ctypes.Structure):
+    _fields_ = [
+        ("index", ctypes.c_int32),
+        ("kind", ctypes.c_int32),
+        ("critical", ctypes.c_int32),
+        ("message", ctypes.c_char * 128),
+    ]
+
+
+M_VRAM, M_ACTIVITY, M_POWER, M_TEMP, M_CLOCK, M_ENERGY, M_ECC, M_XGMI, M_BADPAGES, M_PROCS = (1 << i for i in range(10))
+
+EVENT_NAMES = {
+    1: "vm_fault",
+    2: "thermal_throttle",
+    3: "gpu_pre_reset",
+    4: "gpu_post_reset",
+    100: "ecc_uncorrectable",
+    101: "xgmi_link_error",
+    102: "device_lost",
+    103: "bad_pages",
+}
+
+
+def _lib() -> ctypes.CDLL:
+    lib = native.load(LIB)
+    if getattr(lib, "_at_typed", False):
+        return lib
+    c = ctypes
+    lib.at_abi_version.restype = c.c_int
+    lib.at_enumerate.argtypes = [c.c_char_p, c.POINTER(_Gpu), c.c_int, c.POINTER(c.c_int)]
+    lib.at_links.argtypes = [c.c_char_p, c.POINTER(_Link), c.c_int, c.POINTER(c.c_int)]
+    lib.at_probe.argtypes = [c.c_char_p, c.c_int, c.c_char_p, c.c_int]
+    lib.at_smi_open.restype = c.c_int
+    lib.at_smi_count.restype = c.c_int
+    lib.at_smi_collect.argtypes = [c.POINTER(_Metrics), c.c_int, c.POINTER(c.c_int)]
+    lib.at_smi_driver_version.argtypes = [c.c_char_p, c.c_int]
+    lib.at_smi_set_compute_partition.argtypes = [c.c_int, c.c_char_p]
+    lib.at_smi_set_memory_partition.argtypes = [c.c_int, c.c_char_p]
+    lib.at_smi_get_partitions.argtypes = [c.c_int, c.c_char_p, c.c_int, c.c_char_p, c.c_int]
+    lib.at_health_poll.argtypes = [c.c_int, c.POINTER(_Event), c.c_int, c.POINTER(c.c_int)]
+    lib._at_typed = True
+    return lib
+
+
+def _s(b: bytes) -> str:
+    return b.decode("utf-8", "replace")
+
+
+@dataclass(frozen=True)
+class GpuDevice:
+    """One schedulable GPU (a whole MI355X in SPX, one partition in DPX/QPX/CPX)."""
+
+    index: int
+    kfd_node: int
+    gpu_id: int
+    arch: str
+    gfx_target_version: int
+    cu_count: int
+    simd_count: int
+    num_xcc: int
+    lds_size_kib: int
+    max_engine_clk_mhz: int
+    vram_bytes: int
+    render_minor: int
+    bdf: str
+    vendor_id: int
+    device_id: int
+    unique_id: int
+    hive_id: int
+    xgmi_links: int
+    numa_node: int
+    physical_index: int
+    partition_index: int
+    partition_count: int
+    compute_partition: str
+    memory_partition: str
+
+    @property
+    def render_node(self) -> str:
+        return f"/dev/dri/renderD{self.render_minor}"
+
+    @property
+    def device_id_str(self) -> str:
+        """Stable kubelet device ID: PCI BDF (+ partition suffix when partitioned)."""
+        return self.bdf if self.partition_count <= 1 else f"{self.bdf}-p{self.partition_index}"
+
+    def as_dict(self) -> dict:
+        return asdict(self)
+
+
+@dataclass(frozen=True)
+class GpuLink:
+    src: int
+    dst: int
+    type: int
+    weight: int
+    min_bandwidth_mbps: int
+    max_bandwidth_mbps: int
+
+    @property
+    def is_xgmi(self) -> bool:
+        return self.type == LINK_XGMI
+
+
+def _root(root: str | None) -> bytes:
+    return (root or "/").encode()
+
+
+def enumerate_gpus(root: str | None = None) -> list[GpuDevice]:
+    lib = _lib()
+    n = ctypes.c_int(0)
+    lib.at_enumerate(_root(root), None, 0, ctypes.byref(n))
+    if n.value == 0:
+        return []
+    arr = (_Gpu * n.value)()
+    cnt = ctypes.c_int(0)
+    rc = lib.at_enumerate(_root(root), arr, n.value, ctypes.byref(cnt))
+    if rc != 0:
+        raise RuntimeError(f"at_enumerate failed rc={rc}")
+    out = []
+    for i in range(cnt.value):
+        g = arr[i]
+        out.append(GpuDevice(
+            index=i, kfd_node=g.kfd_node, gpu_id=g.gpu_id, arch=_s(g.arch), gfx_target_version=g.gfx_target_version,
+            cu_count=g.cu_count, simd_count=g.simd_count, num_xcc=g.num_xcc, lds_size_kib=g.lds_size_kib,
+            max_engine_clk_mhz=g.max_engine_clk_mhz, vram_bytes=g.vram_bytes, render_minor=g.drm_render_minor,
+            bdf=_s(g.bdf), vendor_id=g.vendor_id, device_id=g.device_id, unique_id=g.unique_id, hive_id=g.hive_id,
+            xgmi_links=g.num_xgmi_links, numa_node=g.numa_node, physical_index=g.physical_index,
+            partition_index=g.partition_index, partition_count=g.partition_count,
+            compute_partition=_s(g.compute_partition), memory_partition=_s(g.memory_partition)))
+    return out
+
+
+def links(root: str | None = None) -> list[GpuLink]:
+    lib = _lib()
+    n = ctypes.c_int(0)
+    lib.at_links(_root(root), None, 0, ctypes.byref(n))
+    if n.value == 0:
+        return []
+    arr = (_Link * n.value)()
+    cnt = ctypes.c_int(0)
+    lib.at_links(_root(root), arr, n.value, ctypes.byref(cnt))
+    return [GpuLink(l.from_gpu, l.to_gpu, l.type, l.weight, l.min_bandwidth_mbps, l.max_bandwidth_mbps)
+            for l in arr[: cnt.value]]
+
+
+def probe(root: str | None = None, expect_gpus: int = 0) -> tuple[bool, str]:
+    """N1 driver readiness (amdgpu live, /dev/kfd, KFD GPU nodes, render nodes)."""
+    buf = ctypes.create_string_buffer(256)
+    rc = _lib().at_probe(_root(root), expect_gpus, buf, len(buf))
+    return rc == 0, _s(buf.value)
+
+
+@dataclass
+class GpuMetrics:
+    index: int
+    bdf: str
+    uuid: str
+    market_name: str
+    values: dict = field(default_factory=dict)
+
+
+_METRIC_FIELDS = {
+    M_VRAM: ("vram_total_bytes", "vram_used_bytes"),
+    M_ACTIVITY: ("gfx_activity_pct", "umc_activity_pct", "mm_activity_pct"),
+    M_POWER: ("socket_power_w", "power_limit_w"),
+    M_TEMP: ("temp_hotspot_c", "temp_mem_c", "temp_edge_c"),
+    M_CLOCK: ("gfx_clk_mhz", "mem_clk_mhz"),
+    M_ENERGY: ("energy_j",),
+    M_ECC: ("ecc_correctable", "ecc_uncorrectable", "ecc_deferred"),
+    M_XGMI: ("xgmi_links_total", "xgmi_links_up", "xgmi_links_error"),
+    M_BADPAGES: ("bad_pages",),
+    M_PROCS: ("num_processes",),
+}
+
+
+class Smi:
+    """N4 collector handle (libamd_smi via the native library)."""
+
+    def __init__(self):
+        self._lib = _lib()
+        rc = self._lib.at_smi_open()
+        if rc != 0:
+            raise native.NativeUnavailable(f"amd-smi unavailable (rc={rc})")
+        self._open = True
+
+    def close(self) -> None:
+        if self._open:
+            self._lib.at_smi_close()
+            self._open = False
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def count(self) -> int:
+        return max(0, self._lib.at_smi_count())
+
+    def collect(self) -> list[GpuMetrics]:
+        n = self.count()
+        if n == 0:
+            return []
+        arr = (_Metrics * n)()
+        cnt = ctypes.c_int(0)
+        rc = self._lib.at_smi_collect(arr, n, ctypes.byref(cnt))
+        if rc != 0:
+            raise RuntimeError(f"at_smi_collect rc={rc}")
+        out = []
+        for m in arr[: cnt.value]:
+            vals = {}
+            for bit, names in _METRIC_FIELDS.items():
+                if m.valid_mask & bit:
+                    for nm in names:
+                        vals[nm] = getattr(m, nm)
+            out.append(GpuMetrics(m.index, _s(m.bdf), _s(m.uuid), _s(m.market_name), vals))
+        return out
+
+    def driver_version(self) -> str:
+        buf = ctypes.create_string_buffer(256)
+        return _s(buf.value) if self._lib.at_smi_driver_version(buf, len(buf)) == 0 else ""
+
+    def partitions(self, index: int) -> tuple[str, str]:
+        c = ctypes.create_string_buffer(32)
+        m = ctypes.create_string_buffer(32)
+        self._lib.at_smi_get_partitions(index, c, 32, m, 32)
+        return _s(c.value), _s(m.value)
+
+    def set_compute_partition(self, index: int, mode: str) -> int:
+        return self._lib.at_smi_set_compute_partition(index, mode.encode())
+
+    def set_memory_partition(self, index: int, mode: str) -> int:
+        return self._lib.at_smi_set_memory_partition(index, mode.encode())
+
+
+@dataclass(frozen=True)
+class HealthEvent:
+    index: int
+    kind: str
+    critical: bool
+    message: str
+
+
+class HealthWatcher:
+    """N6: amd-smi event notifications + ECC/xGMI/bad-page deltas."""
+
+    def __init__(self):
+        self._lib = _lib()
+        rc = self._lib.at_health_start()
+        if rc != 0:
+            raise native.NativeUnavailable(f"health watcher unavailable (rc={rc})")
+
+    def poll(self, timeout_ms: int = 1000) -> list[HealthEvent]:
+        arr = (_Event * 64)()
+        cnt = ctypes.c_int(0)
+        self._lib.at_health_poll(timeout_ms, arr, 64, ctypes.byref(cnt))
+        return [HealthEvent(e.index, EVENT_NAMES.get(e.kind, str(e.kind)), bool(e.critical), _s(e.message))
+                for e in arr[: min(cnt.value, 64)]]
+
+    def close(self) -> None:
+        self._lib.at_health_stop()

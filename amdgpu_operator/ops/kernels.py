@@ -1,0 +1,255 @@
+"""Python bindings for the hand-written gfx950 validator kernels (K1-K4).
+
+Thin :mod:`ctypes` layer over ``libamdgpu_validator.so``
+(``native/validator/validator_kernels.hip``).  Tensors are PyTorch-ROCm device
+tensors; every call is enqueued on the current HIP stream.  Host-side shape
+checks mirror the kernel's assumptions, and the C launchers check them again
+(they return ``hipErrorInvalidValue`` instead of launching), so a bad shape
+never reaches the GPU.
+
+There is deliberately no eager-PyTorch fallback: if the library is missing
+:class:`amdgpu_operator.native.NativeUnavailable` is raised.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+from .. import native
+
+LIB_NAME = "libamdgpu_validator.so"
+
+GEMM_BM = 256
+GEMM_BN = 256
+GEMM_BK = 64
+
+_c_i64 = ctypes.c_int64
+_c_ptr = ctypes.c_void_p
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def _lib() -> ctypes.CDLL:
+    lib = native.load(LIB_NAME)
+    if getattr(lib, "_avk_typed", False):
+        return lib
+    P, I, I64, U64, F, S = _c_ptr, ctypes.c_int, _c_i64, ctypes.c_uint64, ctypes.c_float, _c_ptr
+    sig = {
+        "avk_abi_version": ([], I),
+        "avk_fill_uniform_f32": ([P, I64, U64, F, F, S], I),
+        "avk_fill_uniform_bf16": ([P, I64, U64, F, F, S], I),
+        "avk_vector_add_f32": ([P, P, P, I64, S], I),
+        "avk_gemm_bf16_nt": ([P, P, P, I, I, I, I, S], I),
+        "avk_gemv_rows": ([P, I, P, P, I, I, S], I),
+        "avk_gemv_cols_bf16": ([P, P, P, I, I, S], I),
+        "avk_hbm_copy": ([P, P, I64, I, I, S], I),
+        "avk_checksum": ([P, I64, P, S], I),
+        "avk_max_abs_diff_f32": ([P, P, I64, P, S], I),
+        "avk_allreduce_oneshot_f32": ([ctypes.POINTER(P), I, P, I64, S], I),
+        "avk_allreduce_twoshot_f32": ([ctypes.POINTER(P), ctypes.POINTER(P), I, I, I64, S], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    lib._avk_typed = True
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise KernelError(f"{what} failed with hipError {rc}")
+
+
+def _stream(stream=None) -> int:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _require(t, dtype, name: str, numel_multiple: int = 1) -> None:
+    import torch
+
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a GPU tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.data_ptr() % 16:
+        raise ValueError(f"{name} must be 16-byte aligned")
+    if t.numel() % numel_multiple:
+        raise ValueError(f"{name}.numel() must be a multiple of {numel_multiple}")
+
+
+def abi_version() -> int:
+    return _lib().avk_abi_version()
+
+
+def fill_uniform_(t, seed: int, lo: float = -1.0, hi: float = 1.0, stream=None):
+    """Deterministic device-side uniform fill (fp32 or bf16)."""
+    import torch
+
+    seed &= (1 << 64) - 1
+    if t.dtype == torch.float32:
+        _require(t, torch.float32, "t")
+        _check(_lib().avk_fill_uniform_f32(t.data_ptr(), t.numel(), seed, lo, hi, _stream(stream)), "fill_f32")
+    elif t.dtype == torch.bfloat16:
+        _require(t, torch.bfloat16, "t", 8)
+        _check(_lib().avk_fill_uniform_bf16(t.data_ptr(), t.numel(), seed, lo, hi, _stream(stream)), "fill_bf16")
+    else:
+        raise ValueError(f"unsupported dtype {t.dtype}")
+    return t
+
+
+def vector_add(a, b, out=None, stream=None):
+    """K1: ``out = a + b`` (fp32)."""
+    import torch
+
+    _require(a, torch.float32, "a")
+    _require(b, torch.float32, "b")
+    if a.numel() != b.numel():
+        raise ValueError("a and b differ in size")
+    if out is None:
+        out = torch.empty_like(a)
+    _require(out, torch.float32, "out")
+    _check(_lib().avk_vector_add_f32(a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), _stream(stream)), "vector_add")
+    return out
+
+
+def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None):
+    """K2: ``out[M,N] = a[M,K] @ bt[N,K].T`` on MFMA (bf16 in, fp32 accumulate).
+
+    M and N must be multiples of 256 and K of 64 (the kernel has no edge
+    tiles; the validator picks its shapes accordingly).
+    """
+    import torch
+
+    _require(a, torch.bfloat16, "a")
+    _require(bt, torch.bfloat16, "bt")
+    if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
+        raise ValueError(f"bad GEMM operands {tuple(a.shape)} x {tuple(bt.shape)}^T")
+    M, K = a.shape
+    N = bt.shape[0]
+    if M % GEMM_BM or N % GEMM_BN or K % GEMM_BK:
+        raise ValueError(f"GEMM shape {M}x{N}x{K} must be multiples of {GEMM_BM}x{GEMM_BN}x{GEMM_BK}")
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=out_dtype or torch.bfloat16)
+    if out.shape != (M, N) or out.dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("bad GEMM output")
+    _require(out, out.dtype, "out")
+    rc = _lib().avk_gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
+                                 M, N, K, _stream(stream))
+    _check(rc, "gemm_bf16_nt")
+    return out
+
+
+def gemv_rows(x, v, out=None, stream=None):
+    """``out[r] = sum_c x[r, c] * v[c]`` (x bf16 or fp32)."""
+    import torch
+
+    R, C = x.shape
+    _require(x, x.dtype, "x", 8)
+    _require(v, torch.float32, "v")
+    if C % 8 or v.numel() != C:
+        raise ValueError("gemv_rows shape mismatch")
+    if out is None:
+        out = torch.empty(R, device=x.device, dtype=torch.float32)
+    _check(_lib().avk_gemv_rows(x.data_ptr(), int(x.dtype == torch.bfloat16), v.data_ptr(), out.data_ptr(), R, C,
+                                _stream(stream)), "gemv_rows")
+    return out
+
+
+def gemv_cols_bf16(x, v, out=None, stream=None):
+    """``out[c] = sum_r x[r, c] * v[r]`` (x bf16)."""
+    import torch
+
+    R, C = x.shape
+    _require(x, torch.bfloat16, "x", 8)
+    _require(v, torch.float32, "v")
+    if C % 8 or v.numel() != R:
+        raise ValueError("gemv_cols shape mismatch")
+    if out is None:
+        out = torch.zeros(C, device=x.device, dtype=torch.float32)
+    else:
+        out.zero_()
+    _check(_lib().avk_gemv_cols_bf16(x.data_ptr(), v.data_ptr(), out.data_ptr(), R, C, _stream(stream)), "gemv_cols")
+    return out
+
+
+def hbm_copy(src, dst, num_cus: int = 256, variant: int = 0, stream=None):
+    """K3: streaming copy of ``src`` into ``dst`` (any dtype, 16-B multiple)."""
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != nbytes or nbytes % 16:
+        raise ValueError("hbm_copy size mismatch")
+    if not (src.is_cuda and dst.is_cuda and src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("hbm_copy needs contiguous GPU tensors")
+    _check(_lib().avk_hbm_copy(src.data_ptr(), dst.data_ptr(), nbytes, num_cus, variant, _stream(stream)), "hbm_copy")
+    return dst
+
+
+def checksum(t, scratch=None, stream=None) -> int:
+    import torch
+
+    nbytes = t.numel() * t.element_size()
+    if scratch is None:
+        scratch = torch.empty(1, device=t.device, dtype=torch.int64)
+    _check(_lib().avk_checksum(t.data_ptr(), nbytes, scratch.data_ptr(), _stream(stream)), "checksum")
+    return int(scratch.item()) & ((1 << 64) - 1)
+
+
+def max_abs_diff(a, b, stream=None) -> float:
+    import torch
+
+    _require(a, torch.float32, "a")
+    _require(b, torch.float32, "b")
+    if a.numel() != b.numel():
+        raise ValueError("size mismatch")
+    out = torch.empty(1, device=a.device, dtype=torch.int32)
+    _check(_lib().avk_max_abs_diff_f32(a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(), _stream(stream)), "max_abs_diff")
+    return float(out.view(torch.float32).item())
+
+
+def _ptr_array(ptrs):
+    arr = (_c_ptr * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr
+
+
+def allreduce_oneshot(inputs_or_ptrs, out, count: int | None = None, stream=None):
+    """K4 one-shot: ``out = sum(inputs)``; inputs are tensors or raw peer pointers."""
+    import torch
+
+    _require(out, torch.float32, "out", 4)
+    ptrs = [x.data_ptr() if isinstance(x, torch.Tensor) else int(x) for x in inputs_or_ptrs]
+    n = count if count is not None else out.numel()
+    if not 1 <= len(ptrs) <= 8:
+        raise ValueError("1..8 peers supported")
+    _check(_lib().avk_allreduce_oneshot_f32(_ptr_array(ptrs), len(ptrs), out.data_ptr(), n, _stream(stream)), "allreduce_oneshot")
+    return out
+
+
+def allreduce_twoshot_slice(in_ptrs, out_ptrs, rank: int, count: int, stream=None):
+    """K4 two-shot: reduce this rank's slice and write it into every peer output."""
+    if len(in_ptrs) != len(out_ptrs) or not 1 <= len(in_ptrs) <= 8:
+        raise ValueError("bad peer tables")
+    _check(_lib().avk_allreduce_twoshot_f32(_ptr_array([int(p) for p in in_ptrs]), _ptr_array([int(p) for p in out_ptrs]),
+                                            len(in_ptrs), rank, count, _stream(stream)), "allreduce_twoshot")
+
+
+@dataclass
+class GemmShape:
+    m: int
+    n: int
+    k: int
+
+    @property
+    def flops(self) -> float:
+        return 2.0 * self.m * self.n * self.k

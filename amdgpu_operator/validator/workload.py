@@ -1,0 +1,284 @@
+"""Validator GPU workload: the steps that gate a node's ``validated`` state.
+
+Reference parity: the upstream operator-validator (implied by the reference's
+"Running or Completed" pods, ``/root/reference/README.md:199``) runs CUDA
+``vectorAdd``.  The MI355X validator runs, per GPU:
+
+1. ``hip``      - device open + properties (gfx950, 256 CUs, HBM size)
+2. ``vecadd``   - K1, exact check
+3. ``gemm``     - K2 MFMA bf16 GEMM, Freivalds check (C·x == A·(Bᵀ·x)) on an
+                  fp32-output pass, then a timed bf16-output pass (TFLOP/s)
+4. ``hbm``      - K3 streaming copy, checksum-verified, GB/s
+5. ``xgmi``     - K4 one-shot all-reduce over n emulated peers (1-GPU box) or
+                  real peers (IPC-mapped over xGMI, multi-GPU), exact check
+6. ``rccl``     - RCCL all-reduce (``torch.distributed`` backend "nccl" is RCCL
+                  on ROCm) across every GPU of the node, exact check + busBW
+
+Each step records wall time; the sum is the validator's contribution to
+time-to-Ready.  A step that fails raises :class:`ValidationFailed` and the
+node is not marked validated.
+"""
+
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Any
+
+from ..ops import kernels as K
+
+
+class ValidationFailed(RuntimeError):
+    def __init__(self, step: str, detail: str):
+        super().__init__(f"validation step {step!r} failed: {detail}")
+        self.step = step
+        self.detail = detail
+
+
+@dataclass
+class WorkloadConfig:
+    """Sizes of the validator workload (defaults = the production gate)."""
+
+    vecadd_elems: int = 1 << 24
+    gemm_m: int = 4096
+    gemm_n: int = 4096
+    gemm_k: int = 4096
+    gemm_iters: int = 3
+    hbm_bytes: int = 1 << 30
+    hbm_iters: int = 3
+    xgmi_peers: int = 8
+    xgmi_elems: int = 1 << 22
+    rccl_elems: int = 1 << 24  # 64 MiB fp32 per GPU
+    rccl_iters: int = 2
+    freivalds_tol: float = 2e-3
+    min_gemm_tflops: float = 0.0  # perf floor (0 = report only)
+    min_hbm_gbps: float = 0.0
+    seed: int = 0x5EED
+
+    @classmethod
+    def quick(cls) -> "WorkloadConfig":
+        return cls(vecadd_elems=1 << 20, gemm_m=512, gemm_n=512, gemm_k=512, gemm_iters=1, hbm_bytes=1 << 24,
+                   hbm_iters=1, xgmi_elems=1 << 16, rccl_elems=1 << 16, rccl_iters=1)
+
+
+@dataclass
+class StepResult:
+    name: str
+    ok: bool
+    seconds: float
+    metrics: dict[str, Any] = field(default_factory=dict)
+
+
+@dataclass
+class WorkloadReport:
+    device: dict[str, Any]
+    steps: list[StepResult]
+
+    @property
+    def ok(self) -> bool:
+        return all(s.ok for s in self.steps)
+
+    @property
+    def seconds(self) -> float:
+        return sum(s.seconds for s in self.steps)
+
+    def as_dict(self) -> dict[str, Any]:
+        return {
+            "ok": self.ok,
+            "seconds": self.seconds,
+            "device": self.device,
+            "steps": [{"name": s.name, "ok": s.ok, "seconds": s.seconds, **s.metrics} for s in self.steps],
+        }
+
+
+class _Timer:
+    def __init__(self, torch, device):
+        self.torch = torch
+        self.device = device
+
+    def __enter__(self):
+        self.torch.cuda.synchronize(self.device)
+        self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        self.torch.cuda.synchronize(self.device)
+        self.dt = time.perf_counter() - self.t0
+        return False
+
+
+def _events_ms(torch, fn, iters: int) -> float:
+    """Median per-iteration device time of ``fn`` in ms (HIP events)."""
+    times = []
+    for _ in range(iters):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        times.append(s.elapsed_time(e))
+    times.sort()
+    return times[len(times) // 2]
+
+
+class ValidatorWorkload:
+    """Runs the validator steps on one GPU (``device``), optionally with a
+    torch.distributed process group spanning the node's GPUs for the RCCL step.
+    Buffers are allocated once and reused across :meth:`run` calls (a resident
+    validator re-validates after driver/health events without re-allocating)."""
+
+    def __init__(self, device: int = 0, cfg: WorkloadConfig | None = None, process_group=None):
+        import torch
+
+        self.torch = torch
+        self.cfg = cfg or WorkloadConfig()
+        self.device = torch.device("cuda", device)
+        self.pg = process_group
+        self._bufs: dict[str, Any] = {}
+
+    # ------------------------------------------------------------ helpers
+    def _buf(self, name: str, shape, dtype):
+        t = self._bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = self.torch.empty(shape, device=self.device, dtype=dtype)
+            self._bufs[name] = t
+        return t
+
+    def device_info(self) -> dict[str, Any]:
+        p = self.torch.cuda.get_device_properties(self.device)
+        return {
+            "name": p.name,
+            "arch": getattr(p, "gcnArchName", ""),
+            "cus": p.multi_processor_count,
+            "hbm_bytes": p.total_memory,
+            "index": self.device.index,
+        }
+
+    # -------------------------------------------------------------- steps
+    def step_hip(self) -> StepResult:
+        t0 = time.perf_counter()
+        info = self.device_info()
+        self.torch.cuda.synchronize(self.device)
+        ok = info["arch"].startswith("gfx950") or info["arch"] == ""
+        return StepResult("hip", ok, time.perf_counter() - t0, {"arch": info["arch"], "cus": info["cus"]})
+
+    def step_vecadd(self) -> StepResult:
+        torch, cfg = self.torch, self.cfg
+        n = cfg.vecadd_elems
+        a = self._buf("va", (n,), torch.float32)
+        b = self._buf("vb", (n,), torch.float32)
+        c = self._buf("vc", (n,), torch.float32)
+        with _Timer(torch, self.device) as tm:
+            K.fill_uniform_(a, cfg.seed + 1)
+            K.fill_uniform_(b, cfg.seed + 2)
+            K.vector_add(a, b, c)
+            ok = bool(torch.equal(c, a + b))
+        if not ok:
+            raise ValidationFailed("vecadd", "c != a + b")
+        return StepResult("vecadd", ok, tm.dt, {"elems": n})
+
+    def step_gemm(self) -> StepResult:
+        torch, cfg = self.torch, self.cfg
+        M, N, Kd = cfg.gemm_m, cfg.gemm_n, cfg.gemm_k
+        a = self._buf("ga", (M, Kd), torch.bfloat16)
+        bt = self._buf("gb", (N, Kd), torch.bfloat16)
+        c32 = self._buf("gc32", (M, N), torch.float32)
+        c16 = self._buf("gc16", (M, N), torch.bfloat16)
+        x = self._buf("gx", (N,), torch.float32)
+        with _Timer(torch, self.device) as tm:
+            K.fill_uniform_(a, cfg.seed + 3)
+            K.fill_uniform_(bt, cfg.seed + 4)
+            K.fill_uniform_(x, cfg.seed + 5)
+            K.gemm_bf16_nt(a, bt, out=c32)
+            # Freivalds: C x  vs  A (Bt^T x)
+            y1 = K.gemv_rows(c32, x)
+            z = K.gemv_cols_bf16(bt, x)
+            y2 = K.gemv_rows(a, z)
+            err = (y1 - y2).abs().max().item()
+            scale = y2.abs().max().item() + 1e-30
+            rel = err / scale
+            ok = math.isfinite(rel) and rel <= cfg.freivalds_tol
+            ms = _events_ms(torch, lambda: K.gemm_bf16_nt(a, bt, out=c16), max(1, cfg.gemm_iters))
+        tflops = 2.0 * M * N * Kd / (ms * 1e-3) / 1e12
+        if not ok:
+            raise ValidationFailed("gemm", f"Freivalds relative error {rel:.3e} > {cfg.freivalds_tol:.1e}")
+        if cfg.min_gemm_tflops and tflops < cfg.min_gemm_tflops:
+            raise ValidationFailed("gemm", f"{tflops:.0f} TFLOP/s below floor {cfg.min_gemm_tflops}")
+        return StepResult("gemm", ok, tm.dt, {"shape": [M, N, Kd], "freivalds_rel_err": rel, "ms": ms, "tflops": tflops})
+
+    def step_hbm(self) -> StepResult:
+        torch, cfg = self.torch, self.cfg
+        n = cfg.hbm_bytes // 4
+        src = self._buf("hs", (n,), torch.float32)
+        dst = self._buf("hd", (n,), torch.float32)
+        cus = self.torch.cuda.get_device_properties(self.device).multi_processor_count
+        with _Timer(torch, self.device) as tm:
+            K.fill_uniform_(src, cfg.seed + 6)
+            ms = _events_ms(torch, lambda: K.hbm_copy(src, dst, num_cus=cus), max(1, cfg.hbm_iters))
+            ok = K.checksum(src) == K.checksum(dst)
+        gbps = 2.0 * cfg.hbm_bytes / (ms * 1e-3) / 1e9
+        if not ok:
+            raise ValidationFailed("hbm", "copy checksum mismatch")
+        if cfg.min_hbm_gbps and gbps < cfg.min_hbm_gbps:
+            raise ValidationFailed("hbm", f"{gbps:.0f} GB/s below floor {cfg.min_hbm_gbps}")
+        return StepResult("hbm", ok, tm.dt, {"bytes": cfg.hbm_bytes, "ms": ms, "gbps": gbps})
+
+    def step_xgmi_emulated(self) -> StepResult:
+        """K4 over ``xgmi_peers`` buffers on this GPU (algorithm check; the
+        real peer-pointer path is :mod:`amdgpu_operator.parallel.xgmi`)."""
+        torch, cfg = self.torch, self.cfg
+        n, P = cfg.xgmi_elems, cfg.xgmi_peers
+        ins = [self._buf(f"xi{r}", (n,), torch.float32) for r in range(P)]
+        out = self._buf("xo", (n,), torch.float32)
+        with _Timer(torch, self.device) as tm:
+            for r, t in enumerate(ins):
+                K.fill_uniform_(t, cfg.seed + 100 + r)
+            K.allreduce_oneshot(ins, out)
+            ref = torch.stack(ins).sum(0)
+            err = K.max_abs_diff(out, ref)
+            ok = err <= 1e-5 * P
+        if not ok:
+            raise ValidationFailed("xgmi", f"one-shot all-reduce error {err:.3e}")
+        return StepResult("xgmi", ok, tm.dt, {"peers": P, "elems": n, "max_abs_err": err})
+
+    def step_rccl(self) -> StepResult:
+        torch, cfg = self.torch, self.cfg
+        import torch.distributed as dist
+
+        if self.pg is None and not dist.is_initialized():
+            return StepResult("rccl", True, 0.0, {"skipped": "no process group"})
+        world = dist.get_world_size(self.pg)
+        rank = dist.get_rank(self.pg)
+        n = cfg.rccl_elems
+        buf = self._buf("rb", (n,), torch.float32)
+        with _Timer(torch, self.device) as tm:
+            # rank r contributes (r + 1): the sum is world*(world+1)/2 exactly in fp32
+            buf.fill_(float(rank + 1))
+            dist.all_reduce(buf, group=self.pg)
+            expect = world * (world + 1) / 2.0
+            ok = bool(torch.all(buf == expect).item())
+            ms = _events_ms(torch, lambda: dist.all_reduce(buf, group=self.pg), max(1, cfg.rccl_iters))
+        nbytes = n * 4
+        algbw = nbytes / (ms * 1e-3) / 1e9
+        busbw = algbw * (2 * (world - 1) / world) if world > 1 else 0.0
+        if not ok:
+            raise ValidationFailed("rccl", "all-reduce result mismatch")
+        return StepResult("rccl", ok, tm.dt, {"world": world, "bytes": nbytes, "ms": ms, "algbw_gbps": algbw,
+                                              "busbw_gbps": busbw})
+
+    STEPS = ("hip", "vecadd", "gemm", "hbm", "xgmi", "rccl")
+
+    def run(self, steps: tuple[str, ...] | None = None) -> WorkloadReport:
+        self.torch.cuda.set_device(self.device)
+        fns = {
+            "hip": self.step_hip,
+            "vecadd": self.step_vecadd,
+            "gemm": self.step_gemm,
+            "hbm": self.step_hbm,
+            "xgmi": self.step_xgmi_emulated,
+            "rccl": self.step_rccl,
+        }
+        results = [fns[s]() for s in (steps or self.STEPS)]
+        return WorkloadReport(self.device_info(), results)

@@ -1,0 +1,503 @@
+// Operator-validator GPU workload for MI355X (gfx950 / CDNA4).
+//
+// Capability parity: the reference's "Running or Completed" validator pods
+// (/root/reference/README.md:199) run an upstream CUDA vectorAdd sample.  This
+// file is the MI355X-native replacement described in SURVEY.md §2.D:
+//   K1 vector_add      - fp32 c = a + b, 16 B/lane, grid-stride
+//   K2 gemm_bf16_nt    - bf16 MFMA GEMM (v_mfma_f32_16x16x32_bf16), 256x256x64
+//                        block tile, 8 waves, global_load_lds staging into an
+//                        XOR-swizzled LDS image, XCD-aware tile order
+//   K3 hbm_copy        - float4 streaming copy (HBM3E bandwidth check)
+//   K4 allreduce_*     - one-shot / two-shot sum over n peer buffers (peer
+//                        pointers over xGMI, or n emulated buffers on one GPU)
+// plus helpers for the correctness gates (device RNG fill, Freivalds GEMV
+// check, checksum, max-abs-diff).
+//
+// Everything is exported through a C ABI (avk_*) so the same library serves
+// the Python control plane (ctypes, torch tensors) and the standalone
+// C++ validator binary (validator_main.cpp).  Every launcher validates the
+// shapes its kernel assumes and returns hipErrorInvalidValue instead of
+// launching an out-of-bounds grid.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+#define AVK_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kNumXcd = 8;
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// uniform in [lo, hi) from a 24-bit mantissa
+__device__ __forceinline__ float u01(uint64_t h) {
+  return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+
+// ---------------------------------------------------------------- fills ----
+
+__global__ __launch_bounds__(256) void fill_uniform_f32_kernel(float* __restrict__ p, int64_t n,
+                                                               uint64_t seed, float lo, float hi) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * 256;
+  float scale = hi - lo;
+  for (; i < n; i += stride) p[i] = lo + scale * u01(splitmix64(seed ^ (uint64_t)i * 0xD1B54A32D192ED03ull));
+}
+
+__global__ __launch_bounds__(256) void fill_uniform_bf16_kernel(__bf16* __restrict__ p, int64_t n8,
+                                                                uint64_t seed, float lo, float hi) {
+  // n8 = number of 8-element (16 B) groups
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * 256;
+  float scale = hi - lo;
+  for (; i < n8; i += stride) {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint64_t idx = (uint64_t)(i * 8 + j);
+      v[j] = (__bf16)(lo + scale * u01(splitmix64(seed ^ idx * 0xD1B54A32D192ED03ull)));
+    }
+    reinterpret_cast<bf16x8*>(p)[i] = v;
+  }
+}
+
+// ------------------------------------------------------------ K1 vector add ----
+
+__global__ __launch_bounds__(256) void vector_add_kernel(const float4* __restrict__ a,
+                                                         const float4* __restrict__ b,
+                                                         float4* __restrict__ c, int64_t n4) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * 256;
+  for (; i < n4; i += stride) {
+    float4 x = a[i], y = b[i];
+    c[i] = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+  }
+}
+
+__global__ void vector_add_tail_kernel(const float* a, const float* b, float* c, int64_t start, int64_t n) {
+  int64_t i = start + threadIdx.x;
+  if (i < n) c[i] = a[i] + b[i];
+}
+
+// --------------------------------------------------------- K2 bf16 MFMA GEMM ----
+//
+// C[M][N] = A[M][K] · Bt[N][K]^T   (both operands K-contiguous, "NT")
+//
+// Block tile 256x256, K-step 64, 512 threads = 8 waves arranged 2 (M) x 4 (N);
+// each wave owns a 128x64 output = 8x4 tiles of v_mfma_f32_16x16x32_bf16.
+// LDS holds two stages of {A 256x64, B 256x64} bf16 = 2 x 64 KiB.  Each stage
+// is filled by global_load_lds_dwordx4: one wave-instruction writes 1 KiB =
+// 8 rows x 128 B lane-linearly; the bank swizzle lives on the SOURCE address
+// (logical 16-B chunk = physical chunk ^ ((row >> 1) & 7)) and the same XOR is
+// applied on the ds_read_b128 side, which makes every 16-lane ds_read_b128
+// group of a fragment read hit 16 distinct 16-B slots (conflict-free).
+
+namespace gemm {
+constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
+constexpr int TILE_BYTES = BM * BK * 2;      // 32 KiB (A or B of one stage)
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;  // 64 KiB
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;   // 128 KiB
+constexpr int GROUP_M = 4;                   // tile rows per L2 band
+}  // namespace gemm
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+__device__ __forceinline__ void gemm_stage(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                                           int K, int m0, int n0, int k0, char* stage_base, int wave,
+                                           int lane) {
+  using namespace gemm;
+  const int rsub = lane >> 3;
+  const int pc = lane & 7;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = wave * 4 + i;  // 1 KiB piece, 0..31
+    const int r = p * 8 + rsub;  // tile row 0..255
+    const int lc = pc ^ ((r >> 1) & 7);
+    const __bf16* srcA = A + (size_t)(m0 + r) * K + k0 + lc * 8;
+    const __bf16* srcB = Bt + (size_t)(n0 + r) * K + k0 + lc * 8;
+    __builtin_amdgcn_global_load_lds(srcA, (lds_void_ptr)(stage_base + p * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(srcB, (lds_void_ptr)(stage_base + TILE_BYTES + p * 1024), 16, 0, 0);
+  }
+}
+
+template <bool OUT_F32>
+__global__ __launch_bounds__(gemm::NTHR, 2) void gemm_bf16_nt_kernel(const __bf16* __restrict__ A,
+                                                                     const __bf16* __restrict__ Bt,
+                                                                     void* __restrict__ Cv, int M, int N,
+                                                                     int K) {
+  using namespace gemm;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2;  // 0..1
+  const int wn = wave & 3;   // 0..3
+
+  // XCD-aware, bijective block remap: blocks b and b+8 share an XCD under the
+  // observed round-robin dispatch; give each XCD a contiguous run of tiles.
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid % kNumXcd;
+  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
+  // grouped ordering: GROUP_M tile rows swept column by column
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid % per_group;
+  const int tm = first_m + in_group % gsize;
+  const int tn = in_group / gsize;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  gemm_stage(A, Bt, K, m0, n0, 0, smem, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // per-lane fragment offsets (row = lane&15 inside a 16-row tile; swizzle
+  // term (row>>1)&7 only depends on lane because tile rows are multiples of 16)
+  const int frow = lane & 15;
+  const int fsw = (frow >> 1) & 7;
+  const int fq = lane >> 4;  // which 8-element k group
+  const int a_row_base = (wm * 128 + frow) * 128;
+  const int b_row_base = (wn * 64 + frow) * 128;
+
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nk) gemm_stage(A, Bt, K, m0, n0, (t + 1) * BK, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
+    const char* As = cur;
+    const char* Bs = cur + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int pcol = ((s * 4 + fq) ^ fsw) * 16;
+      bf16x8 a[8], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + b_row_base + j * 16 * 128 + pcol);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + a_row_base + i * 16 * 128 + pcol);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + reg
+  const int crow0 = m0 + wm * 128 + fq * 4;
+  const int ccol0 = n0 + wn * 64 + frow;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const size_t idx = (size_t)(crow0 + i * 16 + r) * N + ccol0 + j * 16;
+        if constexpr (OUT_F32)
+          reinterpret_cast<float*>(Cv)[idx] = acc[i][j][r];
+        else
+          reinterpret_cast<__bf16*>(Cv)[idx] = (__bf16)acc[i][j][r];
+      }
+}
+
+// ------------------------------------------------- Freivalds check GEMVs ----
+// y[r] = sum_c X[r][c] * v[c]   (X bf16 or f32, row-major, one wave per row)
+template <typename T>
+__global__ __launch_bounds__(256) void gemv_rows_kernel(const T* __restrict__ X, const float* __restrict__ v,
+                                                        float* __restrict__ y, int R, int C) {
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= R) return;
+  const T* row = X + (size_t)wave * C;
+  float s = 0.f;
+  for (int c = lane * 8; c < C; c += 64 * 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += (float)row[c + j] * v[c + j];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) y[wave] = s;
+}
+
+// z[c] += sum_{r in slice} X[r][c] * v[r]   (X bf16 row-major), 8 cols per lane
+__global__ __launch_bounds__(256) void gemv_cols_bf16_kernel(const __bf16* __restrict__ X,
+                                                             const float* __restrict__ v,
+                                                             float* __restrict__ z, int R, int C,
+                                                             int rows_per_slice) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c0 >= C) return;
+  const int r0 = blockIdx.y * rows_per_slice;
+  const int r1 = min(R, r0 + rows_per_slice);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < r1; ++r) {
+    bf16x8 x = *reinterpret_cast<const bf16x8*>(X + (size_t)r * C + c0);
+    const float vr = v[r];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += (float)x[j] * vr;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) atomicAdd(z + c0 + j, s[j]);
+}
+
+// ------------------------------------------------------------ K3 HBM copy ----
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void hbm_copy_kernel(const f32x4* __restrict__ s, f32x4* __restrict__ d,
+                                                       int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * 256 * U;
+  int64_t i = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  for (; i + (U - 1) * 256 < n; i += stride) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(s + i + u * 256) : s[i + u * 256];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (NT) __builtin_nontemporal_store(v[u], d + i + u * 256);
+      else d[i + u * 256] = v[u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (i + u * 256 < n) d[i + u * 256] = s[i + u * 256];
+}
+
+// 64-bit wrapping sum of 32-bit words (copy integrity check)
+__global__ __launch_bounds__(256) void checksum_kernel(const uint4* __restrict__ p, int64_t n4,
+                                                       unsigned long long* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  unsigned long long s = 0;
+  for (; i < n4; i += stride) {
+    uint4 v = p[i];
+    s += (unsigned long long)v.x * 1u + (unsigned long long)v.y * 3u + (unsigned long long)v.z * 5u +
+         (unsigned long long)v.w * 7u + (unsigned long long)(i & 0xffff);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+}
+
+// max |a-b| over fp32 arrays; result written as float bits via atomicMax on uint
+__global__ __launch_bounds__(256) void max_abs_diff_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                           int64_t n, unsigned int* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  float m = 0.f;
+  for (; i < n; i += stride) {
+    float d = fabsf(a[i] - b[i]);
+    m = (d != d) ? __int_as_float(0x7f800000) : fmaxf(m, d);  // NaN -> +inf so the gate fails
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// ------------------------------------------------------- K4 all-reduce ----
+// Peer pointer table lives in kernel arguments (<= 8 peers).
+struct PeerPtrs {
+  const float* p[8];
+};
+struct PeerPtrsMut {
+  float* p[8];
+};
+
+// one-shot: out[i] = sum_r in_r[i] for every i (each rank reads every peer)
+template <int NP>
+__global__ __launch_bounds__(256) void allreduce_oneshot_f32_kernel(PeerPtrs in, float* __restrict__ out,
+                                                                    int64_t n4, int np_runtime) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int np = NP > 0 ? NP : np_runtime;
+  for (; i < n4; i += stride) {
+    float4 s = reinterpret_cast<const float4*>(in.p[0])[i];
+#pragma unroll
+    for (int r = 1; r < (NP > 0 ? NP : 8); ++r) {
+      if (NP == 0 && r >= np) break;
+      float4 v = reinterpret_cast<const float4*>(in.p[r])[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
+}
+
+// two-shot phase 1 (reduce-scatter): rank `rank` reduces slice [lo, hi) of the
+// float4 index space from every peer and writes the sum into EVERY peer's
+// output buffer (remote writes over xGMI) -> after phase 1 on all ranks plus a
+// cross-device barrier, every output holds the full result.
+__global__ __launch_bounds__(256) void allreduce_twoshot_f32_kernel(PeerPtrs in, PeerPtrsMut out, int np,
+                                                                    int64_t lo, int64_t hi) {
+  int64_t i = lo + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (; i < hi; i += stride) {
+    float4 s = reinterpret_cast<const float4*>(in.p[0])[i];
+    for (int r = 1; r < np; ++r) {
+      float4 v = reinterpret_cast<const float4*>(in.p[r])[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    for (int r = 0; r < np; ++r) reinterpret_cast<float4*>(out.p[r])[i] = s;
+  }
+}
+
+inline int grid_for(int64_t work_items, int per_block, int max_blocks) {
+  int64_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > max_blocks) g = max_blocks;
+  return (int)g;
+}
+
+}  // namespace
+
+// ============================================================== C ABI ====
+
+AVK_API int avk_abi_version() { return 1; }
+
+AVK_API int avk_fill_uniform_f32(float* p, int64_t n, uint64_t seed, float lo, float hi, hipStream_t s) {
+  if (!p || n < 0) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  fill_uniform_f32_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(p, n, seed, lo, hi);
+  return hipGetLastError();
+}
+
+AVK_API int avk_fill_uniform_bf16(void* p, int64_t n, uint64_t seed, float lo, float hi, hipStream_t s) {
+  if (!p || n < 0 || (n % 8) != 0 || ((uintptr_t)p % 16) != 0) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  fill_uniform_bf16_kernel<<<grid_for(n / 8, 256, 8192), 256, 0, s>>>((__bf16*)p, n / 8, seed, lo, hi);
+  return hipGetLastError();
+}
+
+AVK_API int avk_vector_add_f32(const float* a, const float* b, float* c, int64_t n, hipStream_t s) {
+  if (!a || !b || !c || n < 0) return hipErrorInvalidValue;
+  if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16 != 0) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  if (n4 > 0) vector_add_kernel<<<grid_for(n4, 256, 2048), 256, 0, s>>>((const float4*)a, (const float4*)b, (float4*)c, n4);
+  if (n4 * 4 < n) vector_add_tail_kernel<<<1, 64, 0, s>>>(a, b, c, n4 * 4, n);
+  return hipGetLastError();
+}
+
+AVK_API int avk_gemm_bf16_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K,
+                             hipStream_t s) {
+  using namespace gemm;
+  if (!A || !Bt || !C || M <= 0 || N <= 0 || K <= 0) return hipErrorInvalidValue;
+  if (M % BM || N % BN || K % BK) return hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)Bt | (uintptr_t)C) % 16 != 0) return hipErrorInvalidValue;
+  const int nwg = (M / BM) * (N / BN);
+  if (out_f32)
+    gemm_bf16_nt_kernel<true><<<nwg, NTHR, 0, s>>>((const __bf16*)A, (const __bf16*)Bt, C, M, N, K);
+  else
+    gemm_bf16_nt_kernel<false><<<nwg, NTHR, 0, s>>>((const __bf16*)A, (const __bf16*)Bt, C, M, N, K);
+  return hipGetLastError();
+}
+
+// y = X v ; X is [R][C] row-major (bf16 when x_is_bf16, else f32); C % 8 == 0
+AVK_API int avk_gemv_rows(const void* X, int x_is_bf16, const float* v, float* y, int R, int C, hipStream_t s) {
+  if (!X || !v || !y || R <= 0 || C <= 0 || C % 8) return hipErrorInvalidValue;
+  const int blocks = (R + 3) / 4;
+  if (x_is_bf16)
+    gemv_rows_kernel<__bf16><<<blocks, 256, 0, s>>>((const __bf16*)X, v, y, R, C);
+  else
+    gemv_rows_kernel<float><<<blocks, 256, 0, s>>>((const float*)X, v, y, R, C);
+  return hipGetLastError();
+}
+
+// z = X^T v accumulated into z (caller zeroes z); X bf16 [R][C], C % 8 == 0
+AVK_API int avk_gemv_cols_bf16(const void* X, const float* v, float* z, int R, int C, hipStream_t s) {
+  if (!X || !v || !z || R <= 0 || C <= 0 || C % 8 || ((uintptr_t)X % 16)) return hipErrorInvalidValue;
+  const int bx = (C / 8 + 255) / 256;
+  int slices = 256 / bx;
+  if (slices < 1) slices = 1;
+  if (slices > R) slices = R;
+  const int rows_per_slice = (R + slices - 1) / slices;
+  dim3 grid(bx, (R + rows_per_slice - 1) / rows_per_slice);
+  gemv_cols_bf16_kernel<<<grid, 256, 0, s>>>((const __bf16*)X, v, z, R, C, rows_per_slice);
+  return hipGetLastError();
+}
+
+// variant: 0 = plain loads/stores, 1 = nontemporal
+AVK_API int avk_hbm_copy(const void* src, void* dst, int64_t bytes, int num_cus, int variant, hipStream_t s) {
+  if (!src || !dst || bytes <= 0 || bytes % 16 || (((uintptr_t)src | (uintptr_t)dst) % 16)) return hipErrorInvalidValue;
+  const int64_t n = bytes / 16;
+  const int blocks = (num_cus > 0 ? num_cus : 256) * 8;
+  const int g = grid_for(n, 256 * 4, blocks);
+  if (variant == 1)
+    hbm_copy_kernel<4, true><<<g, 256, 0, s>>>((const f32x4*)src, (f32x4*)dst, n);
+  else
+    hbm_copy_kernel<4, false><<<g, 256, 0, s>>>((const f32x4*)src, (f32x4*)dst, n);
+  return hipGetLastError();
+}
+
+AVK_API int avk_checksum(const void* p, int64_t bytes, unsigned long long* out_dev, hipStream_t s) {
+  if (!p || !out_dev || bytes <= 0 || bytes % 16 || ((uintptr_t)p % 16)) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(out_dev, 0, sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  checksum_kernel<<<grid_for(bytes / 16, 256, 4096), 256, 0, s>>>((const uint4*)p, bytes / 16, out_dev);
+  return hipGetLastError();
+}
+
+AVK_API int avk_max_abs_diff_f32(const float* a, const float* b, int64_t n, unsigned int* out_dev, hipStream_t s) {
+  if (!a || !b || !out_dev || n <= 0) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(out_dev, 0, sizeof(unsigned int), s);
+  if (e != hipSuccess) return e;
+  max_abs_diff_kernel<<<grid_for(n, 256, 4096), 256, 0, s>>>(a, b, n, out_dev);
+  return hipGetLastError();
+}
+
+// ptrs: host array of np device pointers (peer-mapped or local); count % 4 == 0
+AVK_API int avk_allreduce_oneshot_f32(const float* const* ptrs, int np, float* out, int64_t count, hipStream_t s) {
+  if (!ptrs || !out || np < 1 || np > 8 || count <= 0 || count % 4) return hipErrorInvalidValue;
+  PeerPtrs pp{};
+  for (int r = 0; r < np; ++r) {
+    if (!ptrs[r] || ((uintptr_t)ptrs[r] % 16)) return hipErrorInvalidValue;
+    pp.p[r] = ptrs[r];
+  }
+  const int64_t n4 = count / 4;
+  const int g = grid_for(n4, 256, 256 * 8);
+  switch (np) {
+    case 2: allreduce_oneshot_f32_kernel<2><<<g, 256, 0, s>>>(pp, out, n4, np); break;
+    case 4: allreduce_oneshot_f32_kernel<4><<<g, 256, 0, s>>>(pp, out, n4, np); break;
+    case 8: allreduce_oneshot_f32_kernel<8><<<g, 256, 0, s>>>(pp, out, n4, np); break;
+    default: allreduce_oneshot_f32_kernel<0><<<g, 256, 0, s>>>(pp, out, n4, np); break;
+  }
+  return hipGetLastError();
+}
+
+// two-shot slice for `rank`: reduce slice of the float4 space, broadcast into all outs
+AVK_API int avk_allreduce_twoshot_f32(const float* const* in_ptrs, float* const* out_ptrs, int np, int rank,
+                                      int64_t count, hipStream_t s) {
+  if (!in_ptrs || !out_ptrs || np < 1 || np > 8 || rank < 0 || rank >= np || count <= 0 || count % 4)
+    return hipErrorInvalidValue;
+  PeerPtrs pi{};
+  PeerPtrsMut po{};
+  for (int r = 0; r < np; ++r) {
+    if (!in_ptrs[r] || !out_ptrs[r]) return hipErrorInvalidValue;
+    pi.p[r] = in_ptrs[r];
+    po.p[r] = out_ptrs[r];
+  }
+  const int64_t n4 = count / 4;
+  const int64_t per = (n4 + np - 1) / np;
+  const int64_t lo = per * rank;
+  const int64_t hi = lo + per < n4 ? lo + per : n4;
+  if (hi <= lo) return hipSuccess;
+  allreduce_twoshot_f32_kernel<<<grid_for(hi - lo, 256, 256 * 8), 256, 0, s>>>(pi, po, np, lo, hi);
+  return hipGetLastError();
+}

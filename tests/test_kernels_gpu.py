@@ -1,0 +1,160 @@
+"""Numerics of the hand-written gfx950 validator kernels vs plain PyTorch fp32.
+
+Every test here runs the native HIP path (``libamdgpu_validator.so``); there is
+no fallback, so a missing library fails the test instead of passing on eager
+PyTorch.
+"""
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from amdgpu_operator.ops import kernels as K  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def test_abi_version():
+    assert K.abi_version() == 1
+
+
+@pytest.mark.parametrize("n", [1, 7, 1024, (1 << 20) + 3])
+def test_vector_add_exact(n):
+    a = torch.randn(n, device=DEV)
+    b = torch.randn(n, device=DEV)
+    if a.data_ptr() % 16 or b.data_ptr() % 16:
+        pytest.skip("allocator returned unaligned block")
+    c = K.vector_add(a, b)
+    assert torch.equal(c, a + b)
+
+
+@pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 320), (1024, 1024, 1024), (2048, 1024, 4096)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_gemm_vs_fp32_reference(shape, out_dtype):
+    M, N, Kd = shape
+    g = torch.Generator(device=DEV).manual_seed(M + N + Kd)
+    a = (torch.rand(M, Kd, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
+    bt = (torch.rand(N, Kd, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
+    ref = a.float() @ bt.float().t()
+    out = K.gemm_bf16_nt(a, bt, out_dtype=out_dtype)
+    err = (out.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    tol = 1e-5 * Kd if out_dtype == torch.float32 else 8e-3 * scale
+    assert err <= tol, (err, tol)
+
+
+def test_gemm_exact_integer_asymmetric():
+    # A = small integers, B asymmetric: a transposed C-write or a swapped
+    # fragment map changes the result; all sums are exact in fp32.
+    M, N, Kd = 512, 256, 128
+    i = torch.arange(M, device=DEV).view(M, 1)
+    k = torch.arange(Kd, device=DEV).view(1, Kd)
+    a = ((i * 3 + k * 7) % 5 - 2).to(torch.bfloat16)
+    n = torch.arange(N, device=DEV).view(N, 1)
+    bt = ((n * 11 + k * 2 + (n > k).long()) % 7 - 3).to(torch.bfloat16)
+    ref = a.double() @ bt.double().t()
+    out = K.gemm_bf16_nt(a, bt, out_dtype=torch.float32)
+    assert torch.equal(out.double(), ref)
+
+
+def test_gemm_identity_asymmetric():
+    N = 256
+    a = torch.eye(N, device=DEV, dtype=torch.bfloat16)
+    bt = (torch.arange(N * N, device=DEV).view(N, N) % 97).to(torch.bfloat16)
+    out = K.gemm_bf16_nt(a, bt, out_dtype=torch.float32)
+    assert torch.equal(out, bt.float().t())
+
+
+def test_gemm_rejects_bad_shapes():
+    a = torch.zeros(100, 64, device=DEV, dtype=torch.bfloat16)
+    bt = torch.zeros(256, 64, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        K.gemm_bf16_nt(a, bt)
+
+
+def test_fill_uniform_deterministic_and_bounded():
+    t1 = K.fill_uniform_(torch.empty(1 << 16, device=DEV), 42, -1, 1)
+    t2 = K.fill_uniform_(torch.empty(1 << 16, device=DEV), 42, -1, 1)
+    assert torch.equal(t1, t2)
+    assert t1.min() >= -1 and t1.max() < 1 and t1.std() > 0.5
+    b = K.fill_uniform_(torch.empty(1 << 16, device=DEV, dtype=torch.bfloat16), 7, 0, 2)
+    assert b.float().min() >= 0 and b.float().max() <= 2
+
+
+def test_gemv_rows_cols():
+    R, C = 384, 512
+    x = (torch.rand(R, C, device=DEV) * 2 - 1).to(torch.bfloat16)
+    v = torch.randn(C, device=DEV)
+    w = torch.randn(R, device=DEV)
+    torch.testing.assert_close(K.gemv_rows(x, v), x.float() @ v, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(K.gemv_cols_bf16(x, w), x.float().t() @ w, rtol=1e-4, atol=1e-3)
+    xf = x.float()
+    torch.testing.assert_close(K.gemv_rows(xf, v), xf @ v, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("nbytes", [16, 4096, 3 << 20, (1 << 26) + 16])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_hbm_copy_and_checksum(nbytes, variant):
+    src = torch.randint(0, 255, (nbytes,), device=DEV, dtype=torch.uint8)
+    dst = torch.zeros_like(src)
+    K.hbm_copy(src, dst, variant=variant)
+    assert torch.equal(src, dst)
+    assert K.checksum(src) == K.checksum(dst)
+    dst[nbytes // 2] ^= 1
+    assert K.checksum(src) != K.checksum(dst)
+
+
+def test_max_abs_diff():
+    a = torch.zeros(10000, device=DEV)
+    b = torch.zeros(10000, device=DEV)
+    b[1234] = -3.5
+    assert K.max_abs_diff(a, b) == 3.5
+    b[5] = float("nan")
+    assert K.max_abs_diff(a, b) == float("inf")
+
+
+@pytest.mark.parametrize("peers", [1, 2, 3, 4, 8])
+def test_allreduce_oneshot_emulated(peers):
+    n = 1 << 18
+    ins = [torch.randn(n, device=DEV) for _ in range(peers)]
+    out = torch.empty(n, device=DEV)
+    K.allreduce_oneshot(ins, out)
+    torch.testing.assert_close(out, torch.stack(ins).sum(0), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("peers", [2, 4, 8])
+def test_allreduce_twoshot_emulated(peers):
+    n = (1 << 16) + 4 * 3
+    ins = [torch.randn(n, device=DEV) for _ in range(peers)]
+    outs = [torch.zeros(n, device=DEV) for _ in range(peers)]
+    for r in range(peers):
+        K.allreduce_twoshot_slice([t.data_ptr() for t in ins], [t.data_ptr() for t in outs], r, n)
+    ref = torch.stack(ins).sum(0)
+    for o in outs:
+        torch.testing.assert_close(o, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_workload_quick_end_to_end():
+    from amdgpu_operator.validator.workload import ValidatorWorkload, WorkloadConfig
+
+    rep = ValidatorWorkload(0, WorkloadConfig.quick()).run()
+    assert rep.ok, rep.as_dict()
+    names = [s.name for s in rep.steps]
+    assert names == list(ValidatorWorkload.STEPS)
+
+
+def test_workload_detects_bad_gemm(monkeypatch):
+    from amdgpu_operator.validator import workload as W
+
+    real = K.gemm_bf16_nt
+
+    def broken(a, bt, out=None, out_dtype=None, stream=None):
+        o = real(a, bt, out=out, out_dtype=out_dtype, stream=stream)
+        o[17, 3:40] += 10.0  # corrupt part of one tile
+        return o
+
+    monkeypatch.setattr(W.K, "gemm_bf16_nt", broken)
+    wl = W.ValidatorWorkload(0, W.WorkloadConfig.quick())
+    with pytest.raises(W.ValidationFailed):
+        wl.step_gemm()

@@ -1,0 +1,122 @@
+"""Micro-benchmarks of the validator kernels vs the vendor libraries.
+
+Interleaved rounds in ONE process (cdna_hip_programming.md §5.4 rule 24), random
+uniform [-1, 1) operands (rule 25).  Prints one JSON document.
+"""
+
+import argparse
+import json
+import statistics
+import time
+
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from amdgpu_operator.ops import kernels as K  # noqa: E402
+
+
+def time_ms(fn, iters):
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def bench_gemm(n, rounds, iters):
+    a = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+    bt = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+    K.fill_uniform_(a, 1)
+    K.fill_uniform_(bt, 2)
+    c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+    c2 = torch.empty_like(c)
+    b = bt.t()
+    ours, lib = [], []
+    for _ in range(3):
+        K.gemm_bf16_nt(a, bt, out=c)
+        torch.matmul(a, b, out=c2)
+    for _ in range(rounds):
+        ours.append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c), iters))
+        lib.append(time_ms(lambda: torch.matmul(a, b, out=c2), iters))
+    fl = 2.0 * n ** 3
+    err = (c.float() - c2.float()).abs().max().item()
+    return {
+        "n": n,
+        "ours_ms_median": statistics.median(ours),
+        "ours_tflops": fl / statistics.median(ours) / 1e9,
+        "ours_tflops_best": fl / min(ours) / 1e9,
+        "hipblaslt_ms_median": statistics.median(lib),
+        "hipblaslt_tflops": fl / statistics.median(lib) / 1e9,
+        "max_abs_diff_vs_hipblaslt": err,
+    }
+
+
+def bench_hbm(nbytes, rounds, iters):
+    src = torch.empty(nbytes // 4, device="cuda")
+    dst = torch.empty_like(src)
+    K.fill_uniform_(src, 3)
+    res = {"bytes": nbytes}
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    arms = {
+        "ours_plain": lambda: K.hbm_copy(src, dst, cus, 0),
+        "ours_nt": lambda: K.hbm_copy(src, dst, cus, 1),
+        "torch_copy": lambda: dst.copy_(src),
+    }
+    samples = {k: [] for k in arms}
+    for fn in arms.values():
+        fn()
+    for _ in range(rounds):
+        for k, fn in arms.items():
+            samples[k].append(time_ms(fn, iters))
+    for k, v in samples.items():
+        res[k + "_gbps"] = 2 * nbytes / statistics.median(v) / 1e6
+    return res
+
+
+def bench_vecadd(n, iters):
+    a = torch.empty(n, device="cuda")
+    b = torch.empty(n, device="cuda")
+    c = torch.empty(n, device="cuda")
+    K.fill_uniform_(a, 1)
+    K.fill_uniform_(b, 2)
+    ms = time_ms(lambda: K.vector_add(a, b, c), iters)
+    ms_t = time_ms(lambda: torch.add(a, b, out=c), iters)
+    return {"n": n, "ours_gbps": 12 * n / ms / 1e6, "torch_gbps": 12 * n / ms_t / 1e6}
+
+
+def bench_oneshot(n, peers, iters):
+    ins = [torch.empty(n, device="cuda") for _ in range(peers)]
+    for i, t in enumerate(ins):
+        K.fill_uniform_(t, i)
+    out = torch.empty(n, device="cuda")
+    ms = time_ms(lambda: K.allreduce_oneshot(ins, out), iters)
+    return {"n": n, "peers": peers, "ms": ms, "read_gbps": (peers + 1) * 4 * n / ms / 1e6}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    args = ap.parse_args()
+    t0 = time.time()
+    out = {"device": torch.cuda.get_device_name(0)}
+    if args.quick:
+        out["gemm"] = [bench_gemm(4096, 2, 5)]
+        out["hbm"] = bench_hbm(1 << 30, 2, 5)
+    else:
+        out["gemm"] = [bench_gemm(n, 5, 10) for n in (4096, 8192)]
+        out["hbm"] = bench_hbm(4 << 30, 5, 5)
+        out["vecadd"] = bench_vecadd(1 << 26, 20)
+        out["oneshot"] = bench_oneshot(1 << 24, 8, 10)
+    out["wall_s"] = time.time() - t0
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
