@@ -1,0 +1,261 @@
+"""Kubernetes client interface used by every component of the operator.
+
+Two implementations with the same methods:
+
+* :class:`LocalClient` - direct calls into :class:`~.fakeapi.FakeApiServer`
+  (unit / integration tests, bench);
+* :class:`RestClient` - the Kubernetes REST API over HTTP(S) (in-cluster
+  service-account config or a kubeconfig), including streaming watches.  It is
+  exercised in tests against the fake server's HTTP front end
+  (:mod:`.httpapi`).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import threading
+from urllib.parse import quote, urlencode
+
+from . import resources as R
+from .fakeapi import AlreadyExists, ApiError, Conflict, FakeApiServer, NotFound
+
+__all__ = ["LocalClient", "RestClient", "ApiError", "NotFound", "AlreadyExists", "Conflict", "apply_object"]
+
+
+class LocalClient:
+    def __init__(self, server: FakeApiServer):
+        self.server = server
+
+    def create(self, obj):
+        return self.server.create(obj)
+
+    def get(self, api_version, kind, name, namespace=None):
+        return self.server.get(api_version, kind, name, namespace)
+
+    def list(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
+        return self.server.list(api_version, kind, namespace, label_selector, field_selector)
+
+    def update(self, obj):
+        return self.server.update(obj)
+
+    def update_status(self, obj):
+        return self.server.update(obj, subresource="status")
+
+    def patch(self, api_version, kind, name, patch, namespace=None, subresource=None):
+        return self.server.patch(api_version, kind, name, patch, namespace, subresource)
+
+    def delete(self, api_version, kind, name, namespace=None):
+        return self.server.delete(api_version, kind, name, namespace)
+
+    def watch(self, api_version, kind, namespace=None, label_selector=None, field_selector=None,
+              resource_version=None, stop: threading.Event | None = None, timeout=None):
+        w = self.server.watch(api_version, kind, namespace, label_selector, field_selector, resource_version)
+        try:
+            yield from w.stream(timeout=timeout, stop=stop)
+        finally:
+            self.server.stop_watch(w)
+
+
+def _raise_for(resp) -> None:
+    if resp.status_code < 400:
+        return
+    try:
+        body = resp.json()
+        reason, msg = body.get("reason", ""), body.get("message", "")
+    except ValueError:
+        reason, msg = "", resp.text[:500]
+    if resp.status_code == 404:
+        raise NotFound(msg)
+    if resp.status_code == 409:
+        raise AlreadyExists(msg) if reason == "AlreadyExists" else Conflict(msg)
+    raise ApiError(resp.status_code, reason or "Error", msg)
+
+
+class RestClient:
+    """Minimal Kubernetes REST client (JSON, merge-patch, streaming watch)."""
+
+    SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+    def __init__(self, base_url: str, token: str | None = None, verify=True, cert=None, timeout: float = 30.0):
+        import requests
+
+        self.base = base_url.rstrip("/")
+        self.session = requests.Session()
+        self.session.verify = verify
+        if cert:
+            self.session.cert = cert
+        if token:
+            self.session.headers["Authorization"] = f"Bearer {token}"
+        self.session.headers["Accept"] = "application/json"
+        self.timeout = timeout
+
+    @classmethod
+    def from_incluster(cls) -> "RestClient":
+        host = os.environ["KUBERNETES_SERVICE_HOST"]
+        port = os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+        with open(os.path.join(cls.SA_DIR, "token")) as f:
+            token = f.read().strip()
+        return cls(f"https://{host}:{port}", token=token, verify=os.path.join(cls.SA_DIR, "ca.crt"))
+
+    @classmethod
+    def from_kubeconfig(cls, path: str | None = None, context: str | None = None) -> "RestClient":
+        import base64
+        import tempfile
+
+        import yaml
+
+        path = path or os.environ.get("KUBECONFIG") or os.path.expanduser("~/.kube/config")
+        with open(path) as f:
+            cfg = yaml.safe_load(f)
+        ctx_name = context or cfg.get("current-context")
+        ctx = next(c["context"] for c in cfg["contexts"] if c["name"] == ctx_name)
+        cluster = next(c["cluster"] for c in cfg["clusters"] if c["name"] == ctx["cluster"])
+        user = next(u["user"] for u in cfg["users"] if u["name"] == ctx["user"])
+
+        def materialise(data_key, file_key, src):
+            if src.get(file_key):
+                return src[file_key]
+            if src.get(data_key):
+                fd, p = tempfile.mkstemp(prefix="kube-")
+                with os.fdopen(fd, "wb") as fh:
+                    fh.write(base64.b64decode(src[data_key]))
+                return p
+            return None
+
+        verify = materialise("certificate-authority-data", "certificate-authority", cluster) or True
+        if cluster.get("insecure-skip-tls-verify"):
+            verify = False
+        cert = None
+        cc = materialise("client-certificate-data", "client-certificate", user)
+        ck = materialise("client-key-data", "client-key", user)
+        if cc and ck:
+            cert = (cc, ck)
+        return cls(cluster["server"], token=user.get("token"), verify=verify, cert=cert)
+
+    # -------------------------------------------------------------- helpers
+    def _url(self, t: R.ResourceType, namespace=None, name=None, sub=None, query=None) -> str:
+        u = self.base + t.path(namespace, quote(name) if name else None)
+        if sub:
+            u += "/" + sub
+        if query:
+            u += "?" + urlencode({k: v for k, v in query.items() if v not in (None, "")})
+        return u
+
+    def create(self, obj):
+        t = R.rtype_of(obj)
+        r = self.session.post(self._url(t, R.ns_of(obj) if t.namespaced else None), data=json.dumps(obj),
+                              headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        _raise_for(r)
+        return r.json()
+
+    def get(self, api_version, kind, name, namespace=None):
+        t = R.rtype(api_version, kind)
+        r = self.session.get(self._url(t, namespace, name), timeout=self.timeout)
+        _raise_for(r)
+        return r.json()
+
+    def list(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
+        t = R.rtype(api_version, kind)
+        if isinstance(label_selector, dict):
+            label_selector = ",".join(f"{k}={v}" for k, v in label_selector.items())
+        r = self.session.get(self._url(t, namespace, query={"labelSelector": label_selector,
+                                                           "fieldSelector": field_selector}), timeout=self.timeout)
+        _raise_for(r)
+        return r.json().get("items", [])
+
+    def update(self, obj):
+        t = R.rtype_of(obj)
+        r = self.session.put(self._url(t, R.ns_of(obj), R.name_of(obj)), data=json.dumps(obj),
+                             headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        _raise_for(r)
+        return r.json()
+
+    def update_status(self, obj):
+        t = R.rtype_of(obj)
+        r = self.session.put(self._url(t, R.ns_of(obj), R.name_of(obj), "status"), data=json.dumps(obj),
+                             headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        _raise_for(r)
+        return r.json()
+
+    def patch(self, api_version, kind, name, patch, namespace=None, subresource=None):
+        t = R.rtype(api_version, kind)
+        r = self.session.patch(self._url(t, namespace, name, subresource), data=json.dumps(patch),
+                               headers={"Content-Type": "application/merge-patch+json"}, timeout=self.timeout)
+        _raise_for(r)
+        return r.json()
+
+    def delete(self, api_version, kind, name, namespace=None):
+        t = R.rtype(api_version, kind)
+        r = self.session.delete(self._url(t, namespace, name), timeout=self.timeout)
+        _raise_for(r)
+
+    def watch(self, api_version, kind, namespace=None, label_selector=None, field_selector=None,
+              resource_version=None, stop: threading.Event | None = None, timeout=None):
+        t = R.rtype(api_version, kind)
+        if isinstance(label_selector, dict):
+            label_selector = ",".join(f"{k}={v}" for k, v in label_selector.items())
+        q = {"watch": "1", "labelSelector": label_selector, "fieldSelector": field_selector,
+             "resourceVersion": resource_version, "timeoutSeconds": int(timeout) if timeout else None}
+        with self.session.get(self._url(t, namespace, query=q), stream=True,
+                              timeout=(self.timeout, None)) as r:
+            _raise_for(r)
+            for line in r.iter_lines():
+                if stop is not None and stop.is_set():
+                    return
+                if not line:
+                    continue
+                ev = json.loads(line)
+                if ev.get("type") == "ERROR":
+                    raise ApiError(int(ev["object"].get("code", 500)), ev["object"].get("reason", ""),
+                                   ev["object"].get("message", ""))
+                yield ev["type"], ev["object"]
+
+
+def contains(live, desired) -> bool:
+    """True when every field of ``desired`` is present with the same value in
+    ``live`` (server-side defaults on ``live`` are ignored)."""
+    if isinstance(desired, dict):
+        if not isinstance(live, dict):
+            return False
+        return all(k in live and contains(live[k], v) for k, v in desired.items())
+    if isinstance(desired, list):
+        if not isinstance(live, list) or len(live) != len(desired):
+            return False
+        return all(contains(a, b) for a, b in zip(live, desired))
+    return live == desired
+
+
+def apply_object(client, obj: dict, field_owner: str = "amd-gpu-operator") -> tuple[dict, str]:
+    """Create or update ``obj`` when the live object no longer contains it.
+
+    Returns ``(object, action)`` with action in {"created", "updated", "unchanged"}.
+    Drift made by someone else (a changed or removed field we own) is reverted:
+    reconcile is level-triggered.  Server-added defaults do not count as drift.
+    """
+    t = R.rtype_of(obj)
+    obj = R.deep(obj)
+    ann = R.meta(obj).setdefault("annotations", {})
+    ann.setdefault("amd.com/managed-by", field_owner)
+    ann["amd.com/last-applied-hash"] = R.spec_hash(obj)
+    try:
+        cur = client.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
+    except NotFound:
+        try:
+            return client.create(obj), "created"
+        except AlreadyExists:
+            cur = client.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
+    desired = {k: v for k, v in obj.items() if k != "status"}
+    if contains(cur, desired):
+        return cur, "unchanged"
+    obj["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
+    # keep fields other controllers own on the live object
+    for k in ("ownerReferences", "finalizers"):
+        if k in cur["metadata"] and k not in obj["metadata"]:
+            obj["metadata"][k] = cur["metadata"][k]
+    try:
+        return client.update(obj), "updated"
+    except Conflict:
+        cur = client.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
+        obj["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
+        return client.update(obj), "updated"

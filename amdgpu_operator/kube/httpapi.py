@@ -1,0 +1,159 @@
+"""HTTP front end for :class:`~.fakeapi.FakeApiServer` with real REST paths.
+
+Serves ``/api/v1/...`` and ``/apis/<group>/<version>/...`` (namespaced and
+cluster-scoped, ``/status`` subresource, ``?watch=1`` streaming JSON lines,
+``labelSelector`` / ``fieldSelector``, merge-patch).  Lets the production
+:class:`~.client.RestClient` be tested end-to-end over HTTP.
+"""
+
+from __future__ import annotations
+
+import json
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from urllib.parse import parse_qs, unquote, urlparse
+
+from . import resources as R
+from .fakeapi import ApiError, FakeApiServer
+
+
+def _parse_path(path: str):
+    """-> (ResourceType, namespace, name, subresource)"""
+    segs = [unquote(s) for s in path.strip("/").split("/") if s]
+    if not segs:
+        raise ApiError(404, "NotFound", path)
+    if segs[0] == "api":
+        group, version, rest = "", segs[1], segs[2:]
+    elif segs[0] == "apis":
+        group, version, rest = segs[1], segs[2], segs[3:]
+    else:
+        raise ApiError(404, "NotFound", path)
+    ns = None
+    if len(rest) >= 2 and rest[0] == "namespaces" and len(rest) > 2:
+        ns, rest = rest[1], rest[2:]
+    if not rest:
+        raise ApiError(404, "NotFound", path)
+    plural = rest[0]
+    name = rest[1] if len(rest) > 1 else None
+    sub = rest[2] if len(rest) > 2 else None
+    t = R.BY_PLURAL.get((group, version, plural))
+    if t is None:
+        raise ApiError(404, "NotFound", f"no resource {group}/{version}/{plural}")
+    return t, ns, name, sub
+
+
+class _Handler(BaseHTTPRequestHandler):
+    server_version = "fake-kube-apiserver/0.1"
+    protocol_version = "HTTP/1.1"
+    api: FakeApiServer  # set on the subclass
+
+    def log_message(self, fmt, *args):  # quiet
+        pass
+
+    def _send(self, code: int, body: dict) -> None:
+        data = json.dumps(body).encode()
+        self.send_response(code)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(data)))
+        self.end_headers()
+        self.wfile.write(data)
+
+    def _error(self, e: ApiError) -> None:
+        self._send(e.code, {"kind": "Status", "apiVersion": "v1", "status": "Failure", "reason": e.reason,
+                            "message": e.message, "code": e.code})
+
+    def _body(self) -> dict:
+        n = int(self.headers.get("Content-Length") or 0)
+        return json.loads(self.rfile.read(n) or b"{}")
+
+    def _dispatch(self, method: str) -> None:
+        u = urlparse(self.path)
+        q = {k: v[-1] for k, v in parse_qs(u.query).items()}
+        try:
+            t, ns, name, sub = _parse_path(u.path)
+            api = self.api
+            if method == "GET" and name is None:
+                if q.get("watch") in ("1", "true"):
+                    return self._watch(t, ns, q)
+                items = api.list(t.api_version, t.kind, ns, q.get("labelSelector"), q.get("fieldSelector"))
+                return self._send(200, {"apiVersion": t.api_version, "kind": t.kind + "List", "items": items,
+                                        "metadata": {"resourceVersion": str(api.resource_version())}})
+            if method == "GET":
+                return self._send(200, api.get(t.api_version, t.kind, name, ns))
+            if method == "POST":
+                obj = self._body()
+                if ns and t.namespaced:
+                    obj.setdefault("metadata", {})["namespace"] = ns
+                return self._send(201, api.create(obj))
+            if method == "PUT":
+                return self._send(200, api.update(self._body(), subresource=sub))
+            if method == "PATCH":
+                return self._send(200, api.patch(t.api_version, t.kind, name, self._body(), ns, subresource=sub))
+            if method == "DELETE":
+                api.delete(t.api_version, t.kind, name, ns)
+                return self._send(200, {"kind": "Status", "apiVersion": "v1", "status": "Success"})
+            raise ApiError(405, "MethodNotAllowed", method)
+        except ApiError as e:
+            self._error(e)
+        except (ValueError, KeyError) as e:
+            self._error(ApiError(400, "BadRequest", str(e)))
+
+    def _watch(self, t, ns, q) -> None:
+        timeout = float(q["timeoutSeconds"]) if q.get("timeoutSeconds") else None
+        w = self.api.watch(t.api_version, t.kind, ns, q.get("labelSelector"), q.get("fieldSelector"),
+                           q.get("resourceVersion"))
+        self.send_response(200)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Transfer-Encoding", "chunked")
+        self.end_headers()
+        try:
+            for etype, obj in w.stream(timeout=timeout, stop=self.server.stopping):
+                line = (json.dumps({"type": etype, "object": obj}) + "\n").encode()
+                self.wfile.write(b"%x\r\n%s\r\n" % (len(line), line))
+                self.wfile.flush()
+            self.wfile.write(b"0\r\n\r\n")
+        except (BrokenPipeError, ConnectionResetError):
+            pass
+        finally:
+            self.api.stop_watch(w)
+            self.close_connection = True
+
+    def do_GET(self):
+        self._dispatch("GET")
+
+    def do_POST(self):
+        self._dispatch("POST")
+
+    def do_PUT(self):
+        self._dispatch("PUT")
+
+    def do_PATCH(self):
+        self._dispatch("PATCH")
+
+    def do_DELETE(self):
+        self._dispatch("DELETE")
+
+
+class HttpApiServer:
+    """Run the fake apiserver on ``127.0.0.1:<port>`` in a background thread."""
+
+    def __init__(self, api: FakeApiServer, host: str = "127.0.0.1", port: int = 0):
+        handler = type("Handler", (_Handler,), {"api": api})
+        self.httpd = ThreadingHTTPServer((host, port), handler)
+        self.httpd.daemon_threads = True
+        self.httpd.stopping = threading.Event()
+        self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True, name="fake-apiserver-http")
+
+    @property
+    def url(self) -> str:
+        h, p = self.httpd.server_address[:2]
+        return f"http://{h}:{p}"
+
+    def start(self) -> "HttpApiServer":
+        self.thread.start()
+        return self
+
+    def stop(self) -> None:
+        self.httpd.stopping.set()
+        self.httpd.shutdown()
+        self.httpd.server_close()

@@ -1,0 +1,547 @@
+// amdgpu-validator: the operator-validator workload as one native process per
+// GPU (one validator pod container per allocated GPU).
+//
+// Reference parity: the reference expects validator pods to end "Completed"
+// (/root/reference/README.md:199); upstream they run CUDA vectorAdd.  This
+// binary runs, on its GPU:
+//   hip     device open, gfx950 check, properties
+//   vecadd  K1, exact host check
+//   gemm    K2 MFMA bf16 GEMM: Freivalds check on an fp32-output pass, timed
+//           bf16 pass, N7 counter gate (MFMA MOPS / busy cycles) when enabled
+//   hbm     K3 streaming copy, checksum-verified bandwidth
+//   xgmi    K4 one-shot all-reduce: emulated peers on 1 GPU, or real peers
+//           (hipIpc-mapped buffers of the other validator ranks, over xGMI)
+//   rccl    ncclAllReduce across all validator ranks of the node (RCCL over
+//           xGMI), exact check + algBW/busBW
+// Ranks of one node rendezvous through files in --rendezvous DIR (the host's
+// validations directory): the RCCL unique id, IPC handles and step barriers.
+// Prints one JSON report; exit status 0 = validated.
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include "avk.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+struct Args {
+  int device = 0;
+  int rank = 0;
+  int world = 1;
+  std::string rendezvous = "/tmp/amdgpu-validator";
+  std::string run_id = "run";
+  std::string steps = "hip,vecadd,gemm,hbm,xgmi,rccl";
+  int gemm_n = 4096;
+  int gemm_iters = 3;
+  long long hbm_bytes = 1ll << 30;
+  long long rccl_elems = 1ll << 24;
+  long long xgmi_elems = 1ll << 22;
+  int emulated_peers = 8;
+  double min_gemm_tflops = 0;
+  double min_hbm_gbps = 0;
+  double timeout_s = 120;
+  bool counter_gate = false;
+  bool any_arch = false;
+  std::string ready_file;
+};
+
+struct Step {
+  std::string name;
+  bool ok = true;
+  double seconds = 0;
+  std::string detail;  // JSON object body (without braces)
+};
+
+#define HIP_OK(x)                                                                      \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define AVK_OK(x)                                                                     \
+  do {                                                                                \
+    int e_ = (x);                                                                     \
+    if (e_ != 0) throw std::runtime_error(std::string(#x) + " rc=" + std::to_string(e_)); \
+  } while (0)
+#define NCCL_OK(x)                                                                    \
+  do {                                                                                \
+    ncclResult_t r_ = (x);                                                            \
+    if (r_ != ncclSuccess) throw std::runtime_error(std::string(#x) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+double secs(Clock::time_point a) { return std::chrono::duration<double>(Clock::now() - a).count(); }
+
+std::string fmt(const char* f, ...) __attribute__((format(printf, 1, 2)));
+std::string fmt(const char* f, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  return buf;
+}
+
+// ------------------------------------------------------------ rendezvous ----
+struct Rendezvous {
+  std::string dir;
+  int rank, world;
+  double timeout_s;
+
+  std::string path(const std::string& name) const { return dir + "/" + name; }
+
+  void publish(const std::string& name, const void* data, size_t n) const {
+    const std::string tmp = path(name + ".tmp." + std::to_string(getpid()));
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) throw std::runtime_error("rendezvous: cannot write " + tmp);
+    fwrite(data, 1, n, f);
+    fclose(f);
+    if (rename(tmp.c_str(), path(name).c_str()) != 0) throw std::runtime_error("rendezvous: rename failed");
+  }
+
+  std::vector<char> fetch(const std::string& name, size_t n) const {
+    auto t0 = Clock::now();
+    for (;;) {
+      FILE* f = fopen(path(name).c_str(), "rb");
+      if (f) {
+        std::vector<char> buf(n);
+        size_t got = fread(buf.data(), 1, n, f);
+        fclose(f);
+        if (got == n) return buf;
+      }
+      if (secs(t0) > timeout_s) throw std::runtime_error("rendezvous: timeout waiting for " + name);
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    }
+  }
+
+  void barrier(const std::string& tag) const {
+    char one = 1;
+    publish("barrier-" + tag + "-" + std::to_string(rank), &one, 1);
+    for (int r = 0; r < world; ++r) fetch("barrier-" + tag + "-" + std::to_string(r), 1);
+  }
+};
+
+// ------------------------------------------------------------------ steps ----
+Step step_hip(const Args& a, hipDeviceProp_t* prop) {
+  auto t0 = Clock::now();
+  Step s{"hip"};
+  HIP_OK(hipSetDevice(a.device));
+  HIP_OK(hipGetDeviceProperties(prop, a.device));
+  HIP_OK(hipFree(nullptr));  // force context creation
+  const bool arch_ok = a.any_arch || strncmp(prop->gcnArchName, "gfx950", 6) == 0;
+  s.ok = arch_ok;
+  s.seconds = secs(t0);
+  s.detail = fmt("\"arch\": \"%s\", \"cus\": %d, \"hbm_bytes\": %zu, \"name\": \"%s\"", prop->gcnArchName,
+                 prop->multiProcessorCount, prop->totalGlobalMem, prop->name);
+  return s;
+}
+
+Step step_vecadd(const Args&, hipStream_t st) {
+  auto t0 = Clock::now();
+  Step s{"vecadd"};
+  const int64_t n = 1 << 24;
+  float *a, *b, *c;
+  HIP_OK(hipMalloc(&a, n * 4));
+  HIP_OK(hipMalloc(&b, n * 4));
+  HIP_OK(hipMalloc(&c, n * 4));
+  AVK_OK(avk_fill_uniform_f32(a, n, 11, -1, 1, st));
+  AVK_OK(avk_fill_uniform_f32(b, n, 12, -1, 1, st));
+  AVK_OK(avk_vector_add_f32(a, b, c, n, st));
+  std::vector<float> ha(n), hb(n), hc(n);
+  HIP_OK(hipMemcpyAsync(ha.data(), a, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(hb.data(), b, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(hc.data(), c, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  int64_t bad = 0;
+  for (int64_t i = 0; i < n; ++i) bad += (hc[i] != ha[i] + hb[i]);
+  (void)hipFree(a);
+  (void)hipFree(b);
+  (void)hipFree(c);
+  s.ok = bad == 0;
+  s.seconds = secs(t0);
+  s.detail = fmt("\"elems\": %lld, \"mismatches\": %lld", (long long)n, (long long)bad);
+  return s;
+}
+
+Step step_gemm(const Args& a, hipStream_t st) {
+  auto t0 = Clock::now();
+  Step s{"gemm"};
+  const int n = a.gemm_n;
+  void *A, *B, *C16;
+  float *C32, *x, *y1, *z, *y2;
+  HIP_OK(hipMalloc(&A, (size_t)n * n * 2));
+  HIP_OK(hipMalloc(&B, (size_t)n * n * 2));
+  HIP_OK(hipMalloc(&C16, (size_t)n * n * 2));
+  HIP_OK(hipMalloc(&C32, (size_t)n * n * 4));
+  HIP_OK(hipMalloc(&x, n * 4));
+  HIP_OK(hipMalloc(&y1, n * 4));
+  HIP_OK(hipMalloc(&y2, n * 4));
+  HIP_OK(hipMalloc(&z, n * 4));
+  AVK_OK(avk_fill_uniform_bf16(A, (int64_t)n * n, 21, -1, 1, st));
+  AVK_OK(avk_fill_uniform_bf16(B, (int64_t)n * n, 22, -1, 1, st));
+  AVK_OK(avk_fill_uniform_f32(x, n, 23, -1, 1, st));
+  // correctness pass (fp32 out) + Freivalds: C x == A (Bt^T x)
+  AVK_OK(avk_gemm_bf16_nt(A, B, C32, 1, n, n, n, st));
+  AVK_OK(avk_gemv_rows(C32, 0, x, y1, n, n, st));
+  HIP_OK(hipMemsetAsync(z, 0, n * 4, st));
+  AVK_OK(avk_gemv_cols_bf16(B, x, z, n, n, st));
+  AVK_OK(avk_gemv_rows(A, 1, z, y2, n, n, st));
+  std::vector<float> h1(n), h2(n);
+  HIP_OK(hipMemcpyAsync(h1.data(), y1, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(h2.data(), y2, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  double err = 0, scale = 1e-30;
+  for (int i = 0; i < n; ++i) {
+    err = std::max(err, (double)std::fabs(h1[i] - h2[i]));
+    scale = std::max(scale, (double)std::fabs(h2[i]));
+  }
+  const double rel = err / scale;
+  const bool numerics_ok = std::isfinite(rel) && rel <= 2e-3;
+  // timed pass (bf16 out), counter gate on the first timed dispatch
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  AVK_OK(avk_gemm_bf16_nt(A, B, C16, 0, n, n, n, st));  // warm
+  const bool gate = a.counter_gate && avk_prof_active();
+  if (gate) avk_prof_arm("gemm_bf16_nt");
+  HIP_OK(hipEventRecord(e0, st));
+  for (int i = 0; i < a.gemm_iters; ++i) AVK_OK(avk_gemm_bf16_nt(A, B, C16, 0, n, n, n, st));
+  HIP_OK(hipEventRecord(e1, st));
+  HIP_OK(hipEventSynchronize(e1));
+  if (gate) avk_prof_disarm();
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= a.gemm_iters;
+  const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
+  std::string gate_json = "\"counter_gate\": \"off\"";
+  bool gate_ok = true;
+  if (a.counter_gate) {
+    if (!gate) {
+      gate_ok = false;
+      gate_json = "\"counter_gate\": \"unavailable\"";
+    } else {
+      HIP_OK(hipDeviceSynchronize());
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      const double mops = avk_prof_value("SQ_INSTS_VALU_MFMA_MOPS_BF16");
+      const double busy = avk_prof_value("SQ_VALU_MFMA_BUSY_CYCLES");
+      const double waves = avk_prof_value("SQ_WAVES");
+      const double gui = avk_prof_value("GRBM_GUI_ACTIVE");
+      const int disp = avk_prof_dispatches();
+      const double flops = 2.0 * n * (double)n * n * disp;
+      gate_ok = disp > 0 && mops > 0 && busy > 0;
+      gate_json = fmt("\"counter_gate\": \"%s\", \"dispatches\": %d, \"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.6g, "
+                      "\"SQ_VALU_MFMA_BUSY_CYCLES\": %.6g, \"SQ_WAVES\": %.6g, \"GRBM_GUI_ACTIVE\": %.6g, "
+                      "\"flop_per_mop\": %.6g",
+                      gate_ok ? "pass" : "fail", disp, mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0);
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) (void)hipFree(p);
+  const bool perf_ok = a.min_gemm_tflops <= 0 || tflops >= a.min_gemm_tflops;
+  s.ok = numerics_ok && gate_ok && perf_ok;
+  s.seconds = secs(t0);
+  s.detail = fmt("\"n\": %d, \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, ", n, rel, ms, tflops) + gate_json;
+  return s;
+}
+
+Step step_hbm(const Args& a, hipStream_t st, int cus) {
+  auto t0 = Clock::now();
+  Step s{"hbm"};
+  const int64_t bytes = a.hbm_bytes;
+  void *src, *dst;
+  unsigned long long* cs;
+  HIP_OK(hipMalloc(&src, bytes));
+  HIP_OK(hipMalloc(&dst, bytes));
+  HIP_OK(hipMalloc(&cs, 16));
+  AVK_OK(avk_fill_uniform_f32((float*)src, bytes / 4, 31, -1, 1, st));
+  AVK_OK(avk_hbm_copy(src, dst, bytes, cus, 1, st));  // warm
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  const int iters = 3;
+  HIP_OK(hipEventRecord(e0, st));
+  for (int i = 0; i < iters; ++i) AVK_OK(avk_hbm_copy(src, dst, bytes, cus, 1, st));
+  HIP_OK(hipEventRecord(e1, st));
+  HIP_OK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= iters;
+  unsigned long long h[2];
+  AVK_OK(avk_checksum(src, bytes, cs, st));
+  HIP_OK(hipMemcpyAsync(&h[0], cs, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  AVK_OK(avk_checksum(dst, bytes, cs, st));
+  HIP_OK(hipMemcpyAsync(&h[1], cs, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(src);
+  (void)hipFree(dst);
+  (void)hipFree(cs);
+  const double gbps = 2.0 * bytes / (ms * 1e-3) / 1e9;
+  s.ok = h[0] == h[1] && (a.min_hbm_gbps <= 0 || gbps >= a.min_hbm_gbps);
+  s.seconds = secs(t0);
+  s.detail = fmt("\"bytes\": %lld, \"ms\": %.4f, \"gbps\": %.1f, \"checksum_match\": %s", (long long)bytes, ms, gbps,
+                 h[0] == h[1] ? "true" : "false");
+  return s;
+}
+
+Step step_xgmi(const Args& a, hipStream_t st, const Rendezvous& rv) {
+  auto t0 = Clock::now();
+  Step s{"xgmi"};
+  const int64_t n = a.xgmi_elems;
+  const int np = a.world > 1 ? a.world : a.emulated_peers;
+  std::vector<float*> local(np, nullptr);  // emulated inputs, or expected-value scratch
+  float *in = nullptr, *out, *expect;
+  HIP_OK(hipMalloc(&out, n * 4));
+  HIP_OK(hipMalloc(&expect, n * 4));
+  std::vector<const float*> ptrs(np);
+  std::vector<hipIpcMemHandle_t> handles(np);
+  if (a.world > 1) {
+    HIP_OK(hipMalloc(&in, n * 4));
+    AVK_OK(avk_fill_uniform_f32(in, n, 1000 + a.rank, -1, 1, st));
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipIpcGetMemHandle(&handles[a.rank], in));
+    rv.publish(a.run_id + "-ipc-" + std::to_string(a.rank), &handles[a.rank], sizeof(hipIpcMemHandle_t));
+    for (int r = 0; r < np; ++r) {
+      if (r == a.rank) {
+        ptrs[r] = in;
+        continue;
+      }
+      auto buf = rv.fetch(a.run_id + "-ipc-" + std::to_string(r), sizeof(hipIpcMemHandle_t));
+      memcpy(&handles[r], buf.data(), sizeof(hipIpcMemHandle_t));
+      void* p = nullptr;
+      HIP_OK(hipIpcOpenMemHandle(&p, handles[r], hipIpcMemLazyEnablePeerAccess));
+      ptrs[r] = (const float*)p;
+    }
+    rv.barrier(a.run_id + "-xgmi-in");
+  } else {
+    for (int r = 0; r < np; ++r) {
+      HIP_OK(hipMalloc(&local[r], n * 4));
+      AVK_OK(avk_fill_uniform_f32(local[r], n, 1000 + r, -1, 1, st));
+      ptrs[r] = local[r];
+    }
+  }
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  HIP_OK(hipEventRecord(e0, st));
+  AVK_OK(avk_allreduce_oneshot_f32(ptrs.data(), np, out, n, st));
+  HIP_OK(hipEventRecord(e1, st));
+  HIP_OK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  // expected value: regenerate every rank's input locally (deterministic fill) and sum
+  float* tmp;
+  HIP_OK(hipMalloc(&tmp, n * 4));
+  HIP_OK(hipMemsetAsync(expect, 0, n * 4, st));
+  for (int r = 0; r < np; ++r) {
+    AVK_OK(avk_fill_uniform_f32(tmp, n, 1000 + r, -1, 1, st));
+    const float* two[2] = {expect, tmp};
+    AVK_OK(avk_allreduce_oneshot_f32(two, 2, expect, n, st));
+  }
+  unsigned int* md;
+  HIP_OK(hipMalloc(&md, 4));
+  AVK_OK(avk_max_abs_diff_f32(out, expect, n, md, st));
+  unsigned int bits = 0;
+  HIP_OK(hipMemcpyAsync(&bits, md, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  float err;
+  memcpy(&err, &bits, 4);
+  if (a.world > 1) {
+    rv.barrier(a.run_id + "-xgmi-out");  // peers finished reading our buffer
+    for (int r = 0; r < np; ++r)
+      if (r != a.rank) (void)hipIpcCloseMemHandle((void*)ptrs[r]);
+    (void)hipFree(in);
+  }
+  for (float* p : local) (void)hipFree(p);
+  (void)hipFree(out);
+  (void)hipFree(expect);
+  (void)hipFree(tmp);
+  (void)hipFree(md);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  s.ok = std::isfinite(err) && err <= 1e-5f * np;
+  s.seconds = secs(t0);
+  s.detail = fmt("\"peers\": %d, \"emulated\": %s, \"elems\": %lld, \"ms\": %.4f, \"read_gbps\": %.1f, \"max_abs_err\": %.3e",
+                 np, a.world > 1 ? "false" : "true", (long long)n, ms, (np * 4.0 * n) / (ms * 1e-3) / 1e9, err);
+  return s;
+}
+
+Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv) {
+  auto t0 = Clock::now();
+  Step s{"rccl"};
+  ncclUniqueId id;
+  const std::string idname = a.run_id + "-nccl-id";
+  if (a.rank == 0) {
+    NCCL_OK(ncclGetUniqueId(&id));
+    rv.publish(idname, &id, sizeof(id));
+  } else {
+    auto buf = rv.fetch(idname, sizeof(id));
+    memcpy(&id, buf.data(), sizeof(id));
+  }
+  auto ti = Clock::now();
+  ncclComm_t comm;
+  NCCL_OK(ncclCommInitRank(&comm, a.world, id, a.rank));
+  const double init_s = secs(ti);
+  const int64_t n = a.rccl_elems;
+  float* buf;
+  HIP_OK(hipMalloc(&buf, n * 4));
+  std::vector<float> host(n, (float)(a.rank + 1));
+  HIP_OK(hipMemcpyAsync(buf, host.data(), n * 4, hipMemcpyHostToDevice, st));
+  NCCL_OK(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
+  HIP_OK(hipMemcpyAsync(host.data(), buf, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  const float expect = a.world * (a.world + 1) / 2.0f;
+  int64_t bad = 0;
+  for (int64_t i = 0; i < n; ++i) bad += host[i] != expect;
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  const int iters = 5;
+  HIP_OK(hipEventRecord(e0, st));
+  for (int i = 0; i < iters; ++i) NCCL_OK(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
+  HIP_OK(hipEventRecord(e1, st));
+  HIP_OK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= iters;
+  NCCL_OK(ncclCommDestroy(comm));
+  (void)hipFree(buf);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  const double algbw = n * 4.0 / (ms * 1e-3) / 1e9;
+  const double busbw = a.world > 1 ? algbw * 2.0 * (a.world - 1) / a.world : 0.0;
+  s.ok = bad == 0;
+  s.seconds = secs(t0);
+  s.detail = fmt("\"world\": %d, \"bytes\": %lld, \"comm_init_s\": %.4f, \"ms\": %.4f, \"algbw_gbps\": %.1f, "
+                 "\"busbw_gbps\": %.1f, \"mismatches\": %lld",
+                 a.world, (long long)(n * 4), init_s, ms, algbw, busbw, (long long)bad);
+  return s;
+}
+
+bool has_step(const Args& a, const char* name) {
+  std::stringstream ss(a.steps);
+  std::string t;
+  while (std::getline(ss, t, ','))
+    if (t == name) return true;
+  return false;
+}
+
+void usage(const char* p) {
+  fprintf(stderr,
+          "usage: %s [--device N] [--rank R --world W --rendezvous DIR --run-id ID] [--steps a,b,...]\n"
+          "          [--gemm N] [--gemm-iters K] [--hbm-bytes B] [--rccl-elems E] [--xgmi-elems E]\n"
+          "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--ready-file PATH]\n",
+          p);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  auto t_start = Clock::now();
+  Args a;
+  for (int i = 1; i < argc; ++i) {
+    std::string k = argv[i];
+    auto v = [&]() -> const char* {
+      if (i + 1 >= argc) {
+        usage(argv[0]);
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (k == "--device") a.device = atoi(v());
+    else if (k == "--rank") a.rank = atoi(v());
+    else if (k == "--world") a.world = atoi(v());
+    else if (k == "--rendezvous") a.rendezvous = v();
+    else if (k == "--run-id") a.run_id = v();
+    else if (k == "--steps") a.steps = v();
+    else if (k == "--gemm") a.gemm_n = atoi(v());
+    else if (k == "--gemm-iters") a.gemm_iters = atoi(v());
+    else if (k == "--hbm-bytes") a.hbm_bytes = atoll(v());
+    else if (k == "--rccl-elems") a.rccl_elems = atoll(v());
+    else if (k == "--xgmi-elems") a.xgmi_elems = atoll(v());
+    else if (k == "--emulated-peers") a.emulated_peers = atoi(v());
+    else if (k == "--min-gemm-tflops") a.min_gemm_tflops = atof(v());
+    else if (k == "--min-hbm-gbps") a.min_hbm_gbps = atof(v());
+    else if (k == "--timeout") a.timeout_s = atof(v());
+    else if (k == "--counter-gate") a.counter_gate = true;
+    else if (k == "--any-arch") a.any_arch = true;
+    else if (k == "--ready-file") a.ready_file = v();
+    else {
+      usage(argv[0]);
+      return 2;
+    }
+  }
+  if (a.world < 1 || a.rank < 0 || a.rank >= a.world || a.gemm_n <= 0 || a.gemm_n % 256 || a.hbm_bytes <= 0 ||
+      a.hbm_bytes % 16 || a.rccl_elems <= 0 || a.xgmi_elems <= 0 || a.xgmi_elems % 4 || a.emulated_peers < 1 ||
+      a.emulated_peers > 8 || a.world > 8) {
+    fprintf(stderr, "amdgpu-validator: invalid arguments (gemm %% 256, sizes %% 16, world <= 8)\n");
+    return 2;
+  }
+  mkdir(a.rendezvous.c_str(), 0755);
+  Rendezvous rv{a.rendezvous, a.rank, a.world, a.timeout_s};
+  std::vector<Step> steps;
+  bool ok = true;
+  std::string error;
+  hipStream_t st = nullptr;
+  hipDeviceProp_t prop;
+  memset(&prop, 0, sizeof(prop));
+  try {
+    steps.push_back(step_hip(a, &prop));
+    ok = steps.back().ok;
+    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
+    if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st)), steps.back().ok);
+    if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
+    if (ok && has_step(a, "xgmi")) ok = (steps.push_back(step_xgmi(a, st, rv)), steps.back().ok);
+    if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, rv)), steps.back().ok);
+  } catch (const std::exception& e) {
+    ok = false;
+    error = e.what();
+  }
+  if (st) (void)hipStreamDestroy(st);
+  const double total = secs(t_start);
+  std::string out = fmt("{\"ok\": %s, \"rank\": %d, \"world\": %d, \"device\": %d, \"seconds\": %.4f, ", ok ? "true" : "false",
+                        a.rank, a.world, a.device, total);
+  if (!error.empty()) {
+    std::string esc;
+    for (char c : error) esc += (c == '"' || c == '\\') ? '\'' : c;
+    out += "\"error\": \"" + esc + "\", ";
+  }
+  out += "\"steps\": [";
+  for (size_t i = 0; i < steps.size(); ++i) {
+    out += fmt("%s{\"name\": \"%s\", \"ok\": %s, \"seconds\": %.4f", i ? ", " : "", steps[i].name.c_str(),
+               steps[i].ok ? "true" : "false", steps[i].seconds);
+    if (!steps[i].detail.empty()) out += ", " + steps[i].detail;
+    out += "}";
+  }
+  out += "]}";
+  puts(out.c_str());
+  fflush(stdout);
+  if (ok && !a.ready_file.empty()) {
+    FILE* f = fopen(a.ready_file.c_str(), "w");
+    if (f) {
+      fprintf(f, "%s\n", out.c_str());
+      fclose(f);
+    }
+  }
+  return ok ? 0 : 1;
+}
