@@ -1,0 +1,328 @@
+"""ClusterPolicy (``amd.com/v1``) spec and the Helm values that produce it.
+
+Reference parity: the reference installs the operator with seven value
+overrides (/root/reference/README.md:104-110)::
+
+    driver.enabled=true  toolkit.enabled=true  devicePlugin.enabled=true
+    nodeStatusExporter.enabled=true  gfd.enabled=true  migManager.enabled=false
+    operator.cleanupCRD=true
+
+The same keys are accepted here with the same meaning (``migManager`` is the
+MI355X partition manager; ``partitionManager`` is accepted as an alias, as is
+``metricsExporter`` for ``dcgmExporter``), plus AMD-specific keys.  Values map
+1:1 onto the ClusterPolicy spec and are validated with
+pydantic; unknown keys are rejected so typos fail the install instead of being
+silently ignored.
+"""
+
+from __future__ import annotations
+
+from typing import Literal
+
+from pydantic import BaseModel, ConfigDict, Field, model_validator
+
+from .. import API_GROUP, API_VERSION, DEFAULT_NAMESPACE, RESOURCE_NAME
+
+DEFAULT_REPOSITORY = "registry.local/amd-gpu-operator"
+DEFAULT_VERSION = "0.1.0"
+ROCM_VERSION = "7.2.0"
+
+
+class _M(BaseModel):
+    model_config = ConfigDict(extra="forbid", populate_by_name=True)
+
+
+class Image(_M):
+    repository: str = DEFAULT_REPOSITORY
+    image: str = ""
+    version: str = DEFAULT_VERSION
+    imagePullPolicy: Literal["Always", "IfNotPresent", "Never"] = "IfNotPresent"
+    imagePullSecrets: list[str] = Field(default_factory=list)
+
+    def ref(self, default_image: str) -> str:
+        return f"{self.repository}/{self.image or default_image}:{self.version}"
+
+
+class Resources(_M):
+    requests: dict[str, str] = Field(default_factory=dict)
+    limits: dict[str, str] = Field(default_factory=dict)
+
+
+class Operand(Image):
+    enabled: bool = True
+    env: list[dict] = Field(default_factory=list)
+    args: list[str] = Field(default_factory=list)
+    resources: Resources = Field(default_factory=Resources)
+
+
+class UpgradePolicy(_M):
+    autoUpgrade: bool = True
+    maxParallelUpgrades: int = 1
+    drainEnabled: bool = True
+    drainTimeoutSeconds: int = 300
+    podDeletionForce: bool = False
+
+
+class DriverSpec(Operand):
+    """amdgpu DKMS + ROCm userspace for gfx950 (README.md:104,212)."""
+
+    image: str = "amd-driver"
+    rocmVersion: str = ROCM_VERSION
+    driverVersion: str = "6.12.12"
+    usePrecompiled: bool = False
+    blacklistAmdgpuInbox: bool = True
+    kernelModuleParams: dict[str, str] = Field(default_factory=dict)
+    startupProbeTimeoutSeconds: int = 600
+    upgradePolicy: UpgradePolicy = Field(default_factory=UpgradePolicy)
+
+
+class CDISpec(_M):
+    enabled: bool = True
+    default: bool = False
+    specDir: str = "/var/run/cdi"
+
+
+class ToolkitSpec(Operand):
+    """OCI hook + CDI spec + containerd patch (README.md:105,210)."""
+
+    image: str = "amd-container-toolkit"
+    installDir: str = "/usr/local/amd"
+    runtime: Literal["containerd", "docker", "crio"] = "containerd"
+    containerdConfig: str = "/etc/containerd/config.toml"
+    containerdSocket: str = "/run/containerd/containerd.sock"
+    runtimeClass: str = "amd"
+    cdi: CDISpec = Field(default_factory=CDISpec)
+    mountRocm: bool = False
+
+
+class DevicePluginSpec(Operand):
+    """kubelet device plugin for amd.com/gpu (README.md:106,211)."""
+
+    image: str = "amd-device-plugin"
+    resourceName: str = RESOURCE_NAME
+    partitionStrategy: Literal["single", "mixed"] = "single"
+    passDeviceSpecs: bool = True
+    cdiAnnotations: bool = False
+    healthPollMs: int = 1000
+
+
+class ServiceMonitor(_M):
+    enabled: bool = False
+    interval: str = "15s"
+    additionalLabels: dict[str, str] = Field(default_factory=dict)
+
+
+class MetricsExporterSpec(Operand):
+    """amd-smi based DCGM-exporter equivalent (README.md:204,213)."""
+
+    image: str = "amd-metrics-exporter"
+    port: int = 9400
+    intervalSeconds: float = 1.0
+    podAttribution: bool = True
+    serviceMonitor: ServiceMonitor = Field(default_factory=ServiceMonitor)
+
+
+class NodeStatusExporterSpec(Operand):
+    """Operand / validation readiness metrics (README.md:107)."""
+
+    image: str = "amd-node-status-exporter"
+    port: int = 8000
+
+
+class GFDSpec(Operand):
+    """GPU feature discovery labels (README.md:108,202,209)."""
+
+    image: str = "gpu-feature-discovery"
+    intervalSeconds: float = 60.0
+    labelPrefix: str = "amd.com"
+
+
+class NFDSpec(Operand):
+    """Node feature discovery (PCI vendor 0x1002 scan)."""
+
+    image: str = "node-feature-discovery"
+    intervalSeconds: float = 60.0
+
+
+class PartitionManagerSpec(Operand):
+    """MIG-manager analog: compute (SPX/DPX/QPX/CPX) + memory (NPS1/NPS2) partitions.
+    Disabled by default, as in the reference (README.md:109)."""
+
+    enabled: bool = False
+    image: str = "amd-partition-manager"
+    defaultComputePartition: Literal["SPX", "DPX", "TPX", "QPX", "CPX"] = "SPX"
+    defaultMemoryPartition: Literal["NPS1", "NPS2", "NPS4", "NPS8"] = "NPS1"
+    configLabel: str = "amd.com/gpu.partition-config"
+    profiles: dict[str, dict[str, str]] = Field(default_factory=lambda: {
+        "all-spx": {"compute": "SPX", "memory": "NPS1"},
+        "all-dpx": {"compute": "DPX", "memory": "NPS2"},
+        "all-qpx": {"compute": "QPX", "memory": "NPS1"},
+        "all-cpx": {"compute": "CPX", "memory": "NPS2"},
+    })
+
+
+class WorkloadSpec(_M):
+    gemmN: int = 4096
+    gemmIters: int = 3
+    hbmBytes: int = 1 << 30
+    rcclElems: int = 1 << 24
+    xgmiElems: int = 1 << 22
+    minGemmTflops: float = 0.0
+    minHbmGbps: float = 0.0
+    counterGate: bool = True
+
+
+class ValidatorSpec(Operand):
+    """Operator validator: driver, toolkit, workload (HIP + MFMA + RCCL), plugin."""
+
+    image: str = "amd-operator-validator"
+    workload: WorkloadSpec = Field(default_factory=WorkloadSpec)
+    pluginValidation: bool = True
+    validationsDir: str = "/run/amd/validations"
+
+
+class OperatorSpec(_M):
+    defaultRuntime: Literal["containerd", "docker", "crio"] = "containerd"
+    runtimeClass: str = "amd"
+    cleanupCRD: bool = False  # README.md:110 sets it true
+    upgradeCRD: bool = True
+    logLevel: Literal["debug", "info", "warning", "error"] = "info"
+    reconcileIntervalSeconds: float = 30.0
+
+
+class DaemonsetsSpec(_M):
+    priorityClassName: str = "system-node-critical"
+    tolerations: list[dict] = Field(default_factory=lambda: [
+        {"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}])
+    labels: dict[str, str] = Field(default_factory=dict)
+    annotations: dict[str, str] = Field(default_factory=dict)
+    updateStrategy: Literal["RollingUpdate", "OnDelete"] = "RollingUpdate"
+    maxUnavailable: str = "1"
+
+
+class ClusterPolicySpec(_M):
+    operator: OperatorSpec = Field(default_factory=OperatorSpec)
+    daemonsets: DaemonsetsSpec = Field(default_factory=DaemonsetsSpec)
+    driver: DriverSpec = Field(default_factory=DriverSpec)
+    toolkit: ToolkitSpec = Field(default_factory=ToolkitSpec)
+    devicePlugin: DevicePluginSpec = Field(default_factory=DevicePluginSpec)
+    dcgmExporter: MetricsExporterSpec = Field(default_factory=MetricsExporterSpec, alias="metricsExporter")
+    nodeStatusExporter: NodeStatusExporterSpec = Field(default_factory=NodeStatusExporterSpec)
+    gfd: GFDSpec = Field(default_factory=GFDSpec)
+    nfd: NFDSpec = Field(default_factory=NFDSpec)
+    migManager: PartitionManagerSpec = Field(default_factory=PartitionManagerSpec, alias="partitionManager")
+    validator: ValidatorSpec = Field(default_factory=ValidatorSpec)
+
+    @model_validator(mode="before")
+    @classmethod
+    def _aliases(cls, data):
+        if isinstance(data, dict):
+            data = dict(data)
+            for alias, key in (("metricsExporter", "dcgmExporter"), ("partitionManager", "migManager")):
+                if alias in data and key in data:
+                    raise ValueError(f"set either {alias} or {key}, not both")
+                if alias in data:
+                    data[key] = data.pop(alias)
+        return data
+
+    @model_validator(mode="after")
+    def _consistency(self):
+        if self.devicePlugin.enabled and not self.driver.enabled and not self.toolkit.enabled:
+            pass  # host-installed driver/toolkit is a supported setup
+        if self.migManager.enabled and self.devicePlugin.partitionStrategy == "single":
+            pass  # partitions are advertised as amd.com/gpu
+        return self
+
+
+# operand state order: each gated on the previous ones
+STATES = [
+    ("pre-requisites", None),
+    ("state-driver", "driver"),
+    ("state-container-toolkit", "toolkit"),
+    ("state-operator-validation", "validator"),
+    ("state-device-plugin", "devicePlugin"),
+    ("state-metrics-exporter", "dcgmExporter"),
+    ("state-node-feature-discovery", "nfd"),
+    ("state-gpu-feature-discovery", "gfd"),
+    ("state-partition-manager", "migManager"),
+    ("state-node-status-exporter", "nodeStatusExporter"),
+]
+
+
+class HelmValues(_M):
+    """Top-level chart values (``deploy/helm/amd-gpu-operator/values.yaml``)."""
+
+    model_config = ConfigDict(extra="allow", populate_by_name=True)
+    namespace: str = DEFAULT_NAMESPACE
+    operator: dict = Field(default_factory=dict)
+
+
+def spec_from_values(values: dict) -> ClusterPolicySpec:
+    """Helm values -> ClusterPolicy spec (chart-only keys are dropped)."""
+    v = dict(values or {})
+    for chart_only in ("namespace", "nameOverride", "fullnameOverride", "crds", "rbac", "serviceAccount",
+                       "operatorImage", "nodeSelector", "podSecurityContext"):
+        v.pop(chart_only, None)
+    op = dict(v.get("operator") or {})
+    for chart_only in ("image", "repository", "version", "imagePullPolicy", "resources", "replicas"):
+        op.pop(chart_only, None)
+    if op or "operator" in v:
+        v["operator"] = op
+    return ClusterPolicySpec.model_validate(v)
+
+
+def parse_set_flags(flags: list[str]) -> dict:
+    """``--set a.b=c`` strings -> nested values dict (bools/ints parsed like Helm)."""
+    out: dict = {}
+    for f in flags:
+        key, _, raw = f.partition("=")
+        val: object = raw
+        if raw in ("true", "false"):
+            val = raw == "true"
+        else:
+            try:
+                val = int(raw)
+            except ValueError:
+                try:
+                    val = float(raw)
+                except ValueError:
+                    val = raw
+        cur = out
+        parts = key.split(".")
+        for p in parts[:-1]:
+            cur = cur.setdefault(p, {})
+        cur[parts[-1]] = val
+    return out
+
+
+def deep_merge(base: dict, over: dict) -> dict:
+    out = dict(base)
+    for k, v in over.items():
+        if isinstance(v, dict) and isinstance(out.get(k), dict):
+            out[k] = deep_merge(out[k], v)
+        else:
+            out[k] = v
+    return out
+
+
+def cluster_policy(name: str = "cluster-policy", spec: ClusterPolicySpec | dict | None = None) -> dict:
+    if isinstance(spec, dict) or spec is None:
+        spec = ClusterPolicySpec.model_validate(spec or {})
+    return {
+        "apiVersion": f"{API_GROUP}/{API_VERSION}",
+        "kind": "ClusterPolicy",
+        "metadata": {"name": name},
+        "spec": spec.model_dump(mode="json", by_alias=False),
+    }
+
+
+# the exact install command of the reference, as values (README.md:101-110)
+REFERENCE_SET_FLAGS = [
+    "driver.enabled=true",
+    "toolkit.enabled=true",
+    "devicePlugin.enabled=true",
+    "nodeStatusExporter.enabled=true",
+    "gfd.enabled=true",
+    "migManager.enabled=false",
+    "operator.cleanupCRD=true",
+]

@@ -1,0 +1,278 @@
+"""Operand sub-commands shared by the real container entry point
+(``amdgpu-operator <cmd>``, :mod:`.main`) and the simulated kubelet.
+
+Each operand is a function of (NodeEnv, parsed args, stop event, ready
+callback): the container entry point passes the process environment and a
+never-set stop event; the simulated cluster passes the simulated node's
+environment and the pod's stop event.
+"""
+
+from __future__ import annotations
+
+import argparse
+import threading
+
+from ..nodeenv import NodeEnv
+from ..utils.logs import get_logger
+
+log = get_logger("amdgpu.operand")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="amdgpu-operator", description="MI355X GPU operator components")
+    sub = p.add_subparsers(dest="cmd", required=True)
+
+    d = sub.add_parser("driver", help="driver DaemonSet containers")
+    d.add_argument("action", choices=["install", "monitor", "prepare-upgrade", "smi"])
+    d.add_argument("--interval", type=float, default=10.0)
+
+    t = sub.add_parser("toolkit", help="container toolkit installer")
+    t.add_argument("action", choices=["install", "uninstall"])
+    t.add_argument("--runtime-class", default=None)
+    t.add_argument("--no-cdi", action="store_true")
+    t.add_argument("--mount-rocm", action="store_true")
+
+    v = sub.add_parser("validate", help="operator-validator steps")
+    v.add_argument("step", choices=["driver", "toolkit", "workload", "plugin", "complete"])
+    v.add_argument("--resource", default="amd.com/gpu")
+    v.add_argument("--timeout", type=float, default=600.0)
+
+    dp = sub.add_parser("device-plugin", help="kubelet device plugin for amd.com/gpu")
+    dp.add_argument("--resource-name", default="amd.com/gpu")
+    dp.add_argument("--partition-strategy", default="single", choices=["single", "mixed"])
+    dp.add_argument("--health-poll-ms", type=int, default=1000)
+    dp.add_argument("--cdi", action="store_true")
+    dp.add_argument("--no-health", action="store_true")
+
+    me = sub.add_parser("metrics-exporter", help="amd-smi metrics exporter (DCGM-exporter equivalent)")
+    me.add_argument("--port", type=int, default=9400)
+    me.add_argument("--interval", type=float, default=1.0)
+    me.add_argument("--pod-attribution", action="store_true")
+    me.add_argument("--dcgm-names", action="store_true")
+    me.add_argument("--fixture", default=None, help="serve an amd-smi metric JSON capture instead of live data")
+
+    ns = sub.add_parser("node-status-exporter", help="validation-status metrics")
+    ns.add_argument("--port", type=int, default=8000)
+
+    nfd = sub.add_parser("nfd", help="node feature discovery (PCI scan)")
+    nfd.add_argument("--interval", type=float, default=60.0)
+    nfd.add_argument("--oneshot", action="store_true")
+
+    gfd = sub.add_parser("gfd", help="GPU feature discovery labels")
+    gfd.add_argument("--interval", type=float, default=60.0)
+    gfd.add_argument("--label-prefix", default="amd.com")
+    gfd.add_argument("--oneshot", action="store_true")
+
+    pm = sub.add_parser("partition-manager", help="compute/memory partition manager")
+    pm.add_argument("--config-label", default="amd.com/gpu.partition-config")
+    pm.add_argument("--default-compute", default="SPX")
+    pm.add_argument("--default-memory", default="NPS1")
+    pm.add_argument("--interval", type=float, default=30.0)
+    return p
+
+
+def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
+    """``validate workload|plugin`` forward unknown args to amdgpu-validator."""
+    known, extra = [], []
+    i = 0
+    while i < len(args):
+        a = args[i]
+        if a in ("--resource", "--timeout"):
+            known += args[i:i + 2]
+            i += 2
+            continue
+        if a.startswith("--") or extra:
+            extra.append(a)
+        else:
+            known.append(a)
+        i += 1
+    return known, extra
+
+
+def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lambda: None,
+                container_env: dict | None = None) -> int:
+    """Run one operand sub-command. Blocks for long-running operands until ``stop``."""
+    cenv = container_env or {}
+    if argv and argv[0] == "validate":
+        known, extra = _split_passthrough(argv[1:])
+        a = build_parser().parse_args(["validate", *known])
+    else:
+        a = build_parser().parse_args(argv)
+        extra = []
+    cmd = a.cmd
+
+    if cmd == "driver":
+        from ..driver import manager as drv
+
+        if a.action == "install":
+            drv.install(env, stop=stop)
+            ready()
+            stop.wait()
+        elif a.action == "monitor":
+            ready()
+            drv.monitor(env, stop, interval=max(env.poll_s, min(a.interval, 10.0)))
+        elif a.action == "prepare-upgrade":
+            drv.prepare_upgrade(env, cenv.get("AMDGPU_DRIVER_VERSION", ""), cenv.get("DRAIN_ENABLED", "true") == "true")
+        else:
+            print(drv.smi_table(env))
+        return 0
+
+    if cmd == "toolkit":
+        from ..toolkit import install as tk
+
+        if a.action == "install":
+            tk.install(env, runtime_class=a.runtime_class or cenv.get("RUNTIME_CLASS", "amd"),
+                       cdi_enabled=not a.no_cdi and cenv.get("CDI_ENABLED", "true") == "true",
+                       mount_rocm=a.mount_rocm or cenv.get("MOUNT_ROCM") == "true")
+            ready()
+            stop.wait()
+        else:
+            tk.uninstall(env)
+        return 0
+
+    if cmd == "validate":
+        from ..validator import validate as V
+
+        if a.step == "driver":
+            V.wait_ready(env, "driver", a.timeout, stop)
+            V.validate_driver(env, a.timeout, stop)
+        elif a.step == "toolkit":
+            V.wait_ready(env, "toolkit", a.timeout, stop)
+        elif a.step == "workload":
+            if V.read_ready(env, "workload") is None:
+                V.validate_workload(env, extra, a.timeout)
+        elif a.step == "plugin":
+            if V.read_ready(env, "plugin") is None:
+                pod_args = _plugin_pod_args(extra)
+                V.validate_plugin(env, a.resource, pod_args=pod_args, timeout=a.timeout, stop=stop)
+        else:
+            V.complete(env)
+            ready()
+            stop.wait()
+        return 0
+
+    if cmd == "device-plugin":
+        from ..deviceplugin.server import DevicePluginManager, PluginConfig
+
+        cfg = PluginConfig(resource_name=a.resource_name, socket_dir=env.device_plugin_dir, sysfs_root=env.sysfs_root(),
+                           cdi_enabled=a.cdi, partition_strategy=a.partition_strategy, health_poll_ms=a.health_poll_ms,
+                           watch_interval_s=max(0.05, min(0.5, env.poll_s * 10)))
+        health = None
+        if not a.no_health and not env.extra.get("no_health"):
+            try:
+                from ..discovery.topology import HealthWatcher
+
+                hw = HealthWatcher()
+                health = hw.poll
+            except Exception as e:  # noqa: BLE001 - no amd-smi (CPU box): serve without health events
+                log.info("health watcher unavailable: %s", e)
+        mgr = DevicePluginManager(cfg, health_poll=health)
+        mgr.start()
+        ready()
+        stop.wait()
+        mgr.stop()
+        return 0
+
+    if cmd == "metrics-exporter":
+        from ..exporter.metrics import FixtureSource, MetricsExporter, MetricsHttpServer, PodAttribution, SmiSource
+
+        source = None
+        if a.fixture:
+            source = FixtureSource(a.fixture)
+        else:
+            try:
+                source = SmiSource()
+            except Exception as e:  # noqa: BLE001
+                fx = env.extra.get("metrics_fixture")
+                if not fx:
+                    raise
+                log.info("amd-smi unavailable (%s); serving fixture", e)
+                source = FixtureSource(fx)
+        attribution = PodAttribution(env.pod_resources_socket) if a.pod_attribution else None
+        ex = MetricsExporter(source, env.node_name, a.interval, attribution, a.dcgm_names)
+        ex.collect_once()
+        port = 0 if env.extra.get("ephemeral_ports") else a.port
+        srv = MetricsHttpServer(ex, "127.0.0.1" if port == 0 else "0.0.0.0", port).start()
+        env.extra.setdefault("ports", {})["metrics-exporter"] = srv.port
+        th = threading.Thread(target=ex.run, daemon=True, name="metrics-collect")
+        th.start()
+        ready()
+        stop.wait()
+        ex.stop()
+        srv.stop()
+        return 0
+
+    if cmd == "node-status-exporter":
+        from ..exporter.metrics import MetricsHttpServer, NodeStatusExporter
+
+        ex = NodeStatusExporter(env.validations_dir, env.node_name)
+        port = 0 if env.extra.get("ephemeral_ports") else a.port
+        srv = MetricsHttpServer(ex, "127.0.0.1" if port == 0 else "0.0.0.0", port).start()
+        env.extra.setdefault("ports", {})["node-status-exporter"] = srv.port
+        ready()
+        stop.wait()
+        srv.stop()
+        return 0
+
+    if cmd in ("nfd", "gfd"):
+        from ..discovery import labels as L
+        from ..discovery import topology
+
+        def once():
+            if cmd == "nfd":
+                L.sync_node_labels(env.client, env.node_name, L.nfd_labels(env.sysfs_root()), (L.NFD_PREFIX + "pci-",))
+            else:
+                gpus = topology.enumerate_gpus(env.sysfs_root())
+                L.sync_node_labels(env.client, env.node_name, L.gfd_labels(gpus, env.sysfs_root(), a.label_prefix),
+                                   (f"{a.label_prefix}/gpu.",))
+
+        once()
+        ready()
+        if a.oneshot:
+            return 0
+        while not stop.wait(max(env.poll_s, min(a.interval, 60.0))):
+            once()
+        return 0
+
+    if cmd == "partition-manager":
+        from ..partition import manager as PM
+
+        backend = env.extra.get("partition_backend") or PM.SmiBackend()
+        default = PM.Profile(a.default_compute, a.default_memory)
+        profiles = env.extra.get("partition_profiles") or {
+            "all-spx": {"compute": "SPX", "memory": "NPS1"}, "all-dpx": {"compute": "DPX", "memory": "NPS2"},
+            "all-qpx": {"compute": "QPX", "memory": "NPS1"}, "all-cpx": {"compute": "CPX", "memory": "NPS2"}}
+        PM.reconcile_node(env, backend, profiles, default, a.config_label)
+        ready()
+        while not stop.wait(max(env.poll_s, min(a.interval, 30.0))):
+            try:
+                PM.reconcile_node(env, backend, profiles, default, a.config_label)
+            except Exception as e:  # noqa: BLE001
+                log.error("partition reconcile failed: %s", e)
+        return 0
+
+    raise SystemExit(f"unknown command {cmd}")
+
+
+def _plugin_pod_args(extra: list[str]) -> list[str]:
+    """Per-pod workload (1 GPU each): quick kernels, no cross-pod collectives."""
+    out = ["--steps", "hip,vecadd,gemm"]
+    if "--gemm" in extra:
+        out += ["--gemm", extra[extra.index("--gemm") + 1]]
+    else:
+        out += ["--gemm", "1024"]
+    return out
+
+
+def run_in_sim(cluster, run, container: dict, argv: list[str], init: bool) -> None:
+    """Simulated kubelet hook: run the operand for ``container`` of ``run``'s pod."""
+    cenv = {e["name"]: e["value"] for e in container.get("env", []) if "value" in e}
+    env = run.node.env
+    env.extra.setdefault("ephemeral_ports", True)
+    env.extra.setdefault("no_health", True)
+
+    def ready():
+        if not init:
+            run.set_ready(container["name"])
+
+    run_operand(env, argv, run.stop, ready, cenv)

@@ -1,0 +1,143 @@
+"""``amdgpu-operator verify``: the reference's manual checks, machine-asserted (C13).
+
+The reference verifies the install by hand (/root/reference/README.md):
+
+=====================================================  =====================================
+reference command                                      assertion here
+=====================================================  =====================================
+kubectl get nodes -o wide (README.md:80)               every node Ready
+kubectl get pods -n gpu-operator-resources (:116,195)   every operand pod Running / Completed
+kubectl get nodes -l nvidia.com/gpu.present=true (:119)  >= 1 node labelled amd.com/gpu.present
+describe nodes | grep Allocatable nvidia.com/gpu (:122)  Allocatable amd.com/gpu > 0 per GPU node
+get pods -A | grep nvidia-driver-daemonset (:132)       driver pods 2/2 Running, 0 restarts
+exec ... -c nvidia-driver-ctr -- nvidia-smi (:152)      amd-driver-ctr present (SMI table via
+                                                        ``amdgpu-operator driver smi``)
+(validator "Completed", :199)                           node labelled amd.com/gpu.validated
+=====================================================  =====================================
+
+Output: one JSON document (``--json``) or a table; exit 0 only if all pass.
+"""
+
+from __future__ import annotations
+
+import json
+from dataclasses import asdict, dataclass, field
+
+from .. import LABEL_PRESENT, RESOURCE_NAME
+from ..kube import resources as R
+
+EXPECTED_OPERANDS = {
+    "amd-driver-daemonset": "driver",
+    "amd-container-toolkit-daemonset": "toolkit",
+    "amd-device-plugin-daemonset": "devicePlugin",
+    "amd-operator-validator": "validator",
+    "gpu-feature-discovery": "gfd",
+    "amd-metrics-exporter": "dcgmExporter",
+    "amd-node-status-exporter": "nodeStatusExporter",
+    "node-feature-discovery-worker": "nfd",
+}
+
+
+@dataclass
+class Check:
+    name: str
+    ok: bool
+    detail: str = ""
+    reference: str = ""
+
+
+@dataclass
+class Report:
+    checks: list[Check] = field(default_factory=list)
+
+    @property
+    def ok(self) -> bool:
+        return all(c.ok for c in self.checks)
+
+    def add(self, name: str, ok: bool, detail: str = "", reference: str = "") -> None:
+        self.checks.append(Check(name, bool(ok), detail, reference))
+
+    def as_dict(self) -> dict:
+        return {"ok": self.ok, "checks": [asdict(c) for c in self.checks]}
+
+    def table(self) -> str:
+        w = max(len(c.name) for c in self.checks) if self.checks else 10
+        lines = [f"{'CHECK'.ljust(w)}  RESULT  DETAIL"]
+        for c in self.checks:
+            lines.append(f"{c.name.ljust(w)}  {'PASS' if c.ok else 'FAIL':6s}  {c.detail}")
+        lines.append(f"overall: {'PASS' if self.ok else 'FAIL'}")
+        return "\n".join(lines)
+
+
+def _pod_ok(p: dict) -> tuple[bool, str]:
+    st = p.get("status") or {}
+    phase = st.get("phase", "Pending")
+    cs = st.get("containerStatuses") or []
+    ready = sum(1 for c in cs if c.get("ready"))
+    restarts = sum(int(c.get("restartCount", 0)) for c in cs)
+    ok = phase == "Succeeded" or (phase == "Running" and ready == len(cs) and len(cs) > 0)
+    return ok, f"{phase} {ready}/{len(cs)} restarts={restarts}"
+
+
+def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> Report:
+    rep = Report()
+    nodes = client.list("v1", "Node")
+    not_ready = [n["metadata"]["name"] for n in nodes
+                 if (R.condition(n, "Ready") or {}).get("status") not in ("True", None)]
+    rep.add("nodes-ready", not not_ready, f"{len(nodes)} node(s), not ready: {not_ready or 'none'}", "README.md:80")
+
+    gpu_nodes = [n for n in nodes if (n["metadata"].get("labels") or {}).get(LABEL_PRESENT) == "true"]
+    rep.add("gpu-nodes-labelled", bool(gpu_nodes), f"{len(gpu_nodes)} node(s) with {LABEL_PRESENT}=true", "README.md:119")
+
+    for n in gpu_nodes:
+        name = n["metadata"]["name"]
+        alloc = ((n.get("status") or {}).get("allocatable") or {}).get(RESOURCE_NAME, "0")
+        try:
+            count = int(alloc)
+        except ValueError:
+            count = 0
+        want = expect_gpus_per_node
+        ok = count > 0 and (want is None or count == want)
+        rep.add(f"allocatable[{name}]", ok, f"{RESOURCE_NAME}={count}" + (f" (expected {want})" if want else ""),
+                "README.md:122")
+        validated = (n["metadata"].get("labels") or {}).get("amd.com/gpu.validated") == "true"
+        rep.add(f"validated[{name}]", validated, "amd.com/gpu.validated=true" if validated else "not validated",
+                "README.md:199")
+
+    pods = client.list("v1", "Pod", namespace)
+    bad = []
+    for p in pods:
+        ok, d = _pod_ok(p)
+        if not ok:
+            bad.append(f"{p['metadata']['name']}: {d}")
+    rep.add("operand-pods-running", bool(pods) and not bad,
+            f"{len(pods)} pod(s) in {namespace}; failing: {bad or 'none'}", "README.md:116,195-207")
+
+    drv = [p for p in pods if p["metadata"]["name"].startswith("amd-driver-daemonset")]
+    drv_ok = bool(drv) or not gpu_nodes
+    details = []
+    for p in drv:
+        ok, d = _pod_ok(p)
+        names = [c["name"] for c in p["spec"].get("containers", [])]
+        drv_ok &= ok and len(names) == 2 and "amd-driver-ctr" in names
+        details.append(f"{p['metadata']['name']} {d} containers={names}")
+    rep.add("driver-daemonset", drv_ok, "; ".join(details) or "no driver pods", "README.md:132-143,152")
+
+    present = {p["metadata"].get("labels", {}).get("app") for p in pods}
+    try:
+        cp = client.list("amd.com/v1", "ClusterPolicy")
+    except Exception:  # noqa: BLE001 - CRD missing
+        cp = []
+    spec = (cp[0].get("spec") if cp else {}) or {}
+    missing = [ds for ds, key in EXPECTED_OPERANDS.items()
+               if (spec.get(key) or {}).get("enabled", True) and gpu_nodes and ds not in present]
+    rep.add("operands-deployed", not missing, f"missing: {missing or 'none'}", "README.md:201-207")
+    state = ((cp[0].get("status") or {}).get("state") if cp else "absent")
+    rep.add("cluster-policy-ready", state == "ready", f"ClusterPolicy state={state}", "README.md:101 (--wait)")
+    return rep
+
+
+def main_verify(client, namespace: str, as_json: bool, expect: int | None) -> int:
+    rep = verify(client, namespace, expect)
+    print(json.dumps(rep.as_dict(), indent=1) if as_json else rep.table())
+    return 0 if rep.ok else 1

@@ -1,0 +1,364 @@
+"""Operand manifests rendered from the ClusterPolicy spec, one bundle per state.
+
+Names follow the reference's operand pods (/root/reference/README.md:132,152,
+184,201-207) with the AMD prefix:
+
+  nvidia-driver-daemonset / nvidia-driver-ctr   -> amd-driver-daemonset / amd-driver-ctr (2/2 containers)
+  nvidia-container-toolkit-daemonset            -> amd-container-toolkit-daemonset
+  nvidia-device-plugin-daemonset                -> amd-device-plugin-daemonset
+  nvidia-dcgm-exporter                          -> amd-metrics-exporter
+  gpu-feature-discovery                         -> gpu-feature-discovery
+  (node status exporter, validator, NFD, MIG mgr)-> amd-node-status-exporter, amd-operator-validator,
+                                                    node-feature-discovery-worker, amd-partition-manager
+
+Every operand container runs the same ``amdgpu-operator`` entry point with a
+sub-command (``amdgpu_operator/cli/main.py``).  GPU operands are scheduled by
+the per-node ``amd.com/gpu.deploy.<operand>=true`` labels the operator sets.
+Ordering between operands is enforced on the node by init containers that
+wait for validation files in the host's ``/run/amd/validations`` directory
+(driver-ready -> toolkit-ready -> workload-ready -> plugin-ready).
+"""
+
+from __future__ import annotations
+
+from ..api.clusterpolicy import ClusterPolicySpec
+
+DEPLOY_LABEL = "amd.com/gpu.deploy.{}"
+APP_LABEL = "app"
+VALIDATIONS_HOST_DIR = "/run/amd/validations"
+
+# state -> (operand key in spec, deploy-label suffix)
+OPERAND_LABELS = {
+    "driver": "driver",
+    "toolkit": "container-toolkit",
+    "validator": "operator-validator",
+    "devicePlugin": "device-plugin",
+    "dcgmExporter": "metrics-exporter",
+    "gfd": "gpu-feature-discovery",
+    "migManager": "partition-manager",
+    "nodeStatusExporter": "node-status-exporter",
+}
+
+
+def owner_ref(cp: dict) -> list[dict]:
+    md = cp["metadata"]
+    return [{"apiVersion": cp["apiVersion"], "kind": cp["kind"], "name": md["name"], "uid": md.get("uid", ""),
+             "controller": True, "blockOwnerDeletion": True}]
+
+
+def _meta(name: str, ns: str | None, labels: dict, owner: list[dict] | None, extra_labels=None, annotations=None):
+    m = {"name": name, "labels": {**labels, **(extra_labels or {})}}
+    if ns:
+        m["namespace"] = ns
+    if owner:
+        m["ownerReferences"] = owner
+    if annotations:
+        m["annotations"] = dict(annotations)
+    return m
+
+
+def _hostpath(name: str, path: str, type_: str = "DirectoryOrCreate") -> dict:
+    return {"name": name, "hostPath": {"path": path, "type": type_}}
+
+
+def _mount(name: str, path: str, ro: bool = False, propagation: str | None = None) -> dict:
+    m = {"name": name, "mountPath": path}
+    if ro:
+        m["readOnly"] = True
+    if propagation:
+        m["mountPropagation"] = propagation
+    return m
+
+
+def _container(name: str, image: str, pull: str, args: list[str], mounts=None, env=None, privileged=False,
+               resources=None, readiness=None, ports=None) -> dict:
+    c = {"name": name, "image": image, "imagePullPolicy": pull, "command": ["amdgpu-operator"], "args": list(args),
+         "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
+                 {"name": "OPERATOR_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}}]
+         + list(env or []),
+         "volumeMounts": list(mounts or [])}
+    if privileged:
+        c["securityContext"] = {"privileged": True}
+    if resources and (resources.get("requests") or resources.get("limits")):
+        c["resources"] = {k: v for k, v in resources.items() if v}
+    if readiness:
+        c["readinessProbe"] = readiness
+    if ports:
+        c["ports"] = ports
+    return c
+
+
+def _wait_init(name: str, image: str, pull: str, what: str, extra_args=()) -> dict:
+    """Init container that blocks until a validation file exists on the host."""
+    return _container(name, image, pull, ["validate", what, *extra_args],
+                      mounts=[_mount("run-amd-validations", VALIDATIONS_HOST_DIR, propagation="HostToContainer"),
+                              _mount("host-sys", "/host/sys", ro=True)],
+                      privileged=True)
+
+
+def _daemonset(spec: ClusterPolicySpec, ns: str, owner, name: str, operand_key: str | None, sa: str,
+               containers: list, init_containers: list = (), volumes: list = (), host_pid: bool = False,
+               host_network: bool = False, node_selector: dict | None = None, extra_labels=None) -> dict:
+    ds = spec.daemonsets
+    labels = {APP_LABEL: name, "app.kubernetes.io/part-of": "amd-gpu-operator",
+              "app.kubernetes.io/managed-by": "amd-gpu-operator"}
+    if node_selector is None:
+        node_selector = {DEPLOY_LABEL.format(OPERAND_LABELS[operand_key]): "true"} if operand_key else {}
+    tmpl_spec = {
+        "serviceAccountName": sa,
+        "priorityClassName": ds.priorityClassName,
+        "tolerations": [dict(t) for t in ds.tolerations],
+        "nodeSelector": node_selector,
+        "hostPID": host_pid,
+        "hostNetwork": host_network,
+        "initContainers": list(init_containers),
+        "containers": list(containers),
+        "volumes": list(volumes),
+    }
+    strategy = {"type": ds.updateStrategy}
+    if ds.updateStrategy == "RollingUpdate":
+        strategy["rollingUpdate"] = {"maxUnavailable": ds.maxUnavailable}
+    return {
+        "apiVersion": "apps/v1",
+        "kind": "DaemonSet",
+        "metadata": _meta(name, ns, labels, owner, {**ds.labels, **(extra_labels or {})}, ds.annotations),
+        "spec": {
+            "selector": {"matchLabels": {APP_LABEL: name}},
+            "updateStrategy": strategy,
+            "template": {"metadata": {"labels": {**labels, **ds.labels}, "annotations": dict(ds.annotations)},
+                         "spec": tmpl_spec},
+        },
+    }
+
+
+def _sa(name: str, ns: str, owner) -> dict:
+    return {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": _meta(name, ns, {APP_LABEL: name}, owner)}
+
+
+def _cluster_role(name: str, rules: list[dict], owner) -> dict:
+    return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+            "metadata": _meta(name, None, {APP_LABEL: name}, owner), "rules": rules}
+
+
+def _cluster_binding(name: str, sa: str, ns: str, owner) -> dict:
+    return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
+            "metadata": _meta(name, None, {APP_LABEL: name}, owner),
+            "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": name},
+            "subjects": [{"kind": "ServiceAccount", "name": sa, "namespace": ns}]}
+
+
+def _service(name: str, ns: str, owner, port: int, port_name: str = "metrics") -> dict:
+    return {"apiVersion": "v1", "kind": "Service",
+            "metadata": _meta(name, ns, {APP_LABEL: name}, owner),
+            "spec": {"selector": {APP_LABEL: name}, "ports": [{"name": port_name, "port": port, "targetPort": port,
+                                                                "protocol": "TCP"}],
+                     "type": "ClusterIP"}}
+
+
+NODE_RW_RULES = [
+    {"apiGroups": [""], "resources": ["nodes"], "verbs": ["get", "list", "watch", "patch", "update"]},
+    {"apiGroups": [""], "resources": ["pods"], "verbs": ["get", "list", "watch", "create", "delete"]},
+    {"apiGroups": [""], "resources": ["events"], "verbs": ["create", "patch"]},
+]
+
+
+# ------------------------------------------------------------------ states ----
+
+def state_prerequisites(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    objs = []
+    rc = spec.operator.runtimeClass
+    if spec.toolkit.enabled and rc:
+        objs.append({"apiVersion": "node.k8s.io/v1", "kind": "RuntimeClass",
+                     "metadata": _meta(rc, None, {APP_LABEL: "amd-gpu-operator"}, owner), "handler": rc})
+    return objs
+
+
+def state_driver(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    d = spec.driver
+    name, sa = "amd-driver-daemonset", "amd-driver"
+    image = d.ref("amd-driver")
+    env = [{"name": "ROCM_VERSION", "value": d.rocmVersion}, {"name": "AMDGPU_DRIVER_VERSION", "value": d.driverVersion},
+           {"name": "AMDGPU_USE_PRECOMPILED", "value": str(d.usePrecompiled).lower()},
+           {"name": "AMDGPU_BLACKLIST_INBOX", "value": str(d.blacklistAmdgpuInbox).lower()},
+           {"name": "AMDGPU_MODULE_PARAMS", "value": " ".join(f"{k}={v}" for k, v in sorted(d.kernelModuleParams.items()))}
+           ] + list(d.env)
+    mounts = [_mount("run-amd", "/run/amd", propagation="Bidirectional"), _mount("host-root", "/host", ro=True,
+                                                                                 propagation="HostToContainer"),
+              _mount("lib-modules", "/lib/modules"), _mount("dev", "/dev"), _mount("host-sys", "/host/sys", ro=True),
+              _mount("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    readiness = {"exec": {"command": ["amdgpu-probe", "--root", "/host", "--ready-file",
+                                      f"{VALIDATIONS_HOST_DIR}/driver-ready"]},
+                 "initialDelaySeconds": 5, "periodSeconds": 10, "failureThreshold": 60}
+    ctr = _container("amd-driver-ctr", image, d.imagePullPolicy, ["driver", "install", *d.args], mounts, env, True,
+                     d.resources.model_dump(), readiness)
+    health = _container("amd-driver-health", image, d.imagePullPolicy, ["driver", "monitor"],
+                        [_mount("host-sys", "/host/sys", ro=True), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)],
+                        privileged=True)
+    init = _container("amd-driver-manager", image, d.imagePullPolicy, ["driver", "prepare-upgrade"],
+                      [_mount("run-amd", "/run/amd")],
+                      [{"name": "DRAIN_ENABLED", "value": str(d.upgradePolicy.drainEnabled).lower()},
+                       {"name": "DRAIN_TIMEOUT_SECONDS", "value": str(d.upgradePolicy.drainTimeoutSeconds)}], True)
+    vols = [_hostpath("run-amd", "/run/amd"), _hostpath("host-root", "/", "Directory"),
+            _hostpath("lib-modules", "/lib/modules"), _hostpath("dev", "/dev", "Directory"),
+            _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
+            _daemonset(spec, ns, owner, name, "driver", sa, [ctr, health], [init], vols, host_pid=True)]
+
+
+def state_toolkit(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    t = spec.toolkit
+    name, sa = "amd-container-toolkit-daemonset", "amd-container-toolkit"
+    image = t.ref("amd-container-toolkit")
+    env = [{"name": "RUNTIME", "value": t.runtime}, {"name": "CONTAINERD_CONFIG", "value": t.containerdConfig},
+           {"name": "CONTAINERD_SOCKET", "value": t.containerdSocket}, {"name": "RUNTIME_CLASS", "value": t.runtimeClass},
+           {"name": "INSTALL_DIR", "value": t.installDir}, {"name": "CDI_ENABLED", "value": str(t.cdi.enabled).lower()},
+           {"name": "CDI_SPEC_DIR", "value": t.cdi.specDir}, {"name": "MOUNT_ROCM", "value": str(t.mountRocm).lower()}
+           ] + list(t.env)
+    mounts = [_mount("containerd-config", "/runtime/config-dir"), _mount("containerd-socket", "/runtime/sock-dir"),
+              _mount("install-dir", t.installDir), _mount("cdi-dir", t.cdi.specDir),
+              _mount("host-sys", "/host/sys", ro=True), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    ctr = _container("amd-container-toolkit-ctr", image, t.imagePullPolicy, ["toolkit", "install", *t.args], mounts, env,
+                     True, t.resources.model_dump())
+    init = _wait_init("driver-validation", image, t.imagePullPolicy, "driver")
+    vols = [_hostpath("containerd-config", t.containerdConfig.rsplit("/", 1)[0]),
+            _hostpath("containerd-socket", t.containerdSocket.rsplit("/", 1)[0]),
+            _hostpath("install-dir", t.installDir), _hostpath("cdi-dir", t.cdi.specDir),
+            _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "toolkit", sa, [ctr], [init], vols, host_pid=True)]
+
+
+def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    v = spec.validator
+    name, sa = "amd-operator-validator", "amd-operator-validator"
+    image = v.ref("amd-operator-validator")
+    w = v.workload
+    wl_args = ["--gemm", str(w.gemmN), "--gemm-iters", str(w.gemmIters), "--hbm-bytes", str(w.hbmBytes),
+               "--rccl-elems", str(w.rcclElems), "--xgmi-elems", str(w.xgmiElems)]
+    if w.minGemmTflops:
+        wl_args += ["--min-gemm-tflops", str(w.minGemmTflops)]
+    if w.minHbmGbps:
+        wl_args += ["--min-hbm-gbps", str(w.minHbmGbps)]
+    if w.counterGate:
+        wl_args += ["--counter-gate"]
+    inits = [_wait_init("driver-validation", image, v.imagePullPolicy, "driver")]
+    if spec.toolkit.enabled:
+        inits.append(_wait_init("toolkit-validation", image, v.imagePullPolicy, "toolkit"))
+    inits.append(_wait_init("workload-validation", image, v.imagePullPolicy, "workload", wl_args))
+    if v.pluginValidation and spec.devicePlugin.enabled:
+        inits.append(_wait_init("plugin-validation", image, v.imagePullPolicy, "plugin",
+                                ["--resource", spec.devicePlugin.resourceName, *wl_args]))
+    ctr = _container("amd-operator-validator", image, v.imagePullPolicy, ["validate", "complete"],
+                     [_mount("run-amd-validations", VALIDATIONS_HOST_DIR)], list(v.env), True,
+                     v.resources.model_dump())
+    vols = [_hostpath("run-amd-validations", VALIDATIONS_HOST_DIR), _hostpath("host-sys", "/sys", "Directory")]
+    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
+            _daemonset(spec, ns, owner, name, "validator", sa, [ctr], inits, vols)]
+
+
+def state_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    p = spec.devicePlugin
+    name, sa = "amd-device-plugin-daemonset", "amd-device-plugin"
+    image = p.ref("amd-device-plugin")
+    args = ["device-plugin", "--resource-name", p.resourceName, "--partition-strategy", p.partitionStrategy,
+            "--health-poll-ms", str(p.healthPollMs)]
+    if spec.toolkit.enabled and spec.toolkit.cdi.enabled and p.cdiAnnotations:
+        args.append("--cdi")
+    ctr = _container("amd-device-plugin", image, p.imagePullPolicy, args + list(p.args),
+                     [_mount("device-plugin", "/var/lib/kubelet/device-plugins"), _mount("host-sys", "/host/sys", ro=True)],
+                     list(p.env), True, p.resources.model_dump())
+    inits = [_wait_init("toolkit-validation", image, p.imagePullPolicy, "toolkit" if spec.toolkit.enabled else "driver")]
+    vols = [_hostpath("device-plugin", "/var/lib/kubelet/device-plugins"), _hostpath("host-sys", "/sys", "Directory"),
+            _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "devicePlugin", sa, [ctr], inits, vols)]
+
+
+def state_metrics_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    m = spec.dcgmExporter
+    name, sa = "amd-metrics-exporter", "amd-metrics-exporter"
+    image = m.ref("amd-metrics-exporter")
+    args = ["metrics-exporter", "--port", str(m.port), "--interval", str(m.intervalSeconds)]
+    if m.podAttribution:
+        args.append("--pod-attribution")
+    ctr = _container("amd-metrics-exporter", image, m.imagePullPolicy, args + list(m.args),
+                     [_mount("pod-resources", "/var/lib/kubelet/pod-resources", ro=True),
+                      _mount("host-sys", "/host/sys", ro=True)], list(m.env), True, m.resources.model_dump(),
+                     ports=[{"name": "metrics", "containerPort": m.port}])
+    inits = [_wait_init("driver-validation", image, m.imagePullPolicy, "driver")]
+    vols = [_hostpath("pod-resources", "/var/lib/kubelet/pod-resources"), _hostpath("host-sys", "/sys", "Directory"),
+            _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    objs = [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "dcgmExporter", sa, [ctr], inits, vols),
+            _service(name, ns, owner, m.port)]
+    if m.serviceMonitor.enabled:
+        objs.append({"apiVersion": "monitoring.coreos.com/v1", "kind": "ServiceMonitor",
+                     "metadata": _meta(name, ns, {APP_LABEL: name}, owner, m.serviceMonitor.additionalLabels),
+                     "spec": {"selector": {"matchLabels": {APP_LABEL: name}},
+                              "endpoints": [{"port": "metrics", "interval": m.serviceMonitor.interval}]}})
+    return objs
+
+
+def state_nfd(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    n = spec.nfd
+    name, sa = "node-feature-discovery-worker", "node-feature-discovery"
+    image = n.ref("node-feature-discovery")
+    ctr = _container("nfd-worker", image, n.imagePullPolicy, ["nfd", "--interval", str(n.intervalSeconds)],
+                     [_mount("host-sys", "/host/sys", ro=True)], list(n.env), False, n.resources.model_dump())
+    vols = [_hostpath("host-sys", "/sys", "Directory")]
+    # runs on every node: it is what identifies the GPU nodes in the first place
+    ds = _daemonset(spec, ns, owner, name, None, sa, [ctr], [], vols, node_selector={})
+    ds["spec"]["template"]["spec"]["tolerations"].append({"operator": "Exists"})
+    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner), ds]
+
+
+def state_gfd(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    g = spec.gfd
+    name, sa = "gpu-feature-discovery", "gpu-feature-discovery"
+    image = g.ref("gpu-feature-discovery")
+    ctr = _container("gpu-feature-discovery", image, g.imagePullPolicy,
+                     ["gfd", "--interval", str(g.intervalSeconds), "--label-prefix", g.labelPrefix] + list(g.args),
+                     [_mount("host-sys", "/host/sys", ro=True)], list(g.env), False, g.resources.model_dump())
+    inits = [_wait_init("driver-validation", image, g.imagePullPolicy, "driver")]
+    vols = [_hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
+            _daemonset(spec, ns, owner, name, "gfd", sa, [ctr], inits, vols)]
+
+
+def state_partition_manager(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    p = spec.migManager
+    name, sa = "amd-partition-manager", "amd-partition-manager"
+    image = p.ref("amd-partition-manager")
+    ctr = _container("amd-partition-manager", image, p.imagePullPolicy,
+                     ["partition-manager", "--config-label", p.configLabel, "--default-compute",
+                      p.defaultComputePartition, "--default-memory", p.defaultMemoryPartition] + list(p.args),
+                     [_mount("host-sys", "/host/sys"), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)],
+                     list(p.env), True, p.resources.model_dump())
+    inits = [_wait_init("driver-validation", image, p.imagePullPolicy, "driver")]
+    vols = [_hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
+            _daemonset(spec, ns, owner, name, "migManager", sa, [ctr], inits, vols, host_pid=True)]
+
+
+def state_node_status_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    n = spec.nodeStatusExporter
+    name, sa = "amd-node-status-exporter", "amd-node-status-exporter"
+    image = n.ref("amd-node-status-exporter")
+    ctr = _container("amd-node-status-exporter", image, n.imagePullPolicy,
+                     ["node-status-exporter", "--port", str(n.port)] + list(n.args),
+                     [_mount("run-amd-validations", VALIDATIONS_HOST_DIR, ro=True)], list(n.env), False,
+                     n.resources.model_dump(), ports=[{"name": "metrics", "containerPort": n.port}])
+    vols = [_hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "nodeStatusExporter", sa, [ctr], [], vols),
+            _service(name, ns, owner, n.port)]
+
+
+STATE_BUILDERS = {
+    "pre-requisites": state_prerequisites,
+    "state-driver": state_driver,
+    "state-container-toolkit": state_toolkit,
+    "state-operator-validation": state_validator,
+    "state-device-plugin": state_device_plugin,
+    "state-metrics-exporter": state_metrics_exporter,
+    "state-node-feature-discovery": state_nfd,
+    "state-gpu-feature-discovery": state_gfd,
+    "state-partition-manager": state_partition_manager,
+    "state-node-status-exporter": state_node_status_exporter,
+}

@@ -1,0 +1,78 @@
+"""GPU node detection and operand deploy labels.
+
+Reference parity: GPU nodes carry ``nvidia.com/gpu.present=true``
+(/root/reference/README.md:119) - set by the operator from NFD's PCI labels.
+Here: a node is an AMD GPU node when NFD (ours or upstream) reports PCI vendor
+``0x1002`` with a display / processing-accelerator class, or when the node
+already advertises ``amd.com/gpu``.  GPU nodes get ``amd.com/gpu.present=true``
+and one ``amd.com/gpu.deploy.<operand>`` label per operand; a user-set
+``false`` deploy label opts a node out of that operand and is preserved.
+"""
+
+from __future__ import annotations
+
+from .. import LABEL_PRESENT, RESOURCE_NAME
+from ..api.clusterpolicy import ClusterPolicySpec
+from .manifests import DEPLOY_LABEL, OPERAND_LABELS
+
+NFD_PCI_LABELS = (
+    "feature.node.kubernetes.io/pci-1002.present",       # vendor only
+    "feature.node.kubernetes.io/pci-1200_1002.present",  # processing accelerator (MI series)
+    "feature.node.kubernetes.io/pci-0380_1002.present",  # display controller
+    "feature.node.kubernetes.io/pci-0300_1002.present",  # VGA
+)
+
+
+def is_gpu_node(node: dict) -> bool:
+    labels = node.get("metadata", {}).get("labels") or {}
+    if any(labels.get(k) == "true" for k in NFD_PCI_LABELS):
+        return True
+    cap = (node.get("status") or {}).get("capacity") or {}
+    try:
+        if int(cap.get(RESOURCE_NAME, "0")) > 0:
+            return True
+    except ValueError:
+        pass
+    return labels.get(LABEL_PRESENT) == "true" and labels.get("amd.com/gpu.present.source") == "manual"
+
+
+def desired_labels(node: dict, spec: ClusterPolicySpec) -> dict:
+    """Label patch (value None = remove) for one node."""
+    labels = node.get("metadata", {}).get("labels") or {}
+    patch: dict = {}
+    gpu = is_gpu_node(node)
+    if gpu:
+        if labels.get(LABEL_PRESENT) != "true":
+            patch[LABEL_PRESENT] = "true"
+        for key, suffix in OPERAND_LABELS.items():
+            lbl = DEPLOY_LABEL.format(suffix)
+            enabled = getattr(spec, key).enabled
+            if not enabled:
+                if lbl in labels:
+                    patch[lbl] = None
+                continue
+            if labels.get(lbl) == "false":
+                continue  # user opt-out is sticky
+            if labels.get(lbl) != "true":
+                patch[lbl] = "true"
+    else:
+        if LABEL_PRESENT in labels and labels.get("amd.com/gpu.present.source") != "manual":
+            patch[LABEL_PRESENT] = None
+        for suffix in OPERAND_LABELS.values():
+            lbl = DEPLOY_LABEL.format(suffix)
+            if lbl in labels:
+                patch[lbl] = None
+    return patch
+
+
+def label_nodes(client, spec: ClusterPolicySpec) -> tuple[int, int]:
+    """Apply GPU/deploy labels to every node. Returns (gpu_nodes, patched)."""
+    gpu_nodes = patched = 0
+    for node in client.list("v1", "Node"):
+        if is_gpu_node(node):
+            gpu_nodes += 1
+        patch = desired_labels(node, spec)
+        if patch:
+            client.patch("v1", "Node", node["metadata"]["name"], {"metadata": {"labels": patch}})
+            patched += 1
+    return gpu_nodes, patched

@@ -1,0 +1,271 @@
+"""ClusterPolicy reconciler: the operator controller.
+
+Reference parity: ``helm install --wait gpu-operator`` starts the operator,
+which turns the ClusterPolicy (values at /root/reference/README.md:104-110)
+into operand DaemonSets and labels GPU nodes (README.md:119); the reference
+then checks that every operand pod is Running/Completed (README.md:199-207).
+
+Behaviour (level-triggered, idempotent, resumable from any point - all state
+lives in Kubernetes objects):
+
+1. pick the active ClusterPolicy (oldest; others are marked ``ignored``);
+2. validate the spec (pydantic) - an invalid spec sets ``state=error``;
+3. label nodes (``amd.com/gpu.present``, ``amd.com/gpu.deploy.<operand>``);
+4. walk the ordered states, applying every enabled state's manifests (drift
+   is reverted) and deleting disabled states' objects; a state is ready when
+   all of its DaemonSets report every scheduled pod ready and updated;
+5. write ``status``: ``state`` (ready / notReady / error), per-state readiness,
+   conditions, and per-state time-to-ready spans since the policy was created
+   (the time-to-Ready breakdown of SURVEY.md §5.1).
+
+Dependencies between operands are enforced on the node by the operands' init
+containers, not by the reconciler, so every state is applied on every pass
+(same as the upstream controller stepping through all states).
+"""
+
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+
+from pydantic import ValidationError
+
+from .. import API_GROUP, API_VERSION
+from ..api.clusterpolicy import STATES, ClusterPolicySpec
+from ..kube import resources as R
+from ..kube.client import NotFound, apply_object
+from ..utils.logs import get_logger
+from .manifests import STATE_BUILDERS, owner_ref
+from .nodes import label_nodes
+
+CP_API = f"{API_GROUP}/{API_VERSION}"
+log = get_logger("amdgpu.operator")
+
+
+@dataclass
+class StateResult:
+    name: str
+    enabled: bool
+    ready: bool
+    objects: int = 0
+    changed: int = 0
+    detail: str = ""
+
+
+@dataclass
+class ReconcileResult:
+    policy: str | None
+    state: str
+    states: list[StateResult] = field(default_factory=list)
+    gpu_nodes: int = 0
+    seconds: float = 0.0
+
+    @property
+    def ready(self) -> bool:
+        return self.state == "ready"
+
+
+def daemonset_ready(ds: dict) -> tuple[bool, str]:
+    st = ds.get("status") or {}
+    desired = int(st.get("desiredNumberScheduled", 0))
+    ready = int(st.get("numberReady", 0))
+    updated = int(st.get("updatedNumberScheduled", desired))
+    if "observedGeneration" not in st:
+        return False, "not yet observed by the DaemonSet controller"
+    gen_ok = int(st["observedGeneration"]) >= int(ds["metadata"].get("generation", 1))
+    ok = gen_ok and ready >= desired and updated >= desired
+    return ok, f"{ready}/{desired} ready"
+
+
+class ClusterPolicyReconciler:
+    def __init__(self, client, namespace: str, clock=time.time):
+        self.client = client
+        self.namespace = namespace
+        self.clock = clock
+        self._ready_at: dict[str, dict[str, float]] = {}  # policy uid -> state -> seconds since creation
+        self._created_at: dict[str, float] = {}
+        self.reconciles = 0
+
+    # ------------------------------------------------------------------ helpers
+    def _active_policy(self) -> dict | None:
+        cps = self.client.list(CP_API, "ClusterPolicy")
+        if not cps:
+            return None
+        cps.sort(key=lambda c: (c["metadata"].get("creationTimestamp", ""), int(c["metadata"].get("resourceVersion", 0))))
+        active = cps[0]
+        for other in cps[1:]:
+            if (other.get("status") or {}).get("state") != "ignored":
+                other["status"] = {"state": "ignored", "message": f"only {active['metadata']['name']} is reconciled"}
+                try:
+                    self.client.update_status(other)
+                except Exception as e:  # noqa: BLE001
+                    log.warning("status update of ignored policy failed: %s", e)
+        return active
+
+    def _delete_objects(self, objs: list[dict]) -> int:
+        n = 0
+        for o in objs:
+            t = R.rtype_of(o)
+            try:
+                self.client.delete(t.api_version, t.kind, R.name_of(o), R.ns_of(o) if t.namespaced else None)
+                n += 1
+            except NotFound:
+                pass
+        return n
+
+    # ---------------------------------------------------------------- reconcile
+    def reconcile(self) -> ReconcileResult:
+        t0 = time.perf_counter()
+        self.reconciles += 1
+        cp = self._active_policy()
+        if cp is None:
+            return ReconcileResult(None, "absent")
+        uid = cp["metadata"].get("uid", cp["metadata"]["name"])
+        if uid not in self._created_at:
+            self._created_at[uid] = self.clock()
+        try:
+            spec = ClusterPolicySpec.model_validate(cp.get("spec") or {})
+        except ValidationError as e:
+            msg = str(e).splitlines()[0] if str(e) else "invalid spec"
+            self._write_status(cp, "error", [], 0, error=msg)
+            return ReconcileResult(cp["metadata"]["name"], "error", seconds=time.perf_counter() - t0)
+
+        gpu_nodes, patched = label_nodes(self.client, spec)
+        owner = owner_ref(cp)
+        results: list[StateResult] = []
+        for state, key in STATES:
+            enabled = key is None or getattr(spec, key).enabled
+            objs = STATE_BUILDERS[state](spec, self.namespace, owner)
+            if not enabled:
+                self._delete_objects(objs)
+                results.append(StateResult(state, False, True, 0, 0, "disabled"))
+                continue
+            changed = 0
+            ready = True
+            detail = []
+            for o in objs:
+                live, action = apply_object(self.client, o)
+                changed += action != "unchanged"
+                if o["kind"] == "DaemonSet":
+                    ok, d = daemonset_ready(live)
+                    gpu_scoped = bool(o["spec"]["template"]["spec"].get("nodeSelector"))
+                    if ok and gpu_scoped and gpu_nodes > 0 and int((live.get("status") or {}).get(
+                            "desiredNumberScheduled", 0)) == 0:
+                        ok, d = False, "not yet scheduled on the GPU nodes"
+                    ready &= ok
+                    detail.append(f"{o['metadata']['name']}: {d}")
+            results.append(StateResult(state, True, ready, len(objs), changed, "; ".join(detail)))
+            if ready and (gpu_nodes == 0 or not patched):
+                self._ready_at.setdefault(uid, {}).setdefault(state, self.clock() - self._created_at[uid])
+
+        overall = "ready" if all(r.ready for r in results) else "notReady"
+        if overall == "ready" and patched:
+            overall = "notReady"  # node labels just changed: DaemonSet status is stale
+        if overall == "ready" and spec.validator.enabled and gpu_nodes:
+            from ..validator.validate import VALIDATED_LABEL
+            from .nodes import is_gpu_node
+
+            pending = [n["metadata"]["name"] for n in self.client.list("v1", "Node")
+                       if is_gpu_node(n) and (n["metadata"].get("labels") or {}).get(VALIDATED_LABEL) != "true"]
+            if pending:
+                overall = "notReady"
+        self._write_status(cp, overall, results, gpu_nodes)
+        res = ReconcileResult(cp["metadata"]["name"], overall, results, gpu_nodes, time.perf_counter() - t0)
+        log.debug("reconciled %s: %s (%.3fs)", res.policy, overall, res.seconds)
+        return res
+
+    def _write_status(self, cp: dict, state: str, results: list[StateResult], gpu_nodes: int, error: str = "") -> None:
+        uid = cp["metadata"].get("uid", cp["metadata"]["name"])
+        try:
+            live = self.client.get(CP_API, "ClusterPolicy", cp["metadata"]["name"])
+        except NotFound:
+            return
+        status = dict(live.get("status") or {})
+        before = R.deep(status)
+        status["state"] = state
+        status["namespace"] = self.namespace
+        status["gpuNodes"] = gpu_nodes
+        status["states"] = {r.name: ("disabled" if not r.enabled else "ready" if r.ready else "notReady")
+                            for r in results}
+        spans = self._ready_at.get(uid, {})
+        if spans:
+            status["stateReadySeconds"] = {k: round(v, 4) for k, v in spans.items()}
+        if state == "ready" and "timeToReadySeconds" not in status and uid in self._created_at:
+            status["timeToReadySeconds"] = round(self.clock() - self._created_at[uid], 4)
+        now = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+        not_ready = [r.name for r in results if r.enabled and not r.ready]
+        R.set_condition(status, "Ready", state == "ready", "Reconciled" if state == "ready" else
+                        ("Error" if state == "error" else "OperandNotReady"),
+                        error or (f"waiting for {', '.join(not_ready)}" if not_ready else "all operands ready"), now)
+        R.set_condition(status, "Error", state == "error", "ReconcileFailed" if error else "NoError", error, now)
+        if status == before:
+            return
+        live["status"] = status
+        try:
+            self.client.update_status(live)
+        except Exception as e:  # noqa: BLE001 - next pass retries
+            log.warning("status update failed: %s", e)
+
+    # ------------------------------------------------------------------- loop
+    def run(self, stop: threading.Event, resync_s: float = 30.0, debounce_s: float = 0.02,
+            on_result=None) -> None:
+        """Watch-driven loop: ClusterPolicy, Node, DaemonSet and Pod events in the
+        operand namespace trigger a (debounced) reconcile; plus periodic resync."""
+        events: queue.Queue = queue.Queue()
+        watches = [(CP_API, "ClusterPolicy", None), ("v1", "Node", None), ("apps/v1", "DaemonSet", self.namespace)]
+        threads = []
+        for av, kind, ns in watches:
+            th = threading.Thread(target=self._pump, args=(av, kind, ns, events, stop), daemon=True,
+                                  name=f"operator-watch-{kind}")
+            th.start()
+            threads.append(th)
+        events.put("start")
+        last = 0.0
+        while not stop.is_set():
+            try:
+                events.get(timeout=min(resync_s, 0.5))
+            except queue.Empty:
+                if time.monotonic() - last < resync_s:
+                    continue
+            time.sleep(debounce_s)
+            while True:  # coalesce bursts
+                try:
+                    events.get_nowait()
+                except queue.Empty:
+                    break
+            try:
+                res = self.reconcile()
+            except Exception as e:  # noqa: BLE001 - keep the controller alive
+                log.exception("reconcile failed: %s", e)
+                stop.wait(0.5)
+                continue
+            last = time.monotonic()
+            if on_result is not None:
+                on_result(res)
+
+    def _pump(self, av, kind, ns, events: queue.Queue, stop: threading.Event) -> None:
+        while not stop.is_set():
+            try:
+                for _etype, _obj in self.client.watch(av, kind, namespace=ns, stop=stop):
+                    events.put(kind)
+            except Exception as e:  # noqa: BLE001 - re-establish the watch
+                log.debug("watch %s ended: %s", kind, e)
+                stop.wait(0.5)
+
+
+def cleanup_crd(client, crd_name: str = f"clusterpolicies.{API_GROUP}") -> bool:
+    """Helm pre-delete hook (``operator.cleanupCRD``, README.md:110): delete the
+    ClusterPolicy objects, then the CRD.  Returns True if the CRD existed."""
+    for cp in client.list(CP_API, "ClusterPolicy"):
+        try:
+            client.delete(CP_API, "ClusterPolicy", cp["metadata"]["name"])
+        except NotFound:
+            pass
+    try:
+        client.delete("apiextensions.k8s.io/v1", "CustomResourceDefinition", crd_name)
+        return True
+    except NotFound:
+        return False

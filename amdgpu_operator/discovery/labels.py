@@ -1,0 +1,157 @@
+"""Node feature discovery (C7) and GPU feature discovery (C6) labels.
+
+Reference parity: ``gpu-feature-discovery`` "detects GPUs and labels nodes
+that have them" (/root/reference/README.md:108,202,209); GPU nodes are then
+selected by label (README.md:119).  Upstream GFD depends on NFD's PCI labels;
+here both are implemented natively over the same sysfs view:
+
+* NFD-lite: ``feature.node.kubernetes.io/pci-<class>_<vendor>.present`` (the
+  NFD default device label fields) and ``pci-1002.present`` for every AMD
+  display / processing-accelerator PCI function, plus
+  ``kernel-loadedmodule.amdgpu`` when the module is live.
+* GFD: the MI355X capability set - product, CDNA4 family, gfx950 arch, device
+  count, HBM per device, CUs/XCCs/LDS, MFMA data types (bf16, fp16, OCP fp8,
+  fp6, fp4, f32, f64; no xf32 on gfx950), xGMI hive and link count, compute /
+  memory partition mode, driver and ROCm versions.
+"""
+
+from __future__ import annotations
+
+import os
+import re
+
+from .topology import GpuDevice
+
+NFD_PREFIX = "feature.node.kubernetes.io/"
+AMD_VENDOR = "1002"
+GPU_CLASSES = ("1200", "0380", "0300")  # processing accelerator, display, VGA
+
+PRODUCTS = {
+    0x75A3: "AMD-Instinct-MI355X",
+    0x75A0: "AMD-Instinct-MI350X",
+    0x74A1: "AMD-Instinct-MI300X",
+    0x74A5: "AMD-Instinct-MI325X",
+}
+FAMILIES = {"gfx950": "CDNA4", "gfx942": "CDNA3", "gfx90a": "CDNA2", "gfx908": "CDNA"}
+MFMA_TYPES = {
+    "CDNA4": {"bf16": True, "fp16": True, "fp8": True, "fp6": True, "fp4": True, "fp32": True, "fp64": True,
+              "int8": True, "xf32": False},
+    "CDNA3": {"bf16": True, "fp16": True, "fp8": True, "fp6": False, "fp4": False, "fp32": True, "fp64": True,
+              "int8": True, "xf32": True},
+}
+# labels the operator owns (never removed by the GFD sweep)
+OPERATOR_OWNED = ("amd.com/gpu.present", "amd.com/gpu.deploy.", "amd.com/gpu.validated",
+                  "amd.com/gpu.partition-config", "amd.com/gpu.present.source")
+
+_VALUE_RE = re.compile(r"[^A-Za-z0-9_.-]")
+
+
+def label_value(v) -> str:
+    """Kubernetes label value: <= 63 chars of [A-Za-z0-9_.-], alnum at both ends."""
+    s = _VALUE_RE.sub("-", str(v))[:63]
+    return s.strip("-_.")
+
+
+def _read(path: str) -> str | None:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _root_join(root: str, rel: str) -> str:
+    return os.path.join(root or "/", rel.lstrip("/"))
+
+
+def nfd_labels(root: str = "/") -> dict[str, str]:
+    labels: dict[str, str] = {}
+    pci = _root_join(root, "sys/bus/pci/devices")
+    try:
+        devs = sorted(os.listdir(pci))
+    except OSError:
+        devs = []
+    for d in devs:
+        vendor = (_read(os.path.join(pci, d, "vendor")) or "").lower().replace("0x", "")
+        cls = (_read(os.path.join(pci, d, "class")) or "").lower().replace("0x", "")
+        if not vendor or not cls:
+            continue
+        cls4 = cls.zfill(6)[:4]
+        labels[f"{NFD_PREFIX}pci-{cls4}_{vendor}.present"] = "true"
+        if vendor == AMD_VENDOR and cls4 in GPU_CLASSES:
+            labels[f"{NFD_PREFIX}pci-{AMD_VENDOR}.present"] = "true"
+    if _read(_root_join(root, "sys/module/amdgpu/initstate")) == "live":
+        labels[f"{NFD_PREFIX}kernel-loadedmodule.amdgpu"] = "true"
+    ver = _read(_root_join(root, "proc/sys/kernel/osrelease"))
+    if ver:
+        labels[f"{NFD_PREFIX}kernel-version.full"] = label_value(ver)
+    return labels
+
+
+def rocm_version(root: str = "/") -> str:
+    for p in ("opt/rocm/.info/version", "opt/rocm/.info/version-dev"):
+        v = _read(_root_join(root, p))
+        if v:
+            return v.split("-")[0]
+    return os.environ.get("ROCM_VERSION", "")
+
+
+def gfd_labels(gpus: list[GpuDevice], root: str = "/", prefix: str = "amd.com") -> dict[str, str]:
+    p = f"{prefix}/gpu"
+    if not gpus:
+        return {}
+    g0 = gpus[0]
+    family = FAMILIES.get(g0.arch, "unknown")
+    physical = len({g.physical_index for g in gpus})
+    numa = sorted({g.numa_node for g in gpus if g.numa_node >= 0})
+    labels = {
+        f"{p}.count": str(len(gpus)),
+        f"{p}.physical-count": str(physical),
+        f"{p}.product": label_value(PRODUCTS.get(g0.device_id, f"AMD-GPU-{g0.device_id:04x}")),
+        f"{p}.device-id": f"{g0.device_id:04x}",
+        f"{p}.family": family,
+        f"{p}.arch": label_value(g0.arch),
+        f"{p}.memory": str(g0.vram_bytes // (1024 * 1024)),
+        f"{p}.memory-gib": str(round(g0.vram_bytes / 2**30)),
+        f"{p}.compute-units": str(g0.cu_count),
+        f"{p}.xcc": str(g0.num_xcc),
+        f"{p}.lds-kib": str(g0.lds_size_kib),
+        f"{p}.wavefront-size": "64",
+        f"{p}.max-clock-mhz": str(g0.max_engine_clk_mhz),
+        f"{p}.compute-partition": label_value(g0.compute_partition or "SPX"),
+        f"{p}.memory-partition": label_value(g0.memory_partition or "NPS1"),
+        f"{p}.partition-capable": "true" if family == "CDNA4" or family == "CDNA3" else "false",
+        f"{p}.numa-nodes": label_value("-".join(str(n) for n in numa) or "none"),
+    }
+    for dtype, ok in MFMA_TYPES.get(family, {}).items():
+        labels[f"{p}.mfma.{dtype}"] = "true" if ok else "false"
+    hives = {g.hive_id for g in gpus if g.hive_id}
+    labels[f"{p}.xgmi.links"] = str(g0.xgmi_links)
+    labels[f"{p}.xgmi.hive"] = label_value(f"{min(hives):x}") if hives else "none"
+    labels[f"{p}.xgmi.hives"] = str(len(hives))
+    drv = _read(_root_join(root, "sys/module/amdgpu/version"))
+    if drv:
+        labels[f"{p}.driver-version"] = label_value(drv)
+    rocm = rocm_version(root)
+    if rocm:
+        labels[f"{p}.rocm-version"] = label_value(rocm)
+    return labels
+
+
+def sync_node_labels(client, node_name: str, desired: dict[str, str], owned_prefixes: tuple[str, ...]) -> dict:
+    """Set ``desired`` and remove stale labels under ``owned_prefixes``
+    (operator-owned labels are never removed). Returns the applied patch."""
+    node = client.get("v1", "Node", node_name)
+    cur = node.get("metadata", {}).get("labels") or {}
+    patch: dict = {}
+    for k, v in desired.items():
+        if cur.get(k) != v:
+            patch[k] = v
+    for k in cur:
+        if k in desired or any(k.startswith(o) for o in OPERATOR_OWNED):
+            continue
+        if any(k.startswith(pfx) for pfx in owned_prefixes):
+            patch[k] = None
+    if patch:
+        client.patch("v1", "Node", node_name, {"metadata": {"labels": patch}})
+    return patch

@@ -1,0 +1,354 @@
+"""GPU metrics exporter (DCGM-exporter equivalent, C9) and node-status
+exporter (C8), both serving Prometheus text format on ``/metrics``.
+
+Reference parity: ``nvidia-dcgm-exporter`` "collects GPU metrics for
+monitoring" (/root/reference/README.md:204,213) and ``nodeStatusExporter`` is
+enabled (README.md:107).  The MI355X exporter reads every GPU through the N4
+native collector (libamd_smi, one native call per interval for all GPUs and
+fields), attributes GPUs to pods through the kubelet pod-resources API, and
+caches the snapshot so a scrape never touches the hardware.
+
+Metric names (``amd_gpu_*``) and their DCGM counterparts
+(``--dcgm-names`` additionally emits the DCGM_FI_DEV_* aliases):
+
+====================================  ==================================
+amd_gpu_gfx_activity_percent          DCGM_FI_DEV_GPU_UTIL
+amd_gpu_umc_activity_percent          DCGM_FI_DEV_MEM_COPY_UTIL
+amd_gpu_vram_used_bytes / _free       DCGM_FI_DEV_FB_USED / _FREE (MiB)
+amd_gpu_power_watts                   DCGM_FI_DEV_POWER_USAGE
+amd_gpu_energy_joules_total           DCGM_FI_DEV_TOTAL_ENERGY_CONSUMPTION (mJ)
+amd_gpu_temperature_hotspot_celsius   DCGM_FI_DEV_GPU_TEMP
+amd_gpu_temperature_memory_celsius    DCGM_FI_DEV_MEMORY_TEMP
+amd_gpu_gfx_clock_mhz / mem_clock     DCGM_FI_DEV_SM_CLOCK / _MEM_CLOCK
+amd_gpu_ecc_uncorrectable_total       DCGM_FI_DEV_ECC_DBE_VOL_TOTAL
+amd_gpu_ecc_correctable_total         DCGM_FI_DEV_ECC_SBE_VOL_TOTAL
+amd_gpu_retired_pages                 DCGM_FI_DEV_RETIRED_DBE
+amd_gpu_xgmi_links_up / _link_errors  DCGM_FI_DEV_NVLINK_* (link health)
+====================================  ==================================
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+from dataclasses import dataclass
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+from ..utils.logs import get_logger
+
+log = get_logger("amdgpu.exporter")
+
+# (metric, field, type, help, dcgm alias, dcgm scale)
+FIELDS = [
+    ("amd_gpu_gfx_activity_percent", "gfx_activity_pct", "gauge", "Graphics/compute engine activity (%)",
+     "DCGM_FI_DEV_GPU_UTIL", 1.0),
+    ("amd_gpu_umc_activity_percent", "umc_activity_pct", "gauge", "Memory controller activity (%)",
+     "DCGM_FI_DEV_MEM_COPY_UTIL", 1.0),
+    ("amd_gpu_mm_activity_percent", "mm_activity_pct", "gauge", "Multimedia engine activity (%)", None, 1.0),
+    ("amd_gpu_vram_total_bytes", "vram_total_bytes", "gauge", "HBM capacity (bytes)", None, 1.0),
+    ("amd_gpu_vram_used_bytes", "vram_used_bytes", "gauge", "HBM in use (bytes)", "DCGM_FI_DEV_FB_USED", 1 / 2**20),
+    ("amd_gpu_power_watts", "socket_power_w", "gauge", "Socket power (W)", "DCGM_FI_DEV_POWER_USAGE", 1.0),
+    ("amd_gpu_power_limit_watts", "power_limit_w", "gauge", "Socket power limit (W)", None, 1.0),
+    ("amd_gpu_temperature_hotspot_celsius", "temp_hotspot_c", "gauge", "Hotspot temperature (C)",
+     "DCGM_FI_DEV_GPU_TEMP", 1.0),
+    ("amd_gpu_temperature_memory_celsius", "temp_mem_c", "gauge", "HBM temperature (C)", "DCGM_FI_DEV_MEMORY_TEMP", 1.0),
+    ("amd_gpu_temperature_edge_celsius", "temp_edge_c", "gauge", "Edge temperature (C)", None, 1.0),
+    ("amd_gpu_gfx_clock_mhz", "gfx_clk_mhz", "gauge", "Graphics clock (MHz)", "DCGM_FI_DEV_SM_CLOCK", 1.0),
+    ("amd_gpu_mem_clock_mhz", "mem_clk_mhz", "gauge", "Memory clock (MHz)", "DCGM_FI_DEV_MEM_CLOCK", 1.0),
+    ("amd_gpu_energy_joules_total", "energy_j", "counter", "Energy consumed (J)",
+     "DCGM_FI_DEV_TOTAL_ENERGY_CONSUMPTION", 1000.0),
+    ("amd_gpu_ecc_correctable_total", "ecc_correctable", "counter", "Correctable ECC errors",
+     "DCGM_FI_DEV_ECC_SBE_VOL_TOTAL", 1.0),
+    ("amd_gpu_ecc_uncorrectable_total", "ecc_uncorrectable", "counter", "Uncorrectable ECC errors",
+     "DCGM_FI_DEV_ECC_DBE_VOL_TOTAL", 1.0),
+    ("amd_gpu_ecc_deferred_total", "ecc_deferred", "counter", "Deferred ECC errors", None, 1.0),
+    ("amd_gpu_xgmi_links_total", "xgmi_links_total", "gauge", "xGMI links", None, 1.0),
+    ("amd_gpu_xgmi_links_up", "xgmi_links_up", "gauge", "xGMI links up", None, 1.0),
+    ("amd_gpu_xgmi_link_errors", "xgmi_links_error", "gauge", "xGMI links in error", None, 1.0),
+    ("amd_gpu_retired_pages", "bad_pages", "gauge", "Retired (bad) HBM pages", "DCGM_FI_DEV_RETIRED_DBE", 1.0),
+    ("amd_gpu_processes", "num_processes", "gauge", "Processes using the GPU", None, 1.0),
+]
+
+
+def _esc(v: str) -> str:
+    return str(v).replace("\\", "\\\\").replace("\n", "\\n").replace('"', '\\"')
+
+
+def _labels(d: dict) -> str:
+    return "{" + ",".join(f'{k}="{_esc(v)}"' for k, v in d.items()) + "}" if d else ""
+
+
+@dataclass
+class Sample:
+    index: int
+    bdf: str
+    uuid: str
+    product: str
+    values: dict
+
+
+class FixtureSource:
+    """Metrics from an ``amd-smi metric --json`` capture (tests / demos)."""
+
+    def __init__(self, path: str, gpus: int | None = None):
+        with open(path) as f:
+            self.doc = json.load(f)
+        self.gpus = gpus
+
+    @staticmethod
+    def _v(x):
+        if isinstance(x, dict):
+            x = x.get("value")
+        try:
+            return float(x)
+        except (TypeError, ValueError):
+            return None
+
+    def collect(self) -> list[Sample]:
+        out = []
+        entries = self.doc if isinstance(self.doc, list) else self.doc.get("gpu_data", [self.doc])
+        n = self.gpus or len(entries)
+        for i in range(n):
+            e = entries[i % len(entries)]
+            usage = e.get("usage") or {}
+            power = e.get("power") or {}
+            temp = e.get("temperature") or {}
+            clock = e.get("clock") or {}
+            mem = e.get("mem_usage") or {}
+            ecc = e.get("ecc") or {}
+            vals = {
+                "gfx_activity_pct": self._v(usage.get("gfx_activity")),
+                "umc_activity_pct": self._v(usage.get("umc_activity")),
+                "mm_activity_pct": self._v(usage.get("mm_activity")),
+                "socket_power_w": self._v(power.get("socket_power")),
+                "temp_hotspot_c": self._v(temp.get("hotspot")),
+                "temp_mem_c": self._v(temp.get("mem")),
+                "temp_edge_c": self._v(temp.get("edge")),
+                "gfx_clk_mhz": self._v(((clock.get("gfx_0") or {}).get("clk"))),
+                "mem_clk_mhz": self._v(((clock.get("mem_0") or {}).get("clk"))),
+                "vram_total_bytes": (self._v(mem.get("total_vram")) or 0) * 2**20 or None,
+                "vram_used_bytes": (self._v(mem.get("used_vram")) or 0) * 2**20,
+                "ecc_correctable": self._v(ecc.get("total_correctable_count")) or 0.0,
+                "ecc_uncorrectable": self._v(ecc.get("total_uncorrectable_count")) or 0.0,
+                "ecc_deferred": self._v(ecc.get("total_deferred_count")) or 0.0,
+            }
+            out.append(Sample(i, f"0000:{0x72 + i:02x}:00.0", f"fixture-{i}", "AMD-Instinct-MI355X",
+                              {k: v for k, v in vals.items() if v is not None}))
+        return out
+
+
+class SmiSource:
+    """Live metrics via the N4 native collector (libamd_smi)."""
+
+    def __init__(self):
+        from ..discovery.topology import Smi
+
+        self.smi = Smi()
+
+    def collect(self) -> list[Sample]:
+        return [Sample(m.index, m.bdf, m.uuid, m.market_name, m.values) for m in self.smi.collect()]
+
+    def close(self):
+        self.smi.close()
+
+
+class PodAttribution:
+    """Maps device IDs (PCI BDF[-pN]) to pods via the kubelet pod-resources API."""
+
+    def __init__(self, socket_path: str, resource_prefix: str = "amd.com/gpu"):
+        self.socket_path = socket_path
+        self.prefix = resource_prefix
+
+    def lookup(self) -> dict[str, dict]:
+        import grpc
+
+        from ..deviceplugin import api
+
+        if not os.path.exists(self.socket_path):
+            return {}
+        req, resp, _ = api.POD_RESOURCES_METHODS["List"]
+        with grpc.insecure_channel("unix:" + self.socket_path) as ch:
+            call = ch.unary_unary(api.method_path(api.POD_RESOURCES_SERVICE, "List"),
+                                  request_serializer=req.SerializeToString, response_deserializer=resp.FromString)
+            out = call(req(), timeout=2)
+        m: dict[str, dict] = {}
+        for pr in out.pod_resources:
+            for c in pr.containers:
+                for d in c.devices:
+                    if not d.resource_name.startswith(self.prefix):
+                        continue
+                    for dev in d.device_ids:
+                        m[dev] = {"namespace": pr.namespace, "pod": pr.name, "container": c.name}
+        return m
+
+
+class MetricsExporter:
+    def __init__(self, source, node_name: str = "", interval_s: float = 1.0, attribution: PodAttribution | None = None,
+                 dcgm_names: bool = False):
+        self.source = source
+        self.node = node_name
+        self.interval = interval_s
+        self.attribution = attribution
+        self.dcgm_names = dcgm_names
+        self._snapshot: list[Sample] = []
+        self._pods: dict[str, dict] = {}
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self.collections = 0
+        self.last_collect_s = 0.0
+        self.errors = 0
+
+    def collect_once(self) -> None:
+        t0 = time.perf_counter()
+        try:
+            snap = self.source.collect()
+            pods = self.attribution.lookup() if self.attribution else {}
+        except Exception as e:  # noqa: BLE001 - keep serving the last snapshot
+            self.errors += 1
+            log.warning("collect failed: %s", e)
+            return
+        with self._lock:
+            self._snapshot, self._pods = snap, pods
+            self.collections += 1
+            self.last_collect_s = time.perf_counter() - t0
+
+    def run(self) -> None:
+        while not self._stop.is_set():
+            self.collect_once()
+            self._stop.wait(self.interval)
+
+    def stop(self) -> None:
+        self._stop.set()
+
+    def render(self) -> str:
+        with self._lock:
+            snap, pods = list(self._snapshot), dict(self._pods)
+        lines = []
+        for metric, fld, mtype, help_, alias, scale in FIELDS:
+            rows = [s for s in snap if fld in s.values]
+            if not rows:
+                continue
+            names = [(metric, 1.0)] + ([(alias, scale)] if self.dcgm_names and alias else [])
+            for name, sc in names:
+                lines.append(f"# HELP {name} {help_}")
+                lines.append(f"# TYPE {name} {mtype}")
+                for s in rows:
+                    lab = {"gpu": str(s.index), "bdf": s.bdf, "uuid": s.uuid, "product": s.product}
+                    if self.node:
+                        lab["node"] = self.node
+                    pod = pods.get(s.bdf) or next((v for k, v in pods.items() if k.startswith(s.bdf + "-p")), None)
+                    if pod:
+                        lab.update(pod)
+                    lines.append(f"{name}{_labels(lab)} {s.values[fld] * sc:.6g}")
+            if fld == "vram_used_bytes":
+                tot = [s for s in snap if "vram_total_bytes" in s.values]
+                if tot:
+                    lines.append("# HELP amd_gpu_vram_free_bytes HBM free (bytes)")
+                    lines.append("# TYPE amd_gpu_vram_free_bytes gauge")
+                    for s in tot:
+                        lab = {"gpu": str(s.index), "bdf": s.bdf, "uuid": s.uuid, "product": s.product}
+                        if self.node:
+                            lab["node"] = self.node
+                        free = s.values["vram_total_bytes"] - s.values.get("vram_used_bytes", 0)
+                        lines.append(f"amd_gpu_vram_free_bytes{_labels(lab)} {free:.6g}")
+        lines += [
+            "# HELP amd_gpu_exporter_collections_total Completed collection passes",
+            "# TYPE amd_gpu_exporter_collections_total counter",
+            f"amd_gpu_exporter_collections_total {self.collections}",
+            "# HELP amd_gpu_exporter_collect_seconds Duration of the last collection pass",
+            "# TYPE amd_gpu_exporter_collect_seconds gauge",
+            f"amd_gpu_exporter_collect_seconds {self.last_collect_s:.6g}",
+            "# HELP amd_gpu_exporter_errors_total Failed collection passes",
+            "# TYPE amd_gpu_exporter_errors_total counter",
+            f"amd_gpu_exporter_errors_total {self.errors}",
+        ]
+        return "\n".join(lines) + "\n"
+
+
+class NodeStatusExporter:
+    """Operand readiness / validation metrics from the validations directory."""
+
+    STEPS = ("driver", "toolkit", "workload", "plugin", "complete")
+
+    def __init__(self, validations_dir: str, node_name: str = ""):
+        self.dir = validations_dir
+        self.node = node_name
+        self.scrapes = 0
+
+    def render(self) -> str:
+        from ..validator.validate import READY_FILES
+
+        self.scrapes += 1
+        lab_node = {"node": self.node} if self.node else {}
+        lines = ["# HELP amd_gpu_operator_node_validation_ready Validation step completed (1) or not (0)",
+                 "# TYPE amd_gpu_operator_node_validation_ready gauge"]
+        secs = []
+        for s in self.STEPS:
+            p = os.path.join(self.dir, READY_FILES[s])
+            ok = os.path.exists(p)
+            lines.append(f"amd_gpu_operator_node_validation_ready{_labels({**lab_node, 'step': s})} {int(ok)}")
+            if ok:
+                try:
+                    with open(p) as f:
+                        d = json.load(f)
+                    if isinstance(d.get("seconds"), (int, float)):
+                        secs.append((s, d["seconds"]))
+                except (OSError, ValueError):
+                    pass
+        lines += ["# HELP amd_gpu_operator_node_validation_seconds Duration of each validation step",
+                  "# TYPE amd_gpu_operator_node_validation_seconds gauge"]
+        for s, v in secs:
+            lines.append(f"amd_gpu_operator_node_validation_seconds{_labels({**lab_node, 'step': s})} {v:.6g}")
+        validated = os.path.exists(os.path.join(self.dir, READY_FILES["complete"]))
+        lines += ["# HELP amd_gpu_operator_node_validated Node passed every validation step",
+                  "# TYPE amd_gpu_operator_node_validated gauge",
+                  f"amd_gpu_operator_node_validated{_labels(lab_node)} {int(validated)}",
+                  "# HELP amd_gpu_operator_node_status_scrapes_total Scrapes served",
+                  "# TYPE amd_gpu_operator_node_status_scrapes_total counter",
+                  f"amd_gpu_operator_node_status_scrapes_total{_labels(lab_node)} {self.scrapes}"]
+        return "\n".join(lines) + "\n"
+
+
+class MetricsHttpServer:
+    """``/metrics`` + ``/healthz`` for any object with ``render() -> str``."""
+
+    def __init__(self, renderer, host: str = "0.0.0.0", port: int = 9400):
+        r = renderer
+
+        class H(BaseHTTPRequestHandler):
+            def log_message(self, *a):
+                pass
+
+            def do_GET(self):
+                if self.path.startswith("/metrics"):
+                    body = r.render().encode()
+                    ctype = "text/plain; version=0.0.4; charset=utf-8"
+                elif self.path.startswith("/healthz"):
+                    body, ctype = b"ok\n", "text/plain"
+                else:
+                    self.send_response(404)
+                    self.end_headers()
+                    return
+                self.send_response(200)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        self.httpd = ThreadingHTTPServer((host, port), H)
+        self.httpd.daemon_threads = True
+        self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True, name="metrics-http")
+
+    @property
+    def port(self) -> int:
+        return self.httpd.server_address[1]
+
+    def start(self) -> "MetricsHttpServer":
+        self.thread.start()
+        return self
+
+    def stop(self) -> None:
+        self.httpd.shutdown()
+        self.httpd.server_close()

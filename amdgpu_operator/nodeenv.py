@@ -1,0 +1,87 @@
+"""Per-node environment shared by the operands (host paths, API client).
+
+In a real cluster every operand container builds this from its environment
+(``NODE_NAME``, ``OPERATOR_NAMESPACE``) and the host paths mounted by its
+DaemonSet (``controller/manifests.py``).  The simulated cluster
+(``testing/simcluster.py``) builds one per simulated node pointing at
+temporary directories, so the operand code paths are identical.
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import time
+from dataclasses import dataclass, field
+from typing import Callable
+
+from . import DEFAULT_NAMESPACE
+
+
+@dataclass
+class ProcResult:
+    rc: int
+    stdout: str
+    stderr: str
+    seconds: float
+
+
+def run_local(argv: list[str], env: dict | None = None, timeout: float = 300.0) -> ProcResult:
+    """Run a native tool as a child process (never exec in-process)."""
+    t0 = time.perf_counter()
+    full_env = dict(os.environ)
+    full_env.update(env or {})
+    try:
+        p = subprocess.run(argv, capture_output=True, text=True, env=full_env, timeout=timeout)
+        return ProcResult(p.returncode, p.stdout, p.stderr, time.perf_counter() - t0)
+    except subprocess.TimeoutExpired as e:
+        return ProcResult(124, e.stdout or "", (e.stderr or "") + "\ntimeout", time.perf_counter() - t0)
+
+
+@dataclass
+class NodeEnv:
+    node_name: str
+    client: object
+    host_root: str = "/"                      # sysfs/devfs root the topology library reads
+    validations_dir: str = "/run/amd/validations"
+    device_plugin_dir: str = "/var/lib/kubelet/device-plugins"
+    pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
+    cdi_dir: str = "/var/run/cdi"
+    containerd_config: str = "/etc/containerd/config.toml"
+    install_dir: str = "/usr/local/amd"
+    namespace: str = DEFAULT_NAMESPACE
+    poll_s: float = 1.0
+    # how GPU processes are started: (argv, env, device_index or None) -> ProcResult.
+    # The bench routes device d to the torch.distributed rank that owns GPU d.
+    launcher: Callable[..., ProcResult] | None = None
+    extra: dict = field(default_factory=dict)
+
+    @classmethod
+    def from_environ(cls, client) -> "NodeEnv":
+        e = os.environ
+        return cls(
+            node_name=e.get("NODE_NAME", os.uname().nodename),
+            client=client,
+            host_root=e.get("HOST_ROOT", "/host" if os.path.isdir("/host/sys") else "/"),
+            validations_dir=e.get("VALIDATIONS_DIR", "/run/amd/validations"),
+            device_plugin_dir=e.get("DEVICE_PLUGIN_DIR", "/var/lib/kubelet/device-plugins"),
+            pod_resources_socket=e.get("POD_RESOURCES_SOCKET", "/var/lib/kubelet/pod-resources/kubelet.sock"),
+            cdi_dir=e.get("CDI_SPEC_DIR", "/var/run/cdi"),
+            containerd_config=e.get("CONTAINERD_CONFIG", "/etc/containerd/config.toml"),
+            install_dir=e.get("INSTALL_DIR", "/usr/local/amd"),
+            namespace=e.get("OPERATOR_NAMESPACE", DEFAULT_NAMESPACE),
+            poll_s=float(e.get("VALIDATION_POLL_S", "1.0")),
+        )
+
+    def validation_file(self, name: str) -> str:
+        return os.path.join(self.validations_dir, name)
+
+    def sysfs_root(self) -> str:
+        """Root for the topology library (host sysfs is mounted at /host/sys)."""
+        return self.host_root
+
+    def launch(self, argv: list[str], env: dict | None = None, device: int | None = None,
+               timeout: float = 300.0) -> ProcResult:
+        if self.launcher is not None:
+            return self.launcher(argv, env or {}, device, timeout)
+        return run_local(argv, env, timeout)

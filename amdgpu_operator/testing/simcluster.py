@@ -1,0 +1,542 @@
+"""Simulated Kubernetes cluster that runs the REAL operand code (C14).
+
+SURVEY.md §4.2 / §7.4: without kind, kubectl, docker or root, the product is
+exercised end to end in-process:
+
+* :class:`~amdgpu_operator.kube.fakeapi.FakeApiServer` as the API server;
+* a DaemonSet controller (pods per eligible node, rolling re-creation on
+  template change, DaemonSet status);
+* one simulated kubelet per node that runs pods: init containers in order,
+  then the main containers, each mapped to the operand function its
+  ``amdgpu-operator <subcommand>`` args name (the same functions the CLI runs
+  inside the real images) - plus ``amdgpu-validator`` workload pods, which go
+  through the device-plugin gRPC Allocate, the native OCI hook on a synthetic
+  bundle, and the native validator binary on the allocated GPU;
+* :class:`~amdgpu_operator.testing.fakekubelet.FakeKubelet` per node (device
+  plugin registration / ListAndWatch / Allocate / pod-resources) feeding the
+  node's Allocatable ``amd.com/gpu``.
+
+Each node has its own host directories (validations, device-plugins, CDI,
+containerd config) under ``workdir``; its sysfs root is a synthetic MI355X tree
+(``fakesys``) or, on a GPU box, the real ``/``.  With ``fake_gpu=True`` GPU
+processes are not started (CPU-only tests) and report a synthetic success.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import shlex
+import threading
+import time
+import uuid
+from dataclasses import dataclass, field
+
+from .. import API_GROUP, API_VERSION, DEFAULT_NAMESPACE, RESOURCE_NAME
+from ..api.clusterpolicy import cluster_policy, spec_from_values
+from ..controller.reconciler import ClusterPolicyReconciler
+from ..kube import resources as R
+from ..kube.client import LocalClient, NotFound
+from ..kube.fakeapi import FakeApiServer
+from ..nodeenv import NodeEnv, ProcResult, run_local
+from ..utils.logs import get_logger
+from . import fakesys
+from .fakekubelet import FakeKubelet
+
+log = get_logger("amdgpu.sim")
+CP_API = f"{API_GROUP}/{API_VERSION}"
+
+
+@dataclass
+class NodeSpec:
+    name: str
+    gpus: int = 8                     # 0 = CPU-only node
+    compute_partition: str = "SPX"
+    memory_partition: str = "NPS1"
+    sysfs_root: str | None = None     # None = synthetic tree; "/" = this machine
+
+
+@dataclass
+class SimNode:
+    spec: NodeSpec
+    dir: str
+    env: NodeEnv
+    kubelet: FakeKubelet
+    pods: dict = field(default_factory=dict)  # pod name -> _PodRun
+
+
+def fake_validator_result(argv: list[str]) -> ProcResult:
+    """Synthetic ``amdgpu-validator`` output for CPU-only runs."""
+    def arg(name, default):
+        return argv[argv.index(name) + 1] if name in argv else default
+
+    steps = arg("--steps", "hip,vecadd,gemm,hbm,xgmi,rccl").split(",")
+    rep = {"ok": True, "simulated": True, "rank": int(arg("--rank", "0")), "world": int(arg("--world", "1")),
+           "device": int(arg("--device", "0")), "seconds": 0.0,
+           "steps": [{"name": s, "ok": True, "seconds": 0.0, "simulated": True} for s in steps]}
+    return ProcResult(0, json.dumps(rep) + "\n", "", 0.0)
+
+
+class _PodRun:
+    def __init__(self, cluster: "SimCluster", node: SimNode, pod: dict):
+        self.cluster = cluster
+        self.node = node
+        self.pod = pod
+        self.name = pod["metadata"]["name"]
+        self.ns = pod["metadata"].get("namespace", "default")
+        self.stop = threading.Event()
+        self.ready: dict[str, bool] = {}
+        self.thread = threading.Thread(target=self._run, daemon=True, name=f"pod-{self.name}")
+        self.cleanups: list = []
+        self.restarts = 0
+
+    # ------------------------------------------------------------- status
+    def _status(self, phase: str, init_done: bool, reason: str = "", message: str = "") -> None:
+        spec = self.pod["spec"]
+        ctrs = spec.get("containers", [])
+        all_ready = init_done and bool(ctrs) and all(self.ready.get(c["name"]) for c in ctrs)
+        now = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+        st = {
+            "phase": phase,
+            "hostIP": "10.0.0.1",
+            "conditions": [
+                {"type": "PodScheduled", "status": "True"},
+                {"type": "Initialized", "status": "True" if init_done else "False"},
+                {"type": "ContainersReady", "status": "True" if all_ready else "False"},
+                {"type": "Ready", "status": "True" if all_ready else "False", "lastTransitionTime": now},
+            ],
+            "containerStatuses": [{"name": c["name"], "ready": bool(self.ready.get(c["name"])),
+                                   "restartCount": self.restarts,
+                                   "state": {"running": {}} if phase == "Running" else {"terminated": {"reason": reason}}}
+                                  for c in ctrs],
+        }
+        if reason:
+            st["reason"] = reason
+        if message:
+            st["message"] = message[:2000]
+        try:
+            cur = self.cluster.client.get("v1", "Pod", self.name, self.ns)
+        except NotFound:
+            return
+        if cur.get("status") == st:
+            return
+        cur["status"] = st
+        try:
+            self.cluster.client.update_status(cur)
+        except Exception:  # noqa: BLE001 - pod deleted meanwhile / conflict: next update wins
+            pass
+
+    # ----------------------------------------------------------- lifecycle
+    def _run(self) -> None:
+        restart = self.pod["spec"].get("restartPolicy", "Always") != "Never"
+        backoff = self.cluster.poll_s * 10
+        while not self.stop.is_set():
+            failed = self._run_once()
+            if not failed or not restart:
+                return
+            self.restarts += 1
+            if self.stop.wait(backoff):
+                return
+            backoff = min(backoff * 2, 2.0)
+
+    def _run_once(self) -> bool:
+        """One pass of init + main containers; True when something failed."""
+        spec = self.pod["spec"]
+        self.ready.clear()
+        self._status("Pending", False)
+        try:
+            for c in spec.get("initContainers", []):
+                if self.stop.is_set():
+                    return False
+                self.cluster.run_container(self, c, init=True)
+            self._status("Running", True)
+            threads = []
+            errors = []
+            for c in spec.get("containers", []):
+                def body(c=c):
+                    try:
+                        self.cluster.run_container(self, c, init=False)
+                    except Exception as e:  # noqa: BLE001
+                        errors.append(f"{c['name']}: {e}")
+                th = threading.Thread(target=body, daemon=True, name=f"ctr-{self.name}-{c['name']}")
+                th.start()
+                threads.append(th)
+            for th in threads:
+                th.join()
+            if self.stop.is_set():
+                return False
+            if errors:
+                log.warning("pod %s failed: %s", self.name, "; ".join(errors))
+                self._status("Failed", True, "Error", "; ".join(errors))
+                return True
+            self._status("Succeeded", True, "Completed")
+            return False
+        except Exception as e:  # noqa: BLE001 - init container failure
+            if not self.stop.is_set():
+                log.warning("pod %s failed: %s", self.name, e)
+                self._status("Failed", False, "Error", str(e))
+            return True
+        finally:
+            for fn in reversed(self.cleanups):
+                try:
+                    fn()
+                except Exception:  # noqa: BLE001
+                    pass
+
+    def set_ready(self, container: str) -> None:
+        self.ready[container] = True
+        self._status("Running", True)
+
+
+class SimCluster:
+    def __init__(self, workdir: str, nodes: list[NodeSpec], namespace: str = DEFAULT_NAMESPACE,
+                 fake_gpu: bool = True, poll_s: float = 0.01, launcher=None):
+        self.workdir = workdir
+        self.namespace = namespace
+        self.fake_gpu = fake_gpu
+        self.poll_s = poll_s
+        self.launcher = launcher
+        self.api = FakeApiServer()
+        self.client = LocalClient(self.api)
+        self.nodes: dict[str, SimNode] = {}
+        self.stop_event = threading.Event()
+        self._threads: list[threading.Thread] = []
+        self._lock = threading.RLock()
+        self.reconciler: ClusterPolicyReconciler | None = None
+        self.events: list[tuple[float, str, str]] = []
+        self._node_specs = nodes
+
+    # -------------------------------------------------------------- setup
+    def _make_node(self, ns: NodeSpec) -> SimNode:
+        d = os.path.join(self.workdir, ns.name)
+        os.makedirs(d, exist_ok=True)
+        if ns.sysfs_root is None:
+            root = os.path.join(d, "host")
+            if ns.gpus > 0:
+                fakesys.build_node(root, ns.gpus, ns.compute_partition, ns.memory_partition)
+            else:
+                os.makedirs(os.path.join(root, "sys/bus/pci/devices"), exist_ok=True)
+                fakesys._w(os.path.join(root, "sys/bus/pci/devices/0000:00:01.0/vendor"), "0x1022\n")
+                fakesys._w(os.path.join(root, "sys/bus/pci/devices/0000:00:01.0/class"), "0x060000\n")
+        else:
+            root = ns.sysfs_root
+        dp_dir = os.path.join(d, "device-plugins")
+        podres = os.path.join(d, "pod-resources", "kubelet.sock")
+        kubelet = FakeKubelet(dp_dir, podres)
+        env = NodeEnv(node_name=ns.name, client=self.client, host_root=root,
+                      validations_dir=os.path.join(d, "validations"), device_plugin_dir=dp_dir,
+                      pod_resources_socket=podres, cdi_dir=os.path.join(d, "cdi"),
+                      containerd_config=os.path.join(d, "etc/containerd/config.toml"),
+                      install_dir=os.path.join(d, "usr/local/amd"), namespace=self.namespace, poll_s=self.poll_s,
+                      launcher=self._launch)
+        if self.fake_gpu:
+            env.extra["metrics_fixture"] = os.path.join(fakesys.REAL_FIXTURE, "amd-smi-metric.json")
+        os.makedirs(os.path.dirname(env.containerd_config), exist_ok=True)
+        with open(env.containerd_config, "w") as f:  # the reference's own containerd edit (README.md:15-17)
+            f.write('version = 2\n[plugins."io.containerd.grpc.v1.cri".containerd.runtimes.runc.options]\n'
+                    "  SystemdCgroup = true\n")
+        return SimNode(ns, d, env, kubelet)
+
+    def _launch(self, argv, env, device, timeout) -> ProcResult:
+        if self.fake_gpu and argv and os.path.basename(argv[0]) == "amdgpu-validator":
+            return fake_validator_result(argv)
+        if self.launcher is not None:
+            return self.launcher(argv, env, device, timeout)
+        return run_local(argv, env, timeout)
+
+    def start(self) -> "SimCluster":
+        self.client.create(R.new("v1", "Namespace", self.namespace))
+        for ns in self._node_specs:
+            node = self._make_node(ns)
+            node.kubelet.start()
+            self.nodes[ns.name] = node
+            self.client.create({"apiVersion": "v1", "kind": "Node",
+                                "metadata": {"name": ns.name, "labels": {"kubernetes.io/hostname": ns.name}},
+                                "status": {"capacity": {"cpu": "128"}, "allocatable": {"cpu": "128"},
+                                           "conditions": [{"type": "Ready", "status": "True"}]}})
+        self._spawn(self._ds_controller_loop, "sim-ds-controller")
+        for node in self.nodes.values():
+            self._spawn(lambda n=node: self._kubelet_loop(n), f"sim-kubelet-{node.spec.name}")
+            self._spawn(lambda n=node: self._node_status_loop(n), f"sim-nodestatus-{node.spec.name}")
+        return self
+
+    def _spawn(self, fn, name: str) -> None:
+        th = threading.Thread(target=fn, daemon=True, name=name)
+        th.start()
+        self._threads.append(th)
+
+    def install_crd(self) -> None:
+        from ..helm.render import load_crd
+
+        self.client.create(load_crd())
+
+    def install_operator(self, values: dict | None = None, name: str = "cluster-policy") -> dict:
+        """``helm install`` equivalent: CRD + ClusterPolicy from values + operator loop."""
+        try:
+            self.install_crd()
+        except Exception:  # noqa: BLE001 - already installed
+            pass
+        cp = self.client.create(cluster_policy(name, spec_from_values(values or {})))
+        self.start_reconciler()
+        return cp
+
+    def start_reconciler(self) -> ClusterPolicyReconciler:
+        if self.reconciler is None:
+            self.reconciler = ClusterPolicyReconciler(self.client, self.namespace)
+            self._spawn(lambda: self.reconciler.run(self.stop_event, resync_s=1.0, debounce_s=0.005),
+                        "sim-operator")
+        return self.reconciler
+
+    def stop(self) -> None:
+        self.stop_event.set()
+        for node in self.nodes.values():
+            for run in list(node.pods.values()):
+                run.stop.set()
+        for node in self.nodes.values():
+            for run in list(node.pods.values()):
+                run.thread.join(timeout=5)
+            node.kubelet.stop()
+        for th in self._threads:
+            th.join(timeout=5)
+
+    # --------------------------------------------------- DaemonSet controller
+    @staticmethod
+    def _template_hash(ds: dict) -> str:
+        return hashlib.sha1(json.dumps(ds["spec"]["template"], sort_keys=True).encode()).hexdigest()[:10]
+
+    def _eligible(self, ds: dict, node: dict) -> bool:
+        tspec = ds["spec"]["template"]["spec"]
+        return R.node_selector_matches(node, tspec.get("nodeSelector"), tspec.get("affinity"))
+
+    def sync_daemonsets(self) -> None:
+        with self._lock:
+            nodes = self.client.list("v1", "Node")
+            for ds in self.client.list("apps/v1", "DaemonSet"):
+                ns = ds["metadata"]["namespace"]
+                name = ds["metadata"]["name"]
+                h = self._template_hash(ds)
+                pods = {p["spec"]["nodeName"]: p for p in self.client.list(
+                    "v1", "Pod", ns, label_selector={"app": name}) if any(
+                    r.get("uid") == ds["metadata"]["uid"] for r in p["metadata"].get("ownerReferences", []))}
+                eligible = [n for n in nodes if self._eligible(ds, n)]
+                want = {n["metadata"]["name"] for n in eligible}
+                for node_name, p in pods.items():
+                    stale = p["metadata"].get("labels", {}).get("controller-revision-hash") != h
+                    if node_name not in want or stale:
+                        try:
+                            self.client.delete("v1", "Pod", p["metadata"]["name"], ns)
+                        except NotFound:
+                            pass
+                for node_name in want:
+                    p = pods.get(node_name)
+                    if p is not None and p["metadata"].get("labels", {}).get("controller-revision-hash") == h:
+                        continue
+                    tmpl = R.deep(ds["spec"]["template"])
+                    suffix = hashlib.sha1(f"{name}/{node_name}/{h}".encode()).hexdigest()[:5]
+                    pod = {"apiVersion": "v1", "kind": "Pod",
+                           "metadata": {"name": f"{name}-{suffix}", "namespace": ns,
+                                        "labels": {**tmpl.get("metadata", {}).get("labels", {}),
+                                                   "controller-revision-hash": h},
+                                        "ownerReferences": [{"apiVersion": "apps/v1", "kind": "DaemonSet", "name": name,
+                                                             "uid": ds["metadata"]["uid"], "controller": True}]},
+                           "spec": {**tmpl["spec"], "nodeName": node_name}}
+                    try:
+                        self.client.create(pod)
+                    except Exception:  # noqa: BLE001 - AlreadyExists while the old one terminates
+                        pass
+                # status
+                pods_now = [p for p in self.client.list("v1", "Pod", ns, label_selector={"app": name})
+                            if p["spec"].get("nodeName") in want]
+                ready = sum(1 for p in pods_now if R.condition(p, "Ready") and R.condition(p, "Ready")["status"] == "True"
+                            and p["metadata"]["labels"].get("controller-revision-hash") == h)
+                updated = sum(1 for p in pods_now if p["metadata"]["labels"].get("controller-revision-hash") == h)
+                st = {"desiredNumberScheduled": len(want), "currentNumberScheduled": len(pods_now),
+                      "numberReady": ready, "updatedNumberScheduled": updated, "numberAvailable": ready,
+                      "numberMisscheduled": 0, "observedGeneration": ds["metadata"].get("generation", 1)}
+                if ds.get("status") != st:
+                    ds["status"] = st
+                    try:
+                        self.client.update_status(ds)
+                    except Exception:  # noqa: BLE001
+                        pass
+
+    def _ds_controller_loop(self) -> None:
+        import queue
+
+        q: queue.Queue = queue.Queue()
+
+        def pump(av, kind):
+            while not self.stop_event.is_set():
+                try:
+                    for _ in self.client.watch(av, kind, stop=self.stop_event):
+                        q.put(kind)
+                except Exception:  # noqa: BLE001
+                    self.stop_event.wait(0.1)
+
+        for av, kind in (("apps/v1", "DaemonSet"), ("v1", "Node"), ("v1", "Pod")):
+            threading.Thread(target=pump, args=(av, kind), daemon=True, name=f"sim-ds-watch-{kind}").start()
+        while not self.stop_event.is_set():
+            try:
+                q.get(timeout=0.5)
+            except Exception:  # noqa: BLE001 - idle resync
+                pass
+            while not q.empty():
+                q.get_nowait()
+            try:
+                self.sync_daemonsets()
+            except Exception as e:  # noqa: BLE001
+                log.warning("ds sync: %s", e)
+
+    # -------------------------------------------------------------- kubelet
+    def _kubelet_loop(self, node: SimNode) -> None:
+        sel = f"spec.nodeName={node.spec.name}"
+        while not self.stop_event.is_set():
+            try:
+                for etype, pod in self.client.watch("v1", "Pod", field_selector=sel, stop=self.stop_event):
+                    self._on_pod(node, etype, pod)
+            except Exception as e:  # noqa: BLE001
+                log.debug("kubelet watch: %s", e)
+                self.stop_event.wait(0.1)
+
+    def _on_pod(self, node: SimNode, etype: str, pod: dict) -> None:
+        name = pod["metadata"]["name"]
+        if etype == "DELETED":
+            run = node.pods.pop(name, None)
+            if run is not None:
+                run.stop.set()
+                node.kubelet.release(run.ns, name)
+            return
+        if etype == "ADDED" and name not in node.pods:
+            run = _PodRun(self, node, pod)
+            node.pods[name] = run
+            run.thread.start()
+
+    def _node_status_loop(self, node: SimNode) -> None:
+        last = None
+        while not self.stop_event.wait(self.poll_s):
+            caps = {}
+            for res in list(node.kubelet.resources):
+                caps[res] = (node.kubelet.capacity(res), node.kubelet.allocatable(res))
+            if caps == last:
+                continue
+            try:
+                cur = self.client.get("v1", "Node", node.spec.name)
+                st = cur.setdefault("status", {})
+                cap = st.setdefault("capacity", {})
+                alloc = st.setdefault("allocatable", {})
+                for res, (c, a) in caps.items():
+                    cap[res] = str(c)
+                    alloc[res] = str(a)
+                self.client.update_status(cur)
+                last = caps
+            except Exception:  # noqa: BLE001
+                pass
+
+    # ------------------------------------------------------------ containers
+    def run_container(self, run: _PodRun, c: dict, init: bool) -> None:
+        cmd = list(c.get("command") or []) + list(c.get("args") or [])
+        if not cmd:
+            raise RuntimeError(f"container {c['name']} has no command")
+        prog = os.path.basename(cmd[0])
+        if prog == "amdgpu-operator":
+            from ..cli import operands
+
+            operands.run_in_sim(self, run, c, cmd[1:], init)
+        elif prog == "amdgpu-validator":
+            self._run_gpu_workload(run, c, cmd)
+        else:
+            raise RuntimeError(f"unknown program {prog}")
+
+    def _run_gpu_workload(self, run: _PodRun, c: dict, cmd: list[str]) -> None:
+        """Non-operand pod with GPU limits: Allocate -> OCI hook -> validator."""
+        from .. import native
+
+        node = run.node
+        limits = (c.get("resources") or {}).get("limits") or {}
+        gpu_res = [(k, int(v)) for k, v in limits.items() if k.startswith(RESOURCE_NAME)]
+        envs: dict[str, str] = {}
+        devices: list[int] = []
+        if gpu_res:
+            res, n = gpu_res[0]
+            if not node.kubelet.wait_registered(res, timeout=30):
+                raise RuntimeError(f"resource {res} not registered on {node.spec.name}")
+            ids, resp = node.kubelet.allocate(res, n, run.ns, run.name, c["name"])
+            envs = dict(resp.envs)
+            devices = [int(x) for x in envs.get("AMD_VISIBLE_DEVICES", "").split(",") if x != ""]
+            try:
+                cur = self.client.get("v1", "Pod", run.name, run.ns)
+                self.client.patch("v1", "Pod", run.name, {"metadata": {"annotations": {
+                    "amd.com/gpu.allocated": ",".join(ids)}}}, run.ns)
+            except NotFound:
+                pass
+            # OCI hook on a synthetic bundle, exactly as runc would call it (state on stdin)
+            bundle = os.path.join(node.dir, "bundles", run.name)
+            os.makedirs(bundle, exist_ok=True)
+            with open(os.path.join(bundle, "config.json"), "w") as f:
+                json.dump({"ociVersion": "1.1.0", "process": {"args": cmd, "env": [f"{k}={v}" for k, v in envs.items()]},
+                           "root": {"path": "rootfs"}, "linux": {}}, f)
+            state = json.dumps({"ociVersion": "1.1.0", "id": run.name, "status": "creating", "pid": os.getpid(),
+                                "bundle": bundle})
+            import subprocess
+
+            p = subprocess.run([str(native.binary("amdgpu-oci-hook")), "prestart", "--root", node.env.sysfs_root()],
+                               input=state, capture_output=True, text=True, timeout=30)
+            if p.returncode != 0:
+                raise RuntimeError(f"OCI hook failed: {p.stderr.strip()}")
+            with open(os.path.join(bundle, "config.json")) as f:
+                spec = json.load(f)
+            paths = {d["path"] for d in spec.get("linux", {}).get("devices", [])}
+            if "/dev/kfd" not in paths:
+                raise RuntimeError("OCI hook did not inject /dev/kfd")
+        argv = [str(native.binary("amdgpu-validator"))] + cmd[1:]
+        proc_env = {}
+        dev = devices[0] if devices else None
+        if devices:
+            proc_env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
+        res = node.env.launch(argv, proc_env, device=dev, timeout=600)
+        if res.rc != 0:
+            raise RuntimeError(f"workload failed rc={res.rc}: {res.stderr.strip()[-500:]} {res.stdout.strip()[-500:]}")
+
+    # -------------------------------------------------------------- queries
+    def policy(self) -> dict | None:
+        try:
+            return self.client.get(CP_API, "ClusterPolicy", "cluster-policy")
+        except NotFound:
+            return None
+
+    def is_ready(self, expect_allocatable: dict[str, int] | None = None) -> bool:
+        cp = self.policy()
+        if not cp or (cp.get("status") or {}).get("state") != "ready":
+            return False
+        for node in self.nodes.values():
+            if node.spec.gpus <= 0:
+                continue
+            n = self.client.get("v1", "Node", node.spec.name)
+            if (n["metadata"].get("labels") or {}).get("amd.com/gpu.validated") != "true":
+                return False
+            want = (expect_allocatable or {}).get(node.spec.name)
+            if want is not None:
+                have = int(((n.get("status") or {}).get("allocatable") or {}).get(RESOURCE_NAME, "0"))
+                if have != want:
+                    return False
+        return True
+
+    def wait_ready(self, timeout: float = 60.0, expect_allocatable: dict[str, int] | None = None) -> float:
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < timeout:
+            if self.is_ready(expect_allocatable):
+                return time.perf_counter() - t0
+            time.sleep(self.poll_s)
+        raise TimeoutError(f"cluster not ready after {timeout}s: {json.dumps((self.policy() or {}).get('status'))[:2000]}")
+
+    def pods(self, namespace: str | None = None) -> list[dict]:
+        return self.client.list("v1", "Pod", namespace or self.namespace)
+
+
+def new_id() -> str:
+    return uuid.uuid4().hex[:8]
+
+
+def _quote(argv) -> str:
+    return " ".join(shlex.quote(a) for a in argv)

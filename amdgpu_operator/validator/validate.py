@@ -1,0 +1,267 @@
+"""Operator-validator steps (init containers of ``amd-operator-validator``).
+
+Reference parity: validator pods that end ``Completed`` (/root/reference/
+README.md:199).  The steps and the host files they produce, in order:
+
+==================  =====================================================  =================
+step                what it checks                                         ready file
+==================  =====================================================  =================
+driver              N1 probe: amdgpu live, /dev/kfd, KFD GPU nodes, render  driver-ready
+toolkit             toolkit installed (CDI spec + runtime config)           toolkit-ready
+workload            one native ``amdgpu-validator`` process per GPU: HIP    workload-ready
+                    vectorAdd, MFMA GEMM + counter gate, HBM, xGMI one-shot
+                    all-reduce, RCCL all-reduce across ALL GPUs over xGMI
+plugin              node Allocatable ``amd.com/gpu`` == GPUs found, then    plugin-ready
+                    one pod per GPU requesting ``amd.com/gpu: 1`` (device
+                    plugin Allocate -> OCI hook -> HIP workload) Succeeded
+complete            node labelled ``amd.com/gpu.validated=true`` with the    validated
+                    per-step durations (time-to-Ready breakdown)
+==================  =====================================================  =================
+
+Other operands gate on these files (their init containers run
+``amdgpu-operator validate <step>`` in wait mode).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+import uuid
+from concurrent.futures import ThreadPoolExecutor
+
+from .. import RESOURCE_NAME, native
+from ..nodeenv import NodeEnv
+from ..utils.logs import get_logger
+
+log = get_logger("amdgpu.validator")
+
+READY_FILES = {
+    "driver": "driver-ready",
+    "toolkit": "toolkit-ready",
+    "workload": "workload-ready",
+    "plugin": "plugin-ready",
+    "complete": "validated",
+}
+VALIDATED_LABEL = "amd.com/gpu.validated"
+WORKLOAD_POD_LABEL = "amd.com/validator-workload"
+
+
+class StepFailed(RuntimeError):
+    pass
+
+
+def write_ready(env: NodeEnv, step: str, payload: dict) -> str:
+    os.makedirs(env.validations_dir, exist_ok=True)
+    path = env.validation_file(READY_FILES[step])
+    tmp = f"{path}.tmp.{os.getpid()}.{threading.get_ident()}"
+    with open(tmp, "w") as f:
+        json.dump({"step": step, "node": env.node_name, "time": time.time(), **payload}, f)
+    os.replace(tmp, path)
+    return path
+
+
+def read_ready(env: NodeEnv, step: str) -> dict | None:
+    try:
+        with open(env.validation_file(READY_FILES[step])) as f:
+            txt = f.read()
+    except OSError:
+        return None
+    try:
+        return json.loads(txt)
+    except ValueError:
+        return {"raw": txt.strip()}
+
+
+def clear_ready(env: NodeEnv, steps=READY_FILES) -> None:
+    for s in steps:
+        try:
+            os.unlink(env.validation_file(READY_FILES[s]))
+        except OSError:
+            pass
+
+
+def wait_ready(env: NodeEnv, step: str, timeout: float = 600.0, stop: threading.Event | None = None) -> dict:
+    deadline = time.monotonic() + timeout
+    while True:
+        d = read_ready(env, step)
+        if d is not None:
+            return d
+        if time.monotonic() >= deadline:
+            raise StepFailed(f"timed out waiting for {READY_FILES[step]}")
+        if stop is not None and stop.wait(env.poll_s):
+            raise StepFailed("stopped")
+        if stop is None:
+            time.sleep(env.poll_s)
+
+
+# -------------------------------------------------------------------- steps --
+
+def validate_driver(env: NodeEnv, timeout: float = 600.0, stop=None) -> dict:
+    """N1 probe of the host, retried until ``timeout`` (driver still loading)."""
+    from ..discovery import topology
+
+    t0 = time.perf_counter()
+    deadline = time.monotonic() + timeout
+    while True:
+        ok, msg = topology.probe(env.sysfs_root())
+        if ok:
+            gpus = topology.enumerate_gpus(env.sysfs_root())
+            out = {"ok": True, "message": msg, "gpus": len(gpus), "seconds": time.perf_counter() - t0}
+            write_ready(env, "driver", out)
+            return out
+        if time.monotonic() >= deadline:
+            raise StepFailed(f"driver not ready: {msg}")
+        if stop is not None:
+            if stop.wait(env.poll_s):
+                raise StepFailed("stopped")
+        else:
+            time.sleep(env.poll_s)
+
+
+def workload_argv(args: list[str], rank: int, world: int, rendezvous: str, run_id: str, device: int) -> list[str]:
+    return [str(native.binary("amdgpu-validator")), "--device", str(device), "--rank", str(rank), "--world",
+            str(world), "--rendezvous", rendezvous, "--run-id", run_id, *args]
+
+
+def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: float = 600.0) -> dict:
+    """One native validator process per GPU, all ranks in one RCCL communicator."""
+    from ..discovery import topology
+
+    t0 = time.perf_counter()
+    gpus = topology.enumerate_gpus(env.sysfs_root())
+    if not gpus:
+        raise StepFailed("no GPUs to validate")
+    world = len(gpus)
+    args = list(args or [])
+    if world > 8:
+        # partitioned GPUs: the xGMI one-shot kernel takes <= 8 peers; RCCL still spans all
+        args = _drop_step(args, "xgmi")
+    run_id = uuid.uuid4().hex[:12]
+    rdv = os.path.join(env.validations_dir, "rendezvous", run_id)
+    os.makedirs(rdv, exist_ok=True)
+    counter_env = {"AMDGPU_VALIDATOR_COUNTERS": "1"} if "--counter-gate" in args else {}
+
+    def one(rank: int):
+        argv = workload_argv(args, rank, world, rdv, run_id, gpus[rank].index)
+        return env.launch(argv, counter_env, device=gpus[rank].index, timeout=timeout)
+
+    with ThreadPoolExecutor(max_workers=world) as ex:
+        results = list(ex.map(one, range(world)))
+    reports = []
+    for r, res in enumerate(results):
+        try:
+            rep = json.loads(res.stdout.strip().splitlines()[-1]) if res.stdout.strip() else {}
+        except ValueError:
+            rep = {"raw": res.stdout[-2000:]}
+        rep["rc"] = res.rc
+        rep["process_seconds"] = round(res.seconds, 4)
+        if res.rc != 0:
+            rep["stderr"] = res.stderr[-2000:]
+        reports.append(rep)
+    ok = all(r.get("rc") == 0 and r.get("ok") for r in reports)
+    summary = {"ok": ok, "world": world, "seconds": time.perf_counter() - t0, "ranks": reports}
+    if not ok:
+        bad = [(i, r.get("error") or r.get("stderr", "")[-300:]) for i, r in enumerate(reports) if not r.get("ok")]
+        raise StepFailed(f"workload validation failed on ranks {bad}")
+    write_ready(env, "workload", summary)
+    return summary
+
+
+def _drop_step(args: list[str], step: str) -> list[str]:
+    out = list(args)
+    if "--steps" in out:
+        i = out.index("--steps")
+        out[i + 1] = ",".join(s for s in out[i + 1].split(",") if s != step)
+    else:
+        out += ["--steps", ",".join(s for s in ("hip", "vecadd", "gemm", "hbm", "xgmi", "rccl") if s != step)]
+    return out
+
+
+def _node(env: NodeEnv) -> dict:
+    return env.client.get("v1", "Node", env.node_name)
+
+
+def allocatable(node: dict, resource: str) -> int:
+    try:
+        return int(((node.get("status") or {}).get("allocatable") or {}).get(resource, "0"))
+    except ValueError:
+        return 0
+
+
+def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | None = None,
+                    pod_args: list[str] | None = None, timeout: float = 600.0, stop=None) -> dict:
+    """Wait for Allocatable == GPUs, then run one 1-GPU pod per device."""
+    from ..discovery import topology
+
+    t0 = time.perf_counter()
+    if expect is None:
+        expect = len(topology.enumerate_gpus(env.sysfs_root()))
+    deadline = time.monotonic() + timeout
+    while True:
+        n = allocatable(_node(env), resource)
+        if n >= expect:
+            break
+        if time.monotonic() >= deadline:
+            raise StepFailed(f"allocatable {resource}={n}, expected {expect}")
+        if stop is not None and stop.wait(env.poll_s):
+            raise StepFailed("stopped")
+        if stop is None:
+            time.sleep(env.poll_s)
+    t_alloc = time.perf_counter() - t0
+    run_id = uuid.uuid4().hex[:8]
+    pod_args = list(pod_args or ["--steps", "hip,vecadd,gemm", "--gemm", "1024"])
+    names = []
+    for i in range(expect):
+        name = f"amd-validator-workload-{run_id}-{i}"
+        pod = {
+            "apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": name, "namespace": env.namespace,
+                         "labels": {"app": "amd-validator-workload", WORKLOAD_POD_LABEL: run_id}},
+            "spec": {
+                "nodeName": env.node_name,
+                "restartPolicy": "Never",
+                "tolerations": [{"key": resource, "operator": "Exists", "effect": "NoSchedule"}],
+                "containers": [{"name": "workload", "image": "amd-operator-validator",
+                                "command": ["amdgpu-validator"], "args": pod_args,
+                                "resources": {"limits": {resource: "1"}, "requests": {resource: "1"}}}],
+            },
+        }
+        env.client.create(pod)
+        names.append(name)
+    phases = {}
+    while True:
+        phases = {n: ((env.client.get("v1", "Pod", n, env.namespace).get("status") or {}).get("phase", "Pending"))
+                  for n in names}
+        if all(p in ("Succeeded", "Failed") for p in phases.values()):
+            break
+        if time.monotonic() >= deadline:
+            break
+        if stop is not None and stop.wait(env.poll_s):
+            break
+        if stop is None:
+            time.sleep(env.poll_s)
+    pods = [env.client.get("v1", "Pod", n, env.namespace) for n in names]
+    devices = [((p.get("metadata", {}).get("annotations") or {}).get("amd.com/gpu.allocated", "")) for p in pods]
+    for n in names:
+        try:
+            env.client.delete("v1", "Pod", n, env.namespace)
+        except Exception:  # noqa: BLE001
+            pass
+    if not all(p == "Succeeded" for p in phases.values()):
+        raise StepFailed(f"plugin validation pods did not succeed: {phases}")
+    summary = {"ok": True, "pods": expect, "devices": devices, "allocatable_wait_s": round(t_alloc, 4),
+               "seconds": time.perf_counter() - t0}
+    write_ready(env, "plugin", summary)
+    return summary
+
+
+def complete(env: NodeEnv) -> dict:
+    """Mark the node validated (label + annotation with the step durations)."""
+    steps = {s: (read_ready(env, s) or {}).get("seconds") for s in ("driver", "workload", "plugin")}
+    ann = {"amd.com/gpu.validation": json.dumps({k: round(v, 4) for k, v in steps.items() if v is not None})}
+    env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": {VALIDATED_LABEL: "true"},
+                                                                "annotations": ann}})
+    write_ready(env, "complete", {"steps": steps})
+    return {"ok": True, "steps": steps}

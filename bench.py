@@ -1,0 +1,261 @@
+"""Headline benchmark: validator time-to-Ready + allocatable amd.com/gpu.
+
+Metric (BASELINE.json): "validator pod time-to-Ready (s) + allocatable
+amd.com/gpu at 1/2/4/8 MI355X".  One step = one full operator bring-up on a
+node with N MI355X GPUs, measured from ClusterPolicy creation (the moment
+``helm install`` of /root/reference/README.md:101-110 creates it) until the
+node is validated and advertises ``amd.com/gpu: N``:
+
+  operator reconcile -> NFD labels -> operator GPU-node labels -> driver probe
+  (N1) -> container toolkit (CDI spec + containerd drop-in, N2) -> validator
+  workload: one native process per GPU (HIP vectorAdd, MFMA bf16 GEMM with
+  rocprofiler counter gate, HBM stream, xGMI one-shot all-reduce, RCCL
+  all-reduce across all N GPUs over xGMI) -> device plugin registers over
+  kubelet gRPC (ListAndWatch: N healthy) -> plugin validation: N pods x 1 GPU,
+  each GetPreferredAllocation/Allocate -> native OCI hook on an OCI bundle ->
+  HIP workload on its GPU -> node labelled validated.
+
+Kubernetes itself is simulated in-process (fake apiserver + kubelet, no
+kind/kubectl on the box); every GPU-touching step runs for real on the
+MI355X.  Under ``torch.distributed.run`` each rank owns one GPU and starts that
+GPU's processes (gloo control channel); the node is the N GPUs of the job.
+
+Reference number: no time-to-Ready is published; BASELINE.md gives <= ~600 s
+(10 min pod AGE, README.md:202-206) and 1 allocatable GPU per node.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_TTR_S = 600.0
+METRIC = "validator pod time-to-Ready (s) + allocatable amd.com/gpu at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--fake-gpu", action="store_true", help="CPU-only: synthetic sysfs, no GPU processes")
+    ap.add_argument("--sysfs-root", default=None, help="default: / when a GPU is present, else synthetic")
+    ap.add_argument("--quick-workload", action="store_true", help="small validator sizes (CI)")
+    ap.add_argument("--no-counter-gate", action="store_true", help="skip the rocprofiler counter gate (outer profiler)")
+    ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--detail", default=None, help="write per-step breakdown JSON here")
+    return ap.parse_args()
+
+
+def gpu_available() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> dict:
+    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, deep_merge, parse_set_flags
+    from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
+
+    root = None if fake_gpu else (args.sysfs_root or "/")
+    node = NodeSpec("mi355x-node-0", gpus=n_gpus, sysfs_root=root)
+    values = parse_set_flags(REFERENCE_SET_FLAGS)
+    if args.no_counter_gate:
+        values = deep_merge(values, {"validator": {"workload": {"counterGate": False}}})
+    if args.quick_workload:
+        values = deep_merge(values, {"validator": {"workload": {"gemmN": 1024, "hbmBytes": 1 << 26,
+                                                                "rcclElems": 1 << 20, "xgmiElems": 1 << 20}}})
+    d = tempfile.mkdtemp(prefix="step-", dir=workdir)
+    cluster = SimCluster(d, [node], fake_gpu=fake_gpu, poll_s=0.005, launcher=launcher).start()
+    try:
+        t0 = time.perf_counter()
+        cluster.install_operator(values)
+        ttr = cluster.wait_ready(args.timeout, {"mi355x-node-0": n_gpus})
+        t_total = time.perf_counter() - t0
+        cp = cluster.policy()
+        nobj = cluster.client.get("v1", "Node", "mi355x-node-0")
+        alloc = int(nobj["status"]["allocatable"].get("amd.com/gpu", "0"))
+        nd = cluster.nodes["mi355x-node-0"]
+        from amdgpu_operator.validator.validate import read_ready
+
+        wl = read_ready(nd.env, "workload") or {}
+        plug = read_ready(nd.env, "plugin") or {}
+        ranks = wl.get("ranks", [])
+        steps = {}
+        for r in ranks:
+            for s in r.get("steps", []):
+                steps.setdefault(s["name"], []).append(s)
+        return {
+            "time_to_ready_s": ttr,
+            "wall_s": t_total,
+            "allocatable": alloc,
+            "policy_state_seconds": (cp.get("status") or {}).get("stateReadySeconds"),
+            "workload_seconds": wl.get("seconds"),
+            "workload_process_seconds": [r.get("process_seconds") for r in ranks],
+            "plugin_seconds": plug.get("seconds"),
+            "plugin_devices": plug.get("devices"),
+            "gemm_tflops": [s.get("tflops") for s in steps.get("gemm", [])],
+            "gemm_counter_gate": [s.get("counter_gate") for s in steps.get("gemm", [])],
+            "hbm_gbps": [s.get("gbps") for s in steps.get("hbm", [])],
+            "xgmi_read_gbps": [s.get("read_gbps") for s in steps.get("xgmi", [])],
+            "rccl_busbw_gbps": [s.get("busbw_gbps") for s in steps.get("rccl", [])],
+            "rccl_comm_init_s": [s.get("comm_init_s") for s in steps.get("rccl", [])],
+            "rank0_step_seconds": {s["name"]: s.get("seconds") for s in (ranks[0].get("steps", []) if ranks else [])},
+            "rank0_total_seconds": ranks[0].get("seconds") if ranks else None,
+            "labels": {k: v for k, v in (nobj["metadata"].get("labels") or {}).items()
+                       if k in ("amd.com/gpu.product", "amd.com/gpu.arch", "amd.com/gpu.family", "amd.com/gpu.memory",
+                                "amd.com/gpu.xgmi.links", "amd.com/gpu.count", "amd.com/gpu.validated")},
+        }
+    finally:
+        cluster.stop()
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus != world:
+        args.gpus = world
+    has_gpu = gpu_available()
+    fake_gpu = args.fake_gpu or not has_gpu
+
+    import torch
+
+    dist = None
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        group = dist.group.WORLD
+    if has_gpu:
+        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+
+    from amdgpu_operator.parallel.launcher import DistributedLauncher
+
+    launcher = DistributedLauncher(rank, world, group) if world > 1 else None
+    n_gpus = args.gpus
+    if not fake_gpu and rank == 0:
+        from amdgpu_operator.discovery import topology
+
+        present = len(topology.enumerate_gpus(args.sysfs_root or "/"))
+        if present > n_gpus:
+            os.environ["AMDGPU_VISIBLE_GPUS"] = ",".join(str(i) for i in range(n_gpus))
+        elif present < n_gpus:
+            raise SystemExit(f"requested {n_gpus} GPUs, node exposes {present}")
+
+    workdir = tempfile.mkdtemp(prefix="amdgpu-bench-")
+    results: list[dict] = []
+    errors: list[str] = []
+
+    def driver_thread(n_steps: int, out: list):
+        try:
+            for _ in range(n_steps):
+                out.append(one_bring_up(args, n_gpus, launcher, workdir, fake_gpu))
+        except Exception as e:  # noqa: BLE001
+            import traceback
+
+            errors.append(f"{e}\n{traceback.format_exc()}")
+        finally:
+            if launcher is not None:
+                launcher.request_stop()
+
+    def phase(n_steps: int, out: list) -> None:
+        if world == 1:
+            driver_thread(n_steps, out)
+            return
+        if rank == 0:
+            th = threading.Thread(target=driver_thread, args=(n_steps, out), daemon=True)
+            th.start()
+            launcher._stop_requested.clear()
+            th_started = th
+            launcher.serve()
+            th_started.join()
+        else:
+            launcher.serve()
+
+    def sync():
+        if world > 1:
+            dist.barrier()
+        if has_gpu:
+            torch.cuda.synchronize()
+
+    # warmup (page-in, first HIP/RCCL init of the box)
+    warm: list = []
+    if args.warmup > 0:
+        phase(args.warmup, warm)
+        if world > 1:
+            launcher = DistributedLauncher(rank, world, group)
+    sync()
+    t0 = time.perf_counter()
+    phase(args.steps, results)
+    sync()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        box = [elapsed]
+        all_el = [None] * world
+        dist.all_gather_object(all_el, elapsed)
+        elapsed = max(all_el)
+        err_box = [errors]
+        dist.broadcast_object_list(err_box, src=0)
+        errors = err_box[0]
+    if rank == 0:
+        if errors:
+            print(errors[0], file=sys.stderr)
+            raise SystemExit(1)
+        ttr = [r["time_to_ready_s"] for r in results]
+        mean_ttr = sum(ttr) / len(ttr)
+        alloc = results[-1]["allocatable"]
+        out = {
+            "metric": METRIC,
+            "value": round(mean_ttr, 4),
+            "unit": "s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1000, 2),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": round(mean_ttr / BASELINE_TTR_S, 6),
+            "dtype": "bf16",
+            "data": "synthetic" + (" (simulated GPUs: no GPU present)" if fake_gpu else ""),
+            "config": {
+                "model": "amd-gpu-operator ClusterPolicy bring-up (reference --set flags) + HIP/MFMA/RCCL validator",
+                "global_batch": n_gpus,
+                "seq_len": 0,
+                "parallelism": f"dp{n_gpus}",
+                "allocatable_amd_com_gpu": alloc,
+                "time_to_ready_s": [round(x, 4) for x in ttr],
+                "time_to_ready_min_s": round(min(ttr), 4),
+                "gemm_tflops_per_gpu": results[-1]["gemm_tflops"],
+                "hbm_gbps_per_gpu": results[-1]["hbm_gbps"],
+                "rccl_busbw_gbps": results[-1]["rccl_busbw_gbps"],
+                "counter_gate": results[-1]["gemm_counter_gate"],
+            },
+        }
+        print(json.dumps(out))
+        if args.detail:
+            with open(args.detail, "w") as f:
+                json.dump({"summary": out, "steps": results, "warmup": warm}, f, indent=1)
+    shutil.rmtree(workdir, ignore_errors=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

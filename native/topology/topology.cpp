@@ -12,6 +12,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -111,9 +112,32 @@ struct KfdNode {
 
 std::string topo_dir(const char* root) { return join(root, "sys/class/kfd/kfd/topology/nodes"); }
 
+// AMDGPU_VISIBLE_GPUS="0,2,0000:a4:00.0": node-level allow-list (enumeration
+// index or PCI BDF), e.g. GPUs reserved for the host or a partial-node job.
+bool visible(size_t index, const Props& p) {
+  const char* env = getenv("AMDGPU_VISIBLE_GPUS");
+  if (!env || !*env) return true;
+  const unsigned loc = (unsigned)get(p, "location_id"), dom = (unsigned)get(p, "domain");
+  char bdf[32];
+  snprintf(bdf, sizeof(bdf), "%04x:%02x:%02x.%x", dom & 0xffff, (loc >> 8) & 0xff, (loc >> 3) & 0x1f, loc & 7);
+  std::stringstream ss(env);
+  std::string tok;
+  while (std::getline(ss, tok, ',')) {
+    tok = trim(tok);
+    if (tok.empty()) continue;
+    if (tok.find_first_not_of("0123456789") == std::string::npos) {
+      if ((size_t)atoi(tok.c_str()) == index) return true;
+    } else if (tok == bdf) {
+      return true;
+    }
+  }
+  return false;
+}
+
 // GPU nodes in KFD order (CPU nodes have simd_count == 0 or gpu_id == 0)
 std::vector<KfdNode> gpu_nodes(const char* root) {
   std::vector<KfdNode> out;
+  size_t gpu_index = 0;
   const std::string base = topo_dir(root);
   for (int n : numeric_entries(base)) {
     const std::string nd = base + "/" + std::to_string(n);
@@ -123,7 +147,7 @@ std::vector<KfdNode> gpu_nodes(const char* root) {
     std::string gid;
     k.gpu_id = read_file(nd + "/gpu_id", &gid) ? (unsigned)strtoul(trim(gid).c_str(), nullptr, 10) : 0;
     if (get(k.props, "simd_count") == 0 || k.gpu_id == 0) continue;
-    out.push_back(k);
+    if (visible(gpu_index++, k.props)) out.push_back(k);
   }
   return out;
 }

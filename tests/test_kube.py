@@ -1,0 +1,140 @@
+"""Fake API server semantics and the REST client over HTTP."""
+
+import threading
+import time
+
+import pytest
+
+from amdgpu_operator.kube import resources as R
+from amdgpu_operator.kube.client import AlreadyExists, Conflict, LocalClient, NotFound, RestClient, apply_object
+from amdgpu_operator.kube.fakeapi import FakeApiServer
+from amdgpu_operator.kube.httpapi import HttpApiServer
+
+
+@pytest.fixture(params=["local", "rest"])
+def client(request):
+    api = FakeApiServer()
+    if request.param == "local":
+        yield LocalClient(api)
+        return
+    srv = HttpApiServer(api).start()
+    try:
+        yield RestClient(srv.url)
+    finally:
+        srv.stop()
+
+
+def test_crud_and_selectors(client):
+    client.create(R.new("v1", "Namespace", "ns"))
+    client.create(R.new("v1", "Node", "a", labels={"gpu": "yes", "zone": "z1"}))
+    client.create(R.new("v1", "Node", "b", labels={"zone": "z2"}))
+    assert [n["metadata"]["name"] for n in client.list("v1", "Node", label_selector="gpu=yes")] == ["a"]
+    assert len(client.list("v1", "Node", label_selector="zone in (z1,z2)")) == 2
+    assert [n["metadata"]["name"] for n in client.list("v1", "Node", label_selector="!gpu")] == ["b"]
+    assert [n["metadata"]["name"] for n in client.list("v1", "Node", label_selector="zone!=z1")] == ["b"]
+    with pytest.raises(AlreadyExists):
+        client.create(R.new("v1", "Node", "a"))
+    with pytest.raises(NotFound):
+        client.get("v1", "Node", "zz")
+    p = client.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "ns"},
+                       "spec": {"nodeName": "a"}})
+    assert client.list("v1", "Pod", "ns", field_selector="spec.nodeName=a")[0]["metadata"]["uid"] == p["metadata"]["uid"]
+    assert client.list("v1", "Pod", "ns", field_selector="spec.nodeName=b") == []
+
+
+def test_conflict_and_status_subresource(client):
+    n = client.create(R.new("v1", "Node", "a"))
+    stale = dict(n)
+    n["metadata"]["labels"] = {"x": "1"}
+    n2 = client.update(n)
+    assert int(n2["metadata"]["generation"]) == 1  # metadata-only change
+    with pytest.raises(Conflict):
+        client.update(stale)
+    n2["status"] = {"allocatable": {"amd.com/gpu": "8"}}
+    client.update_status(n2)
+    cur = client.get("v1", "Node", "a")
+    assert cur["status"]["allocatable"]["amd.com/gpu"] == "8"
+    cur["status"] = {}
+    cur["spec"] = {"unschedulable": True}
+    cur = client.update(cur)  # main endpoint ignores status
+    assert cur["status"]["allocatable"]["amd.com/gpu"] == "8" and cur["metadata"]["generation"] == 2
+
+
+def test_merge_patch_removes_keys(client):
+    client.create(R.new("v1", "Node", "a", labels={"x": "1", "y": "2"}))
+    client.patch("v1", "Node", "a", {"metadata": {"labels": {"x": None, "z": "3"}}})
+    assert client.get("v1", "Node", "a")["metadata"]["labels"] == {"y": "2", "z": "3"}
+
+
+def test_watch_stream(client):
+    client.create(R.new("v1", "Namespace", "ns"))
+    events = []
+    stop = threading.Event()
+
+    def w():
+        for et, obj in client.watch("apps/v1", "DaemonSet", namespace="ns", stop=stop, timeout=5):
+            events.append((et, obj["metadata"]["name"]))
+            if len(events) == 3:
+                return
+
+    th = threading.Thread(target=w)
+    th.start()
+    time.sleep(0.3)
+    client.create(R.new("apps/v1", "DaemonSet", "d", "ns", spec={"a": 1}))
+    client.patch("apps/v1", "DaemonSet", "d", {"spec": {"a": 2}}, "ns")
+    client.delete("apps/v1", "DaemonSet", "d", "ns")
+    th.join(timeout=10)
+    stop.set()
+    assert events == [("ADDED", "d"), ("MODIFIED", "d"), ("DELETED", "d")]
+
+
+def test_watch_from_resource_version():
+    api = FakeApiServer()
+    c = LocalClient(api)
+    c.create(R.new("v1", "Node", "a"))
+    rv = api.resource_version()
+    c.create(R.new("v1", "Node", "b"))
+    got = [o["metadata"]["name"] for _, o in c.watch("v1", "Node", resource_version=rv, timeout=0.3)]
+    assert got == ["b"]
+
+
+def test_owner_reference_gc_and_namespace_delete(client):
+    client.create(R.new("v1", "Namespace", "ns"))
+    owner = client.create(R.new("amd.com/v1", "ClusterPolicy", "cp"))
+    ds = R.new("apps/v1", "DaemonSet", "d", "ns")
+    ds["metadata"]["ownerReferences"] = [{"uid": owner["metadata"]["uid"], "kind": "ClusterPolicy", "name": "cp"}]
+    client.create(ds)
+    client.create(R.new("v1", "ConfigMap", "c", "ns"))
+    client.delete("amd.com/v1", "ClusterPolicy", "cp")
+    with pytest.raises(NotFound):
+        client.get("apps/v1", "DaemonSet", "d", "ns")
+    client.delete("v1", "Namespace", "ns")
+    with pytest.raises(NotFound):
+        client.get("v1", "ConfigMap", "c", "ns")
+
+
+def test_apply_object_reverts_drift(client):
+    client.create(R.new("v1", "Namespace", "ns"))
+    ds = R.new("apps/v1", "DaemonSet", "d", "ns", spec={"template": {"spec": {"containers": [{"name": "x"}]}}})
+    assert apply_object(client, ds)[1] == "created"
+    assert apply_object(client, ds)[1] == "unchanged"
+    client.patch("apps/v1", "DaemonSet", "d", {"spec": {"template": {"spec": {"containers": [{"name": "hacked"}]}}}},
+                 "ns")
+    assert apply_object(client, ds)[1] == "updated"
+    assert client.get("apps/v1", "DaemonSet", "d", "ns")["spec"]["template"]["spec"]["containers"][0]["name"] == "x"
+    # server-side defaults on the live object are not drift
+    client.patch("apps/v1", "DaemonSet", "d", {"spec": {"revisionHistoryLimit": 10}}, "ns")
+    assert apply_object(client, ds)[1] == "unchanged"
+
+
+def test_selector_parser_edge_cases():
+    reqs = R.parse_selector("a=b, c in (x, y),!d,e")
+    assert R.matches({"a": "b", "c": "y", "e": "1"}, reqs)
+    assert not R.matches({"a": "b", "c": "z", "e": "1"}, reqs)
+    assert not R.matches({"a": "b", "c": "x", "d": "1", "e": "1"}, reqs)
+    assert R.matches({"k": "v"}, R.parse_selector({"matchLabels": {"k": "v"}}))
+    node = {"metadata": {"labels": {"gpu": "true", "zone": "a"}}}
+    aff = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+        {"matchExpressions": [{"key": "zone", "operator": "In", "values": ["a"]}]}]}}}
+    assert R.node_selector_matches(node, {"gpu": "true"}, aff)
+    assert not R.node_selector_matches(node, {"gpu": "false"})

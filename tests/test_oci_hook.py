@@ -1,0 +1,137 @@
+"""N2 OCI hook / CDI generator on synthetic bundles (SURVEY.md §4.2 native tier)."""
+
+import json
+import os
+import subprocess
+
+import pytest
+
+from amdgpu_operator import native
+from amdgpu_operator.testing import fakesys
+
+HOOK = str(native.binary("amdgpu-oci-hook"))
+
+
+@pytest.fixture
+def root(tmp_path):
+    r = str(tmp_path / "host")
+    fakesys.build_node(r, 4)
+    return r
+
+
+def bundle(tmp_path, env=None, annotations=None, extra=None):
+    b = tmp_path / "bundle"
+    b.mkdir(exist_ok=True)
+    spec = {"ociVersion": "1.1.0", "process": {"args": ["sh"], "env": env or ["PATH=/usr/bin"]},
+            "root": {"path": "rootfs"}, "linux": {"resources": {"devices": [{"allow": False, "access": "rwm"}]}}}
+    if annotations:
+        spec["annotations"] = annotations
+    if extra:
+        spec.update(extra)
+    (b / "config.json").write_text(json.dumps(spec))
+    return str(b)
+
+
+def run(args, input_=None):
+    return subprocess.run([HOOK, *args], capture_output=True, text=True, input=input_, timeout=30)
+
+
+def spec_of(b):
+    with open(os.path.join(b, "config.json")) as f:
+        return json.load(f)
+
+
+def test_version():
+    assert run(["--version"]).stdout.startswith("amdgpu-oci-hook")
+
+
+def test_cdi_spec(root):
+    p = run(["cdi", "--root", root])
+    assert p.returncode == 0, p.stderr
+    spec = json.loads(p.stdout)
+    assert spec["cdiVersion"] == "0.6.0" and spec["kind"] == "amd.com/gpu"
+    names = [d["name"] for d in spec["devices"]]
+    assert names == ["0", "1", "2", "3", "all"]
+    dev0 = spec["devices"][0]["containerEdits"]["deviceNodes"][0]
+    assert dev0 == {"path": "/dev/dri/renderD128", "type": "c", "major": 226, "minor": 128, "permissions": "rw"}
+    kfd = spec["containerEdits"]["deviceNodes"][0]
+    assert kfd["path"] == "/dev/kfd" and kfd["major"] == 241
+    assert len(spec["devices"][-1]["containerEdits"]["deviceNodes"]) == 4
+
+
+def test_cdi_to_file_with_rocm_mount(root, tmp_path):
+    out = str(tmp_path / "cdi" / "amd.json")
+    os.makedirs(os.path.dirname(out))
+    p = run(["cdi", "--root", root, "--output", out, "--mount-rocm", "--rocm-dir", "/opt/rocm"])
+    assert p.returncode == 0, p.stderr
+    spec = json.load(open(out))
+    assert spec["containerEdits"]["mounts"][0]["hostPath"] == "/opt/rocm"
+
+
+def test_apply_from_env_is_idempotent(root, tmp_path):
+    b = bundle(tmp_path, env=["PATH=/usr/bin", "AMD_VISIBLE_DEVICES=1,3"])
+    for _ in range(2):
+        p = run(["apply", "--bundle", b, "--root", root])
+        assert p.returncode == 0, p.stderr
+    s = spec_of(b)
+    paths = [d["path"] for d in s["linux"]["devices"]]
+    assert paths == ["/dev/kfd", "/dev/dri/renderD136", "/dev/dri/renderD152"]
+    rules = [r for r in s["linux"]["resources"]["devices"] if r["allow"]]
+    assert {(r["major"], r["minor"]) for r in rules} == {(241, 0), (226, 136), (226, 152)}
+    assert s["annotations"]["amd.com/gpu.injected"] == "1,3"
+    assert s["linux"]["resources"]["devices"][0] == {"allow": False, "access": "rwm"}  # existing deny-all kept
+
+
+def test_prestart_reads_oci_state_from_stdin(root, tmp_path):
+    b = bundle(tmp_path, annotations={"amd.com/gpu.devices": "all"})
+    state = json.dumps({"ociVersion": "1.1.0", "id": "c1", "status": "creating", "pid": 1, "bundle": b})
+    p = run(["prestart", "--root", root], state)
+    assert p.returncode == 0, p.stderr
+    assert len(spec_of(b)["linux"]["devices"]) == 5
+
+
+def test_selectors_bdf_and_unknown(root, tmp_path):
+    b = bundle(tmp_path)
+    p = run(["apply", "--bundle", b, "--root", root, "--devices", "0000:0a:00.0"])
+    assert p.returncode == 0, p.stderr
+    assert [d["path"] for d in spec_of(b)["linux"]["devices"]][1] == "/dev/dri/renderD136"
+    p = run(["apply", "--bundle", b, "--root", root, "--devices", "7"])
+    assert p.returncode == 1 and "unknown device" in p.stderr
+
+
+def test_non_gpu_container_untouched(root, tmp_path):
+    b = bundle(tmp_path)
+    before = open(os.path.join(b, "config.json")).read()
+    assert run(["apply", "--bundle", b, "--root", root]).returncode == 0
+    assert open(os.path.join(b, "config.json")).read() == before
+    assert run(["apply", "--bundle", b, "--root", root, "--devices", "none"]).returncode == 0
+
+
+def test_mount_rocm_and_dry_run(root, tmp_path):
+    b = bundle(tmp_path, env=["AMD_VISIBLE_DEVICES=0"])
+    p = run(["apply", "--bundle", b, "--root", root, "--mount-rocm", "--dry-run"])
+    assert p.returncode == 0
+    out = json.loads(p.stdout)
+    assert out["mounts"][0]["destination"] == "/opt/rocm" and "ro" in out["mounts"][0]["options"]
+    assert "devices" not in spec_of(b)["linux"]  # dry run did not write
+
+
+@pytest.mark.parametrize("bad", ['{"bundle": 5}', "not json", "{}"])
+def test_bad_state(root, bad):
+    p = run(["prestart", "--root", root], bad)
+    assert p.returncode == 1
+
+
+def test_bad_config_json(root, tmp_path):
+    b = tmp_path / "bb"
+    b.mkdir()
+    (b / "config.json").write_text('{"process": {"env": ["AMD_VISIBLE_DEVICES=0"]}, "x": [1, 2,')
+    p = run(["apply", "--bundle", str(b), "--root", root])
+    assert p.returncode == 1 and "json" in p.stderr
+
+
+def test_json_roundtrip_escapes(root, tmp_path):
+    b = bundle(tmp_path, env=['AMD_VISIBLE_DEVICES=0', 'X=a"b\\cé\n'], extra={"hostname": "h☃"})
+    assert run(["apply", "--bundle", b, "--root", root]).returncode == 0
+    s = spec_of(b)
+    assert 'X=a"b\\cé\n' in s["process"]["env"] and s["hostname"] == "h☃"
