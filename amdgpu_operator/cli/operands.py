@@ -33,7 +33,7 @@ def build_parser() -> argparse.ArgumentParser:
     t.add_argument("--mount-rocm", action="store_true")
 
     v = sub.add_parser("validate", help="operator-validator steps")
-    v.add_argument("step", choices=["driver", "toolkit", "workload", "plugin", "complete"])
+    v.add_argument("step", choices=["driver", "toolkit", "workload", "plugin", "gpu", "complete"])
     v.add_argument("--resource", default="amd.com/gpu")
     v.add_argument("--timeout", type=float, default=600.0)
 
@@ -145,6 +145,8 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             if V.read_ready(env, "plugin") is None:
                 pod_args = _plugin_pod_args(extra)
                 V.validate_plugin(env, a.resource, pod_args=pod_args, timeout=a.timeout, stop=stop)
+        elif a.step == "gpu":
+            V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop)
         else:
             V.complete(env)
             ready()

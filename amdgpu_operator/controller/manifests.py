@@ -243,10 +243,14 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     inits = [_wait_init("driver-validation", image, v.imagePullPolicy, "driver")]
     if spec.toolkit.enabled:
         inits.append(_wait_init("toolkit-validation", image, v.imagePullPolicy, "toolkit"))
-    inits.append(_wait_init("workload-validation", image, v.imagePullPolicy, "workload", wl_args))
     if v.pluginValidation and spec.devicePlugin.enabled:
-        inits.append(_wait_init("plugin-validation", image, v.imagePullPolicy, "plugin",
+        # workload (all GPUs, RCCL over xGMI) and plugin (1-GPU pods through the
+        # device plugin + OCI hook) validation run concurrently: the plugin pods
+        # only need a registered device plugin, not the workload result
+        inits.append(_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu",
                                 ["--resource", spec.devicePlugin.resourceName, *wl_args]))
+    else:
+        inits.append(_wait_init("workload-validation", image, v.imagePullPolicy, "workload", wl_args))
     ctr = _container("amd-operator-validator", image, v.imagePullPolicy, ["validate", "complete"],
                      [_mount("run-amd-validations", VALIDATIONS_HOST_DIR)], list(v.env), True,
                      v.resources.model_dump())

@@ -212,13 +212,21 @@ class RestClient:
                 yield ev["type"], ev["object"]
 
 
-def contains(live, desired) -> bool:
+# maps the operator owns completely: an extra key on the live object is drift
+# (e.g. a nodeSelector key would move operand pods), not a server default
+EXACT_KEYS = ("nodeSelector", "matchLabels", "args", "command")
+
+
+def contains(live, desired, key: str = "") -> bool:
     """True when every field of ``desired`` is present with the same value in
-    ``live`` (server-side defaults on ``live`` are ignored)."""
+    ``live`` (server-side defaults on ``live`` are ignored, except under the
+    fully-owned :data:`EXACT_KEYS`)."""
+    if key in EXACT_KEYS:
+        return live == desired
     if isinstance(desired, dict):
         if not isinstance(live, dict):
             return False
-        return all(k in live and contains(live[k], v) for k, v in desired.items())
+        return all(k in live and contains(live[k], v, k) for k, v in desired.items())
     if isinstance(desired, list):
         if not isinstance(live, list) or len(live) != len(desired):
             return False

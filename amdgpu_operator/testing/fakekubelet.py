@@ -51,6 +51,7 @@ class FakeKubelet:
         self.assignments: dict[tuple[str, str, str], tuple[str, list[str]]] = {}  # (ns,pod,ctr) -> (res, ids)
         self.register_calls = 0
         self._lock = threading.Lock()
+        self._alloc_lock = threading.Lock()
         self._server: grpc.Server | None = None
         self._podres_server: grpc.Server | None = None
         self._registered = threading.Condition()
@@ -216,6 +217,11 @@ class FakeKubelet:
     # ------------------------------------------------------------- allocation
     def allocate(self, resource: str, count: int, namespace: str = "default", pod: str = "pod",
                  container: str = "main", must_include: list[str] | None = None):
+        # kubelet's device manager admits one pod at a time (devicemanager mutex)
+        with self._alloc_lock:
+            return self._allocate(resource, count, namespace, pod, container, must_include)
+
+    def _allocate(self, resource, count, namespace, pod, container, must_include):
         res = self.resources[resource]
         free = self.free_devices(resource)
         if count > len(free):

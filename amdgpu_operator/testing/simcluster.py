@@ -240,7 +240,12 @@ class SimCluster:
 
     def _launch(self, argv, env, device, timeout) -> ProcResult:
         if self.fake_gpu and argv and os.path.basename(argv[0]) == "amdgpu-validator":
-            return fake_validator_result(argv)
+            if self.fake_gpu != "procs":
+                return fake_validator_result(argv)
+            # run a stand-in process through the real launcher path (multi-rank rehearsal)
+            import sys
+
+            argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", *argv[1:]]
         if self.launcher is not None:
             return self.launcher(argv, env, device, timeout)
         return run_local(argv, env, timeout)
@@ -391,6 +396,8 @@ class SimCluster:
     # -------------------------------------------------------------- kubelet
     def _kubelet_loop(self, node: SimNode) -> None:
         sel = f"spec.nodeName={node.spec.name}"
+        threading.Thread(target=self._kubelet_resync, args=(node,), daemon=True,
+                         name=f"sim-kubelet-resync-{node.spec.name}").start()
         while not self.stop_event.is_set():
             try:
                 for etype, pod in self.client.watch("v1", "Pod", field_selector=sel, stop=self.stop_event):
@@ -399,7 +406,27 @@ class SimCluster:
                 log.debug("kubelet watch: %s", e)
                 self.stop_event.wait(0.1)
 
+    def _kubelet_resync(self, node: SimNode) -> None:
+        """Periodic relist (like kubelet's sync loop): pods missed by the watch
+        are started, pods deleted behind its back are stopped."""
+        sel = f"spec.nodeName={node.spec.name}"
+        while not self.stop_event.wait(0.5):
+            try:
+                live = {p["metadata"]["name"]: p for p in self.client.list("v1", "Pod", field_selector=sel)}
+            except Exception:  # noqa: BLE001
+                continue
+            with self._lock:
+                for name, pod in live.items():
+                    if name not in node.pods:
+                        self._on_pod(node, "ADDED", pod)
+                for name in [n for n in node.pods if n not in live]:
+                    self._on_pod(node, "DELETED", {"metadata": {"name": name}})
+
     def _on_pod(self, node: SimNode, etype: str, pod: dict) -> None:
+        with self._lock:
+            self._on_pod_locked(node, etype, pod)
+
+    def _on_pod_locked(self, node: SimNode, etype: str, pod: dict) -> None:
         name = pod["metadata"]["name"]
         if etype == "DELETED":
             run = node.pods.pop(name, None)
@@ -528,7 +555,23 @@ class SimCluster:
             if self.is_ready(expect_allocatable):
                 return time.perf_counter() - t0
             time.sleep(self.poll_s)
-        raise TimeoutError(f"cluster not ready after {timeout}s: {json.dumps((self.policy() or {}).get('status'))[:2000]}")
+        raise TimeoutError(f"cluster not ready after {timeout}s:\n{self.diagnostics()}")
+
+    def diagnostics(self) -> str:
+        """Policy status, node labels/allocatable and every pod's phase (debugging aid)."""
+        out = {"policy": (self.policy() or {}).get("status"), "nodes": {}, "pods": {}}
+        for n in self.client.list("v1", "Node"):
+            out["nodes"][n["metadata"]["name"]] = {
+                "labels": {k: v for k, v in (n["metadata"].get("labels") or {}).items() if k.startswith("amd.com")},
+                "allocatable": (n.get("status") or {}).get("allocatable")}
+        for p in self.client.list("v1", "Pod"):
+            st = p.get("status") or {}
+            out["pods"][p["metadata"]["name"]] = {"phase": st.get("phase"), "message": st.get("message", "")[:500],
+                                                  "ready": [c.get("ready") for c in st.get("containerStatuses", [])]}
+        for name, node in self.nodes.items():
+            out["nodes"].setdefault(name, {})["validations"] = sorted(os.listdir(node.env.validations_dir)) \
+                if os.path.isdir(node.env.validations_dir) else []
+        return json.dumps(out, indent=1, default=str)[:20000]
 
     def pods(self, namespace: str | None = None) -> list[dict]:
         return self.client.list("v1", "Pod", namespace or self.namespace)

@@ -142,15 +142,27 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     rdv = os.path.join(env.validations_dir, "rendezvous", run_id)
     os.makedirs(rdv, exist_ok=True)
     counter_env = {"AMDGPU_VALIDATOR_COUNTERS": "1"} if "--counter-gate" in args else {}
+    steps = _steps_of(args)
+    kernel_steps = [s for s in steps if s != "rccl"]
+    # RCCL runs in its own process per GPU, concurrently with the kernel
+    # checks: loading librccl (~570 MB of device code) and its communicator
+    # set-up would otherwise hold the HIP runtime of the kernel process.  A
+    # single-GPU node has no collective to validate (no xGMI peer).
+    run_rccl = "rccl" in steps and world > 1
+    jobs = [(r, _with_steps(args, kernel_steps), run_id, counter_env) for r in range(world)]
+    if run_rccl:
+        jobs += [(r, _with_steps(_drop_flag(args, "--counter-gate"), ["hip", "rccl"]), run_id + "-rccl", {})
+                 for r in range(world)]
 
-    def one(rank: int):
-        argv = workload_argv(args, rank, world, rdv, run_id, gpus[rank].index)
-        return env.launch(argv, counter_env, device=gpus[rank].index, timeout=timeout)
+    def one(job):
+        rank, jargs, rid, jenv = job
+        argv = workload_argv(jargs, rank, world, rdv, rid, gpus[rank].index)
+        return env.launch(argv, jenv, device=gpus[rank].index, timeout=timeout)
 
-    with ThreadPoolExecutor(max_workers=world) as ex:
-        results = list(ex.map(one, range(world)))
+    with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+        results = list(ex.map(one, jobs))
     reports = []
-    for r, res in enumerate(results):
+    for (rank, _, rid, _), res in zip(jobs, results):
         try:
             rep = json.loads(res.stdout.strip().splitlines()[-1]) if res.stdout.strip() else {}
         except ValueError:
@@ -159,7 +171,21 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         rep["process_seconds"] = round(res.seconds, 4)
         if res.rc != 0:
             rep["stderr"] = res.stderr[-2000:]
-        reports.append(rep)
+        if rid.endswith("-rccl"):
+            main = reports[rank]
+            main["steps"] = main.get("steps", []) + [s for s in rep.get("steps", []) if s.get("name") == "rccl"]
+            main["ok"] = bool(main.get("ok")) and bool(rep.get("ok"))
+            main["rc"] = main.get("rc", 0) or rep["rc"]
+            main["rccl_process_seconds"] = rep["process_seconds"]
+            if rep.get("error"):
+                main["error"] = rep["error"]
+            if res.rc != 0:
+                main["stderr"] = rep.get("stderr", "")
+        else:
+            reports.append(rep)
+    if "rccl" in steps and not run_rccl:
+        for rep in reports:
+            rep.setdefault("steps", []).append({"name": "rccl", "ok": True, "skipped": "single GPU: no xGMI peer"})
     ok = all(r.get("rc") == 0 and r.get("ok") for r in reports)
     summary = {"ok": ok, "world": world, "seconds": time.perf_counter() - t0, "ranks": reports}
     if not ok:
@@ -167,6 +193,27 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         raise StepFailed(f"workload validation failed on ranks {bad}")
     write_ready(env, "workload", summary)
     return summary
+
+
+ALL_STEPS = ("hip", "vecadd", "gemm", "hbm", "xgmi", "rccl")
+
+
+def _steps_of(args: list[str]) -> list[str]:
+    if "--steps" in args:
+        return [s for s in args[args.index("--steps") + 1].split(",") if s]
+    return list(ALL_STEPS)
+
+
+def _with_steps(args: list[str], steps: list[str]) -> list[str]:
+    out = list(args)
+    if "--steps" in out:
+        i = out.index("--steps")
+        del out[i:i + 2]
+    return out + ["--steps", ",".join(steps if "hip" in steps else ["hip", *steps])]
+
+
+def _drop_flag(args: list[str], flag: str) -> list[str]:
+    return [a for a in args if a != flag]
 
 
 def _drop_step(args: list[str], step: str) -> list[str]:
@@ -255,6 +302,38 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                "seconds": time.perf_counter() - t0}
     write_ready(env, "plugin", summary)
     return summary
+
+
+def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURCE_NAME,
+                 pod_args: list[str] | None = None, timeout: float = 600.0, stop=None) -> dict:
+    """Workload and plugin validation concurrently (each skipped if already done)."""
+    t0 = time.perf_counter()
+    results: dict = {}
+    errors: list[str] = []
+
+    def workload():
+        try:
+            if read_ready(env, "workload") is None:
+                results["workload"] = validate_workload(env, workload_args, timeout)
+        except Exception as e:  # noqa: BLE001
+            errors.append(f"workload: {e}")
+
+    def plugin():
+        try:
+            if read_ready(env, "plugin") is None:
+                results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop)
+        except Exception as e:  # noqa: BLE001
+            errors.append(f"plugin: {e}")
+
+    threads = [threading.Thread(target=workload, name="validate-workload"),
+               threading.Thread(target=plugin, name="validate-plugin")]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    if errors:
+        raise StepFailed("; ".join(errors))
+    return {"ok": True, "seconds": time.perf_counter() - t0, **results}
 
 
 def complete(env: NodeEnv) -> dict:

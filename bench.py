@@ -48,10 +48,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--fake-gpu", action="store_true", help="CPU-only: synthetic sysfs, no GPU processes")
+    ap.add_argument("--fake-gpu-procs", action="store_true",
+                    help="CPU-only, but start stand-in validator processes through the rank launcher")
     ap.add_argument("--sysfs-root", default=None, help="default: / when a GPU is present, else synthetic")
     ap.add_argument("--quick-workload", action="store_true", help="small validator sizes (CI)")
     ap.add_argument("--no-counter-gate", action="store_true", help="skip the rocprofiler counter gate (outer profiler)")
-    ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--detail", default=None, help="write per-step breakdown JSON here")
     return ap.parse_args()
 
@@ -131,7 +133,9 @@ def main():
     if world > 1 and args.gpus != world:
         args.gpus = world
     has_gpu = gpu_available()
-    fake_gpu = args.fake_gpu or not has_gpu
+    fake_gpu = args.fake_gpu or args.fake_gpu_procs or not has_gpu
+    if fake_gpu and args.fake_gpu_procs:
+        fake_gpu = "procs"
 
     import torch
 
@@ -163,6 +167,9 @@ def main():
     errors: list[str] = []
 
     def driver_thread(n_steps: int, out: list):
+        import faulthandler
+
+        faulthandler.dump_traceback_later(args.timeout + 60, exit=False)  # stacks if a step wedges
         try:
             for _ in range(n_steps):
                 out.append(one_bring_up(args, n_gpus, launcher, workdir, fake_gpu))
@@ -171,6 +178,7 @@ def main():
 
             errors.append(f"{e}\n{traceback.format_exc()}")
         finally:
+            faulthandler.cancel_dump_traceback_later()
             if launcher is not None:
                 launcher.request_stop()
 

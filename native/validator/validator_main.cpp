@@ -17,6 +17,7 @@
 // validations directory): the RCCL unique id, IPC handles and step barriers.
 // Prints one JSON report; exit status 0 = validated.
 
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -41,6 +42,41 @@
 namespace {
 
 using Clock = std::chrono::steady_clock;
+
+// RCCL is dlopen'ed (not linked): librccl's device code is large and loading
+// it costs ~0.5 s of process start-up plus ~1.5 s of kernel loading in
+// ncclCommInitRank.  Only the rccl step needs it, and that step's init runs on
+// a background thread while the kernel steps execute (see main()).
+struct Rccl {
+  void* dl = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+
+  bool load(std::string* err) {
+    for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+      dl = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+      if (dl) break;
+    }
+    if (!dl) {
+      *err = std::string("dlopen librccl failed: ") + dlerror();
+      return false;
+    }
+    GetUniqueId = reinterpret_cast<decltype(GetUniqueId)>(dlsym(dl, "ncclGetUniqueId"));
+    CommInitRank = reinterpret_cast<decltype(CommInitRank)>(dlsym(dl, "ncclCommInitRank"));
+    AllReduce = reinterpret_cast<decltype(AllReduce)>(dlsym(dl, "ncclAllReduce"));
+    CommDestroy = reinterpret_cast<decltype(CommDestroy)>(dlsym(dl, "ncclCommDestroy"));
+    GetErrorString = reinterpret_cast<decltype(GetErrorString)>(dlsym(dl, "ncclGetErrorString"));
+    if (!GetUniqueId || !CommInitRank || !AllReduce || !CommDestroy || !GetErrorString) {
+      *err = "librccl is missing NCCL API symbols";
+      return false;
+    }
+    return true;
+  }
+};
+Rccl g_rccl;
 
 struct Args {
   int device = 0;
@@ -83,7 +119,7 @@ struct Step {
 #define NCCL_OK(x)                                                                    \
   do {                                                                                \
     ncclResult_t r_ = (x);                                                            \
-    if (r_ != ncclSuccess) throw std::runtime_error(std::string(#x) + ": " + ncclGetErrorString(r_)); \
+    if (r_ != ncclSuccess) throw std::runtime_error(std::string(#x) + ": " + g_rccl.GetErrorString(r_)); \
   } while (0)
 
 double secs(Clock::time_point a) { return std::chrono::duration<double>(Clock::now() - a).count(); }
@@ -391,28 +427,50 @@ Step step_xgmi(const Args& a, hipStream_t st, const Rendezvous& rv) {
   return s;
 }
 
-Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv) {
+// Communicator set-up, run on its own thread from the start of the process.
+struct RcclInit {
+  ncclComm_t comm = nullptr;
+  double init_s = 0, load_s = 0;
+  std::string error;
+};
+
+void rccl_init(const Args& a, const Rendezvous& rv, RcclInit* out) {
+  try {
+    auto t0 = Clock::now();
+    std::string err;
+    if (!g_rccl.load(&err)) throw std::runtime_error(err);
+    out->load_s = secs(t0);
+    HIP_OK(hipSetDevice(a.device));
+    ncclUniqueId id;
+    const std::string idname = a.run_id + "-nccl-id";
+    if (a.rank == 0) {
+      NCCL_OK(g_rccl.GetUniqueId(&id));
+      rv.publish(idname, &id, sizeof(id));
+    } else {
+      auto buf = rv.fetch(idname, sizeof(id));
+      memcpy(&id, buf.data(), sizeof(id));
+    }
+    auto ti = Clock::now();
+    NCCL_OK(g_rccl.CommInitRank(&out->comm, a.world, id, a.rank));
+    out->init_s = secs(ti);
+  } catch (const std::exception& e) {
+    out->error = e.what();
+  }
+}
+
+Step step_rccl(const Args& a, hipStream_t st, std::thread* init_thread, RcclInit* ri) {
   auto t0 = Clock::now();
   Step s{"rccl"};
-  ncclUniqueId id;
-  const std::string idname = a.run_id + "-nccl-id";
-  if (a.rank == 0) {
-    NCCL_OK(ncclGetUniqueId(&id));
-    rv.publish(idname, &id, sizeof(id));
-  } else {
-    auto buf = rv.fetch(idname, sizeof(id));
-    memcpy(&id, buf.data(), sizeof(id));
-  }
-  auto ti = Clock::now();
-  ncclComm_t comm;
-  NCCL_OK(ncclCommInitRank(&comm, a.world, id, a.rank));
-  const double init_s = secs(ti);
+  init_thread->join();
+  const double wait_s = secs(t0);
+  if (!ri->error.empty()) throw std::runtime_error("rccl init: " + ri->error);
+  ncclComm_t comm = ri->comm;
   const int64_t n = a.rccl_elems;
   float* buf;
   HIP_OK(hipMalloc(&buf, n * 4));
   std::vector<float> host(n, (float)(a.rank + 1));
   HIP_OK(hipMemcpyAsync(buf, host.data(), n * 4, hipMemcpyHostToDevice, st));
-  NCCL_OK(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
+  NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
   HIP_OK(hipMemcpyAsync(host.data(), buf, n * 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   const float expect = a.world * (a.world + 1) / 2.0f;
@@ -423,13 +481,13 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv) {
   HIP_OK(hipEventCreate(&e1));
   const int iters = 5;
   HIP_OK(hipEventRecord(e0, st));
-  for (int i = 0; i < iters; ++i) NCCL_OK(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
+  for (int i = 0; i < iters; ++i) NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
   HIP_OK(hipEventRecord(e1, st));
   HIP_OK(hipEventSynchronize(e1));
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));
   ms /= iters;
-  NCCL_OK(ncclCommDestroy(comm));
+  NCCL_OK(g_rccl.CommDestroy(comm));
   (void)hipFree(buf);
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
@@ -437,9 +495,9 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv) {
   const double busbw = a.world > 1 ? algbw * 2.0 * (a.world - 1) / a.world : 0.0;
   s.ok = bad == 0;
   s.seconds = secs(t0);
-  s.detail = fmt("\"world\": %d, \"bytes\": %lld, \"comm_init_s\": %.4f, \"ms\": %.4f, \"algbw_gbps\": %.1f, "
-                 "\"busbw_gbps\": %.1f, \"mismatches\": %lld",
-                 a.world, (long long)(n * 4), init_s, ms, algbw, busbw, (long long)bad);
+  s.detail = fmt("\"world\": %d, \"bytes\": %lld, \"lib_load_s\": %.4f, \"comm_init_s\": %.4f, \"init_wait_s\": %.4f, "
+                 "\"ms\": %.4f, \"algbw_gbps\": %.1f, \"busbw_gbps\": %.1f, \"mismatches\": %lld",
+                 a.world, (long long)(n * 4), ri->load_s, ri->init_s, wait_s, ms, algbw, busbw, (long long)bad);
   return s;
 }
 
@@ -510,19 +568,23 @@ int main(int argc, char** argv) {
   hipStream_t st = nullptr;
   hipDeviceProp_t prop;
   memset(&prop, 0, sizeof(prop));
+  std::thread rccl_thread;
+  RcclInit rccl_state;
   try {
     steps.push_back(step_hip(a, &prop));
     ok = steps.back().ok;
+    if (ok && has_step(a, "rccl")) rccl_thread = std::thread(rccl_init, std::cref(a), std::cref(rv), &rccl_state);
     HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
     if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st)), steps.back().ok);
     if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
     if (ok && has_step(a, "xgmi")) ok = (steps.push_back(step_xgmi(a, st, rv)), steps.back().ok);
-    if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, rv)), steps.back().ok);
+    if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, &rccl_thread, &rccl_state)), steps.back().ok);
   } catch (const std::exception& e) {
     ok = false;
     error = e.what();
   }
+  if (rccl_thread.joinable()) rccl_thread.join();
   if (st) (void)hipStreamDestroy(st);
   const double total = secs(t_start);
   std::string out = fmt("{\"ok\": %s, \"rank\": %d, \"world\": %d, \"device\": %d, \"seconds\": %.4f, ", ok ? "true" : "false",

@@ -1,0 +1,199 @@
+"""ClusterPolicy reconciler: states, node labels, drift, disable/enable,
+invalid specs, multiple policies, CRD cleanup."""
+
+import pytest
+
+from amdgpu_operator.api.clusterpolicy import (REFERENCE_SET_FLAGS, ClusterPolicySpec, cluster_policy,
+                                               parse_set_flags, spec_from_values)
+from amdgpu_operator.controller.manifests import STATE_BUILDERS
+from amdgpu_operator.controller.nodes import desired_labels, is_gpu_node
+from amdgpu_operator.controller.reconciler import CP_API, ClusterPolicyReconciler, cleanup_crd
+from amdgpu_operator.helm.crd import crd
+from amdgpu_operator.kube import resources as R
+from amdgpu_operator.kube.client import LocalClient, NotFound
+from amdgpu_operator.kube.fakeapi import FakeApiServer
+
+NS = "gpu-operator-resources"
+GPU_LABEL = {"feature.node.kubernetes.io/pci-1200_1002.present": "true"}
+
+
+@pytest.fixture
+def env():
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Namespace", NS))
+    c.create(R.new("v1", "Node", "gpu-a", labels=GPU_LABEL))
+    c.create(R.new("v1", "Node", "cpu-a"))
+    return c, ClusterPolicyReconciler(c, NS)
+
+
+def ds_names(c):
+    return sorted(d["metadata"]["name"] for d in c.list("apps/v1", "DaemonSet", NS))
+
+
+def mark_all_ds_ready(c, desired=1):
+    for ds in c.list("apps/v1", "DaemonSet", NS):
+        ds["status"] = {"desiredNumberScheduled": desired, "numberReady": desired, "updatedNumberScheduled": desired,
+                        "observedGeneration": ds["metadata"]["generation"]}
+        c.update_status(ds)
+
+
+def test_reference_install_creates_expected_operands(env):
+    c, rec = env
+    c.create(cluster_policy(spec=spec_from_values(parse_set_flags(REFERENCE_SET_FLAGS))))
+    res = rec.reconcile()
+    assert res.state == "notReady" and res.gpu_nodes == 1
+    assert ds_names(c) == ["amd-container-toolkit-daemonset", "amd-device-plugin-daemonset", "amd-driver-daemonset",
+                           "amd-metrics-exporter", "amd-node-status-exporter", "amd-operator-validator",
+                           "gpu-feature-discovery", "node-feature-discovery-worker"]
+    # migManager.enabled=false -> no partition manager (README.md:109)
+    assert "amd-partition-manager" not in ds_names(c)
+    labels = c.get("v1", "Node", "gpu-a")["metadata"]["labels"]
+    assert labels["amd.com/gpu.present"] == "true"
+    assert labels["amd.com/gpu.deploy.driver"] == "true"
+    assert "amd.com/gpu.deploy.partition-manager" not in labels
+    assert "amd.com/gpu.present" not in c.get("v1", "Node", "cpu-a")["metadata"]["labels"] if c.get(
+        "v1", "Node", "cpu-a")["metadata"].get("labels") else True
+    drv = c.get("apps/v1", "DaemonSet", "amd-driver-daemonset", NS)
+    ctrs = [x["name"] for x in drv["spec"]["template"]["spec"]["containers"]]
+    assert ctrs == ["amd-driver-ctr", "amd-driver-health"]  # 2/2 like README.md:138-139
+    assert drv["spec"]["template"]["spec"]["nodeSelector"] == {"amd.com/gpu.deploy.driver": "true"}
+
+
+def test_ready_requires_daemonsets_and_validated_nodes(env):
+    c, rec = env
+    c.create(cluster_policy())
+    rec.reconcile()
+    mark_all_ds_ready(c)
+    assert rec.reconcile().state == "notReady"  # node not validated yet
+    c.patch("v1", "Node", "gpu-a", {"metadata": {"labels": {"amd.com/gpu.validated": "true"}}})
+    res = rec.reconcile()
+    assert res.state == "ready"
+    st = c.get(CP_API, "ClusterPolicy", "cluster-policy")["status"]
+    assert st["state"] == "ready" and st["timeToReadySeconds"] >= 0
+    assert R.condition(c.get(CP_API, "ClusterPolicy", "cluster-policy"), "Ready")["status"] == "True"
+
+
+def test_reconcile_is_idempotent_and_reverts_drift(env):
+    c, rec = env
+    c.create(cluster_policy())
+    rec.reconcile()
+    assert sum(s.changed for s in rec.reconcile().states) == 0
+    c.patch("apps/v1", "DaemonSet", "amd-device-plugin-daemonset",
+            {"spec": {"template": {"spec": {"nodeSelector": {"x": "y"}}}}}, NS)
+    res = rec.reconcile()
+    assert sum(s.changed for s in res.states) == 1
+    ds = c.get("apps/v1", "DaemonSet", "amd-device-plugin-daemonset", NS)
+    assert ds["spec"]["template"]["spec"]["nodeSelector"] == {"amd.com/gpu.deploy.device-plugin": "true"}
+    c.delete("apps/v1", "DaemonSet", "gpu-feature-discovery", NS)
+    rec.reconcile()
+    assert "gpu-feature-discovery" in ds_names(c)
+
+
+def test_disable_operand_removes_objects_and_labels(env):
+    c, rec = env
+    c.create(cluster_policy())
+    rec.reconcile()
+    cp = c.get(CP_API, "ClusterPolicy", "cluster-policy")
+    cp["spec"]["gfd"]["enabled"] = False
+    cp["spec"]["migManager"]["enabled"] = True
+    c.update(cp)
+    res = rec.reconcile()
+    assert "gpu-feature-discovery" not in ds_names(c)
+    assert "amd-partition-manager" in ds_names(c)
+    labels = c.get("v1", "Node", "gpu-a")["metadata"]["labels"]
+    assert "amd.com/gpu.deploy.gpu-feature-discovery" not in labels
+    assert labels["amd.com/gpu.deploy.partition-manager"] == "true"
+    assert {s.name: s.enabled for s in res.states}["state-gpu-feature-discovery"] is False
+
+
+def test_user_opt_out_label_is_sticky(env):
+    c, rec = env
+    c.patch("v1", "Node", "gpu-a", {"metadata": {"labels": {"amd.com/gpu.deploy.driver": "false"}}})
+    c.create(cluster_policy())
+    rec.reconcile()
+    assert c.get("v1", "Node", "gpu-a")["metadata"]["labels"]["amd.com/gpu.deploy.driver"] == "false"
+
+
+def test_node_losing_gpu_is_unlabelled(env):
+    c, rec = env
+    c.create(cluster_policy())
+    rec.reconcile()
+    c.patch("v1", "Node", "gpu-a", {"metadata": {"labels": {k: None for k in GPU_LABEL}}})
+    rec.reconcile()
+    labels = c.get("v1", "Node", "gpu-a")["metadata"]["labels"]
+    assert not any(k.startswith("amd.com/gpu.") for k in labels)
+
+
+def test_invalid_spec_sets_error(env):
+    c, rec = env
+    bad = cluster_policy()
+    bad["spec"]["driver"]["enabeld"] = True
+    c.create(bad)
+    res = rec.reconcile()
+    assert res.state == "error"
+    st = c.get(CP_API, "ClusterPolicy", "cluster-policy")["status"]
+    assert st["state"] == "error" and R.condition({"status": st}, "Error")["status"] == "True"
+    assert c.list("apps/v1", "DaemonSet", NS) == []
+
+
+def test_second_policy_is_ignored(env):
+    c, rec = env
+    c.create(cluster_policy("first"))
+    c.create(cluster_policy("second"))
+    rec.reconcile()
+    assert c.get(CP_API, "ClusterPolicy", "second")["status"]["state"] == "ignored"
+
+
+def test_zero_gpu_cluster_converges(env):
+    c, rec = env
+    c.delete("v1", "Node", "gpu-a")
+    c.create(cluster_policy())
+    rec.reconcile()
+    mark_all_ds_ready(c, desired=0)
+    for ds in c.list("apps/v1", "DaemonSet", NS):
+        if ds["metadata"]["name"].startswith("node-feature"):
+            ds["status"] = {"desiredNumberScheduled": 1, "numberReady": 1, "updatedNumberScheduled": 1,
+                            "observedGeneration": 1}
+            c.update_status(ds)
+    assert rec.reconcile().state == "ready"
+
+
+def test_owner_references_make_operands_garbage_collected(env):
+    c, rec = env
+    c.create(cluster_policy())
+    rec.reconcile()
+    c.delete(CP_API, "ClusterPolicy", "cluster-policy")
+    assert c.list("apps/v1", "DaemonSet", NS) == []
+
+
+def test_cleanup_crd(env):
+    c, rec = env
+    c.create(crd())
+    c.create(cluster_policy())
+    assert cleanup_crd(c) is True
+    assert c.list(CP_API, "ClusterPolicy") == []
+    with pytest.raises(NotFound):
+        c.get("apiextensions.k8s.io/v1", "CustomResourceDefinition", "clusterpolicies.amd.com")
+    assert cleanup_crd(c) is False
+
+
+def test_every_state_builder_yields_valid_objects():
+    spec = ClusterPolicySpec.model_validate({"migManager": {"enabled": True},
+                                             "dcgmExporter": {"serviceMonitor": {"enabled": True}}})
+    owner = [{"uid": "u", "kind": "ClusterPolicy", "name": "cp", "apiVersion": CP_API}]
+    for name, fn in STATE_BUILDERS.items():
+        for o in fn(spec, NS, owner):
+            R.rtype_of(o)  # registered kind
+            assert o["metadata"]["name"]
+            if o["kind"] == "DaemonSet":
+                t = o["spec"]["template"]
+                assert t["metadata"]["labels"]["app"] == o["metadata"]["name"]
+                assert all(ct["command"] == ["amdgpu-operator"] for ct in t["spec"]["containers"])
+
+
+def test_node_detection_rules():
+    assert is_gpu_node({"metadata": {"labels": {"feature.node.kubernetes.io/pci-1002.present": "true"}}})
+    assert is_gpu_node({"metadata": {}, "status": {"capacity": {"amd.com/gpu": "8"}}})
+    assert not is_gpu_node({"metadata": {"labels": {"feature.node.kubernetes.io/pci-10de.present": "true"}}})
+    patch = desired_labels({"metadata": {"labels": GPU_LABEL}}, ClusterPolicySpec())
+    assert patch["amd.com/gpu.present"] == "true"

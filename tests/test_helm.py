@@ -1,0 +1,102 @@
+"""Helm chart: reference install flags, generated CRD/values freshness,
+template rendering (no helm binary in the environment)."""
+
+import os
+
+import pytest
+import yaml
+
+from amdgpu_operator.api.clusterpolicy import (REFERENCE_SET_FLAGS, ClusterPolicySpec, parse_set_flags,
+                                               spec_from_values)
+from amdgpu_operator.helm import render as H
+from amdgpu_operator.helm.crd import crd_yaml
+from amdgpu_operator.helm.values import values_yaml
+
+
+def test_crd_file_is_generated_from_spec():
+    with open(os.path.join(H.CHART_DIR, "crds", "amd.com_clusterpolicies.yaml")) as f:
+        assert f.read() == crd_yaml(), "run python -m amdgpu_operator.helm.crd > deploy/.../crds/amd.com_clusterpolicies.yaml"
+
+
+def test_values_file_is_generated_from_spec():
+    with open(os.path.join(H.CHART_DIR, "values.yaml")) as f:
+        assert f.read() == values_yaml(), "run python -m amdgpu_operator.helm.values > deploy/helm/amd-gpu-operator/values.yaml"
+
+
+def test_reference_set_flags_render():
+    docs = H.render_chart(set_flags=REFERENCE_SET_FLAGS)
+    kinds = {(d["kind"], d["metadata"]["name"]) for d in docs}
+    assert ("ClusterPolicy", "cluster-policy") in kinds
+    assert ("Deployment", "amd-gpu-operator") in kinds
+    assert ("Job", "amd-gpu-operator-cleanup-crd") in kinds  # operator.cleanupCRD=true
+    cp = next(d for d in docs if d["kind"] == "ClusterPolicy")
+    spec = ClusterPolicySpec.model_validate(cp["spec"])
+    want = spec_from_values(H.chart_values(set_flags=REFERENCE_SET_FLAGS))
+    assert spec == want
+    assert spec.driver.enabled and spec.toolkit.enabled and spec.devicePlugin.enabled
+    assert spec.nodeStatusExporter.enabled and spec.gfd.enabled and not spec.migManager.enabled
+    assert spec.operator.cleanupCRD
+    job = next(d for d in docs if d["metadata"]["name"] == "amd-gpu-operator-cleanup-crd")
+    assert job["metadata"]["annotations"]["helm.sh/hook"] == "pre-delete"
+    assert job["spec"]["template"]["spec"]["containers"][0]["args"] == ["cleanup-crd"]
+
+
+def test_cleanup_hook_absent_by_default():
+    docs = H.render_chart()
+    assert not any(d["metadata"]["name"] == "amd-gpu-operator-cleanup-crd" for d in docs)
+
+
+def test_namespace_and_release_flow_into_objects():
+    docs = H.render_chart(release_name="rel", namespace="gpu-operator-resources")
+    dep = next(d for d in docs if d["kind"] == "Deployment")
+    assert dep["metadata"]["namespace"] == "gpu-operator-resources"
+    assert dep["metadata"]["labels"]["app.kubernetes.io/instance"] == "rel"
+    assert dep["spec"]["template"]["spec"]["containers"][0]["args"][:3] == ["operator", "--namespace",
+                                                                            "gpu-operator-resources"]
+    crb = next(d for d in docs if d["kind"] == "ClusterRoleBinding")
+    assert crb["subjects"][0]["namespace"] == "gpu-operator-resources"
+
+
+def test_overrides_reach_the_cluster_policy():
+    docs = H.render_chart(set_flags=["devicePlugin.partitionStrategy=mixed", "dcgmExporter.port=9500",
+                                     "validator.workload.gemmN=8192", "migManager.enabled=true"])
+    cp = next(d for d in docs if d["kind"] == "ClusterPolicy")
+    s = ClusterPolicySpec.model_validate(cp["spec"])
+    assert s.devicePlugin.partitionStrategy == "mixed" and s.dcgmExporter.port == 9500
+    assert s.validator.workload.gemmN == 8192 and s.migManager.enabled
+
+
+def test_crd_schema_accepts_rendered_spec_keys():
+    crd = H.load_crd()
+    props = crd["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]["spec"]["properties"]
+    for key in ("driver", "toolkit", "devicePlugin", "nodeStatusExporter", "gfd", "migManager", "operator",
+                "dcgmExporter", "validator", "nfd", "daemonsets"):
+        assert key in props, key
+    assert props["driver"]["properties"]["enabled"]["type"] == "boolean"
+    assert "$ref" not in yaml.safe_dump(crd)
+
+
+def test_values_aliases():
+    assert spec_from_values({"partitionManager": {"enabled": True}}).migManager.enabled
+    assert spec_from_values({"metricsExporter": {"port": 1}}).dcgmExporter.port == 1
+    with pytest.raises(Exception):
+        spec_from_values({"metricsExporter": {}, "dcgmExporter": {}})
+    assert parse_set_flags(["a.b=1", "a.c=true", "d=x", "e=1.5"]) == {"a": {"b": 1, "c": True}, "d": "x", "e": 1.5}
+
+
+def test_template_engine_subset(tmp_path):
+    chart = tmp_path / "c"
+    (chart / "templates").mkdir(parents=True)
+    (chart / "Chart.yaml").write_text("name: c\nversion: 1.0.0\nappVersion: '2'\n")
+    (chart / "templates" / "_h.tpl").write_text('{{- define "n" -}}{{ .Values.x | default "dflt" }}{{- end -}}')
+    (chart / "templates" / "a.yaml").write_text(
+        "a: {{ include \"n\" . }}\n"
+        "{{- if .Values.flag }}\nb: yes\n{{- else if .Values.other }}\nb: other\n{{- else }}\nb: no\n{{- end }}\n"
+        "c: {{ .Values.s | quote }}\n"
+        "d:{{- toYaml .Values.m | nindent 2 }}\n"
+        "{{- range .Values.l }}\n- {{ . }}\n{{- end }}\n"
+        "e: {{ not .Values.flag }}\n")
+    out = H.Renderer(str(chart), {"flag": False, "other": True, "s": 'q"x', "m": {"k": [1, 2]}, "l": [7, 8]}).render()
+    text = out["a.yaml"]
+    assert "a: dflt" in text and "b: other" in text and 'c: "q\\"x"' in text
+    assert "d:\n  k:\n  - 1\n  - 2" in text and "- 7\n- 8" in text and "e: true" in text
