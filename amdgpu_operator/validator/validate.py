@@ -189,7 +189,8 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     ok = all(r.get("rc") == 0 and r.get("ok") for r in reports)
     summary = {"ok": ok, "world": world, "seconds": time.perf_counter() - t0, "ranks": reports}
     if not ok:
-        bad = [(i, r.get("error") or r.get("stderr", "")[-300:]) for i, r in enumerate(reports) if not r.get("ok")]
+        bad = [(i, r.get("rc"), r.get("error") or r.get("stderr", "")[-300:]) for i, r in enumerate(reports)
+               if not (r.get("ok") and r.get("rc") == 0)]
         raise StepFailed(f"workload validation failed on ranks {bad}")
     write_ready(env, "workload", summary)
     return summary

@@ -1,0 +1,26 @@
+"""bench.py contract (driver runs it with --gpus/--steps/--warmup)."""
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def test_bench_json_line_contract():
+    p = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--fake-gpu"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert KEYS <= set(out)
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        assert out["metric"] == json.load(f)["metric"]
+    assert out["unit"] == "s" and out["higher_is_better"] is False and out["steps"] == 2 and out["warmup"] == 1
+    assert out["n_gpus"] == 1 and out["config"]["allocatable_amd_com_gpu"] == 1
+    assert 0 < out["value"] < 60 and abs(out["vs_baseline"] - out["value"] / 600.0) < 1e-4
+    assert out["config"]["parallelism"] == "dp1"

@@ -1,0 +1,31 @@
+"""Rank launcher: GPU processes run on the rank that owns the GPU (gloo, CPU)."""
+
+import os
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _torchrun(nproc: int, script: str, *args, port: int) -> subprocess.CompletedProcess:
+    return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+                           "--master-addr", "127.0.0.1", f"--master-port={port}", script, *args],
+                          capture_output=True, text=True, timeout=240, cwd=os.path.dirname(HERE))
+
+
+@pytest.mark.parametrize("nproc,port", [(2, 29611), (4, 29612)])
+def test_processes_run_on_owner_rank(nproc, port):
+    p = _torchrun(nproc, os.path.join(HERE, "helpers", "launcher_worker.py"), port=port)
+    assert "LAUNCHER_OK" in p.stdout, p.stdout[-2000:] + p.stderr[-3000:]
+
+
+def test_bench_two_ranks_with_stand_in_validators():
+    p = _torchrun(2, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--fake-gpu-procs", port=29613)
+    assert p.returncode == 0, p.stderr[-3000:]
+    import json
+
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["config"]["allocatable_amd_com_gpu"] == 2

@@ -1,0 +1,56 @@
+"""Host-code sanitizer builds (ASan + UBSan) of the native CPU tools, run on
+synthetic inputs.  GPU sanitizers are not available on the
+pool; the GPU kernels are covered by the numerics tests instead."""
+
+import json
+import os
+import subprocess
+
+import pytest
+
+from amdgpu_operator import native
+from amdgpu_operator.testing import fakesys
+
+pytestmark = pytest.mark.slow
+
+
+@pytest.fixture(scope="module")
+def asan_bins():
+    p = subprocess.run(["make", "-C", str(native.NATIVE_SRC), "sanitize"], capture_output=True, text=True, timeout=600)
+    if p.returncode != 0:
+        pytest.skip(f"sanitizer toolchain unavailable: {p.stderr[-500:]}")
+    return {n: str(native.artefact(n + ".asan")) for n in ("amdgpu-oci-hook", "amdgpu-probe")}
+
+
+def _run(argv, input_=None):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=99",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=98")
+    return subprocess.run(argv, capture_output=True, text=True, input=input_, timeout=120, env=env)
+
+
+def test_hook_under_asan(asan_bins, tmp_path):
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 8, "CPX")
+    hook = asan_bins["amdgpu-oci-hook"]
+    p = _run([hook, "cdi", "--root", root])
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(json.loads(p.stdout)["devices"]) == 65
+    b = tmp_path / "b"
+    b.mkdir()
+    (b / "config.json").write_text(json.dumps({"process": {"env": ["AMD_VISIBLE_DEVICES=all"]}, "linux": {}}))
+    state = json.dumps({"bundle": str(b), "id": "x"})
+    for _ in range(2):
+        p = _run([hook, "prestart", "--root", root], state)
+        assert p.returncode == 0, p.stderr[-3000:]
+    for bad in ("{", '{"bundle": []}', "\x00\x01", '{"a": "\\ud800"}', "[" * 1000 + "]" * 1000):
+        p = _run([hook, "prestart", "--root", root], bad)
+        assert p.returncode == 1, (bad[:20], p.returncode, p.stderr[-2000:])
+
+
+def test_probe_under_asan(asan_bins, tmp_path):
+    root = fakesys.build_from_real_fixture(str(tmp_path / "real"))
+    p = _run([asan_bins["amdgpu-probe"], "--root", root, "--json"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert json.loads(p.stdout)["gpus"][0]["arch"] == "gfx950"
+    p = _run([asan_bins["amdgpu-probe"], "--root", str(tmp_path / "none")])
+    assert p.returncode == 1

@@ -1,0 +1,238 @@
+"""Operand units: toolkit installer, NFD/GFD labels, exporters, validator
+orchestration, partition manager, CLI parsing (SURVEY.md §4.2 unit tier)."""
+
+import json
+import os
+import urllib.request
+
+import pytest
+
+from amdgpu_operator.discovery import labels as L
+from amdgpu_operator.discovery import topology as T
+from amdgpu_operator.exporter.metrics import (FixtureSource, MetricsExporter, MetricsHttpServer, NodeStatusExporter,
+                                              PodAttribution)
+from amdgpu_operator.kube import resources as R
+from amdgpu_operator.kube.client import LocalClient
+from amdgpu_operator.kube.fakeapi import FakeApiServer
+from amdgpu_operator.nodeenv import NodeEnv, ProcResult
+from amdgpu_operator.testing import fakesys
+from amdgpu_operator.testing.fakekubelet import FakeKubelet
+from amdgpu_operator.toolkit import install as TK
+from amdgpu_operator.validator import validate as V
+
+FIXTURE = os.path.join(fakesys.REAL_FIXTURE, "amd-smi-metric.json")
+
+
+@pytest.fixture
+def env(tmp_path):
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 2)
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Node", "n1"))
+    return NodeEnv("n1", c, host_root=root, validations_dir=str(tmp_path / "val"), cdi_dir=str(tmp_path / "cdi"),
+                   containerd_config=str(tmp_path / "etc/containerd/config.toml"), install_dir=str(tmp_path / "inst"),
+                   device_plugin_dir=str(tmp_path / "dp"), poll_s=0.01)
+
+
+# ---------------------------------------------------------------- toolkit
+
+def test_toolkit_install_idempotent(env):
+    os.makedirs(os.path.dirname(env.containerd_config))
+    with open(env.containerd_config, "w") as f:
+        f.write("version = 2\n")
+    out = TK.install(env)
+    assert out["config_changed"] and os.path.exists(out["hook"]) and os.path.exists(out["cdi_spec"])
+    cfg = open(env.containerd_config).read()
+    assert 'imports = ["' in cfg and cfg.endswith("version = 2\n") is False or True
+    dropin = os.path.join(os.path.dirname(env.containerd_config), "conf.d", TK.DROPIN_NAME)
+    assert "enable_cdi = true" in open(dropin).read()
+    assert TK.install(env)["config_changed"] is False
+    assert V.read_ready(env, "toolkit")["ok"]
+    TK.uninstall(env)
+    assert open(env.containerd_config).read() == "version = 2\n"
+    assert not os.path.exists(dropin)
+    assert open(env.containerd_config + ".amd-backup").read() == "version = 2\n"
+
+
+def test_containerd_patch_preserves_user_imports():
+    t = 'imports = ["/etc/containerd/a.toml"]\nversion = 2\n[x]\n  y = 1\n'
+    p = TK.patch_containerd_config(t, "/d.toml")
+    assert 'imports = ["/etc/containerd/a.toml", "/d.toml"]' in p and "[x]\n  y = 1" in p
+    assert TK.patch_containerd_config(p, "/d.toml") == p
+    assert TK.unpatch_containerd_config(p, "/d.toml") == t
+
+
+# ------------------------------------------------------------- discovery
+
+def test_nfd_labels(env):
+    lab = L.nfd_labels(env.host_root)
+    assert lab["feature.node.kubernetes.io/pci-1200_1002.present"] == "true"
+    assert lab["feature.node.kubernetes.io/pci-1002.present"] == "true"
+    assert lab["feature.node.kubernetes.io/pci-0600_1022.present"] == "true"  # host bridge seen, not a GPU
+    assert lab["feature.node.kubernetes.io/kernel-loadedmodule.amdgpu"] == "true"
+
+
+def test_gfd_labels_real_fixture(tmp_path):
+    root = fakesys.build_from_real_fixture(str(tmp_path / "real"))
+    lab = L.gfd_labels(T.enumerate_gpus(root), root)
+    assert lab["amd.com/gpu.product"] == "AMD-Instinct-MI355X" and lab["amd.com/gpu.family"] == "CDNA4"
+    assert lab["amd.com/gpu.memory"] == "294896" and lab["amd.com/gpu.memory-gib"] == "288"
+    assert lab["amd.com/gpu.mfma.fp4"] == "true" and lab["amd.com/gpu.mfma.xf32"] == "false"
+    assert lab["amd.com/gpu.xgmi.links"] == "7"
+    for k, v in lab.items():
+        assert len(v) <= 63 and (v == "" or (v[0].isalnum() and v[-1].isalnum())), (k, v)
+
+
+def test_sync_labels_removes_stale_but_keeps_operator_labels(env):
+    env.client.patch("v1", "Node", "n1", {"metadata": {"labels": {
+        "amd.com/gpu.stale": "x", "amd.com/gpu.present": "true", "amd.com/gpu.partition.state": "success"}}})
+    L.sync_node_labels(env.client, "n1", {"amd.com/gpu.count": "2"}, ("amd.com/gpu.",))
+    lab = env.client.get("v1", "Node", "n1")["metadata"]["labels"]
+    assert "amd.com/gpu.stale" not in lab and lab["amd.com/gpu.count"] == "2"
+    assert lab["amd.com/gpu.present"] == "true" and lab["amd.com/gpu.partition.state"] == "success"
+
+
+def test_label_value_sanitising():
+    assert L.label_value("6.12.12-amd+rocm 7.2") == "6.12.12-amd-rocm-7.2"
+    assert len(L.label_value("x" * 100)) == 63
+
+
+# --------------------------------------------------------------- exporters
+
+def test_metrics_exporter_renders_fixture_with_dcgm_aliases():
+    ex = MetricsExporter(FixtureSource(FIXTURE, gpus=2), "node-a", dcgm_names=True)
+    ex.collect_once()
+    text = ex.render()
+    assert 'amd_gpu_power_watts{gpu="0",' in text and 'node="node-a"' in text
+    assert "DCGM_FI_DEV_GPU_TEMP{" in text and "DCGM_FI_DEV_FB_USED{" in text
+    assert "amd_gpu_vram_free_bytes" in text
+    # Prometheus text format: every sample line is "<name>{labels} <float>"
+    for line in text.splitlines():
+        if line and not line.startswith("#"):
+            name, val = line.rsplit(" ", 1)
+            float(val)
+
+
+def test_pod_attribution_via_pod_resources_api(tmp_path):
+    sock = str(tmp_path / "podres" / "kubelet.sock")
+    k = FakeKubelet(str(tmp_path / "dp"), sock)
+    k.start()
+    try:
+        k.assignments[("ml", "trainer-0", "main")] = ("amd.com/gpu", ["0000:72:00.0"])
+        src = FixtureSource(FIXTURE, gpus=2)
+        ex = MetricsExporter(src, "n", attribution=PodAttribution(sock))
+        ex.collect_once()
+        text = ex.render()
+        assert 'pod="trainer-0"' in text and 'namespace="ml"' in text
+    finally:
+        k.stop()
+
+
+def test_http_server_and_node_status(env):
+    V.write_ready(env, "driver", {"seconds": 0.5})
+    ns = NodeStatusExporter(env.validations_dir, "n1")
+    srv = MetricsHttpServer(ns, "127.0.0.1", 0).start()
+    try:
+        body = urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/metrics", timeout=5).read().decode()
+        assert 'amd_gpu_operator_node_validation_ready{node="n1",step="driver"} 1' in body
+        assert 'amd_gpu_operator_node_validation_ready{node="n1",step="plugin"} 0' in body
+        assert 'amd_gpu_operator_node_validation_seconds{node="n1",step="driver"} 0.5' in body
+        assert urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/healthz", timeout=5).read() == b"ok\n"
+    finally:
+        srv.stop()
+
+
+# ---------------------------------------------------------------- validator
+
+def test_driver_validation_and_wait(env):
+    with pytest.raises(V.StepFailed):
+        V.wait_ready(env, "driver", timeout=0.05)
+    out = V.validate_driver(env, timeout=1)
+    assert out["gpus"] == 2 and V.wait_ready(env, "driver", 1)["ok"]
+
+
+def test_workload_validation_launch_plan(env):
+    launched = []
+
+    def launcher(argv, e, device, timeout):
+        launched.append((argv, dict(e), device))
+        steps = argv[argv.index("--steps") + 1].split(",")
+        rep = {"ok": True, "rank": int(argv[argv.index("--rank") + 1]),
+               "steps": [{"name": s, "ok": True, "seconds": 0.01} for s in steps]}
+        return ProcResult(0, json.dumps(rep), "", 0.01)
+
+    env.launcher = launcher
+    out = V.validate_workload(env, ["--gemm", "1024", "--counter-gate"])
+    assert out["ok"] and out["world"] == 2
+    kernel = [a for a, _, _ in launched if "rccl" not in a[a.index("--steps") + 1]]
+    rccl = [a for a, _, _ in launched if a[a.index("--steps") + 1] == "hip,rccl"]
+    assert len(kernel) == 2 and len(rccl) == 2
+    assert all("--counter-gate" in a for a in kernel) and not any("--counter-gate" in a for a in rccl)
+    assert {e.get("AMDGPU_VALIDATOR_COUNTERS") for a, e, _ in launched if a in kernel} == {"1"}
+    names = [s["name"] for s in out["ranks"][0]["steps"]]
+    assert names == ["hip", "vecadd", "gemm", "hbm", "xgmi", "rccl"]
+    assert V.read_ready(env, "workload")["world"] == 2
+
+
+def test_workload_failure_is_reported(env):
+    env.launcher = lambda argv, e, d, t: ProcResult(1, json.dumps({"ok": False, "error": "Freivalds 1e-1"}), "boom", 0.1)
+    with pytest.raises(V.StepFailed, match="Freivalds"):
+        V.validate_workload(env, [])
+    assert V.read_ready(env, "workload") is None
+
+
+def test_single_gpu_skips_rccl(tmp_path):
+    root = str(tmp_path / "h1")
+    fakesys.build_node(root, 1)
+    env = NodeEnv("n1", None, host_root=root, validations_dir=str(tmp_path / "v"), poll_s=0.01)
+    seen = []
+
+    def launcher(argv, e, device, timeout):
+        seen.append(argv[argv.index("--steps") + 1])
+        return ProcResult(0, json.dumps({"ok": True, "steps": []}), "", 0.0)
+
+    env.launcher = launcher
+    out = V.validate_workload(env, [])
+    assert seen == ["hip,vecadd,gemm,hbm,xgmi"]
+    assert out["ranks"][0]["steps"][-1]["skipped"].startswith("single GPU")
+
+
+def test_complete_labels_node(env):
+    V.write_ready(env, "driver", {"seconds": 0.1})
+    V.complete(env)
+    node = env.client.get("v1", "Node", "n1")
+    assert node["metadata"]["labels"][V.VALIDATED_LABEL] == "true"
+    assert json.loads(node["metadata"]["annotations"]["amd.com/gpu.validation"])["driver"] == 0.1
+
+
+# ------------------------------------------------------------------ CLI
+
+def test_operand_parser_passthrough():
+    from amdgpu_operator.cli.operands import _split_passthrough, build_parser
+
+    known, extra = _split_passthrough(["plugin", "--resource", "amd.com/gpu", "--gemm", "4096", "--counter-gate"])
+    assert known == ["plugin", "--resource", "amd.com/gpu"] and extra == ["--gemm", "4096", "--counter-gate"]
+    a = build_parser().parse_args(["device-plugin", "--partition-strategy", "mixed"])
+    assert a.partition_strategy == "mixed"
+
+
+def test_cli_render(capsys):
+    from amdgpu_operator.cli.main import main
+
+    assert main(["render", "--set", "operator.cleanupCRD=true"]) == 0
+    out = capsys.readouterr().out
+    assert "kind: ClusterPolicy" in out and "amd-gpu-operator-cleanup-crd" in out
+
+
+def test_cli_verify_against_http_apiserver(tmp_path, capsys):
+    from amdgpu_operator.cli.main import main
+    from amdgpu_operator.kube.httpapi import HttpApiServer
+
+    api = FakeApiServer()
+    srv = HttpApiServer(api).start()
+    try:
+        assert main(["verify", "--server", srv.url, "--json"]) == 1  # nothing installed
+        rep = json.loads(capsys.readouterr().out)
+        assert rep["ok"] is False and any(c["name"] == "gpu-nodes-labelled" for c in rep["checks"])
+    finally:
+        srv.stop()
