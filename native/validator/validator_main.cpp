@@ -183,7 +183,7 @@ Step step_hip(const Args& a, hipDeviceProp_t* prop) {
   const bool arch_ok = a.any_arch || strncmp(prop->gcnArchName, "gfx950", 6) == 0;
   s.ok = arch_ok;
   s.seconds = secs(t0);
-  s.detail = fmt("\"arch\": \"%s\", \"cus\": %d, \"hbm_bytes\": %zu, \"name\": \"%s\"", prop->gcnArchName,
+  s.detail = fmt("\"arch\": \"%s\", \"cus\": %d, \"hbm_bytes\": %zu, \"device_name\": \"%s\"", prop->gcnArchName,
                  prop->multiProcessorCount, prop->totalGlobalMem, prop->name);
   return s;
 }
