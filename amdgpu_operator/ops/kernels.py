@@ -43,6 +43,7 @@ def _lib() -> ctypes.CDLL:
         "avk_fill_uniform_bf16": ([P, I64, U64, F, F, S], I),
         "avk_vector_add_f32": ([P, P, P, I64, S], I),
         "avk_gemm_bf16_nt": ([P, P, P, I, I, I, I, S], I),
+        "avk_gemm_bf16_nt_variant": ([P, P, P, I, I, I, I, I, S], I),
         "avk_gemv_rows": ([P, I, P, P, I, I, S], I),
         "avk_gemv_cols_bf16": ([P, P, P, I, I, S], I),
         "avk_hbm_copy": ([P, P, I64, I, I, S], I),
@@ -123,11 +124,12 @@ def vector_add(a, b, out=None, stream=None):
     return out
 
 
-def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None):
+def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int = 0):
     """K2: ``out[M,N] = a[M,K] @ bt[N,K].T`` on MFMA (bf16 in, fp32 accumulate).
 
     M and N must be multiples of 256 and K of 64 (the kernel has no edge
-    tiles; the validator picks its shapes accordingly).
+    tiles; the validator picks its shapes accordingly).  ``variant`` 0 is the
+    4-slot LDS-DMA ring (default), 1 the 2-stage double buffer.
     """
     import torch
 
@@ -144,8 +146,8 @@ def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None):
     if out.shape != (M, N) or out.dtype not in (torch.bfloat16, torch.float32):
         raise ValueError("bad GEMM output")
     _require(out, out.dtype, "out")
-    rc = _lib().avk_gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
-                                 M, N, K, _stream(stream))
+    rc = _lib().avk_gemm_bf16_nt_variant(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
+                                         M, N, K, variant, _stream(stream))
     _check(rc, "gemm_bf16_nt")
     return out
 

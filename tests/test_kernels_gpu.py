@@ -29,22 +29,25 @@ def test_vector_add_exact(n):
     assert torch.equal(c, a + b)
 
 
-@pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 320), (1024, 1024, 1024), (2048, 1024, 4096)])
+@pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 320), (1024, 1024, 1024), (2048, 1024, 4096),
+                                   (256, 512, 192), (512, 256, 128)])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
-def test_gemm_vs_fp32_reference(shape, out_dtype):
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_gemm_vs_fp32_reference(shape, out_dtype, variant):
     M, N, Kd = shape
     g = torch.Generator(device=DEV).manual_seed(M + N + Kd)
     a = (torch.rand(M, Kd, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
     bt = (torch.rand(N, Kd, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
     ref = a.float() @ bt.float().t()
-    out = K.gemm_bf16_nt(a, bt, out_dtype=out_dtype)
+    out = K.gemm_bf16_nt(a, bt, out_dtype=out_dtype, variant=variant)
     err = (out.float() - ref).abs().max().item()
     scale = ref.abs().max().item()
     tol = 1e-5 * Kd if out_dtype == torch.float32 else 8e-3 * scale
     assert err <= tol, (err, tol)
 
 
-def test_gemm_exact_integer_asymmetric():
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_gemm_exact_integer_asymmetric(variant):
     # A = small integers, B asymmetric: a transposed C-write or a swapped
     # fragment map changes the result; all sums are exact in fp32.
     M, N, Kd = 512, 256, 128
@@ -54,7 +57,7 @@ def test_gemm_exact_integer_asymmetric():
     n = torch.arange(N, device=DEV).view(N, 1)
     bt = ((n * 11 + k * 2 + (n > k).long()) % 7 - 3).to(torch.bfloat16)
     ref = a.double() @ bt.double().t()
-    out = K.gemm_bf16_nt(a, bt, out_dtype=torch.float32)
+    out = K.gemm_bf16_nt(a, bt, out_dtype=torch.float32, variant=variant)
     assert torch.equal(out.double(), ref)
 
 

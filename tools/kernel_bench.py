@@ -38,17 +38,27 @@ def bench_gemm(n, rounds, iters):
     c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
     c2 = torch.empty_like(c)
     b = bt.t()
-    ours, lib = [], []
+    ours, lib, v1, v2, v3 = [], [], [], [], []
     for _ in range(3):
         K.gemm_bf16_nt(a, bt, out=c)
+        K.gemm_bf16_nt(a, bt, out=c, variant=1)
+        K.gemm_bf16_nt(a, bt, out=c, variant=2)
+        K.gemm_bf16_nt(a, bt, out=c, variant=3)
         torch.matmul(a, b, out=c2)
     for _ in range(rounds):
         ours.append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c), iters))
+        v1.append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c, variant=1), iters))
+        v2.append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c, variant=2), iters))
+        v3.append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c, variant=3), iters))
         lib.append(time_ms(lambda: torch.matmul(a, b, out=c2), iters))
     fl = 2.0 * n ** 3
+    K.gemm_bf16_nt(a, bt, out=c)
     err = (c.float() - c2.float()).abs().max().item()
     return {
         "n": n,
+        "dbuf_tflops": fl / statistics.median(v1) / 1e9,
+        "ring_tflops": fl / statistics.median(v2) / 1e9,
+        "w4_tflops": fl / statistics.median(v3) / 1e9,
         "ours_ms_median": statistics.median(ours),
         "ours_tflops": fl / statistics.median(ours) / 1e9,
         "ours_tflops_best": fl / min(ours) / 1e9,
