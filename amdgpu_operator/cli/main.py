@@ -8,6 +8,8 @@ Sub-commands:
 * ``verify``                - machine-checked version of README.md:113-215
 * ``render``                - render the chart with ``--set`` flags (helm template)
 * ``simulate``              - bring up a simulated cluster and report time-to-Ready
+* ``collectives``           - RCCL sweep (all-reduce / all-gather / reduce-scatter, algBW + busBW);
+                              one rank per GPU under ``torch.distributed.run``
 * ``driver|toolkit|validate|device-plugin|metrics-exporter|node-status-exporter|nfd|gfd|partition-manager``
                             - operand containers (see :mod:`.operands`)
 """
@@ -48,7 +50,8 @@ def _common(p):
     p.add_argument("--log-level", default="info")
 
 
-def _health_server(port: int):
+def _health_server(port: int, metrics=None):
+    """``/healthz`` (liveness/readiness probes) and ``/metrics`` (operator self-metrics)."""
     from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
     class H(BaseHTTPRequestHandler):
@@ -56,6 +59,13 @@ def _health_server(port: int):
             pass
 
         def do_GET(self):
+            if self.path.startswith("/metrics") and metrics is not None:
+                body = metrics.render().encode()
+                self.send_response(200)
+                self.send_header("Content-Type", "text/plain; version=0.0.4")
+                self.end_headers()
+                self.wfile.write(body)
+                return
             self.send_response(200 if self.path.startswith("/healthz") else 404)
             self.end_headers()
             self.wfile.write(b"ok\n")
@@ -106,14 +116,23 @@ def main(argv: list[str] | None = None) -> int:
     sm.add_argument("--set", action="append", default=[])
     sm.add_argument("--real-gpus", action="store_true", help="use this machine's GPUs and sysfs")
     sm.add_argument("--timeout", type=float, default=120)
+    co = sub.add_parser("collectives", help="RCCL collective sweep (run under torch.distributed.run)")
+    co.add_argument("--min-bytes", type=int, default=8)
+    co.add_argument("--max-bytes", type=int, default=1 << 30)
+    co.add_argument("--factor", type=int, default=4)
+    co.add_argument("--ops", default="allreduce,allgather,reducescatter")
+    co.add_argument("--dtype", default="float32", choices=("float32", "bfloat16"))
+    co.add_argument("--iters", type=int, default=10)
+    co.add_argument("--backend", default=None, help="nccl (RCCL, default with a GPU) or gloo")
+    co.add_argument("--json", action="store_true")
     args = ap.parse_args(argv)
     logs.setup(getattr(args, "log_level", "info"))
 
     if args.cmd == "operator":
         from ..controller.reconciler import ClusterPolicyReconciler
 
-        _health_server(args.health_port)
         rec = ClusterPolicyReconciler(_client(args), args.namespace)
+        _health_server(args.health_port, rec.metrics)
         rec.run(threading.Event(), resync_s=args.resync)
         return 0
     if args.cmd == "cleanup-crd":
@@ -158,7 +177,37 @@ def main(argv: list[str] | None = None) -> int:
             return 0 if rep.ok else 1
         finally:
             c.stop()
+    if args.cmd == "collectives":
+        return _collectives(args)
     return 2
+
+
+def _collectives(args) -> int:
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from ..parallel import collectives as C
+
+    cuda = torch.cuda.is_available()
+    backend = args.backend or ("nccl" if cuda else "gloo")
+    if "RANK" not in os.environ:  # single process: world of one
+        os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get(
+            "MASTER_PORT", "29531"))
+    local = int(os.environ.get("LOCAL_RANK", os.environ["RANK"]))
+    device = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
+    if backend == "nccl":
+        torch.cuda.set_device(device)
+    dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
+    try:
+        rows = C.sweep(C.default_sizes(args.min_bytes, args.max_bytes, args.factor), tuple(args.ops.split(",")),
+                       getattr(torch, args.dtype), device, iters=args.iters)
+        if dist.get_rank() == 0:
+            print(json.dumps(C.rows_as_dicts(rows)) if args.json else C.format_table(rows))
+        return 0 if all(r.ok for r in rows) else 1
+    finally:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -80,6 +80,56 @@ def daemonset_ready(ds: dict) -> tuple[bool, str]:
     return ok, f"{ready}/{desired} ready"
 
 
+class ReconcileMetrics:
+    """Operator self-metrics: reconcile count/duration, the
+    policy state, per-state ready spans and time-to-Ready, in Prometheus text
+    format for the operator's ``/metrics`` endpoint."""
+
+    BUCKETS = (0.001, 0.005, 0.01, 0.05, 0.1, 0.5, 1.0, 5.0)
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.count = 0
+        self.errors = 0
+        self.sum = 0.0
+        self.buckets = [0] * len(self.BUCKETS)
+        self.state = "absent"
+        self.ready_spans: dict[str, float] = {}
+        self.time_to_ready: float | None = None
+
+    def observe(self, res: "ReconcileResult", spans: dict[str, float], ttr: float | None) -> None:
+        with self._lock:
+            self.count += 1
+            self.errors += res.state == "error"
+            self.sum += res.seconds
+            for i, b in enumerate(self.BUCKETS):
+                if res.seconds <= b:
+                    self.buckets[i] += 1
+            self.state = res.state
+            self.ready_spans = dict(spans)
+            if ttr is not None:
+                self.time_to_ready = ttr
+
+    def render(self) -> str:
+        p = "amd_gpu_operator_"
+        with self._lock:
+            out = [f"# TYPE {p}reconcile_total counter", f"{p}reconcile_total {self.count}",
+                   f"# TYPE {p}reconcile_errors_total counter", f"{p}reconcile_errors_total {self.errors}",
+                   f"# TYPE {p}reconcile_duration_seconds histogram"]
+            for b, n in zip(self.BUCKETS, self.buckets):
+                out.append(f'{p}reconcile_duration_seconds_bucket{{le="{b}"}} {n}')
+            out += [f'{p}reconcile_duration_seconds_bucket{{le="+Inf"}} {self.count}',
+                    f"{p}reconcile_duration_seconds_sum {self.sum:.6f}",
+                    f"{p}reconcile_duration_seconds_count {self.count}",
+                    f"# TYPE {p}policy_ready gauge", f"{p}policy_ready {int(self.state == 'ready')}",
+                    f"# TYPE {p}state_ready_seconds gauge"]
+            for k, v in sorted(self.ready_spans.items()):
+                out.append(f'{p}state_ready_seconds{{state="{k}"}} {v:.4f}')
+            if self.time_to_ready is not None:
+                out += [f"# TYPE {p}time_to_ready_seconds gauge", f"{p}time_to_ready_seconds {self.time_to_ready:.4f}"]
+        return "\n".join(out) + "\n"
+
+
 class ClusterPolicyReconciler:
     def __init__(self, client, namespace: str, clock=time.time):
         self.client = client
@@ -87,7 +137,9 @@ class ClusterPolicyReconciler:
         self.clock = clock
         self._ready_at: dict[str, dict[str, float]] = {}  # policy uid -> state -> seconds since creation
         self._created_at: dict[str, float] = {}
+        self._ttr: dict[str, float] = {}
         self.reconciles = 0
+        self.metrics = ReconcileMetrics()
 
     # ------------------------------------------------------------------ helpers
     def _active_policy(self) -> dict | None:
@@ -131,7 +183,9 @@ class ClusterPolicyReconciler:
         except ValidationError as e:
             msg = str(e).splitlines()[0] if str(e) else "invalid spec"
             self._write_status(cp, "error", [], 0, error=msg)
-            return ReconcileResult(cp["metadata"]["name"], "error", seconds=time.perf_counter() - t0)
+            res = ReconcileResult(cp["metadata"]["name"], "error", seconds=time.perf_counter() - t0)
+            self.metrics.observe(res, {}, None)
+            return res
 
         gpu_nodes, patched = label_nodes(self.client, spec)
         owner = owner_ref(cp)
@@ -173,7 +227,10 @@ class ClusterPolicyReconciler:
             if pending:
                 overall = "notReady"
         self._write_status(cp, overall, results, gpu_nodes)
+        if overall == "ready":
+            self._ttr.setdefault(uid, self.clock() - self._created_at[uid])
         res = ReconcileResult(cp["metadata"]["name"], overall, results, gpu_nodes, time.perf_counter() - t0)
+        self.metrics.observe(res, self._ready_at.get(uid, {}), self._ttr.get(uid))
         log.debug("reconciled %s: %s (%.3fs)", res.policy, overall, res.seconds)
         return res
 

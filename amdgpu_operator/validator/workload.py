@@ -251,22 +251,52 @@ class ValidatorWorkload:
             return StepResult("rccl", True, 0.0, {"skipped": "no process group"})
         world = dist.get_world_size(self.pg)
         rank = dist.get_rank(self.pg)
-        n = cfg.rccl_elems
+        n = (cfg.rccl_elems // world) * world
+        per = n // world
         buf = self._buf("rb", (n,), torch.float32)
+        aux = self._buf("rx", (n,), torch.float32)
+        expect = world * (world + 1) / 2.0
+        iters = max(1, cfg.rccl_iters)
+        ar_f = 2 * (world - 1) / world if world > 1 else 0.0
+        gs_f = (world - 1) / world if world > 1 else 0.0
+        coll: dict[str, dict[str, float]] = {}
+
+        def record(name, nbytes, ms, factor, ok):
+            algbw = nbytes / (ms * 1e-3) / 1e9
+            coll[name] = {"bytes": nbytes, "ms": ms, "algbw_gbps": algbw, "busbw_gbps": algbw * factor, "ok": ok}
+            if not ok:
+                raise ValidationFailed("rccl", f"{name} result mismatch")
+
         with _Timer(torch, self.device) as tm:
-            # rank r contributes (r + 1): the sum is world*(world+1)/2 exactly in fp32
+            # rank r contributes (r + 1): every result below is exact in fp32 and bf16
             buf.fill_(float(rank + 1))
             dist.all_reduce(buf, group=self.pg)
-            expect = world * (world + 1) / 2.0
             ok = bool(torch.all(buf == expect).item())
-            ms = _events_ms(torch, lambda: dist.all_reduce(buf, group=self.pg), max(1, cfg.rccl_iters))
-        nbytes = n * 4
-        algbw = nbytes / (ms * 1e-3) / 1e9
-        busbw = algbw * (2 * (world - 1) / world) if world > 1 else 0.0
-        if not ok:
-            raise ValidationFailed("rccl", "all-reduce result mismatch")
-        return StepResult("rccl", ok, tm.dt, {"world": world, "bytes": nbytes, "ms": ms, "algbw_gbps": algbw,
-                                              "busbw_gbps": busbw})
+            record("allreduce_f32", n * 4, _events_ms(torch, lambda: dist.all_reduce(buf, group=self.pg), iters), ar_f,
+                   ok)
+            b16 = aux.view(torch.bfloat16)[:n]
+            b16.fill_(float(rank + 1))
+            dist.all_reduce(b16, group=self.pg)
+            ok = bool(torch.all(b16 == expect).item())
+            record("allreduce_bf16", n * 2, _events_ms(torch, lambda: dist.all_reduce(b16, group=self.pg), iters),
+                   ar_f, ok)
+            src = buf[:per]
+            src.fill_(float(rank + 1))
+            dist.all_gather_into_tensor(aux, src, group=self.pg)
+            want = torch.arange(world, device=aux.device, dtype=torch.float32).repeat_interleave(per) + 1
+            ok = bool(torch.equal(aux, want))
+            record("allgather_f32", n * 4,
+                   _events_ms(torch, lambda: dist.all_gather_into_tensor(aux, src, group=self.pg), iters), gs_f, ok)
+            buf.fill_(float(rank + 1))
+            out = aux[:per]
+            dist.reduce_scatter_tensor(out, buf, group=self.pg)
+            ok = bool(torch.all(out == expect).item())
+            record("reducescatter_f32", n * 4,
+                   _events_ms(torch, lambda: dist.reduce_scatter_tensor(out, buf, group=self.pg), iters), gs_f, ok)
+        ar = coll["allreduce_f32"]
+        return StepResult("rccl", True, tm.dt, {"world": world, "bytes": n * 4, "ms": ar["ms"],
+                                                "algbw_gbps": ar["algbw_gbps"], "busbw_gbps": ar["busbw_gbps"],
+                                                "collectives": coll})
 
     STEPS = ("hip", "vecadd", "gemm", "hbm", "xgmi", "rccl")
 

@@ -52,6 +52,9 @@ struct Rccl {
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*ReduceScatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                                hipStream_t) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
 
@@ -67,9 +70,12 @@ struct Rccl {
     GetUniqueId = reinterpret_cast<decltype(GetUniqueId)>(dlsym(dl, "ncclGetUniqueId"));
     CommInitRank = reinterpret_cast<decltype(CommInitRank)>(dlsym(dl, "ncclCommInitRank"));
     AllReduce = reinterpret_cast<decltype(AllReduce)>(dlsym(dl, "ncclAllReduce"));
+    AllGather = reinterpret_cast<decltype(AllGather)>(dlsym(dl, "ncclAllGather"));
+    ReduceScatter = reinterpret_cast<decltype(ReduceScatter)>(dlsym(dl, "ncclReduceScatter"));
     CommDestroy = reinterpret_cast<decltype(CommDestroy)>(dlsym(dl, "ncclCommDestroy"));
     GetErrorString = reinterpret_cast<decltype(GetErrorString)>(dlsym(dl, "ncclGetErrorString"));
-    if (!GetUniqueId || !CommInitRank || !AllReduce || !CommDestroy || !GetErrorString) {
+    if (!GetUniqueId || !CommInitRank || !AllReduce || !AllGather || !ReduceScatter || !CommDestroy ||
+        !GetErrorString) {
       *err = "librccl is missing NCCL API symbols";
       return false;
     }
@@ -458,6 +464,34 @@ void rccl_init(const Args& a, const Rendezvous& rv, RcclInit* out) {
   }
 }
 
+// Times `iters` back-to-back launches of `launch` on `st` (ms per launch).
+template <typename F>
+float time_collective(hipStream_t st, int iters, F launch) {
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  HIP_OK(hipEventRecord(e0, st));
+  for (int i = 0; i < iters; ++i) launch();
+  HIP_OK(hipEventRecord(e1, st));
+  HIP_OK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return ms / iters;
+}
+
+// bf16 bit pattern of a float that bf16 holds exactly (small integers here)
+uint16_t bf16_bits(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (uint16_t)(u >> 16);
+}
+
+// RCCL over xGMI: fp32 + bf16 all-reduce, all-gather and reduce-scatter, each
+// checked exactly (rank r contributes r+1) and timed; busBW uses the usual
+// ring factors (all-reduce 2(n-1)/n, gather/scatter (n-1)/n) so the numbers
+// compare with rccl-tests.  SURVEY.md §2.E call sites.
 Step step_rccl(const Args& a, hipStream_t st, std::thread* init_thread, RcclInit* ri) {
   auto t0 = Clock::now();
   Step s{"rccl"};
@@ -465,39 +499,90 @@ Step step_rccl(const Args& a, hipStream_t st, std::thread* init_thread, RcclInit
   const double wait_s = secs(t0);
   if (!ri->error.empty()) throw std::runtime_error("rccl init: " + ri->error);
   ncclComm_t comm = ri->comm;
-  const int64_t n = a.rccl_elems;
+  const int W = a.world;
+  const int64_t n = (a.rccl_elems / W) * W;  // divisible for the gather/scatter shapes
+  const int64_t per = n / W;
+  const int iters = 5;
+  const float expect_sum = W * (W + 1) / 2.0f;
   float* buf;
+  float* aux;
   HIP_OK(hipMalloc(&buf, n * 4));
-  std::vector<float> host(n, (float)(a.rank + 1));
+  HIP_OK(hipMalloc(&aux, n * 4));
+  std::vector<float> host(n);
+  std::string detail;
+  int64_t total_bad = 0;
+  auto report = [&](const char* name, int64_t bytes, float ms, double busf, int64_t bad) {
+    const double algbw = bytes / (ms * 1e-3) / 1e9;
+    detail += fmt("%s\"%s\": {\"bytes\": %lld, \"ms\": %.4f, \"algbw_gbps\": %.1f, \"busbw_gbps\": %.1f, "
+                  "\"mismatches\": %lld}",
+                  detail.empty() ? "" : ", ", name, (long long)bytes, ms, algbw, algbw * busf, (long long)bad);
+    total_bad += bad;
+  };
+
+  // fp32 all-reduce
+  std::fill(host.begin(), host.end(), (float)(a.rank + 1));
   HIP_OK(hipMemcpyAsync(buf, host.data(), n * 4, hipMemcpyHostToDevice, st));
   NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
   HIP_OK(hipMemcpyAsync(host.data(), buf, n * 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
-  const float expect = a.world * (a.world + 1) / 2.0f;
   int64_t bad = 0;
-  for (int64_t i = 0; i < n; ++i) bad += host[i] != expect;
-  hipEvent_t e0, e1;
-  HIP_OK(hipEventCreate(&e0));
-  HIP_OK(hipEventCreate(&e1));
-  const int iters = 5;
-  HIP_OK(hipEventRecord(e0, st));
-  for (int i = 0; i < iters; ++i) NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
-  HIP_OK(hipEventRecord(e1, st));
-  HIP_OK(hipEventSynchronize(e1));
-  float ms = 0;
-  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-  ms /= iters;
+  for (int64_t i = 0; i < n; ++i) bad += host[i] != expect_sum;
+  float ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st)); });
+  const double ar_algbw = n * 4.0 / (ms * 1e-3) / 1e9;
+  const double ar_busbw = W > 1 ? ar_algbw * 2.0 * (W - 1) / W : 0.0;
+  const float ar_ms = ms;
+  report("allreduce_f32", n * 4, ms, W > 1 ? 2.0 * (W - 1) / W : 0.0, bad);
+
+  // bf16 all-reduce (sums up to 36 are exact in bf16)
+  {
+    std::vector<uint16_t> h16(n, bf16_bits((float)(a.rank + 1)));
+    HIP_OK(hipMemcpyAsync(aux, h16.data(), n * 2, hipMemcpyHostToDevice, st));
+    NCCL_OK(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st));
+    HIP_OK(hipMemcpyAsync(h16.data(), aux, n * 2, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const uint16_t want = bf16_bits(expect_sum);
+    bad = 0;
+    for (int64_t i = 0; i < n; ++i) bad += h16[i] != want;
+    ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st)); });
+    report("allreduce_bf16", n * 2, ms, W > 1 ? 2.0 * (W - 1) / W : 0.0, bad);
+  }
+
+  // all-gather: rank r's block holds r+1
+  {
+    std::fill(host.begin(), host.begin() + per, (float)(a.rank + 1));
+    HIP_OK(hipMemcpyAsync(buf, host.data(), per * 4, hipMemcpyHostToDevice, st));
+    NCCL_OK(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st));
+    HIP_OK(hipMemcpyAsync(host.data(), aux, n * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    bad = 0;
+    for (int64_t i = 0; i < n; ++i) bad += host[i] != (float)(i / per + 1);
+    ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st)); });
+    report("allgather_f32", n * 4, ms, W > 1 ? (W - 1.0) / W : 0.0, bad);
+  }
+
+  // reduce-scatter: every element of every rank holds r+1
+  {
+    std::fill(host.begin(), host.end(), (float)(a.rank + 1));
+    HIP_OK(hipMemcpyAsync(buf, host.data(), n * 4, hipMemcpyHostToDevice, st));
+    NCCL_OK(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st));
+    HIP_OK(hipMemcpyAsync(host.data(), aux, per * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    bad = 0;
+    for (int64_t i = 0; i < per; ++i) bad += host[i] != expect_sum;
+    ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st)); });
+    report("reducescatter_f32", n * 4, ms, W > 1 ? (W - 1.0) / W : 0.0, bad);
+  }
+
   NCCL_OK(g_rccl.CommDestroy(comm));
   (void)hipFree(buf);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  const double algbw = n * 4.0 / (ms * 1e-3) / 1e9;
-  const double busbw = a.world > 1 ? algbw * 2.0 * (a.world - 1) / a.world : 0.0;
-  s.ok = bad == 0;
+  (void)hipFree(aux);
+  s.ok = total_bad == 0;
   s.seconds = secs(t0);
   s.detail = fmt("\"world\": %d, \"bytes\": %lld, \"lib_load_s\": %.4f, \"comm_init_s\": %.4f, \"init_wait_s\": %.4f, "
-                 "\"ms\": %.4f, \"algbw_gbps\": %.1f, \"busbw_gbps\": %.1f, \"mismatches\": %lld",
-                 a.world, (long long)(n * 4), ri->load_s, ri->init_s, wait_s, ms, algbw, busbw, (long long)bad);
+                 "\"ms\": %.4f, \"algbw_gbps\": %.1f, \"busbw_gbps\": %.1f, \"mismatches\": %lld, \"collectives\": {",
+                 W, (long long)(n * 4), ri->load_s, ri->init_s, wait_s, ar_ms, ar_algbw, ar_busbw,
+                 (long long)total_bad) +
+             detail + "}";
   return s;
 }
 

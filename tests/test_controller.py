@@ -197,3 +197,30 @@ def test_node_detection_rules():
     assert not is_gpu_node({"metadata": {"labels": {"feature.node.kubernetes.io/pci-10de.present": "true"}}})
     patch = desired_labels({"metadata": {"labels": GPU_LABEL}}, ClusterPolicySpec())
     assert patch["amd.com/gpu.present"] == "true"
+
+
+def test_operator_metrics_endpoint(env):
+    import urllib.request
+
+    from amdgpu_operator.cli.main import _health_server
+
+    c, rec = env
+    c.create(cluster_policy())
+    rec.reconcile()
+    mark_all_ds_ready(c)
+    c.patch("v1", "Node", "gpu-a", {"metadata": {"labels": {"amd.com/gpu.validated": "true"}}})
+    assert rec.reconcile().state == "ready"
+    srv = _health_server(0, rec.metrics)
+    try:
+        port = srv.server_address[1]
+        text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+        assert urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=5).read() == b"ok\n"
+    finally:
+        srv.shutdown()
+    samples = dict(line.rsplit(" ", 1) for line in text.splitlines() if line and not line.startswith("#"))
+    assert samples["amd_gpu_operator_reconcile_total"] == "2"
+    assert samples["amd_gpu_operator_reconcile_duration_seconds_count"] == "2"
+    assert samples['amd_gpu_operator_reconcile_duration_seconds_bucket{le="+Inf"}'] == "2"
+    assert samples["amd_gpu_operator_policy_ready"] == "1"
+    assert float(samples["amd_gpu_operator_time_to_ready_seconds"]) >= 0
+    assert 'amd_gpu_operator_state_ready_seconds{state="state-driver"}' in samples

@@ -161,3 +161,27 @@ def test_workload_detects_bad_gemm(monkeypatch):
     wl = W.ValidatorWorkload(0, W.WorkloadConfig.quick())
     with pytest.raises(W.ValidationFailed):
         wl.step_gemm()
+
+
+def test_workload_rccl_collectives_single_rank(tmp_path):
+    import json
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import json, torch, torch.distributed as dist\n"
+        "from amdgpu_operator.validator.workload import ValidatorWorkload, WorkloadConfig\n"
+        "torch.cuda.set_device(0)\n"
+        "dist.init_process_group('nccl', rank=0, world_size=1, init_method='tcp://127.0.0.1:29617',"
+        " device_id=torch.device('cuda', 0))\n"
+        "r = ValidatorWorkload(0, WorkloadConfig.quick()).step_rccl()\n"
+        "dist.destroy_process_group()\n"
+        "print(json.dumps({'ok': r.ok, **r.metrics}))\n")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=repo,
+                       env={**os.environ, "PYTHONPATH": repo})
+    assert p.returncode == 0, p.stderr[-3000:]
+    rep = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rep["ok"] and rep["world"] == 1
+    assert set(rep["collectives"]) == {"allreduce_f32", "allreduce_bf16", "allgather_f32", "reducescatter_f32"}

@@ -61,7 +61,23 @@ def test_validator_ipc_peer_path_two_processes_one_gpu(tmp_path):
 def test_validator_single_rank_rccl(tmp_path):
     rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,rccl", "--rccl-elems", "1048576"])
     assert rc == 0 and rep["ok"], rep
-    assert {s["name"]: s for s in rep["steps"]}["rccl"]["mismatches"] == 0
+    r = {s["name"]: s for s in rep["steps"]}["rccl"]
+    assert r["mismatches"] == 0
+    assert set(r["collectives"]) == {"allreduce_f32", "allreduce_bf16", "allgather_f32", "reducescatter_f32"}
+    assert all(c["mismatches"] == 0 and c["ms"] > 0 for c in r["collectives"].values())
+
+
+def test_collectives_sweep_rccl_one_gpu():
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-m", "amdgpu_operator", "collectives", "--max-bytes", str(64 << 20),
+                        "--iters", "3", "--json"], capture_output=True, text=True, timeout=300, cwd=repo,
+                       env={**os.environ, "PYTHONPATH": repo, "MASTER_PORT": "29611"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    rows = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("[")][-1])
+    assert rows and all(r["ok"] and r["world"] == 1 for r in rows)
+    assert {r["op"] for r in rows} == {"allreduce", "allgather", "reducescatter"}
 
 
 def test_validator_rejects_bad_arguments():
