@@ -89,8 +89,12 @@ static bool enumerate(Api* a) {
 
 using namespace at_smi;
 
+// bounded copy that always NUL-terminates (amd-smi strings may exceed our fields)
 static void copy_str(char* dst, size_t cap, const char* s) {
-  snprintf(dst, cap, "%s", s ? s : "");
+  if (cap == 0) return;
+  const size_t n = s ? strnlen(s, cap - 1) : 0;
+  if (n) memcpy(dst, s, n);
+  dst[n] = '\0';
 }
 
 extern "C" {

@@ -383,13 +383,27 @@ __device__ __forceinline__ void wait_slice_vmcnt(int ahead) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool OUT_F32>
+// LOAD_IN_M moves the slice t+3 LDS-DMA out of R(t) into M(t), one piece
+// after every two MFMA rows: a piece costs ~60 issue cycles among bare MFMAs
+// but 100-185 inside a read burst (MI355X_MICROARCH.md constants table), and
+// R is the segment the partner's MFMAs wait for.  The refill is then issued
+// in segments 2t+1 (group 0) / 2t+2 (group 1), still after barrier 2t, and is
+// never skipped (past the last slice it re-reads slice nk-1 into a slot no one
+// reads again), so the waits are constant: group 0 after M(t) has slices t+2,
+// t+3 newer than t+1 in flight -> vmcnt(8); group 1 after R(t) has issued only
+// up to t+2 -> vmcnt(4).
+//
+// NSLOT = 5 (LOAD_IN_M only) deepens the ring to the full 160 KiB of LDS:
+// slice t+4 is refilled in M(t) and every wait allows one more slice in flight.
+template <bool OUT_F32, bool LOAD_IN_M, int NSLOT = 4>
 __global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_pp_kernel(const __bf16* __restrict__ A,
                                                                         const __bf16* __restrict__ Bt,
                                                                         void* __restrict__ Cv, int M, int N,
                                                                         int K) {
   using namespace gring;
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  static_assert(NSLOT == 4 || (NSLOT == 5 && LOAD_IN_M), "ring depth");
+  constexpr int AHEAD = NSLOT - 1;  // slices in flight beyond the one being read
+  __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -416,10 +430,20 @@ __global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_pp_kernel(const _
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK;
+  if constexpr (LOAD_IN_M) {
 #pragma unroll
-  for (int s = 0; s < 3; ++s)
-    if (s < nk) ring_stage(A, Bt, K, m0, n0, s * BK, smem + s * SLOT_BYTES, wave, lane);
-  wait_slice_vmcnt(min(2, nk - 1));
+    for (int s = 0; s < AHEAD; ++s)
+      ring_stage(A, Bt, K, m0, n0, min(s, nk - 1) * BK, smem + s * SLOT_BYTES, wave, lane);
+    if constexpr (AHEAD == 4)
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+      if (s < nk) ring_stage(A, Bt, K, m0, n0, s * BK, smem + s * SLOT_BYTES, wave, lane);
+    wait_slice_vmcnt(min(2, nk - 1));
+  }
   wg_barrier();
   if (lag) wg_barrier();
 
@@ -427,29 +451,64 @@ __global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_pp_kernel(const _
   const int pcol = ((lane >> 4) ^ (((frow >> 3) & 1) * 3)) * 16;
   const int a_off = (wm * 128 + frow) * 64 + pcol;
   const int b_off = OP_BYTES + (wn * 64 + frow) * 64 + pcol;
+  const int rsub = lane >> 2, pc = lane & 3;
 
   for (int t = 0; t < nk; ++t) {
     // ---- R(t)
-    if (t + 3 < nk) ring_stage(A, Bt, K, m0, n0, (t + 3) * BK, smem + ((t + 3) & 3) * SLOT_BYTES, wave, lane);
-    const char* slot = smem + (t & 3) * SLOT_BYTES;
+    if (!LOAD_IN_M && t + 3 < nk)
+      ring_stage(A, Bt, K, m0, n0, (t + 3) * BK, smem + ((t + 3) & 3) * SLOT_BYTES, wave, lane);
+    const char* slot = smem + (t % NSLOT) * SLOT_BYTES;
     bf16x8 a[8], b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(slot + b_off + j * 1024);
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(slot + a_off + i * 1024);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lag) wait_slice_vmcnt(min(2, nk - 2 - t));
+    if (lag) {
+      if constexpr (LOAD_IN_M && AHEAD == 4)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if constexpr (LOAD_IN_M)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else
+        wait_slice_vmcnt(min(2, nk - 2 - t));
+    }
     wg_barrier();
     // ---- M(t)
+    char* sslot = smem + ((t + AHEAD) % NSLOT) * SLOT_BYTES;
+    const int kload = min(t + AHEAD, nk - 1) * BK;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      if (LOAD_IN_M && (i & 1)) {  // piece k = i>>1: operand k>>1, rows ((wave*2 + (k&1))*16 + rsub)
+        const int k = i >> 1;
+        const int p = wave * 2 + (k & 1);
+        const int r = p * 16 + rsub;
+        const int lc = pc ^ (((r >> 3) & 1) * 3);
+        const __bf16* src = (k < 2 ? A + (size_t)(m0 + r) * K : Bt + (size_t)(n0 + r) * K) + kload + lc * 8;
+        __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)(sslot + (k < 2 ? 0 : OP_BYTES) + p * 1024), 16, 0, 0);
+      }
+    }
+    if constexpr (LOAD_IN_M) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);  // two MFMA rows
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one LDS-DMA piece
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
-    if (!lag) wait_slice_vmcnt(min(2, nk - 2 - t));
+    if (!lag) {
+      if constexpr (LOAD_IN_M && AHEAD == 4)
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if constexpr (LOAD_IN_M)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else
+        wait_slice_vmcnt(min(2, nk - 2 - t));
+    }
     if (!(lag && t == nk - 1)) wg_barrier();
   }
+  if constexpr (LOAD_IN_M) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy refills drained
 
   // acc[i][j] = C^T fragment: lane holds C[i*16 + (lane&15)][j*16 + (lane>>4)*4 + 0..3]
   const int crow = m0 + wm * 128 + frow;
@@ -805,8 +864,8 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
   const __bf16* b = (const __bf16*)Bt;
   switch (variant) {
     case 0:
-      if (out_f32) gemm_bf16_nt_pp_kernel<true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
-      else gemm_bf16_nt_pp_kernel<false><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
+      if (out_f32) gemm_bf16_nt_pp_kernel<true, false><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
+      else gemm_bf16_nt_pp_kernel<false, false><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
       break;
     case 1:
       if (out_f32) gemm_bf16_nt_kernel<true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
@@ -819,6 +878,14 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
     case 3:
       if (out_f32) gemm_bf16_nt_w4_kernel<true><<<nwg, gw4::NTHR, 0, s>>>(a, b, C, M, N, K);
       else gemm_bf16_nt_w4_kernel<false><<<nwg, gw4::NTHR, 0, s>>>(a, b, C, M, N, K);
+      break;
+    case 4:
+      if (out_f32) gemm_bf16_nt_pp_kernel<true, true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
+      else gemm_bf16_nt_pp_kernel<false, true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
+      break;
+    case 5:
+      if (out_f32) gemm_bf16_nt_pp_kernel<true, true, 5><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
+      else gemm_bf16_nt_pp_kernel<false, true, 5><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
       break;
     default:
       return hipErrorInvalidValue;

@@ -54,3 +54,31 @@ def test_probe_under_asan(asan_bins, tmp_path):
     assert json.loads(p.stdout)["gpus"][0]["arch"] == "gfx950"
     p = _run([asan_bins["amdgpu-probe"], "--root", str(tmp_path / "none")])
     assert p.returncode == 1
+
+
+@pytest.mark.parametrize("gpus,mode", [(1, "SPX"), (8, "SPX"), (8, "CPX"), (4, "DPX")])
+def test_topology_library_under_asan(asan_bins, tmp_path, gpus, mode):
+    """N3 (+ the N4/N6 unavailable paths) under ASan/UBSan, cross-checked with the ctypes view."""
+    from amdgpu_operator.discovery import topology as T
+
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, gpus, mode)
+    p = _run([str(native.artefact("topo-selftest.asan")), root, "--smi"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    rep = json.loads(p.stdout)
+    py = T.enumerate_gpus(root)
+    assert rep["enumerate_rc"] == 0 and rep["probe_rc"] == 0
+    assert [g["bdf"] for g in rep["gpus"]] == [g.bdf for g in py]
+    assert {g["partition"] for g in rep["gpus"]} == {mode}
+    assert rep["links"] == len(T.links(root))
+    if len(py) > 1:
+        assert rep["nospc_rc"] == -28  # AT_ERR_NOSPC: short buffer reported, not overrun
+    assert rep["smi_open_rc"] in (0, -95) and rep["health_poll_rc"] in (0, -95)
+
+
+def test_topology_library_under_asan_real_fixture(asan_bins, tmp_path):
+    root = fakesys.build_from_real_fixture(str(tmp_path / "real"))
+    p = _run([str(native.artefact("topo-selftest.asan")), root])
+    assert p.returncode == 0, p.stderr[-3000:]
+    rep = json.loads(p.stdout)
+    assert rep["gpus"][0]["arch"] == "gfx950" and rep["gpus"][0]["cu"] == 256

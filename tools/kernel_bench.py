@@ -30,7 +30,12 @@ def time_ms(fn, iters):
     return s.elapsed_time(e) / iters
 
 
+GEMM_VARIANTS = {0: "default", 1: "dbuf", 2: "ring", 3: "w4", 4: "pp_load_in_m", 5: "pp_load_in_m_5slot"}
+
+
 def bench_gemm(n, rounds, iters):
+    """Every K2 variant and hipBLASLt, interleaved round by round on the same
+    random operands (cdna_hip_programming.md §5.4 rules 24-25)."""
     a = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
     bt = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
     K.fill_uniform_(a, 1)
@@ -38,34 +43,32 @@ def bench_gemm(n, rounds, iters):
     c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
     c2 = torch.empty_like(c)
     b = bt.t()
-    ours, lib, v1, v2, v3 = [], [], [], [], []
+    times = {v: [] for v in GEMM_VARIANTS}
+    lib = []
     for _ in range(3):
-        K.gemm_bf16_nt(a, bt, out=c)
-        K.gemm_bf16_nt(a, bt, out=c, variant=1)
-        K.gemm_bf16_nt(a, bt, out=c, variant=2)
-        K.gemm_bf16_nt(a, bt, out=c, variant=3)
+        for v in GEMM_VARIANTS:
+            K.gemm_bf16_nt(a, bt, out=c, variant=v)
         torch.matmul(a, b, out=c2)
     for _ in range(rounds):
-        ours.append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c), iters))
-        v1.append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c, variant=1), iters))
-        v2.append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c, variant=2), iters))
-        v3.append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c, variant=3), iters))
+        for v in GEMM_VARIANTS:
+            times[v].append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c, variant=v), iters))
         lib.append(time_ms(lambda: torch.matmul(a, b, out=c2), iters))
     fl = 2.0 * n ** 3
     K.gemm_bf16_nt(a, bt, out=c)
     err = (c.float() - c2.float()).abs().max().item()
-    return {
-        "n": n,
-        "dbuf_tflops": fl / statistics.median(v1) / 1e9,
-        "ring_tflops": fl / statistics.median(v2) / 1e9,
-        "w4_tflops": fl / statistics.median(v3) / 1e9,
+    out = {"n": n}
+    for v, name in GEMM_VARIANTS.items():
+        out[f"{name}_tflops"] = fl / statistics.median(times[v]) / 1e9
+    ours = times[0]
+    out.update({
         "ours_ms_median": statistics.median(ours),
         "ours_tflops": fl / statistics.median(ours) / 1e9,
         "ours_tflops_best": fl / min(ours) / 1e9,
         "hipblaslt_ms_median": statistics.median(lib),
         "hipblaslt_tflops": fl / statistics.median(lib) / 1e9,
         "max_abs_diff_vs_hipblaslt": err,
-    }
+    })
+    return out
 
 
 def bench_hbm(nbytes, rounds, iters):
