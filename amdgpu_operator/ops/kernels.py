@@ -128,8 +128,9 @@ def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int = 0)
     """K2: ``out[M,N] = a[M,K] @ bt[N,K].T`` on MFMA (bf16 in, fp32 accumulate).
 
     M and N must be multiples of 256 and K of 64 (the kernel has no edge
-    tiles; the validator picks its shapes accordingly).  ``variant`` 0 is the
-    4-slot LDS-DMA ring (default), 1 the 2-stage double buffer.
+    tiles; the validator picks its shapes accordingly).  ``variant`` selects
+    the kernel (0 = the default ring + ping-pong; 1-5 are the A/B reference
+    kernels listed at ``avk_gemm_bf16_nt_variant`` in validator_kernels.hip).
     """
     import torch
 

@@ -851,8 +851,15 @@ AVK_API int avk_vector_add_f32(const float* a, const float* b, float* c, int64_t
   return hipGetLastError();
 }
 
-// variant 0 = ring + ping-pong (default), 1 = 2-stage double buffer, 2 = ring
-// without the ping-pong (the last two are kept as A/B reference points)
+// Variants (profiles/r1_gemm/kernel_bench_variants.json; 8192^3 random bf16):
+//   0 ring + ping-pong, LDS-DMA issued in the MFMA segment (default)  1327-1356 TF/s
+//   1 2-stage double buffer, one barrier per K-step                   1252-1298
+//   2 4-slot ring without the ping-pong                                1213-1253
+//   3 4 waves x 128x128 (one wave per SIMD)                            1228-1271
+//   4 ring + ping-pong, LDS-DMA issued in the read segment             1312-1338
+//   5 as 0 with a 5-slot (160 KiB) ring                                1310-1328
+// A finer split (two 16-MFMA phases per slice, 4 barriers) measured 1308:
+// not kept.
 AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K,
                                      int variant, hipStream_t s) {
   using namespace gemm;
@@ -864,8 +871,8 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
   const __bf16* b = (const __bf16*)Bt;
   switch (variant) {
     case 0:
-      if (out_f32) gemm_bf16_nt_pp_kernel<true, false><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
-      else gemm_bf16_nt_pp_kernel<false, false><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
+      if (out_f32) gemm_bf16_nt_pp_kernel<true, true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
+      else gemm_bf16_nt_pp_kernel<false, true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
       break;
     case 1:
       if (out_f32) gemm_bf16_nt_kernel<true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
@@ -880,8 +887,8 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
       else gemm_bf16_nt_w4_kernel<false><<<nwg, gw4::NTHR, 0, s>>>(a, b, C, M, N, K);
       break;
     case 4:
-      if (out_f32) gemm_bf16_nt_pp_kernel<true, true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
-      else gemm_bf16_nt_pp_kernel<false, true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
+      if (out_f32) gemm_bf16_nt_pp_kernel<true, false><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
+      else gemm_bf16_nt_pp_kernel<false, false><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
       break;
     case 5:
       if (out_f32) gemm_bf16_nt_pp_kernel<true, true, 5><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);

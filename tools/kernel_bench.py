@@ -30,7 +30,7 @@ def time_ms(fn, iters):
     return s.elapsed_time(e) / iters
 
 
-GEMM_VARIANTS = {0: "default", 1: "dbuf", 2: "ring", 3: "w4", 4: "pp_load_in_m", 5: "pp_load_in_m_5slot"}
+GEMM_VARIANTS = {0: "default", 1: "dbuf", 2: "ring", 3: "w4", 4: "pp_load_in_r", 5: "pp_5slot"}
 
 
 def bench_gemm(n, rounds, iters):
