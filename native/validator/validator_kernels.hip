@@ -73,15 +73,26 @@ __global__ __launch_bounds__(256) void fill_uniform_bf16_kernel(__bf16* __restri
 
 // ------------------------------------------------------------ K1 vector add ----
 
-__global__ __launch_bounds__(256) void vector_add_kernel(const float4* __restrict__ a,
-                                                         const float4* __restrict__ b,
-                                                         float4* __restrict__ c, int64_t n4) {
-  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  int64_t stride = (int64_t)gridDim.x * 256;
-  for (; i < n4; i += stride) {
-    float4 x = a[i], y = b[i];
-    c[i] = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+// U float4s per lane per iteration, nontemporal (streamed once) - the K3
+// sweep's best copy shape (profiles/r1_hbm)
+template <int U>
+__global__ __launch_bounds__(256) void vector_add_kernel(const f32x4* __restrict__ a, const f32x4* __restrict__ b,
+                                                         f32x4* __restrict__ c, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * 256 * U;
+  int64_t i = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  for (; i + (U - 1) * 256 < n4; i += stride) {
+    f32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x[u] = __builtin_nontemporal_load(a + i + u * 256);
+      y[u] = __builtin_nontemporal_load(b + i + u * 256);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(x[u] + y[u], c + i + u * 256);
   }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (i + u * 256 < n4) c[i + u * 256] = a[i + u * 256] + b[i + u * 256];
 }
 
 __global__ void vector_add_tail_kernel(const float* a, const float* b, float* c, int64_t start, int64_t n) {
@@ -778,22 +789,29 @@ struct PeerPtrsMut {
   float* p[8];
 };
 
-// one-shot: out[i] = sum_r in_r[i] for every i (each rank reads every peer)
+// one-shot: out[i] = sum_r in_r[i] for every i (each rank reads every peer).
+// Every peer's float4 is loaded before the first add (NP loads in flight per
+// lane; over xGMI each peer sits behind its own link), streamed nontemporal.
 template <int NP>
 __global__ __launch_bounds__(256) void allreduce_oneshot_f32_kernel(PeerPtrs in, float* __restrict__ out,
                                                                     int64_t n4, int np_runtime) {
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  const int np = NP > 0 ? NP : np_runtime;
-  for (; i < n4; i += stride) {
-    float4 s = reinterpret_cast<const float4*>(in.p[0])[i];
+  if constexpr (NP > 0) {
+    for (; i < n4; i += stride) {
+      f32x4 v[NP];
 #pragma unroll
-    for (int r = 1; r < (NP > 0 ? NP : 8); ++r) {
-      if (NP == 0 && r >= np) break;
-      float4 v = reinterpret_cast<const float4*>(in.p[r])[i];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      for (int r = 0; r < NP; ++r) v[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[r]) + i);
+#pragma unroll
+      for (int r = 1; r < NP; ++r) v[0] += v[r];
+      __builtin_nontemporal_store(v[0], reinterpret_cast<f32x4*>(out) + i);
     }
-    reinterpret_cast<float4*>(out)[i] = s;
+  } else {
+    for (; i < n4; i += stride) {
+      f32x4 acc = reinterpret_cast<const f32x4*>(in.p[0])[i];
+      for (int r = 1; r < np_runtime; ++r) acc += reinterpret_cast<const f32x4*>(in.p[r])[i];
+      reinterpret_cast<f32x4*>(out)[i] = acc;
+    }
   }
 }
 
@@ -846,7 +864,8 @@ AVK_API int avk_vector_add_f32(const float* a, const float* b, float* c, int64_t
   if (!a || !b || !c || n < 0) return hipErrorInvalidValue;
   if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16 != 0) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
-  if (n4 > 0) vector_add_kernel<<<grid_for(n4, 256, 2048), 256, 0, s>>>((const float4*)a, (const float4*)b, (float4*)c, n4);
+  if (n4 > 0)
+    vector_add_kernel<4><<<grid_for(n4, 256 * 4, 4096), 256, 0, s>>>((const f32x4*)a, (const f32x4*)b, (f32x4*)c, n4);
   if (n4 * 4 < n) vector_add_tail_kernel<<<1, 64, 0, s>>>(a, b, c, n4 * 4, n);
   return hipGetLastError();
 }
@@ -930,15 +949,33 @@ AVK_API int avk_gemv_cols_bf16(const void* X, const float* v, float* z, int R, i
 }
 
 // variant: 0 = plain loads/stores, 1 = nontemporal
+// variant bit 0: nontemporal loads/stores; bits 1-2: float4s per lane per
+// iteration (0 -> 4, 1 -> 8, 2 -> 2, 3 -> 1).  Grid = num_cus * 16 blocks of
+// 256: the sweep in profiles/r1_hbm (1 GiB, read + write counted) peaks at
+// 6.30 TB/s for nontemporal x4 at 16 blocks/CU vs 6.10 at 8 and 5.08 for
+// torch's copy_.
 AVK_API int avk_hbm_copy(const void* src, void* dst, int64_t bytes, int num_cus, int variant, hipStream_t s) {
   if (!src || !dst || bytes <= 0 || bytes % 16 || (((uintptr_t)src | (uintptr_t)dst) % 16)) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 7) return hipErrorInvalidValue;
   const int64_t n = bytes / 16;
-  const int blocks = (num_cus > 0 ? num_cus : 256) * 8;
-  const int g = grid_for(n, 256 * 4, blocks);
-  if (variant == 1)
-    hbm_copy_kernel<4, true><<<g, 256, 0, s>>>((const f32x4*)src, (f32x4*)dst, n);
-  else
-    hbm_copy_kernel<4, false><<<g, 256, 0, s>>>((const f32x4*)src, (f32x4*)dst, n);
+  const int blocks = (num_cus > 0 ? num_cus : 256) * 16;
+  const bool nt = variant & 1;
+  const int u = (const int[]){4, 8, 2, 1}[(variant >> 1) & 3];
+  const int g = grid_for(n, 256 * u, blocks);
+  const f32x4* a = (const f32x4*)src;
+  f32x4* d = (f32x4*)dst;
+#define AVK_COPY(U)                                                      \
+  if (nt)                                                                \
+    hbm_copy_kernel<U, true><<<g, 256, 0, s>>>(a, d, n);                 \
+  else                                                                   \
+    hbm_copy_kernel<U, false><<<g, 256, 0, s>>>(a, d, n);
+  switch (u) {
+    case 8: AVK_COPY(8) break;
+    case 2: AVK_COPY(2) break;
+    case 1: AVK_COPY(1) break;
+    default: AVK_COPY(4) break;
+  }
+#undef AVK_COPY
   return hipGetLastError();
 }
 
@@ -967,7 +1004,7 @@ AVK_API int avk_allreduce_oneshot_f32(const float* const* ptrs, int np, float* o
     pp.p[r] = ptrs[r];
   }
   const int64_t n4 = count / 4;
-  const int g = grid_for(n4, 256, 256 * 8);
+  const int g = grid_for(n4, 256, 256 * 16);
   switch (np) {
     case 2: allreduce_oneshot_f32_kernel<2><<<g, 256, 0, s>>>(pp, out, n4, np); break;
     case 4: allreduce_oneshot_f32_kernel<4><<<g, 256, 0, s>>>(pp, out, n4, np); break;
