@@ -42,6 +42,7 @@ def _lib() -> ctypes.CDLL:
         "avk_fill_uniform_f32": ([P, I64, U64, F, F, S], I),
         "avk_fill_uniform_bf16": ([P, I64, U64, F, F, S], I),
         "avk_vector_add_f32": ([P, P, P, I64, S], I),
+        "avk_vector_add_verify_f32": ([P, P, P, I64, P, S], I),
         "avk_gemm_bf16_nt": ([P, P, P, I, I, I, I, S], I),
         "avk_gemm_bf16_nt_variant": ([P, P, P, I, I, I, I, I, S], I),
         "avk_gemv_rows": ([P, I, P, P, I, I, S], I),
@@ -122,6 +123,20 @@ def vector_add(a, b, out=None, stream=None):
     _require(out, torch.float32, "out")
     _check(_lib().avk_vector_add_f32(a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), _stream(stream)), "vector_add")
     return out
+
+
+def vector_add_verify(a, b, c, stream=None) -> int:
+    """K1 check on the device: number of i with ``c[i] != a[i] + b[i]``."""
+    import torch
+
+    for t, n in ((a, "a"), (b, "b"), (c, "c")):
+        _require(t, torch.float32, n)
+    if not a.numel() == b.numel() == c.numel():
+        raise ValueError("size mismatch")
+    bad = torch.empty(1, device=a.device, dtype=torch.int64)
+    _check(_lib().avk_vector_add_verify_f32(a.data_ptr(), b.data_ptr(), c.data_ptr(), a.numel(), bad.data_ptr(),
+                                            _stream(stream)), "vector_add_verify")
+    return int(bad.item())
 
 
 def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int = 0):

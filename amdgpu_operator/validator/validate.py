@@ -141,7 +141,11 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     run_id = uuid.uuid4().hex[:12]
     rdv = os.path.join(env.validations_dir, "rendezvous", run_id)
     os.makedirs(rdv, exist_ok=True)
-    counter_env = {"AMDGPU_VALIDATOR_COUNTERS": "1"} if "--counter-gate" in args else {}
+    # N7: the counter gate is a rocprofiler-sdk tool library loaded only into
+    # the gated kernel processes (the binary does not link the SDK)
+    counter_env = ({"AMDGPU_VALIDATOR_COUNTERS": "1",
+                    "ROCP_TOOL_LIBRARIES": str(native.artefact("libamdgpu_counter_gate.so"))}
+                   if "--counter-gate" in args else {})
     steps = _steps_of(args)
     kernel_steps = [s for s in steps if s != "rccl"]
     # RCCL runs in its own process per GPU, concurrently with the kernel

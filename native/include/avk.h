@@ -14,6 +14,8 @@ int avk_abi_version(void);
 int avk_fill_uniform_f32(float* p, int64_t n, uint64_t seed, float lo, float hi, hipStream_t s);
 int avk_fill_uniform_bf16(void* p, int64_t n, uint64_t seed, float lo, float hi, hipStream_t s);
 int avk_vector_add_f32(const float* a, const float* b, float* c, int64_t n, hipStream_t s);
+int avk_vector_add_verify_f32(const float* a, const float* b, const float* c, int64_t n, unsigned long long* bad_dev,
+                              hipStream_t s);
 int avk_gemm_bf16_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K, hipStream_t s);
 int avk_gemv_rows(const void* X, int x_is_bf16, const float* v, float* y, int R, int C, hipStream_t s);
 int avk_gemv_cols_bf16(const void* X, const float* v, float* z, int R, int C, hipStream_t s);
@@ -24,6 +26,8 @@ int avk_allreduce_oneshot_f32(const float* const* ptrs, int np, float* out, int6
 int avk_allreduce_twoshot_f32(const float* const* in_ptrs, float* const* out_ptrs, int np, int rank, int64_t count,
                               hipStream_t s);
 
+// N7 counter gate: exported by libamdgpu_counter_gate.so (a rocprofiler-sdk
+// tool), resolved at run time by the validator (validator_main.cpp, Gate)
 int avk_prof_active(void);
 void avk_prof_arm(const char* kernel_substr);
 void avk_prof_disarm(void);

@@ -3,11 +3,12 @@
 // The validator decides a node is Ready from correctness AND hardware
 // evidence that the MFMA pipes executed: it reads
 // per-dispatch PMC counters of its own GEMM through the rocprofiler-sdk
-// dispatch counting service.  This translation unit defines the
-// `rocprofiler_configure` tool entry point that rocprofiler-register looks for
-// when the HIP runtime initialises; the tool is only activated when
-// AMDGPU_VALIDATOR_COUNTERS=1 (otherwise rocprofiler_configure returns null and
-// the process runs unprofiled, e.g. under an outer rocprofv3).
+// dispatch counting service.  Built as libamdgpu_counter_gate.so: a
+// rocprofiler-sdk tool library loaded through ROCP_TOOL_LIBRARIES (the
+// validator sets it for gated runs before its first HIP call; the operator
+// sets it in the pod env).  Its `rocprofiler_configure` entry point activates
+// the tool only when AMDGPU_VALIDATOR_COUNTERS=1 (otherwise it returns null
+// and the process runs unprofiled, e.g. under an outer rocprofv3).
 //
 // gfx950 has no derived-counter XML in ROCm 7.2 (MI355X_MICROARCH.md
 // §rocprofv3 PMC slots), so only raw counters are requested:

@@ -100,6 +100,22 @@ __global__ void vector_add_tail_kernel(const float* a, const float* b, float* c,
   if (i < n) c[i] = a[i] + b[i];
 }
 
+// K1 check: counts c[i] != a[i] + b[i] on the device (the validator also
+// spot-checks a prefix on the host), so the 16M-element check costs one
+// stream over HBM instead of a 192 MB device-to-host copy
+__global__ __launch_bounds__(256) void vector_add_verify_kernel(const float* __restrict__ a,
+                                                                const float* __restrict__ b,
+                                                                const float* __restrict__ c, int64_t n,
+                                                                unsigned long long* __restrict__ bad) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  unsigned long long m = 0;
+  for (; i < n; i += stride) m += c[i] != a[i] + b[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m += __shfl_xor(m, off, 64);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, m);
+}
+
 // --------------------------------------------------------- K2 bf16 MFMA GEMM ----
 //
 // C[M][N] = A[M][K] · Bt[N][K]^T   (both operands K-contiguous, "NT")
@@ -879,6 +895,15 @@ AVK_API int avk_vector_add_f32(const float* a, const float* b, float* c, int64_t
 //   5 as 0 with a 5-slot (160 KiB) ring                                1310-1328
 // A finer split (two 16-MFMA phases per slice, 4 barriers) measured 1308:
 // not kept.
+AVK_API int avk_vector_add_verify_f32(const float* a, const float* b, const float* c, int64_t n,
+                                      unsigned long long* bad_dev, hipStream_t s) {
+  if (!a || !b || !c || !bad_dev || n <= 0) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(bad_dev, 0, sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  vector_add_verify_kernel<<<grid_for(n, 256, 4096), 256, 0, s>>>(a, b, c, n, bad_dev);
+  return hipGetLastError();
+}
+
 AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K,
                                      int variant, hipStream_t s) {
   using namespace gemm;

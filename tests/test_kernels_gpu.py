@@ -185,3 +185,16 @@ def test_workload_rccl_collectives_single_rank(tmp_path):
     rep = json.loads(p.stdout.strip().splitlines()[-1])
     assert rep["ok"] and rep["world"] == 1
     assert set(rep["collectives"]) == {"allreduce_f32", "allreduce_bf16", "allgather_f32", "reducescatter_f32"}
+
+
+def test_vector_add_verify_counts_corruption():
+    n = (1 << 20) + 3
+    a = torch.empty(n, device="cuda")
+    b = torch.empty(n, device="cuda")
+    K.fill_uniform_(a, 5)
+    K.fill_uniform_(b, 6)
+    c = K.vector_add(a, b)
+    assert K.vector_add_verify(a, b, c) == 0
+    c[5] += 1.0
+    c[n - 1] = float("nan")
+    assert K.vector_add_verify(a, b, c) == 2

@@ -37,6 +37,15 @@ def test_validator_all_local_steps_with_counter_gate(tmp_path):
     assert steps["xgmi"]["emulated"] and steps["xgmi"]["max_abs_err"] <= 8e-5
 
 
+def test_validator_counter_gate_tool_library_from_env(tmp_path):
+    # the operator's path: the tool library is named explicitly (validate.py)
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--gemm", "1024", "--counter-gate"],
+                   {"AMDGPU_VALIDATOR_COUNTERS": "1",
+                    "ROCP_TOOL_LIBRARIES": str(native.artefact("libamdgpu_counter_gate.so"))})
+    assert rc == 0 and rep["ok"], rep
+    assert {s["name"]: s for s in rep["steps"]}["gemm"]["counter_gate"] == "pass"
+
+
 def test_validator_counter_gate_unavailable_fails_closed(tmp_path):
     # gate requested but the tool was not activated: must not silently pass
     rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--counter-gate"])
