@@ -139,6 +139,25 @@ constexpr int GROUP_M = 4;                   // tile rows per L2 band
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
+// Diagnostic build only (-DAVK_STAMPS, tools/gemm_stamps.py): s_memtime at
+// the segment boundaries of the ping-pong GEMM for the first workgroups, to
+// split a slice into read / wait / barrier / MFMA time.  The shipped library
+// compiles every AVK_STAMP away.
+#ifdef AVK_STAMPS
+constexpr int kStampBlocks = 4, kStampSlices = 32, kStampPoints = 6;
+__device__ unsigned long long g_stamps[kStampBlocks * 8 * kStampSlices * kStampPoints];
+#define AVK_STAMP(t, k)                                                                              \
+  do {                                                                                               \
+    if (blockIdx.x < kStampBlocks && (t) < kStampSlices && (threadIdx.x & 63) == 0)                 \
+      g_stamps[((blockIdx.x * 8 + (threadIdx.x >> 6)) * kStampSlices + (t)) * kStampPoints + (k)] = \
+          __builtin_amdgcn_s_memtime();                                                              \
+  } while (0)
+#else
+#define AVK_STAMP(t, k) \
+  do {                  \
+  } while (0)
+#endif
+
 __device__ __forceinline__ void gemm_stage(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                                            int K, int m0, int n0, int k0, char* stage_base, int wave,
                                            int lane) {
@@ -481,6 +500,7 @@ __global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_pp_kernel(const _
   const int rsub = lane >> 2, pc = lane & 3;
 
   for (int t = 0; t < nk; ++t) {
+    AVK_STAMP(t, 0);
     // ---- R(t)
     if (!LOAD_IN_M && t + 3 < nk)
       ring_stage(A, Bt, K, m0, n0, (t + 3) * BK, smem + ((t + 3) & 3) * SLOT_BYTES, wave, lane);
@@ -491,6 +511,7 @@ __global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_pp_kernel(const _
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(slot + a_off + i * 1024);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    AVK_STAMP(t, 1);
     if (lag) {
       if constexpr (LOAD_IN_M && AHEAD == 4)
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -499,7 +520,9 @@ __global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_pp_kernel(const _
       else
         wait_slice_vmcnt(min(2, nk - 2 - t));
     }
+    AVK_STAMP(t, 2);
     wg_barrier();
+    AVK_STAMP(t, 3);
     // ---- M(t)
     char* sslot = smem + ((t + AHEAD) % NSLOT) * SLOT_BYTES;
     const int kload = min(t + AHEAD, nk - 1) * BK;
@@ -525,6 +548,7 @@ __global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_pp_kernel(const _
       }
     }
     __builtin_amdgcn_s_setprio(0);
+    AVK_STAMP(t, 4);
     if (!lag) {
       if constexpr (LOAD_IN_M && AHEAD == 4)
         asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
@@ -533,6 +557,7 @@ __global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_pp_kernel(const _
       else
         wait_slice_vmcnt(min(2, nk - 2 - t));
     }
+    AVK_STAMP(t, 5);
     if (!(lag && t == nk - 1)) wg_barrier();
   }
   if constexpr (LOAD_IN_M) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy refills drained
@@ -861,6 +886,13 @@ inline int grid_for(int64_t work_items, int per_block, int max_blocks) {
 // ============================================================== C ABI ====
 
 AVK_API int avk_abi_version() { return 1; }
+
+#ifdef AVK_STAMPS
+AVK_API int avk_stamps_read(unsigned long long* host, int n) {
+  const int total = kStampBlocks * 8 * kStampSlices * kStampPoints;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * (n < total ? n : total));
+}
+#endif
 
 AVK_API int avk_fill_uniform_f32(float* p, int64_t n, uint64_t seed, float lo, float hi, hipStream_t s) {
   if (!p || n < 0) return hipErrorInvalidValue;
