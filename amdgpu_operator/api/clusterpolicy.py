@@ -119,6 +119,7 @@ class MetricsExporterSpec(Operand):
     port: int = 9400
     intervalSeconds: float = 1.0
     podAttribution: bool = True
+    dcgmNames: bool = False  # also emit DCGM_FI_DEV_* series for existing dashboards
     serviceMonitor: ServiceMonitor = Field(default_factory=ServiceMonitor)
 
 

@@ -8,6 +8,7 @@ Sub-commands:
 * ``verify``                - machine-checked version of README.md:113-215
 * ``render``                - render the chart with ``--set`` flags (helm template)
 * ``simulate``              - bring up a simulated cluster and report time-to-Ready
+* ``preflight``             - node prerequisites of README.md:5-49 + the GPU/driver state, checked (``--fix``)
 * ``collectives``           - RCCL sweep (all-reduce / all-gather / reduce-scatter, algBW + busBW);
                               one rank per GPU under ``torch.distributed.run``
 * ``driver|toolkit|validate|device-plugin|metrics-exporter|node-status-exporter|nfd|gfd|partition-manager``
@@ -116,6 +117,12 @@ def main(argv: list[str] | None = None) -> int:
     sm.add_argument("--set", action="append", default=[])
     sm.add_argument("--real-gpus", action="store_true", help="use this machine's GPUs and sysfs")
     sm.add_argument("--timeout", type=float, default=120)
+    pf = sub.add_parser("preflight", help="check (and --fix) a node's prerequisites before kubeadm join")
+    pf.add_argument("--root", default="/")
+    pf.add_argument("--fix", action="store_true")
+    pf.add_argument("--json", action="store_true")
+    pf.add_argument("--expect-gpus", type=int, default=None)
+    pf.add_argument("--no-gpu", action="store_true", help="control-plane / CPU node: skip the GPU checks")
     co = sub.add_parser("collectives", help="RCCL collective sweep (run under torch.distributed.run)")
     co.add_argument("--min-bytes", type=int, default=8)
     co.add_argument("--max-bytes", type=int, default=1 << 30)
@@ -179,6 +186,10 @@ def main(argv: list[str] | None = None) -> int:
             c.stop()
     if args.cmd == "collectives":
         return _collectives(args)
+    if args.cmd == "preflight":
+        from .preflight import main_preflight
+
+        return main_preflight(args.root, args.fix, args.json, args.expect_gpus, not args.no_gpu)
     return 2
 
 

@@ -100,7 +100,16 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
         ok = count > 0 and (want is None or count == want)
         rep.add(f"allocatable[{name}]", ok, f"{RESOURCE_NAME}={count}" + (f" (expected {want})" if want else ""),
                 "README.md:122")
-        validated = (n["metadata"].get("labels") or {}).get("amd.com/gpu.validated") == "true"
+        labels = n["metadata"].get("labels") or {}
+        # what the reference reads off `nvidia-smi` in the driver container
+        # (README.md:152-166: product, memory, GPU count) comes from GFD labels
+        prod, mem, arch = (labels.get("amd.com/gpu.product"), labels.get("amd.com/gpu.memory"),
+                           labels.get("amd.com/gpu.arch"))
+        cnt = labels.get("amd.com/gpu.count")
+        inv_ok = bool(prod and mem and arch) and (cnt is None or int(cnt) > 0)
+        rep.add(f"gpu-inventory[{name}]", inv_ok,
+                f"product={prod} arch={arch} memory={mem}MiB count={cnt}", "README.md:152-166")
+        validated = labels.get("amd.com/gpu.validated") == "true"
         rep.add(f"validated[{name}]", validated, "amd.com/gpu.validated=true" if validated else "not validated",
                 "README.md:199")
 

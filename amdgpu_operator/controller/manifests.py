@@ -283,6 +283,8 @@ def state_metrics_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict
     args = ["metrics-exporter", "--port", str(m.port), "--interval", str(m.intervalSeconds)]
     if m.podAttribution:
         args.append("--pod-attribution")
+    if m.dcgmNames:
+        args.append("--dcgm-names")
     ctr = _container("amd-metrics-exporter", image, m.imagePullPolicy, args + list(m.args),
                      [_mount("pod-resources", "/var/lib/kubelet/pod-resources", ro=True),
                       _mount("host-sys", "/host/sys", ro=True)], list(m.env), True, m.resources.model_dump(),
