@@ -36,6 +36,8 @@ def build_parser() -> argparse.ArgumentParser:
     v.add_argument("step", choices=["driver", "toolkit", "workload", "plugin", "gpu", "complete"])
     v.add_argument("--resource", default="amd.com/gpu")
     v.add_argument("--timeout", type=float, default=600.0)
+    v.add_argument("--wait-toolkit", action="store_true",
+                   help="gpu: plugin validation waits for the toolkit; the workload starts right away")
 
     dp = sub.add_parser("device-plugin", help="kubelet device plugin for amd.com/gpu")
     dp.add_argument("--resource-name", default="amd.com/gpu")
@@ -80,6 +82,10 @@ def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
         if a in ("--resource", "--timeout"):
             known += args[i:i + 2]
             i += 2
+            continue
+        if a == "--wait-toolkit":
+            known.append(a)
+            i += 1
             continue
         if a.startswith("--") or extra:
             extra.append(a)
@@ -146,7 +152,8 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                 pod_args = _plugin_pod_args(extra)
                 V.validate_plugin(env, a.resource, pod_args=pod_args, timeout=a.timeout, stop=stop)
         elif a.step == "gpu":
-            V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop)
+            V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
+                           wait_toolkit=a.wait_toolkit)
         else:
             V.complete(env)
             ready()

@@ -241,15 +241,17 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     if w.counterGate:
         wl_args += ["--counter-gate"]
     inits = [_wait_init("driver-validation", image, v.imagePullPolicy, "driver")]
-    if spec.toolkit.enabled:
-        inits.append(_wait_init("toolkit-validation", image, v.imagePullPolicy, "toolkit"))
     if v.pluginValidation and spec.devicePlugin.enabled:
         # workload (all GPUs, RCCL over xGMI) and plugin (1-GPU pods through the
-        # device plugin + OCI hook) validation run concurrently: the plugin pods
-        # only need a registered device plugin, not the workload result
-        inits.append(_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu",
-                                ["--resource", spec.devicePlugin.resourceName, *wl_args]))
+        # device plugin + OCI hook) validation run concurrently.  The workload
+        # needs only the driver (its processes run in this pod, not through the
+        # runtime hook), so it overlaps the toolkit install; the plugin pods
+        # wait for the toolkit inside the step.
+        extra = ["--resource", spec.devicePlugin.resourceName] + (["--wait-toolkit"] if spec.toolkit.enabled else [])
+        inits.append(_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args]))
     else:
+        if spec.toolkit.enabled:
+            inits.append(_wait_init("toolkit-validation", image, v.imagePullPolicy, "toolkit"))
         inits.append(_wait_init("workload-validation", image, v.imagePullPolicy, "workload", wl_args))
     ctr = _container("amd-operator-validator", image, v.imagePullPolicy, ["validate", "complete"],
                      [_mount("run-amd-validations", VALIDATIONS_HOST_DIR)], list(v.env), True,

@@ -310,8 +310,14 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
 
 
 def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURCE_NAME,
-                 pod_args: list[str] | None = None, timeout: float = 600.0, stop=None) -> dict:
-    """Workload and plugin validation concurrently (each skipped if already done)."""
+                 pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
+                 wait_toolkit: bool = False) -> dict:
+    """Workload and plugin validation concurrently (each skipped if already done).
+
+    Only the driver gates the workload: its processes run in this privileged
+    pod, not through the container runtime, so they start while the toolkit
+    is still being installed.  The plugin pods go through the runtime hook
+    and therefore wait for the toolkit (``wait_toolkit``) before running."""
     t0 = time.perf_counter()
     results: dict = {}
     errors: list[str] = []
@@ -325,6 +331,8 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
 
     def plugin():
         try:
+            if wait_toolkit:
+                wait_ready(env, "toolkit", timeout, stop)
             if read_ready(env, "plugin") is None:
                 results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop)
         except Exception as e:  # noqa: BLE001

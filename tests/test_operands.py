@@ -236,3 +236,19 @@ def test_cli_verify_against_http_apiserver(tmp_path, capsys):
         assert rep["ok"] is False and any(c["name"] == "gpu-nodes-labelled" for c in rep["checks"])
     finally:
         srv.stop()
+
+
+def test_gpu_validation_overlaps_workload_with_toolkit_install(env):
+    """The workload needs only the driver; plugin pods wait for the toolkit."""
+    seen_toolkit = []
+
+    def launcher(argv, e, device, timeout):
+        seen_toolkit.append(V.read_ready(env, "toolkit"))
+        steps = argv[argv.index("--steps") + 1].split(",")
+        return ProcResult(0, json.dumps({"ok": True, "steps": [{"name": s, "ok": True} for s in steps]}), "", 0.0)
+
+    env.launcher = launcher
+    with pytest.raises(V.StepFailed, match="toolkit"):
+        V.validate_gpu(env, [], timeout=0.3, wait_toolkit=True)
+    assert seen_toolkit and all(t is None for t in seen_toolkit)
+    assert V.read_ready(env, "workload")["ok"] and V.read_ready(env, "plugin") is None
