@@ -344,8 +344,12 @@ Step step_gemm(const Args& a, hipStream_t st) {
       gate_ok = false;
       gate_json = "\"counter_gate\": \"unavailable\"";
     } else {
+      // the dispatch-counting record callback runs on the profiler's thread
+      // after the dispatch retires: poll for it (bounded) instead of sleeping
       HIP_OK(hipDeviceSynchronize());
-      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      const auto tw = Clock::now();
+      while ((g_gate.dispatches() == 0 || g_gate.value("SQ_INSTS_VALU_MFMA_MOPS_BF16") < 0) && secs(tw) < 0.5)
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
       const double mops = g_gate.value("SQ_INSTS_VALU_MFMA_MOPS_BF16");
       const double busy = g_gate.value("SQ_VALU_MFMA_BUSY_CYCLES");
       const double waves = g_gate.value("SQ_WAVES");
