@@ -37,6 +37,8 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# child processes (stand-in validators, operand helpers) import the package too
+os.environ["PYTHONPATH"] = os.pathsep.join([ROOT] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
 
 BASELINE_TTR_S = 600.0
 METRIC = "validator pod time-to-Ready (s) + allocatable amd.com/gpu at 1/2/4/8 MI355X"
