@@ -139,13 +139,17 @@ def vector_add_verify(a, b, c, stream=None) -> int:
     return int(bad.item())
 
 
-def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int = 0):
+GEMM_DEFAULT_VARIANT = 6
+
+
+def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int = GEMM_DEFAULT_VARIANT):
     """K2: ``out[M,N] = a[M,K] @ bt[N,K].T`` on MFMA (bf16 in, fp32 accumulate).
 
     M and N must be multiples of 256 and K of 64 (the kernel has no edge
     tiles; the validator picks its shapes accordingly).  ``variant`` selects
-    the kernel (0 = the default ring + ping-pong; 1-5 are the A/B reference
-    kernels listed at ``avk_gemm_bf16_nt_variant`` in validator_kernels.hip).
+    the kernel (default 6 = the 8-phase quadrant pipeline, the kernel the
+    native validator runs; 0-9 are the A/B kernels listed with their measured
+    TF/s above ``avk_gemm_bf16_nt_variant`` in validator_kernels.hip).
     """
     import torch
 

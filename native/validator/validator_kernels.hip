@@ -5,7 +5,8 @@
 // file is the MI355X-native replacement described in SURVEY.md §2.D:
 //   K1 vector_add      - fp32 c = a + b, 16 B/lane, grid-stride
 //   K2 gemm_bf16_nt    - bf16 MFMA GEMM (v_mfma_f32_16x16x32_bf16), 256x256x64
-//                        block tile, 8 waves, global_load_lds staging into an
+//                        block tile, 8 waves in two ping-pong groups, 8-phase
+//                        quadrant pipeline, global_load_lds staging into an
 //                        XOR-swizzled LDS image, XCD-aware tile order
 //   K3 hbm_copy        - float4 streaming copy (HBM3E bandwidth check)
 //   K4 allreduce_*     - one-shot / two-shot sum over n peer buffers (peer
@@ -730,6 +731,239 @@ __global__ __launch_bounds__(gw4::NTHR, 1) void gemm_bf16_nt_w4_kernel(const __b
     }
 }
 
+// ------------------- K2 GEMM, 8-phase quadrant pipeline (BK = 64, 2 buffers) ----
+//
+// Same 256x256 block, 8 waves (2M x 4N, 128x64 per wave, 16x16x32 MFMA) and
+// two-group ping-pong as gemm_bf16_nt_pp_kernel, but the unit of work is a
+// wave QUADRANT (64 rows x 32 cols x K 64 = 16 MFMAs) and the unit of staging
+// a HALF-TILE (16 KiB) that is refilled as soon as its fragments are in
+// registers (cdna_hip_programming.md §5 "The 256² 8-phase template").
+//
+// A K-tile (64 deep) lives in one of two 64 KiB buffers as four half-tiles:
+//   A0 / A1  = quadrant rows 0..63 / 64..127 of BOTH row groups (128 rows)
+//   B0 / B1  = quadrant cols 0..31 / 32..63 of all four column groups
+// (128-B rows, source-side XOR swizzle chunk ^ ((row >> 1) & 7): every 16-lane
+// ds_read_b128 group hits 16 distinct bank slots).  Phases of K-tile t:
+//   phase  reads (regs)         MFMAs     refill issued (LDS slot freed)
+//   0      A0 -> a, B0 -> b0    Q(0,0)    A1 of K-tile t+1 (other buffer)
+//   1      B1 -> b1             Q(0,1)    A0 of K-tile t+2 (read in phase 0)
+//   2      A1 -> a              Q(1,1)    B0 of K-tile t+2 (read in phase 0)
+//   3      -                    Q(1,0)    B1 of K-tile t+2 (read in phase 1)
+// so every half-tile is issued 6-7 phases before it is read, and at every
+// wait five younger half-tiles (10 LDS-DMAs per wave) may stay in flight.
+// A phase = read segment | barrier | MFMA segment | barrier; group 1 (waves
+// 4-7) passes one extra barrier up front, so each SIMD alternates one wave
+// reading with one wave issuing MFMAs.  Barrier b separates segments b, b+1;
+// group 0 reads phase R in segment 2R, group 1 in 2R+1.
+//   RAW  data read in phase R was issued by phase R-6; every wave retires it
+//        before barrier 2R-1 (group 0 at the end of its MFMA segment R-1,
+//        group 1 at the end of its read segment R-1) with vmcnt(10) - or
+//        vmcnt(8) for group 1 when the refill sits in the MFMA segment
+//        (LOAD_IN_M: issued only through R-2 at that point).
+//   WAR  a slot is refilled one phase after its last read; those reads were
+//        retired by lgkmcnt(0) BEFORE the reading phase's first barrier, which
+//        every wave passes before it issues the refill.
+// Past the last K-tile the refills re-read K-tile nk-1 into slots no one reads
+// again, which keeps every wait count constant; vmcnt(0) drains them at exit.
+namespace g8 {
+constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
+constexpr int HT_BYTES = 128 * BK * 2;    // 16 KiB half-tile: 128 rows x 128 B
+constexpr int BUF_BYTES = 4 * HT_BYTES;   // 64 KiB: A0 A1 B0 B1
+constexpr int LDS_BYTES = 2 * BUF_BYTES;  // 128 KiB
+constexpr int GROUP_M = 4;
+constexpr int HA0 = 0, HA1 = 1, HB0 = 2, HB1 = 3;
+}  // namespace g8
+
+// this wave's 2 pieces (8 rows x 128 B each) of half-tile HT of K-tile kt
+template <int HT>
+__device__ __forceinline__ void g8_issue(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, int K, int m0,
+                                         int n0, int kt, char* buf, int wave, int lane) {
+  using namespace g8;
+  const int rsub = lane >> 3, pc = lane & 7;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = wave * 2 + i;   // piece 0..15
+    const int lr = p * 8 + rsub;  // half-tile row 0..127
+    const int lc = pc ^ ((lr >> 1) & 7);
+    const __bf16* src;
+    if constexpr (HT == HA0 || HT == HA1)
+      src = A + (size_t)(m0 + (lr >> 6) * 128 + (HT == HA1 ? 64 : 0) + (lr & 63)) * K;
+    else
+      src = Bt + (size_t)(n0 + (lr >> 5) * 64 + (HT == HB1 ? 32 : 0) + (lr & 31)) * K;
+    __builtin_amdgcn_global_load_lds(src + kt * BK + lc * 8, (lds_void_ptr)(buf + HT * HT_BYTES + p * 1024), 16, 0, 0);
+  }
+}
+
+// A quadrant fragments: 4 row tiles x 2 k-halves (8 x ds_read_b128)
+__device__ __forceinline__ void g8_read_a(bf16x8 (&a)[4][2], const char* ht, int wm, int lane) {
+  const int fr = lane & 15, fq = lane >> 4, fsw = fr >> 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      a[i][s] = *reinterpret_cast<const bf16x8*>(ht + (wm * 64 + i * 16 + fr) * 128 + (((s * 4 + fq) ^ fsw) << 4));
+}
+
+// B quadrant fragments: 2 col tiles x 2 k-halves (4 x ds_read_b128)
+__device__ __forceinline__ void g8_read_b(bf16x8 (&b)[2][2], const char* ht, int wn, int lane) {
+  const int fr = lane & 15, fq = lane >> 4, fsw = fr >> 1;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      b[j][s] = *reinterpret_cast<const bf16x8*>(ht + (wn * 32 + j * 16 + fr) * 128 + (((s * 4 + fq) ^ fsw) << 4));
+}
+
+template <int N>
+__device__ __forceinline__ void g8_vmwait() {
+  if constexpr (N == 6)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 10)
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else
+    static_assert(N == 6 || N == 8 || N == 10, "vmcnt");
+}
+
+// One phase from the first barrier on: MFMAs of quadrant (MQ, NQ) and the
+// refill of half-tile HT (K-tile kt into buf).  VM_LEAD / VM_LAG are the
+// vmcnt counts of group 0 (end of MFMA segment) and group 1 (end of read
+// segment).  EARLY_LGKM retires this phase's ds_reads before the first
+// barrier (needed when the next phase refills a slot read here); otherwise
+// the compiler's own lgkmcnt waits land between the MFMAs.
+template <int MQ, int NQ, int HT, bool LOAD_IN_M, int VM_LEAD, int VM_LAG, bool EARLY_LGKM>
+__device__ __forceinline__ void g8_phase(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2],
+                                         const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, int K, int m0,
+                                         int n0, int kt, char* buf, int wave, int lane, bool lag, bool skip_last) {
+  if constexpr (!LOAD_IN_M) g8_issue<HT>(A, Bt, K, m0, n0, kt, buf, wave, lane);
+  if constexpr (EARLY_LGKM) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lag) g8_vmwait<VM_LAG>();
+  wg_barrier();
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[MQ * 4 + i][NQ * 2 + j] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s], a[i][s], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+  if constexpr (LOAD_IN_M) {
+    g8_issue<HT>(A, Bt, K, m0, n0, kt, buf, wave, lane);
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one LDS-DMA piece
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+  }
+  __builtin_amdgcn_s_setprio(0);
+  if (!lag) g8_vmwait<VM_LEAD>();
+  if (!skip_last) wg_barrier();
+}
+
+// BAL (balanced reads, 8/4/8/4 ds_read_b128 per phase instead of 12/4/8/0):
+// phase 3 of K-tile t also reads B0 of K-tile t+1 into a second register set
+// (b0n), which phase 0 then takes over.  That read is 5 phases after its
+// issue (4t-2 -> 4t+3), so one fewer half-tile may stay in flight: vmcnt(8),
+// or vmcnt(6) for group 1 with LOAD_IN_M.  B0's slot is now last read 3
+// phases before its refill, so only phase 0 (A0, refilled in phase 1) retires
+// its reads before the first barrier.
+template <bool OUT_F32, bool LOAD_IN_M, bool BAL>
+__global__ __launch_bounds__(g8::NTHR, 2) void gemm_bf16_nt_8p_kernel(const __bf16* __restrict__ A,
+                                                                     const __bf16* __restrict__ Bt,
+                                                                     void* __restrict__ Cv, int M, int N, int K) {
+  using namespace g8;
+  constexpr int VM_LEAD = BAL ? 8 : 10;
+  constexpr int VM_LAG = LOAD_IN_M ? VM_LEAD - 2 : VM_LEAD;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const bool lag = wm == 1;  // wave-uniform
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid % kNumXcd;
+  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
+  const int per_group = GROUP_M * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid % per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  // prologue = the issues the steady state makes in phases -7..-1:
+  // K-tile 0 complete, K-tile 1 without A1 (issued by phase 0)
+  const int k1 = min(1, nk - 1);
+  g8_issue<HA0>(A, Bt, K, m0, n0, 0, smem, wave, lane);
+  g8_issue<HB0>(A, Bt, K, m0, n0, 0, smem, wave, lane);
+  g8_issue<HB1>(A, Bt, K, m0, n0, 0, smem, wave, lane);
+  g8_issue<HA1>(A, Bt, K, m0, n0, 0, smem, wave, lane);
+  g8_issue<HA0>(A, Bt, K, m0, n0, k1, smem + BUF_BYTES, wave, lane);
+  g8_issue<HB0>(A, Bt, K, m0, n0, k1, smem + BUF_BYTES, wave, lane);
+  g8_issue<HB1>(A, Bt, K, m0, n0, k1, smem + BUF_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0, B0 of K-tile 0 landed
+  wg_barrier();
+  if (lag) wg_barrier();
+
+  bf16x8 a[4][2], b0[2][2], b1[2][2], b0n[2][2];
+  if constexpr (BAL) g8_read_b(b0n, smem + HB0 * HT_BYTES, wn, lane);
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * BUF_BYTES;
+    char* nxt = smem + ((t + 1) & 1) * BUF_BYTES;
+    const int kn1 = min(t + 1, nk - 1), kn2 = min(t + 2, nk - 1);
+    g8_read_a(a, cur + HA0 * HT_BYTES, wm, lane);
+    if constexpr (BAL) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) b0[j][s] = b0n[j][s];
+    } else {
+      g8_read_b(b0, cur + HB0 * HT_BYTES, wn, lane);
+    }
+    g8_phase<0, 0, HA1, LOAD_IN_M, VM_LEAD, VM_LAG, true>(acc, a, b0, A, Bt, K, m0, n0, kn1, nxt, wave, lane, lag,
+                                                          false);
+    g8_read_b(b1, cur + HB1 * HT_BYTES, wn, lane);
+    g8_phase<0, 1, HA0, LOAD_IN_M, VM_LEAD, VM_LAG, !BAL>(acc, a, b1, A, Bt, K, m0, n0, kn2, cur, wave, lane, lag,
+                                                          false);
+    g8_read_a(a, cur + HA1 * HT_BYTES, wm, lane);
+    g8_phase<1, 1, HB0, LOAD_IN_M, VM_LEAD, VM_LAG, !BAL>(acc, a, b1, A, Bt, K, m0, n0, kn2, cur, wave, lane, lag,
+                                                          false);
+    if constexpr (BAL) g8_read_b(b0n, nxt + HB0 * HT_BYTES, wn, lane);  // unused past the last K-tile
+    g8_phase<1, 0, HB1, LOAD_IN_M, VM_LEAD, VM_LAG, !BAL>(acc, a, b0, A, Bt, K, m0, n0, kn2, cur, wave, lane, lag,
+                                                          lag && t == nk - 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  const int crow = m0 + wm * 128 + (lane & 15);
+  const int ccol = n0 + wn * 64 + (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const size_t idx = (size_t)(crow + i * 16) * N + ccol + j * 16;
+      if constexpr (OUT_F32) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + idx) = acc[i][j];
+      } else {
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 v = {(__bf16)acc[i][j][0], (__bf16)acc[i][j][1], (__bf16)acc[i][j][2], (__bf16)acc[i][j][3]};
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(Cv) + idx) = v;
+      }
+    }
+}
+
 // ------------------------------------------------- Freivalds check GEMVs ----
 // y[r] = sum_c X[r][c] * v[c]   (X bf16 or f32, row-major, one wave per row)
 template <typename T>
@@ -918,15 +1152,23 @@ AVK_API int avk_vector_add_f32(const float* a, const float* b, float* c, int64_t
   return hipGetLastError();
 }
 
-// Variants (profiles/r1_gemm/kernel_bench_variants.json; 8192^3 random bf16):
-//   0 ring + ping-pong, LDS-DMA issued in the MFMA segment (default)  1327-1356 TF/s
-//   1 2-stage double buffer, one barrier per K-step                   1252-1298
-//   2 4-slot ring without the ping-pong                                1213-1253
-//   3 4 waves x 128x128 (one wave per SIMD)                            1228-1271
-//   4 ring + ping-pong, LDS-DMA issued in the read segment             1312-1338
-//   5 as 0 with a 5-slot (160 KiB) ring                                1310-1328
-// A finer split (two 16-MFMA phases per slice, 4 barriers) measured 1308:
-// not kept.
+// Variants (interleaved A/B on uniform random bf16, one process, same box;
+// profiles/r1_gemm/kernel_bench_8phase.json, 15 rounds each):
+//                                                                   4096^3  8192^3 TF/s
+//   6 8-phase quadrant pipeline, refill in the read segment (DEFAULT) 1323    1367
+//   0 ring + ping-pong, LDS-DMA issued in the MFMA segment            1275    1362
+//   8 as 6 with balanced reads (8/4/8/4 per phase)                    1263    1309
+//   7 / 9 as 6 / 8 with the refill in the MFMA segment                1186    1354 (7)
+//   1 2-stage double buffer, one barrier per K-step                   1183    1275
+//   2 4-slot ring without the ping-pong                               1127    1237
+//   3 4 waves x 128x128 (one wave per SIMD)                           1125    1261
+//   4 ring + ping-pong, LDS-DMA issued in the read segment            1248    1336
+//   5 as 0 with a 5-slot (160 KiB) ring                               1225    1334
+//   hipBLASLt (torch.matmul) on the same operands                     1548    1672
+// A finer split of the ring (two 16-MFMA phases per slice, 4 barriers)
+// measured 1308 at 8192^3: not kept.
+constexpr int kDefaultGemmVariant = 6;
+
 AVK_API int avk_vector_add_verify_f32(const float* a, const float* b, const float* c, int64_t n,
                                       unsigned long long* bad_dev, hipStream_t s) {
   if (!a || !b || !c || !bad_dev || n <= 0) return hipErrorInvalidValue;
@@ -970,6 +1212,16 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
       if (out_f32) gemm_bf16_nt_pp_kernel<true, true, 5><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
       else gemm_bf16_nt_pp_kernel<false, true, 5><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
       break;
+#define AVK_G8(V, LIM, BAL)                                                                       \
+    case V:                                                                                     \
+      if (out_f32) gemm_bf16_nt_8p_kernel<true, LIM, BAL><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K); \
+      else gemm_bf16_nt_8p_kernel<false, LIM, BAL><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K);        \
+      break;
+    AVK_G8(6, false, false)
+    AVK_G8(7, true, false)
+    AVK_G8(8, false, true)
+    AVK_G8(9, true, true)
+#undef AVK_G8
     default:
       return hipErrorInvalidValue;
   }
@@ -978,7 +1230,7 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
 
 AVK_API int avk_gemm_bf16_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K,
                              hipStream_t s) {
-  return avk_gemm_bf16_nt_variant(A, Bt, C, out_f32, M, N, K, 0, s);
+  return avk_gemm_bf16_nt_variant(A, Bt, C, out_f32, M, N, K, kDefaultGemmVariant, s);
 }
 
 // y = X v ; X is [R][C] row-major (bf16 when x_is_bf16, else f32); C % 8 == 0

@@ -30,12 +30,15 @@ def time_ms(fn, iters):
     return s.elapsed_time(e) / iters
 
 
-GEMM_VARIANTS = {0: "default", 1: "dbuf", 2: "ring", 3: "w4", 4: "pp_load_in_r", 5: "pp_5slot"}
+GEMM_VARIANTS = {6: "default_8phase", 0: "ring_pingpong", 1: "dbuf", 2: "ring", 3: "w4", 4: "pp_load_in_r", 5: "pp_5slot",
+                 7: "8phase_load_in_m", 8: "8phase_bal_load_in_r", 9: "8phase_bal_load_in_m"}
 
 
-def bench_gemm(n, rounds, iters):
-    """Every K2 variant and hipBLASLt, interleaved round by round on the same
-    random operands (cdna_hip_programming.md §5.4 rules 24-25)."""
+def bench_gemm(n, rounds, iters, variants=None):
+    """Every K2 variant (or the ``variants`` subset) and hipBLASLt, interleaved
+    round by round on the same random operands (cdna_hip_programming.md §5.4
+    rules 24-25)."""
+    sel = {v: GEMM_VARIANTS[v] for v in (variants if variants is not None else GEMM_VARIANTS)}
     a = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
     bt = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
     K.fill_uniform_(a, 1)
@@ -43,23 +46,23 @@ def bench_gemm(n, rounds, iters):
     c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
     c2 = torch.empty_like(c)
     b = bt.t()
-    times = {v: [] for v in GEMM_VARIANTS}
+    times = {v: [] for v in sel}
     lib = []
     for _ in range(3):
-        for v in GEMM_VARIANTS:
+        for v in sel:
             K.gemm_bf16_nt(a, bt, out=c, variant=v)
         torch.matmul(a, b, out=c2)
     for _ in range(rounds):
-        for v in GEMM_VARIANTS:
+        for v in sel:
             times[v].append(time_ms(lambda: K.gemm_bf16_nt(a, bt, out=c, variant=v), iters))
         lib.append(time_ms(lambda: torch.matmul(a, b, out=c2), iters))
     fl = 2.0 * n ** 3
     K.gemm_bf16_nt(a, bt, out=c)
     err = (c.float() - c2.float()).abs().max().item()
     out = {"n": n}
-    for v, name in GEMM_VARIANTS.items():
+    for v, name in sel.items():
         out[f"{name}_tflops"] = fl / statistics.median(times[v]) / 1e9
-    ours = times[0]
+    ours = times[next(iter(sel))]
     out.update({
         "ours_ms_median": statistics.median(ours),
         "ours_tflops": fl / statistics.median(ours) / 1e9,
@@ -116,10 +119,15 @@ def bench_oneshot(n, peers, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--gemm-variants", type=int, nargs="+", default=None,
+                    help="GEMM A/B only: these variants (the first is reported as ours) vs hipBLASLt")
+    ap.add_argument("--rounds", type=int, default=5)
     args = ap.parse_args()
     t0 = time.time()
     out = {"device": torch.cuda.get_device_name(0)}
-    if args.quick:
+    if args.gemm_variants:
+        out["gemm"] = [bench_gemm(n, args.rounds, 10, args.gemm_variants) for n in (4096, 8192)]
+    elif args.quick:
         out["gemm"] = [bench_gemm(4096, 2, 5)]
         out["hbm"] = bench_hbm(1 << 30, 2, 5)
     else:
