@@ -120,6 +120,17 @@ def validate_driver(env: NodeEnv, timeout: float = 600.0, stop=None) -> dict:
             time.sleep(env.poll_s)
 
 
+def gate_env() -> dict:
+    """Environment of a counter-gated validator process: the N7 tool library
+    and its four-counter definitions.  Both must be in place before the
+    process starts (the SDK loads with the HIP runtime and must see ONE
+    counter set: a definition path changed after it loaded leaves the
+    dispatch records unnamed and the gate fails closed)."""
+    return {"AMDGPU_VALIDATOR_COUNTERS": "1",
+            "ROCP_TOOL_LIBRARIES": str(native.artefact("libamdgpu_counter_gate.so")),
+            "ROCPROFILER_METRICS_PATH": str(native.artefact("gate-metrics"))}
+
+
 def workload_argv(args: list[str], rank: int, world: int, rendezvous: str, run_id: str, device: int) -> list[str]:
     return [str(native.binary("amdgpu-validator")), "--device", str(device), "--rank", str(rank), "--world",
             str(world), "--rendezvous", rendezvous, "--run-id", run_id, *args]
@@ -143,9 +154,7 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     os.makedirs(rdv, exist_ok=True)
     # N7: the counter gate is a rocprofiler-sdk tool library loaded only into
     # the gated kernel processes (the binary does not link the SDK)
-    counter_env = ({"AMDGPU_VALIDATOR_COUNTERS": "1",
-                    "ROCP_TOOL_LIBRARIES": str(native.artefact("libamdgpu_counter_gate.so"))}
-                   if "--counter-gate" in args else {})
+    counter_env = gate_env() if "--counter-gate" in args else {}
     steps = _steps_of(args)
     kernel_steps = [s for s in steps if s != "rccl"]
     # RCCL runs in its own process per GPU, concurrently with the kernel
@@ -333,6 +342,8 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
         try:
             if wait_toolkit:
                 wait_ready(env, "toolkit", timeout, stop)
+            if os.environ.get("AMDGPU_EXPERIMENT_PLUGIN_AFTER_WORKLOAD"):  # start-up contention experiment
+                wait_ready(env, "workload", timeout, stop)
             if read_ready(env, "plugin") is None:
                 results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop)
         except Exception as e:  # noqa: BLE001

@@ -19,22 +19,41 @@
 #include <rocprofiler-sdk/rocprofiler.h>
 
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #define GATE_API extern "C" __attribute__((visibility("default")))
 
+// Start-up cost (validator process with the gate, profiles/r1_bench): the
+// kernel-symbol tracing that maps kernel ids to names made rocprofiler-sdk
+// walk every code object the process loads, and building the counter config
+// (iterate + query every counter the agent supports) sat inside the gated
+// dispatch.  Now the dispatch is identified by arming: the validator arms the
+// gate, enqueues ONE GEMM on its only stream and waits for it, so the first
+// dispatch seen while armed is that GEMM (one-shot arm; the name filter still
+// applies when AMDGPU_GATE_KERNEL_NAMES=1 turns symbol tracing back on).  The
+// per-agent counter configs are built on a helper thread started by
+// tool_init, while the runtime finishes its own start-up and the validator
+// runs its earlier steps; a dispatch that needs a config before the thread
+// is done waits for it.
+
 namespace {
+
+using Clock = std::chrono::steady_clock;
 
 const char* kCounters[] = {"SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"};
 
 std::mutex g_mu;
 std::atomic<bool> g_active{false};
 std::atomic<bool> g_armed{false};
+bool g_trace_names = false;
 std::string g_filter;
 std::map<uint64_t, std::string> g_kernel_names;                 // kernel_id -> name
 std::map<uint64_t, rocprofiler_counter_config_id_t> g_configs;  // agent handle -> config
@@ -42,6 +61,13 @@ std::map<uint64_t, std::string> g_counter_names;                // counter id ->
 std::map<std::string, double> g_values;
 int g_dispatches = 0;
 rocprofiler_context_id_t g_ctx{};
+
+// helper-thread state (configs for every GPU agent)
+std::mutex g_cfg_mu;
+std::condition_variable g_cfg_cv;
+bool g_cfg_done = false;
+double g_cfg_seconds = -1.0;
+std::thread g_cfg_thread;
 
 void code_object_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_user_data_t*, void*) {
   if (record.kind == ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT &&
@@ -55,6 +81,7 @@ void code_object_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_us
 
 struct CounterSearch {
   std::vector<rocprofiler_counter_id_t> found;
+  std::map<uint64_t, std::string> names;
 };
 
 rocprofiler_status_t collect_counters(rocprofiler_agent_id_t, rocprofiler_counter_id_t* counters, size_t n, void* ud) {
@@ -66,32 +93,81 @@ rocprofiler_status_t collect_counters(rocprofiler_agent_id_t, rocprofiler_counte
     for (const char* want : kCounters) {
       if (info.name && strcmp(info.name, want) == 0) {
         s->found.push_back(counters[i]);
-        g_counter_names[counters[i].handle] = want;
+        s->names[counters[i].handle] = want;
       }
     }
   }
   return ROCPROFILER_STATUS_SUCCESS;
 }
 
+rocprofiler_counter_config_id_t make_config(rocprofiler_agent_id_t agent) {
+  CounterSearch s;
+  rocprofiler_iterate_agent_supported_counters(agent, collect_counters, &s);
+  rocprofiler_counter_config_id_t cfg{};
+  if (s.found.empty() ||
+      rocprofiler_create_counter_config(agent, s.found.data(), s.found.size(), &cfg) != ROCPROFILER_STATUS_SUCCESS)
+    cfg.handle = 0;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_counter_names.insert(s.names.begin(), s.names.end());
+  return cfg;
+}
+
+rocprofiler_status_t gpu_agents(rocprofiler_agent_version_t, const void** agents, size_t n, void* ud) {
+  auto* out = static_cast<std::vector<rocprofiler_agent_id_t>*>(ud);
+  for (size_t i = 0; i < n; ++i) {
+    const auto* a = static_cast<const rocprofiler_agent_v0_t*>(agents[i]);
+    if (a->type == ROCPROFILER_AGENT_TYPE_GPU) out->push_back(a->id);
+  }
+  return ROCPROFILER_STATUS_SUCCESS;
+}
+
+void build_configs() {
+  const auto t0 = Clock::now();
+  std::vector<rocprofiler_agent_id_t> agents;
+  rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, gpu_agents, sizeof(rocprofiler_agent_v0_t),
+                                     &agents);
+  std::map<uint64_t, rocprofiler_counter_config_id_t> built;
+  for (auto ag : agents) built[ag.handle] = make_config(ag);
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto& kv : built) g_configs.emplace(kv.first, kv.second);
+  }
+  std::lock_guard<std::mutex> lk(g_cfg_mu);
+  g_cfg_seconds = std::chrono::duration<double>(Clock::now() - t0).count();
+  g_cfg_done = true;
+  g_cfg_cv.notify_all();
+}
+
+void wait_configs() {
+  std::unique_lock<std::mutex> lk(g_cfg_mu);
+  g_cfg_cv.wait_for(lk, std::chrono::seconds(5), [] { return g_cfg_done; });
+}
+
 void dispatch_cb(rocprofiler_dispatch_counting_service_data_t data, rocprofiler_counter_config_id_t* config,
                  rocprofiler_user_data_t*, void*) {
   if (!g_armed.load()) return;
-  std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_kernel_names.find(data.dispatch_info.kernel_id);
-  if (!g_filter.empty() && (it == g_kernel_names.end() || it->second.find(g_filter) == std::string::npos)) return;
-  const uint64_t agent = data.dispatch_info.agent_id.handle;
-  auto cit = g_configs.find(agent);
-  if (cit == g_configs.end()) {
-    CounterSearch s;
-    rocprofiler_iterate_agent_supported_counters(data.dispatch_info.agent_id, collect_counters, &s);
-    rocprofiler_counter_config_id_t cfg{};
-    if (s.found.empty() ||
-        rocprofiler_create_counter_config(data.dispatch_info.agent_id, s.found.data(), s.found.size(), &cfg) !=
-            ROCPROFILER_STATUS_SUCCESS)
-      cfg.handle = 0;
-    cit = g_configs.emplace(agent, cfg).first;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_trace_names && !g_filter.empty()) {
+      auto it = g_kernel_names.find(data.dispatch_info.kernel_id);
+      if (it == g_kernel_names.end() || it->second.find(g_filter) == std::string::npos) return;
+    }
   }
-  if (cit->second.handle) *config = cit->second;
+  if (!g_armed.exchange(false)) return;  // one-shot: the first dispatch after arm
+  wait_configs();
+  const uint64_t agent = data.dispatch_info.agent_id.handle;
+  rocprofiler_counter_config_id_t cfg{};
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto cit = g_configs.find(agent);
+    if (cit != g_configs.end()) cfg = cit->second;
+  }
+  if (!cfg.handle) {  // agent the helper did not see: build it here
+    cfg = make_config(data.dispatch_info.agent_id);
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_configs[agent] = cfg;
+  }
+  if (cfg.handle) *config = cfg;
 }
 
 void record_cb(rocprofiler_dispatch_counting_service_data_t, rocprofiler_counter_record_t* recs, size_t n,
@@ -106,19 +182,35 @@ void record_cb(rocprofiler_dispatch_counting_service_data_t, rocprofiler_counter
   }
 }
 
+bool env_is(const char* name, const char* val) {
+  const char* e = getenv(name);
+  return e && strcmp(e, val) == 0;
+}
+
 int tool_init(rocprofiler_client_finalize_t, void*) {
   if (rocprofiler_create_context(&g_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
-  rocprofiler_configure_callback_tracing_service(g_ctx, ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT, nullptr, 0,
-                                                 code_object_cb, nullptr);
+  g_trace_names = env_is("AMDGPU_GATE_KERNEL_NAMES", "1");
+  if (g_trace_names)
+    rocprofiler_configure_callback_tracing_service(g_ctx, ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT, nullptr, 0,
+                                                   code_object_cb, nullptr);
   if (rocprofiler_configure_callback_dispatch_counting_service(g_ctx, dispatch_cb, nullptr, record_cb, nullptr) !=
       ROCPROFILER_STATUS_SUCCESS)
     return -1;
   if (rocprofiler_start_context(g_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
+  if (env_is("AMDGPU_GATE_LAZY_CONFIG", "1")) {
+    std::lock_guard<std::mutex> lk(g_cfg_mu);
+    g_cfg_done = true;  // dispatch_cb builds the config itself
+  } else {
+    g_cfg_thread = std::thread(build_configs);
+  }
   g_active = true;
   return 0;
 }
 
-void tool_fini(void*) { g_active = false; }
+void tool_fini(void*) {
+  g_active = false;
+  if (g_cfg_thread.joinable()) g_cfg_thread.join();
+}
 
 rocprofiler_tool_configure_result_t g_cfg = {sizeof(rocprofiler_tool_configure_result_t), tool_init, tool_fini, nullptr};
 
@@ -154,4 +246,10 @@ GATE_API double avk_prof_value(const char* counter) {
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_values.find(counter ? counter : "");
   return it == g_values.end() ? -1.0 : it->second;
+}
+
+// seconds the helper thread took to build the counter configs (-1: not run)
+GATE_API double avk_prof_config_seconds() {
+  std::lock_guard<std::mutex> lk(g_cfg_mu);
+  return g_cfg_seconds;
 }

@@ -98,19 +98,29 @@ struct Gate {
   void (*disarm)() = nullptr;
   int (*dispatches)() = nullptr;
   double (*value)(const char*) = nullptr;
+  double (*config_seconds)() = nullptr;  // optional
 
-  static std::string default_path() {
+  static std::string exe_dir() {
     char buf[4096];
     const ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
-    if (n <= 0) return "libamdgpu_counter_gate.so";
+    if (n <= 0) return "";
     buf[n] = 0;
     std::string exe(buf);
-    return exe.substr(0, exe.rfind('/') + 1) + "libamdgpu_counter_gate.so";
+    return exe.substr(0, exe.rfind('/') + 1);
   }
-  // before the first HIP call: ask rocprofiler-sdk to load the tool
+  static std::string default_path() { return exe_dir() + "libamdgpu_counter_gate.so"; }
+  // before the first HIP call: ask rocprofiler-sdk to load the tool, with the
+  // gate's four-counter definitions (the SDK's full counter_defs.yaml parse
+  // costs its config set-up ~0.05 s, tools/gate_startup.py).  A caller that
+  // names the tool itself (validate.py gate_env) has the SDK loading with the
+  // runtime, before main: then its environment is left exactly as given -
+  // switching the definition path under a loaded SDK leaves the dispatch
+  // records unnamed and the gate fails closed.
   static void request() {
     const char* e = getenv("AMDGPU_VALIDATOR_COUNTERS");
     if (!e || strcmp(e, "1") != 0 || getenv("ROCP_TOOL_LIBRARIES")) return;
+    const std::string metrics = exe_dir() + "gate-metrics";
+    if (access((metrics + "/counter_defs.yaml").c_str(), R_OK) == 0) setenv("ROCPROFILER_METRICS_PATH", metrics.c_str(), 0);
     setenv("ROCP_TOOL_LIBRARIES", default_path().c_str(), 0);
   }
   bool resolve() {
@@ -130,6 +140,7 @@ struct Gate {
     disarm = reinterpret_cast<void (*)()>(dlsym(h, "avk_prof_disarm"));
     dispatches = reinterpret_cast<int (*)()>(dlsym(h, "avk_prof_dispatches"));
     value = reinterpret_cast<double (*)(const char*)>(dlsym(h, "avk_prof_value"));
+    config_seconds = reinterpret_cast<double (*)()>(dlsym(h, "avk_prof_config_seconds"));
     return active && arm && disarm && dispatches && value;
   }
   bool usable() { return (active || resolve()) && active(); }
@@ -327,6 +338,7 @@ Step step_gemm(const Args& a, hipStream_t st) {
   // counter gate on one extra dispatch: counter collection serialises
   // dispatches, so it must not overlap the timed ones
   const bool gate = a.counter_gate && g_gate.usable();
+  const auto tg = Clock::now();
   if (gate) {
     g_gate.arm("gemm_bf16_nt");
     AVK_OK(avk_gemm_bf16_nt(A, B, C16, 0, n, n, n, st));
@@ -359,8 +371,9 @@ Step step_gemm(const Args& a, hipStream_t st) {
       gate_ok = disp > 0 && mops > 0 && busy > 0;
       gate_json = fmt("\"counter_gate\": \"%s\", \"dispatches\": %d, \"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.6g, "
                       "\"SQ_VALU_MFMA_BUSY_CYCLES\": %.6g, \"SQ_WAVES\": %.6g, \"GRBM_GUI_ACTIVE\": %.6g, "
-                      "\"flop_per_mop\": %.6g",
-                      gate_ok ? "pass" : "fail", disp, mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0);
+                      "\"flop_per_mop\": %.6g, \"gate_seconds\": %.4f, \"gate_config_seconds\": %.4f",
+                      gate_ok ? "pass" : "fail", disp, mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0,
+                      secs(tg), g_gate.config_seconds ? g_gate.config_seconds() : -1.0);
     }
   }
   (void)hipEventDestroy(e0);

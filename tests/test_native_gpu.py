@@ -39,11 +39,30 @@ def test_validator_all_local_steps_with_counter_gate(tmp_path):
 
 def test_validator_counter_gate_tool_library_from_env(tmp_path):
     # the operator's path: the tool library is named explicitly (validate.py)
+    from amdgpu_operator.validator.validate import gate_env
+
     rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--gemm", "1024", "--counter-gate"],
-                   {"AMDGPU_VALIDATOR_COUNTERS": "1",
-                    "ROCP_TOOL_LIBRARIES": str(native.artefact("libamdgpu_counter_gate.so"))})
+                   gate_env())
+    assert rc == 0 and rep["ok"], rep
+    g = {s["name"]: s for s in rep["steps"]}["gemm"]
+    assert g["counter_gate"] == "pass" and g["dispatches"] == 1 and g["flop_per_mop"] == 512
+
+
+def test_validator_counter_gate_sdk_definitions(tmp_path):
+    # the tool named by the caller with the SDK's own full counter set: the
+    # gate must work with either definition file, as long as it is one set
+    env = {**gate_env_full(), "AMDGPU_GATE_KERNEL_NAMES": "1"}
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--gemm", "1024", "--counter-gate"], env)
     assert rc == 0 and rep["ok"], rep
     assert {s["name"]: s for s in rep["steps"]}["gemm"]["counter_gate"] == "pass"
+
+
+def gate_env_full():
+    from amdgpu_operator.validator.validate import gate_env
+
+    env = gate_env()
+    env.pop("ROCPROFILER_METRICS_PATH")
+    return env
 
 
 def test_validator_counter_gate_unavailable_fails_closed(tmp_path):
