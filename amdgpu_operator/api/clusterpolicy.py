@@ -72,6 +72,7 @@ class DriverSpec(Operand):
     usePrecompiled: bool = False
     blacklistAmdgpuInbox: bool = True
     kernelModuleParams: dict[str, str] = Field(default_factory=dict)
+    repository: str = ""  # package mirror for air-gapped clusters (default repo.radeon.com)
     startupProbeTimeoutSeconds: int = 600
     upgradePolicy: UpgradePolicy = Field(default_factory=UpgradePolicy)
 

@@ -180,8 +180,9 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     env = [{"name": "ROCM_VERSION", "value": d.rocmVersion}, {"name": "AMDGPU_DRIVER_VERSION", "value": d.driverVersion},
            {"name": "AMDGPU_USE_PRECOMPILED", "value": str(d.usePrecompiled).lower()},
            {"name": "AMDGPU_BLACKLIST_INBOX", "value": str(d.blacklistAmdgpuInbox).lower()},
-           {"name": "AMDGPU_MODULE_PARAMS", "value": " ".join(f"{k}={v}" for k, v in sorted(d.kernelModuleParams.items()))}
-           ] + list(d.env)
+           {"name": "AMDGPU_MODULE_PARAMS", "value": " ".join(f"{k}={v}" for k, v in sorted(d.kernelModuleParams.items()))},
+           {"name": "AMDGPU_WAIT_SECONDS", "value": str(d.startupProbeTimeoutSeconds)}
+           ] + ([{"name": "AMDGPU_REPO_BASE", "value": d.repository}] if d.repository else []) + list(d.env)
     mounts = [_mount("run-amd", "/run/amd", propagation="Bidirectional"), _mount("host-root", "/host", ro=True,
                                                                                  propagation="HostToContainer"),
               _mount("lib-modules", "/lib/modules"), _mount("dev", "/dev"), _mount("host-sys", "/host/sys", ro=True),

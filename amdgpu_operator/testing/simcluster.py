@@ -27,7 +27,9 @@ from __future__ import annotations
 import hashlib
 import json
 import os
+import shutil
 import shlex
+import tempfile
 import threading
 import time
 import uuid
@@ -206,8 +208,21 @@ class SimCluster:
         self.reconciler: ClusterPolicyReconciler | None = None
         self.events: list[tuple[float, str, str]] = []
         self._node_specs = nodes
+        self._short_dirs: list[str] = []
 
     # -------------------------------------------------------------- setup
+    # a unix socket path must fit sockaddr_un.sun_path (108 bytes); the node's
+    # own directory can be deeper (pytest-xdist temp dirs), so its sockets
+    # then live in a short private directory removed by stop()
+    SOCKET_PATH_BUDGET = 40
+
+    def _socket_dir(self, node_dir: str) -> str:
+        if len(node_dir) <= self.SOCKET_PATH_BUDGET:
+            return node_dir
+        d = tempfile.mkdtemp(prefix="amdgpu-sock-")
+        self._short_dirs.append(d)
+        return d
+
     def _make_node(self, ns: NodeSpec) -> SimNode:
         d = os.path.join(self.workdir, ns.name)
         os.makedirs(d, exist_ok=True)
@@ -221,8 +236,9 @@ class SimCluster:
                 fakesys._w(os.path.join(root, "sys/bus/pci/devices/0000:00:01.0/class"), "0x060000\n")
         else:
             root = ns.sysfs_root
-        dp_dir = os.path.join(d, "device-plugins")
-        podres = os.path.join(d, "pod-resources", "kubelet.sock")
+        sockets = self._socket_dir(d)
+        dp_dir = os.path.join(sockets, "device-plugins")
+        podres = os.path.join(sockets, "pod-resources", "kubelet.sock")
         kubelet = FakeKubelet(dp_dir, podres)
         env = NodeEnv(node_name=ns.name, client=self.client, host_root=root,
                       validations_dir=os.path.join(d, "validations"), device_plugin_dir=dp_dir,
@@ -304,6 +320,8 @@ class SimCluster:
             node.kubelet.stop()
         for th in self._threads:
             th.join(timeout=5)
+        for d in self._short_dirs:
+            shutil.rmtree(d, ignore_errors=True)
 
     # --------------------------------------------------- DaemonSet controller
     @staticmethod
