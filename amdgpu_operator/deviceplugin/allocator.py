@@ -14,7 +14,8 @@ minimises a communication cost built from the KFD link table:
 * spreading over NUMA nodes adds a penalty per extra node.
 
 Exact search for small candidate sets (≤ 5,000 subsets); otherwise greedy
-growth from every seed device, keeping the cheapest result.  Ties break on
+growth from one seed per (physical GPU, NUMA node), keeping the cheapest
+result.  Ties break on
 device order so the answer is deterministic (kubelet retries are stable).
 """
 
@@ -42,6 +43,14 @@ class TopologyCost:
         self.devices = {d.id: d for d in devices}
         self.order = {d.id: i for i, d in enumerate(devices)}
         self.pair_weight = pair_weight
+        self._matrix: list[list[int]] | None = None
+
+    def matrix(self) -> list[list[int]]:
+        """Pair costs of every device pair, indexed by device order (built once)."""
+        if self._matrix is None:
+            ids = list(self.order)
+            self._matrix = [[self.pair(a, b) if a != b else 0 for b in ids] for a in ids]
+        return self._matrix
 
     def pair(self, a: str, b: str) -> int:
         da, db = self.devices[a], self.devices[b]
@@ -70,34 +79,80 @@ class TopologyCost:
 
 
 def preferred(cost: TopologyCost, available: list[str], must_include: list[str], size: int) -> list[str]:
-    avail = [d for d in available if d in cost.devices]
-    must = [d for d in must_include if d in cost.devices]
+    """Cheapest ``size``-subset of ``available`` containing ``must_include``.
+
+    The pair costs of the candidates are tabulated once per call (n <= 64
+    partitions: 4 K entries), so the exact search and the greedy growth index
+    lists instead of re-deriving link weights; greedy seeds one device per
+    (physical GPU, NUMA node), since partitions of one GPU are interchangeable
+    under the cost model, and keeps each candidate's summed cost to the
+    selection up to date as the selection grows (O(size x n) per seed).
+    """
+    must = list(dict.fromkeys(d for d in must_include if d in cost.devices))
     if size <= 0:
         return []
     if len(must) >= size:
         return sorted(must, key=lambda d: cost.order[d])[:size]
-    pool = [d for d in avail if d not in must]
+    must_set = set(must)
+    pool = [d for d in dict.fromkeys(available) if d in cost.devices and d not in must_set]
     need = size - len(must)
     if need > len(pool):
         return sorted(must + pool, key=lambda d: cost.order[d])
     pool.sort(key=lambda d: cost.order[d])
 
-    if comb(len(pool), need) <= EXACT_LIMIT:
-        best = min((list(c) for c in itertools.combinations(pool, need)), key=lambda c: cost.key(must + c))
-        return sorted(must + best, key=lambda d: cost.order[d])
+    ids = must + pool
+    n, m = len(ids), len(must)
+    full = cost.matrix()
+    g = [cost.order[d] for d in ids]
+    w = [[full[a][b] for b in g] for a in g]
+    numa = [cost.devices[d].numa for d in ids]
+    phys = [cost.devices[d].physical for d in ids]
+    rank = [cost.order[d] for d in ids]
 
-    best_sel = None
-    seeds = pool if not must else [None]
+    def key(sel) -> tuple:  # == cost.key on the selected ids
+        c = 0
+        for x in range(len(sel)):
+            row = w[sel[x]]
+            for y in range(x + 1, len(sel)):
+                c += row[sel[y]]
+        nodes = {numa[i] for i in sel if numa[i] >= 0}
+        c += NUMA_SPREAD_PENALTY * max(0, len(nodes) - 1) + len({phys[i] for i in sel}) - 1
+        return c, sorted(rank[i] for i in sel)
+
+    base = list(range(m))
+    if comb(n - m, need) <= EXACT_LIMIT:
+        best = min((base + list(c) for c in itertools.combinations(range(m, n), need)), key=key)
+        return sorted((ids[i] for i in best), key=lambda d: cost.order[d])
+
+    if m:
+        seeds: list[int | None] = [None]
+    else:
+        seen, seeds = set(), []
+        for i in range(n):
+            if (phys[i], numa[i]) not in seen:
+                seen.add((phys[i], numa[i]))
+                seeds.append(i)
+    best_sel, best_key = None, None
     for seed in seeds:
-        sel = list(must) + ([seed] if seed is not None else [])
-        rest = [d for d in pool if d not in sel]
+        sel = base + ([seed] if seed is not None else [])
+        acc = [0] * n
+        taken = [False] * n
+        for s_ in sel:
+            taken[s_] = True
+            row = w[s_]
+            for i in range(n):
+                acc[i] += row[i]
         while len(sel) < size:
-            nxt = min(rest, key=lambda d: (sum(cost.pair(d, s) for s in sel), cost.order[d]))
+            nxt = min((i for i in range(n) if not taken[i]), key=lambda i: (acc[i], rank[i]))
             sel.append(nxt)
-            rest.remove(nxt)
-        if best_sel is None or cost.key(sel) < cost.key(best_sel):
-            best_sel = sel
-    return sorted(best_sel, key=lambda d: cost.order[d])
+            taken[nxt] = True
+            row = w[nxt]
+            for i in range(n):
+                acc[i] += row[i]
+        k = key(sel)
+        if best_key is None or k < best_key:
+            best_sel, best_key = sel, k
+    return sorted((ids[i] for i in best_sel), key=lambda d: cost.order[d])
 
 
 def from_topology(gpus, links, id_of) -> TopologyCost:

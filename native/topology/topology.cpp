@@ -9,7 +9,9 @@
 //   sys/module/amdgpu/initstate, dev/kfd, dev/dri/renderD<minor>
 
 #include <dirent.h>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -31,12 +33,23 @@ std::string join(const char* root, const std::string& rel) {
   return r + rel;
 }
 
+// sysfs attributes are small: one open + read(2) + close, no iostreams (a
+// CPX node has ~4 K io_link property files; stream set-up dominated the scan)
 bool read_file(const std::string& path, std::string* out) {
-  std::ifstream f(path);
-  if (!f) return false;
-  std::stringstream ss;
-  ss << f.rdbuf();
-  *out = ss.str();
+  const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return false;
+  out->clear();
+  char buf[4096];
+  for (;;) {
+    const ssize_t n = read(fd, buf, sizeof(buf));
+    if (n < 0) {
+      close(fd);
+      return false;
+    }
+    if (n == 0) break;
+    out->append(buf, (size_t)n);
+  }
+  close(fd);
   return true;
 }
 
@@ -53,13 +66,20 @@ Props read_props(const std::string& path) {
   Props p;
   std::string text;
   if (!read_file(path, &text)) return p;
-  std::istringstream is(text);
-  std::string line;
-  while (std::getline(is, line)) {
-    std::istringstream ls(line);
-    std::string key;
-    unsigned long long v = 0;
-    if (ls >> key >> v) p[key] = v;
+  // "key value\n" lines; a line whose value does not parse is skipped
+  const char* c = text.c_str();
+  const char* end = c + text.size();
+  while (c < end) {
+    const char* eol = static_cast<const char*>(memchr(c, '\n', (size_t)(end - c)));
+    if (!eol) eol = end;
+    const char* k = c;
+    while (k < eol && (*k == ' ' || *k == '\t')) ++k;
+    const char* ke = k;
+    while (ke < eol && *ke != ' ' && *ke != '\t') ++ke;
+    const char* v = ke;
+    while (v < eol && (*v == ' ' || *v == '\t')) ++v;
+    if (ke > k && v < eol && *v >= '0' && *v <= '9') p[std::string(k, ke)] = strtoull(v, nullptr, 10);
+    c = eol + 1;
   }
   return p;
 }
