@@ -52,6 +52,9 @@ def _lib() -> ctypes.CDLL:
         "avk_max_abs_diff_f32": ([P, P, I64, P, S], I),
         "avk_allreduce_oneshot_f32": ([ctypes.POINTER(P), I, P, I64, S], I),
         "avk_allreduce_twoshot_f32": ([ctypes.POINTER(P), ctypes.POINTER(P), I, I, I64, S], I),
+        "avk_mfma_probe_count": ([], I),
+        "avk_mfma_probe_name": ([I], ctypes.c_char_p),
+        "avk_mfma_probe": ([I, U64, ctypes.POINTER(I), S], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -264,6 +267,18 @@ def allreduce_twoshot_slice(in_ptrs, out_ptrs, rank: int, count: int, stream=Non
         raise ValueError("bad peer tables")
     _check(_lib().avk_allreduce_twoshot_f32(_ptr_array([int(p) for p in in_ptrs]), _ptr_array([int(p) for p in out_ptrs]),
                                             len(in_ptrs), rank, count, _stream(stream)), "allreduce_twoshot")
+
+
+def mfma_probe(seed: int = 1, stream=None) -> dict[str, int]:
+    """K5: one MFMA tile per CDNA4 matrix data type, checked exactly against an
+    integer reference; returns ``{dtype: mismatching outputs}`` (0 = works)."""
+    lib = _lib()
+    out = {}
+    for kind in range(lib.avk_mfma_probe_count()):
+        bad = ctypes.c_int(-1)
+        _check(lib.avk_mfma_probe(kind, seed & ((1 << 64) - 1), ctypes.byref(bad), _stream(stream)), "mfma_probe")
+        out[lib.avk_mfma_probe_name(kind).decode()] = bad.value
+    return out
 
 
 @dataclass

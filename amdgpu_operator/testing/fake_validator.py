@@ -19,7 +19,7 @@ def main(argv: list[str]) -> int:
 
     rank, world = int(arg("--rank", "0")), int(arg("--world", "1"))
     rdv, run_id = arg("--rendezvous", "/tmp/amdgpu-validator"), arg("--run-id", "run")
-    steps = arg("--steps", "hip,vecadd,gemm,hbm,xgmi,rccl").split(",")
+    steps = arg("--steps", "hip,vecadd,gemm,mfma,hbm,xgmi,rccl").split(",")
     t0 = time.perf_counter()
     os.makedirs(rdv, exist_ok=True)
     if "rccl" in steps and world > 1:  # barrier like the RCCL unique-id exchange

@@ -73,7 +73,7 @@ def fake_validator_result(argv: list[str]) -> ProcResult:
     def arg(name, default):
         return argv[argv.index(name) + 1] if name in argv else default
 
-    steps = arg("--steps", "hip,vecadd,gemm,hbm,xgmi,rccl").split(",")
+    steps = arg("--steps", "hip,vecadd,gemm,mfma,hbm,xgmi,rccl").split(",")
     rep = {"ok": True, "simulated": True, "rank": int(arg("--rank", "0")), "world": int(arg("--world", "1")),
            "device": int(arg("--device", "0")), "seconds": 0.0,
            "steps": [{"name": s, "ok": True, "seconds": 0.0, "simulated": True} for s in steps]}

@@ -9,8 +9,9 @@ step                what it checks                                         ready
 driver              N1 probe: amdgpu live, /dev/kfd, KFD GPU nodes, render  driver-ready
 toolkit             toolkit installed (CDI spec + runtime config)           toolkit-ready
 workload            one native ``amdgpu-validator`` process per GPU: HIP    workload-ready
-                    vectorAdd, MFMA GEMM + counter gate, HBM, xGMI one-shot
-                    all-reduce, RCCL all-reduce across ALL GPUs over xGMI
+                    vectorAdd, MFMA GEMM + counter gate, one exact MFMA tile
+                    per CDNA4 data type, HBM, xGMI one-shot all-reduce,
+                    RCCL all-reduce across ALL GPUs over xGMI
 plugin              node Allocatable ``amd.com/gpu`` == GPUs found, then    plugin-ready
                     one pod per GPU requesting ``amd.com/gpu: 1`` (device
                     plugin Allocate -> OCI hook -> HIP workload) Succeeded
@@ -45,6 +46,7 @@ READY_FILES = {
     "complete": "validated",
 }
 VALIDATED_LABEL = "amd.com/gpu.validated"
+MFMA_LABEL = "amd.com/gpu.validated.mfma"  # data types whose MFMA tile checked out on every GPU
 WORKLOAD_POD_LABEL = "amd.com/validator-workload"
 
 
@@ -209,7 +211,7 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     return summary
 
 
-ALL_STEPS = ("hip", "vecadd", "gemm", "hbm", "xgmi", "rccl")
+ALL_STEPS = ("hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl")
 
 
 def _steps_of(args: list[str]) -> list[str]:
@@ -236,7 +238,7 @@ def _drop_step(args: list[str], step: str) -> list[str]:
         i = out.index("--steps")
         out[i + 1] = ",".join(s for s in out[i + 1].split(",") if s != step)
     else:
-        out += ["--steps", ",".join(s for s in ("hip", "vecadd", "gemm", "hbm", "xgmi", "rccl") if s != step)]
+        out += ["--steps", ",".join(s for s in ALL_STEPS if s != step)]
     return out
 
 
@@ -360,11 +362,32 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
     return {"ok": True, "seconds": time.perf_counter() - t0, **results}
 
 
+def validated_mfma_dtypes(workload: dict | None) -> list[str]:
+    """MFMA data types that passed the K5 probe on every rank of the workload
+    report (empty when the step did not run, e.g. simulated GPUs)."""
+    ranks = (workload or {}).get("ranks") or []
+    sets = []
+    for r in ranks:
+        step = next((s for s in r.get("steps", []) if s.get("name") == "mfma"), None)
+        if not step or not isinstance(step.get("dtypes"), dict):
+            return []
+        sets.append([k for k, ok in step["dtypes"].items() if ok is True])
+    if not sets:
+        return []
+    common = set(sets[0]).intersection(*sets[1:])
+    return [d for d in sets[0] if d in common]
+
+
 def complete(env: NodeEnv) -> dict:
-    """Mark the node validated (label + annotation with the step durations)."""
+    """Mark the node validated: label, the MFMA data types the probe confirmed
+    (``amd.com/gpu.validated.mfma=f16.bf16.fp8...``, next to GFD's per-arch
+    ``amd.com/gpu.mfma.*`` claims) and an annotation with the step durations."""
     steps = {s: (read_ready(env, s) or {}).get("seconds") for s in ("driver", "workload", "plugin")}
     ann = {"amd.com/gpu.validation": json.dumps({k: round(v, 4) for k, v in steps.items() if v is not None})}
-    env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": {VALIDATED_LABEL: "true"},
-                                                                "annotations": ann}})
-    write_ready(env, "complete", {"steps": steps})
-    return {"ok": True, "steps": steps}
+    labels = {VALIDATED_LABEL: "true"}
+    dtypes = validated_mfma_dtypes(read_ready(env, "workload"))
+    if dtypes:
+        labels[MFMA_LABEL] = ".".join(dtypes)[:63]
+    env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": labels, "annotations": ann}})
+    write_ready(env, "complete", {"steps": steps, "mfma_dtypes": dtypes})
+    return {"ok": True, "steps": steps, "mfma_dtypes": dtypes}

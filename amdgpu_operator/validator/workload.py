@@ -8,6 +8,8 @@ Reference parity: the upstream operator-validator (implied by the reference's
 2. ``vecadd``   - K1, exact check
 3. ``gemm``     - K2 MFMA bf16 GEMM, Freivalds check (C·x == A·(Bᵀ·x)) on an
                   fp32-output pass, then a timed bf16-output pass (TFLOP/s)
+   ``mfma``     - K5 one exact MFMA tile per CDNA4 data type (f16, bf16, fp8,
+                  bf8, int8, block-scaled fp8/fp6/fp4, f32, f64)
 4. ``hbm``      - K3 streaming copy, checksum-verified, GB/s
 5. ``xgmi``     - K4 one-shot all-reduce over n emulated peers (1-GPU box) or
                   real peers (IPC-mapped over xGMI, multi-GPU), exact check
@@ -298,7 +300,16 @@ class ValidatorWorkload:
                                                 "algbw_gbps": ar["algbw_gbps"], "busbw_gbps": ar["busbw_gbps"],
                                                 "collectives": coll})
 
-    STEPS = ("hip", "vecadd", "gemm", "hbm", "xgmi", "rccl")
+    def step_mfma(self) -> StepResult:
+        """K5: one exact MFMA tile per CDNA4 matrix data type."""
+        t0 = time.perf_counter()
+        res = K.mfma_probe(self.cfg.seed, stream=self.torch.cuda.current_stream(self.device))
+        failed = [k for k, bad in res.items() if bad != 0]
+        if failed:
+            raise ValidationFailed("mfma", f"data types with wrong MFMA results: {failed}")
+        return StepResult("mfma", True, time.perf_counter() - t0, {"dtypes": {k: v == 0 for k, v in res.items()}})
+
+    STEPS = ("hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl")
 
     def run(self, steps: tuple[str, ...] | None = None) -> WorkloadReport:
         self.torch.cuda.set_device(self.device)
@@ -306,6 +317,7 @@ class ValidatorWorkload:
             "hip": self.step_hip,
             "vecadd": self.step_vecadd,
             "gemm": self.step_gemm,
+            "mfma": self.step_mfma,
             "hbm": self.step_hbm,
             "xgmi": self.step_xgmi_emulated,
             "rccl": self.step_rccl,

@@ -11,6 +11,9 @@
 //   K3 hbm_copy        - float4 streaming copy (HBM3E bandwidth check)
 //   K4 allreduce_*     - one-shot / two-shot sum over n peer buffers (peer
 //                        pointers over xGMI, or n emulated buffers on one GPU)
+//   K5 mfma_probe      - one MFMA tile per CDNA4 matrix data type (f16, bf16,
+//                        fp8, bf8, int8, block-scaled fp8/fp6/fp4, f32, f64),
+//                        checked exactly on the host
 // plus helpers for the correctness gates (device RNG fill, Freivalds GEMV
 // check, checksum, max-abs-diff).
 //
@@ -22,6 +25,9 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+
+#include <vector>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1108,6 +1114,53 @@ __global__ __launch_bounds__(256) void allreduce_twoshot_f32_kernel(PeerPtrs in,
   }
 }
 
+// ------------------------------------------------ K5 MFMA data-type probe ----
+// One wave, one 16x16 output tile per matrix-core data type the node's GFD
+// labels advertise for CDNA4 (amd.com/gpu.mfma.*): f16, bf16, OCP fp8 and bf8,
+// int8, the block-scaled f8f6f4 forms with fp8 / fp6 / fp4 operands (scale 1),
+// f32 and f64.  The host lays out each lane's operand fragment (lane-major:
+// fragment of lane l at byte l * FRAG), so the kernel only loads, issues the
+// MFMA and stores each lane's 4 accumulators; avk_mfma_probe checks the tile
+// exactly against an integer reference.
+template <int KIND>
+__global__ __launch_bounds__(64) void mfma_probe_kernel(const void* __restrict__ A, const void* __restrict__ B,
+                                                        void* __restrict__ D) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  typedef int i32x8 __attribute__((ext_vector_type(8)));
+  typedef double f64x4 __attribute__((ext_vector_type(4)));
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  const int l = threadIdx.x;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (KIND == 0) {
+    reinterpret_cast<f32x4*>(D)[l] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+        reinterpret_cast<const f16x8*>(A)[l], reinterpret_cast<const f16x8*>(B)[l], z, 0, 0, 0);
+  } else if constexpr (KIND == 1) {
+    reinterpret_cast<f32x4*>(D)[l] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+        reinterpret_cast<const bf16x8*>(A)[l], reinterpret_cast<const bf16x8*>(B)[l], z, 0, 0, 0);
+  } else if constexpr (KIND == 2) {
+    reinterpret_cast<f32x4*>(D)[l] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(
+        reinterpret_cast<const long*>(A)[l], reinterpret_cast<const long*>(B)[l], z, 0, 0, 0);
+  } else if constexpr (KIND == 3) {
+    reinterpret_cast<f32x4*>(D)[l] = __builtin_amdgcn_mfma_f32_16x16x32_bf8_bf8(
+        reinterpret_cast<const long*>(A)[l], reinterpret_cast<const long*>(B)[l], z, 0, 0, 0);
+  } else if constexpr (KIND == 4) {
+    reinterpret_cast<i32x4*>(D)[l] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+        reinterpret_cast<const i32x4*>(A)[l], reinterpret_cast<const i32x4*>(B)[l], (i32x4){0, 0, 0, 0}, 0, 0, 0);
+  } else if constexpr (KIND >= 5 && KIND <= 7) {
+    // operand formats (cbsz / blgp): 0 fp8 e4m3, 2 fp6 e2m3, 4 fp4 e2m1; E8M0 scale 127 = 1.0
+    constexpr int FMT = KIND == 5 ? 0 : (KIND == 6 ? 2 : 4);
+    reinterpret_cast<f32x4*>(D)[l] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+        reinterpret_cast<const i32x8*>(A)[l], reinterpret_cast<const i32x8*>(B)[l], z, FMT, FMT, 0, 127, 0, 127);
+  } else if constexpr (KIND == 8) {
+    reinterpret_cast<f32x4*>(D)[l] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+        reinterpret_cast<const float*>(A)[l], reinterpret_cast<const float*>(B)[l], z, 0, 0, 0);
+  } else {
+    reinterpret_cast<f64x4*>(D)[l] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+        reinterpret_cast<const double*>(A)[l], reinterpret_cast<const double*>(B)[l], (f64x4){0., 0., 0., 0.}, 0, 0,
+        0);
+  }
+}
+
 inline int grid_for(int64_t work_items, int per_block, int max_blocks) {
   int64_t g = (work_items + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -1342,4 +1395,126 @@ AVK_API int avk_allreduce_twoshot_f32(const float* const* in_ptrs, float* const*
   if (hi <= lo) return hipSuccess;
   allreduce_twoshot_f32_kernel<<<grid_for(hi - lo, 256, 256 * 8), 256, 0, s>>>(pi, po, np, lo, hi);
   return hipGetLastError();
+}
+
+// ---------------------------------------------------------- K5 host side ----
+namespace {
+struct ProbeKind {
+  const char* name;
+  int k;          // K of one MFMA
+  int elem_bits;  // operand element width
+  int frag;       // bytes per lane fragment in the lane-major buffer
+  bool fp64;      // f64 C/D layout
+};
+constexpr ProbeKind kProbe[] = {
+    {"f16", 32, 16, 16, false},   {"bf16", 32, 16, 16, false}, {"fp8", 32, 8, 8, false},
+    {"bf8", 32, 8, 8, false},     {"i8", 64, 8, 16, false},    {"mxfp8", 128, 8, 32, false},
+    {"mxfp6", 128, 6, 32, false}, {"mxfp4", 128, 4, 32, false}, {"f32", 4, 32, 4, false},
+    {"f64", 4, 64, 8, true},
+};
+constexpr int kProbeKinds = sizeof(kProbe) / sizeof(kProbe[0]);
+
+// bit pattern of a small integer v in [-2, 2] in each operand format
+uint64_t probe_encode(int kind, int v) {
+  const int a = v < 0 ? -v : v;
+  const bool neg = v < 0;
+  switch (kind) {
+    case 0: return (neg ? 0x8000 : 0) | (a == 0 ? 0 : a == 1 ? 0x3C00 : 0x4000);  // f16
+    case 1: return (neg ? 0x8000 : 0) | (a == 0 ? 0 : a == 1 ? 0x3F80 : 0x4000);  // bf16
+    case 2: case 5: return (neg ? 0x80 : 0) | (a == 0 ? 0 : a == 1 ? 0x38 : 0x40);  // e4m3
+    case 3: return (neg ? 0x80 : 0) | (a == 0 ? 0 : a == 1 ? 0x3C : 0x40);  // e5m2
+    case 4: return (uint64_t)(uint8_t)(int8_t)v;                           // int8
+    case 6: return (neg ? 0x20 : 0) | (a == 0 ? 0 : a == 1 ? 0x08 : 0x10);  // fp6 e2m3
+    case 7: return (neg ? 0x8 : 0) | (a == 0 ? 0 : a == 1 ? 0x2 : 0x4);     // fp4 e2m1
+    case 8: { float f = (float)v; uint32_t u; memcpy(&u, &f, 4); return u; }
+    default: { double f = (double)v; uint64_t u; memcpy(&u, &f, 8); return u; }
+  }
+}
+
+void put_bits(uint8_t* p, int bit, int width, uint64_t v) {
+  for (int b = 0; b < width; ++b)
+    if ((v >> b) & 1) p[(bit + b) >> 3] |= (uint8_t)(1u << ((bit + b) & 7));
+}
+
+// lane l holds X[row l & 15][k = (l >> 4) * E + j], j < E (E = K / 4 elements)
+void probe_fragments(int kind, const std::vector<int>& X, std::vector<uint8_t>* out) {
+  const ProbeKind& pk = kProbe[kind];
+  const int E = pk.k / 4;
+  out->assign(64 * pk.frag, 0);
+  for (int l = 0; l < 64; ++l)
+    for (int j = 0; j < E; ++j)
+      put_bits(out->data() + l * pk.frag, j * pk.elem_bits, pk.elem_bits,
+               probe_encode(kind, X[(l & 15) * pk.k + (l >> 4) * E + j]));
+}
+}  // namespace
+
+AVK_API int avk_mfma_probe_count() { return kProbeKinds; }
+
+AVK_API const char* avk_mfma_probe_name(int kind) {
+  return kind >= 0 && kind < kProbeKinds ? kProbe[kind].name : "";
+}
+
+// Runs probe `kind` on the current device; *mismatches = output elements that
+// differ from the exact integer reference (0 = the data type works).
+AVK_API int avk_mfma_probe(int kind, uint64_t seed, int* mismatches, hipStream_t s) {
+  if (kind < 0 || kind >= kProbeKinds || !mismatches) return hipErrorInvalidValue;
+  const ProbeKind& pk = kProbe[kind];
+  std::vector<int> a(16 * pk.k), bt(16 * pk.k);  // A[16][K], Bt[16][K] (= B^T)
+  uint64_t h = seed * 0x9E3779B97F4A7C15ull + (uint64_t)kind;
+  auto next = [&h]() {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 29;
+    return (int)(h % 5) - 2;
+  };
+  for (int& v : a) v = next();
+  for (int& v : bt) v = next();
+  std::vector<uint8_t> fa, fb;
+  probe_fragments(kind, a, &fa);
+  probe_fragments(kind, bt, &fb);
+  const size_t dbytes = 64 * 4 * (pk.fp64 ? 8 : 4);
+  void *da = nullptr, *db = nullptr, *dd = nullptr;
+  hipError_t e = hipMalloc(&da, fa.size());
+  if (e == hipSuccess) e = hipMalloc(&db, fb.size());
+  if (e == hipSuccess) e = hipMalloc(&dd, dbytes);
+  if (e == hipSuccess) e = hipMemcpyAsync(da, fa.data(), fa.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(db, fb.data(), fb.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    switch (kind) {
+#define AVK_PROBE(K) case K: mfma_probe_kernel<K><<<1, 64, 0, s>>>(da, db, dd); break;
+      AVK_PROBE(0) AVK_PROBE(1) AVK_PROBE(2) AVK_PROBE(3) AVK_PROBE(4)
+      AVK_PROBE(5) AVK_PROBE(6) AVK_PROBE(7) AVK_PROBE(8) AVK_PROBE(9)
+#undef AVK_PROBE
+    }
+    e = hipGetLastError();
+  }
+  std::vector<uint8_t> out(dbytes);
+  if (e == hipSuccess) e = hipMemcpyAsync(out.data(), dd, dbytes, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  for (void* p : {da, db, dd})
+    if (p) (void)hipFree(p);
+  if (e != hipSuccess) return e;
+  int bad = 0;
+  for (int l = 0; l < 64; ++l)
+    for (int i = 0; i < 4; ++i) {
+      // C/D maps (cdna_hip_programming.md §3): col = lane & 15; row = 4*(lane>>4) + i, f64: (lane>>4) + 4*i
+      const int col = l & 15, row = pk.fp64 ? (l >> 4) + 4 * i : 4 * (l >> 4) + i;
+      long long ref = 0;
+      for (int k = 0; k < pk.k; ++k) ref += (long long)a[row * pk.k + k] * bt[col * pk.k + k];
+      double got;
+      if (pk.fp64) {
+        memcpy(&got, out.data() + (l * 4 + i) * 8, 8);
+      } else if (kind == 4) {
+        int32_t v;
+        memcpy(&v, out.data() + (l * 4 + i) * 4, 4);
+        got = v;
+      } else {
+        float v;
+        memcpy(&v, out.data() + (l * 4 + i) * 4, 4);
+        got = v;
+      }
+      bad += got != (double)ref;
+    }
+  *mismatches = bad;
+  return hipSuccess;
 }

@@ -153,7 +153,7 @@ struct Args {
   int world = 1;
   std::string rendezvous = "/tmp/amdgpu-validator";
   std::string run_id = "run";
-  std::string steps = "hip,vecadd,gemm,hbm,xgmi,rccl";
+  std::string steps = "hip,vecadd,gemm,mfma,hbm,xgmi,rccl";
   int gemm_n = 4096;
   int gemm_iters = 3;
   long long hbm_bytes = 1ll << 30;
@@ -425,6 +425,28 @@ Step step_hbm(const Args& a, hipStream_t st, int cus) {
   s.seconds = secs(t0);
   s.detail = fmt("\"bytes\": %lld, \"ms\": %.4f, \"gbps\": %.1f, \"checksum_match\": %s", (long long)bytes, ms, gbps,
                  h[0] == h[1] ? "true" : "false");
+  return s;
+}
+
+// K5: every CDNA4 matrix-core data type the GFD labels advertise, one exact tile each
+Step step_mfma(hipStream_t st) {
+  auto t0 = Clock::now();
+  Step s{"mfma"};
+  std::string d = "\"dtypes\": {";
+  std::string failed;
+  bool ok = true;
+  for (int k = 0; k < avk_mfma_probe_count(); ++k) {
+    int bad = -1;
+    AVK_OK(avk_mfma_probe(k, 0x5EED + k, &bad, st));
+    d += fmt("%s\"%s\": %s", k ? ", " : "", avk_mfma_probe_name(k), bad == 0 ? "true" : "false");
+    if (bad != 0) {
+      ok = false;
+      failed += std::string(failed.empty() ? "" : ",") + avk_mfma_probe_name(k);
+    }
+  }
+  s.ok = ok;
+  s.seconds = secs(t0);
+  s.detail = d + "}" + (failed.empty() ? "" : ", \"failed\": \"" + failed + "\"");
   return s;
 }
 
@@ -740,6 +762,7 @@ int main(int argc, char** argv) {
     HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
     if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st)), steps.back().ok);
+    if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
     if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
     if (ok && has_step(a, "xgmi")) ok = (steps.push_back(step_xgmi(a, st, rv)), steps.back().ok);
     if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, &rccl_thread, &rccl_state)), steps.back().ok);

@@ -198,3 +198,11 @@ def test_vector_add_verify_counts_corruption():
     c[5] += 1.0
     c[n - 1] = float("nan")
     assert K.vector_add_verify(a, b, c) == 2
+
+
+@pytest.mark.parametrize("seed", [1, 7])
+def test_mfma_probe_every_cdna4_dtype_exact(seed):
+    # K5: f16, bf16, OCP fp8/bf8, int8, block-scaled fp8/fp6/fp4 (scale 1), f32, f64
+    res = K.mfma_probe(seed)
+    assert set(res) == {"f16", "bf16", "fp8", "bf8", "i8", "mxfp8", "mxfp6", "mxfp4", "f32", "f64"}
+    assert all(v == 0 for v in res.values()), res

@@ -23,10 +23,12 @@ def _run(args, env=None, timeout=120):
 
 
 def test_validator_all_local_steps_with_counter_gate(tmp_path):
-    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,vecadd,gemm,hbm,xgmi", "--counter-gate"],
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,vecadd,gemm,mfma,hbm,xgmi", "--counter-gate"],
                    {"AMDGPU_VALIDATOR_COUNTERS": "1"})
     assert rc == 0 and rep["ok"], rep
     steps = {s["name"]: s for s in rep["steps"]}
+    assert steps["mfma"]["dtypes"] == {d: True for d in ("f16", "bf16", "fp8", "bf8", "i8", "mxfp8", "mxfp6", "mxfp4",
+                                                         "f32", "f64")}
     assert steps["hip"]["arch"].startswith("gfx950") and steps["hip"]["cus"] == 256
     assert steps["vecadd"]["mismatches"] == 0
     g = steps["gemm"]

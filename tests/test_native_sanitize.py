@@ -2,6 +2,7 @@
 synthetic inputs.  GPU sanitizers are not available on the
 pool; the GPU kernels are covered by the numerics tests instead."""
 
+import fcntl
 import json
 import os
 import subprocess
@@ -16,7 +17,12 @@ pytestmark = pytest.mark.slow
 
 @pytest.fixture(scope="module")
 def asan_bins():
-    p = subprocess.run(["make", "-C", str(native.NATIVE_SRC), "sanitize"], capture_output=True, text=True, timeout=600)
+    # xdist workers each build this fixture: serialise make so no worker runs
+    # a binary another worker's make is relinking
+    with open(os.path.join(str(native.NATIVE_SRC), ".sanitize.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        p = subprocess.run(["make", "-C", str(native.NATIVE_SRC), "sanitize"], capture_output=True, text=True,
+                           timeout=600)
     if p.returncode != 0:
         pytest.skip(f"sanitizer toolchain unavailable: {p.stderr[-500:]}")
     return {n: str(native.artefact(n + ".asan")) for n in ("amdgpu-oci-hook", "amdgpu-probe")}

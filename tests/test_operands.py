@@ -170,7 +170,7 @@ def test_workload_validation_launch_plan(env):
     assert all("--counter-gate" in a for a in kernel) and not any("--counter-gate" in a for a in rccl)
     assert {e.get("AMDGPU_VALIDATOR_COUNTERS") for a, e, _ in launched if a in kernel} == {"1"}
     names = [s["name"] for s in out["ranks"][0]["steps"]]
-    assert names == ["hip", "vecadd", "gemm", "hbm", "xgmi", "rccl"]
+    assert names == ["hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl"]
     assert V.read_ready(env, "workload")["world"] == 2
 
 
@@ -193,7 +193,7 @@ def test_single_gpu_skips_rccl(tmp_path):
 
     env.launcher = launcher
     out = V.validate_workload(env, [])
-    assert seen == ["hip,vecadd,gemm,hbm,xgmi"]
+    assert seen == ["hip,vecadd,gemm,mfma,hbm,xgmi"]
     assert out["ranks"][0]["steps"][-1]["skipped"].startswith("single GPU")
 
 
@@ -203,6 +203,20 @@ def test_complete_labels_node(env):
     node = env.client.get("v1", "Node", "n1")
     assert node["metadata"]["labels"][V.VALIDATED_LABEL] == "true"
     assert json.loads(node["metadata"]["annotations"]["amd.com/gpu.validation"])["driver"] == 0.1
+    assert V.MFMA_LABEL not in node["metadata"]["labels"]  # no probe results: no claim
+
+
+def test_complete_publishes_mfma_types_confirmed_on_every_gpu(env):
+    def rank(dtypes):
+        return {"steps": [{"name": "hip", "ok": True}, {"name": "mfma", "ok": True, "dtypes": dtypes}]}
+
+    V.write_ready(env, "workload", {"ranks": [rank({"f16": True, "bf16": True, "mxfp4": True, "f64": True}),
+                                              rank({"f16": True, "bf16": True, "mxfp4": False, "f64": True})]})
+    out = V.complete(env)
+    assert out["mfma_dtypes"] == ["f16", "bf16", "f64"]
+    labels = env.client.get("v1", "Node", "n1")["metadata"]["labels"]
+    assert labels[V.MFMA_LABEL] == "f16.bf16.f64"
+    assert V.validated_mfma_dtypes({"ranks": [{"steps": [{"name": "hip"}]}]}) == []
 
 
 # ------------------------------------------------------------------ CLI
