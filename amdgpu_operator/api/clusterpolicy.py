@@ -172,6 +172,9 @@ class WorkloadSpec(_M):
     minGemmTflops: float = 0.0
     minHbmGbps: float = 0.0
     counterGate: bool = True
+    # run the RCCL check (own process, world 1) on a single-GPU node too: the
+    # multi-GPU critical path, rehearsed where there is no xGMI peer
+    rcclSingleGpu: bool = False
 
 
 class ValidatorSpec(Operand):

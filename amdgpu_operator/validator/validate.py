@@ -157,13 +157,16 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     # N7: the counter gate is a rocprofiler-sdk tool library loaded only into
     # the gated kernel processes (the binary does not link the SDK)
     counter_env = gate_env() if "--counter-gate" in args else {}
+    rccl_single = "--rccl-single-gpu" in args  # validate.py's own flag, not the binary's
+    args = _drop_flag(args, "--rccl-single-gpu")
     steps = _steps_of(args)
     kernel_steps = [s for s in steps if s != "rccl"]
     # RCCL runs in its own process per GPU, concurrently with the kernel
     # checks: loading librccl (~570 MB of device code) and its communicator
     # set-up would otherwise hold the HIP runtime of the kernel process.  A
-    # single-GPU node has no collective to validate (no xGMI peer).
-    run_rccl = "rccl" in steps and world > 1
+    # single-GPU node has no collective to validate (no xGMI peer) unless
+    # rcclSingleGpu asks for the rehearsal.
+    run_rccl = "rccl" in steps and (world > 1 or rccl_single)
     jobs = [(r, _with_steps(args, kernel_steps), run_id, counter_env) for r in range(world)]
     if run_rccl:
         jobs += [(r, _with_steps(_drop_flag(args, "--counter-gate"), ["hip", "rccl"]), run_id + "-rccl", {})

@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--sysfs-root", default=None, help="default: / when a GPU is present, else synthetic")
     ap.add_argument("--quick-workload", action="store_true", help="small validator sizes (CI)")
     ap.add_argument("--no-counter-gate", action="store_true", help="skip the rocprofiler counter gate (outer profiler)")
+    ap.add_argument("--rccl-single-gpu", action="store_true",
+                    help="rehearsal: run the RCCL validation process at N=1 too (multi-GPU critical path)")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--detail", default=None, help="write per-step breakdown JSON here")
     return ap.parse_args()
@@ -78,6 +80,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
     values = parse_set_flags(REFERENCE_SET_FLAGS)
     if args.no_counter_gate:
         values = deep_merge(values, {"validator": {"workload": {"counterGate": False}}})
+    if args.rccl_single_gpu:
+        values = deep_merge(values, {"validator": {"workload": {"rcclSingleGpu": True}}})
     if args.quick_workload:
         values = deep_merge(values, {"validator": {"workload": {"gemmN": 1024, "hbmBytes": 1 << 26,
                                                                 "rcclElems": 1 << 20, "xgmiElems": 1 << 20}}})
@@ -116,6 +120,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
             "xgmi_read_gbps": [s.get("read_gbps") for s in steps.get("xgmi", [])],
             "rccl_busbw_gbps": [s.get("busbw_gbps") for s in steps.get("rccl", [])],
             "rccl_comm_init_s": [s.get("comm_init_s") for s in steps.get("rccl", [])],
+            "rccl_library": [s.get("library") for s in steps.get("rccl", [])],
+            "rccl_process_seconds": [r.get("rccl_process_seconds") for r in ranks],
             "rank0_step_seconds": {s["name"]: s.get("seconds") for s in (ranks[0].get("steps", []) if ranks else [])},
             "rank0_total_seconds": ranks[0].get("seconds") if ranks else None,
             "labels": {k: v for k, v in (nobj["metadata"].get("labels") or {}).items()
@@ -255,6 +261,7 @@ def main():
                 "gemm_tflops_per_gpu": results[-1]["gemm_tflops"],
                 "hbm_gbps_per_gpu": results[-1]["hbm_gbps"],
                 "rccl_busbw_gbps": results[-1]["rccl_busbw_gbps"],
+                "rccl_comm_init_s": results[-1]["rccl_comm_init_s"],
                 "counter_gate": results[-1]["gemm_counter_gate"],
             },
         }

@@ -45,8 +45,12 @@ using Clock = std::chrono::steady_clock;
 
 // RCCL is dlopen'ed (not linked): librccl's device code is large and loading
 // it costs ~0.5 s of process start-up plus ~1.5 s of kernel loading in
-// ncclCommInitRank.  Only the rccl step needs it, and that step's init runs on
-// a background thread while the kernel steps execute (see main()).
+// ncclCommInitRank.  Only the rccl step needs it.  The dlopen runs on the main
+// thread before the first HIP call: librccl's static initialisers register
+// its fat binaries with the HIP runtime, and running them on a second thread
+// while the main thread is inside HIP deadlocked (both threads parked on
+// futexes, seen on MI355X boxes).  ncclCommInitRank then runs on a background
+// thread while the kernel steps execute (see main()).
 struct Rccl {
   void* dl = nullptr;
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
@@ -58,13 +62,45 @@ struct Rccl {
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
 
-  bool load(std::string* err) {
-    for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
-      dl = dlopen(n, RTLD_NOW | RTLD_LOCAL);
-      if (dl) break;
+  std::string path;  // the library that was loaded
+
+  // The gfx950-only RCCL built next to this binary (native/Makefile,
+  // amdgpu_operator/toolkit/fatbin.py) when every GPU of the node is gfx950;
+  // AMDGPU_RCCL_LIBRARY overrides (empty = the system library).
+  static std::string preferred(const std::string& exe_dir) {
+    if (const char* e = getenv("AMDGPU_RCCL_LIBRARY")) return e;
+    const std::string slim = exe_dir + "rccl-gfx950/librccl.so.1";
+    if (access(slim.c_str(), R_OK) != 0) return "";
+    int gpus = 0;
+    for (int n = 0; n < 4096; ++n) {
+      std::ifstream f("/sys/class/kfd/kfd/topology/nodes/" + std::to_string(n) + "/properties");
+      if (!f) break;
+      std::string k;
+      long long v = 0;
+      while (f >> k >> v) {
+        if (k != "gfx_target_version" || v == 0) continue;  // 0 = CPU node
+        if (v != 90500) return "";
+        ++gpus;
+      }
+    }
+    return gpus ? slim : "";
+  }
+
+  bool load(const std::string& exe_dir, std::string* err) {
+    const std::string want = preferred(exe_dir);
+    std::vector<std::string> names;
+    if (!want.empty()) names.push_back(want);
+    for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) names.push_back(n);
+    for (const auto& n : names) {
+      dl = dlopen(n.c_str(), RTLD_NOW | RTLD_LOCAL);
+      if (dl) {
+        path = n;
+        break;
+      }
+      if (n == want) *err = std::string("dlopen ") + n + ": " + dlerror() + "; ";
     }
     if (!dl) {
-      *err = std::string("dlopen librccl failed: ") + dlerror();
+      *err += std::string("dlopen librccl failed: ") + dlerror();
       return false;
     }
     GetUniqueId = reinterpret_cast<decltype(GetUniqueId)>(dlsym(dl, "ncclGetUniqueId"));
@@ -165,6 +201,7 @@ struct Args {
   double timeout_s = 120;
   bool counter_gate = false;
   bool any_arch = false;
+  bool rccl_destroy = false;  // ncclCommDestroy before exit (default: barrier + exit, see step_rccl)
   std::string ready_file;
 };
 
@@ -541,10 +578,7 @@ struct RcclInit {
 
 void rccl_init(const Args& a, const Rendezvous& rv, RcclInit* out) {
   try {
-    auto t0 = Clock::now();
-    std::string err;
-    if (!g_rccl.load(&err)) throw std::runtime_error(err);
-    out->load_s = secs(t0);
+    if (!g_rccl.dl) throw std::runtime_error("librccl not loaded");
     HIP_OK(hipSetDevice(a.device));
     ncclUniqueId id;
     const std::string idname = a.run_id + "-nccl-id";
@@ -591,7 +625,7 @@ uint16_t bf16_bits(float f) {
 // checked exactly (rank r contributes r+1) and timed; busBW uses the usual
 // ring factors (all-reduce 2(n-1)/n, gather/scatter (n-1)/n) so the numbers
 // compare with rccl-tests.  SURVEY.md §2.E call sites.
-Step step_rccl(const Args& a, hipStream_t st, std::thread* init_thread, RcclInit* ri) {
+Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread* init_thread, RcclInit* ri) {
   auto t0 = Clock::now();
   Step s{"rccl"};
   init_thread->join();
@@ -619,11 +653,13 @@ Step step_rccl(const Args& a, hipStream_t st, std::thread* init_thread, RcclInit
   };
 
   // fp32 all-reduce
+  const auto t_first = Clock::now();
   std::fill(host.begin(), host.end(), (float)(a.rank + 1));
   HIP_OK(hipMemcpyAsync(buf, host.data(), n * 4, hipMemcpyHostToDevice, st));
   NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
   HIP_OK(hipMemcpyAsync(host.data(), buf, n * 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
+  const double first_s = secs(t_first);
   int64_t bad = 0;
   for (int64_t i = 0; i < n; ++i) bad += host[i] != expect_sum;
   float ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st)); });
@@ -672,16 +708,29 @@ Step step_rccl(const Args& a, hipStream_t st, std::thread* init_thread, RcclInit
     report("reducescatter_f32", n * 4, ms, W > 1 ? (W - 1.0) / W : 0.0, bad);
   }
 
-  NCCL_OK(g_rccl.CommDestroy(comm));
-  (void)hipFree(buf);
-  (void)hipFree(aux);
+  const double checks_s = secs(t_first);
+  // No ncclCommDestroy: it costs ~0.4 s (proxy shutdown, measured on MI355X,
+  // tools/rccl_init_probe.py) and the process leaves right after the report
+  // without runtime teardown (main).  What destroy would guarantee - no rank
+  // exits while a peer's kernel may still touch its IPC-mapped buffers - comes
+  // from this barrier: every rank has synchronised its stream before it
+  // arrives, so after it no collective of this communicator is in flight.
+  const auto t_destroy = Clock::now();
+  rv.barrier(a.run_id + "-rccl-done");
+  if (a.rccl_destroy) NCCL_OK(g_rccl.CommDestroy(comm));
+  const double destroy_s = secs(t_destroy);
+  if (a.rccl_destroy) {
+    (void)hipFree(buf);
+    (void)hipFree(aux);
+  }
   s.ok = total_bad == 0;
   s.seconds = secs(t0);
   s.detail = fmt("\"world\": %d, \"bytes\": %lld, \"lib_load_s\": %.4f, \"comm_init_s\": %.4f, \"init_wait_s\": %.4f, "
+                 "\"first_allreduce_s\": %.4f, \"checks_s\": %.4f, \"finish_s\": %.4f, "
                  "\"ms\": %.4f, \"algbw_gbps\": %.1f, \"busbw_gbps\": %.1f, \"mismatches\": %lld, \"collectives\": {",
-                 W, (long long)(n * 4), ri->load_s, ri->init_s, wait_s, ar_ms, ar_algbw, ar_busbw,
-                 (long long)total_bad) +
-             detail + "}";
+                 W, (long long)(n * 4), ri->load_s, ri->init_s, wait_s, first_s, checks_s, destroy_s, ar_ms, ar_algbw,
+                 ar_busbw, (long long)total_bad) +
+             detail + "}, \"library\": \"" + g_rccl.path + "\"";
   return s;
 }
 
@@ -697,7 +746,8 @@ void usage(const char* p) {
   fprintf(stderr,
           "usage: %s [--device N] [--rank R --world W --rendezvous DIR --run-id ID] [--steps a,b,...]\n"
           "          [--gemm N] [--gemm-iters K] [--hbm-bytes B] [--rccl-elems E] [--xgmi-elems E]\n"
-          "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--ready-file PATH]\n",
+          "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--rccl-destroy]\n"
+          "          [--ready-file PATH]\n",
           p);
 }
 
@@ -732,6 +782,7 @@ int main(int argc, char** argv) {
     else if (k == "--timeout") a.timeout_s = atof(v());
     else if (k == "--counter-gate") a.counter_gate = true;
     else if (k == "--any-arch") a.any_arch = true;
+    else if (k == "--rccl-destroy") a.rccl_destroy = true;
     else if (k == "--ready-file") a.ready_file = v();
     else {
       usage(argv[0]);
@@ -755,17 +806,24 @@ int main(int argc, char** argv) {
   memset(&prop, 0, sizeof(prop));
   std::thread rccl_thread;
   RcclInit rccl_state;
+  if (has_step(a, "rccl")) {  // before any HIP call: see the note at struct Rccl
+    auto tl = Clock::now();
+    std::string err;
+    if (!g_rccl.load(Gate::exe_dir(), &err)) rccl_state.error = err;
+    rccl_state.load_s = secs(tl);
+  }
   try {
     steps.push_back(step_hip(a, &prop));
     ok = steps.back().ok;
-    if (ok && has_step(a, "rccl")) rccl_thread = std::thread(rccl_init, std::cref(a), std::cref(rv), &rccl_state);
+    if (ok && has_step(a, "rccl") && rccl_state.error.empty())
+      rccl_thread = std::thread(rccl_init, std::cref(a), std::cref(rv), &rccl_state);
     HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
     if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st)), steps.back().ok);
     if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
     if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
     if (ok && has_step(a, "xgmi")) ok = (steps.push_back(step_xgmi(a, st, rv)), steps.back().ok);
-    if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, &rccl_thread, &rccl_state)), steps.back().ok);
+    if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, rv, &rccl_thread, &rccl_state)), steps.back().ok);
   } catch (const std::exception& e) {
     ok = false;
     error = e.what();

@@ -1,5 +1,7 @@
 #!/bin/bash
-# Full GPU tier + N=1 headline bench (what the driver runs at round end)
+# Full GPU tier + N=1 headline bench (what the driver runs at round end),
+# then the N=1 bench with the RCCL validation process rehearsed (the critical
+# path of a multi-GPU node: tools/rccl_init_probe.py).
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-full}
@@ -13,4 +15,7 @@ rc=$?; echo "smoke rc=$rc"; tail -1 $O/smoke.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python3 -u bench.py --steps 8 --warmup 1 --detail $O/bench_detail.json > $O/bench.json 2> $O/bench.err
 rc=$?; echo "bench rc=$rc"; cat $O/bench.json; tail -3 $O/bench.err
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python3 -u bench.py --steps 8 --warmup 1 --rccl-single-gpu --detail $O/bench_rccl_detail.json > $O/bench_rccl.json 2> $O/bench_rccl.err
+rc=$?; echo "bench rccl rehearsal rc=$rc"; cat $O/bench_rccl.json; tail -3 $O/bench_rccl.err
 exit $rc
