@@ -94,6 +94,20 @@ class ToolkitSpec(Operand):
     runtimeClass: str = "amd"
     cdi: CDISpec = Field(default_factory=CDISpec)
     mountRocm: bool = False
+    # prestart-hook device-list policy (the NVIDIA toolkit's
+    # accept-nvidia-visible-devices-as-volume-mounts / -envvar-when-unprivileged)
+    acceptDeviceListAsVolumeMounts: bool = False
+    acceptEnvvarUnprivileged: bool = True
+
+
+class DevicePluginConfigRef(_M):
+    """ConfigMap of device-plugin config files (deviceplugin/config.py): ``name``
+    in the operator namespace, ``default`` key for nodes without the
+    ``amd.com/device-plugin.config`` label.  Same shape as the NVIDIA
+    operator's ``devicePlugin.config`` (time-slicing lives there)."""
+
+    name: str = ""
+    default: str = ""
 
 
 class DevicePluginSpec(Operand):
@@ -102,9 +116,13 @@ class DevicePluginSpec(Operand):
     image: str = "amd-device-plugin"
     resourceName: str = RESOURCE_NAME
     partitionStrategy: Literal["single", "mixed"] = "single"
+    deviceIDStrategy: Literal["bdf", "uuid", "index"] = "bdf"
+    deviceListStrategy: list[Literal["envvar", "volume-mounts", "cdi-annotations", "cdi-cri"]] = Field(
+        default_factory=lambda: ["envvar"])
     passDeviceSpecs: bool = True
     cdiAnnotations: bool = False
     healthPollMs: int = 1000
+    config: DevicePluginConfigRef = Field(default_factory=DevicePluginConfigRef)
 
 
 class ServiceMonitor(_M):

@@ -45,6 +45,14 @@ def build_parser() -> argparse.ArgumentParser:
     dp.add_argument("--health-poll-ms", type=int, default=1000)
     dp.add_argument("--cdi", action="store_true")
     dp.add_argument("--no-health", action="store_true")
+    dp.add_argument("--device-id-strategy", default="bdf", choices=["bdf", "uuid", "index"])
+    dp.add_argument("--device-list-strategy", default="envvar",
+                    help="comma list of envvar, volume-mounts, cdi-annotations, cdi-cri")
+    dp.add_argument("--no-device-specs", action="store_true", help="no DeviceSpecs in Allocate (CDI / hook inject)")
+    dp.add_argument("--config-file", default=None, help="device-plugin config file (flags + sharing)")
+    dp.add_argument("--config-map", default=None, help="NAMESPACE/NAME of a ConfigMap of config files")
+    dp.add_argument("--config-default", default="", help="ConfigMap key used when the node has no config label")
+    dp.add_argument("--config-poll", type=float, default=5.0, help="seconds between config label/ConfigMap checks")
 
     me = sub.add_parser("metrics-exporter", help="amd-smi metrics exporter (DCGM-exporter equivalent)")
     me.add_argument("--port", type=int, default=9400)
@@ -64,6 +72,8 @@ def build_parser() -> argparse.ArgumentParser:
     gfd.add_argument("--interval", type=float, default=60.0)
     gfd.add_argument("--label-prefix", default="amd.com")
     gfd.add_argument("--oneshot", action="store_true")
+    gfd.add_argument("--device-plugin-config-map", default=None, help="NAMESPACE/NAME: sharing labels")
+    gfd.add_argument("--device-plugin-config-default", default="")
 
     pm = sub.add_parser("partition-manager", help="compute/memory partition manager")
     pm.add_argument("--config-label", default="amd.com/gpu.partition-config")
@@ -129,7 +139,9 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         if a.action == "install":
             tk.install(env, runtime_class=a.runtime_class or cenv.get("RUNTIME_CLASS", "amd"),
                        cdi_enabled=not a.no_cdi and cenv.get("CDI_ENABLED", "true") == "true",
-                       mount_rocm=a.mount_rocm or cenv.get("MOUNT_ROCM") == "true")
+                       mount_rocm=a.mount_rocm or cenv.get("MOUNT_ROCM") == "true",
+                       args=tk.hook_args(cenv.get("ACCEPT_DEVICE_LIST_AS_VOLUME_MOUNTS") == "true",
+                                         cenv.get("ACCEPT_ENVVAR_UNPRIVILEGED", "true") == "true"))
             ready()
             stop.wait()
         else:
@@ -163,9 +175,31 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
     if cmd == "device-plugin":
         from ..deviceplugin.server import DevicePluginManager, PluginConfig
 
+        from ..deviceplugin import config as DC
+
+        def load_config():
+            """(key, config) for this node: ConfigMap key chosen by node label / default, or a file."""
+            if a.config_map:
+                ns_, _, name = a.config_map.rpartition("/")
+                cm = _get_or_empty(env.client, "ConfigMap", name, ns_ or env.namespace)
+                node = _get_or_empty(env.client, "Node", env.node_name)
+                k, c = DC.select(cm.get("data") or {}, (node.get("metadata") or {}).get("labels"), a.config_default)
+                return k, (c if k else cli_config)
+            if a.config_file:
+                with open(a.config_file) as f:
+                    return a.config_file, DC.parse(f.read())
+            return "", cli_config
+
+        # command-line flags = the config when no file / ConfigMap key applies
+        cli_config = DC.DevicePluginConfig.model_validate({"flags": {
+            "partitionStrategy": a.partition_strategy, "deviceIDStrategy": a.device_id_strategy,
+            "deviceListStrategy": [x for x in a.device_list_strategy.split(",") if x],
+            "passDeviceSpecs": not a.no_device_specs}})
+
+        key, dcfg = load_config()
         cfg = PluginConfig(resource_name=a.resource_name, socket_dir=env.device_plugin_dir, sysfs_root=env.sysfs_root(),
                            cdi_enabled=a.cdi, partition_strategy=a.partition_strategy, health_poll_ms=a.health_poll_ms,
-                           watch_interval_s=max(0.05, min(0.5, env.poll_s * 10)))
+                           watch_interval_s=max(0.05, min(0.5, env.poll_s * 10)), device_config=dcfg)
         health = None
         if not a.no_health and not env.extra.get("no_health"):
             try:
@@ -177,8 +211,20 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                 log.info("health watcher unavailable: %s", e)
         mgr = DevicePluginManager(cfg, health_poll=health)
         mgr.start()
+        log.info("device plugin serving %s (config %r)", sorted(mgr.servers), key)
         ready()
-        stop.wait()
+        if a.config_map:  # the config-manager loop: follow the node label and the ConfigMap
+            while not stop.wait(max(env.poll_s, a.config_poll)):
+                try:
+                    new_key, new_cfg = load_config()
+                except Exception as e:  # noqa: BLE001 - keep serving the last good config
+                    log.error("device-plugin config: %s", e)
+                    continue
+                if mgr.reconfigure(new_cfg):
+                    log.info("device-plugin config %r -> %r", key, new_key)
+                    key = new_key
+        else:
+            stop.wait()
         mgr.stop()
         return 0
 
@@ -232,8 +278,25 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                 L.sync_node_labels(env.client, env.node_name, L.nfd_labels(env.sysfs_root()), (L.NFD_PREFIX + "pci-",))
             else:
                 gpus = topology.enumerate_gpus(env.sysfs_root())
-                L.sync_node_labels(env.client, env.node_name, L.gfd_labels(gpus, env.sysfs_root(), a.label_prefix),
-                                   (f"{a.label_prefix}/gpu.",))
+                labels = L.gfd_labels(gpus, env.sysfs_root(), a.label_prefix)
+                if labels:
+                    labels = L.sharing_labels(labels, plugin_config(), prefix=a.label_prefix)
+                L.sync_node_labels(env.client, env.node_name, labels, (f"{a.label_prefix}/gpu.",))
+
+        def plugin_config():
+            if cmd != "gfd" or not a.device_plugin_config_map:
+                return None
+            from ..deviceplugin import config as DC
+
+            ns_, _, name = a.device_plugin_config_map.rpartition("/")
+            cm = _get_or_empty(env.client, "ConfigMap", name, ns_ or env.namespace)
+            node = _get_or_empty(env.client, "Node", env.node_name)
+            try:
+                return DC.select(cm.get("data") or {}, (node.get("metadata") or {}).get("labels"),
+                                 a.device_plugin_config_default)[1]
+            except (KeyError, ValueError) as e:
+                log.error("device-plugin config for labels: %s", e)
+                return None
 
         once()
         ready()
@@ -261,6 +324,18 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         return 0
 
     raise SystemExit(f"unknown command {cmd}")
+
+
+def _get_or_empty(client, kind: str, name: str, namespace: str | None = None) -> dict:
+    """A core/v1 object, or {} when it does not exist (yet)."""
+    from ..kube.fakeapi import ApiError
+
+    try:
+        return client.get("v1", kind, name, namespace) or {}
+    except ApiError as e:  # both clients raise it (REST: from the HTTP status)
+        if e.code == 404:
+            return {}
+        raise
 
 
 def _plugin_pod_args(extra: list[str]) -> list[str]:

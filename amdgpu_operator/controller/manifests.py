@@ -160,6 +160,10 @@ NODE_RW_RULES = [
     {"apiGroups": [""], "resources": ["pods"], "verbs": ["get", "list", "watch", "create", "delete"]},
     {"apiGroups": [""], "resources": ["events"], "verbs": ["create", "patch"]},
 ]
+PLUGIN_CONFIG_RULES = [
+    {"apiGroups": [""], "resources": ["nodes"], "verbs": ["get", "list", "watch"]},
+    {"apiGroups": [""], "resources": ["configmaps"], "verbs": ["get", "list", "watch"]},
+]
 
 
 # ------------------------------------------------------------------ states ----
@@ -213,7 +217,9 @@ def state_toolkit(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     env = [{"name": "RUNTIME", "value": t.runtime}, {"name": "CONTAINERD_CONFIG", "value": t.containerdConfig},
            {"name": "CONTAINERD_SOCKET", "value": t.containerdSocket}, {"name": "RUNTIME_CLASS", "value": t.runtimeClass},
            {"name": "INSTALL_DIR", "value": t.installDir}, {"name": "CDI_ENABLED", "value": str(t.cdi.enabled).lower()},
-           {"name": "CDI_SPEC_DIR", "value": t.cdi.specDir}, {"name": "MOUNT_ROCM", "value": str(t.mountRocm).lower()}
+           {"name": "CDI_SPEC_DIR", "value": t.cdi.specDir}, {"name": "MOUNT_ROCM", "value": str(t.mountRocm).lower()},
+           {"name": "ACCEPT_DEVICE_LIST_AS_VOLUME_MOUNTS", "value": str(t.acceptDeviceListAsVolumeMounts).lower()},
+           {"name": "ACCEPT_ENVVAR_UNPRIVILEGED", "value": str(t.acceptEnvvarUnprivileged).lower()},
            ] + list(t.env)
     mounts = [_mount("containerd-config", "/runtime/config-dir"), _mount("containerd-socket", "/runtime/sock-dir"),
               _mount("install-dir", t.installDir), _mount("cdi-dir", t.cdi.specDir),
@@ -269,16 +275,23 @@ def state_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     name, sa = "amd-device-plugin-daemonset", "amd-device-plugin"
     image = p.ref("amd-device-plugin")
     args = ["device-plugin", "--resource-name", p.resourceName, "--partition-strategy", p.partitionStrategy,
-            "--health-poll-ms", str(p.healthPollMs)]
+            "--health-poll-ms", str(p.healthPollMs), "--device-id-strategy", p.deviceIDStrategy,
+            "--device-list-strategy", ",".join(p.deviceListStrategy)]
     if spec.toolkit.enabled and spec.toolkit.cdi.enabled and p.cdiAnnotations:
         args.append("--cdi")
+    if not p.passDeviceSpecs:
+        args.append("--no-device-specs")
+    rbac = []
+    if p.config.name:  # config-manager loop: reads the ConfigMap and this node's config label
+        args += ["--config-map", f"{ns}/{p.config.name}", "--config-default", p.config.default]
+        rbac = [_cluster_role(sa, PLUGIN_CONFIG_RULES, owner), _cluster_binding(sa, sa, ns, owner)]
     ctr = _container("amd-device-plugin", image, p.imagePullPolicy, args + list(p.args),
                      [_mount("device-plugin", "/var/lib/kubelet/device-plugins"), _mount("host-sys", "/host/sys", ro=True)],
                      list(p.env), True, p.resources.model_dump())
     inits = [_wait_init("toolkit-validation", image, p.imagePullPolicy, "toolkit" if spec.toolkit.enabled else "driver")]
     vols = [_hostpath("device-plugin", "/var/lib/kubelet/device-plugins"), _hostpath("host-sys", "/sys", "Directory"),
             _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
-    return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "devicePlugin", sa, [ctr], inits, vols)]
+    return [_sa(sa, ns, owner), *rbac, _daemonset(spec, ns, owner, name, "devicePlugin", sa, [ctr], inits, vols)]
 
 
 def state_metrics_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
@@ -324,13 +337,16 @@ def state_gfd(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     g = spec.gfd
     name, sa = "gpu-feature-discovery", "gpu-feature-discovery"
     image = g.ref("gpu-feature-discovery")
-    ctr = _container("gpu-feature-discovery", image, g.imagePullPolicy,
-                     ["gfd", "--interval", str(g.intervalSeconds), "--label-prefix", g.labelPrefix] + list(g.args),
+    args = ["gfd", "--interval", str(g.intervalSeconds), "--label-prefix", g.labelPrefix]
+    if spec.devicePlugin.config.name:  # sharing labels follow the device-plugin config
+        args += ["--device-plugin-config-map", f"{ns}/{spec.devicePlugin.config.name}",
+                 "--device-plugin-config-default", spec.devicePlugin.config.default]
+    ctr = _container("gpu-feature-discovery", image, g.imagePullPolicy, args + list(g.args),
                      [_mount("host-sys", "/host/sys", ro=True)], list(g.env), False, g.resources.model_dump())
     inits = [_wait_init("driver-validation", image, g.imagePullPolicy, "driver")]
     vols = [_hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
-    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
-            _daemonset(spec, ns, owner, name, "gfd", sa, [ctr], inits, vols)]
+    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES + PLUGIN_CONFIG_RULES[1:], owner),
+            _cluster_binding(sa, sa, ns, owner), _daemonset(spec, ns, owner, name, "gfd", sa, [ctr], inits, vols)]
 
 
 def state_partition_manager(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:

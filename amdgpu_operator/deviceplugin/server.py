@@ -16,6 +16,11 @@ implements the kubelet ``v1beta1`` DevicePlugin service over a unix socket:
   xGMI hive) and, when enabled, CDI device names for containerd;
 * ``PreStartContainer`` is a no-op (not required).
 
+GPU sharing, device-ID and device-list strategies come from the plugin config
+file (:mod:`.config`, the k8s-device-plugin config shape): a time-sliced GPU is
+advertised as ``<id>::<k>`` replicas, Allocate maps replicas back to the
+physical GPU, and preferred allocation spreads replicas least-loaded first.
+
 The plugin is stateless: kubelet checkpoints assignments.
 """
 
@@ -34,6 +39,7 @@ import grpc
 from .. import RESOURCE_NAME
 from . import api
 from .allocator import from_topology, preferred
+from .config import REPLICA_SEP, DevicePluginConfig
 
 log = logging.getLogger("amdgpu.deviceplugin")
 
@@ -52,6 +58,26 @@ class PluginConfig:
     watch_interval_s: float = 0.5
     rocm_mount: str | None = None
     extra_env: dict = field(default_factory=dict)
+    device_config: DevicePluginConfig | None = None  # config file: flags + sharing
+
+    @property
+    def config(self) -> DevicePluginConfig:
+        return self.device_config or DevicePluginConfig()
+
+    @property
+    def id_strategy(self) -> str:
+        return self.config.flags.deviceIDStrategy
+
+    @property
+    def list_strategies(self) -> list[str]:
+        out = list(self.config.flags.deviceListStrategy)
+        if self.cdi_enabled and "cdi-cri" not in out:  # legacy --cdi flag
+            out.append("cdi-cri")
+        return out
+
+    @property
+    def pass_device_specs(self) -> bool:
+        return self.config.flags.passDeviceSpecs
 
     @property
     def kubelet_path(self) -> str:
@@ -60,6 +86,19 @@ class PluginConfig:
     @property
     def endpoint_path(self) -> str:
         return os.path.join(self.socket_dir, self.endpoint)
+
+
+CONTAINER_DEVICES_DIR = "/var/run/amd-container-devices"  # volume-mounts list strategy (read by the OCI hook)
+
+
+def base_id(dev, strategy: str) -> str:
+    """kubelet device ID of a GPU (or partition) under ``deviceIDStrategy``."""
+    if strategy == "index":
+        return str(dev.index)
+    if strategy == "uuid" and dev.unique_id:
+        u = f"GPU-{dev.unique_id:016x}"
+        return u if dev.partition_count <= 1 else f"{u}-p{dev.partition_index}"
+    return dev.device_id_str
 
 
 def resource_for(dev, cfg: PluginConfig) -> str:
@@ -75,13 +114,24 @@ def resource_for(dev, cfg: PluginConfig) -> str:
 class DevicePluginServer:
     """One kubelet device-plugin endpoint serving one resource name."""
 
-    def __init__(self, cfg: PluginConfig, devices, links=(), resource_name: str | None = None):
+    def __init__(self, cfg: PluginConfig, devices, links=(), resource_name: str | None = None, replicas: int = 1,
+                 fail_requests_gt_one: bool = False):
         self.cfg = cfg
         self.resource_name = resource_name or cfg.resource_name
         self.devices = list(devices)
-        self._by_id = {d.device_id_str: d for d in self.devices}
-        self._health = {d.device_id_str: api.HEALTHY for d in self.devices}
-        self._cost = from_topology(self.devices, links, lambda g: g.device_id_str)
+        self.replicas = max(1, int(replicas))
+        self.fail_requests_gt_one = fail_requests_gt_one and self.replicas > 1
+        self._ids_of: dict[str, list[str]] = {}  # physical key (device_id_str) -> advertised ids
+        self._by_id = {}
+        for d in self.devices:
+            b = base_id(d, cfg.id_strategy)
+            ids = [b] if self.replicas == 1 else [f"{b}{REPLICA_SEP}{k}" for k in range(self.replicas)]
+            self._ids_of[d.device_id_str] = ids
+            for i in ids:
+                self._by_id[i] = d
+        self._order = {d.device_id_str: n for n, d in enumerate(self.devices)}
+        self._health = {i: api.HEALTHY for i in self._by_id}
+        self._cost = from_topology(self.devices, links, lambda g: self._ids_of[g.device_id_str][0])
         self._cv = threading.Condition()
         self._version = 0
         self._stop = threading.Event()
@@ -94,13 +144,18 @@ class DevicePluginServer:
 
     # ------------------------------------------------------------------ health
     def set_health(self, device_id: str, healthy: bool, reason: str = "") -> None:
+        """``device_id``: a physical GPU (every replica of it) or one advertised ID."""
         state = api.HEALTHY if healthy else api.UNHEALTHY
+        ids = self._ids_of.get(device_id) or ([device_id] if device_id in self._health else [])
         with self._cv:
-            if device_id not in self._health or self._health[device_id] == state:
+            ids = [i for i in ids if self._health[i] != state]
+            if not ids:
                 return
-            self._health[device_id] = state
+            for i in ids:
+                self._health[i] = state
             self._version += 1
-            self.events.append({"t": time.time(), "device": device_id, "health": state, "reason": reason})
+            self.events.append({"t": time.time(), "device": device_id, "health": state, "reason": reason,
+                                "ids": len(ids)})
             self._cv.notify_all()
         log.warning("device %s -> %s %s", device_id, state, reason)
 
@@ -112,9 +167,10 @@ class DevicePluginServer:
         with self._cv:
             resp = api.pb["ListAndWatchResponse"]()
             for d in self.devices:
-                dev = resp.devices.add(ID=d.device_id_str, health=self._health[d.device_id_str])
-                if d.numa_node >= 0:
-                    dev.topology.nodes.add(ID=d.numa_node)
+                for i in self._ids_of[d.device_id_str]:
+                    dev = resp.devices.add(ID=i, health=self._health[i])
+                    if d.numa_node >= 0:
+                        dev.topology.nodes.add(ID=d.numa_node)
             return resp, self._version
 
     # ------------------------------------------------------------ gRPC methods
@@ -140,19 +196,57 @@ class DevicePluginServer:
         for creq in request.container_requests:
             with self._cv:
                 avail = [i for i in creq.available_deviceIDs if self._health.get(i) == api.HEALTHY]
-            ids = preferred(self._cost, avail, list(creq.must_include_deviceIDs), creq.allocation_size)
+            must = list(creq.must_include_deviceIDs)
+            if self.replicas > 1:
+                ids = self._preferred_replicas(avail, must, creq.allocation_size)
+            else:
+                ids = preferred(self._cost, avail, must, creq.allocation_size)
             out.container_responses.add(deviceIDs=ids)
         return out
 
+    def _preferred_replicas(self, avail: list[str], must: list[str], size: int) -> list[str]:
+        """Time-sliced GPUs: take replicas from GPUs not yet in this request,
+        then from the GPU with the most free replicas (least loaded), then in
+        device order - N shared pods land on N different GPUs first."""
+        chosen = [i for i in must if i in self._by_id]
+        free: dict[str, list[str]] = {}
+        for i in avail:
+            if i in self._by_id and i not in chosen:
+                free.setdefault(self._by_id[i].device_id_str, []).append(i)
+        in_request: dict[str, int] = {}
+        for i in chosen:
+            k = self._by_id[i].device_id_str
+            in_request[k] = in_request.get(k, 0) + 1
+        while len(chosen) < size and free:
+            k = min(free, key=lambda g: (in_request.get(g, 0), -len(free[g]), self._order[g]))
+            chosen.append(free[k].pop(0))
+            in_request[k] = in_request.get(k, 0) + 1
+            if not free[k]:
+                del free[k]
+        return chosen
+
     def container_response(self, ids):
         r = api.pb["ContainerAllocateResponse"]()
-        devs = [self._by_id[i] for i in ids]
-        r.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
-        for d in devs:
-            r.devices.add(container_path=d.render_node, host_path=d.render_node, permissions="rw")
+        devs = list({self._by_id[i].device_id_str: self._by_id[i] for i in ids}.values())  # replicas -> GPU
+        if self.cfg.pass_device_specs:
+            r.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
+            for d in devs:
+                r.devices.add(container_path=d.render_node, host_path=d.render_node, permissions="rw")
         indices = ",".join(str(d.index) for d in devs)
-        r.envs["AMD_VISIBLE_DEVICES"] = indices
-        r.envs["AMD_GPU_DEVICE_IDS"] = ",".join(ids)
+        strategies = self.cfg.list_strategies
+        if "envvar" in strategies:
+            r.envs["AMD_VISIBLE_DEVICES"] = indices
+            r.envs["AMD_GPU_DEVICE_IDS"] = ",".join(ids)
+        if "volume-mounts" in strategies:  # unprivileged pods cannot forge a mount list (OCI hook reads it)
+            for d in devs:
+                r.mounts.add(container_path=f"{CONTAINER_DEVICES_DIR}/{d.index}", host_path="/dev/null",
+                             read_only=True)
+        if "cdi-annotations" in strategies:
+            key = "cdi.k8s.io/amd-device-plugin_" + "".join(c if c.isalnum() else "-" for c in self.resource_name)
+            r.annotations[key] = ",".join(f"{self.cfg.cdi_kind}={d.index}" for d in devs)
+        if self.replicas > 1:
+            r.annotations["amd.com/gpu.sharing"] = "time-slicing"
+            r.annotations["amd.com/gpu.replicas"] = ",".join(ids)
         for k, v in self.cfg.extra_env.items():
             r.envs[k] = v
         r.annotations["amd.com/gpu.devices"] = indices
@@ -162,7 +256,7 @@ class DevicePluginServer:
             r.annotations["amd.com/gpu.xgmi-hive"] = ",".join(hives)
         if self.cfg.rocm_mount:
             r.mounts.add(container_path=self.cfg.rocm_mount, host_path=self.cfg.rocm_mount, read_only=True)
-        if self.cfg.cdi_enabled:
+        if "cdi-cri" in strategies:
             for d in devs:
                 r.cdi_devices.add(name=f"{self.cfg.cdi_kind}={d.index}")
         return r
@@ -174,6 +268,10 @@ class DevicePluginServer:
             unknown = [i for i in ids if i not in self._by_id]
             if unknown:
                 context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unknown device ids {unknown}")
+            if self.fail_requests_gt_one and len(ids) > 1:
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT,
+                              f"time-sliced {self.resource_name}: request for {len(ids)} replicas, at most 1 allowed "
+                              "(failRequestsGreaterThanOne)")
             with self._cv:
                 bad = [i for i in ids if self._health[i] != api.HEALTHY]
             if bad:
@@ -207,7 +305,10 @@ class DevicePluginServer:
     def _endpoint(self) -> str:
         if self.resource_name == self.cfg.resource_name:
             return self.cfg.endpoint
-        return self.cfg.endpoint.replace(".sock", "-" + self.resource_name.rsplit("-", 1)[-1] + ".sock")
+        tail = self.resource_name[len(self.cfg.resource_name):] if self.resource_name.startswith(
+            self.cfg.resource_name) else self.resource_name
+        tail = "".join(c if c.isalnum() else "-" for c in tail).strip("-")
+        return self.cfg.endpoint.replace(".sock", "-" + tail + ".sock")
 
     def register(self, timeout: float = 5.0) -> None:
         with grpc.insecure_channel("unix:" + self.cfg.kubelet_path) as ch:
@@ -271,17 +372,61 @@ class DevicePluginManager:
         from ..discovery import topology
 
         self.cfg = cfg
+        if cfg.device_config is not None:  # the config file's flags win over the command line
+            cfg.partition_strategy = cfg.device_config.flags.partitionStrategy
         self.devices = devices if devices is not None else topology.enumerate_gpus(cfg.sysfs_root)
         self.links = links if links is not None else topology.links(cfg.sysfs_root)
-        groups: dict[str, list] = {}
-        for d in self.devices:
-            groups.setdefault(resource_for(d, cfg), []).append(d)
-        self.servers = {r: DevicePluginServer(cfg, devs, self.links, r) for r, devs in groups.items()}
+        self.servers = self._build_servers()
         self._health_poll = health_poll
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
+        self._registered = True
+        self._lock = threading.Lock()
+
+    def _build_servers(self) -> dict[str, DevicePluginServer]:
+        """One server per resource name: partition strategy first, then the
+        time-slicing rule of that resource (replicas, optional rename)."""
+        dc = self.cfg.config
+        ts = dc.sharing.timeSlicing
+        groups: dict[str, tuple[list, int]] = {}
+        for d in self.devices:
+            res = resource_for(d, self.cfg)
+            rule = dc.shared_for(res)
+            reps = 1
+            if rule is not None and rule.selects(d):
+                res, reps = dc.shared_name(res, rule), rule.replicas
+            devs, r0 = groups.setdefault(res, ([], reps))
+            if r0 != reps:
+                raise ValueError(f"{res}: GPUs with different replica counts ({r0}, {reps}) need distinct names "
+                                 "(set rename or renameByDefault)")
+            devs.append(d)
+        return {r: DevicePluginServer(self.cfg, devs, self.links, r, replicas=reps,
+                                      fail_requests_gt_one=ts.failRequestsGreaterThanOne)
+                for r, (devs, reps) in groups.items()}
+
+    def reconfigure(self, device_config: DevicePluginConfig | None) -> bool:
+        """Apply a new config file (node label or ConfigMap changed): stop the
+        servers, rebuild them for the new resource layout, register again.
+        Returns False when the config is unchanged."""
+        from .config import dumps
+
+        if dumps(device_config or DevicePluginConfig()) == dumps(self.cfg.config):
+            return False
+        with self._lock:
+            old = self.servers
+            self.cfg.device_config = device_config
+            if device_config is not None:
+                self.cfg.partition_strategy = device_config.flags.partitionStrategy
+            self.servers = self._build_servers()
+            for s in old.values():
+                s.stop()
+            for s in self.servers.values():
+                s.start(register=self._registered)
+        log.info("device-plugin config applied: %s", sorted(self.servers))
+        return True
 
     def start(self, register: bool = True) -> None:
+        self._registered = register
         for s in self.servers.values():
             s.start(register=register)
         if self._health_poll is not None:
@@ -303,11 +448,11 @@ class DevicePluginManager:
                     continue
                 healthy = not ev.critical if ev.kind != "gpu_post_reset" else True
                 if ev.critical or ev.kind == "gpu_post_reset":
-                    for s in self.servers.values():
+                    for s in list(self.servers.values()):
                         s.set_health(d.device_id_str, healthy, f"{ev.kind}: {ev.message}")
 
     def set_health(self, device_id: str, healthy: bool, reason: str = "") -> None:
-        for s in self.servers.values():
+        for s in list(self.servers.values()):
             s.set_health(device_id, healthy, reason)
 
     def stop(self) -> None:

@@ -138,6 +138,23 @@ def gfd_labels(gpus: list[GpuDevice], root: str = "/", prefix: str = "amd.com") 
     return labels
 
 
+def sharing_labels(labels: dict[str, str], plugin_config, resource: str = "amd.com/gpu",
+                   prefix: str = "amd.com") -> dict[str, str]:
+    """GPU-sharing labels from the device-plugin config (deviceplugin/config.py):
+    ``gpu.replicas``, ``gpu.sharing-strategy`` and, when the shared GPUs keep
+    the plain resource name, ``-SHARED`` on the product label (as upstream GFD
+    marks time-sliced GPUs)."""
+    p = f"{prefix}/gpu"
+    out = dict(labels)
+    rule = plugin_config.shared_for(resource) if plugin_config is not None else None
+    replicas = rule.replicas if rule is not None else 1
+    out[f"{p}.replicas"] = str(replicas)
+    out[f"{p}.sharing-strategy"] = "time-slicing" if replicas > 1 else "none"
+    if replicas > 1 and plugin_config.shared_name(resource, rule) == resource and f"{p}.product" in out:
+        out[f"{p}.product"] = label_value(out[f"{p}.product"] + "-SHARED")
+    return out
+
+
 def sync_node_labels(client, node_name: str, desired: dict[str, str], owned_prefixes: tuple[str, ...]) -> dict:
     """Set ``desired`` and remove stale labels under ``owned_prefixes``
     (operator-owned labels are never removed). Returns the applied patch."""

@@ -93,6 +93,13 @@ class FakeKubelet:
                     res.cv.notify_all()
         except grpc.RpcError:
             pass  # plugin went away or channel closed
+        with self._lock:
+            current = self.resources.get(res.name) is res
+        if current:  # endpoint gone without a new registration: kubelet marks its devices unhealthy
+            with res.cv:
+                res.devices = {i: api.UNHEALTHY for i in res.devices}
+                res.updates += 1
+                res.cv.notify_all()
 
     # -------------------------------------------------------------- lifecycle
     def start(self) -> None:

@@ -16,8 +16,13 @@
 //             requested render nodes to linux.devices, allow them in
 //             linux.resources.devices, optionally bind-mount ROCm read-only.
 //             Idempotent.  Requested devices come from --devices, or the
-//             container's AMD_VISIBLE_DEVICES env (set by the device plugin's
-//             Allocate), or the amd.com/gpu.devices annotation.
+//             device plugin's volume-mounts list (/dev/null bind mounts at
+//             /var/run/amd-container-devices/<sel>, with
+//             --accept-volume-mounts), or the container's AMD_VISIBLE_DEVICES
+//             env (set by the device plugin's Allocate; with
+//             --envvar-privileged-only only for containers holding
+//             CAP_SYS_ADMIN, so an unprivileged pod cannot name GPUs it was
+//             not allocated), or the amd.com/gpu.devices annotation.
 //   prestart  OCI hook entry point: reads the container state JSON on stdin
 //             (ociVersion/id/pid/bundle) and runs `apply` on that bundle.
 //
@@ -56,7 +61,11 @@ struct Opts {
   bool mount_rocm = false;
   bool dry_run = false;
   bool partitions = true;
+  bool accept_volume_mounts = false;   // device list from /var/run/amd-container-devices/<sel> mounts
+  bool envvar_privileged_only = false;  // AMD_VISIBLE_DEVICES only from CAP_SYS_ADMIN containers
 };
+
+constexpr const char* kDeviceListDir = "/var/run/amd-container-devices/";
 
 std::string join(const std::string& root, const std::string& rel) {
   std::string r = root.empty() ? "/" : root;
@@ -279,6 +288,33 @@ std::string env_lookup(const mj::Value& spec, const std::string& key) {
   return found ? val : "";
 }
 
+// Device selectors the device plugin passed as mounts (volume-mounts list
+// strategy): destination /var/run/amd-container-devices/<sel>, one per GPU.
+std::string volume_mount_list(const mj::Value& spec) {
+  const mj::Value* mounts = spec.find("mounts");
+  if (!mounts || !mounts->is_array()) return "";
+  const std::string dir = kDeviceListDir;
+  std::string out;
+  for (const mj::Value& m : mounts->arr()) {
+    const mj::Value* d = m.is_object() ? m.find("destination") : nullptr;
+    if (!d || !d->is_string() || d->str().compare(0, dir.size(), dir) != 0) continue;
+    const std::string sel = d->str().substr(dir.size());
+    if (sel.empty() || sel.find('/') != std::string::npos) continue;
+    out += (out.empty() ? "" : ",") + sel;
+  }
+  return out;
+}
+
+bool privileged(const mj::Value& spec) {
+  const mj::Value* proc = spec.find("process");
+  const mj::Value* caps = proc ? proc->find("capabilities") : nullptr;
+  const mj::Value* bounding = caps ? caps->find("bounding") : nullptr;
+  if (!bounding || !bounding->is_array()) return false;
+  for (const mj::Value& c : bounding->arr())
+    if (c.is_string() && c.str() == "CAP_SYS_ADMIN") return true;
+  return false;
+}
+
 void add_device(mj::Value& spec, const DevNode& d) {
   mj::Value& linux_ = spec["linux"];
   mj::Value& devs = linux_["devices"];
@@ -374,7 +410,8 @@ int cmd_apply(const Opts& o) {
     return 1;
   }
   std::string sel = o.devices;
-  if (sel.empty()) sel = env_lookup(spec, "AMD_VISIBLE_DEVICES");
+  if (sel.empty() && o.accept_volume_mounts) sel = volume_mount_list(spec);
+  if (sel.empty() && (!o.envvar_privileged_only || privileged(spec))) sel = env_lookup(spec, "AMD_VISIBLE_DEVICES");
   if (sel.empty()) {
     const mj::Value* ann = spec.find("annotations");
     const mj::Value* a = ann ? ann->find("amd.com/gpu.devices") : nullptr;
@@ -441,7 +478,8 @@ int cmd_prestart(Opts o) {
 void usage() {
   fprintf(stderr,
           "usage: amdgpu-oci-hook {cdi|apply|prestart|--version} [--root DIR] [--bundle DIR] [--devices SEL]\n"
-          "                       [--output FILE] [--rocm-dir DIR] [--mount-rocm] [--kind KIND] [--dry-run]\n");
+          "                       [--output FILE] [--rocm-dir DIR] [--mount-rocm] [--kind KIND] [--dry-run]\n"
+          "                       [--accept-volume-mounts] [--envvar-privileged-only]\n");
 }
 
 }  // namespace
@@ -473,6 +511,8 @@ int main(int argc, char** argv) {
     else if (a == "--kind") ok = next(&o.kind);
     else if (a == "--mount-rocm") o.mount_rocm = true;
     else if (a == "--dry-run") o.dry_run = true;
+    else if (a == "--accept-volume-mounts") o.accept_volume_mounts = true;
+    else if (a == "--envvar-privileged-only") o.envvar_privileged_only = true;
     else ok = false;
     if (!ok) {
       usage();
