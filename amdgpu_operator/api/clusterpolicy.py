@@ -193,6 +193,10 @@ class WorkloadSpec(_M):
     # run the RCCL check (own process, world 1) on a single-GPU node too: the
     # multi-GPU critical path, rehearsed where there is no xGMI peer
     rcclSingleGpu: bool = False
+    # RCCL check in its own process per GPU ("separate", default) or inside the
+    # kernel-check process ("shared": one process start + HIP init fewer, the
+    # RCCL code-object load overlaps the kernel steps)
+    rcclProcess: Literal["separate", "shared"] = "separate"
 
 
 class ValidatorSpec(Operand):

@@ -249,6 +249,8 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         wl_args += ["--counter-gate"]
     if w.rcclSingleGpu:
         wl_args += ["--rccl-single-gpu"]
+    if w.rcclProcess == "shared":
+        wl_args += ["--rccl-shared-process"]
     inits = [_wait_init("driver-validation", image, v.imagePullPolicy, "driver")]
     if v.pluginValidation and spec.devicePlugin.enabled:
         # workload (all GPUs, RCCL over xGMI) and plugin (1-GPU pods through the

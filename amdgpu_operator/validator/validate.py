@@ -157,8 +157,9 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     # N7: the counter gate is a rocprofiler-sdk tool library loaded only into
     # the gated kernel processes (the binary does not link the SDK)
     counter_env = gate_env() if "--counter-gate" in args else {}
-    rccl_single = "--rccl-single-gpu" in args  # validate.py's own flag, not the binary's
-    args = _drop_flag(args, "--rccl-single-gpu")
+    rccl_single = "--rccl-single-gpu" in args  # validate.py's own flags, not the binary's
+    rccl_shared = "--rccl-shared-process" in args
+    args = _drop_flag(_drop_flag(args, "--rccl-single-gpu"), "--rccl-shared-process")
     steps = _steps_of(args)
     kernel_steps = [s for s in steps if s != "rccl"]
     # RCCL runs in its own process per GPU, concurrently with the kernel
@@ -167,8 +168,10 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     # single-GPU node has no collective to validate (no xGMI peer) unless
     # rcclSingleGpu asks for the rehearsal.
     run_rccl = "rccl" in steps and (world > 1 or rccl_single)
+    if run_rccl and rccl_shared:  # one process per GPU runs the kernel checks and RCCL
+        kernel_steps = kernel_steps + ["rccl"]
     jobs = [(r, _with_steps(args, kernel_steps), run_id, counter_env) for r in range(world)]
-    if run_rccl:
+    if run_rccl and not rccl_shared:
         jobs += [(r, _with_steps(_drop_flag(args, "--counter-gate"), ["hip", "rccl"]), run_id + "-rccl", {})
                  for r in range(world)]
 
@@ -201,6 +204,9 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
                 main["stderr"] = rep.get("stderr", "")
         else:
             reports.append(rep)
+    if run_rccl and rccl_shared:
+        for rep in reports:
+            rep["rccl_process_seconds"] = rep.get("process_seconds")
     if "rccl" in steps and not run_rccl:
         for rep in reports:
             rep.setdefault("steps", []).append({"name": "rccl", "ok": True, "skipped": "single GPU: no xGMI peer"})

@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-counter-gate", action="store_true", help="skip the rocprofiler counter gate (outer profiler)")
     ap.add_argument("--rccl-single-gpu", action="store_true",
                     help="rehearsal: run the RCCL validation process at N=1 too (multi-GPU critical path)")
+    ap.add_argument("--rccl-process", choices=["separate", "shared"], default=None,
+                    help="RCCL check in its own process per GPU or in the kernel-check process")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--detail", default=None, help="write per-step breakdown JSON here")
     return ap.parse_args()
@@ -82,6 +84,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
         values = deep_merge(values, {"validator": {"workload": {"counterGate": False}}})
     if args.rccl_single_gpu:
         values = deep_merge(values, {"validator": {"workload": {"rcclSingleGpu": True}}})
+    if args.rccl_process:
+        values = deep_merge(values, {"validator": {"workload": {"rcclProcess": args.rccl_process}}})
     if args.quick_workload:
         values = deep_merge(values, {"validator": {"workload": {"gemmN": 1024, "hbmBytes": 1 << 26,
                                                                 "rcclElems": 1 << 20, "xgmiElems": 1 << 20}}})
