@@ -131,6 +131,14 @@ class ServiceMonitor(_M):
     additionalLabels: dict[str, str] = Field(default_factory=dict)
 
 
+class MetricsConfigRef(_M):
+    """ConfigMap holding a dcgm-exporter style counters CSV (``key``) that
+    selects the exported series; empty ``name`` = every series."""
+
+    name: str = ""
+    key: str = "metrics.csv"
+
+
 class MetricsExporterSpec(Operand):
     """amd-smi based DCGM-exporter equivalent (README.md:204,213)."""
 
@@ -140,6 +148,7 @@ class MetricsExporterSpec(Operand):
     podAttribution: bool = True
     dcgmNames: bool = False  # also emit DCGM_FI_DEV_* series for existing dashboards
     serviceMonitor: ServiceMonitor = Field(default_factory=ServiceMonitor)
+    config: MetricsConfigRef = Field(default_factory=lambda: MetricsConfigRef())
 
 
 class NodeStatusExporterSpec(Operand):

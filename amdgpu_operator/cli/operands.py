@@ -60,6 +60,8 @@ def build_parser() -> argparse.ArgumentParser:
     me.add_argument("--pod-attribution", action="store_true")
     me.add_argument("--dcgm-names", action="store_true")
     me.add_argument("--fixture", default=None, help="serve an amd-smi metric JSON capture instead of live data")
+    me.add_argument("--metrics-config", default=None, help="dcgm-exporter style CSV of series to export")
+    me.add_argument("--metrics-config-map", default=None, help="NAMESPACE/NAME/KEY of a ConfigMap holding that CSV")
 
     ns = sub.add_parser("node-status-exporter", help="validation-status metrics")
     ns.add_argument("--port", type=int, default=8000)
@@ -243,8 +245,25 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                     raise
                 log.info("amd-smi unavailable (%s); serving fixture", e)
                 source = FixtureSource(fx)
+        from ..exporter.metrics import parse_metrics_csv
+
         attribution = PodAttribution(env.pod_resources_socket) if a.pod_attribution else None
-        ex = MetricsExporter(source, env.node_name, a.interval, attribution, a.dcgm_names)
+        selection = None
+        csv_text = None
+        if a.metrics_config:
+            with open(a.metrics_config) as f:
+                csv_text = f.read()
+        elif a.metrics_config_map:
+            ns_, name, key = (a.metrics_config_map.split("/") + ["", "", ""])[:3]
+            csv_text = (_get_or_empty(env.client, "ConfigMap", name, ns_ or env.namespace).get("data") or {}).get(
+                key or "metrics.csv")
+            if csv_text is None:
+                log.error("metrics config %s not found: exporting every series", a.metrics_config_map)
+        if csv_text is not None:
+            selection, unsupported = parse_metrics_csv(csv_text)
+            if unsupported:
+                log.warning("metrics config: no MI355X source for %s", ", ".join(unsupported))
+        ex = MetricsExporter(source, env.node_name, a.interval, attribution, a.dcgm_names, selection)
         ex.collect_once()
         port = 0 if env.extra.get("ephemeral_ports") else a.port
         srv = MetricsHttpServer(ex, "127.0.0.1" if port == 0 else "0.0.0.0", port).start()

@@ -305,6 +305,10 @@ def state_metrics_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict
         args.append("--pod-attribution")
     if m.dcgmNames:
         args.append("--dcgm-names")
+    rbac = []
+    if m.config.name:
+        args += ["--metrics-config-map", f"{ns}/{m.config.name}/{m.config.key}"]
+        rbac = [_cluster_role(sa, PLUGIN_CONFIG_RULES[1:], owner), _cluster_binding(sa, sa, ns, owner)]
     ctr = _container("amd-metrics-exporter", image, m.imagePullPolicy, args + list(m.args),
                      [_mount("pod-resources", "/var/lib/kubelet/pod-resources", ro=True),
                       _mount("host-sys", "/host/sys", ro=True)], list(m.env), True, m.resources.model_dump(),
@@ -312,7 +316,7 @@ def state_metrics_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict
     inits = [_wait_init("driver-validation", image, m.imagePullPolicy, "driver")]
     vols = [_hostpath("pod-resources", "/var/lib/kubelet/pod-resources"), _hostpath("host-sys", "/sys", "Directory"),
             _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
-    objs = [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "dcgmExporter", sa, [ctr], inits, vols),
+    objs = [_sa(sa, ns, owner), *rbac, _daemonset(spec, ns, owner, name, "dcgmExporter", sa, [ctr], inits, vols),
             _service(name, ns, owner, m.port)]
     if m.serviceMonitor.enabled:
         objs.append({"apiVersion": "monitoring.coreos.com/v1", "kind": "ServiceMonitor",

@@ -91,6 +91,21 @@ class _Metrics(ctypes.Structure):
         ("xgmi_links_error", ctypes.c_uint32),
         ("bad_pages", ctypes.c_uint32),
         ("num_processes", ctypes.c_uint32),
+        ("xgmi_read_bytes", ctypes.c_uint64),
+        ("xgmi_write_bytes", ctypes.c_uint64),
+        ("pcie_bandwidth_gbps", ctypes.c_uint64),
+        ("pcie_replay_count", ctypes.c_uint64),
+        ("pcie_nak_sent", ctypes.c_uint64),
+        ("pcie_nak_rcvd", ctypes.c_uint64),
+        ("prochot_residency", ctypes.c_uint64),
+        ("ppt_residency", ctypes.c_uint64),
+        ("socket_thermal_residency", ctypes.c_uint64),
+        ("hbm_thermal_residency", ctypes.c_uint64),
+        ("vram_max_bandwidth_gbps", ctypes.c_uint64),
+        ("xgmi_link_speed_gbps", ctypes.c_uint32),
+        ("pcie_link_width", ctypes.c_uint32),
+        ("pcie_link_speed_mts", ctypes.c_uint32),
+        ("throttle_status", ctypes.c_uint32),
         ("valid_mask", ctypes.c_uint32),
     ]
 
@@ -104,7 +119,8 @@ class _Event(ctypes.Structure):
     ]
 
 
-M_VRAM, M_ACTIVITY, M_POWER, M_TEMP, M_CLOCK, M_ENERGY, M_ECC, M_XGMI, M_BADPAGES, M_PROCS = (1 << i for i in range(10))
+M_VRAM, M_ACTIVITY, M_POWER, M_TEMP, M_CLOCK, M_ENERGY, M_ECC, M_XGMI, M_BADPAGES, M_PROCS, M_GPU_METRICS = (
+    1 << i for i in range(11))
 
 EVENT_NAMES = {
     1: "vm_fault",
@@ -268,6 +284,10 @@ _METRIC_FIELDS = {
     M_XGMI: ("xgmi_links_total", "xgmi_links_up", "xgmi_links_error"),
     M_BADPAGES: ("bad_pages",),
     M_PROCS: ("num_processes",),
+    M_GPU_METRICS: ("xgmi_read_bytes", "xgmi_write_bytes", "pcie_bandwidth_gbps", "pcie_replay_count", "pcie_nak_sent",
+                    "pcie_nak_rcvd", "prochot_residency", "ppt_residency", "socket_thermal_residency",
+                    "hbm_thermal_residency", "vram_max_bandwidth_gbps", "xgmi_link_speed_gbps", "pcie_link_width",
+                    "pcie_link_speed_mts", "throttle_status"),
 }
 
 

@@ -24,7 +24,17 @@ amd_gpu_ecc_uncorrectable_total       DCGM_FI_DEV_ECC_DBE_VOL_TOTAL
 amd_gpu_ecc_correctable_total         DCGM_FI_DEV_ECC_SBE_VOL_TOTAL
 amd_gpu_retired_pages                 DCGM_FI_DEV_RETIRED_DBE
 amd_gpu_xgmi_links_up / _link_errors  DCGM_FI_DEV_NVLINK_* (link health)
+amd_gpu_xgmi_{read,write}_bytes_total (NVLink traffic: per-GPU xGMI bytes)
+amd_gpu_pcie_replay_total             DCGM_FI_DEV_PCIE_REPLAY_COUNTER
+amd_gpu_pcie_link_width               DCGM_FI_DEV_PCIE_LINK_WIDTH
+amd_gpu_throttle_*_residency_total    (DCGM_FI_DEV_*_VIOLATION analogs)
 ====================================  ==================================
+
+Metric selection (``--metrics-config`` / ``dcgmExporter.config``): the
+dcgm-exporter counters CSV format, one ``NAME, type, help`` line per series.
+NAME is an ``amd_gpu_*`` metric or the DCGM field it stands for, so an existing
+dcgm-exporter CSV keeps producing the series its dashboards query; DCGM fields
+with no MI355X source (e.g. ENC/DEC utilisation) are reported and skipped.
 """
 
 from __future__ import annotations
@@ -49,6 +59,7 @@ FIELDS = [
     ("amd_gpu_mm_activity_percent", "mm_activity_pct", "gauge", "Multimedia engine activity (%)", None, 1.0),
     ("amd_gpu_vram_total_bytes", "vram_total_bytes", "gauge", "HBM capacity (bytes)", None, 1.0),
     ("amd_gpu_vram_used_bytes", "vram_used_bytes", "gauge", "HBM in use (bytes)", "DCGM_FI_DEV_FB_USED", 1 / 2**20),
+    ("amd_gpu_vram_free_bytes", "vram_free_bytes", "gauge", "HBM free (bytes)", "DCGM_FI_DEV_FB_FREE", 1 / 2**20),
     ("amd_gpu_power_watts", "socket_power_w", "gauge", "Socket power (W)", "DCGM_FI_DEV_POWER_USAGE", 1.0),
     ("amd_gpu_power_limit_watts", "power_limit_w", "gauge", "Socket power limit (W)", None, 1.0),
     ("amd_gpu_temperature_hotspot_celsius", "temp_hotspot_c", "gauge", "Hotspot temperature (C)",
@@ -69,7 +80,67 @@ FIELDS = [
     ("amd_gpu_xgmi_link_errors", "xgmi_links_error", "gauge", "xGMI links in error", None, 1.0),
     ("amd_gpu_retired_pages", "bad_pages", "gauge", "Retired (bad) HBM pages", "DCGM_FI_DEV_RETIRED_DBE", 1.0),
     ("amd_gpu_processes", "num_processes", "gauge", "Processes using the GPU", None, 1.0),
+    # PMFW metrics table (amdsmi_get_gpu_metrics_info)
+    ("amd_gpu_xgmi_read_bytes_total", "xgmi_read_bytes", "counter", "Bytes read over xGMI, all links", None, 1.0),
+    ("amd_gpu_xgmi_write_bytes_total", "xgmi_write_bytes", "counter", "Bytes written over xGMI, all links", None, 1.0),
+    ("amd_gpu_xgmi_link_speed_gbps", "xgmi_link_speed_gbps", "gauge", "xGMI link bit rate (Gb/s)", None, 1.0),
+    ("amd_gpu_pcie_bandwidth_gbps", "pcie_bandwidth_gbps", "gauge", "PCIe bandwidth, instantaneous (GB/s)", None, 1.0),
+    ("amd_gpu_pcie_replay_total", "pcie_replay_count", "counter", "PCIe replays",
+     "DCGM_FI_DEV_PCIE_REPLAY_COUNTER", 1.0),
+    ("amd_gpu_pcie_nak_sent_total", "pcie_nak_sent", "counter", "PCIe NAKs sent", None, 1.0),
+    ("amd_gpu_pcie_nak_received_total", "pcie_nak_rcvd", "counter", "PCIe NAKs received", None, 1.0),
+    ("amd_gpu_pcie_link_width", "pcie_link_width", "gauge", "PCIe link width (lanes)", "DCGM_FI_DEV_PCIE_LINK_WIDTH",
+     1.0),
+    ("amd_gpu_pcie_link_speed_mts", "pcie_link_speed_mts", "gauge", "PCIe link speed (MT/s)", None, 1.0),
+    ("amd_gpu_throttle_prochot_residency_total", "prochot_residency", "counter", "PROCHOT throttle residency",
+     None, 1.0),
+    ("amd_gpu_throttle_ppt_residency_total", "ppt_residency", "counter", "Package power throttle residency", None,
+     1.0),
+    ("amd_gpu_throttle_socket_thermal_residency_total", "socket_thermal_residency", "counter",
+     "Socket thermal throttle residency", None, 1.0),
+    ("amd_gpu_throttle_hbm_thermal_residency_total", "hbm_thermal_residency", "counter",
+     "HBM thermal throttle residency", None, 1.0),
+    ("amd_gpu_throttle_status", "throttle_status", "gauge", "Throttle status bitmask", None, 1.0),
+    ("amd_gpu_vram_max_bandwidth_gbps", "vram_max_bandwidth_gbps", "gauge", "HBM bandwidth at max memory clock (GB/s)",
+     None, 1.0),
 ]
+# DCGM fields with no MI355X source: accepted in a metrics CSV, reported as unsupported
+DCGM_UNSUPPORTED = {"DCGM_FI_DEV_ENC_UTIL", "DCGM_FI_DEV_DEC_UTIL", "DCGM_FI_DEV_XID_ERRORS",
+                    "DCGM_FI_DEV_VGPU_LICENSE_STATUS", "DCGM_FI_DEV_NVLINK_BANDWIDTH_TOTAL"}
+
+
+@dataclass(frozen=True)
+class Series:
+    name: str
+    field: str
+    type: str
+    help: str
+    scale: float
+
+
+def parse_metrics_csv(text: str) -> tuple[list[Series], list[str]]:
+    """dcgm-exporter counters CSV (``NAME, type, help``; ``#`` comments) ->
+    (series to export, names with no MI355X source)."""
+    by_name = {}
+    for metric, fld, mtype, help_, alias, scale in FIELDS:
+        by_name[metric] = Series(metric, fld, mtype, help_, 1.0)
+        if alias:
+            by_name[alias] = Series(alias, fld, mtype, help_, scale)
+    out, missing = [], []
+    for raw in text.splitlines():
+        line = raw.strip()
+        if not line or line.startswith("#"):
+            continue
+        parts = [p.strip() for p in line.split(",", 2)]
+        name = parts[0]
+        base = by_name.get(name)
+        if base is None:
+            missing.append(name)
+            continue
+        mtype = parts[1] if len(parts) > 1 and parts[1] in ("gauge", "counter") else base.type
+        help_ = parts[2] if len(parts) > 2 and parts[2] else base.help
+        out.append(Series(name, base.field, mtype, help_, base.scale))
+    return out, missing
 
 
 def _esc(v: str) -> str:
@@ -118,6 +189,8 @@ class FixtureSource:
             clock = e.get("clock") or {}
             mem = e.get("mem_usage") or {}
             ecc = e.get("ecc") or {}
+            pcie = e.get("pcie") or {}
+            throttle = e.get("throttle") or {}
             vals = {
                 "gfx_activity_pct": self._v(usage.get("gfx_activity")),
                 "umc_activity_pct": self._v(usage.get("umc_activity")),
@@ -133,6 +206,15 @@ class FixtureSource:
                 "ecc_correctable": self._v(ecc.get("total_correctable_count")) or 0.0,
                 "ecc_uncorrectable": self._v(ecc.get("total_uncorrectable_count")) or 0.0,
                 "ecc_deferred": self._v(ecc.get("total_deferred_count")) or 0.0,
+                "pcie_link_width": self._v(pcie.get("width")),
+                "pcie_link_speed_mts": (self._v(pcie.get("speed")) or 0) * 1000 or None,
+                "pcie_replay_count": self._v(pcie.get("replay_count")),
+                "pcie_nak_sent": self._v(pcie.get("nak_sent_count")),
+                "pcie_nak_rcvd": self._v(pcie.get("nak_received_count")),
+                "prochot_residency": self._v(throttle.get("prochot_accumulated")),
+                "ppt_residency": self._v(throttle.get("ppt_accumulated")),
+                "socket_thermal_residency": self._v(throttle.get("socket_thermal_accumulated")),
+                "hbm_thermal_residency": self._v(throttle.get("hbm_thermal_accumulated")),
             }
             out.append(Sample(i, f"0000:{0x72 + i:02x}:00.0", f"fixture-{i}", "AMD-Instinct-MI355X",
                               {k: v for k, v in vals.items() if v is not None}))
@@ -186,8 +268,9 @@ class PodAttribution:
 
 class MetricsExporter:
     def __init__(self, source, node_name: str = "", interval_s: float = 1.0, attribution: PodAttribution | None = None,
-                 dcgm_names: bool = False):
+                 dcgm_names: bool = False, selection: list[Series] | None = None):
         self.source = source
+        self.selection = selection  # None = every field (plus DCGM aliases with dcgm_names)
         self.node = node_name
         self.interval = interval_s
         self.attribution = attribution
@@ -204,6 +287,10 @@ class MetricsExporter:
         t0 = time.perf_counter()
         try:
             snap = self.source.collect()
+            for smp in snap:
+                v = smp.values
+                if "vram_total_bytes" in v and "vram_used_bytes" in v and "vram_free_bytes" not in v:
+                    smp.values = dict(v, vram_free_bytes=max(0.0, float(v["vram_total_bytes"]) - v["vram_used_bytes"]))
             pods = self.attribution.lookup() if self.attribution else {}
         except Exception as e:  # noqa: BLE001 - keep serving the last snapshot
             self.errors += 1
@@ -222,37 +309,34 @@ class MetricsExporter:
     def stop(self) -> None:
         self._stop.set()
 
+    def _series(self) -> list[Series]:
+        if self.selection is not None:
+            return self.selection
+        out = []
+        for metric, fld, mtype, help_, alias, scale in FIELDS:
+            out.append(Series(metric, fld, mtype, help_, 1.0))
+            if self.dcgm_names and alias:
+                out.append(Series(alias, fld, mtype, help_, scale))
+        return out
+
     def render(self) -> str:
         with self._lock:
             snap, pods = list(self._snapshot), dict(self._pods)
         lines = []
-        for metric, fld, mtype, help_, alias, scale in FIELDS:
-            rows = [s for s in snap if fld in s.values]
+        for ser in self._series():
+            rows = [s for s in snap if ser.field in s.values]
             if not rows:
                 continue
-            names = [(metric, 1.0)] + ([(alias, scale)] if self.dcgm_names and alias else [])
-            for name, sc in names:
-                lines.append(f"# HELP {name} {help_}")
-                lines.append(f"# TYPE {name} {mtype}")
-                for s in rows:
-                    lab = {"gpu": str(s.index), "bdf": s.bdf, "uuid": s.uuid, "product": s.product}
-                    if self.node:
-                        lab["node"] = self.node
-                    pod = pods.get(s.bdf) or next((v for k, v in pods.items() if k.startswith(s.bdf + "-p")), None)
-                    if pod:
-                        lab.update(pod)
-                    lines.append(f"{name}{_labels(lab)} {s.values[fld] * sc:.6g}")
-            if fld == "vram_used_bytes":
-                tot = [s for s in snap if "vram_total_bytes" in s.values]
-                if tot:
-                    lines.append("# HELP amd_gpu_vram_free_bytes HBM free (bytes)")
-                    lines.append("# TYPE amd_gpu_vram_free_bytes gauge")
-                    for s in tot:
-                        lab = {"gpu": str(s.index), "bdf": s.bdf, "uuid": s.uuid, "product": s.product}
-                        if self.node:
-                            lab["node"] = self.node
-                        free = s.values["vram_total_bytes"] - s.values.get("vram_used_bytes", 0)
-                        lines.append(f"amd_gpu_vram_free_bytes{_labels(lab)} {free:.6g}")
+            lines.append(f"# HELP {ser.name} {ser.help}")
+            lines.append(f"# TYPE {ser.name} {ser.type}")
+            for s in rows:
+                lab = {"gpu": str(s.index), "bdf": s.bdf, "uuid": s.uuid, "product": s.product}
+                if self.node:
+                    lab["node"] = self.node
+                pod = pods.get(s.bdf) or next((v for k, v in pods.items() if k.startswith(s.bdf + "-p")), None)
+                if pod:
+                    lab.update(pod)
+                lines.append(f"{ser.name}{_labels(lab)} {s.values[ser.field] * ser.scale:.6g}")
         lines += [
             "# HELP amd_gpu_exporter_collections_total Completed collection passes",
             "# TYPE amd_gpu_exporter_collections_total counter",
@@ -276,6 +360,16 @@ class NodeStatusExporter:
         self.dir = validations_dir
         self.node = node_name
         self.scrapes = 0
+
+    def _series(self) -> list[Series]:
+        if self.selection is not None:
+            return self.selection
+        out = []
+        for metric, fld, mtype, help_, alias, scale in FIELDS:
+            out.append(Series(metric, fld, mtype, help_, 1.0))
+            if self.dcgm_names and alias:
+                out.append(Series(alias, fld, mtype, help_, scale))
+        return out
 
     def render(self) -> str:
         from ..validator.validate import READY_FILES

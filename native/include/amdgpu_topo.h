@@ -107,6 +107,22 @@ typedef struct {
   uint32_t xgmi_links_error;
   uint32_t bad_pages;
   uint32_t num_processes;
+  // amdsmi_get_gpu_metrics_info (PMFW metrics table), AT_M_GPU_METRICS
+  uint64_t xgmi_read_bytes;      // accumulated over every xGMI link (table: KB)
+  uint64_t xgmi_write_bytes;
+  uint64_t pcie_bandwidth_gbps;  // instantaneous PCIe bandwidth (GB/s)
+  uint64_t pcie_replay_count;    // accumulated PCIe replays
+  uint64_t pcie_nak_sent;
+  uint64_t pcie_nak_rcvd;
+  uint64_t prochot_residency;    // throttle residency accumulators (PMFW units)
+  uint64_t ppt_residency;
+  uint64_t socket_thermal_residency;
+  uint64_t hbm_thermal_residency;
+  uint64_t vram_max_bandwidth_gbps;
+  uint32_t xgmi_link_speed_gbps;
+  uint32_t pcie_link_width;
+  uint32_t pcie_link_speed_mts;  // table: 0.1 GT/s
+  uint32_t throttle_status;
   uint32_t valid_mask;          // AT_M_* bits for fields that were read
 } at_metrics_t;
 
@@ -120,6 +136,7 @@ typedef struct {
 #define AT_M_XGMI (1u << 7)
 #define AT_M_BADPAGES (1u << 8)
 #define AT_M_PROCS (1u << 9)
+#define AT_M_GPU_METRICS (1u << 10)
 
 // Opens libamd_smi (dlopen) and initialises it; AT_ERR_UNSUPPORTED when the
 // library or a GPU is unavailable.  Reference-counted, thread-safe.

@@ -66,6 +66,7 @@ static bool load_api(Api* a) {
   sym(a->dl, "amdsmi_set_gpu_event_notification_mask", &a->evt_mask);
   sym(a->dl, "amdsmi_get_gpu_event_notification", &a->evt_get);
   sym(a->dl, "amdsmi_stop_gpu_event_notification", &a->evt_stop);
+  sym(a->dl, "amdsmi_get_gpu_metrics_info", &a->gpu_metrics);
   return true;
 }
 
@@ -88,6 +89,10 @@ static bool enumerate(Api* a) {
 }  // namespace at_smi
 
 using namespace at_smi;
+
+// PMFW table fields read all-ones when the firmware does not report them
+static bool valid64(uint64_t v) { return v != UINT64_MAX; }
+static uint64_t or0(uint64_t v) { return valid64(v) ? v : 0; }
 
 // bounded copy that always NUL-terminates (amd-smi strings may exceed our fields)
 static void copy_str(char* dst, size_t cap, const char* s) {
@@ -251,6 +256,33 @@ AT_API int at_smi_collect(at_metrics_t* out, int max, int* count) {
       if (st == AMDSMI_STATUS_SUCCESS || st == AMDSMI_STATUS_OUT_OF_RESOURCES) {
         m.num_processes = np;
         m.valid_mask |= AT_M_PROCS;
+      }
+    }
+    if (a.gpu_metrics) {
+      // one PMFW table read per GPU: xGMI traffic, PCIe health, throttle residency
+      // (the MI355X counterparts of DCGM's NVLink / PCIe / violation fields)
+      static thread_local amdsmi_gpu_metrics_t gm;
+      memset(&gm, 0, sizeof(gm));
+      if (a.gpu_metrics(h, &gm) == AMDSMI_STATUS_SUCCESS) {
+        m.xgmi_read_bytes = m.xgmi_write_bytes = 0;
+        for (int l = 0; l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l) {
+          if (valid64(gm.xgmi_read_data_acc[l])) m.xgmi_read_bytes += gm.xgmi_read_data_acc[l] * 1024ull;
+          if (valid64(gm.xgmi_write_data_acc[l])) m.xgmi_write_bytes += gm.xgmi_write_data_acc[l] * 1024ull;
+        }
+        m.pcie_bandwidth_gbps = or0(gm.pcie_bandwidth_inst);
+        m.pcie_replay_count = or0(gm.pcie_replay_count_acc);
+        m.pcie_nak_sent = gm.pcie_nak_sent_count_acc == UINT32_MAX ? 0 : gm.pcie_nak_sent_count_acc;
+        m.pcie_nak_rcvd = gm.pcie_nak_rcvd_count_acc == UINT32_MAX ? 0 : gm.pcie_nak_rcvd_count_acc;
+        m.prochot_residency = or0(gm.prochot_residency_acc);
+        m.ppt_residency = or0(gm.ppt_residency_acc);
+        m.socket_thermal_residency = or0(gm.socket_thm_residency_acc);
+        m.hbm_thermal_residency = or0(gm.hbm_thm_residency_acc);
+        m.vram_max_bandwidth_gbps = or0(gm.vram_max_bandwidth);
+        m.xgmi_link_speed_gbps = gm.xgmi_link_speed == UINT16_MAX ? 0 : gm.xgmi_link_speed;
+        m.pcie_link_width = gm.pcie_link_width == UINT16_MAX ? 0 : gm.pcie_link_width;
+        m.pcie_link_speed_mts = gm.pcie_link_speed == UINT16_MAX ? 0 : gm.pcie_link_speed * 100u;
+        m.throttle_status = gm.throttle_status == UINT32_MAX ? 0 : gm.throttle_status;
+        m.valid_mask |= AT_M_GPU_METRICS;
       }
     }
   }

@@ -37,6 +37,7 @@ struct Api {
   amdsmi_status_t (*evt_mask)(amdsmi_processor_handle, uint64_t) = nullptr;
   amdsmi_status_t (*evt_get)(int, uint32_t*, amdsmi_evt_notification_data_t*) = nullptr;
   amdsmi_status_t (*evt_stop)(amdsmi_processor_handle) = nullptr;
+  amdsmi_status_t (*gpu_metrics)(amdsmi_processor_handle, amdsmi_gpu_metrics_t*) = nullptr;
   std::vector<amdsmi_processor_handle> gpus;
 };
 

@@ -133,6 +133,9 @@ def test_smi_collector_and_health_watcher():
         m = smi.collect()[0]
         assert m.values["vram_total_bytes"] > 280 * 2**30
         assert "socket_power_w" in m.values and "temp_hotspot_c" in m.values
+        # PMFW metrics table (amdsmi_get_gpu_metrics_info): PCIe link, xGMI counters, HBM peak bandwidth
+        assert m.values["pcie_link_width"] > 0 and m.values["vram_max_bandwidth_gbps"] > 1000
+        assert "xgmi_read_bytes" in m.values and "ppt_residency" in m.values
         assert smi.partitions(0)[0] in ("SPX", "DPX", "QPX", "CPX", "")
     hw = T.HealthWatcher()
     try:

@@ -113,6 +113,37 @@ def test_metrics_exporter_renders_fixture_with_dcgm_aliases():
             float(val)
 
 
+def test_metrics_exporter_pmfw_fields_from_fixture():
+    ex = MetricsExporter(FixtureSource(FIXTURE, gpus=1), "node-a", dcgm_names=True)
+    ex.collect_once()
+    text = ex.render()
+    assert 'amd_gpu_pcie_link_width{gpu="0",' in text and "DCGM_FI_DEV_PCIE_LINK_WIDTH{" in text
+    assert "amd_gpu_pcie_replay_total{" in text and "DCGM_FI_DEV_PCIE_REPLAY_COUNTER{" in text
+    assert "amd_gpu_throttle_ppt_residency_total{" in text and "DCGM_FI_DEV_FB_FREE{" in text
+
+
+def test_metrics_csv_selects_series_dcgm_names_kept():
+    from amdgpu_operator.exporter.metrics import parse_metrics_csv
+
+    csv = """# Format
+# DCGM FIELD, Prometheus metric type, help message
+DCGM_FI_DEV_GPU_UTIL,      gauge, GPU utilization (in %).
+DCGM_FI_DEV_FB_USED,       gauge, Framebuffer memory used (in MiB).
+DCGM_FI_DEV_ENC_UTIL,      gauge, Encoder utilization (in %).
+amd_gpu_xgmi_read_bytes_total, counter,
+"""
+    sel, missing = parse_metrics_csv(csv)
+    assert [x.name for x in sel] == ["DCGM_FI_DEV_GPU_UTIL", "DCGM_FI_DEV_FB_USED", "amd_gpu_xgmi_read_bytes_total"]
+    assert missing == ["DCGM_FI_DEV_ENC_UTIL"]
+    assert sel[1].scale == 1 / 2**20 and sel[0].help == "GPU utilization (in %)."
+    assert sel[2].help  # empty help column falls back to the built-in one
+    ex = MetricsExporter(FixtureSource(FIXTURE, gpus=2), "n", selection=sel)
+    ex.collect_once()
+    series = {ln.split("{")[0] for ln in ex.render().splitlines() if ln and not ln.startswith("#")}
+    assert "DCGM_FI_DEV_GPU_UTIL" in series and "DCGM_FI_DEV_FB_USED" in series
+    assert "amd_gpu_power_watts" not in series  # not selected
+
+
 def test_pod_attribution_via_pod_resources_api(tmp_path):
     sock = str(tmp_path / "podres" / "kubelet.sock")
     k = FakeKubelet(str(tmp_path / "dp"), sock)
