@@ -206,8 +206,14 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     vols = [_hostpath("run-amd", "/run/amd"), _hostpath("host-root", "/", "Directory"),
             _hostpath("lib-modules", "/lib/modules"), _hostpath("dev", "/dev", "Directory"),
             _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
-    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
-            _daemonset(spec, ns, owner, name, "driver", sa, [ctr, health], [init], vols, host_pid=True)]
+    ds = _daemonset(spec, ns, owner, name, "driver", sa, [ctr, health], [init], vols, host_pid=True)
+    # what the pods install, for the upgrade controller (controller/upgrade.py)
+    from .upgrade import HASH_LABEL, driver_spec_hash
+
+    ds["spec"]["template"]["metadata"]["labels"][HASH_LABEL] = driver_spec_hash(spec)
+    if d.upgradePolicy.autoUpgrade:  # node-by-node rollout driven by the upgrade controller
+        ds["spec"]["updateStrategy"] = {"type": "OnDelete"}
+    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner), ds]
 
 
 def state_toolkit(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:

@@ -215,6 +215,14 @@ class ClusterPolicyReconciler:
             if ready and (gpu_nodes == 0 or not patched):
                 self._ready_at.setdefault(uid, {}).setdefault(state, self.clock() - self._created_at[uid])
 
+        upgrade = None
+        if spec.driver.enabled and spec.driver.upgradePolicy.autoUpgrade and gpu_nodes:
+            from .upgrade import DriverUpgradeController
+
+            try:
+                upgrade = DriverUpgradeController(self.client, self.namespace, self.clock).step(spec)
+            except Exception as e:  # noqa: BLE001 - next pass retries
+                log.warning("driver upgrade pass failed: %s", e)
         overall = "ready" if all(r.ready for r in results) else "notReady"
         if overall == "ready" and patched:
             overall = "notReady"  # node labels just changed: DaemonSet status is stale
@@ -226,7 +234,7 @@ class ClusterPolicyReconciler:
                        if is_gpu_node(n) and (n["metadata"].get("labels") or {}).get(VALIDATED_LABEL) != "true"]
             if pending:
                 overall = "notReady"
-        self._write_status(cp, overall, results, gpu_nodes)
+        self._write_status(cp, overall, results, gpu_nodes, upgrade=upgrade)
         if overall == "ready":
             self._ttr.setdefault(uid, self.clock() - self._created_at[uid])
         res = ReconcileResult(cp["metadata"]["name"], overall, results, gpu_nodes, time.perf_counter() - t0)
@@ -234,7 +242,8 @@ class ClusterPolicyReconciler:
         log.debug("reconciled %s: %s (%.3fs)", res.policy, overall, res.seconds)
         return res
 
-    def _write_status(self, cp: dict, state: str, results: list[StateResult], gpu_nodes: int, error: str = "") -> None:
+    def _write_status(self, cp: dict, state: str, results: list[StateResult], gpu_nodes: int, error: str = "",
+                      upgrade: dict | None = None) -> None:
         uid = cp["metadata"].get("uid", cp["metadata"]["name"])
         try:
             live = self.client.get(CP_API, "ClusterPolicy", cp["metadata"]["name"])
@@ -245,6 +254,8 @@ class ClusterPolicyReconciler:
         status["state"] = state
         status["namespace"] = self.namespace
         status["gpuNodes"] = gpu_nodes
+        if upgrade is not None and (upgrade["nodes"] or "driverUpgrade" in status):
+            status["driverUpgrade"] = upgrade
         status["states"] = {r.name: ("disabled" if not r.enabled else "ready" if r.ready else "notReady")
                             for r in results}
         spans = self._ready_at.get(uid, {})

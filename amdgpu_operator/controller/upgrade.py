@@ -1,0 +1,206 @@
+"""Cluster-wide driver upgrade controller (``driver.upgradePolicy``).
+
+Reference parity: the reference installs the operator with the driver
+DaemonSet enabled (/root/reference/README.md:104) and its pods run the driver
+container (README.md:132-143,212).  Changing the driver version on a running
+cluster must not take every GPU node down at once, so with
+``driver.upgradePolicy.autoUpgrade`` the driver DaemonSet uses ``OnDelete`` and
+this controller walks GPU nodes through the upgrade one bounded batch at a
+time (``maxParallelUpgrades``), tracked in a node label as upstream does::
+
+    upgrade-required -> cordon-required -> pod-deletion-required
+      -> pod-restart-required -> validation-required -> uncordon-required
+      -> upgrade-done                       (or upgrade-failed on timeout)
+
+* outdated = the node's driver pod carries an older ``amd.com/driver-spec-hash``
+  template label than the current driver spec;
+* cordon: ``spec.unschedulable`` (only nodes the operator cordoned are
+  uncordoned again, recorded in an annotation);
+* pod deletion: GPU pods (``amd.com/gpu*`` limits) are evicted when
+  ``drainEnabled``; with it off the node waits until they finish;
+* pod restart: the old driver pod is deleted, the DaemonSet creates the new
+  one, whose ``amd-driver-manager`` init container unloads the old module;
+* validation: the new driver pod is Ready and the node carries
+  ``amd.com/gpu.validated=true`` again (the validator re-ran on the new driver).
+
+The controller is level-triggered: every reconcile recomputes from the node
+labels, so an operator restart resumes mid-upgrade.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import json
+import time
+
+from ..api.clusterpolicy import ClusterPolicySpec
+from ..kube import resources as R
+from ..kube.fakeapi import NotFound
+from ..utils.logs import get_logger
+
+log = get_logger("amdgpu.upgrade")
+
+STATE_LABEL = "amd.com/gpu-driver-upgrade-state"
+HASH_LABEL = "amd.com/driver-spec-hash"
+CORDONED_ANN = "amd.com/gpu-driver-upgrade.cordoned"
+SINCE_ANN = "amd.com/gpu-driver-upgrade.since"
+DRIVER_DS = "amd-driver-daemonset"
+VALIDATOR_DS = "amd-operator-validator"
+
+REQUIRED, CORDON, POD_DELETION, POD_RESTART = ("upgrade-required", "cordon-required", "pod-deletion-required",
+                                               "pod-restart-required")
+VALIDATION, UNCORDON, DONE, FAILED = "validation-required", "uncordon-required", "upgrade-done", "upgrade-failed"
+ACTIVE = (CORDON, POD_DELETION, POD_RESTART, VALIDATION, UNCORDON)
+
+
+def driver_spec_hash(spec: ClusterPolicySpec) -> str:
+    """Identity of what the driver pods install (image, versions, module params)."""
+    d = spec.driver
+    key = {"ref": d.ref("amd-driver"), "rocm": d.rocmVersion, "driver": d.driverVersion,
+           "precompiled": d.usePrecompiled, "params": d.kernelModuleParams, "args": d.args, "env": d.env}
+    return hashlib.sha1(json.dumps(key, sort_keys=True).encode()).hexdigest()[:16]
+
+
+def _uses_gpu(pod: dict) -> bool:
+    for c in (pod.get("spec") or {}).get("containers", []):
+        lim = ((c.get("resources") or {}).get("limits") or {})
+        if any(k.startswith("amd.com/gpu") for k in lim):
+            return True
+    return False
+
+
+class DriverUpgradeController:
+    def __init__(self, client, namespace: str, clock=time.time):
+        self.client = client
+        self.namespace = namespace
+        self.clock = clock
+
+    def _set(self, node: dict, state: str, extra_ann: dict | None = None, unschedulable: bool | None = None) -> None:
+        name = node["metadata"]["name"]
+        patch: dict = {"metadata": {"labels": {STATE_LABEL: state},
+                                    "annotations": {SINCE_ANN: str(round(self.clock(), 3)), **(extra_ann or {})}}}
+        if unschedulable is not None:
+            patch["spec"] = {"unschedulable": unschedulable}
+        self.client.patch("v1", "Node", name, patch)
+        node["metadata"].setdefault("labels", {})[STATE_LABEL] = state
+        node["metadata"].setdefault("annotations", {}).update(patch["metadata"]["annotations"])
+        if unschedulable is not None:
+            node.setdefault("spec", {})["unschedulable"] = unschedulable
+        log.info("driver upgrade %s -> %s", name, state)
+
+    def _driver_pods(self) -> dict[str, dict]:
+        return {p["spec"].get("nodeName"): p for p in self.client.list("v1", "Pod", self.namespace,
+                                                                      label_selector={"app": DRIVER_DS})}
+
+    def step(self, spec: ClusterPolicySpec) -> dict:
+        """One level-triggered pass over every driver node; returns a status summary."""
+        from ..validator.validate import VALIDATED_LABEL
+        from .manifests import DEPLOY_LABEL, OPERAND_LABELS
+
+        pol = spec.driver.upgradePolicy
+        desired = driver_spec_hash(spec)
+        deploy = DEPLOY_LABEL.format(OPERAND_LABELS["driver"])
+        nodes = [n for n in self.client.list("v1", "Node") if (n["metadata"].get("labels") or {}).get(deploy) == "true"]
+        pods = self._driver_pods()
+        now = self.clock()
+        timeout = max(1.0, float(pol.drainTimeoutSeconds))
+
+        def state(n):
+            return (n["metadata"].get("labels") or {}).get(STATE_LABEL, "")
+
+        def since(n):
+            try:
+                return float((n["metadata"].get("annotations") or {}).get(SINCE_ANN, now))
+            except ValueError:
+                return now
+
+        # 1. mark outdated nodes
+        for n in nodes:
+            pod = pods.get(n["metadata"]["name"])
+            outdated = pod is not None and (pod["metadata"].get("labels") or {}).get(HASH_LABEL) != desired
+            if outdated and state(n) in ("", DONE, FAILED):
+                if state(n) == FAILED and now - since(n) < timeout:
+                    continue  # back off before retrying a failed node
+                self._set(n, REQUIRED)
+        # 2. admit a bounded batch
+        active = sum(1 for n in nodes if state(n) in ACTIVE)
+        budget = (pol.maxParallelUpgrades - active) if pol.maxParallelUpgrades > 0 else len(nodes)
+        for n in sorted(nodes, key=lambda x: x["metadata"]["name"]):
+            if budget <= 0:
+                break
+            if state(n) == REQUIRED:
+                self._set(n, CORDON)
+                budget -= 1
+        # 3. advance every active node as far as it can go this pass
+        for n in nodes:
+            name = n["metadata"]["name"]
+            for _ in range(len(ACTIVE)):
+                st = state(n)
+                if st == CORDON:
+                    was = bool((n.get("spec") or {}).get("unschedulable"))
+                    self._set(n, POD_DELETION, {CORDONED_ANN: "false" if was else "true"}, unschedulable=True)
+                elif st == POD_DELETION:
+                    gpu_pods = [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={name}")
+                                if _uses_gpu(p)]
+                    if gpu_pods and pol.drainEnabled:
+                        for p in gpu_pods:
+                            try:
+                                self.client.delete("v1", "Pod", p["metadata"]["name"], p["metadata"].get("namespace"))
+                            except NotFound:
+                                pass
+                        gpu_pods = []
+                    if gpu_pods and now - since(n) > timeout:
+                        if not pol.podDeletionForce:
+                            self._set(n, FAILED, unschedulable=None)
+                            break
+                        for p in gpu_pods:
+                            try:
+                                self.client.delete("v1", "Pod", p["metadata"]["name"], p["metadata"].get("namespace"))
+                            except NotFound:
+                                pass
+                        gpu_pods = []
+                    if gpu_pods:
+                        break  # wait for the workloads to finish
+                    self._set(n, POD_RESTART)
+                elif st == POD_RESTART:
+                    pod = pods.get(name)
+                    if pod is not None and (pod["metadata"].get("labels") or {}).get(HASH_LABEL) != desired:
+                        try:
+                            self.client.delete("v1", "Pod", pod["metadata"]["name"], self.namespace)
+                        except NotFound:
+                            pass
+                    # the node is validated again only by a validator run on the new driver
+                    self.client.patch("v1", "Node", name, {"metadata": {"labels": {VALIDATED_LABEL: None}}})
+                    for vp in self.client.list("v1", "Pod", self.namespace, label_selector={"app": VALIDATOR_DS},
+                                               field_selector=f"spec.nodeName={name}"):
+                        try:
+                            self.client.delete("v1", "Pod", vp["metadata"]["name"], self.namespace)
+                        except NotFound:
+                            pass
+                    self._set(n, VALIDATION)
+                    break  # the DaemonSet controller creates the new pods
+                elif st == VALIDATION:
+                    pod = self._driver_pods().get(name)
+                    fresh = pod is not None and (pod["metadata"].get("labels") or {}).get(HASH_LABEL) == desired
+                    ready = fresh and (R.condition(pod, "Ready") or {}).get("status") == "True"
+                    cur = self.client.get("v1", "Node", name)
+                    validated = (cur["metadata"].get("labels") or {}).get(VALIDATED_LABEL) == "true"
+                    if ready and validated:
+                        self._set(n, UNCORDON)
+                    elif now - since(n) > max(timeout, spec.driver.startupProbeTimeoutSeconds):
+                        self._set(n, FAILED)
+                        break
+                    else:
+                        break
+                elif st == UNCORDON:
+                    ours = (n["metadata"].get("annotations") or {}).get(CORDONED_ANN) == "true"
+                    self._set(n, DONE, unschedulable=False if ours else None)
+                else:
+                    break
+        counts: dict[str, int] = {}
+        for n in self.client.list("v1", "Node"):
+            st = (n["metadata"].get("labels") or {}).get(STATE_LABEL)
+            if st:
+                counts[st] = counts.get(st, 0) + 1
+        return {"desiredHash": desired, "nodes": counts,
+                "inProgress": sum(v for k, v in counts.items() if k in ACTIVE + (REQUIRED,))}

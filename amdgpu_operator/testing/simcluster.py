@@ -92,9 +92,17 @@ class _PodRun:
         self.thread = threading.Thread(target=self._run, daemon=True, name=f"pod-{self.name}")
         self.cleanups: list = []
         self.restarts = 0
+        self._status_lock = threading.Lock()
 
     # ------------------------------------------------------------- status
     def _status(self, phase: str, init_done: bool, reason: str = "", message: str = "") -> None:
+        # containers report readiness from their own threads: compute and write
+        # the status under one lock, or a slower writer's stale view of
+        # self.ready overwrites a newer one (a container ready forever unseen)
+        with self._status_lock:
+            self._status_locked(phase, init_done, reason, message)
+
+    def _status_locked(self, phase: str, init_done: bool, reason: str, message: str) -> None:
         spec = self.pod["spec"]
         ctrs = spec.get("containers", [])
         all_ready = init_done and bool(ctrs) and all(self.ready.get(c["name"]) for c in ctrs)
@@ -344,17 +352,19 @@ class SimCluster:
                     r.get("uid") == ds["metadata"]["uid"] for r in p["metadata"].get("ownerReferences", []))}
                 eligible = [n for n in nodes if self._eligible(ds, n)]
                 want = {n["metadata"]["name"] for n in eligible}
+                on_delete = (ds["spec"].get("updateStrategy") or {}).get("type") == "OnDelete"
                 for node_name, p in pods.items():
                     stale = p["metadata"].get("labels", {}).get("controller-revision-hash") != h
-                    if node_name not in want or stale:
+                    if node_name not in want or (stale and not on_delete):
                         try:
                             self.client.delete("v1", "Pod", p["metadata"]["name"], ns)
                         except NotFound:
                             pass
                 for node_name in want:
                     p = pods.get(node_name)
-                    if p is not None and p["metadata"].get("labels", {}).get("controller-revision-hash") == h:
-                        continue
+                    if p is not None and (on_delete or p["metadata"].get("labels", {}).get(
+                            "controller-revision-hash") == h):
+                        continue  # OnDelete: an outdated pod stays until someone deletes it
                     tmpl = R.deep(ds["spec"]["template"])
                     suffix = hashlib.sha1(f"{name}/{node_name}/{h}".encode()).hexdigest()[:5]
                     pod = {"apiVersion": "v1", "kind": "Pod",
