@@ -190,6 +190,7 @@ class ClusterPolicyReconciler:
         gpu_nodes, patched = label_nodes(self.client, spec)
         owner = owner_ref(cp)
         results: list[StateResult] = []
+        driver_live = None
         for state, key in STATES:
             enabled = key is None or getattr(spec, key).enabled
             objs = STATE_BUILDERS[state](spec, self.namespace, owner)
@@ -203,6 +204,8 @@ class ClusterPolicyReconciler:
             for o in objs:
                 live, action = apply_object(self.client, o)
                 changed += action != "unchanged"
+                if o["kind"] == "DaemonSet" and state == "state-driver":
+                    driver_live = live
                 if o["kind"] == "DaemonSet":
                     ok, d = daemonset_ready(live)
                     gpu_scoped = bool(o["spec"]["template"]["spec"].get("nodeSelector"))
@@ -216,7 +219,8 @@ class ClusterPolicyReconciler:
                 self._ready_at.setdefault(uid, {}).setdefault(state, self.clock() - self._created_at[uid])
 
         upgrade = None
-        if spec.driver.enabled and spec.driver.upgradePolicy.autoUpgrade and gpu_nodes:
+        if spec.driver.enabled and spec.driver.upgradePolicy.autoUpgrade and gpu_nodes and self._upgrade_pending(
+                driver_live):
             from .upgrade import DriverUpgradeController
 
             try:
@@ -241,6 +245,17 @@ class ClusterPolicyReconciler:
         self.metrics.observe(res, self._ready_at.get(uid, {}), self._ttr.get(uid))
         log.debug("reconciled %s: %s (%.3fs)", res.policy, overall, res.seconds)
         return res
+
+    def _upgrade_pending(self, driver_ds: dict | None) -> bool:
+        """Run the upgrade controller only while there is something to do: an
+        outdated driver pod (OnDelete leaves it in place) or a node mid-upgrade."""
+        from .upgrade import DONE, STATE_LABEL
+
+        st = (driver_ds or {}).get("status") or {}
+        if int(st.get("updatedNumberScheduled", 0)) < int(st.get("currentNumberScheduled", 0)):
+            return True
+        return any((n["metadata"].get("labels") or {}).get(STATE_LABEL, DONE) != DONE
+                   for n in self.client.list("v1", "Node"))
 
     def _write_status(self, cp: dict, state: str, results: list[StateResult], gpu_nodes: int, error: str = "",
                       upgrade: dict | None = None) -> None:
