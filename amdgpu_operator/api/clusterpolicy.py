@@ -98,6 +98,7 @@ class ToolkitSpec(Operand):
     # accept-nvidia-visible-devices-as-volume-mounts / -envvar-when-unprivileged)
     acceptDeviceListAsVolumeMounts: bool = False
     acceptEnvvarUnprivileged: bool = True
+    setAsDefault: bool = False  # make the amd runtime containerd's default_runtime_name
 
 
 class DevicePluginConfigRef(_M):
@@ -236,8 +237,16 @@ class DaemonsetsSpec(_M):
     maxUnavailable: str = "1"
 
 
+class PSASpec(_M):
+    """Pod Security Admission: label the operand namespace ``privileged`` (the
+    driver, toolkit and plugin pods need host access)."""
+
+    enabled: bool = False
+
+
 class ClusterPolicySpec(_M):
     operator: OperatorSpec = Field(default_factory=OperatorSpec)
+    psa: PSASpec = Field(default_factory=PSASpec)
     daemonsets: DaemonsetsSpec = Field(default_factory=DaemonsetsSpec)
     driver: DriverSpec = Field(default_factory=DriverSpec)
     toolkit: ToolkitSpec = Field(default_factory=ToolkitSpec)

@@ -143,7 +143,8 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                        cdi_enabled=not a.no_cdi and cenv.get("CDI_ENABLED", "true") == "true",
                        mount_rocm=a.mount_rocm or cenv.get("MOUNT_ROCM") == "true",
                        args=tk.hook_args(cenv.get("ACCEPT_DEVICE_LIST_AS_VOLUME_MOUNTS") == "true",
-                                         cenv.get("ACCEPT_ENVVAR_UNPRIVILEGED", "true") == "true"))
+                                         cenv.get("ACCEPT_ENVVAR_UNPRIVILEGED", "true") == "true"),
+                       set_as_default=cenv.get("CONTAINERD_SET_AS_DEFAULT") == "true")
             ready()
             stop.wait()
         else:

@@ -91,16 +91,25 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
 
     for n in gpu_nodes:
         name = n["metadata"]["name"]
-        alloc = ((n.get("status") or {}).get("allocatable") or {}).get(RESOURCE_NAME, "0")
-        try:
-            count = int(alloc)
-        except ValueError:
-            count = 0
-        want = expect_gpus_per_node
-        ok = count > 0 and (want is None or count == want)
-        rep.add(f"allocatable[{name}]", ok, f"{RESOURCE_NAME}={count}" + (f" (expected {want})" if want else ""),
-                "README.md:122")
         labels = n["metadata"].get("labels") or {}
+        # amd.com/gpu, partition (-cpx ...) and time-sliced (.shared / renamed) resources all count;
+        # time-slicing multiplies the advertised devices by the replicas GFD publishes
+        allocs = (n.get("status") or {}).get("allocatable") or {}
+        count = 0
+        for k, v in allocs.items():
+            if k == RESOURCE_NAME or k.startswith((RESOURCE_NAME + "-", RESOURCE_NAME + ".")):
+                try:
+                    count += int(v)
+                except ValueError:
+                    pass
+        try:
+            replicas = max(1, int(labels.get("amd.com/gpu.replicas", "1")))
+        except ValueError:
+            replicas = 1
+        want = expect_gpus_per_node * replicas if expect_gpus_per_node else None
+        ok = count > 0 and (want is None or count == want)
+        rep.add(f"allocatable[{name}]", ok, f"{RESOURCE_NAME}*={count}" + (f" (expected {want})" if want else ""),
+                "README.md:122")
         # what the reference reads off `nvidia-smi` in the driver container
         # (README.md:152-166: product, memory, GPU count) comes from GFD labels
         prod, mem, arch = (labels.get("amd.com/gpu.product"), labels.get("amd.com/gpu.memory"),

@@ -226,6 +226,7 @@ def state_toolkit(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
            {"name": "CDI_SPEC_DIR", "value": t.cdi.specDir}, {"name": "MOUNT_ROCM", "value": str(t.mountRocm).lower()},
            {"name": "ACCEPT_DEVICE_LIST_AS_VOLUME_MOUNTS", "value": str(t.acceptDeviceListAsVolumeMounts).lower()},
            {"name": "ACCEPT_ENVVAR_UNPRIVILEGED", "value": str(t.acceptEnvvarUnprivileged).lower()},
+           {"name": "CONTAINERD_SET_AS_DEFAULT", "value": str(t.setAsDefault).lower()},
            ] + list(t.env)
     mounts = [_mount("containerd-config", "/runtime/config-dir"), _mount("containerd-socket", "/runtime/sock-dir"),
               _mount("install-dir", t.installDir), _mount("cdi-dir", t.cdi.specDir),

@@ -187,6 +187,8 @@ class ClusterPolicyReconciler:
             self.metrics.observe(res, {}, None)
             return res
 
+        if spec.psa.enabled:
+            self._label_namespace_psa()
         gpu_nodes, patched = label_nodes(self.client, spec)
         owner = owner_ref(cp)
         results: list[StateResult] = []
@@ -245,6 +247,17 @@ class ClusterPolicyReconciler:
         self.metrics.observe(res, self._ready_at.get(uid, {}), self._ttr.get(uid))
         log.debug("reconciled %s: %s (%.3fs)", res.policy, overall, res.seconds)
         return res
+
+    PSA_LABELS = {f"pod-security.kubernetes.io/{mode}": "privileged" for mode in ("enforce", "audit", "warn")}
+
+    def _label_namespace_psa(self) -> None:
+        try:
+            ns = self.client.get("v1", "Namespace", self.namespace)
+        except NotFound:
+            return
+        labels = ns["metadata"].get("labels") or {}
+        if any(labels.get(k) != v for k, v in self.PSA_LABELS.items()):
+            self.client.patch("v1", "Namespace", self.namespace, {"metadata": {"labels": self.PSA_LABELS}})
 
     def _upgrade_pending(self, driver_ds: dict | None) -> bool:
         """Run the upgrade controller only while there is something to do: an

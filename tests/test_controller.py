@@ -224,3 +224,20 @@ def test_operator_metrics_endpoint(env):
     assert samples["amd_gpu_operator_policy_ready"] == "1"
     assert float(samples["amd_gpu_operator_time_to_ready_seconds"]) >= 0
     assert 'amd_gpu_operator_state_ready_seconds{state="state-driver"}' in samples
+
+
+def test_psa_labels_operand_namespace(env):
+    c, rec = env
+    c.create(cluster_policy(spec={"psa": {"enabled": True}}))
+    rec.reconcile()
+    labels = c.get("v1", "Namespace", NS)["metadata"]["labels"]
+    assert labels["pod-security.kubernetes.io/enforce"] == "privileged"
+    assert labels["pod-security.kubernetes.io/warn"] == "privileged"
+
+
+def test_toolkit_set_as_default_runtime():
+    from amdgpu_operator.toolkit.install import dropin_config
+
+    txt = dropin_config("amd", "/usr/local/amd/amdgpu-oci-hook", "/var/run/cdi", set_as_default=True)
+    assert 'default_runtime_name = "amd"' in txt
+    assert "default_runtime_name" not in dropin_config("amd", "/h", "/var/run/cdi")

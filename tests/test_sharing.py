@@ -273,5 +273,9 @@ def test_node_label_switches_plugin_config_in_cluster(tmp_path):
             time.sleep(0.1)
         assert n["status"]["allocatable"]["amd.com/gpu"] == "8"
         assert n["metadata"]["labels"]["amd.com/gpu.sharing-strategy"] == "time-slicing"
+        from amdgpu_operator.cli.verify import verify
+
+        rep = verify(c.client, c.namespace, expect_gpus_per_node=2)  # 2 GPUs x 4 replicas
+        assert rep.ok, rep.table()
     finally:
         c.stop()
