@@ -75,6 +75,9 @@ class DriverSpec(Operand):
     repository: str = ""  # package mirror for air-gapped clusters (default repo.radeon.com)
     startupProbeTimeoutSeconds: int = 600
     upgradePolicy: UpgradePolicy = Field(default_factory=UpgradePolicy)
+    # per-node-pool drivers: one driver DaemonSet per AMDGPUDriver object
+    # (api/driver_cr.py) instead of the single ClusterPolicy-wide one
+    useDriverCRD: bool = False
 
 
 class CDISpec(_M):

@@ -177,9 +177,10 @@ def state_prerequisites(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     return objs
 
 
-def state_driver(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-driver-daemonset",
+                 node_selector: dict | None = None) -> list[dict]:
     d = spec.driver
-    name, sa = "amd-driver-daemonset", "amd-driver"
+    sa = "amd-driver"
     image = d.ref("amd-driver")
     env = [{"name": "ROCM_VERSION", "value": d.rocmVersion}, {"name": "AMDGPU_DRIVER_VERSION", "value": d.driverVersion},
            {"name": "AMDGPU_USE_PRECOMPILED", "value": str(d.usePrecompiled).lower()},
@@ -206,12 +207,16 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     vols = [_hostpath("run-amd", "/run/amd"), _hostpath("host-root", "/", "Directory"),
             _hostpath("lib-modules", "/lib/modules"), _hostpath("dev", "/dev", "Directory"),
             _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
-    ds = _daemonset(spec, ns, owner, name, "driver", sa, [ctr, health], [init], vols, host_pid=True)
+    sel = None
+    if node_selector is not None:  # AMDGPUDriver pool: the driver deploy label plus the pool's selector
+        sel = {DEPLOY_LABEL.format(OPERAND_LABELS["driver"]): "true", **node_selector}
+    ds = _daemonset(spec, ns, owner, name, "driver", sa, [ctr, health], [init], vols, host_pid=True,
+                    node_selector=sel)
     # what the pods install, for the upgrade controller (controller/upgrade.py)
     from .upgrade import HASH_LABEL, driver_spec_hash
 
     ds["spec"]["template"]["metadata"]["labels"][HASH_LABEL] = driver_spec_hash(spec)
-    if d.upgradePolicy.autoUpgrade:  # node-by-node rollout driven by the upgrade controller
+    if d.upgradePolicy.autoUpgrade and node_selector is None:  # node-by-node rollout (controller/upgrade.py)
         ds["spec"]["updateStrategy"] = {"type": "OnDelete"}
     return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner), ds]
 
@@ -388,6 +393,54 @@ def state_node_status_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[
     vols = [_hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
     return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "nodeStatusExporter", sa, [ctr], [], vols),
             _service(name, ns, owner, n.port)]
+
+
+def state_driver_pools(spec: ClusterPolicySpec, ns: str, owner, drivers: list[dict],
+                       nodes: list[dict]) -> tuple[list[dict], dict[str, dict]]:
+    """``driver.useDriverCRD``: one driver DaemonSet per AMDGPUDriver object
+    (api/driver_cr.py), owned by it.  Returns (objects, status per object);
+    GPU nodes selected by more than one object are reported, not deployed."""
+    from ..api.driver_cr import AMDGPUDriverSpec
+
+    deploy = DEPLOY_LABEL.format(OPERAND_LABELS["driver"])
+    gpu_nodes = [n for n in nodes if (n["metadata"].get("labels") or {}).get(deploy) == "true"]
+    parsed, statuses = {}, {}
+    for cr in drivers:
+        name = cr["metadata"]["name"]
+        try:
+            parsed[name] = AMDGPUDriverSpec.model_validate(cr.get("spec") or {})
+        except ValueError as e:
+            statuses[name] = {"state": "error", "message": str(e).splitlines()[0], "nodeCount": 0, "nodes": []}
+    matches: dict[str, list[str]] = {}
+    for n in gpu_nodes:
+        labels = n["metadata"].get("labels") or {}
+        for name, dspec in parsed.items():
+            if all(labels.get(k) == v for k, v in dspec.nodeSelector.items()):
+                matches.setdefault(n["metadata"]["name"], []).append(name)
+    conflicts = {node: crs for node, crs in matches.items() if len(crs) > 1}
+    objs: list[dict] = []
+    for cr in drivers:
+        name = cr["metadata"]["name"]
+        if name not in parsed:
+            continue
+        mine = sorted(node for node, crs in matches.items() if crs == [name])
+        clash = sorted(node for node, crs in conflicts.items() if name in crs)
+        if clash:
+            statuses[name] = {"state": "error", "nodeCount": len(mine), "nodes": mine,
+                              "message": f"nodes selected by more than one AMDGPUDriver: {clash}"}
+            continue
+        pool_spec = spec.model_copy(update={"driver": parsed[name]})
+        pool_objs = state_driver(pool_spec, ns, owner, name=f"amd-driver-daemonset-{name}",
+                                 node_selector=parsed[name].nodeSelector)
+        for o in pool_objs:
+            if o["kind"] == "DaemonSet":  # the pool's DaemonSet goes with its AMDGPUDriver
+                o["metadata"]["ownerReferences"] = owner_ref({**cr, "apiVersion": cr.get("apiVersion", "amd.com/v1"),
+                                                              "kind": "AMDGPUDriver"})
+                objs.append(o)
+            elif not any(x["kind"] == o["kind"] and x["metadata"]["name"] == o["metadata"]["name"] for x in objs):
+                objs.append(o)  # shared RBAC, owned by the ClusterPolicy
+        statuses[name] = {"state": "pending", "nodeCount": len(mine), "nodes": mine, "message": ""}
+    return objs, statuses
 
 
 STATE_BUILDERS = {

@@ -193,9 +193,14 @@ class ClusterPolicyReconciler:
         owner = owner_ref(cp)
         results: list[StateResult] = []
         driver_live = None
+        pool_status = None
+        ds_ready: dict[str, bool] = {}
         for state, key in STATES:
             enabled = key is None or getattr(spec, key).enabled
             objs = STATE_BUILDERS[state](spec, self.namespace, owner)
+            if state == "state-driver" and enabled and spec.driver.useDriverCRD:
+                self._delete_objects([o for o in objs if o["kind"] == "DaemonSet"])  # the policy-wide one
+                objs, pool_status = self._driver_pools(spec, owner)
             if not enabled:
                 self._delete_objects(objs)
                 results.append(StateResult(state, False, True, 0, 0, "disabled"))
@@ -210,12 +215,16 @@ class ClusterPolicyReconciler:
                     driver_live = live
                 if o["kind"] == "DaemonSet":
                     ok, d = daemonset_ready(live)
+                    ds_ready[o["metadata"]["name"]] = ok
                     gpu_scoped = bool(o["spec"]["template"]["spec"].get("nodeSelector"))
                     if ok and gpu_scoped and gpu_nodes > 0 and int((live.get("status") or {}).get(
                             "desiredNumberScheduled", 0)) == 0:
                         ok, d = False, "not yet scheduled on the GPU nodes"
                     ready &= ok
                     detail.append(f"{o['metadata']['name']}: {d}")
+            if state == "state-driver" and pool_status is not None:
+                self._write_pool_status(pool_status, ds_ready)
+                ready &= all(st["state"] != "error" for st in pool_status.values())
             results.append(StateResult(state, True, ready, len(objs), changed, "; ".join(detail)))
             if ready and (gpu_nodes == 0 or not patched):
                 self._ready_at.setdefault(uid, {}).setdefault(state, self.clock() - self._created_at[uid])
@@ -247,6 +256,28 @@ class ClusterPolicyReconciler:
         self.metrics.observe(res, self._ready_at.get(uid, {}), self._ttr.get(uid))
         log.debug("reconciled %s: %s (%.3fs)", res.policy, overall, res.seconds)
         return res
+
+    def _driver_pools(self, spec, owner) -> tuple[list[dict], dict]:
+        from .manifests import state_driver_pools
+
+        drivers = self.client.list(CP_API, "AMDGPUDriver")
+        return state_driver_pools(spec, self.namespace, owner, drivers, self.client.list("v1", "Node"))
+
+    def _write_pool_status(self, statuses: dict[str, dict], ds_ready: dict[str, bool]) -> None:
+        """AMDGPUDriver status: ready when its DaemonSet is (readiness from this pass)."""
+        for name, st in statuses.items():
+            if st["state"] == "pending":
+                st["state"] = "ready" if ds_ready.get(f"amd-driver-daemonset-{name}") else "notReady"
+            try:
+                live = self.client.get(CP_API, "AMDGPUDriver", name)
+            except NotFound:
+                continue
+            if live.get("status") != st:
+                live["status"] = st
+                try:
+                    self.client.update_status(live)
+                except Exception as e:  # noqa: BLE001
+                    log.warning("AMDGPUDriver %s status: %s", name, e)
 
     PSA_LABELS = {f"pod-security.kubernetes.io/{mode}": "privileged" for mode in ("enforce", "audit", "warn")}
 
@@ -311,7 +342,8 @@ class ClusterPolicyReconciler:
         """Watch-driven loop: ClusterPolicy, Node, DaemonSet and Pod events in the
         operand namespace trigger a (debounced) reconcile; plus periodic resync."""
         events: queue.Queue = queue.Queue()
-        watches = [(CP_API, "ClusterPolicy", None), ("v1", "Node", None), ("apps/v1", "DaemonSet", self.namespace)]
+        watches = [(CP_API, "ClusterPolicy", None), ("v1", "Node", None), ("apps/v1", "DaemonSet", self.namespace),
+                   (CP_API, "AMDGPUDriver", None)]
         threads = []
         for av, kind, ns in watches:
             th = threading.Thread(target=self._pump, args=(av, kind, ns, events, stop), daemon=True,
@@ -360,6 +392,12 @@ def cleanup_crd(client, crd_name: str = f"clusterpolicies.{API_GROUP}") -> bool:
             client.delete(CP_API, "ClusterPolicy", cp["metadata"]["name"])
         except NotFound:
             pass
+    try:  # AMDGPUDriver objects and their CRD go too (driver.useDriverCRD)
+        for d in client.list(CP_API, "AMDGPUDriver"):
+            client.delete(CP_API, "AMDGPUDriver", d["metadata"]["name"])
+        client.delete("apiextensions.k8s.io/v1", "CustomResourceDefinition", f"amdgpudrivers.{API_GROUP}")
+    except NotFound:
+        pass
     try:
         client.delete("apiextensions.k8s.io/v1", "CustomResourceDefinition", crd_name)
         return True

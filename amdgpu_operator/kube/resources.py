@@ -56,6 +56,7 @@ _TYPES = [
     ResourceType("apiextensions.k8s.io", "v1", "CustomResourceDefinition", "customresourcedefinitions", False),
     ResourceType("monitoring.coreos.com", "v1", "ServiceMonitor", "servicemonitors", True),
     ResourceType("amd.com", "v1", "ClusterPolicy", "clusterpolicies", False),
+    ResourceType("amd.com", "v1", "AMDGPUDriver", "amdgpudrivers", False),
 ]
 
 REGISTRY: dict[tuple[str, str], ResourceType] = {(t.api_version, t.kind): t for t in _TYPES}
