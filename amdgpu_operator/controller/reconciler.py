@@ -25,7 +25,6 @@ containers, not by the reconciler, so every state is applied on every pass
 
 from __future__ import annotations
 
-import logging
 import queue
 import threading
 import time
