@@ -199,7 +199,11 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             "deviceListStrategy": [x for x in a.device_list_strategy.split(",") if x],
             "passDeviceSpecs": not a.no_device_specs}})
 
-        key, dcfg = load_config()
+        try:
+            key, dcfg = load_config()
+        except (KeyError, ValueError) as e:  # bad label / config: serve the command-line config, say why
+            log.error("device-plugin config: %s; serving the command-line flags", e)
+            key, dcfg = "", cli_config
         cfg = PluginConfig(resource_name=a.resource_name, socket_dir=env.device_plugin_dir, sysfs_root=env.sysfs_root(),
                            cdi_enabled=a.cdi, partition_strategy=a.partition_strategy, health_poll_ms=a.health_poll_ms,
                            watch_interval_s=max(0.05, min(0.5, env.poll_s * 10)), device_config=dcfg)

@@ -279,3 +279,17 @@ def test_node_label_switches_plugin_config_in_cluster(tmp_path):
         assert rep.ok, rep.table()
     finally:
         c.stop()
+
+
+def test_unknown_config_key_falls_back_to_command_line_flags(tmp_path):
+    c = SimCluster(str(tmp_path / "c"), [NodeSpec("gpu-1", 2)], fake_gpu=True).start()
+    try:
+        c.client.patch("v1", "Node", "gpu-1", {"metadata": {"labels": {DC.CONFIG_LABEL: "no-such-key"}}})
+        c.client.create({"apiVersion": "v1", "kind": "ConfigMap",
+                         "metadata": {"name": "plugin-config", "namespace": c.namespace}, "data": {"shared4": SHARED4}})
+        values = deep_merge(parse_set_flags(REFERENCE_SET_FLAGS),
+                            {"devicePlugin": {"config": {"name": "plugin-config"}}})
+        c.install_operator(values)
+        c.wait_ready(60, {"gpu-1": 2})  # plugin serves unshared GPUs instead of crash-looping
+    finally:
+        c.stop()
