@@ -52,6 +52,8 @@ def _lib() -> ctypes.CDLL:
         "avk_max_abs_diff_f32": ([P, P, I64, P, S], I),
         "avk_allreduce_oneshot_f32": ([ctypes.POINTER(P), I, P, I64, S], I),
         "avk_allreduce_twoshot_f32": ([ctypes.POINTER(P), ctypes.POINTER(P), I, I, I64, S], I),
+        "avk_fill_const": ([P, I64, I, ctypes.c_float, S], I),
+        "avk_check_blocks": ([P, I64, I, I64, ctypes.c_float, ctypes.c_float, P, S], I),
         "avk_mfma_probe_count": ([], I),
         "avk_mfma_probe_name": ([I], ctypes.c_char_p),
         "avk_mfma_probe": ([I, U64, ctypes.POINTER(I), S], I),
@@ -267,6 +269,30 @@ def allreduce_twoshot_slice(in_ptrs, out_ptrs, rank: int, count: int, stream=Non
         raise ValueError("bad peer tables")
     _check(_lib().avk_allreduce_twoshot_f32(_ptr_array([int(p) for p in in_ptrs]), _ptr_array([int(p) for p in out_ptrs]),
                                             len(in_ptrs), rank, count, _stream(stream)), "allreduce_twoshot")
+
+
+def _f32_or_bf16(x, name: str) -> int:
+    import torch
+
+    _require(x, x.dtype if x.dtype in (torch.float32, torch.bfloat16) else torch.float32, name)
+    return int(x.dtype == torch.bfloat16)
+
+
+def fill_const(x, value: float, stream=None) -> None:
+    """Fill an fp32 or bf16 tensor with ``value`` on the device (RCCL-step operands)."""
+    bf16 = _f32_or_bf16(x, "x")
+    _check(_lib().avk_fill_const(x.data_ptr(), x.numel(), bf16, float(value), _stream(stream)), "fill_const")
+
+
+def check_blocks(x, block: int, base: float, step: float, stream=None) -> int:
+    """Count elements with x[i] != base + (i // block) * step (device-side check)."""
+    import torch
+
+    bf16 = _f32_or_bf16(x, "x")
+    bad = torch.zeros(1, dtype=torch.int64, device=x.device)
+    _check(_lib().avk_check_blocks(x.data_ptr(), x.numel(), bf16, int(block), float(base), float(step),
+                                   bad.data_ptr(), _stream(stream)), "check_blocks")
+    return int(bad.item())
 
 
 def mfma_probe(seed: int = 1, stream=None) -> dict[str, int]:

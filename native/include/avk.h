@@ -25,6 +25,9 @@ int avk_max_abs_diff_f32(const float* a, const float* b, int64_t n, unsigned int
 int avk_allreduce_oneshot_f32(const float* const* ptrs, int np, float* out, int64_t count, hipStream_t s);
 int avk_allreduce_twoshot_f32(const float* const* in_ptrs, float* const* out_ptrs, int np, int rank, int64_t count,
                               hipStream_t s);
+int avk_fill_const(void* x, int64_t n, int is_bf16, float value, hipStream_t s);
+int avk_check_blocks(const void* x, int64_t n, int is_bf16, int64_t block, float base, float step,
+                     unsigned long long* bad_dev, hipStream_t s);
 int avk_mfma_probe_count(void);
 const char* avk_mfma_probe_name(int kind);
 int avk_mfma_probe(int kind, uint64_t seed, int* mismatches, hipStream_t s);

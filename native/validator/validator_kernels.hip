@@ -123,6 +123,39 @@ __global__ __launch_bounds__(256) void vector_add_verify_kernel(const float* __r
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, m);
 }
 
+// ------------------------------------------- collective operand fill / check ----
+// The RCCL step's operands are filled and checked on the device: rank r fills
+// r+1, and element i of a result must equal base + (i / block) * step (a
+// constant for all-reduce / reduce-scatter, the source rank's value for
+// all-gather).  No host round trip of the 64 MB buffers.
+template <typename T>
+__global__ __launch_bounds__(256) void fill_const_kernel(T* __restrict__ x, int64_t n, T v) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (; i < n; i += stride) x[i] = v;
+}
+
+// f32: exact compare; bf16 (is_bf16): compare the bit pattern of the expected
+// value rounded to bf16 (exact for the small integers used)
+template <bool kBf16>
+__global__ __launch_bounds__(256) void check_blocks_kernel(const void* __restrict__ x, int64_t n, int64_t block,
+                                                           float base, float step, unsigned long long* __restrict__ bad) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  unsigned long long m = 0;
+  for (; i < n; i += stride) {
+    const float want = base + (float)(i / block) * step;
+    if constexpr (kBf16) {
+      m += static_cast<const uint16_t*>(x)[i] != (uint16_t)(__float_as_uint(want) >> 16);
+    } else {
+      m += static_cast<const float*>(x)[i] != want;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m += __shfl_xor(m, off, 64);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, m);
+}
+
 // --------------------------------------------------------- K2 bf16 MFMA GEMM ----
 //
 // C[M][N] = A[M][K] · Bt[N][K]^T   (both operands K-contiguous, "NT")
@@ -1228,6 +1261,28 @@ AVK_API int avk_vector_add_verify_f32(const float* a, const float* b, const floa
   hipError_t e = hipMemsetAsync(bad_dev, 0, sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
   vector_add_verify_kernel<<<grid_for(n, 256, 4096), 256, 0, s>>>(a, b, c, n, bad_dev);
+  return hipGetLastError();
+}
+
+AVK_API int avk_fill_const(void* x, int64_t n, int is_bf16, float value, hipStream_t s) {
+  if (!x || n <= 0) return hipErrorInvalidValue;
+  if (is_bf16)
+    fill_const_kernel<uint16_t><<<grid_for(n, 256, 4096), 256, 0, s>>>(static_cast<uint16_t*>(x), n,
+                                                                       (uint16_t)(__builtin_bit_cast(uint32_t, value) >> 16));
+  else
+    fill_const_kernel<float><<<grid_for(n, 256, 4096), 256, 0, s>>>(static_cast<float*>(x), n, value);
+  return hipGetLastError();
+}
+
+AVK_API int avk_check_blocks(const void* x, int64_t n, int is_bf16, int64_t block, float base, float step,
+                             unsigned long long* bad_dev, hipStream_t s) {
+  if (!x || !bad_dev || n <= 0 || block <= 0) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(bad_dev, 0, sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  if (is_bf16)
+    check_blocks_kernel<true><<<grid_for(n, 256, 4096), 256, 0, s>>>(x, n, block, base, step, bad_dev);
+  else
+    check_blocks_kernel<false><<<grid_for(n, 256, 4096), 256, 0, s>>>(x, n, block, base, step, bad_dev);
   return hipGetLastError();
 }
 

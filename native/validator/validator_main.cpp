@@ -614,13 +614,6 @@ float time_collective(hipStream_t st, int iters, F launch) {
   return ms / iters;
 }
 
-// bf16 bit pattern of a float that bf16 holds exactly (small integers here)
-uint16_t bf16_bits(float f) {
-  uint32_t u;
-  memcpy(&u, &f, 4);
-  return (uint16_t)(u >> 16);
-}
-
 // RCCL over xGMI: fp32 + bf16 all-reduce, all-gather and reduce-scatter, each
 // checked exactly (rank r contributes r+1) and timed; busBW uses the usual
 // ring factors (all-reduce 2(n-1)/n, gather/scatter (n-1)/n) so the numbers
@@ -639,9 +632,10 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread*
   const float expect_sum = W * (W + 1) / 2.0f;
   float* buf;
   float* aux;
+  unsigned long long* bad_dev;
   HIP_OK(hipMalloc(&buf, n * 4));
   HIP_OK(hipMalloc(&aux, n * 4));
-  std::vector<float> host(n);
+  HIP_OK(hipMalloc(&bad_dev, sizeof(unsigned long long)));
   std::string detail;
   int64_t total_bad = 0;
   auto report = [&](const char* name, int64_t bytes, float ms, double busf, int64_t bad) {
@@ -651,17 +645,23 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread*
                   detail.empty() ? "" : ", ", name, (long long)bytes, ms, algbw, algbw * busf, (long long)bad);
     total_bad += bad;
   };
+  // operands filled and results checked on the device (avk_fill_const /
+  // avk_check_blocks): element i must be base + (i / block) * step
+  auto check = [&](const void* x, int64_t count, int bf16, int64_t block, float base, float step) -> int64_t {
+    AVK_OK(avk_check_blocks(x, count, bf16, block, base, step, bad_dev, st));
+    unsigned long long bad = 0;
+    HIP_OK(hipMemcpyAsync(&bad, bad_dev, sizeof(bad), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    return (int64_t)bad;
+  };
+  const float mine = (float)(a.rank + 1);
 
   // fp32 all-reduce
   const auto t_first = Clock::now();
-  std::fill(host.begin(), host.end(), (float)(a.rank + 1));
-  HIP_OK(hipMemcpyAsync(buf, host.data(), n * 4, hipMemcpyHostToDevice, st));
+  AVK_OK(avk_fill_const(buf, n, 0, mine, st));
   NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
-  HIP_OK(hipMemcpyAsync(host.data(), buf, n * 4, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  int64_t bad = check(buf, n, 0, n, expect_sum, 0.0f);
   const double first_s = secs(t_first);
-  int64_t bad = 0;
-  for (int64_t i = 0; i < n; ++i) bad += host[i] != expect_sum;
   float ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st)); });
   const double ar_algbw = n * 4.0 / (ms * 1e-3) / 1e9;
   const double ar_busbw = W > 1 ? ar_algbw * 2.0 * (W - 1) / W : 0.0;
@@ -669,44 +669,25 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread*
   report("allreduce_f32", n * 4, ms, W > 1 ? 2.0 * (W - 1) / W : 0.0, bad);
 
   // bf16 all-reduce (sums up to 36 are exact in bf16)
-  {
-    std::vector<uint16_t> h16(n, bf16_bits((float)(a.rank + 1)));
-    HIP_OK(hipMemcpyAsync(aux, h16.data(), n * 2, hipMemcpyHostToDevice, st));
-    NCCL_OK(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st));
-    HIP_OK(hipMemcpyAsync(h16.data(), aux, n * 2, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    const uint16_t want = bf16_bits(expect_sum);
-    bad = 0;
-    for (int64_t i = 0; i < n; ++i) bad += h16[i] != want;
-    ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st)); });
-    report("allreduce_bf16", n * 2, ms, W > 1 ? 2.0 * (W - 1) / W : 0.0, bad);
-  }
+  AVK_OK(avk_fill_const(aux, n, 1, mine, st));
+  NCCL_OK(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st));
+  bad = check(aux, n, 1, n, expect_sum, 0.0f);
+  ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st)); });
+  report("allreduce_bf16", n * 2, ms, W > 1 ? 2.0 * (W - 1) / W : 0.0, bad);
 
   // all-gather: rank r's block holds r+1
-  {
-    std::fill(host.begin(), host.begin() + per, (float)(a.rank + 1));
-    HIP_OK(hipMemcpyAsync(buf, host.data(), per * 4, hipMemcpyHostToDevice, st));
-    NCCL_OK(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st));
-    HIP_OK(hipMemcpyAsync(host.data(), aux, n * 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    bad = 0;
-    for (int64_t i = 0; i < n; ++i) bad += host[i] != (float)(i / per + 1);
-    ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st)); });
-    report("allgather_f32", n * 4, ms, W > 1 ? (W - 1.0) / W : 0.0, bad);
-  }
+  AVK_OK(avk_fill_const(buf, per, 0, mine, st));
+  NCCL_OK(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st));
+  bad = check(aux, n, 0, per, 1.0f, 1.0f);
+  ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st)); });
+  report("allgather_f32", n * 4, ms, W > 1 ? (W - 1.0) / W : 0.0, bad);
 
   // reduce-scatter: every element of every rank holds r+1
-  {
-    std::fill(host.begin(), host.end(), (float)(a.rank + 1));
-    HIP_OK(hipMemcpyAsync(buf, host.data(), n * 4, hipMemcpyHostToDevice, st));
-    NCCL_OK(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st));
-    HIP_OK(hipMemcpyAsync(host.data(), aux, per * 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    bad = 0;
-    for (int64_t i = 0; i < per; ++i) bad += host[i] != expect_sum;
-    ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st)); });
-    report("reducescatter_f32", n * 4, ms, W > 1 ? (W - 1.0) / W : 0.0, bad);
-  }
+  AVK_OK(avk_fill_const(buf, n, 0, mine, st));
+  NCCL_OK(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st));
+  bad = check(aux, per, 0, per, expect_sum, 0.0f);
+  ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st)); });
+  report("reducescatter_f32", n * 4, ms, W > 1 ? (W - 1.0) / W : 0.0, bad);
 
   const double checks_s = secs(t_first);
   // No ncclCommDestroy: it costs ~0.4 s (proxy shutdown, measured on MI355X,
@@ -722,6 +703,7 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread*
   if (a.rccl_destroy) {
     (void)hipFree(buf);
     (void)hipFree(aux);
+    (void)hipFree(bad_dev);
   }
   s.ok = total_bad == 0;
   s.seconds = secs(t0);

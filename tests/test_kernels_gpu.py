@@ -206,3 +206,22 @@ def test_mfma_probe_every_cdna4_dtype_exact(seed):
     res = K.mfma_probe(seed)
     assert set(res) == {"f16", "bf16", "fp8", "bf8", "i8", "mxfp8", "mxfp6", "mxfp4", "f32", "f64"}
     assert all(v == 0 for v in res.values()), res
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_fill_const_and_block_check_match_torch(dtype):
+    # RCCL-step operand fill and result check (device side) vs a PyTorch reference
+    dt = getattr(torch, dtype)
+    per, blocks = 4096 + 3, 64  # values 1..64: exact in bf16
+    n = per * blocks
+    x = torch.empty(n, dtype=dt, device="cuda")
+    K.fill_const(x, 3.0)
+    assert torch.equal(x.float().cpu(), torch.full((n,), 3.0))
+    assert K.check_blocks(x, n, 3.0, 0.0) == 0
+    y = (1.0 + torch.div(torch.arange(n, device="cuda"), per, rounding_mode="floor")).to(dt)  # all-gather pattern
+    assert K.check_blocks(y, per, 1.0, 1.0) == 0
+    assert K.check_blocks(y, per, 1.0, 2.0) == int((y.float() != 1.0 + 2.0 * torch.div(
+        torch.arange(n, device="cuda"), per, rounding_mode="floor")).sum())
+    y[5] += 1
+    y[n - 1] = float("nan")
+    assert K.check_blocks(y, per, 1.0, 1.0) == 2
