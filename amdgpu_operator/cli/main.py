@@ -123,6 +123,12 @@ def main(argv: list[str] | None = None) -> int:
     pf.add_argument("--json", action="store_true")
     pf.add_argument("--expect-gpus", type=int, default=None)
     pf.add_argument("--no-gpu", action="store_true", help="control-plane / CPU node: skip the GPU checks")
+    mg = sub.add_parser("must-gather", help="archive cluster + node state for troubleshooting (README.md:172-187)")
+    _common(mg)
+    mg.add_argument("--output", default="amdgpu-must-gather.tar.gz")
+    mg.add_argument("--node-root", default=None, help="also collect this host's GPU state (e.g. / on a GPU node)")
+    mg.add_argument("--validations-dir", default="/run/amd/validations")
+    mg.add_argument("--no-cluster", action="store_true", help="node state only (no API access)")
     co = sub.add_parser("collectives", help="RCCL collective sweep (run under torch.distributed.run)")
     co.add_argument("--min-bytes", type=int, default=8)
     co.add_argument("--max-bytes", type=int, default=1 << 30)
@@ -148,11 +154,12 @@ def main(argv: list[str] | None = None) -> int:
         print(json.dumps({"crd_deleted": cleanup_crd(_client(args))}))
         return 0
     if args.cmd == "apply-crd":
-        from ..helm.crd import crd
+        from ..helm.crd import crd, driver_crd
         from ..kube.client import apply_object
 
-        _, action = apply_object(_client(args), crd())
-        print(json.dumps({"crd": action}))
+        client = _client(args)
+        out = {c["metadata"]["name"]: apply_object(client, c)[1] for c in (crd(), driver_crd())}
+        print(json.dumps({"crds": out}))
         return 0
     if args.cmd == "verify":
         from .verify import main_verify
@@ -186,6 +193,13 @@ def main(argv: list[str] | None = None) -> int:
             c.stop()
     if args.cmd == "collectives":
         return _collectives(args)
+    if args.cmd == "must-gather":
+        from .gather import must_gather
+
+        summary = must_gather(None if args.no_cluster else _client(args), args.namespace, args.output,
+                              args.node_root, args.validations_dir)
+        print(json.dumps({"output": args.output, "summary": summary}, indent=1))
+        return 0
     if args.cmd == "preflight":
         from .preflight import main_preflight
 

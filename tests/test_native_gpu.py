@@ -177,3 +177,11 @@ def test_sim_cluster_on_real_gpu():
         assert gemm["counter_gate"] == "pass"
     finally:
         c.stop()
+
+
+def test_must_gather_node_state_on_mi355x(tmp_path):
+    from amdgpu_operator.cli.gather import gather_node
+
+    node = gather_node("/", str(tmp_path))
+    assert node["probe"]["ok"] and node["gpus"] and all(g["arch"] == "gfx950" for g in node["gpus"])
+    assert node["metrics"] and node["metrics"][0]["vram_total_bytes"] > 280 * 2**30
