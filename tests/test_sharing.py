@@ -293,3 +293,48 @@ def test_unknown_config_key_falls_back_to_command_line_flags(tmp_path):
         c.wait_ready(60, {"gpu-1": 2})  # plugin serves unshared GPUs instead of crash-looping
     finally:
         c.stop()
+
+
+def test_reconfigure_under_concurrent_allocations(node):
+    """Config flips (time-slicing on/off) while pods are admitted: no deadlock,
+    and the final config is what kubelet sees (SURVEY.md §5.2 race tier)."""
+    import threading
+
+    root, sock, k = node
+    m = _start(root, sock, "")
+    stop = threading.Event()
+    done = {"ok": 0, "err": 0}
+
+    def admit():
+        n = 0
+        while not stop.is_set():
+            res = next(iter(k.resources), None)
+            try:
+                k.allocate(res, 1, pod=f"p{n}")
+                k.release("default", f"p{n}")
+                done["ok"] += 1
+            except Exception:  # noqa: BLE001 - plugin mid-restart / resource renamed: kubelet retries
+                done["err"] += 1
+            n += 1
+
+    th = threading.Thread(target=admit, daemon=True)
+    try:
+        assert k.wait_registered("amd.com/gpu", 10, min_devices=8)
+        th.start()
+        for i in range(6):
+            m.reconfigure(DC.parse(SHARED4 if i % 2 == 0 else "flags: {deviceIDStrategy: index}"))
+            time.sleep(0.05)
+        stop.set()
+        th.join(10)
+        assert not th.is_alive()
+        assert k.wait_registered("amd.com/gpu", 10, min_devices=8)
+        deadline = time.time() + 10
+        while sorted(k.resources["amd.com/gpu"].devices) != [str(i) for i in range(8)] and time.time() < deadline:
+            time.sleep(0.05)
+        assert sorted(k.resources["amd.com/gpu"].devices) == [str(i) for i in range(8)]  # last config: index IDs
+        assert done["ok"] > 0
+        ids, _ = k.allocate("amd.com/gpu", 2, pod="final")
+        assert len(ids) == 2
+    finally:
+        stop.set()
+        m.stop()
