@@ -25,6 +25,9 @@ import shlex
 
 import yaml
 
+# libyaml's safe loader when PyYAML was built with it (the CRD parses ~10x faster), else the pure-Python one
+_Loader = getattr(yaml, "CSafeLoader", yaml.SafeLoader)
+
 from ..api.clusterpolicy import deep_merge, parse_set_flags
 
 CHART_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
@@ -117,7 +120,7 @@ class Renderer:
                  namespace: str = "gpu-operator-resources"):
         self.chart_dir = chart_dir
         with open(os.path.join(chart_dir, "Chart.yaml")) as f:
-            self.chart = yaml.safe_load(f)
+            self.chart = yaml.load(f, Loader=_Loader)
         self.values = values
         self.release = {"Name": release_name, "Namespace": namespace, "Service": "Helm", "IsInstall": True}
         self.defines: dict[str, list] = {}
@@ -301,7 +304,7 @@ class Renderer:
 def chart_values(overrides: dict | None = None, set_flags: list[str] | None = None,
                  chart_dir: str = CHART_DIR) -> dict:
     with open(os.path.join(chart_dir, "values.yaml")) as f:
-        values = yaml.safe_load(f) or {}
+        values = yaml.load(f, Loader=_Loader) or {}
     if overrides:
         values = deep_merge(values, overrides)
     if set_flags:
@@ -317,12 +320,12 @@ def render_chart(values: dict | None = None, set_flags: list[str] | None = None,
     crd_dir = os.path.join(chart_dir, "crds")
     for fn in sorted(os.listdir(crd_dir)):
         with open(os.path.join(crd_dir, fn)) as f:
-            docs += [d for d in yaml.safe_load_all(f) if d]
+            docs += [d for d in yaml.load_all(f, Loader=_Loader) if d]
     for _, text in Renderer(chart_dir, vals, release_name, namespace).render().items():
-        docs += [d for d in yaml.safe_load_all(text) if d]
+        docs += [d for d in yaml.load_all(text, Loader=_Loader) if d]
     return docs
 
 
 def load_crd(chart_dir: str = CHART_DIR) -> dict:
     with open(os.path.join(chart_dir, "crds", "amd.com_clusterpolicies.yaml")) as f:
-        return yaml.safe_load(f)
+        return yaml.load(f, Loader=_Loader)

@@ -110,8 +110,21 @@ def new(api_version: str, kind: str, name: str, namespace: str | None = None, la
     return o
 
 
+_ATOMS = (str, int, float, bool, type(None))
+
+
 def deep(obj):
-    return copy.deepcopy(obj)
+    """Deep copy of a JSON-shaped object (dict / list / scalars): what every
+    API object is.  ~6x faster than copy.deepcopy (no memo table), and the
+    fake API server copies on every create/get/list/watch event."""
+    t = type(obj)
+    if t is dict:
+        return {k: deep(v) for k, v in obj.items()}
+    if t is list:
+        return [deep(v) for v in obj]
+    if t in _ATOMS:
+        return obj
+    return copy.deepcopy(obj)  # anything else (tuples, custom objects): the general path
 
 
 def spec_hash(obj: dict) -> str:

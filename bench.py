@@ -93,6 +93,7 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
     cluster = SimCluster(d, [node], fake_gpu=fake_gpu, poll_s=0.005, launcher=launcher).start()
     try:
         t0 = time.perf_counter()
+        t0_wall = time.time()
         cluster.install_operator(values)
         ttr = cluster.wait_ready(args.timeout, {"mi355x-node-0": n_gpus})
         t_total = time.perf_counter() - t0
@@ -109,8 +110,14 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
         for r in ranks:
             for s in r.get("steps", []):
                 steps.setdefault(s["name"], []).append(s)
+        timeline = {}  # seconds after ClusterPolicy creation at which each ready file was written
+        for step in ("driver", "toolkit", "workload", "plugin", "complete"):
+            r = read_ready(nd.env, step) or {}
+            if "time" in r:
+                timeline[step] = round(r["time"] - t0_wall, 4)
         return {
             "time_to_ready_s": ttr,
+            "timeline_s": timeline,
             "wall_s": t_total,
             "allocatable": alloc,
             "policy_state_seconds": (cp.get("status") or {}).get("stateReadySeconds"),
