@@ -95,6 +95,12 @@ class ReconcileMetrics:
         self.state = "absent"
         self.ready_spans: dict[str, float] = {}
         self.time_to_ready: float | None = None
+        self.upgrade_nodes: dict[str, int] = {}  # driver-upgrade state -> nodes
+
+    def observe_upgrade(self, upgrade: dict | None) -> None:
+        with self._lock:
+            if upgrade is not None:
+                self.upgrade_nodes = dict(upgrade.get("nodes") or {})
 
     def observe(self, res: "ReconcileResult", spans: dict[str, float], ttr: float | None) -> None:
         with self._lock:
@@ -126,6 +132,10 @@ class ReconcileMetrics:
                 out.append(f'{p}state_ready_seconds{{state="{k}"}} {v:.4f}')
             if self.time_to_ready is not None:
                 out += [f"# TYPE {p}time_to_ready_seconds gauge", f"{p}time_to_ready_seconds {self.time_to_ready:.4f}"]
+            if self.upgrade_nodes:
+                out.append(f"# TYPE {p}driver_upgrade_nodes gauge")
+                for k, v in sorted(self.upgrade_nodes.items()):
+                    out.append(f'{p}driver_upgrade_nodes{{state="{k}"}} {v}')
         return "\n".join(out) + "\n"
 
 
@@ -249,6 +259,7 @@ class ClusterPolicyReconciler:
             if pending:
                 overall = "notReady"
         self._write_status(cp, overall, results, gpu_nodes, upgrade=upgrade)
+        self.metrics.observe_upgrade(upgrade)
         if overall == "ready":
             self._ttr.setdefault(uid, self.clock() - self._created_at[uid])
         res = ReconcileResult(cp["metadata"]["name"], overall, results, gpu_nodes, time.perf_counter() - t0)

@@ -72,6 +72,7 @@ def test_rolling_driver_upgrade_one_node_at_a_time(tmp_path):
         while c.policy()["status"]["driverUpgrade"]["nodes"] != {U.DONE: 3} and time.time() < deadline:
             time.sleep(0.05)
         assert c.policy()["status"]["driverUpgrade"]["nodes"] == {U.DONE: 3}
+        assert 'amd_gpu_operator_driver_upgrade_nodes{state="upgrade-done"} 3' in c.reconciler.metrics.render()
     finally:
         c.stop()
 

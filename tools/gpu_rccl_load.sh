@@ -1,4 +1,5 @@
 #!/bin/bash
+# built by: /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/native/co_load_probe.cpp -o tools/native/co_load_probe
 # RCCL start-up on the GPU box: trimmed vs system library (validator rccl
 # step, phase-timed) and the bare cost of loading RCCL's gfx950 code object.
 set -u
