@@ -97,7 +97,7 @@ class ToolkitSpec(Operand):
     runtimeClass: str = "amd"
     cdi: CDISpec = Field(default_factory=CDISpec)
     mountRocm: bool = False
-    # prestart-hook device-list policy (the NVIDIA toolkit's
+    # OCI-hook device-list policy (the NVIDIA toolkit's
     # accept-nvidia-visible-devices-as-volume-mounts / -envvar-when-unprivileged)
     acceptDeviceListAsVolumeMounts: bool = False
     acceptEnvvarUnprivileged: bool = True

@@ -123,14 +123,16 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         from ..driver import manager as drv
 
         if a.action == "install":
-            drv.install(env, stop=stop)
+            drv.install(env, stop=stop, cenv=cenv)
             ready()
             stop.wait()
         elif a.action == "monitor":
             ready()
             drv.monitor(env, stop, interval=max(env.poll_s, min(a.interval, 10.0)))
         elif a.action == "prepare-upgrade":
-            drv.prepare_upgrade(env, cenv.get("AMDGPU_DRIVER_VERSION", ""), cenv.get("DRAIN_ENABLED", "true") == "true")
+            drv.prepare_upgrade(env, cenv.get("AMDGPU_DRIVER_VERSION", ""), cenv.get("DRAIN_ENABLED", "true") == "true",
+                                cenv.get("AMDGPU_DRIVER_SPEC_HASH", ""),
+                                float(cenv.get("DRAIN_TIMEOUT_SECONDS", "300")))
         else:
             print(drv.smi_table(env))
         return 0
@@ -139,14 +141,17 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         from ..toolkit import install as tk
 
         if a.action == "install":
-            tk.install(env, runtime_class=a.runtime_class or cenv.get("RUNTIME_CLASS", "amd"),
-                       cdi_enabled=not a.no_cdi and cenv.get("CDI_ENABLED", "true") == "true",
-                       mount_rocm=a.mount_rocm or cenv.get("MOUNT_ROCM") == "true",
-                       args=tk.hook_args(cenv.get("ACCEPT_DEVICE_LIST_AS_VOLUME_MOUNTS") == "true",
-                                         cenv.get("ACCEPT_ENVVAR_UNPRIVILEGED", "true") == "true"),
-                       set_as_default=cenv.get("CONTAINERD_SET_AS_DEFAULT") == "true")
+            kw = dict(runtime_class=a.runtime_class or cenv.get("RUNTIME_CLASS", "amd"),
+                      cdi_enabled=not a.no_cdi and cenv.get("CDI_ENABLED", "true") == "true",
+                      mount_rocm=a.mount_rocm or cenv.get("MOUNT_ROCM") == "true",
+                      args=tk.hook_args(cenv.get("ACCEPT_DEVICE_LIST_AS_VOLUME_MOUNTS") == "true",
+                                        cenv.get("ACCEPT_ENVVAR_UNPRIVILEGED", "true") == "true"),
+                      set_as_default=cenv.get("CONTAINERD_SET_AS_DEFAULT") == "true")
+            tk.install(env, **kw)
             ready()
-            stop.wait()
+            # a driver reload / loss clears toolkit-ready: redo the install (the
+            # CDI spec follows the new device nodes) once the driver is back
+            tk.keep_ready(env, stop, lambda: tk.install(env, **kw), interval=max(env.poll_s, 0.01))
         else:
             tk.uninstall(env)
         return 0

@@ -179,10 +179,14 @@ def state_prerequisites(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
 
 def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-driver-daemonset",
                  node_selector: dict | None = None) -> list[dict]:
+    from .upgrade import HASH_LABEL, driver_spec_hash
+
     d = spec.driver
     sa = "amd-driver"
     image = d.ref("amd-driver")
+    spec_hash = driver_spec_hash(spec)
     env = [{"name": "ROCM_VERSION", "value": d.rocmVersion}, {"name": "AMDGPU_DRIVER_VERSION", "value": d.driverVersion},
+           {"name": "AMDGPU_DRIVER_SPEC_HASH", "value": spec_hash},
            {"name": "AMDGPU_USE_PRECOMPILED", "value": str(d.usePrecompiled).lower()},
            {"name": "AMDGPU_BLACKLIST_INBOX", "value": str(d.blacklistAmdgpuInbox).lower()},
            {"name": "AMDGPU_MODULE_PARAMS", "value": " ".join(f"{k}={v}" for k, v in sorted(d.kernelModuleParams.items()))},
@@ -200,10 +204,14 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-drive
     health = _container("amd-driver-health", image, d.imagePullPolicy, ["driver", "monitor"],
                         [_mount("host-sys", "/host/sys", ro=True), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)],
                         privileged=True)
+    # the init container compares the live module with this spec and unloads it
+    # on a mismatch, so it gets the same driver env as amd-driver-ctr
     init = _container("amd-driver-manager", image, d.imagePullPolicy, ["driver", "prepare-upgrade"],
-                      [_mount("run-amd", "/run/amd")],
-                      [{"name": "DRAIN_ENABLED", "value": str(d.upgradePolicy.drainEnabled).lower()},
-                       {"name": "DRAIN_TIMEOUT_SECONDS", "value": str(d.upgradePolicy.drainTimeoutSeconds)}], True)
+                      [_mount("run-amd", "/run/amd"), _mount("lib-modules", "/lib/modules"),
+                       _mount("host-sys", "/host/sys", ro=True)],
+                      env + [{"name": "DRAIN_ENABLED", "value": str(d.upgradePolicy.drainEnabled).lower()},
+                             {"name": "DRAIN_TIMEOUT_SECONDS", "value": str(d.upgradePolicy.drainTimeoutSeconds)}],
+                      True)
     vols = [_hostpath("run-amd", "/run/amd"), _hostpath("host-root", "/", "Directory"),
             _hostpath("lib-modules", "/lib/modules"), _hostpath("dev", "/dev", "Directory"),
             _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
@@ -213,9 +221,7 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-drive
     ds = _daemonset(spec, ns, owner, name, "driver", sa, [ctr, health], [init], vols, host_pid=True,
                     node_selector=sel)
     # what the pods install, for the upgrade controller (controller/upgrade.py)
-    from .upgrade import HASH_LABEL, driver_spec_hash
-
-    ds["spec"]["template"]["metadata"]["labels"][HASH_LABEL] = driver_spec_hash(spec)
+    ds["spec"]["template"]["metadata"]["labels"][HASH_LABEL] = spec_hash
     if d.upgradePolicy.autoUpgrade and node_selector is None:  # node-by-node rollout (controller/upgrade.py)
         ds["spec"]["updateStrategy"] = {"type": "OnDelete"}
     return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner), ds]

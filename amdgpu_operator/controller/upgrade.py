@@ -17,11 +17,18 @@ time (``maxParallelUpgrades``), tracked in a node label as upstream does::
 * cordon: ``spec.unschedulable`` (only nodes the operator cordoned are
   uncordoned again, recorded in an annotation);
 * pod deletion: GPU pods (``amd.com/gpu*`` limits) are evicted when
-  ``drainEnabled``; with it off the node waits until they finish;
+  ``drainEnabled``; with it off the node waits until they finish.  Either way
+  the node moves on only once a fresh list shows no GPU pod left, Terminating
+  ones included (they still hold ``/dev/kfd``), bounded by
+  ``drainTimeoutSeconds`` (then force-deleted with ``podDeletionForce``, else
+  ``upgrade-failed``);
 * pod restart: the old driver pod is deleted, the DaemonSet creates the new
   one, whose ``amd-driver-manager`` init container unloads the old module;
-* validation: the new driver pod is Ready and the node carries
-  ``amd.com/gpu.validated=true`` again (the validator re-ran on the new driver).
+* validation: the new driver pod is Ready, it reports the module it loaded for
+  this spec (``amd.com/gpu-driver.spec-hash`` node annotation, written by
+  ``driver/manager.py`` only after the old module was unloaded and the new one
+  came up) and the node carries ``amd.com/gpu.validated=true`` again (the
+  validator re-ran on the new driver).
 
 The controller is level-triggered: every reconcile recomputes from the node
 labels, so an operator restart resumes mid-upgrade.
@@ -44,6 +51,9 @@ STATE_LABEL = "amd.com/gpu-driver-upgrade-state"
 HASH_LABEL = "amd.com/driver-spec-hash"
 CORDONED_ANN = "amd.com/gpu-driver-upgrade.cordoned"
 SINCE_ANN = "amd.com/gpu-driver-upgrade.since"
+# written by the driver container once the module it installed is live
+LOADED_HASH_ANN = "amd.com/gpu-driver.spec-hash"
+LOADED_VERSION_ANN = "amd.com/gpu-driver.version"
 DRIVER_DS = "amd-driver-daemonset"
 VALIDATOR_DS = "amd-operator-validator"
 
@@ -83,14 +93,34 @@ class DriverUpgradeController:
             patch["spec"] = {"unschedulable": unschedulable}
         self.client.patch("v1", "Node", name, patch)
         node["metadata"].setdefault("labels", {})[STATE_LABEL] = state
-        node["metadata"].setdefault("annotations", {}).update(patch["metadata"]["annotations"])
+        anns = node["metadata"].setdefault("annotations", {})
+        for k, v in patch["metadata"]["annotations"].items():
+            if v is None:
+                anns.pop(k, None)
+            else:
+                anns[k] = v
         if unschedulable is not None:
             node.setdefault("spec", {})["unschedulable"] = unschedulable
         log.info("driver upgrade %s -> %s", name, state)
 
+    def _gpu_pods(self, node_name: str) -> list[dict]:
+        return [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={node_name}") if _uses_gpu(p)]
+
+    def _delete_pod(self, pod: dict, grace: int | None = None) -> None:
+        try:
+            self.client.delete("v1", "Pod", pod["metadata"]["name"], pod["metadata"].get("namespace"),
+                               grace_period_seconds=grace)
+        except NotFound:
+            pass
+
     def _driver_pods(self) -> dict[str, dict]:
-        return {p["spec"].get("nodeName"): p for p in self.client.list("v1", "Pod", self.namespace,
-                                                                      label_selector={"app": DRIVER_DS})}
+        """Driver pod per node; a live pod wins over one still Terminating."""
+        out: dict[str, dict] = {}
+        for p in self.client.list("v1", "Pod", self.namespace, label_selector={"app": DRIVER_DS}):
+            node = p["spec"].get("nodeName")
+            if node not in out or out[node]["metadata"].get("deletionTimestamp"):
+                out[node] = p
+        return out
 
     def step(self, spec: ClusterPolicySpec) -> dict:
         """One level-triggered pass over every driver node; returns a status summary."""
@@ -137,30 +167,28 @@ class DriverUpgradeController:
             for _ in range(len(ACTIVE)):
                 st = state(n)
                 if st == CORDON:
-                    was = bool((n.get("spec") or {}).get("unschedulable"))
-                    self._set(n, POD_DELETION, {CORDONED_ANN: "false" if was else "true"}, unschedulable=True)
+                    # a retry after upgrade-failed finds the node cordoned by the
+                    # first attempt: keep that attempt's record of who cordoned it
+                    ann = {} if CORDONED_ANN in (n["metadata"].get("annotations") or {}) else \
+                        {CORDONED_ANN: "false" if (n.get("spec") or {}).get("unschedulable") else "true"}
+                    self._set(n, POD_DELETION, ann, unschedulable=True)
                 elif st == POD_DELETION:
-                    gpu_pods = [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={name}")
-                                if _uses_gpu(p)]
-                    if gpu_pods and pol.drainEnabled:
+                    expired = now - since(n) > timeout
+                    gpu_pods = self._gpu_pods(name)
+                    evict = pol.drainEnabled or (expired and pol.podDeletionForce)
+                    if gpu_pods and evict:
                         for p in gpu_pods:
-                            try:
-                                self.client.delete("v1", "Pod", p["metadata"]["name"], p["metadata"].get("namespace"))
-                            except NotFound:
-                                pass
-                        gpu_pods = []
-                    if gpu_pods and now - since(n) > timeout:
-                        if not pol.podDeletionForce:
-                            self._set(n, FAILED, unschedulable=None)
-                            break
-                        for p in gpu_pods:
-                            try:
-                                self.client.delete("v1", "Pod", p["metadata"]["name"], p["metadata"].get("namespace"))
-                            except NotFound:
-                                pass
-                        gpu_pods = []
+                            # a deleted pod stays Terminating for its grace period and
+                            # keeps /dev/kfd open; past the drain timeout it is forced
+                            terminating = bool(p["metadata"].get("deletionTimestamp"))
+                            if terminating and not (expired and pol.podDeletionForce):
+                                continue
+                            self._delete_pod(p, 0 if terminating else None)
+                        gpu_pods = self._gpu_pods(name)
                     if gpu_pods:
-                        break  # wait for the workloads to finish
+                        if expired and not pol.podDeletionForce:
+                            self._set(n, FAILED)
+                        break  # wait for the workloads to finish / terminate
                     self._set(n, POD_RESTART)
                 elif st == POD_RESTART:
                     pod = pods.get(name)
@@ -185,7 +213,9 @@ class DriverUpgradeController:
                     ready = fresh and (R.condition(pod, "Ready") or {}).get("status") == "True"
                     cur = self.client.get("v1", "Node", name)
                     validated = (cur["metadata"].get("labels") or {}).get(VALIDATED_LABEL) == "true"
-                    if ready and validated:
+                    # the new driver pod reports the spec it actually loaded (driver/manager.py)
+                    loaded = (cur["metadata"].get("annotations") or {}).get(LOADED_HASH_ANN) == desired
+                    if ready and validated and loaded:
                         self._set(n, UNCORDON)
                     elif now - since(n) > max(timeout, spec.driver.startupProbeTimeoutSeconds):
                         self._set(n, FAILED)
@@ -194,7 +224,8 @@ class DriverUpgradeController:
                         break
                 elif st == UNCORDON:
                     ours = (n["metadata"].get("annotations") or {}).get(CORDONED_ANN) == "true"
-                    self._set(n, DONE, unschedulable=False if ours else None)
+                    # the cordon record belongs to this upgrade only; the next one records afresh
+                    self._set(n, DONE, {CORDONED_ANN: None}, unschedulable=False if ours else None)
                 else:
                     break
         counts: dict[str, int] = {}

@@ -15,14 +15,16 @@ node" (/root/reference/README.md:212); its pods run ``2/2`` containers
   ``driver-ready`` when the driver disappears (driver crash / unload), so the
   dependent operands re-gate.
 * ``prepare-upgrade`` - init container: when the loaded driver differs from
-  the requested version, evict GPU pods from the node (drain) and clear the
-  validation files before the new driver is installed.
+  the requested version or driver spec, evict GPU pods from the node (drain),
+  clear the validation files and unload the old module before the new driver
+  is installed.
 * ``smi``      - ``amd-smi``-style device table inside ``amd-driver-ctr``
   (the ``kubectl exec ... nvidia-smi`` check of README.md:152).
 """
 
 from __future__ import annotations
 
+import json
 import os
 import subprocess
 import threading
@@ -37,6 +39,7 @@ INSTALL_SCRIPT = "/usr/local/bin/amd-driver-install.sh"
 
 
 def loaded_version(env: NodeEnv) -> str:
+    """``/sys/module/amdgpu/version``; empty for an inbox / built-in module."""
     try:
         with open(os.path.join(env.sysfs_root(), "sys/module/amdgpu/version")) as f:
             return f.read().strip()
@@ -44,16 +47,108 @@ def loaded_version(env: NodeEnv) -> str:
         return ""
 
 
-def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None = None) -> dict:
+class HostModule:
+    """The node's real amdgpu module: ``install.sh`` of the driver image and
+    ``modprobe -r``.  The simulated cluster substitutes
+    :class:`~amdgpu_operator.testing.fakesys.SimModule` (``env.extra["kmod"]``)."""
+
+    def __init__(self, script: str | None = None):
+        self.script = script or INSTALL_SCRIPT
+
+    def can_install(self) -> bool:
+        return os.path.exists(self.script) and os.access(self.script, os.X_OK)
+
+    def install(self, env: NodeEnv, cenv: dict, timeout: float) -> None:
+        subprocess.run([self.script], check=True, timeout=timeout, env={**os.environ, **cenv})
+
+    def unload(self, env: NodeEnv, timeout: float = 120.0) -> None:
+        p = subprocess.run(["modprobe", "-r", "amdgpu"], capture_output=True, text=True, timeout=timeout)
+        if p.returncode != 0:
+            raise RuntimeError(f"modprobe -r amdgpu failed ({p.returncode}): {p.stderr.strip()}")
+
+
+def _kmod(env: NodeEnv):
+    return env.extra.get("kmod") or HostModule(INSTALL_SCRIPT)
+
+
+def _state_path(env: NodeEnv) -> str:
+    """What the operator last installed on this node (``/run/amd/driver-state.json``:
+    survives driver pod restarts, not reboots - like the loaded module)."""
+    return os.path.join(os.path.dirname(env.validations_dir.rstrip("/")), "driver-state.json")
+
+
+def read_state(env: NodeEnv) -> dict:
+    try:
+        with open(_state_path(env)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def _write_state(env: NodeEnv, state: dict | None) -> None:
+    path = _state_path(env)
+    if state is None:
+        try:
+            os.unlink(path)
+        except FileNotFoundError:
+            pass
+        return
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(state, f)
+    os.replace(tmp, path)
+
+
+def outdated(env: NodeEnv, desired_version: str, spec_hash: str = "") -> str:
+    """Why the live module does not satisfy the requested driver ("" = it does).
+
+    A module that reports a version must report the requested one; one the
+    operator installed must have been installed for the current driver spec
+    (module parameters, image and ROCm release are in the hash, not in the
+    module version).  An inbox / built-in module reports no version: it is
+    replaced only when the image can install one (see :func:`install`)."""
+    cur = loaded_version(env)
+    if desired_version and cur and cur != desired_version:
+        return f"loaded {cur}, requested {desired_version}"
+    rec = read_state(env).get("specHash", "")
+    if spec_hash and rec and rec != spec_hash:
+        return f"loaded for driver spec {rec}, current spec {spec_hash}"
+    return ""
+
+
+def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None = None,
+            cenv: dict | None = None) -> dict:
+    """``amd-driver-ctr``: make the requested driver live, then publish it.
+
+    ``cenv`` is the container environment of the driver spec
+    (``AMDGPU_DRIVER_VERSION``, ``AMDGPU_DRIVER_SPEC_HASH``, module params ...).
+    The install script runs when the module is not live, or when the live one
+    is not the requested one (it unloads it first).  Without an installer
+    (preinstalled host driver) a live module is accepted as host-managed, but
+    a live module of another version fails loudly.  After the module is up
+    the loaded version is checked against the request, recorded on the host
+    and published as node annotations for the upgrade controller."""
+    from ..controller.upgrade import LOADED_HASH_ANN, LOADED_VERSION_ANN
     from ..discovery import topology
 
+    cenv = dict(cenv or {})
+    want = cenv.get("AMDGPU_DRIVER_VERSION", "")
+    spec_hash = cenv.get("AMDGPU_DRIVER_SPEC_HASH", "")
+    kmod = _kmod(env)
     t0 = time.perf_counter()
     ran_script = False
-    if os.path.exists(INSTALL_SCRIPT) and os.access(INSTALL_SCRIPT, os.X_OK):
-        ok, _ = topology.probe(env.sysfs_root())
-        if not ok:
-            subprocess.run([INSTALL_SCRIPT], check=True, timeout=timeout)
+    live, _ = topology.probe(env.sysfs_root())
+    why = "" if not live else outdated(env, want, spec_hash)
+    if not live or why:
+        if kmod.can_install():
+            if why:
+                log.info("replacing the live driver: %s", why)
+                cenv["AMDGPU_FORCE_RELOAD"] = "true"
+            kmod.install(env, cenv, timeout)
             ran_script = True
+        elif why:
+            raise RuntimeError(f"driver mismatch and no installer in this image: {why}")
     deadline = time.monotonic() + timeout
     while True:
         ok, msg = topology.probe(env.sysfs_root())
@@ -63,9 +158,20 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
             raise RuntimeError(f"driver did not come up: {msg}")
         if (stop.wait(env.poll_s) if stop is not None else (time.sleep(env.poll_s) or False)):
             raise RuntimeError("stopped")
+    cur = loaded_version(env)
+    if ran_script and want and cur != want:
+        raise RuntimeError(f"installed driver reports version {cur or 'none'}, requested {want}")
+    host_managed = not ran_script and not cur
+    _write_state(env, {"version": cur, "specHash": spec_hash, "installed": ran_script, "hostManaged": host_managed,
+                       "ts": round(time.time(), 3)})
+    try:
+        env.client.patch("v1", "Node", env.node_name, {"metadata": {"annotations": {
+            LOADED_VERSION_ANN: cur or "host", LOADED_HASH_ANN: spec_hash or None}}})
+    except Exception as e:  # noqa: BLE001 - the ready file below still gates the operands
+        log.warning("could not annotate node %s: %s", env.node_name, e)
     gpus = topology.enumerate_gpus(env.sysfs_root())
-    out = {"ok": True, "message": msg, "gpus": len(gpus), "driver_version": loaded_version(env),
-           "installed": ran_script, "seconds": time.perf_counter() - t0}
+    out = {"ok": True, "message": msg, "gpus": len(gpus), "driver_version": cur, "installed": ran_script,
+           "host_managed": host_managed, "seconds": time.perf_counter() - t0}
     write_ready(env, "driver", out)
     return out
 
@@ -86,15 +192,40 @@ def monitor(env: NodeEnv, stop: threading.Event, interval: float = 10.0) -> None
         monitor_once(env)
 
 
-def prepare_upgrade(env: NodeEnv, desired_version: str, drain: bool = True) -> dict:
-    cur = loaded_version(env)
-    if not cur or not desired_version or cur == desired_version:
-        return {"upgrade": False, "loaded": cur}
-    from ..partition.manager import evict_gpu_pods
+def prepare_upgrade(env: NodeEnv, desired_version: str, drain: bool = True, spec_hash: str = "",
+                    drain_timeout: float = 300.0) -> dict:
+    """``amd-driver-manager`` init container of a (new) driver pod.
 
+    When the live module is not the requested one (version, or the driver
+    spec it was installed for), GPU pods are evicted, the validations are
+    cleared and the old module is unloaded, so ``amd-driver-ctr`` installs
+    the new one.  An unload failure raises: the init container fails and the
+    kubelet retries it, instead of the node passing as upgraded with the old
+    module still loaded."""
+    from ..discovery import topology
+
+    cur = loaded_version(env)
+    live, _ = topology.probe(env.sysfs_root())
+    why = outdated(env, desired_version, spec_hash) if live else ""
+    if not why:
+        return {"upgrade": False, "loaded": cur}
+    kmod = _kmod(env)
+    if not kmod.can_install():
+        raise RuntimeError(f"driver upgrade needed ({why}) but this image has no installer")
+    from ..partition.manager import evict_gpu_pods, wait_gpu_pods_gone
+
+    log.info("driver upgrade: %s", why)
     evicted = evict_gpu_pods(env) if drain else []
     clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
-    return {"upgrade": True, "loaded": cur, "desired": desired_version, "evicted": evicted}
+    if not wait_gpu_pods_gone(env, drain_timeout):
+        log.warning("GPU pods still on the node after %.0f s; unloading anyway", drain_timeout)
+    kmod.unload(env)
+    _write_state(env, None)
+    still, _ = topology.probe(env.sysfs_root())
+    if still:
+        raise RuntimeError("amdgpu still live after unload")
+    return {"upgrade": True, "loaded": cur, "desired": desired_version, "reason": why, "evicted": evicted,
+            "unloaded": True}
 
 
 def smi_table(env: NodeEnv) -> str:

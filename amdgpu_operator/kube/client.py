@@ -45,8 +45,8 @@ class LocalClient:
     def patch(self, api_version, kind, name, patch, namespace=None, subresource=None):
         return self.server.patch(api_version, kind, name, patch, namespace, subresource)
 
-    def delete(self, api_version, kind, name, namespace=None):
-        return self.server.delete(api_version, kind, name, namespace)
+    def delete(self, api_version, kind, name, namespace=None, grace_period_seconds=None):
+        return self.server.delete(api_version, kind, name, namespace, grace_period_seconds)
 
     def watch(self, api_version, kind, namespace=None, label_selector=None, field_selector=None,
               resource_version=None, stop: threading.Event | None = None, timeout=None):
@@ -185,9 +185,10 @@ class RestClient:
         _raise_for(r)
         return r.json()
 
-    def delete(self, api_version, kind, name, namespace=None):
+    def delete(self, api_version, kind, name, namespace=None, grace_period_seconds=None):
         t = R.rtype(api_version, kind)
-        r = self.session.delete(self._url(t, namespace, name), timeout=self.timeout)
+        q = None if grace_period_seconds is None else {"gracePeriodSeconds": str(int(grace_period_seconds))}
+        r = self.session.delete(self._url(t, namespace, name, query=q), timeout=self.timeout)
         _raise_for(r)
 
     def watch(self, api_version, kind, namespace=None, label_selector=None, field_selector=None,

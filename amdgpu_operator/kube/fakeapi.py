@@ -119,6 +119,8 @@ class FakeApiServer:
         self._history: list[tuple[int, str, dict]] = []  # for watch-from-resourceVersion
         self.request_count = 0
         self.hooks: list = []  # callables(event_type, obj) run synchronously after commit
+        # Pods on a node stay Terminating until a zero-grace delete (see delete())
+        self.graceful_pod_deletion = False
 
     # ------------------------------------------------------------------ core
     def _bump(self, obj: dict) -> None:
@@ -240,14 +242,31 @@ class FakeApiServer:
             merged["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
             return self.update(merged, subresource=subresource)
 
-    def delete(self, api_version: str, kind: str, name: str, namespace: str | None = None) -> None:
+    def delete(self, api_version: str, kind: str, name: str, namespace: str | None = None,
+               grace_period_seconds: int | None = None) -> None:
+        """Delete an object.  With :attr:`graceful_pod_deletion` a Pod bound to
+        a node is only marked Terminating (``deletionTimestamp``) and stays
+        listed until its kubelet confirms with a zero-grace delete, as on a
+        real API server; ``grace_period_seconds=0`` removes it at once."""
         self.request_count += 1
         t = R.rtype(api_version, kind)
         with self._lock:
             k = self._key(t, namespace, name)
-            o = self._store.pop(k, None)
-            if o is None:
+            cur = self._store.get(k)
+            if cur is None:
                 raise NotFound(f"{kind} {namespace}/{name}")
+            if (self.graceful_pod_deletion and kind == "Pod" and grace_period_seconds != 0
+                    and (cur.get("spec") or {}).get("nodeName")):
+                if not cur["metadata"].get("deletionTimestamp"):
+                    grace = grace_period_seconds
+                    if grace is None:
+                        grace = int((cur.get("spec") or {}).get("terminationGracePeriodSeconds", 30))
+                    cur["metadata"]["deletionTimestamp"] = _now()
+                    cur["metadata"]["deletionGracePeriodSeconds"] = grace
+                    self._bump(cur)
+                    self._emit("MODIFIED", cur)
+                return
+            o = self._store.pop(k)
             self._bump(o)
             self._emit("DELETED", o)
             uid = o["metadata"]["uid"]

@@ -90,7 +90,8 @@ class _Handler(BaseHTTPRequestHandler):
             if method == "PATCH":
                 return self._send(200, api.patch(t.api_version, t.kind, name, self._body(), ns, subresource=sub))
             if method == "DELETE":
-                api.delete(t.api_version, t.kind, name, ns)
+                grace = q.get("gracePeriodSeconds")
+                api.delete(t.api_version, t.kind, name, ns, None if grace in (None, "") else int(grace))
                 return self._send(200, {"kind": "Status", "apiVersion": "v1", "status": "Success"})
             raise ApiError(405, "MethodNotAllowed", method)
         except ApiError as e:

@@ -20,6 +20,7 @@ through ``amdsmi_set_gpu_compute_partition`` / ``amdsmi_set_gpu_memory_partition
 from __future__ import annotations
 
 import os
+import time
 from dataclasses import dataclass
 
 from ..nodeenv import NodeEnv
@@ -147,6 +148,18 @@ def evict_gpu_pods(env: NodeEnv) -> list[str]:
             env.client.delete("v1", "Pod", pod["metadata"]["name"], pod["metadata"].get("namespace"))
             out.append(f"{pod['metadata'].get('namespace')}/{pod['metadata']['name']}")
     return out
+
+
+def wait_gpu_pods_gone(env: NodeEnv, timeout: float) -> bool:
+    """Poll until no GPU pod is left on the node, Terminating ones included
+    (they hold ``/dev/kfd`` until their containers exit)."""
+    deadline = time.monotonic() + timeout
+    while True:
+        if not any(_uses_gpu(p) for p in env.client.list("v1", "Pod", field_selector=f"spec.nodeName={env.node_name}")):
+            return True
+        if time.monotonic() >= deadline:
+            return False
+        time.sleep(env.poll_s)
 
 
 def restart_device_plugin(env: NodeEnv) -> None:

@@ -167,5 +167,47 @@ def build_from_real_fixture(root: str, driver_loaded: bool = True) -> str:
     return root
 
 
+class SimModule:
+    """Simulated amdgpu kernel module of a fake node (the driver manager's
+    module backend in the simulated cluster, ``NodeEnv.extra["kmod"]``).
+
+    ``install`` does what ``deploy/images/amd-driver/install.sh`` does to the
+    host: unload a live module, then load the requested version (module
+    state, version, ``/dev/kfd``).  ``busy=True`` makes unloading fail, as
+    ``modprobe -r`` does while a process holds the device.  ``log`` records
+    the operations for tests."""
+
+    def __init__(self, root: str):
+        self.root = root
+        self.busy = False
+        self.log: list[str] = []
+
+    def can_install(self) -> bool:
+        return True
+
+    def _live(self) -> bool:
+        return os.path.exists(f"{self.root}/sys/module/amdgpu/initstate")
+
+    def unload(self, env=None, timeout: float = 0.0) -> None:
+        if self.busy:
+            self.log.append("unload-failed")
+            raise RuntimeError("modprobe -r amdgpu: Module amdgpu is in use")
+        for p in ("sys/module/amdgpu/initstate", "sys/module/amdgpu/version", "dev/kfd"):
+            try:
+                os.unlink(f"{self.root}/{p}")
+            except FileNotFoundError:
+                pass
+        self.log.append("unload")
+
+    def install(self, env, cenv: dict, timeout: float) -> None:
+        if self._live():
+            self.unload()
+        version = cenv.get("AMDGPU_DRIVER_VERSION") or "6.12.12"
+        _w(f"{self.root}/sys/module/amdgpu/version", f"{version}\n")
+        _w(f"{self.root}/sys/module/amdgpu/initstate", "live\n")
+        _w(f"{self.root}/dev/kfd", "")
+        self.log.append(f"install {version} {cenv.get('AMDGPU_MODULE_PARAMS', '')}".rstrip())
+
+
 def clear(root: str) -> None:
     shutil.rmtree(root, ignore_errors=True)

@@ -10,8 +10,9 @@ exercised end to end in-process:
   then the main containers, each mapped to the operand function its
   ``amdgpu-operator <subcommand>`` args name (the same functions the CLI runs
   inside the real images) - plus ``amdgpu-validator`` workload pods, which go
-  through the device-plugin gRPC Allocate, the native OCI hook on a synthetic
-  bundle, and the native validator binary on the allocated GPU;
+  through the device-plugin gRPC Allocate, the native OCI hook's precreate
+  stage on a synthetic runtime spec, and the native validator binary on the
+  allocated GPU;
 * :class:`~amdgpu_operator.testing.fakekubelet.FakeKubelet` per node (device
   plugin registration / ListAndWatch / Allocate / pod-resources) feeding the
   node's Allocatable ``amd.com/gpu``.
@@ -66,6 +67,7 @@ class SimNode:
     env: NodeEnv
     kubelet: FakeKubelet
     pods: dict = field(default_factory=dict)  # pod name -> _PodRun
+    terminating: set = field(default_factory=set)  # pods between graceful delete and removal
 
 
 def fake_validator_result(argv: list[str]) -> ProcResult:
@@ -201,13 +203,19 @@ class _PodRun:
 
 class SimCluster:
     def __init__(self, workdir: str, nodes: list[NodeSpec], namespace: str = DEFAULT_NAMESPACE,
-                 fake_gpu: bool = True, poll_s: float = 0.01, launcher=None):
+                 fake_gpu: bool = True, poll_s: float = 0.01, launcher=None,
+                 termination_s: float | None = None):
+        """``termination_s``: model graceful pod deletion - a deleted pod stays
+        Terminating (listed, with ``deletionTimestamp``) for that many seconds
+        (capped by its own grace period) before its kubelet removes it."""
         self.workdir = workdir
+        self.termination_s = termination_s
         self.namespace = namespace
         self.fake_gpu = fake_gpu
         self.poll_s = poll_s
         self.launcher = launcher
         self.api = FakeApiServer()
+        self.api.graceful_pod_deletion = termination_s is not None
         self.client = LocalClient(self.api)
         self.nodes: dict[str, SimNode] = {}
         self.stop_event = threading.Event()
@@ -254,6 +262,8 @@ class SimCluster:
                       containerd_config=os.path.join(d, "etc/containerd/config.toml"),
                       install_dir=os.path.join(d, "usr/local/amd"), namespace=self.namespace, poll_s=self.poll_s,
                       launcher=self._launch)
+        if ns.sysfs_root is None and ns.gpus > 0:  # driver installs / unloads act on the fake tree
+            env.extra["kmod"] = fakesys.SimModule(root)
         if self.fake_gpu:
             env.extra["metrics_fixture"] = os.path.join(fakesys.REAL_FIXTURE, "amd-smi-metric.json")
         os.makedirs(os.path.dirname(env.containerd_config), exist_ok=True)
@@ -445,7 +455,7 @@ class SimCluster:
                 continue
             with self._lock:
                 for name, pod in live.items():
-                    if name not in node.pods:
+                    if name not in node.pods or pod["metadata"].get("deletionTimestamp"):
                         self._on_pod(node, "ADDED", pod)
                 for name in [n for n in node.pods if n not in live]:
                     self._on_pod(node, "DELETED", {"metadata": {"name": name}})
@@ -456,6 +466,9 @@ class SimCluster:
 
     def _on_pod_locked(self, node: SimNode, etype: str, pod: dict) -> None:
         name = pod["metadata"]["name"]
+        if etype != "DELETED" and pod["metadata"].get("deletionTimestamp"):
+            self._terminate(node, pod)
+            return
         if etype == "DELETED":
             run = node.pods.pop(name, None)
             if run is not None:
@@ -466,6 +479,29 @@ class SimCluster:
             run = _PodRun(self, node, pod)
             node.pods[name] = run
             run.thread.start()
+
+    def _terminate(self, node: SimNode, pod: dict) -> None:
+        """Graceful deletion: stop the containers, then confirm the delete once
+        the termination time has passed (what the kubelet does)."""
+        name, ns = pod["metadata"]["name"], pod["metadata"].get("namespace", "default")
+        if name in node.terminating:
+            return
+        node.terminating.add(name)
+        run = node.pods.get(name)
+        if run is not None:
+            run.stop.set()
+        grace = float(pod["metadata"].get("deletionGracePeriodSeconds", 30))
+        delay = min(grace, self.termination_s or 0.0)
+
+        def finish():
+            if not self.stop_event.wait(delay):
+                try:
+                    self.client.delete("v1", "Pod", name, ns, grace_period_seconds=0)
+                except NotFound:
+                    pass
+            node.terminating.discard(name)
+
+        threading.Thread(target=finish, daemon=True, name=f"sim-terminate-{name}").start()
 
     def _node_status_loop(self, node: SimNode) -> None:
         last = None
@@ -525,22 +561,17 @@ class SimCluster:
                     "amd.com/gpu.allocated": ",".join(ids)}}}, run.ns)
             except NotFound:
                 pass
-            # OCI hook on a synthetic bundle, exactly as runc would call it (state on stdin)
-            bundle = os.path.join(node.dir, "bundles", run.name)
-            os.makedirs(bundle, exist_ok=True)
-            with open(os.path.join(bundle, "config.json"), "w") as f:
-                json.dump({"ociVersion": "1.1.0", "process": {"args": cmd, "env": [f"{k}={v}" for k, v in envs.items()]},
-                           "root": {"path": "rootfs"}, "linux": {}}, f)
-            state = json.dumps({"ociVersion": "1.1.0", "id": run.name, "status": "creating", "pid": os.getpid(),
-                                "bundle": bundle})
+            # OCI hook at the hooks.d precreate stage, exactly as CRI-O / podman
+            # call it: the runtime spec on stdin, the edited spec on stdout
+            spec = {"ociVersion": "1.1.0", "process": {"args": cmd, "env": [f"{k}={v}" for k, v in envs.items()]},
+                    "root": {"path": "rootfs"}, "linux": {}}
             import subprocess
 
-            p = subprocess.run([str(native.binary("amdgpu-oci-hook")), "prestart", "--root", node.env.sysfs_root()],
-                               input=state, capture_output=True, text=True, timeout=30)
+            p = subprocess.run([str(native.binary("amdgpu-oci-hook")), "precreate", "--root", node.env.sysfs_root()],
+                               input=json.dumps(spec), capture_output=True, text=True, timeout=30)
             if p.returncode != 0:
                 raise RuntimeError(f"OCI hook failed: {p.stderr.strip()}")
-            with open(os.path.join(bundle, "config.json")) as f:
-                spec = json.load(f)
+            spec = json.loads(p.stdout)
             paths = {d["path"] for d in spec.get("linux", {}).get("devices", [])}
             if "/dev/kfd" not in paths:
                 raise RuntimeError("OCI hook did not inject /dev/kfd")

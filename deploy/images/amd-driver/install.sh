@@ -2,7 +2,7 @@
 # Install + load the amdgpu kernel module for the running host kernel and the
 # ROCm userspace (gfx950 / MI355X), then wait for /dev/kfd.  Invoked by
 # `amdgpu-operator driver install` (amdgpu_operator/driver/manager.py) when the
-# N1 probe says the driver is not live.  Reference parity: the driver
+# N1 probe says the driver is not live, or the live one is not the requested one.  Reference parity: the driver
 # DaemonSet "installs the NVIDIA driver on the node" (README.md:212 of the
 # reference); here it is the amdgpu DKMS module + ROCm for gfx950.
 #
@@ -15,6 +15,8 @@
 #   AMDGPU_MODULE_PARAMS    extra `modprobe amdgpu` parameters
 #   AMDGPU_REPO_BASE        package mirror (air-gapped clusters); default repo.radeon.com
 #   AMDGPU_WAIT_SECONDS     how long to wait for /dev/kfd after modprobe (default 600)
+#   AMDGPU_FORCE_RELOAD     true: replace a live module even when its version
+#                           matches (the driver spec changed, e.g. module params)
 # Test hooks (tests/test_driver.py runs this script against a fake root):
 #   AMDGPU_SYS_ROOT / AMDGPU_DEV_ROOT / AMDGPU_ETC_ROOT  replace /sys, /dev, /etc
 #   KVER overrides `uname -r`; apt-get, modprobe, curl, gpg come from PATH.
@@ -28,9 +30,18 @@ REPO_BASE=${AMDGPU_REPO_BASE:-https://repo.radeon.com}
 log() { echo "{\"ts\": $(date +%s), \"component\": \"amd-driver-install\", \"msg\": \"$*\"}"; }
 live() { [ "$(cat "$SYS/module/amdgpu/initstate" 2>/dev/null || true)" = "live" ]; }
 
-if live && [ -e "$DEV/kfd" ]; then
-  log "amdgpu already live ($(cat "$SYS/module/amdgpu/version" 2>/dev/null || echo inbox)); nothing to install"
-  exit 0
+loaded_version() { cat "$SYS/module/amdgpu/version" 2>/dev/null || true; }
+
+# A live module is kept only when it is the requested one.  An inbox module
+# (no version file) is kept unless the manager asks for a reload, as it does
+# when the driver spec changed (AMDGPU_FORCE_RELOAD=true).
+if live && [ -e "$DEV/kfd" ] && [ "${AMDGPU_FORCE_RELOAD:-false}" != "true" ]; then
+  LV=$(loaded_version)
+  if [ -z "$LV" ] || [ -z "${AMDGPU_DRIVER_VERSION:-}" ] || [ "$LV" = "$AMDGPU_DRIVER_VERSION" ]; then
+    log "amdgpu already live (${LV:-inbox}); nothing to install"
+    exit 0
+  fi
+  log "amdgpu ${LV} live, ${AMDGPU_DRIVER_VERSION} requested: replacing it"
 fi
 : "${AMDGPU_DRIVER_VERSION:?AMDGPU_DRIVER_VERSION is required}"
 
@@ -64,7 +75,11 @@ if [ -n "${ROCM_VERSION:-}" ]; then
 fi
 
 if live; then
-  modprobe -r amdgpu || log "could not unload the running amdgpu (GPU in use?)"
+  # loading the new module over a live one would leave the old one in place
+  if ! modprobe -r amdgpu; then
+    log "could not unload the running amdgpu (GPU in use?)"
+    exit 1
+  fi
 fi
 # shellcheck disable=SC2086
 modprobe amdgpu ${AMDGPU_MODULE_PARAMS:-}
@@ -76,4 +91,9 @@ if ! [ -e "$DEV/kfd" ]; then
   log "amdgpu loaded but $DEV/kfd missing after ${WAIT}s"
   exit 1
 fi
-log "amdgpu $(cat "$SYS/module/amdgpu/version" 2>/dev/null || echo unknown) live"
+LV=$(loaded_version)
+if [ -n "$LV" ] && [ "$LV" != "$AMDGPU_DRIVER_VERSION" ]; then
+  log "amdgpu ${LV} loaded, ${AMDGPU_DRIVER_VERSION} requested"
+  exit 1
+fi
+log "amdgpu ${LV:-unknown} live"

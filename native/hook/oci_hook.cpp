@@ -4,7 +4,7 @@
 // container runtime (Docker, containerd) needs to use the GPU"
 // (/root/reference/README.md:105,203,210).  Upstream that is
 // nvidia-container-runtime + libnvidia-container; here there is NO runtime shim
-// (BASELINE.json north star).  Two integration paths, both produced by this
+// (BASELINE.json north star).  The runtime integration modes, all in this
 // one binary:
 //
 //   cdi       Generate a CDI spec (kind amd.com/gpu) from the live KFD/DRM
@@ -15,16 +15,27 @@
 //   apply     Edit an OCI bundle's config.json in place: add /dev/kfd and the
 //             requested render nodes to linux.devices, allow them in
 //             linux.resources.devices, optionally bind-mount ROCm read-only.
-//             Idempotent.  Requested devices come from --devices, or the
-//             device plugin's volume-mounts list (/dev/null bind mounts at
-//             /var/run/amd-container-devices/<sel>, with
-//             --accept-volume-mounts), or the container's AMD_VISIBLE_DEVICES
-//             env (set by the device plugin's Allocate; with
-//             --envvar-privileged-only only for containers holding
-//             CAP_SYS_ADMIN, so an unprivileged pod cannot name GPUs it was
-//             not allocated), or the amd.com/gpu.devices annotation.
-//   prestart  OCI hook entry point: reads the container state JSON on stdin
-//             (ociVersion/id/pid/bundle) and runs `apply` on that bundle.
+//             Idempotent.  For tools that prepare a bundle before `create`.
+//   precreate hooks.d "precreate" stage (CRI-O, podman): the runtime spec on
+//             stdin, the edited spec on stdout - the same edits as `apply`,
+//             made before the OCI runtime loads the spec, so they take effect.
+//   prestart  hooks.d / config.json "prestart" stage: the runtime has already
+//             loaded the spec, so editing config.json would change nothing.
+//             Reads the container state (pid, bundle) on stdin, selects the
+//             devices from the bundle's (read-only) config.json, then creates
+//             the device nodes inside the container (/proc/<pid>/root/dev) and
+//             allows them in its cgroup-v1 device controller.  On cgroup v2
+//             device access is an eBPF program the runtime attached at create
+//             time, which a hook cannot extend: it fails and names precreate /
+//             CDI instead of starting a container without its GPUs.
+//
+// Which devices: --devices, else the device plugin's volume-mounts list
+// (/dev/null bind mounts at /var/run/amd-container-devices/<sel>, with
+// --accept-volume-mounts), else the container's AMD_VISIBLE_DEVICES env (set
+// by the device plugin's Allocate) or the amd.com/gpu.devices annotation.
+// With --envvar-privileged-only the env AND the annotation are honoured only
+// for containers holding CAP_SYS_ADMIN: runtimes copy pod annotations into the
+// container spec, so an unprivileged pod must not name GPUs through either.
 //
 // Device selectors: "all", "none"/"void", or a comma list of indices into the
 // enumeration order, PCI BDFs ("0000:a4:00.0") or KFD unique ids ("0x...").
@@ -49,7 +60,7 @@
 
 namespace {
 
-const char* kVersion = "amdgpu-oci-hook 0.1.0";
+const char* kVersion = "amdgpu-oci-hook 0.2.0";
 
 struct Opts {
   std::string root = "/";
@@ -62,7 +73,9 @@ struct Opts {
   bool dry_run = false;
   bool partitions = true;
   bool accept_volume_mounts = false;   // device list from /var/run/amd-container-devices/<sel> mounts
-  bool envvar_privileged_only = false;  // AMD_VISIBLE_DEVICES only from CAP_SYS_ADMIN containers
+  bool envvar_privileged_only = false;  // env / annotation only from CAP_SYS_ADMIN containers
+  std::string proc_root = "/proc";      // prestart: /proc/<pid>/{root,cgroup} (tests: a fake tree)
+  std::string cgroup_root = "/sys/fs/cgroup";
 };
 
 constexpr const char* kDeviceListDir = "/var/run/amd-container-devices/";
@@ -387,6 +400,76 @@ void set_env(mj::Value& spec, const std::string& key, const std::string& value) 
   env.push(key + "=" + value);
 }
 
+// Devices the container asked for (see the header for the precedence).
+std::string requested(const Opts& o, const mj::Value& spec) {
+  if (!o.devices.empty()) return o.devices;
+  std::string sel;
+  if (o.accept_volume_mounts) sel = volume_mount_list(spec);
+  if (!sel.empty()) return sel;
+  const bool trusted = !o.envvar_privileged_only || privileged(spec);
+  if (!trusted) return "";
+  sel = env_lookup(spec, "AMD_VISIBLE_DEVICES");
+  if (sel.empty()) {
+    const mj::Value* ann = spec.find("annotations");
+    const mj::Value* a = ann ? ann->find("amd.com/gpu.devices") : nullptr;
+    if (a && a->is_string()) sel = a->str();
+  }
+  return sel;
+}
+
+// /dev/kfd plus the selected render nodes; false (with *err) on a bad selector.
+bool plan_devices(const Opts& o, const mj::Value& spec, std::vector<DevNode>* nodes, std::string* injected,
+                  std::string* err) {
+  nodes->clear();
+  injected->clear();
+  std::vector<at_gpu_t> gpus = enumerate(o);
+  std::vector<int> idx;
+  if (!select(gpus, requested(o, spec), &idx, err)) return false;
+  if (idx.empty()) return true;  // not a GPU container
+  DevNode kfd;
+  if (!kfd_node(o, &kfd)) {
+    *err = "cannot resolve /dev/kfd";
+    return false;
+  }
+  nodes->push_back(kfd);
+  for (int i : idx) {
+    DevNode rn;
+    render_node(o, gpus[i], &rn);
+    nodes->push_back(rn);
+    *injected += (injected->empty() ? "" : ",") + std::to_string(i);
+  }
+  return true;
+}
+
+// Spec edits shared by `apply` and `precreate`; *changed = false for a non-GPU container.
+bool edit_spec(const Opts& o, mj::Value& spec, bool* changed, std::string* err) {
+  *changed = false;
+  if (!spec.is_object()) {
+    *err = "runtime spec is not an object";
+    return false;
+  }
+  std::vector<DevNode> nodes;
+  std::string injected;
+  if (!plan_devices(o, spec, &nodes, &injected, err)) return false;
+  if (nodes.empty()) return true;
+  for (const DevNode& d : nodes) add_device(spec, d);
+  if (o.mount_rocm) add_mount(spec, o.rocm_dir);
+  set_env(spec, "AMD_VISIBLE_DEVICES", injected);
+  spec["annotations"]["amd.com/gpu.injected"] = injected;
+  *changed = true;
+  return true;
+}
+
+bool parse_json(const std::string& text, const std::string& what, mj::Value* out) {
+  try {
+    *out = mj::parse(text);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "amdgpu-oci-hook: %s: %s\n", what.c_str(), e.what());
+    return false;
+  }
+  return true;
+}
+
 int cmd_apply(const Opts& o) {
   if (o.bundle.empty()) {
     fprintf(stderr, "amdgpu-oci-hook: --bundle required\n");
@@ -399,51 +482,17 @@ int cmd_apply(const Opts& o) {
     return 1;
   }
   mj::Value spec;
-  try {
-    spec = mj::parse(text);
-  } catch (const std::exception& e) {
-    fprintf(stderr, "amdgpu-oci-hook: %s: %s\n", cfg_path.c_str(), e.what());
-    return 1;
-  }
-  if (!spec.is_object()) {
-    fprintf(stderr, "amdgpu-oci-hook: config.json is not an object\n");
-    return 1;
-  }
-  std::string sel = o.devices;
-  if (sel.empty() && o.accept_volume_mounts) sel = volume_mount_list(spec);
-  if (sel.empty() && (!o.envvar_privileged_only || privileged(spec))) sel = env_lookup(spec, "AMD_VISIBLE_DEVICES");
-  if (sel.empty()) {
-    const mj::Value* ann = spec.find("annotations");
-    const mj::Value* a = ann ? ann->find("amd.com/gpu.devices") : nullptr;
-    if (a && a->is_string()) sel = a->str();
-  }
-  std::vector<at_gpu_t> gpus = enumerate(o);
-  std::vector<int> idx;
+  if (!parse_json(text, cfg_path, &spec)) return 1;
+  bool changed = false;
   std::string err;
-  if (!select(gpus, sel, &idx, &err)) {
+  if (!edit_spec(o, spec, &changed, &err)) {
     fprintf(stderr, "amdgpu-oci-hook: %s\n", err.c_str());
     return 1;
   }
-  if (idx.empty()) {
+  if (!changed) {
     if (o.dry_run) printf("{\"devices\": []}\n");
     return 0;  // not a GPU container: leave the spec untouched
   }
-  DevNode kfd;
-  if (!kfd_node(o, &kfd)) {
-    fprintf(stderr, "amdgpu-oci-hook: cannot resolve /dev/kfd\n");
-    return 1;
-  }
-  add_device(spec, kfd);
-  std::string injected;
-  for (int i : idx) {
-    DevNode rn;
-    render_node(o, gpus[i], &rn);
-    add_device(spec, rn);
-    injected += (injected.empty() ? "" : ",") + std::to_string(i);
-  }
-  if (o.mount_rocm) add_mount(spec, o.rocm_dir);
-  set_env(spec, "AMD_VISIBLE_DEVICES", injected);
-  spec["annotations"]["amd.com/gpu.injected"] = injected;
   const std::string out = spec.dump(2) + "\n";
   if (o.dry_run) {
     fputs(out.c_str(), stdout);
@@ -456,30 +505,144 @@ int cmd_apply(const Opts& o) {
   return 0;
 }
 
+// hooks.d precreate: spec in on stdin, (edited) spec out on stdout - always
+// the whole spec, unchanged for a non-GPU container.
+int cmd_precreate(const Opts& o) {
+  std::stringstream ss;
+  ss << std::cin.rdbuf();
+  mj::Value spec;
+  if (!parse_json(ss.str(), "runtime spec on stdin", &spec)) return 1;
+  bool changed = false;
+  std::string err;
+  if (!edit_spec(o, spec, &changed, &err)) {
+    fprintf(stderr, "amdgpu-oci-hook: %s\n", err.c_str());
+    return 1;
+  }
+  const std::string out = spec.dump(2) + "\n";
+  if (fwrite(out.data(), 1, out.size(), stdout) != out.size() || fflush(stdout) != 0) {
+    fprintf(stderr, "amdgpu-oci-hook: cannot write the spec to stdout\n");
+    return 1;
+  }
+  return 0;
+}
+
+// The container's device cgroup from /proc/<pid>/cgroup: "v1:<path>" for a
+// cgroup-v1 devices hierarchy, "v2:<path>" for the unified hierarchy.
+std::string device_cgroup(const Opts& o, long pid) {
+  std::string text;
+  if (!read_file(join(o.proc_root, std::to_string(pid) + "/cgroup"), &text)) return "";
+  std::stringstream ss(text);
+  std::string line, v2;
+  while (std::getline(ss, line)) {
+    const size_t a = line.find(':'), b = a == std::string::npos ? a : line.find(':', a + 1);
+    if (b == std::string::npos) continue;
+    const std::string ctrls = line.substr(a + 1, b - a - 1), path = line.substr(b + 1);
+    std::stringstream cs(ctrls);
+    std::string c;
+    while (std::getline(cs, c, ','))
+      if (c == "devices") return "v1:" + path;
+    if (line.compare(0, 3, "0::") == 0) v2 = "v2:" + path;
+  }
+  return v2;
+}
+
+// hooks.d / config.json prestart: act on the created container (see header).
 int cmd_prestart(Opts o) {
   std::stringstream ss;
   ss << std::cin.rdbuf();
   mj::Value st;
-  try {
-    st = mj::parse(ss.str());
-  } catch (const std::exception& e) {
-    fprintf(stderr, "amdgpu-oci-hook: bad OCI state on stdin: %s\n", e.what());
-    return 1;
-  }
+  if (!parse_json(ss.str(), "OCI state on stdin", &st)) return 1;
   const mj::Value* b = st.find("bundle");
+  const mj::Value* p = st.find("pid");
   if (!b || !b->is_string()) {
     fprintf(stderr, "amdgpu-oci-hook: OCI state has no bundle\n");
     return 1;
   }
-  o.bundle = b->str();
-  return cmd_apply(o);
+  if (!p || !p->is_number() || p->num() <= 0) {
+    fprintf(stderr, "amdgpu-oci-hook: OCI state has no container pid\n");
+    return 1;
+  }
+  const long pid = (long)p->num();
+  std::string text;
+  const std::string cfg_path = b->str() + "/config.json";
+  mj::Value spec;
+  if (!read_file(cfg_path, &text) || !parse_json(text, cfg_path, &spec)) {
+    fprintf(stderr, "amdgpu-oci-hook: cannot read %s\n", cfg_path.c_str());
+    return 1;
+  }
+  std::vector<DevNode> nodes;
+  std::string injected, err;
+  if (!spec.is_object() || !plan_devices(o, spec, &nodes, &injected, &err)) {
+    fprintf(stderr, "amdgpu-oci-hook: %s\n", err.empty() ? "config.json is not an object" : err.c_str());
+    return 1;
+  }
+  if (nodes.empty()) {
+    if (o.dry_run) printf("{\"devices\": []}\n");
+    return 0;
+  }
+  const std::string cg = device_cgroup(o, pid);
+  if (cg.compare(0, 3, "v1:") != 0) {
+    fprintf(stderr,
+            "amdgpu-oci-hook: container %ld is not in a cgroup-v1 devices hierarchy (%s): a prestart hook cannot grant "
+            "device access; install the hook at the precreate stage or use CDI (amd.com/gpu=<id>)\n",
+            pid, cg.empty() ? "no cgroup" : cg.c_str());
+    return 1;
+  }
+  const std::string rootfs = join(o.proc_root, std::to_string(pid) + "/root");
+  const std::string allow = join(join(o.cgroup_root, "devices"), cg.substr(3)) + "/devices.allow";
+  mj::Value plan = mj::Value::object();
+  mj::Value mk = mj::Value::array(), rules = mj::Value::array();
+  for (const DevNode& d : nodes) {
+    mj::Value m = mj::Value::object();
+    m["path"] = join(rootfs, d.path);
+    m["major"] = d.major;
+    m["minor"] = d.minor;
+    mk.push(m);
+    rules.push("c " + std::to_string(d.major) + ":" + std::to_string(d.minor) + " rwm");
+  }
+  plan["mknod"] = mk;
+  plan["devices.allow"] = allow;
+  plan["rules"] = rules;
+  plan["injected"] = injected;
+  if (o.dry_run) {
+    fputs((plan.dump(2) + "\n").c_str(), stdout);
+    return 0;
+  }
+  // cgroup first: a node the container cannot open is useless, and a failed
+  // write must not leave half-made device nodes behind
+  for (const mj::Value& r : rules.arr()) {
+    std::ofstream f(allow, std::ios::app);  // one rule per write(2), as cgroupfs wants
+    if (!f || !(f << r.str()) || !f.flush()) {
+      fprintf(stderr, "amdgpu-oci-hook: cannot write '%s' to %s: %s\n", r.str().c_str(), allow.c_str(),
+              strerror(errno));
+      return 1;
+    }
+  }
+  for (const DevNode& d : nodes) {
+    const std::string path = join(rootfs, d.path);
+    const std::string dir = path.substr(0, path.rfind('/'));
+    std::string acc;
+    std::stringstream ds(dir.substr(1));
+    std::string part;
+    while (std::getline(ds, part, '/')) {
+      acc += "/" + part;
+      mkdir(acc.c_str(), 0755);
+    }
+    if (mknod(path.c_str(), S_IFCHR | 0666, makedev(d.major, d.minor)) != 0 && errno != EEXIST) {
+      fprintf(stderr, "amdgpu-oci-hook: mknod %s: %s\n", path.c_str(), strerror(errno));
+      return 1;
+    }
+    chmod(path.c_str(), 0666);
+  }
+  return 0;
 }
 
 void usage() {
   fprintf(stderr,
-          "usage: amdgpu-oci-hook {cdi|apply|prestart|--version} [--root DIR] [--bundle DIR] [--devices SEL]\n"
-          "                       [--output FILE] [--rocm-dir DIR] [--mount-rocm] [--kind KIND] [--dry-run]\n"
-          "                       [--accept-volume-mounts] [--envvar-privileged-only]\n");
+          "usage: amdgpu-oci-hook {cdi|apply|precreate|prestart|--version} [--root DIR] [--bundle DIR]\n"
+          "                       [--devices SEL] [--output FILE] [--rocm-dir DIR] [--mount-rocm] [--kind KIND]\n"
+          "                       [--dry-run] [--accept-volume-mounts] [--envvar-privileged-only]\n"
+          "                       [--proc-root DIR] [--cgroup-root DIR]\n");
 }
 
 }  // namespace
@@ -513,6 +676,8 @@ int main(int argc, char** argv) {
     else if (a == "--dry-run") o.dry_run = true;
     else if (a == "--accept-volume-mounts") o.accept_volume_mounts = true;
     else if (a == "--envvar-privileged-only") o.envvar_privileged_only = true;
+    else if (a == "--proc-root") ok = next(&o.proc_root);
+    else if (a == "--cgroup-root") ok = next(&o.cgroup_root);
     else ok = false;
     if (!ok) {
       usage();
@@ -521,6 +686,7 @@ int main(int argc, char** argv) {
   }
   if (cmd == "cdi") return cmd_cdi(o);
   if (cmd == "apply") return cmd_apply(o);
+  if (cmd == "precreate") return cmd_precreate(o);
   if (cmd == "prestart") return cmd_prestart(o);
   usage();
   return 2;

@@ -26,10 +26,14 @@ STUB = r'''#!/bin/bash
 echo "$(basename "$0") $*" >> "$FAKE_LOG"
 case "$(basename "$0")" in
   modprobe)
-    if [ "$1" = "-r" ]; then rm -f "$AMDGPU_SYS_ROOT/module/amdgpu/initstate"; exit 0; fi
+    if [ "$1" = "-r" ]; then
+      [ -z "${FAKE_MODPROBE_BUSY:-}" ] || { echo "modprobe: FATAL: Module amdgpu is in use." >&2; exit 1; }
+      rm -f "$AMDGPU_SYS_ROOT/module/amdgpu/initstate" "$AMDGPU_SYS_ROOT/module/amdgpu/version" "$AMDGPU_DEV_ROOT/kfd"
+      exit 0
+    fi
     mkdir -p "$AMDGPU_SYS_ROOT/module/amdgpu"
     echo live > "$AMDGPU_SYS_ROOT/module/amdgpu/initstate"
-    echo 6.12.12 > "$AMDGPU_SYS_ROOT/module/amdgpu/version"
+    echo "${FAKE_MODULE_VERSION:-$AMDGPU_DRIVER_VERSION}" > "$AMDGPU_SYS_ROOT/module/amdgpu/version"
     [ -n "${FAKE_MODPROBE_NO_KFD:-}" ] || : > "$AMDGPU_DEV_ROOT/kfd" ;;
   curl) echo "-----BEGIN PGP PUBLIC KEY BLOCK-----" ;;
   gpg) while [ $# -gt 0 ]; do [ "$1" = "-o" ] && { cat > "$2"; exit 0; }; shift; done; cat > /dev/null ;;
@@ -121,6 +125,48 @@ def test_inbox_module_is_unloaded_before_the_new_one(fake_host):
     assert log.index("modprobe -r amdgpu") < log.index("modprobe amdgpu")
 
 
+def _live_module(tmp, version="6.12.12"):
+    (tmp / "sys/module/amdgpu").mkdir(parents=True, exist_ok=True)
+    (tmp / "sys/module/amdgpu/initstate").write_text("live\n")
+    (tmp / "sys/module/amdgpu/version").write_text(version + "\n")
+    (tmp / "dev/kfd").write_text("")
+
+
+def test_live_module_of_another_version_is_replaced(fake_host):
+    tmp, env = fake_host
+    _live_module(tmp, "6.10.5")
+    r = run_script(env)  # requests 6.12.12
+    assert r.returncode == 0, r.stdout + r.stderr
+    log = calls(tmp)
+    assert log.index("modprobe -r amdgpu") < log.index("modprobe amdgpu")
+    assert (tmp / "sys/module/amdgpu/version").read_text().strip() == "6.12.12"
+    assert "6.10.5 live, 6.12.12 requested: replacing" in r.stdout
+
+
+def test_force_reload_replaces_a_matching_module(fake_host):
+    tmp, env = fake_host
+    _live_module(tmp, "6.12.12")
+    r = run_script(env, AMDGPU_FORCE_RELOAD="true", AMDGPU_MODULE_PARAMS="noretry=0")
+    assert r.returncode == 0, r.stderr
+    log = calls(tmp)
+    assert log.index("modprobe -r amdgpu") < log.index("modprobe amdgpu noretry=0")
+
+
+def test_unload_failure_fails_the_install(fake_host):
+    tmp, env = fake_host
+    _live_module(tmp, "6.10.5")
+    r = run_script(env, FAKE_MODPROBE_BUSY="1")
+    assert r.returncode == 1 and "could not unload" in r.stdout
+    assert "modprobe amdgpu" not in calls(tmp)  # never loads over the old module
+    assert (tmp / "sys/module/amdgpu/version").read_text().strip() == "6.10.5"
+
+
+def test_wrong_version_after_load_fails(fake_host):
+    tmp, env = fake_host
+    r = run_script(env, FAKE_MODULE_VERSION="6.8.0")
+    assert r.returncode == 1 and "6.8.0 loaded, 6.12.12 requested" in r.stdout
+
+
 def test_missing_headers_fall_back_and_version_is_required(fake_host):
     tmp, env = fake_host
     r = run_script(env, FAKE_APT_FAIL_HEADERS="1")
@@ -170,7 +216,68 @@ def test_monitor_clears_validations_when_driver_disappears(node_env):
     assert V.read_ready(node_env, "driver") is None and V.read_ready(node_env, "workload") is None
 
 
+def test_install_replaces_a_mismatched_module_through_the_backend(node_env):
+    kmod = fakesys.SimModule(node_env.sysfs_root())
+    node_env.extra["kmod"] = kmod
+    out = DM.install(node_env, timeout=5, cenv={"AMDGPU_DRIVER_VERSION": "6.14.0", "AMDGPU_DRIVER_SPEC_HASH": "h2"})
+    assert out["installed"] and out["driver_version"] == "6.14.0"
+    assert kmod.log == ["unload", "install 6.14.0"]
+    assert DM.read_state(node_env) | {"ts": 0} == {"version": "6.14.0", "specHash": "h2", "installed": True,
+                                                   "hostManaged": False, "ts": 0}
+    ann = node_env.client.get("v1", "Node", "n1")["metadata"]["annotations"]
+    assert ann["amd.com/gpu-driver.version"] == "6.14.0" and ann["amd.com/gpu-driver.spec-hash"] == "h2"
+    # same version, same spec: nothing to do
+    out = DM.install(node_env, timeout=5, cenv={"AMDGPU_DRIVER_VERSION": "6.14.0", "AMDGPU_DRIVER_SPEC_HASH": "h2"})
+    assert not out["installed"] and kmod.log == ["unload", "install 6.14.0"]
+    # same version, new spec (e.g. module params): reloaded
+    out = DM.install(node_env, timeout=5, cenv={"AMDGPU_DRIVER_VERSION": "6.14.0", "AMDGPU_DRIVER_SPEC_HASH": "h3",
+                                                "AMDGPU_MODULE_PARAMS": "noretry=1"})
+    assert out["installed"] and kmod.log[-1] == "install 6.14.0 noretry=1"
+
+
+def test_install_without_installer(node_env, monkeypatch, tmp_path):
+    monkeypatch.setattr(DM, "INSTALL_SCRIPT", str(tmp_path / "absent.sh"))
+    with pytest.raises(RuntimeError, match="loaded 6.12.12, requested 6.14.0"):
+        DM.install(node_env, timeout=5, cenv={"AMDGPU_DRIVER_VERSION": "6.14.0"})
+    assert V.read_ready(node_env, "driver") is None
+    # an inbox / built-in module reports no version: accepted as host-managed
+    os.unlink(os.path.join(node_env.sysfs_root(), "sys/module/amdgpu/version"))
+    out = DM.install(node_env, timeout=5, cenv={"AMDGPU_DRIVER_VERSION": "6.14.0"})
+    assert out["host_managed"] and not out["installed"]
+    assert node_env.client.get("v1", "Node", "n1")["metadata"]["annotations"]["amd.com/gpu-driver.version"] == "host"
+
+
+def test_prepare_upgrade_unloads_the_old_module(node_env):
+    kmod = fakesys.SimModule(node_env.sysfs_root())
+    node_env.extra["kmod"] = kmod
+    DM.install(node_env, timeout=5, cenv={"AMDGPU_DRIVER_VERSION": "6.12.12", "AMDGPU_DRIVER_SPEC_HASH": "h1"})
+    assert DM.prepare_upgrade(node_env, "6.12.12", spec_hash="h1")["upgrade"] is False
+    out = DM.prepare_upgrade(node_env, "6.12.12", spec_hash="h2")  # same version, new driver spec
+    assert out["upgrade"] and out["unloaded"] and "driver spec h1" in out["reason"]
+    assert kmod.log == ["unload"] and DM.loaded_version(node_env) == ""
+    assert DM.read_state(node_env) == {}
+    # the driver container then installs the requested module
+    out = DM.install(node_env, timeout=5, cenv={"AMDGPU_DRIVER_VERSION": "6.12.12", "AMDGPU_DRIVER_SPEC_HASH": "h2"})
+    assert out["installed"] and DM.read_state(node_env)["specHash"] == "h2"
+
+
+def test_prepare_upgrade_fails_when_the_module_cannot_be_unloaded(node_env):
+    kmod = fakesys.SimModule(node_env.sysfs_root())
+    kmod.busy = True
+    node_env.extra["kmod"] = kmod
+    with pytest.raises(RuntimeError, match="in use"):
+        DM.prepare_upgrade(node_env, "6.14.0", drain_timeout=0.1)
+    assert DM.loaded_version(node_env) == "6.12.12"
+
+
+def test_prepare_upgrade_without_installer_refuses(node_env, monkeypatch, tmp_path):
+    monkeypatch.setattr(DM, "INSTALL_SCRIPT", str(tmp_path / "absent.sh"))
+    with pytest.raises(RuntimeError, match="no installer"):
+        DM.prepare_upgrade(node_env, "6.14.0")
+
+
 def test_prepare_upgrade_drains_only_on_version_change(node_env):
+    node_env.extra["kmod"] = fakesys.SimModule(node_env.sysfs_root())
     DM.install(node_env, timeout=5)
     cur = DM.loaded_version(node_env)
     assert cur
@@ -181,8 +288,8 @@ def test_prepare_upgrade_drains_only_on_version_change(node_env):
                "spec": {"nodeName": "n1", "containers": [{"name": "c"}]}}
     node_env.client.create(gpu_pod)
     node_env.client.create(cpu_pod)
-    out = DM.prepare_upgrade(node_env, "99.0")
-    assert out["upgrade"] and out["desired"] == "99.0"
+    out = DM.prepare_upgrade(node_env, "99.0", drain_timeout=1)
+    assert out["upgrade"] and out["desired"] == "99.0" and out["unloaded"]
     names = {p["metadata"]["name"] for p in node_env.client.list("v1", "Pod", "default")}
     assert "web" in names and "train" not in names
     assert V.read_ready(node_env, "driver") is None

@@ -44,12 +44,23 @@ def test_hook_under_asan(asan_bins, tmp_path):
     b = tmp_path / "b"
     b.mkdir()
     (b / "config.json").write_text(json.dumps({"process": {"env": ["AMD_VISIBLE_DEVICES=all"]}, "linux": {}}))
-    state = json.dumps({"bundle": str(b), "id": "x"})
+    spec = (b / "config.json").read_text()
     for _ in range(2):
-        p = _run([hook, "prestart", "--root", root], state)
+        p = _run([hook, "precreate", "--root", root], spec)
         assert p.returncode == 0, p.stderr[-3000:]
+        assert len(json.loads(p.stdout)["linux"]["devices"]) == 65
+    proc = tmp_path / "proc"
+    (proc / "9/root").mkdir(parents=True)
+    (proc / "9/cgroup").write_text("5:devices:/k/c\n")
+    state = json.dumps({"bundle": str(b), "id": "x", "pid": 9})
+    p = _run([hook, "prestart", "--root", root, "--proc-root", str(proc), "--dry-run"], state)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(json.loads(p.stdout)["mknod"]) == 65
     for bad in ("{", '{"bundle": []}', "\x00\x01", '{"a": "\\ud800"}', "[" * 1000 + "]" * 1000):
         p = _run([hook, "prestart", "--root", root], bad)
+        assert p.returncode == 1, (bad[:20], p.returncode, p.stderr[-2000:])
+    for bad in ("{", "\x00\x01", "[" * 1000 + "]" * 1000, '"spec"'):  # not a JSON object
+        p = _run([hook, "precreate", "--root", root], bad)
         assert p.returncode == 1, (bad[:20], p.returncode, p.stderr[-2000:])
 
 

@@ -2,6 +2,7 @@
 
 import json
 import os
+import stat
 import subprocess
 
 import pytest
@@ -82,12 +83,85 @@ def test_apply_from_env_is_idempotent(root, tmp_path):
     assert s["linux"]["resources"]["devices"][0] == {"allow": False, "access": "rwm"}  # existing deny-all kept
 
 
-def test_prestart_reads_oci_state_from_stdin(root, tmp_path):
-    b = bundle(tmp_path, annotations={"amd.com/gpu.devices": "all"})
-    state = json.dumps({"ociVersion": "1.1.0", "id": "c1", "status": "creating", "pid": 1, "bundle": b})
-    p = run(["prestart", "--root", root], state)
+def _proc_tree(tmp_path, pid, cgroup_text):
+    """Fake /proc/<pid>/{root,cgroup} for the prestart stage."""
+    proc = tmp_path / "proc"
+    (proc / str(pid) / "root").mkdir(parents=True)
+    (proc / str(pid) / "cgroup").write_text(cgroup_text)
+    return str(proc)
+
+
+def test_precreate_edits_the_spec_on_stdin(root, tmp_path):
+    spec = {"ociVersion": "1.1.0", "process": {"args": ["sh"], "env": ["AMD_VISIBLE_DEVICES=1,3"]},
+            "root": {"path": "rootfs"}, "linux": {}}
+    p = run(["precreate", "--root", root], json.dumps(spec))
     assert p.returncode == 0, p.stderr
-    assert len(spec_of(b)["linux"]["devices"]) == 5
+    out = json.loads(p.stdout)
+    assert [d["path"] for d in out["linux"]["devices"]] == ["/dev/kfd", "/dev/dri/renderD136", "/dev/dri/renderD152"]
+    assert "AMD_VISIBLE_DEVICES=1,3" in out["process"]["env"]
+    # a non-GPU container comes back unchanged (the runtime uses whatever is on stdout)
+    plain = {"ociVersion": "1.1.0", "process": {"args": ["sh"], "env": ["PATH=/bin"]}, "linux": {}}
+    p = run(["precreate", "--root", root], json.dumps(plain))
+    assert p.returncode == 0 and json.loads(p.stdout) == plain
+    assert run(["precreate", "--root", root], "not json").returncode == 1
+
+
+def test_prestart_creates_nodes_in_the_container_and_allows_them(root, tmp_path):
+    """prestart runs after the runtime loaded config.json: it acts on the live
+    container (device nodes under /proc/<pid>/root, cgroup-v1 devices.allow)
+    and leaves config.json alone."""
+    b = bundle(tmp_path, env=["AMD_VISIBLE_DEVICES=2"])
+    before = open(os.path.join(b, "config.json")).read()
+    proc = _proc_tree(tmp_path, 4242, "12:devices:/kubepods/pod1/c1\n11:memory:/kubepods/pod1/c1\n")
+    cg = tmp_path / "cgroup"
+    (cg / "devices/kubepods/pod1/c1").mkdir(parents=True)
+    state = json.dumps({"ociVersion": "1.1.0", "id": "c1", "status": "created", "pid": 4242, "bundle": b})
+    args = ["prestart", "--root", root, "--proc-root", proc, "--cgroup-root", str(cg)]
+    p = run([*args, "--dry-run"], state)
+    assert p.returncode == 0, p.stderr
+    plan = json.loads(p.stdout)
+    assert [m["path"] for m in plan["mknod"]] == [f"{proc}/4242/root/dev/kfd", f"{proc}/4242/root/dev/dri/renderD144"]
+    assert plan["rules"] == ["c 241:0 rwm", "c 226:144 rwm"] and plan["injected"] == "2"
+    assert plan["devices.allow"] == f"{cg}/devices/kubepods/pod1/c1/devices.allow"
+    p = run(args, state)
+    allow = (cg / "devices/kubepods/pod1/c1/devices.allow").read_text()
+    assert allow == "c 241:0 rwmc 226:144 rwm"  # two writes (cgroupfs takes one rule per write)
+    node = tmp_path / "proc/4242/root/dev/dri/renderD144"
+    if p.returncode == 0:  # this process may create device nodes
+        assert stat.S_ISCHR(os.stat(node).st_mode) and os.major(os.stat(node).st_rdev) == 226
+    else:  # no CAP_MKNOD here: the failure names the node
+        assert "mknod" in p.stderr and "renderD" in p.stderr or "kfd" in p.stderr
+    assert open(os.path.join(b, "config.json")).read() == before
+
+
+def test_prestart_refuses_cgroup_v2(root, tmp_path):
+    b = bundle(tmp_path, env=["AMD_VISIBLE_DEVICES=0"])
+    proc = _proc_tree(tmp_path, 77, "0::/kubepods.slice/pod1/c1\n")
+    state = json.dumps({"ociVersion": "1.1.0", "id": "c1", "pid": 77, "bundle": b})
+    p = run(["prestart", "--root", root, "--proc-root", proc], state)
+    assert p.returncode == 1 and "precreate" in p.stderr and "cgroup-v1" in p.stderr
+    # a non-GPU container needs nothing from the hook, whatever the cgroup version
+    b2 = tmp_path / "b2"
+    b2.mkdir()
+    (b2 / "config.json").write_text(json.dumps({"process": {"env": []}}))
+    st2 = json.dumps({"pid": 77, "bundle": str(b2)})
+    assert run(["prestart", "--root", root, "--proc-root", proc], st2).returncode == 0
+
+
+def test_annotation_needs_privilege_with_envvar_privileged_only(root, tmp_path):
+    """Runtimes copy pod annotations into the spec: with --envvar-privileged-only
+    an unprivileged container cannot name GPUs through amd.com/gpu.devices."""
+    b = bundle(tmp_path, annotations={"amd.com/gpu.devices": "all"})
+    p = run(["apply", "--bundle", b, "--root", root, "--dry-run", "--envvar-privileged-only"])
+    assert p.returncode == 0 and json.loads(p.stdout) == {"devices": []}
+    b = bundle(tmp_path, annotations={"amd.com/gpu.devices": "all"},
+               extra={"process": {"args": ["sh"], "env": [], "capabilities": {"bounding": ["CAP_SYS_ADMIN"]}}})
+    p = run(["apply", "--bundle", b, "--root", root, "--dry-run", "--envvar-privileged-only"])
+    assert json.loads(p.stdout)["annotations"]["amd.com/gpu.injected"] == "0,1,2,3"
+    # without the policy flag the annotation still selects devices (trusted runtimes)
+    b = bundle(tmp_path, annotations={"amd.com/gpu.devices": "1"})
+    p = run(["apply", "--bundle", b, "--root", root, "--dry-run"])
+    assert json.loads(p.stdout)["annotations"]["amd.com/gpu.injected"] == "1"
 
 
 def test_selectors_bdf_and_unknown(root, tmp_path):
@@ -116,7 +190,7 @@ def test_mount_rocm_and_dry_run(root, tmp_path):
     assert "devices" not in spec_of(b)["linux"]  # dry run did not write
 
 
-@pytest.mark.parametrize("bad", ['{"bundle": 5}', "not json", "{}"])
+@pytest.mark.parametrize("bad", ['{"bundle": 5}', "not json", "{}", '{"bundle": "/nonexistent"}'])
 def test_bad_state(root, bad):
     p = run(["prestart", "--root", root], bad)
     assert p.returncode == 1

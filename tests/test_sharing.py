@@ -237,7 +237,9 @@ def test_toolkit_writes_hooks_d_entry_with_policy(tmp_path):
     args = tk.hook_args(accept_volume_mounts=True, envvar_unprivileged=False)
     assert args == ["--accept-volume-mounts", "--envvar-privileged-only"]
     j = json.loads(tk.oci_hook_json("/usr/local/amd/amdgpu-oci-hook", args))
-    assert j["hook"]["args"] == ["amdgpu-oci-hook", "prestart", *args] and j["stages"] == ["prestart"]
+    assert j["hook"]["args"] == ["amdgpu-oci-hook", "precreate", *args] and j["stages"] == ["precreate"]
+    drop = tk.dropin_config("amd", "/usr/local/amd/amdgpu-oci-hook", "/var/run/cdi", args)
+    assert 'pod_annotations = ["cdi.k8s.io/*"]' in drop and "amd.com/gpu.*" not in drop
 
 
 # ------------------------------------------------------------ GFD + integration
