@@ -210,6 +210,10 @@ class WorkloadSpec(_M):
     # kernel-check process ("shared": one process start + HIP init fewer, the
     # RCCL code-object load overlaps the kernel steps)
     rcclProcess: Literal["separate", "shared"] = "separate"
+    # start the validator processes while the driver is still being validated:
+    # they load their libraries and wait behind a start gate, so process start
+    # is off the time-to-Ready critical path (no GPU call before the gate opens)
+    prespawn: bool = True
 
 
 class ValidatorSpec(Operand):

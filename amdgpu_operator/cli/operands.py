@@ -38,6 +38,8 @@ def build_parser() -> argparse.ArgumentParser:
     v.add_argument("--timeout", type=float, default=600.0)
     v.add_argument("--wait-toolkit", action="store_true",
                    help="gpu: plugin validation waits for the toolkit; the workload starts right away")
+    v.add_argument("--with-driver", action="store_true",
+                   help="gpu: validate the driver here too; workload processes start at once behind a start gate")
 
     dp = sub.add_parser("device-plugin", help="kubelet device plugin for amd.com/gpu")
     dp.add_argument("--resource-name", default="amd.com/gpu")
@@ -95,7 +97,7 @@ def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
             known += args[i:i + 2]
             i += 2
             continue
-        if a == "--wait-toolkit":
+        if a in ("--wait-toolkit", "--with-driver"):
             known.append(a)
             i += 1
             continue
@@ -173,7 +175,7 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                 V.validate_plugin(env, a.resource, pod_args=pod_args, timeout=a.timeout, stop=stop)
         elif a.step == "gpu":
             V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
-                           wait_toolkit=a.wait_toolkit)
+                           wait_toolkit=a.wait_toolkit, with_driver=a.with_driver)
         else:
             V.complete(env)
             ready()

@@ -270,7 +270,13 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     if w.rcclProcess == "shared":
         wl_args += ["--rccl-shared-process"]
     inits = [_wait_init("driver-validation", image, v.imagePullPolicy, "driver")]
-    if v.pluginValidation and spec.devicePlugin.enabled:
+    if v.pluginValidation and spec.devicePlugin.enabled and w.prespawn:
+        # one init container validates the driver and, meanwhile, starts the
+        # workload processes behind their start gate (validate.py validate_gpu)
+        extra = ["--resource", spec.devicePlugin.resourceName, "--with-driver"] + \
+            (["--wait-toolkit"] if spec.toolkit.enabled else [])
+        inits = [_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args])]
+    elif v.pluginValidation and spec.devicePlugin.enabled:
         # workload (all GPUs, RCCL over xGMI) and plugin (1-GPU pods through the
         # device plugin + OCI hook) validation run concurrently.  The workload
         # needs only the driver (its processes run in this pod, not through the

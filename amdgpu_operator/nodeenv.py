@@ -9,8 +9,10 @@ temporary directories, so the operand code paths are identical.
 
 from __future__ import annotations
 
+import json
 import os
 import subprocess
+import threading
 import time
 from dataclasses import dataclass, field
 from typing import Callable
@@ -26,11 +28,75 @@ class ProcResult:
     seconds: float
 
 
+# In a child's environment: its result is final once it has printed its JSON
+# report and closed stdout/stderr (amdgpu-validator does), so the caller need
+# not wait for the process exit - the kernel's teardown of a GPU process
+# (KFD queues, VM, device memory) then runs off the time-to-Ready path.
+REPORT_EARLY_ENV = "AMDGPU_REPORT_EARLY"
+
+
+def report_rc(stdout: str) -> int:
+    """Exit status implied by the last stdout line (a JSON report with ``ok``)."""
+    lines = stdout.strip().splitlines()
+    try:
+        return 0 if lines and json.loads(lines[-1]).get("ok") is True else 1
+    except ValueError:
+        return 1
+
+
+class PipeReader:
+    """Drain a child's stdout and stderr on two threads (no pipe can fill up)."""
+
+    def __init__(self, proc: subprocess.Popen):
+        self.proc = proc
+        self._out: list[str] = []
+        self._err: list[str] = []
+        self._threads = [threading.Thread(target=lambda: self._out.append(proc.stdout.read()), daemon=True),
+                         threading.Thread(target=lambda: self._err.append(proc.stderr.read()), daemon=True)]
+        for th in self._threads:
+            th.start()
+
+    def eof(self) -> bool:
+        return not any(th.is_alive() for th in self._threads)
+
+    def join(self, timeout: float | None) -> bool:
+        deadline = None if timeout is None else time.monotonic() + timeout
+        for th in self._threads:
+            th.join(None if deadline is None else max(0.0, deadline - time.monotonic()))
+        return self.eof()
+
+    def text(self) -> tuple[str, str]:
+        return "".join(self._out), "".join(self._err)
+
+    def result(self, t0: float) -> ProcResult:
+        """At EOF: the exit status if the child is gone, else the report's
+        verdict (a reaper thread collects the exit later)."""
+        out, err = self.text()
+        rc = self.proc.poll()
+        if rc is None:
+            rc = report_rc(out)
+            threading.Thread(target=self.proc.wait, daemon=True).start()
+        return ProcResult(rc, out, err, time.perf_counter() - t0)
+
+
 def run_local(argv: list[str], env: dict | None = None, timeout: float = 300.0) -> ProcResult:
     """Run a native tool as a child process (never exec in-process)."""
     t0 = time.perf_counter()
     full_env = dict(os.environ)
     full_env.update(env or {})
+    if full_env.get(REPORT_EARLY_ENV) == "1":
+        p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=full_env)
+        reader = PipeReader(p)
+        if not reader.join(timeout):
+            p.kill()
+            reader.join(5)
+            try:
+                p.wait(5)
+            except subprocess.TimeoutExpired:
+                pass
+            out, err = reader.text()
+            return ProcResult(124, out, err + "\ntimeout", time.perf_counter() - t0)
+        return reader.result(t0)
     try:
         p = subprocess.run(argv, capture_output=True, text=True, env=full_env, timeout=timeout)
         return ProcResult(p.returncode, p.stdout, p.stderr, time.perf_counter() - t0)

@@ -26,14 +26,24 @@ import threading
 import time
 from concurrent.futures import Future
 
-from ..nodeenv import ProcResult
+from ..nodeenv import REPORT_EARLY_ENV, PipeReader, ProcResult
 
 
 class _Running:
-    def __init__(self, rid: int, proc: subprocess.Popen, t0: float):
+    def __init__(self, rid: int, proc: subprocess.Popen, t0: float, early: bool):
         self.rid = rid
         self.proc = proc
         self.t0 = t0
+        self.reader = PipeReader(proc)
+        self.early = early  # done at the report (pipes closed), not at the exit
+
+    def done(self) -> bool:
+        return self.reader.eof() and (self.early or self.proc.poll() is not None)
+
+    def result(self) -> ProcResult:
+        if not self.early:
+            self.proc.wait()
+        return self.reader.result(self.t0)
 
 
 def _spawn(argv: list[str], env: dict) -> subprocess.Popen:
@@ -97,15 +107,15 @@ class DistributedLauncher:
                 return
             for rid, argv, env, device in batch:
                 if device % self.world == self.rank:
-                    running.append(_Running(rid, _spawn(argv, env), time.perf_counter()))
+                    running.append(_Running(rid, _spawn(argv, env), time.perf_counter(),
+                                            (env or {}).get(REPORT_EARLY_ENV) == "1"))
             done = []
             still = []
             for r in running:
-                if r.proc.poll() is None:
+                if not r.done():
                     still.append(r)
                     continue
-                out, err = r.proc.communicate()
-                done.append((r.rid, ProcResult(r.proc.returncode, out, err, time.perf_counter() - r.t0)))
+                done.append((r.rid, r.result()))
             running = still
             gathered = [None] * self.world if self.rank == 0 else None
             dist.gather_object(done, gathered, dst=0, group=self.group)

@@ -13,9 +13,32 @@ import sys
 import time
 
 
+def wait_start_gate(path: str | None, timeout: float = 120.0) -> str:
+    """The native validator's ``--start-gate``: block until the file has a
+    verdict; "go" releases the process (same protocol as validator_main.cpp)."""
+    if not path:
+        return "go"
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        try:
+            with open(path) as f:
+                text = f.read().strip()
+            if text:
+                return text
+        except FileNotFoundError:
+            pass
+        time.sleep(0.001)
+    return "timeout"
+
+
 def main(argv: list[str]) -> int:
     def arg(name, default):
         return argv[argv.index(name) + 1] if name in argv else default
+
+    verdict = wait_start_gate(arg("--start-gate", None))
+    if verdict != "go":
+        print(json.dumps({"ok": False, "error": f"start gate: {verdict}", "steps": []}))
+        return 3
 
     rank, world = int(arg("--rank", "0")), int(arg("--world", "1"))
     rdv, run_id = arg("--rendezvous", "/tmp/amdgpu-validator"), arg("--run-id", "run")

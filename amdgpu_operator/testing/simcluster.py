@@ -42,7 +42,7 @@ from ..controller.reconciler import ClusterPolicyReconciler
 from ..kube import resources as R
 from ..kube.client import LocalClient, NotFound
 from ..kube.fakeapi import FakeApiServer
-from ..nodeenv import NodeEnv, ProcResult, run_local
+from ..nodeenv import REPORT_EARLY_ENV, NodeEnv, ProcResult, run_local
 from ..utils.logs import get_logger
 from . import fakesys
 from .fakekubelet import FakeKubelet
@@ -275,6 +275,12 @@ class SimCluster:
     def _launch(self, argv, env, device, timeout) -> ProcResult:
         if self.fake_gpu and argv and os.path.basename(argv[0]) == "amdgpu-validator":
             if self.fake_gpu != "procs":
+                from .fake_validator import wait_start_gate
+
+                gate = argv[argv.index("--start-gate") + 1] if "--start-gate" in argv else None
+                verdict = wait_start_gate(gate, timeout)
+                if verdict != "go":
+                    return ProcResult(3, json.dumps({"ok": False, "error": f"start gate: {verdict}"}) + "\n", "", 0.0)
                 return fake_validator_result(argv)
             # run a stand-in process through the real launcher path (multi-rank rehearsal)
             import sys
@@ -542,6 +548,7 @@ class SimCluster:
     def _run_gpu_workload(self, run: _PodRun, c: dict, cmd: list[str]) -> None:
         """Non-operand pod with GPU limits: Allocate -> OCI hook -> validator."""
         from .. import native
+        from ..validator.validate import REPORT_EARLY
 
         node = run.node
         limits = (c.get("resources") or {}).get("limits") or {}
@@ -576,7 +583,7 @@ class SimCluster:
             if "/dev/kfd" not in paths:
                 raise RuntimeError("OCI hook did not inject /dev/kfd")
         argv = [str(native.binary("amdgpu-validator"))] + cmd[1:]
-        proc_env = {}
+        proc_env = {REPORT_EARLY_ENV: "1"} if REPORT_EARLY else {}
         dev = devices[0] if devices else None
         if devices:
             proc_env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)

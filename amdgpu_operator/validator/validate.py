@@ -33,7 +33,7 @@ import uuid
 from concurrent.futures import ThreadPoolExecutor
 
 from .. import RESOURCE_NAME, native
-from ..nodeenv import NodeEnv
+from ..nodeenv import REPORT_EARLY_ENV, NodeEnv
 from ..utils.logs import get_logger
 
 log = get_logger("amdgpu.validator")
@@ -48,6 +48,8 @@ READY_FILES = {
 VALIDATED_LABEL = "amd.com/gpu.validated"
 MFMA_LABEL = "amd.com/gpu.validated.mfma"  # data types whose MFMA tile checked out on every GPU
 WORKLOAD_POD_LABEL = "amd.com/validator-workload"
+# take a validator process's result at its report, not at its exit (A/B: =0)
+REPORT_EARLY = os.environ.get("AMDGPU_VALIDATOR_REPORT_EARLY", "1") == "1"
 
 
 class StepFailed(RuntimeError):
@@ -138,8 +140,14 @@ def workload_argv(args: list[str], rank: int, world: int, rendezvous: str, run_i
             str(world), "--rendezvous", rendezvous, "--run-id", run_id, *args]
 
 
-def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: float = 600.0) -> dict:
-    """One native validator process per GPU, all ranks in one RCCL communicator."""
+def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: float = 600.0,
+                      start_gate: str | None = None) -> dict:
+    """One native validator process per GPU, all ranks in one RCCL communicator.
+
+    ``start_gate``: a file the processes wait on before their first HIP call
+    (``amdgpu-validator --start-gate``): "go" releases them, anything else
+    aborts them.  The caller spawns them before the driver is validated and
+    writes the verdict afterwards (:func:`validate_gpu`)."""
     from ..discovery import topology
 
     t0 = time.perf_counter()
@@ -177,7 +185,13 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
 
     def one(job):
         rank, jargs, rid, jenv = job
+        # the report (pipes closed) is the result: the process exit and the
+        # kernel's teardown of its GPU state do not hold up the node
+        if REPORT_EARLY:
+            jenv = {**jenv, REPORT_EARLY_ENV: "1"}
         argv = workload_argv(jargs, rank, world, rdv, rid, gpus[rank].index)
+        if start_gate:
+            argv += ["--start-gate", start_gate]
         return env.launch(argv, jenv, device=gpus[rank].index, timeout=timeout)
 
     with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
@@ -331,26 +345,56 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
 
 def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURCE_NAME,
                  pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
-                 wait_toolkit: bool = False) -> dict:
+                 wait_toolkit: bool = False, with_driver: bool = False) -> dict:
     """Workload and plugin validation concurrently (each skipped if already done).
 
     Only the driver gates the workload: its processes run in this privileged
     pod, not through the container runtime, so they start while the toolkit
     is still being installed.  The plugin pods go through the runtime hook
-    and therefore wait for the toolkit (``wait_toolkit``) before running."""
+    and therefore wait for the toolkit (``wait_toolkit``) before running.
+
+    ``with_driver``: this step also validates the driver (instead of a
+    separate init container before it).  The workload processes are spawned
+    right away behind a start gate, so their exec and library loading overlap
+    the driver wait; the gate opens only once :func:`validate_driver` passed
+    (and aborts them if it failed), so no GPU call precedes the driver."""
     t0 = time.perf_counter()
     results: dict = {}
     errors: list[str] = []
+    gate = None
+    driver_done = threading.Event()
+    if with_driver:
+        os.makedirs(env.validations_dir, exist_ok=True)
+        gate = os.path.join(env.validations_dir, f".start-gate-{uuid.uuid4().hex[:12]}")
+
+    def driver():
+        verdict = "abort"
+        try:
+            wait_ready(env, "driver", timeout, stop)
+            results["driver"] = validate_driver(env, timeout, stop)
+            verdict = "go"
+        except Exception as e:  # noqa: BLE001
+            errors.append(f"driver: {e}")
+        finally:
+            tmp = f"{gate}.tmp"
+            with open(tmp, "w") as f:
+                f.write(verdict)
+            os.replace(tmp, gate)
+            driver_done.set()
 
     def workload():
         try:
             if read_ready(env, "workload") is None:
-                results["workload"] = validate_workload(env, workload_args, timeout)
+                results["workload"] = validate_workload(env, workload_args, timeout, start_gate=gate)
         except Exception as e:  # noqa: BLE001
             errors.append(f"workload: {e}")
 
     def plugin():
         try:
+            if with_driver:
+                driver_done.wait()
+                if "driver" not in results:
+                    return
             if wait_toolkit:
                 wait_ready(env, "toolkit", timeout, stop)
             if os.environ.get("AMDGPU_EXPERIMENT_PLUGIN_AFTER_WORKLOAD"):  # start-up contention experiment
@@ -362,10 +406,19 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
 
     threads = [threading.Thread(target=workload, name="validate-workload"),
                threading.Thread(target=plugin, name="validate-plugin")]
-    for th in threads:
-        th.start()
-    for th in threads:
-        th.join()
+    if with_driver:
+        threads.insert(0, threading.Thread(target=driver, name="validate-driver"))
+    try:
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+    finally:
+        if gate:
+            try:
+                os.unlink(gate)
+            except FileNotFoundError:
+                pass
     if errors:
         raise StepFailed("; ".join(errors))
     return {"ok": True, "seconds": time.perf_counter() - t0, **results}

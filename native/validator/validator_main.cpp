@@ -16,7 +16,12 @@
 // Ranks of one node rendezvous through files in --rendezvous DIR (the host's
 // validations directory): the RCCL unique id, IPC handles and step barriers.
 // Prints one JSON report; exit status 0 = validated.
+// --start-gate FILE: the process may be spawned before the driver is
+// validated; it loads its libraries, then waits (no HIP call yet) until FILE
+// reads "go" - anything else aborts with status 3 - so exec and dynamic
+// linking overlap the driver validation instead of following it.
 
+#include <dirent.h>
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -128,6 +133,34 @@ Rccl g_rccl;
 // plugin-validation pods and the RCCL processes do not need.  The gate's
 // functions are looked up in the already-loaded tool (RTLD_NOLOAD); absent
 // tool = "unavailable" = fail closed.
+bool read_small(const std::string& path, std::string* out) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return false;
+  char buf[64];
+  const size_t n = fread(buf, 1, sizeof(buf), f);
+  fclose(f);
+  out->assign(buf, n);
+  return true;
+}
+
+// is one of this process's descriptors open on `target`?
+bool fd_open_to(const char* target) {
+  DIR* d = opendir("/proc/self/fd");
+  if (!d) return false;
+  bool found = false;
+  while (dirent* e = readdir(d)) {
+    char link[64], buf[256];
+    snprintf(link, sizeof(link), "/proc/self/fd/%s", e->d_name);
+    const ssize_t n = readlink(link, buf, sizeof(buf) - 1);
+    if (n > 0) {
+      buf[n] = 0;
+      if (strcmp(buf, target) == 0) found = true;
+    }
+  }
+  closedir(d);
+  return found;
+}
+
 struct Gate {
   int (*active)() = nullptr;
   void (*arm)(const char*) = nullptr;
@@ -188,6 +221,7 @@ struct Args {
   int rank = 0;
   int world = 1;
   std::string rendezvous = "/tmp/amdgpu-validator";
+  std::string start_gate;  // file whose content ("go" / anything else) releases the first HIP call
   std::string run_id = "run";
   std::string steps = "hip,vecadd,gemm,mfma,hbm,xgmi,rccl";
   int gemm_n = 4096;
@@ -729,7 +763,7 @@ void usage(const char* p) {
           "usage: %s [--device N] [--rank R --world W --rendezvous DIR --run-id ID] [--steps a,b,...]\n"
           "          [--gemm N] [--gemm-iters K] [--hbm-bytes B] [--rccl-elems E] [--xgmi-elems E]\n"
           "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--rccl-destroy]\n"
-          "          [--ready-file PATH]\n",
+          "          [--ready-file PATH] [--start-gate FILE]\n",
           p);
 }
 
@@ -766,6 +800,7 @@ int main(int argc, char** argv) {
     else if (k == "--any-arch") a.any_arch = true;
     else if (k == "--rccl-destroy") a.rccl_destroy = true;
     else if (k == "--ready-file") a.ready_file = v();
+    else if (k == "--start-gate") a.start_gate = v();
     else {
       usage(argv[0]);
       return 2;
@@ -794,6 +829,39 @@ int main(int argc, char** argv) {
     if (!g_rccl.load(Gate::exe_dir(), &err)) rccl_state.error = err;
     rccl_state.load_s = secs(tl);
   }
+  // Start gate: the process was spawned before the driver was validated, so
+  // its exec, dynamic linking and library constructors overlap that wait;
+  // nothing here has touched the GPU yet (kfd_open_at_gate reports whether
+  // the runtime opened /dev/kfd early, which would make the pre-spawn unsafe).
+  double gate_wait_s = -1;
+  bool kfd_early = false;
+  if (!a.start_gate.empty()) {
+    auto tg = Clock::now();
+    kfd_early = fd_open_to("/dev/kfd");
+    std::string verdict;
+    for (;;) {
+      std::string text;
+      if (read_small(a.start_gate, &text)) {
+        while (!text.empty() && (text.back() == '\n' || text.back() == ' ')) text.pop_back();
+        if (!text.empty()) {
+          verdict = text;
+          break;
+        }
+      }
+      if (secs(tg) > a.timeout_s) {
+        verdict = "timeout";
+        break;
+      }
+      usleep(250);
+    }
+    gate_wait_s = secs(tg);
+    if (verdict != "go") {
+      printf("{\"ok\": false, \"rank\": %d, \"world\": %d, \"device\": %d, \"error\": \"start gate: %s\", "
+             "\"steps\": []}\n", a.rank, a.world, a.device, verdict == "timeout" ? "timeout" : "aborted");
+      fflush(stdout);
+      _exit(3);
+    }
+  }
   try {
     steps.push_back(step_hip(a, &prop));
     ok = steps.back().ok;
@@ -815,6 +883,9 @@ int main(int argc, char** argv) {
   const double total = secs(t_start);
   std::string out = fmt("{\"ok\": %s, \"rank\": %d, \"world\": %d, \"device\": %d, \"seconds\": %.4f, ", ok ? "true" : "false",
                         a.rank, a.world, a.device, total);
+  if (gate_wait_s >= 0)
+    out += fmt("\"start_gate\": {\"wait_s\": %.4f, \"kfd_open_at_gate\": %s, \"steps_s\": %.4f}, ", gate_wait_s,
+               kfd_early ? "true" : "false", total - gate_wait_s);
   if (!error.empty()) {
     std::string esc;
     for (char c : error) esc += (c == '"' || c == '\\') ? '\'' : c;
@@ -847,5 +918,13 @@ int main(int argc, char** argv) {
   // AMDGPU_VALIDATOR_TEARDOWN=1: normal exit (profilers such as rocprofv3
   // write their results from the runtime's teardown)
   if (const char* t = getenv("AMDGPU_VALIDATOR_TEARDOWN"); t && strcmp(t, "1") == 0) return ok ? 0 : 1;
+  // Close our ends of stdout/stderr before exiting: a parent that takes the
+  // report as the result (AMDGPU_REPORT_EARLY) sees EOF now, while the
+  // kernel is still releasing this process's GPU queues and memory.
+  if (const int dn = open("/dev/null", O_WRONLY); dn >= 0) {
+    dup2(dn, 1);
+    dup2(dn, 2);
+    close(dn);
+  }
   _exit(ok ? 0 : 1);
 }

@@ -29,3 +29,23 @@ def test_bench_two_ranks_with_stand_in_validators():
     line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["config"]["allocatable_amd_com_gpu"] == 2
+
+
+def test_run_local_takes_the_report_before_the_exit():
+    """AMDGPU_REPORT_EARLY: the result is the child's report once it closed its
+    pipes; its (slow) exit is reaped in the background."""
+    import time
+
+    from amdgpu_operator.nodeenv import run_local
+
+    child = ("import json,os,sys,time;print(json.dumps({'ok': %s}));sys.stdout.flush();"
+             "n=os.open(os.devnull,os.O_WRONLY);os.dup2(n,1);os.dup2(n,2);time.sleep(3)")
+    t0 = time.perf_counter()
+    r = run_local([sys.executable, "-c", child % "True"], {"AMDGPU_REPORT_EARLY": "1"}, timeout=30)
+    assert r.rc == 0 and time.perf_counter() - t0 < 2.0 and '"ok": true' in r.stdout
+    r = run_local([sys.executable, "-c", child % "False"], {"AMDGPU_REPORT_EARLY": "1"}, timeout=30)
+    assert r.rc == 1  # the report's verdict
+    r = run_local([sys.executable, "-c", "import sys; sys.exit(7)"], {"AMDGPU_REPORT_EARLY": "1"}, timeout=30)
+    assert r.rc == 7  # already exited: its real status
+    r = run_local([sys.executable, "-c", "import time; time.sleep(5)"], {"AMDGPU_REPORT_EARLY": "1"}, timeout=0.5)
+    assert r.rc == 124

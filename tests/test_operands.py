@@ -297,3 +297,75 @@ def test_gpu_validation_overlaps_workload_with_toolkit_install(env):
         V.validate_gpu(env, [], timeout=0.3, wait_toolkit=True)
     assert seen_toolkit and all(t is None for t in seen_toolkit)
     assert V.read_ready(env, "workload")["ok"] and V.read_ready(env, "plugin") is None
+
+
+def _gated_launcher(env, log):
+    """Stand-in validator honouring --start-gate: records when it was spawned
+    and what the gate said, like amdgpu-validator does before its first HIP call."""
+    from amdgpu_operator.testing.fake_validator import wait_start_gate
+
+    def launcher(argv, e, device, timeout):
+        gate = argv[argv.index("--start-gate") + 1] if "--start-gate" in argv else None
+        log.append(("spawn", V.read_ready(env, "driver") is not None))
+        verdict = wait_start_gate(gate, 5)
+        log.append(("gate", verdict))
+        if verdict != "go":
+            return ProcResult(3, json.dumps({"ok": False, "error": f"start gate: {verdict}"}), "", 0.0)
+        steps = argv[argv.index("--steps") + 1].split(",")
+        return ProcResult(0, json.dumps({"ok": True, "steps": [{"name": s, "ok": True} for s in steps]}), "", 0.0)
+
+    return launcher
+
+
+def test_prespawned_workload_waits_for_driver_validation(env):
+    """with_driver: the validator processes start before the driver is ready,
+    and are released only after the driver validation passed."""
+    import threading
+    import time as _t
+
+    log = []
+    env.launcher = _gated_launcher(env, log)
+    for f in os.listdir(env.validations_dir) if os.path.isdir(env.validations_dir) else []:
+        os.unlink(os.path.join(env.validations_dir, f))
+
+    def driver_comes_up():
+        _t.sleep(0.2)
+        V.write_ready(env, "driver", {"ok": True})
+
+    th = threading.Thread(target=driver_comes_up)
+    th.start()
+    with pytest.raises(V.StepFailed, match="plugin"):  # no device plugin here: only the plugin step fails
+        V.validate_gpu(env, [], timeout=0.6, with_driver=True)
+    th.join()
+    spawns = [x for x in log if x[0] == "spawn"]
+    assert spawns and all(ready is False for _, ready in spawns)  # spawned before the driver was ready
+    assert [x for x in log if x[0] == "gate"] == [("gate", "go")] * len(spawns)
+    assert V.read_ready(env, "workload")["ok"]
+    assert not [f for f in os.listdir(env.validations_dir) if f.startswith(".start-gate")]  # gate file removed
+
+
+def test_prespawned_workload_aborts_when_the_driver_fails(env, monkeypatch):
+    log = []
+    env.launcher = _gated_launcher(env, log)
+    monkeypatch.setattr(V, "validate_driver", lambda *a, **k: (_ for _ in ()).throw(V.StepFailed("no kfd")))
+    V.write_ready(env, "driver", {"ok": True})
+    with pytest.raises(V.StepFailed, match="driver: no kfd"):
+        V.validate_gpu(env, [], timeout=1, with_driver=True)
+    assert ("gate", "abort") in log and V.read_ready(env, "workload") is None
+
+
+def test_validator_manifest_prespawn():
+    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, ClusterPolicySpec, deep_merge, parse_set_flags
+    from amdgpu_operator.controller import manifests as M
+
+    ref = parse_set_flags(REFERENCE_SET_FLAGS)
+
+    def inits(values):
+        ds = [o for o in M.state_validator(ClusterPolicySpec.model_validate(values), "ns", None)
+              if o["kind"] == "DaemonSet"][0]
+        return [(c["name"], c["args"]) for c in ds["spec"]["template"]["spec"]["initContainers"]]
+
+    on = inits(ref)
+    assert [n for n, _ in on] == ["gpu-validation"] and "--with-driver" in on[0][1]
+    off = inits(deep_merge(ref, {"validator": {"workload": {"prespawn": False}}}))
+    assert [n for n, _ in off] == ["driver-validation", "gpu-validation"] and "--with-driver" not in off[1][1]
