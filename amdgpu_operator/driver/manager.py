@@ -61,10 +61,16 @@ class HostModule:
     def install(self, env: NodeEnv, cenv: dict, timeout: float) -> None:
         subprocess.run([self.script], check=True, timeout=timeout, env={**os.environ, **cenv})
 
-    def unload(self, env: NodeEnv, timeout: float = 120.0) -> None:
-        p = subprocess.run(["modprobe", "-r", "amdgpu"], capture_output=True, text=True, timeout=timeout)
-        if p.returncode != 0:
-            raise RuntimeError(f"modprobe -r amdgpu failed ({p.returncode}): {p.stderr.strip()}")
+    def unload(self, env: NodeEnv, timeout: float = 120.0, retry_s: float = 5.0) -> None:
+        # a process that just exited may still be releasing its device files
+        deadline = time.monotonic() + retry_s
+        while True:
+            p = subprocess.run(["modprobe", "-r", "amdgpu"], capture_output=True, text=True, timeout=timeout)
+            if p.returncode == 0:
+                return
+            if time.monotonic() >= deadline:
+                raise RuntimeError(f"modprobe -r amdgpu failed ({p.returncode}): {p.stderr.strip()}")
+            time.sleep(0.5)
 
 
 def _kmod(env: NodeEnv):
@@ -117,6 +123,17 @@ def outdated(env: NodeEnv, desired_version: str, spec_hash: str = "") -> str:
     return ""
 
 
+def _release_gated_validators(env: NodeEnv) -> None:
+    """Validator processes waiting at their start gate may hold /dev/kfd
+    (validator/validate.py prespawn_safe): abort them before the module goes."""
+    from ..validator.validate import abort_start_gates
+
+    aborted = abort_start_gates(env)
+    if aborted:
+        log.info("aborted %d validator start gate(s) before the driver change", len(aborted))
+        time.sleep(0.2)  # they poll their gate every 0.25 ms and exit at once
+
+
 def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None = None,
             cenv: dict | None = None) -> dict:
     """``amd-driver-ctr``: make the requested driver live, then publish it.
@@ -145,6 +162,8 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
             if why:
                 log.info("replacing the live driver: %s", why)
                 cenv["AMDGPU_FORCE_RELOAD"] = "true"
+            if live:
+                _release_gated_validators(env)
             kmod.install(env, cenv, timeout)
             ran_script = True
         elif why:
@@ -219,6 +238,7 @@ def prepare_upgrade(env: NodeEnv, desired_version: str, drain: bool = True, spec
     clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
     if not wait_gpu_pods_gone(env, drain_timeout):
         log.warning("GPU pods still on the node after %.0f s; unloading anyway", drain_timeout)
+    _release_gated_validators(env)
     kmod.unload(env)
     _write_state(env, None)
     still, _ = topology.probe(env.sysfs_root())

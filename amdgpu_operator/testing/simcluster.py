@@ -197,6 +197,7 @@ class _PodRun:
                     pass
 
     def set_ready(self, container: str) -> None:
+        self.cluster.trace("container-ready", f"{self.name}/{container}")
         self.ready[container] = True
         self._status("Running", True)
 
@@ -216,12 +217,15 @@ class SimCluster:
         self.launcher = launcher
         self.api = FakeApiServer()
         self.api.graceful_pod_deletion = termination_s is not None
+        self.api.hooks.append(self._trace_api)
         self.client = LocalClient(self.api)
         self.nodes: dict[str, SimNode] = {}
         self.stop_event = threading.Event()
         self._threads: list[threading.Thread] = []
         self._lock = threading.RLock()
         self.reconciler: ClusterPolicyReconciler | None = None
+        # bring-up trace: (perf_counter, what, detail) - pods created/deleted,
+        # containers started/finished (bench.py --detail prints it per step)
         self.events: list[tuple[float, str, str]] = []
         self._node_specs = nodes
         self._short_dirs: list[str] = []
@@ -530,20 +534,37 @@ class SimCluster:
             except Exception:  # noqa: BLE001
                 pass
 
+    # --------------------------------------------------------------- trace
+    def trace(self, what: str, detail: str) -> None:
+        self.events.append((time.perf_counter(), what, detail))
+
+    def _trace_api(self, etype: str, obj: dict) -> None:
+        if obj.get("kind") == "Pod" and etype in ("ADDED", "DELETED"):
+            self.trace(f"pod-{etype.lower()}", obj["metadata"]["name"])
+
+    def trace_since(self, t0: float) -> list[tuple[float, str, str]]:
+        """Events after ``t0`` (perf_counter), times relative to it."""
+        return [(round(t - t0, 4), w, d) for t, w, d in list(self.events) if t >= t0]
+
     # ------------------------------------------------------------ containers
     def run_container(self, run: _PodRun, c: dict, init: bool) -> None:
         cmd = list(c.get("command") or []) + list(c.get("args") or [])
         if not cmd:
             raise RuntimeError(f"container {c['name']} has no command")
         prog = os.path.basename(cmd[0])
-        if prog == "amdgpu-operator":
-            from ..cli import operands
+        label = f"{run.name}/{c['name']}"
+        self.trace("container-start", label)
+        try:
+            if prog == "amdgpu-operator":
+                from ..cli import operands
 
-            operands.run_in_sim(self, run, c, cmd[1:], init)
-        elif prog == "amdgpu-validator":
-            self._run_gpu_workload(run, c, cmd)
-        else:
-            raise RuntimeError(f"unknown program {prog}")
+                operands.run_in_sim(self, run, c, cmd[1:], init)
+            elif prog == "amdgpu-validator":
+                self._run_gpu_workload(run, c, cmd)
+            else:
+                raise RuntimeError(f"unknown program {prog}")
+        finally:
+            self.trace("container-end", label)
 
     def _run_gpu_workload(self, run: _PodRun, c: dict, cmd: list[str]) -> None:
         """Non-operand pod with GPU limits: Allocate -> OCI hook -> validator."""

@@ -343,6 +343,56 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     return summary
 
 
+START_GATE_PREFIX = ".start-gate-"
+
+
+def prespawn_safe(env: NodeEnv) -> bool:
+    """May validator processes start before the driver validation?
+
+    A gated process (the counter-gate tool initialises the HSA runtime as
+    the process loads) opens ``/dev/kfd`` before its start gate, so it is
+    spawned early only when the kernel driver is already live and no driver
+    upgrade is under way on the node.  The driver manager aborts pending
+    gates before it unloads a module (driver/manager.py), so an early
+    process never holds the device against a driver replacement."""
+    from ..controller.upgrade import ACTIVE, STATE_LABEL
+    from ..discovery import topology
+
+    if not topology.probe(env.sysfs_root())[0]:
+        return False
+    try:
+        node = env.client.get("v1", "Node", env.node_name)
+    except Exception:  # noqa: BLE001 - no API answer: take the safe path
+        return False
+    return (node["metadata"].get("labels") or {}).get(STATE_LABEL) not in ACTIVE
+
+
+def abort_start_gates(env: NodeEnv) -> list[str]:
+    """Release every validator process still waiting at its start gate with
+    "abort" (they exit without touching the GPU further); returns the gates."""
+    out = []
+    try:
+        names = os.listdir(env.validations_dir)
+    except FileNotFoundError:
+        return out
+    for name in names:
+        if not name.startswith(START_GATE_PREFIX) or name.endswith(".tmp"):
+            continue
+        path = os.path.join(env.validations_dir, name)
+        try:
+            with open(path) as f:
+                if f.read().strip():
+                    continue  # verdict already given
+        except FileNotFoundError:
+            continue
+        tmp = f"{path}.abort.tmp"
+        with open(tmp, "w") as f:
+            f.write("abort")
+        os.replace(tmp, path)
+        out.append(name)
+    return out
+
+
 def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURCE_NAME,
                  pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                  wait_toolkit: bool = False, with_driver: bool = False) -> dict:
@@ -354,18 +404,21 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
     and therefore wait for the toolkit (``wait_toolkit``) before running.
 
     ``with_driver``: this step also validates the driver (instead of a
-    separate init container before it).  The workload processes are spawned
-    right away behind a start gate, so their exec and library loading overlap
-    the driver wait; the gate opens only once :func:`validate_driver` passed
-    (and aborts them if it failed), so no GPU call precedes the driver."""
+    separate init container before it).  When :func:`prespawn_safe`, the
+    workload processes are spawned right away behind a start gate, so their
+    exec and library loading overlap the driver wait; the gate opens only once
+    :func:`validate_driver` passed (and aborts them if it failed), so none of
+    the validator's own GPU work precedes the driver validation."""
     t0 = time.perf_counter()
     results: dict = {}
     errors: list[str] = []
     gate = None
     driver_done = threading.Event()
+    prespawn = with_driver and prespawn_safe(env)
     if with_driver:
         os.makedirs(env.validations_dir, exist_ok=True)
-        gate = os.path.join(env.validations_dir, f".start-gate-{uuid.uuid4().hex[:12]}")
+        gate = os.path.join(env.validations_dir, f"{START_GATE_PREFIX}{uuid.uuid4().hex[:12]}")
+        open(gate, "w").close()  # empty = no verdict yet (driver/manager.py may abort it)
 
     def driver():
         verdict = "abort"
@@ -384,6 +437,10 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
 
     def workload():
         try:
+            if with_driver and not prespawn:  # spawn only once the driver passed
+                driver_done.wait()
+                if "driver" not in results:
+                    return
             if read_ready(env, "workload") is None:
                 results["workload"] = validate_workload(env, workload_args, timeout, start_gate=gate)
         except Exception as e:  # noqa: BLE001

@@ -121,6 +121,7 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
                 timeline[step] = round(r["time"] - t0_wall, 4)
         return {
             "time_to_ready_s": ttr,
+            "trace": cluster.trace_since(t0),
             "timeline_s": timeline,
             "wall_s": t_total,
             "allocatable": alloc,

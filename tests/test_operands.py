@@ -369,3 +369,39 @@ def test_validator_manifest_prespawn():
     assert [n for n, _ in on] == ["gpu-validation"] and "--with-driver" in on[0][1]
     off = inits(deep_merge(ref, {"validator": {"workload": {"prespawn": False}}}))
     assert [n for n, _ in off] == ["driver-validation", "gpu-validation"] and "--with-driver" not in off[1][1]
+
+
+def test_no_prespawn_while_the_driver_is_not_live_or_upgrading(env):
+    """Early processes would open /dev/kfd before their gate (the counter-gate
+    tool starts the HSA runtime at load): not before the module is live, not
+    during a driver upgrade - then they are spawned after the validation."""
+    from amdgpu_operator.controller.upgrade import POD_RESTART, STATE_LABEL
+
+    assert V.prespawn_safe(env)
+    env.client.patch("v1", "Node", "n1", {"metadata": {"labels": {STATE_LABEL: POD_RESTART}}})
+    assert not V.prespawn_safe(env)
+    log = []
+    env.launcher = _gated_launcher(env, log)
+    V.write_ready(env, "driver", {"ok": True})
+    with pytest.raises(V.StepFailed, match="plugin"):
+        V.validate_gpu(env, [], timeout=0.5, with_driver=True)
+    spawns = [x for x in log if x[0] == "spawn"]
+    assert spawns and all(ready for _, ready in spawns)  # after the driver validation
+    env.client.patch("v1", "Node", "n1", {"metadata": {"labels": {STATE_LABEL: None}}})
+    os.unlink(os.path.join(env.sysfs_root(), "dev/kfd"))
+    assert not V.prespawn_safe(env)
+
+
+def test_driver_change_aborts_waiting_start_gates(env):
+    from amdgpu_operator.driver import manager as DM
+
+    os.makedirs(env.validations_dir, exist_ok=True)
+    waiting = os.path.join(env.validations_dir, V.START_GATE_PREFIX + "a")
+    released = os.path.join(env.validations_dir, V.START_GATE_PREFIX + "b")
+    open(waiting, "w").close()
+    with open(released, "w") as f:
+        f.write("go")
+    env.extra["kmod"] = fakesys.SimModule(env.sysfs_root())
+    out = DM.prepare_upgrade(env, "9.9.9", drain_timeout=0.1)
+    assert out["unloaded"]
+    assert open(waiting).read() == "abort" and open(released).read() == "go"
