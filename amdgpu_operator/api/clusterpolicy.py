@@ -203,6 +203,10 @@ class WorkloadSpec(_M):
     minGemmTflops: float = 0.0
     minHbmGbps: float = 0.0
     counterGate: bool = True
+    # how the gate reads the counters: "aql" - AQL profiling packets around one
+    # more dispatch of the GEMM on the validator's own HSA queue (no profiler
+    # runtime in the process); "sdk" - the rocprofiler-sdk tool library
+    counterGateMode: Literal["aql", "sdk"] = "aql"
     # run the RCCL check (own process, world 1) on a single-GPU node too: the
     # multi-GPU critical path, rehearsed where there is no xGMI peer
     rcclSingleGpu: bool = False

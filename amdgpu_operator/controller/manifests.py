@@ -264,7 +264,7 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     if w.minHbmGbps:
         wl_args += ["--min-hbm-gbps", str(w.minHbmGbps)]
     if w.counterGate:
-        wl_args += ["--counter-gate"]
+        wl_args += ["--counter-gate"] + (["--gate-mode", "sdk"] if w.counterGateMode == "sdk" else [])
     if w.rcclSingleGpu:
         wl_args += ["--rccl-single-gpu"]
     if w.rcclProcess == "shared":

@@ -135,6 +135,10 @@ def gate_env() -> dict:
             "ROCPROFILER_METRICS_PATH": str(native.artefact("gate-metrics"))}
 
 
+def _arg_value(args: list[str], flag: str) -> str | None:
+    return args[args.index(flag) + 1] if flag in args and args.index(flag) + 1 < len(args) else None
+
+
 def workload_argv(args: list[str], rank: int, world: int, rendezvous: str, run_id: str, device: int) -> list[str]:
     return [str(native.binary("amdgpu-validator")), "--device", str(device), "--rank", str(rank), "--world",
             str(world), "--rendezvous", rendezvous, "--run-id", run_id, *args]
@@ -164,7 +168,9 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     os.makedirs(rdv, exist_ok=True)
     # N7: the counter gate is a rocprofiler-sdk tool library loaded only into
     # the gated kernel processes (the binary does not link the SDK)
-    counter_env = gate_env() if "--counter-gate" in args else {}
+    # (the default AQL-packet gate needs no tool library: only --gate-mode sdk)
+    sdk_gate = "--counter-gate" in args and _arg_value(args, "--gate-mode") == "sdk"
+    counter_env = gate_env() if sdk_gate else {}
     rccl_single = "--rccl-single-gpu" in args  # validate.py's own flags, not the binary's
     rccl_shared = "--rccl-shared-process" in args
     args = _drop_flag(_drop_flag(args, "--rccl-single-gpu"), "--rccl-shared-process")
@@ -346,18 +352,23 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
 START_GATE_PREFIX = ".start-gate-"
 
 
-def prespawn_safe(env: NodeEnv) -> bool:
+def prespawn_safe(env: NodeEnv, sdk_gate: bool = False) -> bool:
     """May validator processes start before the driver validation?
 
-    A gated process (the counter-gate tool initialises the HSA runtime as
-    the process loads) opens ``/dev/kfd`` before its start gate, so it is
-    spawned early only when the kernel driver is already live and no driver
-    upgrade is under way on the node.  The driver manager aborts pending
-    gates before it unloads a module (driver/manager.py), so an early
-    process never holds the device against a driver replacement."""
+    Without a profiler tool a process touches no device before its start
+    gate (``kfd_open_at_gate`` false), so it may always start early.  With
+    the rocprofiler-sdk gate (``--gate-mode sdk``) the tool initialises the
+    HSA runtime as the process loads and opens ``/dev/kfd`` before the gate:
+    such a process is spawned early only when the kernel driver is already
+    live and no driver upgrade is under way on the node.  Either way the
+    driver manager aborts pending gates before it unloads a module
+    (driver/manager.py), so an early process never holds the device against
+    a driver replacement."""
     from ..controller.upgrade import ACTIVE, STATE_LABEL
     from ..discovery import topology
 
+    if not sdk_gate:
+        return True
     if not topology.probe(env.sysfs_root())[0]:
         return False
     try:
@@ -414,7 +425,8 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
     errors: list[str] = []
     gate = None
     driver_done = threading.Event()
-    prespawn = with_driver and prespawn_safe(env)
+    sdk_gate = "--counter-gate" in workload_args and _arg_value(workload_args, "--gate-mode") == "sdk"
+    prespawn = with_driver and prespawn_safe(env, sdk_gate)
     if with_driver:
         os.makedirs(env.validations_dir, exist_ok=True)
         gate = os.path.join(env.validations_dir, f"{START_GATE_PREFIX}{uuid.uuid4().hex[:12]}")

@@ -59,6 +59,8 @@ def parse():
                     help="rehearsal: run the RCCL validation process at N=1 too (multi-GPU critical path)")
     ap.add_argument("--rccl-process", choices=["separate", "shared"], default=None,
                     help="RCCL check in its own process per GPU or in the kernel-check process")
+    ap.add_argument("--gate-mode", choices=["aql", "sdk"], default=None,
+                    help="counter gate through AQL profiling packets (default) or the rocprofiler-sdk tool")
     ap.add_argument("--no-prespawn", action="store_true",
                     help="start the validator processes only after the driver validation (A/B of the start gate)")
     ap.add_argument("--timeout", type=float, default=120.0)
@@ -88,6 +90,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
         values = deep_merge(values, {"validator": {"workload": {"rcclSingleGpu": True}}})
     if args.rccl_process:
         values = deep_merge(values, {"validator": {"workload": {"rcclProcess": args.rccl_process}}})
+    if args.gate_mode:
+        values = deep_merge(values, {"validator": {"workload": {"counterGateMode": args.gate_mode}}})
     if args.no_prespawn:
         values = deep_merge(values, {"validator": {"workload": {"prespawn": False}}})
     if args.quick_workload:

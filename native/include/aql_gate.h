@@ -1,0 +1,31 @@
+// N7 counter gate without a profiler runtime: PMC counters of one dispatch of
+// the validator's own GEMM, read through AQL profiling packets on a private
+// HSA queue (native/prof/aql_gate.cpp).
+#pragma once
+
+#include <cstdint>
+
+#define AVK_AQL_GATE_COUNTERS 4
+
+struct avk_aql_gate_result {
+  // SQ_INSTS_VALU_MFMA_MOPS_BF16, SQ_VALU_MFMA_BUSY_CYCLES, SQ_WAVES, GRBM_GUI_ACTIVE
+  double values[AVK_AQL_GATE_COUNTERS];
+  int samples[AVK_AQL_GATE_COUNTERS];  // per-instance samples summed into each value
+  double setup_s;                      // aqlprofile load, queue, code object, buffers
+  double dispatch_s;                   // start packet -> stop packet completion
+};
+
+extern "C" {
+// Counter names in the order of avk_aql_gate_result::values.
+const char* avk_aql_gate_counter_name(int i);
+
+// Dispatch gemm_bf16_nt_8p_kernel<false,false,false> (C = A * Bt^T, bf16 out)
+// from the code object at `code_object` on the GPU at `pci_bus_id`
+// ("dddd:bb:dd.f", hipDeviceGetPCIBusId), bracketed by aqlprofile start/stop
+// packets on a private queue, and sum every per-instance counter sample.  A,
+// Bt and C are device pointers (hipMalloc); M, N and K are multiples of 256
+// (the kernel's tile).  Waits at most timeout_s for the stop packet.  Returns
+// 0, or -1 with a message in err.
+int avk_aql_gate_gemm(const char* pci_bus_id, const void* A, const void* Bt, void* C, int M, int N, int K,
+                      const char* code_object, double timeout_s, avk_aql_gate_result* out, char* err, int errlen);
+}

@@ -7,7 +7,10 @@
 //   hip     device open, gfx950 check, properties
 //   vecadd  K1, exact host check
 //   gemm    K2 MFMA bf16 GEMM: Freivalds check on an fp32-output pass, timed
-//           bf16 pass, N7 counter gate (MFMA MOPS / busy cycles) when enabled
+//           bf16 pass, N7 counter gate (MFMA MOPS / busy cycles) when enabled:
+//           AQL profiling packets around one more dispatch on a private HSA
+//           queue (--gate-mode aql, default) or the rocprofiler-sdk tool
+//           library (--gate-mode sdk)
 //   hbm     K3 streaming copy, checksum-verified bandwidth
 //   xgmi    K4 one-shot all-reduce: emulated peers on 1 GPU, or real peers
 //           (hipIpc-mapped buffers of the other validator ranks, over xGMI)
@@ -42,6 +45,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "aql_gate.h"
 #include "avk.h"
 
 namespace {
@@ -222,6 +226,7 @@ struct Args {
   int world = 1;
   std::string rendezvous = "/tmp/amdgpu-validator";
   std::string start_gate;  // file whose content ("go" / anything else) releases the first HIP call
+  std::string gate_mode = "aql";  // counter gate: "aql" (AQL profiling packets) or "sdk" (rocprofiler-sdk tool)
   std::string run_id = "run";
   std::string steps = "hip,vecadd,gemm,mfma,hbm,xgmi,rccl";
   int gemm_n = 4096;
@@ -363,6 +368,51 @@ Step step_vecadd(const Args&, hipStream_t st) {
   return s;
 }
 
+// N7 on AQL profiling packets (prof/aql_gate.cpp): one more dispatch of the
+// same GEMM on a private queue between PM4 start/stop packets.  Its output is
+// checked against the HIP path's (checksum of C before and after, C zeroed in
+// between), so the counted dispatch is the validated computation, not a stand-in.
+bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, hipStream_t st, std::string* json) {
+  const auto tg = Clock::now();
+  unsigned long long* cs;
+  HIP_OK(hipMalloc(&cs, 16));
+  HIP_OK(hipMemsetAsync(cs, 0, 16, st));
+  AVK_OK(avk_checksum(C16, (int64_t)n * n * 2, cs, st));
+  HIP_OK(hipMemsetAsync(C16, 0, (size_t)n * n * 2, st));
+  HIP_OK(hipStreamSynchronize(st));
+  char bus[64] = {0};
+  HIP_OK(hipDeviceGetPCIBusId(bus, sizeof(bus), a.device));
+  const std::string co = Gate::exe_dir() + "validator_kernels.co";
+  avk_aql_gate_result r;
+  char err[512] = {0};
+  const int rc = avk_aql_gate_gemm(bus, A, B, C16, n, n, n, co.c_str(), 5.0, &r, err, sizeof(err));
+  unsigned long long sums[2] = {0, 0};
+  if (rc == 0) {
+    AVK_OK(avk_checksum(C16, (int64_t)n * n * 2, cs + 1, st));
+    HIP_OK(hipMemcpyAsync(sums, cs, 16, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
+  (void)hipFree(cs);
+  if (rc != 0) {
+    std::string esc;
+    for (const char* c = err; *c; ++c) esc += (*c == '"' || *c == '\\') ? '\'' : *c;
+    *json = "\"counter_gate\": \"unavailable\", \"gate_mode\": \"aql\", \"gate_error\": \"" + esc + "\"";
+    return false;
+  }
+  const double mops = r.values[0], busy = r.values[1], waves = r.values[2], gui = r.values[3];
+  const double flops = 2.0 * n * (double)n * n;
+  const bool same = sums[0] == sums[1] && sums[0] != 0;
+  const bool ok = mops > 0 && busy > 0 && same;
+  *json = fmt("\"counter_gate\": \"%s\", \"gate_mode\": \"aql\", \"dispatches\": 1, "
+              "\"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.0f, \"SQ_VALU_MFMA_BUSY_CYCLES\": %.0f, \"SQ_WAVES\": %.0f, "
+              "\"GRBM_GUI_ACTIVE\": %.0f, \"flop_per_mop\": %.6g, \"samples\": [%d, %d, %d, %d], "
+              "\"gated_output_matches\": %s, \"gate_seconds\": %.4f, \"gate_setup_seconds\": %.4f, "
+              "\"gate_dispatch_seconds\": %.4f",
+              ok ? "pass" : "fail", mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0, r.samples[0], r.samples[1],
+              r.samples[2], r.samples[3], same ? "true" : "false", secs(tg), r.setup_s, r.dispatch_s);
+  return ok;
+}
+
 Step step_gemm(const Args& a, hipStream_t st) {
   auto t0 = Clock::now();
   Step s{"gemm"};
@@ -408,6 +458,22 @@ Step step_gemm(const Args& a, hipStream_t st) {
   HIP_OK(hipEventSynchronize(e1));
   // counter gate on one extra dispatch: counter collection serialises
   // dispatches, so it must not overlap the timed ones
+  if (a.counter_gate && a.gate_mode == "aql") {
+    std::string gate_json;
+    const bool gate_ok = aql_gate(a, A, B, C16, n, st, &gate_json);
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= a.gemm_iters;
+    const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) (void)hipFree(p);
+    const bool perf_ok = a.min_gemm_tflops <= 0 || tflops >= a.min_gemm_tflops;
+    s.ok = numerics_ok && gate_ok && perf_ok;
+    s.seconds = secs(t0);
+    s.detail = fmt("\"n\": %d, \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, ", n, rel, ms, tflops) + gate_json;
+    return s;
+  }
   const bool gate = a.counter_gate && g_gate.usable();
   const auto tg = Clock::now();
   if (gate) {
@@ -440,8 +506,9 @@ Step step_gemm(const Args& a, hipStream_t st) {
       const int disp = g_gate.dispatches();
       const double flops = 2.0 * n * (double)n * n * (disp > 0 ? disp : 1);
       gate_ok = disp > 0 && mops > 0 && busy > 0;
-      gate_json = fmt("\"counter_gate\": \"%s\", \"dispatches\": %d, \"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.6g, "
-                      "\"SQ_VALU_MFMA_BUSY_CYCLES\": %.6g, \"SQ_WAVES\": %.6g, \"GRBM_GUI_ACTIVE\": %.6g, "
+      gate_json = fmt("\"counter_gate\": \"%s\", \"gate_mode\": \"sdk\", \"dispatches\": %d, "
+                      "\"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.0f, "
+                      "\"SQ_VALU_MFMA_BUSY_CYCLES\": %.0f, \"SQ_WAVES\": %.0f, \"GRBM_GUI_ACTIVE\": %.0f, "
                       "\"flop_per_mop\": %.6g, \"gate_seconds\": %.4f, \"gate_config_seconds\": %.4f",
                       gate_ok ? "pass" : "fail", disp, mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0,
                       secs(tg), g_gate.config_seconds ? g_gate.config_seconds() : -1.0);
@@ -763,7 +830,7 @@ void usage(const char* p) {
           "usage: %s [--device N] [--rank R --world W --rendezvous DIR --run-id ID] [--steps a,b,...]\n"
           "          [--gemm N] [--gemm-iters K] [--hbm-bytes B] [--rccl-elems E] [--xgmi-elems E]\n"
           "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--rccl-destroy]\n"
-          "          [--ready-file PATH] [--start-gate FILE]\n",
+          "          [--ready-file PATH] [--start-gate FILE] [--gate-mode aql|sdk]\n",
           p);
 }
 
@@ -801,6 +868,7 @@ int main(int argc, char** argv) {
     else if (k == "--rccl-destroy") a.rccl_destroy = true;
     else if (k == "--ready-file") a.ready_file = v();
     else if (k == "--start-gate") a.start_gate = v();
+    else if (k == "--gate-mode") a.gate_mode = v();
     else {
       usage(argv[0]);
       return 2;
@@ -812,7 +880,11 @@ int main(int argc, char** argv) {
     fprintf(stderr, "amdgpu-validator: invalid arguments (gemm %% 256, sizes %% 16, world <= 64, xgmi needs world <= 8)\n");
     return 2;
   }
-  if (a.counter_gate) Gate::request();
+  if (a.gate_mode != "aql" && a.gate_mode != "sdk") {
+    fprintf(stderr, "amdgpu-validator: --gate-mode is aql or sdk\n");
+    return 2;
+  }
+  if (a.counter_gate && a.gate_mode == "sdk") Gate::request();
   mkdir(a.rendezvous.c_str(), 0755);
   Rendezvous rv{a.rendezvous, a.rank, a.world, a.timeout_s};
   std::vector<Step> steps;

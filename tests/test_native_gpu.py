@@ -23,8 +23,8 @@ def _run(args, env=None, timeout=120):
 
 
 def test_validator_all_local_steps_with_counter_gate(tmp_path):
-    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,vecadd,gemm,mfma,hbm,xgmi", "--counter-gate"],
-                   {"AMDGPU_VALIDATOR_COUNTERS": "1"})
+    # default gate: AQL profiling packets on the validator's own queue
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,vecadd,gemm,mfma,hbm,xgmi", "--counter-gate"])
     assert rc == 0 and rep["ok"], rep
     steps = {s["name"]: s for s in rep["steps"]}
     assert steps["mfma"]["dtypes"] == {d: True for d in ("f16", "bf16", "fp8", "bf8", "i8", "mxfp8", "mxfp6", "mxfp4",
@@ -34,6 +34,9 @@ def test_validator_all_local_steps_with_counter_gate(tmp_path):
     g = steps["gemm"]
     assert g["freivalds_rel_err"] < 1e-4 and g["counter_gate"] == "pass"
     assert g["flop_per_mop"] == 512  # one MFMA "MOP" = 512 FLOP on gfx950 (16x16x32 bf16 = 32 MOPs)
+    assert g["gate_mode"] == "aql" and g["gated_output_matches"]
+    assert g["SQ_WAVES"] == (4096 // 256) ** 2 * 8  # 256x256 tiles, 8 waves each
+    assert g["samples"] == [32, 32, 32, 8]  # per-SE/XCC instances of the SQ counters, 8 GRBM
     assert g["tflops"] > 300
     assert steps["hbm"]["checksum_match"] and steps["hbm"]["gbps"] > 2000
     assert steps["xgmi"]["emulated"] and steps["xgmi"]["max_abs_err"] <= 8e-5
@@ -43,8 +46,8 @@ def test_validator_counter_gate_tool_library_from_env(tmp_path):
     # the operator's path: the tool library is named explicitly (validate.py)
     from amdgpu_operator.validator.validate import gate_env
 
-    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--gemm", "1024", "--counter-gate"],
-                   gate_env())
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--gemm", "1024", "--counter-gate",
+                    "--gate-mode", "sdk"], gate_env())
     assert rc == 0 and rep["ok"], rep
     g = {s["name"]: s for s in rep["steps"]}["gemm"]
     assert g["counter_gate"] == "pass" and g["dispatches"] == 1 and g["flop_per_mop"] == 512
@@ -54,7 +57,8 @@ def test_validator_counter_gate_sdk_definitions(tmp_path):
     # the tool named by the caller with the SDK's own full counter set: the
     # gate must work with either definition file, as long as it is one set
     env = {**gate_env_full(), "AMDGPU_GATE_KERNEL_NAMES": "1"}
-    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--gemm", "1024", "--counter-gate"], env)
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--gemm", "1024", "--counter-gate",
+                    "--gate-mode", "sdk"], env)
     assert rc == 0 and rep["ok"], rep
     assert {s["name"]: s for s in rep["steps"]}["gemm"]["counter_gate"] == "pass"
 
@@ -68,10 +72,32 @@ def gate_env_full():
 
 
 def test_validator_counter_gate_unavailable_fails_closed(tmp_path):
-    # gate requested but the tool was not activated: must not silently pass
-    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--counter-gate"])
+    # sdk gate requested but the tool was not activated: must not silently pass
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--counter-gate", "--gate-mode", "sdk"])
     assert rc == 1 and not rep["ok"]
     assert {s["name"]: s for s in rep["steps"]}["gemm"]["counter_gate"] == "unavailable"
+
+
+def test_validator_aql_gate_fails_closed_without_its_code_object(tmp_path):
+    # the AQL gate dispatches the GEMM from validator_kernels.co next to the
+    # binary: a copy of the binary without it cannot pass the gate
+    import shutil
+
+    exe = tmp_path / "amdgpu-validator"
+    shutil.copy2(VALIDATOR, exe)
+    p = subprocess.run([str(exe), "--rendezvous", str(tmp_path / "rv"), "--steps", "hip,gemm", "--gemm", "1024",
+                        "--counter-gate"], capture_output=True, text=True, timeout=120)
+    rep = json.loads(p.stdout.strip().splitlines()[-1])
+    g = {s["name"]: s for s in rep["steps"]}["gemm"]
+    assert p.returncode == 1 and g["counter_gate"] == "unavailable" and "validator_kernels.co" in g["gate_error"]
+
+
+def test_validator_aql_gate_small_and_rectangular_work(tmp_path):
+    # 1024^3: 16 workgroups; the gate must still count every wave and MOP
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--gemm", "1024", "--counter-gate"])
+    assert rc == 0 and rep["ok"], rep
+    g = {s["name"]: s for s in rep["steps"]}["gemm"]
+    assert g["SQ_WAVES"] == 16 * 8 and g["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 == 2 * 1024 ** 3
 
 
 def test_validator_ipc_peer_path_two_processes_one_gpu(tmp_path):

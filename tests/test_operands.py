@@ -199,10 +199,19 @@ def test_workload_validation_launch_plan(env):
     rccl = [a for a, _, _ in launched if a[a.index("--steps") + 1] == "hip,rccl"]
     assert len(kernel) == 2 and len(rccl) == 2
     assert all("--counter-gate" in a for a in kernel) and not any("--counter-gate" in a for a in rccl)
-    assert {e.get("AMDGPU_VALIDATOR_COUNTERS") for a, e, _ in launched if a in kernel} == {"1"}
+    # the default AQL-packet gate needs no profiler tool in the process
+    assert {e.get("AMDGPU_VALIDATOR_COUNTERS") for a, e, _ in launched if a in kernel} == {None}
     names = [s["name"] for s in out["ranks"][0]["steps"]]
     assert names == ["hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl"]
     assert V.read_ready(env, "workload")["world"] == 2
+    launched.clear()
+    for f in os.listdir(env.validations_dir):
+        if f.endswith("-ready"):
+            os.unlink(os.path.join(env.validations_dir, f))
+    V.validate_workload(env, ["--gemm", "1024", "--counter-gate", "--gate-mode", "sdk"])
+    kernel = [(a, e) for a, e, _ in launched if "rccl" not in a[a.index("--steps") + 1]]
+    assert kernel and all(e.get("AMDGPU_VALIDATOR_COUNTERS") == "1" and "libamdgpu_counter_gate.so" in
+                          e.get("ROCP_TOOL_LIBRARIES", "") for _, e in kernel)
 
 
 def test_workload_failure_is_reported(env):
@@ -377,19 +386,20 @@ def test_no_prespawn_while_the_driver_is_not_live_or_upgrading(env):
     during a driver upgrade - then they are spawned after the validation."""
     from amdgpu_operator.controller.upgrade import POD_RESTART, STATE_LABEL
 
-    assert V.prespawn_safe(env)
+    assert V.prespawn_safe(env, sdk_gate=True)
     env.client.patch("v1", "Node", "n1", {"metadata": {"labels": {STATE_LABEL: POD_RESTART}}})
-    assert not V.prespawn_safe(env)
+    assert not V.prespawn_safe(env, sdk_gate=True)
+    assert V.prespawn_safe(env)  # the AQL gate opens nothing before the start gate
     log = []
     env.launcher = _gated_launcher(env, log)
     V.write_ready(env, "driver", {"ok": True})
     with pytest.raises(V.StepFailed, match="plugin"):
-        V.validate_gpu(env, [], timeout=0.5, with_driver=True)
+        V.validate_gpu(env, ["--counter-gate", "--gate-mode", "sdk"], timeout=0.5, with_driver=True)
     spawns = [x for x in log if x[0] == "spawn"]
     assert spawns and all(ready for _, ready in spawns)  # after the driver validation
     env.client.patch("v1", "Node", "n1", {"metadata": {"labels": {STATE_LABEL: None}}})
     os.unlink(os.path.join(env.sysfs_root(), "dev/kfd"))
-    assert not V.prespawn_safe(env)
+    assert not V.prespawn_safe(env, sdk_gate=True) and V.prespawn_safe(env)
 
 
 def test_driver_change_aborts_waiting_start_gates(env):
