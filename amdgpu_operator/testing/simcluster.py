@@ -581,6 +581,7 @@ class SimCluster:
             if not node.kubelet.wait_registered(res, timeout=30):
                 raise RuntimeError(f"resource {res} not registered on {node.spec.name}")
             ids, resp = node.kubelet.allocate(res, n, run.ns, run.name, c["name"])
+            self.trace("gpu-pod-allocated", run.name)
             envs = dict(resp.envs)
             devices = [int(x) for x in envs.get("AMD_VISIBLE_DEVICES", "").split(",") if x != ""]
             try:
@@ -603,12 +604,14 @@ class SimCluster:
             paths = {d["path"] for d in spec.get("linux", {}).get("devices", [])}
             if "/dev/kfd" not in paths:
                 raise RuntimeError("OCI hook did not inject /dev/kfd")
+        self.trace("gpu-pod-hooked", run.name)
         argv = [str(native.binary("amdgpu-validator"))] + cmd[1:]
         proc_env = {REPORT_EARLY_ENV: "1"} if REPORT_EARLY else {}
         dev = devices[0] if devices else None
         if devices:
-            proc_env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
+            proc_env.update(container_device_env(node.env.sysfs_root(), devices))
         res = node.env.launch(argv, proc_env, device=dev, timeout=600)
+        self.trace("gpu-pod-reported", run.name)
         if res.rc != 0:
             raise RuntimeError(f"workload failed rc={res.rc}: {res.stderr.strip()[-500:]} {res.stdout.strip()[-500:]}")
 
@@ -662,6 +665,24 @@ class SimCluster:
 
     def pods(self, namespace: str | None = None) -> list[dict]:
         return self.client.list("v1", "Pod", namespace or self.namespace)
+
+
+def container_device_env(sysfs_root: str, devices: list[int]) -> dict:
+    """What a GPU container's runtime sees: only its allocated devices.
+
+    The hook / CDI give the container just the allocated render nodes, so its
+    HSA runtime enumerates only those GPUs.  A process on the host gets the
+    same view from ``ROCR_VISIBLE_DEVICES`` with the GPUs' KFD unique ids
+    (ROCr's "GPU-<id>" UUIDs), which also keeps the runtime from initialising
+    every other GPU of an 8-GPU node; devices without a unique id fall back
+    to HIP-level ordinals."""
+    from ..discovery import topology
+
+    gpus = {g.index: g for g in topology.enumerate_gpus(sysfs_root)}
+    sel = [gpus.get(d) for d in devices]
+    if all(g is not None and g.unique_id for g in sel):
+        return {"ROCR_VISIBLE_DEVICES": ",".join(f"GPU-{g.unique_id:016x}" for g in sel)}
+    return {"HIP_VISIBLE_DEVICES": ",".join(str(d) for d in devices)}
 
 
 def new_id() -> str:

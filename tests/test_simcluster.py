@@ -158,3 +158,17 @@ def test_partition_profile_validation():
         Profile("SPX", "NPS2").validate()
     with pytest.raises(ValueError):
         Profile("XPX", "NPS1").validate()
+
+
+def test_gpu_pod_sees_only_its_allocated_devices(tmp_path):
+    """A GPU pod's process gets the container's view: ROCr limited to the
+    allocated GPUs by their KFD unique ids (rocminfo's "GPU-<hex>" UUIDs)."""
+    from amdgpu_operator.testing import fakesys
+    from amdgpu_operator.testing.simcluster import container_device_env
+
+    root = fakesys.build_from_real_fixture(str(tmp_path / "real"))
+    assert container_device_env(root, [0]) == {"ROCR_VISIBLE_DEVICES": "GPU-9048305841f546bf"}  # rocminfo.txt
+    synth = str(tmp_path / "synth")
+    fakesys.build_node(synth, 4)
+    env = container_device_env(synth, [1, 3])
+    assert list(env) == ["ROCR_VISIBLE_DEVICES"] and env["ROCR_VISIBLE_DEVICES"].count("GPU-") == 2
