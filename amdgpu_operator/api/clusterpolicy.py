@@ -320,7 +320,7 @@ def spec_from_values(values: dict) -> ClusterPolicySpec:
                        "operatorImage", "nodeSelector", "podSecurityContext"):
         v.pop(chart_only, None)
     op = dict(v.get("operator") or {})
-    for chart_only in ("image", "repository", "version", "imagePullPolicy", "resources", "replicas"):
+    for chart_only in ("image", "repository", "version", "imagePullPolicy", "resources", "replicas", "leaderElection"):
         op.pop(chart_only, None)
     if op or "operator" in v:
         v["operator"] = op

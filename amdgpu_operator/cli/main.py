@@ -99,6 +99,10 @@ def main(argv: list[str] | None = None) -> int:
     _common(op)
     op.add_argument("--health-port", type=int, default=8081)
     op.add_argument("--resync", type=float, default=30.0)
+    op.add_argument("--leader-elect", action="store_true",
+                    help="run the controller only while holding the Lease (replicas > 1: warm standbys)")
+    op.add_argument("--leader-election-id", default="amd-gpu-operator-leader")
+    op.add_argument("--lease-seconds", type=float, default=15.0)
     cl = sub.add_parser("cleanup-crd", help="delete ClusterPolicies and the CRD")
     _common(cl)
     ac = sub.add_parser("apply-crd", help="create/update the ClusterPolicy CRD")
@@ -144,10 +148,24 @@ def main(argv: list[str] | None = None) -> int:
     if args.cmd == "operator":
         from ..controller.reconciler import ClusterPolicyReconciler
 
-        rec = ClusterPolicyReconciler(_client(args), args.namespace)
+        client = _client(args)
+        rec = ClusterPolicyReconciler(client, args.namespace)
         _health_server(args.health_port, rec.metrics)
-        rec.run(threading.Event(), resync_s=args.resync)
-        return 0
+        if not args.leader_elect:
+            rec.run(threading.Event(), resync_s=args.resync)
+            return 0
+        import os
+        import socket
+
+        from ..kube.leader import LeaderElector
+
+        identity = os.environ.get("POD_NAME") or f"{socket.gethostname()}_{os.getpid()}"
+        elector = LeaderElector(client, args.leader_election_id, args.namespace, identity,
+                                lease_s=args.lease_seconds, renew_deadline_s=args.lease_seconds * 2 / 3,
+                                retry_period_s=args.lease_seconds / 7.5)
+        lost = elector.run(threading.Event(), lambda ended: rec.run(ended, resync_s=args.resync))
+        # leadership lost: exit so the Deployment restarts this replica as a standby
+        return 1 if lost else 0
     if args.cmd == "cleanup-crd":
         from ..controller.reconciler import cleanup_crd
 

@@ -87,6 +87,34 @@ def build_parser() -> argparse.ArgumentParser:
     return p
 
 
+def _validate(env, a, extra, stop, ready) -> int:
+    """``validate <step>``: the operator-validator's init and main containers."""
+    from ..validator import validate as V
+
+    if a.step == "driver":
+        V.wait_ready(env, "driver", a.timeout, stop)
+        V.validate_driver(env, a.timeout, stop)
+    elif a.step == "toolkit":
+        V.wait_ready(env, "toolkit", a.timeout, stop)
+    elif a.step == "workload":
+        if V.read_ready(env, "workload") is None:
+            V.validate_workload(env, extra, a.timeout)
+    elif a.step == "plugin":
+        if V.read_ready(env, "plugin") is None:
+            pod_args = _plugin_pod_args(extra)
+            V.validate_plugin(env, a.resource, pod_args=pod_args, timeout=a.timeout, stop=stop)
+    elif a.step == "gpu":
+        V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
+                       wait_toolkit=a.wait_toolkit, with_driver=a.with_driver)
+    else:
+        res = V.complete(env)
+        steps = ", ".join(f"{k} {v:.2f} s" for k, v in res["steps"].items() if v is not None)
+        _node_event(env, "Normal", "GPUValidated", f"GPUs validated ({steps})" if steps else "GPUs validated")
+        ready()
+        stop.wait()
+    return 0
+
+
 def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
     """``validate workload|plugin`` forward unknown args to amdgpu-validator."""
     known, extra = [], []
@@ -161,26 +189,12 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
     if cmd == "validate":
         from ..validator import validate as V
 
-        if a.step == "driver":
-            V.wait_ready(env, "driver", a.timeout, stop)
-            V.validate_driver(env, a.timeout, stop)
-        elif a.step == "toolkit":
-            V.wait_ready(env, "toolkit", a.timeout, stop)
-        elif a.step == "workload":
-            if V.read_ready(env, "workload") is None:
-                V.validate_workload(env, extra, a.timeout)
-        elif a.step == "plugin":
-            if V.read_ready(env, "plugin") is None:
-                pod_args = _plugin_pod_args(extra)
-                V.validate_plugin(env, a.resource, pod_args=pod_args, timeout=a.timeout, stop=stop)
-        elif a.step == "gpu":
-            V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
-                           wait_toolkit=a.wait_toolkit, with_driver=a.with_driver)
-        else:
-            V.complete(env)
-            ready()
-            stop.wait()
-        return 0
+        try:
+            return _validate(env, a, extra, stop, ready)
+        except V.StepFailed as e:
+            if not stop.is_set():  # a pod being deleted is not a failed validation
+                _node_event(env, "Warning", "ValidationFailed", f"{a.step} validation failed: {e}")
+            raise
 
     if cmd == "device-plugin":
         from ..deviceplugin.server import DevicePluginManager, PluginConfig
@@ -367,6 +381,19 @@ def _get_or_empty(client, kind: str, name: str, namespace: str | None = None) ->
         if e.code == 404:
             return {}
         raise
+
+
+def _node_event(env: NodeEnv, etype: str, reason: str, message: str) -> None:
+    """An Event on this operand's Node (best effort)."""
+    from ..kube.events import EventRecorder
+
+    if env.client is None:
+        return
+    try:
+        node = env.client.get("v1", "Node", env.node_name)
+    except Exception:  # noqa: BLE001
+        return
+    EventRecorder(env.client, "amd-operator-validator", host=env.node_name).record(node, etype, reason, message)
 
 
 def _plugin_pod_args(extra: list[str]) -> list[str]:

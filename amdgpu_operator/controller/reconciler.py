@@ -36,6 +36,7 @@ from .. import API_GROUP, API_VERSION
 from ..api.clusterpolicy import STATES, ClusterPolicySpec
 from ..kube import resources as R
 from ..kube.client import NotFound, apply_object
+from ..kube.events import NORMAL, WARNING, EventRecorder
 from ..utils.logs import get_logger
 from .manifests import STATE_BUILDERS, owner_ref
 from .nodes import label_nodes
@@ -149,6 +150,8 @@ class ClusterPolicyReconciler:
         self._ttr: dict[str, float] = {}
         self.reconciles = 0
         self.metrics = ReconcileMetrics()
+        self.events = EventRecorder(client, "amd-gpu-operator")
+        self._last_state: dict[str, str] = {}  # policy uid -> state last reported by an Event
 
     # ------------------------------------------------------------------ helpers
     def _active_policy(self) -> dict | None:
@@ -192,6 +195,7 @@ class ClusterPolicyReconciler:
         except ValidationError as e:
             msg = str(e).splitlines()[0] if str(e) else "invalid spec"
             self._write_status(cp, "error", [], 0, error=msg)
+            self._state_event(cp, "error", msg)
             res = ReconcileResult(cp["metadata"]["name"], "error", seconds=time.perf_counter() - t0)
             self.metrics.observe(res, {}, None)
             return res
@@ -244,7 +248,7 @@ class ClusterPolicyReconciler:
             from .upgrade import DriverUpgradeController
 
             try:
-                upgrade = DriverUpgradeController(self.client, self.namespace, self.clock).step(spec)
+                upgrade = DriverUpgradeController(self.client, self.namespace, self.clock, self.events).step(spec)
             except Exception as e:  # noqa: BLE001 - next pass retries
                 log.warning("driver upgrade pass failed: %s", e)
         overall = "ready" if all(r.ready for r in results) else "notReady"
@@ -262,10 +266,28 @@ class ClusterPolicyReconciler:
         self.metrics.observe_upgrade(upgrade)
         if overall == "ready":
             self._ttr.setdefault(uid, self.clock() - self._created_at[uid])
+        waiting = [r.name for r in results if r.enabled and not r.ready]
+        self._state_event(cp, overall, f"waiting for {', '.join(waiting)}" if waiting else
+                          "waiting for GPU node validation" if overall != "ready" else
+                          f"all operands ready on {gpu_nodes} GPU node(s) (time-to-Ready {self._ttr.get(uid, 0):.2f} s)")
         res = ReconcileResult(cp["metadata"]["name"], overall, results, gpu_nodes, time.perf_counter() - t0)
         self.metrics.observe(res, self._ready_at.get(uid, {}), self._ttr.get(uid))
         log.debug("reconciled %s: %s (%.3fs)", res.policy, overall, res.seconds)
         return res
+
+    def _state_event(self, cp: dict, state: str, message: str) -> None:
+        """One Event per ClusterPolicy state change (``kubectl describe clusterpolicy``)."""
+        uid = cp["metadata"].get("uid", cp["metadata"]["name"])
+        prev = self._last_state.get(uid)
+        if prev == state or (prev is None and state == "notReady"):
+            return  # the first notReady of a fresh install is not news
+        self._last_state[uid] = state
+        if state == "ready":
+            self.events.record(cp, NORMAL, "Ready", message)
+        elif state == "error":
+            self.events.record(cp, WARNING, "ReconcileFailed", message)
+        else:
+            self.events.record(cp, WARNING, "NotReady", message)
 
     def _driver_pools(self, spec, owner) -> tuple[list[dict], dict]:
         from .manifests import state_driver_pools

@@ -80,10 +80,11 @@ def _uses_gpu(pod: dict) -> bool:
 
 
 class DriverUpgradeController:
-    def __init__(self, client, namespace: str, clock=time.time):
+    def __init__(self, client, namespace: str, clock=time.time, events=None):
         self.client = client
         self.namespace = namespace
         self.clock = clock
+        self.events = events  # kube.events.EventRecorder: one Event per node transition
 
     def _set(self, node: dict, state: str, extra_ann: dict | None = None, unschedulable: bool | None = None) -> None:
         name = node["metadata"]["name"]
@@ -102,6 +103,14 @@ class DriverUpgradeController:
         if unschedulable is not None:
             node.setdefault("spec", {})["unschedulable"] = unschedulable
         log.info("driver upgrade %s -> %s", name, state)
+        if self.events is not None:
+            from ..kube.events import NORMAL, WARNING
+
+            if state == FAILED:
+                self.events.record(node, WARNING, "DriverUpgradeFailed",
+                                   "driver upgrade did not complete in time; the node stays cordoned until a retry succeeds")
+            else:
+                self.events.record(node, NORMAL, "DriverUpgrade", f"driver upgrade: {state}")
 
     def _gpu_pods(self, node_name: str) -> list[dict]:
         return [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={node_name}") if _uses_gpu(p)]

@@ -48,6 +48,7 @@ _TYPES = [
     ResourceType("apps", "v1", "DaemonSet", "daemonsets", True),
     ResourceType("apps", "v1", "Deployment", "deployments", True),
     ResourceType("batch", "v1", "Job", "jobs", True),
+    ResourceType("coordination.k8s.io", "v1", "Lease", "leases", True),
     ResourceType("rbac.authorization.k8s.io", "v1", "ClusterRole", "clusterroles", False),
     ResourceType("rbac.authorization.k8s.io", "v1", "ClusterRoleBinding", "clusterrolebindings", False),
     ResourceType("rbac.authorization.k8s.io", "v1", "Role", "roles", True),
