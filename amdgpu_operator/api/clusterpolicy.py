@@ -94,6 +94,8 @@ class ToolkitSpec(Operand):
     runtime: Literal["containerd", "docker", "crio"] = "containerd"
     containerdConfig: str = "/etc/containerd/config.toml"
     containerdSocket: str = "/run/containerd/containerd.sock"
+    crioConfigDir: str = "/etc/crio/crio.conf.d"  # runtime: crio
+    dockerConfig: str = "/etc/docker/daemon.json"  # runtime: docker
     runtimeClass: str = "amd"
     cdi: CDISpec = Field(default_factory=CDISpec)
     mountRocm: bool = False

@@ -176,7 +176,8 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                       mount_rocm=a.mount_rocm or cenv.get("MOUNT_ROCM") == "true",
                       args=tk.hook_args(cenv.get("ACCEPT_DEVICE_LIST_AS_VOLUME_MOUNTS") == "true",
                                         cenv.get("ACCEPT_ENVVAR_UNPRIVILEGED", "true") == "true"),
-                      set_as_default=cenv.get("CONTAINERD_SET_AS_DEFAULT") == "true")
+                      set_as_default=cenv.get("CONTAINERD_SET_AS_DEFAULT") == "true",
+                      runtime=cenv.get("RUNTIME", "containerd"), pid_file=cenv.get("RUNTIME_PID_FILE") or None)
             tk.install(env, **kw)
             ready()
             # a driver reload / loss clears toolkit-ready: redo the install (the

@@ -21,6 +21,8 @@ wait for validation files in the host's ``/run/amd/validations`` directory
 
 from __future__ import annotations
 
+import os
+
 from ..api.clusterpolicy import ClusterPolicySpec
 
 DEPLOY_LABEL = "amd.com/gpu.deploy.{}"
@@ -239,16 +241,28 @@ def state_toolkit(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
            {"name": "ACCEPT_ENVVAR_UNPRIVILEGED", "value": str(t.acceptEnvvarUnprivileged).lower()},
            {"name": "CONTAINERD_SET_AS_DEFAULT", "value": str(t.setAsDefault).lower()},
            ] + list(t.env)
-    mounts = [_mount("containerd-config", "/runtime/config-dir"), _mount("containerd-socket", "/runtime/sock-dir"),
-              _mount("install-dir", t.installDir), _mount("cdi-dir", t.cdi.specDir),
-              _mount("host-sys", "/host/sys", ro=True), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    # the runtime's host directories are mounted at their host paths, so the
+    # paths the installer writes into the runtime's configuration (imports,
+    # hooks dirs, CDI dirs) are the paths the runtime itself reads
+    if t.runtime == "containerd":
+        runtime_dirs = [os.path.dirname(t.containerdConfig), os.path.dirname(t.containerdSocket)]
+        env.append({"name": "RUNTIME_PID_FILE", "value": os.path.join(os.path.dirname(t.containerdSocket),
+                                                                        "containerd.pid")})
+    elif t.runtime == "crio":
+        runtime_dirs = [t.crioConfigDir]
+    else:
+        runtime_dirs = [os.path.dirname(t.dockerConfig)]
+    env += [{"name": "CRIO_CONFIG_DIR", "value": t.crioConfigDir}, {"name": "DOCKER_CONFIG", "value": t.dockerConfig}]
+    runtime_mounts = [(f"runtime-dir-{i}", d) for i, d in enumerate(dict.fromkeys(runtime_dirs))]
+    mounts = [_mount(n, d) for n, d in runtime_mounts] + [
+        _mount("install-dir", t.installDir), _mount("cdi-dir", t.cdi.specDir),
+        _mount("host-sys", "/host/sys", ro=True), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)]
     ctr = _container("amd-container-toolkit-ctr", image, t.imagePullPolicy, ["toolkit", "install", *t.args], mounts, env,
                      True, t.resources.model_dump())
     init = _wait_init("driver-validation", image, t.imagePullPolicy, "driver")
-    vols = [_hostpath("containerd-config", t.containerdConfig.rsplit("/", 1)[0]),
-            _hostpath("containerd-socket", t.containerdSocket.rsplit("/", 1)[0]),
-            _hostpath("install-dir", t.installDir), _hostpath("cdi-dir", t.cdi.specDir),
-            _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    vols = [_hostpath(n, d, "DirectoryOrCreate") for n, d in runtime_mounts] + [
+        _hostpath("install-dir", t.installDir), _hostpath("cdi-dir", t.cdi.specDir),
+        _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
     return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "toolkit", sa, [ctr], [init], vols, host_pid=True)]
 
 

@@ -114,6 +114,8 @@ class NodeEnv:
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     cdi_dir: str = "/var/run/cdi"
     containerd_config: str = "/etc/containerd/config.toml"
+    crio_config_dir: str = "/etc/crio/crio.conf.d"
+    docker_config: str = "/etc/docker/daemon.json"
     install_dir: str = "/usr/local/amd"
     namespace: str = DEFAULT_NAMESPACE
     poll_s: float = 1.0
@@ -134,6 +136,8 @@ class NodeEnv:
             pod_resources_socket=e.get("POD_RESOURCES_SOCKET", "/var/lib/kubelet/pod-resources/kubelet.sock"),
             cdi_dir=e.get("CDI_SPEC_DIR", "/var/run/cdi"),
             containerd_config=e.get("CONTAINERD_CONFIG", "/etc/containerd/config.toml"),
+            crio_config_dir=e.get("CRIO_CONFIG_DIR", "/etc/crio/crio.conf.d"),
+            docker_config=e.get("DOCKER_CONFIG", "/etc/docker/daemon.json"),
             install_dir=e.get("INSTALL_DIR", "/usr/local/amd"),
             namespace=e.get("OPERATOR_NAMESPACE", DEFAULT_NAMESPACE),
             poll_s=float(e.get("VALIDATION_POLL_S", "1.0")),

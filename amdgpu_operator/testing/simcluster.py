@@ -264,6 +264,8 @@ class SimCluster:
                       validations_dir=os.path.join(d, "validations"), device_plugin_dir=dp_dir,
                       pod_resources_socket=podres, cdi_dir=os.path.join(d, "cdi"),
                       containerd_config=os.path.join(d, "etc/containerd/config.toml"),
+                      crio_config_dir=os.path.join(d, "etc/crio/crio.conf.d"),
+                      docker_config=os.path.join(d, "etc/docker/daemon.json"),
                       install_dir=os.path.join(d, "usr/local/amd"), namespace=self.namespace, poll_s=self.poll_s,
                       launcher=self._launch)
         if ns.sysfs_root is None and ns.gpus > 0:  # driver installs / unloads act on the fake tree

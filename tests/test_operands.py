@@ -54,6 +54,65 @@ def test_toolkit_install_idempotent(env):
     assert open(env.containerd_config + ".amd-backup").read() == "version = 2\n"
 
 
+@pytest.fixture
+def rt_env(env, tmp_path):
+    env.crio_config_dir = str(tmp_path / "etc/crio/crio.conf.d")
+    env.docker_config = str(tmp_path / "etc/docker/daemon.json")
+    return env
+
+
+def test_toolkit_crio_dropin(rt_env):
+    out = TK.install(rt_env, runtime="crio")
+    assert out["runtime"] == "crio" and out["config_changed"] and out["restart_required"]
+    text = open(os.path.join(rt_env.crio_config_dir, TK.CRIO_DROPIN)).read()
+    hooks_d = os.path.join(rt_env.install_dir, TK.HOOKS_D)
+    assert f'"{hooks_d}"' in text and '"/usr/share/containers/oci/hooks.d"' in text  # CRI-O's own dirs kept
+    assert f'cdi_spec_dirs = ["{rt_env.cdi_dir}", "/etc/cdi"]' in text
+    hook = json.load(open(os.path.join(hooks_d, TK.HOOK_JSON)))
+    assert hook["stages"] == ["precreate"]
+    assert TK.install(rt_env, runtime="crio")["config_changed"] is False
+    TK.uninstall(rt_env)
+    assert not os.path.exists(os.path.join(rt_env.crio_config_dir, TK.CRIO_DROPIN))
+
+
+def test_toolkit_docker_daemon_json(rt_env):
+    os.makedirs(os.path.dirname(rt_env.docker_config))
+    user = {"log-driver": "json-file", "features": {"buildkit": True}, "cdi-spec-dirs": ["/opt/cdi"]}
+    with open(rt_env.docker_config, "w") as f:
+        json.dump(user, f)
+    out = TK.install(rt_env, runtime="docker")
+    assert out["config_changed"] and out["restart_required"]
+    cfg = json.load(open(rt_env.docker_config))
+    assert cfg["features"] == {"buildkit": True, "cdi": True} and cfg["log-driver"] == "json-file"
+    assert cfg["cdi-spec-dirs"] == [rt_env.cdi_dir, "/etc/cdi", "/opt/cdi"]
+    assert TK.install(rt_env, runtime="docker")["config_changed"] is False
+    TK.uninstall(rt_env)
+    assert json.load(open(rt_env.docker_config)) == user  # the user's values back
+    with pytest.raises(ValueError):
+        TK.install(rt_env, runtime="podman")
+
+
+def test_toolkit_daemonset_mounts_runtime_dirs_at_host_paths():
+    """The installer writes host paths into the runtime config (imports,
+    hooks dirs), so the runtime's directories are mounted at those paths."""
+    from amdgpu_operator.api.clusterpolicy import ClusterPolicySpec
+    from amdgpu_operator.controller import manifests as M
+
+    for runtime, must in (("containerd", ["/etc/containerd", "/run/containerd"]), ("crio", ["/etc/crio/crio.conf.d"]),
+                          ("docker", ["/etc/docker"])):
+        spec = ClusterPolicySpec.model_validate({"toolkit": {"runtime": runtime}})
+        ds = [o for o in M.state_toolkit(spec, "ns", None) if o["kind"] == "DaemonSet"][0]
+        pod = ds["spec"]["template"]["spec"]
+        ctr = pod["containers"][0]
+        paths = {m["mountPath"] for m in ctr["volumeMounts"]}
+        host = {v["hostPath"]["path"] for v in pod["volumes"]}
+        assert all(p in paths and p in host for p in must), (runtime, paths)
+        env = {e["name"]: e.get("value") for e in ctr["env"]}
+        assert env["RUNTIME"] == runtime
+        if runtime == "containerd":
+            assert env["RUNTIME_PID_FILE"] == "/run/containerd/containerd.pid"
+
+
 def test_containerd_patch_preserves_user_imports():
     t = 'imports = ["/etc/containerd/a.toml"]\nversion = 2\n[x]\n  y = 1\n'
     p = TK.patch_containerd_config(t, "/d.toml")
