@@ -94,8 +94,14 @@ def _wait_init(name: str, image: str, pull: str, what: str, extra_args=()) -> di
     """Init container that blocks until a validation file exists on the host."""
     return _container(name, image, pull, ["validate", what, *extra_args],
                       mounts=[_mount("run-amd-validations", VALIDATIONS_HOST_DIR, propagation="HostToContainer"),
-                              _mount("host-sys", "/host/sys", ro=True)],
+                              *_host_view()],
                       privileged=True)
+
+
+def _host_view() -> list[dict]:
+    """/host/sys + /host/dev: what the N1 probe and the topology reader need
+    (NodeEnv.host_root = /host inside operand containers)."""
+    return [_mount("host-sys", "/host/sys", ro=True), _mount("host-dev", "/host/dev", ro=True)]
 
 
 def _daemonset(spec: ClusterPolicySpec, ns: str, owner, name: str, operand_key: str | None, sa: str,
@@ -106,6 +112,15 @@ def _daemonset(spec: ClusterPolicySpec, ns: str, owner, name: str, operand_key: 
               "app.kubernetes.io/managed-by": "amd-gpu-operator"}
     if node_selector is None:
         node_selector = {DEPLOY_LABEL.format(OPERAND_LABELS[operand_key]): "true"} if operand_key else {}
+    volumes = list(volumes)
+    # the host's /sys and /dev as the N1 probe reads them (NodeEnv host_root
+    # "/host"): any container mounting them gets the volume without each
+    # state builder repeating it
+    have = {v["name"] for v in volumes}
+    mounted = {m["name"] for c in [*containers, *init_containers] for m in c.get("volumeMounts", [])}
+    for vol_name, host_path in (("host-sys", "/sys"), ("host-dev", "/dev")):
+        if vol_name in mounted and vol_name not in have:
+            volumes.append(_hostpath(vol_name, host_path, "Directory"))
     tmpl_spec = {
         "serviceAccountName": sa,
         "priorityClassName": ds.priorityClassName,
@@ -115,7 +130,7 @@ def _daemonset(spec: ClusterPolicySpec, ns: str, owner, name: str, operand_key: 
         "hostNetwork": host_network,
         "initContainers": list(init_containers),
         "containers": list(containers),
-        "volumes": list(volumes),
+        "volumes": volumes,
     }
     strategy = {"type": ds.updateStrategy}
     if ds.updateStrategy == "RollingUpdate":
@@ -204,13 +219,11 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-drive
     ctr = _container("amd-driver-ctr", image, d.imagePullPolicy, ["driver", "install", *d.args], mounts, env, True,
                      d.resources.model_dump(), readiness)
     health = _container("amd-driver-health", image, d.imagePullPolicy, ["driver", "monitor"],
-                        [_mount("host-sys", "/host/sys", ro=True), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)],
-                        privileged=True)
+                        [*_host_view(), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)], privileged=True)
     # the init container compares the live module with this spec and unloads it
     # on a mismatch, so it gets the same driver env as amd-driver-ctr
     init = _container("amd-driver-manager", image, d.imagePullPolicy, ["driver", "prepare-upgrade"],
-                      [_mount("run-amd", "/run/amd"), _mount("lib-modules", "/lib/modules"),
-                       _mount("host-sys", "/host/sys", ro=True)],
+                      [_mount("run-amd", "/run/amd"), _mount("lib-modules", "/lib/modules"), *_host_view()],
                       env + [{"name": "DRAIN_ENABLED", "value": str(d.upgradePolicy.drainEnabled).lower()},
                              {"name": "DRAIN_TIMEOUT_SECONDS", "value": str(d.upgradePolicy.drainTimeoutSeconds)}],
                       True)
@@ -256,7 +269,7 @@ def state_toolkit(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     runtime_mounts = [(f"runtime-dir-{i}", d) for i, d in enumerate(dict.fromkeys(runtime_dirs))]
     mounts = [_mount(n, d) for n, d in runtime_mounts] + [
         _mount("install-dir", t.installDir), _mount("cdi-dir", t.cdi.specDir),
-        _mount("host-sys", "/host/sys", ro=True), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)]
+        *_host_view(), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)]
     ctr = _container("amd-container-toolkit-ctr", image, t.imagePullPolicy, ["toolkit", "install", *t.args], mounts, env,
                      True, t.resources.model_dump())
     init = _wait_init("driver-validation", image, t.imagePullPolicy, "driver")
@@ -326,7 +339,7 @@ def state_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         args += ["--config-map", f"{ns}/{p.config.name}", "--config-default", p.config.default]
         rbac = [_cluster_role(sa, PLUGIN_CONFIG_RULES, owner), _cluster_binding(sa, sa, ns, owner)]
     ctr = _container("amd-device-plugin", image, p.imagePullPolicy, args + list(p.args),
-                     [_mount("device-plugin", "/var/lib/kubelet/device-plugins"), _mount("host-sys", "/host/sys", ro=True)],
+                     [_mount("device-plugin", "/var/lib/kubelet/device-plugins"), *_host_view()],
                      list(p.env), True, p.resources.model_dump())
     inits = [_wait_init("toolkit-validation", image, p.imagePullPolicy, "toolkit" if spec.toolkit.enabled else "driver")]
     vols = [_hostpath("device-plugin", "/var/lib/kubelet/device-plugins"), _hostpath("host-sys", "/sys", "Directory"),
@@ -349,7 +362,7 @@ def state_metrics_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict
         rbac = [_cluster_role(sa, PLUGIN_CONFIG_RULES[1:], owner), _cluster_binding(sa, sa, ns, owner)]
     ctr = _container("amd-metrics-exporter", image, m.imagePullPolicy, args + list(m.args),
                      [_mount("pod-resources", "/var/lib/kubelet/pod-resources", ro=True),
-                      _mount("host-sys", "/host/sys", ro=True)], list(m.env), True, m.resources.model_dump(),
+                      *_host_view()], list(m.env), True, m.resources.model_dump(),
                      ports=[{"name": "metrics", "containerPort": m.port}])
     inits = [_wait_init("driver-validation", image, m.imagePullPolicy, "driver")]
     vols = [_hostpath("pod-resources", "/var/lib/kubelet/pod-resources"), _hostpath("host-sys", "/sys", "Directory"),

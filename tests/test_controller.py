@@ -241,3 +241,33 @@ def test_toolkit_set_as_default_runtime():
     txt = dropin_config("amd", "/usr/local/amd/amdgpu-oci-hook", "/var/run/cdi", set_as_default=True)
     assert 'default_runtime_name = "amd"' in txt
     assert "default_runtime_name" not in dropin_config("amd", "/h", "/var/run/cdi")
+
+
+def test_every_mount_has_a_volume_and_probing_containers_see_host_dev():
+    """Operands read the host through NodeEnv.host_root=/host: the N1 probe
+    needs /host/sys AND /host/dev (sys/module/amdgpu, /dev/kfd, render
+    nodes), so every container that probes the driver mounts both."""
+    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, ClusterPolicySpec, parse_set_flags
+    from amdgpu_operator.controller import manifests as M
+
+    spec = ClusterPolicySpec.model_validate(parse_set_flags(REFERENCE_SET_FLAGS))
+    probing = (["validate", "driver"], ["validate", "gpu"], ["driver", "install"], ["driver", "monitor"],
+               ["driver", "prepare-upgrade"])
+    seen = 0
+    for state, builder in M.STATE_BUILDERS.items():
+        for o in builder(spec, "ns", None):
+            if o["kind"] != "DaemonSet":
+                continue
+            pod = o["spec"]["template"]["spec"]
+            vols = {v["name"]: v for v in pod["volumes"]}
+            for c in pod.get("initContainers", []) + pod["containers"]:
+                mounts = {m["name"]: m["mountPath"] for m in c.get("volumeMounts", [])}
+                assert set(mounts) <= set(vols), (o["metadata"]["name"], c["name"], set(mounts) - set(vols))
+                args = c.get("args") or []
+                if any(args[:2] == p for p in probing):
+                    seen += 1
+                    paths = set(mounts.values())
+                    assert "/host/sys" in paths and ("/host/dev" in paths or "/host" in paths), (c["name"], paths)
+                    if "host-dev" in mounts:
+                        assert vols["host-dev"]["hostPath"]["path"] == "/dev"
+    assert seen >= 5
