@@ -190,6 +190,10 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
     if cmd == "validate":
         from ..validator import validate as V
 
+        if cenv.get("VALIDATOR_IMAGE"):
+            env.extra["validator_image"] = {
+                "image": cenv["VALIDATOR_IMAGE"], "pull_policy": cenv.get("VALIDATOR_IMAGE_PULL_POLICY"),
+                "pull_secrets": [x for x in cenv.get("VALIDATOR_IMAGE_PULL_SECRETS", "").split(",") if x]}
         try:
             return _validate(env, a, extra, stop, ready)
         except V.StepFailed as e:

@@ -90,12 +90,18 @@ def _container(name: str, image: str, pull: str, args: list[str], mounts=None, e
     return c
 
 
-def _wait_init(name: str, image: str, pull: str, what: str, extra_args=()) -> dict:
+def _wait_init(name: str, image: str, pull: str, what: str, extra_args=(), env=None) -> dict:
     """Init container that blocks until a validation file exists on the host."""
     return _container(name, image, pull, ["validate", what, *extra_args],
                       mounts=[_mount("run-amd-validations", VALIDATIONS_HOST_DIR, propagation="HostToContainer"),
                               *_host_view()],
-                      privileged=True)
+                      env=env, privileged=True)
+
+
+def _workload_pod_env(v, image: str) -> list[dict]:
+    """What the plugin-validation pods the validator creates run: its own image."""
+    return [{"name": "VALIDATOR_IMAGE", "value": image}, {"name": "VALIDATOR_IMAGE_PULL_POLICY", "value": v.imagePullPolicy},
+            {"name": "VALIDATOR_IMAGE_PULL_SECRETS", "value": ",".join(v.imagePullSecrets)}]
 
 
 def _host_view() -> list[dict]:
@@ -106,8 +112,10 @@ def _host_view() -> list[dict]:
 
 def _daemonset(spec: ClusterPolicySpec, ns: str, owner, name: str, operand_key: str | None, sa: str,
                containers: list, init_containers: list = (), volumes: list = (), host_pid: bool = False,
-               host_network: bool = False, node_selector: dict | None = None, extra_labels=None) -> dict:
+               host_network: bool = False, node_selector: dict | None = None, extra_labels=None,
+               operand=None) -> dict:
     ds = spec.daemonsets
+    operand = operand if operand is not None else (getattr(spec, operand_key) if operand_key else None)
     labels = {APP_LABEL: name, "app.kubernetes.io/part-of": "amd-gpu-operator",
               "app.kubernetes.io/managed-by": "amd-gpu-operator"}
     if node_selector is None:
@@ -132,6 +140,8 @@ def _daemonset(spec: ClusterPolicySpec, ns: str, owner, name: str, operand_key: 
         "containers": list(containers),
         "volumes": volumes,
     }
+    if operand is not None and operand.imagePullSecrets:  # private registries (<operand>.imagePullSecrets)
+        tmpl_spec["imagePullSecrets"] = [{"name": n} for n in operand.imagePullSecrets]
     strategy = {"type": ds.updateStrategy}
     if ds.updateStrategy == "RollingUpdate":
         strategy["rollingUpdate"] = {"maxUnavailable": ds.maxUnavailable}
@@ -302,15 +312,17 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         # workload processes behind their start gate (validate.py validate_gpu)
         extra = ["--resource", spec.devicePlugin.resourceName, "--with-driver"] + \
             (["--wait-toolkit"] if spec.toolkit.enabled else [])
-        inits = [_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args])]
-    elif v.pluginValidation and spec.devicePlugin.enabled:
+        inits = [_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args],
+                            env=_workload_pod_env(v, image))]
+    elif v.pluginValidation and spec.devicePlugin.enabled:  # (validation pods: _workload_pod_env)
         # workload (all GPUs, RCCL over xGMI) and plugin (1-GPU pods through the
         # device plugin + OCI hook) validation run concurrently.  The workload
         # needs only the driver (its processes run in this pod, not through the
         # runtime hook), so it overlaps the toolkit install; the plugin pods
         # wait for the toolkit inside the step.
         extra = ["--resource", spec.devicePlugin.resourceName] + (["--wait-toolkit"] if spec.toolkit.enabled else [])
-        inits.append(_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args]))
+        inits.append(_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args],
+                                env=_workload_pod_env(v, image)))
     else:
         if spec.toolkit.enabled:
             inits.append(_wait_init("toolkit-validation", image, v.imagePullPolicy, "toolkit"))
@@ -385,7 +397,7 @@ def state_nfd(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
                      [_mount("host-sys", "/host/sys", ro=True)], list(n.env), False, n.resources.model_dump())
     vols = [_hostpath("host-sys", "/sys", "Directory")]
     # runs on every node: it is what identifies the GPU nodes in the first place
-    ds = _daemonset(spec, ns, owner, name, None, sa, [ctr], [], vols, node_selector={})
+    ds = _daemonset(spec, ns, owner, name, None, sa, [ctr], [], vols, node_selector={}, operand=n)
     ds["spec"]["template"]["spec"]["tolerations"].append({"operator": "Exists"})
     return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner), ds]
 

@@ -283,8 +283,19 @@ def allocatable(node: dict, resource: str) -> int:
 
 
 def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | None = None,
-                    pod_args: list[str] | None = None, timeout: float = 600.0, stop=None) -> dict:
-    """Wait for Allocatable == GPUs, then run one 1-GPU pod per device."""
+                    pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
+                    image: str | None = None, pull_policy: str = "IfNotPresent",
+                    pull_secrets: list[str] | None = None) -> dict:
+    """Wait for Allocatable == GPUs, then run one 1-GPU pod per device.
+
+    The pods run the validator's own image (``VALIDATOR_IMAGE`` in the
+    validator container's env, with its pull policy and secrets, which
+    cli/operands.py puts in ``env.extra["validator_image"]``)."""
+    pod_image = env.extra.get("validator_image") or {}  # from the container env (cli/operands.py)
+    image = image or pod_image.get("image") or "amd-operator-validator"
+    pull_policy = pod_image.get("pull_policy") or pull_policy
+    if pull_secrets is None:
+        pull_secrets = list(pod_image.get("pull_secrets") or [])
     from ..discovery import topology
 
     t0 = time.perf_counter()
@@ -315,11 +326,13 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                 "nodeName": env.node_name,
                 "restartPolicy": "Never",
                 "tolerations": [{"key": resource, "operator": "Exists", "effect": "NoSchedule"}],
-                "containers": [{"name": "workload", "image": "amd-operator-validator",
+                "containers": [{"name": "workload", "image": image, "imagePullPolicy": pull_policy,
                                 "command": ["amdgpu-validator"], "args": pod_args,
                                 "resources": {"limits": {resource: "1"}, "requests": {resource: "1"}}}],
             },
         }
+        if pull_secrets:
+            pod["spec"]["imagePullSecrets"] = [{"name": x} for x in pull_secrets]
         env.client.create(pod)
         names.append(name)
     phases = {}

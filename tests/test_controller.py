@@ -271,3 +271,67 @@ def test_every_mount_has_a_volume_and_probing_containers_see_host_dev():
                     if "host-dev" in mounts:
                         assert vols["host-dev"]["hostPath"]["path"] == "/dev"
     assert seen >= 5
+
+
+def test_image_pull_secrets_and_validation_pod_image():
+    """<operand>.imagePullSecrets reach the pods; the plugin-validation pods the
+    validator creates run the validator's configured image, not a bare name."""
+    from amdgpu_operator.api.clusterpolicy import ClusterPolicySpec
+    from amdgpu_operator.controller import manifests as M
+
+    spec = ClusterPolicySpec.model_validate({
+        "validator": {"repository": "registry.example/amd", "version": "1.2.3", "imagePullSecrets": ["regcred"]},
+        "nfd": {"imagePullSecrets": ["nfdcred"]}})
+    ds = [o for o in M.state_validator(spec, "ns", None) if o["kind"] == "DaemonSet"][0]
+    pod = ds["spec"]["template"]["spec"]
+    assert pod["imagePullSecrets"] == [{"name": "regcred"}]
+    env = {e["name"]: e.get("value") for e in pod["initContainers"][0]["env"]}
+    assert env["VALIDATOR_IMAGE"] == "registry.example/amd/amd-operator-validator:1.2.3"
+    assert env["VALIDATOR_IMAGE_PULL_SECRETS"] == "regcred"
+    nfd = [o for o in M.state_nfd(spec, "ns", None) if o["kind"] == "DaemonSet"][0]
+    assert nfd["spec"]["template"]["spec"]["imagePullSecrets"] == [{"name": "nfdcred"}]
+    drv = [o for o in M.state_driver(spec, "ns", None) if o["kind"] == "DaemonSet"][0]
+    assert "imagePullSecrets" not in drv["spec"]["template"]["spec"]
+
+
+def test_plugin_validation_pods_use_the_validator_image(tmp_path):
+    import threading
+    import time
+
+    from amdgpu_operator.kube import resources as R
+    from amdgpu_operator.kube.client import LocalClient
+    from amdgpu_operator.kube.fakeapi import FakeApiServer
+    from amdgpu_operator.nodeenv import NodeEnv
+    from amdgpu_operator.testing import fakesys
+    from amdgpu_operator.validator import validate as V
+
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 1)
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Namespace", "gpu-operator-resources"))
+    node = R.new("v1", "Node", "n1")
+    node["status"] = {"allocatable": {"amd.com/gpu": "1"}}
+    c.create(node)
+    env = NodeEnv("n1", c, host_root=root, validations_dir=str(tmp_path / "val"), poll_s=0.01)
+    env.extra["validator_image"] = {"image": "reg/amd-operator-validator:9", "pull_policy": "Always",
+                                    "pull_secrets": ["s1"]}
+    seen = []
+
+    def kubelet():  # completes the pod like a kubelet would
+        deadline = time.time() + 5
+        while time.time() < deadline:
+            for p in c.list("v1", "Pod", "gpu-operator-resources"):
+                seen.append(p["spec"])
+                p["status"] = {"phase": "Succeeded"}
+                c.update_status(p)
+                return
+            time.sleep(0.01)
+
+    th = threading.Thread(target=kubelet)
+    th.start()
+    os_ready = V.validate_plugin(env, timeout=5)
+    th.join()
+    assert os_ready["ok"] and seen
+    ctr = seen[0]["containers"][0]
+    assert ctr["image"] == "reg/amd-operator-validator:9" and ctr["imagePullPolicy"] == "Always"
+    assert seen[0]["imagePullSecrets"] == [{"name": "s1"}]
