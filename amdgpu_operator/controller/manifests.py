@@ -90,12 +90,17 @@ def _container(name: str, image: str, pull: str, args: list[str], mounts=None, e
     return c
 
 
-def _wait_init(name: str, image: str, pull: str, what: str, extra_args=(), env=None) -> dict:
+def _wait_init(name: str, image: str, pull: str, what: str, extra_args=(), env=None, mounts=()) -> dict:
     """Init container that blocks until a validation file exists on the host."""
     return _container(name, image, pull, ["validate", what, *extra_args],
                       mounts=[_mount("run-amd-validations", VALIDATIONS_HOST_DIR, propagation="HostToContainer"),
-                              *_host_view()],
+                              *_host_view(), *mounts],
                       env=env, privileged=True)
+
+
+# the kubelet's pod-resources socket: the validator reads the device
+# manager's allocatable devices there (deviceplugin/podresources.py)
+POD_RESOURCES_MOUNT = {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources", "readOnly": True}
 
 
 def _workload_pod_env(v, image: str) -> list[dict]:
@@ -313,7 +318,7 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         extra = ["--resource", spec.devicePlugin.resourceName, "--with-driver"] + \
             (["--wait-toolkit"] if spec.toolkit.enabled else [])
         inits = [_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args],
-                            env=_workload_pod_env(v, image))]
+                            env=_workload_pod_env(v, image), mounts=[POD_RESOURCES_MOUNT])]
     elif v.pluginValidation and spec.devicePlugin.enabled:  # (validation pods: _workload_pod_env)
         # workload (all GPUs, RCCL over xGMI) and plugin (1-GPU pods through the
         # device plugin + OCI hook) validation run concurrently.  The workload
@@ -322,7 +327,7 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         # wait for the toolkit inside the step.
         extra = ["--resource", spec.devicePlugin.resourceName] + (["--wait-toolkit"] if spec.toolkit.enabled else [])
         inits.append(_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args],
-                                env=_workload_pod_env(v, image)))
+                                env=_workload_pod_env(v, image), mounts=[POD_RESOURCES_MOUNT]))
     else:
         if spec.toolkit.enabled:
             inits.append(_wait_init("toolkit-validation", image, v.imagePullPolicy, "toolkit"))
@@ -331,6 +336,8 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
                      [_mount("run-amd-validations", VALIDATIONS_HOST_DIR)], list(v.env), True,
                      v.resources.model_dump())
     vols = [_hostpath("run-amd-validations", VALIDATIONS_HOST_DIR), _hostpath("host-sys", "/sys", "Directory")]
+    if any(m["name"] == "pod-resources" for c in inits for m in c["volumeMounts"]):
+        vols.append(_hostpath("pod-resources", "/var/lib/kubelet/pod-resources"))
     return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
             _daemonset(spec, ns, owner, name, "validator", sa, [ctr], inits, vols)]
 

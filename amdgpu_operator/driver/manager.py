@@ -169,13 +169,13 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
         elif why:
             raise RuntimeError(f"driver mismatch and no installer in this image: {why}")
     deadline = time.monotonic() + timeout
-    while True:
+    for delay in env.waits():
         ok, msg = topology.probe(env.sysfs_root())
         if ok:
             break
         if time.monotonic() >= deadline:
             raise RuntimeError(f"driver did not come up: {msg}")
-        if (stop.wait(env.poll_s) if stop is not None else (time.sleep(env.poll_s) or False)):
+        if (stop.wait(delay) if stop is not None else (time.sleep(delay) or False)):
             raise RuntimeError("stopped")
     cur = loaded_version(env)
     if ran_script and want and cur != want:

@@ -20,7 +20,7 @@ from urllib.parse import quote, urlencode
 from . import resources as R
 from .fakeapi import AlreadyExists, ApiError, Conflict, FakeApiServer, NotFound
 
-__all__ = ["LocalClient", "RestClient", "ApiError", "NotFound", "AlreadyExists", "Conflict", "apply_object"]
+__all__ = ["LocalClient", "RestClient", "ApiError", "NotFound", "AlreadyExists", "Conflict", "apply_object", "wait_for"]
 
 
 class LocalClient:
@@ -35,6 +35,11 @@ class LocalClient:
 
     def list(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
         return self.server.list(api_version, kind, namespace, label_selector, field_selector)
+
+    def list_rv(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
+        """Items plus a resourceVersion to watch from (changes after it are replayed)."""
+        rv = self.server.resource_version()
+        return self.server.list(api_version, kind, namespace, label_selector, field_selector), str(rv)
 
     def update(self, obj):
         return self.server.update(obj)
@@ -156,13 +161,17 @@ class RestClient:
         return r.json()
 
     def list(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
+        return self.list_rv(api_version, kind, namespace, label_selector, field_selector)[0]
+
+    def list_rv(self, api_version, kind, namespace=None, label_selector=None, field_selector=None):
         t = R.rtype(api_version, kind)
         if isinstance(label_selector, dict):
             label_selector = ",".join(f"{k}={v}" for k, v in label_selector.items())
         r = self.session.get(self._url(t, namespace, query={"labelSelector": label_selector,
                                                            "fieldSelector": field_selector}), timeout=self.timeout)
         _raise_for(r)
-        return r.json().get("items", [])
+        body = r.json()
+        return body.get("items", []), (body.get("metadata") or {}).get("resourceVersion")
 
     def update(self, obj):
         t = R.rtype_of(obj)
@@ -211,6 +220,67 @@ class RestClient:
                     raise ApiError(int(ev["object"].get("code", 500)), ev["object"].get("reason", ""),
                                    ev["object"].get("message", ""))
                 yield ev["type"], ev["object"]
+
+
+def wait_for(client, api_version: str, kind: str, done, namespace=None, name: str | None = None,
+             label_selector=None, field_selector: str | None = None, timeout: float = 60.0,
+             stop: threading.Event | None = None, poll_s: float = 1.0) -> tuple[dict, bool]:
+    """Block until ``done(objects)`` holds for the ``kind`` objects named
+    ``name`` (and/or matching the selectors); ``objects`` maps name -> object.
+
+    List, then watch from the list's resourceVersion (client-go's
+    list-watch): the condition is checked on the listed state (an empty one
+    included) and again on every change, so it is seen as soon as it holds,
+    and waiting costs one open request instead of a GET per object per poll.
+    The list-watch restarts when the server ends the watch (timeout, 410
+    Gone); if watching fails altogether (RBAC, proxy) it lists every
+    ``poll_s``.  Returns ``(objects, True)``, or the last state and False on
+    timeout / ``stop``.
+    """
+    import time
+
+    fields = ",".join(f for f in (f"metadata.name={name}" if name else None, field_selector) if f) or None
+    deadline = time.monotonic() + timeout
+    objs: dict = {}
+    watch_ok = True
+    while True:
+        try:
+            items, rv = client.list_rv(api_version, kind, namespace, label_selector, fields)
+            objs = {o["metadata"]["name"]: o for o in items}
+        except (ApiError, OSError, ValueError):
+            rv = None
+        if done(objs):
+            return objs, True
+        remaining = deadline - time.monotonic()
+        if remaining <= 0 or (stop is not None and stop.is_set()):
+            return objs, False
+        if watch_ok and rv is not None:
+            try:
+                for etype, obj in client.watch(api_version, kind, namespace, label_selector, fields,
+                                               resource_version=rv, stop=stop,
+                                               timeout=max(1.0, min(remaining, 30.0))):
+                    n = obj["metadata"]["name"]
+                    if etype == "DELETED":
+                        objs.pop(n, None)
+                    elif etype in ("ADDED", "MODIFIED"):
+                        objs[n] = obj
+                    else:
+                        continue  # BOOKMARK
+                    if done(objs):
+                        return objs, True
+                    if time.monotonic() >= deadline:
+                        return objs, False
+                continue  # watch ended: list again
+            except ApiError as e:
+                if e.code != 410:  # 410 Gone: resourceVersion too old, list again
+                    watch_ok = False
+            except (OSError, ValueError):
+                watch_ok = False
+        wait = min(poll_s, max(0.0, deadline - time.monotonic()))
+        if stop is not None:
+            stop.wait(wait)
+        else:
+            time.sleep(wait)
 
 
 # maps the operator owns completely: an extra key on the live object is drift

@@ -304,6 +304,9 @@ class FakeApiServer:
                 for erv, etype, obj in self._history:
                     if erv > rv:
                         w.offer(etype, obj)
+            else:  # like kube-apiserver: the current state as synthetic ADDED events first
+                for obj in self._store.values():
+                    w.offer("ADDED", obj)
             self._watches.append(w)
         return w
 

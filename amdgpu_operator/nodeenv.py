@@ -143,6 +143,16 @@ class NodeEnv:
             poll_s=float(e.get("VALIDATION_POLL_S", "1.0")),
         )
 
+    def waits(self, first_s: float = 0.005, factor: float = 1.5):
+        """Sleep lengths for polling a local condition (a ready file, the
+        driver's sysfs): start at ``first_s`` and grow to ``poll_s``, so a
+        condition that turns true quickly is seen within milliseconds and a
+        long wait still costs one check per ``poll_s``."""
+        d = min(first_s, self.poll_s)
+        while True:
+            yield d
+            d = min(self.poll_s, d * factor)
+
     def validation_file(self, name: str) -> str:
         return os.path.join(self.validations_dir, name)
 

@@ -20,7 +20,6 @@ through ``amdsmi_set_gpu_compute_partition`` / ``amdsmi_set_gpu_memory_partition
 from __future__ import annotations
 
 import os
-import time
 from dataclasses import dataclass
 
 from ..nodeenv import NodeEnv
@@ -151,15 +150,13 @@ def evict_gpu_pods(env: NodeEnv) -> list[str]:
 
 
 def wait_gpu_pods_gone(env: NodeEnv, timeout: float) -> bool:
-    """Poll until no GPU pod is left on the node, Terminating ones included
+    """Wait until no GPU pod is left on the node, Terminating ones included
     (they hold ``/dev/kfd`` until their containers exit)."""
-    deadline = time.monotonic() + timeout
-    while True:
-        if not any(_uses_gpu(p) for p in env.client.list("v1", "Pod", field_selector=f"spec.nodeName={env.node_name}")):
-            return True
-        if time.monotonic() >= deadline:
-            return False
-        time.sleep(env.poll_s)
+    from ..kube.client import wait_for
+
+    _, ok = wait_for(env.client, "v1", "Pod", lambda pods: not any(_uses_gpu(p) for p in pods.values()),
+                     field_selector=f"spec.nodeName={env.node_name}", timeout=timeout, poll_s=env.poll_s)
+    return ok
 
 
 def restart_device_plugin(env: NodeEnv) -> None:

@@ -149,8 +149,8 @@ class FakeKubelet:
     def _podres_allocatable(self, request, context):
         out = api.podres["AllocatableResourcesResponse"]()
         for name, res in list(self.resources.items()):
-            with res.cv:
-                ids = [i for i, h in res.devices.items() if h == api.HEALTHY]
+            with res.cv:  # like the kubelet's device manager: every reported device, healthy or not
+                ids = list(res.devices)
             out.devices.add(resource_name=name, device_ids=ids)
         return out
 
@@ -232,7 +232,10 @@ class FakeKubelet:
         res = self.resources[resource]
         free = self.free_devices(resource)
         if count > len(free):
-            raise RuntimeError(f"insufficient {resource}: want {count}, free {len(free)}")
+            with self._lock:
+                holders = sorted({k[1] for k, (r, _) in self.assignments.items() if r == resource})
+            raise RuntimeError(f"insufficient {resource}: want {count}, free {len(free)} "
+                               f"(devices {len(res.devices)}, healthy {self.allocatable(resource)}, held by {holders})")
         ids = free[:count]
         if res.options.get_preferred_allocation_available:
             req, resp, _ = api.DEVICE_PLUGIN_METHODS["GetPreferredAllocation"]

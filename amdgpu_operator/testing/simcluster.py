@@ -205,15 +205,23 @@ class _PodRun:
 class SimCluster:
     def __init__(self, workdir: str, nodes: list[NodeSpec], namespace: str = DEFAULT_NAMESPACE,
                  fake_gpu: bool = True, poll_s: float = 0.01, launcher=None,
-                 termination_s: float | None = None):
+                 termination_s: float | None = None, agent_poll_s: float | None = None,
+                 node_status_s: float | None = None):
         """``termination_s``: model graceful pod deletion - a deleted pod stays
         Terminating (listed, with ``deletionTimestamp``) for that many seconds
-        (capped by its own grace period) before its kubelet removes it."""
+        (capped by its own grace period) before its kubelet removes it.
+        ``poll_s`` paces the simulated kubelet / controllers; ``agent_poll_s``
+        is the operands' own ``VALIDATION_POLL_S`` (default: ``poll_s``).
+        ``node_status_s`` models the kubelet's ``nodeStatusUpdateFrequency``
+        (10 s by default on a real kubelet): device-plugin capacity reaches
+        ``Node.status`` only on that tick (default: every ``poll_s``)."""
         self.workdir = workdir
         self.termination_s = termination_s
         self.namespace = namespace
         self.fake_gpu = fake_gpu
         self.poll_s = poll_s
+        self.agent_poll_s = poll_s if agent_poll_s is None else agent_poll_s
+        self.node_status_s = poll_s if node_status_s is None else node_status_s
         self.launcher = launcher
         self.api = FakeApiServer()
         self.api.graceful_pod_deletion = termination_s is not None
@@ -266,7 +274,7 @@ class SimCluster:
                       containerd_config=os.path.join(d, "etc/containerd/config.toml"),
                       crio_config_dir=os.path.join(d, "etc/crio/crio.conf.d"),
                       docker_config=os.path.join(d, "etc/docker/daemon.json"),
-                      install_dir=os.path.join(d, "usr/local/amd"), namespace=self.namespace, poll_s=self.poll_s,
+                      install_dir=os.path.join(d, "usr/local/amd"), namespace=self.namespace, poll_s=self.agent_poll_s,
                       launcher=self._launch)
         if ns.sysfs_root is None and ns.gpus > 0:  # driver installs / unloads act on the fake tree
             env.extra["kmod"] = fakesys.SimModule(root)
@@ -468,6 +476,10 @@ class SimCluster:
             with self._lock:
                 for name, pod in live.items():
                     if name not in node.pods or pod["metadata"].get("deletionTimestamp"):
+                        try:  # listed before a delete the watch has handled since: do not run it again
+                            pod = self.client.get("v1", "Pod", name, pod["metadata"].get("namespace"))
+                        except NotFound:
+                            continue
                         self._on_pod(node, "ADDED", pod)
                 for name in [n for n in node.pods if n not in live]:
                     self._on_pod(node, "DELETED", {"metadata": {"name": name}})
@@ -516,8 +528,17 @@ class SimCluster:
         threading.Thread(target=finish, daemon=True, name=f"sim-terminate-{name}").start()
 
     def _node_status_loop(self, node: SimNode) -> None:
+        """The kubelet's node-status sync: device-plugin capacity is published
+        on every ``node_status_s`` tick (with client-go style 4% jitter when
+        modelling a real period), not when a plugin registers."""
+        import random
+
         last = None
-        while not self.stop_event.wait(self.poll_s):
+        period = self.node_status_s
+        modelled = period > self.poll_s
+        delay = random.uniform(0, period) if modelled else period  # tick phase: the kubelet started long before
+        while not self.stop_event.wait(delay):
+            delay = period * (1 + 0.04 * random.random()) if modelled else period
             caps = {}
             for res in list(node.kubelet.resources):
                 caps[res] = (node.kubelet.capacity(res), node.kubelet.allocatable(res))

@@ -33,6 +33,7 @@ import uuid
 from concurrent.futures import ThreadPoolExecutor
 
 from .. import RESOURCE_NAME, native
+from ..kube.client import wait_for
 from ..nodeenv import REPORT_EARLY_ENV, NodeEnv
 from ..utils.logs import get_logger
 
@@ -88,16 +89,16 @@ def clear_ready(env: NodeEnv, steps=READY_FILES) -> None:
 
 def wait_ready(env: NodeEnv, step: str, timeout: float = 600.0, stop: threading.Event | None = None) -> dict:
     deadline = time.monotonic() + timeout
-    while True:
+    for delay in env.waits():
         d = read_ready(env, step)
         if d is not None:
             return d
         if time.monotonic() >= deadline:
             raise StepFailed(f"timed out waiting for {READY_FILES[step]}")
-        if stop is not None and stop.wait(env.poll_s):
+        if stop is not None and stop.wait(delay):
             raise StepFailed("stopped")
         if stop is None:
-            time.sleep(env.poll_s)
+            time.sleep(delay)
 
 
 # -------------------------------------------------------------------- steps --
@@ -108,7 +109,7 @@ def validate_driver(env: NodeEnv, timeout: float = 600.0, stop=None) -> dict:
 
     t0 = time.perf_counter()
     deadline = time.monotonic() + timeout
-    while True:
+    for delay in env.waits():
         ok, msg = topology.probe(env.sysfs_root())
         if ok:
             gpus = topology.enumerate_gpus(env.sysfs_root())
@@ -118,10 +119,10 @@ def validate_driver(env: NodeEnv, timeout: float = 600.0, stop=None) -> dict:
         if time.monotonic() >= deadline:
             raise StepFailed(f"driver not ready: {msg}")
         if stop is not None:
-            if stop.wait(env.poll_s):
+            if stop.wait(delay):
                 raise StepFailed("stopped")
         else:
-            time.sleep(env.poll_s)
+            time.sleep(delay)
 
 
 def gate_env() -> dict:
@@ -282,11 +283,40 @@ def allocatable(node: dict, resource: str) -> int:
         return 0
 
 
+def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: float, stop) -> str | None:
+    """Wait until the kubelet's device manager holds ``expect`` devices of
+    ``resource`` (pod-resources ``GetAllocatableResources``,
+    deviceplugin/podresources.py).  Returns "kubelet", or None when that API
+    is not reachable (the caller falls back to ``Node.status``)."""
+    from ..deviceplugin.podresources import KubeletDevices
+
+    kd = KubeletDevices(env.pod_resources_socket)
+    if not kd.available():
+        return None
+    try:
+        for delay in env.waits():
+            n = kd.count(resource)
+            if n is None:
+                return None
+            if n >= expect:
+                return "kubelet"
+            if time.monotonic() >= deadline:
+                raise StepFailed(f"kubelet holds {n} {resource} devices, expected {expect}")
+            if stop is not None and stop.wait(delay):
+                raise StepFailed("stopped")
+            if stop is None:
+                time.sleep(delay)
+    finally:
+        kd.close()
+    return None
+
+
 def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | None = None,
                     pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                     image: str | None = None, pull_policy: str = "IfNotPresent",
                     pull_secrets: list[str] | None = None) -> dict:
-    """Wait for Allocatable == GPUs, then run one 1-GPU pod per device.
+    """Wait until the kubelet holds one device per GPU, then run one 1-GPU
+    pod per device.
 
     The pods run the validator's own image (``VALIDATOR_IMAGE`` in the
     validator container's env, with its pull policy and secrets, which
@@ -302,16 +332,18 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     if expect is None:
         expect = len(topology.enumerate_gpus(env.sysfs_root()))
     deadline = time.monotonic() + timeout
-    while True:
-        n = allocatable(_node(env), resource)
-        if n >= expect:
-            break
-        if time.monotonic() >= deadline:
-            raise StepFailed(f"allocatable {resource}={n}, expected {expect}")
-        if stop is not None and stop.wait(env.poll_s):
-            raise StepFailed("stopped")
-        if stop is None:
-            time.sleep(env.poll_s)
+    source = _wait_kubelet_devices(env, resource, expect, deadline, stop)
+    if source is None:  # no pod-resources API: wait for the kubelet to publish Node.status.allocatable
+        source = "node-status"
+        nodes, ok = wait_for(env.client, "v1", "Node",
+                             lambda o: allocatable(o.get(env.node_name) or {}, resource) >= expect,
+                             name=env.node_name, timeout=max(0.0, deadline - time.monotonic()), stop=stop,
+                             poll_s=env.poll_s)
+        if not ok:
+            if stop is not None and stop.is_set():
+                raise StepFailed("stopped")
+            raise StepFailed(f"allocatable {resource}={allocatable(nodes.get(env.node_name) or {}, resource)}, "
+                             f"expected {expect}")
     t_alloc = time.perf_counter() - t0
     run_id = uuid.uuid4().hex[:8]
     pod_args = list(pod_args or ["--steps", "hip,vecadd,gemm", "--gemm", "1024"])
@@ -335,19 +367,16 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
             pod["spec"]["imagePullSecrets"] = [{"name": x} for x in pull_secrets]
         env.client.create(pod)
         names.append(name)
-    phases = {}
-    while True:
-        phases = {n: ((env.client.get("v1", "Pod", n, env.namespace).get("status") or {}).get("phase", "Pending"))
-                  for n in names}
-        if all(p in ("Succeeded", "Failed") for p in phases.values()):
-            break
-        if time.monotonic() >= deadline:
-            break
-        if stop is not None and stop.wait(env.poll_s):
-            break
-        if stop is None:
-            time.sleep(env.poll_s)
-    pods = [env.client.get("v1", "Pod", n, env.namespace) for n in names]
+
+    def phase(o):
+        return (o.get("status") or {}).get("phase", "Pending")
+
+    live, _ = wait_for(env.client, "v1", "Pod", lambda objs: all(
+        n in objs and phase(objs[n]) in ("Succeeded", "Failed") for n in names), namespace=env.namespace,
+        label_selector=f"{WORKLOAD_POD_LABEL}={run_id}", timeout=max(0.0, deadline - time.monotonic()),
+        stop=stop, poll_s=env.poll_s)
+    phases = {n: phase(live[n]) if n in live else "Missing" for n in names}
+    pods = [live.get(n) or {} for n in names]
     devices = [((p.get("metadata", {}).get("annotations") or {}).get("amd.com/gpu.allocated", "")) for p in pods]
     for n in names:
         try:
@@ -357,6 +386,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     if not all(p == "Succeeded" for p in phases.values()):
         raise StepFailed(f"plugin validation pods did not succeed: {phases}")
     summary = {"ok": True, "pods": expect, "devices": devices, "allocatable_wait_s": round(t_alloc, 4),
+               "allocatable_source": source,
                "seconds": time.perf_counter() - t0}
     write_ready(env, "plugin", summary)
     return summary

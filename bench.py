@@ -63,6 +63,10 @@ def parse():
                     help="counter gate through AQL profiling packets (default) or the rocprofiler-sdk tool")
     ap.add_argument("--no-prespawn", action="store_true",
                     help="start the validator processes only after the driver validation (A/B of the start gate)")
+    ap.add_argument("--kubelet-status-s", type=float, default=10.0,
+                    help="simulated kubelet nodeStatusUpdateFrequency: Node.status.allocatable follows on that tick")
+    ap.add_argument("--agent-poll-s", type=float, default=None,
+                    help="operands' VALIDATION_POLL_S (default: the production default of NodeEnv)")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--detail", default=None, help="write per-step breakdown JSON here")
     return ap.parse_args()
@@ -97,13 +101,20 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
     if args.quick_workload:
         values = deep_merge(values, {"validator": {"workload": {"gemmN": 1024, "hbmBytes": 1 << 26,
                                                                 "rcclElems": 1 << 20, "xgmiElems": 1 << 20}}})
+    from amdgpu_operator.nodeenv import NodeEnv
+
     d = tempfile.mkdtemp(prefix="step-", dir=workdir)
-    cluster = SimCluster(d, [node], fake_gpu=fake_gpu, poll_s=0.005, launcher=launcher).start()
+    agent_poll = NodeEnv.poll_s if args.agent_poll_s is None else args.agent_poll_s
+    cluster = SimCluster(d, [node], fake_gpu=fake_gpu, poll_s=0.005, launcher=launcher, agent_poll_s=agent_poll,
+                         node_status_s=args.kubelet_status_s or None).start()
     try:
         t0 = time.perf_counter()
         t0_wall = time.time()
         cluster.install_operator(values)
-        ttr = cluster.wait_ready(args.timeout, {"mi355x-node-0": n_gpus})
+        ttr = cluster.wait_ready(args.timeout)  # validator pod Ready: node validated, policy ready
+        # the kubelet then publishes amd.com/gpu in Node.status on its own status tick
+        cluster.wait_ready(args.timeout, {"mi355x-node-0": n_gpus})
+        alloc_visible = time.perf_counter() - t0
         t_total = time.perf_counter() - t0
         cp = cluster.policy()
         nobj = cluster.client.get("v1", "Node", "mi355x-node-0")
@@ -125,6 +136,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
                 timeline[step] = round(r["time"] - t0_wall, 4)
         return {
             "time_to_ready_s": ttr,
+            "allocatable_visible_s": alloc_visible,
+            "allocatable_source": plug.get("allocatable_source"),
             "trace": cluster.trace_since(t0),
             "timeline_s": timeline,
             "wall_s": t_total,
@@ -177,6 +190,7 @@ def main():
     if has_gpu:
         torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
 
+    from amdgpu_operator.nodeenv import NodeEnv
     from amdgpu_operator.parallel.launcher import DistributedLauncher
 
     launcher = DistributedLauncher(rank, world, group) if world > 1 else None
@@ -278,6 +292,9 @@ def main():
                 "allocatable_amd_com_gpu": alloc,
                 "time_to_ready_s": [round(x, 4) for x in ttr],
                 "time_to_ready_min_s": round(min(ttr), 4),
+                "allocatable_visible_s": [round(r["allocatable_visible_s"], 3) for r in results],
+                "kubelet_node_status_s": args.kubelet_status_s,
+                "validation_poll_s": NodeEnv.poll_s if args.agent_poll_s is None else args.agent_poll_s,
                 "gemm_tflops_per_gpu": results[-1]["gemm_tflops"],
                 "hbm_gbps_per_gpu": results[-1]["hbm_gbps"],
                 "rccl_busbw_gbps": results[-1]["rccl_busbw_gbps"],

@@ -138,3 +138,62 @@ def test_selector_parser_edge_cases():
         {"matchExpressions": [{"key": "zone", "operator": "In", "values": ["a"]}]}]}}}
     assert R.node_selector_matches(node, {"gpu": "true"}, aff)
     assert not R.node_selector_matches(node, {"gpu": "false"})
+
+
+def test_unversioned_watch_starts_with_current_state(client):
+    """kube-apiserver semantics: a watch without resourceVersion first
+    replays the current objects as ADDED."""
+    client.create(R.new("v1", "Node", "a"))
+    client.create(R.new("v1", "Node", "b"))
+    got = [(et, o["metadata"]["name"]) for et, o in client.watch("v1", "Node", timeout=0.3)]
+    assert sorted(got) == [("ADDED", "a"), ("ADDED", "b")]
+
+
+def test_wait_for_list_then_watch(client):
+    from amdgpu_operator.kube.client import wait_for
+
+    client.create(R.new("v1", "Namespace", "ns"))
+    # an empty state can satisfy the condition at once (no event ever comes)
+    objs, ok = wait_for(client, "v1", "Pod", lambda o: not o, namespace="ns", timeout=2)
+    assert ok and objs == {}
+    for i in range(3):
+        client.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"p{i}", "namespace": "ns",
+                                                                       "labels": {"run": "x"}}, "spec": {}})
+
+    def finish():
+        time.sleep(0.2)
+        for i in range(3):
+            p = client.get("v1", "Pod", f"p{i}", "ns")
+            p["status"] = {"phase": "Succeeded"}
+            client.update_status(p)
+
+    th = threading.Thread(target=finish)
+    th.start()
+    t0 = time.monotonic()
+    objs, ok = wait_for(client, "v1", "Pod", lambda o: len(o) == 3 and all(
+        (p.get("status") or {}).get("phase") == "Succeeded" for p in o.values()),
+        namespace="ns", label_selector="run=x", timeout=10, poll_s=5.0)
+    th.join()
+    assert ok and sorted(objs) == ["p0", "p1", "p2"]
+    assert time.monotonic() - t0 < 2.0  # event-driven, not one poll_s per check
+    # a single object by name; a timeout returns the last state
+    objs, ok = wait_for(client, "v1", "Pod", lambda o: False, namespace="ns", name="p1", timeout=0.3)
+    assert not ok and list(objs) == ["p1"]
+
+
+def test_wait_for_falls_back_to_listing():
+    """No watch permission: wait_for lists every poll_s instead."""
+    from amdgpu_operator.kube.client import wait_for
+    from amdgpu_operator.kube.fakeapi import ApiError
+
+    class NoWatch(LocalClient):
+        def watch(self, *a, **kw):
+            raise ApiError(403, "Forbidden", "watch not allowed")
+            yield  # pragma: no cover
+
+    c = NoWatch(FakeApiServer())
+    c.create(R.new("v1", "Node", "a"))
+    threading.Timer(0.2, lambda: c.patch("v1", "Node", "a", {"metadata": {"labels": {"x": "1"}}})).start()
+    objs, ok = wait_for(c, "v1", "Node", lambda o: "x" in (o.get("a", {}).get("metadata", {}).get("labels") or {}),
+                        name="a", timeout=5, poll_s=0.05)
+    assert ok

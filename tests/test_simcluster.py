@@ -172,3 +172,47 @@ def test_gpu_pod_sees_only_its_allocated_devices(tmp_path):
     fakesys.build_node(synth, 4)
     env = container_device_env(synth, [1, 3])
     assert list(env) == ["ROCR_VISIBLE_DEVICES"] and env["ROCR_VISIBLE_DEVICES"].count("GPU-") == 2
+
+
+def test_validation_does_not_wait_for_the_kubelet_status_tick(cluster_factory):
+    """A real kubelet publishes device-plugin capacity in Node.status only on
+    its nodeStatusUpdateFrequency tick (10 s default).  The validator reads the
+    device manager through pod-resources instead, so the node is validated
+    well before Node.status.allocatable shows the GPUs."""
+    from amdgpu_operator.validator.validate import read_ready
+
+    c = cluster_factory([NodeSpec("gpu-1", 8)], agent_poll_s=1.0, node_status_s=20.0)
+    c.install_operator(REF)
+    ttr = c.wait_ready(15)
+    assert ttr < 10.0
+    plug = read_ready(c.nodes["gpu-1"].env, "plugin")
+    assert plug["allocatable_source"] == "kubelet" and plug["pods"] == 8
+    c.wait_ready(30, {"gpu-1": 8})  # the kubelet does publish them, on its own tick
+
+
+def test_kubelet_devices_client(tmp_path):
+    from amdgpu_operator.deviceplugin.podresources import KubeletDevices
+    from amdgpu_operator.deviceplugin.server import DevicePluginManager, PluginConfig
+    from amdgpu_operator.testing import fakesys
+    from amdgpu_operator.testing.fakekubelet import FakeKubelet
+
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 4)
+    sock = str(tmp_path / "pr" / "kubelet.sock")
+    assert KubeletDevices(sock).count("amd.com/gpu") is None  # no socket: caller falls back
+    k = FakeKubelet(str(tmp_path / "dp"), sock)
+    k.start()
+    m = DevicePluginManager(PluginConfig(socket_dir=str(tmp_path / "dp"), sysfs_root=root, watch_interval_s=0.05))
+    try:
+        kd = KubeletDevices(sock)
+        assert kd.count("amd.com/gpu") == 0
+        m.start()
+        assert k.wait_registered("amd.com/gpu", 10, min_devices=4)
+        assert kd.count("amd.com/gpu") == 4
+        m.set_health(m.devices[0].device_id_str, False, "test")
+        time.sleep(0.2)
+        assert kd.count("amd.com/gpu") == 4  # the device manager lists unhealthy devices too
+        kd.close()
+    finally:
+        m.stop()
+        k.stop()
