@@ -206,7 +206,8 @@ class SimCluster:
     def __init__(self, workdir: str, nodes: list[NodeSpec], namespace: str = DEFAULT_NAMESPACE,
                  fake_gpu: bool = True, poll_s: float = 0.01, launcher=None,
                  termination_s: float | None = None, agent_poll_s: float | None = None,
-                 node_status_s: float | None = None):
+                 node_status_s: float | None = None, operator_resync_s: float = 1.0,
+                 operator_debounce_s: float = 0.005):
         """``termination_s``: model graceful pod deletion - a deleted pod stays
         Terminating (listed, with ``deletionTimestamp``) for that many seconds
         (capped by its own grace period) before its kubelet removes it.
@@ -222,6 +223,8 @@ class SimCluster:
         self.poll_s = poll_s
         self.agent_poll_s = poll_s if agent_poll_s is None else agent_poll_s
         self.node_status_s = poll_s if node_status_s is None else node_status_s
+        self.operator_resync_s = operator_resync_s
+        self.operator_debounce_s = operator_debounce_s
         self.launcher = launcher
         self.api = FakeApiServer()
         self.api.graceful_pod_deletion = termination_s is not None
@@ -343,7 +346,8 @@ class SimCluster:
     def start_reconciler(self) -> ClusterPolicyReconciler:
         if self.reconciler is None:
             self.reconciler = ClusterPolicyReconciler(self.client, self.namespace)
-            self._spawn(lambda: self.reconciler.run(self.stop_event, resync_s=1.0, debounce_s=0.005),
+            self._spawn(lambda: self.reconciler.run(self.stop_event, resync_s=self.operator_resync_s,
+                                                    debounce_s=self.operator_debounce_s),
                         "sim-operator")
         return self.reconciler
 

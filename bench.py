@@ -106,7 +106,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
     d = tempfile.mkdtemp(prefix="step-", dir=workdir)
     agent_poll = NodeEnv.poll_s if args.agent_poll_s is None else args.agent_poll_s
     cluster = SimCluster(d, [node], fake_gpu=fake_gpu, poll_s=0.005, launcher=launcher, agent_poll_s=agent_poll,
-                         node_status_s=args.kubelet_status_s or None).start()
+                         node_status_s=args.kubelet_status_s or None,
+                         operator_resync_s=30.0, operator_debounce_s=0.02).start()  # cli/main.py defaults
     try:
         t0 = time.perf_counter()
         t0_wall = time.time()
