@@ -150,6 +150,7 @@ class ClusterPolicyReconciler:
         self._ttr: dict[str, float] = {}
         self.reconciles = 0
         self.metrics = ReconcileMetrics()
+        self._verified: dict = {}  # apply_object fast path: key -> (resourceVersion, desired hash)
         self.events = EventRecorder(client, "amd-gpu-operator")
         self._last_state: dict[str, str] = {}  # policy uid -> state last reported by an Event
 
@@ -222,7 +223,7 @@ class ClusterPolicyReconciler:
             ready = True
             detail = []
             for o in objs:
-                live, action = apply_object(self.client, o)
+                live, action = apply_object(self.client, o, verified=self._verified)
                 changed += action != "unchanged"
                 if o["kind"] == "DaemonSet" and state == "state-driver":
                     driver_live = live

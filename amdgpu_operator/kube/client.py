@@ -305,18 +305,27 @@ def contains(live, desired, key: str = "") -> bool:
     return live == desired
 
 
-def apply_object(client, obj: dict, field_owner: str = "amd-gpu-operator") -> tuple[dict, str]:
+def apply_object(client, obj: dict, field_owner: str = "amd-gpu-operator",
+                 verified: dict | None = None) -> tuple[dict, str]:
     """Create or update ``obj`` when the live object no longer contains it.
 
     Returns ``(object, action)`` with action in {"created", "updated", "unchanged"}.
     Drift made by someone else (a changed or removed field we own) is reverted:
     reconcile is level-triggered.  Server-added defaults do not count as drift.
+
+    ``verified`` (a dict the caller keeps across passes) remembers, per object,
+    the resourceVersion at which the live object was last found to contain
+    the desired state with a given hash: while neither changed, the field-by-
+    field comparison is skipped (any write by anyone bumps resourceVersion).
     """
     t = R.rtype_of(obj)
-    obj = R.deep(obj)
-    ann = R.meta(obj).setdefault("annotations", {})
+    md = dict(R.meta(obj))  # copy the levels this function writes; the rest is only read
+    md["annotations"] = dict(md.get("annotations") or {})
+    obj = {**obj, "metadata": md}
+    ann = md["annotations"]
     ann.setdefault("amd.com/managed-by", field_owner)
-    ann["amd.com/last-applied-hash"] = R.spec_hash(obj)
+    ann["amd.com/last-applied-hash"] = want = R.spec_hash(obj)
+    key = (t.api_version, t.kind, R.ns_of(obj), R.name_of(obj))
     try:
         cur = client.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
     except NotFound:
@@ -324,8 +333,13 @@ def apply_object(client, obj: dict, field_owner: str = "amd-gpu-operator") -> tu
             return client.create(obj), "created"
         except AlreadyExists:
             cur = client.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
+    rv = (cur.get("metadata") or {}).get("resourceVersion")
+    if verified is not None and rv and verified.get(key) == (rv, want):
+        return cur, "unchanged"
     desired = {k: v for k, v in obj.items() if k != "status"}
     if contains(cur, desired):
+        if verified is not None and rv:
+            verified[key] = (rv, want)
         return cur, "unchanged"
     obj["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
     # keep fields other controllers own on the live object

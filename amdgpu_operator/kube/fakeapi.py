@@ -20,6 +20,7 @@ paths, so :class:`amdgpu_operator.kube.client.RestClient` is tested over HTTP.
 from __future__ import annotations
 
 import itertools
+import pickle
 import queue
 import threading
 import time
@@ -71,6 +72,15 @@ def _field_ok(obj: dict, field_selector: str | None) -> bool:
     return True
 
 
+def _pack(obj: dict) -> bytes:
+    return pickle.dumps(obj, pickle.HIGHEST_PROTOCOL)
+
+
+def _copy(obj: dict) -> dict:
+    """Deep copy of a JSON-shaped object through pickle (C speed)."""
+    return pickle.loads(_pack(obj))
+
+
 class _Watch:
     def __init__(self, t: R.ResourceType, namespace, label_selector, field_selector):
         self.t = t
@@ -80,14 +90,16 @@ class _Watch:
         self.q: queue.Queue = queue.Queue()
         self.closed = False
 
-    def offer(self, etype: str, obj: dict) -> None:
+    def offer(self, etype: str, obj: dict, blob: bytes | None = None) -> None:
+        """``blob``: the object pickled once by the server for every watcher;
+        each consumer unpickles its own copy (3x cheaper than a deep copy)."""
         if self.closed or R.rtype_of(obj) != self.t:
             return
         if self.t.namespaced and self.namespace and R.ns_of(obj) != self.namespace:
             return
         if not R.matches(R.labels_of(obj), self.reqs) or not _field_ok(obj, self.field_selector):
             return
-        self.q.put((etype, R.deep(obj)))
+        self.q.put((etype, blob if blob is not None else _pack(obj)))
 
     def stream(self, timeout: float | None = None, stop: threading.Event | None = None):
         """Yield (type, obj) until closed, ``stop`` is set or ``timeout`` passes idle."""
@@ -102,7 +114,7 @@ class _Watch:
                 continue
             if item is None:
                 return
-            yield item
+            yield item[0], pickle.loads(item[1])
 
     def close(self) -> None:
         self.closed = True
@@ -116,7 +128,10 @@ class FakeApiServer:
         self._rv = itertools.count(1)
         self._last_rv = 0
         self._watches: list[_Watch] = []
-        self._history: list[tuple[int, str, dict]] = []  # for watch-from-resourceVersion
+        self._history: list[tuple[int, str, bytes]] = []  # for watch-from-resourceVersion
+        # every stored object, pickled at its last write: reads hand out
+        # pickle.loads copies (the store itself is never handed out)
+        self._blobs: dict[tuple, bytes] = {}
         self.request_count = 0
         self.hooks: list = []  # callables(event_type, obj) run synchronously after commit
         # Pods on a node stay Terminating until a zero-grace delete (see delete())
@@ -129,13 +144,24 @@ class FakeApiServer:
         obj["metadata"]["resourceVersion"] = str(rv)
 
     def _emit(self, etype: str, obj: dict) -> None:
-        self._history.append((int(obj["metadata"]["resourceVersion"]), etype, R.deep(obj)))
+        blob = _pack(obj)
+        k = R.key_of(obj)
+        if etype == "DELETED":
+            self._blobs.pop(k, None)
+        else:
+            self._blobs[k] = blob
+        self._history.append((int(obj["metadata"]["resourceVersion"]), etype, blob))
         if len(self._history) > 20000:
             del self._history[:5000]
         for w in list(self._watches):
-            w.offer(etype, obj)
+            w.offer(etype, obj, blob)
         for h in list(self.hooks):
-            h(etype, R.deep(obj))
+            h(etype, pickle.loads(blob))
+
+    def _out(self, k: tuple, o: dict) -> dict:
+        """A caller's copy of the stored object ``o`` at key ``k``."""
+        b = self._blobs.get(k)
+        return pickle.loads(b) if b is not None else R.deep(o)
 
     def _key(self, t: R.ResourceType, namespace, name) -> tuple:
         return (t.api_version, t.kind, namespace if t.namespaced else None, name)
@@ -143,7 +169,7 @@ class FakeApiServer:
     # ------------------------------------------------------------------ verbs
     def create(self, obj: dict) -> dict:
         self.request_count += 1
-        obj = R.deep(obj)
+        obj = _copy(obj)
         t = R.rtype_of(obj)
         md = R.meta(obj)
         if not md.get("name"):
@@ -170,16 +196,17 @@ class FakeApiServer:
             self._bump(obj)
             self._store[k] = obj
             self._emit("ADDED", obj)
-            return R.deep(obj)
+            return self._out(k, obj)
 
     def get(self, api_version: str, kind: str, name: str, namespace: str | None = None) -> dict:
         self.request_count += 1
         t = R.rtype(api_version, kind)
         with self._lock:
-            o = self._store.get(self._key(t, namespace, name))
+            k = self._key(t, namespace, name)
+            o = self._store.get(k)
             if o is None:
                 raise NotFound(f"{kind} {namespace}/{name}")
-            return R.deep(o)
+            return self._out(k, o)
 
     def list(self, api_version: str, kind: str, namespace: str | None = None, label_selector=None,
              field_selector: str | None = None) -> list[dict]:
@@ -188,13 +215,14 @@ class FakeApiServer:
         reqs = R.parse_selector(label_selector)
         with self._lock:
             out = []
-            for (av, kd, ns, _), o in self._store.items():
+            for k, o in self._store.items():
+                av, kd, ns, _ = k
                 if av != t.api_version or kd != t.kind:
                     continue
                 if t.namespaced and namespace and ns != namespace:
                     continue
                 if R.matches(R.labels_of(o), reqs) and _field_ok(o, field_selector):
-                    out.append(R.deep(o))
+                    out.append(self._out(k, o))
             out.sort(key=lambda o: (R.ns_of(o) or "", R.name_of(o)))
             return out
 
@@ -203,7 +231,7 @@ class FakeApiServer:
 
     def update(self, obj: dict, subresource: str | None = None) -> dict:
         self.request_count += 1
-        obj = R.deep(obj)
+        obj = _copy(obj)
         t = R.rtype_of(obj)
         md = R.meta(obj)
         with self._lock:
@@ -215,13 +243,13 @@ class FakeApiServer:
             if rv and rv != cur["metadata"]["resourceVersion"]:
                 raise Conflict(f"{t.kind} {md.get('name')}: resourceVersion {rv} != {cur['metadata']['resourceVersion']}")
             if subresource == "status":
-                new = R.deep(cur)
+                new = self._out(k, cur)
                 new["status"] = obj.get("status", {})
             else:
                 new = obj
                 # the main endpoint never changes status (status subresource semantics)
                 if "status" in cur:
-                    new["status"] = R.deep(cur["status"])
+                    new["status"] = self._out(k, cur)["status"]
                 else:
                     new.pop("status", None)
                 for f in ("uid", "creationTimestamp", "generation"):
@@ -232,7 +260,7 @@ class FakeApiServer:
             self._bump(new)
             self._store[k] = new
             self._emit("MODIFIED", new)
-            return R.deep(new)
+            return self._out(k, new)
 
     def patch(self, api_version: str, kind: str, name: str, patch: dict, namespace: str | None = None,
               subresource: str | None = None) -> dict:
@@ -301,12 +329,12 @@ class FakeApiServer:
         with self._lock:
             if resource_version not in (None, "", "0", 0):
                 rv = int(resource_version)
-                for erv, etype, obj in self._history:
+                for erv, etype, blob in self._history:
                     if erv > rv:
-                        w.offer(etype, obj)
+                        w.offer(etype, pickle.loads(blob), blob)
             else:  # like kube-apiserver: the current state as synthetic ADDED events first
-                for obj in self._store.values():
-                    w.offer("ADDED", obj)
+                for k, obj in self._store.items():
+                    w.offer("ADDED", obj, self._blobs.get(k))
             self._watches.append(w)
         return w
 

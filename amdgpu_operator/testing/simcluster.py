@@ -240,6 +240,7 @@ class SimCluster:
         self.events: list[tuple[float, str, str]] = []
         self._node_specs = nodes
         self._short_dirs: list[str] = []
+        self._hashes: dict[tuple, str] = {}
 
     # -------------------------------------------------------------- setup
     # a unix socket path must fit sockaddr_un.sun_path (108 bytes); the node's
@@ -366,9 +367,14 @@ class SimCluster:
             shutil.rmtree(d, ignore_errors=True)
 
     # --------------------------------------------------- DaemonSet controller
-    @staticmethod
-    def _template_hash(ds: dict) -> str:
-        return hashlib.sha1(json.dumps(ds["spec"]["template"], sort_keys=True).encode()).hexdigest()[:10]
+    def _template_hash(self, ds: dict) -> str:
+        """controller-revision-hash of the pod template (cached per spec generation)."""
+        md = ds["metadata"]
+        k = (md.get("uid"), md.get("generation"))
+        h = self._hashes.get(k)
+        if h is None:
+            h = self._hashes[k] = hashlib.sha1(json.dumps(ds["spec"]["template"], sort_keys=True).encode()).hexdigest()[:10]
+        return h
 
     def _eligible(self, ds: dict, node: dict) -> bool:
         tspec = ds["spec"]["template"]["spec"]
@@ -377,13 +383,17 @@ class SimCluster:
     def sync_daemonsets(self) -> None:
         with self._lock:
             nodes = self.client.list("v1", "Node")
+            all_pods: dict[tuple, list] = {}  # (namespace, owner uid) -> pods: one list per sync
+            for p in self.client.list("v1", "Pod"):
+                for r in p["metadata"].get("ownerReferences") or []:
+                    if r.get("kind") == "DaemonSet":
+                        all_pods.setdefault((p["metadata"].get("namespace"), r.get("uid")), []).append(p)
             for ds in self.client.list("apps/v1", "DaemonSet"):
                 ns = ds["metadata"]["namespace"]
                 name = ds["metadata"]["name"]
                 h = self._template_hash(ds)
-                pods = {p["spec"]["nodeName"]: p for p in self.client.list(
-                    "v1", "Pod", ns, label_selector={"app": name}) if any(
-                    r.get("uid") == ds["metadata"]["uid"] for r in p["metadata"].get("ownerReferences", []))}
+                owned = all_pods.get((ns, ds["metadata"]["uid"]), [])
+                pods = {p["spec"]["nodeName"]: p for p in owned}
                 eligible = [n for n in nodes if self._eligible(ds, n)]
                 want = {n["metadata"]["name"] for n in eligible}
                 on_delete = (ds["spec"].get("updateStrategy") or {}).get("type") == "OnDelete"
@@ -409,12 +419,11 @@ class SimCluster:
                                                              "uid": ds["metadata"]["uid"], "controller": True}]},
                            "spec": {**tmpl["spec"], "nodeName": node_name}}
                     try:
-                        self.client.create(pod)
+                        owned.append(self.client.create(pod))
                     except Exception:  # noqa: BLE001 - AlreadyExists while the old one terminates
                         pass
-                # status
-                pods_now = [p for p in self.client.list("v1", "Pod", ns, label_selector={"app": name})
-                            if p["spec"].get("nodeName") in want]
+                # status (pods deleted above drop out on the next sync, as with an informer cache)
+                pods_now = [p for p in owned if p["spec"].get("nodeName") in want]
                 ready = sum(1 for p in pods_now if R.condition(p, "Ready") and R.condition(p, "Ready")["status"] == "True"
                             and p["metadata"]["labels"].get("controller-revision-hash") == h)
                 updated = sum(1 for p in pods_now if p["metadata"]["labels"].get("controller-revision-hash") == h)

@@ -113,18 +113,27 @@ def test_owner_reference_gc_and_namespace_delete(client):
         client.get("v1", "ConfigMap", "c", "ns")
 
 
-def test_apply_object_reverts_drift(client):
+@pytest.mark.parametrize("cached", [False, True])
+def test_apply_object_reverts_drift(client, cached):
+    verified = {} if cached else None  # the reconciler's fast path must not hide drift
     client.create(R.new("v1", "Namespace", "ns"))
     ds = R.new("apps/v1", "DaemonSet", "d", "ns", spec={"template": {"spec": {"containers": [{"name": "x"}]}}})
-    assert apply_object(client, ds)[1] == "created"
-    assert apply_object(client, ds)[1] == "unchanged"
+    before = R.deep(ds)
+    assert apply_object(client, ds, verified=verified)[1] == "created"
+    assert apply_object(client, ds, verified=verified)[1] == "unchanged"
+    assert apply_object(client, ds, verified=verified)[1] == "unchanged"
     client.patch("apps/v1", "DaemonSet", "d", {"spec": {"template": {"spec": {"containers": [{"name": "hacked"}]}}}},
                  "ns")
-    assert apply_object(client, ds)[1] == "updated"
+    assert apply_object(client, ds, verified=verified)[1] == "updated"
     assert client.get("apps/v1", "DaemonSet", "d", "ns")["spec"]["template"]["spec"]["containers"][0]["name"] == "x"
     # server-side defaults on the live object are not drift
     client.patch("apps/v1", "DaemonSet", "d", {"spec": {"revisionHistoryLimit": 10}}, "ns")
-    assert apply_object(client, ds)[1] == "unchanged"
+    assert apply_object(client, ds, verified=verified)[1] == "unchanged"
+    # a changed desired object is applied even when the live one is unchanged
+    ds2 = R.deep(ds)
+    ds2["spec"]["template"]["spec"]["containers"][0]["name"] = "y"
+    assert apply_object(client, ds2, verified=verified)[1] == "updated"
+    assert ds == before  # the caller's object is not modified
 
 
 def test_selector_parser_edge_cases():
