@@ -405,7 +405,7 @@ def _plugin_pod_args(extra: list[str]) -> list[str]:
     """Per-pod workload (1 GPU each): the pod can open its allocated GPU and run
     a kernel (HIP init + exact vectorAdd).  Kept tiny on purpose: it runs
     concurrently with the node's workload validation on the same GPUs."""
-    return ["--steps", "hip,vecadd"]
+    return ["--steps", "hip,vecadd", "--vecadd-elems", str(1 << 20)]
 
 
 def run_in_sim(cluster, run, container: dict, argv: list[str], init: bool) -> None:

@@ -143,15 +143,18 @@ class NodeEnv:
             poll_s=float(e.get("VALIDATION_POLL_S", "1.0")),
         )
 
-    def waits(self, first_s: float = 0.005, factor: float = 1.5):
-        """Sleep lengths for polling a local condition (a ready file, the
-        driver's sysfs): start at ``first_s`` and grow to ``poll_s``, so a
-        condition that turns true quickly is seen within milliseconds and a
-        long wait still costs one check per ``poll_s``."""
-        d = min(first_s, self.poll_s)
+    def waits(self, first_s: float = 0.002, factor: float = 1.5, cap_s: float = 0.02):
+        """Sleep lengths for polling a cheap local condition that no event
+        announces (the driver's sysfs, the kubelet's device list): start at
+        ``first_s`` and grow to ``min(cap_s, poll_s)``.  One check costs ~0.1
+        ms, so the 20 ms cap keeps a long wait at 0.5% of a core while a
+        condition is seen within 20 ms of turning true.  (Ready files are
+        waited for with inotify: utils/fswait.py.)"""
+        cap = min(cap_s, self.poll_s)
+        d = min(first_s, cap)
         while True:
             yield d
-            d = min(self.poll_s, d * factor)
+            d = min(cap, d * factor)
 
     def validation_file(self, name: str) -> str:
         return os.path.join(self.validations_dir, name)

@@ -642,7 +642,9 @@ class SimCluster:
                 raise RuntimeError("OCI hook did not inject /dev/kfd")
         self.trace("gpu-pod-hooked", run.name)
         argv = [str(native.binary("amdgpu-validator"))] + cmd[1:]
-        proc_env = {REPORT_EARLY_ENV: "1"} if REPORT_EARLY else {}
+        proc_env = {e["name"]: e["value"] for e in c.get("env") or [] if "value" in e}  # the container's env
+        if REPORT_EARLY:
+            proc_env[REPORT_EARLY_ENV] = "1"
         dev = devices[0] if devices else None
         if devices:
             proc_env.update(container_device_env(node.env.sysfs_root(), devices))

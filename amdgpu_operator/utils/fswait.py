@@ -1,0 +1,109 @@
+"""Wait for a file to appear: inotify on its directory, polling as a backstop.
+
+The operands hand readiness to each other through files in the validations
+directory (``/run/amd/validations`` on the host, mounted into every operand
+pod with HostToContainer propagation).  A ready file is written as a temp
+file and renamed into place (validator/validate.py ``write_ready``), which
+inotify reports on the directory as IN_MOVED_TO, so a waiter wakes when the
+file lands instead of at its next poll.  inotify sees writes from every
+container because they all share the host directory's inode.  The directory
+is re-checked every ``poll_s`` anyway (a directory created after the watch
+started, filesystems without inotify).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import ctypes.util
+import os
+import select
+import struct
+import threading
+import time
+
+IN_CLOSE_WRITE = 0x00000008
+IN_MOVED_TO = 0x00000080
+IN_CREATE = 0x00000100
+IN_NONBLOCK = 0o4000
+IN_CLOEXEC = 0o2000000
+
+_libc = None
+
+
+def _lib():
+    global _libc
+    if _libc is None:
+        lib = ctypes.CDLL(ctypes.util.find_library("c") or "libc.so.6", use_errno=True)
+        lib.inotify_init1.argtypes = [ctypes.c_int]
+        lib.inotify_add_watch.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_uint32]
+        _libc = lib
+    return _libc
+
+
+class DirWatch:
+    """inotify watch on one directory (entries created, written or moved in)."""
+
+    def __init__(self, directory: str):
+        self.fd = -1
+        try:
+            lib = _lib()
+            fd = lib.inotify_init1(IN_NONBLOCK | IN_CLOEXEC)
+            if fd < 0:
+                return
+            if lib.inotify_add_watch(fd, os.fsencode(directory), IN_CREATE | IN_MOVED_TO | IN_CLOSE_WRITE) < 0:
+                os.close(fd)
+                return
+            self.fd = fd
+        except (OSError, AttributeError):
+            self.fd = -1
+
+    @property
+    def active(self) -> bool:
+        return self.fd >= 0
+
+    def wait(self, timeout: float) -> bool:
+        """Block up to ``timeout`` for an event; drain it.  True on an event."""
+        if self.fd < 0:
+            time.sleep(max(0.0, timeout))
+            return False
+        r, _, _ = select.select([self.fd], [], [], max(0.0, timeout))
+        if not r:
+            return False
+        try:
+            while os.read(self.fd, 65536):
+                pass
+        except BlockingIOError:
+            pass
+        return True
+
+    def close(self) -> None:
+        if self.fd >= 0:
+            os.close(self.fd)
+            self.fd = -1
+
+
+def wait_for_file(path: str, timeout: float, stop: threading.Event | None = None, poll_s: float = 1.0,
+                  check=os.path.exists) -> bool:
+    """True once ``check(path)`` holds (default: the file exists); False on
+    timeout or ``stop``.  Wakes on inotify events in the file's directory and
+    re-checks at least every ``poll_s`` (every 50 ms when a ``stop`` event is
+    given, to notice it; every 10 ms without inotify)."""
+    deadline = time.monotonic() + timeout
+    if check(path):
+        return True
+    directory = os.path.dirname(path) or "."
+    os.makedirs(directory, exist_ok=True)
+    w = DirWatch(directory)
+    period = poll_s if w.active else min(poll_s, 0.01)
+    if stop is not None:
+        period = min(period, 0.05)
+    try:
+        while True:
+            if check(path):  # checked after the watch is armed: a file landing in between is not missed
+                return True
+            left = deadline - time.monotonic()
+            if left <= 0 or (stop is not None and stop.is_set()):
+                return False
+            w.wait(min(left, period))
+    finally:
+        w.close()

@@ -88,17 +88,14 @@ def clear_ready(env: NodeEnv, steps=READY_FILES) -> None:
 
 
 def wait_ready(env: NodeEnv, step: str, timeout: float = 600.0, stop: threading.Event | None = None) -> dict:
-    deadline = time.monotonic() + timeout
-    for delay in env.waits():
-        d = read_ready(env, step)
-        if d is not None:
-            return d
-        if time.monotonic() >= deadline:
-            raise StepFailed(f"timed out waiting for {READY_FILES[step]}")
-        if stop is not None and stop.wait(delay):
-            raise StepFailed("stopped")
-        if stop is None:
-            time.sleep(delay)
+    from ..utils.fswait import wait_for_file
+
+    path = env.validation_file(READY_FILES[step])
+    if wait_for_file(path, timeout, stop, env.poll_s, check=lambda p: read_ready(env, step) is not None):
+        return read_ready(env, step)
+    if stop is not None and stop.is_set():
+        raise StepFailed("stopped")
+    raise StepFailed(f"timed out waiting for {READY_FILES[step]}")
 
 
 # -------------------------------------------------------------------- steps --
@@ -283,6 +280,14 @@ def allocatable(node: dict, resource: str) -> int:
         return 0
 
 
+# The plugin-validation pod proves its allocated GPU runs a kernel from inside
+# a container; its few small copies go through blit kernels instead of the
+# SDMA engines, whose first use costs a fresh process ~8 ms of queue set-up
+# (tools/plugin_pod_probe.sh, profiles/r2_ttr/plugin_pod_probe.txt).  The
+# node's workload validation keeps SDMA on, so the copy engines are exercised.
+PLUGIN_POD_ENV = [{"name": "HSA_ENABLE_SDMA", "value": "0"}]
+
+
 def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: float, stop) -> str | None:
     """Wait until the kubelet's device manager holds ``expect`` devices of
     ``resource`` (pod-resources ``GetAllocatableResources``,
@@ -359,7 +364,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                 "restartPolicy": "Never",
                 "tolerations": [{"key": resource, "operator": "Exists", "effect": "NoSchedule"}],
                 "containers": [{"name": "workload", "image": image, "imagePullPolicy": pull_policy,
-                                "command": ["amdgpu-validator"], "args": pod_args,
+                                "command": ["amdgpu-validator"], "args": pod_args, "env": PLUGIN_POD_ENV,
                                 "resources": {"limits": {resource: "1"}, "requests": {resource: "1"}}}],
             },
         }

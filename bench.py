@@ -131,16 +131,20 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
             for s in r.get("steps", []):
                 steps.setdefault(s["name"], []).append(s)
         timeline = {}  # seconds after ClusterPolicy creation at which each ready file was written
+        step_seconds = {}  # each step's own duration as its operand reported it
         for step in ("driver", "toolkit", "workload", "plugin", "complete"):
             r = read_ready(nd.env, step) or {}
             if "time" in r:
                 timeline[step] = round(r["time"] - t0_wall, 4)
+            if isinstance(r.get("seconds"), (int, float)):
+                step_seconds[step] = round(r["seconds"], 4)
         return {
             "time_to_ready_s": ttr,
             "allocatable_visible_s": alloc_visible,
             "allocatable_source": plug.get("allocatable_source"),
             "trace": cluster.trace_since(t0),
             "timeline_s": timeline,
+            "step_seconds": step_seconds,
             "wall_s": t_total,
             "allocatable": alloc,
             "policy_state_seconds": (cp.get("status") or {}).get("stateReadySeconds"),

@@ -232,6 +232,7 @@ struct Args {
   int gemm_n = 4096;
   int gemm_iters = 3;
   long long hbm_bytes = 1ll << 30;
+  long long vecadd_elems = 1ll << 24;  // K1 size; plugin-validation pods only prove device access (1 Mi)
   long long rccl_elems = 1ll << 24;
   long long xgmi_elems = 1ll << 22;
   int emulated_peers = 8;
@@ -333,10 +334,11 @@ Step step_hip(const Args& a, hipDeviceProp_t* prop) {
   return s;
 }
 
-Step step_vecadd(const Args&, hipStream_t st) {
+Step step_vecadd(const Args& args, hipStream_t st) {
   auto t0 = Clock::now();
   Step s{"vecadd"};
-  const int64_t n = 1 << 24;
+  const int64_t n = args.vecadd_elems;
+  if (n < (1 << 16) || n > (1ll << 30)) throw std::runtime_error("--vecadd-elems must be in [65536, 2^30]");
   float *a, *b, *c;
   HIP_OK(hipMalloc(&a, n * 4));
   HIP_OK(hipMalloc(&b, n * 4));
@@ -828,7 +830,7 @@ bool has_step(const Args& a, const char* name) {
 void usage(const char* p) {
   fprintf(stderr,
           "usage: %s [--device N] [--rank R --world W --rendezvous DIR --run-id ID] [--steps a,b,...]\n"
-          "          [--gemm N] [--gemm-iters K] [--hbm-bytes B] [--rccl-elems E] [--xgmi-elems E]\n"
+          "          [--gemm N] [--gemm-iters K] [--hbm-bytes B] [--vecadd-elems N] [--rccl-elems E] [--xgmi-elems E]\n"
           "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--rccl-destroy]\n"
           "          [--ready-file PATH] [--start-gate FILE] [--gate-mode aql|sdk]\n",
           p);
@@ -857,6 +859,7 @@ int main(int argc, char** argv) {
     else if (k == "--gemm") a.gemm_n = atoi(v());
     else if (k == "--gemm-iters") a.gemm_iters = atoi(v());
     else if (k == "--hbm-bytes") a.hbm_bytes = atoll(v());
+    else if (k == "--vecadd-elems") a.vecadd_elems = atoll(v());
     else if (k == "--rccl-elems") a.rccl_elems = atoll(v());
     else if (k == "--xgmi-elems") a.xgmi_elems = atoll(v());
     else if (k == "--emulated-peers") a.emulated_peers = atoi(v());
