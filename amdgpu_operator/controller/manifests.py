@@ -101,6 +101,9 @@ def _wait_init(name: str, image: str, pull: str, what: str, extra_args=(), env=N
 # the kubelet's pod-resources socket: the validator reads the device
 # manager's allocatable devices there (deviceplugin/podresources.py)
 POD_RESOURCES_MOUNT = {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources", "readOnly": True}
+# ...and watches the device-plugins directory, where the kubelet checkpoints
+# each device-list update (validate.py _wait_kubelet_devices)
+DEVICE_PLUGINS_MOUNT = {"name": "device-plugin", "mountPath": "/var/lib/kubelet/device-plugins", "readOnly": True}
 
 
 def _workload_pod_env(v, image: str) -> list[dict]:
@@ -318,7 +321,7 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         extra = ["--resource", spec.devicePlugin.resourceName, "--with-driver"] + \
             (["--wait-toolkit"] if spec.toolkit.enabled else [])
         inits = [_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args],
-                            env=_workload_pod_env(v, image), mounts=[POD_RESOURCES_MOUNT])]
+                            env=_workload_pod_env(v, image), mounts=[POD_RESOURCES_MOUNT, DEVICE_PLUGINS_MOUNT])]
     elif v.pluginValidation and spec.devicePlugin.enabled:  # (validation pods: _workload_pod_env)
         # workload (all GPUs, RCCL over xGMI) and plugin (1-GPU pods through the
         # device plugin + OCI hook) validation run concurrently.  The workload
@@ -327,7 +330,7 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         # wait for the toolkit inside the step.
         extra = ["--resource", spec.devicePlugin.resourceName] + (["--wait-toolkit"] if spec.toolkit.enabled else [])
         inits.append(_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args],
-                                env=_workload_pod_env(v, image), mounts=[POD_RESOURCES_MOUNT]))
+                                env=_workload_pod_env(v, image), mounts=[POD_RESOURCES_MOUNT, DEVICE_PLUGINS_MOUNT]))
     else:
         if spec.toolkit.enabled:
             inits.append(_wait_init("toolkit-validation", image, v.imagePullPolicy, "toolkit"))
@@ -337,7 +340,8 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
                      v.resources.model_dump())
     vols = [_hostpath("run-amd-validations", VALIDATIONS_HOST_DIR), _hostpath("host-sys", "/sys", "Directory")]
     if any(m["name"] == "pod-resources" for c in inits for m in c["volumeMounts"]):
-        vols.append(_hostpath("pod-resources", "/var/lib/kubelet/pod-resources"))
+        vols += [_hostpath("pod-resources", "/var/lib/kubelet/pod-resources"),
+                 _hostpath("device-plugin", "/var/lib/kubelet/device-plugins")]
     return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
             _daemonset(spec, ns, owner, name, "validator", sa, [ctr], inits, vols)]
 

@@ -19,6 +19,7 @@ It behaves like kubelet's device manager where the plugin can observe it:
 
 from __future__ import annotations
 
+import json
 import os
 import threading
 from concurrent import futures
@@ -91,6 +92,7 @@ class FakeKubelet:
                     res.numa = {d.ID: [n.ID for n in d.topology.nodes] for d in msg.devices}
                     res.updates += 1
                     res.cv.notify_all()
+                self._write_checkpoint()
         except grpc.RpcError:
             pass  # plugin went away or channel closed
         with self._lock:
@@ -100,6 +102,25 @@ class FakeKubelet:
                 res.devices = {i: api.UNHEALTHY for i in res.devices}
                 res.updates += 1
                 res.cv.notify_all()
+
+    CHECKPOINT = "kubelet_internal_checkpoint"
+
+    def _write_checkpoint(self) -> None:
+        """Like the kubelet's device manager: every device-list update and
+        allocation is checkpointed in the device-plugins directory (temp file
+        + rename), which is what a watcher of that directory sees."""
+        with self._lock:
+            data = {"RegisteredDevices": {r: list(res.devices) for r, res in self.resources.items()},
+                    "PodDeviceEntries": [{"PodUID": f"{k[0]}/{k[1]}", "ContainerName": k[2], "ResourceName": v[0],
+                                          "DeviceIDs": list(v[1])} for k, v in self.assignments.items()]}
+        path = os.path.join(self.dir, self.CHECKPOINT)
+        tmp = f"{path}.tmp.{threading.get_ident()}"
+        try:
+            with open(tmp, "w") as f:
+                json.dump({"Data": data}, f)
+            os.replace(tmp, path)
+        except OSError:
+            pass
 
     # -------------------------------------------------------------- lifecycle
     def start(self) -> None:
@@ -255,6 +276,7 @@ class FakeKubelet:
         out = call(r, timeout=5)
         with self._lock:
             self.assignments[(namespace, pod, container)] = (resource, ids)
+        self._write_checkpoint()
         return ids, out.container_responses[0]
 
     def release(self, namespace: str, pod: str) -> None:

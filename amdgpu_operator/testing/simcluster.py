@@ -650,6 +650,12 @@ class SimCluster:
             proc_env.update(container_device_env(node.env.sysfs_root(), devices))
         res = node.env.launch(argv, proc_env, device=dev, timeout=600)
         self.trace("gpu-pod-reported", run.name)
+        try:  # the process's own step times, for the bring-up breakdown
+            rep = json.loads(res.stdout.strip().splitlines()[-1])
+            steps = " ".join(f"{x['name']}={x.get('seconds', 0):.4f}" for x in rep.get("steps", []))
+            self.trace("gpu-pod-steps", f"{run.name} total={rep.get('seconds', 0):.4f} {steps}")
+        except (ValueError, IndexError, KeyError, TypeError):
+            pass
         if res.rc != 0:
             raise RuntimeError(f"workload failed rc={res.rc}: {res.stderr.strip()[-500:]} {res.stdout.strip()[-500:]}")
 

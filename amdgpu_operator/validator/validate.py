@@ -295,11 +295,18 @@ def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: fl
     is not reachable (the caller falls back to ``Node.status``)."""
     from ..deviceplugin.podresources import KubeletDevices
 
+    from ..utils.fswait import DirWatch
+
     kd = KubeletDevices(env.pod_resources_socket)
     if not kd.available():
         return None
+    # the kubelet checkpoints every device-list update into the device-plugins
+    # directory (and the plugin's socket appears there first): an inotify event
+    # there restarts the fast polling, so registration is seen within ~1 ms
+    w = DirWatch(env.device_plugin_dir) if os.path.isdir(env.device_plugin_dir) else None
     try:
-        for delay in env.waits():
+        waits = env.waits()
+        while True:
             n = kd.count(resource)
             if n is None:
                 return None
@@ -307,13 +314,20 @@ def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: fl
                 return "kubelet"
             if time.monotonic() >= deadline:
                 raise StepFailed(f"kubelet holds {n} {resource} devices, expected {expect}")
-            if stop is not None and stop.wait(delay):
+            if stop is not None and stop.is_set():
                 raise StepFailed("stopped")
-            if stop is None:
+            delay = next(waits)
+            if w is not None and w.active:
+                if w.wait(delay):
+                    waits = env.waits(first_s=0.0005)
+            elif stop is not None:
+                stop.wait(delay)
+            else:
                 time.sleep(delay)
     finally:
         kd.close()
-    return None
+        if w is not None:
+            w.close()
 
 
 def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | None = None,

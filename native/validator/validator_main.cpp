@@ -241,6 +241,7 @@ struct Args {
   double timeout_s = 120;
   bool counter_gate = false;
   bool any_arch = false;
+  bool null_stream = false;   // run the steps on the legacy null stream instead of a created one
   bool rccl_destroy = false;  // ncclCommDestroy before exit (default: barrier + exit, see step_rccl)
   std::string ready_file;
 };
@@ -860,6 +861,7 @@ int main(int argc, char** argv) {
     else if (k == "--gemm-iters") a.gemm_iters = atoi(v());
     else if (k == "--hbm-bytes") a.hbm_bytes = atoll(v());
     else if (k == "--vecadd-elems") a.vecadd_elems = atoll(v());
+    else if (k == "--null-stream") a.null_stream = true;
     else if (k == "--rccl-elems") a.rccl_elems = atoll(v());
     else if (k == "--xgmi-elems") a.xgmi_elems = atoll(v());
     else if (k == "--emulated-peers") a.emulated_peers = atoi(v());
@@ -909,6 +911,7 @@ int main(int argc, char** argv) {
   // nothing here has touched the GPU yet (kfd_open_at_gate reports whether
   // the runtime opened /dev/kfd early, which would make the pre-spawn unsafe).
   double gate_wait_s = -1;
+  double stream_create_s = -1;
   bool kfd_early = false;
   if (!a.start_gate.empty()) {
     auto tg = Clock::now();
@@ -942,7 +945,9 @@ int main(int argc, char** argv) {
     ok = steps.back().ok;
     if (ok && has_step(a, "rccl") && rccl_state.error.empty())
       rccl_thread = std::thread(rccl_init, std::cref(a), std::cref(rv), &rccl_state);
-    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const auto ts = Clock::now();
+    if (!a.null_stream) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    stream_create_s = secs(ts);
     if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
     if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st)), steps.back().ok);
     if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
@@ -958,6 +963,7 @@ int main(int argc, char** argv) {
   const double total = secs(t_start);
   std::string out = fmt("{\"ok\": %s, \"rank\": %d, \"world\": %d, \"device\": %d, \"seconds\": %.4f, ", ok ? "true" : "false",
                         a.rank, a.world, a.device, total);
+  if (stream_create_s >= 0) out += fmt("\"stream_create_s\": %.4f, ", stream_create_s);
   if (gate_wait_s >= 0)
     out += fmt("\"start_gate\": {\"wait_s\": %.4f, \"kfd_open_at_gate\": %s, \"steps_s\": %.4f}, ", gate_wait_s,
                kfd_early ? "true" : "false", total - gate_wait_s);
