@@ -302,7 +302,8 @@ def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: fl
         return None
     # the kubelet checkpoints every device-list update into the device-plugins
     # directory (and the plugin's socket appears there first): an inotify event
-    # there restarts the fast polling, so registration is seen within ~1 ms
+    # there triggers a look at once, so registration is seen within ~1 ms
+    # instead of at the next backed-off poll
     w = DirWatch(env.device_plugin_dir) if os.path.isdir(env.device_plugin_dir) else None
     try:
         waits = env.waits()
@@ -318,8 +319,7 @@ def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: fl
                 raise StepFailed("stopped")
             delay = next(waits)
             if w is not None and w.active:
-                if w.wait(delay):
-                    waits = env.waits(first_s=0.0005)
+                w.wait(delay)  # an event (checkpoint written, socket created) means: look now
             elif stop is not None:
                 stop.wait(delay)
             else:
@@ -364,6 +364,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
             raise StepFailed(f"allocatable {resource}={allocatable(nodes.get(env.node_name) or {}, resource)}, "
                              f"expected {expect}")
     t_alloc = time.perf_counter() - t0
+    marks = {"start": time.time() - (time.perf_counter() - t0), "devices_seen": time.time()}
     run_id = uuid.uuid4().hex[:8]
     pod_args = list(pod_args or ["--steps", "hip,vecadd,gemm", "--gemm", "1024"])
     names = []
@@ -386,6 +387,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
             pod["spec"]["imagePullSecrets"] = [{"name": x} for x in pull_secrets]
         env.client.create(pod)
         names.append(name)
+    marks["pods_created"] = time.time()
 
     def phase(o):
         return (o.get("status") or {}).get("phase", "Pending")
@@ -405,7 +407,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     if not all(p == "Succeeded" for p in phases.values()):
         raise StepFailed(f"plugin validation pods did not succeed: {phases}")
     summary = {"ok": True, "pods": expect, "devices": devices, "allocatable_wait_s": round(t_alloc, 4),
-               "allocatable_source": source,
+               "allocatable_source": source, "marks": {k: round(v, 4) for k, v in marks.items()},
                "seconds": time.perf_counter() - t0}
     write_ready(env, "plugin", summary)
     return summary

@@ -138,6 +138,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
                 timeline[step] = round(r["time"] - t0_wall, 4)
             if isinstance(r.get("seconds"), (int, float)):
                 step_seconds[step] = round(r["seconds"], 4)
+            for k, v in (r.get("marks") or {}).items():  # wall-clock marks inside a step
+                timeline[f"{step}.{k}"] = round(v - t0_wall, 4)
         return {
             "time_to_ready_s": ttr,
             "allocatable_visible_s": alloc_visible,
