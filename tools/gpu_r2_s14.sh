@@ -2,7 +2,7 @@
 # Round 2: GPU tier + bench at production settings after the inotify / SDMA changes
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r2s14
+O=$R/gpurun_out/${TAG:-r2s14}
 mkdir -p $O
 cd $R
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > $O/gpu_tests.log 2>&1
