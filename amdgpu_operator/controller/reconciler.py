@@ -370,19 +370,39 @@ class ClusterPolicyReconciler:
             log.warning("status update failed: %s", e)
 
     # ------------------------------------------------------------------- loop
+    def cached_kinds(self) -> list[tuple]:
+        """What the loop reads through informer caches (kube/informer.py):
+        (api_version, kind, namespace, triggers a reconcile)."""
+        ns = self.namespace
+        return [(CP_API, "ClusterPolicy", None, True), ("v1", "Node", None, True), ("apps/v1", "DaemonSet", ns, True),
+                (CP_API, "AMDGPUDriver", None, True), ("v1", "Namespace", None, False),
+                ("v1", "ServiceAccount", ns, False), ("v1", "Service", ns, False),
+                ("rbac.authorization.k8s.io/v1", "ClusterRole", None, False),
+                ("rbac.authorization.k8s.io/v1", "ClusterRoleBinding", None, False),
+                ("node.k8s.io/v1", "RuntimeClass", None, False),
+                ("monitoring.coreos.com/v1", "ServiceMonitor", ns, False)]
+
     def run(self, stop: threading.Event, resync_s: float = 30.0, debounce_s: float = 0.02,
-            on_result=None) -> None:
-        """Watch-driven loop: ClusterPolicy, Node, DaemonSet and Pod events in the
-        operand namespace trigger a (debounced) reconcile; plus periodic resync."""
+            on_result=None, cache: bool = True) -> None:
+        """Watch-driven loop: ClusterPolicy, Node, DaemonSet (operand
+        namespace) and AMDGPUDriver changes trigger a (debounced) reconcile;
+        plus periodic resync.  With ``cache`` the loop reads the objects it
+        owns from informer caches kept by the same watches (a pass then makes
+        no GETs) and writes through to the server."""
         events: queue.Queue = queue.Queue()
-        watches = [(CP_API, "ClusterPolicy", None), ("v1", "Node", None), ("apps/v1", "DaemonSet", self.namespace),
-                   (CP_API, "AMDGPUDriver", None)]
-        threads = []
-        for av, kind, ns in watches:
-            th = threading.Thread(target=self._pump, args=(av, kind, ns, events, stop), daemon=True,
-                                  name=f"operator-watch-{kind}")
-            th.start()
-            threads.append(th)
+        if cache:
+            from ..kube.informer import CachedClient
+
+            server = self.client
+            # reads of a kind go to the server until its informer has synced,
+            # so the first pass does not wait for the initial lists
+            self.client = CachedClient(server, self.cached_kinds(), stop, on_event=events.put)
+        else:
+            watches = [(CP_API, "ClusterPolicy", None), ("v1", "Node", None), ("apps/v1", "DaemonSet", self.namespace),
+                       (CP_API, "AMDGPUDriver", None)]
+            for av, kind, ns in watches:
+                threading.Thread(target=self._pump, args=(av, kind, ns, events, stop), daemon=True,
+                                 name=f"operator-watch-{kind}").start()
         events.put("start")
         last = 0.0
         while not stop.is_set():

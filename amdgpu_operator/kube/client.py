@@ -210,7 +210,9 @@ class RestClient:
         with self.session.get(self._url(t, namespace, query=q), stream=True,
                               timeout=(self.timeout, None)) as r:
             _raise_for(r)
-            for line in r.iter_lines():
+            # chunk_size=None: hand over each chunk as it arrives (the default
+            # 512-byte reads hold a small event until more bytes follow)
+            for line in r.iter_lines(chunk_size=None):
                 if stop is not None and stop.is_set():
                     return
                 if not line:
@@ -326,13 +328,14 @@ def apply_object(client, obj: dict, field_owner: str = "amd-gpu-operator",
     ann.setdefault("amd.com/managed-by", field_owner)
     ann["amd.com/last-applied-hash"] = want = R.spec_hash(obj)
     key = (t.api_version, t.kind, R.ns_of(obj), R.name_of(obj))
+    server = client.uncached() if hasattr(client, "uncached") else client  # past a read cache (kube/informer.py)
     try:
         cur = client.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
     except NotFound:
         try:
             return client.create(obj), "created"
-        except AlreadyExists:
-            cur = client.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
+        except AlreadyExists:  # created meanwhile by someone else: the cache may not have it yet
+            cur = server.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
     rv = (cur.get("metadata") or {}).get("resourceVersion")
     if verified is not None and rv and verified.get(key) == (rv, want):
         return cur, "unchanged"
@@ -348,7 +351,7 @@ def apply_object(client, obj: dict, field_owner: str = "amd-gpu-operator",
             obj["metadata"][k] = cur["metadata"][k]
     try:
         return client.update(obj), "updated"
-    except Conflict:
-        cur = client.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
+    except Conflict:  # our copy was stale: re-read from the server, not from a cache
+        cur = server.get(t.api_version, t.kind, R.name_of(obj), R.ns_of(obj))
         obj["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
         return client.update(obj), "updated"

@@ -45,6 +45,9 @@ def _parse_path(path: str):
 class _Handler(BaseHTTPRequestHandler):
     server_version = "fake-kube-apiserver/0.1"
     protocol_version = "HTTP/1.1"
+    # headers and body go out in separate writes: with Nagle on, the body
+    # waits for the client's delayed ACK of the headers (~40 ms per request)
+    disable_nagle_algorithm = True
     api: FakeApiServer  # set on the subclass
 
     def log_message(self, fmt, *args):  # quiet

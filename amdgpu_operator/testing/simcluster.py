@@ -207,7 +207,7 @@ class SimCluster:
                  fake_gpu: bool = True, poll_s: float = 0.01, launcher=None,
                  termination_s: float | None = None, agent_poll_s: float | None = None,
                  node_status_s: float | None = None, operator_resync_s: float = 1.0,
-                 operator_debounce_s: float = 0.005):
+                 operator_debounce_s: float = 0.005, http_api: bool = False):
         """``termination_s``: model graceful pod deletion - a deleted pod stays
         Terminating (listed, with ``deletionTimestamp``) for that many seconds
         (capped by its own grace period) before its kubelet removes it.
@@ -215,7 +215,11 @@ class SimCluster:
         is the operands' own ``VALIDATION_POLL_S`` (default: ``poll_s``).
         ``node_status_s`` models the kubelet's ``nodeStatusUpdateFrequency``
         (10 s by default on a real kubelet): device-plugin capacity reaches
-        ``Node.status`` only on that tick (default: every ``poll_s``)."""
+        ``Node.status`` only on that tick (default: every ``poll_s``).
+        ``http_api``: the operator and every operand talk to the API server
+        through :class:`~..kube.client.RestClient` over HTTP (real REST paths,
+        chunked watches, merge-patch, gracePeriodSeconds), as in a cluster; the
+        simulated kubelet and DaemonSet controller stay in-process."""
         self.workdir = workdir
         self.termination_s = termination_s
         self.namespace = namespace
@@ -229,7 +233,15 @@ class SimCluster:
         self.api = FakeApiServer()
         self.api.graceful_pod_deletion = termination_s is not None
         self.api.hooks.append(self._trace_api)
-        self.client = LocalClient(self.api)
+        self.client = LocalClient(self.api)  # the simulated kubelets / controllers
+        self._http = None
+        self.agent_client = self.client  # what the operator and the operands use
+        if http_api:
+            from ..kube.client import RestClient
+            from ..kube.httpapi import HttpApiServer
+
+            self._http = HttpApiServer(self.api).start()
+            self.agent_client = RestClient(self._http.url)
         self.nodes: dict[str, SimNode] = {}
         self.stop_event = threading.Event()
         self._threads: list[threading.Thread] = []
@@ -272,7 +284,7 @@ class SimCluster:
         dp_dir = os.path.join(sockets, "device-plugins")
         podres = os.path.join(sockets, "pod-resources", "kubelet.sock")
         kubelet = FakeKubelet(dp_dir, podres)
-        env = NodeEnv(node_name=ns.name, client=self.client, host_root=root,
+        env = NodeEnv(node_name=ns.name, client=self.agent_client, host_root=root,
                       validations_dir=os.path.join(d, "validations"), device_plugin_dir=dp_dir,
                       pod_resources_socket=podres, cdi_dir=os.path.join(d, "cdi"),
                       containerd_config=os.path.join(d, "etc/containerd/config.toml"),
@@ -346,7 +358,7 @@ class SimCluster:
 
     def start_reconciler(self) -> ClusterPolicyReconciler:
         if self.reconciler is None:
-            self.reconciler = ClusterPolicyReconciler(self.client, self.namespace)
+            self.reconciler = ClusterPolicyReconciler(self.agent_client, self.namespace)
             self._spawn(lambda: self.reconciler.run(self.stop_event, resync_s=self.operator_resync_s,
                                                     debounce_s=self.operator_debounce_s),
                         "sim-operator")
@@ -365,6 +377,8 @@ class SimCluster:
             th.join(timeout=5)
         for d in self._short_dirs:
             shutil.rmtree(d, ignore_errors=True)
+        if self._http is not None:
+            self._http.stop()
 
     # --------------------------------------------------- DaemonSet controller
     def _template_hash(self, ds: dict) -> str:

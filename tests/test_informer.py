@@ -1,0 +1,138 @@
+"""kube/informer.py: watch-backed read caches for the operator loop."""
+
+import threading
+import time
+
+import pytest
+
+from amdgpu_operator.kube import resources as R
+from amdgpu_operator.kube.client import LocalClient, NotFound, RestClient, apply_object
+from amdgpu_operator.kube.fakeapi import FakeApiServer
+from amdgpu_operator.kube.httpapi import HttpApiServer
+from amdgpu_operator.kube.informer import CachedClient
+
+
+@pytest.fixture(params=["local", "rest"])
+def server(request):
+    api = FakeApiServer()
+    if request.param == "local":
+        yield api, LocalClient(api)
+        return
+    srv = HttpApiServer(api).start()
+    try:
+        yield api, RestClient(srv.url)
+    finally:
+        srv.stop()
+
+
+def until(cond, timeout=5.0):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if cond():
+            return True
+        time.sleep(0.005)
+    return False
+
+
+def test_reads_come_from_the_cache_and_follow_the_watch(server):
+    api, client = server
+    other = LocalClient(api)  # someone else writing
+    other.create(R.new("v1", "Namespace", "ns"))
+    other.create(R.new("v1", "Node", "a", labels={"gpu": "yes"}))
+    stop = threading.Event()
+    seen = []
+    c = CachedClient(client, [("v1", "Node", None, True), ("v1", "ServiceAccount", "ns")], stop, on_event=seen.append)
+    try:
+        assert c.wait_synced(5)
+        before = api.request_count
+        assert c.get("v1", "Node", "a")["metadata"]["labels"] == {"gpu": "yes"}
+        assert [n["metadata"]["name"] for n in c.list("v1", "Node", label_selector="gpu=yes")] == ["a"]
+        assert api.request_count == before  # no server round trip
+        other.patch("v1", "Node", "a", {"metadata": {"labels": {"gpu": "no"}}})
+        assert until(lambda: c.get("v1", "Node", "a")["metadata"]["labels"]["gpu"] == "no")
+        assert "Node" in seen
+        other.delete("v1", "Node", "a")
+        assert until(lambda: not c.list("v1", "Node"))
+        with pytest.raises(NotFound):
+            c.get("v1", "Node", "a")
+        # a namespaced kind outside the informer's namespace reads through
+        other.create(R.new("v1", "Namespace", "elsewhere"))
+        other.create(R.new("v1", "ServiceAccount", "sa", "elsewhere"))
+        assert c.get("v1", "ServiceAccount", "sa", "elsewhere")["metadata"]["name"] == "sa"
+    finally:
+        stop.set()
+
+
+def test_write_through_and_stale_events(server):
+    api, client = server
+    LocalClient(api).create(R.new("v1", "Namespace", "ns"))
+    stop = threading.Event()
+    c = CachedClient(client, [("v1", "ServiceAccount", "ns")], stop)
+    try:
+        assert c.wait_synced(5)
+        sa = c.create(R.new("v1", "ServiceAccount", "sa", "ns"))
+        assert c.get("v1", "ServiceAccount", "sa", "ns")["metadata"]["uid"] == sa["metadata"]["uid"]  # at once
+        inf = c.informers[("v1", "ServiceAccount")]
+        newer = c.patch("v1", "ServiceAccount", "sa", {"metadata": {"labels": {"v": "2"}}}, "ns")
+        inf.put(sa)  # an older event arriving late must not win
+        assert c.get("v1", "ServiceAccount", "sa", "ns")["metadata"]["resourceVersion"] == \
+            newer["metadata"]["resourceVersion"]
+        c.delete("v1", "ServiceAccount", "sa", "ns")
+        with pytest.raises(NotFound):
+            c.get("v1", "ServiceAccount", "sa", "ns")
+    finally:
+        stop.set()
+
+
+def test_apply_recovers_from_a_stale_cache():
+    api = FakeApiServer()
+    client = LocalClient(api)
+    client.create(R.new("v1", "Namespace", "ns"))
+    stop = threading.Event()
+    c = CachedClient(client, [("apps/v1", "DaemonSet", "ns")], stop)
+    try:
+        assert c.wait_synced(5)
+        ds = R.new("apps/v1", "DaemonSet", "d", "ns", spec={"template": {"spec": {"containers": [{"name": "x"}]}}})
+        assert apply_object(c, ds)[1] == "created"
+        # someone else changes the object; the cache is made stale on purpose
+        inf = c.informers[("apps/v1", "DaemonSet")]
+        stale = c.get("apps/v1", "DaemonSet", "d", "ns")
+        client.patch("apps/v1", "DaemonSet", "d", {"spec": {"template": {"spec": {"containers": [{"name": "y"}]}}}},
+                     "ns")
+        until(lambda: c.get("apps/v1", "DaemonSet", "d", "ns")["spec"]["template"]["spec"]["containers"][0]["name"]
+              == "y")
+        with inf._lock:  # roll the cache back to the stale copy
+            import pickle
+
+            inf._store[("ns", "d")] = pickle.dumps(stale)
+            inf._rvs[("ns", "d")] = int(stale["metadata"]["resourceVersion"])
+        want = R.deep(ds)
+        want["spec"]["template"]["spec"]["containers"][0]["name"] = "z"
+        # stale resourceVersion -> Conflict -> re-read from the server (not the cache) -> update
+        assert apply_object(c, want)[1] == "updated"
+        assert client.get("apps/v1", "DaemonSet", "d", "ns")["spec"]["template"]["spec"]["containers"][0]["name"] == "z"
+    finally:
+        stop.set()
+
+
+def test_kind_the_server_does_not_serve_reads_through():
+    """An informer whose list 404s (a CRD that is not installed) gives up and
+    reads go to the server."""
+    from amdgpu_operator.kube.fakeapi import ApiError
+
+    class NoMonitors(LocalClient):
+        def list_rv(self, api_version, kind, *a, **kw):
+            if kind == "ServiceMonitor":
+                raise ApiError(404, "NotFound", "the server could not find the requested resource")
+            return super().list_rv(api_version, kind, *a, **kw)
+
+    api = FakeApiServer()
+    stop = threading.Event()
+    c = CachedClient(NoMonitors(api), [("monitoring.coreos.com/v1", "ServiceMonitor", "ns")], stop)
+    try:
+        assert c.wait_synced(5)
+        assert c.informers[("monitoring.coreos.com/v1", "ServiceMonitor")].failed.is_set()
+        with pytest.raises(NotFound):
+            c.get("monitoring.coreos.com/v1", "ServiceMonitor", "m", "ns")
+    finally:
+        stop.set()

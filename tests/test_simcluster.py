@@ -216,3 +216,19 @@ def test_kubelet_devices_client(tmp_path):
     finally:
         m.stop()
         k.stop()
+
+
+def test_bring_up_over_http_rest_client(cluster_factory):
+    """The operator and every operand use the production RestClient against
+    the API server's HTTP front end: REST paths, chunked watches (list-then-
+    watch waits included), merge-patch, status subresource, graceful deletes."""
+    from amdgpu_operator.kube.client import RestClient
+
+    c = cluster_factory([NodeSpec("gpu-1", 2), NodeSpec("cpu-1", 0)], http_api=True, termination_s=0.2)
+    assert isinstance(c.agent_client, RestClient)
+    c.install_operator(REF)
+    c.wait_ready(60, {"gpu-1": 2})
+    assert labels(c, "gpu-1").get("amd.com/gpu.validated") == "true"
+    assert "amd.com/gpu.present" not in labels(c, "cpu-1")
+    rep = verify(c.agent_client, c.namespace, expect_gpus_per_node=2)
+    assert rep.ok, rep.as_dict()
