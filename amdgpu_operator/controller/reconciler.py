@@ -390,12 +390,14 @@ class ClusterPolicyReconciler:
         owns from informer caches kept by the same watches (a pass then makes
         no GETs) and writes through to the server."""
         events: queue.Queue = queue.Queue()
+        server = self.client
         if cache:
             from ..kube.informer import CachedClient
 
-            server = self.client
             # reads of a kind go to the server until its informer has synced,
-            # so the first pass does not wait for the initial lists
+            # so the first pass does not wait for the initial lists; the
+            # informers end with ``stop`` (e.g. leadership lost), and so does
+            # this wrapping: a later run() builds fresh caches
             self.client = CachedClient(server, self.cached_kinds(), stop, on_event=events.put)
         else:
             watches = [(CP_API, "ClusterPolicy", None), ("v1", "Node", None), ("apps/v1", "DaemonSet", self.namespace),
@@ -404,6 +406,12 @@ class ClusterPolicyReconciler:
                 threading.Thread(target=self._pump, args=(av, kind, ns, events, stop), daemon=True,
                                  name=f"operator-watch-{kind}").start()
         events.put("start")
+        try:
+            self._loop(stop, events, resync_s, debounce_s, on_result)
+        finally:
+            self.client = server
+
+    def _loop(self, stop, events, resync_s, debounce_s, on_result) -> None:
         last = 0.0
         while not stop.is_set():
             try:

@@ -136,3 +136,31 @@ def test_kind_the_server_does_not_serve_reads_through():
             c.get("monitoring.coreos.com/v1", "ServiceMonitor", "m", "ns")
     finally:
         stop.set()
+
+
+def test_reconciler_loop_rebuilds_its_caches_per_run():
+    """Leadership lost and regained: run() ends (its informers stop with it)
+    and a later run() must not read from the stopped caches."""
+    from amdgpu_operator.api.clusterpolicy import cluster_policy, spec_from_values
+    from amdgpu_operator.controller.reconciler import ClusterPolicyReconciler
+    from amdgpu_operator.helm.render import load_crd
+    from amdgpu_operator.kube.informer import CachedClient
+
+    api = FakeApiServer()
+    client = LocalClient(api)
+    client.create(load_crd())
+    client.create(R.new("v1", "Namespace", "gpu-operator-resources"))  # helm --create-namespace
+    client.create(cluster_policy("cluster-policy", spec_from_values({})))
+    rec = ClusterPolicyReconciler(client, "gpu-operator-resources")
+    for _ in range(2):
+        stop = threading.Event()
+        seen = []
+        th = threading.Thread(target=rec.run, args=(stop,), kwargs={"resync_s": 0.2, "on_result": seen.append},
+                              daemon=True)
+        th.start()
+        assert until(lambda: len(seen) >= 2)
+        assert isinstance(rec.client, CachedClient)
+        stop.set()
+        th.join(5)
+        assert rec.client is client
+    assert client.list("apps/v1", "DaemonSet", "gpu-operator-resources")  # the operands were applied

@@ -65,7 +65,7 @@ def bring_up(n_nodes: int, timeout: float) -> dict:
     work = tempfile.mkdtemp(prefix="fleet-")
     nodes = [NodeSpec(f"n{i:03d}", gpus=8) for i in range(n_nodes)]
     cluster = SimCluster(work, nodes, fake_gpu=True, poll_s=0.01)
-    cluster.client = CountingClient(cluster.api)
+    cluster.client = cluster.agent_client = CountingClient(cluster.api)
     cluster.start()
     try:
         cluster.client.reset()
