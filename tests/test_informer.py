@@ -164,3 +164,28 @@ def test_reconciler_loop_rebuilds_its_caches_per_run():
         th.join(5)
         assert rec.client is client
     assert client.list("apps/v1", "DaemonSet", "gpu-operator-resources")  # the operands were applied
+
+
+def test_informer_survives_an_api_server_restart():
+    """kube-apiserver restarts (upgrades, failover) end every watch: the
+    informer relists and keeps following changes made meanwhile."""
+    api = FakeApiServer()
+    srv = HttpApiServer(api).start()
+    port = srv.httpd.server_address[1]
+    client = RestClient(srv.url, timeout=2.0)
+    local = LocalClient(api)
+    local.create(R.new("v1", "Node", "a"))
+    stop = threading.Event()
+    c = CachedClient(client, [("v1", "Node", None, True)], stop)
+    try:
+        assert c.wait_synced(5)
+        srv.stop()
+        local.create(R.new("v1", "Node", "b"))  # changes while the server is away
+        local.delete("v1", "Node", "a")
+        srv = HttpApiServer(api, port=port).start()
+        assert until(lambda: [n["metadata"]["name"] for n in c.list("v1", "Node")] == ["b"], timeout=10)
+        local.create(R.new("v1", "Node", "c"))
+        assert until(lambda: len(c.list("v1", "Node")) == 2, timeout=5)
+    finally:
+        stop.set()
+        srv.stop()
