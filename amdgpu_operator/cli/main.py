@@ -121,6 +121,9 @@ def main(argv: list[str] | None = None) -> int:
     sm.add_argument("--set", action="append", default=[])
     sm.add_argument("--real-gpus", action="store_true", help="use this machine's GPUs and sysfs")
     sm.add_argument("--timeout", type=float, default=120)
+    sm.add_argument("--nodes", type=int, default=1, help="GPU nodes in the simulated cluster")
+    sm.add_argument("--http-api", action="store_true",
+                    help="operator and operands talk to the API server over HTTP (RestClient), as in a cluster")
     pf = sub.add_parser("preflight", help="check (and --fix) a node's prerequisites before kubeadm join")
     pf.add_argument("--root", default="/")
     pf.add_argument("--fix", action="store_true")
@@ -199,13 +202,17 @@ def main(argv: list[str] | None = None) -> int:
         from .verify import verify
 
         d = tempfile.mkdtemp(prefix="amdgpu-sim-")
-        node = NodeSpec("node-0", args.gpus, args.partition, sysfs_root="/" if args.real_gpus else None)
-        c = SimCluster(d, [node], fake_gpu=not args.real_gpus).start()
+        if args.real_gpus and args.nodes != 1:
+            raise SystemExit("--real-gpus simulates one node (this machine)")
+        nodes = [NodeSpec(f"node-{i}", args.gpus, args.partition, sysfs_root="/" if args.real_gpus else None)
+                 for i in range(args.nodes)]
+        c = SimCluster(d, nodes, fake_gpu=not args.real_gpus, http_api=args.http_api).start()
         try:
             c.install_operator(parse_set_flags(args.set))
             ttr = c.wait_ready(args.timeout)
-            rep = verify(c.client, c.namespace)
-            print(json.dumps({"time_to_ready_s": round(ttr, 4), "verify": rep.as_dict()}, indent=1))
+            rep = verify(c.agent_client, c.namespace)
+            print(json.dumps({"time_to_ready_s": round(ttr, 4), "nodes": args.nodes, "http_api": args.http_api,
+                              "verify": rep.as_dict()}, indent=1))
             return 0 if rep.ok else 1
         finally:
             c.stop()

@@ -474,3 +474,11 @@ def test_driver_change_aborts_waiting_start_gates(env):
     out = DM.prepare_upgrade(env, "9.9.9", drain_timeout=0.1)
     assert out["unloaded"]
     assert open(waiting).read() == "abort" and open(released).read() == "go"
+
+
+def test_cli_simulate_two_nodes_over_http(capsys):
+    from amdgpu_operator.cli.main import main
+
+    assert main(["simulate", "--gpus", "2", "--nodes", "2", "--http-api", "--timeout", "90"]) == 0
+    out = json.loads(capsys.readouterr().out)
+    assert out["nodes"] == 2 and out["http_api"] and out["verify"]["ok"]
