@@ -32,6 +32,28 @@ class KubeletDevices:
     def available(self) -> bool:
         return os.path.exists(self.socket_path)
 
+    def connect(self, timeout: float = 2.0) -> bool:
+        """Open the channel ahead of the first query (a fresh gRPC channel's
+        connect costs milliseconds that would otherwise land on the first
+        poll after the device plugin registers)."""
+        if not self.available():
+            return False
+        try:
+            self._channel()
+            grpc.channel_ready_future(self._ch).result(timeout=timeout)
+            return True
+        except (grpc.FutureTimeoutError, grpc.RpcError):
+            return False
+
+    def _channel(self):
+        if self._call is None:
+            req, resp, _ = api.POD_RESOURCES_METHODS["GetAllocatableResources"]
+            self._ch = grpc.insecure_channel("unix:" + self.socket_path)
+            self._call = self._ch.unary_unary(
+                api.method_path(api.POD_RESOURCES_SERVICE, "GetAllocatableResources"),
+                request_serializer=req.SerializeToString, response_deserializer=resp.FromString)
+        return self._call
+
     def allocatable(self, timeout: float = 2.0) -> dict[str, list[str]] | None:
         """resource name -> device IDs the kubelet can allocate, or None when
         the API is not reachable (no socket, kubelet < 1.23 without the
@@ -39,14 +61,9 @@ class KubeletDevices:
         if not self.available():
             return None
         try:
-            if self._call is None:
-                req, resp, _ = api.POD_RESOURCES_METHODS["GetAllocatableResources"]
-                self._ch = grpc.insecure_channel("unix:" + self.socket_path)
-                self._call = self._ch.unary_unary(
-                    api.method_path(api.POD_RESOURCES_SERVICE, "GetAllocatableResources"),
-                    request_serializer=req.SerializeToString, response_deserializer=resp.FromString)
+            call = self._channel()
             req = api.POD_RESOURCES_METHODS["GetAllocatableResources"][0]
-            out = self._call(req(), timeout=timeout)
+            out = call(req(), timeout=timeout)
         except grpc.RpcError:
             self.close()
             return None

@@ -288,7 +288,8 @@ def allocatable(node: dict, resource: str) -> int:
 PLUGIN_POD_ENV = [{"name": "HSA_ENABLE_SDMA", "value": "0"}]
 
 
-def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: float, stop) -> str | None:
+def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: float, stop,
+                          kd=None) -> str | None:
     """Wait until the kubelet's device manager holds ``expect`` devices of
     ``resource`` (pod-resources ``GetAllocatableResources``,
     deviceplugin/podresources.py).  Returns "kubelet", or None when that API
@@ -297,7 +298,7 @@ def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: fl
 
     from ..utils.fswait import DirWatch
 
-    kd = KubeletDevices(env.pod_resources_socket)
+    kd = kd or KubeletDevices(env.pod_resources_socket)
     if not kd.available():
         return None
     # the kubelet checkpoints every device-list update into the device-plugins
@@ -333,7 +334,7 @@ def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: fl
 def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | None = None,
                     pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                     image: str | None = None, pull_policy: str = "IfNotPresent",
-                    pull_secrets: list[str] | None = None) -> dict:
+                    pull_secrets: list[str] | None = None, kubelet=None) -> dict:
     """Wait until the kubelet holds one device per GPU, then run one 1-GPU
     pod per device.
 
@@ -351,7 +352,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     if expect is None:
         expect = len(topology.enumerate_gpus(env.sysfs_root()))
     deadline = time.monotonic() + timeout
-    source = _wait_kubelet_devices(env, resource, expect, deadline, stop)
+    source = _wait_kubelet_devices(env, resource, expect, deadline, stop, kubelet)
     if source is None:  # no pod-resources API: wait for the kubelet to publish Node.status.allocatable
         source = "node-status"
         nodes, ok = wait_for(env.client, "v1", "Node",
@@ -523,6 +524,10 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
             errors.append(f"workload: {e}")
 
     def plugin():
+        from ..deviceplugin.podresources import KubeletDevices
+
+        kubelet = KubeletDevices(env.pod_resources_socket)
+        kubelet.connect()  # while the driver and toolkit are still being validated
         try:
             if with_driver:
                 driver_done.wait()
@@ -533,9 +538,12 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
             if os.environ.get("AMDGPU_EXPERIMENT_PLUGIN_AFTER_WORKLOAD"):  # start-up contention experiment
                 wait_ready(env, "workload", timeout, stop)
             if read_ready(env, "plugin") is None:
-                results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop)
+                results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop,
+                                                    kubelet=kubelet)
         except Exception as e:  # noqa: BLE001
             errors.append(f"plugin: {e}")
+        finally:
+            kubelet.close()
 
     threads = [threading.Thread(target=workload, name="validate-workload"),
                threading.Thread(target=plugin, name="validate-plugin")]
