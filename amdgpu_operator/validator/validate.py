@@ -526,8 +526,10 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
     def plugin():
         from ..deviceplugin.podresources import KubeletDevices
 
+        # the channel opens at the first query: connecting it up front
+        # (channel_ready_future) cost the bring-up 0.2 s on the MI355X box,
+        # interleaved A/B in profiles/r2_ttr/preconnect_ab.json
         kubelet = KubeletDevices(env.pod_resources_socket)
-        kubelet.connect()  # while the driver and toolkit are still being validated
         try:
             if with_driver:
                 driver_done.wait()
