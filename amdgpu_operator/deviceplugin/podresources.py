@@ -32,19 +32,6 @@ class KubeletDevices:
     def available(self) -> bool:
         return os.path.exists(self.socket_path)
 
-    def connect(self, timeout: float = 2.0) -> bool:
-        """Open the channel ahead of the first query.  Not used on the
-        validator's path: a channel connected early (channel_ready_future)
-        slowed the whole bring-up process by 0.2 s on the MI355X box."""
-        if not self.available():
-            return False
-        try:
-            self._channel()
-            grpc.channel_ready_future(self._ch).result(timeout=timeout)
-            return True
-        except (grpc.FutureTimeoutError, grpc.RpcError):
-            return False
-
     def _channel(self):
         if self._call is None:
             req, resp, _ = api.POD_RESOURCES_METHODS["GetAllocatableResources"]

@@ -527,8 +527,8 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
         from ..deviceplugin.podresources import KubeletDevices
 
         # the channel opens at the first query: connecting it up front
-        # (channel_ready_future) cost the bring-up 0.2 s on the MI355X box,
-        # interleaved A/B in profiles/r2_ttr/preconnect_ab.json
+        # (grpc.channel_ready_future) cost the bring-up 0.2 s on the MI355X
+        # box, interleaved A/B in profiles/r2_ttr/preconnect_ab.json
         kubelet = KubeletDevices(env.pod_resources_socket)
         try:
             if with_driver:
