@@ -17,7 +17,6 @@ import ctypes
 import ctypes.util
 import os
 import select
-import struct
 import threading
 import time
 
