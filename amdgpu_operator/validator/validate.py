@@ -143,18 +143,13 @@ def workload_argv(args: list[str], rank: int, world: int, rendezvous: str, run_i
 
 
 def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: float = 600.0,
-                      start_gate: str | None = None, hold_exit: str | None = None) -> dict:
+                      start_gate: str | None = None) -> dict:
     """One native validator process per GPU, all ranks in one RCCL communicator.
 
     ``start_gate``: a file the processes wait on before their first HIP call
     (``amdgpu-validator --start-gate``): "go" releases them, anything else
     aborts them.  The caller spawns them before the driver is validated and
-    writes the verdict afterwards (:func:`validate_gpu`).
-
-    ``hold_exit``: a file (empty) the processes wait on after their report
-    (``--hold-exit``); they exit once it has content or is removed, so the
-    kernel's teardown of their GPU state does not overlap the start of the
-    node's other GPU processes."""
+    writes the verdict afterwards (:func:`validate_gpu`)."""
     from ..discovery import topology
 
     t0 = time.perf_counter()
@@ -201,8 +196,6 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         argv = workload_argv(jargs, rank, world, rdv, rid, gpus[rank].index)
         if start_gate:
             argv += ["--start-gate", start_gate]
-        if hold_exit and REPORT_EARLY:  # only a caller that takes the report early can let them linger
-            argv += ["--hold-exit", hold_exit]
         return env.launch(argv, jenv, device=gpus[rank].index, timeout=timeout)
 
     with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
@@ -422,17 +415,6 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
 
 
 START_GATE_PREFIX = ".start-gate-"
-EXIT_HOLD_PREFIX = ".exit-hold-"
-# hold the workload processes' exit until the plugin pods are running
-# (AMDGPU_VALIDATOR_HOLD_EXIT=0 turns it off)
-HOLD_EXIT = os.environ.get("AMDGPU_VALIDATOR_HOLD_EXIT", "1") == "1"
-
-
-def release_file(path: str, verdict: str) -> None:
-    tmp = f"{path}.{verdict}.tmp"
-    with open(tmp, "w") as f:
-        f.write(verdict)
-    os.replace(tmp, path)
 
 
 def prespawn_safe(env: NodeEnv, sdk_gate: bool = False) -> bool:
@@ -470,12 +452,6 @@ def abort_start_gates(env: NodeEnv) -> list[str]:
     except FileNotFoundError:
         return out
     for name in names:
-        if name.startswith(EXIT_HOLD_PREFIX) and not name.endswith(".tmp"):
-            try:  # processes past their report, holding their exit: let them go (they hold /dev/kfd)
-                release_file(os.path.join(env.validations_dir, name), "exit")
-            except OSError:
-                pass
-            continue
         if not name.startswith(START_GATE_PREFIX) or name.endswith(".tmp"):
             continue
         path = os.path.join(env.validations_dir, name)
@@ -520,18 +496,6 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
         os.makedirs(env.validations_dir, exist_ok=True)
         gate = os.path.join(env.validations_dir, f"{START_GATE_PREFIX}{uuid.uuid4().hex[:12]}")
         open(gate, "w").close()  # empty = no verdict yet (driver/manager.py may abort it)
-    hold = None
-    if HOLD_EXIT and REPORT_EARLY:
-        os.makedirs(env.validations_dir, exist_ok=True)
-        hold = os.path.join(env.validations_dir, f"{EXIT_HOLD_PREFIX}{uuid.uuid4().hex[:12]}")
-        open(hold, "w").close()
-
-    def release_hold():
-        if hold:
-            try:
-                release_file(hold, "exit")
-            except OSError:
-                pass
 
     def driver():
         verdict = "abort"
@@ -555,8 +519,7 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
                 if "driver" not in results:
                     return
             if read_ready(env, "workload") is None:
-                results["workload"] = validate_workload(env, workload_args, timeout, start_gate=gate,
-                                                        hold_exit=hold)
+                results["workload"] = validate_workload(env, workload_args, timeout, start_gate=gate)
         except Exception as e:  # noqa: BLE001
             errors.append(f"workload: {e}")
 
@@ -583,7 +546,6 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
             errors.append(f"plugin: {e}")
         finally:
             kubelet.close()
-            release_hold()  # the plugin pods' processes are done: the workload processes may exit now
 
     threads = [threading.Thread(target=workload, name="validate-workload"),
                threading.Thread(target=plugin, name="validate-plugin")]
@@ -595,13 +557,11 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
         for th in threads:
             th.join()
     finally:
-        release_hold()
-        for path in (gate, hold):
-            if path:
-                try:
-                    os.unlink(path)
-                except FileNotFoundError:
-                    pass
+        if gate:
+            try:
+                os.unlink(gate)
+            except FileNotFoundError:
+                pass
     if errors:
         raise StepFailed("; ".join(errors))
     return {"ok": True, "seconds": time.perf_counter() - t0, **results}

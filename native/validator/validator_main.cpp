@@ -226,7 +226,6 @@ struct Args {
   int world = 1;
   std::string rendezvous = "/tmp/amdgpu-validator";
   std::string start_gate;  // file whose content ("go" / anything else) releases the first HIP call
-  std::string hold_exit;   // after the report: exit only once this file has content (or after 60 s)
   std::string gate_mode = "aql";  // counter gate: "aql" (AQL profiling packets) or "sdk" (rocprofiler-sdk tool)
   std::string run_id = "run";
   std::string steps = "hip,vecadd,gemm,mfma,hbm,xgmi,rccl";
@@ -863,7 +862,6 @@ int main(int argc, char** argv) {
     else if (k == "--hbm-bytes") a.hbm_bytes = atoll(v());
     else if (k == "--vecadd-elems") a.vecadd_elems = atoll(v());
     else if (k == "--null-stream") a.null_stream = true;
-    else if (k == "--hold-exit") a.hold_exit = v();
     else if (k == "--rccl-elems") a.rccl_elems = atoll(v());
     else if (k == "--xgmi-elems") a.xgmi_elems = atoll(v());
     else if (k == "--emulated-peers") a.emulated_peers = atoi(v());
@@ -1008,16 +1006,6 @@ int main(int argc, char** argv) {
     dup2(dn, 1);
     dup2(dn, 2);
     close(dn);
-  }
-  // --hold-exit: the kernel's teardown of this process (KFD queues, VM,
-  // device memory) delays the next process that opens /dev/kfd by up to
-  // ~0.14 s (flush_workqueue).  Hold the exit, report already out, until the
-  // caller has started its other GPU processes (the plugin-validation pods).
-  if (!a.hold_exit.empty()) {
-    const auto th = Clock::now();
-    std::string text;
-    // released by any content, or by the file's removal
-    while (secs(th) < 60.0 && read_small(a.hold_exit, &text) && text.empty()) usleep(2000);
   }
   _exit(ok ? 0 : 1);
 }

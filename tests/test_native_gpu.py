@@ -214,30 +214,3 @@ def test_must_gather_node_state_on_mi355x(tmp_path):
     node = gather_node("/", str(tmp_path))
     assert node["probe"]["ok"] and node["gpus"] and all(g["arch"] == "gfx950" for g in node["gpus"])
     assert node["metrics"] and node["metrics"][0]["vram_total_bytes"] > 280 * 2**30
-
-
-def test_validator_holds_its_exit_after_the_report(tmp_path):
-    """--hold-exit: the report (and EOF on stdout) comes first, the process
-    exits only once the hold file has content, so its GPU teardown can be
-    kept off other processes' start-up."""
-    import subprocess
-    import time
-
-    from amdgpu_operator import native
-
-    hold = tmp_path / "hold"
-    hold.write_text("")
-    p = subprocess.Popen([str(native.binary("amdgpu-validator")), "--rendezvous", str(tmp_path / "rv"), "--steps",
-                          "hip,vecadd", "--vecadd-elems", str(1 << 20), "--hold-exit", str(hold)],
-                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    try:
-        out = p.stdout.read()  # EOF: the report is out and stdout is closed
-        assert json.loads(out.strip().splitlines()[-1])["ok"] is True
-        time.sleep(0.3)
-        assert p.poll() is None  # still holding
-        hold.write_text("exit")
-        assert p.wait(timeout=10) == 0
-    finally:
-        if p.poll() is None:
-            p.kill()
-            p.wait(5)

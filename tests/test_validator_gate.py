@@ -35,18 +35,3 @@ def test_gate_times_out(tmp_path):
     p = subprocess.run([VALIDATOR, "--rendezvous", str(tmp_path / "rv"), "--steps", "hip", "--start-gate",
                         str(tmp_path / "never"), "--timeout", "0.2"], capture_output=True, text=True, timeout=30)
     assert p.returncode == 3 and "start gate: timeout" in p.stdout
-
-
-def test_driver_manager_releases_held_exits(tmp_path):
-    """A driver unload must not wait for validator processes holding their
-    exit (they keep /dev/kfd open): abort_start_gates releases them too."""
-    from amdgpu_operator.nodeenv import NodeEnv
-    from amdgpu_operator.validator import validate as V
-
-    env = NodeEnv("n", None, validations_dir=str(tmp_path))
-    hold = tmp_path / f"{V.EXIT_HOLD_PREFIX}abc"
-    hold.write_text("")
-    gate = tmp_path / f"{V.START_GATE_PREFIX}def"
-    gate.write_text("")
-    V.abort_start_gates(env)
-    assert hold.read_text() == "exit" and gate.read_text() == "abort"
