@@ -1,6 +1,6 @@
 #!/bin/bash
 # ncclCommInitRank cost of the validator's RCCL step (1 rank) under RCCL
-# settings that only matter off-node or for algorithm tables, interleaved,
+# settings (off-node, algorithm tables, buffer and FIFO sizes, channel count), interleaved,
 # 5 rounds: lib_load_s, comm_init_s and the process wall (ms)
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 V=amdgpu_operator/_native/amdgpu-validator
@@ -15,6 +15,8 @@ run() {
 for i in 1 2 3 4 5; do
   run base X=1
   run noib NCCL_IB_DISABLE=1
-  run noib_nomsccl NCCL_IB_DISABLE=1 RCCL_MSCCL_ENABLE=0 RCCL_MSCCLPP_ENABLE=0
-  run noib_nomsccl_nonet NCCL_IB_DISABLE=1 RCCL_MSCCL_ENABLE=0 RCCL_MSCCLPP_ENABLE=0 NCCL_NET_PLUGIN=none
+  run fifo4k NCCL_WORK_FIFO_DEPTH=4096
+  run buf1m NCCL_BUFFSIZE=1048576
+  run ch4 NCCL_MAX_NCHANNELS=4
+  run runtime_connect NCCL_RUNTIME_CONNECT=1
 done
