@@ -9,8 +9,10 @@ is ncclCommInitRank's kernel set-up: 1.56 s of its 1.65 s on MI355X
 (RCCL "Init timings", profiles/r1_bench/rccl_init_probe.json), on the
 time-to-Ready critical path of every node with >= 2 GPUs.  The driver /
 toolkit images of this operator target gfx950 only, so the validator image
-ships an RCCL whose bundle holds just the gfx950 code object (77 MB
-compressed, 569 MB uncompressed).
+ships an RCCL whose bundle holds just the gfx950 code object, DWARF stripped
+(108 MB).  It is stored uncompressed: decoding the 15.5 MB zstd form cost
+ncclCommInitRank another ~80 ms (0.44 -> 0.36 s median, interleaved A/B on
+MI355X, profiles/r2_ttr/rccl_lib_probe.txt).
 
 How (no relink: the host code and every virtual address stay as they are):
 
@@ -108,15 +110,21 @@ def _md5_low(data) -> int:
     return struct.unpack("<Q", hashlib.md5(data).digest()[:8])[0]
 
 
-def build_ccob(code_object: bytes, triple: str, level: int = 3) -> bytes:
-    """A two-entry bundle (empty host entry + the code object), compressed the
-    way clang-offload-bundler --compress writes format v3."""
+def build_bundle(code_object: bytes, triple: str) -> bytes:
+    """A two-entry uncompressed offload bundle (empty host entry + the code
+    object at the first page boundary)."""
     entries = [(HOST_TRIPLE, 0), (triple, len(code_object))]
     hdr = bytearray(BUNDLE_MAGIC + struct.pack("<Q", len(entries)))
     for t, size in entries:
         hdr += struct.pack("<QQQ", PAGE, size, len(t)) + t.encode()
     assert len(hdr) <= PAGE
-    bundle = bytes(hdr) + bytes(PAGE - len(hdr)) + code_object
+    return bytes(hdr) + bytes(PAGE - len(hdr)) + code_object
+
+
+def build_ccob(code_object: bytes, triple: str, level: int = 3) -> bytes:
+    """The same bundle compressed the way clang-offload-bundler --compress
+    writes format v3."""
+    bundle = build_bundle(code_object, triple)
     z = _zstd()
     cap = z.ZSTD_compressBound(len(bundle))
     out = ctypes.create_string_buffer(cap)
@@ -192,16 +200,18 @@ def strip_debug(co: bytes, objcopy: str = OBJCOPY) -> bytes:
     return out
 
 
-def slim_library(src: str, dst: str, arch: str = "gfx950", level: int = 3, strip: bool = True) -> dict:
+def slim_library(src: str, dst: str, arch: str = "gfx950", level: int = 3, strip: bool = True,
+                 compress: bool = True) -> dict:
     """Write ``dst``: ``src`` with a .hip_fatbin holding only ``arch`` (debug
-    sections stripped unless ``strip`` is false)."""
+    sections stripped unless ``strip`` is false; an uncompressed bundle with
+    ``compress`` false, which the HIP runtime uses without decompressing)."""
     elf, entries, bundle = fatbin_of(src)
     triple, co = code_object(bundle, entries, arch)
     del bundle
     full_bytes = len(co)
     if strip:
         co = strip_debug(co)
-    ccob = build_ccob(co, triple, level)
+    ccob = build_ccob(co, triple, level) if compress else build_bundle(co, triple)
     data = elf.data
     fb = elf.section(".hip_fatbin")
     fb_off, fb_addr, fb_size = fb[4], fb[3], fb[5]
@@ -307,6 +317,8 @@ def mmap_bundle_header(path: str) -> tuple[int, int, int]:
         strtab = m[st[4]:st[4] + st[5]]
         for s in shdrs:
             if strtab[s[0]:strtab.index(b"\0", s[0])] == b".hip_fatbin":
+                if m[s[4]:s[4] + 24] == BUNDLE_MAGIC:  # uncompressed bundle
+                    return 0, s[5], s[5]
                 _, ver, _, total, unc, _ = CCOB_HDR.unpack_from(m, s[4])
                 return ver, total, unc
     raise KeyError(".hip_fatbin")
@@ -323,9 +335,10 @@ if __name__ == "__main__":
     ap.add_argument("--level", type=int, default=3)
     ap.add_argument("--verify", action="store_true")
     ap.add_argument("--keep-debug", action="store_true")
+    ap.add_argument("--uncompressed", action="store_true", help="store the bundle without zstd")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(os.path.abspath(a.dst)), exist_ok=True)
-    rep = slim_library(a.src, a.dst, a.arch, a.level, strip=not a.keep_debug)
+    rep = slim_library(a.src, a.dst, a.arch, a.level, strip=not a.keep_debug, compress=not a.uncompressed)
     if a.verify:
         rep["verify"] = verify_library(a.dst, a.src, a.arch)
         if not rep["verify"]["ok"]:

@@ -49,23 +49,26 @@ def test_source_bundle_has_both_arches(libs):
     assert any(t.endswith("--gfx950") for t in triples) and any(t.endswith("--gfx942") for t in triples)
 
 
-@pytest.mark.parametrize("kind,strip", [("note", True), ("note", False), ("plain", True)])
-def test_trim_keeps_only_gfx950_and_loads(libs, kind, strip):
+@pytest.mark.parametrize("kind,strip,compress", [("note", True, True), ("note", False, True), ("plain", True, True),
+                                                   ("note", True, False)])
+def test_trim_keeps_only_gfx950_and_loads(libs, kind, strip, compress):
     src = libs[kind]
-    dst = str(libs["dir"] / f"out_{kind}_{strip}.so")
-    rep = F.slim_library(src, dst, "gfx950", strip=strip)
+    dst = str(libs["dir"] / f"out_{kind}_{strip}_{compress}.so")
+    rep = F.slim_library(src, dst, "gfx950", strip=strip, compress=compress)
+    if not compress:
+        assert F.mmap_bundle_header(dst)[0] == 0  # plain __CLANG_OFFLOAD_BUNDLE__
     v = F.verify_library(dst, src, "gfx950")
     assert v["ok"], v
     assert v["entries"] == [F.HOST_TRIPLE, "hipv4-amdgcn-amd-amdhsa--gfx950"]
     assert v["stripped"] == strip
     if strip:
         assert rep["code_object_bytes"] < rep["code_object_bytes_with_debug"]
-    if kind == "note" and strip:  # segment split: the file shrinks, PT_NOTE slot becomes a PT_LOAD
+    if kind == "note" and strip and compress:  # segment split: the file shrinks, PT_NOTE slot becomes a PT_LOAD
         assert rep["file_bytes"] < rep["source_file_bytes"]
         elf = F.Elf(open(dst, "rb").read())
         assert not any(p[0] == F.PT_NOTE for p in elf.phdrs)
         assert sum(p[0] == F.PT_LOAD for p in elf.phdrs) == sum(p[0] == F.PT_LOAD for p in F.Elf(open(src, "rb").read()).phdrs) + 1
-    else:
+    elif compress:
         assert rep["file_bytes"] == rep["source_file_bytes"]
     # the dynamic loader maps it and the host code runs (static init registered the bundle)
     assert ctypes.CDLL(dst).answer() == 42
@@ -99,17 +102,20 @@ def test_makefile_rccl_artefact_is_trimmed():
     if not os.path.exists(path):
         pytest.skip("native artefacts not built")
     ver, total, unc = F.mmap_bundle_header(str(path))
-    assert ver == 3 and total < 64 << 20 and unc < 256 << 20  # vs 571 MB / 5.3 GB in ROCm's librccl
+    # stored uncompressed (the runtime skips a 108 MB zstd decode in ncclCommInitRank):
+    # one code object instead of ROCm's 571 MB bundle / 5.3 GB uncompressed
+    assert ver == 0 and total == unc < 256 << 20
     rep = json.loads(open(os.path.join(os.path.dirname(path), "trim.json")).read())
     assert rep["source_entries"] > 1 and rep["code_object_bytes"] < rep["code_object_bytes_with_debug"]
 
 
 @pytest.mark.gpu
-def test_trimmed_kernel_runs_on_mi355x(libs):
+@pytest.mark.parametrize("compress", [True, False], ids=["zstd", "plain"])
+def test_trimmed_kernel_runs_on_mi355x(libs, compress):
     import torch
 
-    dst = str(libs["dir"] / "gpu_trim.so")
-    F.slim_library(libs["note"], dst, "gfx950", strip=True)
+    dst = str(libs["dir"] / f"gpu_trim_{compress}.so")
+    F.slim_library(libs["note"], dst, "gfx950", strip=True, compress=compress)
     x = torch.zeros(1000, device="cuda")
     torch.cuda.synchronize()
     lib = ctypes.CDLL(dst)
