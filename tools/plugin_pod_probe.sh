@@ -16,8 +16,11 @@ run() {  # name, env..., -- args
 }
 A="--steps hip,vecadd --vecadd-elems 1048576"
 for i in 1 2 3 4 5 6; do
-  run stream HSA_ENABLE_SDMA=0 -- $A
-  sleep 0.3
-  run null HSA_ENABLE_SDMA=0 -- $A --null-stream
-  sleep 0.3
+  for v in "base" "devkarg0 HIP_FORCE_DEV_KERNARG=0" "fgskarg ROC_USE_FGS_KERNARG=1" \
+           "skipcopy ROC_SKIP_KERNEL_ARG_COPY=1" "coherent HIP_HOST_COHERENT=1"; do
+    set -- $v
+    name=$1; shift
+    run $name HSA_ENABLE_SDMA=0 "$@" -- $A
+    sleep 0.3
+  done
 done
