@@ -77,12 +77,48 @@ def _raise_for(resp) -> None:
     raise ApiError(resp.status_code, reason or "Error", msg)
 
 
+class TokenFileAuth:
+    """Bearer token read from a file and re-read as it rotates.
+
+    The kubelet refreshes a pod's projected service-account token (valid for
+    an hour where the API server does not extend it) well before expiry; like
+    client-go, the client re-reads the file at most every ``reload_s`` so a
+    long-running operator keeps authenticating."""
+
+    def __init__(self, path: str, reload_s: float = 60.0, clock=None):
+        import time
+
+        self.path = path
+        self.reload_s = reload_s
+        self.clock = clock or time.monotonic
+        self._token = ""
+        self._read_at = None
+        self._lock = threading.Lock()
+
+    def token(self) -> str:
+        with self._lock:
+            now = self.clock()
+            if self._read_at is None or now - self._read_at >= self.reload_s:
+                try:
+                    with open(self.path) as f:
+                        self._token = f.read().strip()
+                except OSError:
+                    pass  # keep the last token; the API server says whether it still works
+                self._read_at = now
+            return self._token
+
+    def __call__(self, request):  # requests' auth hook
+        request.headers["Authorization"] = f"Bearer {self.token()}"
+        return request
+
+
 class RestClient:
     """Minimal Kubernetes REST client (JSON, merge-patch, streaming watch)."""
 
     SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
-    def __init__(self, base_url: str, token: str | None = None, verify=True, cert=None, timeout: float = 30.0):
+    def __init__(self, base_url: str, token: str | None = None, verify=True, cert=None, timeout: float = 30.0,
+                 token_file: str | None = None):
         import requests
 
         self.base = base_url.rstrip("/")
@@ -90,7 +126,9 @@ class RestClient:
         self.session.verify = verify
         if cert:
             self.session.cert = cert
-        if token:
+        if token_file:
+            self.session.auth = TokenFileAuth(token_file)
+        elif token:
             self.session.headers["Authorization"] = f"Bearer {token}"
         self.session.headers["Accept"] = "application/json"
         self.timeout = timeout
@@ -99,9 +137,8 @@ class RestClient:
     def from_incluster(cls) -> "RestClient":
         host = os.environ["KUBERNETES_SERVICE_HOST"]
         port = os.environ.get("KUBERNETES_SERVICE_PORT", "443")
-        with open(os.path.join(cls.SA_DIR, "token")) as f:
-            token = f.read().strip()
-        return cls(f"https://{host}:{port}", token=token, verify=os.path.join(cls.SA_DIR, "ca.crt"))
+        return cls(f"https://{host}:{port}", token_file=os.path.join(cls.SA_DIR, "token"),
+                   verify=os.path.join(cls.SA_DIR, "ca.crt"))
 
     @classmethod
     def from_kubeconfig(cls, path: str | None = None, context: str | None = None) -> "RestClient":
@@ -136,7 +173,8 @@ class RestClient:
         ck = materialise("client-key-data", "client-key", user)
         if cc and ck:
             cert = (cc, ck)
-        return cls(cluster["server"], token=user.get("token"), verify=verify, cert=cert)
+        return cls(cluster["server"], token=user.get("token"), verify=verify, cert=cert,
+                   token_file=user.get("tokenFile"))
 
     # -------------------------------------------------------------- helpers
     def _url(self, t: R.ResourceType, namespace=None, name=None, sub=None, query=None) -> str:

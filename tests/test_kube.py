@@ -206,3 +206,64 @@ def test_wait_for_falls_back_to_listing():
     objs, ok = wait_for(c, "v1", "Node", lambda o: "x" in (o.get("a", {}).get("metadata", {}).get("labels") or {}),
                         name="a", timeout=5, poll_s=0.05)
     assert ok
+
+
+def test_token_file_auth_follows_rotation(tmp_path):
+    """In-cluster: the projected service-account token rotates; the client
+    re-reads it (at most every reload period), as client-go does."""
+    from amdgpu_operator.kube.client import TokenFileAuth
+
+    now = [0.0]
+    tok = tmp_path / "token"
+    tok.write_text("first\n")
+    auth = TokenFileAuth(str(tok), reload_s=60.0, clock=lambda: now[0])
+
+    class Req:
+        headers: dict = {}
+
+    r = Req()
+    r.headers = {}
+    assert auth(r).headers["Authorization"] == "Bearer first"
+    tok.write_text("second\n")
+    now[0] = 30.0
+    assert auth(r).headers["Authorization"] == "Bearer first"  # within the reload period
+    now[0] = 61.0
+    assert auth(r).headers["Authorization"] == "Bearer second"
+    tok.unlink()
+    now[0] = 200.0
+    assert auth(r).headers["Authorization"] == "Bearer second"  # unreadable: keep the last one
+
+
+def test_rest_client_sends_the_rotated_token(tmp_path):
+    """End to end over HTTP: every request carries the current token."""
+    import http.server
+    import json as _json
+    import threading as _th
+
+    seen = []
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            seen.append(self.headers.get("Authorization"))
+            body = _json.dumps({"apiVersion": "v1", "kind": "Node", "metadata": {"name": "a"}}).encode()
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    _th.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        tok = tmp_path / "token"
+        tok.write_text("t1")
+        c = RestClient(f"http://127.0.0.1:{srv.server_address[1]}", token_file=str(tok))
+        c.session.auth.reload_s = 0.0
+        c.get("v1", "Node", "a")
+        tok.write_text("t2")
+        c.get("v1", "Node", "a")
+        assert seen == ["Bearer t1", "Bearer t2"]
+    finally:
+        srv.shutdown()
