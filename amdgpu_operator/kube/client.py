@@ -133,6 +133,37 @@ class RestClient:
         self.session.headers["Accept"] = "application/json"
         self.timeout = timeout
 
+    RETRIES = 4
+
+    def _call(self, method: str, url: str, **kw):
+        """One request, retried like client-go: on 429 / 503 (the server did
+        not process it; honour Retry-After, else back off), and on connection
+        errors for reads only (a write may have landed)."""
+        import time
+
+        import requests
+
+        delay = 0.1
+        for attempt in range(self.RETRIES + 1):
+            try:
+                r = self.session.request(method, url, timeout=self.timeout, **kw)
+            except requests.ConnectionError:
+                if method != "GET" or attempt == self.RETRIES:
+                    raise
+                time.sleep(delay)
+                delay = min(delay * 2, 2.0)
+                continue
+            if r.status_code in (429, 503) and attempt < self.RETRIES:
+                try:
+                    wait = float(r.headers.get("Retry-After", ""))
+                except ValueError:
+                    wait = delay
+                time.sleep(min(max(wait, 0.0), 10.0))
+                delay = min(delay * 2, 2.0)
+                continue
+            return r
+        return r
+
     @classmethod
     def from_incluster(cls) -> "RestClient":
         host = os.environ["KUBERNETES_SERVICE_HOST"]
@@ -187,14 +218,14 @@ class RestClient:
 
     def create(self, obj):
         t = R.rtype_of(obj)
-        r = self.session.post(self._url(t, R.ns_of(obj) if t.namespaced else None), data=json.dumps(obj),
-                              headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        r = self._call("POST", self._url(t, R.ns_of(obj) if t.namespaced else None), data=json.dumps(obj),
+                       headers={"Content-Type": "application/json"})
         _raise_for(r)
         return r.json()
 
     def get(self, api_version, kind, name, namespace=None):
         t = R.rtype(api_version, kind)
-        r = self.session.get(self._url(t, namespace, name), timeout=self.timeout)
+        r = self._call("GET", self._url(t, namespace, name))
         _raise_for(r)
         return r.json()
 
@@ -205,37 +236,37 @@ class RestClient:
         t = R.rtype(api_version, kind)
         if isinstance(label_selector, dict):
             label_selector = ",".join(f"{k}={v}" for k, v in label_selector.items())
-        r = self.session.get(self._url(t, namespace, query={"labelSelector": label_selector,
-                                                           "fieldSelector": field_selector}), timeout=self.timeout)
+        r = self._call("GET", self._url(t, namespace, query={"labelSelector": label_selector,
+                                                            "fieldSelector": field_selector}))
         _raise_for(r)
         body = r.json()
         return body.get("items", []), (body.get("metadata") or {}).get("resourceVersion")
 
     def update(self, obj):
         t = R.rtype_of(obj)
-        r = self.session.put(self._url(t, R.ns_of(obj), R.name_of(obj)), data=json.dumps(obj),
-                             headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        r = self._call("PUT", self._url(t, R.ns_of(obj), R.name_of(obj)), data=json.dumps(obj),
+                       headers={"Content-Type": "application/json"})
         _raise_for(r)
         return r.json()
 
     def update_status(self, obj):
         t = R.rtype_of(obj)
-        r = self.session.put(self._url(t, R.ns_of(obj), R.name_of(obj), "status"), data=json.dumps(obj),
-                             headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        r = self._call("PUT", self._url(t, R.ns_of(obj), R.name_of(obj), "status"), data=json.dumps(obj),
+                       headers={"Content-Type": "application/json"})
         _raise_for(r)
         return r.json()
 
     def patch(self, api_version, kind, name, patch, namespace=None, subresource=None):
         t = R.rtype(api_version, kind)
-        r = self.session.patch(self._url(t, namespace, name, subresource), data=json.dumps(patch),
-                               headers={"Content-Type": "application/merge-patch+json"}, timeout=self.timeout)
+        r = self._call("PATCH", self._url(t, namespace, name, subresource), data=json.dumps(patch),
+                       headers={"Content-Type": "application/merge-patch+json"})
         _raise_for(r)
         return r.json()
 
     def delete(self, api_version, kind, name, namespace=None, grace_period_seconds=None):
         t = R.rtype(api_version, kind)
         q = None if grace_period_seconds is None else {"gracePeriodSeconds": str(int(grace_period_seconds))}
-        r = self.session.delete(self._url(t, namespace, name, query=q), timeout=self.timeout)
+        r = self._call("DELETE", self._url(t, namespace, name, query=q))
         _raise_for(r)
 
     def watch(self, api_version, kind, namespace=None, label_selector=None, field_selector=None,

@@ -267,3 +267,58 @@ def test_rest_client_sends_the_rotated_token(tmp_path):
         assert seen == ["Bearer t1", "Bearer t2"]
     finally:
         srv.shutdown()
+
+
+def test_rest_client_retries_throttling_and_reads():
+    """429 / 503 with Retry-After are retried for every verb (the server did
+    not act); a refused connection only for reads."""
+    import http.server
+    import json as _json
+    import threading as _th
+
+    import requests
+
+    hits = {"GET": 0, "POST": 0}
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def _reply(self, verb):
+            hits[verb] += 1
+            if hits[verb] <= 2:
+                self.send_response(429 if verb == "GET" else 503)
+                self.send_header("Retry-After", "0")
+                self.send_header("Content-Length", "0")
+                self.end_headers()
+                return
+            body = _json.dumps({"apiVersion": "v1", "kind": "Node", "metadata": {"name": "a"}}).encode()
+            self.send_response(200 if verb == "GET" else 201)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def do_GET(self):
+            self._reply("GET")
+
+        def do_POST(self):
+            n = int(self.headers.get("Content-Length") or 0)
+            self.rfile.read(n)
+            self._reply("POST")
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    _th.Thread(target=srv.serve_forever, daemon=True).start()
+    port = srv.server_address[1]
+    try:
+        c = RestClient(f"http://127.0.0.1:{port}")
+        assert c.get("v1", "Node", "a")["metadata"]["name"] == "a" and hits["GET"] == 3
+        assert c.create(R.new("v1", "Node", "a"))["metadata"]["name"] == "a" and hits["POST"] == 3
+    finally:
+        srv.shutdown()
+        srv.server_close()
+    dead = RestClient(f"http://127.0.0.1:{port}")
+    dead.RETRIES = 1
+    with pytest.raises(requests.ConnectionError):
+        dead.create(R.new("v1", "Node", "b"))  # a write is not repeated blindly
+    with pytest.raises(requests.ConnectionError):
+        dead.get("v1", "Node", "a")
