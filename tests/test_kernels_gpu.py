@@ -117,6 +117,30 @@ def test_max_abs_diff():
     assert K.max_abs_diff(a, b) == float("inf")
 
 
+@pytest.mark.parametrize("n,offset", [(1, 0), (7, 1), (1 << 20, 0), ((1 << 22) + 3, 1), ((1 << 24) + 5, 2)])
+def test_max_abs_diff_matches_torch(n, offset):
+    """Against the fp32 PyTorch reference, including unaligned starts (scalar
+    path) and tails past the last float4."""
+    base_a = torch.randn(n + offset, device=DEV)
+    base_b = base_a + 1e-3 * torch.randn(n + offset, device=DEV)
+    a, b = base_a[offset:], base_b[offset:]
+    want = (a - b).abs().max().item()
+    assert K.max_abs_diff(a, b) == want
+
+
+@pytest.mark.parametrize("nbytes", [16, 4096, (1 << 20) + 48, 1 << 26])
+def test_checksum_matches_reference(nbytes):
+    """sum over 16-byte words i of (x + 3y + 5z + 7w + i mod 65536) mod 2^64."""
+    import numpy as np
+
+    src = torch.randint(0, 256, (nbytes,), device=DEV, dtype=torch.uint8)
+    w = src.cpu().numpy().view(np.uint32).reshape(-1, 4).astype(np.uint64)
+    idx = np.arange(w.shape[0], dtype=np.uint64) & np.uint64(0xFFFF)
+    with np.errstate(over="ignore"):
+        want = int((w[:, 0] + 3 * w[:, 1] + 5 * w[:, 2] + 7 * w[:, 3] + idx).sum(dtype=np.uint64))
+    assert K.checksum(src) == want
+
+
 @pytest.mark.parametrize("peers", [1, 2, 3, 4, 8])
 def test_allreduce_oneshot_emulated(peers):
     n = 1 << 18
