@@ -35,6 +35,8 @@ def build_parser() -> argparse.ArgumentParser:
     v = sub.add_parser("validate", help="operator-validator steps")
     v.add_argument("step", choices=["driver", "toolkit", "workload", "plugin", "gpu", "complete"])
     v.add_argument("--resource", default="amd.com/gpu")
+    v.add_argument("--partition-strategy", default="single", choices=["single", "mixed"],
+                   help="the device plugin's: under mixed, partitioned GPUs are amd.com/gpu-<mode>")
     v.add_argument("--timeout", type=float, default=600.0)
     v.add_argument("--wait-toolkit", action="store_true",
                    help="gpu: plugin validation waits for the toolkit; the workload starts right away")
@@ -102,10 +104,12 @@ def _validate(env, a, extra, stop, ready) -> int:
     elif a.step == "plugin":
         if V.read_ready(env, "plugin") is None:
             pod_args = _plugin_pod_args(extra)
-            V.validate_plugin(env, a.resource, pod_args=pod_args, timeout=a.timeout, stop=stop)
+            V.validate_plugin(env, a.resource, pod_args=pod_args, timeout=a.timeout, stop=stop,
+                              partition_strategy=a.partition_strategy)
     elif a.step == "gpu":
         V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
-                       wait_toolkit=a.wait_toolkit, with_driver=a.with_driver)
+                       wait_toolkit=a.wait_toolkit, with_driver=a.with_driver,
+                       partition_strategy=a.partition_strategy)
     else:
         res = V.complete(env)
         steps = ", ".join(f"{k} {v:.2f} s" for k, v in res["steps"].items() if v is not None)
@@ -121,7 +125,7 @@ def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
     i = 0
     while i < len(args):
         a = args[i]
-        if a in ("--resource", "--timeout"):
+        if a in ("--resource", "--timeout", "--partition-strategy"):
             known += args[i:i + 2]
             i += 2
             continue

@@ -315,11 +315,14 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     if w.rcclProcess == "shared":
         wl_args += ["--rccl-shared-process"]
     inits = [_wait_init("driver-validation", image, v.imagePullPolicy, "driver")]
+    # the plugin pods request what the device plugin advertises (its resource
+    # name, and amd.com/gpu-<mode> for partitioned GPUs under "mixed")
+    plugin_res = ["--resource", spec.devicePlugin.resourceName,
+                  "--partition-strategy", spec.devicePlugin.partitionStrategy]
     if v.pluginValidation and spec.devicePlugin.enabled and w.prespawn:
         # one init container validates the driver and, meanwhile, starts the
         # workload processes behind their start gate (validate.py validate_gpu)
-        extra = ["--resource", spec.devicePlugin.resourceName, "--with-driver"] + \
-            (["--wait-toolkit"] if spec.toolkit.enabled else [])
+        extra = [*plugin_res, "--with-driver"] + (["--wait-toolkit"] if spec.toolkit.enabled else [])
         inits = [_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args],
                             env=_workload_pod_env(v, image), mounts=[POD_RESOURCES_MOUNT, DEVICE_PLUGINS_MOUNT])]
     elif v.pluginValidation and spec.devicePlugin.enabled:  # (validation pods: _workload_pod_env)
@@ -328,7 +331,7 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         # needs only the driver (its processes run in this pod, not through the
         # runtime hook), so it overlaps the toolkit install; the plugin pods
         # wait for the toolkit inside the step.
-        extra = ["--resource", spec.devicePlugin.resourceName] + (["--wait-toolkit"] if spec.toolkit.enabled else [])
+        extra = plugin_res + (["--wait-toolkit"] if spec.toolkit.enabled else [])
         inits.append(_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args],
                                 env=_workload_pod_env(v, image), mounts=[POD_RESOURCES_MOUNT, DEVICE_PLUGINS_MOUNT]))
     else:

@@ -106,9 +106,9 @@ def resource_for(dev, cfg: PluginConfig) -> str:
 
     ``single``: every device (whole GPU or partition) is ``amd.com/gpu``.
     ``mixed``: partitioned devices are ``amd.com/gpu-<mode>`` (e.g. ``-cpx``)."""
-    if cfg.partition_strategy == "mixed" and dev.partition_count > 1 and dev.compute_partition:
-        return f"{cfg.resource_name}-{dev.compute_partition.lower()}"
-    return cfg.resource_name
+    from ..discovery import topology
+
+    return topology.partition_resource(dev, cfg.resource_name, cfg.partition_strategy)
 
 
 class DevicePluginServer:

@@ -219,6 +219,15 @@ def _root(root: str | None) -> bytes:
     return (root or "/").encode()
 
 
+def partition_resource(dev: GpuDevice, resource_name: str, strategy: str = "single") -> str:
+    """Extended-resource name a device is advertised under: ``resource_name``,
+    or ``<resource_name>-<mode>`` for a partitioned GPU under the ``mixed``
+    strategy (the device plugin's and the validator's shared rule)."""
+    if strategy == "mixed" and dev.partition_count > 1 and dev.compute_partition:
+        return f"{resource_name}-{dev.compute_partition.lower()}"
+    return resource_name
+
+
 def enumerate_gpus(root: str | None = None) -> list[GpuDevice]:
     lib = _lib()
     n = ctypes.c_int(0)

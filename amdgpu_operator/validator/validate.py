@@ -288,10 +288,23 @@ def allocatable(node: dict, resource: str) -> int:
 PLUGIN_POD_ENV = [{"name": "HSA_ENABLE_SDMA", "value": "0"}]
 
 
-def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: float, stop,
-                          kd=None) -> str | None:
-    """Wait until the kubelet's device manager holds ``expect`` devices of
-    ``resource`` (pod-resources ``GetAllocatableResources``,
+def expected_devices(env: NodeEnv, resource: str = RESOURCE_NAME, partition_strategy: str = "single") -> dict:
+    """Devices the device plugin advertises on this node, per resource name:
+    every GPU (or partition) under ``resource``, except that under the
+    ``mixed`` strategy partitioned GPUs are ``<resource>-<mode>``
+    (discovery/topology.py partition_resource, which the plugin uses too)."""
+    from ..discovery import topology
+
+    out: dict[str, int] = {}
+    for dev in topology.enumerate_gpus(env.sysfs_root()):
+        r = topology.partition_resource(dev, resource, partition_strategy)
+        out[r] = out.get(r, 0) + 1
+    return out
+
+
+def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, kd=None) -> str | None:
+    """Wait until the kubelet's device manager holds the ``expected`` number
+    of devices of each resource (pod-resources ``GetAllocatableResources``,
     deviceplugin/podresources.py).  Returns "kubelet", or None when that API
     is not reachable (the caller falls back to ``Node.status``)."""
     from ..deviceplugin.podresources import KubeletDevices
@@ -309,13 +322,16 @@ def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: fl
     try:
         waits = env.waits()
         while True:
-            n = kd.count(resource)
-            if n is None:
-                return None
-            if n >= expect:
+            held = {}
+            for resource in expected:
+                n = kd.count(resource)
+                if n is None:
+                    return None
+                held[resource] = n
+            if all(held[r] >= n for r, n in expected.items()):
                 return "kubelet"
             if time.monotonic() >= deadline:
-                raise StepFailed(f"kubelet holds {n} {resource} devices, expected {expect}")
+                raise StepFailed(f"kubelet holds {held} devices, expected {expected}")
             if stop is not None and stop.is_set():
                 raise StepFailed("stopped")
             delay = next(waits)
@@ -334,9 +350,12 @@ def _wait_kubelet_devices(env: NodeEnv, resource: str, expect: int, deadline: fl
 def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | None = None,
                     pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                     image: str | None = None, pull_policy: str = "IfNotPresent",
-                    pull_secrets: list[str] | None = None, kubelet=None) -> dict:
-    """Wait until the kubelet holds one device per GPU, then run one 1-GPU
-    pod per device.
+                    pull_secrets: list[str] | None = None, kubelet=None,
+                    partition_strategy: str = "single") -> dict:
+    """Wait until the kubelet holds one device per GPU (or partition), then
+    run one 1-device pod per device, each requesting the resource its device
+    is advertised under (:func:`expected_devices`; ``expect`` overrides the
+    count of ``resource``).
 
     The pods run the validator's own image (``VALIDATOR_IMAGE`` in the
     validator container's env, with its pull policy and secrets, which
@@ -346,30 +365,28 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     pull_policy = pod_image.get("pull_policy") or pull_policy
     if pull_secrets is None:
         pull_secrets = list(pod_image.get("pull_secrets") or [])
-    from ..discovery import topology
-
     t0 = time.perf_counter()
-    if expect is None:
-        expect = len(topology.enumerate_gpus(env.sysfs_root()))
+    expected = {resource: expect} if expect is not None else expected_devices(env, resource, partition_strategy)
     deadline = time.monotonic() + timeout
-    source = _wait_kubelet_devices(env, resource, expect, deadline, stop, kubelet)
+    source = _wait_kubelet_devices(env, expected, deadline, stop, kubelet)
     if source is None:  # no pod-resources API: wait for the kubelet to publish Node.status.allocatable
         source = "node-status"
         nodes, ok = wait_for(env.client, "v1", "Node",
-                             lambda o: allocatable(o.get(env.node_name) or {}, resource) >= expect,
+                             lambda o: all(allocatable(o.get(env.node_name) or {}, r) >= n
+                                           for r, n in expected.items()),
                              name=env.node_name, timeout=max(0.0, deadline - time.monotonic()), stop=stop,
                              poll_s=env.poll_s)
         if not ok:
             if stop is not None and stop.is_set():
                 raise StepFailed("stopped")
-            raise StepFailed(f"allocatable {resource}={allocatable(nodes.get(env.node_name) or {}, resource)}, "
-                             f"expected {expect}")
+            node = nodes.get(env.node_name) or {}
+            raise StepFailed(f"allocatable {({r: allocatable(node, r) for r in expected})}, expected {expected}")
     t_alloc = time.perf_counter() - t0
     marks = {"start": time.time() - (time.perf_counter() - t0), "devices_seen": time.time()}
     run_id = uuid.uuid4().hex[:8]
     pod_args = list(pod_args or ["--steps", "hip,vecadd,gemm", "--gemm", "1024"])
     names = []
-    for i in range(expect):
+    for i, res in enumerate(r for r, n in sorted(expected.items()) for _ in range(n)):
         name = f"amd-validator-workload-{run_id}-{i}"
         pod = {
             "apiVersion": "v1", "kind": "Pod",
@@ -381,7 +398,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                 "tolerations": [{"key": resource, "operator": "Exists", "effect": "NoSchedule"}],
                 "containers": [{"name": "workload", "image": image, "imagePullPolicy": pull_policy,
                                 "command": ["amdgpu-validator"], "args": pod_args, "env": PLUGIN_POD_ENV,
-                                "resources": {"limits": {resource: "1"}, "requests": {resource: "1"}}}],
+                                "resources": {"limits": {res: "1"}, "requests": {res: "1"}}}],
             },
         }
         if pull_secrets:
@@ -407,7 +424,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
             pass
     if not all(p == "Succeeded" for p in phases.values()):
         raise StepFailed(f"plugin validation pods did not succeed: {phases}")
-    summary = {"ok": True, "pods": expect, "devices": devices, "allocatable_wait_s": round(t_alloc, 4),
+    summary = {"ok": True, "pods": len(names), "resources": expected, "devices": devices, "allocatable_wait_s": round(t_alloc, 4),
                "allocatable_source": source, "marks": {k: round(v, 4) for k, v in marks.items()},
                "seconds": time.perf_counter() - t0}
     write_ready(env, "plugin", summary)
@@ -471,7 +488,7 @@ def abort_start_gates(env: NodeEnv) -> list[str]:
 
 def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURCE_NAME,
                  pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
-                 wait_toolkit: bool = False, with_driver: bool = False) -> dict:
+                 wait_toolkit: bool = False, with_driver: bool = False, partition_strategy: str = "single") -> dict:
     """Workload and plugin validation concurrently (each skipped if already done).
 
     Only the driver gates the workload: its processes run in this privileged
@@ -541,7 +558,7 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
                 wait_ready(env, "workload", timeout, stop)
             if read_ready(env, "plugin") is None:
                 results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop,
-                                                    kubelet=kubelet)
+                                                    kubelet=kubelet, partition_strategy=partition_strategy)
         except Exception as e:  # noqa: BLE001
             errors.append(f"plugin: {e}")
         finally:

@@ -75,6 +75,20 @@ def test_cpx_node_advertises_partitions(cluster_factory):
     assert lab["amd.com/gpu.physical-count"] == "2" and lab["amd.com/gpu.compute-units"] == "32"
 
 
+def test_cpx_mixed_strategy_validates_partition_resources(cluster_factory):
+    """Under ``partitionStrategy=mixed`` partitioned GPUs are advertised as
+    amd.com/gpu-cpx: the plugin validation waits for and requests those."""
+    c = cluster_factory([NodeSpec("gpu-1", 2, "CPX", "NPS2")])
+    c.install_operator(parse_set_flags(REFERENCE_SET_FLAGS + ["devicePlugin.partitionStrategy=mixed"]))
+    c.wait_ready(60)
+    node = c.client.get("v1", "Node", "gpu-1")
+    assert node["status"]["allocatable"].get("amd.com/gpu-cpx") == "16"
+    from amdgpu_operator.validator.validate import read_ready
+
+    plugin = read_ready(c.nodes["gpu-1"].env, "plugin")
+    assert plugin["resources"] == {"amd.com/gpu-cpx": 16} and plugin["pods"] == 16
+
+
 def test_unhealthy_gpu_drops_allocatable(cluster_factory):
     c = cluster_factory([NodeSpec("gpu-1", 4)])
     c.install_operator(REF)
