@@ -15,6 +15,7 @@ VERSION = "v1beta1"
 DEVICE_PLUGIN_PATH = "/var/lib/kubelet/device-plugins/"
 KUBELET_SOCKET = DEVICE_PLUGIN_PATH + "kubelet.sock"
 POD_RESOURCES_SOCKET = "/var/lib/kubelet/pod-resources/kubelet.sock"
+REPLICA_SEP = "::"  # time-sliced replica IDs: "<device id>::<replica>" (config.py)
 HEALTHY = "Healthy"
 UNHEALTHY = "Unhealthy"
 

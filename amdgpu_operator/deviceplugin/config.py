@@ -44,10 +44,10 @@ import yaml
 from pydantic import BaseModel, ConfigDict, Field, field_validator
 
 from .. import RESOURCE_NAME
+from .api import REPLICA_SEP  # noqa: F401 - "<device id>::<replica>"
 
 CONFIG_LABEL = "amd.com/device-plugin.config"
 SHARED_SUFFIX = ".shared"
-REPLICA_SEP = "::"
 
 ListStrategy = Literal["envvar", "volume-mounts", "cdi-annotations", "cdi-cri"]
 

@@ -302,11 +302,33 @@ def expected_devices(env: NodeEnv, resource: str = RESOURCE_NAME, partition_stra
     return out
 
 
-def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, kd=None) -> str | None:
-    """Wait until the kubelet's device manager holds the ``expected`` number
-    of devices of each resource (pod-resources ``GetAllocatableResources``,
-    deviceplugin/podresources.py).  Returns "kubelet", or None when that API
-    is not reachable (the caller falls back to ``Node.status``)."""
+def _device_plan(expected: dict, held: dict[str, list[str]]) -> dict | None:
+    """Pods to run per resource, from the kubelet's devices, or None while
+    the plugin's devices are not all there.
+
+    The ``expected`` resources, once each holds its count of distinct GPUs
+    (time-sliced replicas ``<id>::<n>`` count once).  A device-plugin config
+    file can rename them (time-slicing ``rename`` / ``renameByDefault``,
+    deviceplugin/config.py), which the validator's flags do not know: then
+    every resource of the vendor domain (``amd.com/``) counts, one pod per
+    distinct GPU it holds."""
+    from ..deviceplugin.api import REPLICA_SEP
+
+    def gpus(ids):
+        return len({i.split(REPLICA_SEP, 1)[0] for i in ids})
+
+    if all(gpus(held.get(r, ())) >= n for r, n in expected.items()):
+        return dict(expected)
+    domain = next(iter(expected)).split("/", 1)[0] + "/"
+    plan = {r: gpus(ids) for r, ids in held.items() if r.startswith(domain) and ids}
+    return plan if sum(plan.values()) >= sum(expected.values()) else None
+
+
+def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, kd=None) -> dict | None:
+    """Wait until the kubelet's device manager holds the ``expected`` devices
+    (pod-resources ``GetAllocatableResources``, deviceplugin/podresources.py;
+    :func:`_device_plan`).  Returns the pods to run per resource, or None when
+    that API is not reachable (the caller falls back to ``Node.status``)."""
     from ..deviceplugin.podresources import KubeletDevices
 
     from ..utils.fswait import DirWatch
@@ -322,16 +344,15 @@ def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, k
     try:
         waits = env.waits()
         while True:
-            held = {}
-            for resource in expected:
-                n = kd.count(resource)
-                if n is None:
-                    return None
-                held[resource] = n
-            if all(held[r] >= n for r, n in expected.items()):
-                return "kubelet"
+            held = kd.allocatable()
+            if held is None:
+                return None
+            plan = _device_plan(expected, held)
+            if plan is not None:
+                return plan
             if time.monotonic() >= deadline:
-                raise StepFailed(f"kubelet holds {held} devices, expected {expected}")
+                raise StepFailed(f"kubelet holds {({r: len(v) for r, v in held.items()})} devices, "
+                                 f"expected {expected}")
             if stop is not None and stop.is_set():
                 raise StepFailed("stopped")
             delay = next(waits)
@@ -368,9 +389,10 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     t0 = time.perf_counter()
     expected = {resource: expect} if expect is not None else expected_devices(env, resource, partition_strategy)
     deadline = time.monotonic() + timeout
-    source = _wait_kubelet_devices(env, expected, deadline, stop, kubelet)
-    if source is None:  # no pod-resources API: wait for the kubelet to publish Node.status.allocatable
-        source = "node-status"
+    plan = _wait_kubelet_devices(env, expected, deadline, stop, kubelet)
+    source = "kubelet"
+    if plan is None:  # no pod-resources API: wait for the kubelet to publish Node.status.allocatable
+        source, plan = "node-status", expected
         nodes, ok = wait_for(env.client, "v1", "Node",
                              lambda o: all(allocatable(o.get(env.node_name) or {}, r) >= n
                                            for r, n in expected.items()),
@@ -386,7 +408,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     run_id = uuid.uuid4().hex[:8]
     pod_args = list(pod_args or ["--steps", "hip,vecadd,gemm", "--gemm", "1024"])
     names = []
-    for i, res in enumerate(r for r, n in sorted(expected.items()) for _ in range(n)):
+    for i, res in enumerate(r for r, n in sorted(plan.items()) for _ in range(n)):
         name = f"amd-validator-workload-{run_id}-{i}"
         pod = {
             "apiVersion": "v1", "kind": "Pod",
@@ -424,7 +446,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
             pass
     if not all(p == "Succeeded" for p in phases.values()):
         raise StepFailed(f"plugin validation pods did not succeed: {phases}")
-    summary = {"ok": True, "pods": len(names), "resources": expected, "devices": devices, "allocatable_wait_s": round(t_alloc, 4),
+    summary = {"ok": True, "pods": len(names), "resources": plan, "devices": devices, "allocatable_wait_s": round(t_alloc, 4),
                "allocatable_source": source, "marks": {k: round(v, 4) for k, v in marks.items()},
                "seconds": time.perf_counter() - t0}
     write_ready(env, "plugin", summary)

@@ -340,3 +340,43 @@ def test_reconfigure_under_concurrent_allocations(node):
     finally:
         stop.set()
         m.stop()
+
+
+def test_device_plan_from_kubelet_view():
+    from amdgpu_operator.validator.validate import _device_plan
+
+    ids = [f"0000:{i:02x}:00.0" for i in range(4)]
+    assert _device_plan({"amd.com/gpu": 4}, {"amd.com/gpu": ids[:3]}) is None
+    assert _device_plan({"amd.com/gpu": 4}, {"amd.com/gpu": ids}) == {"amd.com/gpu": 4}
+    # time-sliced replicas of 2 GPUs are not 4 GPUs
+    reps = [f"{i}::{r}" for i in ids[:2] for r in range(2)]
+    assert _device_plan({"amd.com/gpu": 4}, {"amd.com/gpu": reps}) is None
+    # renamed by a config file (renameByDefault): one pod per GPU of the renamed resource
+    shared = [f"{i}::{r}" for i in ids for r in range(4)]
+    assert _device_plan({"amd.com/gpu": 4}, {"amd.com/gpu.shared": shared}) == {"amd.com/gpu.shared": 4}
+    assert _device_plan({"amd.com/gpu": 4}, {"amd.com/gpu.shared": shared[:8], "other.io/x": ids}) is None
+
+
+def test_plugin_validation_with_renamed_shared_resource(tmp_path):
+    """A default plugin config that renames the time-sliced resource
+    (amd.com/gpu.shared): the validator's --resource flag does not know the
+    new name; it reads it from the kubelet and the node still validates."""
+    c = SimCluster(str(tmp_path / "c"), [NodeSpec("gpu-1", 2)], fake_gpu=True).start()
+    try:
+        renamed = "version: v1\nsharing:\n  timeSlicing:\n    renameByDefault: true\n    resources:\n" \
+                  "      - name: amd.com/gpu\n        replicas: 4\n"
+        c.client.create({"apiVersion": "v1", "kind": "ConfigMap",
+                         "metadata": {"name": "plugin-config", "namespace": c.namespace},
+                         "data": {"renamed": renamed}})
+        values = deep_merge(parse_set_flags(REFERENCE_SET_FLAGS),
+                            {"devicePlugin": {"config": {"name": "plugin-config", "default": "renamed"}}})
+        c.install_operator(values)
+        c.wait_ready(60)
+        n = c.client.get("v1", "Node", "gpu-1")
+        assert n["status"]["allocatable"].get("amd.com/gpu.shared") == "8"
+        from amdgpu_operator.validator.validate import read_ready
+
+        plugin = read_ready(c.nodes["gpu-1"].env, "plugin")
+        assert plugin["resources"] == {"amd.com/gpu.shared": 2} and plugin["allocatable_source"] == "kubelet"
+    finally:
+        c.stop()
