@@ -392,17 +392,31 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     plan = _wait_kubelet_devices(env, expected, deadline, stop, kubelet)
     source = "kubelet"
     if plan is None:  # no pod-resources API: wait for the kubelet to publish Node.status.allocatable
-        source, plan = "node-status", expected
-        nodes, ok = wait_for(env.client, "v1", "Node",
-                             lambda o: all(allocatable(o.get(env.node_name) or {}, r) >= n
-                                           for r, n in expected.items()),
+        source = "node-status"
+
+        def node_plan(node: dict):
+            # counts only: replicas are not told apart here, so a renamed
+            # resource gets as many pods as there are GPUs, not replicas
+            alloc = (node.get("status") or {}).get("allocatable") or {}
+            plan = _device_plan(expected, {r: [f"{r}#{i}" for i in range(allocatable(node, r))] for r in alloc})
+            if plan is None or plan == expected:
+                return plan
+            left, capped = sum(expected.values()), {}
+            for r, n in sorted(plan.items()):
+                if left > 0:
+                    capped[r] = min(n, left)
+                    left -= capped[r]
+            return capped
+
+        nodes, ok = wait_for(env.client, "v1", "Node", lambda o: node_plan(o.get(env.node_name) or {}) is not None,
                              name=env.node_name, timeout=max(0.0, deadline - time.monotonic()), stop=stop,
                              poll_s=env.poll_s)
+        node = nodes.get(env.node_name) or {}
         if not ok:
             if stop is not None and stop.is_set():
                 raise StepFailed("stopped")
-            node = nodes.get(env.node_name) or {}
             raise StepFailed(f"allocatable {({r: allocatable(node, r) for r in expected})}, expected {expected}")
+        plan = node_plan(node)
     t_alloc = time.perf_counter() - t0
     marks = {"start": time.time() - (time.perf_counter() - t0), "devices_seen": time.time()}
     run_id = uuid.uuid4().hex[:8]

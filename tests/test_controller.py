@@ -335,3 +335,16 @@ def test_plugin_validation_pods_use_the_validator_image(tmp_path):
     ctr = seen[0]["containers"][0]
     assert ctr["image"] == "reg/amd-operator-validator:9" and ctr["imagePullPolicy"] == "Always"
     assert seen[0]["imagePullSecrets"] == [{"name": "s1"}]
+    assert os_ready["allocatable_source"] == "node-status"
+    # a config file renamed the (time-sliced) resource: Node.status shows
+    # only amd.com/gpu.shared replicas; one pod for the node's one GPU
+    node = c.get("v1", "Node", "n1")
+    node["status"] = {"allocatable": {"amd.com/gpu.shared": "4"}}
+    c.update_status(node)
+    seen.clear()
+    th = threading.Thread(target=kubelet)
+    th.start()
+    rep = V.validate_plugin(env, timeout=5)
+    th.join()
+    assert rep["resources"] == {"amd.com/gpu.shared": 1} and rep["pods"] == 1
+    assert seen[0]["containers"][0]["resources"]["limits"] == {"amd.com/gpu.shared": "1"}
