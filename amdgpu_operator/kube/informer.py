@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import pickle
 import threading
+import time
 
 from . import resources as R
 from .fakeapi import ApiError, _field_ok
@@ -43,8 +44,9 @@ class Informer:
     """List-then-watch cache of one kind (optionally one namespace)."""
 
     def __init__(self, client, api_version: str, kind: str, namespace: str | None = None, on_event=None,
-                 relist_wait_s: float = 1.0):
+                 relist_wait_s: float = 1.0, watch_timeout_s: float = 300.0):
         self.client = client
+        self.watch_timeout_s = watch_timeout_s
         self.api_version = api_version
         self.kind = kind
         self.namespace = namespace
@@ -135,19 +137,28 @@ class Informer:
             self.synced.set()
             if self.on_event is not None:
                 self.on_event(self.kind)
+            # a watch that times out is resumed from the last version seen;
+            # only an error (410 Gone, network) costs a relist
             try:
-                for etype, obj in self.client.watch(self.api_version, self.kind, self.namespace,
-                                                    resource_version=rv, stop=stop, timeout=300):
-                    if etype == "DELETED":
-                        self.remove(R.ns_of(obj) if obj.get("metadata", {}).get("namespace") else None,
-                                    R.name_of(obj), _rv(obj))
-                    elif etype in ("ADDED", "MODIFIED"):
-                        self.put(obj)
-                    else:
-                        continue
-                    if self.on_event is not None:
-                        self.on_event(self.kind)
-            except Exception as e:  # noqa: BLE001 - watch ended (410 Gone, timeout, network): relist
+                while not stop.is_set():
+                    began, events = time.monotonic(), 0
+                    for etype, obj in self.client.watch(self.api_version, self.kind, self.namespace,
+                                                        resource_version=rv, stop=stop,
+                                                        timeout=self.watch_timeout_s):
+                        rv = (obj.get("metadata") or {}).get("resourceVersion") or rv
+                        events += 1
+                        if etype == "DELETED":
+                            self.remove(R.ns_of(obj) if obj.get("metadata", {}).get("namespace") else None,
+                                        R.name_of(obj), _rv(obj))
+                        elif etype in ("ADDED", "MODIFIED"):
+                            self.put(obj)
+                        else:
+                            continue  # BOOKMARK: only the version moves
+                        if self.on_event is not None:
+                            self.on_event(self.kind)
+                    if not events and time.monotonic() - began < 1.0:
+                        stop.wait(self.relist_wait_s)  # closed at once: do not spin on a failing server
+            except Exception as e:  # noqa: BLE001 - watch failed (410 Gone, network): relist
                 log.debug("informer %s watch: %s", self.kind, e)
 
 
@@ -170,8 +181,6 @@ class CachedClient:
         return self._client
 
     def wait_synced(self, timeout: float = 10.0) -> bool:
-        import time
-
         deadline = time.monotonic() + timeout
         for inf in self.informers.values():
             while not (inf.synced.is_set() or inf.failed.is_set()):

@@ -189,3 +189,29 @@ def test_informer_survives_an_api_server_restart():
     finally:
         stop.set()
         srv.stop()
+
+
+def test_timed_out_watch_resumes_without_a_relist():
+    """A watch that ends at its timeout resumes from the last version seen
+    (client-go's reflector); only an error costs a full list."""
+    from amdgpu_operator.kube.informer import Informer
+
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Namespace", "ns"))
+    lists = []
+    orig = c.list_rv
+    c.list_rv = lambda *a, **kw: (lists.append(1), orig(*a, **kw))[1]
+    stop = threading.Event()
+    inf = Informer(c, "v1", "ConfigMap", "ns", watch_timeout_s=0.2).start(stop)
+    try:
+        assert inf.synced.wait(5)
+        for i in range(3):
+            c.create(R.new("v1", "ConfigMap", f"cm{i}", "ns"))
+            time.sleep(0.3)  # each watch times out between writes
+        deadline = time.time() + 5
+        while time.time() < deadline and len(inf.list("ns")) < 3:
+            time.sleep(0.01)
+        assert [R.name_of(o) for o in inf.list("ns")] == ["cm0", "cm1", "cm2"]
+        assert len(lists) == 1
+    finally:
+        stop.set()
