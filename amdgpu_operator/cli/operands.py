@@ -329,7 +329,10 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
 
         def once():
             if cmd == "nfd":
-                L.sync_node_labels(env.client, env.node_name, L.nfd_labels(env.sysfs_root()), (L.NFD_PREFIX + "pci-",))
+                from ..controller.nodes import NFD_SCANNED_ANN
+
+                L.sync_node_labels(env.client, env.node_name, L.nfd_labels(env.sysfs_root()), (L.NFD_PREFIX + "pci-",),
+                                   {NFD_SCANNED_ANN: "true"})
             else:
                 gpus = topology.enumerate_gpus(env.sysfs_root())
                 labels = L.gfd_labels(gpus, env.sysfs_root(), a.label_prefix)

@@ -21,6 +21,9 @@ NFD_PCI_LABELS = (
     "feature.node.kubernetes.io/pci-0380_1002.present",  # display controller
     "feature.node.kubernetes.io/pci-0300_1002.present",  # VGA
 )
+# written by our NFD worker (cli/operands.py nfd) with its first label sync: a
+# node without it has not been scanned yet, so "no GPU labels" means nothing
+NFD_SCANNED_ANN = "nfd.amd.com/scanned"
 
 
 def is_gpu_node(node: dict) -> bool:
@@ -34,6 +37,14 @@ def is_gpu_node(node: dict) -> bool:
     except ValueError:
         pass
     return labels.get(LABEL_PRESENT) == "true" and labels.get("amd.com/gpu.present.source") == "manual"
+
+
+def nfd_scanned(node: dict) -> bool:
+    """Our NFD worker has run on the node, or another NFD left PCI labels."""
+    meta = node.get("metadata") or {}
+    if (meta.get("annotations") or {}).get(NFD_SCANNED_ANN):
+        return True
+    return any(k.startswith("feature.node.kubernetes.io/pci-") for k in meta.get("labels") or {})
 
 
 def desired_labels(node: dict, spec: ClusterPolicySpec) -> dict:
@@ -65,14 +76,17 @@ def desired_labels(node: dict, spec: ClusterPolicySpec) -> dict:
     return patch
 
 
-def label_nodes(client, spec: ClusterPolicySpec) -> tuple[int, int]:
-    """Apply GPU/deploy labels to every node. Returns (gpu_nodes, patched)."""
-    gpu_nodes = patched = 0
+def label_nodes(client, spec: ClusterPolicySpec) -> tuple[int, int, int]:
+    """Apply GPU/deploy labels to every node. Returns (gpu_nodes, patched,
+    nfd_scanned): the last counts nodes our NFD worker has labelled."""
+    gpu_nodes = patched = scanned = 0
     for node in client.list("v1", "Node"):
         if is_gpu_node(node):
             gpu_nodes += 1
+        if nfd_scanned(node):
+            scanned += 1
         patch = desired_labels(node, spec)
         if patch:
             client.patch("v1", "Node", node["metadata"]["name"], {"metadata": {"labels": patch}})
             patched += 1
-    return gpu_nodes, patched
+    return gpu_nodes, patched, scanned

@@ -203,7 +203,7 @@ class ClusterPolicyReconciler:
 
         if spec.psa.enabled:
             self._label_namespace_psa()
-        gpu_nodes, patched = label_nodes(self.client, spec)
+        gpu_nodes, patched, nfd_scanned = label_nodes(self.client, spec)
         owner = owner_ref(cp)
         results: list[StateResult] = []
         driver_live = None
@@ -222,6 +222,7 @@ class ClusterPolicyReconciler:
             changed = 0
             ready = True
             detail = []
+            pods_ready = 0
             for o in objs:
                 live, action = apply_object(self.client, o, verified=self._verified)
                 changed += action != "unchanged"
@@ -230,12 +231,19 @@ class ClusterPolicyReconciler:
                 if o["kind"] == "DaemonSet":
                     ok, d = daemonset_ready(live)
                     ds_ready[o["metadata"]["name"]] = ok
+                    pods_ready += int((live.get("status") or {}).get("numberReady", 0))
                     gpu_scoped = bool(o["spec"]["template"]["spec"].get("nodeSelector"))
                     if ok and gpu_scoped and gpu_nodes > 0 and int((live.get("status") or {}).get(
                             "desiredNumberScheduled", 0)) == 0:
                         ok, d = False, "not yet scheduled on the GPU nodes"
                     ready &= ok
                     detail.append(f"{o['metadata']['name']}: {d}")
+            if state == "state-node-feature-discovery" and ready:
+                # each NFD pod labels its node before it turns Ready; a Node read
+                # older than the DaemonSet status would count a GPU node as none
+                if nfd_scanned < pods_ready:
+                    ready = False
+                    detail.append(f"{nfd_scanned}/{pods_ready} nodes labelled")
             if state == "state-driver" and pool_status is not None:
                 self._write_pool_status(pool_status, ds_ready)
                 ready &= all(st["state"] != "error" for st in pool_status.values())

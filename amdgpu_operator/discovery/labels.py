@@ -155,10 +155,14 @@ def sharing_labels(labels: dict[str, str], plugin_config, resource: str = "amd.c
     return out
 
 
-def sync_node_labels(client, node_name: str, desired: dict[str, str], owned_prefixes: tuple[str, ...]) -> dict:
+def sync_node_labels(client, node_name: str, desired: dict[str, str], owned_prefixes: tuple[str, ...],
+                     annotations: dict[str, str] | None = None) -> dict:
     """Set ``desired`` and remove stale labels under ``owned_prefixes``
-    (operator-owned labels are never removed). Returns the applied patch."""
+    (operator-owned labels are never removed); ``annotations`` are set in the
+    same patch when missing. Returns the applied label patch."""
     node = client.get("v1", "Node", node_name)
+    cur_ann = node.get("metadata", {}).get("annotations") or {}
+    ann = {k: v for k, v in (annotations or {}).items() if cur_ann.get(k) != v}
     cur = node.get("metadata", {}).get("labels") or {}
     patch: dict = {}
     for k, v in desired.items():
@@ -169,6 +173,9 @@ def sync_node_labels(client, node_name: str, desired: dict[str, str], owned_pref
             continue
         if any(k.startswith(pfx) for pfx in owned_prefixes):
             patch[k] = None
-    if patch:
-        client.patch("v1", "Node", node_name, {"metadata": {"labels": patch}})
+    if patch or ann:
+        meta: dict = {"labels": patch}
+        if ann:
+            meta["annotations"] = ann
+        client.patch("v1", "Node", node_name, {"metadata": meta})
     return patch

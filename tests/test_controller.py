@@ -6,7 +6,7 @@ import pytest
 from amdgpu_operator.api.clusterpolicy import (REFERENCE_SET_FLAGS, ClusterPolicySpec, cluster_policy,
                                                parse_set_flags, spec_from_values)
 from amdgpu_operator.controller.manifests import STATE_BUILDERS
-from amdgpu_operator.controller.nodes import desired_labels, is_gpu_node
+from amdgpu_operator.controller.nodes import NFD_SCANNED_ANN, desired_labels, is_gpu_node
 from amdgpu_operator.controller.reconciler import CP_API, ClusterPolicyReconciler, cleanup_crd
 from amdgpu_operator.helm.crd import crd
 from amdgpu_operator.kube import resources as R
@@ -155,6 +155,12 @@ def test_zero_gpu_cluster_converges(env):
             ds["status"] = {"desiredNumberScheduled": 1, "numberReady": 1, "updatedNumberScheduled": 1,
                             "observedGeneration": 1}
             c.update_status(ds)
+    # the NFD pod is Ready but the node shows no scan yet (a Node read older
+    # than the DaemonSet status): zero GPU nodes is not yet an answer
+    res = rec.reconcile()
+    assert res.state == "notReady"
+    assert "0/1 nodes labelled" in next(r.detail for r in res.states if r.name == "state-node-feature-discovery")
+    c.patch("v1", "Node", "cpu-a", {"metadata": {"annotations": {NFD_SCANNED_ANN: "true"}}})
     assert rec.reconcile().state == "ready"
 
 
