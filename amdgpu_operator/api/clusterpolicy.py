@@ -196,6 +196,30 @@ class PartitionManagerSpec(Operand):
     })
 
 
+class SandboxWorkloadsSpec(_M):
+    """VM passthrough next to containers (the NVIDIA operator's
+    ``sandboxWorkloads``): a GPU node's ``amd.com/gpu.workload.config`` label
+    (``container`` | ``vm-passthrough``, default ``defaultWorkload``) picks
+    which operands it runs.  Off by default: every GPU node is a container node."""
+
+    enabled: bool = False
+    defaultWorkload: Literal["container", "vm-passthrough"] = "container"
+
+
+class VFIOManagerSpec(Operand):
+    """Binds a passthrough node's GPUs (whole IOMMU groups) to vfio-pci."""
+
+    image: str = "amd-vfio-manager"
+    kfdIdleTimeoutSeconds: int = 300  # wait this long for GPU users before unbinding from amdgpu
+
+
+class SandboxDevicePluginSpec(Operand):
+    """Advertises vfio-bound GPUs per product (``amd.com/MI355X``) for VMs."""
+
+    image: str = "amd-sandbox-device-plugin"
+    resourcePrefix: str = "amd.com"
+
+
 class WorkloadSpec(_M):
     gemmN: int = 4096
     gemmIters: int = 3
@@ -270,6 +294,9 @@ class ClusterPolicySpec(_M):
     nfd: NFDSpec = Field(default_factory=NFDSpec)
     migManager: PartitionManagerSpec = Field(default_factory=PartitionManagerSpec, alias="partitionManager")
     validator: ValidatorSpec = Field(default_factory=ValidatorSpec)
+    sandboxWorkloads: SandboxWorkloadsSpec = Field(default_factory=SandboxWorkloadsSpec)
+    vfioManager: VFIOManagerSpec = Field(default_factory=VFIOManagerSpec)
+    sandboxDevicePlugin: SandboxDevicePluginSpec = Field(default_factory=SandboxDevicePluginSpec)
 
     @model_validator(mode="before")
     @classmethod
@@ -304,7 +331,31 @@ STATES = [
     ("state-gpu-feature-discovery", "gfd"),
     ("state-partition-manager", "migManager"),
     ("state-node-status-exporter", "nodeStatusExporter"),
+    # sandboxWorkloads (vm-passthrough nodes)
+    ("state-vfio-manager", "vfioManager"),
+    ("state-sandbox-validation", "sandboxValidator"),
+    ("state-sandbox-device-plugin", "sandboxDevicePlugin"),
 ]
+
+SANDBOX_OPERANDS = ("vfioManager", "sandboxValidator", "sandboxDevicePlugin")
+# which operands a GPU node runs for its amd.com/gpu.workload.config
+WORKLOAD_OPERANDS = {
+    "container": ("driver", "toolkit", "validator", "devicePlugin", "dcgmExporter", "gfd", "migManager",
+                  "nodeStatusExporter"),
+    "vm-passthrough": SANDBOX_OPERANDS,
+}
+
+
+def operand_enabled(spec: ClusterPolicySpec, key: str | None) -> bool:
+    """Is the operand of a state (``STATES`` key) switched on by the spec?
+    Sandbox operands need ``sandboxWorkloads.enabled``; the sandbox validator
+    follows ``validator.enabled``."""
+    if key is None:
+        return True
+    if key in SANDBOX_OPERANDS:
+        own = spec.validator.enabled if key == "sandboxValidator" else getattr(spec, key).enabled
+        return spec.sandboxWorkloads.enabled and own
+    return getattr(spec, key).enabled
 
 
 class HelmValues(_M):

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import argparse
 import threading
+import time
 
 from ..nodeenv import NodeEnv
 from ..utils.logs import get_logger
@@ -33,7 +34,8 @@ def build_parser() -> argparse.ArgumentParser:
     t.add_argument("--mount-rocm", action="store_true")
 
     v = sub.add_parser("validate", help="operator-validator steps")
-    v.add_argument("step", choices=["driver", "toolkit", "workload", "plugin", "gpu", "complete"])
+    v.add_argument("step", choices=["driver", "toolkit", "workload", "plugin", "gpu", "complete", "vfio",
+                                    "sandbox-complete"])
     v.add_argument("--resource", default="amd.com/gpu")
     v.add_argument("--partition-strategy", default="single", choices=["single", "mixed"],
                    help="the device plugin's: under mixed, partitioned GPUs are amd.com/gpu-<mode>")
@@ -86,7 +88,61 @@ def build_parser() -> argparse.ArgumentParser:
     pm.add_argument("--default-compute", default="SPX")
     pm.add_argument("--default-memory", default="NPS1")
     pm.add_argument("--interval", type=float, default=30.0)
+
+    vm = sub.add_parser("vfio-manager", help="bind GPUs to vfio-pci for VM passthrough (sandbox workloads)")
+    vm.add_argument("action", choices=["bind", "unbind"])
+    vm.add_argument("--kfd-idle-timeout", type=float, default=300.0)
+    vm.add_argument("--interval", type=float, default=30.0)
+
+    sdp = sub.add_parser("sandbox-device-plugin", help="kubelet device plugin for vfio-bound GPUs")
+    sdp.add_argument("--resource-prefix", default="amd.com")
+    sdp.add_argument("--health-poll-ms", type=int, default=1000)
     return p
+
+
+def _pci(env: NodeEnv):
+    from ..sandbox.vfio import PciSysfs
+
+    return env.extra.get("pci_backend") or PciSysfs(env.sysfs_root())
+
+
+def _vfio_manager(env: NodeEnv, a, stop: threading.Event, ready) -> int:
+    """``vfio-manager bind``: GPUs to vfio-pci, then keep them there; when the
+    pod goes because the node left vm-passthrough, hand them back to amdgpu
+    (a plain pod restart leaves running VMs their devices)."""
+    from ..controller.manifests import DEPLOY_LABEL, OPERAND_LABELS
+    from ..sandbox import vfio as VF
+    from ..validator import validate as V
+
+    pci = _pci(env)
+    if a.action == "unbind":
+        VF.unbind_all(pci)
+        V.clear_ready(env, ("vfio", "sandbox"))
+        return 0
+
+    def bind():
+        res = VF.bind_all(pci, a.kfd_idle_timeout, stop)
+        if any(r.changed for r in res) or V.read_ready(env, "vfio") is None:
+            # the GPUs left amdgpu: the container-path validations no longer hold
+            V.clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
+            V.write_ready(env, "vfio", {"groups": [r.__dict__ for r in res], "seconds": time.perf_counter() - t0})
+        return res
+
+    t0 = time.perf_counter()
+    bind()
+    ready()
+    while not stop.wait(max(env.poll_s, min(a.interval, 30.0))):
+        try:
+            bind()
+        except VF.VfioError as e:
+            log.error("vfio rebind: %s", e)
+    node = _get_or_empty(env.client, "Node", env.node_name) if env.client is not None else {}
+    label = DEPLOY_LABEL.format(OPERAND_LABELS["vfioManager"])
+    if node and (node["metadata"].get("labels") or {}).get(label) != "true":
+        VF.unbind_all(pci)
+        V.clear_ready(env, ("vfio", "sandbox"))
+        log.info("node left vm-passthrough: GPUs returned to %s", VF.HOST_DRIVER)
+    return 0
 
 
 def _validate(env, a, extra, stop, ready) -> int:
@@ -110,6 +166,13 @@ def _validate(env, a, extra, stop, ready) -> int:
         V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
                        wait_toolkit=a.wait_toolkit, with_driver=a.with_driver,
                        partition_strategy=a.partition_strategy)
+    elif a.step == "vfio":
+        V.validate_vfio(env, _pci(env), a.timeout, stop)
+    elif a.step == "sandbox-complete":
+        res = V.complete_sandbox(env)
+        _node_event(env, "Normal", "GPUValidated", f"{res['gpus']} GPU(s) ready for VM passthrough")
+        ready()
+        stop.wait()
     else:
         res = V.complete(env)
         steps = ", ".join(f"{k} {v:.2f} s" for k, v in res["steps"].items() if v is not None)
@@ -361,6 +424,23 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             return 0
         while not stop.wait(max(env.poll_s, min(a.interval, 60.0))):
             once()
+        return 0
+
+    if cmd == "vfio-manager":
+        return _vfio_manager(env, a, stop, ready)
+
+    if cmd == "sandbox-device-plugin":
+        from ..deviceplugin.server import PluginConfig
+        from ..sandbox.plugin import SandboxPluginManager
+
+        cfg = PluginConfig(socket_dir=env.device_plugin_dir, sysfs_root=env.sysfs_root(),
+                           health_poll_ms=a.health_poll_ms, watch_interval_s=max(0.05, min(0.5, env.poll_s * 10)))
+        mgr = SandboxPluginManager(cfg, _pci(env), a.resource_prefix)
+        mgr.start()
+        log.info("sandbox device plugin serving %s", {r: len(s.devices) for r, s in mgr.servers.items()})
+        ready()
+        stop.wait()
+        mgr.stop()
         return 0
 
     if cmd == "partition-manager":

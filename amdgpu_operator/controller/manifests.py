@@ -39,6 +39,9 @@ OPERAND_LABELS = {
     "gfd": "gpu-feature-discovery",
     "migManager": "partition-manager",
     "nodeStatusExporter": "node-status-exporter",
+    "vfioManager": "vfio-manager",
+    "sandboxValidator": "sandbox-validator",
+    "sandboxDevicePlugin": "sandbox-device-plugin",
 }
 
 
@@ -460,6 +463,49 @@ def state_node_status_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[
             _service(name, ns, owner, n.port)]
 
 
+def state_vfio_manager(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    """vm-passthrough nodes: GPUs (whole IOMMU groups) to vfio-pci (sandbox/vfio.py)."""
+    m = spec.vfioManager
+    name, sa = "amd-vfio-manager", "amd-vfio-manager"
+    image = m.ref("amd-vfio-manager")
+    ctr = _container("amd-vfio-manager", image, m.imagePullPolicy,
+                     ["vfio-manager", "bind", "--kfd-idle-timeout", str(m.kfdIdleTimeoutSeconds)] + list(m.args),
+                     [_mount("host-sys", "/host/sys"), _mount("host-dev", "/host/dev", ro=True),
+                      _mount("lib-modules", "/lib/modules", ro=True),
+                      _mount("run-amd-validations", VALIDATIONS_HOST_DIR)], list(m.env), True, m.resources.model_dump())
+    vols = [_hostpath("host-sys", "/sys", "Directory"), _hostpath("host-dev", "/dev", "Directory"),
+            _hostpath("lib-modules", "/lib/modules", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "vfioManager", sa, [ctr], [], vols, host_pid=True)]
+
+
+def state_sandbox_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    """vm-passthrough nodes: every GPU on vfio-pci with its /dev/vfio group node."""
+    v = spec.validator
+    name, sa = "amd-sandbox-validator", "amd-sandbox-validator"
+    image = v.ref("amd-operator-validator")
+    init = _wait_init("vfio-pci-validation", image, v.imagePullPolicy, "vfio")
+    ctr = _container("amd-sandbox-validator", image, v.imagePullPolicy, ["validate", "sandbox-complete"],
+                     [_mount("run-amd-validations", VALIDATIONS_HOST_DIR)], list(v.env), True, v.resources.model_dump())
+    vols = [_hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
+            _daemonset(spec, ns, owner, name, "sandboxValidator", sa, [ctr], [init], vols, operand=v)]
+
+
+def state_sandbox_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    """vm-passthrough nodes: vfio GPUs as amd.com/<product> (sandbox/plugin.py)."""
+    p = spec.sandboxDevicePlugin
+    name, sa = "amd-sandbox-device-plugin-daemonset", "amd-sandbox-device-plugin"
+    image = p.ref("amd-sandbox-device-plugin")
+    ctr = _container("amd-sandbox-device-plugin", image, p.imagePullPolicy,
+                     ["sandbox-device-plugin", "--resource-prefix", p.resourcePrefix] + list(p.args),
+                     [_mount("device-plugin", "/var/lib/kubelet/device-plugins"), *_host_view()],
+                     list(p.env), True, p.resources.model_dump())
+    init = _wait_init("vfio-pci-validation", image, p.imagePullPolicy, "vfio")
+    vols = [_hostpath("device-plugin", "/var/lib/kubelet/device-plugins"), _hostpath("host-sys", "/sys", "Directory"),
+            _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "sandboxDevicePlugin", sa, [ctr], [init], vols)]
+
+
 def state_driver_pools(spec: ClusterPolicySpec, ns: str, owner, drivers: list[dict],
                        nodes: list[dict]) -> tuple[list[dict], dict[str, dict]]:
     """``driver.useDriverCRD``: one driver DaemonSet per AMDGPUDriver object
@@ -519,4 +565,7 @@ STATE_BUILDERS = {
     "state-gpu-feature-discovery": state_gfd,
     "state-partition-manager": state_partition_manager,
     "state-node-status-exporter": state_node_status_exporter,
+    "state-vfio-manager": state_vfio_manager,
+    "state-sandbox-validation": state_sandbox_validator,
+    "state-sandbox-device-plugin": state_sandbox_device_plugin,
 }

@@ -12,8 +12,13 @@ and one ``amd.com/gpu.deploy.<operand>`` label per operand; a user-set
 from __future__ import annotations
 
 from .. import LABEL_PRESENT, RESOURCE_NAME
-from ..api.clusterpolicy import ClusterPolicySpec
+from ..api.clusterpolicy import WORKLOAD_OPERANDS, ClusterPolicySpec, operand_enabled
+from ..sandbox import WORKLOAD_CONFIG_LABEL, WORKLOADS
+from ..utils.logs import get_logger
 from .manifests import DEPLOY_LABEL, OPERAND_LABELS
+
+log = get_logger("amdgpu.nodes")
+VALIDATED_LABELS = ("amd.com/gpu.validated", "amd.com/gpu.validated.mfma")
 
 NFD_PCI_LABELS = (
     "feature.node.kubernetes.io/pci-1002.present",       # vendor only
@@ -47,6 +52,21 @@ def nfd_scanned(node: dict) -> bool:
     return any(k.startswith("feature.node.kubernetes.io/pci-") for k in meta.get("labels") or {})
 
 
+def node_workload(node: dict, spec: ClusterPolicySpec) -> str:
+    """``container`` or ``vm-passthrough``: the node's
+    ``amd.com/gpu.workload.config`` label under ``sandboxWorkloads``, else
+    ``sandboxWorkloads.defaultWorkload``; always ``container`` without sandbox mode."""
+    if not spec.sandboxWorkloads.enabled:
+        return "container"
+    val = (node.get("metadata", {}).get("labels") or {}).get(WORKLOAD_CONFIG_LABEL)
+    if val in WORKLOADS:
+        return val
+    if val is not None:
+        log.warning("node %s: unknown %s=%r, using %s", node.get("metadata", {}).get("name"), WORKLOAD_CONFIG_LABEL,
+                    val, spec.sandboxWorkloads.defaultWorkload)
+    return spec.sandboxWorkloads.defaultWorkload
+
+
 def desired_labels(node: dict, spec: ClusterPolicySpec) -> dict:
     """Label patch (value None = remove) for one node."""
     labels = node.get("metadata", {}).get("labels") or {}
@@ -55,17 +75,25 @@ def desired_labels(node: dict, spec: ClusterPolicySpec) -> dict:
     if gpu:
         if labels.get(LABEL_PRESENT) != "true":
             patch[LABEL_PRESENT] = "true"
+        mine = WORKLOAD_OPERANDS[node_workload(node, spec)]
+        switched = False
         for key, suffix in OPERAND_LABELS.items():
             lbl = DEPLOY_LABEL.format(suffix)
-            enabled = getattr(spec, key).enabled
-            if not enabled:
+            if not operand_enabled(spec, key) or key not in mine:
                 if lbl in labels:
                     patch[lbl] = None
+                    switched |= labels[lbl] == "true" and operand_enabled(spec, key)
                 continue
             if labels.get(lbl) == "false":
                 continue  # user opt-out is sticky
             if labels.get(lbl) != "true":
                 patch[lbl] = "true"
+        if switched:
+            # the node changed workload (container <-> vm-passthrough): its
+            # validation was for the other one
+            for lbl in VALIDATED_LABELS:
+                if lbl in labels:
+                    patch[lbl] = None
     else:
         if LABEL_PRESENT in labels and labels.get("amd.com/gpu.present.source") != "manual":
             patch[LABEL_PRESENT] = None
@@ -76,17 +104,30 @@ def desired_labels(node: dict, spec: ClusterPolicySpec) -> dict:
     return patch
 
 
-def label_nodes(client, spec: ClusterPolicySpec) -> tuple[int, int, int]:
+def label_nodes(client, spec: ClusterPolicySpec) -> tuple[int, int, int, list[dict]]:
     """Apply GPU/deploy labels to every node. Returns (gpu_nodes, patched,
-    nfd_scanned): the last counts nodes our NFD worker has labelled."""
+    nfd_scanned, labels): nfd_scanned counts nodes our NFD worker has
+    labelled, labels is each node's label set after this pass."""
     gpu_nodes = patched = scanned = 0
+    views = []
     for node in client.list("v1", "Node"):
         if is_gpu_node(node):
             gpu_nodes += 1
         if nfd_scanned(node):
             scanned += 1
         patch = desired_labels(node, spec)
+        view = dict(node["metadata"].get("labels") or {})
         if patch:
             client.patch("v1", "Node", node["metadata"]["name"], {"metadata": {"labels": patch}})
             patched += 1
-    return gpu_nodes, patched, scanned
+            for k, v in patch.items():
+                if v is None:
+                    view.pop(k, None)
+                else:
+                    view[k] = v
+        views.append(view)
+    return gpu_nodes, patched, scanned, views
+
+
+def nodes_selected(views: list[dict], selector: dict) -> int:
+    return sum(1 for lb in views if all(lb.get(k) == v for k, v in selector.items()))

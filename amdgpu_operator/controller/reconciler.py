@@ -33,13 +33,13 @@ from dataclasses import dataclass, field
 from pydantic import ValidationError
 
 from .. import API_GROUP, API_VERSION
-from ..api.clusterpolicy import STATES, ClusterPolicySpec
+from ..api.clusterpolicy import STATES, ClusterPolicySpec, operand_enabled
 from ..kube import resources as R
 from ..kube.client import NotFound, apply_object
 from ..kube.events import NORMAL, WARNING, EventRecorder
 from ..utils.logs import get_logger
 from .manifests import STATE_BUILDERS, owner_ref
-from .nodes import label_nodes
+from .nodes import label_nodes, nodes_selected
 
 CP_API = f"{API_GROUP}/{API_VERSION}"
 log = get_logger("amdgpu.operator")
@@ -203,14 +203,14 @@ class ClusterPolicyReconciler:
 
         if spec.psa.enabled:
             self._label_namespace_psa()
-        gpu_nodes, patched, nfd_scanned = label_nodes(self.client, spec)
+        gpu_nodes, patched, nfd_scanned, node_labels = label_nodes(self.client, spec)
         owner = owner_ref(cp)
         results: list[StateResult] = []
         driver_live = None
         pool_status = None
         ds_ready: dict[str, bool] = {}
         for state, key in STATES:
-            enabled = key is None or getattr(spec, key).enabled
+            enabled = operand_enabled(spec, key)
             objs = STATE_BUILDERS[state](spec, self.namespace, owner)
             if state == "state-driver" and enabled and spec.driver.useDriverCRD:
                 self._delete_objects([o for o in objs if o["kind"] == "DaemonSet"])  # the policy-wide one
@@ -232,9 +232,9 @@ class ClusterPolicyReconciler:
                     ok, d = daemonset_ready(live)
                     ds_ready[o["metadata"]["name"]] = ok
                     pods_ready += int((live.get("status") or {}).get("numberReady", 0))
-                    gpu_scoped = bool(o["spec"]["template"]["spec"].get("nodeSelector"))
-                    if ok and gpu_scoped and gpu_nodes > 0 and int((live.get("status") or {}).get(
-                            "desiredNumberScheduled", 0)) == 0:
+                    sel = o["spec"]["template"]["spec"].get("nodeSelector") or {}
+                    if ok and sel and int((live.get("status") or {}).get("desiredNumberScheduled", 0)) == 0 \
+                            and nodes_selected(node_labels, sel):
                         ok, d = False, "not yet scheduled on the GPU nodes"
                     ready &= ok
                     detail.append(f"{o['metadata']['name']}: {d}")

@@ -40,7 +40,7 @@ MFMA_TYPES = {
               "int8": True, "xf32": True},
 }
 # labels the operator owns (never removed by the GFD sweep)
-OPERATOR_OWNED = ("amd.com/gpu.present", "amd.com/gpu.deploy.", "amd.com/gpu.validated",
+OPERATOR_OWNED = ("amd.com/gpu.present", "amd.com/gpu.deploy.", "amd.com/gpu.validated", "amd.com/gpu.workload.config",
                   "amd.com/gpu.partition-config", "amd.com/gpu.partition.", "amd.com/gpu.present.source")
 
 _VALUE_RE = re.compile(r"[^A-Za-z0-9_.-]")

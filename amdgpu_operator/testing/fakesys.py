@@ -25,12 +25,20 @@ HBM_BYTES = 309220868096
 MI355X_DEVICE_ID = 0x75A3
 PARTITION_SPLIT = {"SPX": 1, "DPX": 2, "TPX": 3, "QPX": 4, "CPX": 8}
 HIVE_ID = 6032565651074706519
+IOMMU_GROUP_BASE = 40
 
 
 def _w(path: str, text: str) -> None:
     os.makedirs(os.path.dirname(path), exist_ok=True)
     with open(path, "w") as f:
         f.write(text)
+
+
+def _link(target: str, path: str) -> None:
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    if os.path.lexists(path):
+        os.unlink(path)
+    os.symlink(target, path)
 
 
 def _props(d: dict) -> str:
@@ -141,6 +149,20 @@ def build_node(root: str, gpus: int = 8, compute_partition: str = "SPX", memory_
         _w(f"{pci}/available_memory_partition", "NPS1, NPS2\n")
     for h in range(hidden_peers):
         _w(f"{base}/{node + h}/io_links/0/.hidden", "")
+    # PCI driver binding and IOMMU groups (vfio-manager, sandbox workloads):
+    # one group per GPU, bound to amdgpu while the module is live
+    _w(f"{root}/sys/bus/pci/drivers_probe", "")
+    if driver_loaded:
+        _w(f"{root}/sys/bus/pci/drivers/amdgpu/unbind", "")
+    for n, bdf in enumerate(dict.fromkeys(g.bdf for g in out)):
+        group = str(IOMMU_GROUP_BASE + n)
+        gdir = f"{root}/sys/kernel/iommu_groups/{group}/devices"
+        os.makedirs(gdir, exist_ok=True)
+        _link(f"../../../../bus/pci/devices/{bdf}", f"{gdir}/{bdf}")
+        _link(f"../../../../kernel/iommu_groups/{group}", f"{root}/sys/bus/pci/devices/{bdf}/iommu_group")
+        _w(f"{root}/sys/bus/pci/devices/{bdf}/driver_override", "(null)\n")
+        if driver_loaded:
+            _link("../../../../bus/pci/drivers/amdgpu", f"{root}/sys/bus/pci/devices/{bdf}/driver")
     # a non-GPU PCI device to make sure discovery filters by vendor/class
     _w(f"{root}/sys/bus/pci/devices/0000:00:01.0/vendor", "0x1022\n")
     _w(f"{root}/sys/bus/pci/devices/0000:00:01.0/class", "0x060000\n")
@@ -211,3 +233,76 @@ class SimModule:
 
 def clear(root: str) -> None:
     shutil.rmtree(root, ignore_errors=True)
+
+
+class FakePciKernel:
+    """The kernel side of PCI driver binding on a fake tree: applies the
+    sysfs writes :class:`amdgpu_operator.sandbox.vfio.PciSysfs` makes
+    (``driver_override``, ``<driver>/unbind``, ``drivers_probe``) the way
+    the PCI core does, and ``modprobe vfio-pci``.  ``busy`` holds fake KFD
+    process IDs (GPU users that block an unbind from amdgpu)."""
+
+    def __new__(cls, root: str):
+        from ..sandbox.vfio import PciSysfs
+
+        class _Kernel(PciSysfs):
+            def write(self, path: str, text: str) -> None:
+                super().write(path, text)
+                self._apply(os.path.relpath(path, self.path("sys/bus/pci")), text.strip())
+
+            def _dev(self, bdf: str) -> str:
+                return self.path("sys/bus/pci/devices", bdf)
+
+            def _apply(self, rel: str, val: str) -> None:
+                parts = rel.split(os.sep)
+                if rel == "drivers_probe":
+                    self._probe(val)
+                elif parts[-1] == "unbind":
+                    # devices/<bdf>/driver/unbind or drivers/<name>/unbind
+                    bdf = parts[1] if parts[0] == "devices" else val
+                    link = os.path.join(self._dev(bdf), "driver")
+                    if os.path.lexists(link):
+                        drv = os.path.basename(os.path.realpath(link))
+                        os.unlink(link)
+                        if drv == "vfio-pci":
+                            grp = self.function(bdf).iommu_group
+                            if grp and not any(self.function(b).driver == "vfio-pci" for b in self.group_members(grp)):
+                                try:
+                                    os.unlink(self.vfio_dev(grp))
+                                except OSError:
+                                    pass
+
+            def _probe(self, bdf: str) -> None:
+                if os.path.lexists(os.path.join(self._dev(bdf), "driver")):
+                    return
+                try:
+                    with open(os.path.join(self._dev(bdf), "driver_override")) as f:
+                        override = f.read().strip()
+                except OSError:
+                    override = ""
+                drv = override if override and override != "(null)" else "amdgpu"
+                if not self.driver_loaded(drv):
+                    return
+                _link(f"../../../../bus/pci/drivers/{drv}", os.path.join(self._dev(bdf), "driver"))
+                if drv == "vfio-pci":
+                    grp = self.function(bdf).iommu_group
+                    _w(self.path("dev/vfio/vfio"), "")
+                    if grp:
+                        _w(self.vfio_dev(grp), "")
+
+            def load_module(self, name: str) -> None:
+                self.modprobes.append(name)
+                if name in ("vfio-pci", "vfio_pci"):
+                    _w(self.path("sys/bus/pci/drivers/vfio-pci/unbind"), "")
+
+            def set_busy(self, pids) -> None:
+                procs = self.path("sys/class/kfd/kfd/proc")
+                if os.path.isdir(procs):
+                    for p in os.listdir(procs):
+                        os.rmdir(os.path.join(procs, p))
+                for p in pids:
+                    os.makedirs(os.path.join(procs, str(p)), exist_ok=True)
+
+        k = _Kernel(root)
+        k.modprobes = []
+        return k

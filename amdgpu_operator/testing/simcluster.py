@@ -294,6 +294,7 @@ class SimCluster:
                       launcher=self._launch)
         if ns.sysfs_root is None and ns.gpus > 0:  # driver installs / unloads act on the fake tree
             env.extra["kmod"] = fakesys.SimModule(root)
+            env.extra["pci_backend"] = fakesys.FakePciKernel(root)  # vfio-manager binds act on the fake tree
         if self.fake_gpu:
             env.extra["metrics_fixture"] = os.path.join(fakesys.REAL_FIXTURE, "amd-smi-metric.json")
         os.makedirs(os.path.dirname(env.containerd_config), exist_ok=True)
@@ -680,7 +681,7 @@ class SimCluster:
         except NotFound:
             return None
 
-    def is_ready(self, expect_allocatable: dict[str, int] | None = None) -> bool:
+    def is_ready(self, expect_allocatable: dict[str, int | dict] | None = None) -> bool:
         cp = self.policy()
         if not cp or (cp.get("status") or {}).get("state") != "ready":
             return False
@@ -691,13 +692,14 @@ class SimCluster:
             if (n["metadata"].get("labels") or {}).get("amd.com/gpu.validated") != "true":
                 return False
             want = (expect_allocatable or {}).get(node.spec.name)
-            if want is not None:
-                have = int(((n.get("status") or {}).get("allocatable") or {}).get(RESOURCE_NAME, "0"))
-                if have != want:
-                    return False
+            if want is not None:  # a count of amd.com/gpu, or {resource: count}
+                alloc = (n.get("status") or {}).get("allocatable") or {}
+                for res, count in (want.items() if isinstance(want, dict) else [(RESOURCE_NAME, want)]):
+                    if int(alloc.get(res, "0")) != count:
+                        return False
         return True
 
-    def wait_ready(self, timeout: float = 60.0, expect_allocatable: dict[str, int] | None = None) -> float:
+    def wait_ready(self, timeout: float = 60.0, expect_allocatable: dict[str, int | dict] | None = None) -> float:
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < timeout:
             if self.is_ready(expect_allocatable):

@@ -45,6 +45,8 @@ READY_FILES = {
     "workload": "workload-ready",
     "plugin": "plugin-ready",
     "complete": "validated",
+    "vfio": "vfio-ready",          # sandbox workloads: GPUs bound to vfio-pci
+    "sandbox": "sandbox-validated",
 }
 VALIDATED_LABEL = "amd.com/gpu.validated"
 MFMA_LABEL = "amd.com/gpu.validated.mfma"  # data types whose MFMA tile checked out on every GPU
@@ -649,3 +651,32 @@ def complete(env: NodeEnv) -> dict:
     env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": labels, "annotations": ann}})
     write_ready(env, "complete", {"steps": steps, "mfma_dtypes": dtypes})
     return {"ok": True, "steps": steps, "mfma_dtypes": dtypes}
+
+
+# ------------------------------------------------------- sandbox workloads --
+
+def validate_vfio(env: NodeEnv, pci, timeout: float = 600.0, stop=None) -> dict:
+    """vm-passthrough node: the vfio-manager has run and every AMD GPU sits on
+    vfio-pci with its ``/dev/vfio/<group>`` node (retried until ``timeout``)."""
+    from ..sandbox.vfio import check_bound
+
+    t0 = time.perf_counter()
+    wait_ready(env, "vfio", timeout, stop)
+    deadline = time.monotonic() + timeout
+    for delay in env.waits():
+        ok, msg, detail = check_bound(pci)
+        if ok:
+            return {"ok": True, "message": msg, "gpus": detail, "seconds": time.perf_counter() - t0}
+        if time.monotonic() >= deadline or (stop is not None and stop.is_set()):
+            raise StepFailed(msg)
+        time.sleep(delay)
+
+
+def complete_sandbox(env: NodeEnv) -> dict:
+    """Mark a vm-passthrough node validated (same label as the container path)."""
+    vf = read_ready(env, "vfio") or {}
+    gpus = sum(len(g.get("gpus", [])) for g in vf.get("groups", []))
+    ann = {"amd.com/gpu.validation": json.dumps({"vfio": round(vf.get("seconds", 0.0), 4), "workload": "vm-passthrough"})}
+    env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": {VALIDATED_LABEL: "true"}, "annotations": ann}})
+    write_ready(env, "sandbox", {"gpus": gpus})
+    return {"ok": True, "gpus": gpus}
