@@ -36,6 +36,28 @@ EXPECTED_OPERANDS = {
     "amd-node-status-exporter": "nodeStatusExporter",
     "node-feature-discovery-worker": "nfd",
 }
+# vm-passthrough nodes (sandboxWorkloads) run these instead of the container operands
+EXPECTED_SANDBOX_OPERANDS = {
+    "amd-vfio-manager": "vfioManager",
+    "amd-sandbox-validator": "validator",
+    "amd-sandbox-device-plugin-daemonset": "sandboxDevicePlugin",
+}
+PASSTHROUGH_LABEL = "amd.com/gpu.deploy.vfio-manager"
+
+
+def _passthrough(node: dict) -> bool:
+    return (node["metadata"].get("labels") or {}).get(PASSTHROUGH_LABEL) == "true"
+
+
+def _count(allocs: dict, match) -> int:
+    n = 0
+    for k, v in allocs.items():
+        if match(k):
+            try:
+                n += int(v)
+            except ValueError:
+                pass
+    return n
 
 
 @dataclass
@@ -92,16 +114,24 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
     for n in gpu_nodes:
         name = n["metadata"]["name"]
         labels = n["metadata"].get("labels") or {}
+        allocs = (n.get("status") or {}).get("allocatable") or {}
+        if _passthrough(n):
+            # VM passthrough: the GPUs are amd.com/<product> (vfio-pci), not amd.com/gpu
+            from ..sandbox.plugin import PRODUCT_NAMES
+
+            names = {f"amd.com/{p}" for p in PRODUCT_NAMES.values()}
+            count = _count(allocs, lambda k: k in names or k.startswith("amd.com/AMD_GPU_"))
+            want = expect_gpus_per_node
+            rep.add(f"allocatable[{name}]", count > 0 and (want is None or count == want),
+                    f"vm-passthrough amd.com/<product>={count}" + (f" (expected {want})" if want else ""),
+                    "README.md:122")
+            validated = labels.get("amd.com/gpu.validated") == "true"
+            rep.add(f"validated[{name}]", validated, "GPUs on vfio-pci" if validated else "not validated",
+                    "README.md:199")
+            continue
         # amd.com/gpu, partition (-cpx ...) and time-sliced (.shared / renamed) resources all count;
         # time-slicing multiplies the advertised devices by the replicas GFD publishes
-        allocs = (n.get("status") or {}).get("allocatable") or {}
-        count = 0
-        for k, v in allocs.items():
-            if k == RESOURCE_NAME or k.startswith((RESOURCE_NAME + "-", RESOURCE_NAME + ".")):
-                try:
-                    count += int(v)
-                except ValueError:
-                    pass
+        count = _count(allocs, lambda k: k == RESOURCE_NAME or k.startswith((RESOURCE_NAME + "-", RESOURCE_NAME + ".")))
         try:
             replicas = max(1, int(labels.get("amd.com/gpu.replicas", "1")))
         except ValueError:
@@ -131,8 +161,10 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
     rep.add("operand-pods-running", bool(pods) and not bad,
             f"{len(pods)} pod(s) in {namespace}; failing: {bad or 'none'}", "README.md:116,195-207")
 
+    container_nodes = [n for n in gpu_nodes if not _passthrough(n)]
+    vm_nodes = [n for n in gpu_nodes if _passthrough(n)]
     drv = [p for p in pods if p["metadata"]["name"].startswith("amd-driver-daemonset")]
-    drv_ok = bool(drv) or not gpu_nodes
+    drv_ok = bool(drv) or not container_nodes
     details = []
     for p in drv:
         ok, d = _pod_ok(p)
@@ -148,7 +180,10 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
         cp = []
     spec = (cp[0].get("spec") if cp else {}) or {}
     missing = [ds for ds, key in EXPECTED_OPERANDS.items()
-               if (spec.get(key) or {}).get("enabled", True) and gpu_nodes and ds not in present]
+               if (spec.get(key) or {}).get("enabled", True) and ds not in present
+               and (container_nodes if key != "nfd" else gpu_nodes)]
+    missing += [ds for ds, key in EXPECTED_SANDBOX_OPERANDS.items()
+                if vm_nodes and (spec.get(key) or {}).get("enabled", True) and ds not in present]
     rep.add("operands-deployed", not missing, f"missing: {missing or 'none'}", "README.md:201-207")
     state = ((cp[0].get("status") or {}).get("state") if cp else "absent")
     rep.add("cluster-policy-ready", state == "ready", f"ClusterPolicy state={state}", "README.md:101 (--wait)")

@@ -179,6 +179,11 @@ def test_sim_container_and_passthrough_nodes(tmp_path):
         assert "amd-vfio-manager" in pods and "amd-driver-daemonset" not in pods
         alloc = c.client.get("v1", "Node", "vm-0")["status"]["allocatable"]
         assert int(alloc.get("amd.com/gpu", "0")) == 0
+        from amdgpu_operator.cli.verify import verify
+
+        rep = verify(c.client, c.namespace, 2)  # the reference's checks pass on a mixed cluster
+        assert rep.ok, rep.table()
+        assert "vm-passthrough amd.com/<product>=2" in next(x.detail for x in rep.checks if x.name == "allocatable[vm-0]")
         # back to containers: GPUs return to amdgpu, the container path validates the node again
         c.client.patch("v1", "Node", "vm-0", {"metadata": {"labels": {WORKLOAD_CONFIG_LABEL: "container"}}})
         deadline = time.time() + 60
