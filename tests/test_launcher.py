@@ -21,14 +21,20 @@ def test_processes_run_on_owner_rank(nproc, port):
     assert "LAUNCHER_OK" in p.stdout, p.stdout[-2000:] + p.stderr[-3000:]
 
 
-def test_bench_two_ranks_with_stand_in_validators():
-    p = _torchrun(2, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--fake-gpu-procs", port=29613)
+@pytest.mark.parametrize("nproc,warmup,port", [(2, 0, 29613), (8, 1, 29614)])
+def test_bench_ranks_with_stand_in_validators(nproc, warmup, port):
+    """The driver's scaling launch (torchrun, one rank per GPU) on CPU: 8 ranks
+    and a warm-up phase exercise the launcher hand-over between phases."""
+    p = _torchrun(nproc, "bench.py", "--gpus", str(nproc), "--steps", "1", "--warmup", str(warmup),
+                  "--fake-gpu-procs", port=port)
     assert p.returncode == 0, p.stderr[-3000:]
     import json
 
-    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
-    out = json.loads(line)
-    assert out["n_gpus"] == 2 and out["config"]["allocatable_amd_com_gpu"] == 2
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 prints the one JSON line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == nproc and out["config"]["allocatable_amd_com_gpu"] == nproc
+    assert out["config"]["parallelism"] == f"dp{nproc}" and out["steps"] == 1 and out["warmup"] == warmup
 
 
 def test_run_local_takes_the_report_before_the_exit():
