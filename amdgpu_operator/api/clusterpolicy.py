@@ -104,6 +104,7 @@ class ToolkitSpec(Operand):
     acceptDeviceListAsVolumeMounts: bool = False
     acceptEnvvarUnprivileged: bool = True
     setAsDefault: bool = False  # make the amd runtime containerd's default_runtime_name
+    cleanupOnExit: bool = True  # restore the runtime config when the toolkit pod goes (helm uninstall)
 
 
 class DevicePluginConfigRef(_M):

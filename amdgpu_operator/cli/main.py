@@ -90,8 +90,14 @@ def main(argv: list[str] | None = None) -> int:
             client = None  # node-local operands (driver, toolkit) work without the API
         env = NodeEnv.from_environ(client)
         import os
+        import signal
 
-        return run_operand(env, argv, threading.Event(), container_env=dict(os.environ))
+        # the kubelet stops a container with SIGTERM: operands then run their
+        # shutdown (toolkit cleanup, vfio unbind, plugin socket removal)
+        stop = threading.Event()
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            signal.signal(sig, lambda *_: stop.set())
+        return run_operand(env, argv, stop, container_env=dict(os.environ))
 
     ap = argparse.ArgumentParser(prog="amdgpu-operator")
     sub = ap.add_subparsers(dest="cmd", required=True)

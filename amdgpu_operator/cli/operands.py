@@ -250,8 +250,12 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             # a driver reload / loss clears toolkit-ready: redo the install (the
             # CDI spec follows the new device nodes) once the driver is back
             tk.keep_ready(env, stop, lambda: tk.install(env, **kw), interval=max(env.poll_s, 0.01))
+            if cenv.get("CLEANUP_ON_EXIT", "true") == "true":
+                # pod deleted (helm uninstall, toolkit disabled, node no longer a
+                # GPU node): the runtime goes back to the node's own configuration
+                tk.uninstall(env, pid_file=kw["pid_file"])
         else:
-            tk.uninstall(env)
+            tk.uninstall(env, pid_file=cenv.get("RUNTIME_PID_FILE") or None)
         return 0
 
     if cmd == "validate":

@@ -274,6 +274,7 @@ def state_toolkit(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
            {"name": "ACCEPT_DEVICE_LIST_AS_VOLUME_MOUNTS", "value": str(t.acceptDeviceListAsVolumeMounts).lower()},
            {"name": "ACCEPT_ENVVAR_UNPRIVILEGED", "value": str(t.acceptEnvvarUnprivileged).lower()},
            {"name": "CONTAINERD_SET_AS_DEFAULT", "value": str(t.setAsDefault).lower()},
+           {"name": "CLEANUP_ON_EXIT", "value": str(t.cleanupOnExit).lower()},
            ] + list(t.env)
     # the runtime's host directories are mounted at their host paths, so the
     # paths the installer writes into the runtime's configuration (imports,

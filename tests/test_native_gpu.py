@@ -171,6 +171,24 @@ def test_smi_collector_and_health_watcher():
         hw.close()
 
 
+def test_driver_smi_table_on_mi355x(tmp_path):
+    """``kubectl exec ... -c amd-driver-ctr -- amdgpu-operator driver smi``:
+    the table the reference reads off nvidia-smi (README.md:152-167), from the
+    real sysfs and libamd_smi."""
+    from amdgpu_operator.driver import manager as DM
+    from amdgpu_operator.nodeenv import NodeEnv
+
+    table = DM.smi_table(NodeEnv(node_name="box", client=None, host_root="/", validations_dir=str(tmp_path)))
+    rows = [r for r in table.splitlines() if "gfx950" in r]
+    assert rows, table
+    for r in rows:
+        cells = [c.strip() for c in r.strip("|").split("|")]
+        assert cells[3] == "256"
+        used, total = cells[5].removesuffix("MiB").split("/")
+        assert int(total) > 280 * 1024 and 0 <= int(used) <= int(total)  # 288 GB HBM3E per GPU
+        assert int(cells[6]) > 0 and int(cells[7]) > 0  # live power and temperature from amd-smi
+
+
 def test_metrics_exporter_live():
     from amdgpu_operator.exporter.metrics import MetricsExporter, SmiSource
 

@@ -54,6 +54,50 @@ def test_toolkit_install_idempotent(env):
     assert open(env.containerd_config + ".amd-backup").read() == "version = 2\n"
 
 
+def test_toolkit_container_cleans_up_on_sigterm(tmp_path):
+    """The real entry point (``amdgpu-operator toolkit install``) stopped by
+    the kubelet's SIGTERM restores containerd, withdraws toolkit-ready and
+    removes the hook, hooks.d entry and CDI spec; the runtime is signalled."""
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 2)
+    cfg = tmp_path / "etc/containerd/config.toml"
+    cfg.parent.mkdir(parents=True)
+    cfg.write_text("version = 2\n")
+    runtime = subprocess.Popen([sys.executable, "-c", "import signal,time; signal.signal(signal.SIGHUP, lambda *a: "
+                                "print('reload', flush=True)); print('armed', flush=True); time.sleep(60)"],
+                               stdout=subprocess.PIPE, text=True)
+    assert runtime.stdout.readline().strip() == "armed"  # a SIGHUP before the handler would end it
+    pid_file = tmp_path / "containerd.pid"
+    pid_file.write_text(str(runtime.pid))
+    env = {**os.environ, "HOST_ROOT": root, "VALIDATIONS_DIR": str(tmp_path / "val"), "CDI_SPEC_DIR": str(tmp_path / "cdi"),
+           "CONTAINERD_CONFIG": str(cfg), "INSTALL_DIR": str(tmp_path / "inst"), "RUNTIME": "containerd",
+           "RUNTIME_PID_FILE": str(pid_file), "VALIDATION_POLL_S": "0.05", "NODE_NAME": "n1"}
+    env.pop("KUBERNETES_SERVICE_HOST", None)
+    p = subprocess.Popen([sys.executable, "-m", "amdgpu_operator", "toolkit", "install"], env=env,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        ready = tmp_path / "val" / "toolkit-ready"
+        deadline = time.time() + 60
+        while time.time() < deadline and not ready.exists():
+            time.sleep(0.05)
+        assert ready.exists() and "imports" in cfg.read_text()
+        assert (tmp_path / "cdi" / "amd.com-gpu.json").exists()
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(30) == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert cfg.read_text() == "version = 2\n" and not ready.exists()
+    assert not (tmp_path / "cdi" / "amd.com-gpu.json").exists() and not (tmp_path / "inst" / TK.HOOK_NAME).exists()
+    runtime.kill()
+    assert runtime.stdout.read().count("reload") == 2  # install and uninstall each reloaded containerd
+
+
 @pytest.fixture
 def rt_env(env, tmp_path):
     env.crio_config_dir = str(tmp_path / "etc/crio/crio.conf.d")
