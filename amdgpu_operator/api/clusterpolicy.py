@@ -74,6 +74,9 @@ class DriverSpec(Operand):
     kernelModuleParams: dict[str, str] = Field(default_factory=dict)
     repository: str = ""  # package mirror for air-gapped clusters (default repo.radeon.com)
     startupProbeTimeoutSeconds: int = 600
+    # unload the module this driver container installed when the container
+    # stops (not while GPU processes hold it; never a host-managed module)
+    unloadOnExit: bool = True
     upgradePolicy: UpgradePolicy = Field(default_factory=UpgradePolicy)
     # per-node-pool drivers: one driver DaemonSet per AMDGPUDriver object
     # (api/driver_cr.py) instead of the single ClusterPolicy-wide one

@@ -223,6 +223,8 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             drv.install(env, stop=stop, cenv=cenv)
             ready()
             stop.wait()
+            if cenv.get("AMDGPU_UNLOAD_ON_EXIT", "true") == "true":
+                drv.cleanup_on_exit(env)
         elif a.action == "monitor":
             ready()
             drv.monitor(env, stop, interval=max(env.poll_s, min(a.interval, 10.0)))

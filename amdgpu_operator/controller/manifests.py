@@ -228,7 +228,8 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-drive
            {"name": "AMDGPU_USE_PRECOMPILED", "value": str(d.usePrecompiled).lower()},
            {"name": "AMDGPU_BLACKLIST_INBOX", "value": str(d.blacklistAmdgpuInbox).lower()},
            {"name": "AMDGPU_MODULE_PARAMS", "value": " ".join(f"{k}={v}" for k, v in sorted(d.kernelModuleParams.items()))},
-           {"name": "AMDGPU_WAIT_SECONDS", "value": str(d.startupProbeTimeoutSeconds)}
+           {"name": "AMDGPU_WAIT_SECONDS", "value": str(d.startupProbeTimeoutSeconds)},
+           {"name": "AMDGPU_UNLOAD_ON_EXIT", "value": str(d.unloadOnExit).lower()}
            ] + ([{"name": "AMDGPU_REPO_BASE", "value": d.repository}] if d.repository else []) + list(d.env)
     mounts = [_mount("run-amd", "/run/amd", propagation="Bidirectional"), _mount("host-root", "/host", ro=True,
                                                                                  propagation="HostToContainer"),

@@ -180,8 +180,11 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
     cur = loaded_version(env)
     if ran_script and want and cur != want:
         raise RuntimeError(f"installed driver reports version {cur or 'none'}, requested {want}")
-    host_managed = not ran_script and not cur
-    _write_state(env, {"version": cur, "specHash": spec_hash, "installed": ran_script, "hostManaged": host_managed,
+    # a restarted driver pod finds the module its predecessor installed: it stays ours
+    prev = read_state(env)
+    installed = ran_script or bool(prev.get("installed") and prev.get("version") == cur and live)
+    host_managed = not installed and not cur
+    _write_state(env, {"version": cur, "specHash": spec_hash, "installed": installed, "hostManaged": host_managed,
                        "ts": round(time.time(), 3)})
     try:
         env.client.patch("v1", "Node", env.node_name, {"metadata": {"annotations": {
@@ -193,6 +196,39 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
            "host_managed": host_managed, "seconds": time.perf_counter() - t0}
     write_ready(env, "driver", out)
     return out
+
+
+def kfd_users(env: NodeEnv) -> list[str]:
+    """PIDs with the GPU open (``/sys/class/kfd/kfd/proc/<pid>``)."""
+    try:
+        return sorted(p for p in os.listdir(os.path.join(env.sysfs_root(), "sys/class/kfd/kfd/proc")) if p.isdigit())
+    except OSError:
+        return []
+
+
+def cleanup_on_exit(env: NodeEnv) -> dict:
+    """``amd-driver-ctr`` stopped (SIGTERM: helm uninstall, driver disabled, node
+    left the GPU pool): unload the module this container installed, like the
+    upstream driver container's shutdown.  A host-managed or inbox module is
+    left alone, and so is one that still has GPU users (logged: the next driver
+    pod's ``prepare-upgrade`` handles a version change after the drain)."""
+    st = read_state(env)
+    if not st.get("installed"):
+        return {"unloaded": False, "reason": "module not installed by the driver container"}
+    users = kfd_users(env)
+    if users:
+        log.warning("driver stays loaded: GPU in use by %d process(es) %s", len(users), users[:8])
+        return {"unloaded": False, "reason": f"in use by {users[:8]}"}
+    _release_gated_validators(env)
+    clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
+    try:
+        _kmod(env).unload(env)
+    except Exception as e:  # noqa: BLE001 - leave it loaded, say why
+        log.warning("driver unload on exit failed: %s", e)
+        return {"unloaded": False, "reason": str(e)}
+    _write_state(env, None)
+    log.info("amdgpu unloaded on driver container exit")
+    return {"unloaded": True}
 
 
 def monitor_once(env: NodeEnv) -> bool:

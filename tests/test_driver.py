@@ -247,6 +247,32 @@ def test_install_without_installer(node_env, monkeypatch, tmp_path):
     assert node_env.client.get("v1", "Node", "n1")["metadata"]["annotations"]["amd.com/gpu-driver.version"] == "host"
 
 
+def test_driver_container_exit_unloads_only_its_own_idle_module(node_env):
+    kmod = fakesys.SimModule(node_env.sysfs_root())
+    node_env.extra["kmod"] = kmod
+    cenv = {"AMDGPU_DRIVER_VERSION": "6.14.0", "AMDGPU_DRIVER_SPEC_HASH": "h2"}
+    DM.install(node_env, timeout=5, cenv=cenv)
+    # a restarted driver pod keeps the module as container-installed
+    assert not DM.install(node_env, timeout=5, cenv=cenv)["installed"] and DM.read_state(node_env)["installed"]
+    kfd_proc = os.path.join(node_env.sysfs_root(), "sys/class/kfd/kfd/proc/4242")
+    os.makedirs(kfd_proc)
+    out = DM.cleanup_on_exit(node_env)  # a GPU process holds it: stays
+    assert not out["unloaded"] and "4242" in out["reason"] and DM.loaded_version(node_env) == "6.14.0"
+    os.rmdir(kfd_proc)
+    V.write_ready(node_env, "workload", {"ok": True})
+    assert DM.cleanup_on_exit(node_env)["unloaded"]
+    assert kmod.log[-1] == "unload" and DM.loaded_version(node_env) == "" and DM.read_state(node_env) == {}
+    assert V.read_ready(node_env, "driver") is None and V.read_ready(node_env, "workload") is None
+
+
+def test_driver_container_exit_leaves_a_host_module(node_env):
+    kmod = fakesys.SimModule(node_env.sysfs_root())
+    node_env.extra["kmod"] = kmod
+    DM.install(node_env, timeout=5, cenv={"AMDGPU_DRIVER_VERSION": "6.12.12"})  # already live: not ours
+    out = DM.cleanup_on_exit(node_env)
+    assert not out["unloaded"] and kmod.log == [] and DM.loaded_version(node_env) == "6.12.12"
+
+
 def test_prepare_upgrade_unloads_the_old_module(node_env):
     kmod = fakesys.SimModule(node_env.sysfs_root())
     node_env.extra["kmod"] = kmod
