@@ -10,6 +10,7 @@ environment and the pod's stop event.
 from __future__ import annotations
 
 import argparse
+import os
 import threading
 import time
 
@@ -505,6 +506,8 @@ def run_in_sim(cluster, run, container: dict, argv: list[str], init: bool) -> No
     """Simulated kubelet hook: run the operand for ``container`` of ``run``'s pod."""
     cenv = {e["name"]: e["value"] for e in container.get("env", []) if "value" in e}
     env = run.node.env
+    if cenv.get("RUNTIME_PID_FILE"):  # never signal the machine's own container runtime
+        cenv["RUNTIME_PID_FILE"] = os.path.join(run.node.dir, cenv["RUNTIME_PID_FILE"].lstrip("/"))
     env.extra.setdefault("ephemeral_ports", True)
     env.extra.setdefault("no_health", True)
 
