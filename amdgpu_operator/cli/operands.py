@@ -174,12 +174,17 @@ def _validate(env, a, extra, stop, ready) -> int:
         _node_event(env, "Normal", "GPUValidated", f"{res['gpus']} GPU(s) ready for VM passthrough")
         ready()
         stop.wait()
+        V.clear_ready(env, ("sandbox",))
     else:
         res = V.complete(env)
         steps = ", ".join(f"{k} {v:.2f} s" for k, v in res["steps"].items() if v is not None)
         _node_event(env, "Normal", "GPUValidated", f"GPUs validated ({steps})" if steps else "GPUs validated")
         ready()
         stop.wait()
+        # the validator pod goes (new validator image, uninstall): what it
+        # validated is withdrawn, so its successor validates again (the driver
+        # and toolkit files belong to their own operands)
+        V.clear_ready(env, ("workload", "plugin", "complete"))
     return 0
 
 

@@ -130,6 +130,29 @@ def test_driver_loss_triggers_revalidation(cluster_factory):
     assert monitor_once(env) is True
 
 
+def test_replaced_validator_pod_validates_again(cluster_factory):
+    """Deleting the validator pod withdraws its workload/plugin/validated
+    files; the DaemonSet's replacement runs the GPU checks again (the
+    toolkit's file stays with its operand)."""
+    c = cluster_factory([NodeSpec("gpu-1", 2)])
+    c.install_operator(REF)
+    c.wait_ready(60, {"gpu-1": 2})
+    env = c.nodes["gpu-1"].env
+    from amdgpu_operator.validator.validate import read_ready
+
+    before = read_ready(env, "workload")["time"]
+    toolkit_before = read_ready(env, "toolkit")["time"]
+    pod = next(p for p in c.pods() if p["metadata"]["name"].startswith("amd-operator-validator"))
+    c.client.delete("v1", "Pod", pod["metadata"]["name"], c.namespace)
+    deadline = time.time() + 60
+    while time.time() < deadline and (read_ready(env, "complete") is None
+                                      or (read_ready(env, "workload") or {}).get("time", 0) <= before):
+        time.sleep(0.05)
+    assert read_ready(env, "workload")["time"] > before and read_ready(env, "complete") is not None
+    assert read_ready(env, "toolkit")["time"] == toolkit_before  # the toolkit's own file stays
+    c.wait_ready(60, {"gpu-1": 2})
+
+
 def test_metrics_and_node_status_exporters_serve(cluster_factory):
     c = cluster_factory([NodeSpec("gpu-1", 2)])
     c.install_operator(REF)
