@@ -137,7 +137,11 @@ def _vfio_manager(env: NodeEnv, a, stop: threading.Event, ready) -> int:
             bind()
         except VF.VfioError as e:
             log.error("vfio rebind: %s", e)
-    node = _get_or_empty(env.client, "Node", env.node_name) if env.client is not None else {}
+    try:
+        node = _get_or_empty(env.client, "Node", env.node_name) if env.client is not None else {}
+    except Exception as e:  # noqa: BLE001 - API unreachable: keep the GPUs where running VMs expect them
+        log.warning("vfio-manager exit: cannot read node %s: %s", env.node_name, e)
+        node = {}
     label = DEPLOY_LABEL.format(OPERAND_LABELS["vfioManager"])
     if node and (node["metadata"].get("labels") or {}).get(label) != "true":
         VF.unbind_all(pci)

@@ -477,7 +477,9 @@ def state_vfio_manager(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
                       _mount("run-amd-validations", VALIDATIONS_HOST_DIR)], list(m.env), True, m.resources.model_dump())
     vols = [_hostpath("host-sys", "/sys", "Directory"), _hostpath("host-dev", "/dev", "Directory"),
             _hostpath("lib-modules", "/lib/modules", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
-    return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "vfioManager", sa, [ctr], [], vols, host_pid=True)]
+    # reads its Node at exit: GPUs go back to amdgpu only when the node left vm-passthrough
+    return [_sa(sa, ns, owner), _cluster_role(sa, PLUGIN_CONFIG_RULES[:1], owner), _cluster_binding(sa, sa, ns, owner),
+            _daemonset(spec, ns, owner, name, "vfioManager", sa, [ctr], [], vols, host_pid=True)]
 
 
 def state_sandbox_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
