@@ -70,6 +70,11 @@ class SimNode:
     terminating: set = field(default_factory=set)  # pods between graceful delete and removal
 
 
+class AdmissionError(RuntimeError):
+    """The kubelet could not allocate a pod's devices (the pod fails with
+    reason ``UnexpectedAdmissionError``, as on a real kubelet)."""
+
+
 def fake_validator_result(argv: list[str]) -> ProcResult:
     """Synthetic ``amdgpu-validator`` output for CPU-only runs."""
     def arg(name, default):
@@ -165,12 +170,14 @@ class _PodRun:
             self._status("Running", True)
             threads = []
             errors = []
+            reason = []
             for c in spec.get("containers", []):
                 def body(c=c):
                     try:
                         self.cluster.run_container(self, c, init=False)
                     except Exception as e:  # noqa: BLE001
                         errors.append(f"{c['name']}: {e}")
+                        reason.append("UnexpectedAdmissionError" if isinstance(e, AdmissionError) else "Error")
                 th = threading.Thread(target=body, daemon=True, name=f"ctr-{self.name}-{c['name']}")
                 th.start()
                 threads.append(th)
@@ -180,7 +187,7 @@ class _PodRun:
                 return False
             if errors:
                 log.warning("pod %s failed: %s", self.name, "; ".join(errors))
-                self._status("Failed", True, "Error", "; ".join(errors))
+                self._status("Failed", True, reason[0] if reason else "Error", "; ".join(errors))
                 return True
             self._status("Succeeded", True, "Completed")
             return False
@@ -630,8 +637,11 @@ class SimCluster:
         if gpu_res:
             res, n = gpu_res[0]
             if not node.kubelet.wait_registered(res, timeout=30):
-                raise RuntimeError(f"resource {res} not registered on {node.spec.name}")
-            ids, resp = node.kubelet.allocate(res, n, run.ns, run.name, c["name"])
+                raise AdmissionError(f"resource {res} not registered on {node.spec.name}")
+            try:
+                ids, resp = node.kubelet.allocate(res, n, run.ns, run.name, c["name"])
+            except RuntimeError as e:
+                raise AdmissionError(str(e)) from e
             self.trace("gpu-pod-allocated", run.name)
             envs = dict(resp.envs)
             devices = [int(x) for x in envs.get("AMD_VISIBLE_DEVICES", "").split(",") if x != ""]

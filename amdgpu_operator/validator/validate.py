@@ -421,11 +421,9 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
         plan = node_plan(node)
     t_alloc = time.perf_counter() - t0
     marks = {"start": time.time() - (time.perf_counter() - t0), "devices_seen": time.time()}
-    run_id = uuid.uuid4().hex[:8]
     pod_args = list(pod_args or ["--steps", "hip,vecadd,gemm", "--gemm", "1024"])
-    names = []
-    for i, res in enumerate(r for r, n in sorted(plan.items()) for _ in range(n)):
-        name = f"amd-validator-workload-{run_id}-{i}"
+
+    def make_pod(name: str, run_id: str, res: str) -> dict:
         pod = {
             "apiVersion": "v1", "kind": "Pod",
             "metadata": {"name": name, "namespace": env.namespace,
@@ -441,28 +439,52 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
         }
         if pull_secrets:
             pod["spec"]["imagePullSecrets"] = [{"name": x} for x in pull_secrets]
-        env.client.create(pod)
-        names.append(name)
-    marks["pods_created"] = time.time()
+        return pod
 
     def phase(o):
         return (o.get("status") or {}).get("phase", "Pending")
 
-    live, _ = wait_for(env.client, "v1", "Pod", lambda objs: all(
-        n in objs and phase(objs[n]) in ("Succeeded", "Failed") for n in names), namespace=env.namespace,
-        label_selector=f"{WORKLOAD_POD_LABEL}={run_id}", timeout=max(0.0, deadline - time.monotonic()),
-        stop=stop, poll_s=env.poll_s)
-    phases = {n: phase(live[n]) if n in live else "Missing" for n in names}
-    pods = [live.get(n) or {} for n in names]
-    devices = [((p.get("metadata", {}).get("annotations") or {}).get("amd.com/gpu.allocated", "")) for p in pods]
-    for n in names:
-        try:
-            env.client.delete("v1", "Pod", n, env.namespace)
-        except Exception:  # noqa: BLE001
-            pass
-    if not all(p == "Succeeded" for p in phases.values()):
-        raise StepFailed(f"plugin validation pods did not succeed: {phases}")
-    summary = {"ok": True, "pods": len(names), "resources": plan, "devices": devices, "allocatable_wait_s": round(t_alloc, 4),
+    # a pod the kubelet could not admit (UnexpectedAdmissionError: the device
+    # list it planned from was stale, e.g. a re-registering plugin's devices
+    # still unhealthy) is run again; any other failure fails the step
+    todo = [r for r, n in sorted(plan.items()) for _ in range(n)]
+    devices: list[str] = []
+    attempts, backoff = 0, 0.05
+    while todo:
+        attempts += 1
+        run_id = uuid.uuid4().hex[:8]
+        names = {}
+        for i, res in enumerate(todo):
+            name = f"amd-validator-workload-{run_id}-{i}"
+            env.client.create(make_pod(name, run_id, res))
+            names[name] = res
+        marks.setdefault("pods_created", time.time())
+        live, _ = wait_for(env.client, "v1", "Pod", lambda objs: all(
+            n in objs and phase(objs[n]) in ("Succeeded", "Failed") for n in names), namespace=env.namespace,
+            label_selector=f"{WORKLOAD_POD_LABEL}={run_id}", timeout=max(0.0, deadline - time.monotonic()),
+            stop=stop, poll_s=env.poll_s)
+        for n in names:
+            try:
+                env.client.delete("v1", "Pod", n, env.namespace)
+            except Exception:  # noqa: BLE001
+                pass
+        phases = {n: phase(live[n]) if n in live else "Missing" for n in names}
+        retry = [n for n in names if phases[n] == "Failed"
+                 and (live[n].get("status") or {}).get("reason") == "UnexpectedAdmissionError"]
+        hard = {n: p for n, p in phases.items() if p != "Succeeded" and n not in retry}
+        if hard:
+            raise StepFailed(f"plugin validation pods did not succeed: {phases}")
+        devices += [((live[n].get("metadata", {}).get("annotations") or {}).get("amd.com/gpu.allocated", ""))
+                    for n in names if phases[n] == "Succeeded"]
+        todo = [names[n] for n in retry]
+        if todo:
+            if time.monotonic() + backoff >= deadline or (stop is not None and stop.is_set()):
+                raise StepFailed(f"plugin validation pods not admitted: {phases}")
+            log.info("%d plugin validation pod(s) not admitted, retrying in %.2f s", len(todo), backoff)
+            (stop.wait if stop is not None else time.sleep)(backoff)
+            backoff = min(backoff * 2, 2.0)
+    summary = {"ok": True, "pods": len(devices), "resources": plan, "devices": devices, "attempts": attempts,
+               "allocatable_wait_s": round(t_alloc, 4),
                "allocatable_source": source, "marks": {k: round(v, 4) for k, v in marks.items()},
                "seconds": time.perf_counter() - t0}
     write_ready(env, "plugin", summary)

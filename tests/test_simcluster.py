@@ -153,6 +153,40 @@ def test_replaced_validator_pod_validates_again(cluster_factory):
     c.wait_ready(60, {"gpu-1": 2})
 
 
+def test_plugin_pods_not_admitted_are_run_again(cluster_factory):
+    """The kubelet still lists the GPUs but cannot allocate them (devices
+    unhealthy, e.g. a plugin re-registering): the plugin pods fail with
+    UnexpectedAdmissionError and are run again in the same validation step."""
+    import threading
+
+    from amdgpu_operator.deviceplugin import api
+    from amdgpu_operator.validator.validate import read_ready
+
+    c = cluster_factory([NodeSpec("gpu-1", 2)])
+    c.install_operator(REF)
+    c.wait_ready(60, {"gpu-1": 2})
+    node = c.nodes["gpu-1"]
+    res = node.kubelet.resources["amd.com/gpu"]
+    with res.cv:
+        healthy = dict(res.devices)
+        res.devices = {i: api.UNHEALTHY for i in res.devices}
+
+    def heal():
+        with res.cv:
+            res.devices = healthy
+            res.cv.notify_all()
+
+    pod = next(p for p in c.pods() if p["metadata"]["name"].startswith("amd-operator-validator"))
+    t_del = time.time()
+    c.client.delete("v1", "Pod", pod["metadata"]["name"], c.namespace)
+    threading.Timer(0.5, heal).start()
+    deadline = time.time() + 60
+    while time.time() < deadline and (read_ready(node.env, "plugin") or {}).get("time", 0) < t_del:
+        time.sleep(0.05)
+    plug = read_ready(node.env, "plugin")
+    assert plug["ok"] and plug["attempts"] >= 2 and plug["pods"] == 2
+
+
 def test_metrics_and_node_status_exporters_serve(cluster_factory):
     c = cluster_factory([NodeSpec("gpu-1", 2)])
     c.install_operator(REF)
