@@ -1,0 +1,105 @@
+"""Randomized fault injection on the simulated cluster (CPU, fake GPUs).
+
+Two 2-GPU nodes and a CPU node under one ClusterPolicy with sandbox mode on.
+Each step injects one fault, lets it land, then requires the cluster to be
+Ready again with the allocatable each node's workload implies:
+
+  delpod      delete a random operand pod on a GPU node (the DaemonSet replaces it)
+  driverloss  the amdgpu module vanishes and comes back (driver monitor pass)
+  kubelet     the node's kubelet restarts (device plugins re-register)
+  switch      flip a node between container and vm-passthrough
+  spec        toggle gfd / the metrics exporter in the ClusterPolicy
+
+    python tools/chaos_sim.py --seeds 1-5 --steps 10
+
+Prints one line per step and, on a step that never converges, the cluster
+diagnostics; exits 1 if any seed failed.
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import random
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, deep_merge, parse_set_flags  # noqa: E402
+from amdgpu_operator.driver.manager import monitor_once  # noqa: E402
+from amdgpu_operator.sandbox import WORKLOAD_CONFIG_LABEL  # noqa: E402
+from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster  # noqa: E402
+
+FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec")
+
+
+def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
+    rnd = random.Random(seed)
+    d = tempfile.mkdtemp(prefix="chaos-")
+    c = SimCluster(os.path.join(d, "c"), [NodeSpec("g0", 2), NodeSpec("g1", 2), NodeSpec("cpu", 0)], fake_gpu=True,
+                   poll_s=0.005, agent_poll_s=0.05).start()
+    mode = {"g0": "container", "g1": "container"}
+
+    def expect():
+        return {n: (2 if m == "container" else {"amd.com/MI355X": 2}) for n, m in mode.items()}
+
+    try:
+        c.install_operator(deep_merge(parse_set_flags(REFERENCE_SET_FLAGS), {"sandboxWorkloads": {"enabled": True}}))
+        c.wait_ready(timeout, expect())
+        for i in range(steps):
+            fault, node = rnd.choice(FAULTS), rnd.choice(["g0", "g1"])
+            info = ""
+            if fault == "delpod":
+                pods = [p for p in c.pods() if p["spec"].get("nodeName") == node]
+                p = rnd.choice(pods)
+                info = p["metadata"]["name"]
+                c.client.delete("v1", "Pod", info, c.namespace)
+            elif fault == "driverloss" and mode[node] == "container":
+                env = c.nodes[node].env
+                f = os.path.join(env.host_root, "sys/module/amdgpu/initstate")
+                os.rename(f, f + ".gone")
+                monitor_once(env)  # the driver container's health monitor notices
+                os.rename(f + ".gone", f)
+            elif fault == "kubelet":
+                c.nodes[node].kubelet.restart()
+            elif fault == "switch":
+                mode[node] = "vm-passthrough" if mode[node] == "container" else "container"
+                c.client.patch("v1", "Node", node, {"metadata": {"labels": {WORKLOAD_CONFIG_LABEL: mode[node]}}})
+                info = mode[node]
+            elif fault == "spec":
+                cp = c.policy()
+                key = rnd.choice(["gfd", "dcgmExporter"])
+                cp["spec"][key]["enabled"] = not cp["spec"][key]["enabled"]
+                c.client.update(cp)
+                info = f"{key}={cp['spec'][key]['enabled']}"
+            time.sleep(settle_s)
+            t0 = time.time()
+            try:
+                c.wait_ready(timeout, expect())
+            except TimeoutError as e:
+                print(f"seed {seed} step {i} {fault} {node} {info}: NOT READY after {timeout:.0f} s\n{e}", flush=True)
+                return False
+            print(f"seed {seed} step {i} {fault} {node} {info}: ready {time.time() - t0:.2f} s after settling",
+                  flush=True)
+        return True
+    finally:
+        c.stop()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seeds", default="1-3", help="N or A-B")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--settle-s", type=float, default=0.5, help="let the fault land before checking readiness")
+    ap.add_argument("--timeout", type=float, default=60.0)
+    a = ap.parse_args()
+    lo, _, hi = a.seeds.partition("-")
+    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout) for s in range(int(lo), int(hi or lo) + 1)])
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
