@@ -290,12 +290,17 @@ def smi_table(env: NodeEnv) -> str:
 
     gpus = topology.enumerate_gpus(env.sysfs_root())
     metrics = {}
+    version = loaded_version(env)
     try:
         with topology.Smi() as smi:
             metrics = {m.bdf: m.values for m in smi.collect()}
+            version = version or smi.driver_version()  # inbox/DKMS modules without a sysfs version
     except Exception:  # noqa: BLE001 - table without live metrics
         pass
-    lines = [f"amd-gpu-operator driver {loaded_version(env) or 'unknown'}",
+    from ..discovery.labels import rocm_version
+
+    rocm = rocm_version(env.sysfs_root())
+    lines = [f"amd-gpu-operator driver {version or 'unknown'}" + (f"   ROCm {rocm}" if rocm else ""),
              "+-----+--------------+--------+-----+-----------+-----------------+---------+-------+",
              "| GPU | BDF          | Arch   | CUs | Partition | HBM used/total  | Power W | Temp C|",
              "+-----+--------------+--------+-----+-----------+-----------------+---------+-------+"]
