@@ -231,19 +231,69 @@ def cleanup_on_exit(env: NodeEnv) -> dict:
     return {"unloaded": True}
 
 
+LOST_MARKER = ".driver-lost"
+# operands that hold per-driver-instance state: restarted once the driver is back
+RESTART_ON_RECOVERY = ("amd-operator-validator", "amd-device-plugin-daemonset")
+
+
+def _restart_node_operands(env: NodeEnv, apps=RESTART_ON_RECOVERY) -> list[str]:
+    out = []
+    if env.client is None:
+        return out
+    for app in apps:
+        try:
+            pods = env.client.list("v1", "Pod", env.namespace, label_selector=f"app={app}",
+                                   field_selector=f"spec.nodeName={env.node_name}")
+            for pod in pods:
+                env.client.delete("v1", "Pod", pod["metadata"]["name"], env.namespace)
+                out.append(pod["metadata"]["name"])
+        except Exception as e:  # noqa: BLE001 - next monitor pass retries nothing; log it
+            log.warning("could not restart %s on %s: %s", app, env.node_name, e)
+    return out
+
+
 def monitor_once(env: NodeEnv) -> bool:
+    """``amd-driver-health``: one pass of the driver watch.
+
+    Driver lost (probe fails while ``driver-ready`` stands): every validation
+    is withdrawn, the node's ``amd.com/gpu.validated`` label with it, and the
+    loss is remembered.  Driver back after a loss: ``driver-ready`` is written
+    again (the toolkit reinstalls on it) and the validator and device-plugin
+    pods of this node are restarted, so the GPUs are validated and advertised
+    afresh; until then the ClusterPolicy reports the node not validated."""
     from ..discovery import topology
+    from ..validator.validate import MFMA_LABEL, VALIDATED_LABEL
 
     ok, msg = topology.probe(env.sysfs_root())
     path = env.validation_file(READY_FILES["driver"])
+    marker = env.validation_file(LOST_MARKER)
     if not ok and os.path.exists(path):
         log.error("driver lost: %s", msg)
+        os.makedirs(env.validations_dir, exist_ok=True)
+        with open(marker, "w") as f:
+            f.write(msg)
         clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
+        if env.client is not None:
+            try:
+                env.client.patch("v1", "Node", env.node_name,
+                                 {"metadata": {"labels": {VALIDATED_LABEL: None, MFMA_LABEL: None}}})
+            except Exception as e:  # noqa: BLE001
+                log.warning("could not withdraw %s: %s", VALIDATED_LABEL, e)
+    elif ok and os.path.exists(marker) and not os.path.exists(path):
+        gpus = topology.enumerate_gpus(env.sysfs_root())
+        write_ready(env, "driver", {"ok": True, "message": msg, "gpus": len(gpus), "recovered": True,
+                                    "driver_version": loaded_version(env), "seconds": 0.0})
+        os.unlink(marker)
+        restarted = _restart_node_operands(env)
+        log.info("driver back (%s); restarted %s", msg, restarted)
     return ok
 
 
 def monitor(env: NodeEnv, stop: threading.Event, interval: float = 10.0) -> None:
-    while not stop.wait(interval):
+    """Watch the driver every ``interval``; while it is lost, every second
+    (the node is unvalidated until the driver is seen again)."""
+    lost = env.validation_file(LOST_MARKER)
+    while not stop.wait(min(interval, 1.0) if os.path.exists(lost) else interval):
         monitor_once(env)
 
 

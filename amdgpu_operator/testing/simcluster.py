@@ -553,7 +553,10 @@ class SimCluster:
         delay = min(grace, self.termination_s or 0.0)
 
         def finish():
-            if not self.stop_event.wait(delay):
+            t0 = time.monotonic()
+            if run is not None:  # like the kubelet: the delete is confirmed once the containers exited
+                run.thread.join(grace)  # (their shutdown included), or the grace period ran out
+            if not self.stop_event.wait(max(0.0, delay - (time.monotonic() - t0))):
                 try:
                     self.client.delete("v1", "Pod", name, ns, grace_period_seconds=0)
                 except NotFound:
@@ -708,6 +711,15 @@ class SimCluster:
                     if int(alloc.get(res, "0")) != count:
                         return False
         return True
+
+    def wait_for_state(self, state: str, timeout: float = 30.0) -> bool:
+        """Wait until the ClusterPolicy reports ``state``."""
+        deadline = time.perf_counter() + timeout
+        while time.perf_counter() < deadline:
+            if ((self.policy() or {}).get("status") or {}).get("state") == state:
+                return True
+            time.sleep(self.poll_s)
+        return False
 
     def wait_ready(self, timeout: float = 60.0, expect_allocatable: dict[str, int | dict] | None = None) -> float:
         t0 = time.perf_counter()

@@ -126,8 +126,17 @@ def test_driver_loss_triggers_revalidation(cluster_factory):
     assert monitor_once(env) is False
     assert not os.path.exists(env.validation_file("driver-ready"))
     assert not os.path.exists(env.validation_file("validated"))
+    assert "amd.com/gpu.validated" not in labels(c, "gpu-1")  # the policy sees the node unvalidated
+    assert c.wait_for_state("notReady", 10)
+    old_validator = next(p["metadata"]["uid"] for p in c.pods() if p["metadata"]["name"].startswith(
+        "amd-operator-validator"))
     os.rename(initstate + ".gone", initstate)
     assert monitor_once(env) is True
+    # back: driver-ready again, the toolkit reinstalls, a fresh validator validates the node
+    assert os.path.exists(env.validation_file("driver-ready"))
+    c.wait_ready(60, {"gpu-1": 2})
+    assert old_validator not in {p["metadata"]["uid"] for p in c.pods()}
+    assert os.path.exists(env.validation_file("toolkit-ready"))
 
 
 def test_replaced_validator_pod_validates_again(cluster_factory):

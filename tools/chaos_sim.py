@@ -9,6 +9,7 @@ Ready again with the allocatable each node's workload implies:
   kubelet     the node's kubelet restarts (device plugins re-register)
   switch      flip a node between container and vm-passthrough
   spec        toggle gfd / the metrics exporter in the ClusterPolicy
+  upgrade     change driver.driverVersion (node-by-node driver upgrade)
 
     python tools/chaos_sim.py --seeds 1-5 --steps 10
 
@@ -33,7 +34,7 @@ from amdgpu_operator.driver.manager import monitor_once  # noqa: E402
 from amdgpu_operator.sandbox import WORKLOAD_CONFIG_LABEL  # noqa: E402
 from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster  # noqa: E402
 
-FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec")
+FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec", "upgrade")
 
 
 def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
@@ -75,6 +76,12 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
                 cp["spec"][key]["enabled"] = not cp["spec"][key]["enabled"]
                 c.client.update(cp)
                 info = f"{key}={cp['spec'][key]['enabled']}"
+            elif fault == "upgrade":
+                cp = c.policy()
+                cp["spec"]["driver"]["driverVersion"] = "6.14.0" if cp["spec"]["driver"]["driverVersion"] != "6.14.0" \
+                    else "6.12.12"
+                c.client.update(cp)
+                info = cp["spec"]["driver"]["driverVersion"]
             time.sleep(settle_s)
             t0 = time.time()
             try:
