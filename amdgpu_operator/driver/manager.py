@@ -195,6 +195,10 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
     out = {"ok": True, "message": msg, "gpus": len(gpus), "driver_version": cur, "installed": ran_script,
            "host_managed": host_managed, "seconds": time.perf_counter() - t0}
     write_ready(env, "driver", out)
+    try:  # validated afresh: an earlier loss is settled
+        os.unlink(env.validation_file(LOST_MARKER))
+    except FileNotFoundError:
+        pass
     return out
 
 

@@ -743,6 +743,12 @@ class SimCluster:
         for name, node in self.nodes.items():
             out["nodes"].setdefault(name, {})["validations"] = sorted(os.listdir(node.env.validations_dir)) \
                 if os.path.isdir(node.env.validations_dir) else []
+            kmod = node.env.extra.get("kmod")
+            if kmod is not None:
+                from ..driver.manager import read_state
+
+                out["nodes"][name]["module"] = {"live": kmod._live(), "log": list(getattr(kmod, "log", []))[-6:],
+                                                "state": read_state(node.env)}
         return json.dumps(out, indent=1, default=str)[:20000]
 
     def pods(self, namespace: str | None = None) -> list[dict]:

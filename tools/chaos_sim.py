@@ -41,7 +41,7 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
     rnd = random.Random(seed)
     d = tempfile.mkdtemp(prefix="chaos-")
     c = SimCluster(os.path.join(d, "c"), [NodeSpec("g0", 2), NodeSpec("g1", 2), NodeSpec("cpu", 0)], fake_gpu=True,
-                   poll_s=0.005, agent_poll_s=0.05).start()
+                   poll_s=0.005, agent_poll_s=0.05, termination_s=0.0).start()  # kubelet-confirmed pod deletes
     mode = {"g0": "container", "g1": "container"}
 
     def expect():
@@ -88,6 +88,8 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
                 c.wait_ready(timeout, expect())
             except TimeoutError as e:
                 print(f"seed {seed} step {i} {fault} {node} {info}: NOT READY after {timeout:.0f} s\n{e}", flush=True)
+                for t, what, detail in c.trace_since(0)[-120:]:
+                    print(f"  trace {t:9.3f} {what} {detail}")
                 return False
             print(f"seed {seed} step {i} {fault} {node} {info}: ready {time.time() - t0:.2f} s after settling",
                   flush=True)
