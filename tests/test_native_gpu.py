@@ -189,6 +189,26 @@ def test_driver_smi_table_on_mi355x(tmp_path):
         assert int(cells[6]) > 0 and int(cells[7]) > 0  # live power and temperature from amd-smi
 
 
+def test_pci_binding_view_on_mi355x():
+    """vfio-manager's PCI sysfs reader on the real host: the MI355X is an AMD
+    processing accelerator bound to amdgpu, so passthrough validation fails
+    closed and the sandbox plugin has nothing to advertise."""
+    from amdgpu_operator.discovery import topology as T
+    from amdgpu_operator.sandbox import plugin as SP
+    from amdgpu_operator.sandbox import vfio as VF
+
+    pci = VF.PciSysfs("/")
+    gpus = {g.bdf: g for g in pci.gpus()}
+    kfd = [g.bdf for g in T.enumerate_gpus("/")]
+    assert kfd and all(b in gpus for b in kfd), (kfd, sorted(gpus))
+    for b in kfd:
+        g = gpus[b]
+        assert g.device == 0x75A3 and g.cls.startswith("12") and g.driver == "amdgpu", g
+    ok, msg, _ = VF.check_bound(pci)
+    assert not ok and "amdgpu" in msg
+    assert SP.vfio_devices(pci) == [] and SP.resource_name(gpus[kfd[0]].device) == "amd.com/MI355X"
+
+
 def test_metrics_exporter_live():
     from amdgpu_operator.exporter.metrics import MetricsExporter, SmiSource
 
