@@ -85,6 +85,13 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
             time.sleep(settle_s)
             t0 = time.time()
             try:
+                if fault == "upgrade":  # ready is not enough: every container node runs the new driver
+                    want = info
+                    deadline = time.time() + timeout
+                    while time.time() < deadline and not all(
+                            (c.client.get("v1", "Node", n)["metadata"].get("annotations") or {}).get(
+                                "amd.com/gpu-driver.version") == want for n, m in mode.items() if m == "container"):
+                        time.sleep(0.05)
                 c.wait_ready(timeout, expect())
             except TimeoutError as e:
                 print(f"seed {seed} step {i} {fault} {node} {info}: NOT READY after {timeout:.0f} s\n{e}", flush=True)
