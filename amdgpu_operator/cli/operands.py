@@ -467,11 +467,27 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         profiles = env.extra.get("partition_profiles") or {
             "all-spx": {"compute": "SPX", "memory": "NPS1"}, "all-dpx": {"compute": "DPX", "memory": "NPS2"},
             "all-qpx": {"compute": "QPX", "memory": "NPS1"}, "all-cpx": {"compute": "CPX", "memory": "NPS2"}}
-        PM.reconcile_node(env, backend, profiles, default, a.config_label)
+        from ..kube.client import wait_for
+
+        res = PM.reconcile_node(env, backend, profiles, default, a.config_label)
         ready()
-        while not stop.wait(max(env.poll_s, min(a.interval, 30.0))):
+        applied = res.get("profile")
+        while not stop.is_set():
+            # event-driven like the MIG manager: a watch on this Node wakes on a
+            # partition-config label change; the interval is only a resync
             try:
-                PM.reconcile_node(env, backend, profiles, default, a.config_label)
+                wait_for(env.client, "v1", "Node",
+                         lambda objs: (((objs.get(env.node_name) or {}).get("metadata") or {}).get("labels") or {})
+                         .get(a.config_label, "default") != applied,
+                         name=env.node_name, timeout=max(env.poll_s, min(a.interval, 30.0)), stop=stop,
+                         poll_s=env.poll_s)
+            except Exception as e:  # noqa: BLE001 - API hiccup: fall back to the resync period
+                log.warning("partition watch: %s", e)
+                stop.wait(max(env.poll_s, min(a.interval, 30.0)))
+            if stop.is_set():
+                break
+            try:
+                applied = PM.reconcile_node(env, backend, profiles, default, a.config_label).get("profile", applied)
             except Exception as e:  # noqa: BLE001
                 log.error("partition reconcile failed: %s", e)
         return 0

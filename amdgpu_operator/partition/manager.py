@@ -126,7 +126,9 @@ def reconcile_node(env: NodeEnv, backend, profiles: dict, default: Profile,
         log.error("partition apply failed: %s", e)
         return {"changed": False, "error": str(e), "profile": name}
     clear_ready(env, ("workload", "plugin", "complete"))
+    # the plugin re-enumerates the partitions; a fresh validator validates them
     restart_device_plugin(env)
+    restart_validator(env)
     env.client.patch("v1", "Node", env.node_name,
                      {"metadata": {"labels": {STATE_LABEL: "success", APPLIED_LABEL: name, "amd.com/gpu.validated": None}}})
     return {"changed": True, "profile": name, "gpus": todo, "evicted": evicted}
@@ -157,6 +159,12 @@ def wait_gpu_pods_gone(env: NodeEnv, timeout: float) -> bool:
     _, ok = wait_for(env.client, "v1", "Pod", lambda pods: not any(_uses_gpu(p) for p in pods.values()),
                      field_selector=f"spec.nodeName={env.node_name}", timeout=timeout, poll_s=env.poll_s)
     return ok
+
+
+def restart_validator(env: NodeEnv) -> None:
+    for pod in env.client.list("v1", "Pod", env.namespace, label_selector="app=amd-operator-validator",
+                               field_selector=f"spec.nodeName={env.node_name}"):
+        env.client.delete("v1", "Pod", pod["metadata"]["name"], env.namespace)
 
 
 def restart_device_plugin(env: NodeEnv) -> None:

@@ -10,6 +10,7 @@ Ready again with the allocatable each node's workload implies:
   switch      flip a node between container and vm-passthrough
   spec        toggle gfd / the metrics exporter in the ClusterPolicy
   upgrade     change driver.driverVersion (node-by-node driver upgrade)
+  partition   flip a container node between SPX and CPX (partition manager: 2 or 16 devices)
 
     python tools/chaos_sim.py --seeds 1-5 --steps 10
 
@@ -34,7 +35,7 @@ from amdgpu_operator.driver.manager import monitor_once  # noqa: E402
 from amdgpu_operator.sandbox import WORKLOAD_CONFIG_LABEL  # noqa: E402
 from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster  # noqa: E402
 
-FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec", "upgrade")
+FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec", "upgrade", "partition")
 
 
 def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
@@ -43,12 +44,19 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
     c = SimCluster(os.path.join(d, "c"), [NodeSpec("g0", 2), NodeSpec("g1", 2), NodeSpec("cpu", 0)], fake_gpu=True,
                    poll_s=0.005, agent_poll_s=0.05, termination_s=0.0).start()  # kubelet-confirmed pod deletes
     mode = {"g0": "container", "g1": "container"}
+    cpx = {"g0": False, "g1": False}
+    from amdgpu_operator.partition import manager as PM
+
+    for n in mode:  # partition changes act on the fake sysfs tree
+        env = c.nodes[n].env
+        env.extra["partition_backend"] = PM.SysfsBackend(env.host_root, PM.sysfs_partition_rebuilder(env.host_root, 2))
 
     def expect():
-        return {n: (2 if m == "container" else {"amd.com/MI355X": 2}) for n, m in mode.items()}
+        return {n: ((16 if cpx[n] else 2) if m == "container" else {"amd.com/MI355X": 2}) for n, m in mode.items()}
 
     try:
-        c.install_operator(deep_merge(parse_set_flags(REFERENCE_SET_FLAGS), {"sandboxWorkloads": {"enabled": True}}))
+        c.install_operator(deep_merge(parse_set_flags(REFERENCE_SET_FLAGS + ["migManager.enabled=true"]),
+                                      {"sandboxWorkloads": {"enabled": True}}))
         c.wait_ready(timeout, expect())
         for i in range(steps):
             fault, node = rnd.choice(FAULTS), rnd.choice(["g0", "g1"])
@@ -76,6 +84,11 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
                 cp["spec"][key]["enabled"] = not cp["spec"][key]["enabled"]
                 c.client.update(cp)
                 info = f"{key}={cp['spec'][key]['enabled']}"
+            elif fault == "partition" and mode[node] == "container":
+                cpx[node] = not cpx[node]
+                c.client.patch("v1", "Node", node, {"metadata": {"labels": {
+                    "amd.com/gpu.partition-config": "all-cpx" if cpx[node] else "all-spx"}}})
+                info = "CPX" if cpx[node] else "SPX"
             elif fault == "upgrade":
                 cp = c.policy()
                 cp["spec"]["driver"]["driverVersion"] = "6.14.0" if cp["spec"]["driver"]["driverVersion"] != "6.14.0" \
