@@ -38,11 +38,12 @@ from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster  # noqa: E40
 FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec", "upgrade", "partition")
 
 
-def run_seed(seed: int, steps: int, settle_s: float, timeout: float) -> bool:
+def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: bool = False) -> bool:
     rnd = random.Random(seed)
     d = tempfile.mkdtemp(prefix="chaos-")
     c = SimCluster(os.path.join(d, "c"), [NodeSpec("g0", 2), NodeSpec("g1", 2), NodeSpec("cpu", 0)], fake_gpu=True,
-                   poll_s=0.005, agent_poll_s=0.05, termination_s=0.0).start()  # kubelet-confirmed pod deletes
+                   poll_s=0.005, agent_poll_s=0.05, termination_s=0.0,  # kubelet-confirmed pod deletes
+                   http_api=http_api).start()
     mode = {"g0": "container", "g1": "container"}
     cpx = {"g0": False, "g1": False}
     from amdgpu_operator.partition import manager as PM
@@ -124,9 +125,10 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--settle-s", type=float, default=0.5, help="let the fault land before checking readiness")
     ap.add_argument("--timeout", type=float, default=60.0)
+    ap.add_argument("--http-api", action="store_true", help="operator and operands over HTTP (RestClient, informers)")
     a = ap.parse_args()
     lo, _, hi = a.seeds.partition("-")
-    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout) for s in range(int(lo), int(hi or lo) + 1)])
+    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api) for s in range(int(lo), int(hi or lo) + 1)])
     return 0 if ok else 1
 
 
