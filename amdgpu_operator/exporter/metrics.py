@@ -361,17 +361,8 @@ class NodeStatusExporter:
         self.node = node_name
         self.scrapes = 0
 
-    def _series(self) -> list[Series]:
-        if self.selection is not None:
-            return self.selection
-        out = []
-        for metric, fld, mtype, help_, alias, scale in FIELDS:
-            out.append(Series(metric, fld, mtype, help_, 1.0))
-            if self.dcgm_names and alias:
-                out.append(Series(alias, fld, mtype, help_, scale))
-        return out
-
     def render(self) -> str:
+        from ..driver.manager import LOST_MARKER
         from ..validator.validate import READY_FILES
 
         self.scrapes += 1
@@ -399,6 +390,10 @@ class NodeStatusExporter:
         lines += ["# HELP amd_gpu_operator_node_validated Node passed every validation step",
                   "# TYPE amd_gpu_operator_node_validated gauge",
                   f"amd_gpu_operator_node_validated{_labels(lab_node)} {int(validated)}",
+                  "# HELP amd_gpu_operator_node_driver_lost The amdgpu driver went away and is not back yet",
+                  "# TYPE amd_gpu_operator_node_driver_lost gauge",
+                  f"amd_gpu_operator_node_driver_lost{_labels(lab_node)} "
+                  f"{int(os.path.exists(os.path.join(self.dir, LOST_MARKER)))}",
                   "# HELP amd_gpu_operator_node_status_scrapes_total Scrapes served",
                   "# TYPE amd_gpu_operator_node_status_scrapes_total counter",
                   f"amd_gpu_operator_node_status_scrapes_total{_labels(lab_node)} {self.scrapes}"]

@@ -271,7 +271,15 @@ def test_http_server_and_node_status(env):
         assert 'amd_gpu_operator_node_validation_ready{node="n1",step="driver"} 1' in body
         assert 'amd_gpu_operator_node_validation_ready{node="n1",step="plugin"} 0' in body
         assert 'amd_gpu_operator_node_validation_seconds{node="n1",step="driver"} 0.5' in body
+        assert 'amd_gpu_operator_node_driver_lost{node="n1"} 0' in body
         assert urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/healthz", timeout=5).read() == b"ok\n"
+        from amdgpu_operator.driver import manager as DM
+
+        os.unlink(os.path.join(env.host_root, "sys/module/amdgpu/initstate"))  # the driver goes away
+        assert DM.monitor_once(env) is False
+        body = urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/metrics", timeout=5).read().decode()
+        assert 'amd_gpu_operator_node_driver_lost{node="n1"} 1' in body
+        assert 'amd_gpu_operator_node_validation_ready{node="n1",step="driver"} 0' in body
     finally:
         srv.stop()
 
