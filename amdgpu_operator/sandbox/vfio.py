@@ -235,6 +235,35 @@ def unbind_all(pci: PciSysfs) -> list[GroupResult]:
     return out
 
 
+# <linux/vfio.h>: VFIO_GROUP_GET_STATUS = _IO(';', 100 + 3), struct vfio_group_status {argsz, flags}
+VFIO_GROUP_GET_STATUS = (ord(";") << 8) | (100 + 3)
+VFIO_GROUP_FLAGS_VIABLE = 1 << 0
+
+
+def group_viable(dev_path: str) -> bool | None:
+    """Ask the kernel whether a VFIO group is viable (every device of the
+    group bound to a VFIO driver, so a VM may own it).  None when the path
+    is not a VFIO character device (a test tree) or the query is refused."""
+    import fcntl
+    import stat
+    import struct
+
+    try:
+        if not stat.S_ISCHR(os.stat(dev_path).st_mode):
+            return None
+        fd = os.open(dev_path, os.O_RDWR)
+    except OSError:
+        return None
+    try:
+        buf = bytearray(struct.pack("II", 8, 0))
+        fcntl.ioctl(fd, VFIO_GROUP_GET_STATUS, buf, True)
+        return bool(struct.unpack("II", bytes(buf))[1] & VFIO_GROUP_FLAGS_VIABLE)
+    except OSError:  # EBUSY: a VM holds the group already; the binding was checked above
+        return None
+    finally:
+        os.close(fd)
+
+
 def check_bound(pci: PciSysfs) -> tuple[bool, str, list[dict]]:
     """Sandbox validation: every AMD GPU on vfio-pci with its group's device
     node present.  Returns (ok, message, per-GPU detail)."""
@@ -245,9 +274,13 @@ def check_bound(pci: PciSysfs) -> tuple[bool, str, list[dict]]:
     for g in gpus:
         dev = pci.vfio_dev(g.iommu_group) if g.iommu_group else ""
         ok = g.driver == VFIO_DRIVER and bool(dev) and os.path.exists(dev)
-        detail.append({"bdf": g.bdf, "driver": g.driver, "iommu_group": g.iommu_group, "vfio_dev": ok})
+        viable = group_viable(dev) if ok else None
+        detail.append({"bdf": g.bdf, "driver": g.driver, "iommu_group": g.iommu_group, "vfio_dev": ok,
+                       "viable": viable})
         if not ok:
             bad.append(f"{g.bdf} ({g.driver or 'unbound'})")
+        elif viable is False:
+            bad.append(f"{g.bdf} (IOMMU group {g.iommu_group} not viable: a member is on another driver)")
     if bad:
         return False, f"not ready for passthrough: {', '.join(bad)}", detail
     return True, f"{len(gpus)} GPU(s) bound to {VFIO_DRIVER}", detail

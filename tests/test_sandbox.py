@@ -75,6 +75,17 @@ def test_bind_waits_for_gpu_users_then_fails(tree):
     assert len(VF.bind_all(k, timeout=5.0)) == 4
 
 
+def test_group_viability_query(tree, monkeypatch):
+    _, k = tree
+    VF.bind_all(k)
+    grp = k.gpus()[0].iommu_group
+    assert VF.group_viable(k.vfio_dev(grp)) is None  # a regular file in the test tree: not asked
+    assert VF.VFIO_GROUP_GET_STATUS == 0x3B67
+    monkeypatch.setattr(VF, "group_viable", lambda path: not path.endswith("/" + grp))
+    ok, msg, _ = VF.check_bound(k)
+    assert not ok and "not viable" in msg and f"group {grp}" in msg
+
+
 def test_no_iommu_group_is_an_error(tmp_path):
     root = str(tmp_path / "h")
     fakesys.build_node(root, 1)
