@@ -38,29 +38,45 @@ from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster  # noqa: E40
 FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec", "upgrade", "partition")
 
 
-def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: bool = False) -> bool:
+REAL_GPU_FAULTS = ("delpod", "delpod", "kubelet", "spec")  # no root on a GPU box: no module, PCI or partition changes
+
+
+def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: bool = False,
+             real_gpu: bool = False) -> bool:
     rnd = random.Random(seed)
     d = tempfile.mkdtemp(prefix="chaos-")
-    c = SimCluster(os.path.join(d, "c"), [NodeSpec("g0", 2), NodeSpec("g1", 2), NodeSpec("cpu", 0)], fake_gpu=True,
+    if real_gpu:  # one node, this machine's GPU(s): every validation runs on the real device
+        from amdgpu_operator.discovery import topology
+
+        n_gpus = len(topology.enumerate_gpus("/"))
+        nodes, gpu_nodes = [NodeSpec("g0", n_gpus, sysfs_root="/")], ["g0"]
+    else:
+        n_gpus = 2
+        nodes, gpu_nodes = [NodeSpec("g0", 2), NodeSpec("g1", 2), NodeSpec("cpu", 0)], ["g0", "g1"]
+    c = SimCluster(os.path.join(d, "c"), nodes, fake_gpu=not real_gpu,
                    poll_s=0.005, agent_poll_s=0.05, termination_s=0.0,  # kubelet-confirmed pod deletes
                    http_api=http_api).start()
-    mode = {"g0": "container", "g1": "container"}
-    cpx = {"g0": False, "g1": False}
+    mode = {n: "container" for n in gpu_nodes}
+    cpx = {n: False for n in gpu_nodes}
     from amdgpu_operator.partition import manager as PM
 
-    for n in mode:  # partition changes act on the fake sysfs tree
-        env = c.nodes[n].env
-        env.extra["partition_backend"] = PM.SysfsBackend(env.host_root, PM.sysfs_partition_rebuilder(env.host_root, 2))
+    if not real_gpu:
+        for n in mode:  # partition changes act on the fake sysfs tree
+            env = c.nodes[n].env
+            env.extra["partition_backend"] = PM.SysfsBackend(env.host_root,
+                                                             PM.sysfs_partition_rebuilder(env.host_root, 2))
 
     def expect():
-        return {n: ((16 if cpx[n] else 2) if m == "container" else {"amd.com/MI355X": 2}) for n, m in mode.items()}
+        return {n: ((8 * n_gpus if cpx[n] else n_gpus) if m == "container" else {"amd.com/MI355X": n_gpus})
+                for n, m in mode.items()}
 
     try:
-        c.install_operator(deep_merge(parse_set_flags(REFERENCE_SET_FLAGS + ["migManager.enabled=true"]),
-                                      {"sandboxWorkloads": {"enabled": True}}))
+        extra = [] if real_gpu else ["migManager.enabled=true"]
+        c.install_operator(deep_merge(parse_set_flags(REFERENCE_SET_FLAGS + extra),
+                                      {} if real_gpu else {"sandboxWorkloads": {"enabled": True}}))
         c.wait_ready(timeout, expect())
         for i in range(steps):
-            fault, node = rnd.choice(FAULTS), rnd.choice(["g0", "g1"])
+            fault, node = rnd.choice(REAL_GPU_FAULTS if real_gpu else FAULTS), rnd.choice(gpu_nodes)
             info = ""
             if fault == "delpod":
                 pods = [p for p in c.pods() if p["spec"].get("nodeName") == node]
@@ -126,9 +142,11 @@ def main() -> int:
     ap.add_argument("--settle-s", type=float, default=0.5, help="let the fault land before checking readiness")
     ap.add_argument("--timeout", type=float, default=60.0)
     ap.add_argument("--http-api", action="store_true", help="operator and operands over HTTP (RestClient, informers)")
+    ap.add_argument("--real-gpu", action="store_true", help="one node on this machine's GPUs (pod/kubelet/spec faults)")
     a = ap.parse_args()
     lo, _, hi = a.seeds.partition("-")
-    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api) for s in range(int(lo), int(hi or lo) + 1)])
+    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api, a.real_gpu)
+              for s in range(int(lo), int(hi or lo) + 1)])
     return 0 if ok else 1
 
 
