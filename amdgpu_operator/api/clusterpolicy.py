@@ -230,8 +230,32 @@ class WorkloadSpec(_M):
     hbmBytes: int = 1 << 30
     rcclElems: int = 1 << 24
     xgmiElems: int = 1 << 22
-    minGemmTflops: float = 0.0
-    minHbmGbps: float = 0.0
+    # Ready-gate floors, for a whole MI355X (256 CUs; a compute partition is
+    # held to its share of the CUs).  Calibrated from the round-2 driver bench
+    # on MI355X (BENCH_r02.json: GEMM 1,238.5 TF/s at 4096^3, HBM copy
+    # 6,235.9 GB/s at 1 GiB): half the GEMM rate, 60 % of the copy rate.  A GPU
+    # held at low clocks, a slow HBM stack or fenced-off CUs fails the node.
+    # The floors apply at gemmN >= 4096 / hbmBytes >= 1 GiB (smaller runs are
+    # launch-bound and report their rate only); 0 = report only.
+    minGemmTflops: float = 620.0
+    minHbmGbps: float = 3700.0
+    # counter-gate floor on MFMA busy cycles per SIMD-cycle of the counted
+    # GEMM (native/include/gate_policy.h): ~0.49 measured at 4096^3
+    # (profiles/r2_gate/aql_v2.json), floor at 40 % of it
+    minMfmaUtil: float = 0.2
+    # RCCL fp32 all-reduce busBW floor at N >= 2: this many GB/s per peer GPU
+    # (N-1 peers).  A PCIe fallback ring (dead xGMI) delivers ~20-40 GB/s in
+    # total; 15 GB/s per peer is far below any healthy xGMI mesh and still
+    # fails an 8-GPU node routed over PCIe (105 GB/s floor)
+    rcclBusbwPerPeerGbps: float = 15.0
+    # multi-GPU nodes: every pair of GPUs joined by an xGMI link in the KFD
+    # topology and amd-smi reporting the links up, none in error
+    requireXgmiLinks: bool = True
+    # N >= 2: a rank not alive within this long is missing (also bounds the
+    # RCCL communicator set-up); a collective not done within
+    # collectiveTimeoutSeconds aborts the communicator
+    peerTimeoutSeconds: float = 30.0
+    collectiveTimeoutSeconds: float = 30.0
     counterGate: bool = True
     # how the gate reads the counters: "aql" - AQL profiling packets around one
     # more dispatch of the GEMM on the validator's own HSA queue (no profiler

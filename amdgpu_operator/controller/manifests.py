@@ -309,10 +309,13 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     w = v.workload
     wl_args = ["--gemm", str(w.gemmN), "--gemm-iters", str(w.gemmIters), "--hbm-bytes", str(w.hbmBytes),
                "--rccl-elems", str(w.rcclElems), "--xgmi-elems", str(w.xgmiElems)]
-    if w.minGemmTflops:
-        wl_args += ["--min-gemm-tflops", str(w.minGemmTflops)]
-    if w.minHbmGbps:
-        wl_args += ["--min-hbm-gbps", str(w.minHbmGbps)]
+    for flag, val in (("--min-gemm-tflops", w.minGemmTflops), ("--min-hbm-gbps", w.minHbmGbps),
+                      ("--min-mfma-util", w.minMfmaUtil), ("--rccl-busbw-per-peer", w.rcclBusbwPerPeerGbps)):
+        if val:
+            wl_args += [flag, f"{val:g}"]
+    wl_args += ["--peer-timeout", f"{w.peerTimeoutSeconds:g}", "--collective-timeout", f"{w.collectiveTimeoutSeconds:g}"]
+    if w.requireXgmiLinks:
+        wl_args += ["--require-xgmi-links"]
     if w.counterGate:
         wl_args += ["--counter-gate"] + (["--gate-mode", "sdk"] if w.counterGateMode == "sdk" else [])
     if w.rcclSingleGpu:

@@ -1,8 +1,16 @@
 """Stand-in for the native ``amdgpu-validator`` on machines without a GPU.
 
 Accepts the same arguments, rendezvous with its peer ranks through the same
-directory protocol (so multi-rank orchestration is exercised for real) and
-prints the same JSON report shape with ``"simulated": true``.
+directory protocol as ``native/validator/validator_main.cpp`` (liveness
+records ``<run>-alive-<r>`` / ``-failed-`` / ``-done-``, the orchestrator's
+``abort`` file, ``--peer-timeout``), so multi-rank orchestration and its
+bounded failure are exercised for real, and prints the same JSON report shape
+with ``"simulated": true``.
+
+Fault injection for the CPU tests: ``AMDGPU_FAKE_VALIDATOR_FAULT`` =
+``<run-id suffix or *>:<rank>:<kind>`` with kind ``fail`` (report a failure at
+once), ``exit`` (die without a report, after the liveness record) or ``hang``
+(never reach the rendezvous; stops only when aborted).
 """
 
 from __future__ import annotations
@@ -13,9 +21,10 @@ import sys
 import time
 
 
-def wait_start_gate(path: str | None, timeout: float = 120.0) -> str:
+def wait_start_gate(path: str | None, timeout: float = 120.0, abort_path: str | None = None) -> str:
     """The native validator's ``--start-gate``: block until the file has a
-    verdict; "go" releases the process (same protocol as validator_main.cpp)."""
+    verdict; "go" releases the process (same protocol as validator_main.cpp).
+    An abort file in the run's rendezvous directory aborts the wait too."""
     if not path:
         return "go"
     deadline = time.time() + timeout
@@ -27,38 +36,150 @@ def wait_start_gate(path: str | None, timeout: float = 120.0) -> str:
                 return text
         except FileNotFoundError:
             pass
+        if abort_path and os.path.exists(abort_path):
+            return "abort"
         time.sleep(0.001)
     return "timeout"
+
+
+class PeerError(RuntimeError):
+    def __init__(self, peer: int, state: str, msg: str):
+        super().__init__(msg)
+        self.peer = peer
+        self.state = state
+
+
+class Rendezvous:
+    """Python twin of validator_main.cpp's Rendezvous liveness protocol."""
+
+    def __init__(self, rdv: str, run_id: str, rank: int, world: int, peer_timeout: float):
+        self.rdv, self.run_id, self.rank, self.world = rdv, run_id, rank, world
+        self.peer_timeout = peer_timeout
+        self.t0 = time.monotonic()
+
+    def _p(self, name: str) -> str:
+        return os.path.join(self.rdv, name)
+
+    def marker(self, kind: str, r: int) -> str:
+        return self._p(f"{self.run_id}-{kind}-{r}")
+
+    def publish(self, path: str, text: str) -> None:
+        tmp = f"{path}.tmp.{os.getpid()}"
+        with open(tmp, "w") as f:
+            f.write(text)
+        os.replace(tmp, path)
+
+    def announce(self) -> None:
+        self.publish(self.marker("alive", self.rank), f"{os.getpid()} 0\n")
+
+    def finish(self, ok: bool, error: str = "") -> None:
+        self.publish(self.marker("done" if ok else "failed", self.rank), "ok" if ok else error)
+
+    def _read(self, path: str) -> str | None:
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except FileNotFoundError:
+            return None
+
+    def peer(self, r: int) -> tuple[str, str]:
+        if (t := self._read(self.marker("failed", r))) is not None:
+            return "failed", t
+        if self._read(self.marker("done", r)) is not None:
+            return "done", ""
+        t = self._read(self.marker("alive", r))
+        if not t:
+            return "missing", ""
+        pid = int(t.split()[0])
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                state = f.read().rsplit(")", 1)[1].split()[0]
+            if state in ("Z", "X"):
+                raise FileNotFoundError
+        except (FileNotFoundError, IndexError):
+            if self._read(self.marker("done", r)) is not None:
+                return "done", ""
+            return "dead", f"pid {pid}"
+        return "alive", ""
+
+    def watch(self, only: int = -1) -> None:
+        if (why := self._read(self._p("abort"))) is not None:
+            raise PeerError(-1, "aborted", f"run aborted by the orchestrator: {why}")
+        age = time.monotonic() - self.t0
+        for r in range(self.world):
+            if r == self.rank or (only >= 0 and r != only):
+                continue
+            st, d = self.peer(r)
+            if st == "failed":
+                raise PeerError(r, "failed", f"rank {r} failed: {d}")
+            if st == "dead":
+                raise PeerError(r, "dead", f"rank {r} ({d}) exited before the rendezvous completed")
+            if st == "missing" and age > self.peer_timeout:
+                raise PeerError(r, "missing", f"rank {r} never started (no liveness record after {age:.1f} s)")
+
+    def barrier(self, tag: str, timeout: float = 60.0) -> None:
+        self.publish(self._p(f"{self.run_id}-barrier-{tag}-{self.rank}"), "1")
+        deadline = time.monotonic() + timeout
+        for r in range(self.world):
+            while not os.path.exists(self._p(f"{self.run_id}-barrier-{tag}-{r}")):
+                self.watch(r)
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"rendezvous: timeout waiting for rank {r}")
+                time.sleep(0.002)
+
+
+def _fault(run_id: str, rank: int) -> str | None:
+    spec = os.environ.get("AMDGPU_FAKE_VALIDATOR_FAULT", "")
+    for item in filter(None, spec.split(",")):
+        where, r, kind = item.split(":")
+        if (where == "*" or run_id.endswith(where)) and int(r) == rank:
+            return kind
+    return None
 
 
 def main(argv: list[str]) -> int:
     def arg(name, default):
         return argv[argv.index(name) + 1] if name in argv else default
 
-    verdict = wait_start_gate(arg("--start-gate", None))
+    rank, world = int(arg("--rank", "0")), int(arg("--world", "1"))
+    rdv, run_id = arg("--rendezvous", "/tmp/amdgpu-validator"), arg("--run-id", "run")
+    os.makedirs(rdv, exist_ok=True)
+    rv = Rendezvous(rdv, run_id, rank, world, float(arg("--peer-timeout", "30")))
+    if world > 1:
+        rv.announce()
+    fault = _fault(run_id, rank)
+    if fault == "exit":
+        os._exit(9)
+    verdict = wait_start_gate(arg("--start-gate", None), abort_path=os.path.join(rdv, "abort") if world > 1 else None)
     if verdict != "go":
+        if world > 1:
+            rv.finish(False, f"start gate: {verdict}")
         print(json.dumps({"ok": False, "error": f"start gate: {verdict}", "steps": []}))
         return 3
 
-    rank, world = int(arg("--rank", "0")), int(arg("--world", "1"))
-    rdv, run_id = arg("--rendezvous", "/tmp/amdgpu-validator"), arg("--run-id", "run")
     steps = arg("--steps", "hip,vecadd,gemm,mfma,hbm,xgmi,rccl").split(",")
     t0 = time.perf_counter()
-    os.makedirs(rdv, exist_ok=True)
-    if "rccl" in steps and world > 1:  # barrier like the RCCL unique-id exchange
-        open(os.path.join(rdv, f"{run_id}-fake-{rank}"), "w").close()
-        deadline = time.time() + 60
-        while any(not os.path.exists(os.path.join(rdv, f"{run_id}-fake-{r}")) for r in range(world)):
-            if time.time() > deadline:
-                print(json.dumps({"ok": False, "error": "rendezvous timeout"}))
-                return 1
-            time.sleep(0.002)
     rep = {"ok": True, "simulated": True, "rank": rank, "world": world, "device": int(arg("--device", "0")),
            "owner_rank_env": os.environ.get("RANK"), "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES"),
-           "seconds": time.perf_counter() - t0,
            "steps": [{"name": s, "ok": True, "seconds": 0.0, "simulated": True} for s in steps]}
+    try:
+        if fault == "fail":
+            raise RuntimeError("injected failure")
+        if fault == "hang":
+            while True:  # ends only through the abort file (or a kill)
+                rv.watch(rank)
+                time.sleep(0.005)
+        if world > 1 and ("rccl" in steps or "xgmi" in steps or "peers" in steps):
+            rv.barrier("rccl" if "rccl" in steps else "xgmi")  # like the RCCL unique-id exchange
+    except PeerError as e:
+        rep.update(ok=False, error=str(e), failed_peer=e.peer, peer_state=e.state)
+    except RuntimeError as e:
+        rep.update(ok=False, error=str(e))
+    rep["seconds"] = time.perf_counter() - t0
+    if world > 1:
+        rv.finish(rep["ok"], rep.get("error", ""))
     print(json.dumps(rep))
-    return 0
+    return 0 if rep["ok"] else 1
 
 
 if __name__ == "__main__":

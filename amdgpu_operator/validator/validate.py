@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import json
 import os
+import shutil
 import threading
 import time
 import uuid
@@ -34,7 +35,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 from .. import RESOURCE_NAME, native
 from ..kube.client import wait_for
-from ..nodeenv import REPORT_EARLY_ENV, NodeEnv
+from ..nodeenv import REPORT_EARLY_ENV, NodeEnv, report_rc
 from ..utils.logs import get_logger
 
 log = get_logger("amdgpu.validator")
@@ -144,6 +145,82 @@ def workload_argv(args: list[str], rank: int, world: int, rendezvous: str, run_i
             str(world), "--rendezvous", rendezvous, "--run-id", run_id, *args]
 
 
+# Written into a run's rendezvous directory when any rank failed: every
+# sibling still waiting on a peer (RCCL set-up, IPC handles, barriers, its
+# start gate) stops within milliseconds (validator_main.cpp Rendezvous).
+ABORT_FILE = "abort"
+
+
+def abort_run(rdv: str, reason: str) -> None:
+    path = os.path.join(rdv, ABORT_FILE)
+    if os.path.exists(path):
+        return
+    tmp = f"{path}.tmp.{os.getpid()}.{threading.get_ident()}"
+    try:
+        with open(tmp, "w") as f:
+            f.write(reason[:400])
+        os.replace(tmp, path)
+    except OSError:
+        pass
+
+
+def check_fabric(env: NodeEnv, gpus: list, smi_metrics: list | None = None) -> dict:
+    """The xGMI fabric between the validated GPUs is whole.
+
+    Every pair of distinct physical GPUs must share one xGMI hive and be
+    joined by an XGMI link in the KFD topology (``io_links``); where amd-smi
+    answers, each GPU must report at least one link up per physical peer and
+    no link in error (N6 ``amdsmi_get_gpu_xgmi_link_status``).  Partitions of
+    one physical GPU are not peers of each other.  A dead link leaves RCCL
+    routing around it at a fraction of the bandwidth, which the busBW floor
+    may or may not catch; this check names the GPU."""
+    from ..discovery import topology
+
+    phys: dict[str, object] = {}
+    for g in gpus:
+        phys.setdefault(g.bdf, g)
+    out: dict = {"ok": True, "physical_gpus": len(phys), "problems": []}
+    if len(phys) < 2:
+        out["skipped"] = "one physical GPU: no xGMI peer"
+        return out
+    problems = out["problems"]
+    hives = {g.hive_id for g in phys.values()}
+    if 0 in hives or len(hives) != 1:
+        problems.append(f"GPUs are not in one xGMI hive (hive ids {sorted(hives)})")
+    idx = {g.index: g.bdf for g in gpus}
+    linked: set[tuple[str, str]] = set()
+    for lk in topology.links(env.sysfs_root()):
+        if lk.is_xgmi and lk.src in idx and lk.dst in idx:
+            linked.add(tuple(sorted((idx[lk.src], idx[lk.dst]))))
+    bdfs = sorted(phys)
+    missing = [(a, b) for i, a in enumerate(bdfs) for b in bdfs[i + 1:] if (a, b) not in linked]
+    if missing:
+        problems.append(f"no XGMI link between {missing[:8]}" + (f" (+{len(missing) - 8})" if len(missing) > 8 else ""))
+    out["kfd_xgmi_pairs"] = len(linked)
+    if smi_metrics is None:
+        try:
+            with topology.Smi() as smi:
+                smi_metrics = smi.collect()
+        except Exception as e:  # noqa: BLE001 - amd-smi absent (sim, minimal image): KFD view only
+            out["smi"] = f"unavailable: {e}"
+            smi_metrics = []
+    peers = len(phys) - 1
+    live = {}
+    for m in smi_metrics:
+        if m.bdf.lower() not in {b.lower() for b in phys} or "xgmi_links_up" not in m.values:
+            continue
+        up, err = m.values.get("xgmi_links_up", 0), m.values.get("xgmi_links_error", 0)
+        live[m.bdf] = {"up": up, "total": m.values.get("xgmi_links_total", 0), "error": err}
+        if up < peers:
+            problems.append(f"{m.bdf}: {up} xGMI links up, {peers} physical peers")
+        if err:
+            problems.append(f"{m.bdf}: {err} xGMI links in error")
+    if live:
+        out["links"] = live
+    out["ok"] = not problems
+    return out
+
+
 def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: float = 600.0,
                       start_gate: str | None = None) -> dict:
     """One native validator process per GPU, all ranks in one RCCL communicator.
@@ -151,7 +228,21 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     ``start_gate``: a file the processes wait on before their first HIP call
     (``amdgpu-validator --start-gate``): "go" releases them, anything else
     aborts them.  The caller spawns them before the driver is validated and
-    writes the verdict afterwards (:func:`validate_gpu`)."""
+    writes the verdict afterwards (:func:`validate_gpu`).
+
+    Bounded failure at N >= 2: every rank keeps a liveness record in the
+    run's rendezvous directory and watches its peers' while it waits on them
+    (RCCL's non-blocking set-up included), so a rank that never started, died
+    or failed ends the run within milliseconds of being seen - or after
+    ``--peer-timeout`` for one that never appears - with the rank named in the
+    error.  As soon as any process reports a failure this function writes the
+    run's abort file, so siblings that are not waiting on that rank stop too
+    instead of running out their own timeouts.
+
+    validate.py's own flags (not passed to the binary): ``--rccl-single-gpu``,
+    ``--rccl-shared-process``, ``--rccl-busbw-per-peer X`` (the busBW floor,
+    X GB/s per peer GPU: ``--min-rccl-busbw-gbps X*(N-1)``) and
+    ``--require-xgmi-links`` (:func:`check_fabric` on multi-GPU nodes)."""
     from ..discovery import topology
 
     t0 = time.perf_counter()
@@ -173,7 +264,12 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     counter_env = gate_env() if sdk_gate else {}
     rccl_single = "--rccl-single-gpu" in args  # validate.py's own flags, not the binary's
     rccl_shared = "--rccl-shared-process" in args
-    args = _drop_flag(_drop_flag(args, "--rccl-single-gpu"), "--rccl-shared-process")
+    require_links = "--require-xgmi-links" in args
+    per_peer = float(_arg_value(args, "--rccl-busbw-per-peer") or 0.0)
+    args = _drop_value(_drop_flag(_drop_flag(_drop_flag(args, "--rccl-single-gpu"), "--rccl-shared-process"),
+                                  "--require-xgmi-links"), "--rccl-busbw-per-peer")
+    if per_peer > 0 and world > 1:
+        args += ["--min-rccl-busbw-gbps", f"{per_peer * (world - 1):g}"]
     steps = _steps_of(args)
     kernel_steps = [s for s in steps if s != "rccl"]
     # RCCL runs in its own process per GPU, concurrently with the kernel
@@ -189,6 +285,9 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         jobs += [(r, _with_steps(_drop_flag(args, "--counter-gate"), ["hip", "rccl"]), run_id + "-rccl", {})
                  for r in range(world)]
 
+    def failed(res) -> bool:
+        return res.rc != 0 or report_rc(res.stdout) != 0
+
     def one(job):
         rank, jargs, rid, jenv = job
         # the report (pipes closed) is the result: the process exit and the
@@ -198,10 +297,19 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         argv = workload_argv(jargs, rank, world, rdv, rid, gpus[rank].index)
         if start_gate:
             argv += ["--start-gate", start_gate]
-        return env.launch(argv, jenv, device=gpus[rank].index, timeout=timeout)
+        res = env.launch(argv, jenv, device=gpus[rank].index, timeout=timeout)
+        if world > 1 and failed(res):
+            abort_run(rdv, f"{rid} rank {rank} failed (rc {res.rc})")
+        return res
 
-    with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
-        results = list(ex.map(one, jobs))
+    fabric = None
+    try:
+        with ThreadPoolExecutor(max_workers=len(jobs) + 1) as ex:
+            fabric_f = ex.submit(check_fabric, env, gpus) if require_links and world > 1 else None
+            results = list(ex.map(one, jobs))
+            fabric = fabric_f.result() if fabric_f is not None else None
+    finally:
+        shutil.rmtree(rdv, ignore_errors=True)
     reports = []
     for (rank, _, rid, _), res in zip(jobs, results):
         try:
@@ -220,6 +328,9 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
             main["rccl_process_seconds"] = rep["process_seconds"]
             if rep.get("error"):
                 main["error"] = rep["error"]
+            for k in ("failed_peer", "peer_state"):
+                if k in rep:
+                    main[k] = rep[k]
             if res.rc != 0:
                 main["stderr"] = rep.get("stderr", "")
         else:
@@ -232,12 +343,35 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
             rep.setdefault("steps", []).append({"name": "rccl", "ok": True, "skipped": "single GPU: no xGMI peer"})
     ok = all(r.get("rc") == 0 and r.get("ok") for r in reports)
     summary = {"ok": ok, "world": world, "seconds": time.perf_counter() - t0, "ranks": reports}
+    if fabric is not None:
+        summary["fabric"] = fabric
+        if not fabric["ok"]:
+            ok = summary["ok"] = False
     if not ok:
-        bad = [(i, r.get("rc"), r.get("error") or r.get("stderr", "")[-300:]) for i, r in enumerate(reports)
-               if not (r.get("ok") and r.get("rc") == 0)]
-        raise StepFailed(f"workload validation failed on ranks {bad}")
+        raise StepFailed(f"workload validation failed: {failure_summary(reports, fabric)}")
     write_ready(env, "workload", summary)
     return summary
+
+
+def failure_summary(reports: list[dict], fabric: dict | None = None) -> str:
+    """The causes of a failed run first: a rank's own failure, or a peer it
+    found missing/dead; ranks that only stopped because of another's failure
+    (peer state ``failed`` / ``aborted``) come last, as consequences."""
+    causes, consequences = [], []
+    for i, r in enumerate(reports):
+        if r.get("ok") and r.get("rc") == 0:
+            continue
+        msg = r.get("error") or (r.get("stderr") or "")[-300:] or f"rc {r.get('rc')}"
+        bad_steps = [s.get("name") for s in r.get("steps", []) if s.get("ok") is False]
+        item = f"rank {i}: {msg}" + (f" (steps {bad_steps})" if bad_steps else "")
+        (consequences if r.get("peer_state") in ("failed", "aborted") else causes).append(item)
+    parts = []
+    if fabric is not None and not fabric.get("ok"):
+        parts.append("xGMI fabric: " + "; ".join(fabric.get("problems", [])))
+    parts += causes
+    if consequences:
+        parts.append("then " + "; ".join(consequences))
+    return "; ".join(parts) or "no report"
 
 
 ALL_STEPS = ("hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl")
@@ -259,6 +393,18 @@ def _with_steps(args: list[str], steps: list[str]) -> list[str]:
 
 def _drop_flag(args: list[str], flag: str) -> list[str]:
     return [a for a in args if a != flag]
+
+
+def _drop_value(args: list[str], flag: str) -> list[str]:
+    """Remove ``flag VALUE`` pairs."""
+    out, i = [], 0
+    while i < len(args):
+        if args[i] == flag:
+            i += 2
+            continue
+        out.append(args[i])
+        i += 1
+    return out
 
 
 def _drop_step(args: list[str], step: str) -> list[str]:

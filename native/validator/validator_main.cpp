@@ -30,6 +30,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -47,6 +48,7 @@
 
 #include "aql_gate.h"
 #include "avk.h"
+#include "gate_policy.h"
 
 namespace {
 
@@ -70,6 +72,10 @@ struct Rccl {
                                 hipStream_t) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
+  // non-blocking communicator set-up and teardown (bounded failure at N >= 2)
+  ncclResult_t (*CommInitRankConfig)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
+  ncclResult_t (*GetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
 
   std::string path;  // the library that was loaded
 
@@ -119,8 +125,11 @@ struct Rccl {
     ReduceScatter = reinterpret_cast<decltype(ReduceScatter)>(dlsym(dl, "ncclReduceScatter"));
     CommDestroy = reinterpret_cast<decltype(CommDestroy)>(dlsym(dl, "ncclCommDestroy"));
     GetErrorString = reinterpret_cast<decltype(GetErrorString)>(dlsym(dl, "ncclGetErrorString"));
+    CommInitRankConfig = reinterpret_cast<decltype(CommInitRankConfig)>(dlsym(dl, "ncclCommInitRankConfig"));
+    GetAsyncError = reinterpret_cast<decltype(GetAsyncError)>(dlsym(dl, "ncclCommGetAsyncError"));
+    CommAbort = reinterpret_cast<decltype(CommAbort)>(dlsym(dl, "ncclCommAbort"));
     if (!GetUniqueId || !CommInitRank || !AllReduce || !AllGather || !ReduceScatter || !CommDestroy ||
-        !GetErrorString) {
+        !GetErrorString || !CommInitRankConfig || !GetAsyncError || !CommAbort) {
       *err = "librccl is missing NCCL API symbols";
       return false;
     }
@@ -236,9 +245,13 @@ struct Args {
   long long rccl_elems = 1ll << 24;
   long long xgmi_elems = 1ll << 22;
   int emulated_peers = 8;
-  double min_gemm_tflops = 0;
-  double min_hbm_gbps = 0;
+  double min_gemm_tflops = 0;      // for a whole MI355X (256 CUs); applied pro rata to a partition
+  double min_hbm_gbps = 0;         // idem
+  double min_mfma_util = 0;        // counter-gate floor (gate_policy.h), scaled by the launch's occupancy
+  double min_rccl_busbw_gbps = 0;  // fp32 all-reduce busBW floor at world > 1
   double timeout_s = 120;
+  double peer_timeout_s = 30;       // a rank not alive by then is missing; bound on communicator set-up
+  double collective_timeout_s = 30;  // bound on any one collective (or batch of timed collectives)
   bool counter_gate = false;
   bool any_arch = false;
   bool null_stream = false;   // run the steps on the legacy null stream instead of a created one
@@ -281,13 +294,79 @@ std::string fmt(const char* f, ...) {
   return buf;
 }
 
+// AMDGPU_VALIDATOR_TRACE=1: stage transitions on stderr (diagnosing a run that
+// does not end; the report itself stays on stdout)
+const Clock::time_point g_t0 = Clock::now();
+const bool g_trace = [] {
+  const char* e = getenv("AMDGPU_VALIDATOR_TRACE");
+  return e && strcmp(e, "1") == 0;
+}();
+void trace(const char* f, ...) __attribute__((format(printf, 1, 2)));
+void trace(const char* f, ...) {
+  if (!g_trace) return;
+  char buf[512];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  fprintf(stderr, "[validator %8.4f] %s\n", secs(g_t0), buf);
+}
+
 // ------------------------------------------------------------ rendezvous ----
+// A wait on another rank that can no longer succeed: the rank never started,
+// exited, reported a failure, or the orchestrator aborted the run.
+struct PeerError : std::runtime_error {
+  int peer;           // -1: not about one rank (abort file)
+  std::string state;  // missing | dead | failed | aborted
+  PeerError(int p, std::string s, const std::string& msg) : std::runtime_error(msg), peer(p), state(std::move(s)) {}
+};
+
+// start time of a process (clock ticks since boot, /proc/<pid>/stat field 22)
+// and whether it is still running (not a zombie); false if it is gone
+bool proc_alive(long pid, unsigned long long* start) {
+  char path[64];
+  snprintf(path, sizeof(path), "/proc/%ld/stat", pid);
+  FILE* f = fopen(path, "r");
+  if (!f) return false;
+  char buf[1024];
+  const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  const char* p = strrchr(buf, ')');  // comm may contain spaces
+  if (!p) return false;
+  char state = 0;
+  unsigned long long st = 0;
+  // fields after ")": 3 state ... 22 starttime
+  const char* q = p + 2;
+  state = *q;
+  for (int field = 3; field < 22 && *q; ++q)
+    if (*q == ' ') ++field;
+  st = strtoull(q, nullptr, 10);
+  if (start) *start = st;
+  return state != 'Z' && state != 'X';
+}
+
+// Ranks of one validator run meet through files in a directory on the node
+// (--rendezvous; the host's validations dir, validate.py).  Besides the
+// payloads (RCCL unique id, IPC handles, barrier markers) every rank keeps
+// a liveness record there, so that a wait on a peer ends as soon as the
+// peer cannot arrive instead of at a timeout:
+//   <run>-alive-<r>   "pid starttime", written first thing at process start
+//   <run>-failed-<r>  the rank's error, written before it reports a failure
+//   <run>-done-<r>    the rank finished its steps
+//   abort             written by the orchestrator (validate.py) when any
+//                     rank of the run failed: every waiting rank stops
 struct Rendezvous {
   std::string dir;
   int rank, world;
-  double timeout_s;
+  double timeout_s;       // hard bound on any one fetch
+  std::string run_id;
+  double peer_timeout_s;  // a rank not alive this long after our start is missing
+  Clock::time_point t_start;
+  mutable std::atomic<long long> last_watch_ns{0};  // watch() runs on the main and the RCCL set-up thread
 
   std::string path(const std::string& name) const { return dir + "/" + name; }
+  std::string marker(const char* kind, int r) const { return run_id + "-" + kind + "-" + std::to_string(r); }
 
   void publish(const std::string& name, const void* data, size_t n) const {
     const std::string tmp = path(name + ".tmp." + std::to_string(getpid()));
@@ -297,8 +376,84 @@ struct Rendezvous {
     fclose(f);
     if (rename(tmp.c_str(), path(name).c_str()) != 0) throw std::runtime_error("rendezvous: rename failed");
   }
+  void publish_text(const std::string& name, const std::string& text) const { publish(name, text.data(), text.size()); }
 
-  std::vector<char> fetch(const std::string& name, size_t n) const {
+  bool read_text(const std::string& name, std::string* out) const {
+    FILE* f = fopen(path(name).c_str(), "rb");
+    if (!f) return false;
+    char buf[512];
+    const size_t n = fread(buf, 1, sizeof(buf), f);
+    fclose(f);
+    out->assign(buf, n);
+    while (!out->empty() && (out->back() == '\n' || out->back() == ' ')) out->pop_back();
+    return true;
+  }
+
+  void announce() const {
+    unsigned long long st = 0;
+    proc_alive(getpid(), &st);
+    publish_text(marker("alive", rank), fmt("%ld %llu\n", (long)getpid(), st));
+  }
+  void finish(bool ok, const std::string& error) const {
+    try {
+      publish_text(marker(ok ? "done" : "failed", rank), ok ? "ok" : error);
+    } catch (const std::exception&) {
+    }
+  }
+
+  enum class Peer { Missing, Alive, Dead, Failed, Done };
+  Peer peer(int r, std::string* detail) const {
+    std::string t;
+    if (read_text(marker("failed", r), &t)) return *detail = t, Peer::Failed;
+    if (read_text(marker("done", r), &t)) return Peer::Done;
+    if (!read_text(marker("alive", r), &t)) return Peer::Missing;
+    long pid = 0;
+    unsigned long long want = 0, have = 0;
+    if (sscanf(t.c_str(), "%ld %llu", &pid, &want) != 2 || pid <= 0) return Peer::Missing;  // being written
+    if (!proc_alive(pid, &have) || have != want) {
+      // it may have finished between the two reads
+      if (read_text(marker("done", r), &t)) return Peer::Done;
+      if (read_text(marker("failed", r), detail)) return Peer::Failed;
+      *detail = fmt("pid %ld", pid);
+      return Peer::Dead;
+    }
+    return Peer::Alive;
+  }
+
+  void check_abort() const {
+    std::string why;
+    if (read_text("abort", &why)) throw PeerError(-1, "aborted", "run aborted by the orchestrator: " + why);
+  }
+
+  // Throws PeerError when a wait on `only` (or on every other rank, -1) can
+  // no longer succeed.  Rate-limited: callers poll it from 1-2 ms loops.
+  void watch(int only = -1, bool force = false) const {
+    const auto now = Clock::now();
+    const long long ns = std::chrono::duration_cast<std::chrono::nanoseconds>(now.time_since_epoch()).count();
+    if (!force && ns - last_watch_ns.load() < 10'000'000) return;
+    last_watch_ns.store(ns);
+    check_abort();
+    const double age = std::chrono::duration<double>(now - t_start).count();
+    for (int r = 0; r < world; ++r) {
+      if (r == rank || (only >= 0 && r != only)) continue;
+      std::string d;
+      switch (peer(r, &d)) {
+        case Peer::Failed:
+          throw PeerError(r, "failed", fmt("rank %d failed: %s", r, d.c_str()));
+        case Peer::Dead:
+          throw PeerError(r, "dead", fmt("rank %d (%s) exited before the rendezvous completed", r, d.c_str()));
+        case Peer::Missing:
+          if (age > peer_timeout_s)
+            throw PeerError(r, "missing", fmt("rank %d never started (no liveness record after %.1f s)", r, age));
+          break;
+        default:
+          break;
+      }
+    }
+  }
+
+  // wait for a payload published by rank `from` (-1: any rank may be the source)
+  std::vector<char> fetch(const std::string& name, size_t n, int from = -1) const {
     auto t0 = Clock::now();
     for (;;) {
       FILE* f = fopen(path(name).c_str(), "rb");
@@ -308,6 +463,7 @@ struct Rendezvous {
         fclose(f);
         if (got == n) return buf;
       }
+      watch(from);
       if (secs(t0) > timeout_s) throw std::runtime_error("rendezvous: timeout waiting for " + name);
       std::this_thread::sleep_for(std::chrono::milliseconds(2));
     }
@@ -316,7 +472,24 @@ struct Rendezvous {
   void barrier(const std::string& tag) const {
     char one = 1;
     publish("barrier-" + tag + "-" + std::to_string(rank), &one, 1);
-    for (int r = 0; r < world; ++r) fetch("barrier-" + tag + "-" + std::to_string(r), 1);
+    for (int r = 0; r < world; ++r) fetch("barrier-" + tag + "-" + std::to_string(r), 1, r);
+  }
+
+  // every rank of the run has started (or finished)
+  double wait_peers() const {
+    const auto t0 = Clock::now();
+    for (int r = 0; r < world; ++r) {
+      if (r == rank) continue;
+      for (;;) {
+        std::string d;
+        const Peer p = peer(r, &d);
+        if (p == Peer::Alive || p == Peer::Done) break;
+        watch(r, true);
+        if (secs(t0) > timeout_s) throw std::runtime_error(fmt("rendezvous: timeout waiting for rank %d", r));
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+    }
+    return secs(t0);
   }
 };
 
@@ -375,7 +548,8 @@ Step step_vecadd(const Args& args, hipStream_t st) {
 // same GEMM on a private queue between PM4 start/stop packets.  Its output is
 // checked against the HIP path's (checksum of C before and after, C zeroed in
 // between), so the counted dispatch is the validated computation, not a stand-in.
-bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, hipStream_t st, std::string* json) {
+bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int cus, hipStream_t st,
+              std::string* json) {
   const auto tg = Clock::now();
   unsigned long long* cs;
   HIP_OK(hipMalloc(&cs, 16));
@@ -405,18 +579,34 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, hip
   const double mops = r.values[0], busy = r.values[1], waves = r.values[2], gui = r.values[3];
   const double flops = 2.0 * n * (double)n * n;
   const bool same = sums[0] == sums[1] && sums[0] != 0;
-  const bool ok = mops > 0 && busy > 0 && same;
+  avk::GateCounters c;
+  c.mops = mops;
+  c.busy = busy;
+  c.waves = waves;
+  c.gui = gui;
+  c.gui_samples = r.samples[3];
+  c.output_matches = same;
+  const avk::GateVerdict v = avk::gate_verdict(n, n, n, cus, c, a.min_mfma_util);
   *json = fmt("\"counter_gate\": \"%s\", \"gate_mode\": \"aql\", \"dispatches\": 1, "
               "\"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.0f, \"SQ_VALU_MFMA_BUSY_CYCLES\": %.0f, \"SQ_WAVES\": %.0f, "
               "\"GRBM_GUI_ACTIVE\": %.0f, \"flop_per_mop\": %.6g, \"samples\": [%d, %d, %d, %d], "
-              "\"gated_output_matches\": %s, \"gate_seconds\": %.4f, \"gate_setup_seconds\": %.4f, "
-              "\"gate_dispatch_seconds\": %.4f",
-              ok ? "pass" : "fail", mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0, r.samples[0], r.samples[1],
-              r.samples[2], r.samples[3], same ? "true" : "false", secs(tg), r.setup_s, r.dispatch_s);
-  return ok;
+              "\"gated_output_matches\": %s, \"mfma_util\": %.4f, \"mfma_util_floor\": %.4f, "
+              "\"gate_seconds\": %.4f, \"gate_setup_seconds\": %.4f, \"gate_dispatch_seconds\": %.4f",
+              v.ok ? "pass" : "fail", mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0, r.samples[0], r.samples[1],
+              r.samples[2], r.samples[3], same ? "true" : "false", v.mfma_util, v.util_floor, secs(tg), r.setup_s,
+              r.dispatch_s);
+  if (!v.ok) *json += ", \"gate_reason\": \"" + v.reason + "\"";
+  return v.ok;
 }
 
-Step step_gemm(const Args& a, hipStream_t st) {
+// The TF/s floor is calibrated at 4096^3 (BENCH_r02: 1,238 TF/s) and holds
+// for larger problems; a smaller GEMM is launch- and tail-bound (1024^3 runs
+// ~70 TF/s on a healthy MI355X), so below 4096 the rate is reported only.
+double gemm_floor(const Args& a, int n, int cus) {
+  return n >= 4096 ? avk::scale_floor_by_cus(a.min_gemm_tflops, cus) : 0.0;
+}
+
+Step step_gemm(const Args& a, hipStream_t st, int cus) {
   auto t0 = Clock::now();
   Step s{"gemm"};
   const int n = a.gemm_n;
@@ -463,7 +653,7 @@ Step step_gemm(const Args& a, hipStream_t st) {
   // dispatches, so it must not overlap the timed ones
   if (a.counter_gate && a.gate_mode == "aql") {
     std::string gate_json;
-    const bool gate_ok = aql_gate(a, A, B, C16, n, st, &gate_json);
+    const bool gate_ok = aql_gate(a, A, B, C16, n, cus, st, &gate_json);
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
     ms /= a.gemm_iters;
@@ -471,10 +661,12 @@ Step step_gemm(const Args& a, hipStream_t st) {
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) (void)hipFree(p);
-    const bool perf_ok = a.min_gemm_tflops <= 0 || tflops >= a.min_gemm_tflops;
+    const double floor = gemm_floor(a, n, cus);
+    const bool perf_ok = floor <= 0 || tflops >= floor;
     s.ok = numerics_ok && gate_ok && perf_ok;
     s.seconds = secs(t0);
-    s.detail = fmt("\"n\": %d, \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, ", n, rel, ms, tflops) + gate_json;
+    s.detail = fmt("\"n\": %d, \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, \"min_tflops\": %.1f, "
+                   "\"perf_ok\": %s, ", n, rel, ms, tflops, floor, perf_ok ? "true" : "false") + gate_json;
     return s;
   }
   const bool gate = a.counter_gate && g_gate.usable();
@@ -508,22 +700,35 @@ Step step_gemm(const Args& a, hipStream_t st) {
       const double gui = g_gate.value("GRBM_GUI_ACTIVE");
       const int disp = g_gate.dispatches();
       const double flops = 2.0 * n * (double)n * n * (disp > 0 ? disp : 1);
-      gate_ok = disp > 0 && mops > 0 && busy > 0;
+      // the sdk tool reports no per-instance sample count: GRBM_GUI_ACTIVE
+      // is summed over the XCDs (8 on MI355X in SPX, fewer per partition)
+      avk::GateCounters c;
+      c.mops = mops;
+      c.busy = busy;
+      c.waves = waves;
+      c.gui = gui;
+      c.gui_samples = std::max(1, cus / 32);
+      const avk::GateVerdict v = avk::gate_verdict(n, n, n, cus, c, a.min_mfma_util);
+      gate_ok = disp == 1 && v.ok;
       gate_json = fmt("\"counter_gate\": \"%s\", \"gate_mode\": \"sdk\", \"dispatches\": %d, "
                       "\"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.0f, "
                       "\"SQ_VALU_MFMA_BUSY_CYCLES\": %.0f, \"SQ_WAVES\": %.0f, \"GRBM_GUI_ACTIVE\": %.0f, "
-                      "\"flop_per_mop\": %.6g, \"gate_seconds\": %.4f, \"gate_config_seconds\": %.4f",
+                      "\"flop_per_mop\": %.6g, \"mfma_util\": %.4f, \"mfma_util_floor\": %.4f, "
+                      "\"gate_seconds\": %.4f, \"gate_config_seconds\": %.4f",
                       gate_ok ? "pass" : "fail", disp, mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0,
-                      secs(tg), g_gate.config_seconds ? g_gate.config_seconds() : -1.0);
+                      v.mfma_util, v.util_floor, secs(tg), g_gate.config_seconds ? g_gate.config_seconds() : -1.0);
+      if (!gate_ok) gate_json += ", \"gate_reason\": \"" + (disp == 1 ? v.reason : fmt("%d dispatches counted", disp)) + "\"";
     }
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) (void)hipFree(p);
-  const bool perf_ok = a.min_gemm_tflops <= 0 || tflops >= a.min_gemm_tflops;
+  const double floor = gemm_floor(a, n, cus);
+  const bool perf_ok = floor <= 0 || tflops >= floor;
   s.ok = numerics_ok && gate_ok && perf_ok;
   s.seconds = secs(t0);
-  s.detail = fmt("\"n\": %d, \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, ", n, rel, ms, tflops) + gate_json;
+  s.detail = fmt("\"n\": %d, \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, \"min_tflops\": %.1f, "
+                 "\"perf_ok\": %s, ", n, rel, ms, tflops, floor, perf_ok ? "true" : "false") + gate_json;
   return s;
 }
 
@@ -562,9 +767,13 @@ Step step_hbm(const Args& a, hipStream_t st, int cus) {
   (void)hipFree(dst);
   (void)hipFree(cs);
   const double gbps = 2.0 * bytes / (ms * 1e-3) / 1e9;
-  s.ok = h[0] == h[1] && (a.min_hbm_gbps <= 0 || gbps >= a.min_hbm_gbps);
+  // calibrated on a 1 GiB copy; smaller copies are launch-bound: report only
+  const double floor = bytes >= (1ll << 30) ? avk::scale_floor_by_cus(a.min_hbm_gbps, cus) : 0.0;
+  const bool perf_ok = floor <= 0 || gbps >= floor;
+  s.ok = h[0] == h[1] && perf_ok;
   s.seconds = secs(t0);
-  s.detail = fmt("\"bytes\": %lld, \"ms\": %.4f, \"gbps\": %.1f, \"checksum_match\": %s", (long long)bytes, ms, gbps,
+  s.detail = fmt("\"bytes\": %lld, \"ms\": %.4f, \"gbps\": %.1f, \"min_gbps\": %.1f, \"perf_ok\": %s, "
+                 "\"checksum_match\": %s", (long long)bytes, ms, gbps, floor, perf_ok ? "true" : "false",
                  h[0] == h[1] ? "true" : "false");
   return s;
 }
@@ -613,7 +822,7 @@ Step step_xgmi(const Args& a, hipStream_t st, const Rendezvous& rv) {
         ptrs[r] = in;
         continue;
       }
-      auto buf = rv.fetch(a.run_id + "-ipc-" + std::to_string(r), sizeof(hipIpcMemHandle_t));
+      auto buf = rv.fetch(a.run_id + "-ipc-" + std::to_string(r), sizeof(hipIpcMemHandle_t), r);
       memcpy(&handles[r], buf.data(), sizeof(hipIpcMemHandle_t));
       void* p = nullptr;
       HIP_OK(hipIpcOpenMemHandle(&p, handles[r], hipIpcMemLazyEnablePeerAccess));
@@ -674,13 +883,62 @@ Step step_xgmi(const Args& a, hipStream_t st, const Rendezvous& rv) {
 }
 
 // Communicator set-up, run on its own thread from the start of the process.
+// ncclCommInitRank blocks in RCCL's bootstrap until every rank has joined -
+// forever, if one never does.  RCCL 7.2 blocks there even for a non-blocking
+// config (ncclConfig_t.blocking = 0 did not return before the peers arrived,
+// profiles/r3_multirank), so the bound is enforced by the consumer instead:
+// step_rccl waits for `done` while watching the rendezvous, and when a peer
+// is missing, dead or failed - or the set-up outlives --peer-timeout - it
+// reports the failure with the rank named and abandons this thread, which
+// the process exit (_exit) ends.  Nothing GPU-side is left behind: the
+// bootstrap has not allocated device resources before all ranks connect.
 struct RcclInit {
   ncclComm_t comm = nullptr;
   double init_s = 0, load_s = 0;
   std::string error;
+  int failed_peer = -1;
+  std::string peer_state;
+  std::atomic<bool> started{false}, done{false};
+  Clock::time_point t_begin;
+  bool abandoned = false;  // the consumer gave up on it (main must not join)
 };
 
+// ncclCommAbort on a helper thread, waited for at most grace_s: the process
+// reports and exits either way (_exit ends a teardown stuck in the bootstrap)
+void abort_comm(ncclComm_t comm, double grace_s) {
+  if (!comm || !g_rccl.CommAbort) return;
+  auto* done = new std::atomic<bool>(false);  // leaked if the abort outlives us
+  std::thread([comm, done] {
+    g_rccl.CommAbort(comm);
+    done->store(true);
+  }).detach();
+  const auto t0 = Clock::now();
+  while (!done->load() && secs(t0) < grace_s) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+}
+
+// Poll a non-blocking communicator until its pending operation completes.
+void nccl_settle(ncclComm_t comm, const Rendezvous& rv, double deadline_s, const char* what) {
+  const auto t0 = Clock::now();
+  for (;;) {
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t q = g_rccl.GetAsyncError(comm, &st);
+    if (q != ncclSuccess) throw std::runtime_error(std::string("ncclCommGetAsyncError: ") + g_rccl.GetErrorString(q));
+    if (st == ncclSuccess) return;
+    if (st != ncclInProgress) throw std::runtime_error(std::string(what) + ": " + g_rccl.GetErrorString(st));
+    rv.watch();
+    if (secs(t0) > deadline_s) throw std::runtime_error(fmt("%s: not complete within %.1f s", what, deadline_s));
+    if (g_trace) {
+      static thread_local int last = -1;
+      if ((int)secs(t0) != last) trace("%s: in progress %.0f s", what, (double)(last = (int)secs(t0)));
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(500));
+  }
+}
+
 void rccl_init(const Args& a, const Rendezvous& rv, RcclInit* out) {
+  out->t_begin = Clock::now();
+  out->started.store(true);
+  trace("rccl: init thread start");
   try {
     if (!g_rccl.dl) throw std::runtime_error("librccl not loaded");
     HIP_OK(hipSetDevice(a.device));
@@ -690,27 +948,74 @@ void rccl_init(const Args& a, const Rendezvous& rv, RcclInit* out) {
       NCCL_OK(g_rccl.GetUniqueId(&id));
       rv.publish(idname, &id, sizeof(id));
     } else {
-      auto buf = rv.fetch(idname, sizeof(id));
+      auto buf = rv.fetch(idname, sizeof(id), 0);
       memcpy(&id, buf.data(), sizeof(id));
     }
     auto ti = Clock::now();
-    NCCL_OK(g_rccl.CommInitRank(&out->comm, a.world, id, a.rank));
+    trace("rccl: ncclCommInitRank rank %d/%d", a.rank, a.world);
+    ncclComm_t comm = nullptr;
+    NCCL_OK(g_rccl.CommInitRank(&comm, a.world, id, a.rank));
+    trace("rccl: communicator formed");
+    out->comm = comm;
     out->init_s = secs(ti);
+  } catch (const PeerError& e) {
+    out->error = e.what();
+    out->failed_peer = e.peer;
+    out->peer_state = e.state;
   } catch (const std::exception& e) {
     out->error = e.what();
   }
+  out->done.store(true);
 }
 
-// Times `iters` back-to-back launches of `launch` on `st` (ms per launch).
+// The consumer side of the set-up: wait for the init thread, bounded (see
+// RcclInit).  Throws PeerError / runtime_error with the init marked abandoned.
+void await_rccl_init(const Args& a, const Rendezvous& rv, std::thread* th, RcclInit* ri) {
+  while (!ri->done.load()) {
+    try {
+      rv.watch();
+      if (ri->started.load() && secs(ri->t_begin) > a.peer_timeout_s)
+        throw std::runtime_error(fmt("communicator set-up not complete within %.1f s", a.peer_timeout_s));
+    } catch (...) {
+      ri->abandoned = true;
+      trace("rccl: abandoning the set-up thread");
+      throw;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(500));
+  }
+  th->join();
+}
+
+// Wait for `ev` (recorded after collectives on `st`) without blocking in the
+// runtime: a peer that died mid-collective leaves the kernel spinning on its
+// flags, so the wait watches the communicator and the rendezvous and, past
+// --collective-timeout, aborts the communicator (which ends the kernels).
+void wait_collective(hipEvent_t ev, ncclComm_t comm, const Rendezvous& rv, double timeout_s) {
+  const auto t0 = Clock::now();
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) throw std::runtime_error(std::string("hipEventQuery: ") + hipGetErrorString(q));
+    ncclResult_t st = ncclSuccess;
+    if (g_rccl.GetAsyncError(comm, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
+      throw std::runtime_error(std::string("collective failed: ") + g_rccl.GetErrorString(st));
+    rv.watch();
+    if (secs(t0) > timeout_s) throw std::runtime_error(fmt("collective not complete within %.1f s", timeout_s));
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+}
+
+// Times `iters` back-to-back launches of `launch` on `st` (ms per launch),
+// waiting through wait_collective.
 template <typename F>
-float time_collective(hipStream_t st, int iters, F launch) {
+float time_collective(hipStream_t st, int iters, ncclComm_t comm, const Rendezvous& rv, double timeout_s, F launch) {
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, st));
   for (int i = 0; i < iters; ++i) launch();
   HIP_OK(hipEventRecord(e1, st));
-  HIP_OK(hipEventSynchronize(e1));
+  wait_collective(e1, comm, rv, timeout_s);
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));
   (void)hipEventDestroy(e0);
@@ -725,10 +1030,31 @@ float time_collective(hipStream_t st, int iters, F launch) {
 Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread* init_thread, RcclInit* ri) {
   auto t0 = Clock::now();
   Step s{"rccl"};
-  init_thread->join();
+  try {
+    await_rccl_init(a, rv, init_thread, ri);
+  } catch (const PeerError& e) {
+    throw PeerError(e.peer, e.state, std::string("rccl init: ") + e.what());
+  } catch (const std::exception& e) {
+    throw std::runtime_error(std::string("rccl init: ") + e.what());
+  }
   const double wait_s = secs(t0);
-  if (!ri->error.empty()) throw std::runtime_error("rccl init: " + ri->error);
+  if (!ri->error.empty()) {
+    if (ri->failed_peer >= 0 || !ri->peer_state.empty())
+      throw PeerError(ri->failed_peer, ri->peer_state, "rccl init: " + ri->error);
+    throw std::runtime_error("rccl init: " + ri->error);
+  }
   ncclComm_t comm = ri->comm;
+  // a non-blocking communicator may answer a collective with ncclInProgress
+  auto call = [&](ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) nccl_settle(comm, rv, a.collective_timeout_s, what);
+    else if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + g_rccl.GetErrorString(r));
+  };
+  hipEvent_t done_ev;
+  HIP_OK(hipEventCreateWithFlags(&done_ev, hipEventDisableTiming));
+  auto settle = [&] {
+    HIP_OK(hipEventRecord(done_ev, st));
+    wait_collective(done_ev, comm, rv, a.collective_timeout_s);
+  };
   const int W = a.world;
   const int64_t n = (a.rccl_elems / W) * W;  // divisible for the gather/scatter shapes
   const int64_t per = n / W;
@@ -752,6 +1078,7 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread*
   // operands filled and results checked on the device (avk_fill_const /
   // avk_check_blocks): element i must be base + (i / block) * step
   auto check = [&](const void* x, int64_t count, int bf16, int64_t block, float base, float step) -> int64_t {
+    settle();  // the collective that produced x, bounded
     AVK_OK(avk_check_blocks(x, count, bf16, block, base, step, bad_dev, st));
     unsigned long long bad = 0;
     HIP_OK(hipMemcpyAsync(&bad, bad_dev, sizeof(bad), hipMemcpyDeviceToHost, st));
@@ -763,10 +1090,10 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread*
   // fp32 all-reduce
   const auto t_first = Clock::now();
   AVK_OK(avk_fill_const(buf, n, 0, mine, st));
-  NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st));
+  call(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st), "ncclAllReduce");
   int64_t bad = check(buf, n, 0, n, expect_sum, 0.0f);
   const double first_s = secs(t_first);
-  float ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st)); });
+  float ms = time_collective(st, iters, comm, rv, a.collective_timeout_s, [&] { call(g_rccl.AllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, st), "ncclAllReduce"); });
   const double ar_algbw = n * 4.0 / (ms * 1e-3) / 1e9;
   const double ar_busbw = W > 1 ? ar_algbw * 2.0 * (W - 1) / W : 0.0;
   const float ar_ms = ms;
@@ -774,23 +1101,23 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread*
 
   // bf16 all-reduce (sums up to 36 are exact in bf16)
   AVK_OK(avk_fill_const(aux, n, 1, mine, st));
-  NCCL_OK(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st));
+  call(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st), "ncclAllReduce");
   bad = check(aux, n, 1, n, expect_sum, 0.0f);
-  ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st)); });
+  ms = time_collective(st, iters, comm, rv, a.collective_timeout_s, [&] { call(g_rccl.AllReduce(aux, aux, n, ncclBfloat16, ncclSum, comm, st), "ncclAllReduce"); });
   report("allreduce_bf16", n * 2, ms, W > 1 ? 2.0 * (W - 1) / W : 0.0, bad);
 
   // all-gather: rank r's block holds r+1
   AVK_OK(avk_fill_const(buf, per, 0, mine, st));
-  NCCL_OK(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st));
+  call(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st), "ncclAllGather");
   bad = check(aux, n, 0, per, 1.0f, 1.0f);
-  ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st)); });
+  ms = time_collective(st, iters, comm, rv, a.collective_timeout_s, [&] { call(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st), "ncclAllGather"); });
   report("allgather_f32", n * 4, ms, W > 1 ? (W - 1.0) / W : 0.0, bad);
 
   // reduce-scatter: every element of every rank holds r+1
   AVK_OK(avk_fill_const(buf, n, 0, mine, st));
-  NCCL_OK(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st));
+  call(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st), "ncclReduceScatter");
   bad = check(aux, per, 0, per, expect_sum, 0.0f);
-  ms = time_collective(st, iters, [&] { NCCL_OK(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st)); });
+  ms = time_collective(st, iters, comm, rv, a.collective_timeout_s, [&] { call(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st), "ncclReduceScatter"); });
   report("reducescatter_f32", n * 4, ms, W > 1 ? (W - 1.0) / W : 0.0, bad);
 
   const double checks_s = secs(t_first);
@@ -802,22 +1129,63 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread*
   // arrives, so after it no collective of this communicator is in flight.
   const auto t_destroy = Clock::now();
   rv.barrier(a.run_id + "-rccl-done");
-  if (a.rccl_destroy) NCCL_OK(g_rccl.CommDestroy(comm));
+  if (a.rccl_destroy) call(g_rccl.CommDestroy(comm), "ncclCommDestroy");
   const double destroy_s = secs(t_destroy);
   if (a.rccl_destroy) {
     (void)hipFree(buf);
     (void)hipFree(aux);
     (void)hipFree(bad_dev);
   }
-  s.ok = total_bad == 0;
+  (void)hipEventDestroy(done_ev);
+  const bool bw_ok = W <= 1 || a.min_rccl_busbw_gbps <= 0 || ar_busbw >= a.min_rccl_busbw_gbps;
+  s.ok = total_bad == 0 && bw_ok;
   s.seconds = secs(t0);
-  s.detail = fmt("\"world\": %d, \"bytes\": %lld, \"lib_load_s\": %.4f, \"comm_init_s\": %.4f, \"init_wait_s\": %.4f, "
+  s.detail = fmt("\"min_busbw_gbps\": %.1f, \"perf_ok\": %s, ", W > 1 ? a.min_rccl_busbw_gbps : 0.0,
+                 bw_ok ? "true" : "false") +
+             fmt("\"world\": %d, \"bytes\": %lld, \"lib_load_s\": %.4f, \"comm_init_s\": %.4f, \"init_wait_s\": %.4f, "
                  "\"first_allreduce_s\": %.4f, \"checks_s\": %.4f, \"finish_s\": %.4f, "
                  "\"ms\": %.4f, \"algbw_gbps\": %.1f, \"busbw_gbps\": %.1f, \"mismatches\": %lld, \"collectives\": {",
                  W, (long long)(n * 4), ri->load_s, ri->init_s, wait_s, first_s, checks_s, destroy_s, ar_ms, ar_algbw,
                  ar_busbw, (long long)total_bad) +
              detail + "}, \"library\": \"" + g_rccl.path + "\"";
   return s;
+}
+
+// Every rank of the run is up (liveness records, see Rendezvous) before this
+// one touches the GPU: a rank that was never started or died at once fails
+// the run here, named, before any RCCL bootstrap can block on it.
+Step step_peers(const Args& a, const Rendezvous& rv) {
+  auto t0 = Clock::now();
+  Step s{"peers"};
+  const double w = rv.wait_peers();
+  s.seconds = secs(t0);
+  s.detail = fmt("\"world\": %d, \"wait_s\": %.4f", a.world, w);
+  return s;
+}
+
+// --check-gate: the counter-gate verdict on a counter tuple from the command
+// line (CPU only, tests/test_gate_policy.py)
+int check_gate_cli(const std::string& spec, double min_util) {
+  double v[9];
+  int got = 0;
+  std::stringstream ss(spec);
+  std::string t;
+  while (got < 9 && std::getline(ss, t, ',')) v[got++] = atof(t.c_str());
+  if (got != 9) {
+    fprintf(stderr, "--check-gate takes 9 comma-separated numbers\n");
+    return 2;
+  }
+  avk::GateCounters c;
+  c.mops = v[4];
+  c.busy = v[5];
+  c.waves = v[6];
+  c.gui = v[7];
+  c.gui_samples = (int)v[8];
+  const avk::GateVerdict r = avk::gate_verdict((long long)v[0], (long long)v[1], (long long)v[2], (int)v[3], c, min_util);
+  printf("{\"ok\": %s, \"reason\": \"%s\", \"expected_mops\": %.0f, \"expected_waves\": %.0f, "
+         "\"mfma_util\": %.6f, \"mfma_util_floor\": %.6f}\n",
+         r.ok ? "true" : "false", r.reason.c_str(), r.expected_mops, r.expected_waves, r.mfma_util, r.util_floor);
+  return r.ok ? 0 : 1;
 }
 
 bool has_step(const Args& a, const char* name) {
@@ -833,8 +1201,11 @@ void usage(const char* p) {
           "usage: %s [--device N] [--rank R --world W --rendezvous DIR --run-id ID] [--steps a,b,...]\n"
           "          [--gemm N] [--gemm-iters K] [--hbm-bytes B] [--vecadd-elems N] [--rccl-elems E] [--xgmi-elems E]\n"
           "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--rccl-destroy]\n"
-          "          [--ready-file PATH] [--start-gate FILE] [--gate-mode aql|sdk]\n",
-          p);
+          "          [--ready-file PATH] [--start-gate FILE] [--gate-mode aql|sdk] [--min-mfma-util U]\n"
+          "          [--min-rccl-busbw-gbps X] [--peer-timeout S] [--collective-timeout S]\n"
+          "       %s --check-gate M,N,K,CUS,MOPS,BUSY,WAVES,GUI,GUI_SAMPLES [--min-mfma-util U]\n"
+          "          (gate verdict on a counter tuple; no GPU access)\n",
+          p, p);
 }
 
 }  // namespace
@@ -842,6 +1213,7 @@ void usage(const char* p) {
 int main(int argc, char** argv) {
   auto t_start = Clock::now();
   Args a;
+  std::string check_gate;
   for (int i = 1; i < argc; ++i) {
     std::string k = argv[i];
     auto v = [&]() -> const char* {
@@ -867,6 +1239,11 @@ int main(int argc, char** argv) {
     else if (k == "--emulated-peers") a.emulated_peers = atoi(v());
     else if (k == "--min-gemm-tflops") a.min_gemm_tflops = atof(v());
     else if (k == "--min-hbm-gbps") a.min_hbm_gbps = atof(v());
+    else if (k == "--min-mfma-util") a.min_mfma_util = atof(v());
+    else if (k == "--min-rccl-busbw-gbps") a.min_rccl_busbw_gbps = atof(v());
+    else if (k == "--peer-timeout") a.peer_timeout_s = atof(v());
+    else if (k == "--collective-timeout") a.collective_timeout_s = atof(v());
+    else if (k == "--check-gate") check_gate = v();
     else if (k == "--timeout") a.timeout_s = atof(v());
     else if (k == "--counter-gate") a.counter_gate = true;
     else if (k == "--any-arch") a.any_arch = true;
@@ -889,9 +1266,24 @@ int main(int argc, char** argv) {
     fprintf(stderr, "amdgpu-validator: --gate-mode is aql or sdk\n");
     return 2;
   }
+  if (!check_gate.empty()) return check_gate_cli(check_gate, a.min_mfma_util);
+  if (a.peer_timeout_s <= 0 || a.collective_timeout_s <= 0) {
+    fprintf(stderr, "amdgpu-validator: timeouts must be positive\n");
+    return 2;
+  }
   if (a.counter_gate && a.gate_mode == "sdk") Gate::request();
   mkdir(a.rendezvous.c_str(), 0755);
-  Rendezvous rv{a.rendezvous, a.rank, a.world, a.timeout_s};
+  Rendezvous rv{a.rendezvous, a.rank, a.world, a.timeout_s, a.run_id, a.peer_timeout_s, t_start};
+  // liveness record first: peers waiting on this rank can tell "not started
+  // yet" from "gone" from here on
+  if (a.world > 1) {
+    try {
+      rv.announce();
+    } catch (const std::exception& e) {
+      fprintf(stderr, "amdgpu-validator: %s\n", e.what());
+      return 2;
+    }
+  }
   std::vector<Step> steps;
   bool ok = true;
   std::string error;
@@ -926,6 +1318,10 @@ int main(int argc, char** argv) {
           break;
         }
       }
+      if (std::string why; a.world > 1 && rv.read_text("abort", &why)) {  // a sibling rank failed
+        verdict = "abort";
+        break;
+      }
       if (secs(tg) > a.timeout_s) {
         verdict = "timeout";
         break;
@@ -934,13 +1330,17 @@ int main(int argc, char** argv) {
     }
     gate_wait_s = secs(tg);
     if (verdict != "go") {
+      if (a.world > 1) rv.finish(false, "start gate: " + std::string(verdict == "timeout" ? "timeout" : "aborted"));
       printf("{\"ok\": false, \"rank\": %d, \"world\": %d, \"device\": %d, \"error\": \"start gate: %s\", "
              "\"steps\": []}\n", a.rank, a.world, a.device, verdict == "timeout" ? "timeout" : "aborted");
       fflush(stdout);
       _exit(3);
     }
   }
+  int failed_peer = -1;
+  std::string peer_state;
   try {
+    if (a.world > 1 && has_step(a, "peers")) steps.push_back(step_peers(a, rv));
     steps.push_back(step_hip(a, &prop));
     ok = steps.back().ok;
     if (ok && has_step(a, "rccl") && rccl_state.error.empty())
@@ -949,17 +1349,39 @@ int main(int argc, char** argv) {
     if (!a.null_stream) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     stream_create_s = secs(ts);
     if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
-    if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st)), steps.back().ok);
+    if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st, prop.multiProcessorCount)), steps.back().ok);
     if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
     if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
     if (ok && has_step(a, "xgmi")) ok = (steps.push_back(step_xgmi(a, st, rv)), steps.back().ok);
     if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, rv, &rccl_thread, &rccl_state)), steps.back().ok);
+  } catch (const PeerError& e) {
+    ok = false;
+    error = e.what();
+    failed_peer = e.peer;
+    peer_state = e.state;
   } catch (const std::exception& e) {
     ok = false;
     error = e.what();
   }
-  if (rccl_thread.joinable()) rccl_thread.join();
+  if (rccl_thread.joinable()) {
+    if (rccl_state.abandoned) rccl_thread.detach();  // blocked in RCCL's bootstrap: ends with the process
+    else rccl_thread.join();
+  }
+  // a collective that failed or timed out may leave kernels spinning on a
+  // dead peer's flags: abort the communicator (bounded) before reporting
+  if (!ok && rccl_state.comm) abort_comm(rccl_state.comm, 2.0);
+  if (!ok && error.empty()) {
+    for (const auto& stp : steps)
+      if (!stp.ok) {
+        error = "step " + stp.name + " failed";
+        break;
+      }
+  }
+  // siblings learn of the outcome from the rendezvous before the report is out
+  if (a.world > 1) rv.finish(ok, error);
+  trace("steps done (ok=%d)", (int)ok);
   if (st) (void)hipStreamDestroy(st);
+  trace("stream destroyed");
   const double total = secs(t_start);
   std::string out = fmt("{\"ok\": %s, \"rank\": %d, \"world\": %d, \"device\": %d, \"seconds\": %.4f, ", ok ? "true" : "false",
                         a.rank, a.world, a.device, total);
@@ -972,6 +1394,7 @@ int main(int argc, char** argv) {
     for (char c : error) esc += (c == '"' || c == '\\') ? '\'' : c;
     out += "\"error\": \"" + esc + "\", ";
   }
+  if (!peer_state.empty()) out += fmt("\"failed_peer\": %d, \"peer_state\": \"%s\", ", failed_peer, peer_state.c_str());
   out += "\"steps\": [";
   for (size_t i = 0; i < steps.size(); ++i) {
     out += fmt("%s{\"name\": \"%s\", \"ok\": %s, \"seconds\": %.4f", i ? ", " : "", steps[i].name.c_str(),
@@ -980,6 +1403,7 @@ int main(int argc, char** argv) {
     out += "}";
   }
   out += "]}";
+  trace("report");
   puts(out.c_str());
   fflush(stdout);
   if (ok && !a.ready_file.empty()) {
@@ -998,7 +1422,8 @@ int main(int argc, char** argv) {
   fflush(stderr);
   // AMDGPU_VALIDATOR_TEARDOWN=1: normal exit (profilers such as rocprofv3
   // write their results from the runtime's teardown)
-  if (const char* t = getenv("AMDGPU_VALIDATOR_TEARDOWN"); t && strcmp(t, "1") == 0) return ok ? 0 : 1;
+  if (const char* t = getenv("AMDGPU_VALIDATOR_TEARDOWN"); t && strcmp(t, "1") == 0 && !rccl_state.abandoned)
+    return ok ? 0 : 1;
   // Close our ends of stdout/stderr before exiting: a parent that takes the
   // report as the result (AMDGPU_REPORT_EARLY) sees EOF now, while the
   // kernel is still releasing this process's GPU queues and memory.

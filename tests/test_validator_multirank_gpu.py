@@ -1,0 +1,125 @@
+"""N >= 2 validator runs that cannot complete end within their deadline, on
+the one MI355X of the box (tests/test_validator_rendezvous.py has the CPU
+side of the protocol).
+
+Rank 0 runs the RCCL step (ncclCommInitRank on its set-up thread, awaited
+against the rendezvous): its peer is either never launched, or launched and
+killed after publishing its liveness record.  Either way rank 0 must report
+the failed rank by number within the deadline, abandon the set-up thread
+blocked in RCCL's bootstrap and exit - no process of the run may be left
+holding the GPU.
+
+Also here: the Ready-gate floors with teeth - the same binary with a floor
+above what the GPU delivers fails the node."""
+
+import json
+import os
+import subprocess
+import time
+
+import pytest
+
+from amdgpu_operator import native
+
+pytestmark = pytest.mark.gpu
+VALIDATOR = str(native.binary("amdgpu-validator"))
+
+
+def _spawn(rdv, rank, steps, extra=()):
+    return subprocess.Popen([VALIDATOR, "--rank", str(rank), "--world", "2", "--device", "0", "--rendezvous", str(rdv),
+                             "--run-id", "mr", "--steps", steps, "--rccl-elems", "1048576", *extra],
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                            env={**os.environ, "AMDGPU_VALIDATOR_TEARDOWN": "0"})
+
+
+def _gone(pid: int, timeout: float = 15.0) -> bool:
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if not os.path.exists(f"/proc/{pid}"):
+            return True
+        time.sleep(0.05)
+    return False
+
+
+def _kfd_holders(pids) -> list[int]:
+    out = []
+    for pid in pids:
+        try:
+            for fd in os.listdir(f"/proc/{pid}/fd"):
+                if os.readlink(f"/proc/{pid}/fd/{fd}") == "/dev/kfd":
+                    out.append(pid)
+                    break
+        except OSError:
+            pass
+    return out
+
+
+def test_rccl_rank_never_launched_fails_within_deadline(tmp_path):
+    t0 = time.monotonic()
+    p0 = _spawn(tmp_path, 0, "hip,rccl", ["--peer-timeout", "4"])
+    out, err = p0.communicate(timeout=60)
+    took = time.monotonic() - t0
+    rep = json.loads(out.strip().splitlines()[-1])
+    print(json.dumps({"took_s": round(took, 3), "report": rep}))
+    assert p0.returncode == 1 and not rep["ok"]
+    assert rep["failed_peer"] == 1 and rep["peer_state"] == "missing", rep
+    assert "rank 1 never started" in rep["error"] and "rccl init" in rep["error"]
+    assert took < 4 + 10  # deadline + the hip step + a bounded abort
+    p0.wait()
+    assert _gone(p0.pid) and not _kfd_holders([p0.pid])
+
+
+def test_rccl_rank_killed_after_publishing_fails_at_once(tmp_path):
+    gate = tmp_path / "gate"
+    gate.write_text("")
+    p1 = _spawn(tmp_path, 1, "hip,rccl", ["--start-gate", str(gate)])
+    deadline = time.monotonic() + 30
+    while not (tmp_path / "mr-alive-1").exists():
+        assert time.monotonic() < deadline and p1.poll() is None
+        time.sleep(0.01)
+    t0 = time.monotonic()
+    p0 = _spawn(tmp_path, 0, "hip,rccl", ["--peer-timeout", "60"])
+    time.sleep(0.5)  # rank 0 is in its RCCL set-up, rank 1 published and waits at its gate
+    p1.kill()
+    p1.wait()
+    out, err = p0.communicate(timeout=60)
+    took = time.monotonic() - t0
+    rep = json.loads(out.strip().splitlines()[-1])
+    print(json.dumps({"took_s": round(took, 3), "report": rep}))
+    assert p0.returncode == 1 and rep["failed_peer"] == 1 and rep["peer_state"] == "dead", rep
+    assert f"pid {p1.pid}" in rep["error"]
+    assert took < 15  # not the 60 s peer timeout
+    p0.wait()
+    assert _gone(p0.pid) and _gone(p1.pid) and not _kfd_holders([p0.pid, p1.pid])
+
+
+def _local(tmp_path, steps, extra):
+    p = subprocess.run([VALIDATOR, "--rendezvous", str(tmp_path), "--steps", steps, *extra],
+                       capture_output=True, text=True, timeout=120)
+    rep = json.loads(p.stdout.strip().splitlines()[-1])
+    return p.returncode, rep, {s["name"]: s for s in rep["steps"]}
+
+
+def test_default_floors_pass_on_a_healthy_mi355x(tmp_path):
+    rc, rep, st = _local(tmp_path, "hip,gemm,hbm", ["--counter-gate", "--min-gemm-tflops", "620",
+                                                    "--min-hbm-gbps", "3700", "--min-mfma-util", "0.2"])
+    print(json.dumps({k: {f: st[k].get(f) for f in ("tflops", "gbps", "mfma_util", "mfma_util_floor")} for k in st}))
+    assert rc == 0 and rep["ok"], rep
+    assert st["gemm"]["perf_ok"] and st["hbm"]["perf_ok"] and st["gemm"]["counter_gate"] == "pass"
+    assert st["gemm"]["mfma_util"] >= 0.2
+
+
+def test_floor_above_the_gpu_fails_the_node(tmp_path):
+    rc, rep, st = _local(tmp_path, "hip,gemm", ["--min-gemm-tflops", "100000"])
+    assert rc == 1 and not rep["ok"] and st["gemm"]["perf_ok"] is False
+    rc, rep, st = _local(tmp_path, "hip,hbm", ["--min-hbm-gbps", "100000"])
+    assert rc == 1 and st["hbm"]["perf_ok"] is False
+    rc, rep, st = _local(tmp_path, "hip,gemm", ["--counter-gate", "--min-mfma-util", "0.99"])
+    assert rc == 1 and st["gemm"]["counter_gate"] == "fail" and "below floor" in st["gemm"]["gate_reason"]
+
+
+def test_small_gemm_gate_util_recorded(tmp_path):
+    # the plugin-pod size: occupancy-scaled floor still passes
+    rc, rep, st = _local(tmp_path, "hip,gemm", ["--gemm", "1024", "--counter-gate", "--min-mfma-util", "0.2"])
+    print(json.dumps({f: st["gemm"].get(f) for f in ("mfma_util", "mfma_util_floor", "tflops")}))
+    assert rc == 0 and st["gemm"]["counter_gate"] == "pass", rep
