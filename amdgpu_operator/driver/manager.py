@@ -195,11 +195,48 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
     out = {"ok": True, "message": msg, "gpus": len(gpus), "driver_version": cur, "installed": ran_script,
            "host_managed": host_managed, "seconds": time.perf_counter() - t0}
     write_ready(env, "driver", out)
-    try:  # validated afresh: an earlier loss is settled
-        os.unlink(env.validation_file(LOST_MARKER))
-    except FileNotFoundError:
-        pass
+    # The module went away since the node was last validated (lost, or
+    # unloaded by a driver container's exit): what the validator and the
+    # device plugin hold belongs to the old driver instance - their pods
+    # (waiting in stop, or serving stale device handles) are restarted, so the
+    # node is validated and advertised afresh on this driver.
+    if _claim_lost_marker(env):
+        out["restarted"] = _restart_node_operands(env)
+        log.info("driver back after a loss/unload; restarted %s", out["restarted"])
     return out
+
+
+def _claim_lost_marker(env: NodeEnv) -> bool:
+    """Take the loss marker (True for exactly one of the driver container and
+    its health monitor, whichever sees the driver back first)."""
+    marker = env.validation_file(LOST_MARKER)
+    claimed = f"{marker}.claimed.{os.getpid()}.{threading.get_ident()}"
+    try:
+        os.replace(marker, claimed)
+    except FileNotFoundError:
+        return False
+    os.unlink(claimed)
+    return True
+
+
+def _withdraw_validation(env: NodeEnv, reason: str) -> None:
+    """The node's validation no longer holds: remember why (the loss marker,
+    :func:`_claim_lost_marker`), drop every ready file and the node's
+    ``amd.com/gpu.validated`` labels."""
+    from ..validator.validate import MFMA_LABEL, VALIDATED_LABEL
+
+    os.makedirs(env.validations_dir, exist_ok=True)
+    tmp = env.validation_file(LOST_MARKER + ".tmp")
+    with open(tmp, "w") as f:
+        f.write(reason)
+    os.replace(tmp, env.validation_file(LOST_MARKER))
+    clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
+    if env.client is not None:
+        try:
+            env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": {VALIDATED_LABEL: None,
+                                                                                   MFMA_LABEL: None}}})
+        except Exception as e:  # noqa: BLE001
+            log.warning("could not withdraw %s: %s", VALIDATED_LABEL, e)
 
 
 def kfd_users(env: NodeEnv) -> list[str]:
@@ -224,7 +261,9 @@ def cleanup_on_exit(env: NodeEnv) -> dict:
         log.warning("driver stays loaded: GPU in use by %d process(es) %s", len(users), users[:8])
         return {"unloaded": False, "reason": f"in use by {users[:8]}"}
     _release_gated_validators(env)
-    clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
+    # as for a lost driver: the node is unvalidated from here on, and the next
+    # driver pod's install restarts the validator and device plugin
+    _withdraw_validation(env, "amdgpu unloaded on driver container exit")
     try:
         _kmod(env).unload(env)
     except Exception as e:  # noqa: BLE001 - leave it loaded, say why
@@ -266,30 +305,20 @@ def monitor_once(env: NodeEnv) -> bool:
     pods of this node are restarted, so the GPUs are validated and advertised
     afresh; until then the ClusterPolicy reports the node not validated."""
     from ..discovery import topology
-    from ..validator.validate import MFMA_LABEL, VALIDATED_LABEL
 
     ok, msg = topology.probe(env.sysfs_root())
     path = env.validation_file(READY_FILES["driver"])
     marker = env.validation_file(LOST_MARKER)
     if not ok and os.path.exists(path):
         log.error("driver lost: %s", msg)
-        os.makedirs(env.validations_dir, exist_ok=True)
-        with open(marker, "w") as f:
-            f.write(msg)
-        clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
-        if env.client is not None:
-            try:
-                env.client.patch("v1", "Node", env.node_name,
-                                 {"metadata": {"labels": {VALIDATED_LABEL: None, MFMA_LABEL: None}}})
-            except Exception as e:  # noqa: BLE001
-                log.warning("could not withdraw %s: %s", VALIDATED_LABEL, e)
+        _withdraw_validation(env, msg)
     elif ok and os.path.exists(marker) and not os.path.exists(path):
         gpus = topology.enumerate_gpus(env.sysfs_root())
         write_ready(env, "driver", {"ok": True, "message": msg, "gpus": len(gpus), "recovered": True,
                                     "driver_version": loaded_version(env), "seconds": 0.0})
-        os.unlink(marker)
-        restarted = _restart_node_operands(env)
-        log.info("driver back (%s); restarted %s", msg, restarted)
+        if _claim_lost_marker(env):
+            restarted = _restart_node_operands(env)
+            log.info("driver back (%s); restarted %s", msg, restarted)
     return ok
 
 

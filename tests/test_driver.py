@@ -265,6 +265,34 @@ def test_driver_container_exit_unloads_only_its_own_idle_module(node_env):
     assert V.read_ready(node_env, "driver") is None and V.read_ready(node_env, "workload") is None
 
 
+def test_driver_container_exit_withdraws_validation_and_next_install_restarts_operands(node_env):
+    """An unload on exit is a driver loss for the node: the validated labels
+    go at once, and the next driver pod's install restarts the validator and
+    device-plugin pods so the node is validated again on the new module."""
+    kmod = fakesys.SimModule(node_env.sysfs_root())
+    node_env.extra["kmod"] = kmod
+    c = node_env.client
+    cenv = {"AMDGPU_DRIVER_VERSION": "6.14.0", "AMDGPU_DRIVER_SPEC_HASH": "h2"}
+    DM.install(node_env, timeout=5, cenv=cenv)
+    c.create(R.new("v1", "Namespace", node_env.namespace))
+    c.patch("v1", "Node", "n1", {"metadata": {"labels": {V.VALIDATED_LABEL: "true", V.MFMA_LABEL: "bf16"}}})
+    for app in ("amd-operator-validator", "amd-device-plugin-daemonset", "amd-metrics-exporter"):
+        c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"{app}-x", "namespace": node_env.namespace,
+                                                                    "labels": {"app": app}},
+                  "spec": {"nodeName": "n1"}})
+    assert DM.cleanup_on_exit(node_env)["unloaded"]
+    labels = c.get("v1", "Node", "n1")["metadata"].get("labels") or {}
+    assert V.VALIDATED_LABEL not in labels and V.MFMA_LABEL not in labels
+    assert os.path.exists(node_env.validation_file(DM.LOST_MARKER))
+    out = DM.install(node_env, timeout=5, cenv=cenv)  # the replacement driver pod
+    assert out["installed"] and sorted(out["restarted"]) == ["amd-device-plugin-daemonset-x", "amd-operator-validator-x"]
+    assert not os.path.exists(node_env.validation_file(DM.LOST_MARKER))
+    left = {p["metadata"]["name"] for p in c.list("v1", "Pod", node_env.namespace)}
+    assert left == {"amd-metrics-exporter-x"}
+    # and only once: the health monitor finds nothing left to recover
+    assert DM.monitor_once(node_env) and "restarted" not in DM.install(node_env, timeout=5, cenv=cenv)
+
+
 def test_driver_container_exit_leaves_a_host_module(node_env):
     kmod = fakesys.SimModule(node_env.sysfs_root())
     node_env.extra["kmod"] = kmod

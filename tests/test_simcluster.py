@@ -139,6 +139,40 @@ def test_driver_loss_triggers_revalidation(cluster_factory):
     assert os.path.exists(env.validation_file("toolkit-ready"))
 
 
+def test_deleted_driver_pod_that_installed_the_module_revalidates(cluster_factory):
+    """A driver pod that installed amdgpu unloads it when deleted
+    (driver.unloadOnExit): the node loses its validation, and its replacement
+    installs the module again and restarts the validator and device plugin,
+    so the node is validated afresh - not left labelled validated on a
+    module that was gone."""
+    from amdgpu_operator.driver import manager as DM
+    from amdgpu_operator.validator.validate import read_ready
+
+    c = cluster_factory([NodeSpec("gpu-1", 2)])
+    c.install_operator(parse_set_flags(REFERENCE_SET_FLAGS + ["driver.driverVersion=6.14.0"]))
+    c.wait_ready(60, {"gpu-1": 2})
+    env = c.nodes["gpu-1"].env
+    kmod = env.extra["kmod"]
+    assert DM.read_state(env)["installed"] and kmod.log[-1] == "install 6.14.0"
+    before = read_ready(env, "workload")["time"]
+    old = {p["metadata"]["uid"] for p in c.pods() if p["metadata"]["name"].startswith(
+        ("amd-operator-validator", "amd-device-plugin"))}
+    drv = next(p for p in c.pods() if p["metadata"]["name"].startswith("amd-driver-daemonset"))
+    c.client.delete("v1", "Pod", drv["metadata"]["name"], c.namespace)
+    deadline = time.time() + 60
+    while time.time() < deadline and not (
+            (read_ready(env, "workload") or {}).get("time", 0) > before and read_ready(env, "complete")
+            and labels(c, "gpu-1").get("amd.com/gpu.validated") == "true"):
+        time.sleep(0.05)
+    assert kmod.log[-2:] == ["unload", "install 6.14.0"]
+    assert read_ready(env, "workload")["time"] > before  # validated again on the reinstalled module
+    assert labels(c, "gpu-1").get("amd.com/gpu.validated") == "true"
+    new = {p["metadata"]["uid"] for p in c.pods() if p["metadata"]["name"].startswith(
+        ("amd-operator-validator", "amd-device-plugin"))}
+    assert not (old & new)  # both restarted
+    c.wait_ready(60, {"gpu-1": 2})
+
+
 def test_replaced_validator_pod_validates_again(cluster_factory):
     """Deleting the validator pod withdraws its workload/plugin/validated
     files; the DaemonSet's replacement runs the GPU checks again (the
