@@ -42,6 +42,16 @@ def _client(args):
         return RestClient.from_kubeconfig()
 
 
+def _stop_on_signals() -> threading.Event:
+    """An event set by SIGTERM / SIGINT (how the kubelet stops a container)."""
+    import signal
+
+    stop = threading.Event()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, lambda *_: stop.set())
+    return stop
+
+
 def _common(p):
     p.add_argument("--namespace", default=DEFAULT_NAMESPACE)
     p.add_argument("--kubeconfig", default=None)
@@ -90,14 +100,10 @@ def main(argv: list[str] | None = None) -> int:
             client = None  # node-local operands (driver, toolkit) work without the API
         env = NodeEnv.from_environ(client)
         import os
-        import signal
 
         # the kubelet stops a container with SIGTERM: operands then run their
         # shutdown (toolkit cleanup, vfio unbind, plugin socket removal)
-        stop = threading.Event()
-        for sig in (signal.SIGTERM, signal.SIGINT):
-            signal.signal(sig, lambda *_: stop.set())
-        return run_operand(env, argv, stop, container_env=dict(os.environ))
+        return run_operand(env, argv, _stop_on_signals(), container_env=dict(os.environ))
 
     ap = argparse.ArgumentParser(prog="amdgpu-operator")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -160,8 +166,11 @@ def main(argv: list[str] | None = None) -> int:
         client = _client(args)
         rec = ClusterPolicyReconciler(client, args.namespace)
         _health_server(args.health_port, rec.metrics)
+        # a rollout or pod delete (SIGTERM) ends the reconcile loop and, with
+        # leader election, releases the Lease so the standby takes over at once
+        stop = _stop_on_signals()
         if not args.leader_elect:
-            rec.run(threading.Event(), resync_s=args.resync)
+            rec.run(stop, resync_s=args.resync)
             return 0
         import os
         import socket
@@ -172,7 +181,7 @@ def main(argv: list[str] | None = None) -> int:
         elector = LeaderElector(client, args.leader_election_id, args.namespace, identity,
                                 lease_s=args.lease_seconds, renew_deadline_s=args.lease_seconds * 2 / 3,
                                 retry_period_s=args.lease_seconds / 7.5)
-        lost = elector.run(threading.Event(), lambda ended: rec.run(ended, resync_s=args.resync))
+        lost = elector.run(stop, lambda ended: rec.run(ended, resync_s=args.resync))
         # leadership lost: exit so the Deployment restarts this replica as a standby
         return 1 if lost else 0
     if args.cmd == "cleanup-crd":

@@ -8,9 +8,15 @@ over the same DaemonSets.  Same protocol as client-go's leaderelection:
 * the Lease ``spec`` holds ``holderIdentity``, ``leaseDurationSeconds``,
   ``acquireTime``, ``renewTime`` and ``leaseTransitions``;
 * a candidate takes the Lease when it does not exist, when it holds it
-  already, or when ``renewTime + leaseDurationSeconds`` has passed; every
-  write is an update on the read ``resourceVersion``, so of two candidates
-  racing for an expired Lease exactly one wins (the other gets a Conflict);
+  already, when it was released (empty holder), or when the record has not
+  changed for ``leaseDurationSeconds`` of the candidate's OWN monotonic
+  clock: expiry is measured from the local time at which the candidate last
+  saw (holder, renewTime, resourceVersion) change, never by comparing the
+  holder's ``renewTime`` - written with the holder's clock - against the
+  candidate's wall clock, so skewed node clocks cannot hand a live lease to
+  a standby (client-go's observedRecord/observedTime); every write is an
+  update on the read ``resourceVersion``, so of two candidates racing for an
+  expired Lease exactly one wins (the other gets a Conflict);
 * the leader renews every ``retry_period``; if it cannot renew within
   ``renew_deadline`` it stops leading (the caller stops its controller and
   the process exits, so a standby takes over after the lease expires);
@@ -49,7 +55,8 @@ def parse_micro_time(s: str | None) -> float | None:
 
 class LeaderElector:
     def __init__(self, client, name: str, namespace: str, identity: str, lease_s: float = 15.0,
-                 renew_deadline_s: float = 10.0, retry_period_s: float = 2.0, clock=time.time):
+                 renew_deadline_s: float = 10.0, retry_period_s: float = 2.0, clock=time.time,
+                 mono=time.monotonic):
         if not retry_period_s < renew_deadline_s < lease_s:
             raise ValueError("need retry_period < renew_deadline < lease duration")
         self.client = client
@@ -59,9 +66,12 @@ class LeaderElector:
         self.lease_s = lease_s
         self.renew_deadline_s = renew_deadline_s
         self.retry_period_s = retry_period_s
-        self.clock = clock
+        self.clock = clock  # wall time: only what this candidate writes into the Lease
+        self.mono = mono    # local monotonic time: all expiry decisions
         self.leading = threading.Event()
         self.transitions_seen = 0
+        self._observed: tuple | None = None  # (holder, renewTime, resourceVersion) last seen
+        self._observed_at = 0.0               # self.mono() when it last changed
 
     # -------------------------------------------------------------- one try
     def try_acquire_or_renew(self) -> bool:
@@ -81,11 +91,13 @@ class LeaderElector:
                 return False
         spec = lease.setdefault("spec", {})
         holder = spec.get("holderIdentity") or ""
-        renewed = parse_micro_time(spec.get("renewTime")) or 0.0
         duration = float(spec.get("leaseDurationSeconds") or self.lease_s)
         self.transitions_seen = int(spec.get("leaseTransitions") or 0)
-        if holder and holder != self.identity and renewed + duration > now:
-            return False  # someone else holds an unexpired lease
+        record = (holder, spec.get("renewTime"), (lease.get("metadata") or {}).get("resourceVersion"))
+        if record != self._observed:
+            self._observed, self._observed_at = record, self.mono()
+        if holder and holder != self.identity and self._observed_at + duration > self.mono():
+            return False  # someone else renewed it within the last lease duration (as seen here)
         if holder != self.identity:
             spec["leaseTransitions"] = self.transitions_seen + 1
             spec["acquireTime"] = micro_time(now)

@@ -29,8 +29,10 @@ def client():
     return c
 
 
-def elector(client, ident, clock, **kw):
-    return LeaderElector(client, "amd-gpu-operator-leader", NS, ident, clock=clock, **kw)
+def elector(client, ident, clock, mono=None, **kw):
+    # the fake clock drives both the written timestamps and the local expiry clock
+    mono = mono or (clock if isinstance(clock, Clock) else time.monotonic)
+    return LeaderElector(client, "amd-gpu-operator-leader", NS, ident, clock=clock, mono=mono, **kw)
 
 
 def test_micro_time_round_trip():
@@ -45,8 +47,10 @@ def test_one_holder_and_takeover_after_expiry(client):
     assert a.try_acquire_or_renew() and not b.try_acquire_or_renew()
     clock.t += 10
     assert a.try_acquire_or_renew()  # renewed
-    clock.t += 14.9
-    assert not b.try_acquire_or_renew()  # a renewed 14.9 s ago, lease 15 s
+    clock.t += 0.1
+    assert not b.try_acquire_or_renew()  # b sees the renewal 0.1 s after it happened
+    clock.t += 14.8
+    assert not b.try_acquire_or_renew()  # unchanged for 14.8 s of b's clock, lease 15 s
     clock.t += 0.2
     assert b.try_acquire_or_renew()  # expired: b takes over
     spec = client.get(LEASE_API, "Lease", "amd-gpu-operator-leader", NS)["spec"]
@@ -54,14 +58,46 @@ def test_one_holder_and_takeover_after_expiry(client):
     assert not a.try_acquire_or_renew()
 
 
+class SkewedClock:
+    def __init__(self, base: Clock, skew: float):
+        self.base, self.skew = base, skew
+
+    def __call__(self):
+        return self.base.t + self.skew
+
+
+@pytest.mark.parametrize("skew", [-60.0, +60.0])
+def test_clock_skew_does_not_hand_over_a_live_lease(client, skew):
+    """The holder's wall clock is a minute off: its renewTime looks long
+    expired (or far in the future) to the standby.  Expiry is measured on the
+    standby's own clock from the moment it saw the record change, so the
+    standby takes over only after the holder has really stopped renewing."""
+    clock = Clock()
+    a = elector(client, "a", SkewedClock(clock, skew), mono=clock)
+    b = elector(client, "b", clock)
+    assert a.try_acquire_or_renew()
+    for _ in range(10):  # a keeps renewing every 2 s; b keeps looking
+        assert not b.try_acquire_or_renew()
+        clock.t += 2
+        assert a.try_acquire_or_renew()
+    # a dies: the record stops changing; b takes over one lease duration later
+    assert not b.try_acquire_or_renew()
+    clock.t += 14.9
+    assert not b.try_acquire_or_renew()
+    clock.t += 0.2
+    assert b.try_acquire_or_renew()
+
+
 def test_racing_candidates_one_wins(client):
     clock = Clock()
     a = elector(client, "a", clock)
     assert a.try_acquire_or_renew()
-    clock.t += 60  # a is long gone
+    # b and c have watched the lease; a stops renewing and is long gone
+    b, c = elector(client, "b", clock), elector(client, "c", clock)
+    assert not b.try_acquire_or_renew() and not c.try_acquire_or_renew()
+    clock.t += 60
     lease = client.get(LEASE_API, "Lease", "amd-gpu-operator-leader", NS)
     # b and c both read the expired lease; both try to take it on the same resourceVersion
-    b, c = elector(client, "b", clock), elector(client, "c", clock)
     orig_get = client.get
     client.get = lambda *a_, **k: R.deep(lease)
     try:
@@ -196,3 +232,40 @@ def test_bring_up_and_upgrade_leave_events(tmp_path):
         assert f"driver upgrade: {U.CORDON}" in reasons and f"driver upgrade: {U.DONE}" in reasons
     finally:
         c.stop()
+
+
+def test_operator_process_releases_the_lease_on_sigterm(tmp_path):
+    """``amdgpu-operator operator --leader-elect`` (the chart default) stops on
+    SIGTERM and releases its Lease, so a standby does not wait out 15 s."""
+    import os
+    import signal
+    import subprocess
+    import sys
+
+    from amdgpu_operator.kube.httpapi import HttpApiServer
+
+    api = FakeApiServer()
+    LocalClient(api).create(R.new("v1", "Namespace", NS))
+    srv = HttpApiServer(api).start()
+    try:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        p = subprocess.Popen([sys.executable, "-m", "amdgpu_operator", "operator", "--server", srv.url,
+                              "--namespace", NS, "--leader-elect", "--health-port", "0"],
+                             cwd=root, env={**os.environ, "POD_NAME": "op-0"},
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        c = LocalClient(api)
+        deadline = time.time() + 60
+        holder = None
+        while time.time() < deadline and holder != "op-0":
+            try:
+                holder = c.get(LEASE_API, "Lease", "amd-gpu-operator-leader", NS)["spec"]["holderIdentity"]
+            except Exception:  # noqa: BLE001 - not created yet
+                pass
+            time.sleep(0.05)
+        assert holder == "op-0", p.stdout.read() if p.poll() is not None else "no lease"
+        p.send_signal(signal.SIGTERM)
+        rc = p.wait(timeout=20)
+        assert rc == 0
+        assert c.get(LEASE_API, "Lease", "amd-gpu-operator-leader", NS)["spec"]["holderIdentity"] == ""
+    finally:
+        srv.stop()

@@ -106,17 +106,31 @@ def rt_env(env, tmp_path):
 
 
 def test_toolkit_crio_dropin(rt_env):
+    """CRI-O injects the GPUs through CDI; it is never pointed at the
+    precreate hooks.d entry (an extension stage its hooks manager rejects -
+    the entry stays for podman)."""
     out = TK.install(rt_env, runtime="crio")
     assert out["runtime"] == "crio" and out["config_changed"] and out["restart_required"]
     text = open(os.path.join(rt_env.crio_config_dir, TK.CRIO_DROPIN)).read()
-    hooks_d = os.path.join(rt_env.install_dir, TK.HOOKS_D)
-    assert f'"{hooks_d}"' in text and '"/usr/share/containers/oci/hooks.d"' in text  # CRI-O's own dirs kept
+    assert "hooks_dir" not in text
     assert f'cdi_spec_dirs = ["{rt_env.cdi_dir}", "/etc/cdi"]' in text
-    hook = json.load(open(os.path.join(hooks_d, TK.HOOK_JSON)))
-    assert hook["stages"] == ["precreate"]
+    hook = json.load(open(os.path.join(rt_env.install_dir, TK.HOOKS_D, TK.HOOK_JSON)))
+    assert hook["stages"] == ["precreate"]  # podman's entry
     assert TK.install(rt_env, runtime="crio")["config_changed"] is False
     TK.uninstall(rt_env)
     assert not os.path.exists(os.path.join(rt_env.crio_config_dir, TK.CRIO_DROPIN))
+
+
+def test_toolkit_crio_without_cdi_uses_a_prestart_hook(rt_env):
+    TK.install(rt_env, runtime="crio", cdi_enabled=False)
+    text = open(os.path.join(rt_env.crio_config_dir, TK.CRIO_DROPIN)).read()
+    pre_d = os.path.join(rt_env.install_dir, TK.HOOKS_PRESTART_D)
+    assert f'"{pre_d}"' in text and '"/usr/share/containers/oci/hooks.d"' in text  # CRI-O's own dirs kept
+    assert os.path.join(rt_env.install_dir, TK.HOOKS_D) not in text
+    hook = json.load(open(os.path.join(pre_d, TK.HOOK_JSON)))
+    assert hook["stages"] == ["prestart"] and hook["hook"]["args"][1] == "prestart"
+    TK.uninstall(rt_env)
+    assert not os.path.exists(os.path.join(pre_d, TK.HOOK_JSON))
 
 
 def test_toolkit_docker_daemon_json(rt_env):
