@@ -234,7 +234,7 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             ready()
             stop.wait()
             if cenv.get("AMDGPU_UNLOAD_ON_EXIT", "true") == "true":
-                drv.cleanup_on_exit(env)
+                drv.cleanup_on_exit(env, owner=drv.owner_id(cenv))
         elif a.action == "monitor":
             ready()
             drv.monitor(env, stop, interval=max(env.poll_s, min(a.interval, 10.0)))
@@ -530,6 +530,15 @@ def _plugin_pod_args(extra: list[str]) -> list[str]:
 def run_in_sim(cluster, run, container: dict, argv: list[str], init: bool) -> None:
     """Simulated kubelet hook: run the operand for ``container`` of ``run``'s pod."""
     cenv = {e["name"]: e["value"] for e in container.get("env", []) if "value" in e}
+    for e in container.get("env", []):  # the downward API, as the kubelet resolves it
+        path = ((e.get("valueFrom") or {}).get("fieldRef") or {}).get("fieldPath")
+        if path:
+            md = run.pod.get("metadata") or {}
+            val = {"metadata.name": md.get("name"), "metadata.uid": md.get("uid"),
+                   "metadata.namespace": md.get("namespace"),
+                   "spec.nodeName": (run.pod.get("spec") or {}).get("nodeName")}.get(path)
+            if val is not None:
+                cenv[e["name"]] = val
     env = run.node.env
     if cenv.get("RUNTIME_PID_FILE"):  # never signal the machine's own container runtime
         cenv["RUNTIME_PID_FILE"] = os.path.join(run.node.dir, cenv["RUNTIME_PID_FILE"].lstrip("/"))

@@ -79,7 +79,10 @@ def _container(name: str, image: str, pull: str, args: list[str], mounts=None, e
                resources=None, readiness=None, ports=None) -> dict:
     c = {"name": name, "image": image, "imagePullPolicy": pull, "command": ["amdgpu-operator"], "args": list(args),
          "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
-                 {"name": "OPERATOR_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}}]
+                 {"name": "OPERATOR_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}},
+                 # which pod instance an operand is (the driver container's module ownership)
+                 {"name": "POD_NAME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}},
+                 {"name": "POD_UID", "valueFrom": {"fieldRef": {"fieldPath": "metadata.uid"}}}]
          + list(env or []),
          "volumeMounts": list(mounts or [])}
     if privileged:

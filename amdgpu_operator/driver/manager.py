@@ -184,8 +184,11 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
     prev = read_state(env)
     installed = ran_script or bool(prev.get("installed") and prev.get("version") == cur and live)
     host_managed = not installed and not cur
+    # this pod now owns the module: a predecessor still shutting down (a
+    # force-deleted pod whose container outlives its API object) must not
+    # unload it from under us (cleanup_on_exit)
     _write_state(env, {"version": cur, "specHash": spec_hash, "installed": installed, "hostManaged": host_managed,
-                       "ts": round(time.time(), 3)})
+                       "owner": owner_id(cenv), "ts": round(time.time(), 3)})
     try:
         env.client.patch("v1", "Node", env.node_name, {"metadata": {"annotations": {
             LOADED_VERSION_ANN: cur or "host", LOADED_HASH_ANN: spec_hash or None}}})
@@ -247,7 +250,12 @@ def kfd_users(env: NodeEnv) -> list[str]:
         return []
 
 
-def cleanup_on_exit(env: NodeEnv) -> dict:
+def owner_id(cenv: dict) -> str:
+    """The driver pod instance (downward API ``POD_UID``, else ``POD_NAME``)."""
+    return cenv.get("POD_UID") or cenv.get("POD_NAME") or ""
+
+
+def cleanup_on_exit(env: NodeEnv, owner: str = "") -> dict:
     """``amd-driver-ctr`` stopped (SIGTERM: helm uninstall, driver disabled, node
     left the GPU pool): unload the module this container installed, like the
     upstream driver container's shutdown.  A host-managed or inbox module is
@@ -256,6 +264,9 @@ def cleanup_on_exit(env: NodeEnv) -> dict:
     st = read_state(env)
     if not st.get("installed"):
         return {"unloaded": False, "reason": "module not installed by the driver container"}
+    if owner and st.get("owner") and st["owner"] != owner:
+        log.info("driver stays loaded: taken over by driver pod %s", st["owner"])
+        return {"unloaded": False, "reason": f"taken over by {st['owner']}"}
     users = kfd_users(env)
     if users:
         log.warning("driver stays loaded: GPU in use by %d process(es) %s", len(users), users[:8])

@@ -223,7 +223,7 @@ def test_install_replaces_a_mismatched_module_through_the_backend(node_env):
     assert out["installed"] and out["driver_version"] == "6.14.0"
     assert kmod.log == ["unload", "install 6.14.0"]
     assert DM.read_state(node_env) | {"ts": 0} == {"version": "6.14.0", "specHash": "h2", "installed": True,
-                                                   "hostManaged": False, "ts": 0}
+                                                   "hostManaged": False, "owner": "", "ts": 0}
     ann = node_env.client.get("v1", "Node", "n1")["metadata"]["annotations"]
     assert ann["amd.com/gpu-driver.version"] == "6.14.0" and ann["amd.com/gpu-driver.spec-hash"] == "h2"
     # same version, same spec: nothing to do
@@ -291,6 +291,22 @@ def test_driver_container_exit_withdraws_validation_and_next_install_restarts_op
     assert left == {"amd-metrics-exporter-x"}
     # and only once: the health monitor finds nothing left to recover
     assert DM.monitor_once(node_env) and "restarted" not in DM.install(node_env, timeout=5, cenv=cenv)
+
+
+def test_driver_pod_that_was_taken_over_leaves_the_module(node_env):
+    """A force-deleted driver pod can still be shutting down when its
+    replacement has started: the replacement owns the module from its install
+    on, and the old pod's exit must not unload it from under it."""
+    kmod = fakesys.SimModule(node_env.sysfs_root())
+    node_env.extra["kmod"] = kmod
+    cenv = {"AMDGPU_DRIVER_VERSION": "6.14.0", "AMDGPU_DRIVER_SPEC_HASH": "h2"}
+    DM.install(node_env, timeout=5, cenv={**cenv, "POD_UID": "old"})
+    DM.install(node_env, timeout=5, cenv={**cenv, "POD_UID": "new"})  # replacement: takes over
+    assert DM.read_state(node_env)["owner"] == "new"
+    out = DM.cleanup_on_exit(node_env, owner="old")
+    assert not out["unloaded"] and "taken over by new" in out["reason"]
+    assert DM.loaded_version(node_env) == "6.14.0" and V.read_ready(node_env, "driver") is not None
+    assert DM.cleanup_on_exit(node_env, owner="new")["unloaded"]
 
 
 def test_driver_container_exit_leaves_a_host_module(node_env):

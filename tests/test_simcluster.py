@@ -148,7 +148,8 @@ def test_deleted_driver_pod_that_installed_the_module_revalidates(cluster_factor
     from amdgpu_operator.driver import manager as DM
     from amdgpu_operator.validator.validate import read_ready
 
-    c = cluster_factory([NodeSpec("gpu-1", 2)])
+    # kubelet-confirmed deletes: the replacement pod starts after the old one's exit cleanup, as on a cluster
+    c = cluster_factory([NodeSpec("gpu-1", 2)], termination_s=0.0)
     c.install_operator(parse_set_flags(REFERENCE_SET_FLAGS + ["driver.driverVersion=6.14.0"]))
     c.wait_ready(60, {"gpu-1": 2})
     env = c.nodes["gpu-1"].env
@@ -164,6 +165,7 @@ def test_deleted_driver_pod_that_installed_the_module_revalidates(cluster_factor
             (read_ready(env, "workload") or {}).get("time", 0) > before and read_ready(env, "complete")
             and labels(c, "gpu-1").get("amd.com/gpu.validated") == "true"):
         time.sleep(0.05)
+    assert time.time() < deadline, c.diagnostics() if hasattr(c, "diagnostics") else "not revalidated"
     assert kmod.log[-2:] == ["unload", "install 6.14.0"]
     assert read_ready(env, "workload")["time"] > before  # validated again on the reinstalled module
     assert labels(c, "gpu-1").get("amd.com/gpu.validated") == "true"
