@@ -42,6 +42,30 @@ def _client(args):
         return RestClient.from_kubeconfig()
 
 
+def _ready_signal():
+    """``AMDGPU_READY_FILE``: the operand's readiness as a file (written when
+    the operand calls ``ready()``), for a supervisor without in-process
+    callbacks - the simulated kubelet of a ``process_containers`` SimCluster,
+    or a file-based readinessProbe.  ``<file>.started`` records when the
+    operand's main began (interpreter + imports done)."""
+    import os
+
+    path = os.environ.get("AMDGPU_READY_FILE")
+    if not path:
+        return lambda: None
+
+    def write(p, text):
+        tmp = f"{p}.tmp.{os.getpid()}"
+        with open(tmp, "w") as f:
+            f.write(text)
+        os.replace(tmp, p)
+
+    import time
+
+    write(path + ".started", repr(time.time()))
+    return lambda: write(path, repr(time.time()))
+
+
 def _stop_on_signals() -> threading.Event:
     """An event set by SIGTERM / SIGINT (how the kubelet stops a container)."""
     import signal
@@ -93,17 +117,24 @@ def main(argv: list[str] | None = None) -> int:
         from ..nodeenv import NodeEnv
         from .operands import run_operand
 
+        import os
+
         logs.setup()
         try:
             client = RestClient.from_incluster()
         except (KeyError, OSError):
-            client = None  # node-local operands (driver, toolkit) work without the API
+            # outside a pod: a kubeconfig if one is named (the simulated
+            # cluster's operand processes), else node-local operands (driver,
+            # toolkit) work without the API
+            client = RestClient.from_kubeconfig() if os.environ.get("KUBECONFIG") else None
         env = NodeEnv.from_environ(client)
-        import os
+        if os.environ.get("AMDGPU_SIM_NODE") == "1":
+            from ..testing.simcluster import adopt_sim_node_env
 
+            adopt_sim_node_env(env)
         # the kubelet stops a container with SIGTERM: operands then run their
         # shutdown (toolkit cleanup, vfio unbind, plugin socket removal)
-        return run_operand(env, argv, _stop_on_signals(), container_env=dict(os.environ))
+        return run_operand(env, argv, _stop_on_signals(), ready=_ready_signal(), container_env=dict(os.environ))
 
     ap = argparse.ArgumentParser(prog="amdgpu-operator")
     sub = ap.add_subparsers(dest="cmd", required=True)

@@ -527,18 +527,23 @@ def _plugin_pod_args(extra: list[str]) -> list[str]:
     return ["--steps", "hip,vecadd", "--vecadd-elems", str(1 << 20)]
 
 
+def container_env(pod: dict, container: dict) -> dict:
+    """A container's environment as the kubelet builds it: literal values and
+    the downward-API fields the operand manifests use."""
+    cenv = {e["name"]: e["value"] for e in container.get("env", []) if "value" in e}
+    md = pod.get("metadata") or {}
+    fields = {"metadata.name": md.get("name"), "metadata.uid": md.get("uid"), "metadata.namespace": md.get("namespace"),
+              "spec.nodeName": (pod.get("spec") or {}).get("nodeName")}
+    for e in container.get("env", []):
+        path = ((e.get("valueFrom") or {}).get("fieldRef") or {}).get("fieldPath")
+        if path and fields.get(path) is not None:
+            cenv[e["name"]] = fields[path]
+    return cenv
+
+
 def run_in_sim(cluster, run, container: dict, argv: list[str], init: bool) -> None:
     """Simulated kubelet hook: run the operand for ``container`` of ``run``'s pod."""
-    cenv = {e["name"]: e["value"] for e in container.get("env", []) if "value" in e}
-    for e in container.get("env", []):  # the downward API, as the kubelet resolves it
-        path = ((e.get("valueFrom") or {}).get("fieldRef") or {}).get("fieldPath")
-        if path:
-            md = run.pod.get("metadata") or {}
-            val = {"metadata.name": md.get("name"), "metadata.uid": md.get("uid"),
-                   "metadata.namespace": md.get("namespace"),
-                   "spec.nodeName": (run.pod.get("spec") or {}).get("nodeName")}.get(path)
-            if val is not None:
-                cenv[e["name"]] = val
+    cenv = container_env(run.pod, container)
     env = run.node.env
     if cenv.get("RUNTIME_PID_FILE"):  # never signal the machine's own container runtime
         cenv["RUNTIME_PID_FILE"] = os.path.join(run.node.dir, cenv["RUNTIME_PID_FILE"].lstrip("/"))

@@ -107,7 +107,7 @@ class TokenFileAuth:
                 self._read_at = now
             return self._token
 
-    def __call__(self, request):  # requests' auth hook
+    def __call__(self, request):  # the session's auth hook (kube/transport.py)
         request.headers["Authorization"] = f"Bearer {self.token()}"
         return request
 
@@ -119,10 +119,10 @@ class RestClient:
 
     def __init__(self, base_url: str, token: str | None = None, verify=True, cert=None, timeout: float = 30.0,
                  token_file: str | None = None):
-        import requests
+        from .transport import Session
 
         self.base = base_url.rstrip("/")
-        self.session = requests.Session()
+        self.session = Session()  # standard-library HTTP(S) (kube/transport.py: operand start-up cost)
         self.session.verify = verify
         if cert:
             self.session.cert = cert
@@ -141,13 +141,11 @@ class RestClient:
         errors for reads only (a write may have landed)."""
         import time
 
-        import requests
-
         delay = 0.1
         for attempt in range(self.RETRIES + 1):
             try:
                 r = self.session.request(method, url, timeout=self.timeout, **kw)
-            except requests.ConnectionError:
+            except ConnectionError:
                 if method != "GET" or attempt == self.RETRIES:
                     raise
                 time.sleep(delay)

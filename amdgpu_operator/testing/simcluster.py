@@ -29,6 +29,7 @@ import hashlib
 import json
 import os
 import shutil
+import sys
 import shlex
 import tempfile
 import threading
@@ -214,7 +215,7 @@ class SimCluster:
                  fake_gpu: bool = True, poll_s: float = 0.01, launcher=None,
                  termination_s: float | None = None, agent_poll_s: float | None = None,
                  node_status_s: float | None = None, operator_resync_s: float = 1.0,
-                 operator_debounce_s: float = 0.005, http_api: bool = False):
+                 operator_debounce_s: float = 0.005, http_api: bool = False, process_containers: bool = False):
         """``termination_s``: model graceful pod deletion - a deleted pod stays
         Terminating (listed, with ``deletionTimestamp``) for that many seconds
         (capped by its own grace period) before its kubelet removes it.
@@ -226,8 +227,21 @@ class SimCluster:
         ``http_api``: the operator and every operand talk to the API server
         through :class:`~..kube.client.RestClient` over HTTP (real REST paths,
         chunked watches, merge-patch, gracePeriodSeconds), as in a cluster; the
-        simulated kubelet and DaemonSet controller stay in-process."""
+        simulated kubelet and DaemonSet controller stay in-process.
+        ``process_containers``: every operand container (init containers
+        included) runs as its own ``python -m amdgpu_operator <args>``
+        process - the production entry point of the operand images - with
+        the node's host paths and the API server (over HTTP, so implies
+        ``http_api``) in its environment, instead of as a thread of this
+        process; readiness comes from the operand's ready file, a pod delete
+        sends SIGTERM.  Interpreter and import start-up of every operand, and
+        the device plugin's health-watcher start (on in this mode), are then
+        inside the measured bring-up (:attr:`process_stats`)."""
         self.workdir = workdir
+        self.process_containers = process_containers
+        http_api = http_api or process_containers
+        self.process_stats: list[dict] = []  # process_containers: one record per operand process
+        self._kubeconfig = None
         self.termination_s = termination_s
         self.namespace = namespace
         self.fake_gpu = fake_gpu
@@ -249,6 +263,14 @@ class SimCluster:
 
             self._http = HttpApiServer(self.api).start()
             self.agent_client = RestClient(self._http.url)
+            if process_containers:  # what the operand processes read (main.py: KUBECONFIG)
+                self._kubeconfig = os.path.join(workdir, "kubeconfig")
+                os.makedirs(workdir, exist_ok=True)
+                with open(self._kubeconfig, "w") as f:
+                    json.dump({"apiVersion": "v1", "kind": "Config", "current-context": "sim",
+                               "clusters": [{"name": "sim", "cluster": {"server": self._http.url}}],
+                               "users": [{"name": "sim", "user": {}}],
+                               "contexts": [{"name": "sim", "context": {"cluster": "sim", "user": "sim"}}]}, f)
         self.nodes: dict[str, SimNode] = {}
         self.stop_event = threading.Event()
         self._threads: list[threading.Thread] = []
@@ -616,7 +638,9 @@ class SimCluster:
         label = f"{run.name}/{c['name']}"
         self.trace("container-start", label)
         try:
-            if prog == "amdgpu-operator":
+            if prog == "amdgpu-operator" and self.process_containers:
+                self._run_process_container(run, c, cmd, init)
+            elif prog == "amdgpu-operator":
                 from ..cli import operands
 
                 operands.run_in_sim(self, run, c, cmd[1:], init)
@@ -626,6 +650,89 @@ class SimCluster:
                 raise RuntimeError(f"unknown program {prog}")
         finally:
             self.trace("container-end", label)
+
+    def _process_env(self, run: _PodRun, c: dict, ready_file: str) -> dict:
+        """Environment of an operand process: the container's env (downward
+        API resolved) plus what the DaemonSet's host mounts give a real
+        operand, pointed at this simulated node's directories."""
+        from ..cli.operands import container_env
+
+        env = run.node.env
+        cenv = container_env(run.pod, c)
+        if cenv.get("RUNTIME_PID_FILE"):  # never signal the machine's own container runtime
+            cenv["RUNTIME_PID_FILE"] = os.path.join(run.node.dir, cenv["RUNTIME_PID_FILE"].lstrip("/"))
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        penv = dict(os.environ)
+        penv.update(cenv)
+        penv.update({
+            "NODE_NAME": env.node_name, "HOST_ROOT": env.host_root, "VALIDATIONS_DIR": env.validations_dir,
+            "DEVICE_PLUGIN_DIR": env.device_plugin_dir, "POD_RESOURCES_SOCKET": env.pod_resources_socket,
+            "CDI_SPEC_DIR": env.cdi_dir, "CONTAINERD_CONFIG": env.containerd_config,
+            "CRIO_CONFIG_DIR": env.crio_config_dir, "DOCKER_CONFIG": env.docker_config, "INSTALL_DIR": env.install_dir,
+            "OPERATOR_NAMESPACE": env.namespace, "VALIDATION_POLL_S": str(env.poll_s), "KUBECONFIG": self._kubeconfig,
+            "AMDGPU_READY_FILE": ready_file, "AMDGPU_SIM_NODE": "1",
+            "PYTHONPATH": os.pathsep.join([root] + [x for x in os.environ.get("PYTHONPATH", "").split(os.pathsep) if x])})
+        if "kmod" in env.extra:
+            penv["AMDGPU_SIM_KMOD"] = "1"
+        if env.extra.get("metrics_fixture"):
+            penv["AMDGPU_SIM_METRICS_FIXTURE"] = env.extra["metrics_fixture"]
+        if self.fake_gpu:
+            penv["AMDGPU_SIM_FAKE_VALIDATOR"] = "1"
+        penv.pop("KUBERNETES_SERVICE_HOST", None)  # the simulated API server, not a real cluster's
+        return penv
+
+    def _run_process_container(self, run: _PodRun, c: dict, cmd: list[str], init: bool) -> None:
+        """``process_containers``: the operand as its own process (see __init__)."""
+        import signal
+        import subprocess
+
+        from ..utils.fswait import wait_for_file
+
+        d = os.path.join(run.node.dir, "containers", f"{run.name}.{c['name']}.{run.restarts}")
+        os.makedirs(d, exist_ok=True)
+        ready_file = os.path.join(d, "ready")
+        for f in (ready_file, ready_file + ".started"):
+            if os.path.exists(f):
+                os.unlink(f)
+        penv = self._process_env(run, c, ready_file)
+        rec = {"pod": run.name, "container": c["name"], "init": init, "args": cmd[1:3]}
+        t0 = time.perf_counter()
+        rec["spawn"] = t0
+        with open(os.path.join(d, "log"), "w") as log_f:
+            p = subprocess.Popen([sys.executable, "-m", "amdgpu_operator", *cmd[1:]], env=penv, stdout=log_f,
+                                 stderr=subprocess.STDOUT, start_new_session=True)
+        self.process_stats.append(rec)
+
+        def watch_ready():
+            if wait_for_file(ready_file, 600.0, run.stop, 0.002):
+                rec["ready_s"] = round(time.perf_counter() - t0, 4)
+                run.set_ready(c["name"])
+
+        if not init:
+            threading.Thread(target=watch_ready, daemon=True, name=f"ready-{run.name}-{c['name']}").start()
+        while p.poll() is None:
+            if run.stop.wait(0.005):
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait()
+                break
+        rec["exit_s"] = round(time.perf_counter() - t0, 4)
+        rec["rc"] = p.returncode
+        try:
+            with open(ready_file + ".started") as f:
+                rec["started_s"] = round(float(f.read()) - (time.time() - (time.perf_counter() - t0)), 4)
+        except (OSError, ValueError):
+            pass
+        if p.returncode != 0 and not run.stop.is_set():
+            with open(os.path.join(d, "log")) as f:
+                tail = f.read()[-1500:]
+            raise RuntimeError(f"{c['name']} exited {p.returncode}: {tail}")
 
     def _run_gpu_workload(self, run: _PodRun, c: dict, cmd: list[str]) -> None:
         """Non-operand pod with GPU limits: Allocate -> OCI hook -> validator."""
@@ -779,3 +886,26 @@ def new_id() -> str:
 
 def _quote(argv) -> str:
     return " ".join(shlex.quote(a) for a in argv)
+
+
+def adopt_sim_node_env(env: NodeEnv) -> None:
+    """In an operand process started by a ``process_containers`` SimCluster
+    (``AMDGPU_SIM_NODE=1``): the simulated node's stand-ins that a real node
+    has as hardware - the fake kernel module and PCI kernel of the synthetic
+    sysfs tree, the metrics fixture where amd-smi is absent, stand-in
+    validator processes where there is no GPU - and ephemeral ports (several
+    simulated nodes share one host)."""
+    e = os.environ
+    if e.get("AMDGPU_SIM_KMOD") == "1":
+        env.extra["kmod"] = fakesys.SimModule(env.host_root)
+        env.extra["pci_backend"] = fakesys.FakePciKernel(env.host_root)
+    if e.get("AMDGPU_SIM_METRICS_FIXTURE"):
+        env.extra["metrics_fixture"] = e["AMDGPU_SIM_METRICS_FIXTURE"]
+    env.extra["ephemeral_ports"] = True
+    if e.get("AMDGPU_SIM_FAKE_VALIDATOR") == "1":
+        def launch(argv, penv, device, timeout):
+            if os.path.basename(argv[0]) == "amdgpu-validator":
+                argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", *argv[1:]]
+            return run_local(argv, penv, timeout)
+
+        env.launcher = launch

@@ -67,6 +67,12 @@ def parse():
                     help="simulated kubelet nodeStatusUpdateFrequency: Node.status.allocatable follows on that tick")
     ap.add_argument("--agent-poll-s", type=float, default=None,
                     help="operands' VALIDATION_POLL_S (default: the production default of NodeEnv)")
+    ap.add_argument("--mode", choices=["process", "thread"], default="process",
+                    help="operand containers as their own processes (python -m amdgpu_operator <operand>, the "
+                         "operand images' entry point; device-plugin health watcher on) - the headline - or as "
+                         "threads of the bench process (the round-1/2 lower bound)")
+    ap.add_argument("--compare", type=int, default=2,
+                    help="after the timed steps, this many bring-ups in the other --mode (reported, not timed)")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--detail", default=None, help="write per-step breakdown JSON here")
     return ap.parse_args()
@@ -81,7 +87,22 @@ def gpu_available() -> bool:
         return False
 
 
-def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> dict:
+def operand_breakdown(stats: list[dict], t0: float) -> dict:
+    """Per operand container (process mode): when it was spawned (s after
+    ClusterPolicy creation), when its main began (interpreter + imports),
+    and when it was ready (long-running) or exited (init / run-to-completion)."""
+    out = {}
+    for r in stats:
+        key = f"{r['pod'].rsplit('-', 1)[0]}/{r['container']}"
+        e = {"spawn_at_s": round(r["spawn"] - t0, 4)}
+        for k in ("started_s", "ready_s", "exit_s"):
+            if k in r and not (k == "exit_s" and not r.get("init")):
+                e[k] = r[k]
+        out.setdefault(key, e)
+    return out
+
+
+def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode: str = "process") -> dict:
     from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, deep_merge, parse_set_flags
     from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
 
@@ -107,9 +128,11 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
 
     d = tempfile.mkdtemp(prefix="step-", dir=workdir)
     agent_poll = NodeEnv.poll_s if args.agent_poll_s is None else args.agent_poll_s
+    # termination_s=0: kubelet-confirmed pod deletes, as on a cluster
     cluster = SimCluster(d, [node], fake_gpu=fake_gpu, poll_s=0.005, launcher=launcher, agent_poll_s=agent_poll,
-                         node_status_s=args.kubelet_status_s or None,
-                         operator_resync_s=30.0, operator_debounce_s=0.02).start()  # cli/main.py defaults
+                         node_status_s=args.kubelet_status_s or None, termination_s=0.0,
+                         operator_resync_s=30.0, operator_debounce_s=0.02,  # cli/main.py defaults
+                         process_containers=(mode == "process")).start()
     try:
         t0 = time.perf_counter()
         t0_wall = time.time()
@@ -143,6 +166,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool) -> d
             for k, v in (r.get("marks") or {}).items():  # wall-clock marks inside a step
                 timeline[f"{step}.{k}"] = round(v - t0_wall, 4)
         return {
+            "mode": mode,
+            "operands": operand_breakdown(cluster.process_stats, t0) if mode == "process" else None,
             "time_to_ready_s": ttr,
             "allocatable_visible_s": alloc_visible,
             "allocatable_source": plug.get("allocatable_source"),
@@ -217,13 +242,13 @@ def main():
     results: list[dict] = []
     errors: list[str] = []
 
-    def driver_thread(n_steps: int, out: list):
+    def driver_thread(n_steps: int, out: list, mode: str):
         import faulthandler
 
         faulthandler.dump_traceback_later(args.timeout + 60, exit=False)  # stacks if a step wedges
         try:
             for _ in range(n_steps):
-                out.append(one_bring_up(args, n_gpus, launcher, workdir, fake_gpu))
+                out.append(one_bring_up(args, n_gpus, launcher, workdir, fake_gpu, mode))
         except Exception as e:  # noqa: BLE001
             import traceback
 
@@ -233,12 +258,12 @@ def main():
             if launcher is not None:
                 launcher.request_stop()
 
-    def phase(n_steps: int, out: list) -> None:
+    def phase(n_steps: int, out: list, mode: str = args.mode) -> None:
         if world == 1:
-            driver_thread(n_steps, out)
+            driver_thread(n_steps, out, mode)
             return
         if rank == 0:
-            th = threading.Thread(target=driver_thread, args=(n_steps, out), daemon=True)
+            th = threading.Thread(target=driver_thread, args=(n_steps, out, mode), daemon=True)
             th.start()
             launcher._stop_requested.clear()
             th_started = th
@@ -265,6 +290,16 @@ def main():
     sync()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    # the other mode, untimed: in-process (lower bound) next to per-process
+    other = "thread" if args.mode == "process" else "process"
+    compare: list = []
+    do_compare = [args.compare > 0 and not errors]
+    if world > 1:
+        dist.broadcast_object_list(do_compare, src=0)  # every rank takes part in the launcher's loop, or none
+    if do_compare[0]:
+        if world > 1:
+            launcher = DistributedLauncher(rank, world, group)
+        phase(args.compare, compare, other)
     if world > 1:
         box = [elapsed]
         all_el = [None] * world
@@ -309,12 +344,16 @@ def main():
                 "rccl_busbw_gbps": results[-1]["rccl_busbw_gbps"],
                 "rccl_comm_init_s": results[-1]["rccl_comm_init_s"],
                 "counter_gate": results[-1]["gemm_counter_gate"],
+                "operand_mode": args.mode,
+                # per operand container of the last timed bring-up (process mode)
+                "operands": results[-1].get("operands"),
+                f"{other}_mode_time_to_ready_s": [round(r["time_to_ready_s"], 4) for r in compare],
             },
         }
         print(json.dumps(out))
         if args.detail:
             with open(args.detail, "w") as f:
-                json.dump({"summary": out, "steps": results, "warmup": warm}, f, indent=1)
+                json.dump({"summary": out, "steps": results, "warmup": warm, "compare": compare}, f, indent=1)
     shutil.rmtree(workdir, ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()

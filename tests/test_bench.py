@@ -24,3 +24,9 @@ def test_bench_json_line_contract():
     assert out["n_gpus"] == 1 and out["config"]["allocatable_amd_com_gpu"] == 1
     assert 0 < out["value"] < 60 and abs(out["vs_baseline"] - out["value"] / 600.0) < 1e-4
     assert out["config"]["parallelism"] == "dp1"
+    # headline: operands as processes, with their start-up breakdown; in-process figure next to it
+    cfg = out["config"]
+    assert cfg["operand_mode"] == "process" and len(cfg["thread_mode_time_to_ready_s"]) == 2
+    ops = cfg["operands"]
+    assert ops["amd-device-plugin-daemonset/amd-device-plugin"]["ready_s"] > 0
+    assert ops["amd-operator-validator/gpu-validation"]["exit_s"] > 0

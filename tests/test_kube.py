@@ -276,8 +276,6 @@ def test_rest_client_retries_throttling_and_reads():
     import json as _json
     import threading as _th
 
-    import requests
-
     hits = {"GET": 0, "POST": 0}
 
     class H(http.server.BaseHTTPRequestHandler):
@@ -318,7 +316,7 @@ def test_rest_client_retries_throttling_and_reads():
         srv.server_close()
     dead = RestClient(f"http://127.0.0.1:{port}")
     dead.RETRIES = 1
-    with pytest.raises(requests.ConnectionError):
+    with pytest.raises(ConnectionError):
         dead.create(R.new("v1", "Node", "b"))  # a write is not repeated blindly
-    with pytest.raises(requests.ConnectionError):
+    with pytest.raises(ConnectionError):
         dead.get("v1", "Node", "a")

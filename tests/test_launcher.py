@@ -21,12 +21,14 @@ def test_processes_run_on_owner_rank(nproc, port):
     assert "LAUNCHER_OK" in p.stdout, p.stdout[-2000:] + p.stderr[-3000:]
 
 
-@pytest.mark.parametrize("nproc,warmup,port", [(2, 0, 29613), (8, 1, 29614)])
-def test_bench_ranks_with_stand_in_validators(nproc, warmup, port):
-    """The driver's scaling launch (torchrun, one rank per GPU) on CPU: 8 ranks
-    and a warm-up phase exercise the launcher hand-over between phases."""
+@pytest.mark.parametrize("nproc,warmup,port,mode", [(2, 0, 29613, "thread"), (8, 1, 29614, "process")])
+def test_bench_ranks_with_stand_in_validators(nproc, warmup, port, mode):
+    """The driver's scaling launch (torchrun, one rank per GPU) on CPU: 8 ranks,
+    a warm-up phase and the other-mode comparison exercise the launcher
+    hand-over between phases; thread mode routes every GPU process through
+    the rank that owns the GPU, process mode runs the operands as processes."""
     p = _torchrun(nproc, "bench.py", "--gpus", str(nproc), "--steps", "1", "--warmup", str(warmup),
-                  "--fake-gpu-procs", port=port)
+                  "--fake-gpu-procs", "--mode", mode, "--compare", "1", port=port)
     assert p.returncode == 0, p.stderr[-3000:]
     import json
 
@@ -35,6 +37,8 @@ def test_bench_ranks_with_stand_in_validators(nproc, warmup, port):
     out = json.loads(lines[0])
     assert out["n_gpus"] == nproc and out["config"]["allocatable_amd_com_gpu"] == nproc
     assert out["config"]["parallelism"] == f"dp{nproc}" and out["steps"] == 1 and out["warmup"] == warmup
+    other = "thread" if mode == "process" else "process"
+    assert out["config"]["operand_mode"] == mode and len(out["config"][f"{other}_mode_time_to_ready_s"]) == 1
 
 
 def test_run_local_takes_the_report_before_the_exit():

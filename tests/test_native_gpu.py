@@ -223,16 +223,19 @@ def test_metrics_exporter_live():
         src.close()
 
 
-@pytest.mark.parametrize("http_api", [False, True], ids=["local", "http"])
-def test_sim_cluster_on_real_gpu(http_api):
+@pytest.mark.parametrize("mode", ["local", "http", "process"])
+def test_sim_cluster_on_real_gpu(mode):
     """Bring-up on the MI355X; with ``http`` the operator and the operands
-    use the production RestClient against the API server's HTTP front end."""
+    use the production RestClient against the API server's HTTP front end;
+    with ``process`` every operand container is its own process (the device
+    plugin's amd-smi health watcher on)."""
     from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
     from amdgpu_operator.discovery import topology as T
 
     n = len(T.enumerate_gpus("/"))
     d = tempfile.mkdtemp()
-    c = SimCluster(d, [NodeSpec("node-0", n, sysfs_root="/")], fake_gpu=False, poll_s=0.005, http_api=http_api).start()
+    c = SimCluster(d, [NodeSpec("node-0", n, sysfs_root="/")], fake_gpu=False, poll_s=0.005, http_api=mode == "http",
+                   process_containers=mode == "process", termination_s=0.0 if mode == "process" else None).start()
     try:
         c.install_operator({"validator": {"workload": {"gemmN": 1024, "hbmBytes": 1 << 26}}})
         ttr = c.wait_ready(120, {"node-0": n})
