@@ -27,6 +27,9 @@ def build_parser() -> argparse.ArgumentParser:
     d = sub.add_parser("driver", help="driver DaemonSet containers")
     d.add_argument("action", choices=["install", "monitor", "prepare-upgrade", "smi"])
     d.add_argument("--interval", type=float, default=10.0)
+    d.add_argument("--prepare-upgrade", action="store_true",
+                   help="install: run the driver manager's upgrade check (drain + unload of a stale module) first, "
+                        "in this container instead of an init container")
 
     t = sub.add_parser("toolkit", help="container toolkit installer")
     t.add_argument("action", choices=["install", "uninstall"])
@@ -45,6 +48,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="gpu: plugin validation waits for the toolkit; the workload starts right away")
     v.add_argument("--with-driver", action="store_true",
                    help="gpu: validate the driver here too; workload processes start at once behind a start gate")
+    v.add_argument("--complete", action="store_true",
+                   help="gpu: then mark the node validated and stay (the validator's main container)")
 
     dp = sub.add_parser("device-plugin", help="kubelet device plugin for amd.com/gpu")
     dp.add_argument("--resource-name", default="amd.com/gpu")
@@ -171,6 +176,8 @@ def _validate(env, a, extra, stop, ready) -> int:
         V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
                        wait_toolkit=a.wait_toolkit, with_driver=a.with_driver,
                        partition_strategy=a.partition_strategy)
+        if a.complete:
+            return _complete(env, stop, ready)
     elif a.step == "vfio":
         V.validate_vfio(env, _pci(env), a.timeout, stop)
     elif a.step == "sandbox-complete":
@@ -180,16 +187,42 @@ def _validate(env, a, extra, stop, ready) -> int:
         stop.wait()
         V.clear_ready(env, ("sandbox",))
     else:
-        res = V.complete(env)
-        steps = ", ".join(f"{k} {v:.2f} s" for k, v in res["steps"].items() if v is not None)
-        _node_event(env, "Normal", "GPUValidated", f"GPUs validated ({steps})" if steps else "GPUs validated")
-        ready()
-        stop.wait()
-        # the validator pod goes (new validator image, uninstall): what it
-        # validated is withdrawn, so its successor validates again (the driver
-        # and toolkit files belong to their own operands)
-        V.clear_ready(env, ("workload", "plugin", "complete"))
+        return _complete(env, stop, ready)
     return 0
+
+
+def _complete(env, stop, ready) -> int:
+    """The validator's main container: label the node validated, stay Ready."""
+    from ..validator import validate as V
+
+    res = V.complete(env)
+    steps = ", ".join(f"{k} {v:.2f} s" for k, v in res["steps"].items() if v is not None)
+    _node_event(env, "Normal", "GPUValidated", f"GPUs validated ({steps})" if steps else "GPUs validated")
+    ready()
+    stop.wait()
+    # the validator pod goes (new validator image, uninstall): what it
+    # validated is withdrawn, so its successor validates again (the driver
+    # and toolkit files belong to their own operands)
+    V.clear_ready(env, ("workload", "plugin", "complete"))
+    return 0
+
+
+# Container env of an operand that waits for a validation inside its own
+# process instead of behind an init container (ClusterPolicy
+# daemonsets.inContainerGates): comma list of steps (validate.py READY_FILES).
+GATE_ENV = "VALIDATION_GATE"
+GATE_TIMEOUT_S = 3600.0  # then the container fails and the kubelet restarts it
+
+
+def _wait_gates(env: NodeEnv, cenv: dict, stop: threading.Event) -> None:
+    from ..validator import validate as V
+
+    for step in [x for x in cenv.get(GATE_ENV, "").split(",") if x]:
+        t0 = time.perf_counter()
+        V.wait_ready(env, step, GATE_TIMEOUT_S, stop)
+        if step == "driver":  # what the driver-validation init container checked: the N1 probe as well
+            V.validate_driver(env, GATE_TIMEOUT_S, stop)
+        log.info("gate %s open after %.3f s", step, time.perf_counter() - t0)
 
 
 def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
@@ -202,7 +235,7 @@ def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
             known += args[i:i + 2]
             i += 2
             continue
-        if a in ("--wait-toolkit", "--with-driver"):
+        if a in ("--wait-toolkit", "--with-driver", "--complete"):
             known.append(a)
             i += 1
             continue
@@ -225,11 +258,22 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         a = build_parser().parse_args(argv)
         extra = []
     cmd = a.cmd
+    if cenv.get(GATE_ENV):
+        try:
+            _wait_gates(env, cenv, stop)
+        except Exception:  # noqa: BLE001 - stopped while gated: a clean exit, else fail the container
+            if stop.is_set():
+                return 0
+            raise
 
     if cmd == "driver":
         from ..driver import manager as drv
 
         if a.action == "install":
+            if a.prepare_upgrade:
+                drv.prepare_upgrade(env, cenv.get("AMDGPU_DRIVER_VERSION", ""),
+                                    cenv.get("DRAIN_ENABLED", "true") == "true", cenv.get("AMDGPU_DRIVER_SPEC_HASH", ""),
+                                    float(cenv.get("DRAIN_TIMEOUT_SECONDS", "300")))
             drv.install(env, stop=stop, cenv=cenv)
             ready()
             stop.wait()

@@ -104,6 +104,19 @@ def _wait_init(name: str, image: str, pull: str, what: str, extra_args=(), env=N
                       env=env, privileged=True)
 
 
+def _gate(spec: ClusterPolicySpec, ctr: dict, init: dict, step: str) -> list[dict]:
+    """The prerequisite of an operand container: an init container (``init``)
+    or, with ``daemonsets.inContainerGates``, the same wait inside ``ctr``
+    (cli/operands.py VALIDATION_GATE) with the mounts the wait needs.
+    Returns the init containers to use."""
+    if not spec.daemonsets.inContainerGates:
+        return [init]
+    ctr["env"].append({"name": "VALIDATION_GATE", "value": step})
+    have = {m["name"] for m in ctr["volumeMounts"]}
+    ctr["volumeMounts"] += [m for m in init["volumeMounts"] if m["name"] not in have]
+    return []
+
+
 # the kubelet's pod-resources socket: the validator reads the device
 # manager's allocatable devices there (deviceplugin/podresources.py)
 POD_RESOURCES_MOUNT = {"name": "pod-resources", "mountPath": "/var/lib/kubelet/pod-resources", "readOnly": True}
@@ -241,24 +254,26 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-drive
     readiness = {"exec": {"command": ["amdgpu-probe", "--root", "/host", "--ready-file",
                                       f"{VALIDATIONS_HOST_DIR}/driver-ready"]},
                  "initialDelaySeconds": 5, "periodSeconds": 10, "failureThreshold": 60}
-    ctr = _container("amd-driver-ctr", image, d.imagePullPolicy, ["driver", "install", *d.args], mounts, env, True,
-                     d.resources.model_dump(), readiness)
+    drain_env = [{"name": "DRAIN_ENABLED", "value": str(d.upgradePolicy.drainEnabled).lower()},
+                 {"name": "DRAIN_TIMEOUT_SECONDS", "value": str(d.upgradePolicy.drainTimeoutSeconds)}]
+    gated = spec.daemonsets.inContainerGates  # the upgrade check runs in amd-driver-ctr itself
+    ctr = _container("amd-driver-ctr", image, d.imagePullPolicy,
+                     ["driver", "install", *(["--prepare-upgrade"] if gated else []), *d.args], mounts,
+                     env + (drain_env if gated else []), True, d.resources.model_dump(), readiness)
     health = _container("amd-driver-health", image, d.imagePullPolicy, ["driver", "monitor"],
                         [*_host_view(), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)], privileged=True)
     # the init container compares the live module with this spec and unloads it
     # on a mismatch, so it gets the same driver env as amd-driver-ctr
     init = _container("amd-driver-manager", image, d.imagePullPolicy, ["driver", "prepare-upgrade"],
                       [_mount("run-amd", "/run/amd"), _mount("lib-modules", "/lib/modules"), *_host_view()],
-                      env + [{"name": "DRAIN_ENABLED", "value": str(d.upgradePolicy.drainEnabled).lower()},
-                             {"name": "DRAIN_TIMEOUT_SECONDS", "value": str(d.upgradePolicy.drainTimeoutSeconds)}],
-                      True)
+                      env + drain_env, True)
     vols = [_hostpath("run-amd", "/run/amd"), _hostpath("host-root", "/", "Directory"),
             _hostpath("lib-modules", "/lib/modules"), _hostpath("dev", "/dev", "Directory"),
             _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
     sel = None
     if node_selector is not None:  # AMDGPUDriver pool: the driver deploy label plus the pool's selector
         sel = {DEPLOY_LABEL.format(OPERAND_LABELS["driver"]): "true", **node_selector}
-    ds = _daemonset(spec, ns, owner, name, "driver", sa, [ctr, health], [init], vols, host_pid=True,
+    ds = _daemonset(spec, ns, owner, name, "driver", sa, [ctr, health], [] if gated else [init], vols, host_pid=True,
                     node_selector=sel)
     # what the pods install, for the upgrade controller (controller/upgrade.py)
     ds["spec"]["template"]["metadata"]["labels"][HASH_LABEL] = spec_hash
@@ -298,11 +313,11 @@ def state_toolkit(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         *_host_view(), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)]
     ctr = _container("amd-container-toolkit-ctr", image, t.imagePullPolicy, ["toolkit", "install", *t.args], mounts, env,
                      True, t.resources.model_dump())
-    init = _wait_init("driver-validation", image, t.imagePullPolicy, "driver")
+    inits = _gate(spec, ctr, _wait_init("driver-validation", image, t.imagePullPolicy, "driver"), "driver")
     vols = [_hostpath(n, d, "DirectoryOrCreate") for n, d in runtime_mounts] + [
         _hostpath("install-dir", t.installDir), _hostpath("cdi-dir", t.cdi.specDir),
         _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
-    return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "toolkit", sa, [ctr], [init], vols, host_pid=True)]
+    return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "toolkit", sa, [ctr], inits, vols, host_pid=True)]
 
 
 def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
@@ -352,8 +367,15 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     ctr = _container("amd-operator-validator", image, v.imagePullPolicy, ["validate", "complete"],
                      [_mount("run-amd-validations", VALIDATIONS_HOST_DIR)], list(v.env), True,
                      v.resources.model_dump())
+    if spec.daemonsets.inContainerGates and len(inits) == 1 and inits[0]["name"] == "gpu-validation":
+        # the main container validates (driver, workload, plugin) and then
+        # completes: one container start instead of two
+        gi = inits.pop()
+        ctr["args"] = [*gi["args"], "--complete"]
+        ctr["env"] = gi["env"] + list(v.env)
+        ctr["volumeMounts"] = gi["volumeMounts"]
     vols = [_hostpath("run-amd-validations", VALIDATIONS_HOST_DIR), _hostpath("host-sys", "/sys", "Directory")]
-    if any(m["name"] == "pod-resources" for c in inits for m in c["volumeMounts"]):
+    if any(m["name"] == "pod-resources" for c in [*inits, ctr] for m in c["volumeMounts"]):
         vols += [_hostpath("pod-resources", "/var/lib/kubelet/pod-resources"),
                  _hostpath("device-plugin", "/var/lib/kubelet/device-plugins")]
     return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
@@ -378,7 +400,8 @@ def state_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     ctr = _container("amd-device-plugin", image, p.imagePullPolicy, args + list(p.args),
                      [_mount("device-plugin", "/var/lib/kubelet/device-plugins"), *_host_view()],
                      list(p.env), True, p.resources.model_dump())
-    inits = [_wait_init("toolkit-validation", image, p.imagePullPolicy, "toolkit" if spec.toolkit.enabled else "driver")]
+    gate = "toolkit" if spec.toolkit.enabled else "driver"
+    inits = _gate(spec, ctr, _wait_init("toolkit-validation", image, p.imagePullPolicy, gate), gate)
     vols = [_hostpath("device-plugin", "/var/lib/kubelet/device-plugins"), _hostpath("host-sys", "/sys", "Directory"),
             _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
     return [_sa(sa, ns, owner), *rbac, _daemonset(spec, ns, owner, name, "devicePlugin", sa, [ctr], inits, vols)]
@@ -401,7 +424,7 @@ def state_metrics_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict
                      [_mount("pod-resources", "/var/lib/kubelet/pod-resources", ro=True),
                       *_host_view()], list(m.env), True, m.resources.model_dump(),
                      ports=[{"name": "metrics", "containerPort": m.port}])
-    inits = [_wait_init("driver-validation", image, m.imagePullPolicy, "driver")]
+    inits = _gate(spec, ctr, _wait_init("driver-validation", image, m.imagePullPolicy, "driver"), "driver")
     vols = [_hostpath("pod-resources", "/var/lib/kubelet/pod-resources"), _hostpath("host-sys", "/sys", "Directory"),
             _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
     objs = [_sa(sa, ns, owner), *rbac, _daemonset(spec, ns, owner, name, "dcgmExporter", sa, [ctr], inits, vols),
@@ -437,7 +460,7 @@ def state_gfd(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
                  "--device-plugin-config-default", spec.devicePlugin.config.default]
     ctr = _container("gpu-feature-discovery", image, g.imagePullPolicy, args + list(g.args),
                      [_mount("host-sys", "/host/sys", ro=True)], list(g.env), False, g.resources.model_dump())
-    inits = [_wait_init("driver-validation", image, g.imagePullPolicy, "driver")]
+    inits = _gate(spec, ctr, _wait_init("driver-validation", image, g.imagePullPolicy, "driver"), "driver")
     vols = [_hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
     return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES + PLUGIN_CONFIG_RULES[1:], owner),
             _cluster_binding(sa, sa, ns, owner), _daemonset(spec, ns, owner, name, "gfd", sa, [ctr], inits, vols)]
@@ -452,7 +475,7 @@ def state_partition_manager(spec: ClusterPolicySpec, ns: str, owner) -> list[dic
                       p.defaultComputePartition, "--default-memory", p.defaultMemoryPartition] + list(p.args),
                      [_mount("host-sys", "/host/sys"), _mount("run-amd-validations", VALIDATIONS_HOST_DIR)],
                      list(p.env), True, p.resources.model_dump())
-    inits = [_wait_init("driver-validation", image, p.imagePullPolicy, "driver")]
+    inits = _gate(spec, ctr, _wait_init("driver-validation", image, p.imagePullPolicy, "driver"), "driver")
     vols = [_hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
     return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
             _daemonset(spec, ns, owner, name, "migManager", sa, [ctr], inits, vols, host_pid=True)]

@@ -29,4 +29,4 @@ def test_bench_json_line_contract():
     assert cfg["operand_mode"] == "process" and len(cfg["thread_mode_time_to_ready_s"]) == 2
     ops = cfg["operands"]
     assert ops["amd-device-plugin-daemonset/amd-device-plugin"]["ready_s"] > 0
-    assert ops["amd-operator-validator/gpu-validation"]["exit_s"] > 0
+    assert ops["amd-operator-validator/amd-operator-validator"]["ready_s"] > 0

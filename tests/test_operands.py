@@ -499,10 +499,45 @@ def test_validator_manifest_prespawn():
               if o["kind"] == "DaemonSet"][0]
         return [(c["name"], c["args"]) for c in ds["spec"]["template"]["spec"]["initContainers"]]
 
-    on = inits(ref)
+    init_layout = deep_merge(ref, {"daemonsets": {"inContainerGates": False}})
+    on = inits(init_layout)
     assert [n for n, _ in on] == ["gpu-validation"] and "--with-driver" in on[0][1]
-    off = inits(deep_merge(ref, {"validator": {"workload": {"prespawn": False}}}))
+    off = inits(deep_merge(init_layout, {"validator": {"workload": {"prespawn": False}}}))
     assert [n for n, _ in off] == ["driver-validation", "gpu-validation"] and "--with-driver" not in off[1][1]
+    # default (in-container gates): the main container validates, then completes - no init container
+    assert inits(ref) == []
+    ds = [o for o in M.state_validator(ClusterPolicySpec.model_validate(ref), "ns", None) if o["kind"] == "DaemonSet"][0]
+    main = ds["spec"]["template"]["spec"]["containers"][0]
+    assert main["args"][:2] == ["validate", "gpu"] and "--with-driver" in main["args"] and main["args"][-1] == "--complete"
+
+
+def test_in_container_gates_replace_the_init_containers():
+    """Default layout: no operand pod has a waiting init container; each
+    operand container carries its gate, and the driver container runs the
+    upgrade check itself."""
+    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, ClusterPolicySpec, parse_set_flags
+    from amdgpu_operator.controller import manifests as M
+
+    spec = ClusterPolicySpec.model_validate(parse_set_flags(REFERENCE_SET_FLAGS))
+    gates = {}
+    for state, builder in M.STATE_BUILDERS.items():
+        for o in builder(spec, "ns", None):
+            if o["kind"] != "DaemonSet":
+                continue
+            pod = o["spec"]["template"]["spec"]
+            if o["metadata"]["name"].startswith(("amd-sandbox", "amd-vfio")):
+                continue  # VM-passthrough operands (off by default) keep the init-container layout
+            assert pod["initContainers"] == [], o["metadata"]["name"]
+            for c in pod["containers"]:
+                env = {e["name"]: e.get("value") for e in c["env"]}
+                if "VALIDATION_GATE" in env:
+                    gates[c["name"]] = env["VALIDATION_GATE"]
+    assert gates == {"amd-container-toolkit-ctr": "driver", "amd-device-plugin": "toolkit",
+                     "amd-metrics-exporter": "driver", "gpu-feature-discovery": "driver", "amd-partition-manager": "driver"}
+    drv = [o for o in M.state_driver(spec, "ns", None) if o["kind"] == "DaemonSet"][0]
+    ctr = drv["spec"]["template"]["spec"]["containers"][0]
+    assert ctr["args"][:3] == ["driver", "install", "--prepare-upgrade"]
+    assert {"DRAIN_ENABLED", "DRAIN_TIMEOUT_SECONDS"} <= {e["name"] for e in ctr["env"]}
 
 
 def test_no_prespawn_while_the_driver_is_not_live_or_upgrading(env):
