@@ -21,8 +21,8 @@ def test_gate_abort_exits_before_any_hip_call(tmp_path):
         gate.write_text("abort")
 
     th = threading.Thread(target=release)
+    t0 = time.perf_counter()  # before the releaser starts its 0.3 s sleep
     th.start()
-    t0 = time.perf_counter()
     p = subprocess.run([VALIDATOR, "--rendezvous", str(tmp_path / "rv"), "--steps", "hip,vecadd", "--start-gate",
                         str(gate)], capture_output=True, text=True, timeout=30)
     th.join()
