@@ -38,10 +38,7 @@ any GPU is doubled up.
 from __future__ import annotations
 
 import json
-from typing import Literal, Union
-
-import yaml
-from pydantic import BaseModel, ConfigDict, Field, field_validator
+from dataclasses import asdict, dataclass, field, fields
 
 from .. import RESOURCE_NAME
 from .api import REPLICA_SEP  # noqa: F401 - "<device id>::<replica>"
@@ -49,37 +46,85 @@ from .api import REPLICA_SEP  # noqa: F401 - "<device id>::<replica>"
 CONFIG_LABEL = "amd.com/device-plugin.config"
 SHARED_SUFFIX = ".shared"
 
-ListStrategy = Literal["envvar", "volume-mounts", "cdi-annotations", "cdi-cri"]
+LIST_STRATEGIES = ("envvar", "volume-mounts", "cdi-annotations", "cdi-cri")
+
+# Plain dataclasses with explicit validation: the device plugin imports this
+# module at start-up, inside the node's time-to-Ready, and pydantic's import
+# alone cost it ~0.1 s (tools/operand_start_probe.py).  Errors are
+# ValueError, as pydantic's ValidationError is.
 
 
-class _M(BaseModel):
-    model_config = ConfigDict(extra="forbid", populate_by_name=True)
+def _check_keys(where: str, data, allowed) -> dict:
+    if data is None:
+        return {}
+    if not isinstance(data, dict):
+        raise ValueError(f"{where}: expected a mapping, got {type(data).__name__}")
+    extra = set(data) - set(allowed)
+    if extra:
+        raise ValueError(f"{where}: unknown field(s) {sorted(extra)}")
+    return data
 
 
-class Flags(_M):
-    partitionStrategy: Literal["single", "mixed"] = "single"
-    deviceIDStrategy: Literal["bdf", "uuid", "index"] = "bdf"
-    deviceListStrategy: list[ListStrategy] = Field(default_factory=lambda: ["envvar"])
+def _choice(where: str, v, options):
+    if v not in options:
+        raise ValueError(f"{where}: {v!r} is not one of {list(options)}")
+    return v
+
+
+def _bool(where: str, v) -> bool:
+    if not isinstance(v, bool):
+        raise ValueError(f"{where}: expected true/false, got {v!r}")
+    return v
+
+
+@dataclass
+class Flags:
+    partitionStrategy: str = "single"
+    deviceIDStrategy: str = "bdf"
+    deviceListStrategy: list = field(default_factory=lambda: ["envvar"])
     passDeviceSpecs: bool = True
 
-    @field_validator("deviceListStrategy", mode="before")
     @classmethod
-    def _one_or_many(cls, v):
-        return [v] if isinstance(v, str) else v
+    def from_dict(cls, data) -> "Flags":
+        d = _check_keys("flags", data, [f.name for f in fields(cls)])
+        out = cls()
+        if "partitionStrategy" in d:
+            out.partitionStrategy = _choice("flags.partitionStrategy", d["partitionStrategy"], ("single", "mixed"))
+        if "deviceIDStrategy" in d:
+            out.deviceIDStrategy = _choice("flags.deviceIDStrategy", d["deviceIDStrategy"], ("bdf", "uuid", "index"))
+        if "deviceListStrategy" in d:
+            v = d["deviceListStrategy"]
+            v = [v] if isinstance(v, str) else v
+            if not isinstance(v, list) or not v:
+                raise ValueError("deviceListStrategy needs at least one strategy")
+            out.deviceListStrategy = list(dict.fromkeys(_choice("flags.deviceListStrategy", x, LIST_STRATEGIES)
+                                                        for x in v))
+        if "passDeviceSpecs" in d:
+            out.passDeviceSpecs = _bool("flags.passDeviceSpecs", d["passDeviceSpecs"])
+        return out
 
-    @field_validator("deviceListStrategy")
-    @classmethod
-    def _non_empty(cls, v):
-        if not v:
-            raise ValueError("deviceListStrategy needs at least one strategy")
-        return list(dict.fromkeys(v))
 
-
-class SharedResource(_M):
+@dataclass
+class SharedResource:
+    replicas: int
     name: str = RESOURCE_NAME
     rename: str = ""
-    replicas: int = Field(ge=1, le=256)
-    devices: Union[Literal["all"], list[Union[int, str]]] = "all"
+    devices: object = "all"  # "all" or a list of GPU indices / PCI BDFs
+
+    @classmethod
+    def from_dict(cls, data) -> "SharedResource":
+        d = _check_keys("sharing.timeSlicing.resources[]", data, [f.name for f in fields(cls)])
+        r = d.get("replicas")
+        if isinstance(r, bool) or not isinstance(r, int) or not 1 <= r <= 256:
+            raise ValueError(f"replicas must be an integer in [1, 256], got {r!r}")
+        devices = d.get("devices", "all")
+        if devices != "all" and not (isinstance(devices, list) and all(isinstance(x, (int, str)) and not
+                                                                         isinstance(x, bool) for x in devices)):
+            raise ValueError(f"devices must be 'all' or a list of indices / BDFs, got {devices!r}")
+        for k in ("name", "rename"):
+            if k in d and not isinstance(d[k], str):
+                raise ValueError(f"{k} must be a string")
+        return cls(replicas=r, name=d.get("name", RESOURCE_NAME), rename=d.get("rename", ""), devices=devices)
 
     def selects(self, dev) -> bool:
         if self.devices == "all":
@@ -87,20 +132,48 @@ class SharedResource(_M):
         return any(sel == dev.index or sel == dev.bdf or sel == str(dev.index) for sel in self.devices)
 
 
-class TimeSlicing(_M):
+@dataclass
+class TimeSlicing:
     renameByDefault: bool = False
     failRequestsGreaterThanOne: bool = False
-    resources: list[SharedResource] = Field(default_factory=list)
+    resources: list = field(default_factory=list)
+
+    @classmethod
+    def from_dict(cls, data) -> "TimeSlicing":
+        d = _check_keys("sharing.timeSlicing", data, [f.name for f in fields(cls)])
+        res = d.get("resources") or []
+        if not isinstance(res, list):
+            raise ValueError("sharing.timeSlicing.resources must be a list")
+        return cls(renameByDefault=_bool("renameByDefault", d.get("renameByDefault", False)),
+                   failRequestsGreaterThanOne=_bool("failRequestsGreaterThanOne",
+                                                    d.get("failRequestsGreaterThanOne", False)),
+                   resources=[SharedResource.from_dict(r) for r in res])
 
 
-class Sharing(_M):
-    timeSlicing: TimeSlicing = Field(default_factory=TimeSlicing)
+@dataclass
+class Sharing:
+    timeSlicing: TimeSlicing = field(default_factory=TimeSlicing)
+
+    @classmethod
+    def from_dict(cls, data) -> "Sharing":
+        d = _check_keys("sharing", data, ["timeSlicing"])
+        return cls(timeSlicing=TimeSlicing.from_dict(d.get("timeSlicing")))
 
 
-class DevicePluginConfig(_M):
-    version: Literal["v1"] = "v1"
-    flags: Flags = Field(default_factory=Flags)
-    sharing: Sharing = Field(default_factory=Sharing)
+@dataclass
+class DevicePluginConfig:
+    version: str = "v1"
+    flags: Flags = field(default_factory=Flags)
+    sharing: Sharing = field(default_factory=Sharing)
+
+    @classmethod
+    def model_validate(cls, data) -> "DevicePluginConfig":
+        d = _check_keys("config", data, ["version", "flags", "sharing"])
+        return cls(version=_choice("version", d.get("version", "v1"), ("v1",)), flags=Flags.from_dict(d.get("flags")),
+                   sharing=Sharing.from_dict(d.get("sharing")))
+
+    def model_dump(self, mode: str = "json") -> dict:
+        return asdict(self)
 
     def shared_for(self, resource: str) -> SharedResource | None:
         for r in self.sharing.timeSlicing.resources:
@@ -125,6 +198,8 @@ class DevicePluginConfig(_M):
 
 def parse(text: str) -> DevicePluginConfig:
     """YAML (or JSON) config file -> validated config."""
+    import yaml  # only when a config file / ConfigMap key is in use
+
     data = yaml.safe_load(text) if text.strip() else {}
     return DevicePluginConfig.model_validate(data or {})
 

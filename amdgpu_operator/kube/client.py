@@ -174,11 +174,15 @@ class RestClient:
         import base64
         import tempfile
 
-        import yaml
-
         path = path or os.environ.get("KUBECONFIG") or os.path.expanduser("~/.kube/config")
         with open(path) as f:
-            cfg = yaml.safe_load(f)
+            text = f.read()
+        try:  # a JSON kubeconfig needs no YAML parser (operand start-up: kube/transport.py)
+            cfg = json.loads(text)
+        except ValueError:
+            import yaml
+
+            cfg = yaml.safe_load(text)
         ctx_name = context or cfg.get("current-context")
         ctx = next(c["context"] for c in cfg["contexts"] if c["name"] == ctx_name)
         cluster = next(c["cluster"] for c in cfg["clusters"] if c["name"] == ctx["cluster"])
