@@ -276,7 +276,7 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                                     float(cenv.get("DRAIN_TIMEOUT_SECONDS", "300")))
             drv.install(env, stop=stop, cenv=cenv)
             ready()
-            stop.wait()
+            drv.serve_reload_requests(env, stop, cenv)  # until the container stops
             if cenv.get("AMDGPU_UNLOAD_ON_EXIT", "true") == "true":
                 drv.cleanup_on_exit(env, owner=drv.owner_id(cenv))
         elif a.action == "monitor":

@@ -86,6 +86,8 @@ def desired_labels(node: dict, spec: ClusterPolicySpec) -> dict:
                 continue
             if labels.get(lbl) == "false":
                 continue  # user opt-out is sticky
+            if (labels.get(lbl) or "").startswith("paused-for-"):
+                continue  # paused by a node agent (partition manager) for a change: it restores the label
             if labels.get(lbl) != "true":
                 patch[lbl] = "true"
         if switched:

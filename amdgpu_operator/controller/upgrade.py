@@ -50,6 +50,8 @@ log = get_logger("amdgpu.upgrade")
 STATE_LABEL = "amd.com/gpu-driver-upgrade-state"
 HASH_LABEL = "amd.com/driver-spec-hash"
 CORDONED_ANN = "amd.com/gpu-driver-upgrade.cordoned"
+# the new driver pod (uid) after whose readiness the node's validator was restarted
+VALIDATOR_RESTART_ANN = "amd.com/gpu-driver-upgrade.validator-restarted"
 SINCE_ANN = "amd.com/gpu-driver-upgrade.since"
 # written by the driver container once the module it installed is live
 LOADED_HASH_ANN = "amd.com/gpu-driver.spec-hash"
@@ -208,14 +210,8 @@ class DriverUpgradeController:
                             pass
                     # the node is validated again only by a validator run on the new driver
                     self.client.patch("v1", "Node", name, {"metadata": {"labels": {VALIDATED_LABEL: None}}})
-                    for vp in self.client.list("v1", "Pod", self.namespace, label_selector={"app": VALIDATOR_DS},
-                                               field_selector=f"spec.nodeName={name}"):
-                        try:
-                            self.client.delete("v1", "Pod", vp["metadata"]["name"], self.namespace)
-                        except NotFound:
-                            pass
-                    self._set(n, VALIDATION)
-                    break  # the DaemonSet controller creates the new pods
+                    self._set(n, VALIDATION, {VALIDATOR_RESTART_ANN: None})
+                    break  # the DaemonSet controller creates the new driver pod
                 elif st == VALIDATION:
                     pod = self._driver_pods().get(name)
                     fresh = pod is not None and (pod["metadata"].get("labels") or {}).get(HASH_LABEL) == desired
@@ -224,8 +220,26 @@ class DriverUpgradeController:
                     validated = (cur["metadata"].get("labels") or {}).get(VALIDATED_LABEL) == "true"
                     # the new driver pod reports the spec it actually loaded (driver/manager.py)
                     loaded = (cur["metadata"].get("annotations") or {}).get(LOADED_HASH_ANN) == desired
+                    uid = pod["metadata"].get("uid", "") if pod is not None else ""
+                    restarted = (cur["metadata"].get("annotations") or {}).get(VALIDATOR_RESTART_ANN) == uid
+                    if ready and loaded and not restarted:
+                        # only now, with the new module live and its driver-ready
+                        # written, does a fresh validator run: one restarted with the
+                        # driver pod could pass its driver gate on the old driver's
+                        # ready file (the new pod's upgrade check had not cleared it)
+                        # and validate the node on the module being replaced
+                        self.client.patch("v1", "Node", name, {"metadata": {"labels": {VALIDATED_LABEL: None}}})
+                        for vp in self.client.list("v1", "Pod", self.namespace, label_selector={"app": VALIDATOR_DS},
+                                                   field_selector=f"spec.nodeName={name}"):
+                            try:
+                                self.client.delete("v1", "Pod", vp["metadata"]["name"], self.namespace)
+                            except NotFound:
+                                pass
+                        self._set(n, VALIDATION, {VALIDATOR_RESTART_ANN: uid, SINCE_ANN: (n["metadata"].get(
+                            "annotations") or {}).get(SINCE_ANN)})
+                        break
                     if ready and validated and loaded:
-                        self._set(n, UNCORDON)
+                        self._set(n, UNCORDON, {VALIDATOR_RESTART_ANN: None})
                     elif now - since(n) > max(timeout, spec.driver.startupProbeTimeoutSeconds):
                         self._set(n, FAILED)
                         break

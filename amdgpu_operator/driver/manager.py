@@ -61,6 +61,10 @@ class HostModule:
     def install(self, env: NodeEnv, cenv: dict, timeout: float) -> None:
         subprocess.run([self.script], check=True, timeout=timeout, env={**os.environ, **cenv})
 
+    def load(self, env: NodeEnv, timeout: float = 120.0) -> None:
+        """Load the module the host provides (no installer in this image)."""
+        subprocess.run(["modprobe", "amdgpu"], check=True, timeout=timeout, capture_output=True)
+
     def unload(self, env: NodeEnv, timeout: float = 120.0, retry_s: float = 5.0) -> None:
         # a process that just exited may still be releasing its device files
         deadline = time.monotonic() + retry_s
@@ -229,7 +233,7 @@ def _withdraw_validation(env: NodeEnv, reason: str) -> None:
     from ..validator.validate import MFMA_LABEL, VALIDATED_LABEL
 
     os.makedirs(env.validations_dir, exist_ok=True)
-    tmp = env.validation_file(LOST_MARKER + ".tmp")
+    tmp = env.validation_file(f"{LOST_MARKER}.tmp.{os.getpid()}.{threading.get_ident()}")
     with open(tmp, "w") as f:
         f.write(reason)
     os.replace(tmp, env.validation_file(LOST_MARKER))
@@ -240,6 +244,54 @@ def _withdraw_validation(env: NodeEnv, reason: str) -> None:
                                                                                    MFMA_LABEL: None}}})
         except Exception as e:  # noqa: BLE001
             log.warning("could not withdraw %s: %s", VALIDATED_LABEL, e)
+
+
+RELOAD_REQUEST = ".driver-reload-request"  # partition/manager.py: a memory-partition change needs a reload
+
+
+def reload_module(env: NodeEnv, cenv: dict, reason: str, timeout: float = 600.0, stop=None) -> dict:
+    """Unload and load amdgpu again (a memory-partition change takes effect
+    only at the module load).  The validations go first - the health monitor
+    must not read the planned unload as a loss - and pending validator gates
+    are aborted; then the module is loaded the way this container loads it:
+    its install script (container-installed) or ``modprobe amdgpu`` (host
+    module), and ``driver-ready`` is written again by :func:`install`."""
+    kmod = _kmod(env)
+    _release_gated_validators(env)
+    clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
+    log.info("reloading amdgpu: %s", reason)
+    kmod.unload(env)
+    if kmod.can_install():
+        kmod.install(env, {**cenv, "AMDGPU_FORCE_RELOAD": "true"}, timeout)
+    else:
+        kmod.load(env, timeout)
+    return install(env, timeout, stop, cenv)
+
+
+def serve_reload_requests(env: NodeEnv, stop: threading.Event, cenv: dict) -> None:
+    """``amd-driver-ctr`` after its install: the node's module owner, it
+    performs the reloads other node agents ask for (``.driver-reload-request``)
+    until the container stops."""
+    from ..utils.fswait import wait_for_file
+
+    req = env.validation_file(RELOAD_REQUEST)
+    while not stop.is_set():
+        if not wait_for_file(req, 3600.0, stop, max(env.poll_s, 0.05)):
+            continue
+        try:
+            with open(req) as f:
+                reason = json.load(f).get("reason", "requested")
+        except (OSError, ValueError):
+            reason = "requested"
+        try:
+            reload_module(env, cenv, reason, stop=stop)
+        except Exception as e:  # noqa: BLE001 - the requester times out and reports the failure
+            log.error("driver reload failed: %s", e)
+        finally:
+            try:
+                os.unlink(req)
+            except FileNotFoundError:
+                pass
 
 
 def kfd_users(env: NodeEnv) -> list[str]:
@@ -335,10 +387,29 @@ def monitor_once(env: NodeEnv) -> bool:
 
 def monitor(env: NodeEnv, stop: threading.Event, interval: float = 10.0) -> None:
     """Watch the driver every ``interval``; while it is lost, every second
-    (the node is unvalidated until the driver is seen again)."""
+    (the node is unvalidated until the driver is seen again).  A change in
+    the validations directory (a loss marker another agent wrote, a ready
+    file withdrawn) triggers a pass at once."""
+    from ..utils.fswait import DirWatch
+
     lost = env.validation_file(LOST_MARKER)
-    while not stop.wait(min(interval, 1.0) if os.path.exists(lost) else interval):
-        monitor_once(env)
+    os.makedirs(env.validations_dir, exist_ok=True)
+    w = DirWatch(env.validations_dir)
+    try:
+        while not stop.is_set():
+            period = min(interval, 1.0) if os.path.exists(lost) else interval
+            deadline = time.monotonic() + period
+            while not stop.is_set() and time.monotonic() < deadline:
+                if w.active:
+                    if w.wait(min(0.25, max(0.0, deadline - time.monotonic()))):
+                        break  # something changed: look now
+                elif stop.wait(min(0.25, max(0.0, deadline - time.monotonic()))):
+                    break
+            if stop.is_set():
+                return
+            monitor_once(env)
+    finally:
+        w.close()
 
 
 def prepare_upgrade(env: NodeEnv, desired_version: str, drain: bool = True, spec_hash: str = "",

@@ -225,6 +225,17 @@ class SimModule:
         if self._live():
             self.unload()
         version = cenv.get("AMDGPU_DRIVER_VERSION") or "6.12.12"
+        pending = f"{self.root}/.pending-partition"
+        if os.path.exists(pending):  # a memory-partition change takes effect at the module load
+            import json
+            import shutil
+
+            with open(pending) as f:
+                p = json.load(f)
+            shutil.rmtree(f"{self.root}/sys/class/kfd/kfd/topology/nodes", ignore_errors=True)
+            build_node(self.root, p["gpus"], p["compute"], p["memory"])
+            os.unlink(pending)
+            self.log.append(f"partition {p['compute']}/{p['memory']}")
         _w(f"{self.root}/sys/module/amdgpu/version", f"{version}\n")
         _w(f"{self.root}/sys/module/amdgpu/initstate", "live\n")
         _w(f"{self.root}/dev/kfd", "")

@@ -1,6 +1,8 @@
 """Randomized fault injection on the simulated cluster (tools/chaos_sim.py):
 pod deletions, driver loss, kubelet restarts, container <-> vm-passthrough
-switches and ClusterPolicy edits, each followed by convergence to Ready."""
+switches, ClusterPolicy edits, driver upgrades and partition changes (also
+while a process holds the GPU), each followed by convergence to Ready and,
+where the fault must revalidate the node, a fresh validation record."""
 
 import os
 import sys
@@ -15,3 +17,11 @@ def test_cluster_converges_after_each_fault(seed):
     import chaos_sim
 
     assert chaos_sim.run_seed(seed, steps=6, settle_s=0.3, timeout=60.0)
+
+
+def test_a_fault_that_does_not_land_fails_the_harness():
+    """Ready again is not enough: a step that must revalidate the node and
+    leaves no fresh validation record (here a no-op posing as one) fails."""
+    import chaos_sim
+
+    assert not chaos_sim.run_seed(1, steps=2, settle_s=0.1, timeout=3.0, inject_noop=1)

@@ -1,0 +1,170 @@
+"""Partition manager on a fake MI355X node (partition/manager.py): the
+device must be idle - GPU pods gone, the node's own amd-smi/KFD clients
+(device plugin, metrics exporter, validator) paused - before amd-smi may
+change a partition, and a memory-partition (NPS) change goes through the
+driver container's amdgpu reload."""
+
+import os
+import threading
+import time
+
+import pytest
+
+from amdgpu_operator.driver import manager as DM
+from amdgpu_operator.kube import resources as R
+from amdgpu_operator.kube.client import LocalClient
+from amdgpu_operator.kube.fakeapi import FakeApiServer
+from amdgpu_operator.nodeenv import NodeEnv
+from amdgpu_operator.partition import manager as PM
+from amdgpu_operator.testing import fakesys
+
+NS = "gpu-operator-resources"
+PROFILES = {"all-spx": {"compute": "SPX", "memory": "NPS1"}, "all-cpx": {"compute": "CPX", "memory": "NPS2"},
+            "all-qpx": {"compute": "QPX", "memory": "NPS1"}}
+DEFAULT = PM.Profile("SPX", "NPS1")
+
+
+def _pod(name, app=None, gpu=False):
+    ctr = {"name": "c", "image": "x"}
+    if gpu:
+        ctr["resources"] = {"limits": {"amd.com/gpu": "1"}}
+    return {"apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": name, "namespace": NS, "labels": {"app": app} if app else {}},
+            "spec": {"nodeName": "n1", "containers": [ctr]}}
+
+
+@pytest.fixture
+def node(tmp_path):
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 2)
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Namespace", NS))
+    n = R.new("v1", "Node", "n1")
+    n["metadata"]["labels"] = {PM._deploy_label(o): "true" for o in PM.PAUSE_OPERANDS}
+    c.create(n)
+    env = NodeEnv("n1", c, host_root=root, validations_dir=str(tmp_path / "val"), namespace=NS, poll_s=0.01)
+    env.extra["kmod"] = fakesys.SimModule(root)
+    for app in ("amd-device-plugin-daemonset", "amd-metrics-exporter", "amd-operator-validator"):
+        c.create(_pod(f"{app}-x", app))
+    c.create(_pod("workload", gpu=True))
+    return env
+
+
+class NodeAgents:
+    """What the DaemonSet controller + kubelet + driver container do on the
+    node meanwhile: a paused operand's pod goes (and its KFD handle with it,
+    unless ``lingering``), and the driver container serves reload requests."""
+
+    def __init__(self, env, lingering=()):
+        self.env, self.lingering = env, set(lingering)
+        self.stop = threading.Event()
+        self.procs = os.path.join(env.sysfs_root(), "sys/class/kfd/kfd/proc")
+        os.makedirs(self.procs, exist_ok=True)
+        self.pids = {"amd-device-plugin-daemonset": "701", "amd-metrics-exporter": "702"}
+        for pid in self.pids.values():
+            os.makedirs(os.path.join(self.procs, pid))
+        self.threads = [threading.Thread(target=self._ds, daemon=True),
+                        threading.Thread(target=DM.serve_reload_requests, args=(env, self.stop, {}), daemon=True)]
+
+    def _ds(self):
+        c = self.env.client
+        while not self.stop.wait(0.01):
+            labels = c.get("v1", "Node", "n1")["metadata"].get("labels") or {}
+            for op in PM.PAUSE_OPERANDS:
+                if labels.get(PM._deploy_label(op)) != PM.PAUSED:
+                    continue
+                app = PM._app(op)
+                for p in c.list("v1", "Pod", NS, label_selector=f"app={app}"):
+                    c.delete("v1", "Pod", p["metadata"]["name"], NS)
+                pid = self.pids.get(app)
+                if pid and app not in self.lingering and os.path.isdir(os.path.join(self.procs, pid)):
+                    os.rmdir(os.path.join(self.procs, pid))
+
+    def __enter__(self):
+        for th in self.threads:
+            th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        for th in self.threads:
+            th.join(5)
+
+
+def _label(env, key):
+    return (env.client.get("v1", "Node", "n1")["metadata"].get("labels") or {}).get(key)
+
+
+def _modes(env):
+    from amdgpu_operator.discovery import topology
+
+    return {(g.compute_partition, g.memory_partition) for g in topology.enumerate_gpus(env.sysfs_root())}
+
+
+def test_mi355x_profiles_only():
+    PM.Profile("CPX", "NPS2").validate()
+    PM.Profile("QPX", "NPS1").validate()
+    for bad in (("TPX", "NPS1"), ("CPX", "NPS4"), ("QPX", "NPS8"), ("SPX", "NPS2")):
+        with pytest.raises(ValueError):
+            PM.Profile(*bad).validate()
+
+
+def test_busy_backend_refuses_while_kfd_users_exist(node):
+    be = PM.SysfsBackend(node.host_root, PM.sysfs_partition_rebuilder(node.host_root, 2))
+    os.makedirs(os.path.join(node.host_root, "sys/class/kfd/kfd/proc/999"))
+    with pytest.raises(PM.PartitionBusy):
+        be.apply(0, PM.Profile("QPX", "NPS1"))
+    os.rmdir(os.path.join(node.host_root, "sys/class/kfd/kfd/proc/999"))
+    be.apply(0, PM.Profile("QPX", "NPS1"))
+    assert _modes(node) == {("QPX", "NPS1")}
+
+
+def test_lingering_exporter_refuses_the_change_and_restores_the_node(node):
+    be = PM.SysfsBackend(node.host_root, PM.sysfs_partition_rebuilder(node.host_root, 2))
+    node.client.patch("v1", "Node", "n1", {"metadata": {"labels": {"amd.com/gpu.partition-config": "all-qpx"}}})
+    with NodeAgents(node, lingering={"amd-metrics-exporter"}):
+        res = PM.reconcile_node(node, be, PROFILES, DEFAULT, timeout=1.0)
+    assert not res["changed"] and "702" in res["error"]
+    assert _label(node, PM.STATE_LABEL) == "failed" and _modes(node) == {("SPX", "NPS1")}
+    assert all(_label(node, PM._deploy_label(o)) == "true" for o in PM.PAUSE_OPERANDS)  # operands back
+
+
+def test_compute_change_after_the_clients_stopped(node):
+    be = PM.SysfsBackend(node.host_root, PM.sysfs_partition_rebuilder(node.host_root, 2))
+    node.client.patch("v1", "Node", "n1", {"metadata": {"labels": {"amd.com/gpu.partition-config": "all-qpx"}}})
+    with NodeAgents(node):
+        res = PM.reconcile_node(node, be, PROFILES, DEFAULT, timeout=10.0)
+    assert res["changed"] and not res["driver_reloaded"], res
+    assert set(res["paused"]) == set(PM.PAUSE_OPERANDS) and res["evicted"] == [f"{NS}/workload"]
+    assert _modes(node) == {("QPX", "NPS1")} and _label(node, PM.APPLIED_LABEL) == "all-qpx"
+    assert all(_label(node, PM._deploy_label(o)) == "true" for o in PM.PAUSE_OPERANDS)
+    assert node.extra["kmod"].log == []  # no reload for a compute-only change
+
+
+def test_memory_partition_change_goes_through_the_driver_reload(node):
+    be = PM.SysfsBackend(node.host_root, PM.sysfs_partition_rebuilder(node.host_root, 2))
+    DM.install(node, timeout=5)
+    node.client.patch("v1", "Node", "n1", {"metadata": {"labels": {"amd.com/gpu.partition-config": "all-cpx"}}})
+    t0 = time.time()
+    with NodeAgents(node):
+        res = PM.reconcile_node(node, be, PROFILES, DEFAULT, timeout=10.0)
+    assert res["changed"] and res["driver_reloaded"], res
+    assert _modes(node) == {("CPX", "NPS2")}
+    kmod = node.extra["kmod"]
+    assert kmod.log[:2] == ["unload", "partition CPX/NPS2"]  # the new NPS mode came with the module load
+    from amdgpu_operator.validator.validate import read_ready
+
+    assert read_ready(node, "driver")["time"] >= t0 and read_ready(node, "driver")["gpus"] == 16
+    assert not os.path.exists(node.validation_file(PM.RELOAD_REQUEST))
+
+
+def test_memory_change_without_a_driver_container_fails_cleanly(node):
+    be = PM.SysfsBackend(node.host_root, PM.sysfs_partition_rebuilder(node.host_root, 2))
+    node.client.patch("v1", "Node", "n1", {"metadata": {"labels": {"amd.com/gpu.partition-config": "all-cpx"}}})
+    agents = NodeAgents(node)
+    agents.threads = agents.threads[:1]  # no driver container on the node
+    with agents:
+        res = PM.reconcile_node(node, be, PROFILES, DEFAULT, timeout=0.5)
+    assert not res["changed"] and "did not reload" in res["error"]
+    assert _label(node, PM.STATE_LABEL) == "failed"
+    assert all(_label(node, PM._deploy_label(o)) == "true" for o in PM.PAUSE_OPERANDS)

@@ -107,8 +107,17 @@ def test_drain_waits_for_terminating_pods_and_retry_uncordons(tmp_path):
     c.patch("v1", "Node", "n1", {"metadata": {"annotations": {U.LOADED_HASH_ANN: desired}}})
     ctl.step(spec)
     st, n = _node(c)
+    # the new module is live: only now is the validator restarted, and a
+    # validation from before (here: the label set above) no longer counts
+    assert st == U.VALIDATION and VALIDATED_LABEL not in (n["metadata"].get("labels") or {})
+    assert n["metadata"]["annotations"][U.VALIDATOR_RESTART_ANN] == p["metadata"]["uid"]
+    ctl.step(spec)
+    assert _node(c)[0] == U.VALIDATION  # waiting for the fresh validator
+    c.patch("v1", "Node", "n1", {"metadata": {"labels": {VALIDATED_LABEL: "true"}}})  # it validated
+    ctl.step(spec)
+    st, n = _node(c)
     assert st == U.DONE and n["spec"]["unschedulable"] is False
-    assert U.CORDONED_ANN not in n["metadata"]["annotations"]
+    assert U.CORDONED_ANN not in n["metadata"]["annotations"] and U.VALIDATOR_RESTART_ANN not in n["metadata"]["annotations"]
 
 
 def test_user_cordon_survives_a_failed_and_retried_upgrade():

@@ -11,6 +11,18 @@ Ready again with the allocatable each node's workload implies:
   spec        toggle gfd / the metrics exporter in the ClusterPolicy
   upgrade     change driver.driverVersion (node-by-node driver upgrade)
   partition   flip a container node between SPX and CPX (partition manager: 2 or 16 devices)
+  partbusy    the same while a process holds the GPU (a KFD user the node's
+              agents do not own): the change must wait until it is gone
+  noop        (--inject-noop only) claims to revalidate but does nothing: the
+              harness must catch it
+
+Ready again is not enough to pass a step: a fault that must revalidate the
+node (validator pod deleted, driver loss, partition change, driver upgrade,
+workload switch) must leave a strictly newer validation record on it - the
+``workload-ready`` / ``sandbox-validated`` time - and on ``--real-gpu`` that
+record's GEMM step must carry ``counter_gate: pass``.  A kubelet restart must
+show the device plugin registered again.  Each step prints the revalidation
+delay (new record minus fault time).
 
     python tools/chaos_sim.py --seeds 1-5 --steps 10
 
@@ -35,14 +47,31 @@ from amdgpu_operator.driver.manager import monitor_once  # noqa: E402
 from amdgpu_operator.sandbox import WORKLOAD_CONFIG_LABEL  # noqa: E402
 from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster  # noqa: E402
 
-FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec", "upgrade", "partition")
+FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec", "upgrade", "partition", "partbusy")
+REVALIDATE = ("driverloss", "partition", "partbusy", "upgrade", "switch", "noop")
 
 
 REAL_GPU_FAULTS = ("delpod", "delpod", "kubelet", "spec")  # no root on a GPU box: no module, PCI or partition changes
 
 
+def validation_record(c, node: str) -> dict:
+    """The node's latest validation: workload (container) or sandbox time."""
+    from amdgpu_operator.validator.validate import read_ready
+
+    env = c.nodes[node].env
+    wl = read_ready(env, "workload") or {}
+    sb = read_ready(env, "sandbox") or {}
+    return {"time": max(wl.get("time", 0.0), sb.get("time", 0.0)), "workload": wl}
+
+
+def gemm_gate_passed(record: dict) -> bool:
+    ranks = (record.get("workload") or {}).get("ranks") or []
+    gemms = [s for r in ranks for s in r.get("steps", []) if s.get("name") == "gemm"]
+    return bool(gemms) and all(s.get("counter_gate") == "pass" for s in gemms)
+
+
 def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: bool = False,
-             real_gpu: bool = False) -> bool:
+             real_gpu: bool = False, inject_noop: int = -1) -> bool:
     rnd = random.Random(seed)
     d = tempfile.mkdtemp(prefix="chaos-")
     if real_gpu:  # one node, this machine's GPU(s): every validation runs on the real device
@@ -77,11 +106,19 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
         c.wait_ready(timeout, expect())
         for i in range(steps):
             fault, node = rnd.choice(REAL_GPU_FAULTS if real_gpu else FAULTS), rnd.choice(gpu_nodes)
+            if i == inject_noop:
+                fault = "noop"
             info = ""
+            before = {n: validation_record(c, n)["time"] for n in gpu_nodes}
+            regs_before = c.nodes[node].kubelet.register_calls
+            t_fault = time.time()
+            must = {node} if fault in REVALIDATE else set()
             if fault == "delpod":
                 pods = [p for p in c.pods() if p["spec"].get("nodeName") == node]
                 p = rnd.choice(pods)
                 info = p["metadata"]["name"]
+                if info.startswith("amd-operator-validator"):
+                    must = {node}  # its replacement validates the node again
                 c.client.delete("v1", "Pod", info, c.namespace)
             elif fault == "driverloss" and mode[node] == "container":
                 env = c.nodes[node].env
@@ -101,17 +138,38 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
                 cp["spec"][key]["enabled"] = not cp["spec"][key]["enabled"]
                 c.client.update(cp)
                 info = f"{key}={cp['spec'][key]['enabled']}"
-            elif fault == "partition" and mode[node] == "container":
+            elif fault in ("partition", "partbusy") and mode[node] == "container":
+                env = c.nodes[node].env
+                holder = os.path.join(env.host_root, "sys/class/kfd/kfd/proc/4242")
+                if fault == "partbusy":  # a process outside the operator's reach holds the GPU
+                    os.makedirs(holder, exist_ok=True)
+                applied_before = (c.client.get("v1", "Node", node)["metadata"].get("labels") or {}).get(PM.APPLIED_LABEL)
                 cpx[node] = not cpx[node]
                 c.client.patch("v1", "Node", node, {"metadata": {"labels": {
                     "amd.com/gpu.partition-config": "all-cpx" if cpx[node] else "all-spx"}}})
                 info = "CPX" if cpx[node] else "SPX"
+                if fault == "partbusy":
+                    time.sleep(1.0)
+                    applied = (c.client.get("v1", "Node", node)["metadata"].get("labels") or {}).get(PM.APPLIED_LABEL)
+                    if applied != applied_before:
+                        print(f"seed {seed} step {i} partbusy {node}: partition applied while the GPU was held",
+                              flush=True)
+                        return False
+                    os.rmdir(holder)  # the holder exits: the change may go ahead
+                    info += " (held 1 s)"
+            elif fault in ("partition", "partbusy"):
+                must = set()  # vm-passthrough node: nothing to partition
+            elif fault == "noop":
+                info = "claims a revalidation, does nothing"
             elif fault == "upgrade":
                 cp = c.policy()
                 cp["spec"]["driver"]["driverVersion"] = "6.14.0" if cp["spec"]["driver"]["driverVersion"] != "6.14.0" \
                     else "6.12.12"
                 c.client.update(cp)
                 info = cp["spec"]["driver"]["driverVersion"]
+                must = {n for n, m in mode.items() if m == "container"}
+            elif fault == "driverloss":
+                must = set()  # a vm-passthrough node has no driver to lose
             time.sleep(settle_s)
             t0 = time.time()
             try:
@@ -123,13 +181,32 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
                                 "amd.com/gpu-driver.version") == want for n, m in mode.items() if m == "container"):
                         time.sleep(0.05)
                 c.wait_ready(timeout, expect())
+                # the fault must have landed: a fresh validation of every node it concerns
+                deadline = time.time() + timeout
+                while time.time() < deadline and any(validation_record(c, n)["time"] <= before[n] for n in must):
+                    time.sleep(0.05)
+                    c.wait_ready(timeout, expect())
+                while fault == "kubelet" and time.time() < deadline and c.nodes[node].kubelet.register_calls <= regs_before:
+                    time.sleep(0.05)  # the plugin sees the new kubelet.sock within its watch interval
             except TimeoutError as e:
                 print(f"seed {seed} step {i} {fault} {node} {info}: NOT READY after {timeout:.0f} s\n{e}", flush=True)
                 for t, what, detail in c.trace_since(0)[-120:]:
                     print(f"  trace {t:9.3f} {what} {detail}")
                 return False
-            print(f"seed {seed} step {i} {fault} {node} {info}: ready {time.time() - t0:.2f} s after settling",
-                  flush=True)
+            stale = [n for n in must if validation_record(c, n)["time"] <= before[n]]
+            if stale:
+                print(f"seed {seed} step {i} {fault} {node} {info}: Ready, but no fresh validation on {stale}: "
+                      "the fault did not land", flush=True)
+                return False
+            if real_gpu and must and not all(gemm_gate_passed(validation_record(c, n)) for n in must):
+                print(f"seed {seed} step {i} {fault} {node}: revalidated without a passing GEMM counter gate", flush=True)
+                return False
+            if fault == "kubelet" and c.nodes[node].kubelet.register_calls <= regs_before:
+                print(f"seed {seed} step {i} kubelet {node}: the device plugin did not register again", flush=True)
+                return False
+            reval = " ".join(f"{n} revalidated +{validation_record(c, n)['time'] - t_fault:.2f} s" for n in sorted(must))
+            print(f"seed {seed} step {i} {fault} {node} {info}: ready {time.time() - t0:.2f} s after settling"
+                  + (f"; {reval}" if reval else ""), flush=True)
         return True
     finally:
         c.stop()
@@ -143,9 +220,11 @@ def main() -> int:
     ap.add_argument("--timeout", type=float, default=60.0)
     ap.add_argument("--http-api", action="store_true", help="operator and operands over HTTP (RestClient, informers)")
     ap.add_argument("--real-gpu", action="store_true", help="one node on this machine's GPUs (pod/kubelet/spec faults)")
+    ap.add_argument("--inject-noop", type=int, default=-1, metavar="STEP",
+                    help="make step STEP a no-op fault that claims a revalidation (the harness must fail)")
     a = ap.parse_args()
     lo, _, hi = a.seeds.partition("-")
-    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api, a.real_gpu)
+    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api, a.real_gpu, a.inject_noop)
               for s in range(int(lo), int(hi or lo) + 1)])
     return 0 if ok else 1
 
