@@ -129,7 +129,7 @@ def main(argv: list[str] | None = None) -> int:
             client = RestClient.from_kubeconfig() if os.environ.get("KUBECONFIG") else None
         env = NodeEnv.from_environ(client)
         if os.environ.get("AMDGPU_SIM_NODE") == "1":
-            from ..testing.simcluster import adopt_sim_node_env
+            from ..testing.simnode import adopt_sim_node_env
 
             adopt_sim_node_env(env)
         # the kubelet stops a container with SIGTERM: operands then run their

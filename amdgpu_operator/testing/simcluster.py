@@ -703,9 +703,18 @@ class SimCluster:
                                  stderr=subprocess.STDOUT, start_new_session=True)
         self.process_stats.append(rec)
 
+        def started_s():
+            try:  # the operand's main began (interpreter + imports done): wall time in the file
+                with open(ready_file + ".started") as f:
+                    return round(float(f.read()) - (time.time() - (time.perf_counter() - t0)), 4)
+            except (OSError, ValueError):
+                return None
+
         def watch_ready():
             if wait_for_file(ready_file, 600.0, run.stop, 0.002):
                 rec["ready_s"] = round(time.perf_counter() - t0, 4)
+                if started_s() is not None:
+                    rec["started_s"] = started_s()
                 run.set_ready(c["name"])
 
         if not init:
@@ -724,11 +733,8 @@ class SimCluster:
                 break
         rec["exit_s"] = round(time.perf_counter() - t0, 4)
         rec["rc"] = p.returncode
-        try:
-            with open(ready_file + ".started") as f:
-                rec["started_s"] = round(float(f.read()) - (time.time() - (time.perf_counter() - t0)), 4)
-        except (OSError, ValueError):
-            pass
+        if "started_s" not in rec and started_s() is not None:
+            rec["started_s"] = started_s()
         if p.returncode != 0 and not run.stop.is_set():
             with open(os.path.join(d, "log")) as f:
                 tail = f.read()[-1500:]
@@ -887,25 +893,3 @@ def new_id() -> str:
 def _quote(argv) -> str:
     return " ".join(shlex.quote(a) for a in argv)
 
-
-def adopt_sim_node_env(env: NodeEnv) -> None:
-    """In an operand process started by a ``process_containers`` SimCluster
-    (``AMDGPU_SIM_NODE=1``): the simulated node's stand-ins that a real node
-    has as hardware - the fake kernel module and PCI kernel of the synthetic
-    sysfs tree, the metrics fixture where amd-smi is absent, stand-in
-    validator processes where there is no GPU - and ephemeral ports (several
-    simulated nodes share one host)."""
-    e = os.environ
-    if e.get("AMDGPU_SIM_KMOD") == "1":
-        env.extra["kmod"] = fakesys.SimModule(env.host_root)
-        env.extra["pci_backend"] = fakesys.FakePciKernel(env.host_root)
-    if e.get("AMDGPU_SIM_METRICS_FIXTURE"):
-        env.extra["metrics_fixture"] = e["AMDGPU_SIM_METRICS_FIXTURE"]
-    env.extra["ephemeral_ports"] = True
-    if e.get("AMDGPU_SIM_FAKE_VALIDATOR") == "1":
-        def launch(argv, penv, device, timeout):
-            if os.path.basename(argv[0]) == "amdgpu-validator":
-                argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", *argv[1:]]
-            return run_local(argv, penv, timeout)
-
-        env.launcher = launch
