@@ -102,7 +102,7 @@ def gather_node(root: str = "/", validations_dir: str | None = None) -> dict:
 
 
 def summarize(cluster: dict) -> dict:
-    from ..controller.upgrade import DONE, STATE_LABEL
+    from ..wellknown import DONE, UPGRADE_STATE_LABEL as STATE_LABEL
     from ..validator.validate import VALIDATED_LABEL
 
     gpu_nodes = [n for n in cluster["nodes"] if n["labels"].get("amd.com/gpu.present") == "true"]

@@ -116,7 +116,7 @@ def _vfio_manager(env: NodeEnv, a, stop: threading.Event, ready) -> int:
     """``vfio-manager bind``: GPUs to vfio-pci, then keep them there; when the
     pod goes because the node left vm-passthrough, hand them back to amdgpu
     (a plain pod restart leaves running VMs their devices)."""
-    from ..controller.manifests import DEPLOY_LABEL, OPERAND_LABELS
+    from ..wellknown import DEPLOY_LABEL, OPERAND_LABELS
     from ..sandbox import vfio as VF
     from ..validator import validate as V
 
@@ -452,7 +452,7 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
 
         def once():
             if cmd == "nfd":
-                from ..controller.nodes import NFD_SCANNED_ANN
+                from ..wellknown import NFD_SCANNED_ANN
 
                 L.sync_node_labels(env.client, env.node_name, L.nfd_labels(env.sysfs_root()), (L.NFD_PREFIX + "pci-",),
                                    {NFD_SCANNED_ANN: "true"})

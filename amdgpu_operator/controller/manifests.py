@@ -24,25 +24,10 @@ from __future__ import annotations
 import os
 
 from ..api.clusterpolicy import ClusterPolicySpec
+from ..wellknown import DEPLOY_LABEL, OPERAND_LABELS  # noqa: F401 - re-exported
 
-DEPLOY_LABEL = "amd.com/gpu.deploy.{}"
 APP_LABEL = "app"
 VALIDATIONS_HOST_DIR = "/run/amd/validations"
-
-# state -> (operand key in spec, deploy-label suffix)
-OPERAND_LABELS = {
-    "driver": "driver",
-    "toolkit": "container-toolkit",
-    "validator": "operator-validator",
-    "devicePlugin": "device-plugin",
-    "dcgmExporter": "metrics-exporter",
-    "gfd": "gpu-feature-discovery",
-    "migManager": "partition-manager",
-    "nodeStatusExporter": "node-status-exporter",
-    "vfioManager": "vfio-manager",
-    "sandboxValidator": "sandbox-validator",
-    "sandboxDevicePlugin": "sandbox-device-plugin",
-}
 
 
 def owner_ref(cp: dict) -> list[dict]:

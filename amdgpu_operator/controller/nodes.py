@@ -28,7 +28,7 @@ NFD_PCI_LABELS = (
 )
 # written by our NFD worker (cli/operands.py nfd) with its first label sync: a
 # node without it has not been scanned yet, so "no GPU labels" means nothing
-NFD_SCANNED_ANN = "nfd.amd.com/scanned"
+from ..wellknown import NFD_SCANNED_ANN  # noqa: E402,F401 - re-exported
 
 
 def is_gpu_node(node: dict) -> bool:

@@ -47,22 +47,18 @@ from ..utils.logs import get_logger
 
 log = get_logger("amdgpu.upgrade")
 
-STATE_LABEL = "amd.com/gpu-driver-upgrade-state"
+from ..wellknown import UPGRADE_STATE_LABEL as STATE_LABEL  # noqa: E402
 HASH_LABEL = "amd.com/driver-spec-hash"
 CORDONED_ANN = "amd.com/gpu-driver-upgrade.cordoned"
 # the new driver pod (uid) after whose readiness the node's validator was restarted
 VALIDATOR_RESTART_ANN = "amd.com/gpu-driver-upgrade.validator-restarted"
 SINCE_ANN = "amd.com/gpu-driver-upgrade.since"
-# written by the driver container once the module it installed is live
-LOADED_HASH_ANN = "amd.com/gpu-driver.spec-hash"
-LOADED_VERSION_ANN = "amd.com/gpu-driver.version"
+from ..wellknown import LOADED_HASH_ANN, LOADED_VERSION_ANN  # noqa: E402,F401 - written by the driver container
 DRIVER_DS = "amd-driver-daemonset"
 VALIDATOR_DS = "amd-operator-validator"
 
-REQUIRED, CORDON, POD_DELETION, POD_RESTART = ("upgrade-required", "cordon-required", "pod-deletion-required",
-                                               "pod-restart-required")
-VALIDATION, UNCORDON, DONE, FAILED = "validation-required", "uncordon-required", "upgrade-done", "upgrade-failed"
-ACTIVE = (CORDON, POD_DELETION, POD_RESTART, VALIDATION, UNCORDON)
+from ..wellknown import (ACTIVE, CORDON, DONE, FAILED, POD_DELETION, POD_RESTART,  # noqa: E402,F401 - re-exported
+                         REQUIRED, UNCORDON, VALIDATION)
 
 
 def driver_spec_hash(spec: ClusterPolicySpec) -> str:

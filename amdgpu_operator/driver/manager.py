@@ -150,7 +150,7 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
     a live module of another version fails loudly.  After the module is up
     the loaded version is checked against the request, recorded on the host
     and published as node annotations for the upgrade controller."""
-    from ..controller.upgrade import LOADED_HASH_ANN, LOADED_VERSION_ANN
+    from ..wellknown import LOADED_HASH_ANN, LOADED_VERSION_ANN
     from ..discovery import topology
 
     cenv = dict(cenv or {})

@@ -151,7 +151,7 @@ def desired_profile(node: dict, profiles: dict, default: Profile, label: str) ->
 
 
 def _deploy_label(operand: str) -> str:
-    from ..controller.manifests import DEPLOY_LABEL, OPERAND_LABELS
+    from ..wellknown import DEPLOY_LABEL, OPERAND_LABELS
 
     return DEPLOY_LABEL.format(OPERAND_LABELS[operand])
 

@@ -652,7 +652,7 @@ def prespawn_safe(env: NodeEnv, sdk_gate: bool = False) -> bool:
     driver manager aborts pending gates before it unloads a module
     (driver/manager.py), so an early process never holds the device against
     a driver replacement."""
-    from ..controller.upgrade import ACTIVE, STATE_LABEL
+    from ..wellknown import ACTIVE, UPGRADE_STATE_LABEL as STATE_LABEL
     from ..discovery import topology
 
     if not sdk_gate:
