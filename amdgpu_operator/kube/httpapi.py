@@ -138,12 +138,20 @@ class _Handler(BaseHTTPRequestHandler):
         self._dispatch("DELETE")
 
 
+class _Server(ThreadingHTTPServer):
+    # the listen backlog: socketserver's default of 5 overflowed when the
+    # operator's informers and a node's operand processes connected at once,
+    # and a dropped SYN is retried by the client's kernel only after 1 s (a
+    # watch that began a second late looked like a 1 s reconcile stall)
+    request_queue_size = 512
+
+
 class HttpApiServer:
     """Run the fake apiserver on ``127.0.0.1:<port>`` in a background thread."""
 
     def __init__(self, api: FakeApiServer, host: str = "127.0.0.1", port: int = 0):
         handler = type("Handler", (_Handler,), {"api": api})
-        self.httpd = ThreadingHTTPServer((host, port), handler)
+        self.httpd = _Server((host, port), handler)
         self.httpd.daemon_threads = True
         self.httpd.stopping = threading.Event()
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True, name="fake-apiserver-http")
