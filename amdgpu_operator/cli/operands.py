@@ -258,7 +258,10 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         a = build_parser().parse_args(argv)
         extra = []
     cmd = a.cmd
-    if cenv.get(GATE_ENV):
+    # the device plugin prepares (enumeration, sockets, amd-smi health
+    # watcher) once the driver is up and waits for the rest of its gate only
+    # before it registers with the kubelet (advertises)
+    if cenv.get(GATE_ENV) and cmd != "device-plugin":
         try:
             _wait_gates(env, cenv, stop)
         except Exception:  # noqa: BLE001 - stopped while gated: a clean exit, else fail the container
@@ -331,6 +334,17 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
     if cmd == "device-plugin":
         from ..deviceplugin.server import DevicePluginManager, PluginConfig
 
+        gated = bool(cenv.get(GATE_ENV))
+        if gated:  # devices are enumerated from the live driver's KFD topology
+            from ..validator import validate as V
+
+            try:
+                V.wait_ready(env, "driver", GATE_TIMEOUT_S, stop)
+            except V.StepFailed:
+                if stop.is_set():
+                    return 0
+                raise
+
         from ..deviceplugin import config as DC
 
         def load_config():
@@ -370,7 +384,16 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             except Exception as e:  # noqa: BLE001 - no amd-smi (CPU box): serve without health events
                 log.info("health watcher unavailable: %s", e)
         mgr = DevicePluginManager(cfg, health_poll=health)
-        mgr.start()
+        mgr.start(register=not gated)
+        if gated:
+            try:
+                _wait_gates(env, {GATE_ENV: cenv[GATE_ENV]}, stop)
+            except Exception:  # noqa: BLE001 - stopped while gated: a clean exit
+                mgr.stop()
+                if stop.is_set():
+                    return 0
+                raise
+            mgr.register()
         log.info("device plugin serving %s (config %r)", sorted(mgr.servers), key)
         ready()
         if a.config_map:  # the config-manager loop: follow the node label and the ConfigMap

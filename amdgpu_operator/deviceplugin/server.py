@@ -334,6 +334,8 @@ class DevicePluginServer:
     def _watch_kubelet(self) -> None:
         """Re-register when kubelet.sock is re-created (kubelet restart)."""
         while not self._stop.wait(self.cfg.watch_interval_s):
+            if not self.registrations:
+                continue  # prepared but not yet advertised (DevicePluginManager.register)
             ident = self._kubelet_identity()
             if ident is None:
                 self._kubelet_ino = None  # socket gone: re-register when it returns
@@ -432,6 +434,15 @@ class DevicePluginManager:
         if self._health_poll is not None:
             self._thread = threading.Thread(target=self._health_loop, name="amdgpu-dp-health", daemon=True)
             self._thread.start()
+
+    def register(self) -> None:
+        """Advertise: register every server with the kubelet (after a
+        ``start(register=False)`` that prepared them)."""
+        with self._lock:
+            self._registered = True
+            for s in self.servers.values():
+                if not s.registrations:
+                    s.register()
 
     def _health_loop(self) -> None:
         by_index = {d.index: d for d in self.devices}

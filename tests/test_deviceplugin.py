@@ -198,3 +198,31 @@ def test_allocator_greedy_path_large_pool():
     cost = TopologyCost(devs, {})
     sel = preferred(cost, [d.id for d in devs], [], 8)
     assert len({devs[int(i[1:])].physical for i in sel}) == 1
+
+
+def test_prepared_plugin_does_not_register_before_it_is_told(tmp_path):
+    """start(register=False) serves the sockets (the operand's toolkit gate is
+    still closed) but must not advertise - not even through the kubelet
+    watcher - until register()."""
+    import time
+
+    from amdgpu_operator.deviceplugin.server import DevicePluginManager, PluginConfig
+    from amdgpu_operator.testing import fakesys
+    from amdgpu_operator.testing.fakekubelet import FakeKubelet
+
+    root = str(tmp_path / "h")
+    fakesys.build_node(root, 2)
+    dp = tmp_path / "dp"
+    dp.mkdir()
+    k = FakeKubelet(str(dp))
+    k.start()
+    mgr = DevicePluginManager(PluginConfig(socket_dir=str(dp), sysfs_root=root, watch_interval_s=0.02))
+    try:
+        mgr.start(register=False)
+        time.sleep(0.3)  # several kubelet-watch ticks
+        assert k.register_calls == 0
+        mgr.register()
+        assert k.wait_registered("amd.com/gpu", 5, min_devices=2) and k.register_calls == 1
+    finally:
+        mgr.stop()
+        k.stop()
