@@ -266,6 +266,24 @@ def links(root: str | None = None) -> list[GpuLink]:
             for l in arr[: cnt.value]]
 
 
+def visible_devices_env(devices: list["GpuDevice"], all_devices: list["GpuDevice"] | None = None) -> dict:
+    """Environment that limits a process's ROCm runtime to ``devices``.
+
+    ``ROCR_VISIBLE_DEVICES`` with the GPUs' KFD unique ids (ROCr's
+    "GPU-<id>" UUIDs) keeps the HSA runtime from initialising every other GPU
+    of the node - at N = 8 a validator process otherwise sets up all eight
+    agents, and 3N such processes start together (tools/storm_probe.py).
+    Inside, the first listed device is HIP device 0.  Devices without a
+    unique id, or ids shared by several devices (partitions of one GPU),
+    fall back to HIP-level ordinals (``HIP_VISIBLE_DEVICES``: same device
+    numbering inside, no runtime saving)."""
+    ids = [d.unique_id for d in devices]
+    seen = [d.unique_id for d in (all_devices or devices)]
+    if all(ids) and all(seen.count(i) == 1 for i in ids):
+        return {"ROCR_VISIBLE_DEVICES": ",".join(f"GPU-{i:016x}" for i in ids)}
+    return {"HIP_VISIBLE_DEVICES": ",".join(str(d.index) for d in devices)}
+
+
 def probe(root: str | None = None, expect_gpus: int = 0) -> tuple[bool, str]:
     """N1 driver readiness (amdgpu live, /dev/kfd, KFD GPU nodes, render nodes)."""
     buf = ctypes.create_string_buffer(256)

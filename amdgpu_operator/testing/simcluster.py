@@ -872,18 +872,16 @@ def container_device_env(sysfs_root: str, devices: list[int]) -> dict:
     """What a GPU container's runtime sees: only its allocated devices.
 
     The hook / CDI give the container just the allocated render nodes, so its
-    HSA runtime enumerates only those GPUs.  A process on the host gets the
-    same view from ``ROCR_VISIBLE_DEVICES`` with the GPUs' KFD unique ids
-    (ROCr's "GPU-<id>" UUIDs), which also keeps the runtime from initialising
-    every other GPU of an 8-GPU node; devices without a unique id fall back
-    to HIP-level ordinals."""
+    HSA runtime enumerates only those GPUs; a process on the host gets the
+    same view from :func:`~..discovery.topology.visible_devices_env`."""
     from ..discovery import topology
 
-    gpus = {g.index: g for g in topology.enumerate_gpus(sysfs_root)}
-    sel = [gpus.get(d) for d in devices]
-    if all(g is not None and g.unique_id for g in sel):
-        return {"ROCR_VISIBLE_DEVICES": ",".join(f"GPU-{g.unique_id:016x}" for g in sel)}
-    return {"HIP_VISIBLE_DEVICES": ",".join(str(d) for d in devices)}
+    gpus = topology.enumerate_gpus(sysfs_root)
+    by_index = {g.index: g for g in gpus}
+    sel = [by_index.get(d) for d in devices]
+    if any(g is None for g in sel):
+        return {"HIP_VISIBLE_DEVICES": ",".join(str(d) for d in devices)}
+    return topology.visible_devices_env(sel, gpus)
 
 
 def new_id() -> str:

@@ -280,9 +280,18 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     run_rccl = "rccl" in steps and (world > 1 or rccl_single)
     if run_rccl and rccl_shared:  # one process per GPU runs the kernel checks and RCCL
         kernel_steps = kernel_steps + ["rccl"]
+    # With a separate RCCL process per GPU, the kernel-check processes touch
+    # only their own GPU: they see only it (visible_devices_env), and the xGMI
+    # IPC step, which maps every peer's buffer, moves to the RCCL processes
+    # that see all GPUs anyway - it overlaps their communicator set-up.
+    split = world > 1 and run_rccl and not rccl_shared
+    peer_steps = ["hip", "rccl"]
+    if split and "xgmi" in kernel_steps:
+        kernel_steps = [s for s in kernel_steps if s != "xgmi"]
+        peer_steps = ["hip", "xgmi", "rccl"]
     jobs = [(r, _with_steps(args, kernel_steps), run_id, counter_env) for r in range(world)]
     if run_rccl and not rccl_shared:
-        jobs += [(r, _with_steps(_drop_flag(args, "--counter-gate"), ["hip", "rccl"]), run_id + "-rccl", {})
+        jobs += [(r, _with_steps(_drop_flag(args, "--counter-gate"), peer_steps), run_id + "-rccl", {})
                  for r in range(world)]
 
     def failed(res) -> bool:
@@ -294,7 +303,11 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         # kernel's teardown of its GPU state do not hold up the node
         if REPORT_EARLY:
             jenv = {**jenv, REPORT_EARLY_ENV: "1"}
-        argv = workload_argv(jargs, rank, world, rdv, rid, gpus[rank].index)
+        device = gpus[rank].index
+        if split and rid == run_id:  # a kernel-check process: its GPU only, as HIP device 0
+            jenv = {**jenv, **topology.visible_devices_env([gpus[rank]], gpus)}
+            device = 0
+        argv = workload_argv(jargs, rank, world, rdv, rid, device)
         if start_gate:
             argv += ["--start-gate", start_gate]
         res = env.launch(argv, jenv, device=gpus[rank].index, timeout=timeout)
@@ -322,7 +335,8 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
             rep["stderr"] = res.stderr[-2000:]
         if rid.endswith("-rccl"):
             main = reports[rank]
-            main["steps"] = main.get("steps", []) + [s for s in rep.get("steps", []) if s.get("name") == "rccl"]
+            # the peer process's checks (xgmi, rccl); its own hip step is not one
+            main["steps"] = main.get("steps", []) + [s for s in rep.get("steps", []) if s.get("name") != "hip"]
             main["ok"] = bool(main.get("ok")) and bool(rep.get("ok"))
             main["rc"] = main.get("rc", 0) or rep["rc"]
             main["rccl_process_seconds"] = rep["process_seconds"]

@@ -321,8 +321,15 @@ def test_workload_validation_launch_plan(env):
     out = V.validate_workload(env, ["--gemm", "1024", "--counter-gate"])
     assert out["ok"] and out["world"] == 2
     kernel = [a for a, _, _ in launched if "rccl" not in a[a.index("--steps") + 1]]
-    rccl = [a for a, _, _ in launched if a[a.index("--steps") + 1] == "hip,rccl"]
+    rccl = [a for a, _, _ in launched if a[a.index("--steps") + 1] == "hip,xgmi,rccl"]
     assert len(kernel) == 2 and len(rccl) == 2
+    # kernel checks see only their own GPU (as HIP device 0); the xGMI IPC step
+    # runs in the RCCL processes, which see every GPU
+    kenv = [(a, e, d) for a, e, d in launched if a in kernel]
+    assert sorted(d for _, _, d in kenv) == [0, 1] and all(a[a.index("--device") + 1] == "0" for a, _, _ in kenv)
+    assert all(e.get("ROCR_VISIBLE_DEVICES", "").startswith("GPU-") for _, e, _ in kenv)
+    assert len({e["ROCR_VISIBLE_DEVICES"] for _, e, _ in kenv}) == 2
+    assert not any("ROCR_VISIBLE_DEVICES" in e for a, e, _ in launched if a in rccl)
     assert all("--counter-gate" in a for a in kernel) and not any("--counter-gate" in a for a in rccl)
     # the default AQL-packet gate needs no profiler tool in the process
     assert {e.get("AMDGPU_VALIDATOR_COUNTERS") for a, e, _ in launched if a in kernel} == {None}

@@ -123,3 +123,19 @@ def test_small_gemm_gate_util_recorded(tmp_path):
     rc, rep, st = _local(tmp_path, "hip,gemm", ["--gemm", "1024", "--counter-gate", "--min-mfma-util", "0.2"])
     print(json.dumps({f: st["gemm"].get(f) for f in ("mfma_util", "mfma_util_floor", "tflops")}))
     assert rc == 0 and st["gemm"]["counter_gate"] == "pass", rep
+
+
+def test_kernel_check_process_restricted_to_its_gpu(tmp_path):
+    """At N > 1 a kernel-check process sees only its own GPU
+    (topology.visible_devices_env: ROCR_VISIBLE_DEVICES by KFD unique id) and
+    addresses it as HIP device 0."""
+    from amdgpu_operator.discovery import topology
+
+    gpus = topology.enumerate_gpus("/")
+    env = topology.visible_devices_env([gpus[-1]], gpus)
+    assert "ROCR_VISIBLE_DEVICES" in env, env
+    p = subprocess.run([VALIDATOR, "--rendezvous", str(tmp_path), "--device", "0", "--steps", "hip,vecadd,gemm",
+                        "--gemm", "1024"], capture_output=True, text=True, timeout=120, env={**os.environ, **env})
+    rep = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0 and rep["ok"], (rep, p.stderr[-1000:])
+    assert {s["name"]: s for s in rep["steps"]}["hip"]["arch"].startswith("gfx950")
