@@ -72,7 +72,7 @@ class DriverSpec(Operand):
     usePrecompiled: bool = False
     blacklistAmdgpuInbox: bool = True
     kernelModuleParams: dict[str, str] = Field(default_factory=dict)
-    repository: str = ""  # package mirror for air-gapped clusters (default repo.radeon.com)
+    packageRepository: str = ""  # package mirror for air-gapped clusters (default repo.radeon.com)
     startupProbeTimeoutSeconds: int = 600
     # unload the module this driver container installed when the container
     # stops (not while GPU processes hold it; never a host-managed module)

@@ -30,6 +30,8 @@ def build_parser() -> argparse.ArgumentParser:
     d.add_argument("--prepare-upgrade", action="store_true",
                    help="install: run the driver manager's upgrade check (drain + unload of a stale module) first, "
                         "in this container instead of an init container")
+    d.add_argument("--check", action="store_true",
+                   help="smi: exit 1 unless amd-smi reports live power and temperature for every GPU")
 
     t = sub.add_parser("toolkit", help="container toolkit installer")
     t.add_argument("action", choices=["install", "uninstall"])
@@ -290,7 +292,9 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                                 cenv.get("AMDGPU_DRIVER_SPEC_HASH", ""),
                                 float(cenv.get("DRAIN_TIMEOUT_SECONDS", "300")))
         else:
-            print(drv.smi_table(env))
+            snap = drv.smi_snapshot(env)
+            print(drv.smi_table(env, snap))
+            return 1 if a.check and not snap["ok"] else 0
         return 0
 
     if cmd == "toolkit":

@@ -10,8 +10,10 @@ kubectl get pods -n gpu-operator-resources (:116,195)   every operand pod Runnin
 kubectl get nodes -l nvidia.com/gpu.present=true (:119)  >= 1 node labelled amd.com/gpu.present
 describe nodes | grep Allocatable nvidia.com/gpu (:122)  Allocatable amd.com/gpu > 0 per GPU node
 get pods -A | grep nvidia-driver-daemonset (:132)       driver pods 2/2 Running, 0 restarts
-exec ... -c nvidia-driver-ctr -- nvidia-smi (:152)      amd-driver-ctr present (SMI table via
-                                                        ``amdgpu-operator driver smi``)
+exec ... -c nvidia-driver-ctr -- nvidia-smi (:152)      amd-driver-ctr present, and the driver
+                                                        image's amd-smi reports live power and
+                                                        temperature for every GPU (the health
+                                                        container's amd.com/gpu.driver-smi)
 (validator "Completed", :199)                           node labelled amd.com/gpu.validated
 =====================================================  =====================================
 
@@ -25,6 +27,7 @@ from dataclasses import asdict, dataclass, field
 
 from .. import LABEL_PRESENT, RESOURCE_NAME
 from ..kube import resources as R
+from ..wellknown import DRIVER_SMI_ANN
 
 EXPECTED_OPERANDS = {
     "amd-driver-daemonset": "driver",
@@ -108,6 +111,11 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
                  if (R.condition(n, "Ready") or {}).get("status") not in ("True", None)]
     rep.add("nodes-ready", not not_ready, f"{len(nodes)} node(s), not ready: {not_ready or 'none'}", "README.md:80")
 
+    try:
+        cp = client.list("amd.com/v1", "ClusterPolicy")
+    except Exception:  # noqa: BLE001 - CRD missing
+        cp = []
+    spec = (cp[0].get("spec") if cp else {}) or {}
     gpu_nodes = [n for n in nodes if (n["metadata"].get("labels") or {}).get(LABEL_PRESENT) == "true"]
     rep.add("gpu-nodes-labelled", bool(gpu_nodes), f"{len(gpu_nodes)} node(s) with {LABEL_PRESENT}=true", "README.md:119")
 
@@ -151,6 +159,10 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
         validated = labels.get("amd.com/gpu.validated") == "true"
         rep.add(f"validated[{name}]", validated, "amd.com/gpu.validated=true" if validated else "not validated",
                 "README.md:199")
+        if (spec.get("driver") or {}).get("enabled", True):
+            smi = (n["metadata"].get("annotations") or {}).get(DRIVER_SMI_ANN, "")
+            rep.add(f"driver-smi[{name}]", smi.startswith("ok"), smi or "not reported by amd-driver-health",
+                    "README.md:152-167")
 
     pods = client.list("v1", "Pod", namespace)
     bad = []
@@ -174,11 +186,8 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
     rep.add("driver-daemonset", drv_ok, "; ".join(details) or "no driver pods", "README.md:132-143,152")
 
     present = {p["metadata"].get("labels", {}).get("app") for p in pods}
-    try:
-        cp = client.list("amd.com/v1", "ClusterPolicy")
-    except Exception:  # noqa: BLE001 - CRD missing
-        cp = []
-    spec = (cp[0].get("spec") if cp else {}) or {}
+    if drv:  # per-kernel (usePrecompiled) and per-pool (AMDGPUDriver) driver DaemonSets count as the driver
+        present.add("amd-driver-daemonset")
     missing = [ds for ds, key in EXPECTED_OPERANDS.items()
                if (spec.get(key) or {}).get("enabled", True) and ds not in present
                and (container_nodes if key != "nfd" else gpu_nodes)]

@@ -217,12 +217,17 @@ def state_prerequisites(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
 
 
 def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-driver-daemonset",
-                 node_selector: dict | None = None) -> list[dict]:
+                 node_selector: dict | None = None, kernel: str | None = None) -> list[dict]:
+    """The driver DaemonSet: policy-wide, per AMDGPUDriver pool
+    (``node_selector``), or per node kernel (``kernel``, usePrecompiled: the
+    image tagged ``<driverVersion>-<kernel>`` holds modules built for it)."""
     from .upgrade import HASH_LABEL, driver_spec_hash
 
     d = spec.driver
     sa = "amd-driver"
     image = d.ref("amd-driver")
+    if kernel is not None:
+        image = f"{d.repository}/{d.image or 'amd-driver'}:{d.driverVersion}-{kernel}"
     spec_hash = driver_spec_hash(spec)
     env = [{"name": "ROCM_VERSION", "value": d.rocmVersion}, {"name": "AMDGPU_DRIVER_VERSION", "value": d.driverVersion},
            {"name": "AMDGPU_DRIVER_SPEC_HASH", "value": spec_hash},
@@ -231,11 +236,13 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-drive
            {"name": "AMDGPU_MODULE_PARAMS", "value": " ".join(f"{k}={v}" for k, v in sorted(d.kernelModuleParams.items()))},
            {"name": "AMDGPU_WAIT_SECONDS", "value": str(d.startupProbeTimeoutSeconds)},
            {"name": "AMDGPU_UNLOAD_ON_EXIT", "value": str(d.unloadOnExit).lower()}
-           ] + ([{"name": "AMDGPU_REPO_BASE", "value": d.repository}] if d.repository else []) + list(d.env)
+           ] + ([{"name": "AMDGPU_REPO_BASE", "value": d.packageRepository}] if d.packageRepository else []) + list(d.env)
     mounts = [_mount("run-amd", "/run/amd", propagation="Bidirectional"), _mount("host-root", "/host", ro=True,
                                                                                  propagation="HostToContainer"),
               _mount("lib-modules", "/lib/modules"), _mount("dev", "/dev"), _mount("host-sys", "/host/sys", ro=True),
               _mount("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    if not d.usePrecompiled:  # DKMS builds against the node's kernel headers (install.sh ensure_headers)
+        mounts.append(_mount("host-usr-src", "/host/usr/src", ro=True))
     readiness = {"exec": {"command": ["amdgpu-probe", "--root", "/host", "--ready-file",
                                       f"{VALIDATIONS_HOST_DIR}/driver-ready"]},
                  "initialDelaySeconds": 5, "periodSeconds": 10, "failureThreshold": 60}
@@ -255,13 +262,20 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-drive
     vols = [_hostpath("run-amd", "/run/amd"), _hostpath("host-root", "/", "Directory"),
             _hostpath("lib-modules", "/lib/modules"), _hostpath("dev", "/dev", "Directory"),
             _hostpath("host-sys", "/sys", "Directory"), _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    if not d.usePrecompiled:
+        vols.append(_hostpath("host-usr-src", "/usr/src", "DirectoryOrCreate"))
     sel = None
-    if node_selector is not None:  # AMDGPUDriver pool: the driver deploy label plus the pool's selector
+    if kernel is not None:  # one DaemonSet per kernel: the image was built for it
+        sel = {DEPLOY_LABEL.format(OPERAND_LABELS["driver"]): "true", KERNEL_LABEL: kernel}
+    elif node_selector is not None:  # AMDGPUDriver pool: the driver deploy label plus the pool's selector
         sel = {DEPLOY_LABEL.format(OPERAND_LABELS["driver"]): "true", **node_selector}
     ds = _daemonset(spec, ns, owner, name, "driver", sa, [ctr, health], [] if gated else [init], vols, host_pid=True,
                     node_selector=sel)
     # what the pods install, for the upgrade controller (controller/upgrade.py)
     ds["spec"]["template"]["metadata"]["labels"][HASH_LABEL] = spec_hash
+    if kernel is not None:
+        ds["metadata"]["labels"][KERNEL_DS_LABEL] = ds["spec"]["template"]["metadata"]["labels"][KERNEL_DS_LABEL] = \
+            kernel_suffix(kernel)
     if d.upgradePolicy.autoUpgrade and node_selector is None:  # node-by-node rollout (controller/upgrade.py)
         ds["spec"]["updateStrategy"] = {"type": "OnDelete"}
     return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner), ds]
@@ -522,6 +536,50 @@ def state_sandbox_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list
     vols = [_hostpath("device-plugin", "/var/lib/kubelet/device-plugins"), _hostpath("host-sys", "/sys", "Directory"),
             _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
     return [_sa(sa, ns, owner), _daemonset(spec, ns, owner, name, "sandboxDevicePlugin", sa, [ctr], [init], vols)]
+
+
+KERNEL_LABEL = "feature.node.kubernetes.io/kernel-version.full"  # NFD's (discovery/labels.py nfd_labels)
+KERNEL_DS_LABEL = "amd.com/driver-kernel"  # on the per-kernel driver DaemonSets and their pods
+
+
+def kernel_suffix(kernel: str) -> str:
+    """DNS-1123 form of a kernel release for object names and label values
+    (``6.8.0-45-generic`` -> ``6-8-0-45-generic``); long ones keep a hash."""
+    import hashlib
+    import re
+
+    x = re.sub(r"[^a-z0-9-]+", "-", kernel.lower()).strip("-")
+    if len(x) > 40:
+        x = x[:31].rstrip("-") + "-" + hashlib.sha1(kernel.encode()).hexdigest()[:8]
+    return x
+
+
+def state_driver_precompiled(spec: ClusterPolicySpec, ns: str, owner,
+                             nodes: list[dict]) -> tuple[list[dict], list[str]]:
+    """``driver.usePrecompiled``: one driver DaemonSet per kernel release among
+    the driver nodes (NFD's ``kernel-version.full`` label), each running the
+    image built for that kernel (``amd-driver:<driverVersion>-<kernel>``,
+    deploy/images/amd-driver/Dockerfile.precompiled): no compiler, headers or
+    network on the node.  Returns (objects, GPU nodes NFD has not labelled
+    with their kernel yet)."""
+    deploy = DEPLOY_LABEL.format(OPERAND_LABELS["driver"])
+    kernels: set[str] = set()
+    unlabelled = []
+    for n in nodes:
+        labels = n["metadata"].get("labels") or {}
+        if labels.get(deploy) != "true":
+            continue
+        if labels.get(KERNEL_LABEL):
+            kernels.add(labels[KERNEL_LABEL])
+        else:
+            unlabelled.append(n["metadata"]["name"])
+    objs: list[dict] = []
+    for k in sorted(kernels):
+        for o in state_driver(spec, ns, owner, name=f"amd-driver-daemonset-{kernel_suffix(k)}", kernel=k):
+            if o["kind"] == "DaemonSet" or not any(x["kind"] == o["kind"] and x["metadata"]["name"] == o["metadata"]["name"]
+                                                   for x in objs):
+                objs.append(o)
+    return objs, sorted(unlabelled)
 
 
 def state_driver_pools(spec: ClusterPolicySpec, ns: str, owner, drivers: list[dict],

@@ -212,9 +212,18 @@ class ClusterPolicyReconciler:
         for state, key in STATES:
             enabled = operand_enabled(spec, key)
             objs = STATE_BUILDERS[state](spec, self.namespace, owner)
+            unlabelled: list[str] = []
             if state == "state-driver" and enabled and spec.driver.useDriverCRD:
                 self._delete_objects([o for o in objs if o["kind"] == "DaemonSet"])  # the policy-wide one
                 objs, pool_status = self._driver_pools(spec, owner)
+            elif state == "state-driver" and enabled and spec.driver.usePrecompiled:
+                from .manifests import state_driver_precompiled
+
+                self._delete_objects([o for o in objs if o["kind"] == "DaemonSet"])  # the policy-wide one
+                objs, unlabelled = state_driver_precompiled(spec, self.namespace, owner, self.client.list("v1", "Node"))
+            if state == "state-driver":  # per-kernel DaemonSets of kernels no node runs any more
+                self._prune_kernel_daemonsets({o["metadata"]["name"] for o in objs if o["kind"] == "DaemonSet"}
+                                              if enabled else set())
             if not enabled:
                 self._delete_objects(objs)
                 results.append(StateResult(state, False, True, 0, 0, "disabled"))
@@ -244,6 +253,9 @@ class ClusterPolicyReconciler:
                 if nfd_scanned < pods_ready:
                     ready = False
                     detail.append(f"{nfd_scanned}/{pods_ready} nodes labelled")
+            if unlabelled:
+                ready = False
+                detail.append(f"no kernel-version label yet on {unlabelled}")
             if state == "state-driver" and pool_status is not None:
                 self._write_pool_status(pool_status, ds_ready)
                 ready &= all(st["state"] != "error" for st in pool_status.values())
@@ -297,6 +309,13 @@ class ClusterPolicyReconciler:
             self.events.record(cp, WARNING, "ReconcileFailed", message)
         else:
             self.events.record(cp, WARNING, "NotReady", message)
+
+    def _prune_kernel_daemonsets(self, keep: set[str]) -> None:
+        from .manifests import KERNEL_DS_LABEL
+
+        stale = [d for d in self.client.list("apps/v1", "DaemonSet", self.namespace, label_selector=KERNEL_DS_LABEL)
+                 if d["metadata"]["name"] not in keep]
+        self._delete_objects(stale)
 
     def _driver_pools(self, spec, owner) -> tuple[list[dict], dict]:
         from .manifests import state_driver_pools

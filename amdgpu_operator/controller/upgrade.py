@@ -123,7 +123,12 @@ class DriverUpgradeController:
     def _driver_pods(self) -> dict[str, dict]:
         """Driver pod per node; a live pod wins over one still Terminating."""
         out: dict[str, dict] = {}
-        for p in self.client.list("v1", "Pod", self.namespace, label_selector={"app": DRIVER_DS}):
+        from .manifests import KERNEL_DS_LABEL
+
+        pods = self.client.list("v1", "Pod", self.namespace, label_selector={"app": DRIVER_DS})
+        # usePrecompiled: one DaemonSet per kernel, the same driver spec (and hash) on all
+        pods += self.client.list("v1", "Pod", self.namespace, label_selector=KERNEL_DS_LABEL)
+        for p in pods:
             node = p["spec"].get("nodeName")
             if node not in out or out[node]["metadata"].get("deletionTimestamp"):
                 out[node] = p

@@ -82,7 +82,8 @@ def nfd_labels(root: str = "/") -> dict[str, str]:
             labels[f"{NFD_PREFIX}pci-{AMD_VENDOR}.present"] = "true"
     if _read(_root_join(root, "sys/module/amdgpu/initstate")) == "live":
         labels[f"{NFD_PREFIX}kernel-loadedmodule.amdgpu"] = "true"
-    ver = _read(_root_join(root, "proc/sys/kernel/osrelease"))
+    # a container shares the node's kernel: its own uname is the node's
+    ver = _read(_root_join(root, "proc/sys/kernel/osrelease")) or os.uname().release
     if ver:
         labels[f"{NFD_PREFIX}kernel-version.full"] = label_value(ver)
     return labels

@@ -382,6 +382,7 @@ def monitor_once(env: NodeEnv) -> bool:
         if _claim_lost_marker(env):
             restarted = _restart_node_operands(env)
             log.info("driver back (%s); restarted %s", msg, restarted)
+    publish_smi(env, ok and os.path.exists(path))
     return ok
 
 
@@ -396,6 +397,7 @@ def monitor(env: NodeEnv, stop: threading.Event, interval: float = 10.0) -> None
     os.makedirs(env.validations_dir, exist_ok=True)
     w = DirWatch(env.validations_dir)
     try:
+        monitor_once(env)
         while not stop.is_set():
             period = min(interval, 1.0) if os.path.exists(lost) else interval
             deadline = time.monotonic() + period
@@ -449,32 +451,100 @@ def prepare_upgrade(env: NodeEnv, desired_version: str, drain: bool = True, spec
             "unloaded": True}
 
 
-def smi_table(env: NodeEnv) -> str:
-    """Human table like ``amd-smi``/``nvidia-smi`` (README.md:157-167)."""
+def smi_snapshot(env: NodeEnv) -> dict:
+    """What ``amd-smi`` shows from inside the driver image: per-GPU live
+    metrics (power, temperature, HBM use) through the image's libamd_smi; on
+    a simulated node without a GPU the captured MI355X metrics
+    (``env.extra["metrics_fixture"]``).  ``ok`` only when every physical GPU
+    reports live power and temperature; otherwise ``error`` says why."""
     from ..discovery import topology
 
     gpus = topology.enumerate_gpus(env.sysfs_root())
-    metrics = {}
-    version = loaded_version(env)
+    snap = {"source": "amd-smi", "error": "", "version": "", "metrics": {}}
     try:
         with topology.Smi() as smi:
-            metrics = {m.bdf: m.values for m in smi.collect()}
-            version = version or smi.driver_version()  # inbox/DKMS modules without a sysfs version
-    except Exception:  # noqa: BLE001 - table without live metrics
-        pass
+            snap["metrics"] = {m.bdf: m.values for m in smi.collect()}
+            snap["version"] = smi.driver_version()
+    except Exception as e:  # noqa: BLE001 - reported, never a zero reading
+        snap["error"] = f"amd-smi unavailable: {e}"
+        fx = env.extra.get("metrics_fixture")
+        if fx:
+            from ..exporter.metrics import FixtureSource
+
+            samples = FixtureSource(fx).collect()  # captured on one MI355X: every simulated GPU reads it
+            if samples:
+                snap.update(source="fixture", error="",
+                            metrics={g.bdf: samples[i % len(samples)].values for i, g in enumerate(gpus)})
+    live = [b for b, v in snap["metrics"].items() if "socket_power_w" in v and "temp_hotspot_c" in v]
+    physical = len({g.physical_index for g in gpus})
+    snap.update(gpus=len(gpus), physical=physical, live=len(live))
+    if not snap["error"] and (physical == 0 or len(live) < physical):
+        snap["error"] = f"live power/temperature for {len(live)} of {physical} GPUs"
+    snap["ok"] = not snap["error"]
+    return snap
+
+
+def smi_status(snap: dict) -> str:
+    """One-line form for the node annotation ``verify`` reads."""
+    if snap["ok"]:
+        return f"ok: {snap['live']}/{snap['physical']} GPUs live ({snap['source']})"
+    return f"error: {snap['error']}"[:250]
+
+
+def publish_smi(env: NodeEnv, driver_ok: bool, refresh_s: float = 60.0) -> str:
+    """``amd-driver-health``: keep ``amd.com/gpu.driver-smi`` on the Node
+    current - the machine-checked form of ``kubectl exec ... -c
+    amd-driver-ctr -- nvidia-smi`` (README.md:152).  amd-smi is asked again
+    when the driver comes back and every ``refresh_s``; the Node is patched
+    only when the status line changes."""
+    from ..wellknown import DRIVER_SMI_ANN
+
+    last, at = env.extra.get("_smi_published", ("", 0.0))
+    now = time.monotonic()
+    if not driver_ok:
+        status = "error: driver not live"
+    elif last.startswith("ok") and now - at < refresh_s:
+        return last
+    else:
+        status = smi_status(smi_snapshot(env))
+    if status != last and env.client is not None:
+        try:
+            env.client.patch("v1", "Node", env.node_name, {"metadata": {"annotations": {DRIVER_SMI_ANN: status}}})
+        except Exception as e:  # noqa: BLE001 - next pass retries
+            log.warning("could not publish amd-smi status: %s", e)
+            return last
+    env.extra["_smi_published"] = (status, now)
+    return status
+
+
+def smi_table(env: NodeEnv, snap: dict | None = None) -> str:
+    """Human table like ``amd-smi``/``nvidia-smi`` (README.md:157-167).  A
+    GPU amd-smi gives no reading for shows ``n/a``, and the reason is the
+    table's last line - never a zero that reads like a measurement."""
+    from ..discovery import topology
+
+    gpus = topology.enumerate_gpus(env.sysfs_root())
+    snap = snap or smi_snapshot(env)
+    metrics = snap["metrics"]
+    version = loaded_version(env) or snap["version"]  # inbox/DKMS modules without a sysfs version
     from ..discovery.labels import rocm_version
 
     rocm = rocm_version(env.sysfs_root())
+
+    def num(m, key, width):
+        return f"{m[key]:{width}.0f}" if key in m else "n/a".rjust(width)
+
     lines = [f"amd-gpu-operator driver {version or 'unknown'}" + (f"   ROCm {rocm}" if rocm else ""),
              "+-----+--------------+--------+-----+-----------+-----------------+---------+-------+",
              "| GPU | BDF          | Arch   | CUs | Partition | HBM used/total  | Power W | Temp C|",
              "+-----+--------------+--------+-----+-----------+-----------------+---------+-------+"]
     for g in gpus:
         m = metrics.get(g.bdf, {})
-        used = m.get("vram_used_bytes", 0) / 2**20
+        used = f"{m['vram_used_bytes'] / 2**20:6.0f}" if "vram_used_bytes" in m else "n/a".rjust(6)
         total = m.get("vram_total_bytes", g.vram_bytes) / 2**20
         lines.append(f"| {g.index:3d} | {g.bdf:12s} | {g.arch:6s} | {g.cu_count:3d} | "
                      f"{(g.compute_partition or 'SPX') + '/' + (g.memory_partition or 'NPS1'):9s} | "
-                     f"{used:6.0f}/{total:6.0f}MiB | {m.get('socket_power_w', 0):7.0f} | {m.get('temp_hotspot_c', 0):5.0f} |")
+                     f"{used}/{total:6.0f}MiB | {num(m, 'socket_power_w', 7)} | {num(m, 'temp_hotspot_c', 5)} |")
     lines.append("+-----+--------------+--------+-----+-----------+-----------------+---------+-------+")
+    lines.append(f"amd-smi: {smi_status(snap)}")
     return "\n".join(lines)

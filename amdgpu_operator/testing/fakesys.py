@@ -57,7 +57,8 @@ class FakeGpu:
 
 
 def build_node(root: str, gpus: int = 8, compute_partition: str = "SPX", memory_partition: str = "NPS1",
-               driver_loaded: bool = True, xgmi: bool = True, sockets: int = 2, hidden_peers: int = 0) -> list[FakeGpu]:
+               driver_loaded: bool = True, xgmi: bool = True, sockets: int = 2, hidden_peers: int = 0,
+               kernel: str = "6.8.0-45-generic") -> list[FakeGpu]:
     """Write a fake node with ``gpus`` physical MI355X. Returns the GPU nodes.
 
     ``hidden_peers`` adds that many GPU nodes whose properties are unreadable
@@ -65,6 +66,7 @@ def build_node(root: str, gpus: int = 8, compute_partition: str = "SPX", memory_
     """
     split = PARTITION_SPLIT[compute_partition]
     os.makedirs(root, exist_ok=True)
+    _w(f"{root}/proc/sys/kernel/osrelease", kernel + "\n")
     base = os.path.join(root, "sys/class/kfd/kfd/topology/nodes")
     if driver_loaded:
         _w(f"{root}/sys/module/amdgpu/initstate", "live\n")

@@ -59,6 +59,7 @@ class NodeSpec:
     compute_partition: str = "SPX"
     memory_partition: str = "NPS1"
     sysfs_root: str | None = None     # None = synthetic tree; "/" = this machine
+    kernel: str = "6.8.0-45-generic"  # the node's kernel release (synthetic tree)
 
 
 @dataclass
@@ -302,7 +303,7 @@ class SimCluster:
         if ns.sysfs_root is None:
             root = os.path.join(d, "host")
             if ns.gpus > 0:
-                fakesys.build_node(root, ns.gpus, ns.compute_partition, ns.memory_partition)
+                fakesys.build_node(root, ns.gpus, ns.compute_partition, ns.memory_partition, kernel=ns.kernel)
             else:
                 os.makedirs(os.path.join(root, "sys/bus/pci/devices"), exist_ok=True)
                 fakesys._w(os.path.join(root, "sys/bus/pci/devices/0000:00:01.0/vendor"), "0x1022\n")

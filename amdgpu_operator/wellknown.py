@@ -36,3 +36,7 @@ ACTIVE = (CORDON, POD_DELETION, POD_RESTART, VALIDATION, UNCORDON)
 # written by the driver container once the module it installed is live
 LOADED_HASH_ANN = "amd.com/gpu-driver.spec-hash"
 LOADED_VERSION_ANN = "amd.com/gpu-driver.version"
+
+# the driver health container's amd-smi status line (driver/manager.py publish_smi,
+# checked by `amdgpu-operator verify`)
+DRIVER_SMI_ANN = "amd.com/gpu.driver-smi"

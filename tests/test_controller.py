@@ -355,3 +355,82 @@ def test_plugin_validation_pods_use_the_validator_image(tmp_path):
     th.join()
     assert rep["resources"] == {"amd.com/gpu.shared": 1} and rep["pods"] == 1
     assert seen[0]["containers"][0]["resources"]["limits"] == {"amd.com/gpu.shared": "1"}
+
+
+def _driver_ds(spec):
+    from amdgpu_operator.controller import manifests as M
+
+    return [o for o in M.state_driver(spec, "ns", None) if o["kind"] == "DaemonSet"][0]
+
+
+def test_driver_image_and_package_mirror_are_separate():
+    """driver.repository is the image registry like every operand's; the
+    package mirror is driver.packageRepository (round 2 conflated the two and
+    rendered the image as "/amd-driver:<version>")."""
+    spec = ClusterPolicySpec.model_validate({"driver": {"packageRepository": "http://mirror.local"}})
+    ctr = _driver_ds(spec)["spec"]["template"]["spec"]["containers"][0]
+    assert ctr["image"] == "registry.local/amd-gpu-operator/amd-driver:0.1.0"
+    env = {e["name"]: e.get("value") for e in ctr["env"]}
+    assert env["AMDGPU_REPO_BASE"] == "http://mirror.local"
+
+
+def test_dkms_driver_mounts_host_headers_read_only():
+    pod = _driver_ds(ClusterPolicySpec())["spec"]["template"]["spec"]
+    mounts = {m["name"]: m for m in pod["containers"][0]["volumeMounts"]}
+    assert mounts["host-usr-src"]["mountPath"] == "/host/usr/src" and mounts["host-usr-src"]["readOnly"]
+    assert {"name": "host-usr-src", "hostPath": {"path": "/usr/src", "type": "DirectoryOrCreate"}} in pod["volumes"]
+    # the firmware is staged under /run/amd, a hostPath at the same path (install.sh stage_firmware)
+    assert mounts["run-amd"]["mountPath"] == "/run/amd"
+    pre = _driver_ds(ClusterPolicySpec.model_validate({"driver": {"usePrecompiled": True}}))["spec"]["template"]["spec"]
+    assert "host-usr-src" not in {v["name"] for v in pre["volumes"]}
+
+
+def _kernel_node(c, name, kernel):
+    labels = {**GPU_LABEL, **({"feature.node.kubernetes.io/kernel-version.full": kernel} if kernel else {})}
+    c.create(R.new("v1", "Node", name, labels=labels))
+
+
+def test_precompiled_driver_runs_one_daemonset_per_kernel(env):
+    from amdgpu_operator.controller.manifests import KERNEL_LABEL
+
+    c, rec = env
+    c.patch("v1", "Node", "gpu-a", {"metadata": {"labels": {KERNEL_LABEL: "6.8.0-45-generic"}}})
+    _kernel_node(c, "gpu-b", "6.8.0-45-generic")
+    _kernel_node(c, "gpu-c", "5.15.0-119-generic")
+    c.create(cluster_policy(spec={"driver": {"usePrecompiled": True, "driverVersion": "6.12.12",
+                                             "repository": "registry.example/amd"}}))
+    rec.reconcile()
+    drv = {d["metadata"]["name"]: d for d in c.list("apps/v1", "DaemonSet", NS) if "driver" in d["metadata"]["name"]}
+    assert sorted(drv) == ["amd-driver-daemonset-5-15-0-119-generic", "amd-driver-daemonset-6-8-0-45-generic"]
+    d = drv["amd-driver-daemonset-6-8-0-45-generic"]["spec"]["template"]["spec"]
+    assert d["containers"][0]["image"] == "registry.example/amd/amd-driver:6.12.12-6.8.0-45-generic"
+    assert d["nodeSelector"] == {"amd.com/gpu.deploy.driver": "true", KERNEL_LABEL: "6.8.0-45-generic"}
+    env_ = {e["name"]: e.get("value") for e in d["containers"][0]["env"]}
+    assert env_["AMDGPU_USE_PRECOMPILED"] == "true"
+    # the node reboots into a new kernel: its DaemonSet follows, the unused one goes
+    c.patch("v1", "Node", "gpu-c", {"metadata": {"labels": {KERNEL_LABEL: "6.8.0-45-generic"}}})
+    rec.reconcile()
+    assert [n for n in ds_names(c) if "driver" in n] == ["amd-driver-daemonset-6-8-0-45-generic"]
+    # back to DKMS: the policy-wide DaemonSet, no per-kernel ones
+    cp = c.list(CP_API, "ClusterPolicy")[0]
+    cp["spec"]["driver"]["usePrecompiled"] = False
+    c.update(cp)
+    rec.reconcile()
+    assert [n for n in ds_names(c) if "driver" in n] == ["amd-driver-daemonset"]
+
+
+def test_precompiled_waits_for_the_kernel_label(env):
+    c, rec = env  # gpu-a has no kernel-version label yet (NFD has not run)
+    c.create(cluster_policy(spec={"driver": {"usePrecompiled": True}}))
+    res = rec.reconcile()
+    drv = next(r for r in res.states if r.name == "state-driver")
+    assert not drv.ready and "no kernel-version label yet on ['gpu-a']" in drv.detail
+    assert not [n for n in ds_names(c) if "driver" in n]
+
+
+def test_kernel_suffix_is_a_dns_label():
+    from amdgpu_operator.controller.manifests import kernel_suffix
+
+    assert kernel_suffix("6.8.0-45-generic") == "6-8-0-45-generic"
+    long = kernel_suffix("5.14.0-427.13.1.el9_4.x86_64+debug.with.a.very.long.local.suffix")
+    assert len(long) <= 40 and long.replace("-", "").isalnum() and not long.startswith("-")

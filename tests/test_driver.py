@@ -21,8 +21,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCRIPT = os.path.join(ROOT, "deploy/images/amd-driver/install.sh")
 
 # stub commands: log argv; `modprobe amdgpu` brings the fake driver up unless
-# FAKE_MODPROBE_NO_KFD is set (module loads but the KFD node never appears)
-STUB = r'''#!/bin/bash
+# FAKE_MODPROBE_NO_KFD is set (module loads but the KFD node never appears) and
+# logs the kernel's firmware search path as it was at load time
+STUB = r"""#!/bin/bash
 echo "$(basename "$0") $*" >> "$FAKE_LOG"
 case "$(basename "$0")" in
   modprobe)
@@ -31,33 +32,44 @@ case "$(basename "$0")" in
       rm -f "$AMDGPU_SYS_ROOT/module/amdgpu/initstate" "$AMDGPU_SYS_ROOT/module/amdgpu/version" "$AMDGPU_DEV_ROOT/kfd"
       exit 0
     fi
+    echo "fwpath=$(cat "$AMDGPU_SYS_ROOT/module/firmware_class/parameters/path")" >> "$FAKE_LOG"
     mkdir -p "$AMDGPU_SYS_ROOT/module/amdgpu"
     echo live > "$AMDGPU_SYS_ROOT/module/amdgpu/initstate"
     echo "${FAKE_MODULE_VERSION:-$AMDGPU_DRIVER_VERSION}" > "$AMDGPU_SYS_ROOT/module/amdgpu/version"
     [ -n "${FAKE_MODPROBE_NO_KFD:-}" ] || : > "$AMDGPU_DEV_ROOT/kfd" ;;
+  modinfo) [ -n "${FAKE_MODINFO_VERSION:-}" ] || exit 1; echo "$FAKE_MODINFO_VERSION" ;;
   curl) echo "-----BEGIN PGP PUBLIC KEY BLOCK-----" ;;
   gpg) while [ $# -gt 0 ]; do [ "$1" = "-o" ] && { cat > "$2"; exit 0; }; shift; done; cat > /dev/null ;;
   apt-get) if [ -n "${FAKE_APT_FAIL_HEADERS:-}" ] && [[ "$*" == *linux-headers* ]]; then exit 100; fi ;;
 esac
 exit 0
-'''
+"""
+KVER = "6.8.0-45-generic"
 
 
 @pytest.fixture
 def fake_host(tmp_path):
     bindir = tmp_path / "bin"
     bindir.mkdir()
-    for cmd in ("apt-get", "modprobe", "curl", "gpg"):
+    for cmd in ("apt-get", "modprobe", "modinfo", "dpkg", "dkms", "curl", "gpg"):
         p = bindir / cmd
         p.write_text(STUB)
         p.chmod(p.stat().st_mode | stat.S_IXUSR)
-    for d in ("sys", "dev", "etc"):
-        (tmp_path / d).mkdir()
+    for d in ("sys/module/firmware_class/parameters", "dev", "etc", "usr/src", "host/usr/src", "debs"):
+        (tmp_path / d).mkdir(parents=True)
+    (tmp_path / "sys/module/firmware_class/parameters/path").write_text("\n")  # the kernel's default: unset
     (tmp_path / "etc/os-release").write_text('ID=ubuntu\nVERSION_CODENAME=noble\n')
+    fw = tmp_path / "image-fw/amdgpu"  # amdgpu-dkms-firmware, baked at image build
+    fw.mkdir(parents=True)
+    for f in ("gc_9_5_0_mec.bin", "psp_13_0_14_sos.bin", "sdma_4_4_5.bin"):
+        (fw / f).write_bytes(b"\0" * 16)
     env = {"PATH": f"{bindir}:{os.environ['PATH']}", "FAKE_LOG": str(tmp_path / "calls.log"),
            "AMDGPU_SYS_ROOT": str(tmp_path / "sys"), "AMDGPU_DEV_ROOT": str(tmp_path / "dev"),
-           "AMDGPU_ETC_ROOT": str(tmp_path / "etc"), "KVER": "6.8.0-45-generic", "AMDGPU_WAIT_SECONDS": "2",
-           "AMDGPU_DRIVER_VERSION": "6.12.12", "ROCM_VERSION": "7.2.0"}
+           "AMDGPU_ETC_ROOT": str(tmp_path / "etc"), "AMDGPU_USR_SRC": str(tmp_path / "usr/src"),
+           "AMDGPU_HOST_SRC": str(tmp_path / "host/usr/src"), "AMDGPU_DEB_DIR": str(tmp_path / "debs"),
+           "AMDGPU_FIRMWARE_SRC": str(tmp_path / "image-fw"), "AMDGPU_HOST_FIRMWARE_DIR": str(tmp_path / "run/amd/firmware"),
+           "AMDGPU_PRECOMPILED_ROOT": str(tmp_path / "opt/amdgpu"),
+           "KVER": KVER, "AMDGPU_WAIT_SECONDS": "2", "AMDGPU_DRIVER_VERSION": "6.12.12", "ROCM_VERSION": "7.2.0"}
     return tmp_path, env
 
 
@@ -70,33 +82,129 @@ def calls(tmp):
     return p.read_text().splitlines() if p.exists() else []
 
 
+def fetched(log):
+    return [c for c in log if c.split()[0] in ("curl", "apt-get", "gpg")]
+
+
+def _fw_path_at_load(tmp, log):
+    """The firmware search path the kernel saw when `modprobe amdgpu` ran,
+    and the value the script left behind."""
+    i = next(i for i, c in enumerate(log) if c.startswith("modprobe") and "-r" not in c.split())
+    return log[i + 1].split("=", 1)[1], (tmp / "sys/module/firmware_class/parameters/path").read_text()
+
+
 def test_dkms_install_loads_module_and_waits_for_kfd(fake_host):
     tmp, env = fake_host
     r = run_script(env, AMDGPU_MODULE_PARAMS="noretry=1 ras_enable=1")
     assert r.returncode == 0, r.stdout + r.stderr
     log = calls(tmp)
-    assert "apt-get install -y linux-headers-6.8.0-45-generic linux-modules-extra-6.8.0-45-generic" in log
+    assert f"apt-get install -y linux-headers-{KVER} linux-modules-extra-{KVER}" in log
     assert "apt-get install -y amdgpu-dkms" in log
-    assert "apt-get install -y amd-smi-lib rocm-smi-lib" in log
-    assert "modprobe amdgpu noretry=1 ras_enable=1" in log
+    assert log.index("apt-get install -y amdgpu-dkms") < log.index(f"dkms autoinstall -k {KVER}") \
+        < log.index("modprobe amdgpu noretry=1 ras_enable=1")
+    assert not any("amd-smi-lib" in c for c in log)  # amd-smi is baked in the image, never fetched at start
     assert (tmp / "dev/kfd").exists()
     src = (tmp / "etc/apt/sources.list.d/amdgpu.list").read_text()
     assert "repo.radeon.com/amdgpu/6.12.12/ubuntu noble main" in src
-    assert "rocm/apt/7.2.0 noble" in (tmp / "etc/apt/sources.list.d/rocm.list").read_text()
     assert (tmp / "etc/modprobe.d/amd-gpu-operator-blacklist.conf").read_text() == "blacklist amdgpu\n"
     assert "live" in r.stdout.splitlines()[-1]
 
 
-def test_precompiled_mirror_and_no_blacklist(fake_host):
+def test_firmware_path_is_set_before_modprobe_and_restored(fake_host):
     tmp, env = fake_host
-    r = run_script(env, AMDGPU_USE_PRECOMPILED="true", AMDGPU_BLACKLIST_INBOX="false",
-                   AMDGPU_REPO_BASE="http://mirror.local")
-    assert r.returncode == 0, r.stderr
+    host_fw = env["AMDGPU_HOST_FIRMWARE_DIR"]
+    (tmp / "sys/module/firmware_class/parameters/path").write_text("/opt/site-firmware\n")  # an admin's own path
+    r = run_script(env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    at_load, after = _fw_path_at_load(tmp, calls(tmp))
+    assert at_load == host_fw  # the kernel looked in the staged copy while amdgpu probed
+    assert after.strip() == "/opt/site-firmware"  # and the admin's path is back afterwards
+    assert sorted(os.listdir(os.path.join(host_fw, "amdgpu"))) == ["gc_9_5_0_mec.bin", "psp_13_0_14_sos.bin",
+                                                                   "sdma_4_4_5.bin"]
+    assert not os.path.exists(os.path.join(host_fw, ".amdgpu.new"))
+
+
+def test_firmware_path_is_restored_when_the_load_fails(fake_host):
+    tmp, env = fake_host
+    r = run_script(env, FAKE_MODPROBE_NO_KFD="1", AMDGPU_WAIT_SECONDS="1")
+    assert r.returncode == 1 and "kfd missing" in r.stdout
+    at_load, after = _fw_path_at_load(tmp, calls(tmp))
+    assert at_load == env["AMDGPU_HOST_FIRMWARE_DIR"] and after.strip() == ""
+
+
+def test_offline_dkms_with_host_headers_and_baked_package(fake_host):
+    """No network at pod start: the .deb baked in the image builds against the
+    host's /usr/src (hostPath), and the firmware comes from the image."""
+    tmp, env = fake_host
+    (tmp / f"host/usr/src/linux-headers-{KVER}").mkdir()
+    (tmp / "host/usr/src/linux-headers-6.8.0-45").mkdir()  # Ubuntu's common tree
+    deb = tmp / "debs/amdgpu-dkms_6.12.12-2187269.24.04_all.deb"
+    deb.write_bytes(b"!<arch>\n")
+    r = run_script(env)
+    assert r.returncode == 0, r.stdout + r.stderr
     log = calls(tmp)
-    assert "apt-get install -y amdgpu-dkms-firmware amdgpu-6.8.0-45-generic" in log
-    assert not any("amdgpu-dkms" == c.split()[-1] for c in log)
-    assert "curl -fsSL http://mirror.local/rocm/rocm.gpg.key" in log
+    assert fetched(log) == []
+    assert log.index(f"dpkg -i {deb}") < log.index(f"dkms autoinstall -k {KVER}") < log.index("modprobe amdgpu")
+    for tree in (f"linux-headers-{KVER}", "linux-headers-6.8.0-45"):
+        assert os.readlink(tmp / "usr/src" / tree) == str(tmp / "host/usr/src" / tree)
+    assert "using the host's headers" in r.stdout
+
+
+def test_module_already_built_for_this_kernel_is_not_rebuilt(fake_host):
+    tmp, env = fake_host
+    r = run_script(env, FAKE_MODINFO_VERSION="6.12.12")
+    assert r.returncode == 0, r.stdout + r.stderr
+    log = calls(tmp)
+    assert fetched(log) == [] and not any(c.split()[0] in ("dpkg", "dkms") for c in log)
+    assert f"modinfo -k {KVER} -F version amdgpu" in log and "modprobe amdgpu" in log
+    # a module built for another version is rebuilt
+    (tmp / "calls.log").unlink()
+    (tmp / "dev/kfd").unlink()
+    (tmp / "sys/module/amdgpu/initstate").unlink()
+    r = run_script(env, FAKE_MODINFO_VERSION="6.10.5")
+    assert r.returncode == 0 and f"dkms autoinstall -k {KVER}" in calls(tmp)
+
+
+def _precompiled_image(tmp, kernels=(KVER,)):
+    root = tmp / "opt/amdgpu"
+    for k in kernels:
+        (root / "lib/modules" / k / "updates").mkdir(parents=True)
+        (root / "lib/modules" / k / "updates/amdgpu.ko").write_bytes(b"\x7fELF")
+    (root / "firmware/amdgpu").mkdir(parents=True)
+    (root / "firmware/amdgpu/gc_9_5_0_mec.bin").write_bytes(b"\0")
+    return root
+
+
+def test_precompiled_image_loads_without_network(fake_host):
+    tmp, env = fake_host
+    root = _precompiled_image(tmp)
+    r = run_script(env, AMDGPU_USE_PRECOMPILED="true", AMDGPU_BLACKLIST_INBOX="false",
+                   AMDGPU_MODULE_PARAMS="noretry=1")
+    assert r.returncode == 0, r.stdout + r.stderr
+    log = calls(tmp)
+    assert fetched(log) == [] and not any(c.split()[0] in ("dpkg", "dkms", "modinfo") for c in log)
+    assert f"modprobe -d {root} amdgpu noretry=1" in log
+    at_load, _ = _fw_path_at_load(tmp, log)
+    assert at_load == env["AMDGPU_HOST_FIRMWARE_DIR"]
+    assert os.listdir(os.path.join(at_load, "amdgpu")) == ["gc_9_5_0_mec.bin"]
     assert not (tmp / "etc/modprobe.d/amd-gpu-operator-blacklist.conf").exists()
+
+
+def test_precompiled_image_for_another_kernel_fails_and_names_it(fake_host):
+    tmp, env = fake_host
+    _precompiled_image(tmp, kernels=("6.5.0-1-generic",))
+    r = run_script(env, AMDGPU_USE_PRECOMPILED="true")
+    assert r.returncode == 1
+    assert "built for: 6.5.0-1-generic" in r.stdout and f"6.12.12-{KVER}" in r.stdout
+    assert not any(c.startswith("modprobe") for c in calls(tmp)) and fetched(calls(tmp)) == []
+
+
+def test_package_mirror(fake_host):
+    tmp, env = fake_host
+    r = run_script(env, AMDGPU_REPO_BASE="http://mirror.local")
+    assert r.returncode == 0, r.stderr
+    assert "curl -fsSL http://mirror.local/rocm/rocm.gpg.key" in calls(tmp)
+    assert "mirror.local/amdgpu/6.12.12/ubuntu noble" in (tmp / "etc/apt/sources.list.d/amdgpu.list").read_text()
 
 
 def test_already_live_driver_is_left_alone(fake_host):
@@ -107,6 +215,7 @@ def test_already_live_driver_is_left_alone(fake_host):
     r = run_script(env)
     assert r.returncode == 0 and "nothing to install" in r.stdout
     assert calls(tmp) == []
+    assert (tmp / "sys/module/firmware_class/parameters/path").read_text() == "\n"  # untouched
 
 
 def test_loaded_module_without_kfd_fails(fake_host):
@@ -167,11 +276,11 @@ def test_wrong_version_after_load_fails(fake_host):
     assert r.returncode == 1 and "6.8.0 loaded, 6.12.12 requested" in r.stdout
 
 
-def test_missing_headers_fall_back_and_version_is_required(fake_host):
+def test_no_headers_anywhere_fails_clearly_and_version_is_required(fake_host):
     tmp, env = fake_host
     r = run_script(env, FAKE_APT_FAIL_HEADERS="1")
-    assert r.returncode == 0 and "headers for 6.8.0-45-generic not packaged" in r.stdout
-    (tmp / "dev/kfd").unlink()  # driver gone again
+    assert r.returncode == 1 and f"no headers for {KVER}" in r.stdout and "usePrecompiled" in r.stdout
+    assert not any(c.startswith("modprobe") for c in calls(tmp))
     env2 = dict(env)
     env2.pop("AMDGPU_DRIVER_VERSION")
     r = run_script(env2)
@@ -369,3 +478,48 @@ def test_smi_table_lists_every_gpu(node_env):
     table = DM.smi_table(node_env)
     rows = [ln for ln in table.splitlines() if ln.startswith("|") and "gfx950" in ln]
     assert len(rows) == 2 and "SPX/NPS1" in rows[0]
+
+
+def test_smi_without_amd_smi_says_so_instead_of_printing_zeros(node_env):
+    """No GPU here: amd-smi has no reading, and the table says n/a plus why
+    (round 2 printed 0 W / 0 C, which reads like a measurement)."""
+    snap = DM.smi_snapshot(node_env)
+    assert not snap["ok"] and snap["error"]
+    table = DM.smi_table(node_env, snap)
+    rows = [ln for ln in table.splitlines() if "gfx950" in ln]
+    assert all(ln.count("n/a") == 3 for ln in rows), table  # HBM used, power, temperature
+    assert table.splitlines()[-1].startswith("amd-smi: error: ")
+
+
+def test_smi_from_the_captured_mi355x_metrics(node_env):
+    node_env.extra["metrics_fixture"] = os.path.join(fakesys.REAL_FIXTURE, "amd-smi-metric.json")
+    snap = DM.smi_snapshot(node_env)
+    assert snap["ok"] and snap["source"] == "fixture" and snap["live"] == snap["physical"] == 2
+    rows = [ln for ln in DM.smi_table(node_env, snap).splitlines() if "gfx950" in ln]
+    for r in rows:
+        cells = [c.strip() for c in r.strip("|").split("|")]
+        assert float(cells[6]) > 0 and float(cells[7]) > 0
+    assert DM.smi_status(snap) == "ok: 2/2 GPUs live (fixture)"
+
+
+def test_health_container_publishes_the_smi_status(node_env):
+    from amdgpu_operator.cli.verify import verify
+    from amdgpu_operator.wellknown import DRIVER_SMI_ANN
+
+    def ann():
+        return (node_env.client.get("v1", "Node", "n1")["metadata"].get("annotations") or {}).get(DRIVER_SMI_ANN)
+
+    DM.install(node_env, timeout=5)
+    DM.monitor_once(node_env)
+    assert ann().startswith("error: amd-smi unavailable") or ann().startswith("error: live power")
+    node_env.extra["metrics_fixture"] = os.path.join(fakesys.REAL_FIXTURE, "amd-smi-metric.json")
+    node_env.extra.pop("_smi_published")
+    DM.monitor_once(node_env)
+    assert ann() == "ok: 2/2 GPUs live (fixture)"
+    node_env.client.patch("v1", "Node", "n1", {"metadata": {"labels": {"amd.com/gpu.present": "true"}}})
+    assert next(c for c in verify(node_env.client, "default").checks if c.name == "driver-smi[n1]").ok
+    fakesys.SimModule(node_env.host_root).unload(node_env)  # driver lost
+    DM.monitor_once(node_env)
+    assert ann() == "error: driver not live"
+    chk = next(c for c in verify(node_env.client, "default").checks if c.name == "driver-smi[n1]")
+    assert not chk.ok and chk.detail == "error: driver not live"

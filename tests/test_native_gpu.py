@@ -187,6 +187,7 @@ def test_driver_smi_table_on_mi355x(tmp_path):
         used, total = cells[5].removesuffix("MiB").split("/")
         assert int(total) > 280 * 1024 and 0 <= int(used) <= int(total)  # 288 GB HBM3E per GPU
         assert int(cells[6]) > 0 and int(cells[7]) > 0  # live power and temperature from amd-smi
+    assert table.splitlines()[-1].startswith("amd-smi: ok: "), table
 
 
 def test_pci_binding_view_on_mi355x():
