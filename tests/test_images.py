@@ -1,0 +1,55 @@
+"""Slim per-role operand images (tools/image_manifest.py): each image's
+Dockerfile copies exactly the ROCm libraries, native artefacts, distro and
+Python packages its sub-commands need - derived from ``ldd`` of the built
+artefacts (plus the libraries they dlopen) and from importing the role's
+modules - and no runtime image inherits the multi-GB ROCm development image."""
+
+import os
+import re
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import image_manifest as IM  # noqa: E402
+
+
+def test_every_image_copies_what_its_artefacts_need():
+    assert IM.check() == []
+
+
+@pytest.mark.parametrize("role", sorted(IM.ROLES))
+def test_generated_dockerfile_is_current(role):
+    with open(os.path.join(IM.IMAGES, role, "Dockerfile")) as f:
+        assert f.read() == IM.dockerfile(role, IM.requirements(role)), "run: python tools/image_manifest.py generate"
+
+
+@pytest.mark.parametrize("role", [*sorted(IM.ROLES), "amd-driver"])
+def test_runtime_stage_is_not_the_rocm_dev_image(role):
+    with open(os.path.join(IM.IMAGES, role, "Dockerfile")) as f:
+        text = f.read()
+    final = re.findall(r"^FROM (\S+)", text, re.M)[-1]
+    assert "rocm/dev" not in final and final in ("ubuntu:22.04", "${BASE}")
+
+
+def test_roles_need_what_they_run():
+    val = IM.requirements("amd-operator-validator")
+    # HIP runtime + HSA + the AQL profiler it dlopens + the trimmed RCCL's own deps
+    assert {"libamdhip64.so.7", "libhsa-runtime64.so.1", "libhsa-amd-aqlprofile64.so.1",
+            "librocm_smi64.so.1"} <= set(val["rocm_libs"])
+    assert not {"libamd_comgr.so.3", "librocprofiler-sdk.so.1"} & set(val["rocm_libs"])  # SDK gate not shipped
+    assert {"libdrm-amdgpu1", "libnuma1", "libelf1"} <= set(val["apt"])
+    assert IM.requirements("amd-gpu-operator")["rocm_libs"] == []
+    assert {"pydantic", "pyyaml"} <= set(IM.requirements("amd-gpu-operator")["python"])
+    assert {"grpcio", "protobuf"} <= set(IM.requirements("amd-device-plugin")["python"])
+    assert IM.requirements("amd-device-plugin")["rocm_libs"] == ["libamd_smi.so"]
+    assert IM.requirements("amd-container-toolkit")["rocm_libs"] == []
+
+
+def test_dockerfile_parser_sees_a_missing_library():
+    with open(os.path.join(IM.IMAGES, "amd-operator-validator", "Dockerfile")) as f:
+        text = f.read()
+    broken = text.replace("COPY --from=build /opt/rocm/lib/libhsa-runtime64.so.1 /opt/rocm/lib/\n", "")
+    assert "libhsa-runtime64.so.1" not in IM.parse_dockerfile(broken)["rocm_libs"]
+    assert "libhsa-runtime64.so.1" in IM.parse_dockerfile(text)["rocm_libs"]
