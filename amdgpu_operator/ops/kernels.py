@@ -19,6 +19,8 @@ from dataclasses import dataclass
 from .. import native
 
 LIB_NAME = "libamdgpu_validator.so"
+# every GEMM variant of rounds 1-2, for A/B runs: `make -C native lab` (not shipped)
+LAB_LIB_NAME = "lab/libamdgpu_validator_lab.so"
 
 GEMM_BM = 256
 GEMM_BN = 256
@@ -32,8 +34,8 @@ class KernelError(RuntimeError):
     pass
 
 
-def _lib() -> ctypes.CDLL:
-    lib = native.load(LIB_NAME)
+def _lib(name: str = LIB_NAME) -> ctypes.CDLL:
+    lib = native.load(name)
     if getattr(lib, "_avk_typed", False):
         return lib
     P, I, I64, U64, F, S = _c_ptr, ctypes.c_int, _c_i64, ctypes.c_uint64, ctypes.c_float, _c_ptr
@@ -152,9 +154,10 @@ def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int = GE
 
     M and N must be multiples of 256 and K of 64 (the kernel has no edge
     tiles; the validator picks its shapes accordingly).  ``variant`` selects
-    the kernel (default 6 = the 8-phase quadrant pipeline, the kernel the
-    native validator runs; 0-9 are the A/B kernels listed with their measured
-    TF/s above ``avk_gemm_bf16_nt_variant`` in validator_kernels.hip).
+    the kernel: 6 (default) is the 8-phase quadrant pipeline the native
+    validator runs and the only one in the shipped library; 0-5 and 7-9 are
+    the A/B kernels of rounds 1-2, served from the tools build
+    (``make -C native lab``).
     """
     import torch
 
@@ -171,8 +174,9 @@ def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int = GE
     if out.shape != (M, N) or out.dtype not in (torch.bfloat16, torch.float32):
         raise ValueError("bad GEMM output")
     _require(out, out.dtype, "out")
-    rc = _lib().avk_gemm_bf16_nt_variant(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
-                                         M, N, K, variant, _stream(stream))
+    lib = _lib() if variant == GEMM_DEFAULT_VARIANT else _lib(LAB_LIB_NAME)
+    rc = lib.avk_gemm_bf16_nt_variant(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
+                                      M, N, K, variant, _stream(stream))
     _check(rc, "gemm_bf16_nt")
     return out
 

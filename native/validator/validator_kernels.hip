@@ -170,11 +170,14 @@ __global__ __launch_bounds__(256) void check_blocks_kernel(const void* __restric
 // group of a fragment read hit 16 distinct 16-B slots (conflict-free).
 
 namespace gemm {
-constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
+constexpr int BM = 256, BN = 256, BK = 64;   // every variant's block tile (the launcher's shape check)
+#if AVK_GEMM_LAB
 constexpr int TILE_BYTES = BM * BK * 2;      // 32 KiB (A or B of one stage)
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;  // 64 KiB
+constexpr int NTHR = 512;
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;   // 128 KiB
 constexpr int GROUP_M = 4;                   // tile rows per L2 band
+#endif
 }  // namespace gemm
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -198,6 +201,11 @@ __device__ unsigned long long g_stamps[kStampBlocks * 8 * kStampSlices * kStampP
   } while (0)
 #endif
 
+#if AVK_GEMM_LAB
+// Round-1/2 GEMM experiments (variants 0-5, 7-9 of avk_gemm_bf16_nt_variant):
+// built only into the tools library (make -C native lab ->
+// _native/lab/libamdgpu_validator_lab.so) for A/B runs (tools/kernel_bench.py).
+// The shipped library carries the default kernel (variant 6, the 8-phase one below).
 __device__ __forceinline__ void gemm_stage(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                                            int K, int m0, int n0, int k0, char* stage_base, int wave,
                                            int lane) {
@@ -452,6 +460,8 @@ __global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_ring_kernel(const
 // Both groups pass 2*nk+1 barriers.  Operands are swapped in the MFMA
 // (D = B-frag x A-frag = C^T), so each lane ends up with 4 consecutive
 // COLUMNS of one output row: one 16-B (fp32) / 8-B (bf16) store per fragment.
+#endif  // AVK_GEMM_LAB
+
 __device__ __forceinline__ void wg_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::: "memory");
@@ -460,6 +470,7 @@ __device__ __forceinline__ void wg_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+#if AVK_GEMM_LAB
 __device__ __forceinline__ void wait_slice_vmcnt(int ahead) {
   if (ahead >= 2)
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -769,6 +780,8 @@ __global__ __launch_bounds__(gw4::NTHR, 1) void gemm_bf16_nt_w4_kernel(const __b
       }
     }
 }
+
+#endif  // AVK_GEMM_LAB
 
 // ------------------- K2 GEMM, 8-phase quadrant pipeline (BK = 64, 2 buffers) ----
 //
@@ -1337,7 +1350,14 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
   const int nwg = (M / BM) * (N / BN);
   const __bf16* a = (const __bf16*)A;
   const __bf16* b = (const __bf16*)Bt;
+#define AVK_G8(V, LIM, BAL)                                                                       \
+    case V:                                                                                     \
+      if (out_f32) gemm_bf16_nt_8p_kernel<true, LIM, BAL><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K); \
+      else gemm_bf16_nt_8p_kernel<false, LIM, BAL><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K);        \
+      break;
   switch (variant) {
+    AVK_G8(6, false, false)  // the shipped kernel (kDefaultGemmVariant)
+#if AVK_GEMM_LAB
     case 0:
       if (out_f32) gemm_bf16_nt_pp_kernel<true, true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
       else gemm_bf16_nt_pp_kernel<false, true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
@@ -1362,15 +1382,10 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
       if (out_f32) gemm_bf16_nt_pp_kernel<true, true, 5><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
       else gemm_bf16_nt_pp_kernel<false, true, 5><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
       break;
-#define AVK_G8(V, LIM, BAL)                                                                       \
-    case V:                                                                                     \
-      if (out_f32) gemm_bf16_nt_8p_kernel<true, LIM, BAL><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K); \
-      else gemm_bf16_nt_8p_kernel<false, LIM, BAL><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K);        \
-      break;
-    AVK_G8(6, false, false)
     AVK_G8(7, true, false)
     AVK_G8(8, false, true)
     AVK_G8(9, true, true)
+#endif
 #undef AVK_G8
     default:
       return hipErrorInvalidValue;

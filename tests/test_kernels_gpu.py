@@ -32,7 +32,7 @@ def test_vector_add_exact(n):
 @pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 320), (1024, 1024, 1024), (2048, 1024, 4096),
                                    (256, 512, 192), (512, 256, 128)])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [K.GEMM_DEFAULT_VARIANT])
 def test_gemm_vs_fp32_reference(shape, out_dtype, variant):
     M, N, Kd = shape
     g = torch.Generator(device=DEV).manual_seed(M + N + Kd)
@@ -46,7 +46,7 @@ def test_gemm_vs_fp32_reference(shape, out_dtype, variant):
     assert err <= tol, (err, tol)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [K.GEMM_DEFAULT_VARIANT])
 def test_gemm_exact_integer_asymmetric(variant):
     # A = small integers, B asymmetric: a transposed C-write or a swapped
     # fragment map changes the result; all sums are exact in fp32.

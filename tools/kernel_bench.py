@@ -35,7 +35,8 @@ GEMM_VARIANTS = {6: "default_8phase", 0: "ring_pingpong", 1: "dbuf", 2: "ring", 
 
 
 def bench_gemm(n, rounds, iters, variants=None):
-    """Every K2 variant (or the ``variants`` subset) and hipBLASLt, interleaved
+    """Every K2 variant (or the ``variants`` subset; all but the default need
+    ``make -C native lab``) and hipBLASLt, interleaved
     round by round on the same random operands (cdna_hip_programming.md §5.4
     rules 24-25)."""
     sel = {v: GEMM_VARIANTS[v] for v in (variants if variants is not None else GEMM_VARIANTS)}
