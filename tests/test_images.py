@@ -38,7 +38,8 @@ def test_roles_need_what_they_run():
     # HIP runtime + HSA + the AQL profiler it dlopens + the trimmed RCCL's own deps
     assert {"libamdhip64.so.7", "libhsa-runtime64.so.1", "libhsa-amd-aqlprofile64.so.1",
             "librocm_smi64.so.1"} <= set(val["rocm_libs"])
-    assert not {"libamd_comgr.so.3", "librocprofiler-sdk.so.1"} & set(val["rocm_libs"])  # SDK gate not shipped
+    assert "librocprofiler-sdk.so.1" not in val["rocm_libs"]  # the SDK counter gate is not shipped
+    assert "libamd_comgr.so.3" in val["rocm_libs"]  # HIP dlopens it at init (the MI355X trace below)
     assert {"libdrm-amdgpu1", "libnuma1", "libelf1"} <= set(val["apt"])
     assert IM.requirements("amd-gpu-operator")["rocm_libs"] == []
     assert {"pydantic", "pyyaml"} <= set(IM.requirements("amd-gpu-operator")["python"])
@@ -53,3 +54,26 @@ def test_dockerfile_parser_sees_a_missing_library():
     broken = text.replace("COPY --from=build /opt/rocm/lib/libhsa-runtime64.so.1 /opt/rocm/lib/\n", "")
     assert "libhsa-runtime64.so.1" not in IM.parse_dockerfile(broken)["rocm_libs"]
     assert "libhsa-runtime64.so.1" in IM.parse_dockerfile(text)["rocm_libs"]
+
+
+# the interpreter's own extension libraries (python3 package) and the GPU
+# pool's preloaded guard library are not part of a role's closure
+PYTHON_RUNTIME = {"libffi.so.8", "libexpat.so.1", "libbz2.so.1.0", "liblzma.so.5", "libz.so.1"}
+
+
+@pytest.mark.parametrize("run,role", [("validator", "amd-operator-validator"), ("smi", "amd-device-plugin")])
+def test_every_library_loaded_on_the_mi355x_is_in_the_image(run, role):
+    """profiles/r3_images/loaded_libs_mi355x.json: `image_manifest.py trace`
+    on the box (LD_DEBUG=files) - the validator's full step list with the
+    counter gate, and the amd-smi reader.  Each library those processes
+    loaded, dlopen'ed ones included, must be in the role's image."""
+    import json
+
+    with open(os.path.join(ROOT, "profiles/r3_images/loaded_libs_mi355x.json")) as f:
+        trace = json.load(f)[run]
+    assert trace["rc"] == 0
+    req = IM.requirements(role)
+    have = set(req["rocm_libs"]) | set(req["system_libs"]) | {os.path.basename(a) for a in req["native"]}
+    loaded = {os.path.basename(p) for p in trace["loaded"]}
+    loaded = {n for n in loaded if ".cpython-" not in n and "graft" not in n} - PYTHON_RUNTIME
+    assert loaded - have == set()
