@@ -97,37 +97,71 @@ def rocm_version(root: str = "/") -> str:
     return os.environ.get("ROCM_VERSION", "")
 
 
+def _uniform(values, mixed: str = "mixed"):
+    """The single value of ``values``, or ``mixed`` when they differ."""
+    s = set(values)
+    return s.pop() if len(s) == 1 else mixed
+
+
 def gfd_labels(gpus: list[GpuDevice], root: str = "/", prefix: str = "amd.com") -> dict[str, str]:
+    """Node labels from every GPU of the node, not the first one only.
+
+    A property all devices share is labelled with its value; one that
+    differs (a node with GPUs in different partition modes, or mixed SKUs)
+    reads ``mixed``.  Sizes (memory, CUs, clocks, xGMI links) are the
+    minimum over the devices, so a nodeAffinity on them holds for every
+    device the scheduler may hand out; an MFMA data type is ``true`` only
+    when every device has it.  With mixed partition modes each mode also
+    gets ``<prefix>/gpu.<mode>.count`` / ``.memory`` / ``.compute-units`` /
+    ``.product`` - the devices the plugin's ``mixed`` strategy advertises as
+    ``<prefix>/gpu-<mode>`` (``<prefix>/gpu`` for unpartitioned ones) - and
+    mixed SKUs ``<prefix>/gpu.product.<product>.count``."""
     p = f"{prefix}/gpu"
     if not gpus:
         return {}
-    g0 = gpus[0]
-    family = FAMILIES.get(g0.arch, "unknown")
+
+    def product(g):
+        return PRODUCTS.get(g.device_id, f"AMD-GPU-{g.device_id:04x}")
+
+    families = {FAMILIES.get(g.arch, "unknown") for g in gpus}
     physical = len({g.physical_index for g in gpus})
     numa = sorted({g.numa_node for g in gpus if g.numa_node >= 0})
+    modes = [g.compute_partition or "SPX" for g in gpus]
     labels = {
         f"{p}.count": str(len(gpus)),
         f"{p}.physical-count": str(physical),
-        f"{p}.product": label_value(PRODUCTS.get(g0.device_id, f"AMD-GPU-{g0.device_id:04x}")),
-        f"{p}.device-id": f"{g0.device_id:04x}",
-        f"{p}.family": family,
-        f"{p}.arch": label_value(g0.arch),
-        f"{p}.memory": str(g0.vram_bytes // (1024 * 1024)),
-        f"{p}.memory-gib": str(round(g0.vram_bytes / 2**30)),
-        f"{p}.compute-units": str(g0.cu_count),
-        f"{p}.xcc": str(g0.num_xcc),
-        f"{p}.lds-kib": str(g0.lds_size_kib),
+        f"{p}.product": label_value(_uniform(product(g) for g in gpus)),
+        f"{p}.device-id": _uniform(f"{g.device_id:04x}" for g in gpus),
+        f"{p}.family": _uniform(families),
+        f"{p}.arch": label_value(_uniform(g.arch for g in gpus)),
+        f"{p}.memory": str(min(g.vram_bytes for g in gpus) // (1024 * 1024)),
+        f"{p}.memory-gib": str(round(min(g.vram_bytes for g in gpus) / 2**30)),
+        f"{p}.compute-units": str(min(g.cu_count for g in gpus)),
+        f"{p}.xcc": str(min(g.num_xcc for g in gpus)),
+        f"{p}.lds-kib": str(min(g.lds_size_kib for g in gpus)),
         f"{p}.wavefront-size": "64",
-        f"{p}.max-clock-mhz": str(g0.max_engine_clk_mhz),
-        f"{p}.compute-partition": label_value(g0.compute_partition or "SPX"),
-        f"{p}.memory-partition": label_value(g0.memory_partition or "NPS1"),
-        f"{p}.partition-capable": "true" if family == "CDNA4" or family == "CDNA3" else "false",
+        f"{p}.max-clock-mhz": str(min(g.max_engine_clk_mhz for g in gpus)),
+        f"{p}.compute-partition": label_value(_uniform(modes)),
+        f"{p}.memory-partition": label_value(_uniform(g.memory_partition or "NPS1" for g in gpus)),
+        f"{p}.partition-capable": "true" if families <= {"CDNA4", "CDNA3"} else "false",
         f"{p}.numa-nodes": label_value("-".join(str(n) for n in numa) or "none"),
     }
-    for dtype, ok in MFMA_TYPES.get(family, {}).items():
-        labels[f"{p}.mfma.{dtype}"] = "true" if ok else "false"
+    for dtype in sorted({d for f in families for d in MFMA_TYPES.get(f, {})}):
+        labels[f"{p}.mfma.{dtype}"] = "true" if all(MFMA_TYPES.get(f, {}).get(dtype) for f in families) else "false"
+    if len(set(modes)) > 1:
+        for mode in sorted(set(modes)):
+            group = [g for g, m in zip(gpus, modes) if m == mode]
+            m = label_value(mode.lower())
+            labels[f"{p}.{m}.count"] = str(len(group))
+            labels[f"{p}.{m}.memory"] = str(min(g.vram_bytes for g in group) // (1024 * 1024))
+            labels[f"{p}.{m}.compute-units"] = str(min(g.cu_count for g in group))
+            labels[f"{p}.{m}.product"] = label_value(_uniform(product(g) for g in group))
+    products = [product(g) for g in gpus]
+    if len(set(products)) > 1:
+        for prod in sorted(set(products)):
+            labels[f"{p}.product.{label_value(prod)}.count"] = str(products.count(prod))
     hives = {g.hive_id for g in gpus if g.hive_id}
-    labels[f"{p}.xgmi.links"] = str(g0.xgmi_links)
+    labels[f"{p}.xgmi.links"] = str(min(g.xgmi_links for g in gpus))
     labels[f"{p}.xgmi.hive"] = label_value(f"{min(hives):x}") if hives else "none"
     labels[f"{p}.xgmi.hives"] = str(len(hives))
     drv = _read(_root_join(root, "sys/module/amdgpu/version"))

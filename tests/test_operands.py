@@ -590,3 +590,36 @@ def test_cli_simulate_two_nodes_over_http(capsys):
     assert main(["simulate", "--gpus", "2", "--nodes", "2", "--http-api", "--timeout", "90"]) == 0
     out = json.loads(capsys.readouterr().out)
     assert out["nodes"] == 2 and out["http_api"] and out["verify"]["ok"]
+
+
+def test_gfd_labels_describe_every_gpu_of_a_mixed_node(tmp_path):
+    """A node whose GPUs sit in different partition modes is labelled from
+    all of them (round 2 labelled it from the first GPU only): shared values
+    as before, differing ones `mixed`, sizes the minimum, and per-mode
+    counts that match the device plugin's `mixed` resources."""
+    import dataclasses
+
+    fakesys.build_node(str(tmp_path / "a"), 1, "SPX", "NPS1")
+    fakesys.build_node(str(tmp_path / "b"), 1, "CPX", "NPS2")
+    spx, cpx = T.enumerate_gpus(str(tmp_path / "a")), T.enumerate_gpus(str(tmp_path / "b"))
+    cpx = [dataclasses.replace(g, physical_index=1) for g in cpx]
+    lab = L.gfd_labels(spx + cpx, str(tmp_path / "a"))
+    assert lab["amd.com/gpu.count"] == str(1 + len(cpx)) and lab["amd.com/gpu.physical-count"] == "2"
+    assert lab["amd.com/gpu.compute-partition"] == "mixed" and lab["amd.com/gpu.memory-partition"] == "mixed"
+    assert lab["amd.com/gpu.product"] == "AMD-Instinct-MI355X"  # one SKU
+    assert lab["amd.com/gpu.spx.count"] == "1" and lab["amd.com/gpu.cpx.count"] == str(len(cpx))
+    assert int(lab["amd.com/gpu.cpx.compute-units"]) == min(g.cu_count for g in cpx) < int(lab["amd.com/gpu.spx.compute-units"])
+    assert lab["amd.com/gpu.compute-units"] == lab["amd.com/gpu.cpx.compute-units"]  # the minimum over devices
+    assert int(lab["amd.com/gpu.memory"]) == min(g.vram_bytes for g in spx + cpx) // 2**20
+    # the plugin's mixed strategy: amd.com/gpu for SPX, amd.com/gpu-cpx for the partitions
+    res = {T.partition_resource(g, "amd.com/gpu", "mixed") for g in spx + cpx}
+    assert res == {"amd.com/gpu", "amd.com/gpu-cpx"}
+    # mixed SKUs: per-product counts, MFMA types only where all have them
+    mi300 = [dataclasses.replace(spx[0], device_id=0x74A1, arch="gfx942", physical_index=2)]
+    lab = L.gfd_labels(spx + mi300, str(tmp_path / "a"))
+    assert lab["amd.com/gpu.product"] == "mixed" and lab["amd.com/gpu.family"] == "mixed"
+    assert lab["amd.com/gpu.product.AMD-Instinct-MI355X.count"] == "1"
+    assert lab["amd.com/gpu.product.AMD-Instinct-MI300X.count"] == "1"
+    assert lab["amd.com/gpu.mfma.fp4"] == "false" and lab["amd.com/gpu.mfma.bf16"] == "true"
+    for k, v in lab.items():
+        assert len(k.split("/", 1)[1]) <= 63 and len(v) <= 63, (k, v)
