@@ -336,18 +336,22 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             raise
 
     if cmd == "device-plugin":
-        from ..deviceplugin.server import DevicePluginManager, PluginConfig
-
         gated = bool(cenv.get(GATE_ENV))
         if gated:  # devices are enumerated from the live driver's KFD topology
+            import importlib
+
             from ..validator import validate as V
 
+            # grpc (~0.1 s of imports) loads while the driver gate is still closed
+            threading.Thread(target=importlib.import_module, args=("amdgpu_operator.deviceplugin.server",),
+                             name="preload-grpc", daemon=True).start()
             try:
                 V.wait_ready(env, "driver", GATE_TIMEOUT_S, stop)
             except V.StepFailed:
                 if stop.is_set():
                     return 0
                 raise
+        from ..deviceplugin.server import DevicePluginManager, PluginConfig
 
         from ..deviceplugin import config as DC
 
@@ -380,14 +384,11 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                            watch_interval_s=max(0.05, min(0.5, env.poll_s * 10)), device_config=dcfg)
         health = None
         if not a.no_health and not env.extra.get("no_health"):
-            try:
+            def health():  # amd-smi start-up on the health thread, overlapping registration
                 from ..discovery.topology import HealthWatcher
 
-                hw = HealthWatcher()
-                health = hw.poll
-            except Exception as e:  # noqa: BLE001 - no amd-smi (CPU box): serve without health events
-                log.info("health watcher unavailable: %s", e)
-        mgr = DevicePluginManager(cfg, health_poll=health)
+                return HealthWatcher().poll
+        mgr = DevicePluginManager(cfg, health_factory=health)
         mgr.start(register=not gated)
         if gated:
             try:

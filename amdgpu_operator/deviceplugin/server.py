@@ -311,6 +311,7 @@ class DevicePluginServer:
         return self.cfg.endpoint.replace(".sock", "-" + tail + ".sock")
 
     def register(self, timeout: float = 5.0) -> None:
+        t0 = time.perf_counter()
         with grpc.insecure_channel("unix:" + self.cfg.kubelet_path) as ch:
             req_cls, resp_cls, _ = api.REGISTRATION_METHODS["Register"]
             call = ch.unary_unary(api.method_path(api.REGISTRATION_SERVICE, "Register"),
@@ -320,7 +321,8 @@ class DevicePluginServer:
             call(req, timeout=timeout, wait_for_ready=True)
         self.registrations += 1
         self._kubelet_ino = self._kubelet_identity()
-        log.info("registered %s with kubelet (%d devices)", self.resource_name, len(self.devices))
+        log.info("registered %s with kubelet (%d devices) in %.3f s", self.resource_name, len(self.devices),
+                 time.perf_counter() - t0)
 
     def _kubelet_identity(self):
         """(inode, ctime) of kubelet.sock: a re-created socket may reuse the
@@ -370,7 +372,11 @@ class DevicePluginManager:
     routes N6 health events to the owning server."""
 
     def __init__(self, cfg: PluginConfig, devices=None, links=None,
-                 health_poll: Callable[[int], list] | None = None):
+                 health_poll: Callable[[int], list] | None = None,
+                 health_factory: Callable[[], Callable[[int], list]] | None = None):
+        """``health_poll`` polls N6 health events; ``health_factory`` makes
+        that poll function on the health thread instead (amd-smi start-up
+        then overlaps registration instead of delaying it)."""
         from ..discovery import topology
 
         self.cfg = cfg
@@ -380,6 +386,7 @@ class DevicePluginManager:
         self.links = links if links is not None else topology.links(cfg.sysfs_root)
         self.servers = self._build_servers()
         self._health_poll = health_poll
+        self._health_factory = health_factory
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
         self._registered = True
@@ -431,7 +438,7 @@ class DevicePluginManager:
         self._registered = register
         for s in self.servers.values():
             s.start(register=register)
-        if self._health_poll is not None:
+        if self._health_poll is not None or self._health_factory is not None:
             self._thread = threading.Thread(target=self._health_loop, name="amdgpu-dp-health", daemon=True)
             self._thread.start()
 
@@ -445,6 +452,13 @@ class DevicePluginManager:
                     s.register()
 
     def _health_loop(self) -> None:
+        if self._health_poll is None:
+            try:
+                self._health_poll = self._health_factory()
+            except Exception as e:  # noqa: BLE001 - no amd-smi (CPU box): serve without health events
+                log.info("health watcher unavailable: %s", e)
+                return
+            log.info("health watcher live")
         by_index = {d.index: d for d in self.devices}
         while not self._stop.is_set():
             try:

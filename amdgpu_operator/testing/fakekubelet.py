@@ -22,6 +22,7 @@ from __future__ import annotations
 import json
 import os
 import threading
+import time
 from concurrent import futures
 from dataclasses import dataclass, field
 
@@ -51,6 +52,7 @@ class FakeKubelet:
         self.resources: dict[str, _Resource] = {}
         self.assignments: dict[tuple[str, str, str], tuple[str, list[str]]] = {}  # (ns,pod,ctr) -> (res, ids)
         self.register_calls = 0
+        self.register_seconds: list[float] = []  # handler time per Register call
         self._lock = threading.Lock()
         self._alloc_lock = threading.Lock()
         self._server: grpc.Server | None = None
@@ -59,6 +61,7 @@ class FakeKubelet:
 
     # ----------------------------------------------------------- Registration
     def _register(self, request, context):
+        t0 = time.perf_counter()
         if request.version != api.VERSION:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unsupported version {request.version}")
         ep = os.path.join(self.dir, request.endpoint)
@@ -79,6 +82,7 @@ class FakeKubelet:
         res.stream_thread.start()
         with self._registered:
             self._registered.notify_all()
+        self.register_seconds.append(time.perf_counter() - t0)
         return api.pb["Empty"]()
 
     def _watch(self, res: _Resource) -> None:
