@@ -61,8 +61,8 @@ def _mount(name: str, path: str, ro: bool = False, propagation: str | None = Non
 
 
 def _container(name: str, image: str, pull: str, args: list[str], mounts=None, env=None, privileged=False,
-               resources=None, readiness=None, ports=None) -> dict:
-    c = {"name": name, "image": image, "imagePullPolicy": pull, "command": ["amdgpu-operator"], "args": list(args),
+               resources=None, readiness=None, ports=None, command: str = "amdgpu-operator") -> dict:
+    c = {"name": name, "image": image, "imagePullPolicy": pull, "command": [command], "args": list(args),
          "env": [{"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
                  {"name": "OPERATOR_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}},
                  # which pod instance an operand is (the driver container's module ownership)
@@ -440,8 +440,11 @@ def state_nfd(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     n = spec.nfd
     name, sa = "node-feature-discovery-worker", "node-feature-discovery"
     image = n.ref("node-feature-discovery")
-    ctr = _container("nfd-worker", image, n.imagePullPolicy, ["nfd", "--interval", str(n.intervalSeconds)],
-                     [_mount("host-sys", "/host/sys", ro=True)], list(n.env), False, n.resources.model_dump())
+    # the native worker (native/nfd/nfd_worker.cpp): the first operand of every
+    # bring-up, so no interpreter start on the critical path
+    ctr = _container("nfd-worker", image, n.imagePullPolicy, ["--interval", str(n.intervalSeconds)],
+                     [_mount("host-sys", "/host/sys", ro=True)], list(n.env), False, n.resources.model_dump(),
+                     command="amdgpu-nfd")
     vols = [_hostpath("host-sys", "/sys", "Directory")]
     # runs on every node: it is what identifies the GPU nodes in the first place
     ds = _daemonset(spec, ns, owner, name, None, sa, [ctr], [], vols, node_selector={}, operand=n)

@@ -639,12 +639,16 @@ class SimCluster:
         label = f"{run.name}/{c['name']}"
         self.trace("container-start", label)
         try:
-            if prog == "amdgpu-operator" and self.process_containers:
+            if prog in ("amdgpu-operator", "amdgpu-nfd") and self.process_containers:
                 self._run_process_container(run, c, cmd, init)
             elif prog == "amdgpu-operator":
                 from ..cli import operands
 
                 operands.run_in_sim(self, run, c, cmd[1:], init)
+            elif prog == "amdgpu-nfd":  # in-process: the Python worker with the same labels and arguments
+                from ..cli import operands
+
+                operands.run_in_sim(self, run, c, ["nfd", *cmd[1:]], init)
             elif prog == "amdgpu-validator":
                 self._run_gpu_workload(run, c, cmd)
             else:
@@ -699,9 +703,14 @@ class SimCluster:
         rec = {"pod": run.name, "container": c["name"], "init": init, "args": cmd[1:3]}
         t0 = time.perf_counter()
         rec["spawn"] = t0
+        if os.path.basename(cmd[0]) == "amdgpu-nfd":  # the native worker (native/nfd)
+            from .. import native
+
+            argv = [str(native.binary("amdgpu-nfd")), *cmd[1:]]
+        else:
+            argv = [sys.executable, "-m", "amdgpu_operator", *cmd[1:]]
         with open(os.path.join(d, "log"), "w") as log_f:
-            p = subprocess.Popen([sys.executable, "-m", "amdgpu_operator", *cmd[1:]], env=penv, stdout=log_f,
-                                 stderr=subprocess.STDOUT, start_new_session=True)
+            p = subprocess.Popen(argv, env=penv, stdout=log_f, stderr=subprocess.STDOUT, start_new_session=True)
         self.process_stats.append(rec)
 
         def started_s():

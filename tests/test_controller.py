@@ -194,7 +194,7 @@ def test_every_state_builder_yields_valid_objects():
             if o["kind"] == "DaemonSet":
                 t = o["spec"]["template"]
                 assert t["metadata"]["labels"]["app"] == o["metadata"]["name"]
-                assert all(ct["command"] == ["amdgpu-operator"] for ct in t["spec"]["containers"])
+                assert all(ct["command"] in (["amdgpu-operator"], ["amdgpu-nfd"]) for ct in t["spec"]["containers"])
 
 
 def test_node_detection_rules():
