@@ -548,54 +548,73 @@ Step step_vecadd(const Args& args, hipStream_t st) {
 // same GEMM on a private queue between PM4 start/stop packets.  Its output is
 // checked against the HIP path's (checksum of C before and after, C zeroed in
 // between), so the counted dispatch is the validated computation, not a stand-in.
+// The hardware counters are device-wide: a kernel another process runs on the
+// GPU during the counted dispatch (a plugin-validation pod, a user workload
+// during a revalidation) adds its waves and MFMA ops, and the exact
+// invariants fail.  A failed verdict whose output still matched is therefore
+// counted again (kGateAttempts in all): a healthy GPU passes as soon as one
+// dispatch runs alone, a defective one fails every attempt.
+constexpr int kGateAttempts = 3;
+
 bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int cus, hipStream_t st,
               std::string* json) {
   const auto tg = Clock::now();
   unsigned long long* cs;
   HIP_OK(hipMalloc(&cs, 16));
-  HIP_OK(hipMemsetAsync(cs, 0, 16, st));
-  AVK_OK(avk_checksum(C16, (int64_t)n * n * 2, cs, st));
-  HIP_OK(hipMemsetAsync(C16, 0, (size_t)n * n * 2, st));
-  HIP_OK(hipStreamSynchronize(st));
   char bus[64] = {0};
   HIP_OK(hipDeviceGetPCIBusId(bus, sizeof(bus), a.device));
   const std::string co = Gate::exe_dir() + "validator_kernels.co";
   avk_aql_gate_result r;
-  char err[512] = {0};
-  const int rc = avk_aql_gate_gemm(bus, A, B, C16, n, n, n, co.c_str(), 5.0, &r, err, sizeof(err));
-  unsigned long long sums[2] = {0, 0};
-  if (rc == 0) {
-    AVK_OK(avk_checksum(C16, (int64_t)n * n * 2, cs + 1, st));
-    HIP_OK(hipMemcpyAsync(sums, cs, 16, hipMemcpyDeviceToHost, st));
+  avk::GateVerdict v;
+  bool same = false;
+  int attempt = 0;
+  std::string reasons;
+  for (attempt = 1; attempt <= kGateAttempts; ++attempt) {
+    HIP_OK(hipMemsetAsync(cs, 0, 16, st));
+    AVK_OK(avk_checksum(C16, (int64_t)n * n * 2, cs, st));
+    HIP_OK(hipMemsetAsync(C16, 0, (size_t)n * n * 2, st));
     HIP_OK(hipStreamSynchronize(st));
+    char err[512] = {0};
+    const int rc = avk_aql_gate_gemm(bus, A, B, C16, n, n, n, co.c_str(), 5.0, &r, err, sizeof(err));
+    unsigned long long sums[2] = {0, 0};
+    if (rc == 0) {
+      AVK_OK(avk_checksum(C16, (int64_t)n * n * 2, cs + 1, st));
+      HIP_OK(hipMemcpyAsync(sums, cs, 16, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+    }
+    if (rc != 0) {
+      (void)hipFree(cs);
+      std::string esc;
+      for (const char* c = err; *c; ++c) esc += (*c == '"' || *c == '\\') ? '\'' : *c;
+      *json = "\"counter_gate\": \"unavailable\", \"gate_mode\": \"aql\", \"gate_error\": \"" + esc + "\"";
+      return false;
+    }
+    same = sums[0] == sums[1] && sums[0] != 0;
+    avk::GateCounters c;
+    c.mops = r.values[0];
+    c.busy = r.values[1];
+    c.waves = r.values[2];
+    c.gui = r.values[3];
+    c.gui_samples = r.samples[3];
+    c.output_matches = same;
+    v = avk::gate_verdict(n, n, n, cus, c, a.min_mfma_util);
+    if (v.ok || !same) break;  // a wrong result is never retried
+    reasons += (reasons.empty() ? "" : "; ") + v.reason;
   }
+  attempt = std::min(attempt, kGateAttempts);
   (void)hipFree(cs);
-  if (rc != 0) {
-    std::string esc;
-    for (const char* c = err; *c; ++c) esc += (*c == '"' || *c == '\\') ? '\'' : *c;
-    *json = "\"counter_gate\": \"unavailable\", \"gate_mode\": \"aql\", \"gate_error\": \"" + esc + "\"";
-    return false;
-  }
   const double mops = r.values[0], busy = r.values[1], waves = r.values[2], gui = r.values[3];
   const double flops = 2.0 * n * (double)n * n;
-  const bool same = sums[0] == sums[1] && sums[0] != 0;
-  avk::GateCounters c;
-  c.mops = mops;
-  c.busy = busy;
-  c.waves = waves;
-  c.gui = gui;
-  c.gui_samples = r.samples[3];
-  c.output_matches = same;
-  const avk::GateVerdict v = avk::gate_verdict(n, n, n, cus, c, a.min_mfma_util);
-  *json = fmt("\"counter_gate\": \"%s\", \"gate_mode\": \"aql\", \"dispatches\": 1, "
+  *json = fmt("\"counter_gate\": \"%s\", \"gate_mode\": \"aql\", \"dispatches\": 1, \"gate_attempts\": %d, "
               "\"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.0f, \"SQ_VALU_MFMA_BUSY_CYCLES\": %.0f, \"SQ_WAVES\": %.0f, "
               "\"GRBM_GUI_ACTIVE\": %.0f, \"flop_per_mop\": %.6g, \"samples\": [%d, %d, %d, %d], "
               "\"gated_output_matches\": %s, \"mfma_util\": %.4f, \"mfma_util_floor\": %.4f, "
               "\"gate_seconds\": %.4f, \"gate_setup_seconds\": %.4f, \"gate_dispatch_seconds\": %.4f",
-              v.ok ? "pass" : "fail", mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0, r.samples[0], r.samples[1],
-              r.samples[2], r.samples[3], same ? "true" : "false", v.mfma_util, v.util_floor, secs(tg), r.setup_s,
-              r.dispatch_s);
+              v.ok ? "pass" : "fail", attempt, mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0, r.samples[0],
+              r.samples[1], r.samples[2], r.samples[3], same ? "true" : "false", v.mfma_util, v.util_floor, secs(tg),
+              r.setup_s, r.dispatch_s);
   if (!v.ok) *json += ", \"gate_reason\": \"" + v.reason + "\"";
+  if (!reasons.empty()) *json += ", \"gate_retried_after\": \"" + reasons + "\"";
   return v.ok;
 }
 
@@ -645,18 +664,24 @@ Step step_gemm(const Args& a, hipStream_t st, int cus) {
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   AVK_OK(avk_gemm_bf16_nt(A, B, C16, 0, n, n, n, st));  // warm
-  HIP_OK(hipEventRecord(e0, st));
-  for (int i = 0; i < a.gemm_iters; ++i) AVK_OK(avk_gemm_bf16_nt(A, B, C16, 0, n, n, n, st));
-  HIP_OK(hipEventRecord(e1, st));
-  HIP_OK(hipEventSynchronize(e1));
+  // the fastest of kGemmTrials trials of gemm_iters dispatches (see step_hbm)
+  constexpr int kGemmTrials = 3;
+  float best_ms = 0;
+  for (int t = 0; t < kGemmTrials; ++t) {
+    HIP_OK(hipEventRecord(e0, st));
+    for (int i = 0; i < a.gemm_iters; ++i) AVK_OK(avk_gemm_bf16_nt(A, B, C16, 0, n, n, n, st));
+    HIP_OK(hipEventRecord(e1, st));
+    HIP_OK(hipEventSynchronize(e1));
+    float tm = 0;
+    HIP_OK(hipEventElapsedTime(&tm, e0, e1));
+    if (t == 0 || tm < best_ms) best_ms = tm;
+  }
   // counter gate on one extra dispatch: counter collection serialises
   // dispatches, so it must not overlap the timed ones
   if (a.counter_gate && a.gate_mode == "aql") {
     std::string gate_json;
     const bool gate_ok = aql_gate(a, A, B, C16, n, cus, st, &gate_json);
-    float ms = 0;
-    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-    ms /= a.gemm_iters;
+    const float ms = best_ms / a.gemm_iters;
     const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
@@ -677,9 +702,7 @@ Step step_gemm(const Args& a, hipStream_t st, int cus) {
     HIP_OK(hipStreamSynchronize(st));
     g_gate.disarm();
   }
-  float ms = 0;
-  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-  ms /= a.gemm_iters;
+  const float ms = best_ms / a.gemm_iters;
   const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
   std::string gate_json = "\"counter_gate\": \"off\"";
   bool gate_ok = true;
@@ -746,13 +769,19 @@ Step step_hbm(const Args& a, hipStream_t st, int cus) {
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
-  const int iters = 3;
-  HIP_OK(hipEventRecord(e0, st));
-  for (int i = 0; i < iters; ++i) AVK_OK(avk_hbm_copy(src, dst, bytes, cus, 1, st));
-  HIP_OK(hipEventRecord(e1, st));
-  HIP_OK(hipEventSynchronize(e1));
+  // the fastest of several short trials: another process's kernel or queue
+  // set-up on the GPU stalls one trial, not all (the floor judges the device)
+  const int iters = 3, trials = 5;
   float ms = 0;
-  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  for (int t = 0; t < trials; ++t) {
+    HIP_OK(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i) AVK_OK(avk_hbm_copy(src, dst, bytes, cus, 1, st));
+    HIP_OK(hipEventRecord(e1, st));
+    HIP_OK(hipEventSynchronize(e1));
+    float tm = 0;
+    HIP_OK(hipEventElapsedTime(&tm, e0, e1));
+    if (t == 0 || tm < ms) ms = tm;
+  }
   ms /= iters;
   unsigned long long h[2];
   AVK_OK(avk_checksum(src, bytes, cs, st));
@@ -773,8 +802,8 @@ Step step_hbm(const Args& a, hipStream_t st, int cus) {
   s.ok = h[0] == h[1] && perf_ok;
   s.seconds = secs(t0);
   s.detail = fmt("\"bytes\": %lld, \"ms\": %.4f, \"gbps\": %.1f, \"min_gbps\": %.1f, \"perf_ok\": %s, "
-                 "\"checksum_match\": %s", (long long)bytes, ms, gbps, floor, perf_ok ? "true" : "false",
-                 h[0] == h[1] ? "true" : "false");
+                 "\"checksum_match\": %s, \"trials\": %d", (long long)bytes, ms, gbps, floor, perf_ok ? "true" : "false",
+                 h[0] == h[1] ? "true" : "false", trials);
   return s;
 }
 
