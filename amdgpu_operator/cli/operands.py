@@ -388,11 +388,26 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                 from ..discovery.topology import HealthWatcher
 
                 return HealthWatcher().poll
+        def needs_toolkit(c) -> bool:
+            """Allocate responses that rely on what the toolkit installs: CDI
+            device names (its CDI spec), volume-mount device lists or env-var
+            lists without device specs (its OCI hook).  With device specs the
+            kubelet hands the container /dev/kfd and the render nodes itself,
+            and the ROCm userspace is in the workload image - unlike the
+            reference's driver libraries, nothing has to be injected."""
+            f = c.flags if c is not None else cli_config.flags
+            lists = set(f.deviceListStrategy) | ({"cdi-cri"} if a.cdi else set())
+            return bool(lists & {"cdi-annotations", "cdi-cri", "volume-mounts"}) or not f.passDeviceSpecs
+
         mgr = DevicePluginManager(cfg, health_factory=health)
         mgr.start(register=not gated)
         if gated:
+            steps = [x for x in cenv[GATE_ENV].split(",") if x]
+            if not needs_toolkit(dcfg) and "toolkit" in steps:
+                steps.remove("toolkit")  # the validator's plugin check still waits for it (--wait-toolkit)
+                log.info("advertising before the toolkit: allocations carry device specs only")
             try:
-                _wait_gates(env, {GATE_ENV: cenv[GATE_ENV]}, stop)
+                _wait_gates(env, {GATE_ENV: ",".join(steps)}, stop)
             except Exception:  # noqa: BLE001 - stopped while gated: a clean exit
                 mgr.stop()
                 if stop.is_set():
@@ -408,6 +423,11 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                 except Exception as e:  # noqa: BLE001 - keep serving the last good config
                     log.error("device-plugin config: %s", e)
                     continue
+                if gated and needs_toolkit(new_cfg) and "toolkit" in cenv[GATE_ENV].split(","):
+                    from ..validator import validate as V
+
+                    if V.read_ready(env, "toolkit") is None:
+                        continue  # CDI / hook-based allocations only once the toolkit is installed
                 if mgr.reconfigure(new_cfg):
                     log.info("device-plugin config %r -> %r", key, new_key)
                     key = new_key

@@ -226,3 +226,47 @@ def test_prepared_plugin_does_not_register_before_it_is_told(tmp_path):
     finally:
         mgr.stop()
         k.stop()
+
+
+@pytest.mark.parametrize("strategy,before_toolkit", [("envvar", True), ("cdi-cri", False)])
+def test_plugin_advertises_before_the_toolkit_only_when_allocations_need_nothing_from_it(tmp_path, strategy,
+                                                                                         before_toolkit):
+    """Gated on the toolkit (VALIDATION_GATE=toolkit): with device specs the
+    kubelet gives the container /dev/kfd and the render nodes itself, so the
+    plugin registers once the driver is up; CDI device names need the
+    toolkit's CDI spec, so that plugin waits for toolkit-ready."""
+    import threading
+    import time
+
+    from amdgpu_operator.cli.operands import run_operand
+    from amdgpu_operator.kube.client import LocalClient
+    from amdgpu_operator.kube.fakeapi import FakeApiServer
+    from amdgpu_operator.nodeenv import NodeEnv
+    from amdgpu_operator.testing import fakesys
+    from amdgpu_operator.testing.fakekubelet import FakeKubelet
+    from amdgpu_operator.validator import validate as V
+
+    root = str(tmp_path / "h")
+    fakesys.build_node(root, 2)
+    dp = tmp_path / "dp"
+    dp.mkdir()
+    k = FakeKubelet(str(dp))
+    k.start()
+    env = NodeEnv("n1", LocalClient(FakeApiServer()), host_root=root, validations_dir=str(tmp_path / "val"),
+                  device_plugin_dir=str(dp), poll_s=0.01)
+    env.extra["no_health"] = True
+    V.write_ready(env, "driver", {"ok": True})
+    stop = threading.Event()
+    t = threading.Thread(target=run_operand, args=(env, ["device-plugin", "--device-list-strategy", strategy], stop),
+                         kwargs={"container_env": {"VALIDATION_GATE": "toolkit"}}, daemon=True)
+    t.start()
+    try:
+        registered = k.wait_registered("amd.com/gpu", 3 if before_toolkit else 0.5, min_devices=2)
+        assert registered == before_toolkit
+        if not before_toolkit:
+            V.write_ready(env, "toolkit", {"ok": True})
+            assert k.wait_registered("amd.com/gpu", 5, min_devices=2)
+    finally:
+        stop.set()
+        t.join(10)
+        k.stop()
