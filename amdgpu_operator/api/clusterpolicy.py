@@ -356,15 +356,17 @@ class ClusterPolicySpec(_M):
         return self
 
 
-# operand state order: each gated on the previous ones
+# operand state order, also the order a reconcile pass
+# applies them in: node feature discovery first - its labels are what makes
+# a node a GPU node, so every other operand of a bring-up waits for it
 STATES = [
     ("pre-requisites", None),
+    ("state-node-feature-discovery", "nfd"),
     ("state-driver", "driver"),
     ("state-container-toolkit", "toolkit"),
     ("state-operator-validation", "validator"),
     ("state-device-plugin", "devicePlugin"),
     ("state-metrics-exporter", "dcgmExporter"),
-    ("state-node-feature-discovery", "nfd"),
     ("state-gpu-feature-discovery", "gfd"),
     ("state-partition-manager", "migManager"),
     ("state-node-status-exporter", "nodeStatusExporter"),
