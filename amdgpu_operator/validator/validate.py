@@ -486,7 +486,8 @@ def _device_plan(expected: dict, held: dict[str, list[str]]) -> dict | None:
     return plan if sum(plan.values()) >= sum(expected.values()) else None
 
 
-def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, kd=None) -> dict | None:
+def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, kd=None,
+                          shared: set | None = None) -> dict | None:
     """Wait until the kubelet's device manager holds the ``expected`` devices
     (pod-resources ``GetAllocatableResources``, deviceplugin/podresources.py;
     :func:`_device_plan`).  Returns the pods to run per resource, or None when
@@ -511,6 +512,10 @@ def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, k
                 return None
             plan = _device_plan(expected, held)
             if plan is not None:
+                if shared is not None:  # time-sliced resources: replicas <id>::<k>
+                    from ..deviceplugin.api import REPLICA_SEP
+
+                    shared.update(r for r, ids in held.items() if any(REPLICA_SEP in i for i in ids))
                 return plan
             if time.monotonic() >= deadline:
                 raise StepFailed(f"kubelet holds {({r: len(v) for r, v in held.items()})} devices, "
@@ -551,10 +556,12 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     t0 = time.perf_counter()
     expected = {resource: expect} if expect is not None else expected_devices(env, resource, partition_strategy)
     deadline = time.monotonic() + timeout
-    plan = _wait_kubelet_devices(env, expected, deadline, stop, kubelet)
+    shared: set = set()
+    plan = _wait_kubelet_devices(env, expected, deadline, stop, kubelet, shared)
     source = "kubelet"
     if plan is None:  # no pod-resources API: wait for the kubelet to publish Node.status.allocatable
         source = "node-status"
+        shared = set(expected) | {"*"}  # replicas cannot be told apart here: one device per pod
 
         def node_plan(node: dict):
             # counts only: replicas are not told apart here, so a renamed
@@ -583,7 +590,8 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     marks = {"start": time.time() - (time.perf_counter() - t0), "devices_seen": time.time()}
     pod_args = list(pod_args or ["--steps", "hip,vecadd,gemm", "--gemm", "1024"])
 
-    def make_pod(name: str, run_id: str, res: str) -> dict:
+    def make_pod(name: str, run_id: str, res: str, count: int = 1) -> dict:
+        args = pod_args + (["--all-devices"] if count > 1 else [])
         pod = {
             "apiVersion": "v1", "kind": "Pod",
             "metadata": {"name": name, "namespace": env.namespace,
@@ -593,8 +601,8 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                 "restartPolicy": "Never",
                 "tolerations": [{"key": resource, "operator": "Exists", "effect": "NoSchedule"}],
                 "containers": [{"name": "workload", "image": image, "imagePullPolicy": pull_policy,
-                                "command": ["amdgpu-validator"], "args": pod_args, "env": PLUGIN_POD_ENV,
-                                "resources": {"limits": {res: "1"}, "requests": {res: "1"}}}],
+                                "command": ["amdgpu-validator"], "args": args, "env": PLUGIN_POD_ENV,
+                                "resources": {"limits": {res: str(count)}, "requests": {res: str(count)}}}],
             },
         }
         if pull_secrets:
@@ -607,17 +615,23 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     # a pod the kubelet could not admit (UnexpectedAdmissionError: the device
     # list it planned from was stale, e.g. a re-registering plugin's devices
     # still unhealthy) is run again; any other failure fails the step
-    todo = [r for r, n in sorted(plan.items()) for _ in range(n)]
+    # One pod per resource holding all of its devices: every GPU still goes
+    # through Allocate, the OCI hook and a kernel launch, from one process
+    # (at N = 8, 8 fewer process and HIP starts in the node's start-up
+    # storm, profiles/r3_storm).  Time-sliced resources keep one 1-replica
+    # pod per GPU: a multi-replica request may land twice on one GPU.
+    todo = [(r, 1) for r, n in sorted(plan.items()) if r in shared or "*" in shared for _ in range(n)]
+    todo += [(r, n) for r, n in sorted(plan.items()) if r not in shared and "*" not in shared]
     devices: list[str] = []
-    attempts, backoff = 0, 0.05
+    attempts, backoff, pods_run = 0, 0.05, 0
     while todo:
         attempts += 1
         run_id = uuid.uuid4().hex[:8]
         names = {}
-        for i, res in enumerate(todo):
+        for i, (res, count) in enumerate(todo):
             name = f"amd-validator-workload-{run_id}-{i}"
-            env.client.create(make_pod(name, run_id, res))
-            names[name] = res
+            env.client.create(make_pod(name, run_id, res, count))
+            names[name] = (res, count)
         marks.setdefault("pods_created", time.time())
         live, _ = wait_for(env.client, "v1", "Pod", lambda objs: all(
             n in objs and phase(objs[n]) in ("Succeeded", "Failed") for n in names), namespace=env.namespace,
@@ -634,8 +648,11 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
         hard = {n: p for n, p in phases.items() if p != "Succeeded" and n not in retry}
         if hard:
             raise StepFailed(f"plugin validation pods did not succeed: {phases}")
-        devices += [((live[n].get("metadata", {}).get("annotations") or {}).get("amd.com/gpu.allocated", ""))
-                    for n in names if phases[n] == "Succeeded"]
+        for n in names:
+            if phases[n] == "Succeeded":
+                alloc = (live[n].get("metadata", {}).get("annotations") or {}).get("amd.com/gpu.allocated", "")
+                devices += alloc.split(",") if alloc else [""] * names[n][1]
+        pods_run += sum(1 for n in names if phases[n] == "Succeeded")
         todo = [names[n] for n in retry]
         if todo:
             if time.monotonic() + backoff >= deadline or (stop is not None and stop.is_set()):
@@ -643,7 +660,8 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
             log.info("%d plugin validation pod(s) not admitted, retrying in %.2f s", len(todo), backoff)
             (stop.wait if stop is not None else time.sleep)(backoff)
             backoff = min(backoff * 2, 2.0)
-    summary = {"ok": True, "pods": len(devices), "resources": plan, "devices": devices, "attempts": attempts,
+    summary = {"ok": True, "pods": pods_run, "devices_validated": len(devices), "resources": plan, "devices": devices,
+               "attempts": attempts,
                "allocatable_wait_s": round(t_alloc, 4),
                "allocatable_source": source, "marks": {k: round(v, 4) for k, v in marks.items()},
                "seconds": time.perf_counter() - t0}

@@ -255,6 +255,7 @@ struct Args {
   bool counter_gate = false;
   bool any_arch = false;
   bool null_stream = false;   // run the steps on the legacy null stream instead of a created one
+  bool all_devices = false;   // every visible device in turn (a plugin-validation pod holding N GPUs)
   bool rccl_destroy = false;  // ncclCommDestroy before exit (default: barrier + exit, see step_rccl)
   std::string ready_file;
 };
@@ -1263,6 +1264,7 @@ int main(int argc, char** argv) {
     else if (k == "--hbm-bytes") a.hbm_bytes = atoll(v());
     else if (k == "--vecadd-elems") a.vecadd_elems = atoll(v());
     else if (k == "--null-stream") a.null_stream = true;
+    else if (k == "--all-devices") a.all_devices = true;
     else if (k == "--rccl-elems") a.rccl_elems = atoll(v());
     else if (k == "--xgmi-elems") a.xgmi_elems = atoll(v());
     else if (k == "--emulated-peers") a.emulated_peers = atoi(v());
@@ -1289,6 +1291,10 @@ int main(int argc, char** argv) {
       a.hbm_bytes % 16 || a.rccl_elems <= 0 || a.xgmi_elems <= 0 || a.xgmi_elems % 4 || a.emulated_peers < 1 ||
       a.emulated_peers > 8 || a.world > 64 || (a.world > 8 && has_step(a, "xgmi"))) {
     fprintf(stderr, "amdgpu-validator: invalid arguments (gemm %% 256, sizes %% 16, world <= 64, xgmi needs world <= 8)\n");
+    return 2;
+  }
+  if (a.all_devices && (a.world > 1 || has_step(a, "rccl") || has_step(a, "xgmi"))) {
+    fprintf(stderr, "amdgpu-validator: --all-devices runs the single-GPU steps (world 1, no rccl / xgmi)\n");
     return 2;
   }
   if (a.gate_mode != "aql" && a.gate_mode != "sdk") {
@@ -1369,20 +1375,44 @@ int main(int argc, char** argv) {
   int failed_peer = -1;
   std::string peer_state;
   try {
-    if (a.world > 1 && has_step(a, "peers")) steps.push_back(step_peers(a, rv));
-    steps.push_back(step_hip(a, &prop));
-    ok = steps.back().ok;
-    if (ok && has_step(a, "rccl") && rccl_state.error.empty())
-      rccl_thread = std::thread(rccl_init, std::cref(a), std::cref(rv), &rccl_state);
-    const auto ts = Clock::now();
-    if (!a.null_stream) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    stream_create_s = secs(ts);
-    if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
-    if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st, prop.multiProcessorCount)), steps.back().ok);
-    if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
-    if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
-    if (ok && has_step(a, "xgmi")) ok = (steps.push_back(step_xgmi(a, st, rv)), steps.back().ok);
-    if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, rv, &rccl_thread, &rccl_state)), steps.back().ok);
+    if (a.all_devices) {
+      // one process for every GPU the pod holds: each device runs the
+      // single-GPU steps in turn (its step records carry "device")
+      int count = 0;
+      HIP_OK(hipGetDeviceCount(&count));
+      if (count <= 0) throw std::runtime_error("no visible GPU");
+      for (int d = 0; d < count && ok; ++d) {
+        Args ad = a;
+        ad.device = d;
+        const size_t first = steps.size();
+        steps.push_back(step_hip(ad, &prop));
+        ok = steps.back().ok;
+        hipStream_t sd = nullptr;
+        if (!a.null_stream) HIP_OK(hipStreamCreateWithFlags(&sd, hipStreamNonBlocking));
+        if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(ad, sd)), steps.back().ok);
+        if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(ad, sd, prop.multiProcessorCount)), steps.back().ok);
+        if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(sd)), steps.back().ok);
+        if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(ad, sd, prop.multiProcessorCount)), steps.back().ok);
+        if (sd) (void)hipStreamDestroy(sd);
+        for (size_t i = first; i < steps.size(); ++i)
+          steps[i].detail = fmt("\"device\": %d", d) + (steps[i].detail.empty() ? "" : ", " + steps[i].detail);
+      }
+    } else {
+      if (a.world > 1 && has_step(a, "peers")) steps.push_back(step_peers(a, rv));
+      steps.push_back(step_hip(a, &prop));
+      ok = steps.back().ok;
+      if (ok && has_step(a, "rccl") && rccl_state.error.empty())
+        rccl_thread = std::thread(rccl_init, std::cref(a), std::cref(rv), &rccl_state);
+      const auto ts = Clock::now();
+      if (!a.null_stream) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      stream_create_s = secs(ts);
+      if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
+      if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st, prop.multiProcessorCount)), steps.back().ok);
+      if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
+      if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
+      if (ok && has_step(a, "xgmi")) ok = (steps.push_back(step_xgmi(a, st, rv)), steps.back().ok);
+      if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, rv, &rccl_thread, &rccl_state)), steps.back().ok);
+    }
   } catch (const PeerError& e) {
     ok = false;
     error = e.what();
@@ -1413,7 +1443,7 @@ int main(int argc, char** argv) {
   trace("stream destroyed");
   const double total = secs(t_start);
   std::string out = fmt("{\"ok\": %s, \"rank\": %d, \"world\": %d, \"device\": %d, \"seconds\": %.4f, ", ok ? "true" : "false",
-                        a.rank, a.world, a.device, total);
+                        a.rank, a.world, a.all_devices ? -1 : a.device, total);
   if (stream_create_s >= 0) out += fmt("\"stream_create_s\": %.4f, ", stream_create_s);
   if (gate_wait_s >= 0)
     out += fmt("\"start_gate\": {\"wait_s\": %.4f, \"kfd_open_at_gate\": %s, \"steps_s\": %.4f}, ", gate_wait_s,

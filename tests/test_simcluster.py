@@ -86,7 +86,9 @@ def test_cpx_mixed_strategy_validates_partition_resources(cluster_factory):
     from amdgpu_operator.validator.validate import read_ready
 
     plugin = read_ready(c.nodes["gpu-1"].env, "plugin")
-    assert plugin["resources"] == {"amd.com/gpu-cpx": 16} and plugin["pods"] == 16
+    # one pod holding all 16 partitions validates each of them (--all-devices)
+    assert plugin["resources"] == {"amd.com/gpu-cpx": 16} and plugin["pods"] == 1
+    assert plugin["devices_validated"] == 16 and len(set(plugin["devices"])) == 16
 
 
 def test_unhealthy_gpu_drops_allocatable(cluster_factory):
@@ -229,7 +231,7 @@ def test_plugin_pods_not_admitted_are_run_again(cluster_factory):
     while time.time() < deadline and (read_ready(node.env, "plugin") or {}).get("time", 0) < t_del:
         time.sleep(0.05)
     plug = read_ready(node.env, "plugin")
-    assert plug["ok"] and plug["attempts"] >= 2 and plug["pods"] == 2
+    assert plug["ok"] and plug["attempts"] >= 2 and plug["pods"] == 1 and plug["devices_validated"] == 2
 
 
 def test_metrics_and_node_status_exporters_serve(cluster_factory):
@@ -302,7 +304,7 @@ def test_validation_does_not_wait_for_the_kubelet_status_tick(cluster_factory):
     ttr = c.wait_ready(15)
     assert ttr < 10.0
     plug = read_ready(c.nodes["gpu-1"].env, "plugin")
-    assert plug["allocatable_source"] == "kubelet" and plug["pods"] == 8
+    assert plug["allocatable_source"] == "kubelet" and plug["pods"] == 1 and plug["devices_validated"] == 8
     c.wait_ready(30, {"gpu-1": 8})  # the kubelet does publish them, on its own tick
 
 

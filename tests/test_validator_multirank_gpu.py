@@ -139,3 +139,17 @@ def test_kernel_check_process_restricted_to_its_gpu(tmp_path):
     rep = json.loads(p.stdout.strip().splitlines()[-1])
     assert p.returncode == 0 and rep["ok"], (rep, p.stderr[-1000:])
     assert {s["name"]: s for s in rep["steps"]}["hip"]["arch"].startswith("gfx950")
+
+
+def test_all_devices_validates_every_gpu_the_pod_holds(tmp_path):
+    """The plugin-validation pod holds all of a resource's GPUs and checks
+    each one from a single process (--all-devices): every visible device
+    runs hip + vecadd, and each step record names its device."""
+    rc, rep, _ = _local(tmp_path, "hip,vecadd", ["--all-devices"])
+    assert rc == 0 and rep["ok"] and rep["device"] == -1, rep
+    n = sum(1 for s in rep["steps"] if s["name"] == "hip")
+    assert n >= 1 and [(s["device"], s["name"]) for s in rep["steps"]] == \
+        [(d, step) for d in range(n) for step in ("hip", "vecadd")], rep["steps"]
+    # peers-only steps are refused with it
+    p = subprocess.run([VALIDATOR, "--all-devices", "--steps", "hip,rccl"], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 2 and "--all-devices" in p.stderr
