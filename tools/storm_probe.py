@@ -22,6 +22,8 @@ Variants (each repeated ``--reps`` times):
   merged     RCCL folded into the kernel-check process (rcclProcess=shared):
              2N processes
   staggered  the plugin pods start only after the 2N workload processes reported
+  onepod     the round-3 design: the plugin check is one pod holding every GPU
+             (amdgpu-validator --all-devices), 2N + 1 processes
 
 Per process: ``hip`` step (runtime + context init), ``vecadd`` (first kernel
 launch), the process's own total, and spawn-to-report as the orchestrator saw
@@ -82,7 +84,10 @@ def run_variant(variant: str, n: int, real_gpus: int, tmp: str) -> dict:
     root = os.path.join(tmp, f"node-{variant}-{time.monotonic_ns()}")
     fakesys.build_node(root, n)
     env = NodeEnv("storm", None, host_root=root, validations_dir=os.path.join(root, "val"), poll_s=0.01)
-    env.launcher = lambda argv, e, d, t: run_local(_rewrite(argv, real_gpus), e, t)
+    # the fake node's KFD unique ids mean nothing to this machine's runtime:
+    # the kernel-check processes see the real GPUs
+    env.launcher = lambda argv, e, d, t: run_local(_rewrite(argv, real_gpus),
+                                                   {k: v for k, v in e.items() if k != "ROCR_VISIBLE_DEVICES"}, t)
     args = list(KERNEL_ARGS)
     if variant == "merged":
         args.append("--rccl-shared-process")
@@ -100,8 +105,11 @@ def run_variant(variant: str, n: int, real_gpus: int, tmp: str) -> dict:
     def pods():
         jobs = [[str(native.binary("amdgpu-validator")), "--device", str(i % real_gpus), "--rendezvous",
                  env.validations_dir, "--run-id", f"pod{i}", *POD_ARGS] for i in range(n)]
+        if variant == "onepod":
+            jobs = [[str(native.binary("amdgpu-validator")), "--all-devices", "--rendezvous", env.validations_dir,
+                     "--run-id", "pod", *POD_ARGS]]
         penv = {REPORT_EARLY_ENV: "1", **{e["name"]: e["value"] for e in V.PLUGIN_POD_ENV}}
-        with ThreadPoolExecutor(max_workers=n) as ex:
+        with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
             res = list(ex.map(lambda a: run_local(a, penv, 300), jobs))
         out = []
         for r in res:
@@ -133,7 +141,7 @@ def main() -> int:
     # processes is the largest storm of this shape that fits on one device
     ap.add_argument("--gpus", type=int, default=5, help="GPUs of the rehearsed node (3 processes each)")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", default="single,storm,merged,staggered")
+    ap.add_argument("--variants", default="single,storm,onepod,merged,staggered")
     a = ap.parse_args()
     from amdgpu_operator.discovery import topology
 
