@@ -102,6 +102,17 @@ __global__ __launch_bounds__(256) void vector_add_kernel(const f32x4* __restrict
     if (i + u * 256 < n4) c[i + u * 256] = a[i + u * 256] + b[i + u * 256];
 }
 
+// The in-container GPU check (native/validator/gpu_check.cpp) dispatches this
+// through HSA directly: one element per lane, no loop and no implicit kernel
+// arguments (grid and block sizes are not read), so a raw AQL packet with the
+// explicit arguments alone runs it correctly and it always terminates.
+extern "C" __global__ __launch_bounds__(256) void avk_gpu_check_add(const float* __restrict__ a,
+                                                                   const float* __restrict__ b,
+                                                                   float* __restrict__ c, int n) {
+  const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  if (i < n) c[i] = a[i] + b[i];
+}
+
 __global__ void vector_add_tail_kernel(const float* a, const float* b, float* c, int64_t start, int64_t n) {
   int64_t i = start + threadIdx.x;
   if (i < n) c[i] = a[i] + b[i];
