@@ -280,6 +280,11 @@ class ValidatorSpec(Operand):
     image: str = "amd-operator-validator"
     workload: WorkloadSpec = Field(default_factory=WorkloadSpec)
     pluginValidation: bool = True
+    # what a plugin-validation pod runs on the GPUs it was allocated: "hsa" -
+    # amdgpu-gpu-check, a kernel per GPU on the HSA runtime alone (~0.08 s to
+    # its report on MI355X); "hip" - amdgpu-validator hip,vecadd (HIP runtime
+    # and context, ~0.1-0.2 s; profiles/r3_pod_check)
+    pluginPodCheck: Literal["hsa", "hip"] = "hsa"
     validationsDir: str = "/run/amd/validations"
 
 

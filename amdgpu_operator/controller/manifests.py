@@ -343,7 +343,7 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     # the plugin pods request what the device plugin advertises (its resource
     # name, and amd.com/gpu-<mode> for partitioned GPUs under "mixed")
     plugin_res = ["--resource", spec.devicePlugin.resourceName,
-                  "--partition-strategy", spec.devicePlugin.partitionStrategy]
+                  "--partition-strategy", spec.devicePlugin.partitionStrategy, "--pod-check", v.pluginPodCheck]
     if v.pluginValidation and spec.devicePlugin.enabled and w.prespawn:
         # one init container validates the driver and, meanwhile, starts the
         # workload processes behind their start gate (validate.py validate_gpu)

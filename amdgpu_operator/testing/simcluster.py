@@ -334,6 +334,15 @@ class SimCluster:
         return SimNode(ns, d, env, kubelet)
 
     def _launch(self, argv, env, device, timeout) -> ProcResult:
+        if self.fake_gpu and argv and os.path.basename(argv[0]) == "amdgpu-gpu-check":
+            argv = [argv[0], "--steps", "hsa,vecadd"]  # the stand-in reports the check's steps
+            if self.fake_gpu != "procs":
+                return fake_validator_result(argv)
+            import sys
+
+            argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", *argv[1:]]
+            return self.launcher(argv, env, device, timeout) if self.launcher is not None else run_local(argv, env,
+                                                                                                        timeout)
         if self.fake_gpu and argv and os.path.basename(argv[0]) == "amdgpu-validator":
             if self.fake_gpu != "procs":
                 from .fake_validator import wait_start_gate
@@ -649,7 +658,7 @@ class SimCluster:
                 from ..cli import operands
 
                 operands.run_in_sim(self, run, c, ["nfd", *cmd[1:]], init)
-            elif prog == "amdgpu-validator":
+            elif prog in ("amdgpu-validator", "amdgpu-gpu-check"):
                 self._run_gpu_workload(run, c, cmd)
             else:
                 raise RuntimeError(f"unknown program {prog}")
@@ -792,7 +801,7 @@ class SimCluster:
             if "/dev/kfd" not in paths:
                 raise RuntimeError("OCI hook did not inject /dev/kfd")
         self.trace("gpu-pod-hooked", run.name)
-        argv = [str(native.binary("amdgpu-validator"))] + cmd[1:]
+        argv = [str(native.binary(os.path.basename(cmd[0])))] + cmd[1:]
         proc_env = {e["name"]: e["value"] for e in c.get("env") or [] if "value" in e}  # the container's env
         if REPORT_EARLY:
             proc_env[REPORT_EARLY_ENV] = "1"

@@ -34,6 +34,8 @@ def adopt_sim_node_env(env: NodeEnv) -> None:
         def launch(argv, penv, device, timeout):
             if os.path.basename(argv[0]) == "amdgpu-validator":
                 argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", *argv[1:]]
+            elif os.path.basename(argv[0]) == "amdgpu-gpu-check":
+                argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", "--steps", "hsa,vecadd"]
             return run_local(argv, penv, timeout)
 
         env.launcher = launch

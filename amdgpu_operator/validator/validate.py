@@ -539,7 +539,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                     pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                     image: str | None = None, pull_policy: str = "IfNotPresent",
                     pull_secrets: list[str] | None = None, kubelet=None,
-                    partition_strategy: str = "single") -> dict:
+                    partition_strategy: str = "single", pod_check: str = "hsa") -> dict:
     """Wait until the kubelet holds one device per GPU (or partition), then
     run one 1-device pod per device, each requesting the resource its device
     is advertised under (:func:`expected_devices`; ``expect`` overrides the
@@ -591,7 +591,10 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     pod_args = list(pod_args or ["--steps", "hip,vecadd,gemm", "--gemm", "1024"])
 
     def make_pod(name: str, run_id: str, res: str, count: int = 1) -> dict:
-        args = pod_args + (["--all-devices"] if count > 1 else [])
+        if pod_check == "hsa":  # a kernel per allocated GPU on the HSA runtime (native/validator/gpu_check.cpp)
+            command, args = "amdgpu-gpu-check", ["--timeout", "30"]
+        else:
+            command, args = "amdgpu-validator", pod_args + (["--all-devices"] if count > 1 else [])
         pod = {
             "apiVersion": "v1", "kind": "Pod",
             "metadata": {"name": name, "namespace": env.namespace,
@@ -601,7 +604,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                 "restartPolicy": "Never",
                 "tolerations": [{"key": resource, "operator": "Exists", "effect": "NoSchedule"}],
                 "containers": [{"name": "workload", "image": image, "imagePullPolicy": pull_policy,
-                                "command": ["amdgpu-validator"], "args": args, "env": PLUGIN_POD_ENV,
+                                "command": [command], "args": args, "env": PLUGIN_POD_ENV,
                                 "resources": {"limits": {res: str(count)}, "requests": {res: str(count)}}}],
             },
         }
@@ -726,7 +729,8 @@ def abort_start_gates(env: NodeEnv) -> list[str]:
 
 def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURCE_NAME,
                  pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
-                 wait_toolkit: bool = False, with_driver: bool = False, partition_strategy: str = "single") -> dict:
+                 wait_toolkit: bool = False, with_driver: bool = False, partition_strategy: str = "single",
+                 pod_check: str = "hsa") -> dict:
     """Workload and plugin validation concurrently (each skipped if already done).
 
     Only the driver gates the workload: its processes run in this privileged
@@ -796,7 +800,8 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
                 wait_ready(env, "workload", timeout, stop)
             if read_ready(env, "plugin") is None:
                 results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop,
-                                                    kubelet=kubelet, partition_strategy=partition_strategy)
+                                                    kubelet=kubelet, partition_strategy=partition_strategy,
+                                                    pod_check=pod_check)
         except Exception as e:  # noqa: BLE001
             errors.append(f"plugin: {e}")
         finally:

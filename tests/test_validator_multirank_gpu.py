@@ -153,3 +153,15 @@ def test_all_devices_validates_every_gpu_the_pod_holds(tmp_path):
     # peers-only steps are refused with it
     p = subprocess.run([VALIDATOR, "--all-devices", "--steps", "hip,rccl"], capture_output=True, text=True, timeout=30)
     assert p.returncode == 2 and "--all-devices" in p.stderr
+
+
+def test_gpu_check_runs_a_kernel_per_visible_gpu():
+    """The plugin pod's check (amdgpu-gpu-check): HSA runtime only, one
+    host-verified kernel per visible GPU, report in the validator's shape."""
+    check = str(native.binary("amdgpu-gpu-check"))
+    p = subprocess.run([check, "--timeout", "20"], capture_output=True, text=True, timeout=60)
+    rep = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0 and rep["ok"] and rep["devices"] >= 1, rep
+    adds = [s for s in rep["steps"] if s["name"] == "vecadd"]
+    assert len(adds) == rep["devices"] and all(s["mismatches"] == 0 and s["elems"] == 65536 for s in adds)
+    assert all(s["agent"].startswith("gfx950") for s in rep["steps"] if s["name"] == "hsa")
