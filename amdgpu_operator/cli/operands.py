@@ -353,6 +353,7 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                 if stop.is_set():
                     return 0
                 raise
+        t_gate = time.perf_counter()
         from ..deviceplugin.server import DevicePluginManager, PluginConfig
 
         from ..deviceplugin import config as DC
@@ -401,8 +402,12 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             lists = set(f.deviceListStrategy) | ({"cdi-cri"} if a.cdi else set())
             return bool(lists & {"cdi-annotations", "cdi-cri", "volume-mounts"}) or not f.passDeviceSpecs
 
+        t_imp = time.perf_counter()
         mgr = DevicePluginManager(cfg, health_factory=health)
+        t_enum = time.perf_counter()
         mgr.start(register=not gated)
+        log.info("device plugin prepared: imports %.3f s, enumeration %.3f s, serving %.3f s",
+                 t_imp - t_gate, t_enum - t_imp, time.perf_counter() - t_enum)
         if gated:
             steps = [x for x in cenv[GATE_ENV].split(",") if x]
             if not needs_toolkit(dcfg) and "toolkit" in steps:
