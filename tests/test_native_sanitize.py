@@ -25,7 +25,7 @@ def asan_bins():
                            timeout=600)
     if p.returncode != 0:
         pytest.skip(f"sanitizer toolchain unavailable: {p.stderr[-500:]}")
-    return {n: str(native.artefact(n + ".asan")) for n in ("amdgpu-oci-hook", "amdgpu-probe")}
+    return {n: str(native.artefact(n + ".asan")) for n in ("amdgpu-oci-hook", "amdgpu-probe", "amdgpu-nfd")}
 
 
 def _run(argv, input_=None):
@@ -99,3 +99,37 @@ def test_topology_library_under_asan_real_fixture(asan_bins, tmp_path):
     assert p.returncode == 0, p.stderr[-3000:]
     rep = json.loads(p.stdout)
     assert rep["gpus"][0]["arch"] == "gfx950" and rep["gpus"][0]["cu"] == 256
+
+
+def test_nfd_worker_under_asan(asan_bins, tmp_path):
+    """The native NFD worker's sysfs scan, kubeconfig parsing, HTTP exchange
+    and merge patch under ASan/UBSan, against the fake API server over HTTP."""
+    from amdgpu_operator.kube import resources as R
+    from amdgpu_operator.kube.fakeapi import FakeApiServer
+    from amdgpu_operator.kube.httpapi import HttpApiServer
+
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 8, "CPX")
+    p = _run([asan_bins["amdgpu-nfd"], "--print", "--host-root", root])
+    assert p.returncode == 0, p.stderr[-2000:]
+    api = FakeApiServer()
+    api.create(R.new("v1", "Node", "n1", labels={"feature.node.kubernetes.io/pci-0300_10de.present": "true"}))
+    http = HttpApiServer(api).start()
+    try:
+        kc = tmp_path / "kc.json"
+        kc.write_text(json.dumps({"current-context": "c", "clusters": [{"name": "c", "cluster": {"server": http.url}}],
+                                  "users": [{"name": "u", "user": {"token": "t"}}],
+                                  "contexts": [{"name": "c", "context": {"cluster": "c", "user": "u"}}]}))
+        env = dict(os.environ, KUBECONFIG=str(kc), NODE_NAME="n1", HOST_ROOT=root,
+                   ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=99",
+                   UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=98")
+        env.pop("KUBERNETES_SERVICE_HOST", None)
+        for _ in range(2):  # a write, then a no-op pass
+            p = subprocess.run([asan_bins["amdgpu-nfd"], "--oneshot"], capture_output=True, text=True, timeout=120,
+                               env=env)
+            assert p.returncode == 0, p.stderr[-2000:]
+        labels = api.get("v1", "Node", "n1")["metadata"]["labels"]
+        assert labels["feature.node.kubernetes.io/pci-1002.present"] == "true"
+        assert "feature.node.kubernetes.io/pci-0300_10de.present" not in labels
+    finally:
+        http.stop()
