@@ -113,12 +113,22 @@ def _health_server(port: int, metrics=None):
 def main(argv: list[str] | None = None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     if argv and argv[0] in OPERAND_CMDS:
+        import os
+        import time
+
+        trace = os.environ.get("AMDGPU_STARTUP_TRACE")  # "<file>": wall time of each start-up phase
+
+        def mark(what):
+            if trace:
+                with open(trace, "a") as f:
+                    f.write(f"{what} {time.time():.4f}\n")
+
+        mark("main")
         from ..kube.client import RestClient
         from ..nodeenv import NodeEnv
         from .operands import run_operand
 
-        import os
-
+        mark("imports")
         logs.setup()
         try:
             client = RestClient.from_incluster()
@@ -127,11 +137,13 @@ def main(argv: list[str] | None = None) -> int:
             # cluster's operand processes), else node-local operands (driver,
             # toolkit) work without the API
             client = RestClient.from_kubeconfig() if os.environ.get("KUBECONFIG") else None
+        mark("client")
         env = NodeEnv.from_environ(client)
         if os.environ.get("AMDGPU_SIM_NODE") == "1":
             from ..testing.simnode import adopt_sim_node_env
 
             adopt_sim_node_env(env)
+        mark("env")
         # the kubelet stops a container with SIGTERM: operands then run their
         # shutdown (toolkit cleanup, vfio unbind, plugin socket removal)
         return run_operand(env, argv, _stop_on_signals(), ready=_ready_signal(), container_env=dict(os.environ))

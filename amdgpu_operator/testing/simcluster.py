@@ -684,7 +684,7 @@ class SimCluster:
             "CDI_SPEC_DIR": env.cdi_dir, "CONTAINERD_CONFIG": env.containerd_config,
             "CRIO_CONFIG_DIR": env.crio_config_dir, "DOCKER_CONFIG": env.docker_config, "INSTALL_DIR": env.install_dir,
             "OPERATOR_NAMESPACE": env.namespace, "VALIDATION_POLL_S": str(env.poll_s), "KUBECONFIG": self._kubeconfig,
-            "AMDGPU_READY_FILE": ready_file, "AMDGPU_SIM_NODE": "1",
+            "AMDGPU_READY_FILE": ready_file, "AMDGPU_SIM_NODE": "1", "AMDGPU_STARTUP_TRACE": ready_file + ".trace",
             "PYTHONPATH": os.pathsep.join([root] + [x for x in os.environ.get("PYTHONPATH", "").split(os.pathsep) if x])})
         if "kmod" in env.extra:
             penv["AMDGPU_SIM_KMOD"] = "1"
@@ -712,6 +712,8 @@ class SimCluster:
         rec = {"pod": run.name, "container": c["name"], "init": init, "args": cmd[1:3]}
         t0 = time.perf_counter()
         rec["spawn"] = t0
+        rec["spawn_wall"] = time.time()
+        rec["trace_file"] = ready_file + ".trace"
         if os.path.basename(cmd[0]) == "amdgpu-nfd":  # the native worker (native/nfd)
             from .. import native
 
@@ -730,7 +732,11 @@ class SimCluster:
                 return None
 
         def watch_ready():
-            if wait_for_file(ready_file, 600.0, run.stop, 0.002):
+            # inotify wakes this at the rename that publishes the file; the
+            # period only bounds how late a stop is noticed (the harness
+            # shares the GIL with the API server and the fake kubelet: no
+            # tight polling here)
+            if wait_for_file(ready_file, 600.0, run.stop, 0.05):
                 rec["ready_s"] = round(time.perf_counter() - t0, 4)
                 if started_s() is not None:
                     rec["started_s"] = started_s()
@@ -738,18 +744,30 @@ class SimCluster:
 
         if not init:
             threading.Thread(target=watch_ready, daemon=True, name=f"ready-{run.name}-{c['name']}").start()
-        while p.poll() is None:
-            if run.stop.wait(0.005):
+        exited = threading.Event()
+
+        def stop_on_delete():  # the kubelet's SIGTERM (then SIGKILL) when the pod goes
+            while not exited.is_set():
+                if run.stop.wait(0.25):
+                    break
+            if exited.is_set():
+                return
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                return
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
                 try:
-                    os.killpg(p.pid, signal.SIGTERM)
+                    os.killpg(p.pid, signal.SIGKILL)
                 except ProcessLookupError:
                     pass
-                try:
-                    p.wait(timeout=30)
-                except subprocess.TimeoutExpired:
-                    os.killpg(p.pid, signal.SIGKILL)
-                    p.wait()
-                break
+
+        killer = threading.Thread(target=stop_on_delete, daemon=True, name=f"stop-{run.name}-{c['name']}")
+        killer.start()
+        p.wait()  # blocks without waking the interpreter
+        exited.set()
         rec["exit_s"] = round(time.perf_counter() - t0, 4)
         rec["rc"] = p.returncode
         if "started_s" not in rec and started_s() is not None:

@@ -98,6 +98,12 @@ def operand_breakdown(stats: list[dict], t0: float) -> dict:
         for k in ("started_s", "ready_s", "exit_s"):
             if k in r and not (k == "exit_s" and not r.get("init")):
                 e[k] = r[k]
+        # AMDGPU_STARTUP_TRACE: interpreter up (main), imports, API client, node env - s after spawn
+        try:
+            with open(r.get("trace_file", "")) as f:
+                e["startup_s"] = {k: round(float(v) - r["spawn_wall"], 4) for k, v in (ln.split() for ln in f)}
+        except (OSError, ValueError, KeyError):
+            pass
         out.setdefault(key, e)
     return out
 
