@@ -446,7 +446,12 @@ class ClusterPolicyReconciler:
             except queue.Empty:
                 if time.monotonic() - last < resync_s:
                     continue
-            time.sleep(debounce_s)
+            # leading edge: the first event after a quiet spell (a new
+            # ClusterPolicy, a node NFD just labelled) is handled at once; an
+            # event close behind a pass - usually the echo of that pass's own
+            # writes - waits out the debounce so a burst costs one pass
+            if time.monotonic() - last < debounce_s:
+                time.sleep(debounce_s)
             while True:  # coalesce bursts
                 try:
                     events.get_nowait()

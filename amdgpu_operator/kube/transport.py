@@ -1,33 +1,168 @@
-"""HTTP(S) transport of :class:`~.client.RestClient` on the standard library.
+"""HTTP(S) transport of :class:`~.client.RestClient`: HTTP/1.1 on sockets.
 
 Every operand container talks to the API server, and every one of them pays
-its client's import at start-up, inside the node's time-to-Ready: ``requests``
-(with urllib3, idna, charset detection, certifi) costs ~0.15 s of import per
-process on this image, ``http.client`` + ``ssl`` a tenth of that, and the
-operand images need one Python package less.  The surface is the small part
-of a ``requests.Session`` the client uses: ``verify`` / ``cert`` / ``auth`` /
-``headers``, ``request()`` and a streaming ``get()`` with ``iter_lines()``.
+its client's import at start-up, inside the node's time-to-Ready.
+``requests`` (urllib3, idna, charset detection, certifi) cost ~0.15 s of
+import per process on this image; ``http.client`` still ~0.03 s, most of it
+the ``email`` package it parses headers with (bench ``startup_s``: the
+"client" phase).  This module speaks the small part of HTTP/1.1 the API
+server needs on a socket of its own - request line and headers out;
+status, headers and a body framed by Content-Length, chunked transfer
+encoding or connection close back - and loads ``ssl`` only for https.  The
+surface is the part of a ``requests.Session`` the client uses: ``verify`` /
+``cert`` / ``auth`` / ``headers``, ``request()`` and a streaming ``get()``
+with ``iter_lines()``.
 
-Connections are kept alive per thread and per endpoint (``http.client`` is not
-thread-safe); a kept-alive connection the server has since closed is
-detected before reuse, and a request that finds it closed anyway is sent
-once more on a fresh connection (nothing was processed on a dead socket).
-Connection-level failures raise :class:`ConnectionError` (an ``OSError``, as
-``requests.ConnectionError`` is), which the callers' retry logic expects.
+Connections are kept alive per thread and per endpoint; a kept-alive
+connection the server has since closed is detected before reuse, and a
+request that finds it closed anyway is sent once more on a fresh connection
+(nothing was processed on a dead socket).  Connection-level failures raise
+:class:`ConnectionError` (an ``OSError``, as ``requests.ConnectionError``
+is), which the callers' retry logic expects.
 """
 
 from __future__ import annotations
 
-import http.client
 import json
 import select
 import socket
-import ssl
 import threading
 from urllib.parse import urlsplit
 
-_DEAD_CONN = (http.client.RemoteDisconnected, ConnectionResetError, BrokenPipeError, http.client.BadStatusLine,
-              http.client.CannotSendRequest, http.client.ResponseNotReady)
+
+class _Dead(Exception):
+    """The peer closed the connection before a status line arrived."""
+
+
+class _Conn:
+    """One HTTP/1.1 connection (plain or TLS) with a buffered reader."""
+
+    def __init__(self, host: str, port: int, timeout, ssl_context=None):
+        self.host, self.port = host, port
+        self.sock = None
+        self._rfile = None
+        self._timeout = timeout
+        self._ctx = ssl_context
+
+    def connect(self) -> None:
+        sock = socket.create_connection((self.host, self.port), timeout=self._timeout)
+        sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        if self._ctx is not None:
+            sock = self._ctx.wrap_socket(sock, server_hostname=self.host)
+        self.sock = sock
+        self._rfile = sock.makefile("rb")
+
+    def settimeout(self, timeout) -> None:
+        self._timeout = timeout
+        if self.sock is not None:
+            self.sock.settimeout(timeout)
+
+    def close(self) -> None:
+        for x in (self._rfile, self.sock):
+            if x is not None:
+                try:
+                    x.close()
+                except OSError:
+                    pass
+        self.sock = self._rfile = None
+
+    def send(self, method: str, path: str, headers: dict, body: bytes | None) -> None:
+        if self.sock is None:
+            self.connect()
+        host = self.host if ":" not in self.host else f"[{self.host}]"
+        lines = [f"{method} {path} HTTP/1.1", f"Host: {host}:{self.port}"]
+        lines += [f"{k}: {v}" for k, v in headers.items() if k.lower() not in ("host", "content-length")]
+        if body is not None or method in ("POST", "PUT", "PATCH"):
+            lines.append(f"Content-Length: {len(body or b'')}")
+        self.sock.sendall(("\r\n".join(lines) + "\r\n\r\n").encode("latin-1") + (body or b""))
+
+    def read_head(self) -> tuple[int, list[tuple[str, str]], bool]:
+        """Status, headers and whether the server closes after this response."""
+        line = self._rfile.readline(65537)
+        if not line:
+            raise _Dead("connection closed")
+        parts = line.decode("latin-1").split(None, 2)
+        if len(parts) < 2 or not parts[0].startswith("HTTP/"):
+            raise ConnectionError(f"bad status line {line[:80]!r}")
+        status, version = int(parts[1]), parts[0]
+        headers = []
+        while True:
+            h = self._rfile.readline(65537)
+            if h in (b"\r\n", b"\n", b""):
+                break
+            k, _, v = h.decode("latin-1").partition(":")
+            headers.append((k.strip(), v.strip()))
+        conn_hdr = next((v.lower() for k, v in headers if k.lower() == "connection"), "")
+        closes = conn_hdr == "close" or (version == "HTTP/1.0" and conn_hdr != "keep-alive")
+        return status, headers, closes
+
+
+class _Body:
+    """A response body framed by Content-Length, chunked encoding or close."""
+
+    def __init__(self, rfile, headers: dict, method: str, status: int):
+        self._r = rfile
+        te = headers.get("transfer-encoding", "").lower()
+        self._chunked = "chunked" in te
+        cl = headers.get("content-length")
+        self._left = None if self._chunked or cl is None else int(cl)
+        if method == "HEAD" or status in (204, 304) or 100 <= status < 200:
+            self._left = 0
+        self._chunk_left = 0
+        self._done = self._left == 0
+
+    def _next_chunk(self) -> bool:
+        line = self._r.readline(65537)
+        if not line:
+            raise ConnectionError("connection closed inside a chunked body")
+        size = int(line.split(b";", 1)[0].strip() or b"0", 16)
+        if size == 0:  # trailer section up to the blank line
+            while self._r.readline(65537) not in (b"\r\n", b"\n", b""):
+                pass
+            self._done = True
+            return False
+        self._chunk_left = size
+        return True
+
+    def read(self) -> bytes:
+        if self._done:
+            return b""
+        if self._chunked:
+            out = []
+            while self._next_chunk():
+                out.append(self._r.read(self._chunk_left))
+                self._r.readline(3)  # CRLF after the chunk
+            return b"".join(out)
+        data = self._r.read() if self._left is None else self._r.read(self._left)
+        if self._left is not None and len(data) < self._left:
+            raise ConnectionError("connection closed inside the body")
+        self._done = True
+        return data
+
+    def readline(self) -> bytes:
+        """One line of the body (b"" at its end); lines may span chunks."""
+        if self._done:
+            return b""
+        if not self._chunked:
+            line = self._r.readline() if self._left is None else self._r.readline(self._left)
+            if self._left is not None:
+                self._left -= len(line)
+                self._done = self._left <= 0
+            elif not line:
+                self._done = True
+            return line
+        buf = b""
+        while True:
+            if self._chunk_left == 0:
+                if buf.endswith(b"\n") or not self._next_chunk():
+                    return buf
+            piece = self._r.readline(self._chunk_left)
+            self._chunk_left -= len(piece)
+            if self._chunk_left == 0:
+                self._r.readline(3)  # CRLF after the chunk
+            buf += piece
+            if buf.endswith(b"\n"):
+                return buf
 
 
 class Headers(dict):
@@ -47,17 +182,18 @@ class Headers(dict):
 
 
 class Response:
-    def __init__(self, resp: http.client.HTTPResponse, conn=None, body: bytes | None = None):
-        self.status_code = resp.status
-        self.headers = Headers(resp.getheaders())
-        self._resp = resp
+    def __init__(self, status: int, headers: Headers, reader: _Body | None = None, conn=None,
+                 body: bytes | None = None):
+        self.status_code = status
+        self.headers = headers
+        self._reader = reader
         self._conn = conn  # streaming: the connection this response owns
         self._body = body
 
     @property
     def content(self) -> bytes:
         if self._body is None:
-            self._body = self._resp.read()
+            self._body = self._reader.read() if self._reader is not None else b""
         return self._body
 
     @property
@@ -70,7 +206,7 @@ class Response:
     def iter_lines(self, chunk_size=None):
         """Lines of a streamed body as they arrive (each watch event is one)."""
         while True:
-            line = self._resp.readline()
+            line = self._reader.readline()
             if not line:
                 return
             yield line.rstrip(b"\r\n")
@@ -101,11 +237,13 @@ class Session:
         self.auth = None         # callable(PreparedRequest) -> PreparedRequest
         self.headers: dict[str, str] = {}
         self._local = threading.local()
-        self._ssl: ssl.SSLContext | None = None
+        self._ssl = None
         self._ssl_key = None
 
     # ------------------------------------------------------------ internals
-    def _context(self) -> ssl.SSLContext:
+    def _context(self):
+        import ssl  # https only: a plain-HTTP client never loads it
+
         key = (self.verify, self.cert)
         if self._ssl is None or self._ssl_key != key:
             if self.verify is False:
@@ -117,12 +255,12 @@ class Session:
             self._ssl, self._ssl_key = ctx, key
         return self._ssl
 
-    def _new_conn(self, scheme: str, netloc: str, timeout):
+    def _new_conn(self, scheme: str, netloc: str, timeout) -> _Conn:
         host, _, port = netloc.rpartition(":") if netloc.rsplit(":", 1)[-1].isdigit() else (netloc, "", "")
         host = host.strip("[]")
         if scheme == "https":
-            return http.client.HTTPSConnection(host, int(port or 443), timeout=timeout, context=self._context())
-        return http.client.HTTPConnection(host, int(port or 80), timeout=timeout)
+            return _Conn(host, int(port or 443), timeout, self._context())
+        return _Conn(host, int(port or 80), timeout)
 
     @staticmethod
     def _dropped(conn) -> bool:
@@ -144,9 +282,7 @@ class Session:
             conn.close()
         if conn is None:
             conn = pool[(scheme, netloc)] = self._new_conn(scheme, netloc, timeout)
-        conn.timeout = timeout
-        if conn.sock is not None:
-            conn.sock.settimeout(timeout)
+        conn.settimeout(timeout)
         return conn, conn.sock is not None
 
     def _prepare(self, method: str, url: str, data, headers):
@@ -168,29 +304,34 @@ class Session:
             conn = self._new_conn(scheme, netloc, connect_t)
             try:
                 conn.connect()
-                conn.sock.settimeout(read_t)
-                conn.request(method, path, body=body, headers=hdrs)
-                return Response(conn.getresponse(), conn=conn)
-            except (OSError, http.client.HTTPException) as e:
+                conn.settimeout(read_t)
+                conn.send(method, path, hdrs, body)
+                status, headers, _ = conn.read_head()
+                h = Headers(headers)
+                return Response(status, h, _Body(conn._rfile, h, method, status), conn=conn)
+            except (OSError, ValueError, _Dead) as e:
                 conn.close()
                 raise ConnectionError(f"{method} {url}: {e}") from e
         for attempt in (0, 1):
             conn, reused = self._pooled(scheme, netloc, connect_t)
             try:
-                conn.request(method, path, body=body, headers=hdrs)
-                resp = conn.getresponse()
-                payload = resp.read()
-                if resp.will_close:
+                conn.send(method, path, hdrs, body)
+                status, headers, closes = conn.read_head()
+                h = Headers(headers)
+                payload = _Body(conn._rfile, h, method, status).read()
+                if closes or ("content-length" not in h and "chunked" not in h.get("transfer-encoding", "").lower()):
                     conn.close()
-                return Response(resp, body=payload)
-            except _DEAD_CONN as e:
+                return Response(status, h, body=payload)
+            except (_Dead, ConnectionResetError, BrokenPipeError) as e:
                 conn.close()
                 if reused and attempt == 0:
                     continue  # the server had closed the kept-alive connection: nothing was processed
                 raise ConnectionError(f"{method} {url}: {e}") from e
-            except (OSError, http.client.HTTPException) as e:
+            except (OSError, ValueError) as e:
                 conn.close()
                 if isinstance(e, socket.timeout):
+                    raise
+                if isinstance(e, ConnectionError):
                     raise
                 raise ConnectionError(f"{method} {url}: {e}") from e
         raise ConnectionError(f"{method} {url}: no connection")  # not reached

@@ -187,6 +187,7 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             "workload_process_seconds": [r.get("process_seconds") for r in ranks],
             "plugin_seconds": plug.get("seconds"),
             "plugin_devices": plug.get("devices"),
+            "kubelet_register_handler_s": [round(x, 4) for x in nd.kubelet.register_seconds],
             "gemm_tflops": [s.get("tflops") for s in steps.get("gemm", [])],
             "gemm_counter_gate": [s.get("counter_gate") for s in steps.get("gemm", [])],
             "hbm_gbps": [s.get("gbps") for s in steps.get("hbm", [])],

@@ -24,3 +24,19 @@ def test_operand_modules_do_not_import_the_operator_model():
     p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60)
     assert p.returncode == 0, p.stderr
     assert p.stdout.strip() == "", f"operand start-up imports {p.stdout.strip()}"
+
+
+def test_the_api_client_stays_off_http_client():
+    """The RestClient's transport speaks HTTP/1.1 on sockets: building a
+    client and the critical-path operands' modules load neither
+    ``http.client`` (its ``email`` header parsing was ~0.03 s per process)
+    nor ``ssl`` for a plain-HTTP server."""
+    code = ("import sys, json, os, tempfile\n"
+            "import amdgpu_operator.cli.main, amdgpu_operator.cli.operands, amdgpu_operator.driver.manager\n"
+            "import amdgpu_operator.toolkit.install, amdgpu_operator.validator.validate\n"
+            "from amdgpu_operator.kube.client import RestClient\n"
+            "RestClient('http://127.0.0.1:1')\n"
+            "print(','.join(m for m in ('http.client', 'email.parser', 'ssl') if m in sys.modules))")
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.strip() == ""
