@@ -344,9 +344,9 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
 
             from ..validator import validate as V
 
-            # grpc (~0.1 s of imports) loads while the driver gate is still closed
+            # the plugin's modules (allocator, config, rpc) load while the driver gate is still closed
             threading.Thread(target=importlib.import_module, args=("amdgpu_operator.deviceplugin.server",),
-                             name="preload-grpc", daemon=True).start()
+                             name="preload-plugin", daemon=True).start()
             try:
                 V.wait_ready(env, "driver", GATE_TIMEOUT_S, stop)
             except V.StepFailed:

@@ -1,6 +1,9 @@
 """Kubelet device-plugin API ``v1beta1`` and pod-resources API ``v1``.
 
-Wire-compatible hand declarations (SURVEY.md §7.1 lists the field numbers).
+Wire-compatible hand declarations (SURVEY.md §7.1 lists the field numbers),
+encoded by the operator's own codec (rpc/proto.py); the same schema built
+through google.protobuf (:func:`protobuf_classes`, deviceplugin/protodef.py)
+is the reference the codec is tested against.
 The reference relies on the NVIDIA device plugin speaking this API to turn
 GPUs into the ``nvidia.com/gpu`` extended resource
 (/root/reference/README.md:122,205,211,220); this operator speaks the same API
@@ -9,7 +12,7 @@ for ``amd.com/gpu``.
 
 from __future__ import annotations
 
-from .protodef import build_file
+from ..rpc.proto import build_file
 
 VERSION = "v1beta1"
 DEVICE_PLUGIN_PATH = "/var/lib/kubelet/device-plugins/"
@@ -60,7 +63,7 @@ _SERVICES = {
     ],
 }
 
-pb, FILE_DESCRIPTOR = build_file("v1beta1", "deviceplugin/v1beta1/api.proto", _MESSAGES, _SERVICES)
+pb = build_file("v1beta1", _MESSAGES)
 
 REGISTRATION_SERVICE = "v1beta1.Registration"
 DEVICE_PLUGIN_SERVICE = "v1beta1.DevicePlugin"
@@ -88,10 +91,19 @@ _PR_SERVICES = {
     "PodResourcesLister": [("List", "ListPodResourcesRequest", "ListPodResourcesResponse", False),
                            ("GetAllocatableResources", "AllocatableResourcesRequest", "AllocatableResourcesResponse", False)],
 }
-podres, PODRES_FILE_DESCRIPTOR = build_file("v1", "podresources/v1/api.proto", _PR_MESSAGES, _PR_SERVICES)
+podres = build_file("v1", _PR_MESSAGES)
 POD_RESOURCES_SERVICE = "v1.PodResourcesLister"
 POD_RESOURCES_METHODS = {name: (podres[i], podres[o], s) for name, i, o, s in _PR_SERVICES["PodResourcesLister"]}
 
 
 def method_path(service: str, method: str) -> str:
     return f"/{service}/{method}"
+
+
+def protobuf_classes() -> tuple[dict, dict]:
+    """The same messages as google.protobuf classes (tests: the codec's reference)."""
+    from .protodef import build_file as pb_build
+
+    dp, _ = pb_build("v1beta1", "deviceplugin/v1beta1/api.proto", _MESSAGES, _SERVICES)
+    pr, _ = pb_build("v1", "podresources/v1/api.proto", _PR_MESSAGES, _PR_SERVICES)
+    return dp, pr

@@ -16,8 +16,7 @@ from __future__ import annotations
 
 import os
 
-import grpc
-
+from ..rpc import wire
 from . import api
 
 
@@ -35,7 +34,7 @@ class KubeletDevices:
     def _channel(self):
         if self._call is None:
             req, resp, _ = api.POD_RESOURCES_METHODS["GetAllocatableResources"]
-            self._ch = grpc.insecure_channel("unix:" + self.socket_path)
+            self._ch = wire.Channel(self.socket_path)
             self._call = self._ch.unary_unary(
                 api.method_path(api.POD_RESOURCES_SERVICE, "GetAllocatableResources"),
                 request_serializer=req.SerializeToString, response_deserializer=resp.FromString)
@@ -51,7 +50,7 @@ class KubeletDevices:
             call = self._channel()
             req = api.POD_RESOURCES_METHODS["GetAllocatableResources"][0]
             out = call(req(), timeout=timeout)
-        except grpc.RpcError:
+        except wire.RpcError:
             self.close()
             return None
         devs: dict[str, list[str]] = {}

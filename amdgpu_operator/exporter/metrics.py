@@ -244,14 +244,13 @@ class PodAttribution:
         self.prefix = resource_prefix
 
     def lookup(self) -> dict[str, dict]:
-        import grpc
-
         from ..deviceplugin import api
+        from ..rpc import wire
 
         if not os.path.exists(self.socket_path):
             return {}
         req, resp, _ = api.POD_RESOURCES_METHODS["List"]
-        with grpc.insecure_channel("unix:" + self.socket_path) as ch:
+        with wire.Channel(self.socket_path) as ch:
             call = ch.unary_unary(api.method_path(api.POD_RESOURCES_SERVICE, "List"),
                                   request_serializer=req.SerializeToString, response_deserializer=resp.FromString)
             out = call(req(), timeout=2)

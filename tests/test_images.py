@@ -43,7 +43,9 @@ def test_roles_need_what_they_run():
     assert {"libdrm-amdgpu1", "libnuma1", "libelf1"} <= set(val["apt"])
     assert IM.requirements("amd-gpu-operator")["rocm_libs"] == []
     assert {"pydantic", "pyyaml"} <= set(IM.requirements("amd-gpu-operator")["python"])
-    assert {"grpcio", "protobuf"} <= set(IM.requirements("amd-device-plugin")["python"])
+    # the kubelet gRPC runs on the operator's own HTTP/2 stack (rpc/): no grpcio / protobuf in any operand image
+    for role in ("amd-device-plugin", "amd-operator-validator", "amd-metrics-exporter", "amd-sandbox-device-plugin"):
+        assert not {"grpcio", "protobuf"} & set(IM.requirements(role)["python"]), role
     assert IM.requirements("amd-device-plugin")["rocm_libs"] == ["libamd_smi.so"]
     assert IM.requirements("amd-container-toolkit")["rocm_libs"] == []
 
