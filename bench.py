@@ -87,7 +87,7 @@ def gpu_available() -> bool:
         return False
 
 
-def operand_breakdown(stats: list[dict], t0: float) -> dict:
+def operand_breakdown(stats: list[dict], t0: float, t0_wall: float) -> dict:
     """Per operand container (process mode): when it was spawned (s after
     ClusterPolicy creation), when its main began (interpreter + imports),
     and when it was ready (long-running) or exited (init / run-to-completion)."""
@@ -104,6 +104,20 @@ def operand_breakdown(stats: list[dict], t0: float) -> dict:
                 e["startup_s"] = {k: round(float(v) - r["spawn_wall"], 4) for k, v in (ln.split() for ln in f)}
         except (OSError, ValueError, KeyError):
             pass
+        if r["container"] in ("amd-device-plugin", "amd-operator-validator"):
+            # their JSON log lines, s after ClusterPolicy creation (critical-path operands)
+            lines = []
+            try:
+                with open(os.path.join(os.path.dirname(r["trace_file"]), "log")) as f:
+                    for ln in f:
+                        try:
+                            rec = json.loads(ln)
+                            lines.append([round(rec["ts"] - t0_wall, 3), str(rec.get("msg", ""))[:120]])
+                        except (ValueError, KeyError, TypeError):
+                            continue
+            except (OSError, KeyError):
+                pass
+            e["log"] = lines[:30]
         out.setdefault(key, e)
     return out
 
@@ -173,7 +187,7 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
                 timeline[f"{step}.{k}"] = round(v - t0_wall, 4)
         return {
             "mode": mode,
-            "operands": operand_breakdown(cluster.process_stats, t0) if mode == "process" else None,
+            "operands": operand_breakdown(cluster.process_stats, t0, t0_wall) if mode == "process" else None,
             "time_to_ready_s": ttr,
             "allocatable_visible_s": alloc_visible,
             "allocatable_source": plug.get("allocatable_source"),

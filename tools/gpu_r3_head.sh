@@ -12,6 +12,7 @@ rc=$?; echo "gpu tests rc=$rc"; tail -5 $O/gpu_tests.log
 timeout -k 10 300 python3 -u bench.py --gpus 1 --steps 10 --warmup 2 --detail $O/bench_detail.json > $O/bench.json 2> $O/bench.err
 rc=$?; echo "bench rc=$rc"; cat $O/bench.json
 [ $rc -ne 0 ] && exit $rc
+[ -n "${SKIP_PROF:-}" ] && exit 0
 mkdir -p /tmp/rv1
 cd /tmp
 AMDGPU_VALIDATOR_TEARDOWN=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
