@@ -200,9 +200,9 @@ def _complete(env, stop, ready) -> int:
     from ..validator import validate as V
 
     res = V.complete(env)
+    ready()  # the node is labelled validated: the Event below (two API calls) is not on that path
     steps = ", ".join(f"{k} {v:.2f} s" for k, v in res["steps"].items() if v is not None)
     _node_event(env, "Normal", "GPUValidated", f"GPUs validated ({steps})" if steps else "GPUs validated")
-    ready()
     stop.wait()
     # the validator pod goes (new validator image, uninstall): what it
     # validated is withdrawn, so its successor validates again (the driver

@@ -193,15 +193,15 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
     # unload it from under us (cleanup_on_exit)
     _write_state(env, {"version": cur, "specHash": spec_hash, "installed": installed, "hostManaged": host_managed,
                        "owner": owner_id(cenv), "ts": round(time.time(), 3)})
-    try:
-        env.client.patch("v1", "Node", env.node_name, {"metadata": {"annotations": {
-            LOADED_VERSION_ANN: cur or "host", LOADED_HASH_ANN: spec_hash or None}}})
-    except Exception as e:  # noqa: BLE001 - the ready file below still gates the operands
-        log.warning("could not annotate node %s: %s", env.node_name, e)
     gpus = topology.enumerate_gpus(env.sysfs_root())
     out = {"ok": True, "message": msg, "gpus": len(gpus), "driver_version": cur, "installed": ran_script,
            "host_managed": host_managed, "seconds": time.perf_counter() - t0}
-    write_ready(env, "driver", out)
+    write_ready(env, "driver", out)  # the node's operands wait on this file, not on the annotation below
+    try:  # for the upgrade controller (the loaded version / spec it compares with the policy)
+        env.client.patch("v1", "Node", env.node_name, {"metadata": {"annotations": {
+            LOADED_VERSION_ANN: cur or "host", LOADED_HASH_ANN: spec_hash or None}}})
+    except Exception as e:  # noqa: BLE001 - the upgrade controller re-reads it on its next pass
+        log.warning("could not annotate node %s: %s", env.node_name, e)
     # The module went away since the node was last validated (lost, or
     # unloaded by a driver container's exit): what the validator and the
     # device plugin hold belongs to the old driver instance - their pods

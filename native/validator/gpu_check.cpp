@@ -270,8 +270,10 @@ int main(int argc, char** argv) {
     error = f.msg;
   }
   std::string out = "{\"ok\": " + std::string(ok ? "true" : "false") + ", \"devices\": " + std::to_string(ngpu);
-  char b[64];
-  snprintf(b, sizeof b, ", \"seconds\": %.4f", secs(t0));
+  char b[96];
+  // t_main: CLOCK_MONOTONIC at main (steady_clock), comparable with a parent's time.monotonic()
+  snprintf(b, sizeof b, ", \"seconds\": %.4f, \"t_main\": %.6f", secs(t0),
+           std::chrono::duration<double>(t0.time_since_epoch()).count());
   out += b;
   if (!error.empty()) {
     std::string esc;
