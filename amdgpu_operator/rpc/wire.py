@@ -57,11 +57,14 @@ S_HEADER_TABLE_SIZE, S_ENABLE_PUSH, S_MAX_CONCURRENT_STREAMS, S_INITIAL_WINDOW_S
 DEFAULT_WINDOW = 65535
 OUR_WINDOW = 1 << 24  # what we let a peer send before it hears from us
 MAX_WINDOW = (1 << 31) - 1
-MAX_MESSAGE = 64 << 20
+CLIENT_MAX_MESSAGE = 64 << 20  # a response we accept (pod-resources List of a large node)
+SERVER_MAX_MESSAGE = 4 << 20  # a request we accept (gRPC's default receive limit)
+MAX_HEADER_BLOCK = 256 << 10
+MAX_STREAMS = 128  # concurrent calls per connection (SETTINGS_MAX_CONCURRENT_STREAMS)
 
 # HTTP/2 error codes
-NO_ERROR, PROTOCOL_ERROR, INTERNAL_ERROR, FLOW_CONTROL_ERROR, _, STREAM_CLOSED, FRAME_SIZE_ERROR, _, CANCEL, \
-    COMPRESSION_ERROR = range(10)
+NO_ERROR, PROTOCOL_ERROR, INTERNAL_ERROR, FLOW_CONTROL_ERROR, _, STREAM_CLOSED, FRAME_SIZE_ERROR, REFUSED_STREAM, \
+    CANCEL, COMPRESSION_ERROR = range(10)
 
 
 class StatusCode(enum.Enum):
@@ -143,7 +146,7 @@ def grpc_frame(payload: bytes) -> bytes:
 
 class _Stream:
     __slots__ = ("id", "headers", "trailers", "body", "ended", "reset", "send_window", "recv_consumed", "event",
-                 "callbacks", "status_sent")
+                 "callbacks", "status_sent", "too_big")
 
     def __init__(self, sid: int, send_window: int):
         self.id = sid
@@ -157,6 +160,7 @@ class _Stream:
         self.event = threading.Event()  # anything new for a waiting client call
         self.callbacks: list[Callable[[], None]] = []
         self.status_sent = False
+        self.too_big = False  # the peer sent more than the message limit: the rest is dropped
 
 
 class Connection:
@@ -166,6 +170,7 @@ class Connection:
     def __init__(self, sock: socket.socket, client: bool):
         self.sock = sock
         self.client = client
+        self.max_message = CLIENT_MAX_MESSAGE if client else SERVER_MAX_MESSAGE
         self.wlock = threading.Lock()
         self.flow = threading.Condition()  # send windows
         self.decoder = hpack.Decoder()
@@ -198,7 +203,8 @@ class Connection:
 
     def start(self) -> None:
         settings = struct.pack(">HI", S_ENABLE_PUSH, 0) + struct.pack(">HI", S_INITIAL_WINDOW_SIZE, OUR_WINDOW) + \
-            struct.pack(">HI", S_MAX_FRAME_SIZE, 1 << 20)
+            struct.pack(">HI", S_MAX_FRAME_SIZE, 1 << 20) + struct.pack(">HI", S_MAX_CONCURRENT_STREAMS, MAX_STREAMS) + \
+            struct.pack(">HI", S_MAX_HEADER_LIST_SIZE, MAX_HEADER_BLOCK)
         out = (PREFACE if self.client else b"") + self.frame(SETTINGS, 0, 0, settings) + \
             self.frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", OUR_WINDOW - DEFAULT_WINDOW))
         self._send(out)
@@ -353,6 +359,8 @@ class Connection:
                 if self._hdr_block is None or self._hdr_block[0] != sid:
                     raise ConnectionClosed("unexpected CONTINUATION")
                 self._hdr_block[2].extend(payload)
+            if len(self._hdr_block[2]) > MAX_HEADER_BLOCK:
+                raise ConnectionClosed(f"header block above {MAX_HEADER_BLOCK} bytes")
             if flags & END_HEADERS:
                 s, f0, block = self._hdr_block
                 self._hdr_block = None
@@ -364,6 +372,11 @@ class Connection:
                 if st is None:
                     if self.client:
                         return  # a stream we no longer track
+                    if s % 2 == 0:
+                        raise ConnectionClosed(f"client stream id {s} is even")
+                    if len(self.streams) >= MAX_STREAMS:
+                        self.send_rst(s, REFUSED_STREAM)
+                        return
                     st = self.streams[s] = _Stream(s, self.peer_initial_window)
                 on_headers(st, headers, bool(f0 & END_STREAM))
                 if f0 & END_STREAM:
@@ -376,10 +389,11 @@ class Connection:
             self._credit(st, len(payload))
             if st is None:
                 return
-            st.body += data
-            if len(st.body) > MAX_MESSAGE + 5:
-                self.send_rst(sid, FLOW_CONTROL_ERROR)
-                st.reset = FLOW_CONTROL_ERROR
+            if not st.too_big:
+                st.body += data
+                if len(st.body) > self.max_message + 5:
+                    st.too_big = True  # answered RESOURCE_EXHAUSTED once the stream ends
+                    st.body = bytearray()
             if flags & END_STREAM:
                 st.ended = True
                 on_end(st)
@@ -529,6 +543,8 @@ class Server:
             while not self._stopped.is_set():
                 ftype, flags, sid, payload = conn.read_frame()
                 conn.handle_frame(ftype, flags, sid, payload, self._on_headers, lambda st: self._on_end(conn, st))
+                if conn.goaway and not conn.streams:  # the client is done with this connection
+                    break
         except (ConnectionClosed, OSError, struct.error):
             pass
         finally:
@@ -581,6 +597,9 @@ class Server:
         tmo = _parse_timeout(hdrs["grpc-timeout"]) if "grpc-timeout" in hdrs else None
         deadline = None if tmo is None else time.monotonic() + tmo
         ctx = ServicerContext(conn, st, deadline)
+        if st.too_big:
+            self._finish(conn, st, StatusCode.RESOURCE_EXHAUSTED, f"request above {conn.max_message} bytes")
+            return
         try:
             msgs = split_messages(bytes(st.body))
             if len(msgs) != 1:
@@ -797,6 +816,8 @@ class Channel:
             code = StatusCode.UNKNOWN
         if code is not StatusCode.OK:
             raise RpcError(code, _pct_decode(trailers.get("grpc-message", "")))
+        if st.too_big:
+            raise RpcError(StatusCode.RESOURCE_EXHAUSTED, f"response above {conn.max_message} bytes")
         msgs = split_messages(bytes(st.body))
         if len(msgs) != 1:
             raise RpcError(StatusCode.INTERNAL, f"expected one response message, got {len(msgs)}")

@@ -444,3 +444,56 @@ def test_our_client_and_server_together(our_server):
         assert call(r, timeout=5).container_responses[0].envs["ID_7"] == "7" * 1000
         r.container_requests[0].devices_ids.append("x" * 1_000_000)  # 1 MB request, 3 MB response
         assert len(call(r, timeout=10).container_responses[0].envs) == 2
+
+
+def test_server_limits(our_server):
+    """A request above 4 MiB is refused with RESOURCE_EXHAUSTED (gRPC's default
+    receive limit); an oversized header block or an even client stream id
+    ends the connection."""
+    import socket
+    import struct
+
+    path, _ = our_server
+    with grpc.insecure_channel("unix:" + path, options=[("grpc.max_send_message_length", 64 << 20)]) as ch:
+        big = api.pb["AllocateRequest"]()
+        big.container_requests.add(devices_ids=["y" * (5 << 20)])
+        with pytest.raises(grpc.RpcError) as e:
+            _grpcio_call(ch, "Allocate")(big, timeout=10)
+        assert e.value.code() == grpc.StatusCode.RESOURCE_EXHAUSTED
+
+    def raw(frames: bytes) -> bytes:
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.settimeout(5)
+        s.connect(path)
+        got = b""
+        try:
+            s.sendall(wire.PREFACE + wire.Connection.frame(wire.SETTINGS, 0, 0) + frames)
+            while True:
+                chunk = s.recv(65536)
+                if not chunk:
+                    break
+                got += chunk
+        except (ConnectionResetError, BrokenPipeError):  # closed with our frames still unread: also an end
+            got += b"\x00\x00\x00\x07\x00\x00\x00\x00\x00"
+        finally:
+            s.close()
+        return got
+
+    def goaway(got: bytes) -> bool:
+        pos = 0
+        while pos + 9 <= len(got):
+            n = int.from_bytes(got[pos:pos + 3], "big")
+            if got[pos + 3] == wire.GOAWAY:
+                return True
+            pos += 9 + n
+        return False
+
+    hdr = hpack.encode([(":method", "POST"), (":path", "/x"), ("x-pad", "p" * 60000)])
+    flood = wire.Connection.frame(wire.HEADERS, 0, 1, hdr) + b"".join(
+        wire.Connection.frame(wire.CONTINUATION, 0, 1, hdr) for _ in range(5))
+    assert goaway(raw(flood))  # closed once the block passed 256 KiB
+    assert goaway(raw(wire.Connection.frame(wire.HEADERS, wire.END_HEADERS, 2, hpack.encode([(":path", "/x")]))))
+    # a ping is answered with its payload
+    got = raw(wire.Connection.frame(wire.PING, 0, 0, b"12345678") + wire.Connection.frame(wire.GOAWAY, 0, 0,
+                                                                                          struct.pack(">II", 0, 0)))
+    assert b"12345678" in got
