@@ -449,9 +449,12 @@ class ClusterPolicyReconciler:
             # leading edge: the first event after a quiet spell (a new
             # ClusterPolicy, a node NFD just labelled) is handled at once; an
             # event close behind a pass - usually the echo of that pass's own
-            # writes - waits out the debounce so a burst costs one pass
-            if time.monotonic() - last < debounce_s:
-                time.sleep(debounce_s)
+            # writes - waits out the rest of the debounce window so a burst
+            # costs one pass (the rest only: an operand that turns Ready just
+            # after a pass, e.g. the validator, is seen at most debounce_s later)
+            wait = debounce_s - (time.monotonic() - last)
+            if wait > 0:
+                time.sleep(wait)
             while True:  # coalesce bursts
                 try:
                     events.get_nowait()
