@@ -286,5 +286,7 @@ int main(int argc, char** argv) {
   puts(out.c_str());
   fflush(stdout);
   // the report is the result: the runtime's teardown is left to the exit
+  // (AMDGPU_GPU_CHECK_SHUTDOWN=1: hsa_shut_down first - tools/pod_exit_probe.py A/B)
+  if (const char* e = getenv("AMDGPU_GPU_CHECK_SHUTDOWN"); e && e[0] == '1') hsa_shut_down();
   _exit(ok ? 0 : 1);
 }

@@ -32,13 +32,13 @@ WORKLOAD = [os.path.join(NATIVE, "amdgpu-validator"), "--steps", "hip,vecadd,gem
 ENV = {**os.environ, "HSA_ENABLE_SDMA": "0"}
 
 
-def once(with_workload: bool) -> dict:
+def once(with_workload: bool, env: dict | None = None) -> dict:
     wl = None
     if with_workload:
         wl = subprocess.Popen(WORKLOAD, env={**ENV, "AMDGPU_REPORT_EARLY": "1"}, stdout=subprocess.PIPE,
                               stderr=subprocess.DEVNULL)
     t0 = time.monotonic()
-    p = subprocess.Popen(CHECK, env=ENV, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+    p = subprocess.Popen(CHECK, env={**ENV, **(env or {})}, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
     line = p.stdout.readline()
     t_rep = time.monotonic()
     rest = p.stdout.read()
@@ -59,11 +59,13 @@ def once(with_workload: bool) -> dict:
 def main() -> int:
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     once(False)  # page-in
-    runs = {"idle": [], "with_workload": []}
+    runs = {"idle": [], "with_workload": [], "idle_hsa_shut_down": []}
     for _ in range(rounds):
         runs["idle"].append(once(False))
         time.sleep(0.3)  # let the previous processes' teardown finish
         runs["with_workload"].append(once(True))
+        time.sleep(0.3)
+        runs["idle_hsa_shut_down"].append(once(False, {"AMDGPU_GPU_CHECK_SHUTDOWN": "1"}))
         time.sleep(0.3)
     keys = ("main_lag_s", "report_s", "exit_after_report_s", "wall_s", "process_s")
     out = {arm: {"median": {k: round(statistics.median(r[k] for r in v), 4) for k in keys},
