@@ -53,6 +53,8 @@ class FakeKubelet:
         self.assignments: dict[tuple[str, str, str], tuple[str, list[str]]] = {}  # (ns,pod,ctr) -> (res, ids)
         self.register_calls = 0
         self.register_seconds: list[float] = []  # handler time per Register call
+        self.register_walls: list[float] = []  # wall time each Register call arrived
+        self.first_list_walls: dict[str, float] = {}  # resource -> wall time of its first ListAndWatch answer
         self._lock = threading.Lock()
         self._alloc_lock = threading.Lock()
         self._server: grpc.Server | None = None
@@ -62,6 +64,7 @@ class FakeKubelet:
     # ----------------------------------------------------------- Registration
     def _register(self, request, context):
         t0 = time.perf_counter()
+        self.register_walls.append(time.time())
         if request.version != api.VERSION:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"unsupported version {request.version}")
         ep = os.path.join(self.dir, request.endpoint)
@@ -91,6 +94,7 @@ class FakeKubelet:
                                           request_serializer=req.SerializeToString, response_deserializer=resp.FromString)
         try:
             for msg in stream(req(), wait_for_ready=True):
+                self.first_list_walls.setdefault(res.name, time.time())
                 with res.cv:
                     res.devices = {d.ID: d.health for d in msg.devices}
                     res.numa = {d.ID: [n.ID for n in d.topology.nodes] for d in msg.devices}

@@ -738,6 +738,11 @@ class SimCluster:
             # tight polling here)
             if wait_for_file(ready_file, 600.0, run.stop, 0.05):
                 rec["ready_s"] = round(time.perf_counter() - t0, 4)
+                try:  # when the operand wrote it (wall clock), next to when the kubelet saw it
+                    with open(ready_file) as f:
+                        rec["ready_written_s"] = round(float(f.read()) - rec["spawn_wall"], 4)
+                except (OSError, ValueError):
+                    pass
                 if started_s() is not None:
                     rec["started_s"] = started_s()
                 run.set_ready(c["name"])

@@ -95,7 +95,7 @@ def operand_breakdown(stats: list[dict], t0: float, t0_wall: float) -> dict:
     for r in stats:
         key = f"{r['pod'].rsplit('-', 1)[0]}/{r['container']}"
         e = {"spawn_at_s": round(r["spawn"] - t0, 4)}
-        for k in ("started_s", "ready_s", "exit_s"):
+        for k in ("started_s", "ready_written_s", "ready_s", "exit_s"):
             if k in r and not (k == "exit_s" and not r.get("init")):
                 e[k] = r[k]
         # AMDGPU_STARTUP_TRACE: interpreter up (main), imports, API client, node env - s after spawn
@@ -202,6 +202,9 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             "plugin_seconds": plug.get("seconds"),
             "plugin_devices": plug.get("devices"),
             "kubelet_register_handler_s": [round(x, 4) for x in nd.kubelet.register_seconds],
+            # s after ClusterPolicy creation: the plugin's Register arrived / its first device list arrived
+            "kubelet_register_at_s": [round(x - t0_wall, 4) for x in nd.kubelet.register_walls],
+            "kubelet_first_list_at_s": {r: round(x - t0_wall, 4) for r, x in nd.kubelet.first_list_walls.items()},
             "gemm_tflops": [s.get("tflops") for s in steps.get("gemm", [])],
             "gemm_counter_gate": [s.get("counter_gate") for s in steps.get("gemm", [])],
             "hbm_gbps": [s.get("gbps") for s in steps.get("hbm", [])],
