@@ -154,6 +154,8 @@ def main(argv: list[str] | None = None) -> int:
     _common(op)
     op.add_argument("--health-port", type=int, default=8081)
     op.add_argument("--resync", type=float, default=30.0)
+    op.add_argument("--debounce", type=float, default=0.02,
+                    help="an event within this long after a pass waits out the rest of it (bursts cost one pass)")
     op.add_argument("--leader-elect", action="store_true",
                     help="run the controller only while holding the Lease (replicas > 1: warm standbys)")
     op.add_argument("--leader-election-id", default="amd-gpu-operator-leader")
@@ -212,8 +214,16 @@ def main(argv: list[str] | None = None) -> int:
         # a rollout or pod delete (SIGTERM) ends the reconcile loop and, with
         # leader election, releases the Lease so the standby takes over at once
         stop = _stop_on_signals()
+        signal_ready = _ready_signal()  # AMDGPU_READY_FILE: after the first pass (informers live)
+        passes = [0]
+
+        def on_result(_res):
+            passes[0] += 1
+            if passes[0] == 1:
+                signal_ready()
+
         if not args.leader_elect:
-            rec.run(stop, resync_s=args.resync)
+            rec.run(stop, resync_s=args.resync, debounce_s=args.debounce, on_result=on_result)
             return 0
         import os
         import socket
@@ -224,7 +234,8 @@ def main(argv: list[str] | None = None) -> int:
         elector = LeaderElector(client, args.leader_election_id, args.namespace, identity,
                                 lease_s=args.lease_seconds, renew_deadline_s=args.lease_seconds * 2 / 3,
                                 retry_period_s=args.lease_seconds / 7.5)
-        lost = elector.run(stop, lambda ended: rec.run(ended, resync_s=args.resync))
+        lost = elector.run(stop, lambda ended: rec.run(ended, resync_s=args.resync, debounce_s=args.debounce,
+                                                      on_result=on_result))
         # leadership lost: exit so the Deployment restarts this replica as a standby
         return 1 if lost else 0
     if args.cmd == "cleanup-crd":

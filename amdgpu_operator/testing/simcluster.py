@@ -277,6 +277,7 @@ class SimCluster:
         self._threads: list[threading.Thread] = []
         self._lock = threading.RLock()
         self.reconciler: ClusterPolicyReconciler | None = None
+        self._operator_proc = None  # process_containers: the operator as its own process (its Deployment's pod)
         # bring-up trace: (perf_counter, what, detail) - pods created/deleted,
         # containers started/finished (bench.py --detail prints it per step)
         self.events: list[tuple[float, str, str]] = []
@@ -374,7 +375,44 @@ class SimCluster:
         for node in self.nodes.values():
             self._spawn(lambda n=node: self._kubelet_loop(n), f"sim-kubelet-{node.spec.name}")
             self._spawn(lambda n=node: self._node_status_loop(n), f"sim-nodestatus-{node.spec.name}")
+        if self.process_containers:
+            self._start_operator_process()
         return self
+
+    def _start_operator_process(self, timeout: float = 120.0) -> None:
+        """``process_containers``: the operator runs as its own process, as
+        the chart's operator Deployment does, started (CRD installed, first
+        pass done) before the ClusterPolicy appears - its own start-up is not
+        part of a bring-up, as with the in-process reconciler, and its
+        reconcile passes no longer share this process's interpreter lock with
+        the simulated API server and kubelets."""
+        import subprocess
+        import sys
+
+        from ..utils.fswait import wait_for_file
+
+        try:
+            self.install_crd()
+        except Exception:  # noqa: BLE001 - already installed
+            pass
+        d = os.path.join(self.workdir, "operator")
+        os.makedirs(d, exist_ok=True)
+        ready = os.path.join(d, "ready")
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        penv = dict(os.environ)
+        penv.update({"AMDGPU_READY_FILE": ready, "PYTHONPATH": os.pathsep.join(
+            [root] + [x for x in os.environ.get("PYTHONPATH", "").split(os.pathsep) if x])})
+        penv.pop("KUBERNETES_SERVICE_HOST", None)
+        argv = [sys.executable, "-m", "amdgpu_operator", "operator", "--kubeconfig", self._kubeconfig,
+                "--namespace", self.namespace, "--resync", str(self.operator_resync_s),
+                "--debounce", str(self.operator_debounce_s), "--health-port", "0"]
+        with open(os.path.join(d, "log"), "w") as log_f:
+            self._operator_proc = subprocess.Popen(argv, env=penv, stdout=log_f, stderr=subprocess.STDOUT,
+                                                   start_new_session=True)
+        if not wait_for_file(ready, timeout, self.stop_event, 0.05) or self._operator_proc.poll() is not None:
+            with open(os.path.join(d, "log")) as f:
+                tail = f.read()[-2000:]
+            raise RuntimeError(f"operator process did not come up: {tail}")
 
     def _spawn(self, fn, name: str) -> None:
         th = threading.Thread(target=fn, daemon=True, name=name)
@@ -396,7 +434,9 @@ class SimCluster:
         self.start_reconciler()
         return cp
 
-    def start_reconciler(self) -> ClusterPolicyReconciler:
+    def start_reconciler(self) -> ClusterPolicyReconciler | None:
+        if self._operator_proc is not None:
+            return None  # the operator process (process_containers) reconciles
         if self.reconciler is None:
             self.reconciler = ClusterPolicyReconciler(self.agent_client, self.namespace)
             self._spawn(lambda: self.reconciler.run(self.stop_event, resync_s=self.operator_resync_s,
@@ -406,6 +446,20 @@ class SimCluster:
 
     def stop(self) -> None:
         self.stop_event.set()
+        if self._operator_proc is not None:  # SIGTERM, as the Deployment's pod gets it
+            import signal
+            import subprocess
+
+            try:
+                os.killpg(self._operator_proc.pid, signal.SIGTERM)
+                self._operator_proc.wait(timeout=10)
+            except (ProcessLookupError, subprocess.TimeoutExpired):
+                try:
+                    os.killpg(self._operator_proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                self._operator_proc.wait()
+            self._operator_proc = None
         for node in self.nodes.values():
             for run in list(node.pods.values()):
                 run.stop.set()
