@@ -172,8 +172,11 @@ def _decode_str(buf: bytes, pos: int) -> tuple[str, int]:
 class Decoder:
     """One per connection direction: header blocks are decoded in the order they arrive."""
 
-    def __init__(self, max_table_size: int = 4096):
+    def __init__(self, max_table_size: int = 4096, max_list_size: int = 256 << 10):
         self.max_allowed = max_table_size  # our SETTINGS_HEADER_TABLE_SIZE
+        # decoded size bound (RFC 7541 entry sizes): a small block of indexed
+        # references to large table entries must not expand without limit
+        self.max_list_size = max_list_size
         self.max_size = max_table_size
         self.table: list[tuple[str, str]] = []  # newest first
         self.size = 0
@@ -207,28 +210,34 @@ class Decoder:
         out = []
         pos = 0
         n = len(block)
+        total = 0
         while pos < n:
             b = block[pos]
-            if b & 0x80:  # indexed header field
-                idx, pos = decode_int(block, pos, 7)
-                out.append(self._get(idx))
-            elif b & 0xC0 == 0x40:  # literal with incremental indexing
-                idx, pos = decode_int(block, pos, 6)
-                name, pos = (self._get(idx)[0], pos) if idx else _decode_str(block, pos)
-                value, pos = _decode_str(block, pos)
-                self._add(name, value)
-                out.append((name, value))
-            elif b & 0xE0 == 0x20:  # dynamic table size update
+            if b & 0xE0 == 0x20:  # dynamic table size update
                 size, pos = decode_int(block, pos, 5)
                 if size > self.max_allowed:
                     raise HPACKError(f"table size update {size} above {self.max_allowed}")
                 self.max_size = size
                 self._evict()
+                continue
+            if b & 0x80:  # indexed header field
+                idx, pos = decode_int(block, pos, 7)
+                field = self._get(idx)
+            elif b & 0xC0 == 0x40:  # literal with incremental indexing
+                idx, pos = decode_int(block, pos, 6)
+                name, pos = (self._get(idx)[0], pos) if idx else _decode_str(block, pos)
+                value, pos = _decode_str(block, pos)
+                self._add(name, value)
+                field = (name, value)
             else:  # literal without indexing (0000) / never indexed (0001)
                 idx, pos = decode_int(block, pos, 4)
                 name, pos = (self._get(idx)[0], pos) if idx else _decode_str(block, pos)
                 value, pos = _decode_str(block, pos)
-                out.append((name, value))
+                field = (name, value)
+            total += len(field[0]) + len(field[1]) + 32
+            if total > self.max_list_size:
+                raise HPACKError(f"header list above {self.max_list_size} bytes")
+            out.append(field)
         return out
 
 

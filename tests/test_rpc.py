@@ -497,3 +497,13 @@ def test_server_limits(our_server):
     got = raw(wire.Connection.frame(wire.PING, 0, 0, b"12345678") + wire.Connection.frame(wire.GOAWAY, 0, 0,
                                                                                           struct.pack(">II", 0, 0)))
     assert b"12345678" in got
+
+
+def test_hpack_decoded_size_is_bounded():
+    d = hpack.Decoder(4096, max_list_size=64 << 10)
+    big = bytearray(b"\x40\x05x-big")  # literal with incremental indexing, new name
+    hpack.encode_int(big, 4000, 7, 0)
+    big += b"v" * 4000
+    assert d.decode(bytes(big)) == [("x-big", "v" * 4000)]  # one 4 KB entry in the dynamic table
+    with pytest.raises(hpack.HPACKError):
+        d.decode(b"\xbe" * 100)  # 100 one-byte references to it: 400 KB decoded
