@@ -122,6 +122,61 @@ def operand_breakdown(stats: list[dict], t0: float, t0_wall: float) -> dict:
     return out
 
 
+def cpu_throttle_stat() -> dict | None:
+    """The job's cgroup CPU throttling counters (v2 ``cpu.stat`` or v1
+    ``cpu/cpu.stat``), to tell a slow bring-up step that ran into the box's
+    CPU quota (every thread of the job frozen until the next period) from
+    one that was slow on its own."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            lines = [ln.strip().split(":", 2) for ln in f if ln.strip()]
+    except OSError:
+        return None
+    cands = []
+    for _, ctrl, path in lines:
+        if ctrl == "":
+            cands.append(f"/sys/fs/cgroup{path}/cpu.stat")
+        elif "cpu" in ctrl.split(","):
+            cands += [f"/sys/fs/cgroup/{ctrl}{path}/cpu.stat", f"/sys/fs/cgroup/cpu{path}/cpu.stat",
+                      f"/sys/fs/cgroup/cpu,cpuacct{path}/cpu.stat"]
+    for c in cands + ["/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat"]:
+        try:
+            with open(c) as f:
+                kv = dict(ln.split() for ln in f if len(ln.split()) == 2)
+        except (OSError, ValueError):
+            continue
+        if "nr_throttled" in kv:
+            ms = int(kv["throttled_usec"]) / 1e3 if "throttled_usec" in kv else int(kv.get("throttled_time", 0)) / 1e6
+            return {"nr_periods": int(kv.get("nr_periods", 0)), "nr_throttled": int(kv["nr_throttled"]),
+                    "throttled_ms": ms}
+    return None
+
+
+class StallMeter:
+    """A thread of the bench process that wakes every 2 ms: its largest lateness
+    is how long the simulated API server and kubelets (threads of this
+    process) could not run - the interpreter lock held elsewhere, or the
+    process not scheduled."""
+
+    def __init__(self):
+        self.max_s = 0.0
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, daemon=True, name="bench-stall-meter")
+        self._th.start()
+
+    def _run(self):
+        period = 0.002
+        while not self._stop.is_set():
+            t = time.perf_counter()
+            time.sleep(period)
+            self.max_s = max(self.max_s, time.perf_counter() - t - period)
+
+    def stop(self) -> float:
+        self._stop.set()
+        self._th.join()
+        return self.max_s
+
+
 def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode: str = "process") -> dict:
     from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, deep_merge, parse_set_flags
     from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
@@ -154,10 +209,14 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
                          operator_resync_s=30.0, operator_debounce_s=0.02,  # cli/main.py defaults
                          process_containers=(mode == "process")).start()
     try:
+        thr0 = cpu_throttle_stat()
+        stall = StallMeter()
         t0 = time.perf_counter()
         t0_wall = time.time()
         cluster.install_operator(values)
         ttr = cluster.wait_ready(args.timeout)  # validator pod Ready: node validated, policy ready
+        thr1 = cpu_throttle_stat()
+        max_stall = stall.stop()
         # the kubelet then publishes amd.com/gpu in Node.status on its own status tick
         cluster.wait_ready(args.timeout, {"mi355x-node-0": n_gpus})
         alloc_visible = time.perf_counter() - t0
@@ -202,6 +261,11 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             "plugin_seconds": plug.get("seconds"),
             "plugin_devices": plug.get("devices"),
             "kubelet_register_handler_s": [round(x, 4) for x in nd.kubelet.register_seconds],
+            "harness_max_stall_ms": round(max_stall * 1000, 1),
+            # the job's cgroup CPU throttling during the timed bring-up (None: no cgroup stats)
+            "cpu_throttled": None if not (thr0 and thr1) else {
+                "periods": thr1["nr_throttled"] - thr0["nr_throttled"],
+                "ms": round(thr1["throttled_ms"] - thr0["throttled_ms"], 2)},
             # s after ClusterPolicy creation: the plugin's Register arrived / its first device list arrived
             "kubelet_register_at_s": [round(x - t0_wall, 4) for x in nd.kubelet.register_walls],
             "kubelet_first_list_at_s": {r: round(x - t0_wall, 4) for r, x in nd.kubelet.first_list_walls.items()},
