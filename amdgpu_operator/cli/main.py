@@ -144,6 +144,9 @@ def main(argv: list[str] | None = None) -> int:
 
             adopt_sim_node_env(env)
         mark("env")
+        import gc
+
+        gc.freeze()  # the start-up heap (modules, config) is never garbage: later collections skip it
         # the kubelet stops a container with SIGTERM: operands then run their
         # shutdown (toolkit cleanup, vfio unbind, plugin socket removal)
         return run_operand(env, argv, _stop_on_signals(), ready=_ready_signal(), container_env=dict(os.environ))
@@ -215,6 +218,12 @@ def main(argv: list[str] | None = None) -> int:
         # leader election, releases the Lease so the standby takes over at once
         stop = _stop_on_signals()
         signal_ready = _ready_signal()  # AMDGPU_READY_FILE: after the first pass (informers live)
+        import gc
+
+        # a long-running controller: the import-time heap (pydantic models,
+        # the CRD schema) stays out of every later collection
+        gc.collect()
+        gc.freeze()
         passes = [0]
 
         def on_result(_res):

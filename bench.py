@@ -152,6 +152,31 @@ def cpu_throttle_stat() -> dict | None:
     return None
 
 
+class GcMeter:
+    """Collections of the bench process's garbage collector during a bring-up
+    (each holds the interpreter lock, so it stalls the simulated cluster)."""
+
+    def __init__(self):
+        import gc
+
+        self.pauses: list[tuple[int, float]] = []
+        self._t = 0.0
+        self._gc = gc
+        gc.callbacks.append(self._cb)
+
+    def _cb(self, phase, info):
+        if phase == "start":
+            self._t = time.perf_counter()
+        else:
+            self.pauses.append((info.get("generation", -1), time.perf_counter() - self._t))
+
+    def stop(self) -> dict:
+        self._gc.callbacks.remove(self._cb)
+        longest = max((p for _, p in self.pauses), default=0.0)
+        return {"collections": len(self.pauses), "gen2": sum(1 for g, _ in self.pauses if g == 2),
+                "max_ms": round(longest * 1000, 1), "total_ms": round(sum(p for _, p in self.pauses) * 1000, 1)}
+
+
 class StallMeter:
     """A thread of the bench process that wakes every 2 ms: its largest lateness
     is how long the simulated API server and kubelets (threads of this
@@ -160,6 +185,7 @@ class StallMeter:
 
     def __init__(self):
         self.max_s = 0.0
+        self.max_cpu_s = 0.0  # this process's CPU time during the longest stall: ~the stall = a thread held the lock
         self._stop = threading.Event()
         self._th = threading.Thread(target=self._run, daemon=True, name="bench-stall-meter")
         self._th.start()
@@ -167,9 +193,11 @@ class StallMeter:
     def _run(self):
         period = 0.002
         while not self._stop.is_set():
-            t = time.perf_counter()
+            t, c = time.perf_counter(), time.process_time()
             time.sleep(period)
-            self.max_s = max(self.max_s, time.perf_counter() - t - period)
+            late = time.perf_counter() - t - period
+            if late > self.max_s:
+                self.max_s, self.max_cpu_s = late, time.process_time() - c
 
     def stop(self) -> float:
         self._stop.set()
@@ -208,15 +236,29 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
                          node_status_s=args.kubelet_status_s or None, termination_s=0.0,
                          operator_resync_s=30.0, operator_debounce_s=0.02,  # cli/main.py defaults
                          process_containers=(mode == "process")).start()
+    import gc
+
     try:
+        # The simulated API server, kubelets and DaemonSet controller are
+        # threads of this process; a collection of its garbage collector stops
+        # them all (measured: up to ~0.1 s, the slowest bring-ups of a run,
+        # harness_gc).  A cluster's control plane does not pause like that,
+        # so the harness collects before the clock starts and not while it
+        # runs.  The operator and the operands are processes of their own and
+        # keep their collectors.
+        gc.collect()
+        gc.disable()
         thr0 = cpu_throttle_stat()
         stall = StallMeter()
+        gcm = GcMeter()
         t0 = time.perf_counter()
         t0_wall = time.time()
         cluster.install_operator(values)
         ttr = cluster.wait_ready(args.timeout)  # validator pod Ready: node validated, policy ready
         thr1 = cpu_throttle_stat()
         max_stall = stall.stop()
+        gc_stats = gcm.stop()
+        gc.enable()
         # the kubelet then publishes amd.com/gpu in Node.status on its own status tick
         cluster.wait_ready(args.timeout, {"mi355x-node-0": n_gpus})
         alloc_visible = time.perf_counter() - t0
@@ -262,6 +304,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             "plugin_devices": plug.get("devices"),
             "kubelet_register_handler_s": [round(x, 4) for x in nd.kubelet.register_seconds],
             "harness_max_stall_ms": round(max_stall * 1000, 1),
+            "harness_max_stall_cpu_ms": round(stall.max_cpu_s * 1000, 1),
+            "harness_gc": gc_stats,
             # the job's cgroup CPU throttling during the timed bring-up (None: no cgroup stats)
             "cpu_throttled": None if not (thr0 and thr1) else {
                 "periods": thr1["nr_throttled"] - thr0["nr_throttled"],
@@ -284,6 +328,7 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
                                 "amd.com/gpu.xgmi.links", "amd.com/gpu.count", "amd.com/gpu.validated")},
         }
     finally:
+        gc.enable()
         cluster.stop()
         shutil.rmtree(d, ignore_errors=True)
 
