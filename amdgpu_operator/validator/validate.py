@@ -487,7 +487,7 @@ def _device_plan(expected: dict, held: dict[str, list[str]]) -> dict | None:
 
 
 def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, kd=None,
-                          shared: set | None = None) -> dict | None:
+                          shared: set | None = None, log_queries: list | None = None) -> dict | None:
     """Wait until the kubelet's device manager holds the ``expected`` devices
     (pod-resources ``GetAllocatableResources``, deviceplugin/podresources.py;
     :func:`_device_plan`).  Returns the pods to run per resource, or None when
@@ -507,7 +507,11 @@ def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, k
     try:
         waits = env.waits()
         while True:
+            tq = time.time()
             held = kd.allocatable()
+            if log_queries is not None and len(log_queries) < 40:  # (wall start, seconds, devices held)
+                log_queries.append((round(tq, 4), round(time.time() - tq, 4),
+                                    sum(len(v) for v in (held or {}).values())))
             if held is None:
                 return None
             plan = _device_plan(expected, held)
@@ -557,7 +561,8 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     expected = {resource: expect} if expect is not None else expected_devices(env, resource, partition_strategy)
     deadline = time.monotonic() + timeout
     shared: set = set()
-    plan = _wait_kubelet_devices(env, expected, deadline, stop, kubelet, shared)
+    queries: list = []
+    plan = _wait_kubelet_devices(env, expected, deadline, stop, kubelet, shared, queries)
     source = "kubelet"
     if plan is None:  # no pod-resources API: wait for the kubelet to publish Node.status.allocatable
         source = "node-status"
@@ -667,6 +672,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                "attempts": attempts,
                "allocatable_wait_s": round(t_alloc, 4),
                "allocatable_source": source, "marks": {k: round(v, 4) for k, v in marks.items()},
+               "kubelet_queries": queries,
                "seconds": time.perf_counter() - t0}
     write_ready(env, "plugin", summary)
     return summary

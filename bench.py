@@ -301,6 +301,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             "workload_seconds": wl.get("seconds"),
             "workload_process_seconds": [r.get("process_seconds") for r in ranks],
             "plugin_seconds": plug.get("seconds"),
+            # the validator's pod-resources queries: (s after ClusterPolicy creation, duration, devices held)
+            "plugin_kubelet_queries": [(round(q[0] - t0_wall, 4), q[1], q[2]) for q in plug.get("kubelet_queries", [])],
             "plugin_devices": plug.get("devices"),
             "kubelet_register_handler_s": [round(x, 4) for x in nd.kubelet.register_seconds],
             "harness_max_stall_ms": round(max_stall * 1000, 1),
