@@ -28,6 +28,44 @@ IN_CLOEXEC = 0o2000000
 
 _libc = None
 
+# Closing an inotify instance waits for an SRCU grace period in the kernel
+# (fsnotify group teardown): 15-40 ms, measured here and on the MI355X box.
+# Every wait below ends with a close, so a waiter that found its file would
+# sit that long before acting on it (the validator saw the kubelet's devices
+# ~40 ms after its query returned them).  Closes are therefore handed to one
+# background thread per process; os.close releases the interpreter lock.
+_closer_lock = threading.Lock()
+_closer_q = None
+
+
+def _closer(q) -> None:
+    while True:
+        fd = q.get()
+        try:
+            os.close(fd)
+        except OSError:
+            pass
+
+
+def _close_later(fd: int) -> None:
+    global _closer_q
+    with _closer_lock:
+        if _closer_q is None:
+            import queue
+
+            _closer_q = queue.SimpleQueue()
+            threading.Thread(target=_closer, args=(_closer_q,), daemon=True, name="inotify-closer").start()
+        _closer_q.put(fd)
+
+
+def _reset_closer_in_child() -> None:  # a forked child has no closer thread: it starts its own
+    global _closer_q, _closer_lock
+    _closer_q = None
+    _closer_lock = threading.Lock()
+
+
+os.register_at_fork(after_in_child=_reset_closer_in_child)
+
 
 def _lib():
     global _libc
@@ -77,7 +115,7 @@ class DirWatch:
 
     def close(self) -> None:
         if self.fd >= 0:
-            os.close(self.fd)
+            _close_later(self.fd)  # not on the caller's time (see _close_later)
             self.fd = -1
 
 

@@ -68,3 +68,29 @@ def test_dir_watch_sees_create(tmp_path):
         assert w.wait(2.0)
     finally:
         w.close()
+
+
+def test_close_does_not_wait_for_the_kernel(tmp_path):
+    """Closing an inotify instance waits for an SRCU grace period (15-40 ms);
+    DirWatch.close hands it to a background thread, and the fd is closed."""
+    import os
+    import time
+
+    from amdgpu_operator.utils.fswait import DirWatch
+
+    fds, t = [], []
+    for _ in range(5):
+        w = DirWatch(str(tmp_path))
+        assert w.active
+        fds.append(w.fd)
+        t0 = time.perf_counter()
+        w.close()
+        t.append(time.perf_counter() - t0)
+        assert w.fd == -1
+    assert max(t) < 0.01
+    deadline = time.monotonic() + 5
+    while time.monotonic() < deadline and any(os.path.exists(f"/proc/self/fd/{fd}") and
+                                               "inotify" in os.readlink(f"/proc/self/fd/{fd}") for fd in fds):
+        time.sleep(0.05)
+    assert not any(os.path.exists(f"/proc/self/fd/{fd}") and "inotify" in os.readlink(f"/proc/self/fd/{fd}")
+                   for fd in fds)
