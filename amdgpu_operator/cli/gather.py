@@ -24,7 +24,7 @@ import os
 import tarfile
 import time
 
-from ..kube.fakeapi import ApiError
+from ..kube.errors import ApiError
 
 
 def _list(client, api_version: str, kind: str, namespace: str | None = None) -> list[dict]:

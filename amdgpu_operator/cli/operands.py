@@ -596,7 +596,7 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
 
 def _get_or_empty(client, kind: str, name: str, namespace: str | None = None) -> dict:
     """A core/v1 object, or {} when it does not exist (yet)."""
-    from ..kube.fakeapi import ApiError
+    from ..kube.errors import ApiError
 
     try:
         return client.get("v1", kind, name, namespace) or {}

@@ -42,7 +42,7 @@ import time
 
 from ..api.clusterpolicy import ClusterPolicySpec
 from ..kube import resources as R
-from ..kube.fakeapi import NotFound
+from ..kube.errors import NotFound
 from ..utils.logs import get_logger
 
 log = get_logger("amdgpu.upgrade")

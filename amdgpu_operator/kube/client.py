@@ -15,10 +15,14 @@ from __future__ import annotations
 import json
 import os
 import threading
+from typing import TYPE_CHECKING
 from urllib.parse import quote, urlencode
 
 from . import resources as R
-from .fakeapi import AlreadyExists, ApiError, Conflict, FakeApiServer, NotFound
+from .errors import AlreadyExists, ApiError, Conflict, NotFound
+
+if TYPE_CHECKING:
+    from .fakeapi import FakeApiServer
 
 __all__ = ["LocalClient", "RestClient", "ApiError", "NotFound", "AlreadyExists", "Conflict", "apply_object", "wait_for"]
 

@@ -14,11 +14,11 @@ effort: an API error is logged and never fails the caller.
 
 from __future__ import annotations
 
+import os
 import threading
 import time
-import uuid
 
-from .fakeapi import NotFound
+from .errors import NotFound
 from ..utils.logs import get_logger
 
 log = get_logger("amdgpu.events")
@@ -54,7 +54,7 @@ class EventRecorder:
                     self.client.patch("v1", "Event", ev_name, {"count": count + 1, "lastTimestamp": _ts(now)}, ev_ns)
                     self._seen[key] = (ev_ns, ev_name, count + 1, first)
                     return
-                name = f"{md.get('name', 'object')}.{uuid.uuid4().hex[:16]}"
+                name = f"{md.get('name', 'object')}.{os.urandom(8).hex()}"
                 ev = {"apiVersion": "v1", "kind": "Event",
                       "metadata": {"name": name, "namespace": ns},
                       "involvedObject": {"apiVersion": obj.get("apiVersion"), "kind": obj.get("kind"),

@@ -27,29 +27,7 @@ import time
 import uuid
 
 from . import resources as R
-
-
-class ApiError(Exception):
-    def __init__(self, code: int, reason: str, message: str = ""):
-        super().__init__(f"{code} {reason}: {message}")
-        self.code = code
-        self.reason = reason
-        self.message = message
-
-
-class NotFound(ApiError):
-    def __init__(self, msg=""):
-        super().__init__(404, "NotFound", msg)
-
-
-class AlreadyExists(ApiError):
-    def __init__(self, msg=""):
-        super().__init__(409, "AlreadyExists", msg)
-
-
-class Conflict(ApiError):
-    def __init__(self, msg=""):
-        super().__init__(409, "Conflict", msg)
+from .errors import AlreadyExists, ApiError, Conflict, NotFound  # noqa: F401 - re-exported (kube.fakeapi.NotFound)
 
 
 def _now() -> str:

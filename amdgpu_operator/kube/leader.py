@@ -30,7 +30,7 @@ import threading
 import time
 from datetime import datetime, timezone
 
-from .fakeapi import AlreadyExists, Conflict, NotFound
+from .errors import AlreadyExists, Conflict, NotFound
 from ..utils.logs import get_logger
 
 log = get_logger("amdgpu.leader")

@@ -30,7 +30,6 @@ import os
 import shutil
 import threading
 import time
-import uuid
 from concurrent.futures import ThreadPoolExecutor
 
 from .. import RESOURCE_NAME, native
@@ -254,7 +253,7 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     if world > 8:
         # partitioned GPUs: the xGMI one-shot kernel takes <= 8 peers; RCCL still spans all
         args = _drop_step(args, "xgmi")
-    run_id = uuid.uuid4().hex[:12]
+    run_id = os.urandom(6).hex()
     rdv = os.path.join(env.validations_dir, "rendezvous", run_id)
     os.makedirs(rdv, exist_ok=True)
     # N7: the counter gate is a rocprofiler-sdk tool library loaded only into
@@ -634,7 +633,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     attempts, backoff, pods_run = 0, 0.05, 0
     while todo:
         attempts += 1
-        run_id = uuid.uuid4().hex[:8]
+        run_id = os.urandom(4).hex()
         names = {}
         for i, (res, count) in enumerate(todo):
             name = f"amd-validator-workload-{run_id}-{i}"
@@ -759,7 +758,7 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
     prespawn = with_driver and prespawn_safe(env, sdk_gate)
     if with_driver:
         os.makedirs(env.validations_dir, exist_ok=True)
-        gate = os.path.join(env.validations_dir, f"{START_GATE_PREFIX}{uuid.uuid4().hex[:12]}")
+        gate = os.path.join(env.validations_dir, f"{START_GATE_PREFIX}{os.urandom(6).hex()}")
         open(gate, "w").close()  # empty = no verdict yet (driver/manager.py may abort it)
 
     def driver():
