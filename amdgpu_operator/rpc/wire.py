@@ -226,7 +226,13 @@ class Connection:
                 break
         self._send(bytes(frames))
 
-    def send_data(self, st: _Stream, data: bytes, end_stream: bool = False, deadline: float | None = None) -> None:
+    def send_data(self, st: _Stream, data: bytes, end_stream: bool = False, deadline: float | None = None,
+                  pump: Callable[[float], None] | None = None) -> None:
+        """DATA within the peer's windows.  A server's reader thread applies
+        the peer's WINDOW_UPDATEs meanwhile; a client, whose calling thread is
+        its only reader, passes ``pump(timeout)``, which reads and handles
+        frames (a request larger than the server's window would otherwise wait
+        for updates nobody reads)."""
         view = memoryview(data)
         while True:
             with self.flow:
@@ -239,9 +245,18 @@ class Connection:
                     left = None if deadline is None else deadline - time.monotonic()
                     if left is not None and left <= 0:
                         raise TimeoutError("flow-control window stayed closed")
+                    if pump is not None:
+                        break
                     self.flow.wait(0.5 if left is None else min(0.5, left))
-                self.conn_send_window -= n
-                st.send_window -= n
+                if n <= 0 and view:  # client: read the peer's frames, then look again
+                    n = -1
+                else:
+                    self.conn_send_window -= n
+                    st.send_window -= n
+            if n < 0:
+                left = None if deadline is None else deadline - time.monotonic()
+                pump(0.5 if left is None else max(0.001, min(0.5, left)))
+                continue
             chunk, view = view[:n], view[n:]
             last = not view
             self._send(self.frame(DATA, END_STREAM if (end_stream and last) else 0, st.id, bytes(chunk)))
@@ -751,21 +766,42 @@ class Channel:
         if deadline is not None:
             headers.append(("grpc-timeout", _timeout_header(max(0.001, deadline - time.monotonic()))))
         headers += list(metadata or [])
+        def on_headers(s: _Stream, hdrs: list, end: bool) -> None:
+            if s.headers is None:
+                s.headers = hdrs
+            else:
+                s.trailers = hdrs
+            if end and s.trailers is None:  # Trailers-Only
+                s.trailers = hdrs
+
+        def pump(timeout: float) -> None:  # the server's frames while our request waits for its window
+            conn.sock.settimeout(timeout)
+            try:
+                ftype, flags, fsid, fp = conn.read_frame()
+            except socket.timeout:
+                return
+            except OSError as e:
+                raise ConnectionClosed(str(e)) from None
+            finally:
+                try:
+                    conn.sock.settimeout(None)
+                except OSError:
+                    pass
+            conn.handle_frame(ftype, flags, fsid, fp, on_headers, lambda s: None)
+
         try:
             try:
                 conn.send_headers(sid, headers)
-                conn.send_data(st, grpc_frame(payload), end_stream=True, deadline=deadline)
+                conn.send_data(st, grpc_frame(payload), end_stream=True, deadline=deadline, pump=pump)
             except ConnectionClosed:
-                raise _Retry() from None
-            got_any = False
-
-            def on_headers(s: _Stream, hdrs: list, end: bool) -> None:
-                if s.headers is None:
-                    s.headers = hdrs
+                if st.ended or st.reset is not None:  # the server answered (e.g. an error) before all of it
+                    pass
                 else:
-                    s.trailers = hdrs
-                if end and s.trailers is None:  # Trailers-Only
-                    s.trailers = hdrs
+                    raise _Retry() from None
+            except TimeoutError:
+                conn.send_rst(sid)
+                raise RpcError(StatusCode.DEADLINE_EXCEEDED, "deadline exceeded (request not sent)") from None
+            got_any = st.headers is not None
 
             while not st.ended and st.reset is None:
                 if deadline is not None:

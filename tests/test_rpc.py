@@ -396,6 +396,14 @@ def test_our_client_against_grpcio_server(grpcio_server):
                                request_serializer=preq.SerializeToString, response_deserializer=presp.FromString)
         out = pcall(preq(), timeout=10)
         assert len(out.devices) == 20000 and out.devices[-1].device_ids[0].startswith("19999")
+        # a request larger than grpcio's 64 KiB windows: our sender reads the
+        # server's WINDOW_UPDATEs itself (the calling thread is the only reader)
+        assert call(req_cls(version=api.VERSION, endpoint="e" * (2 << 20)), timeout=10) == api.pb["Empty"]()
+        with pytest.raises(wire.RpcError) as e:  # above grpcio's 4 MiB receive limit
+            call(req_cls(version=api.VERSION, endpoint="e" * (5 << 20)), timeout=10)
+        assert e.value.code() in (wire.StatusCode.RESOURCE_EXHAUSTED, wire.StatusCode.CANCELLED,
+                                  wire.StatusCode.INTERNAL)
+        assert call(ok, timeout=5) == api.pb["Empty"]()
         # the server restarts: the kept-alive connection is dead, the next call reconnects
         box["srv"].stop(0).wait()
         box["srv"] = start()
