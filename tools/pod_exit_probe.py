@@ -56,7 +56,33 @@ def once(with_workload: bool, env: dict | None = None) -> dict:
     return out
 
 
+KNOBS = {  # --knobs: ROCr settings that might shorten the check's start or its exit
+    "sdma_on": {"HSA_ENABLE_SDMA": "1"},
+    "interrupt_off": {"HSA_ENABLE_INTERRUPT": "0"},
+    "no_scratch_reclaim": {"HSA_NO_SCRATCH_RECLAIM": "1"},
+    "signal_pool_16": {"ROC_SIGNAL_POOL_SIZE": "16"},
+}
+
+
+def knobs(rounds: int) -> int:
+    """Idle GPU, baseline against each ROCr knob, interleaved round by round."""
+    once(False)
+    arms = {"baseline": {}, **KNOBS}
+    runs = {k: [] for k in arms}
+    for _ in range(rounds):
+        for k, env in arms.items():
+            runs[k].append(once(False, env))
+            time.sleep(0.3)
+    keys = ("main_lag_s", "report_s", "exit_after_report_s", "wall_s", "process_s")
+    out = {arm: {"median": {k: round(statistics.median(r[k] for r in v), 4) for k in keys},
+                 "all_ok": all(r["ok"] and r["rc"] == 0 for r in v)} for arm, v in runs.items()}
+    print(json.dumps(out))
+    return 0 if all(v["all_ok"] for v in out.values()) else 1
+
+
 def main() -> int:
+    if len(sys.argv) > 1 and sys.argv[1] == "--knobs":
+        return knobs(int(sys.argv[2]) if len(sys.argv) > 2 else 6)
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     once(False)  # page-in
     runs = {"idle": [], "with_workload": [], "idle_hsa_shut_down": []}
