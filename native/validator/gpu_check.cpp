@@ -16,6 +16,11 @@
 //   fine-grained system memory the GPU was granted, waits (bounded) and checks
 //   every element on the host.
 //
+// The devices are checked concurrently, one thread each: a pod holding all 8
+// GPUs of a node (one pod per resource, validator/validate.py) would
+// otherwise load the code object and create a queue 8 times in a row
+// (~10 ms each on MI355X) on the bring-up's critical path.
+//
 // Output: one JSON line in the validator's report shape ({"ok", "seconds",
 // "steps": [{"name": "hsa" | "vecadd", "device": d, ...}]}); exit 0 when every
 // device passed.  A dispatch that does not complete within --timeout fails
@@ -31,6 +36,7 @@
 #include <fstream>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -264,7 +270,23 @@ int main(int argc, char** argv) {
     const std::string text = ss.str();
     if (!f || text.empty()) throw Fail{"cannot read " + path};
     const std::vector<char> co(text.begin(), text.end());
-    for (int d = 0; d < ngpu && ok; ++d) ok = check_device(d, ag.gpus[d], pool, co, elems, timeout_s, &steps, &error);
+    std::vector<std::vector<std::string>> dev_steps(ngpu);
+    std::vector<std::string> dev_error(ngpu);
+    std::vector<char> dev_ok(ngpu, 0);
+    std::vector<std::thread> threads;
+    threads.reserve(ngpu);
+    for (int d = 0; d < ngpu; ++d)
+      threads.emplace_back([&, d] {
+        dev_ok[d] = check_device(d, ag.gpus[d], pool, co, elems, timeout_s, &dev_steps[d], &dev_error[d]);
+      });
+    for (auto& t : threads) t.join();
+    for (int d = 0; d < ngpu; ++d) {  // report in device order; the first failing device names the error
+      steps.insert(steps.end(), dev_steps[d].begin(), dev_steps[d].end());
+      if (!dev_ok[d] && ok) {
+        ok = false;
+        error = dev_error[d];
+      }
+    }
   } catch (const Fail& f) {
     ok = false;
     error = f.msg;
