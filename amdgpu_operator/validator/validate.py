@@ -135,6 +135,21 @@ def gate_env() -> dict:
             "ROCPROFILER_METRICS_PATH": str(native.artefact("gate-metrics"))}
 
 
+def thp_malloc_env() -> dict:
+    """glibc's malloc on transparent huge pages (``glibc.malloc.hugetlb=1``,
+    glibc >= 2.35; an older glibc ignores the tunable) for the processes that
+    set up an RCCL communicator.  Most of ``ncclCommInitRank`` is the HIP
+    runtime loading RCCL's ~108 MB of gfx950 device code through freshly
+    allocated host buffers, and most of that was page faults (system time):
+    0.35 s -> 0.22 s per communicator on MI355X, process wall 450 -> 320 ms
+    (tools/rccl_thp_probe.sh, profiles/r3_thp).  The kernel-check and
+    plugin-pod processes showed no change and keep the default."""
+    cur = os.environ.get("GLIBC_TUNABLES", "")
+    if "glibc.malloc.hugetlb" in cur:
+        return {}
+    return {"GLIBC_TUNABLES": f"{cur}:glibc.malloc.hugetlb=1" if cur else "glibc.malloc.hugetlb=1"}
+
+
 def _arg_value(args: list[str], flag: str) -> str | None:
     return args[args.index(flag) + 1] if flag in args and args.index(flag) + 1 < len(args) else None
 
@@ -288,9 +303,10 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     if split and "xgmi" in kernel_steps:
         kernel_steps = [s for s in kernel_steps if s != "xgmi"]
         peer_steps = ["hip", "xgmi", "rccl"]
-    jobs = [(r, _with_steps(args, kernel_steps), run_id, counter_env) for r in range(world)]
+    kernel_env = {**counter_env, **(thp_malloc_env() if run_rccl and rccl_shared else {})}
+    jobs = [(r, _with_steps(args, kernel_steps), run_id, kernel_env) for r in range(world)]
     if run_rccl and not rccl_shared:
-        jobs += [(r, _with_steps(_drop_flag(args, "--counter-gate"), peer_steps), run_id + "-rccl", {})
+        jobs += [(r, _with_steps(_drop_flag(args, "--counter-gate"), peer_steps), run_id + "-rccl", thp_malloc_env())
                  for r in range(world)]
 
     def failed(res) -> bool:
