@@ -26,8 +26,6 @@
 
 #include <dirent.h>
 #include <dlfcn.h>
-#include <link.h>
-#include <sys/mman.h>
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -103,37 +101,6 @@ struct Rccl {
     return gpus ? slim : "";
   }
 
-  // Map the library's read-only segments (RCCL's ~108 MB device-code bundle
-  // among them) into the page tables now, in one madvise per segment, instead
-  // of one page fault per 4 KiB when the HIP runtime reads the bundle inside
-  // ncclCommInitRank.  The load runs before the start gate, so this overlaps
-  // the wait for the driver validation.  AMDGPU_RCCL_POPULATE=0 turns it off
-  // (A/B, tools/rccl_thp_probe.sh); a kernel without MADV_POPULATE_READ
-  // (< 5.14) answers EINVAL and nothing changes.
-  static void populate_read_only_segments(void* handle) {
-    if (const char* e = getenv("AMDGPU_RCCL_POPULATE"); e && e[0] == '0') return;
-    struct link_map* lm = nullptr;
-    if (dlinfo(handle, RTLD_DI_LINKMAP, &lm) != 0 || !lm) return;
-    struct Ctx {
-      ElfW(Addr) base;
-    } ctx{lm->l_addr};
-    dl_iterate_phdr(
-        [](struct dl_phdr_info* info, size_t, void* data) -> int {
-          auto* c = static_cast<Ctx*>(data);
-          if (info->dlpi_addr != c->base) return 0;
-          const long page = sysconf(_SC_PAGESIZE);
-          for (int i = 0; i < info->dlpi_phnum; ++i) {
-            const ElfW(Phdr)& ph = info->dlpi_phdr[i];
-            if (ph.p_type != PT_LOAD || (ph.p_flags & PF_W) || ph.p_memsz == 0) continue;
-            const uintptr_t start = (info->dlpi_addr + ph.p_vaddr) & ~(uintptr_t)(page - 1);
-            const uintptr_t end = info->dlpi_addr + ph.p_vaddr + ph.p_memsz;
-            (void)madvise(reinterpret_cast<void*>(start), end - start, 22 /* MADV_POPULATE_READ */);
-          }
-          return 1;
-        },
-        &ctx);
-  }
-
   bool load(const std::string& exe_dir, std::string* err) {
     const std::string want = preferred(exe_dir);
     std::vector<std::string> names;
@@ -151,7 +118,6 @@ struct Rccl {
       *err += std::string("dlopen librccl failed: ") + dlerror();
       return false;
     }
-    populate_read_only_segments(dl);
     GetUniqueId = reinterpret_cast<decltype(GetUniqueId)>(dlsym(dl, "ncclGetUniqueId"));
     CommInitRank = reinterpret_cast<decltype(CommInitRank)>(dlsym(dl, "ncclCommInitRank"));
     AllReduce = reinterpret_cast<decltype(AllReduce)>(dlsym(dl, "ncclAllReduce"));

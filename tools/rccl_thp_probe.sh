@@ -12,12 +12,9 @@ run() {
   local o
   o=$(env "$@" timeout -k 5 60 $V --steps hip,rccl --rccl-elems 1048576 --rendezvous /tmp/thp-rv --run-id $name-$RANDOM 2>&1) || { echo "$name FAILED: $(echo "$o" | tail -2)"; exit 1; }
   local e=$(date +%s%N)
-  echo "$name wall_ms=$(( (e - s) / 1000000 )) $(echo "$o" | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=[x for x in d["steps"] if x["name"]=="rccl"][0]; print({k: r.get(k) for k in ("lib_load_s","comm_init_s","init_wait_s")})')"
+  echo "$name wall_ms=$(( (e - s) / 1000000 )) $(echo "$o" | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=[x for x in d["steps"] if x["name"]=="rccl"][0]; print({k: r.get(k) for k in ("comm_init_s","init_wait_s")})')"
 }
-# arms: huge pages on/off x the library's read-only segments populated at load (default) or not
 for i in 1 2 3 4 5 6; do
-  run base AMDGPU_RCCL_POPULATE=0
-  run hugetlb1 GLIBC_TUNABLES=glibc.malloc.hugetlb=1 AMDGPU_RCCL_POPULATE=0
-  run hugetlb1_populate GLIBC_TUNABLES=glibc.malloc.hugetlb=1
-  run populate X=1
+  run base X=1
+  run hugetlb1 GLIBC_TUNABLES=glibc.malloc.hugetlb=1
 done
