@@ -932,7 +932,7 @@ __device__ __forceinline__ void g8_phase(f32x4 (&acc)[8][4], const bf16x8 (&a)[4
 // or vmcnt(6) for group 1 with LOAD_IN_M.  B0's slot is now last read 3
 // phases before its refill, so only phase 0 (A0, refilled in phase 1) retires
 // its reads before the first barrier.
-template <bool OUT_F32, bool LOAD_IN_M, bool BAL>
+template <bool OUT_F32, bool LOAD_IN_M, bool BAL, int GM = g8::GROUP_M>
 __global__ __launch_bounds__(g8::NTHR, 2) void gemm_bf16_nt_8p_kernel(const __bf16* __restrict__ A,
                                                                      const __bf16* __restrict__ Bt,
                                                                      void* __restrict__ Cv, int M, int N, int K) {
@@ -952,9 +952,9 @@ __global__ __launch_bounds__(g8::NTHR, 2) void gemm_bf16_nt_8p_kernel(const __bf
   const int xcd = bid % kNumXcd;
   const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
   const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
-  const int per_group = GROUP_M * tiles_n;
-  const int first_m = (wgid / per_group) * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int per_group = GM * tiles_n;  // GM tile rows per L2 band (lab variants 10-12 vary it)
+  const int first_m = (wgid / per_group) * GM;
+  const int gsize = min(tiles_m - first_m, GM);
   const int in_group = wgid % per_group;
   const int m0 = (first_m + in_group % gsize) * BM;
   const int n0 = (in_group / gsize) * BN;
@@ -1396,6 +1396,15 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
     AVK_G8(7, true, false)
     AVK_G8(8, false, true)
     AVK_G8(9, true, true)
+#define AVK_G8M(V, GM)                                                                                    \
+    case V:                                                                                              \
+      if (out_f32) gemm_bf16_nt_8p_kernel<true, false, false, GM><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K); \
+      else gemm_bf16_nt_8p_kernel<false, false, false, GM><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K);        \
+      break;
+    AVK_G8M(10, 8)  // the default kernel with 8 / 16 / 2 tile rows per L2 band
+    AVK_G8M(11, 16)
+    AVK_G8M(12, 2)
+#undef AVK_G8M
 #endif
 #undef AVK_G8
     default:
