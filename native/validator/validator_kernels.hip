@@ -833,7 +833,7 @@ constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
 constexpr int HT_BYTES = 128 * BK * 2;    // 16 KiB half-tile: 128 rows x 128 B
 constexpr int BUF_BYTES = 4 * HT_BYTES;   // 64 KiB: A0 A1 B0 B1
 constexpr int LDS_BYTES = 2 * BUF_BYTES;  // 128 KiB
-constexpr int GROUP_M = 8;  // tile rows per L2 band: +2.4 % at 4096^3, +3.6 % at 8192^3 over 4 (profiles/r3_gemm)
+constexpr int GROUP_M = 4;  // tile rows per L2 band (8 / 16 / 2: lab variants 10-12; profiles/r3_gemm)
 constexpr int HA0 = 0, HA1 = 1, HB0 = 2, HB1 = 3;
 }  // namespace g8
 
@@ -1401,9 +1401,10 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
       if (out_f32) gemm_bf16_nt_8p_kernel<true, false, false, GM><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K); \
       else gemm_bf16_nt_8p_kernel<false, false, false, GM><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K);        \
       break;
-    AVK_G8M(10, 4)  // the default kernel with 4 (round 1-3 default) / 16 / 2 tile rows per L2 band
-    AVK_G8M(11, 16)
-    AVK_G8M(12, 2)
+    AVK_G8M(10, 8)  // the default kernel with 8 / 16 / 2 tile rows per L2 band, and with the default 4 (13):
+    AVK_G8M(11, 16)  // 13 is variant 6 built into the lab library, for same-library A/B (the two libraries'
+    AVK_G8M(12, 2)   // copies of one kernel timed 1-4 % apart, profiles/r3_gemm)
+    AVK_G8M(13, 4)
 #undef AVK_G8M
 #endif
 #undef AVK_G8

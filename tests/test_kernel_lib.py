@@ -19,10 +19,10 @@ def _gemm_kernels(path):
 
 def test_shipped_code_object_has_only_the_default_gemm():
     assert K.GEMM_DEFAULT_VARIANT == 6
-    # <OUT_F32 = false / true, LOAD_IN_M = false, BAL = false, GROUP_M = 8>: the AQL gate's kGemmSymbol
+    # <OUT_F32 = false / true, LOAD_IN_M = false, BAL = false, GROUP_M = 4>: the AQL gate's kGemmSymbol
     # (a prefix match, native/prof/aql_gate.cpp) and its f32 twin
-    assert _gemm_kernels(native.artefact("validator_kernels.co")) == ["gemm_bf16_nt_8p_kernelILb0ELb0ELb0ELi8E",
-                                                                      "gemm_bf16_nt_8p_kernelILb1ELb0ELb0ELi8E"]
+    assert _gemm_kernels(native.artefact("validator_kernels.co")) == ["gemm_bf16_nt_8p_kernelILb0ELb0ELb0ELi4E",
+                                                                      "gemm_bf16_nt_8p_kernelILb1ELb0ELb0ELi4E"]
 
 
 def test_lab_variants_are_served_from_the_tools_build():

@@ -1,5 +1,5 @@
 #!/bin/bash
-# 8-phase GEMM: tile rows per L2 band (GROUP_M 8 = shipped since round 3, lab variants 10/11/12 = 4/16/2).
+# 8-phase GEMM: tile rows per L2 band (GROUP_M 4 = shipped, lab variants 10/11/12/13 = 8/16/2/4).
 # Outputs must equal the shipped kernel's bit for bit (same tiles, another order), then the interleaved timing.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${1:-gemm_group}; mkdir -p $O; cd $R

@@ -32,7 +32,8 @@ def time_ms(fn, iters):
 
 GEMM_VARIANTS = {6: "default_8phase", 0: "ring_pingpong", 1: "dbuf", 2: "ring", 3: "w4", 4: "pp_load_in_r", 5: "pp_5slot",
                  7: "8phase_load_in_m", 8: "8phase_bal_load_in_r", 9: "8phase_bal_load_in_m",
-                 10: "8phase_group_m4", 11: "8phase_group_m16", 12: "8phase_group_m2"}
+                 10: "8phase_group_m8", 11: "8phase_group_m16", 12: "8phase_group_m2",
+                 13: "8phase_lab_copy"}
 
 
 def bench_gemm(n, rounds, iters, variants=None):
