@@ -1,7 +1,7 @@
 """Protocol-buffer messages from a compact schema, in plain Python.
 
 The kubelet APIs the operator speaks (device plugin ``v1beta1``, pod
-resources ``v1``; deviceplugin/api.py) are a few flat messages of strings,
+resources ``v1``; deviceplugin/api.py; /root/reference/README.md:122,211,220) are a few flat messages of strings,
 bools, integers, nested messages and one string map.  Encoding them needs no
 descriptor pool: this module builds message classes straight from the
 ``{"Msg": [(field, number, type, label)]}`` schema and writes/reads the

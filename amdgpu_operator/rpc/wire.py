@@ -1,5 +1,8 @@
 """gRPC over HTTP/2 on unix sockets, in plain Python: the kubelet's transport.
 
+The reference's device plugin turns GPUs into an allocatable extended
+resource through this kubelet API (/root/reference/README.md:122,205,211,220).
+
 The device plugin serves ``v1beta1.DevicePlugin`` to the kubelet and calls
 its ``Registration`` service; the validator and the metrics exporter call the
 kubelet's ``v1.PodResourcesLister``.  All of that is unary calls plus one
