@@ -225,6 +225,9 @@ def main() -> int:
     ap.add_argument("--inject-noop", type=int, default=-1, metavar="STEP",
                     help="make step STEP a no-op fault that claims a revalidation (the harness must fail)")
     a = ap.parse_args()
+    if a.processes and not a.real_gpu:
+        # the fake cluster's partition and PCI backends live in this process (env.extra), out of an operand process's reach
+        ap.error("--processes needs --real-gpu")
     lo, _, hi = a.seeds.partition("-")
     ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api, a.real_gpu, a.inject_noop, a.processes)
               for s in range(int(lo), int(hi or lo) + 1)])
