@@ -75,6 +75,8 @@ def parse():
                     help="after the timed steps, this many bring-ups in the other --mode (reported, not timed)")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--detail", default=None, help="write per-step breakdown JSON here")
+    ap.add_argument("--set", action="append", default=[], dest="extra_set",
+                    help="experiments only: extra Helm --set flags on top of the reference's (the headline uses none)")
     return ap.parse_args()
 
 
@@ -211,7 +213,7 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
 
     root = None if fake_gpu else (args.sysfs_root or "/")
     node = NodeSpec("mi355x-node-0", gpus=n_gpus, sysfs_root=root)
-    values = parse_set_flags(REFERENCE_SET_FLAGS)
+    values = parse_set_flags(REFERENCE_SET_FLAGS + list(args.extra_set))
     if args.no_counter_gate:
         values = deep_merge(values, {"validator": {"workload": {"counterGate": False}}})
     if args.rccl_single_gpu:
