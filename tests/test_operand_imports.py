@@ -1,7 +1,7 @@
 """Operand start-up stays light: an operand container is a fresh
 ``python -m amdgpu_operator <operand>`` process on the node's time-to-Ready
 path, so the modules it runs must not pull in the operator's ClusterPolicy
-model (pydantic), requests or YAML (bench --mode process breakdown,
+model (pydantic), requests, YAML, grpcio or protobuf (bench --mode process breakdown,
 tools/operand_start_probe.py)."""
 
 import os
@@ -15,7 +15,11 @@ OPERAND_MODULES = ["amdgpu_operator.cli.main", "amdgpu_operator.cli.operands", "
                    "amdgpu_operator.exporter.metrics", "amdgpu_operator.discovery.labels",
                    "amdgpu_operator.partition.manager", "amdgpu_operator.kube.client", "amdgpu_operator.kube.events",
                    "amdgpu_operator.testing.simnode", "amdgpu_operator.wellknown"]
-HEAVY = ("pydantic", "requests", "yaml", "amdgpu_operator.api.clusterpolicy", "amdgpu_operator.controller.reconciler")
+HEAVY = ("pydantic", "requests", "yaml", "amdgpu_operator.api.clusterpolicy", "amdgpu_operator.controller.reconciler",
+         # the kubelet gRPC runs on amdgpu_operator.rpc (grpcio + protobuf were ~0.1 s of the plugin's start)
+         "grpc", "google.protobuf",
+         # the simulated API server (the client imports kube.errors) and uuid's platform probe
+         "amdgpu_operator.kube.fakeapi", "uuid")
 
 
 def test_operand_modules_do_not_import_the_operator_model():
