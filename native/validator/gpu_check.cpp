@@ -157,12 +157,15 @@ bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std:
           "executable create");
     check(hsa_executable_load_agent_code_object(exe, gpu, reader, nullptr, nullptr), "load code object");
     check(hsa_executable_freeze(exe, nullptr), "executable freeze");
+    const double co_load_s = secs(t0);
     Kernel k;
     check(hsa_executable_iterate_agent_symbols(exe, gpu, find_kernel, &k), "kernel symbols");
     if (!k.object) throw Fail{std::string(kKernel) + " not in the code object for " + agent_name};
     if (k.kernarg_size < 28) throw Fail{"unexpected kernarg layout"};
+    const auto tq = Clock::now();
     check(hsa_queue_create(gpu, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &queue),
           "queue create");
+    const double queue_s = secs(tq);
     check(hsa_signal_create(1, 0, nullptr, &done), "signal create");
     auto* a = static_cast<float*>(alloc(pool, gpu, n * 4));
     auto* b = static_cast<float*>(alloc(pool, gpu, n * 4));
@@ -179,7 +182,9 @@ bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std:
     memcpy(karg + 8, &b, 8);
     memcpy(karg + 16, &c, 8);
     memcpy(karg + 24, &n, 4);
-    steps->push_back(fmt_step("hsa", d, true, secs(t0), std::string("\"agent\": \"") + agent_name + "\""));
+    char tdet[96];
+    snprintf(tdet, sizeof tdet, "\"co_load_s\": %.4f, \"queue_s\": %.4f, ", co_load_s, queue_s);
+    steps->push_back(fmt_step("hsa", d, true, secs(t0), std::string(tdet) + "\"agent\": \"" + agent_name + "\""));
 
     const auto t1 = Clock::now();
     const uint64_t idx = hsa_queue_add_write_index_relaxed(queue, 1);

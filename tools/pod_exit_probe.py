@@ -49,7 +49,9 @@ def once(with_workload: bool, env: dict | None = None) -> dict:
     out = {"rc": rc, "ok": rep.get("ok"), "main_lag_s": round(rep["t_main"] - t0, 4),
            "report_s": round(t_rep - t0, 4), "eof_after_report_s": round(t_eof - t_rep, 4),
            "exit_after_report_s": round(t_exit - t_rep, 4), "wall_s": round(t_exit - t0, 4),
-           "process_s": rep.get("seconds"), "steps": {s["name"]: s.get("seconds") for s in rep.get("steps", [])}}
+           "process_s": rep.get("seconds"), "steps": {s["name"]: s.get("seconds") for s in rep.get("steps", [])},
+           "hsa_detail": next(({k: s.get(k) for k in ("co_load_s", "queue_s")} for s in rep.get("steps", [])
+                               if s.get("name") == "hsa"), None)}
     if wl is not None:
         wl.stdout.read()
         out["workload_rc"] = wl.wait()
