@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -282,7 +283,13 @@ int main(int argc, char** argv) {
     threads.reserve(ngpu);
     for (int d = 0; d < ngpu; ++d)
       threads.emplace_back([&, d] {
-        dev_ok[d] = check_device(d, ag.gpus[d], pool, co, elems, timeout_s, &dev_steps[d], &dev_error[d]);
+        try {  // nothing may leave a thread (std::terminate): an unexpected error fails this device only
+          dev_ok[d] = check_device(d, ag.gpus[d], pool, co, elems, timeout_s, &dev_steps[d], &dev_error[d]);
+        } catch (const std::exception& e) {
+          dev_error[d] = "device " + std::to_string(d) + ": " + e.what();
+        } catch (...) {
+          dev_error[d] = "device " + std::to_string(d) + ": unexpected error";
+        }
       });
     for (auto& t : threads) t.join();
     for (int d = 0; d < ngpu; ++d) {  // report in device order; the first failing device names the error
