@@ -243,14 +243,22 @@ class WorkloadSpec(_M):
     # GEMM (native/include/gate_policy.h): ~0.49 measured at 4096^3
     # (profiles/r2_gate/aql_v2.json), floor at 40 % of it
     minMfmaUtil: float = 0.2
-    # RCCL fp32 all-reduce busBW floor at N >= 2: this many GB/s per peer GPU
-    # (N-1 peers).  A PCIe fallback ring (dead xGMI) delivers ~20-40 GB/s in
-    # total; 15 GB/s per peer is far below any healthy xGMI mesh and still
-    # fails an 8-GPU node routed over PCIe (105 GB/s floor)
-    rcclBusbwPerPeerGbps: float = 15.0
+    # N >= 2 throughput floors from the xGMI link model (validator/validate.py
+    # fabric_floors): a rank's links to its N-1 peers carry 76 GB/s each per
+    # direction on MI355X (KFD io_links), 532 GB/s at N = 8.  RCCL fp32
+    # all-reduce busBW >= this fraction of that sum x B/(B + 16 MiB) at the
+    # validated size B (64 MiB: 0.8) - 85 GB/s at N = 8, 12 GB/s at N = 2; a
+    # PCIe-routed node (no xGMI) gets ~20-60 GB/s in total and fails
+    rcclBusbwLinkFraction: float = 0.2
+    # K4 one-shot all-reduce: the peer reads (N-1 buffers at once, one per
+    # link) >= this fraction of the same sum - 133 GB/s at N = 8
+    xgmiReadLinkFraction: float = 0.25
     # multi-GPU nodes: every pair of GPUs joined by an xGMI link in the KFD
-    # topology and amd-smi reporting the links up, none in error
+    # topology and amd-smi reporting the links up, none in error, each trained
+    # to >= minXgmiLinkFraction of the KFD nominal rate (rate x width: a link
+    # that came back at half its rate or width is "up" and fails here)
     requireXgmiLinks: bool = True
+    minXgmiLinkFraction: float = 0.9
     # N >= 2: a rank not alive within this long is missing (also bounds the
     # RCCL communicator set-up); a collective not done within
     # collectiveTimeoutSeconds aborts the communicator
@@ -264,10 +272,17 @@ class WorkloadSpec(_M):
     # run the RCCL check (own process, world 1) on a single-GPU node too: the
     # multi-GPU critical path, rehearsed where there is no xGMI peer
     rcclSingleGpu: bool = False
-    # RCCL check in its own process per GPU ("separate", default) or inside the
-    # kernel-check process ("shared": one process start + HIP init fewer, the
-    # RCCL code-object load overlaps the kernel steps)
-    rcclProcess: Literal["separate", "shared"] = "separate"
+    # one validator process per physical GPU runs the kernel checks of every
+    # device of the GPU (its partitions, concurrently), the xGMI one-shot and
+    # RCCL ("shared", default); "separate" puts xGMI + RCCL in a second process
+    # per GPU when that stays within maxGpuProcesses (the storm probe measured
+    # one process per GPU faster at N = 5: profiles/r3_storm)
+    rcclProcess: Literal["separate", "shared"] = "shared"
+    # concurrent GPU processes one node's validation may start (workload
+    # processes + plugin-validation pods): a GPU box admits few processes per
+    # user on its devices (16 measured), and each one's HIP start-up stretches
+    # the others'
+    maxGpuProcesses: int = Field(default=16, ge=2)
     # start the validator processes while the driver is still being validated:
     # they load their libraries and wait behind a start gate, so process start
     # is off the time-to-Ready critical path (no GPU call before the gate opens)
@@ -285,6 +300,12 @@ class ValidatorSpec(Operand):
     # its report on MI355X); "hip" - amdgpu-validator hip,vecadd (HIP runtime
     # and context, ~0.1-0.2 s; profiles/r3_pod_check)
     pluginPodCheck: Literal["hsa", "hip"] = "hsa"
+    # plugin-validation pods: one per resource holding all of its devices
+    # ("perResource", default: fewest processes in the start-up storm), or one
+    # 1-device pod per device ("perDevice": N pods x 1 GPU, each its own
+    # GetPreferredAllocation/Allocate/hook, started at most workload.
+    # maxGpuProcesses - workload processes at a time)
+    pluginPods: Literal["perResource", "perDevice"] = "perResource"
     validationsDir: str = "/run/amd/validations"
 
 

@@ -48,6 +48,8 @@ def build_parser() -> argparse.ArgumentParser:
     v.add_argument("--timeout", type=float, default=600.0)
     v.add_argument("--pod-check", default="hsa", choices=["hsa", "hip"],
                    help="plugin: what the validation pod runs on its GPUs (amdgpu-gpu-check / amdgpu-validator)")
+    v.add_argument("--plugin-pods", default="perResource", choices=["perResource", "perDevice"],
+                   help="plugin: one pod per resource holding all its devices, or one 1-device pod per device")
     v.add_argument("--wait-toolkit", action="store_true",
                    help="gpu: plugin validation waits for the toolkit; the workload starts right away")
     v.add_argument("--with-driver", action="store_true",
@@ -175,11 +177,13 @@ def _validate(env, a, extra, stop, ready) -> int:
         if V.read_ready(env, "plugin") is None:
             pod_args = _plugin_pod_args(extra)
             V.validate_plugin(env, a.resource, pod_args=pod_args, timeout=a.timeout, stop=stop,
-                              partition_strategy=a.partition_strategy, pod_check=a.pod_check)
+                              partition_strategy=a.partition_strategy, pod_check=a.pod_check,
+                              per_device=a.plugin_pods == "perDevice")
     elif a.step == "gpu":
         V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
                        wait_toolkit=a.wait_toolkit, with_driver=a.with_driver,
-                       partition_strategy=a.partition_strategy, pod_check=a.pod_check)
+                       partition_strategy=a.partition_strategy, pod_check=a.pod_check,
+                       per_device=a.plugin_pods == "perDevice")
         if a.complete:
             return _complete(env, stop, ready)
     elif a.step == "vfio":
@@ -235,7 +239,7 @@ def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
     i = 0
     while i < len(args):
         a = args[i]
-        if a in ("--resource", "--timeout", "--partition-strategy", "--pod-check"):
+        if a in ("--resource", "--timeout", "--partition-strategy", "--pod-check", "--plugin-pods"):
             known += args[i:i + 2]
             i += 2
             continue

@@ -327,23 +327,26 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     wl_args = ["--gemm", str(w.gemmN), "--gemm-iters", str(w.gemmIters), "--hbm-bytes", str(w.hbmBytes),
                "--rccl-elems", str(w.rcclElems), "--xgmi-elems", str(w.xgmiElems)]
     for flag, val in (("--min-gemm-tflops", w.minGemmTflops), ("--min-hbm-gbps", w.minHbmGbps),
-                      ("--min-mfma-util", w.minMfmaUtil), ("--rccl-busbw-per-peer", w.rcclBusbwPerPeerGbps)):
+                      ("--min-mfma-util", w.minMfmaUtil), ("--rccl-busbw-link-fraction", w.rcclBusbwLinkFraction),
+                      ("--xgmi-read-link-fraction", w.xgmiReadLinkFraction)):
         if val:
             wl_args += [flag, f"{val:g}"]
-    wl_args += ["--peer-timeout", f"{w.peerTimeoutSeconds:g}", "--collective-timeout", f"{w.collectiveTimeoutSeconds:g}"]
+    wl_args += ["--peer-timeout", f"{w.peerTimeoutSeconds:g}", "--collective-timeout", f"{w.collectiveTimeoutSeconds:g}",
+                "--max-gpu-processes", str(w.maxGpuProcesses)]
     if w.requireXgmiLinks:
-        wl_args += ["--require-xgmi-links"]
+        wl_args += ["--require-xgmi-links", "--min-xgmi-link-fraction", f"{w.minXgmiLinkFraction:g}"]
     if w.counterGate:
         wl_args += ["--counter-gate"] + (["--gate-mode", "sdk"] if w.counterGateMode == "sdk" else [])
     if w.rcclSingleGpu:
         wl_args += ["--rccl-single-gpu"]
-    if w.rcclProcess == "shared":
-        wl_args += ["--rccl-shared-process"]
+    if w.rcclProcess == "separate":
+        wl_args += ["--rccl-separate-process"]
     inits = [_wait_init("driver-validation", image, v.imagePullPolicy, "driver")]
     # the plugin pods request what the device plugin advertises (its resource
     # name, and amd.com/gpu-<mode> for partitioned GPUs under "mixed")
     plugin_res = ["--resource", spec.devicePlugin.resourceName,
-                  "--partition-strategy", spec.devicePlugin.partitionStrategy, "--pod-check", v.pluginPodCheck]
+                  "--partition-strategy", spec.devicePlugin.partitionStrategy, "--pod-check", v.pluginPodCheck,
+                  "--plugin-pods", v.pluginPods]
     if v.pluginValidation and spec.devicePlugin.enabled and w.prespawn:
         # one init container validates the driver and, meanwhile, starts the
         # workload processes behind their start gate (validate.py validate_gpu)

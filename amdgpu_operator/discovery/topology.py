@@ -103,6 +103,7 @@ class _Metrics(ctypes.Structure):
         ("hbm_thermal_residency", ctypes.c_uint64),
         ("vram_max_bandwidth_gbps", ctypes.c_uint64),
         ("xgmi_link_speed_gbps", ctypes.c_uint32),
+        ("xgmi_link_width", ctypes.c_uint32),
         ("pcie_link_width", ctypes.c_uint32),
         ("pcie_link_speed_mts", ctypes.c_uint32),
         ("throttle_status", ctypes.c_uint32),
@@ -313,8 +314,8 @@ _METRIC_FIELDS = {
     M_PROCS: ("num_processes",),
     M_GPU_METRICS: ("xgmi_read_bytes", "xgmi_write_bytes", "pcie_bandwidth_gbps", "pcie_replay_count", "pcie_nak_sent",
                     "pcie_nak_rcvd", "prochot_residency", "ppt_residency", "socket_thermal_residency",
-                    "hbm_thermal_residency", "vram_max_bandwidth_gbps", "xgmi_link_speed_gbps", "pcie_link_width",
-                    "pcie_link_speed_mts", "throttle_status"),
+                    "hbm_thermal_residency", "vram_max_bandwidth_gbps", "xgmi_link_speed_gbps", "xgmi_link_width",
+                    "pcie_link_width", "pcie_link_speed_mts", "throttle_status"),
 }
 
 

@@ -258,13 +258,22 @@ def reload_module(env: NodeEnv, cenv: dict, reason: str, timeout: float = 600.0,
     module), and ``driver-ready`` is written again by :func:`install`."""
     kmod = _kmod(env)
     _release_gated_validators(env)
-    clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
+    # withdrawn like a loss, marker included: if the unload or the load fails
+    # half-way, the health monitor (monitor_once) restores driver-ready as soon
+    # as a module is live again - the old one that would not unload, or a later
+    # load - and restarts the validator and device plugin on it; a successful
+    # reload takes the marker in install()
+    _withdraw_validation(env, f"planned reload: {reason}")
     log.info("reloading amdgpu: %s", reason)
-    kmod.unload(env)
-    if kmod.can_install():
-        kmod.install(env, {**cenv, "AMDGPU_FORCE_RELOAD": "true"}, timeout)
-    else:
-        kmod.load(env, timeout)
+    try:
+        kmod.unload(env)
+        if kmod.can_install():
+            kmod.install(env, {**cenv, "AMDGPU_FORCE_RELOAD": "true"}, timeout)
+        else:
+            kmod.load(env, timeout)
+    except Exception:
+        monitor_once(env)  # the module still (or again) live: the node keeps its driver-ready
+        raise
     return install(env, timeout, stop, cenv)
 
 
@@ -499,6 +508,8 @@ def publish_smi(env: NodeEnv, driver_ok: bool, refresh_s: float = 60.0) -> str:
     only when the status line changes."""
     from ..wellknown import DRIVER_SMI_ANN
 
+    from ..utils import smihold
+
     last, at = env.extra.get("_smi_published", ("", 0.0))
     now = time.monotonic()
     if not driver_ok:
@@ -506,7 +517,12 @@ def publish_smi(env: NodeEnv, driver_ok: bool, refresh_s: float = 60.0) -> str:
     elif last.startswith("ok") and now - at < refresh_s:
         return last
     else:
-        status = smi_status(smi_snapshot(env))
+        # a partition change holds the node's amd-smi clients off (utils/smihold.py):
+        # this poll is skipped, not raced against the apply
+        with smihold.client(env.validations_dir) as allowed:
+            if not allowed:
+                return last
+            status = smi_status(smi_snapshot(env))
     if status != last and env.client is not None:
         try:
             env.client.patch("v1", "Node", env.node_name, {"metadata": {"annotations": {DRIVER_SMI_ANN: status}}})

@@ -20,7 +20,10 @@ node, like the MIG manager's:
    metrics exporter (amd-smi), validator - by setting their deploy labels to
    ``paused-for-partition-change`` (their DaemonSets then remove the pods;
    the operator leaves paused labels alone) and wait until those pods are
-   gone and ``/sys/class/kfd/kfd/proc`` is empty;
+   gone and ``/sys/class/kfd/kfd/proc`` is empty; hold off the node agents
+   that stay (the driver container's amd-smi health poll) through
+   ``.smi-hold`` and wait until none is in an amd-smi session
+   (utils/smihold.py);
 4. apply memory then compute partition on each physical GPU; on a memory
    change ask the node's driver container to reload amdgpu
    (``.driver-reload-request``, driver/manager.py) and wait for the fresh
@@ -79,12 +82,26 @@ AMDSMI_STATUS_BUSY = 30
 
 
 class SmiBackend:
-    """Applies partitions through libamd_smi (root on the node)."""
+    """Applies partitions through libamd_smi (root on the node).  The session
+    is opened on use and closed around a driver reload (:meth:`close`): an
+    amd-smi session keeps the GPUs' DRM nodes open, which would keep amdgpu
+    in use and fail every unload a memory-partition change needs."""
 
     def __init__(self):
-        from ..discovery.topology import Smi
+        self._smi = None
 
-        self.smi = Smi()
+    @property
+    def smi(self):
+        if self._smi is None:
+            from ..discovery.topology import Smi
+
+            self._smi = Smi()
+        return self._smi
+
+    def close(self) -> None:
+        if self._smi is not None:
+            self._smi.close()
+            self._smi = None
 
     def current(self, physical_index: int) -> tuple[str, str]:
         return self.smi.partitions(physical_index)
@@ -108,13 +125,16 @@ class SmiBackend:
 class SysfsBackend:
     """A fake node's partitions (tests, the simulated cluster), with the
     hardware's rules: a change is refused while KFD users exist (the fake
-    tree's ``sys/class/kfd/kfd/proc``), a compute change takes effect at once,
-    a memory change only at the next amdgpu load (the fake module,
-    fakesys.SimModule, applies ``.pending-partition``)."""
+    tree's ``sys/class/kfd/kfd/proc``) or an amd-smi client of the node is
+    in a session (its lease in ``validations_dir``, utils/smihold.py), a
+    compute change takes effect at once, a memory change only at the next
+    amdgpu load (the fake module, fakesys.SimModule, applies
+    ``.pending-partition``)."""
 
-    def __init__(self, root: str, rebuild):
+    def __init__(self, root: str, rebuild, validations_dir: str | None = None):
         self.root = root
         self.rebuild = rebuild  # callable(compute, memory) -> None (re-creates the KFD nodes)
+        self.validations_dir = validations_dir
 
     def current(self, physical_index: int) -> tuple[str, str]:
         from ..discovery import topology
@@ -129,6 +149,12 @@ class SysfsBackend:
         users = [p for p in (os.listdir(procs) if os.path.isdir(procs) else []) if p.isdigit()]
         if users:
             raise PartitionBusy(f"GPU {physical_index} busy: KFD users {users[:8]}")
+        if self.validations_dir:
+            from ..utils import smihold
+
+            clients = smihold.live_clients(self.validations_dir)
+            if clients:
+                raise PartitionBusy(f"GPU {physical_index} busy: amd-smi clients {clients[:8]}")
         c, m = self.current(physical_index)
         if m != profile.memory:
             from ..discovery import topology
@@ -248,18 +274,26 @@ def reconcile_node(env: NodeEnv, backend, profiles: dict, default: Profile,
         log.error("partition %s not applied: %s", name, why)
         return {"changed": False, "error": why, "profile": name}
 
+    from ..utils import smihold
+
     env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": {STATE_LABEL: "pending"}}})
     evicted = evict_gpu_pods(env) if evict else []
     if evict and not wait_gpu_pods_gone(env, timeout):
         return fail("GPU pods still on the node")
     memory_change = any(backend.current(p)[1] != prof.memory for p in todo)
     paused = pause_operands(env)
+    # the node agents that stay (amd-driver-health's amd-smi poll) are held off
+    # the devices for the change (utils/smihold.py)
+    smihold.hold(env.validations_dir, f"partition {name}")
     try:
         if not wait_operands_gone(env, paused, timeout):
             return fail(f"paused operands {paused} still running on the node")
         users = kfd_idle(env, timeout)
         if users:
             return fail(f"GPU still open by process(es) {users[:8]}")
+        clients = smihold.wait_clients_gone(env.validations_dir, timeout)
+        if clients:
+            return fail(f"amd-smi clients {clients[:8]} still in a session")
         try:
             for p in todo:
                 backend.apply(p, prof)
@@ -267,6 +301,8 @@ def reconcile_node(env: NodeEnv, backend, profiles: dict, default: Profile,
             return fail(str(e))
         if memory_change:
             clear_ready(env, ("workload", "plugin", "complete"))
+            if hasattr(backend, "close"):
+                backend.close()  # our own amd-smi session would keep amdgpu from unloading
             if not request_driver_reload(env, f"memory partition {prof.memory}", timeout):
                 return fail("the driver container did not reload amdgpu for the memory partition change")
         left = [p for p in todo if backend.current(p) != (prof.compute, prof.memory)]
@@ -279,6 +315,7 @@ def reconcile_node(env: NodeEnv, backend, profiles: dict, default: Profile,
         return {"changed": True, "profile": name, "gpus": todo, "evicted": evicted, "paused": paused,
                 "driver_reloaded": memory_change}
     finally:
+        smihold.release(env.validations_dir)
         # the device plugin comes back on the new devices, a fresh validator validates them
         resume_operands(env, paused)
 

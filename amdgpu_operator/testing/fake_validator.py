@@ -7,6 +7,14 @@ records ``<run>-alive-<r>`` / ``-failed-`` / ``-done-``, the orchestrator's
 bounded failure are exercised for real, and prints the same JSON report shape
 with ``"simulated": true``.
 
+``--expect-devices N`` (a rank validating a GPU's N partitions) reports the
+kernel steps once per device, with ``"device"`` and ``local_devices``, as the
+native binary does.
+
+``AMDGPU_FAKE_GPU_PROC_LOG=<dir>``: every stand-in writes ``<dir>/<pid>.json``
+with its start and end (``time.monotonic``, comparable across processes) and
+its role, so a test can count how many "GPU processes" were alive at once.
+
 Fault injection for the CPU tests: ``AMDGPU_FAKE_VALIDATOR_FAULT`` =
 ``<run-id suffix or *>:<rank>:<kind>`` with kind ``fail`` (report a failure at
 once), ``exit`` (die without a report, after the liveness record) or ``hang``
@@ -19,6 +27,15 @@ import json
 import os
 import sys
 import time
+
+
+def visible_count(env: dict) -> int | None:
+    """GPUs a (stand-in) GPU process would see: the length of its
+    ``ROCR_VISIBLE_DEVICES`` / ``HIP_VISIBLE_DEVICES`` (None: unrestricted)."""
+    for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        if env.get(k) is not None:
+            return len([x for x in env[k].split(",") if x])
+    return None
 
 
 def wait_start_gate(path: str | None, timeout: float = 120.0, abort_path: str | None = None) -> str:
@@ -137,7 +154,25 @@ def _fault(run_id: str, rank: int) -> str | None:
     return None
 
 
+def _log_lifetime(t_start: float, argv: list[str]) -> None:
+    d = os.environ.get("AMDGPU_FAKE_GPU_PROC_LOG")
+    if not d:
+        return
+    os.makedirs(d, exist_ok=True)
+    role = "validator" if "--rank" in argv or "--local-bdf" in argv else "pod"
+    with open(os.path.join(d, f"{os.getpid()}.json"), "w") as f:
+        json.dump({"start": t_start, "end": time.monotonic(), "role": role, "argv": argv}, f)
+
+
 def main(argv: list[str]) -> int:
+    t_start = time.monotonic()
+    try:
+        return _main(argv)
+    finally:
+        _log_lifetime(t_start, argv)
+
+
+def _main(argv: list[str]) -> int:
     def arg(name, default):
         return argv[argv.index(name) + 1] if name in argv else default
 
@@ -159,9 +194,22 @@ def main(argv: list[str]) -> int:
 
     steps = arg("--steps", "hip,vecadd,gemm,mfma,hbm,xgmi,rccl").split(",")
     t0 = time.perf_counter()
+    if "--pod-check" in argv:  # a plugin-validation pod: every allocated GPU must be in the container
+        expect, seen = int(arg("--expect-devices", "-1")), visible_count(dict(os.environ))
+        if expect >= 0 and seen is not None and seen != expect:
+            print(json.dumps({"ok": False, "simulated": True, "steps": [],
+                              "error": f"{expect} GPU(s) allocated to the pod, {seen} visible"}))
+            return 1
+    ndev = max(1, int(arg("--expect-devices", "1")))
+    per_device = ("vecadd", "gemm", "mfma", "hbm")
+    recs = []
+    for s in steps:
+        for d in (range(ndev) if s in per_device and ndev > 1 else [None]):
+            recs.append({"name": s, "ok": True, "seconds": 0.0, "simulated": True, **({"device": d} if d is not None else {})})
     rep = {"ok": True, "simulated": True, "rank": rank, "world": world, "device": int(arg("--device", "0")),
            "owner_rank_env": os.environ.get("RANK"), "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES"),
-           "steps": [{"name": s, "ok": True, "seconds": 0.0, "simulated": True} for s in steps]}
+           "rocr_visible_devices": os.environ.get("ROCR_VISIBLE_DEVICES"), "local_bdf": arg("--local-bdf", None),
+           "local_devices": list(range(ndev)), "steps": recs}
     try:
         if fault == "fail":
             raise RuntimeError("injected failure")

@@ -77,11 +77,19 @@ class AdmissionError(RuntimeError):
     reason ``UnexpectedAdmissionError``, as on a real kubelet)."""
 
 
-def fake_validator_result(argv: list[str]) -> ProcResult:
+def fake_validator_result(argv: list[str], env: dict | None = None) -> ProcResult:
     """Synthetic ``amdgpu-validator`` output for CPU-only runs."""
+    from .fake_validator import visible_count
+
     def arg(name, default):
         return argv[argv.index(name) + 1] if name in argv else default
 
+    expect = int(arg("--expect-devices", "-1"))
+    seen = visible_count(env or {})
+    if "--pod-check" in argv and expect >= 0 and seen is not None and seen != expect:
+        rep = {"ok": False, "simulated": True, "error": f"{expect} GPU(s) allocated to the pod, {seen} visible",
+               "steps": []}
+        return ProcResult(1, json.dumps(rep) + "\n", "", 0.0)
     steps = arg("--steps", "hip,vecadd,gemm,mfma,hbm,xgmi,rccl").split(",")
     rep = {"ok": True, "simulated": True, "rank": int(arg("--rank", "0")), "world": int(arg("--world", "1")),
            "device": int(arg("--device", "0")), "seconds": 0.0,
@@ -284,6 +292,8 @@ class SimCluster:
         self._node_specs = nodes
         self._short_dirs: list[str] = []
         self._hashes: dict[tuple, str] = {}
+        self.hook_drop_devices = 0  # fault injection: GPUs the runtime leaves out of a GPU container
+        self.pod_reports: dict[str, dict] = {}  # GPU pod name -> its process's JSON report
 
     # -------------------------------------------------------------- setup
     # a unix socket path must fit sockaddr_un.sun_path (108 bytes); the node's
@@ -336,9 +346,10 @@ class SimCluster:
 
     def _launch(self, argv, env, device, timeout) -> ProcResult:
         if self.fake_gpu and argv and os.path.basename(argv[0]) == "amdgpu-gpu-check":
-            argv = [argv[0], "--steps", "hsa,vecadd"]  # the stand-in reports the check's steps
+            expect = ["--expect-devices", argv[argv.index("--expect-devices") + 1]] if "--expect-devices" in argv else []
+            argv = [argv[0], "--steps", "hsa,vecadd", "--pod-check", *expect]  # the stand-in reports the check's steps
             if self.fake_gpu != "procs":
-                return fake_validator_result(argv)
+                return fake_validator_result(argv, env)
             import sys
 
             argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", *argv[1:]]
@@ -877,6 +888,13 @@ class SimCluster:
             paths = {d["path"] for d in spec.get("linux", {}).get("devices", [])}
             if "/dev/kfd" not in paths:
                 raise RuntimeError("OCI hook did not inject /dev/kfd")
+            # the container sees the GPUs whose render nodes the runtime put in
+            # (fault injection: hook_drop_devices leaves the last ones out)
+            from ..discovery import topology
+
+            minors = {g.index: g.render_minor for g in topology.enumerate_gpus(node.env.sysfs_root())}
+            injected = [d for d in devices if f"/dev/dri/renderD{minors.get(d)}" in paths]
+            devices = injected[:max(0, len(injected) - self.hook_drop_devices)] if self.hook_drop_devices else injected
         self.trace("gpu-pod-hooked", run.name)
         argv = [str(native.binary(os.path.basename(cmd[0])))] + cmd[1:]
         proc_env = {e["name"]: e["value"] for e in c.get("env") or [] if "value" in e}  # the container's env
@@ -889,6 +907,7 @@ class SimCluster:
         self.trace("gpu-pod-reported", run.name)
         try:  # the process's own step times, for the bring-up breakdown
             rep = json.loads(res.stdout.strip().splitlines()[-1])
+            self.pod_reports[run.name] = rep
             steps = " ".join(f"{x['name']}={x.get('seconds', 0):.4f}" for x in rep.get("steps", []))
             self.trace("gpu-pod-steps", f"{run.name} total={rep.get('seconds', 0):.4f} {steps}")
         except (ValueError, IndexError, KeyError, TypeError):

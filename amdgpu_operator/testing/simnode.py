@@ -35,7 +35,9 @@ def adopt_sim_node_env(env: NodeEnv) -> None:
             if os.path.basename(argv[0]) == "amdgpu-validator":
                 argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", *argv[1:]]
             elif os.path.basename(argv[0]) == "amdgpu-gpu-check":
-                argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", "--steps", "hsa,vecadd"]
+                expect = argv[argv.index("--expect-devices"):][:2] if "--expect-devices" in argv else []
+                argv = [sys.executable, "-m", "amdgpu_operator.testing.fake_validator", "--steps", "hsa,vecadd",
+                        "--pod-check", *expect]
             return run_local(argv, penv, timeout)
 
         env.launcher = launch

@@ -178,16 +178,73 @@ def abort_run(rdv: str, reason: str) -> None:
         pass
 
 
-def check_fabric(env: NodeEnv, gpus: list, smi_metrics: list | None = None) -> dict:
-    """The xGMI fabric between the validated GPUs is whole.
+# The xGMI link model the multi-GPU gates are derived from.  KFD reports every
+# XGMI io_link's bandwidth per direction: 76,000 MB/s on MI355X (16 lanes x
+# 38 Gb/s; amd-smi shows the same link as bit_rate 38 Gb/s, max_bandwidth
+# 608 Gb/s - tests/fixtures/mi355x).  A rank's collective traffic leaves it
+# over the links to its N-1 peers (one per peer in a full mesh), so the sum
+# of those links' bandwidth bounds what one rank can move per direction.
+#
+#   K4 one-shot (every rank reads all N-1 peer buffers at once, one per link):
+#     floor = xgmiReadLinkFraction x sum(link GB/s)
+#   RCCL fp32 all-reduce busBW at B bytes (bus bandwidth per rank, striped
+#   over the links; the per-launch start-up gives the alpha-beta shape
+#   busBW(B) = peak x B / (B + B_half), B_half = RCCL_HALF_BW_BYTES):
+#     floor = rcclBusbwLinkFraction x sum(link GB/s) x B / (B + B_half)
+#
+# A mesh whose links are all "up" but trained to half their rate halves both
+# measured rates: the link-rate check in check_fabric (amd-smi rate x width
+# against KFD's nominal) names it outright, and the throughput floors catch
+# what the status does not show.  Both fractions sit below the efficiency a
+# healthy mesh delivers so that run-to-run noise never fails a good node;
+# they are model-derived, not yet calibrated on an 8-GPU MI355X run (the
+# builder's box has one GPU) - the driver's scaling run records the measured
+# rates next to the floors (bench.py config.rccl_busbw_gbps / xgmi).
+RCCL_HALF_BW_BYTES = 16 << 20  # ~30 us of launch + sync at ~500 GB/s
+
+
+def _xgmi_link_gbps(env: NodeEnv, gpus: list) -> dict[tuple[int, int], float]:
+    """GB/s per direction of the KFD XGMI link between GPU indices (a, b)."""
+    from ..discovery import topology
+
+    idx = {g.index for g in gpus}
+    out = {}
+    for lk in topology.links(env.sysfs_root()):
+        if lk.is_xgmi and lk.src in idx and lk.dst in idx:
+            out[(lk.src, lk.dst)] = lk.max_bandwidth_mbps / 1000.0
+    return out
+
+
+def fabric_floors(env: NodeEnv, plan: list[list], gpus: list, rccl_fraction: float, xgmi_fraction: float,
+                  rccl_bytes: int) -> dict:
+    """Throughput floors of the multi-GPU steps, from the KFD link model above:
+    per rank the sum of the links from its first device to every peer GPU's
+    first device; the floors use the smallest such sum of the node."""
+    links = _xgmi_link_gbps(env, gpus)
+    sums = []
+    for r, devs in enumerate(plan):
+        me = devs[0].index
+        sums.append(sum(links.get((me, p[0].index), links.get((p[0].index, me), 0.0))
+                        for q, p in enumerate(plan) if q != r))
+    link_sum = min(sums) if sums else 0.0
+    size = rccl_bytes / (rccl_bytes + RCCL_HALF_BW_BYTES) if rccl_bytes > 0 else 0.0
+    return {"link_gbps_per_rank": [round(x, 1) for x in sums],
+            "min_rccl_busbw_gbps": round(rccl_fraction * link_sum * size, 1),
+            "min_xgmi_peer_read_gbps": round(xgmi_fraction * link_sum, 1)}
+
+
+def check_fabric(env: NodeEnv, gpus: list, smi_metrics: list | None = None, min_link_fraction: float = 0.9) -> dict:
+    """The xGMI fabric between the validated GPUs is whole and at speed.
 
     Every pair of distinct physical GPUs must share one xGMI hive and be
     joined by an XGMI link in the KFD topology (``io_links``); where amd-smi
-    answers, each GPU must report at least one link up per physical peer and
-    no link in error (N6 ``amdsmi_get_gpu_xgmi_link_status``).  Partitions of
-    one physical GPU are not peers of each other.  A dead link leaves RCCL
-    routing around it at a fraction of the bandwidth, which the busBW floor
-    may or may not catch; this check names the GPU."""
+    answers, each GPU must report at least one link up per physical peer, no
+    link in error, and its links trained to at least ``min_link_fraction`` of
+    the KFD nominal rate (amd-smi rate x width, e.g. 38 Gb/s x 16 = 76 GB/s,
+    against io_link max_bandwidth; a link that retrained to a lower rate or
+    width is "up" and slow).  Partitions of one physical GPU are not peers of
+    each other.  A dead or slow link leaves RCCL routing around it at a
+    fraction of the bandwidth; this check names the GPU."""
     from ..discovery import topology
 
     phys: dict[str, object] = {}
@@ -203,9 +260,13 @@ def check_fabric(env: NodeEnv, gpus: list, smi_metrics: list | None = None) -> d
         problems.append(f"GPUs are not in one xGMI hive (hive ids {sorted(hives)})")
     idx = {g.index: g.bdf for g in gpus}
     linked: set[tuple[str, str]] = set()
+    nominal: dict[str, float] = {}  # bdf -> slowest nominal KFD XGMI link (GB/s per direction)
     for lk in topology.links(env.sysfs_root()):
-        if lk.is_xgmi and lk.src in idx and lk.dst in idx:
+        if lk.is_xgmi and lk.src in idx and lk.dst in idx and idx[lk.src] != idx[lk.dst]:
             linked.add(tuple(sorted((idx[lk.src], idx[lk.dst]))))
+            if lk.max_bandwidth_mbps:
+                b = idx[lk.src]
+                nominal[b] = min(nominal.get(b, float("inf")), lk.max_bandwidth_mbps / 1000.0)
     bdfs = sorted(phys)
     missing = [(a, b) for i, a in enumerate(bdfs) for b in bdfs[i + 1:] if (a, b) not in linked]
     if missing:
@@ -220,11 +281,21 @@ def check_fabric(env: NodeEnv, gpus: list, smi_metrics: list | None = None) -> d
             smi_metrics = []
     peers = len(phys) - 1
     live = {}
+    lower = {b.lower(): b for b in phys}
     for m in smi_metrics:
-        if m.bdf.lower() not in {b.lower() for b in phys} or "xgmi_links_up" not in m.values:
+        if m.bdf.lower() not in lower or "xgmi_links_up" not in m.values:
             continue
+        bdf = lower[m.bdf.lower()]
         up, err = m.values.get("xgmi_links_up", 0), m.values.get("xgmi_links_error", 0)
-        live[m.bdf] = {"up": up, "total": m.values.get("xgmi_links_total", 0), "error": err}
+        rec = {"up": up, "total": m.values.get("xgmi_links_total", 0), "error": err}
+        speed, width = m.values.get("xgmi_link_speed_gbps", 0), m.values.get("xgmi_link_width", 0)
+        if speed and width:
+            rec["link_gbps"] = speed * width / 8.0
+            want = nominal.get(bdf)
+            if want and rec["link_gbps"] < min_link_fraction * want:
+                problems.append(f"{m.bdf}: xGMI links at {rec['link_gbps']:g} GB/s ({speed} Gb/s x{width}), "
+                                f"nominal {want:g} GB/s")
+        live[m.bdf] = rec
         if up < peers:
             problems.append(f"{m.bdf}: {up} xGMI links up, {peers} physical peers")
         if err:
@@ -235,9 +306,57 @@ def check_fabric(env: NodeEnv, gpus: list, smi_metrics: list | None = None) -> d
     return out
 
 
+def rank_plan(gpus: list) -> list[list]:
+    """The workload's ranks: one per physical GPU, in enumeration order, each
+    with the schedulable devices it validates - the GPU itself in SPX, its
+    compute partitions in DPX/QPX/CPX (they share the GPU's PCI address)."""
+    groups: dict[str, list] = {}
+    for g in gpus:
+        groups.setdefault(g.bdf, []).append(g)
+    return list(groups.values())
+
+
+# Concurrent GPU processes one node's validation may start: the workload
+# processes plus the plugin-validation pods running beside them.  A GPU box
+# caps the processes holding its devices (16 on the MI355X pool this was
+# measured on, tools/storm_probe.py), and the HIP runtime start-up that a
+# crowd of processes stretches is the longest term of the bring-up
+# (BASELINE.md "the N = 8 start-up storm").
+DEFAULT_MAX_GPU_PROCESSES = 16
+
+
+def workload_processes(world: int, run_rccl: bool, separate: bool, budget: int) -> tuple[int, bool]:
+    """(processes, separate) for ``world`` ranks: one process per physical GPU
+    (kernel checks, xGMI and RCCL together), or, when ``separate`` is asked
+    for and fits ``budget``, a second RCCL process per GPU."""
+    if run_rccl and separate and 2 * world <= budget:
+        return 2 * world, True
+    return world, False
+
+
+def planned_workload_processes(env: NodeEnv, args: list[str], budget: int) -> int:
+    """How many processes :func:`validate_workload` would start on this node."""
+    from ..discovery import topology
+
+    world = len(rank_plan(topology.enumerate_gpus(env.sysfs_root())))
+    run_rccl = "rccl" in _steps_of(args) and (world > 1 or "--rccl-single-gpu" in args)
+    return workload_processes(world, run_rccl, "--rccl-separate-process" in args, budget)[0]
+
+
 def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: float = 600.0,
-                      start_gate: str | None = None) -> dict:
-    """One native validator process per GPU, all ranks in one RCCL communicator.
+                      start_gate: str | None = None, budget: int | None = None) -> dict:
+    """One native validator process per physical GPU, all in one RCCL
+    communicator.
+
+    Each process validates every schedulable device of its GPU - the whole
+    GPU in SPX, each compute partition otherwise, concurrently on threads
+    (``amdgpu-validator --local-bdf``) - then runs the xGMI one-shot and the
+    RCCL collectives on its first device, across the physical GPUs.  An 8-GPU
+    node therefore starts 8 processes whatever its partitioning; one process
+    per partition made an 8 x CPX node start 128 and a 64-rank communicator.
+    At N >= 2 each process sees its own devices plus the first device of every
+    peer GPU (``ROCR_VISIBLE_DEVICES``): RCCL's and the IPC step's peer access
+    needs the peers visible, the runtime need not set up the rest.
 
     ``start_gate``: a file the processes wait on before their first HIP call
     (``amdgpu-validator --start-gate``): "go" releases them, anything else
@@ -254,19 +373,25 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     instead of running out their own timeouts.
 
     validate.py's own flags (not passed to the binary): ``--rccl-single-gpu``,
-    ``--rccl-shared-process``, ``--rccl-busbw-per-peer X`` (the busBW floor,
-    X GB/s per peer GPU: ``--min-rccl-busbw-gbps X*(N-1)``) and
-    ``--require-xgmi-links`` (:func:`check_fabric` on multi-GPU nodes)."""
+    ``--rccl-separate-process`` (RCCL in a second process per GPU, when that
+    fits ``budget``; ``--rccl-shared-process`` is the default and accepted),
+    ``--rccl-busbw-link-fraction F`` and ``--xgmi-read-link-fraction F``
+    (the throughput floors of :func:`fabric_floors`, passed to the binary as
+    ``--min-rccl-busbw-gbps`` / ``--min-xgmi-read-gbps``),
+    ``--max-gpu-processes N`` (the budget), ``--require-xgmi-links`` and
+    ``--min-xgmi-link-fraction F`` (:func:`check_fabric` on multi-GPU nodes)."""
     from ..discovery import topology
 
     t0 = time.perf_counter()
     gpus = topology.enumerate_gpus(env.sysfs_root())
     if not gpus:
         raise StepFailed("no GPUs to validate")
-    world = len(gpus)
+    plan = rank_plan(gpus)
+    world = len(plan)
     args = list(args or [])
-    if world > 8:
-        # partitioned GPUs: the xGMI one-shot kernel takes <= 8 peers; RCCL still spans all
+    if budget is None:
+        budget = int(_arg_value(args, "--max-gpu-processes") or DEFAULT_MAX_GPU_PROCESSES)
+    if world > 8:  # the xGMI one-shot kernel takes <= 8 peers; RCCL still spans all
         args = _drop_step(args, "xgmi")
     run_id = os.urandom(6).hex()
     rdv = os.path.join(env.validations_dir, "rendezvous", run_id)
@@ -277,37 +402,48 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     sdk_gate = "--counter-gate" in args and _arg_value(args, "--gate-mode") == "sdk"
     counter_env = gate_env() if sdk_gate else {}
     rccl_single = "--rccl-single-gpu" in args  # validate.py's own flags, not the binary's
-    rccl_shared = "--rccl-shared-process" in args
+    separate = "--rccl-separate-process" in args
     require_links = "--require-xgmi-links" in args
-    per_peer = float(_arg_value(args, "--rccl-busbw-per-peer") or 0.0)
-    args = _drop_value(_drop_flag(_drop_flag(_drop_flag(args, "--rccl-single-gpu"), "--rccl-shared-process"),
-                                  "--require-xgmi-links"), "--rccl-busbw-per-peer")
-    if per_peer > 0 and world > 1:
-        args += ["--min-rccl-busbw-gbps", f"{per_peer * (world - 1):g}"]
+    rccl_frac = float(_arg_value(args, "--rccl-busbw-link-fraction") or 0.0)
+    xgmi_frac = float(_arg_value(args, "--xgmi-read-link-fraction") or 0.0)
+    link_frac = float(_arg_value(args, "--min-xgmi-link-fraction") or 0.9)
+    args = _drop_flag(args, "--rccl-single-gpu", "--rccl-shared-process", "--rccl-separate-process",
+                      "--require-xgmi-links")
+    args = _drop_value(args, "--rccl-busbw-link-fraction", "--xgmi-read-link-fraction", "--min-xgmi-link-fraction",
+                       "--max-gpu-processes")
     steps = _steps_of(args)
-    kernel_steps = [s for s in steps if s != "rccl"]
-    # RCCL runs in its own process per GPU, concurrently with the kernel
-    # checks: loading librccl (~570 MB of device code) and its communicator
-    # set-up would otherwise hold the HIP runtime of the kernel process.  A
-    # single-GPU node has no collective to validate (no xGMI peer) unless
+    # A single-GPU node has no collective to validate (no xGMI peer) unless
     # rcclSingleGpu asks for the rehearsal.
     run_rccl = "rccl" in steps and (world > 1 or rccl_single)
-    if run_rccl and rccl_shared:  # one process per GPU runs the kernel checks and RCCL
-        kernel_steps = kernel_steps + ["rccl"]
-    # With a separate RCCL process per GPU, the kernel-check processes touch
-    # only their own GPU: they see only it (visible_devices_env), and the xGMI
-    # IPC step, which maps every peer's buffer, moves to the RCCL processes
-    # that see all GPUs anyway - it overlaps their communicator set-up.
-    split = world > 1 and run_rccl and not rccl_shared
-    peer_steps = ["hip", "rccl"]
-    if split and "xgmi" in kernel_steps:
-        kernel_steps = [s for s in kernel_steps if s != "xgmi"]
-        peer_steps = ["hip", "xgmi", "rccl"]
-    kernel_env = {**counter_env, **(thp_malloc_env() if run_rccl and rccl_shared else {})}
-    jobs = [(r, _with_steps(args, kernel_steps), run_id, kernel_env) for r in range(world)]
-    if run_rccl and not rccl_shared:
-        jobs += [(r, _with_steps(_drop_flag(args, "--counter-gate"), peer_steps), run_id + "-rccl", thp_malloc_env())
-                 for r in range(world)]
+    floors = None
+    if world > 1 and (rccl_frac > 0 or xgmi_frac > 0):
+        rccl_bytes = 4 * int(_arg_value(args, "--rccl-elems") or (1 << 24))
+        floors = fabric_floors(env, plan, gpus, rccl_frac, xgmi_frac, rccl_bytes)
+        if rccl_frac > 0:
+            args += ["--min-rccl-busbw-gbps", f"{floors['min_rccl_busbw_gbps']:g}"]
+        if xgmi_frac > 0:
+            args += ["--min-xgmi-read-gbps", f"{floors['min_xgmi_peer_read_gbps']:g}"]
+    kernel_steps = [s for s in steps if s not in ("xgmi", "rccl")]
+    xgmi = "xgmi" in steps  # real peers at N >= 2, emulated peers on one device otherwise
+    nproc, separate = workload_processes(world, run_rccl, separate, budget)
+    jobs = []  # (rank, binary flags, run id, env)
+    for r, devs in enumerate(plan):
+        others = [plan[q][0] for q in range(world) if q != r]
+        local = ["--local-bdf", devs[0].bdf]
+        if separate:  # kernel checks of the GPU's devices; xGMI + RCCL in a process of their own
+            jobs.append((r, _with_steps(args, kernel_steps) + local + ["--expect-devices", str(len(devs))], run_id,
+                         {**counter_env, **topology.visible_devices_env(devs, gpus)}))
+            jobs.append((r, _with_steps(_drop_flag(args, "--counter-gate"), ["hip"] + ["xgmi"] * xgmi + ["rccl"])
+                         + local + ["--expect-devices", "1"], run_id + "-rccl",
+                         {**thp_malloc_env(), **topology.visible_devices_env([devs[0], *others], gpus)}))
+            continue
+        jenv = dict(counter_env)
+        if run_rccl:
+            jenv.update(thp_malloc_env())
+        if world > 1:
+            jenv.update(topology.visible_devices_env([*devs, *others], gpus))
+        jobs.append((r, _with_steps(args, kernel_steps + ["xgmi"] * xgmi + ["rccl"] * run_rccl) + local
+                     + ["--expect-devices", str(len(devs))], run_id, jenv))
 
     def failed(res) -> bool:
         return res.rc != 0 or report_rc(res.stdout) != 0
@@ -318,14 +454,11 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         # kernel's teardown of its GPU state do not hold up the node
         if REPORT_EARLY:
             jenv = {**jenv, REPORT_EARLY_ENV: "1"}
-        device = gpus[rank].index
-        if split and rid == run_id:  # a kernel-check process: its GPU only, as HIP device 0
-            jenv = {**jenv, **topology.visible_devices_env([gpus[rank]], gpus)}
-            device = 0
-        argv = workload_argv(jargs, rank, world, rdv, rid, device)
+        argv = workload_argv(jargs, rank, world, rdv, rid, 0)
         if start_gate:
             argv += ["--start-gate", start_gate]
-        res = env.launch(argv, jenv, device=gpus[rank].index, timeout=timeout)
+        # the launcher runs the process on the rank that owns physical GPU `rank`
+        res = env.launch(argv, jenv, device=rank, timeout=timeout)
         if world > 1 and failed(res):
             abort_run(rdv, f"{rid} rank {rank} failed (rc {res.rc})")
         return res
@@ -333,7 +466,8 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     fabric = None
     try:
         with ThreadPoolExecutor(max_workers=len(jobs) + 1) as ex:
-            fabric_f = ex.submit(check_fabric, env, gpus) if require_links and world > 1 else None
+            fabric_f = (ex.submit(check_fabric, env, gpus, None, link_frac) if require_links and world > 1
+                        else None)
             results = list(ex.map(one, jobs))
             fabric = fabric_f.result() if fabric_f is not None else None
     finally:
@@ -364,25 +498,46 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
                 main["stderr"] = rep.get("stderr", "")
         else:
             reports.append(rep)
-    if run_rccl and rccl_shared:
+    if run_rccl and not separate:
         for rep in reports:
             rep["rccl_process_seconds"] = rep.get("process_seconds")
     if "rccl" in steps and not run_rccl:
         for rep in reports:
             rep.setdefault("steps", []).append({"name": "rccl", "ok": True, "skipped": "single GPU: no xGMI peer"})
-    ok = all(r.get("rc") == 0 and r.get("ok") for r in reports)
-    summary = {"ok": ok, "world": world, "seconds": time.perf_counter() - t0, "ranks": reports}
+    problems = device_coverage(plan, reports)
+    ok = all(r.get("rc") == 0 and r.get("ok") for r in reports) and not problems
+    summary = {"ok": ok, "world": world, "devices": len(gpus), "processes": len(jobs),
+               "process_mode": "separate" if separate else "shared", "seconds": time.perf_counter() - t0,
+               "ranks": reports}
+    if problems:
+        summary["coverage_problems"] = problems
+    if floors is not None:
+        summary["floors"] = floors
     if fabric is not None:
         summary["fabric"] = fabric
         if not fabric["ok"]:
             ok = summary["ok"] = False
     if not ok:
-        raise StepFailed(f"workload validation failed: {failure_summary(reports, fabric)}")
+        raise StepFailed(f"workload validation failed: {failure_summary(reports, fabric, problems)}")
     write_ready(env, "workload", summary)
     return summary
 
 
-def failure_summary(reports: list[dict], fabric: dict | None = None) -> str:
+def device_coverage(plan: list[list], reports: list[dict]) -> list[str]:
+    """Every device of every rank reported its kernel steps: a partition
+    the process did not see (wrong visibility, a partition switch under way)
+    fails the run instead of passing on the devices that were there."""
+    problems = []
+    for r, (devs, rep) in enumerate(zip(plan, reports)):
+        if not rep.get("ok"):
+            continue
+        seen = rep.get("local_devices")
+        if seen is not None and len(seen) != len(devs):
+            problems.append(f"rank {r}: {len(seen)} of {len(devs)} devices validated")
+    return problems
+
+
+def failure_summary(reports: list[dict], fabric: dict | None = None, problems: list[str] | None = None) -> str:
     """The causes of a failed run first: a rank's own failure, or a peer it
     found missing/dead; ranks that only stopped because of another's failure
     (peer state ``failed`` / ``aborted``) come last, as consequences."""
@@ -394,7 +549,7 @@ def failure_summary(reports: list[dict], fabric: dict | None = None) -> str:
         bad_steps = [s.get("name") for s in r.get("steps", []) if s.get("ok") is False]
         item = f"rank {i}: {msg}" + (f" (steps {bad_steps})" if bad_steps else "")
         (consequences if r.get("peer_state") in ("failed", "aborted") else causes).append(item)
-    parts = []
+    parts = list(problems or [])
     if fabric is not None and not fabric.get("ok"):
         parts.append("xGMI fabric: " + "; ".join(fabric.get("problems", [])))
     parts += causes
@@ -420,15 +575,15 @@ def _with_steps(args: list[str], steps: list[str]) -> list[str]:
     return out + ["--steps", ",".join(steps if "hip" in steps else ["hip", *steps])]
 
 
-def _drop_flag(args: list[str], flag: str) -> list[str]:
-    return [a for a in args if a != flag]
+def _drop_flag(args: list[str], *flags: str) -> list[str]:
+    return [a for a in args if a not in flags]
 
 
-def _drop_value(args: list[str], flag: str) -> list[str]:
+def _drop_value(args: list[str], *flags: str) -> list[str]:
     """Remove ``flag VALUE`` pairs."""
     out, i = [], 0
     while i < len(args):
-        if args[i] == flag:
+        if args[i] in flags:
             i += 2
             continue
         out.append(args[i])
@@ -558,11 +713,20 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                     pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                     image: str | None = None, pull_policy: str = "IfNotPresent",
                     pull_secrets: list[str] | None = None, kubelet=None,
-                    partition_strategy: str = "single", pod_check: str = "hsa") -> dict:
+                    partition_strategy: str = "single", pod_check: str = "hsa", per_device: bool = False,
+                    max_concurrent: int | None = None) -> dict:
     """Wait until the kubelet holds one device per GPU (or partition), then
-    run one 1-device pod per device, each requesting the resource its device
-    is advertised under (:func:`expected_devices`; ``expect`` overrides the
-    count of ``resource``).
+    prove the device-plugin path with pods: by default one pod per resource
+    holding all of its devices (every device still goes through Allocate, the
+    OCI hook and a kernel launch, from one process - at N = 8, 8 fewer process
+    and HIP starts in the node's start-up storm, profiles/r3_storm); with
+    ``per_device`` one 1-device pod per device (N pods x 1 GPU, each its own
+    GetPreferredAllocation / Allocate / hook), at most ``max_concurrent``
+    running at a time.  Each pod requests the resource its device is
+    advertised under (:func:`expected_devices`; ``expect`` overrides the
+    count of ``resource``) and is told how many devices it was allocated
+    (``--expect-devices``): a device the runtime left out of the container
+    fails the pod instead of passing on the ones that are there.
 
     The pods run the validator's own image (``VALIDATOR_IMAGE`` in the
     validator container's env, with its pull policy and secrets, which
@@ -611,10 +775,11 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     pod_args = list(pod_args or ["--steps", "hip,vecadd,gemm", "--gemm", "1024"])
 
     def make_pod(name: str, run_id: str, res: str, count: int = 1) -> dict:
+        expect = ["--expect-devices", str(count)]
         if pod_check == "hsa":  # a kernel per allocated GPU on the HSA runtime (native/validator/gpu_check.cpp)
-            command, args = "amdgpu-gpu-check", ["--timeout", "30"]
+            command, args = "amdgpu-gpu-check", ["--timeout", "30", *expect]
         else:
-            command, args = "amdgpu-validator", pod_args + (["--all-devices"] if count > 1 else [])
+            command, args = "amdgpu-validator", pod_args + ["--all-devices", *expect]
         pod = {
             "apiVersion": "v1", "kind": "Pod",
             "metadata": {"name": name, "namespace": env.namespace,
@@ -637,14 +802,24 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
 
     # a pod the kubelet could not admit (UnexpectedAdmissionError: the device
     # list it planned from was stale, e.g. a re-registering plugin's devices
-    # still unhealthy) is run again; any other failure fails the step
-    # One pod per resource holding all of its devices: every GPU still goes
-    # through Allocate, the OCI hook and a kernel launch, from one process
-    # (at N = 8, 8 fewer process and HIP starts in the node's start-up
-    # storm, profiles/r3_storm).  Time-sliced resources keep one 1-replica
-    # pod per GPU: a multi-replica request may land twice on one GPU.
-    todo = [(r, 1) for r, n in sorted(plan.items()) if r in shared or "*" in shared for _ in range(n)]
-    todo += [(r, n) for r, n in sorted(plan.items()) if r not in shared and "*" not in shared]
+    # still unhealthy) is run again; any other failure fails the step.
+    # Time-sliced resources keep one 1-replica pod per GPU: a multi-replica
+    # request may land twice on one GPU.
+    def pods_for(one_each: bool) -> list[tuple[str, int]]:
+        single = lambda r: one_each or r in shared or "*" in shared  # noqa: E731
+        return ([(r, 1) for r, n in sorted(plan.items()) if single(r) for _ in range(n)]
+                + [(r, n) for r, n in sorted(plan.items()) if not single(r)])
+
+    todo = pods_for(per_device)
+    fallback = None
+    if per_device and max_concurrent is not None and len(todo) > max(1, max_concurrent):
+        # every 1-device pod must hold its device while the others are admitted
+        # (a finished pod's device goes back to the kubelet and the next pod may
+        # get it again), so they all run at once - or, past the process budget,
+        # one pod per resource instead
+        fallback = f"{len(todo)} 1-device pods exceed the {max_concurrent} GPU processes left: one pod per resource"
+        log.info("plugin validation: %s", fallback)
+        todo = pods_for(False)
     devices: list[str] = []
     attempts, backoff, pods_run = 0, 0.05, 0
     while todo:
@@ -670,7 +845,9 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
                  and (live[n].get("status") or {}).get("reason") == "UnexpectedAdmissionError"]
         hard = {n: p for n, p in phases.items() if p != "Succeeded" and n not in retry}
         if hard:
-            raise StepFailed(f"plugin validation pods did not succeed: {phases}")
+            why = "; ".join(f"{n}: {((live.get(n) or {}).get('status') or {}).get('message', '')[-300:]}"
+                            for n in hard if n in live)
+            raise StepFailed(f"plugin validation pods did not succeed: {phases}" + (f" ({why})" if why else ""))
         for n in names:
             if phases[n] == "Succeeded":
                 alloc = (live[n].get("metadata", {}).get("annotations") or {}).get("amd.com/gpu.allocated", "")
@@ -684,11 +861,13 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
             (stop.wait if stop is not None else time.sleep)(backoff)
             backoff = min(backoff * 2, 2.0)
     summary = {"ok": True, "pods": pods_run, "devices_validated": len(devices), "resources": plan, "devices": devices,
-               "attempts": attempts,
+               "attempts": attempts, "pod_mode": "perDevice" if per_device and not fallback else "perResource",
                "allocatable_wait_s": round(t_alloc, 4),
                "allocatable_source": source, "marks": {k: round(v, 4) for k, v in marks.items()},
                "kubelet_queries": queries,
                "seconds": time.perf_counter() - t0}
+    if fallback:
+        summary["pod_mode_fallback"] = fallback
     write_ready(env, "plugin", summary)
     return summary
 
@@ -751,7 +930,7 @@ def abort_start_gates(env: NodeEnv) -> list[str]:
 def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURCE_NAME,
                  pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                  wait_toolkit: bool = False, with_driver: bool = False, partition_strategy: str = "single",
-                 pod_check: str = "hsa") -> dict:
+                 pod_check: str = "hsa", per_device: bool = False) -> dict:
     """Workload and plugin validation concurrently (each skipped if already done).
 
     Only the driver gates the workload: its processes run in this privileged
@@ -770,6 +949,11 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
     errors: list[str] = []
     gate = None
     driver_done = threading.Event()
+    # the node's GPU-process budget: the workload keeps one process for the
+    # plugin pods, which get what the workload leaves
+    budget = int(_arg_value(workload_args, "--max-gpu-processes") or DEFAULT_MAX_GPU_PROCESSES)
+    wl_procs = 0 if read_ready(env, "workload") is not None else planned_workload_processes(env, workload_args,
+                                                                                             budget - 1)
     sdk_gate = "--counter-gate" in workload_args and _arg_value(workload_args, "--gate-mode") == "sdk"
     prespawn = with_driver and prespawn_safe(env, sdk_gate)
     if with_driver:
@@ -799,7 +983,7 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
                 if "driver" not in results:
                     return
             if read_ready(env, "workload") is None:
-                results["workload"] = validate_workload(env, workload_args, timeout, start_gate=gate)
+                results["workload"] = validate_workload(env, workload_args, timeout, start_gate=gate, budget=budget - 1)
         except Exception as e:  # noqa: BLE001
             errors.append(f"workload: {e}")
 
@@ -822,7 +1006,8 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
             if read_ready(env, "plugin") is None:
                 results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop,
                                                     kubelet=kubelet, partition_strategy=partition_strategy,
-                                                    pod_check=pod_check)
+                                                    pod_check=pod_check, per_device=per_device,
+                                                    max_concurrent=max(1, budget - wl_procs))
         except Exception as e:  # noqa: BLE001
             errors.append(f"plugin: {e}")
         finally:

@@ -73,6 +73,9 @@ def parse():
                          "threads of the bench process (the round-1/2 lower bound)")
     ap.add_argument("--compare", type=int, default=2,
                     help="after the timed steps, this many bring-ups in the other --mode (reported, not timed)")
+    ap.add_argument("--no-pod-workload", action="store_true",
+                    help="skip the config-5 pod workload after the last timed bring-up")
+    ap.add_argument("--pod-gemm", type=int, default=4096, help="GEMM size of the pod workload's pods")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--detail", default=None, help="write per-step breakdown JSON here")
     ap.add_argument("--set", action="append", default=[], dest="extra_set",
@@ -80,13 +83,36 @@ def parse():
     return ap.parse_args()
 
 
-def gpu_available() -> bool:
-    try:
-        import torch
-
-        return torch.cuda.is_available()
-    except Exception:  # noqa: BLE001
+def gpu_available(root: str = "/") -> bool:
+    """GPUs from the KFD topology in sysfs (the N3 library), not from a HIP
+    runtime: the harness never opens the device.  Every GPU process of a
+    bring-up is a child (validator, plugin pod) that the step waits for, so
+    there is no device work of the harness to synchronise, and a HIP context
+    in each harness rank would hold /dev/kfd through every timed bring-up -
+    at N = 8 eight GPU processes that a real control plane does not have."""
+    if not os.path.exists(os.path.join(root, "dev/kfd")):
         return False
+    try:
+        from amdgpu_operator.discovery import topology
+
+        return len(topology.enumerate_gpus(root)) > 0
+    except Exception:  # noqa: BLE001 - no native library: no GPU path
+        return False
+
+
+def holds_kfd() -> bool:
+    """Does this process have /dev/kfd open (a GPU context)?"""
+    try:
+        fds = os.listdir("/proc/self/fd")
+    except OSError:
+        return False
+    for fd in fds:
+        try:
+            if os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd":
+                return True
+        except OSError:
+            continue
+    return False
 
 
 def operand_breakdown(stats: list[dict], t0: float, t0_wall: float) -> dict:
@@ -207,7 +233,8 @@ class StallMeter:
         return self.max_s
 
 
-def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode: str = "process") -> dict:
+def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode: str = "process",
+                 pods: bool = False) -> dict:
     from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, deep_merge, parse_set_flags
     from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
 
@@ -265,6 +292,15 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
         cluster.wait_ready(args.timeout, {"mi355x-node-0": n_gpus})
         alloc_visible = time.perf_counter() - t0
         t_total = time.perf_counter() - t0
+        pod_workload = None
+        if pods:
+            # BASELINE config 5 on the Ready node: user-shaped GEMM pods through
+            # admission, GetPreferredAllocation, Allocate and the OCI hook
+            # (reported next to the headline, not part of it)
+            from amdgpu_operator.testing.podworkload import run_pod_workload
+
+            pod_workload = run_pod_workload(cluster, "mi355x-node-0", n_gpus, gemm_n=args.pod_gemm,
+                                            timeout=args.timeout)
         cp = cluster.policy()
         nobj = cluster.client.get("v1", "Node", "mi355x-node-0")
         alloc = int(nobj["status"]["allocatable"].get("amd.com/gpu", "0"))
@@ -290,6 +326,7 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
                 timeline[f"{step}.{k}"] = round(v - t0_wall, 4)
         return {
             "mode": mode,
+            "pod_workload": pod_workload,
             "operands": operand_breakdown(cluster.process_stats, t0, t0_wall) if mode == "process" else None,
             "time_to_ready_s": ttr,
             "allocatable_visible_s": alloc_visible,
@@ -344,22 +381,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.gpus != world:
         args.gpus = world
-    has_gpu = gpu_available()
+    has_gpu = gpu_available(args.sysfs_root or "/")
     fake_gpu = args.fake_gpu or args.fake_gpu_procs or not has_gpu
     if fake_gpu and args.fake_gpu_procs:
         fake_gpu = "procs"
 
-    import torch
-
     dist = None
     group = None
-    if world > 1:
+    if world > 1:  # the ranks' control channel only (gloo): no rank opens a GPU
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
         group = dist.group.WORLD
-    if has_gpu:
-        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+    del local_rank  # GPU d's processes run on rank d % world (launcher), children of the harness
 
     from amdgpu_operator.nodeenv import NodeEnv
     from amdgpu_operator.parallel.launcher import DistributedLauncher
@@ -384,8 +418,9 @@ def main():
 
         faulthandler.dump_traceback_later(args.timeout + 60, exit=False)  # stacks if a step wedges
         try:
-            for _ in range(n_steps):
-                out.append(one_bring_up(args, n_gpus, launcher, workdir, fake_gpu, mode))
+            for i in range(n_steps):
+                pods = out is results and i == n_steps - 1 and not args.no_pod_workload
+                out.append(one_bring_up(args, n_gpus, launcher, workdir, fake_gpu, mode, pods))
         except Exception as e:  # noqa: BLE001
             import traceback
 
@@ -410,10 +445,10 @@ def main():
             launcher.serve()
 
     def sync():
+        # every GPU process of a step is a child that the step has waited for:
+        # the barrier is the whole synchronisation (see gpu_available)
         if world > 1:
             dist.barrier()
-        if has_gpu:
-            torch.cuda.synchronize()
 
     # warmup (page-in, first HIP/RCCL init of the box)
     warm: list = []
@@ -427,6 +462,7 @@ def main():
     sync()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    kfd_held = holds_kfd()  # after the timed bring-ups, before the other-mode comparison
     # the other mode, untimed: in-process (lower bound) next to per-process
     other = "thread" if args.mode == "process" else "process"
     compare: list = []
@@ -482,8 +518,13 @@ def main():
                 "rccl_comm_init_s": results[-1]["rccl_comm_init_s"],
                 "counter_gate": results[-1]["gemm_counter_gate"],
                 "operand_mode": args.mode,
+                # the harness itself never held a GPU context (no /dev/kfd descriptor)
+                "harness_holds_kfd": kfd_held,
                 # per operand container of the last timed bring-up (process mode)
                 "operands": results[-1].get("operands"),
+                # BASELINE config 5 after the last timed bring-up: N pods x 1 GPU, 1 pod x N (and 2 x 4 at N = 8),
+                # each a random-init bf16 GEMM on the hand-written kernel of its GPUs (not part of `value`)
+                "pod_workload": results[-1].get("pod_workload"),
                 f"{other}_mode_time_to_ready_s": [round(r["time_to_ready_s"], 4) for r in compare],
             },
         }

@@ -120,6 +120,7 @@ typedef struct {
   uint64_t hbm_thermal_residency;
   uint64_t vram_max_bandwidth_gbps;
   uint32_t xgmi_link_speed_gbps;
+  uint32_t xgmi_link_width;  // lanes per xGMI link (x16 on MI355X): link GB/s = speed x width / 8
   uint32_t pcie_link_width;
   uint32_t pcie_link_speed_mts;  // table: 0.1 GT/s
   uint32_t throttle_status;

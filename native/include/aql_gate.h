@@ -21,11 +21,14 @@ const char* avk_aql_gate_counter_name(int i);
 
 // Dispatch gemm_bf16_nt_8p_kernel<false,false,false> (C = A * Bt^T, bf16 out)
 // from the code object at `code_object` on the GPU at `pci_bus_id`
-// ("dddd:bb:dd.f", hipDeviceGetPCIBusId), bracketed by aqlprofile start/stop
+// ("dddd:bb:dd.f", hipDeviceGetPCIBusId; `agent_ordinal` picks among the GPU
+// agents at that address - the compute partitions of one GPU share it, and HIP
+// numbers them in the HSA agents' order), bracketed by aqlprofile start/stop
 // packets on a private queue, and sum every per-instance counter sample.  A,
 // Bt and C are device pointers (hipMalloc); M, N and K are multiples of 256
 // (the kernel's tile).  Waits at most timeout_s for the stop packet.  Returns
 // 0, or -1 with a message in err.
-int avk_aql_gate_gemm(const char* pci_bus_id, const void* A, const void* Bt, void* C, int M, int N, int K,
-                      const char* code_object, double timeout_s, avk_aql_gate_result* out, char* err, int errlen);
+int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt, void* C, int M,
+                      int N, int K, const char* code_object, double timeout_s, avk_aql_gate_result* out, char* err,
+                      int errlen);
 }

@@ -88,6 +88,8 @@ struct Api {
 
 struct AgentSearch {
   uint32_t domain = 0, bdfid = 0;
+  int ordinal = 0;  // which of the GPU agents at this PCI address (compute partitions share it)
+  int seen = 0;
   hsa_agent_t gpu{}, cpu{};
   bool gpu_ok = false, cpu_ok = false;
 };
@@ -103,7 +105,7 @@ hsa_status_t find_agents(hsa_agent_t a, void* d) {
     uint32_t bdf = 0, dom = 0;
     hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
     hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
-    if (bdf == s->bdfid && dom == s->domain) {
+    if (bdf == s->bdfid && dom == s->domain && s->seen++ == s->ordinal) {
       s->gpu = a;
       s->gpu_ok = true;
     }
@@ -224,9 +226,9 @@ extern "C" const char* avk_aql_gate_counter_name(int i) {
   return (i >= 0 && i < AVK_AQL_GATE_COUNTERS) ? kNames[i] : "";
 }
 
-extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, const void* A, const void* Bt, void* C, int M, int N, int K,
-                                 const char* code_object, double timeout_s, avk_aql_gate_result* out, char* err,
-                                 int errlen) {
+extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt, void* C,
+                                 int M, int N, int K, const char* code_object, double timeout_s,
+                                 avk_aql_gate_result* out, char* err, int errlen) {
   const auto t0 = Clock::now();
   memset(out, 0, sizeof(*out));
   hsa_queue_t* queue = nullptr;
@@ -248,6 +250,7 @@ extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, const void* A, const vo
     AgentSearch as;
     as.domain = dom;
     as.bdfid = (bus << 8) | (dev << 3) | fn;
+    as.ordinal = agent_ordinal;
     check(hsa_iterate_agents(find_agents, &as), "iterate agents");
     if (!as.gpu_ok || !as.cpu_ok) throw Fail{std::string("no HSA agent for ") + pci_bus_id};
     hsa_amd_memory_pool_t kpool{0};

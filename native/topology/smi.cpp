@@ -279,6 +279,7 @@ AT_API int at_smi_collect(at_metrics_t* out, int max, int* count) {
         m.hbm_thermal_residency = or0(gm.hbm_thm_residency_acc);
         m.vram_max_bandwidth_gbps = or0(gm.vram_max_bandwidth);
         m.xgmi_link_speed_gbps = gm.xgmi_link_speed == UINT16_MAX ? 0 : gm.xgmi_link_speed;
+        m.xgmi_link_width = gm.xgmi_link_width == UINT16_MAX ? 0 : gm.xgmi_link_width;
         m.pcie_link_width = gm.pcie_link_width == UINT16_MAX ? 0 : gm.pcie_link_width;
         m.pcie_link_speed_mts = gm.pcie_link_speed == UINT16_MAX ? 0 : gm.pcie_link_speed * 100u;
         m.throttle_status = gm.throttle_status == UINT32_MAX ? 0 : gm.throttle_status;

@@ -24,7 +24,8 @@
 // Output: one JSON line in the validator's report shape ({"ok", "seconds",
 // "steps": [{"name": "hsa" | "vecadd", "device": d, ...}]}); exit 0 when every
 // device passed.  A dispatch that does not complete within --timeout fails
-// the check; its queue is left to the process exit.
+// the check; its queue, signal, code object and buffers are left to the
+// process exit.
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <unistd.h>
@@ -149,7 +150,7 @@ bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std:
   hsa_queue_t* queue = nullptr;
   hsa_signal_t done{0};
   std::vector<void*> allocs;
-  bool ok = false, finished = false;
+  bool ok = false, dispatched = false, finished = false;
   char agent_name[64] = {0};
   try {
     hsa_agent_get_info(gpu, HSA_AGENT_INFO_NAME, agent_name);
@@ -211,6 +212,7 @@ bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std:
                      static_cast<uint32_t>(hdr) | (static_cast<uint32_t>(1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS) << 16),
                      __ATOMIC_RELEASE);
     hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+    dispatched = true;
     while (hsa_signal_wait_scacquire(done, HSA_SIGNAL_CONDITION_LT, 1, 1000000, HSA_WAIT_STATE_BLOCKED) >= 1)
       if (secs(t1) > timeout_s) throw Fail{"dispatch did not complete within the timeout"};
     finished = true;
@@ -226,12 +228,17 @@ bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std:
     *error = "device " + std::to_string(d) + ": " + f.msg;
     steps->push_back(fmt_step("vecadd", d, false, secs(t0), ""));
   }
-  if (queue && (finished || !done.handle)) hsa_queue_destroy(queue);  // a stuck one goes with the process
-  if (done.handle) hsa_signal_destroy(done);
-  if (exe.handle) hsa_executable_destroy(exe);
-  if (reader.handle) hsa_code_object_reader_destroy(reader);
-  if (finished)
+  // A dispatch that did not finish may still be running (slow, not dead): its
+  // queue, completion signal, code object and buffers all stay until the
+  // process exit, so the kernel never runs from freed code or signals freed
+  // memory.  (A failure before the dispatch left nothing in flight.)
+  if (!(dispatched && !finished)) {
+    if (queue) hsa_queue_destroy(queue);
+    if (done.handle) hsa_signal_destroy(done);
+    if (exe.handle) hsa_executable_destroy(exe);
+    if (reader.handle) hsa_code_object_reader_destroy(reader);
     for (void* q : allocs) hsa_amd_memory_pool_free(q);
+  }
   return ok;
 }
 
@@ -241,12 +248,14 @@ int main(int argc, char** argv) {
   const auto t0 = Clock::now();
   double timeout_s = 10.0;
   int elems = 1 << 16;
+  int expect = -1;  // --expect-devices: the GPUs the kubelet allocated to this pod
   for (int i = 1; i < argc; ++i) {
     std::string k = argv[i];
     if (k == "--timeout" && i + 1 < argc) timeout_s = atof(argv[++i]);
     else if (k == "--elems" && i + 1 < argc) elems = atoi(argv[++i]);
+    else if (k == "--expect-devices" && i + 1 < argc) expect = atoi(argv[++i]);
     else if (k == "--help" || k == "-h") {
-      fprintf(stderr, "usage: amdgpu-gpu-check [--timeout S] [--elems N]   (every visible GPU)\n");
+      fprintf(stderr, "usage: amdgpu-gpu-check [--timeout S] [--elems N] [--expect-devices N]   (every visible GPU)\n");
       return 2;
     }
     // other flags (the validator's pod arguments) are accepted and ignored
@@ -265,6 +274,11 @@ int main(int argc, char** argv) {
     check(hsa_iterate_agents(find_agents, &ag), "iterate agents");
     ngpu = (int)ag.gpus.size();
     if (ag.gpus.empty()) throw Fail{"no GPU agent visible in this container"};
+    // every allocated device must have been put into the container: a device
+    // the runtime hook or CDI spec left out is a failed check, not a pass on
+    // the ones that are there
+    if (expect >= 0 && ngpu != expect)
+      throw Fail{std::to_string(expect) + " GPU(s) allocated to the pod, " + std::to_string(ngpu) + " visible"};
     if (!ag.cpu_ok) throw Fail{"no CPU agent"};
     hsa_amd_memory_pool_t pool{0};
     check(hsa_amd_agent_iterate_memory_pools(ag.cpu, find_fine_pool, &pool), "memory pools");

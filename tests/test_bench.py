@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
@@ -30,3 +32,34 @@ def test_bench_json_line_contract():
     ops = cfg["operands"]
     assert ops["amd-device-plugin-daemonset/amd-device-plugin"]["ready_s"] > 0
     assert ops["amd-operator-validator/amd-operator-validator"]["ready_s"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_harness_never_opens_the_gpu():
+    """N = 1 on the MI355X: the bench process itself never becomes a KFD
+    process during a bring-up (only its children - validator, plugin pod -
+    do), so the headline measures the operator's GPU processes, not a HIP
+    context of the harness."""
+    import time
+
+    procs = "/sys/class/kfd/kfd/proc"
+    if not os.path.isdir(procs):
+        pytest.skip("no KFD process list in this container")
+    p = subprocess.Popen([sys.executable, "bench.py", "--steps", "1", "--warmup", "0", "--compare", "0"],
+                         cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    seen: set[str] = set()
+    deadline = time.monotonic() + 240
+    while p.poll() is None and time.monotonic() < deadline:
+        try:
+            seen.update(os.listdir(procs))
+        except OSError:
+            pass
+        time.sleep(0.002)
+    if p.poll() is None:
+        p.kill()
+    out, err = p.communicate()
+    assert p.returncode == 0, err[-3000:]
+    line = json.loads([x for x in out.splitlines() if x.startswith("{")][0])
+    assert line["config"]["harness_holds_kfd"] is False
+    assert str(p.pid) not in seen
+    assert seen - {str(os.getpid())}, "no GPU process seen at all: the KFD process list is not being read"

@@ -59,3 +59,30 @@ def test_run_local_takes_the_report_before_the_exit():
     assert r.rc == 7  # already exited: its real status
     r = run_local([sys.executable, "-c", "import time; time.sleep(5)"], {"AMDGPU_REPORT_EARLY": "1"}, timeout=0.5)
     assert r.rc == 124
+
+
+def test_bench_n8_stays_within_the_gpu_process_budget(tmp_path):
+    """The driver's N = 8 launch (torchrun, 8 ranks) on CPU with stand-in GPU
+    processes: no harness rank opens a GPU (harness_holds_kfd false; the
+    stand-ins are the only "GPU processes"), one validator process per GPU
+    plus the plugin pod, and never more than 16 of them alive at once (the
+    box's per-user GPU-process limit, tools/storm_probe.py)."""
+    import json
+
+    from test_simcluster import _peak_concurrency
+
+    log_dir = str(tmp_path / "procs")
+    env = dict(os.environ, AMDGPU_FAKE_GPU_PROC_LOG=log_dir)
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+                        "--master-addr", "127.0.0.1", "--master-port=29615", "bench.py", "--gpus", "8", "--steps", "1",
+                        "--warmup", "0", "--fake-gpu-procs", "--mode", "process", "--compare", "0"],
+                       capture_output=True, text=True, timeout=240, cwd=os.path.dirname(HERE), env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0])
+    assert out["config"]["allocatable_amd_com_gpu"] == 8 and out["config"]["harness_holds_kfd"] is False
+    pw = out["config"]["pod_workload"]  # config 5 after Ready: 8 x 1 GPU, 1 x 8, 2 x 4
+    assert pw["pods"] == 11 and pw["all_succeeded"] and pw["single_gpu_pods_distinct_devices"]
+    assert pw["two_halves_numa_local"] and pw["two_halves_disjoint"]
+    peak, roles = _peak_concurrency(log_dir)
+    assert roles == {"validator": 8, "pod": 1 + 11}, roles  # the plugin-validation pod + the workload's pods
+    assert peak <= 16, peak

@@ -308,6 +308,8 @@ def test_driver_validation_and_wait(env):
 
 
 def test_workload_validation_launch_plan(env):
+    from amdgpu_operator.discovery import topology
+
     launched = []
 
     def launcher(argv, e, device, timeout):
@@ -318,32 +320,48 @@ def test_workload_validation_launch_plan(env):
         return ProcResult(0, json.dumps(rep), "", 0.01)
 
     env.launcher = launcher
+    gpus = topology.enumerate_gpus(env.host_root)
     out = V.validate_workload(env, ["--gemm", "1024", "--counter-gate"])
-    assert out["ok"] and out["world"] == 2
-    kernel = [a for a, _, _ in launched if "rccl" not in a[a.index("--steps") + 1]]
-    rccl = [a for a, _, _ in launched if a[a.index("--steps") + 1] == "hip,xgmi,rccl"]
-    assert len(kernel) == 2 and len(rccl) == 2
-    # kernel checks see only their own GPU (as HIP device 0); the xGMI IPC step
-    # runs in the RCCL processes, which see every GPU
-    kenv = [(a, e, d) for a, e, d in launched if a in kernel]
-    assert sorted(d for _, _, d in kenv) == [0, 1] and all(a[a.index("--device") + 1] == "0" for a, _, _ in kenv)
-    assert all(e.get("ROCR_VISIBLE_DEVICES", "").startswith("GPU-") for _, e, _ in kenv)
-    assert len({e["ROCR_VISIBLE_DEVICES"] for _, e, _ in kenv}) == 2
-    assert not any("ROCR_VISIBLE_DEVICES" in e for a, e, _ in launched if a in rccl)
-    assert all("--counter-gate" in a for a in kernel) and not any("--counter-gate" in a for a in rccl)
-    # the default AQL-packet gate needs no profiler tool in the process
-    assert {e.get("AMDGPU_VALIDATOR_COUNTERS") for a, e, _ in launched if a in kernel} == {None}
+    assert out["ok"] and out["world"] == 2 and out["processes"] == 2 and out["process_mode"] == "shared"
+    # one process per GPU: its kernel checks, the xGMI IPC step and RCCL
+    assert len(launched) == 2
+    for argv, e, device in launched:
+        assert argv[argv.index("--steps") + 1] == "hip,vecadd,gemm,mfma,hbm,xgmi,rccl"
+        assert argv[argv.index("--local-bdf") + 1] == gpus[device].bdf and "--counter-gate" in argv
+        # it sees its own GPU first, then its peer (RCCL and IPC need the peer visible)
+        assert e["ROCR_VISIBLE_DEVICES"].split(",")[0] == f"GPU-{gpus[device].unique_id:016x}"
+        assert len(e["ROCR_VISIBLE_DEVICES"].split(",")) == 2
+        assert "glibc.malloc.hugetlb=1" in e.get("GLIBC_TUNABLES", "")  # RCCL set-up on huge pages
+        # the default AQL-packet gate needs no profiler tool in the process
+        assert e.get("AMDGPU_VALIDATOR_COUNTERS") is None
+    assert sorted(d for _, _, d in launched) == [0, 1]
     names = [s["name"] for s in out["ranks"][0]["steps"]]
     assert names == ["hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl"]
     assert V.read_ready(env, "workload")["world"] == 2
-    launched.clear()
-    for f in os.listdir(env.validations_dir):
-        if f.endswith("-ready"):
-            os.unlink(os.path.join(env.validations_dir, f))
+
+    def reset():
+        launched.clear()
+        for f in os.listdir(env.validations_dir):
+            if f.endswith("-ready"):
+                os.unlink(os.path.join(env.validations_dir, f))
+
+    reset()
     V.validate_workload(env, ["--gemm", "1024", "--counter-gate", "--gate-mode", "sdk"])
+    assert launched and all(e.get("AMDGPU_VALIDATOR_COUNTERS") == "1" and "libamdgpu_counter_gate.so" in
+                            e.get("ROCP_TOOL_LIBRARIES", "") for _, e, _ in launched)
+    # rcclProcess: separate - kernel checks see only their own GPU; the xGMI IPC
+    # step and RCCL run in a second process per GPU, which sees every GPU
+    reset()
+    out = V.validate_workload(env, ["--gemm", "1024", "--counter-gate", "--rccl-separate-process"])
+    assert out["process_mode"] == "separate" and out["processes"] == 4
     kernel = [(a, e) for a, e, _ in launched if "rccl" not in a[a.index("--steps") + 1]]
-    assert kernel and all(e.get("AMDGPU_VALIDATOR_COUNTERS") == "1" and "libamdgpu_counter_gate.so" in
-                          e.get("ROCP_TOOL_LIBRARIES", "") for _, e in kernel)
+    rccl = [(a, e) for a, e, _ in launched if a[a.index("--steps") + 1] == "hip,xgmi,rccl"]
+    assert len(kernel) == 2 and len(rccl) == 2
+    assert all(len(e["ROCR_VISIBLE_DEVICES"].split(",")) == 1 for _, e in kernel)
+    assert all(len(e["ROCR_VISIBLE_DEVICES"].split(",")) == 2 for _, e in rccl)
+    assert all("--counter-gate" in a for a, _ in kernel) and not any("--counter-gate" in a for a, _ in rccl)
+    names = [s["name"] for s in out["ranks"][0]["steps"]]
+    assert names == ["hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl"]
 
 
 def test_workload_failure_is_reported(env):

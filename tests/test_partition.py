@@ -168,3 +168,81 @@ def test_memory_change_without_a_driver_container_fails_cleanly(node):
     assert not res["changed"] and "did not reload" in res["error"]
     assert _label(node, PM.STATE_LABEL) == "failed"
     assert all(_label(node, PM._deploy_label(o)) == "true" for o in PM.PAUSE_OPERANDS)
+
+
+def test_apply_waits_for_a_driver_health_amd_smi_poll(node):
+    """amd-driver-health is not paused for a change (it watches the driver
+    through the reload) and opens amd-smi every minute.  A poll under way
+    when the change starts makes the device BUSY; the change holds further
+    polls off (.smi-hold) and applies once the running one has ended."""
+    from amdgpu_operator.utils import smihold
+
+    be = PM.SysfsBackend(node.host_root, PM.sysfs_partition_rebuilder(node.host_root, 2),
+                         validations_dir=node.validations_dir)
+    node.client.patch("v1", "Node", "n1", {"metadata": {"labels": {"amd.com/gpu.partition-config": "all-qpx"}}})
+    in_poll, ended = threading.Event(), []
+
+    def poll():  # driver/manager.py publish_smi: one slow amd-smi session
+        with smihold.client(node.validations_dir) as allowed:
+            assert allowed
+            in_poll.set()
+            time.sleep(0.4)
+            ended.append(time.monotonic())
+
+    th = threading.Thread(target=poll)
+    th.start()
+    in_poll.wait(5)
+    with pytest.raises(PM.PartitionBusy, match="amd-smi clients"):  # the race the hold-off prevents
+        be.apply(0, PM.Profile("QPX", "NPS1"))
+    applied = []
+    real_apply = be.apply
+    be.apply = lambda p, prof: (applied.append(time.monotonic()), real_apply(p, prof))[1]
+    skipped = []
+
+    def later_polls():  # polls that start during the change are skipped, not raced
+        while not ended:
+            time.sleep(0.01)
+        with smihold.client(node.validations_dir) as allowed:
+            skipped.append(not allowed)
+
+    th2 = threading.Thread(target=later_polls)
+    th2.start()
+    with NodeAgents(node):
+        res = PM.reconcile_node(node, be, PROFILES, DEFAULT, timeout=10.0)
+    th.join()
+    th2.join()
+    assert res["changed"], res
+    assert applied and ended and min(applied) >= ended[0]  # applied only after the poll let go
+    assert skipped == [True]
+    assert _modes(node) == {("QPX", "NPS1")} and not smihold.held(node.validations_dir)
+
+
+def test_publish_smi_skips_its_poll_while_held(node):
+    from amdgpu_operator.utils import smihold
+
+    node.extra["_smi_published"] = ("ok: earlier", 0.0)
+    smihold.hold(node.validations_dir, "partition test")
+    assert DM.publish_smi(node, True, refresh_s=0.0) == "ok: earlier"  # no amd-smi session opened
+    smihold.release(node.validations_dir)
+
+
+def test_failed_unload_during_a_reload_restores_driver_ready(node, monkeypatch):
+    """a reload whose unload fails (amdgpu still in use) must not
+    leave the node's operands gated on a driver-ready that never comes: the
+    module is still live, so driver-ready is written again at once (and the
+    loss marker leaves the recovery to the health monitor otherwise)."""
+    from amdgpu_operator.validator.validate import read_ready
+
+    DM.install(node, timeout=5)
+    kmod = node.extra["kmod"]
+
+    def busy_unload(env=None, timeout=0.0):
+        raise RuntimeError("rmmod: amdgpu in use")
+
+    monkeypatch.setattr(kmod, "unload", busy_unload)
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="in use"):
+        DM.reload_module(node, {}, "memory partition NPS2")
+    ready = read_ready(node, "driver")
+    assert ready and ready["time"] >= t0 and ready.get("recovered")
+    assert not os.path.exists(node.validation_file(DM.LOST_MARKER))  # claimed by the recovery

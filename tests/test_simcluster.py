@@ -251,7 +251,8 @@ def test_partition_manager_repartitions_node(cluster_factory, tmp_path):
 
     c = cluster_factory([NodeSpec("gpu-1", 2)])
     env = c.nodes["gpu-1"].env
-    env.extra["partition_backend"] = PM.SysfsBackend(env.host_root, PM.sysfs_partition_rebuilder(env.host_root, 2))
+    env.extra["partition_backend"] = PM.SysfsBackend(env.host_root, PM.sysfs_partition_rebuilder(env.host_root, 2),
+                                                     validations_dir=env.validations_dir)
     c.install_operator(parse_set_flags(REFERENCE_SET_FLAGS + ["migManager.enabled=true"]))
     c.wait_ready(60, {"gpu-1": 2})
     assert labels(c, "gpu-1")[PM.STATE_LABEL] == "success"
@@ -350,3 +351,107 @@ def test_bring_up_over_http_rest_client(cluster_factory):
     assert "amd.com/gpu.present" not in labels(c, "cpu-1")
     rep = verify(c.agent_client, c.namespace, expect_gpus_per_node=2)
     assert rep.ok, rep.as_dict()
+
+
+def _peak_concurrency(log_dir) -> tuple[int, dict]:
+    """Largest number of stand-in GPU processes alive at once (their logged
+    lifetimes, testing/fake_validator.py AMDGPU_FAKE_GPU_PROC_LOG)."""
+    recs = [json.load(open(os.path.join(log_dir, f))) for f in os.listdir(log_dir)]
+    ev = sorted([(r["start"], 1) for r in recs] + [(r["end"], -1) for r in recs], key=lambda e: (e[0], e[1]))
+    cur = peak = 0
+    for _, d in ev:
+        cur += d
+        peak = max(peak, cur)
+    roles = {}
+    for r in recs:
+        roles[r["role"]] = roles.get(r["role"], 0) + 1
+    return peak, roles
+
+
+def test_8x_cpx_node_validates_64_partitions_within_the_process_budget(tmp_path, monkeypatch):
+    """An 8-GPU node in CPX (64 partitions): the validation starts one
+    workload process per physical GPU plus the plugin pod - at most 16 GPU
+    processes alive at once - and reports every partition's kernel steps."""
+    log_dir = str(tmp_path / "procs")
+    monkeypatch.setenv("AMDGPU_FAKE_GPU_PROC_LOG", log_dir)
+    c = SimCluster(str(tmp_path / "c"), [NodeSpec("gpu-1", 8, "CPX", "NPS2")], fake_gpu="procs").start()
+    try:
+        c.install_operator(REF)
+        c.wait_ready(120, {"gpu-1": 64})
+        from amdgpu_operator.validator.validate import read_ready
+
+        wl = read_ready(c.nodes["gpu-1"].env, "workload")
+        assert wl["world"] == 8 and wl["devices"] == 64 and wl["processes"] == 8
+        for rep in wl["ranks"]:
+            for step in ("vecadd", "gemm"):
+                assert sorted(s["device"] for s in rep["steps"] if s["name"] == step) == list(range(8))
+        peak, roles = _peak_concurrency(log_dir)
+        assert roles == {"validator": 8, "pod": 1}, roles
+        assert peak <= 16, peak
+    finally:
+        c.stop()
+
+
+def test_plugin_pod_missing_an_allocated_device_fails(cluster_factory):
+    """The runtime leaves one of a pod's two allocated GPUs out of the
+    container: the pod's check fails (it is told how many it was given)
+    instead of passing on the one it sees, and the node is not validated."""
+    c = cluster_factory([NodeSpec("gpu-1", 2)])
+    c.hook_drop_devices = 1
+    c.install_operator(REF)
+    deadline = time.time() + 20
+    msg = ""
+    while time.time() < deadline and "1 visible" not in msg:
+        msg = " ".join(((p.get("status") or {}).get("message") or "") for p in c.pods())
+        msg += json.dumps([e for e in c.client.list("v1", "Event")])[-20000:]
+        time.sleep(0.1)
+    assert "2 GPU(s) allocated to the pod, 1 visible" in msg
+    assert labels(c, "gpu-1").get("amd.com/gpu.validated") != "true"
+    c.hook_drop_devices = 0  # the runtime is fixed: the validator's retry validates the node
+    c.wait_ready(60, {"gpu-1": 2})
+
+
+def test_config5_pod_workload_on_an_8_gpu_hive(cluster_factory):
+    """BASELINE config 5 after Ready: 8 pods x 1 GPU land on 8 distinct GPUs,
+    one pod takes all 8, and 2 x 4-GPU pods get disjoint NUMA-local halves
+    whose every pair is xGMI-linked - each through admission,
+    GetPreferredAllocation, Allocate and the OCI hook, running the GEMM pod
+    command with --expect-devices."""
+    from amdgpu_operator.discovery import topology
+    from amdgpu_operator.testing.podworkload import run_pod_workload
+
+    c = cluster_factory([NodeSpec("gpu-1", 8)])
+    c.install_operator(REF)
+    c.wait_ready(60)
+    out = run_pod_workload(c, "gpu-1", 8)
+    assert out["pods"] == 8 + 1 + 2 and out["all_succeeded"] and out["gemm_correct"]
+    assert out["single_gpu_pods_distinct_devices"] and out["two_halves_numa_local"] and out["two_halves_disjoint"]
+    assert out["admission_to_kernel_done_p50_s"] is not None and out["admission_to_kernel_done_p99_s"] is not None
+    assert len(out["batches"]["whole_node"][0]["devices"]) == 8
+    root = c.nodes["gpu-1"].env.sysfs_root()
+    gpus = {g.bdf: g for g in topology.enumerate_gpus(root)}
+    xgmi = {(lk.src, lk.dst) for lk in topology.links(root) if lk.is_xgmi}
+    for half in out["batches"]["two_halves"]:
+        idx = [gpus[d].index for d in half["devices"]]
+        assert len(idx) == 4 and all((a, b) in xgmi for a in idx for b in idx if a != b)
+        assert len({gpus[d].numa_node for d in half["devices"]}) == 1
+    # the kubelet's pod-resources view matches what the pods were given
+    assert all(p["phase"] == "Succeeded" for b in out["batches"].values() for p in b)
+
+
+def test_per_device_plugin_validation_pods(cluster_factory):
+    """validator.pluginPods=perDevice: 8 one-GPU pods, each its own
+    allocation, on 8 distinct GPUs; past the GPU-process budget (2 x CPX = 16
+    partitions + 2 workload processes > 16) it falls back to one pod per
+    resource and says so."""
+    from amdgpu_operator.validator.validate import read_ready
+
+    flags = parse_set_flags(REFERENCE_SET_FLAGS + ["validator.pluginPods=perDevice"])
+    c = cluster_factory([NodeSpec("gpu-1", 8), NodeSpec("gpu-2", 2, "CPX", "NPS2")])
+    c.install_operator(flags)
+    c.wait_ready(90, {"gpu-1": 8, "gpu-2": 16})
+    p1 = read_ready(c.nodes["gpu-1"].env, "plugin")
+    assert p1["pod_mode"] == "perDevice" and p1["pods"] == 8 and len(set(p1["devices"])) == 8
+    p2 = read_ready(c.nodes["gpu-2"].env, "plugin")
+    assert p2["pod_mode"] == "perResource" and p2["pods"] == 1 and "exceed" in p2["pod_mode_fallback"]
+    assert p2["devices_validated"] == 16

@@ -165,3 +165,82 @@ def test_gpu_check_runs_a_kernel_per_visible_gpu():
     adds = [s for s in rep["steps"] if s["name"] == "vecadd"]
     assert len(adds) == rep["devices"] and all(s["mismatches"] == 0 and s["elems"] == 65536 for s in adds)
     assert all(s["agent"].startswith("gfx950") for s in rep["steps"] if s["name"] == "hsa")
+
+
+def test_local_bdf_selects_the_gpu_and_checks_the_device_count(tmp_path):
+    """One process per physical GPU (validate.py rank_plan): --local-bdf picks
+    every visible device at the GPU's PCI address (the GPU in SPX, its
+    partitions otherwise); --expect-devices fails a process that sees fewer."""
+    from amdgpu_operator.discovery import topology
+
+    gpu = topology.enumerate_gpus("/")[0]
+    rc, rep, st = _local(tmp_path, "hip,vecadd,gemm", ["--local-bdf", gpu.bdf.upper(), "--expect-devices", "1",
+                                                        "--gemm", "1024", "--counter-gate"])
+    assert rc == 0 and rep["ok"] and rep["local_devices"] == [0], rep
+    assert st["gemm"]["counter_gate"] == "pass"
+    rc, rep, _ = _local(tmp_path, "hip,vecadd", ["--local-bdf", gpu.bdf, "--expect-devices", "2"])
+    assert rc == 1 and "2 device(s) expected, 1 visible" in rep["error"], rep
+    rc, rep, _ = _local(tmp_path, "hip,vecadd", ["--local-bdf", "0000:ff:1f.7"])
+    assert rc == 1 and "no visible device at 0000:ff:1f.7" in rep["error"], rep
+
+
+def test_all_devices_threaded_path_with_counter_gate(tmp_path):
+    """--all-devices runs each device's steps on a thread of its own (with
+    several devices the gated GEMM goes last, GateTurns); on this box that
+    is one device, in the single-device step order."""
+    rc, rep, _ = _local(tmp_path, "hip,vecadd,gemm,hbm", ["--all-devices", "--gemm", "1024", "--counter-gate",
+                                                          "--hbm-bytes", str(1 << 26)])
+    assert rc == 0 and rep["ok"], rep
+    names = [(s["device"], s["name"]) for s in rep["steps"]]
+    assert names == [(0, "hip"), (0, "vecadd"), (0, "gemm"), (0, "hbm")], names
+    g = [s for s in rep["steps"] if s["name"] == "gemm"][0]
+    assert g["counter_gate"] == "pass" and g["gated_output_matches"]
+
+
+def test_gpu_check_fails_when_an_allocated_gpu_is_missing():
+    check = str(native.binary("amdgpu-gpu-check"))
+    p = subprocess.run([check, "--timeout", "20", "--expect-devices", "2"], capture_output=True, text=True, timeout=60)
+    rep = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 1 and "2 GPU(s) allocated to the pod, 1 visible" in rep["error"], rep
+    p = subprocess.run([check, "--timeout", "20", "--expect-devices", "1"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stdout
+
+
+def test_ipc_one_shot_eight_processes_one_gpu(tmp_path):
+    """K4's multi-process path at its full width: 8 ranks (8 processes) on one
+    GPU exchange IPC handles and each reads all 8 buffers; a peer-read floor
+    above what the device delivers fails every rank (the N >= 2 gate)."""
+    def run(extra, tag):
+        procs = [subprocess.Popen([VALIDATOR, "--rank", str(r), "--world", "8", "--device", "0", "--rendezvous",
+                                   str(tmp_path / tag), "--run-id", tag, "--steps", "hip,xgmi", "--xgmi-elems",
+                                   str(1 << 20), "--peer-timeout", "60", *extra],
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(8)]
+        outs = [p.communicate(timeout=120) for p in procs]
+        return [(p.returncode, json.loads(o.strip().splitlines()[-1]), e) for p, (o, e) in zip(procs, outs)]
+
+    reps = run([], "ok")
+    for rc, rep, err in reps:
+        assert rc == 0 and rep["ok"], (rep, err[-2000:])
+        x = {s["name"]: s for s in rep["steps"]}["xgmi"]
+        assert not x["emulated"] and x["peers"] == 8 and x["max_abs_err"] <= 8e-5 and x["peer_read_gbps"] > 0
+    print(json.dumps([{s["name"]: s for s in r["steps"]}["xgmi"]["peer_read_gbps"] for _, r, _ in reps]))
+    for rc, rep, _ in run(["--min-xgmi-read-gbps", "1e9"], "floor"):
+        x = {s["name"]: s for s in rep["steps"]}["xgmi"]
+        assert rc == 1 and x["perf_ok"] is False and x["max_abs_err"] <= 8e-5
+
+
+def test_xgmi_link_rate_matches_the_kfd_nominal_on_mi355x():
+    """The link-rate check of validate.check_fabric on real data: amd-smi's
+    xGMI rate x width of this GPU against the KFD nominal of its XGMI
+    io_links (76 GB/s per direction) - a healthy GPU must pass."""
+    from amdgpu_operator.discovery import topology
+
+    with topology.Smi() as smi:
+        ms = smi.collect()
+    vals = ms[0].values
+    nominal = [lk.max_bandwidth_mbps / 1000 for lk in topology.links("/") if lk.is_xgmi and lk.max_bandwidth_mbps]
+    print(json.dumps({"speed": vals.get("xgmi_link_speed_gbps"), "width": vals.get("xgmi_link_width"),
+                      "up": vals.get("xgmi_links_up"), "nominal": sorted(set(nominal))}))
+    if not vals.get("xgmi_link_speed_gbps") or not vals.get("xgmi_link_width") or not nominal:
+        pytest.skip("amd-smi reports no xGMI rate/width here")
+    assert vals["xgmi_link_speed_gbps"] * vals["xgmi_link_width"] / 8 >= 0.9 * min(nominal)

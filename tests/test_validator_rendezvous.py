@@ -135,9 +135,9 @@ def env8(tmp_path):
 
 
 def test_sibling_failure_cancels_a_hanging_rank(env8, monkeypatch):
-    # rank 1's RCCL process hangs (alive, not waiting on anyone); rank 0's
-    # kernel process fails: the orchestrator's abort file ends the hang
-    monkeypatch.setenv("AMDGPU_FAKE_VALIDATOR_FAULT", "-rccl:1:hang,*:0:fail")
+    # rank 1 hangs (alive, not waiting on anyone); rank 0 fails: the
+    # orchestrator's abort file ends the hang
+    monkeypatch.setenv("AMDGPU_FAKE_VALIDATOR_FAULT", "*:1:hang,*:0:fail")
     t0 = time.monotonic()
     with pytest.raises(V.StepFailed) as ei:
         V.validate_workload(env8, ["--peer-timeout", "60"], timeout=120)
@@ -148,8 +148,15 @@ def test_sibling_failure_cancels_a_hanging_rank(env8, monkeypatch):
     assert not os.listdir(os.path.join(env8.validations_dir, "rendezvous"))  # run dir removed
 
 
+def test_separate_rccl_process_hang_is_cancelled(env8, monkeypatch):
+    # the second-process layout (rcclProcess: separate): its RCCL process hangs
+    monkeypatch.setenv("AMDGPU_FAKE_VALIDATOR_FAULT", "-rccl:1:hang,*:0:fail")
+    with pytest.raises(V.StepFailed, match="injected failure"):
+        V.validate_workload(env8, ["--peer-timeout", "60", "--rccl-separate-process"], timeout=120)
+
+
 def test_rank_exiting_without_report_is_named(env8, monkeypatch):
-    monkeypatch.setenv("AMDGPU_FAKE_VALIDATOR_FAULT", "-rccl:1:exit")
+    monkeypatch.setenv("AMDGPU_FAKE_VALIDATOR_FAULT", "*:1:exit")
     t0 = time.monotonic()
     with pytest.raises(V.StepFailed) as ei:
         V.validate_workload(env8, ["--peer-timeout", "60"], timeout=120)
@@ -161,7 +168,7 @@ def test_rank_never_started_fails_within_peer_timeout(env8, monkeypatch):
     real = env8.launcher
 
     def launcher(argv, e, device, timeout):
-        if argv[argv.index("--run-id") + 1].endswith("-rccl") and argv[argv.index("--rank") + 1] == "1":
+        if argv[argv.index("--rank") + 1] == "1":
             time.sleep(0.1)
             return ProcResult(127, "", "exec failed: no such file", 0.1)  # never ran
         return real(argv, e, device, timeout)
@@ -182,12 +189,96 @@ def test_validate_flags_translate_to_the_binary(env8, monkeypatch):
         return real(argv, e, device, timeout)
 
     env8.launcher = launcher
-    out = V.validate_workload(env8, ["--rccl-busbw-per-peer", "15", "--require-xgmi-links", "--min-mfma-util", "0.2"])
+    out = V.validate_workload(env8, ["--rccl-busbw-link-fraction", "0.2", "--xgmi-read-link-fraction", "0.25",
+                                     "--require-xgmi-links", "--min-mfma-util", "0.2"])
     assert out["ok"] and out["fabric"]["ok"] and out["fabric"]["physical_gpus"] == 2
+    # one 76 GB/s link per rank (KFD io_links): busBW 0.2 x 76 x 64/(64+16) MiB, reads 0.25 x 76
+    assert out["floors"] == {"link_gbps_per_rank": [76.0, 76.0], "min_rccl_busbw_gbps": 12.2,
+                             "min_xgmi_peer_read_gbps": 19.0}
+    assert len(seen) == 2 and out["processes"] == 2 and out["process_mode"] == "shared"
     for a in seen:
-        assert "--rccl-busbw-per-peer" not in a and "--require-xgmi-links" not in a
-        assert a[a.index("--min-rccl-busbw-gbps") + 1] == "15"  # 15 x (2 - 1)
+        for own in ("--rccl-busbw-link-fraction", "--xgmi-read-link-fraction", "--require-xgmi-links",
+                    "--max-gpu-processes"):
+            assert own not in a
+        assert a[a.index("--min-rccl-busbw-gbps") + 1] == "12.2"
+        assert a[a.index("--min-xgmi-read-gbps") + 1] == "19"
         assert a[a.index("--min-mfma-util") + 1] == "0.2"
+        assert a[a.index("--steps") + 1] == "hip,vecadd,gemm,mfma,hbm,xgmi,rccl"  # one process per GPU
+
+
+# ------------------------------------------- process layout and budget ----
+
+def _fake_env(tmp_path, gpus, partition="SPX"):
+    root = str(tmp_path / "h")
+    fakesys.build_node(root, gpus, compute_partition=partition)
+    env = NodeEnv("n1", None, host_root=root, validations_dir=str(tmp_path / "v"), poll_s=0.01)
+    calls = []
+
+    def launcher(argv, e, device, timeout):
+        calls.append((argv, e, device))
+        return run_local([sys.executable, "-m", "amdgpu_operator.testing.fake_validator", *argv[1:]], e, timeout)
+
+    env.launcher = launcher
+    return env, calls
+
+
+def _by_rank(calls):
+    return sorted(calls, key=lambda c: int(c[0][c[0].index("--rank") + 1]))
+
+
+def test_eight_gpus_start_eight_processes_each_seeing_its_peers(tmp_path):
+    from amdgpu_operator.discovery import topology
+
+    env, calls = _fake_env(tmp_path, 8)
+    gpus = topology.enumerate_gpus(env.host_root)
+    out = V.validate_workload(env, ["--peer-timeout", "60"])
+    assert out["processes"] == 8 and out["world"] == 8 and len(calls) == 8
+    for rank, (argv, e, device) in enumerate(_by_rank(calls)):
+        assert device == rank and argv[argv.index("--local-bdf") + 1] == gpus[rank].bdf
+        ids = e["ROCR_VISIBLE_DEVICES"].split(",")
+        assert len(ids) == 8 and ids[0] == f"GPU-{gpus[rank].unique_id:016x}"  # own GPU first, then its 7 peers
+
+
+def test_separate_rccl_processes_only_within_the_budget(tmp_path):
+    env, calls = _fake_env(tmp_path, 8)
+    out = V.validate_workload(env, ["--peer-timeout", "60", "--rccl-separate-process"], budget=15)
+    assert out["process_mode"] == "shared" and out["processes"] == 8  # 16 would not fit
+    env2, calls2 = _fake_env(tmp_path / "b", 2)
+    out = V.validate_workload(env2, ["--peer-timeout", "60", "--rccl-separate-process"], budget=15)
+    assert out["process_mode"] == "separate" and out["processes"] == 4
+    assert V.planned_workload_processes(env, ["--rccl-separate-process"], 15) == 8
+    assert V.planned_workload_processes(env2, ["--rccl-separate-process"], 15) == 4
+
+
+def test_cpx_node_validates_every_partition_from_one_process_per_gpu(tmp_path):
+    """8 x CPX = 64 partitions: 8 processes (not 64 + 64), a communicator of 8
+    physical ranks, and every partition's kernel steps reported."""
+    env, calls = _fake_env(tmp_path, 8, "CPX")
+    out = V.validate_workload(env, ["--peer-timeout", "60"])
+    assert out["devices"] == 64 and out["world"] == 8 and out["processes"] == 8 and len(calls) == 8
+    for rank, rep in enumerate(out["ranks"]):
+        for step in ("vecadd", "gemm", "mfma", "hbm"):
+            assert sorted(s["device"] for s in rep["steps"] if s["name"] == step) == list(range(8)), (rank, step)
+        names = [s["name"] for s in rep["steps"]]
+        assert names.count("xgmi") == 1 and names.count("rccl") == 1  # xGMI + RCCL across the physical GPUs
+    for rank, (argv, e, _) in enumerate(_by_rank(calls)):
+        assert argv[argv.index("--world") + 1] == "8" and argv[argv.index("--expect-devices") + 1] == "8"
+        assert len(e["ROCR_VISIBLE_DEVICES"].split(",")) == 8 + 7  # its 8 partitions + one device of each peer
+
+
+def test_a_partition_missing_from_a_rank_fails_the_run(tmp_path, monkeypatch):
+    env, calls = _fake_env(tmp_path, 2, "CPX")
+    real = env.launcher
+
+    def launcher(argv, e, device, timeout):  # rank 1's process sees only 7 of its 8 partitions
+        if argv[argv.index("--rank") + 1] == "1":
+            argv = list(argv)
+            argv[argv.index("--expect-devices") + 1] = "7"
+        return real(argv, e, device, timeout)
+
+    env.launcher = launcher
+    with pytest.raises(V.StepFailed, match="rank 1: 7 of 8 devices validated"):
+        V.validate_workload(env, ["--peer-timeout", "60"])
 
 
 # ------------------------------------------------------------ fabric ----
@@ -233,3 +324,43 @@ def test_fabric_check_skips_partitions_of_one_gpu(tmp_path):
     assert len(gpus) == 8
     out = V.check_fabric(env, gpus, [])
     assert out["ok"] and out["physical_gpus"] == 1 and "skipped" in out
+
+
+def test_half_rate_links_fail_closed(tmp_path):
+    """Every link "up", but trained to half its rate: amd-smi's rate x width
+    against the KFD nominal (76 GB/s per direction on MI355X) names it."""
+    from amdgpu_operator.discovery import topology
+
+    root = str(tmp_path / "h")
+    fakesys.build_node(root, 8)
+    env = NodeEnv("n1", None, host_root=root, validations_dir=str(tmp_path / "v"))
+    gpus = topology.enumerate_gpus(root)
+
+    def m(g, speed, width=16):
+        x = _M(g.bdf, 7)
+        x.values.update(xgmi_link_speed_gbps=speed, xgmi_link_width=width)
+        return x
+
+    ok = V.check_fabric(env, gpus, [m(g, 38) for g in gpus])
+    assert ok["ok"] and ok["links"][gpus[0].bdf]["link_gbps"] == 76.0
+    half = V.check_fabric(env, gpus, [m(g, 19) for g in gpus])
+    assert not half["ok"] and all(any(g.bdf in p and "nominal 76 GB/s" in p for p in half["problems"]) for g in gpus)
+    narrow = V.check_fabric(env, gpus, [m(g, 38, 8 if g.index == 2 else 16) for g in gpus])
+    assert not narrow["ok"] and len(narrow["problems"]) == 1 and gpus[2].bdf in narrow["problems"][0]
+
+
+def test_throughput_floors_scale_with_the_links(tmp_path):
+    from amdgpu_operator.discovery import topology
+
+    root = str(tmp_path / "h")
+    fakesys.build_node(root, 8)
+    env = NodeEnv("n1", None, host_root=root, validations_dir=str(tmp_path / "v"))
+    gpus = topology.enumerate_gpus(root)
+    plan = V.rank_plan(gpus)
+    f = V.fabric_floors(env, plan, gpus, 0.2, 0.25, 64 << 20)
+    assert f["link_gbps_per_rank"] == [532.0] * 8  # 7 links x 76 GB/s
+    assert f["min_rccl_busbw_gbps"] == 85.1 and f["min_xgmi_peer_read_gbps"] == 133.0
+    small = V.fabric_floors(env, plan, gpus, 0.2, 0.25, 1 << 20)  # latency-bound size: a lower busBW floor
+    assert small["min_rccl_busbw_gbps"] < 10
+    four = V.fabric_floors(env, plan[:4], gpus, 0.2, 0.25, 64 << 20)
+    assert four["link_gbps_per_rank"] == [228.0] * 4

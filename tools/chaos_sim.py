@@ -93,7 +93,8 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
         for n in mode:  # partition changes act on the fake sysfs tree
             env = c.nodes[n].env
             env.extra["partition_backend"] = PM.SysfsBackend(env.host_root,
-                                                             PM.sysfs_partition_rebuilder(env.host_root, 2))
+                                                             PM.sysfs_partition_rebuilder(env.host_root, 2),
+                                                             validations_dir=env.validations_dir)
 
     def expect():
         return {n: ((8 * n_gpus if cpx[n] else n_gpus) if m == "container" else {"amd.com/MI355X": n_gpus})
