@@ -312,10 +312,14 @@ class Session:
             except (OSError, ValueError, _Dead) as e:
                 conn.close()
                 raise ConnectionError(f"{method} {url}: {e}") from e
+        idempotent = method in ("GET", "HEAD", "OPTIONS")
         for attempt in (0, 1):
             conn, reused = self._pooled(scheme, netloc, connect_t)
+            sent = False
             try:
                 conn.send(method, path, hdrs, body)
+                sent = True
+                conn.settimeout(read_t)
                 status, headers, closes = conn.read_head()
                 h = Headers(headers)
                 payload = _Body(conn._rfile, h, method, status).read()
@@ -324,8 +328,11 @@ class Session:
                 return Response(status, h, body=payload)
             except (_Dead, ConnectionResetError, BrokenPipeError) as e:
                 conn.close()
-                if reused and attempt == 0:
-                    continue  # the server had closed the kept-alive connection: nothing was processed
+                # a kept-alive connection the server had closed: resend when the
+                # request never left, or when running it twice is harmless; a
+                # write that went out may have been applied, so it is not resent
+                if reused and attempt == 0 and (not sent or idempotent):
+                    continue
                 raise ConnectionError(f"{method} {url}: {e}") from e
             except (OSError, ValueError) as e:
                 conn.close()

@@ -396,6 +396,8 @@ class Connection:
                         self.send_rst(s, REFUSED_STREAM)
                         return
                     st = self.streams[s] = _Stream(s, self.peer_initial_window)
+                elif st.ended:  # the peer already closed its side: no second request or reply
+                    return
                 on_headers(st, headers, bool(f0 & END_STREAM))
                 if f0 & END_STREAM:
                     st.ended = True
@@ -406,6 +408,8 @@ class Connection:
             st = self.streams.get(sid)
             self._credit(st, len(payload))
             if st is None:
+                return
+            if st.ended:  # DATA after END_STREAM (half-closed remote): dropped, the call runs once
                 return
             if not st.too_big:
                 st.body += data

@@ -507,6 +507,51 @@ def test_server_limits(our_server):
     assert b"12345678" in got
 
 
+def test_frames_after_end_stream_do_not_run_the_call_again(our_server):
+    """a DATA or HEADERS frame with END_STREAM on a stream that
+    already ended is dropped - one handler run, one reply, one trailer."""
+    import socket
+
+    path, _ = our_server
+    req = api.pb["AllocateRequest"]()
+    req.container_requests.add(devices_ids=["5"])
+    msg = req.SerializeToString()
+    body = b"\x00" + len(msg).to_bytes(4, "big") + msg
+    head = [(":method", "POST"), (":scheme", "http"), (":authority", "x"),
+            (":path", api.method_path(api.DEVICE_PLUGIN_SERVICE, "Allocate")),
+            ("content-type", "application/grpc"), ("te", "trailers")]
+    F = wire.Connection.frame
+    frames = (F(wire.HEADERS, wire.END_HEADERS, 1, hpack.encode(head)) + F(wire.DATA, wire.END_STREAM, 1, body)
+              + F(wire.DATA, wire.END_STREAM, 1, body)
+              + F(wire.HEADERS, wire.END_HEADERS | wire.END_STREAM, 1, hpack.encode(head)))
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    s.connect(path)
+    got = b""
+    try:
+        s.sendall(wire.PREFACE + F(wire.SETTINGS, 0, 0) + frames)
+        s.settimeout(1.0)
+        while True:
+            try:
+                chunk = s.recv(65536)
+            except socket.timeout:
+                break
+            if not chunk:
+                break
+            got += chunk
+    finally:
+        s.close()
+    seen = []
+    pos = 0
+    while pos + 9 <= len(got):
+        n = int.from_bytes(got[pos:pos + 3], "big")
+        ftype, flags, sid = got[pos + 3], got[pos + 4], int.from_bytes(got[pos + 5:pos + 9], "big") & 0x7FFFFFFF
+        if sid == 1:
+            seen.append((ftype, bool(flags & wire.END_STREAM)))
+        pos += 9 + n
+    assert seen.count((wire.DATA, False)) == 1  # the reply message
+    assert sum(1 for t, end in seen if t == wire.HEADERS and end) == 1  # the trailers
+
+
 def test_hpack_decoded_size_is_bounded():
     d = hpack.Decoder(4096, max_list_size=64 << 10)
     big = bytearray(b"\x40\x05x-big")  # literal with incremental indexing, new name

@@ -7,6 +7,7 @@ import socket
 import ssl
 import subprocess
 import threading
+import time
 
 import pytest
 
@@ -15,7 +16,8 @@ from amdgpu_operator.kube import transport as T
 
 class RawServer:
     """Accepts connections and answers each request with the next scripted
-    response bytes (``None``: close the connection without answering)."""
+    response bytes (``None``: close the connection without answering; ``b""``:
+    hold it unanswered for 2 s, then close)."""
 
     def __init__(self, responses, tls=None):
         self.responses = list(responses)
@@ -56,6 +58,9 @@ class RawServer:
                 self.requests.append(head + f.read(n))
                 out = self.responses.pop(0)
                 if out is None:
+                    break
+                if out == b"":
+                    time.sleep(2)
                     break
                 c.sendall(out)
                 if b"Connection: close" in out:
@@ -110,6 +115,28 @@ def test_a_kept_alive_connection_the_server_dropped_is_retried_once():
     assert s.request("GET", srv.url() + "/a", timeout=5).text == "1"
     assert s.request("GET", srv.url() + "/b", timeout=5).text == "2"
     assert srv.connections == 2
+
+
+def test_a_write_the_dropped_connection_may_have_taken_is_not_resent():
+    """the request went out whole before the server closed, so it
+    may have been applied: a POST is not sent a second time."""
+    srv = RawServer([ok(b"1"), None, ok(b"2")])
+    s = T.Session()
+    assert s.request("GET", srv.url() + "/a", timeout=5).text == "1"
+    with pytest.raises(ConnectionError):
+        s.request("POST", srv.url() + "/b", timeout=5, data="{}")
+    assert [r.split(b" ")[0] for r in srv.requests] == [b"GET", b"POST"]
+    assert s.request("GET", srv.url() + "/c", timeout=5).text == "2"  # a fresh connection
+
+
+def test_the_read_timeout_holds_on_a_kept_alive_connection():
+    srv = RawServer([ok(b"1"), b""])
+    s = T.Session()
+    assert s.request("GET", srv.url() + "/a", timeout=(5, 0.3)).text == "1"
+    t0 = time.monotonic()
+    with pytest.raises((socket.timeout, ConnectionError)):
+        s.request("GET", srv.url() + "/b", timeout=(5, 0.3))
+    assert time.monotonic() - t0 < 1.5
 
 
 def test_connection_refused_is_a_connection_error():
