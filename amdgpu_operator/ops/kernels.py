@@ -146,18 +146,23 @@ def vector_add_verify(a, b, c, stream=None) -> int:
     return int(bad.item())
 
 
-GEMM_DEFAULT_VARIANT = 6
+GEMM_DEFAULT_VARIANT = 24   # 4 waves x 128x128, generated main loop (K a multiple of 256)
+GEMM_FALLBACK_VARIANT = 6   # 8-phase, 8 waves (K a multiple of 64)
+GEMM_DEFAULT_K_MULTIPLE = 256
+# variants in the shipped library; the rest need `make -C native lab`
+SHIPPED_GEMM_VARIANTS = (6, 15, 24, 25)
 
 
-def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int = GEMM_DEFAULT_VARIANT):
+def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int | None = None):
     """K2: ``out[M,N] = a[M,K] @ bt[N,K].T`` on MFMA (bf16 in, fp32 accumulate).
 
-    M and N must be multiples of 256 and K of 64 (the kernel has no edge
-    tiles; the validator picks its shapes accordingly).  ``variant`` selects
-    the kernel: 6 (default) is the 8-phase quadrant pipeline the native
-    validator runs and the only one in the shipped library; 0-5 and 7-9 are
-    the A/B kernels of rounds 1-2, served from the tools build
-    (``make -C native lab``).
+    M and N must be multiples of 256 and K of 64 (the kernels have no edge
+    tiles; the validator picks its shapes accordingly).  ``variant=None`` runs
+    what the native validator runs: the 4-wave kernel (GEMM_DEFAULT_VARIANT)
+    when K is a multiple of 256, else the 8-phase kernel
+    (GEMM_FALLBACK_VARIANT).  15 and 25 are the other generated schedules of
+    the 4-wave kernel; the A/B kernels of rounds 1-4 are served from the tools
+    build (``make -C native lab``).
     """
     import torch
 
@@ -174,7 +179,9 @@ def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int = GE
     if out.shape != (M, N) or out.dtype not in (torch.bfloat16, torch.float32):
         raise ValueError("bad GEMM output")
     _require(out, out.dtype, "out")
-    lib = _lib() if variant == GEMM_DEFAULT_VARIANT else _lib(LAB_LIB_NAME)
+    if variant is None:
+        variant = GEMM_DEFAULT_VARIANT if K % GEMM_DEFAULT_K_MULTIPLE == 0 else GEMM_FALLBACK_VARIANT
+    lib = _lib() if variant in SHIPPED_GEMM_VARIANTS else _lib(LAB_LIB_NAME)
     rc = lib.avk_gemm_bf16_nt_variant(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
                                       M, N, K, variant, _stream(stream))
     _check(rc, "gemm_bf16_nt")

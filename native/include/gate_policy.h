@@ -1,18 +1,18 @@
 // N7 counter-gate policy: the verdict on one counted dispatch of the
-// validator's MFMA GEMM (gemm_bf16_nt_8p_kernel, 256x256 tiles, 8 waves per
-// workgroup, v_mfma_f32_16x16x32_bf16).
+// validator's default MFMA GEMM (gemm_default.h: 256x256 tiles,
+// kGemmWavesPerTile waves per workgroup, v_mfma_f32_16x16x32_bf16).
 //
 // The counters of that dispatch are not noisy measurements but exact
 // functions of the launch (BASELINE.md "Round 2: ... AQL-packet gate",
 // profiles/r2_gate/aql_v2.json at 4096^3):
 //   SQ_INSTS_VALU_MFMA_MOPS_BF16 * 512 == 2 * M * N * K   (1 MOP = 512 FLOP)
-//   SQ_WAVES == (M/256) * (N/256) * 8
+//   SQ_WAVES == (M/256) * (N/256) * kGemmWavesPerTile
 // A GPU that drops or duplicates work (a dead CU that never retires its
 // waves, a mis-scheduled dispatch, a corrupted code object) breaks the
 // equalities even when the output checksum happens to match.  The third
 // condition is time-based: MFMA busy cycles over elapsed GPU cycles per SIMD,
 // SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per XCD * SIMDs).  At 4096^3 on
-// a healthy MI355X it reads ~0.49; a starved matrix pipe (HBM stack running
+// a healthy MI355X it read ~0.49 with round 3's 8-wave kernel; a starved matrix pipe (HBM stack running
 // slow, CUs fenced off, the GEMM waiting on a throttled fabric) pulls it down.
 // The floor scales with how many CUs the launch can occupy (tiles / CUs,
 // capped at 1), so a 1024^3 plugin-pod GEMM (16 tiles on 256 CUs) is held to
@@ -26,6 +26,8 @@
 #include <cmath>
 #include <cstdio>
 #include <string>
+
+#include "gemm_default.h"
 
 namespace avk {
 
@@ -53,7 +55,7 @@ inline GateVerdict gate_verdict(long long m, long long n, long long k, int cus, 
   char buf[256];
   v.expected_mops = 2.0 * (double)m * (double)n * (double)k / 512.0;
   const long long tiles = (m / 256) * (n / 256);
-  v.expected_waves = (double)tiles * 8.0;
+  v.expected_waves = (double)tiles * kGemmWavesPerTile;
   const double simds = 4.0 * (cus > 0 ? cus : 0);
   const double gui_per = c.gui_samples > 0 ? c.gui / c.gui_samples : 0.0;
   v.mfma_util = (gui_per > 0 && simds > 0) ? c.busy / (gui_per * simds) : 0.0;
@@ -69,7 +71,7 @@ inline GateVerdict gate_verdict(long long m, long long n, long long k, int cus, 
     snprintf(buf, sizeof(buf), "SQ_INSTS_VALU_MFMA_MOPS_BF16 %.0f != 2MNK/512 = %.0f", c.mops, v.expected_mops);
     v.reason = buf;
   } else if (!(c.waves == v.expected_waves)) {
-    snprintf(buf, sizeof(buf), "SQ_WAVES %.0f != tiles*8 = %.0f", c.waves, v.expected_waves);
+    snprintf(buf, sizeof(buf), "SQ_WAVES %.0f != tiles*%d = %.0f", c.waves, kGemmWavesPerTile, v.expected_waves);
     v.reason = buf;
   } else if (!(c.busy > 0) || !(c.gui > 0) || c.gui_samples <= 0) {
     v.reason = "MFMA busy / GUI active cycles not counted";

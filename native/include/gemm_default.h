@@ -1,0 +1,20 @@
+// The validator's default bf16 GEMM, as the launch sites outside the HIP
+// runtime see it: the N7 AQL gate (prof/aql_gate.cpp) dispatches it from
+// validator_kernels.co on its own HSA queue, and the gate policy
+// (gate_policy.h) derives SQ_WAVES from its waves per tile.  One place, so the
+// kernel the HIP path runs (validator_kernels.hip, kDefaultGemmVariant) and
+// the one the gate counts cannot drift apart (tests/test_kernel_lib.py reads
+// the code object's symbols against this file).
+#pragma once
+
+namespace avk {
+
+// gemm_bf16_nt_4wa_kernel<OUT_F32=false, LOOP=9>: 256x256 tile, 4 waves of
+// 128x128, the generated main loop of schedule 2 (validator/gen_gemm4w_asm.py)
+constexpr const char* kGemmSymbol = "gemm_bf16_nt_4wa_kernelILb0ELi9EE";
+constexpr int kGemmThreads = 256;      // workgroup size
+constexpr int kGemmWavesPerTile = 4;   // kGemmThreads / 64
+constexpr int kGemmTile = 256;         // M and N multiple
+constexpr int kGemmKMultiple = 256;    // K multiple
+
+}  // namespace avk

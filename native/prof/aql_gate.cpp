@@ -6,9 +6,9 @@
 // main and opens /dev/kfd as it loads (profiles/r2_ttr/startup_probe.json).
 // This path asks the hardware directly, the way a profiler does underneath:
 //
-//   * the validator's own GEMM code object (the same gemm_bf16_nt_8p_kernel
-//     the HIP path launches, built device-only next to the binary) is loaded
-//     into an HSA executable;
+//   * the validator's own GEMM code object (the same default kernel the HIP
+//     path launches, gemm_default.h; built device-only next to the binary) is
+//     loaded into an HSA executable;
 //   * libhsa-amd-aqlprofile64 builds the PM4 start/stop command buffers for
 //     the four gfx950 counters of the gate (SQ_INSTS_VALU_MFMA_MOPS_BF16 =
 //     SQ event 52, SQ_VALU_MFMA_BUSY_CYCLES = SQ 93, SQ_WAVES = SQ 4,
@@ -25,6 +25,7 @@
 // complete fails closed instead of blocking the validator.
 
 #include "../include/aql_gate.h"
+#include "../include/gemm_default.h"
 
 #include <dlfcn.h>
 #include <hsa/hsa.h>
@@ -53,7 +54,7 @@ const hsa_ven_amd_aqlprofile_event_t kEvents[AVK_AQL_GATE_COUNTERS] = {
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 4},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, 2},
 };
-const char* kGemmSymbol = "gemm_bf16_nt_8p_kernelILb0ELb0ELb0E";  // <OUT_F32=false, LOAD_IN_M=false, BAL=false>
+using avk::kGemmSymbol;  // the default GEMM (gemm_default.h)
 
 struct Api {
   decltype(&hsa_ven_amd_aqlprofile_validate_event) validate_event = nullptr;
@@ -353,10 +354,10 @@ extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, cons
     p0->completion_signal.handle = 0;
     memset(reinterpret_cast<char*>(p1) + 4, 0, 60);
     const int nwg = (M / 256) * (N / 256);
-    p1->workgroup_size_x = 512;
+    p1->workgroup_size_x = avk::kGemmThreads;
     p1->workgroup_size_y = 1;
     p1->workgroup_size_z = 1;
-    p1->grid_size_x = static_cast<uint32_t>(nwg) * 512u;
+    p1->grid_size_x = static_cast<uint32_t>(nwg) * static_cast<uint32_t>(avk::kGemmThreads);
     p1->grid_size_y = 1;
     p1->grid_size_z = 1;
     p1->private_segment_size = kern.private_size;

@@ -1,0 +1,442 @@
+#!/usr/bin/env python3
+"""Generate gemm4w_asm.inc: the main loop of the 4-wave 256x256 bf16 GEMM
+(validator_kernels.hip, gemm_bf16_nt_4w_kernel) as ONE inline-asm statement.
+
+Why asm: the kernel keeps 256 fp32 accumulators per lane (a 128x128 wave
+tile of v_mfma_f32_16x16x32_bf16) - the whole AGPR half of the register file
+- next to ~100 VGPRs of operand fragments.  hipcc (ROCm 7.2) selects VGPR-form
+MFMAs and then parks a few dozen accumulators in VGPRs, shuffling them through
+v_accvgpr_read/write/mov every slice and spilling to scratch (measured on
+every builtin variant of this loop: 44-840 copies per 64 MFMAs).  Written as
+one statement, every register is placed once and the instruction stream is
+exactly the schedule below; tests/test_gemm4w_asm.py checks this file is
+regenerated whenever the generator changes, and tests/test_kernels_gpu.py
+checks the kernel against an fp32 reference.
+
+Register map (all named, all clobbered by the statement):
+  a[0:255]   acc tile (i, j) of the wave's 8x8 grid at a[4(8i+j) : 4(8i+j)+3]
+  v[0:23]    A fragments of rows 0-5 (re-read in place after their last use)
+  v[24:31] / v[32:39]  A fragments of rows 6, 7: two sets, by slice parity
+  v[40:71] / v[72:103] B fragments 0-7: two sets, by slice parity
+  v104/v105  per-lane LDS byte address of the A / B fragment (slot offset 0)
+  v106       per-lane global byte offset of this lane's 16 B in a piece
+  v107/v108  A / B fragment read address of the slice being read
+Per slice (32 deep, 1,024 MFMA cycles on the SIMD), interleaved between its
+64 MFMAs: the 16 ds_read_b128 of the next slice's fragments, and this wave's
+8 LDS-DMA pieces (global_load_lds_dwordx4, 1 KiB each) of slice s+5 into the
+slot slice s left; then vmcnt(24) (three slices stay in flight), lgkmcnt(0)
+and one s_barrier.  Hazards handled in the text: M0 write -> LDS-DMA one wait
+state (s_nop 0); the last MFMA's result -> the epilogue's v_accvgpr_read
+(s_nop 15 x 2 closes the statement); a fragment register is re-read 3 MFMAs
+after its last use (hipcc's own hazard recognizer pads a DS write after an
+MFMA source read with nothing).
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+
+SLICE_BYTES = 32 * 1024          # one ring slot: A 256x32 + B 256x32 bf16
+NSLOT = 5
+RING_BYTES = NSLOT * SLICE_BYTES  # 160 KiB
+OP_BYTES = 16 * 1024             # one operand's slice
+VM_INFLIGHT = 24                 # 3 slices x 8 pieces per wave
+
+B_READ_AT = {3 * j + 1: j for j in range(8)}          # B fragment j of the next slice after MFMA 3j+1
+A_READ_AT = {8 * i + 10: i for i in range(6)}         # A rows 0-5 in place, 3 MFMAs after their last use
+A_READ_AT.update({25: 6, 28: 7})                      # A rows 6, 7 into the other set
+PIECE_AT = {8 * q + 5: q for q in range(8)}           # LDS-DMA piece q
+
+
+def a_reg(i: int, parity: int) -> str:
+    if i < 6:
+        return f"v[{4 * i}:{4 * i + 3}]"
+    base = 24 + 8 * parity + 4 * (i - 6)
+    return f"v[{base}:{base + 3}]"
+
+
+def b_reg(j: int, parity: int) -> str:
+    base = 40 + 32 * parity + 4 * j
+    return f"v[{base}:{base + 3}]"
+
+
+def acc(i: int, j: int) -> str:
+    n = 4 * (8 * i + j)
+    return f"a[{n}:{n + 3}]"
+
+
+# named SGPRs (clobbered): the inputs are copied in at the start
+SA, SB, ST = "s[80:81]", "s[82:83]", "s[84:85]"
+SA_LO, SA_HI, SB_LO, SB_HI, ST_LO, ST_HI = "s80", "s81", "s82", "s83", "s84", "s85"
+PS, SR, SW, SWAVE, SADV, SITER, STMP, SINC, SWS, SKEEP = ("s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",
+                                                          "s94", "s95")
+SGPRS = range(80, 96)
+
+
+def piece(q: int) -> list[str]:
+    """This wave's piece q of the slice at sA/sB: operand q >> 2, row block
+    (wave*4 + (q & 3)) of 16 rows; source = base + (q & 3) * piece stride."""
+    lo, hi, base = (SA_LO, SA_HI, SA) if q < 4 else (SB_LO, SB_HI, SB)
+    r = q & 3
+    out = []
+    if r == 0:
+        src = base
+    else:
+        out += [f"s_add_u32 {ST_LO}, {lo if r == 1 else ST_LO}, {PS}",
+                f"s_addc_u32 {ST_HI}, {hi if r == 1 else ST_HI}, 0"]
+        src = ST
+    off = (0 if q < 4 else OP_BYTES) + r * 1024
+    if OPTS.get("vgpr_load"):  # ablation: the same load into VGPRs (no LDS write)
+        return out + [f"global_load_dwordx4 v[110:113], v106, {src}"]
+    if OPTS.get("fixed_m0"):  # ablation: no per-piece M0 set-up
+        return out + [f"global_load_lds_dwordx4 v106, {src}"]
+    out += [f"s_add_u32 m0, {SWS}, {off}", "s_nop 0", f"global_load_lds_dwordx4 v106, {src}"]
+    return out
+
+
+OPTS = {"glds": True, "barrier": True, "early_rotate": False, "dsread": True}
+
+
+def rotate() -> list[str]:
+    """Advance to the next slice: the load address moves on while slices are
+    left to load (past the last one the refills re-read it into slots no one
+    reads), the read and refill slots rotate through the ring."""
+    lines = [f"s_cmp_gt_i32 {SADV}, 0", f"s_cselect_b32 {SINC}, 64, 0", f"s_sub_i32 {SADV}, {SADV}, 1",
+             f"s_add_u32 {SA_LO}, {SA_LO}, {SINC}", f"s_addc_u32 {SA_HI}, {SA_HI}, 0",
+             f"s_add_u32 {SB_LO}, {SB_LO}, {SINC}", f"s_addc_u32 {SB_HI}, {SB_HI}, 0"]
+    for reg in (SR, SW):
+        lines += [f"s_add_u32 {reg}, {reg}, {SLICE_BYTES}", f"s_sub_u32 {STMP}, {reg}, {RING_BYTES}",
+                  f"s_cmp_ge_u32 {reg}, {RING_BYTES}", f"s_cselect_b32 {reg}, {STMP}, {reg}"]
+    return lines
+
+
+def slice_body(parity: int, first: bool) -> list[str]:
+    """One slice: MFMAs on the fragments of set `parity`, the next slice's
+    fragments into set 1 - parity, this wave's pieces of the slice to load."""
+    nxt = 1 - parity
+    lines = [f"v_add_u32 v107, {SR}, v104", f"v_add_u32 v108, {SR}, v105", f"s_add_u32 {SWS}, {SW}, {SWAVE}"]
+    rot = rotate()
+    for m in range(64):
+        i, j = m >> 3, m & 7
+        c = "0" if first else acc(i, j)
+        lines.append(f"v_mfma_f32_16x16x32_bf16 {acc(i, j)}, {b_reg(j, parity)}, {a_reg(i, parity)}, {c}")
+        if OPTS["early_rotate"]:  # the slice change's SALU work among the last MFMAs (after the last piece)
+            if 56 <= m < 60:
+                lines += rot[7 + 4 * (m - 56) // 2 * 0 + 2 * (m - 56):7 + 2 * (m - 56) + 2]
+            elif m == 62:
+                lines += rot[0:4]
+            elif m == 63:
+                lines += rot[4:7]
+        if m in B_READ_AT and OPTS["dsread"]:
+            jj = B_READ_AT[m]
+            lines.append(f"ds_read_b128 {b_reg(jj, nxt)}, v108 offset:{jj * 1024}")
+        if m in A_READ_AT and OPTS["dsread"]:
+            ii = A_READ_AT[m]
+            lines.append(f"ds_read_b128 {a_reg(ii, nxt)}, v107 offset:{ii * 1024}")
+        if OPTS["glds"]:
+            at = OPTS.get("piece_at") or PIECE_AT
+            for q in at.get(m, ()) if isinstance(at.get(m), tuple) else ([at[m]] if m in at else []):
+                lines += piece(q)
+    if not OPTS["early_rotate"]:
+        lines += rot
+
+    lines += [f"s_waitcnt vmcnt({VM_INFLIGHT if OPTS['glds'] else 0}) lgkmcnt(0)"]
+    if OPTS.get("fixed_m0"):
+        lines.insert(0, f"s_mov_b32 m0, {SWAVE}")
+    if OPTS["barrier"]:
+        lines += ["s_barrier"]
+    return lines
+
+
+def stage(slot: int) -> list[str]:
+    """Prologue: this wave's 8 pieces of the slice at sA/sB into `slot`, then
+    advance the load address one slice."""
+    out = [f"s_add_u32 {SWS}, {SWAVE}, {slot * SLICE_BYTES}"]
+    for q in range(8):
+        out += piece(q)
+    out += [f"s_add_u32 {SA_LO}, {SA_LO}, 64", f"s_addc_u32 {SA_HI}, {SA_HI}, 0",
+            f"s_add_u32 {SB_LO}, {SB_LO}, 64", f"s_addc_u32 {SB_HI}, {SB_HI}, 0"]
+    return out
+
+
+def program() -> list[str]:
+    lines = [f"s_mov_b32 {SKEEP}, m0",
+             f"s_mov_b32 {SA_LO}, %[a_lo]", f"s_mov_b32 {SA_HI}, %[a_hi]",
+             f"s_mov_b32 {SB_LO}, %[b_lo]", f"s_mov_b32 {SB_HI}, %[b_hi]",
+             f"s_mov_b32 {PS}, %[ps]", f"s_mov_b32 {SWAVE}, %[wave_lds]", f"s_mov_b32 {SADV}, %[adv]",
+             f"s_mov_b32 {SITER}, %[iters]", f"s_mov_b32 {SR}, {SLICE_BYTES}", f"s_mov_b32 {SW}, 0",
+             "v_mov_b32 v104, %[a_off]", "v_mov_b32 v105, %[b_off]", "v_mov_b32 v106, %[g_off]"]
+    for s in range(NSLOT):  # slices 0..4 (K >= 256: nk >= 8 slices)
+        lines += stage(s)
+    # slices 0 and 1 landed (3 in flight), visible to every wave
+    lines += [f"s_waitcnt vmcnt({VM_INFLIGHT})", "s_barrier"]
+    for i in range(8):  # slice 0's fragments into set 0
+        lines.append(f"ds_read_b128 {a_reg(i, 0)}, v104 offset:{i * 1024}")
+    for j in range(8):
+        lines.append(f"ds_read_b128 {b_reg(j, 0)}, v105 offset:{j * 1024}")
+    lines += ["s_waitcnt lgkmcnt(0)", "s_barrier"]  # every wave's reads of slot 0 retired
+    lines += slice_body(0, first=True)   # slice 0 (accumulators start from 0)
+    lines += slice_body(1, first=False)  # slice 1
+    lines += ["1:"]                      # slices 2.. in pairs
+    lines += slice_body(0, first=False)
+    lines += slice_body(1, first=False)
+    lines += [f"s_sub_u32 {SITER}, {SITER}, 1", f"s_cmp_lg_u32 {SITER}, 0", "s_cbranch_scc1 1b"]
+    lines += ["s_waitcnt vmcnt(0)",  # no LDS-DMA may outlive the workgroup
+              "s_nop 15", "s_nop 15",  # last MFMA results -> the epilogue's accumulator reads
+              f"s_mov_b32 m0, {SKEEP}"]
+    return lines
+
+
+HEADER = """// GENERATED by native/validator/gen_gemm4w_asm.py - do not edit; run
+//   python3 native/validator/gen_gemm4w_asm.py > native/validator/gemm4w_asm.inc
+// The 4-wave GEMM main loop as one asm statement (see the generator's
+// docstring for the register map and the schedule).
+"""
+
+
+VARIANTS = {  # function suffix -> options (the shipped loop is "")
+    "": {},
+    "_noglds": {"glds": False},
+    "_nobar": {"barrier": False},
+    "_early": {"early_rotate": True},
+    "_nods": {"dsread": False},
+    "_fixm0": {"fixed_m0": True},
+    "_vgpr": {"vgpr_load": True},
+    "_pairs": {"piece_at": {16 * p + 5: (2 * p, 2 * p + 1) for p in range(4)}},
+    "_burst": {"piece_at": {0: tuple(range(8))}},
+}
+
+
+def render() -> str:
+    out = HEADER
+    for suffix, opts in VARIANTS.items():
+        OPTS.update({"glds": True, "barrier": True, "early_rotate": False, "dsread": True}, **opts)
+        out += render_one(suffix)
+    return out
+
+
+def render_one(suffix: str) -> str:
+    body = "\\n\\t".join(program())
+    clob = ", ".join([f'"v{r}"' for r in range(114)] + [f'"s{r}"' for r in SGPRS] + [f'"a{r}"' for r in range(256)])
+    return ("// a_lo/a_hi, b_lo/b_hi: global byte address of this wave's first A / B piece\n"
+            "// of slice 0; ps: bytes between pieces (16 rows); wave_lds: LDS byte address of\n"
+            "// this wave's first piece in slot 0; adv: nk - 6; iters: (nk - 2) / 2;\n"
+            "// a_off / b_off: per-lane LDS byte address of fragment 0 of A / B in slot 0;\n"
+            "// g_off: per-lane byte offset of the lane's 16 B within a piece.\n"
+            f"__device__ __forceinline__ void avk_g4_mainloop{suffix}(unsigned a_lo, unsigned a_hi, unsigned b_lo, unsigned b_hi,\n"
+            "                                                unsigned ps, unsigned wave_lds, int adv, unsigned iters,\n"
+            "                                                unsigned a_off, unsigned b_off, unsigned g_off) {\n"
+            f'  asm volatile("{body}"\n'
+            "               :\n"
+            "               : [a_lo] \"s\"(a_lo), [a_hi] \"s\"(a_hi), [b_lo] \"s\"(b_lo), [b_hi] \"s\"(b_hi), [ps] \"s\"(ps),\n"
+            "                 [wave_lds] \"s\"(wave_lds), [adv] \"s\"(adv), [iters] \"s\"(iters), [a_off] \"v\"(a_off),\n"
+            "                 [b_off] \"v\"(b_off), [g_off] \"v\"(g_off)\n"
+            f"               : \"memory\", \"scc\", {clob});\n"
+            "}\n")
+
+
+
+
+# ----------------------------------------------------------------- schedule 2 --
+# Fewer and better spread fillers between the MFMAs (counters of schedule 1,
+# profiles/r4_gemm: MFMA util 0.79 even with the loads removed, SALU issue 2x
+# hipBLASLt's): the loop body is unrolled over 10 slices (2 fragment parities
+# x 5 ring slots), so every LDS address is a constant of the slice's
+# position; each piece has its own global base SGPR pair (the wave's rows
+# 16r.. of A or B, set once), the slice's k offset is one VGPR advanced once
+# per slice (held on the last slice once the loads are past it: the refills
+# then re-read it into slots no one reads).  Each MFMA gap carries at most one
+# filler (a DS read, an M0 write or a load) but for the loop's own SALU, the
+# M0 write one MFMA ahead of its load.
+S2_BASE = [f"s[{64 + 2 * q}:{65 + 2 * q}]" for q in range(8)]  # piece q's global base
+S2_WAVE, S2_CNT, S2_KEEP, S2_INC = "s80", "s81", "s82", "s83"
+S2_SGPRS = range(64, 84)
+S2_VOFF = "v106"
+# v104/v105: A/B fragment 0 address in slot 0; v107/v108: + 64 KiB; v109/v110: + 128 KiB
+S2_VBASE = {0: ("v104", "v105", 0), 1: ("v104", "v105", SLICE_BYTES), 2: ("v107", "v108", 0),
+            3: ("v107", "v108", SLICE_BYTES), 4: ("v109", "v110", 0)}
+S2_B_READ = {4 * j + 1: j for j in range(8)}
+S2_A_READ = {8 * i + 10: i for i in range(6)}
+S2_A_READ.update({37: 6, 45: 7})
+S2_M0_AT = {8 * q + 6: q for q in range(8)}
+S2_LOAD_AT = {8 * q + 7: q for q in range(8)}
+S2_ADVANCE_MIN = NSLOT + 1  # slices left after this one for the refill address to move on
+
+
+def s2_m0(slot: int, q: int) -> str:
+    return f"s_add_u32 m0, {S2_WAVE}, {slot * SLICE_BYTES + (0 if q < 4 else OP_BYTES) + (q & 3) * 1024}"
+
+
+def s2_slice(pos: int, first: bool = False, label: str | None = None) -> list[str]:
+    """Slice at body position `pos` (0..9): fragments of parity pos % 2, reads
+    of the next slice from slot (pos + 1) % 5, refill of slot pos % 5."""
+    parity, nxt = pos % 2, 1 - pos % 2
+    rslot, wslot = (pos + 1) % NSLOT, pos % NSLOT
+    va, vb, off = S2_VBASE[rslot]
+    lines = [f"{label}:"] if label else []
+    for m in range(64):
+        i, j = m >> 3, m & 7
+        c = "0" if first else acc(i, j)
+        lines.append(f"v_mfma_f32_16x16x32_bf16 {acc(i, j)}, {b_reg(j, parity)}, {a_reg(i, parity)}, {c}")
+        if m in S2_B_READ:
+            jj = S2_B_READ[m]
+            lines.append(f"ds_read_b128 {b_reg(jj, nxt)}, {vb} offset:{off + jj * 1024}")
+        if m in S2_A_READ:
+            ii = S2_A_READ[m]
+            lines.append(f"ds_read_b128 {a_reg(ii, nxt)}, {va} offset:{off + ii * 1024}")
+        if m in S2_M0_AT:
+            lines.append(s2_m0(wslot, S2_M0_AT[m]))
+        if m in S2_LOAD_AT:
+            lines.append(f"global_load_lds_dwordx4 {S2_VOFF}, {S2_BASE[S2_LOAD_AT[m]]}")
+        if m == 40:  # this slice done: slices left; the refill address moves on while one is left to load
+            lines += [f"s_sub_u32 {S2_CNT}, {S2_CNT}, 1"]
+        if m == 41:
+            lines += [f"s_cmp_ge_u32 {S2_CNT}, {S2_ADVANCE_MIN}", f"s_cselect_b32 {S2_INC}, 64, 0"]
+    lines += [f"v_add_u32 {S2_VOFF}, {S2_INC}, {S2_VOFF}",
+              f"s_waitcnt vmcnt({VM_INFLIGHT}) lgkmcnt(0)", f"s_cmp_eq_u32 {S2_CNT}, 0", "s_cbranch_scc1 3f",
+              "s_barrier"]
+    return lines
+
+
+def program2() -> list[str]:
+    lines = [f"s_mov_b32 {S2_KEEP}, m0",
+             f"s_mov_b32 s64, %[a_lo]", f"s_mov_b32 s65, %[a_hi]",
+             f"s_mov_b32 s72, %[b_lo]", f"s_mov_b32 s73, %[b_hi]"]
+    for q in range(8):  # piece q's base = operand base + (q & 3) * ps
+        if q & 3:
+            lo, prev = 64 + 2 * q, 64 + 2 * (q - 1)
+            lines += [f"s_add_u32 s{lo}, s{prev}, %[ps]", f"s_addc_u32 s{lo + 1}, s{prev + 1}, 0"]
+    lines += [f"s_mov_b32 {S2_WAVE}, %[wave_lds]", f"s_mov_b32 {S2_CNT}, %[nk]",  # slices left, this one included
+              "v_mov_b32 v104, %[a_off]", "v_mov_b32 v105, %[b_off]", f"v_mov_b32 {S2_VOFF}, %[g_off]",
+              f"v_add_u32 v107, {2 * SLICE_BYTES}, v104", f"v_add_u32 v108, {2 * SLICE_BYTES}, v105",
+              f"v_add_u32 v109, {4 * SLICE_BYTES}, v104", f"v_add_u32 v110, {4 * SLICE_BYTES}, v105"]
+    for slot in range(NSLOT):  # slices 0..4 (nk >= 8)
+        for q in range(8):
+            lines += [s2_m0(slot, q), "s_nop 0", f"global_load_lds_dwordx4 {S2_VOFF}, {S2_BASE[q]}"]
+        lines.append(f"v_add_u32 {S2_VOFF}, 64, {S2_VOFF}")
+    lines += [f"s_waitcnt vmcnt({VM_INFLIGHT})", "s_barrier"]  # slices 0, 1 landed and visible
+    for i in range(8):
+        lines.append(f"ds_read_b128 {a_reg(i, 0)}, v104 offset:{i * 1024}")
+    for j in range(8):
+        lines.append(f"ds_read_b128 {b_reg(j, 0)}, v105 offset:{j * 1024}")
+    lines += ["s_waitcnt lgkmcnt(0)", "s_barrier"]  # every wave's reads of slot 0 retired
+    lines += s2_slice(0, first=True)
+    lines += ["s_branch 2f"]
+    lines += ["1:"] + s2_slice(0)
+    lines += s2_slice(1, label="2")
+    for pos in range(2, 10):
+        lines += s2_slice(pos)
+    lines += ["s_branch 1b", "3:",
+              "s_waitcnt vmcnt(0)",  # no LDS-DMA may outlive the workgroup
+              "s_nop 15", "s_nop 15",  # last MFMA results -> the epilogue's accumulator reads
+              f"s_mov_b32 m0, {S2_KEEP}"]
+    return lines
+
+
+def render2() -> str:
+    body = "\\n\\t".join(program2())
+    clob = ", ".join([f'"v{r}"' for r in range(111)] + [f'"s{r}"' for r in S2_SGPRS] + [f'"a{r}"' for r in range(256)])
+    return ("// Schedule 2: a_lo/a_hi, b_lo/b_hi, ps, wave_lds, a_off, b_off, g_off as above;\n"
+            "// nk = K / 32 (a multiple of 8).\n"
+            "__device__ __forceinline__ void avk_g4_mainloop2(unsigned a_lo, unsigned a_hi, unsigned b_lo, unsigned b_hi,\n"
+            "                                                 unsigned ps, unsigned wave_lds, unsigned nk,\n"
+            "                                                 unsigned a_off, unsigned b_off, unsigned g_off) {\n"
+            f'  asm volatile("{body}"\n'
+            "               :\n"
+            "               : [a_lo] \"s\"(a_lo), [a_hi] \"s\"(a_hi), [b_lo] \"s\"(b_lo), [b_hi] \"s\"(b_hi), [ps] \"s\"(ps),\n"
+            "                 [wave_lds] \"s\"(wave_lds), [nk] \"s\"(nk), [a_off] \"v\"(a_off), [b_off] \"v\"(b_off),\n"
+            "                 [g_off] \"v\"(g_off)\n"
+            f"               : \"memory\", \"scc\", {clob});\n"
+            "}\n")
+
+
+# ----------------------------------------------------------------- schedule 3 --
+# Schedule 2's loop with the loads issued in slice PAIRS: on every even slice s
+# each piece of slice s + 4 is followed at once by the same rows' piece of
+# slice s + 5, the other 64 B of the same 128-B lines.  Schedule 2 asks L2
+# for each line twice, 64 B a slice apart (TCC_HIT 2.3x hipBLASLt's at equal
+# misses, profiles/r4_gemm); back to back, the second half can be served by
+# the first request's line (vector L1 / the miss queue).  Slots (s+4) % 5 and
+# s % 5 are both free at the start of an even slice s; every slice ends with
+# vmcnt(16) (the pair issued last stays in flight).
+S3_VOFF2 = "v111"        # S2_VOFF + 64: the pair's second slice
+S3_B_READ = {4 * j + 1: j for j in range(8)}
+S3_A_READ = {8 * i + 12: i for i in range(6)}
+S3_A_READ.update({33: 6, 37: 7})
+S3_M0_AT = {4 * p + 2: p for p in range(16)}
+S3_LOAD_AT = {4 * p + 3: p for p in range(16)}
+S3_VM = 16
+S3_ADVANCE_MIN = 7       # slices left after this one for the next pair to exist
+
+
+def s3_slice(pos: int, first: bool = False, label: str | None = None) -> list[str]:
+    """Slice at body position `pos` (0..9); even positions load the pair
+    (pos + 4, pos + 5): piece q of the pair's first slice goes to slot
+    (pos + 4) % 5, of the second to slot pos % 5."""
+    parity, nxt = pos % 2, 1 - pos % 2
+    rslot = (pos + 1) % NSLOT
+    va, vb, off = S2_VBASE[rslot]
+    loads = pos % 2 == 0
+    slots = ((pos + 4) % NSLOT, pos % NSLOT)
+    lines = [f"{label}:"] if label else []
+    for m in range(64):
+        i, j = m >> 3, m & 7
+        c = "0" if first else acc(i, j)
+        lines.append(f"v_mfma_f32_16x16x32_bf16 {acc(i, j)}, {b_reg(j, parity)}, {a_reg(i, parity)}, {c}")
+        if m in S3_B_READ:
+            jj = S3_B_READ[m]
+            lines.append(f"ds_read_b128 {b_reg(jj, nxt)}, {vb} offset:{off + jj * 1024}")
+        if m in S3_A_READ:
+            ii = S3_A_READ[m]
+            lines.append(f"ds_read_b128 {a_reg(ii, nxt)}, {va} offset:{off + ii * 1024}")
+        if loads and m in S3_M0_AT:
+            p = S3_M0_AT[m]
+            lines.append(s2_m0(slots[p & 1], p >> 1))
+        if loads and m in S3_LOAD_AT:
+            p = S3_LOAD_AT[m]
+            lines.append(f"global_load_lds_dwordx4 {(S2_VOFF, S3_VOFF2)[p & 1]}, {S2_BASE[p >> 1]}")
+        if m == 40:
+            lines += [f"s_sub_u32 {S2_CNT}, {S2_CNT}, 1"]
+        if loads and m == 41:
+            lines += [f"s_cmp_ge_u32 {S2_CNT}, {S3_ADVANCE_MIN}", f"s_cselect_b32 {S2_INC}, 0x80, 0"]
+    if loads:
+        lines += [f"v_add_u32 {S2_VOFF}, {S2_INC}, {S2_VOFF}", f"v_add_u32 {S3_VOFF2}, {S2_INC}, {S3_VOFF2}"]
+    lines += [f"s_waitcnt vmcnt({S3_VM}) lgkmcnt(0)", f"s_cmp_eq_u32 {S2_CNT}, 0", "s_cbranch_scc1 3f",
+              "s_barrier"]
+    return lines
+
+
+def program3() -> list[str]:
+    lines = program2()[:program2().index(f"v_add_u32 v110, {4 * SLICE_BYTES}, v105") + 1]
+    lines.append(f"v_add_u32 {S3_VOFF2}, 64, {S2_VOFF}")
+    for pair in range(2):  # slices 0..3 into slots 0..3, in pairs
+        for p in range(16):
+            lines += [s2_m0(2 * pair + (p & 1), p >> 1), "s_nop 0",
+                      f"global_load_lds_dwordx4 {(S2_VOFF, S3_VOFF2)[p & 1]}, {S2_BASE[p >> 1]}"]
+        lines += [f"v_add_u32 {S2_VOFF}, 0x80, {S2_VOFF}", f"v_add_u32 {S3_VOFF2}, 0x80, {S3_VOFF2}"]
+    lines += [f"s_waitcnt vmcnt({S3_VM})", "s_barrier"]  # slices 0, 1 landed and visible
+    for i in range(8):
+        lines.append(f"ds_read_b128 {a_reg(i, 0)}, v104 offset:{i * 1024}")
+    for j in range(8):
+        lines.append(f"ds_read_b128 {b_reg(j, 0)}, v105 offset:{j * 1024}")
+    lines += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+    lines += s3_slice(0, first=True)
+    lines += ["s_branch 2f"]
+    lines += ["1:"] + s3_slice(0)
+    lines += s3_slice(1, label="2")
+    for pos in range(2, 10):
+        lines += s3_slice(pos)
+    lines += ["s_branch 1b", "3:",
+              "s_waitcnt vmcnt(0)", "s_nop 15", "s_nop 15", f"s_mov_b32 m0, {S2_KEEP}"]
+    return lines
+
+
+def render3() -> str:
+    return render2().replace("avk_g4_mainloop2(", "avk_g4_mainloop3(").replace(
+        "// Schedule 2:", "// Schedule 3 (schedule 2, loads in slice pairs):").replace(
+        "\\n\\t".join(program2()), "\\n\\t".join(program3())).replace(
+        '"v110", ', '"v110", "v111", ')
+
+if __name__ == "__main__":
+    sys.stdout.write(render() + render2() + render3())

@@ -24,6 +24,8 @@
 // launching an out-of-bounds grid.
 
 #include <hip/hip_runtime.h>
+#include <utility>
+#include "gemm_default.h"
 #include <stdint.h>
 #include <string.h>
 
@@ -1027,6 +1029,303 @@ __global__ __launch_bounds__(g8::NTHR, 2) void gemm_bf16_nt_8p_kernel(const __bf
     }
 }
 
+// ------------- K2 GEMM, 4 waves x 128x128, 5-slot LDS-DMA ring (variant 14) ----
+//
+// Same 256x256 block tile, but 4 waves (2M x 2N), each owning 128x128 of the
+// output = 8x8 tiles of v_mfma_f32_16x16x32_bf16 (256 accumulators, the AGPR
+// half of the register file; one wave per SIMD).  Against the 8-wave
+// kernels' 128x64 wave tile this halves the LDS reads per MFMA (16
+// ds_read_b128 per 64 MFMAs instead of 12 per 32: 0.25 vs 0.375), which the
+// round-1/3 counters name as the cost (profiles/r3_gemm: MFMA util 0.66,
+// SQ_WAIT_ANY 29 %; hipBLASLt's MT256x256x64 4-wave kernel 0.88 / 5 %).
+// With no partner wave on the SIMD to hide behind, the wave pipelines
+// itself:
+//   * K is consumed in 32-deep slices (A 256x32 + B 256x32 = 32 KiB) through a
+//     5-slot ring (all 160 KiB of LDS) filled by global_load_lds_dwordx4;
+//     slice s+5 is issued right after barrier s into the slot slice s just
+//     left, so every slice has four barrier intervals (~4 K cycles) to land;
+//   * two fragment register sets (2 x 64 VGPRs): the MFMAs of slice s run on
+//     one while slice s+1's 16 ds_read_b128 fill the other, spread over the
+//     first 48 MFMAs, and the 8 LDS-DMA pieces of slice s+5 sit between
+//     MFMAs too (sched_group_barrier pins the interleave);
+//   * one raw barrier per slice (1,024 MFMA cycles), behind a counted
+//     vmcnt(24) - three slices stay in flight across it - and lgkmcnt(0).
+//   RAW  slice x is read during slice x-1, after barrier x-1; every wave's
+//        pieces of it were waited for (vmcnt) before that barrier.
+//   WAR  slot s%5 is refilled after barrier s; every wave retired its reads
+//        of slice s (issued during slice s-1) before reaching barrier s.
+// LDS image of one operand slice: row r at r*64 B, 16-B chunk c at
+// (c ^ ((-(r >> 2)) & 3)) * 16 - with the ds_read_b128 lane groups
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ... MI355X_MICROARCH.md §LDS) every
+// fragment read of a 16-row tile hits 16 distinct 16-B bank slots; the XOR is
+// applied to the glds SOURCE address (the LDS side is lane-linear) and on
+// the read.  Past the last slice the refills re-read slice nk-1 into slots no
+// one reads, which keeps the wait counts constant; vmcnt(0) drains them.
+namespace g4 {
+constexpr int BM = 256, BN = 256, BKS = 32, NTHR = 256, NSLOT = 5;
+constexpr int OP_BYTES = BM * BKS * 2;          // 16 KiB: one operand's slice, 256 rows x 64 B
+constexpr int SLOT_BYTES = 2 * OP_BYTES;        // 32 KiB
+constexpr int LDS_BYTES = NSLOT * SLOT_BYTES;   // 160 KiB
+constexpr int GROUP_M = 4;                      // tile rows per L2 band
+constexpr int VM_INFLIGHT = (NSLOT - 2) * 8;    // pieces per wave of the slices that may stay in flight
+}  // namespace g4
+
+__device__ __forceinline__ int g4_chunk_xor(int row) { return (-(row >> 2)) & 3; }
+
+template <int N>
+__device__ __forceinline__ void g4_vmwait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Slice s's MFMAs (row-major: MFMA m = 8i + j updates acc[i][j]) on fa / cb;
+// slice s+1's fragments from rslot: A fragment i into fa[i] right after its
+// last use (MFMA 8i+7) - one A register set - and the B fragments into the
+// second set nb early in the slice; this wave's 8 pieces of slice `kload`
+// into wslot between MFMAs.
+__device__ __forceinline__ constexpr bool g4_bread(int m) { return m % 3 == 1 && m / 3 < 8; }
+__device__ __forceinline__ constexpr bool g4_aread(int m) { return m % 8 == 7; }
+__device__ __forceinline__ constexpr bool g4_glds(int m) { return m % 8 == 4; }
+
+__device__ __forceinline__ void g4_slice(f32x4 (&acc)[8][8], bf16x8 (&fa)[8], const bf16x8 (&cb)[8], bf16x8 (&nb)[8],
+                                         const char* rslot, char* wslot, const __bf16* __restrict__ ga,
+                                         const __bf16* __restrict__ gb, size_t piece_stride, int kload, int a_off,
+                                         int b_off, int wave) {
+  using namespace g4;
+  // pin every accumulator to the AGPR file at the slice boundary (an empty
+  // asm, no instruction): the register allocator otherwise parks some of the
+  // 256 in VGPRs and shuffles them through v_accvgpr_read/write every slice
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+#pragma unroll
+  for (int m = 0; m < 64; ++m) {
+    const int i = m >> 3, j = m & 7;
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[j], fa[i], acc[i][j], 0, 0, 0);
+    if (g4_bread(m)) nb[m / 3] = *reinterpret_cast<const bf16x8*>(rslot + b_off + (m / 3) * 1024);
+    if (g4_aread(m)) fa[i] = *reinterpret_cast<const bf16x8*>(rslot + a_off + i * 1024);
+    if (g4_glds(m)) {
+      const int q = m / 8;  // piece: operand q >> 2, row block wave*4 + (q & 3)
+      const __bf16* src = (q < 4 ? ga : gb) + (q & 3) * piece_stride + kload;
+      __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)(wslot + (q < 4 ? 0 : OP_BYTES) + (wave * 4 + (q & 3)) * 1024),
+                                       16, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 64; ++m) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    if (g4_bread(m)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    if (g4_aread(m)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    if (g4_glds(m)) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // LDS-DMA piece
+  }
+}
+
+__device__ __forceinline__ void g4_stage(const __bf16* __restrict__ ga, const __bf16* __restrict__ gb,
+                                         size_t piece_stride, int k0, char* slot, int wave) {
+  using namespace g4;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const __bf16* src = (q < 4 ? ga : gb) + (q & 3) * piece_stride + k0;
+    __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)(slot + (q < 4 ? 0 : OP_BYTES) + (wave * 4 + (q & 3)) * 1024),
+                                     16, 0, 0);
+  }
+}
+
+template <bool OUT_F32>
+__global__ __launch_bounds__(g4::NTHR, 1) void gemm_bf16_nt_4w_kernel(const __bf16* __restrict__ A,
+                                                                     const __bf16* __restrict__ Bt,
+                                                                     void* __restrict__ Cv, int M, int N, int K) {
+  using namespace g4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid % kNumXcd;
+  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
+  const int per_group = GROUP_M * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid % per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // glds source of this lane: row (wave*4 + i)*16 + lane/4 of the operand
+  // tile, logical chunk (lane & 3) ^ xor(row) (the XOR depends on lane/16 only)
+  const int srow = wave * 64 + (lane >> 2);
+  const int schunk = (lane & 3) ^ g4_chunk_xor(lane >> 2);
+  const __bf16* ga = A + (size_t)(m0 + srow) * K + schunk * 8;
+  const __bf16* gb = Bt + (size_t)(n0 + srow) * K + schunk * 8;
+  const size_t piece_stride = (size_t)16 * K;
+  // ds_read_b128 fragment addresses: row (w*128 + i*16 + lane%16), chunk lane/16
+  const int fr = lane & 15;
+  const int fch = ((lane >> 4) ^ g4_chunk_xor(fr)) * 16;
+  const int a_off = (wm * 128 + fr) * 64 + fch;
+  const int b_off = OP_BYTES + (wn * 128 + fr) * 64 + fch;
+
+  const int nk = K / BKS;  // even (K % 256 == 0)
+#pragma unroll
+  for (int s = 0; s < NSLOT; ++s) g4_stage(ga, gb, piece_stride, min(s, nk - 1) * BKS, smem + s * SLOT_BYTES, wave);
+  g4_vmwait<VM_INFLIGHT>();  // slices 0 and 1 landed (own pieces)
+  wg_barrier();
+  bf16x8 fa[8], fb0[8], fb1[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    fa[r] = *reinterpret_cast<const bf16x8*>(smem + a_off + r * 1024);
+    fb0[r] = *reinterpret_cast<const bf16x8*>(smem + b_off + r * 1024);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  wg_barrier();  // every wave's reads of slot 0 retired: it may be refilled
+
+  for (int s = 0; s < nk; s += 2) {
+    g4_slice(acc, fa, fb0, fb1, smem + ((s + 1) % NSLOT) * SLOT_BYTES, smem + (s % NSLOT) * SLOT_BYTES, ga, gb,
+             piece_stride, min(s + NSLOT, nk - 1) * BKS, a_off, b_off, wave);
+    g4_vmwait<VM_INFLIGHT>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wg_barrier();
+    g4_slice(acc, fa, fb1, fb0, smem + ((s + 2) % NSLOT) * SLOT_BYTES, smem + ((s + 1) % NSLOT) * SLOT_BYTES,
+             ga, gb, piece_stride, min(s + 1 + NSLOT, nk - 1) * BKS, a_off, b_off, wave);
+    g4_vmwait<VM_INFLIGHT>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wg_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+
+  // D = Bfrag x Afrag: lane holds row (lane & 15), columns 4*(lane >> 4) + 0..3
+  const int crow = m0 + wm * 128 + fr;
+  const int ccol = n0 + wn * 128 + (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const size_t idx = (size_t)(crow + i * 16) * N + ccol + j * 16;
+      if constexpr (OUT_F32) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + idx) = acc[i][j];
+      } else {
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 v = {(__bf16)acc[i][j][0], (__bf16)acc[i][j][1], (__bf16)acc[i][j][2], (__bf16)acc[i][j][3]};
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(Cv) + idx) = v;
+      }
+    }
+}
+
+// Variant 15: the same 4-wave tile and 5-slot ring, with the main loop as one
+// generated asm statement (gemm4w_asm.inc, native/validator/gen_gemm4w_asm.py):
+// every accumulator stays in its AGPR and every fragment in its VGPR, and the
+// interleave of MFMAs, fragment reads and LDS-DMA pieces is exactly the
+// generator's schedule (hipcc's register allocation of the builtin version
+// above moves accumulators through VGPRs every slice).
+#include "gemm4w_asm.inc"
+
+template <int T>
+__device__ __forceinline__ f32x4 g4_acc() {
+  float x0, x1, x2, x3;
+  asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+               "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+               : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3)
+               : "i"(4 * T), "i"(4 * T + 1), "i"(4 * T + 2), "i"(4 * T + 3));
+  return (f32x4){x0, x1, x2, x3};
+}
+
+template <bool OUT_F32, int T>
+__device__ __forceinline__ void g4_store_tile(void* __restrict__ Cv, int N, int crow, int ccol) {
+  constexpr int i = T >> 3, j = T & 7;
+  const f32x4 v = g4_acc<T>();
+  const size_t idx = (size_t)(crow + i * 16) * N + ccol + j * 16;
+  if constexpr (OUT_F32) {
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + idx) = v;
+  } else {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(Cv) + idx) = h;
+  }
+}
+
+template <bool OUT_F32, int... T>
+__device__ __forceinline__ void g4_store_all(void* __restrict__ Cv, int N, int crow, int ccol,
+                                             std::integer_sequence<int, T...>) {
+  (g4_store_tile<OUT_F32, T>(Cv, N, crow, ccol), ...);
+}
+
+template <bool OUT_F32, int LOOP = 0>
+__global__ __launch_bounds__(g4::NTHR, 1) void gemm_bf16_nt_4wa_kernel(const __bf16* __restrict__ A,
+                                                                      const __bf16* __restrict__ Bt,
+                                                                      void* __restrict__ Cv, int M, int N, int K) {
+  using namespace g4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid % kNumXcd;
+  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
+  const int per_group = GROUP_M * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid % per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  // this wave's first piece: operand rows wave*64 .. +15 (the 4 pieces of a
+  // slice are 16 rows apart); each lane moves 16 B of it: row lane/4, logical
+  // chunk (lane & 3) ^ xor(row) (the XOR depends on lane/16 only)
+  const uint64_t a0 = reinterpret_cast<uint64_t>(A + (size_t)(m0 + wave * 64) * K);
+  const uint64_t b0 = reinterpret_cast<uint64_t>(Bt + (size_t)(n0 + wave * 64) * K);
+  const unsigned g_off = (unsigned)(((lane >> 2) * K + ((lane & 3) ^ g4_chunk_xor(lane >> 2)) * 8) * 2);
+  const unsigned lds = (unsigned)(uintptr_t)smem;
+  const int fr = lane & 15;
+  const int fch = ((lane >> 4) ^ g4_chunk_xor(fr)) * 16;
+  const unsigned a_off = lds + (wm * 128 + fr) * 64 + fch;
+  const unsigned b_off = lds + OP_BYTES + (wn * 128 + fr) * 64 + fch;
+  const int nk = K / BKS;  // >= 8 and even (K % 256 == 0)
+#define AVK_G4_ARGS                                                                                          \
+  __builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),       \
+      __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),   \
+      (unsigned)(16 * K * 2), __builtin_amdgcn_readfirstlane(lds + wave * 4 * 1024), nk - 6,                 \
+      (unsigned)((nk - 2) / 2), a_off, b_off, g_off
+  if constexpr (LOOP == 0) avk_g4_mainloop(AVK_G4_ARGS);
+  else if constexpr (LOOP == 1) avk_g4_mainloop_noglds(AVK_G4_ARGS);
+  else if constexpr (LOOP == 2) avk_g4_mainloop_nobar(AVK_G4_ARGS);
+  else if constexpr (LOOP == 3) avk_g4_mainloop_early(AVK_G4_ARGS);
+  else if constexpr (LOOP == 4) avk_g4_mainloop_nods(AVK_G4_ARGS);
+  else if constexpr (LOOP == 5) avk_g4_mainloop_fixm0(AVK_G4_ARGS);
+  else if constexpr (LOOP == 6) avk_g4_mainloop_vgpr(AVK_G4_ARGS);
+  else if constexpr (LOOP == 7) avk_g4_mainloop_pairs(AVK_G4_ARGS);
+  else if constexpr (LOOP == 8) avk_g4_mainloop_burst(AVK_G4_ARGS);
+  else if constexpr (LOOP == 9)
+    avk_g4_mainloop2(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
+                     __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
+                     (unsigned)(16 * K * 2), __builtin_amdgcn_readfirstlane(lds + wave * 4 * 1024), (unsigned)nk, a_off,
+                     b_off, g_off);
+  else
+    avk_g4_mainloop3(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
+                     __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
+                     (unsigned)(16 * K * 2), __builtin_amdgcn_readfirstlane(lds + wave * 4 * 1024), (unsigned)nk, a_off,
+                     b_off, g_off);
+#undef AVK_G4_ARGS
+
+  // D = Bfrag x Afrag: lane holds row (lane & 15), columns 4*(lane >> 4) + 0..3
+  g4_store_all<OUT_F32>(Cv, N, m0 + wm * 128 + fr, n0 + wn * 128 + (lane >> 4) * 4,
+                        std::make_integer_sequence<int, 64>{});
+}
+
 // ------------------------------------------------- Freivalds check GEMVs ----
 // y[r] = sum_c X[r][c] * v[c]   (X bf16 or f32, row-major, one wave per row)
 template <typename T>
@@ -1319,7 +1618,15 @@ AVK_API int avk_vector_add_f32(const float* a, const float* b, float* c, int64_t
 //   hipBLASLt (torch.matmul) on the same operands                     1548    1672
 // A finer split of the ring (two 16-MFMA phases per slice, 4 barriers)
 // measured 1308 at 8192^3: not kept.
-constexpr int kDefaultGemmVariant = 6;
+// Round 4: the 4-wave kernel with the generated main loop (variants 15, 24,
+// 25; profiles/r4_gemm/) is the default for K a multiple of 256, the 8-phase
+// kernel the fallback for the other K (a multiple of 64).  The AQL gate
+// dispatches the same default (gemm_default.h).
+constexpr int kDefaultGemmVariant = 24;
+constexpr int kFallbackGemmVariant = 6;
+static_assert(avk::kGemmThreads == g4::NTHR && avk::kGemmWavesPerTile * 64 == g4::NTHR &&
+                  avk::kGemmTile == g4::BM && avk::kGemmTile == g4::BN && avk::kGemmKMultiple == 256,
+              "gemm_default.h describes the default kernel");
 
 AVK_API int avk_vector_add_verify_f32(const float* a, const float* b, const float* c, int64_t n,
                                       unsigned long long* bad_dev, hipStream_t s) {
@@ -1367,7 +1674,33 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
       else gemm_bf16_nt_8p_kernel<false, LIM, BAL><<<nwg, g8::NTHR, 0, s>>>(a, b, C, M, N, K);        \
       break;
   switch (variant) {
-    AVK_G8(6, false, false)  // the shipped kernel (kDefaultGemmVariant)
+    AVK_G8(6, false, false)  // kFallbackGemmVariant: 8 waves, K a multiple of 64
+#define AVK_G4A(V, L)                                                                            \
+    case V:                                                                                      \
+      if (K % 256) return hipErrorInvalidValue;                                                  \
+      if (out_f32) gemm_bf16_nt_4wa_kernel<true, L><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);  \
+      else gemm_bf16_nt_4wa_kernel<false, L><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);         \
+      break;
+    // 4 waves x 128x128 per 256x256 tile, 5-slot ring (K: a multiple of 256)
+    AVK_G4A(15, 0)  // schedule 1 of the generated main loop
+    AVK_G4A(24, 9)  // schedule 2: 10-slice unrolled body, constant addresses, one filler per MFMA gap
+    AVK_G4A(25, 10)  // schedule 3: schedule 2 with the loads in slice pairs (whole 128-B lines back to back)
+#if AVK_GEMM_LAB
+    case 14:  // the 4-wave kernel in builtins (hipcc moves accumulators through VGPRs, spills)
+      if (K % 256) return hipErrorInvalidValue;
+      if (out_f32) gemm_bf16_nt_4w_kernel<true><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+      else gemm_bf16_nt_4w_kernel<false><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+      break;
+    AVK_G4A(16, 1)  // ablations of 15 (wrong results by design, timing only): no LDS-DMA
+    AVK_G4A(17, 2)  // no barrier
+    AVK_G4A(18, 3)  // the slice change's SALU work among the last MFMAs (correct)
+    AVK_G4A(19, 4)  // no fragment reads
+    AVK_G4A(20, 5)  // one M0 for every piece (wrong LDS image): the cost of the per-piece M0 set-up
+    AVK_G4A(21, 6)  // the loads into VGPRs instead of LDS (wrong results): glds vs a plain load
+    AVK_G4A(22, 7)  // pieces in pairs (wrong results: M0 / base rewritten before the previous piece read it)
+    AVK_G4A(23, 8)  // pieces in one burst after the barrier (wrong results, as 22)
+#endif
+#undef AVK_G4A
 #if AVK_GEMM_LAB
     case 0:
       if (out_f32) gemm_bf16_nt_pp_kernel<true, true><<<nwg, NTHR, 0, s>>>(a, b, C, M, N, K);
@@ -1416,7 +1749,8 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
 
 AVK_API int avk_gemm_bf16_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K,
                              hipStream_t s) {
-  return avk_gemm_bf16_nt_variant(A, Bt, C, out_f32, M, N, K, kDefaultGemmVariant, s);
+  return avk_gemm_bf16_nt_variant(A, Bt, C, out_f32, M, N, K,
+                                  K % avk::kGemmKMultiple == 0 ? kDefaultGemmVariant : kFallbackGemmVariant, s);
 }
 
 // y = X v ; X is [R][C] row-major (bf16 when x_is_bf16, else f32); C % 8 == 0

@@ -6,6 +6,8 @@ Healthy tuple: the MI355X values of profiles/r2_gate/aql_v2.json (4096^3,
 256 CUs, 8 GRBM instances)."""
 
 import json
+import pathlib
+import re
 import subprocess
 
 import pytest
@@ -13,9 +15,11 @@ import pytest
 from amdgpu_operator import native
 
 VALIDATOR = str(native.binary("amdgpu-validator"))
+_HDR = (pathlib.Path(__file__).resolve().parents[1] / "native" / "include" / "gemm_default.h").read_text()
+WPT = int(re.search(r"kGemmWavesPerTile = (\d+);", _HDR).group(1))  # waves per 256x256 tile of the default GEMM
 N = 4096
 MOPS = 2 * N ** 3 // 512          # 268,435,456
-WAVES = (N // 256) ** 2 * 8       # 2,048
+WAVES = (N // 256) ** 2 * WPT     # 1,024 (4 waves a tile)
 BUSY = MOPS // 2                  # 134,217,728 (measured: exactly MOPS/2)
 GUI = 2134600                     # 8 XCDs summed (~267 k cycles each)
 
@@ -37,7 +41,7 @@ def test_healthy_mi355x_counters_pass():
 
 
 @pytest.mark.parametrize("field,delta,why", [
-    ("waves", -1, "SQ_WAVES"), ("waves", +1, "SQ_WAVES"), ("waves", -8, "SQ_WAVES"),
+    ("waves", -1, "SQ_WAVES"), ("waves", +1, "SQ_WAVES"), ("waves", -WPT, "SQ_WAVES"),
     ("mops", -1, "MFMA_MOPS"), ("mops", +1, "MFMA_MOPS"), ("mops", -32, "MFMA_MOPS")])
 def test_off_by_one_counts_fail_closed(field, delta, why):
     kw = {"mops": MOPS, "waves": WAVES}
@@ -65,7 +69,7 @@ def test_inconsistent_or_missing_counters_fail_closed():
 def test_floor_scales_with_occupancy():
     # 1024^3 plugin-pod GEMM: 16 tiles on 256 CUs -> 1/16 of the floor
     n = 1024
-    mops, waves = 2 * n ** 3 // 512, (n // 256) ** 2 * 8
+    mops, waves = 2 * n ** 3 // 512, (n // 256) ** 2 * WPT
     v = verdict(m=n, n=n, k=n, mops=mops, busy=mops // 2, waves=waves, gui=8 * 40000)
     assert v["mfma_util_floor"] == pytest.approx(0.2 / 16)
     assert v["ok"], v

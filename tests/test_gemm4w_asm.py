@@ -1,0 +1,116 @@
+"""The 4-wave GEMM's generated main loop (native/validator/gen_gemm4w_asm.py
+-> gemm4w_asm.inc): the checked-in file is the generator's output, and the
+schedule keeps the invariants the kernel's correctness rests on (no GPU: the
+instruction text is checked; tests/test_kernels_gpu.py runs the kernel).
+
+Invariants of schedule 2 (the shipped loop, avk_g4_mainloop2):
+  * every slice issues 64 MFMAs, 16 fragment reads and 8 LDS-DMA pieces;
+  * an A fragment register is re-read >= 3 MFMAs after its last use, and B
+    reads only go to the other parity's set;
+  * each piece's M0 write has >= 1 instruction between it and its load, and
+    the next M0 write comes only after that load (M0 is read at issue);
+  * consecutive pieces are >= 8 MFMAs apart (closer spacing was measured to
+    corrupt the LDS image, variants 22/23 of round 4);
+  * at most one filler (DS read, M0 write, load) per MFMA gap;
+  * the slice ends with vmcnt(24) lgkmcnt(0) then s_barrier (3 slices of
+    8 pieces in flight).
+"""
+
+import importlib.util
+import pathlib
+import re
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+GEN = ROOT / "native" / "validator" / "gen_gemm4w_asm.py"
+INC = ROOT / "native" / "validator" / "gemm4w_asm.inc"
+
+
+def _gen():
+    spec = importlib.util.spec_from_file_location("gen_gemm4w_asm", GEN)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_checked_in_inc_is_the_generator_output():
+    g = _gen()
+    assert INC.read_text() == g.render() + g.render2() + g.render3(), \
+        "run: python3 native/validator/gen_gemm4w_asm.py > " + str(INC)
+
+
+def _slices(lines):
+    """Split the program after the first MFMA into slices ending in s_barrier
+    (or the exit branch target)."""
+    out, cur, started = [], [], False
+    for ln in lines:
+        if ln.startswith("v_mfma"):
+            started = True
+        if not started:
+            continue
+        cur.append(ln)
+        if ln == "s_barrier":
+            out.append(cur)
+            cur = []
+    return out
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("sched", [2, 3])
+def test_schedule_slice_invariants(sched):
+    g = _gen()
+    prog = g.program2() if sched == 2 else g.program3()
+    vm = g.VM_INFLIGHT if sched == 2 else g.S3_VM
+    spacing = 8 if sched == 2 else 4
+    slices = _slices(prog)
+    assert len(slices) == 11  # the peeled first slice + the 10-slice body
+    for n, sl in enumerate(slices):
+        body = [ln for ln in sl if not ln.endswith(":")]
+        mfma = [i for i, ln in enumerate(body) if ln.startswith("v_mfma")]
+        assert len(mfma) == 64
+        assert sum(ln.startswith("ds_read_b128") for ln in body) == 16
+        loads = [i for i, ln in enumerate(body) if ln.startswith("global_load_lds_dwordx4")]
+        pos = 0 if n == 0 else n - 1  # body position: the peeled slice 0, then 0..9
+        assert len(loads) == (8 if sched == 2 else 16 if pos % 2 == 0 else 0)
+        assert body[-4:] == [f"s_waitcnt vmcnt({vm}) lgkmcnt(0)", f"s_cmp_eq_u32 {g.S2_CNT}, 0",
+                             "s_cbranch_scc1 3f", "s_barrier"]
+        # one filler per gap
+        for a, b in zip(mfma, mfma[1:]):
+            fill = [ln for ln in body[a + 1:b] if ln.startswith(("ds_read", "global_load", "s_add_u32 m0"))]
+            assert len(fill) <= 1, body[a:b + 1]
+        # M0 write -> its load: at least one instruction between; nothing else writes M0 in between
+        m0 = [i for i, ln in enumerate(body) if ln.startswith("s_add_u32 m0")]
+        assert len(m0) == len(loads)
+        for w, ld in zip(m0, loads):
+            assert 1 < ld - w and not any(ln.startswith("s_add_u32 m0") for ln in body[w + 1:ld])
+        # pieces spaced (schedule 2: 8 MFMAs; schedule 3: 4, each slice pair's halves back to back)
+        at = [sum(1 for i in mfma if i < ld) for ld in loads]
+        assert all(b - a >= spacing for a, b in zip(at, at[1:]))
+        # A rows re-read in place only >= 3 MFMAs after the last MFMA reading them
+        for k, ln in enumerate(body):
+            m = re.match(r"ds_read_b128 (v\[\d+:\d+\])", ln)
+            if not m:
+                continue
+            reg = m.group(1)
+            before = [i for i in mfma if i < k]
+            users = [n for n, i in enumerate(before) if reg in body[i].split(", ")[1:3]]
+            if users:
+                assert len(before) - 1 - users[-1] >= 2, (ln, len(before), users[-1])
+            after = [i for i in mfma if i > k]
+            # the register is not an MFMA source again in this slice (it holds the next slice's fragment)
+            assert not any(reg in body[i].split(", ")[1:3] for i in after), ln
+
+
+def test_schedule2_slot_rotation_covers_the_ring():
+    g = _gen()
+    reads, writes = [], []
+    for pos in range(10):
+        sl = g.s2_slice(pos)
+        m0 = [int(ln.rsplit(", ", 1)[1]) for ln in sl if ln.startswith("s_add_u32 m0")]
+        writes.append(min(m0) // g.SLICE_BYTES)
+        reads.append((pos + 1) % g.NSLOT)
+    assert writes == [p % 5 for p in range(10)]
+    # a slot is refilled only in the slice after the one that read it
+    for pos in range(10):
+        assert writes[pos] == reads[(pos - 1) % 10]

@@ -1,8 +1,11 @@
-"""The shipped validator kernels carry one GEMM: the default 8-phase MFMA
-kernel (variant 6) that the native validator and its AQL counter gate
-dispatch.  The nine A/B kernels of rounds 1-2 live in the tools build
-(``make -C native lab``) only."""
+"""The shipped validator kernels carry the GEMMs the validator runs: the
+default 4-wave kernel with the generated main loop (variant 24, what the
+native validator and its AQL counter gate dispatch when K % 256 == 0, named
+in native/include/gemm_default.h), its two other generated schedules (15,
+25) and the 8-phase fallback for the other K (6).  The A/B kernels of rounds
+1-4 live in the tools build (``make -C native lab``) only."""
 
+import pathlib
 import re
 import subprocess
 
@@ -18,11 +21,23 @@ def _gemm_kernels(path):
 
 
 def test_shipped_code_object_has_only_the_default_gemm():
-    assert K.GEMM_DEFAULT_VARIANT == 6
-    # <OUT_F32 = false / true, LOAD_IN_M = false, BAL = false, GROUP_M = 4>: the AQL gate's kGemmSymbol
-    # (a prefix match, native/prof/aql_gate.cpp) and its f32 twin
-    assert _gemm_kernels(native.artefact("validator_kernels.co")) == ["gemm_bf16_nt_8p_kernelILb0ELb0ELb0ELi4E",
-                                                                      "gemm_bf16_nt_8p_kernelILb1ELb0ELb0ELi4E"]
+    assert (K.GEMM_DEFAULT_VARIANT, K.GEMM_FALLBACK_VARIANT) == (24, 6)
+    # <OUT_F32 = false / true, LOOP = 0 / 9 / 10> and <OUT_F32, LOAD_IN_M = false, BAL = false, GROUP_M = 4>
+    assert _gemm_kernels(native.artefact("validator_kernels.co")) == [
+        "gemm_bf16_nt_4wa_kernelILb0ELi0E", "gemm_bf16_nt_4wa_kernelILb0ELi10E", "gemm_bf16_nt_4wa_kernelILb0ELi9E",
+        "gemm_bf16_nt_4wa_kernelILb1ELi0E", "gemm_bf16_nt_4wa_kernelILb1ELi10E", "gemm_bf16_nt_4wa_kernelILb1ELi9E",
+        "gemm_bf16_nt_8p_kernelILb0ELb0ELb0ELi4E", "gemm_bf16_nt_8p_kernelILb1ELb0ELb0ELi4E"]
+
+
+def test_the_gate_dispatches_the_default_kernel():
+    """gemm_default.h's symbol (the AQL gate's prefix match) names exactly one
+    kernel of the code object: variant 24's bf16-out instance."""
+    hdr = (pathlib.Path(__file__).resolve().parents[1] / "native" / "include" / "gemm_default.h").read_text()
+    sym = re.search(r'kGemmSymbol = "(\w+)"', hdr).group(1)
+    assert [n for n in _gemm_kernels(native.artefact("validator_kernels.co")) if sym.startswith(n)] == \
+        ["gemm_bf16_nt_4wa_kernelILb0ELi9E"]
+    assert int(re.search(r"kGemmThreads = (\d+);", hdr).group(1)) == 64 * int(
+        re.search(r"kGemmWavesPerTile = (\d+);", hdr).group(1)) == 256
 
 
 def test_lab_variants_are_served_from_the_tools_build():

@@ -30,11 +30,15 @@ def test_vector_add_exact(n):
 
 
 @pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 320), (1024, 1024, 1024), (2048, 1024, 4096),
-                                   (256, 512, 192), (512, 256, 128)])
+                                   (256, 512, 192), (512, 256, 128), (256, 256, 256), (768, 512, 2304)])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("variant", [K.GEMM_DEFAULT_VARIANT])
+@pytest.mark.parametrize("variant", [None, K.GEMM_FALLBACK_VARIANT, K.GEMM_DEFAULT_VARIANT, 15, 25])
 def test_gemm_vs_fp32_reference(shape, out_dtype, variant):
+    """None: the validator's dispatch (4-wave kernel when K % 256 == 0, else
+    the 8-phase fallback); the 4-wave variants themselves only take K % 256."""
     M, N, Kd = shape
+    if variant not in (None, K.GEMM_FALLBACK_VARIANT) and Kd % K.GEMM_DEFAULT_K_MULTIPLE:
+        pytest.skip("4-wave kernels take K multiples of 256")
     g = torch.Generator(device=DEV).manual_seed(M + N + Kd)
     a = (torch.rand(M, Kd, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
     bt = (torch.rand(N, Kd, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
@@ -46,11 +50,14 @@ def test_gemm_vs_fp32_reference(shape, out_dtype, variant):
     assert err <= tol, (err, tol)
 
 
-@pytest.mark.parametrize("variant", [K.GEMM_DEFAULT_VARIANT])
-def test_gemm_exact_integer_asymmetric(variant):
+@pytest.mark.parametrize("Kd", [128, 512])
+@pytest.mark.parametrize("variant", [None, K.GEMM_FALLBACK_VARIANT, K.GEMM_DEFAULT_VARIANT, 25])
+def test_gemm_exact_integer_asymmetric(variant, Kd):
     # A = small integers, B asymmetric: a transposed C-write or a swapped
     # fragment map changes the result; all sums are exact in fp32.
-    M, N, Kd = 512, 256, 128
+    if variant not in (None, K.GEMM_FALLBACK_VARIANT) and Kd % K.GEMM_DEFAULT_K_MULTIPLE:
+        pytest.skip("4-wave kernels take K multiples of 256")
+    M, N = 512, 256
     i = torch.arange(M, device=DEV).view(M, 1)
     k = torch.arange(Kd, device=DEV).view(1, Kd)
     a = ((i * 3 + k * 7) % 5 - 2).to(torch.bfloat16)
@@ -74,6 +81,10 @@ def test_gemm_rejects_bad_shapes():
     bt = torch.zeros(256, 64, device=DEV, dtype=torch.bfloat16)
     with pytest.raises(ValueError):
         K.gemm_bf16_nt(a, bt)
+    a = torch.zeros(256, 192, device=DEV, dtype=torch.bfloat16)
+    bt = torch.zeros(256, 192, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(K.KernelError):  # the 4-wave kernel refuses K % 256 != 0 (no silent fallback)
+        K.gemm_bf16_nt(a, bt, variant=K.GEMM_DEFAULT_VARIANT)
 
 
 def test_fill_uniform_deterministic_and_bounded():

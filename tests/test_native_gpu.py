@@ -4,6 +4,8 @@ metrics exporter with live data."""
 
 import json
 import os
+import pathlib
+import re
 import subprocess
 import tempfile
 
@@ -13,6 +15,8 @@ from amdgpu_operator import native
 
 pytestmark = pytest.mark.gpu
 VALIDATOR = str(native.binary("amdgpu-validator"))
+_WPT = int(re.search(r"kGemmWavesPerTile = (\d+);", (pathlib.Path(__file__).resolve().parents[1] / "native" / "include"
+                                                     / "gemm_default.h").read_text()).group(1))
 
 
 def _run(args, env=None, timeout=120):
@@ -35,7 +39,7 @@ def test_validator_all_local_steps_with_counter_gate(tmp_path):
     assert g["freivalds_rel_err"] < 1e-4 and g["counter_gate"] == "pass"
     assert g["flop_per_mop"] == 512  # one MFMA "MOP" = 512 FLOP on gfx950 (16x16x32 bf16 = 32 MOPs)
     assert g["gate_mode"] == "aql" and g["gated_output_matches"]
-    assert g["SQ_WAVES"] == (4096 // 256) ** 2 * 8  # 256x256 tiles, 8 waves each
+    assert g["SQ_WAVES"] == (4096 // 256) ** 2 * _WPT  # 256x256 tiles, the default kernel's waves each
     assert g["samples"] == [32, 32, 32, 8]  # per-SE/XCC instances of the SQ counters, 8 GRBM
     assert g["tflops"] > 300
     assert steps["hbm"]["checksum_match"] and steps["hbm"]["gbps"] > 2000
@@ -97,7 +101,7 @@ def test_validator_aql_gate_small_and_rectangular_work(tmp_path):
     rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--gemm", "1024", "--counter-gate"])
     assert rc == 0 and rep["ok"], rep
     g = {s["name"]: s for s in rep["steps"]}["gemm"]
-    assert g["SQ_WAVES"] == 16 * 8 and g["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 == 2 * 1024 ** 3
+    assert g["SQ_WAVES"] == 16 * _WPT and g["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 == 2 * 1024 ** 3
 
 
 def test_validator_ipc_peer_path_two_processes_one_gpu(tmp_path):

@@ -33,7 +33,10 @@ def time_ms(fn, iters):
 GEMM_VARIANTS = {6: "default_8phase", 0: "ring_pingpong", 1: "dbuf", 2: "ring", 3: "w4", 4: "pp_load_in_r", 5: "pp_5slot",
                  7: "8phase_load_in_m", 8: "8phase_bal_load_in_r", 9: "8phase_bal_load_in_m",
                  10: "8phase_group_m8", 11: "8phase_group_m16", 12: "8phase_group_m2",
-                 13: "8phase_lab_copy"}
+                 13: "8phase_lab_copy", 14: "4wave_builtin", 15: "4wave_asm",
+                 16: "4wave_asm_no_glds", 17: "4wave_asm_no_barrier", 18: "4wave_asm_early_rotate",
+                 19: "4wave_asm_no_dsread", 20: "4wave_asm_fixed_m0", 21: "4wave_asm_vgpr_loads",
+                 22: "4wave_asm_piece_pairs", 23: "4wave_asm_piece_burst", 24: "4wave_asm_sched2", 25: "4wave_asm_sched3"}
 
 
 def bench_gemm(n, rounds, iters, variants=None):
