@@ -150,7 +150,7 @@ GEMM_DEFAULT_VARIANT = 24   # 4 waves x 128x128, generated main loop (K a multip
 GEMM_FALLBACK_VARIANT = 6   # 8-phase, 8 waves (K a multiple of 64)
 GEMM_DEFAULT_K_MULTIPLE = 256
 # variants in the shipped library; the rest need `make -C native lab`
-SHIPPED_GEMM_VARIANTS = (6, 15, 24, 25)
+SHIPPED_GEMM_VARIANTS = (6, 15, 24, 25, 26)
 
 
 def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int | None = None):

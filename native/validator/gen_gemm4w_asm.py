@@ -438,5 +438,138 @@ def render3() -> str:
         "\\n\\t".join(program2()), "\\n\\t".join(program3())).replace(
         '"v110", ', '"v110", "v111", ')
 
+# ----------------------------------------------------------------- schedule 4 --
+# 64-deep K stages in 128-B LDS rows (the shape of hipBLASLt's requests):
+# schedules 1-3 move each operand row as two 64-B halves a slice apart, so
+# every LDS-DMA instruction touches 16 rows x 64 B (TCC_HIT 2.3x hipBLASLt's;
+# the guide's measurement of the same shapes: address-unit busy 2x).  Here a
+# piece is 8 rows x 128 B - whole lines - into an XOR-swizzled [rows][128 B]
+# image, physical 16-B chunk p of row r holding logical chunk p ^ swz(r),
+# swz(r) = ((r & 2) << 1) | ((r & 4) >> 1) (every ds_read_b128 lane group
+# meets 16 distinct bank slots, tests/test_gemm4w_asm.py).
+# The ring holds 5 units of 32 KiB, a unit = one operand of one stage
+# (A_t = unit 2t, B_t = unit 2t + 1, slot = unit % 5).  Sub-slice u (k-half
+# u & 1 of stage u >> 1, 64 MFMAs) reads the fragments of u + 1 and loads
+# unit u + 4 into the slot the last reader left at the barrier before it;
+# units of stage s must be in LDS by the barrier that ends sub-slice 2s - 2:
+# vmcnt(8) after even sub-slices, vmcnt(16) after odd ones.
+S4_SWZ = [((r & 2) << 1) | ((r & 4) >> 1) for r in range(8)]
+UNIT_BYTES = 32 * 1024
+S4_SA, S4_SB = "s[64:65]", "s[66:67]"
+S4_SA_LO, S4_SA_HI, S4_SB_LO, S4_SB_HI = "s64", "s65", "s66", "s67"
+S4_WAVE, S4_CNT, S4_KEEP, S4_INC, S4_ROW = "s68", "s69", "s70", "s71", "s72"
+S4_SGPRS = range(64, 73)
+# fragment address bases: (operand, h) -> VGPR for slots 0/1, 2/3, 4
+S4_FBASE = {("A", 0): ("v104", "v106", "v108"), ("A", 1): ("v105", "v107", "v109"),
+            ("B", 0): ("v110", "v112", "v114"), ("B", 1): ("v111", "v113", "v115")}
+S4_VOFF = [f"v{116 + j}" for j in range(8)]  # piece j's per-lane global offset (rows 8j..)
+S4_VGPRS = 124
+S4_B_READ = {4 * j + 1: j for j in range(8)}
+S4_A_READ = {8 * i + 10: i for i in range(6)}
+S4_A_READ.update({37: 6, 45: 7})
+S4_M0_AT = {8 * q + 6: q for q in range(8)}
+S4_LOAD_AT = {8 * q + 7: q for q in range(8)}
+
+
+def s4_addr(op: str, h: int, slot: int, i: int) -> str:
+    base = S4_FBASE[(op, h)][slot // 2]
+    return f"{base} offset:{(slot % 2) * UNIT_BYTES + i * 2048}"
+
+
+def s4_m0(slot: int, j: int) -> str:
+    return f"s_add_u32 m0, {S4_WAVE}, {slot * UNIT_BYTES + j * 1024}"
+
+
+def s4_slice(pos: int, first: bool = False, label: str | None = None) -> list[str]:
+    """Sub-slice at body position `pos` (u mod 10)."""
+    parity, nxt = pos % 2, 1 - pos % 2
+    stage = (pos + 1) >> 1                 # stage of the fragments read (mod 5)
+    h = (pos + 1) & 1
+    aslot, bslot = (2 * stage) % NSLOT, (2 * stage + 1) % NSLOT
+    lslot = (pos + 4) % NSLOT              # unit u + 4
+    even = pos % 2 == 0                    # the unit loaded is an A unit
+    src = S4_SA if even else S4_SB
+    lines = [f"{label}:"] if label else []
+    for m in range(64):
+        i, j = m >> 3, m & 7
+        c = "0" if first else acc(i, j)
+        lines.append(f"v_mfma_f32_16x16x32_bf16 {acc(i, j)}, {b_reg(j, parity)}, {a_reg(i, parity)}, {c}")
+        if m in S4_B_READ:
+            jj = S4_B_READ[m]
+            lines.append(f"ds_read_b128 {b_reg(jj, nxt)}, {s4_addr('B', h, bslot, jj)}")
+        if m in S4_A_READ:
+            ii = S4_A_READ[m]
+            lines.append(f"ds_read_b128 {a_reg(ii, nxt)}, {s4_addr('A', h, aslot, ii)}")
+        if m in S4_M0_AT:
+            lines.append(s4_m0(lslot, S4_M0_AT[m]))
+        if m in S4_LOAD_AT:
+            lines.append(f"global_load_lds_dwordx4 {S4_VOFF[S4_LOAD_AT[m]]}, {src}")
+        if m == 40:
+            lines += [f"s_sub_u32 {S4_CNT}, {S4_CNT}, 1"]
+        if m == 41:  # the next unit of this operand exists: move its base one stage on
+            lines += [f"s_cmp_ge_u32 {S4_CNT}, {7 if even else 6}", f"s_cselect_b32 {S4_INC}, 0x80, 0"]
+    lo, hi = (S4_SA_LO, S4_SA_HI) if even else (S4_SB_LO, S4_SB_HI)
+    lines += [f"s_add_u32 {lo}, {lo}, {S4_INC}", f"s_addc_u32 {hi}, {hi}, 0",
+              f"s_waitcnt vmcnt({8 if even else 16}) lgkmcnt(0)", f"s_cmp_eq_u32 {S4_CNT}, 0", "s_cbranch_scc1 3f",
+              "s_barrier"]
+    return lines
+
+
+def program4() -> list[str]:
+    lines = [f"s_mov_b32 {S4_KEEP}, m0",
+             f"s_mov_b32 {S4_SA_LO}, %[a_lo]", f"s_mov_b32 {S4_SA_HI}, %[a_hi]",
+             f"s_mov_b32 {S4_SB_LO}, %[b_lo]", f"s_mov_b32 {S4_SB_HI}, %[b_hi]",
+             f"s_mov_b32 {S4_WAVE}, %[wave_lds]", f"s_lshl_b32 {S4_CNT}, %[ns], 1",  # sub-slices left, this one included
+             f"s_mov_b32 {S4_ROW}, %[ps]",
+             "v_mov_b32 v104, %[la0]", "v_mov_b32 v105, %[la1]", "v_mov_b32 v110, %[lb0]", "v_mov_b32 v111, %[lb1]",
+             f"v_mov_b32 {S4_VOFF[0]}, %[g_off]"]
+    for op in ("A", "B"):
+        for h in (0, 1):
+            b0, b2, b4 = S4_FBASE[(op, h)]
+            lines += [f"v_add_u32 {b2}, {2 * UNIT_BYTES}, {b0}", f"v_add_u32 {b4}, {4 * UNIT_BYTES}, {b0}"]
+    for j in range(1, 8):
+        lines.append(f"v_add_u32 {S4_VOFF[j]}, {S4_ROW}, {S4_VOFF[j - 1]}")
+    for unit in range(4):  # A_0, B_0, A_1, B_1 into slots 0..3
+        lo, hi, src = (S4_SA_LO, S4_SA_HI, S4_SA) if unit % 2 == 0 else (S4_SB_LO, S4_SB_HI, S4_SB)
+        for j in range(8):
+            lines += [s4_m0(unit, j), "s_nop 0", f"global_load_lds_dwordx4 {S4_VOFF[j]}, {src}"]
+        lines += ["s_nop 4", f"s_add_u32 {lo}, {lo}, 0x80", f"s_addc_u32 {hi}, {hi}, 0"]
+    lines += ["s_waitcnt vmcnt(16)", "s_barrier"]  # A_0, B_0 landed and visible
+    for i in range(8):
+        lines.append(f"ds_read_b128 {a_reg(i, 0)}, {s4_addr('A', 0, 0, i)}")
+    for j in range(8):
+        lines.append(f"ds_read_b128 {b_reg(j, 0)}, {s4_addr('B', 0, 1, j)}")
+    lines += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+    lines += s4_slice(0, first=True)
+    lines += ["s_branch 2f"]
+    lines += ["1:"] + s4_slice(0)
+    lines += s4_slice(1, label="2")
+    for pos in range(2, 10):
+        lines += s4_slice(pos)
+    lines += ["s_branch 1b", "3:",
+              "s_waitcnt vmcnt(0)", "s_nop 15", "s_nop 15", f"s_mov_b32 m0, {S4_KEEP}"]
+    return lines
+
+
+def render4() -> str:
+    body = "\\n\\t".join(program4())
+    clob = ", ".join([f'"v{r}"' for r in range(S4_VGPRS)] + [f'"s{r}"' for r in S4_SGPRS]
+                     + [f'"a{r}"' for r in range(256)])
+    return ("// Schedule 4: 64-deep stages in 128-B rows.  a_lo/a_hi, b_lo/b_hi: global byte\n"
+            "// address of this wave's first A / B row (rows wave*64..), stage 0; ps: 8 rows\n"
+            "// in bytes; wave_lds: LDS byte address of this wave's first piece (slot 0);\n"
+            "// ns = K / 64; la0/la1, lb0/lb1: per-lane LDS byte address of fragment 0 of\n"
+            "// A / B, k-half 0 / 1, slot 0; g_off: per-lane byte offset in piece 0.\n"
+            "__device__ __forceinline__ void avk_g4_mainloop4(unsigned a_lo, unsigned a_hi, unsigned b_lo, unsigned b_hi,\n"
+            "                                                 unsigned ps, unsigned wave_lds, unsigned ns, unsigned la0,\n"
+            "                                                 unsigned la1, unsigned lb0, unsigned lb1, unsigned g_off) {\n"
+            f'  asm volatile("{body}"\n'
+            "               :\n"
+            "               : [a_lo] \"s\"(a_lo), [a_hi] \"s\"(a_hi), [b_lo] \"s\"(b_lo), [b_hi] \"s\"(b_hi), [ps] \"s\"(ps),\n"
+            "                 [wave_lds] \"s\"(wave_lds), [ns] \"s\"(ns), [la0] \"v\"(la0), [la1] \"v\"(la1),\n"
+            "                 [lb0] \"v\"(lb0), [lb1] \"v\"(lb1), [g_off] \"v\"(g_off)\n"
+            f"               : \"memory\", \"scc\", {clob});\n"
+            "}\n")
+
 if __name__ == "__main__":
-    sys.stdout.write(render() + render2() + render3())
+    sys.stdout.write(render() + render2() + render3() + render4())

@@ -1229,6 +1229,9 @@ __global__ __launch_bounds__(g4::NTHR, 1) void gemm_bf16_nt_4w_kernel(const __bf
 // above moves accumulators through VGPRs every slice).
 #include "gemm4w_asm.inc"
 
+// schedule 4's image: physical 16-B chunk p of a 128-B row r holds logical chunk p ^ g4_swz128(r % 8)
+__device__ __forceinline__ int g4_swz128(int r) { return ((r & 2) << 1) | ((r & 4) >> 1); }
+
 template <int T>
 __device__ __forceinline__ f32x4 g4_acc() {
   float x0, x1, x2, x3;
@@ -1314,7 +1317,18 @@ __global__ __launch_bounds__(g4::NTHR, 1) void gemm_bf16_nt_4wa_kernel(const __b
                      __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
                      (unsigned)(16 * K * 2), __builtin_amdgcn_readfirstlane(lds + wave * 4 * 1024), (unsigned)nk, a_off,
                      b_off, g_off);
-  else
+  else if constexpr (LOOP == 11) {
+    // schedule 4: 8-row x 128-B pieces, rows of the [rows][128 B] image swizzled by g4_swz128
+    const int pr = lane >> 3;
+    const unsigned g4off = (unsigned)((pr * K + ((lane & 7) ^ g4_swz128(pr)) * 8) * 2);
+    const unsigned fch0 = (unsigned)((((lane >> 4) ^ g4_swz128(fr & 7))) * 16);
+    const unsigned fch1 = fch0 ^ 64u;  // k-half 1: logical chunk + 4
+    const unsigned la = lds + (wm * 128 + fr) * 128, lb = lds + (wn * 128 + fr) * 128;
+    avk_g4_mainloop4(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
+                     __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
+                     (unsigned)(8 * K * 2), __builtin_amdgcn_readfirstlane(lds + wave * 8 * 1024), (unsigned)(K / 64),
+                     la + fch0, la + fch1, lb + fch0, lb + fch1, g4off);
+  } else
     avk_g4_mainloop3(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
                      __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
                      (unsigned)(16 * K * 2), __builtin_amdgcn_readfirstlane(lds + wave * 4 * 1024), (unsigned)nk, a_off,
@@ -1685,6 +1699,7 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
     AVK_G4A(15, 0)  // schedule 1 of the generated main loop
     AVK_G4A(24, 9)  // schedule 2: 10-slice unrolled body, constant addresses, one filler per MFMA gap
     AVK_G4A(25, 10)  // schedule 3: schedule 2 with the loads in slice pairs (whole 128-B lines back to back)
+    AVK_G4A(26, 11)  // schedule 4: 64-deep stages in 128-B rows, 8-row x 128-B pieces
 #if AVK_GEMM_LAB
     case 14:  // the 4-wave kernel in builtins (hipcc moves accumulators through VGPRs, spills)
       if (K % 256) return hipErrorInvalidValue;

@@ -34,7 +34,7 @@ def _gen():
 
 def test_checked_in_inc_is_the_generator_output():
     g = _gen()
-    assert INC.read_text() == g.render() + g.render2() + g.render3(), \
+    assert INC.read_text() == g.render() + g.render2() + g.render3() + g.render4(), \
         "run: python3 native/validator/gen_gemm4w_asm.py > " + str(INC)
 
 
@@ -114,3 +114,55 @@ def test_schedule2_slot_rotation_covers_the_ring():
     # a slot is refilled only in the slice after the one that read it
     for pos in range(10):
         assert writes[pos] == reads[(pos - 1) % 10]
+
+
+# ds_read_b128 serves a wave in four groups of 16 lanes; a group is conflict
+# free when its 16 addresses fall in 16 distinct 16-B slots of the 256-B bank row
+_DS_GROUPS = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+              list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32)),
+              list(range(32, 36)) + list(range(44, 48)) + list(range(52, 60)),
+              list(range(36, 44)) + list(range(48, 52)) + list(range(60, 64))]
+
+
+def test_schedule4_image_is_conflict_free_and_a_bijection():
+    g = _gen()
+    swz = g.S4_SWZ
+    assert swz == [((r & 2) << 1) | ((r & 4) >> 1) for r in range(8)]
+    for h in (0, 1):  # k-half of the 64-deep stage
+        for base in range(0, 256, 16):  # fragment rows base..base+15 (wave tile rows)
+            for grp in _DS_GROUPS:
+                slots = set()
+                for lane in grp:
+                    r = base + (lane & 15)
+                    p = (4 * h + (lane >> 4)) ^ swz[r % 8]
+                    slots.add(((r * 128 + p * 16) % 256) // 16)
+                assert len(slots) == 16
+    # the LDS-DMA side: lane l of a piece writes physical chunk l & 7 of row l >> 3 and
+    # fetches logical chunk (l & 7) ^ swz(row): every logical chunk of every row once
+    got = {((lane >> 3), (lane & 7) ^ swz[lane >> 3]) for lane in range(64)}
+    assert got == {(r, c) for r in range(8) for c in range(8)}
+
+
+def test_schedule4_ring_and_counts():
+    """Unit u + 4 loads in sub-slice u into a slot whose unit was last read in
+    sub-slice u - 1 at the latest; the units of stage s are waited for at the
+    barrier ending sub-slice 2s - 2 (vmcnt(8): the 8 pieces issued in it stay
+    out) and never earlier than they were issued."""
+    g = _gen()
+    for pos in range(10):
+        sl = g.s4_slice(pos)
+        m0 = [int(ln.rsplit(", ", 1)[1]) for ln in sl if ln.startswith("s_add_u32 m0")]
+        assert {x // g.UNIT_BYTES for x in m0} == {(pos + 4) % 5}
+        assert sorted(x % g.UNIT_BYTES for x in m0) == [j * 1024 for j in range(8)]
+        assert any(f"vmcnt({8 if pos % 2 == 0 else 16}) lgkmcnt(0)" in ln for ln in sl)
+    # slot reuse: over a long run, the unit in a slot is read (sub-slices 2s-1, 2s for unit of
+    # stage s) strictly before the next unit is loaded into it (sub-slice unit + 4 - 5 + ... )
+    last_read = {}
+    for u in range(0, 200):
+        s = (u + 1) >> 1  # stage whose fragments are read in u
+        for unit in (2 * s, 2 * s + 1):
+            last_read[unit] = u
+        loaded = u + 4
+        prev = loaded - 5  # the unit that slot held
+        if prev >= 0:
+            assert last_read.get(prev, -1) < u, (u, prev)

@@ -1,8 +1,8 @@
 """The shipped validator kernels carry the GEMMs the validator runs: the
 default 4-wave kernel with the generated main loop (variant 24, what the
 native validator and its AQL counter gate dispatch when K % 256 == 0, named
-in native/include/gemm_default.h), its two other generated schedules (15,
-25) and the 8-phase fallback for the other K (6).  The A/B kernels of rounds
+in native/include/gemm_default.h), its other generated schedules (15, 25,
+26) and the 8-phase fallback for the other K (6).  The A/B kernels of rounds
 1-4 live in the tools build (``make -C native lab``) only."""
 
 import pathlib
@@ -22,11 +22,12 @@ def _gemm_kernels(path):
 
 def test_shipped_code_object_has_only_the_default_gemm():
     assert (K.GEMM_DEFAULT_VARIANT, K.GEMM_FALLBACK_VARIANT) == (24, 6)
-    # <OUT_F32 = false / true, LOOP = 0 / 9 / 10> and <OUT_F32, LOAD_IN_M = false, BAL = false, GROUP_M = 4>
-    assert _gemm_kernels(native.artefact("validator_kernels.co")) == [
-        "gemm_bf16_nt_4wa_kernelILb0ELi0E", "gemm_bf16_nt_4wa_kernelILb0ELi10E", "gemm_bf16_nt_4wa_kernelILb0ELi9E",
-        "gemm_bf16_nt_4wa_kernelILb1ELi0E", "gemm_bf16_nt_4wa_kernelILb1ELi10E", "gemm_bf16_nt_4wa_kernelILb1ELi9E",
-        "gemm_bf16_nt_8p_kernelILb0ELb0ELb0ELi4E", "gemm_bf16_nt_8p_kernelILb1ELb0ELb0ELi4E"]
+    # <OUT_F32 = false / true, LOOP = 0 / 9 / 10 / 11: variants 15 / 24 / 25 / 26> and
+    # <OUT_F32, LOAD_IN_M = false, BAL = false, GROUP_M = 4>: variant 6
+    loops = (0, 9, 10, 11)
+    assert _gemm_kernels(native.artefact("validator_kernels.co")) == sorted(
+        [f"gemm_bf16_nt_4wa_kernelILb{f}ELi{lp}E" for f in (0, 1) for lp in loops]
+        + ["gemm_bf16_nt_8p_kernelILb0ELb0ELb0ELi4E", "gemm_bf16_nt_8p_kernelILb1ELb0ELb0ELi4E"])
 
 
 def test_the_gate_dispatches_the_default_kernel():
