@@ -182,6 +182,7 @@ class Connection:
         self.conn_send_window = DEFAULT_WINDOW
         self.conn_recv_consumed = 0
         self.streams: dict[int, _Stream] = {}
+        self.max_peer_sid = 0  # highest stream id the peer opened (ids only grow, RFC 9113 5.1.1)
         self.closed = False
         self.goaway = False
         self.next_id = 1
@@ -392,6 +393,9 @@ class Connection:
                         return  # a stream we no longer track
                     if s % 2 == 0:
                         raise ConnectionClosed(f"client stream id {s} is even")
+                    if s <= self.max_peer_sid:  # a frame for a stream that already closed: not a new call
+                        return
+                    self.max_peer_sid = s
                     if len(self.streams) >= MAX_STREAMS:
                         self.send_rst(s, REFUSED_STREAM)
                         return

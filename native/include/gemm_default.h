@@ -9,9 +9,10 @@
 
 namespace avk {
 
-// gemm_bf16_nt_4wa_kernel<OUT_F32=false, LOOP=9>: 256x256 tile, 4 waves of
-// 128x128, the generated main loop of schedule 2 (validator/gen_gemm4w_asm.py)
-constexpr const char* kGemmSymbol = "gemm_bf16_nt_4wa_kernelILb0ELi9EE";
+// gemm_bf16_nt_4wa_kernel<OUT_F32=false, LOOP=13> (variant 28): 256x256
+// tile, 4 waves of 128x128, the generated main loop of schedule 4c
+// (validator/gen_gemm4w_asm.py: 64-deep stages in 128-B LDS rows)
+constexpr const char* kGemmSymbol = "gemm_bf16_nt_4wa_kernelILb0ELi13EE";
 constexpr int kGemmThreads = 256;      // workgroup size
 constexpr int kGemmWavesPerTile = 4;   // kGemmThreads / 64
 constexpr int kGemmTile = 256;         // M and N multiple

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Generate gemm4w_asm.inc: the main loop of the 4-wave 256x256 bf16 GEMM
-(validator_kernels.hip, gemm_bf16_nt_4w_kernel) as ONE inline-asm statement.
+(validator_kernels.hip, gemm_bf16_nt_4wa_kernel) as ONE inline-asm statement.
 
 Why asm: the kernel keeps 256 fp32 accumulators per lane (a 128x128 wave
 tile of v_mfma_f32_16x16x32_bf16) - the whole AGPR half of the register file
@@ -10,26 +10,37 @@ v_accvgpr_read/write/mov every slice and spilling to scratch (measured on
 every builtin variant of this loop: 44-840 copies per 64 MFMAs).  Written as
 one statement, every register is placed once and the instruction stream is
 exactly the schedule below; tests/test_gemm4w_asm.py checks this file is
-regenerated whenever the generator changes, and tests/test_kernels_gpu.py
-checks the kernel against an fp32 reference.
+regenerated whenever the generator changes and the schedules' invariants,
+tests/test_kernels_gpu.py checks the kernels against an fp32 reference.
+
+Schedules (each a function of this file; profiles/r4_gemm/ has the A/B):
+  1  32-deep slices in a 5-slot ring of 64-B rows, slot registers rotated by
+     SALU every slice (variant 15)
+  2  the same ring, the body unrolled over 10 slices so every address is a
+     constant, one filler per MFMA gap (24)
+  3  2 with each slice pair's pieces back to back (25)
+  4  64-deep stages in 128-B rows: whole-line LDS-DMA pieces, a ring of 5
+     operand units (26); 4b drops the barriers the ring does not need (27);
+     4c also issues each B unit early in its sub-slice (28, SHIPPED)
+The 64-B-row schedules ask L2 for every line twice (TCC_HIT 2.3x hipBLASLt's
+at equal misses): the step from 2 to 4 is worth 11 % (1273 -> 1416 TF/s at
+4096^3) and takes MFMA utilisation from 0.75 to 0.83.
 
 Register map (all named, all clobbered by the statement):
   a[0:255]   acc tile (i, j) of the wave's 8x8 grid at a[4(8i+j) : 4(8i+j)+3]
   v[0:23]    A fragments of rows 0-5 (re-read in place after their last use)
   v[24:31] / v[32:39]  A fragments of rows 6, 7: two sets, by slice parity
   v[40:71] / v[72:103] B fragments 0-7: two sets, by slice parity
-  v104/v105  per-lane LDS byte address of the A / B fragment (slot offset 0)
-  v106       per-lane global byte offset of this lane's 16 B in a piece
-  v107/v108  A / B fragment read address of the slice being read
+  v104..     addresses (per schedule, see its section)
 Per slice (32 deep, 1,024 MFMA cycles on the SIMD), interleaved between its
-64 MFMAs: the 16 ds_read_b128 of the next slice's fragments, and this wave's
-8 LDS-DMA pieces (global_load_lds_dwordx4, 1 KiB each) of slice s+5 into the
-slot slice s left; then vmcnt(24) (three slices stay in flight), lgkmcnt(0)
-and one s_barrier.  Hazards handled in the text: M0 write -> LDS-DMA one wait
-state (s_nop 0); the last MFMA's result -> the epilogue's v_accvgpr_read
-(s_nop 15 x 2 closes the statement); a fragment register is re-read 3 MFMAs
-after its last use (hipcc's own hazard recognizer pads a DS write after an
-MFMA source read with nothing).
+64 MFMAs: the 16 ds_read_b128 of the next slice's fragments and this wave's
+8 LDS-DMA pieces (global_load_lds_dwordx4, 1 KiB each) of a later slice into
+a slot the barrier freed; then the counted vmcnt, lgkmcnt(0) and s_barrier.
+Hazards handled in the text: M0 write -> LDS-DMA one wait state; the last
+MFMA's result -> the epilogue's v_accvgpr_read (s_nop 15 x 2 closes the
+statement); a fragment register is re-read 3 MFMAs after its last use
+(hipcc's own hazard recognizer pads a DS write after an MFMA source read with
+nothing).
 """
 
 from __future__ import annotations
@@ -480,8 +491,17 @@ def s4_m0(slot: int, j: int) -> str:
     return f"s_add_u32 m0, {S4_WAVE}, {slot * UNIT_BYTES + j * 1024}"
 
 
+S4_OPTS = {"odd_barrier": True, "early_b": False}
+S4_M0_EARLY = {4 * q + 2: q for q in range(8)}    # a B unit's pieces in the first half of its sub-slice
+S4_LOAD_EARLY = {4 * q + 3: q for q in range(8)}
+
+
 def s4_slice(pos: int, first: bool = False, label: str | None = None) -> list[str]:
-    """Sub-slice at body position `pos` (u mod 10)."""
+    """Sub-slice at body position `pos` (u mod 10).  Only the barriers that
+    end EVEN sub-slices are needed (the slot a sub-slice refills was last read
+    at or before the even sub-slice before it, and units become visible at
+    even barriers); with S4_OPTS["odd_barrier"] False the odd ones end with
+    the wave's own lgkmcnt(0) only."""
     parity, nxt = pos % 2, 1 - pos % 2
     stage = (pos + 1) >> 1                 # stage of the fragments read (mod 5)
     h = (pos + 1) & 1
@@ -500,18 +520,23 @@ def s4_slice(pos: int, first: bool = False, label: str | None = None) -> list[st
         if m in S4_A_READ:
             ii = S4_A_READ[m]
             lines.append(f"ds_read_b128 {a_reg(ii, nxt)}, {s4_addr('A', h, aslot, ii)}")
-        if m in S4_M0_AT:
-            lines.append(s4_m0(lslot, S4_M0_AT[m]))
-        if m in S4_LOAD_AT:
-            lines.append(f"global_load_lds_dwordx4 {S4_VOFF[S4_LOAD_AT[m]]}, {src}")
+        m0_at, load_at = ((S4_M0_EARLY, S4_LOAD_EARLY) if S4_OPTS["early_b"] and not even
+                          else (S4_M0_AT, S4_LOAD_AT))
+        if m in m0_at:
+            lines.append(s4_m0(lslot, m0_at[m]))
+        if m in load_at:
+            lines.append(f"global_load_lds_dwordx4 {S4_VOFF[load_at[m]]}, {src}")
         if m == 40:
             lines += [f"s_sub_u32 {S4_CNT}, {S4_CNT}, 1"]
         if m == 41:  # the next unit of this operand exists: move its base one stage on
             lines += [f"s_cmp_ge_u32 {S4_CNT}, {7 if even else 6}", f"s_cselect_b32 {S4_INC}, 0x80, 0"]
     lo, hi = (S4_SA_LO, S4_SA_HI) if even else (S4_SB_LO, S4_SB_HI)
-    lines += [f"s_add_u32 {lo}, {lo}, {S4_INC}", f"s_addc_u32 {hi}, {hi}, 0",
-              f"s_waitcnt vmcnt({8 if even else 16}) lgkmcnt(0)", f"s_cmp_eq_u32 {S4_CNT}, 0", "s_cbranch_scc1 3f",
-              "s_barrier"]
+    lines += [f"s_add_u32 {lo}, {lo}, {S4_INC}", f"s_addc_u32 {hi}, {hi}, 0"]
+    if even or S4_OPTS["odd_barrier"]:
+        lines += [f"s_waitcnt vmcnt({8 if even else 16}) lgkmcnt(0)", f"s_cmp_eq_u32 {S4_CNT}, 0",
+                  "s_cbranch_scc1 3f", "s_barrier"]
+    else:
+        lines += ["s_waitcnt lgkmcnt(0)", f"s_cmp_eq_u32 {S4_CNT}, 0", "s_cbranch_scc1 3f"]
     return lines
 
 
@@ -551,8 +576,10 @@ def program4() -> list[str]:
     return lines
 
 
-def render4() -> str:
+def render4(suffix: str = "", **opts) -> str:
+    S4_OPTS.update({"odd_barrier": True, "early_b": False}, **opts)
     body = "\\n\\t".join(program4())
+    S4_OPTS.update(odd_barrier=True, early_b=False)
     clob = ", ".join([f'"v{r}"' for r in range(S4_VGPRS)] + [f'"s{r}"' for r in S4_SGPRS]
                      + [f'"a{r}"' for r in range(256)])
     return ("// Schedule 4: 64-deep stages in 128-B rows.  a_lo/a_hi, b_lo/b_hi: global byte\n"
@@ -560,7 +587,7 @@ def render4() -> str:
             "// in bytes; wave_lds: LDS byte address of this wave's first piece (slot 0);\n"
             "// ns = K / 64; la0/la1, lb0/lb1: per-lane LDS byte address of fragment 0 of\n"
             "// A / B, k-half 0 / 1, slot 0; g_off: per-lane byte offset in piece 0.\n"
-            "__device__ __forceinline__ void avk_g4_mainloop4(unsigned a_lo, unsigned a_hi, unsigned b_lo, unsigned b_hi,\n"
+            f"__device__ __forceinline__ void avk_g4_mainloop4{suffix}(unsigned a_lo, unsigned a_hi, unsigned b_lo, unsigned b_hi,\n"
             "                                                 unsigned ps, unsigned wave_lds, unsigned ns, unsigned la0,\n"
             "                                                 unsigned la1, unsigned lb0, unsigned lb1, unsigned g_off) {\n"
             f'  asm volatile("{body}"\n'
@@ -571,5 +598,10 @@ def render4() -> str:
             f"               : \"memory\", \"scc\", {clob});\n"
             "}\n")
 
+def render_all() -> str:
+    return (render() + render2() + render3() + render4() + render4("b", odd_barrier=False)
+            + render4("c", odd_barrier=False, early_b=True))
+
+
 if __name__ == "__main__":
-    sys.stdout.write(render() + render2() + render3() + render4())
+    sys.stdout.write(render_all())

@@ -1317,17 +1317,22 @@ __global__ __launch_bounds__(g4::NTHR, 1) void gemm_bf16_nt_4wa_kernel(const __b
                      __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
                      (unsigned)(16 * K * 2), __builtin_amdgcn_readfirstlane(lds + wave * 4 * 1024), (unsigned)nk, a_off,
                      b_off, g_off);
-  else if constexpr (LOOP == 11) {
+  else if constexpr (LOOP >= 11 && LOOP <= 13) {
     // schedule 4: 8-row x 128-B pieces, rows of the [rows][128 B] image swizzled by g4_swz128
     const int pr = lane >> 3;
     const unsigned g4off = (unsigned)((pr * K + ((lane & 7) ^ g4_swz128(pr)) * 8) * 2);
     const unsigned fch0 = (unsigned)((((lane >> 4) ^ g4_swz128(fr & 7))) * 16);
     const unsigned fch1 = fch0 ^ 64u;  // k-half 1: logical chunk + 4
     const unsigned la = lds + (wm * 128 + fr) * 128, lb = lds + (wn * 128 + fr) * 128;
-    avk_g4_mainloop4(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
-                     __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
-                     (unsigned)(8 * K * 2), __builtin_amdgcn_readfirstlane(lds + wave * 8 * 1024), (unsigned)(K / 64),
-                     la + fch0, la + fch1, lb + fch0, lb + fch1, g4off);
+#define AVK_G4_ARGS4                                                                                         \
+  __builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),       \
+      __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),   \
+      (unsigned)(8 * K * 2), __builtin_amdgcn_readfirstlane(lds + wave * 8 * 1024), (unsigned)(K / 64),      \
+      la + fch0, la + fch1, lb + fch0, lb + fch1, g4off
+    if constexpr (LOOP == 11) avk_g4_mainloop4(AVK_G4_ARGS4);
+    else if constexpr (LOOP == 12) avk_g4_mainloop4b(AVK_G4_ARGS4);
+    else avk_g4_mainloop4c(AVK_G4_ARGS4);
+#undef AVK_G4_ARGS4
   } else
     avk_g4_mainloop3(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
                      __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
@@ -1632,11 +1637,22 @@ AVK_API int avk_vector_add_f32(const float* a, const float* b, float* c, int64_t
 //   hipBLASLt (torch.matmul) on the same operands                     1548    1672
 // A finer split of the ring (two 16-MFMA phases per slice, 4 barriers)
 // measured 1308 at 8192^3: not kept.
-// Round 4: the 4-wave kernel with the generated main loop (variants 15, 24,
-// 25; profiles/r4_gemm/) is the default for K a multiple of 256, the 8-phase
-// kernel the fallback for the other K (a multiple of 64).  The AQL gate
-// dispatches the same default (gemm_default.h).
-constexpr int kDefaultGemmVariant = 24;
+// Round 4: the 4-wave kernel with the generated main loop is the default for
+// K a multiple of 256, the 8-phase kernel the fallback for the other K (a
+// multiple of 64).  The AQL gate dispatches the same default (gemm_default.h).
+// Interleaved A/B in one process, uniform random operands, TF/s
+// (profiles/r4_gemm/kernel_bench_*.json; hipBLASLt varies by box):
+//                                                          4096^3  8192^3  hipBLASLt
+//   6 8-phase, 8 waves (round 1-3 default, fallback)        1222*   1367*
+//  15 schedule 1 (32-deep, 64-B rows)                       1246    1429    1476 / 1646
+//  24 schedule 2 (unrolled, constant addresses)             1273    1430    same box
+//  25 schedule 3 (slice-pair loads)                         1387    1544    1454 / 1593
+//  26 schedule 4 (64-deep stages, 128-B rows)               1416    1574    same box
+//  27 schedule 4b (barrier after even sub-slices only)      1417    1577    1440 / 1595
+//  28 schedule 4c (4b, B units' pieces early) (DEFAULT)     1418    1578    same box
+//  (* BENCH_r03 / round 1 figures)  MFMA utilisation at 8192^3: schedule 4 0.83,
+//  schedule 2 0.75, hipBLASLt 0.87 (profiles/r4_gemm/pmc_summary_*).
+constexpr int kDefaultGemmVariant = 28;
 constexpr int kFallbackGemmVariant = 6;
 static_assert(avk::kGemmThreads == g4::NTHR && avk::kGemmWavesPerTile * 64 == g4::NTHR &&
                   avk::kGemmTile == g4::BM && avk::kGemmTile == g4::BN && avk::kGemmKMultiple == 256,
@@ -1695,12 +1711,15 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
       if (out_f32) gemm_bf16_nt_4wa_kernel<true, L><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);  \
       else gemm_bf16_nt_4wa_kernel<false, L><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);         \
       break;
-    // 4 waves x 128x128 per 256x256 tile, 5-slot ring (K: a multiple of 256)
-    AVK_G4A(15, 0)  // schedule 1 of the generated main loop
-    AVK_G4A(24, 9)  // schedule 2: 10-slice unrolled body, constant addresses, one filler per MFMA gap
-    AVK_G4A(25, 10)  // schedule 3: schedule 2 with the loads in slice pairs (whole 128-B lines back to back)
-    AVK_G4A(26, 11)  // schedule 4: 64-deep stages in 128-B rows, 8-row x 128-B pieces
+    // 4 waves x 128x128 per 256x256 tile, 5-unit LDS ring (K: a multiple of 256)
+    AVK_G4A(28, 13)  // kDefaultGemmVariant: schedule 4c of the generated main loop
 #if AVK_GEMM_LAB
+    // the other generated schedules (gen_gemm4w_asm.py; profiles/r4_gemm/)
+    AVK_G4A(15, 0)   // 1: 32-deep slices in 64-B rows, rotating slot registers
+    AVK_G4A(24, 9)   // 2: 10-slice unrolled body, constant addresses, one filler per MFMA gap
+    AVK_G4A(25, 10)  // 3: 2 with the loads in slice pairs (whole 128-B lines back to back)
+    AVK_G4A(26, 11)  // 4: 64-deep stages in 128-B rows, 8-row x 128-B pieces
+    AVK_G4A(27, 12)  // 4b: 4 with a barrier after even sub-slices only
     case 14:  // the 4-wave kernel in builtins (hipcc moves accumulators through VGPRs, spills)
       if (K % 256) return hipErrorInvalidValue;
       if (out_f32) gemm_bf16_nt_4w_kernel<true><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);

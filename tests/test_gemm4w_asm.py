@@ -1,19 +1,22 @@
 """The 4-wave GEMM's generated main loop (native/validator/gen_gemm4w_asm.py
 -> gemm4w_asm.inc): the checked-in file is the generator's output, and the
-schedule keeps the invariants the kernel's correctness rests on (no GPU: the
-instruction text is checked; tests/test_kernels_gpu.py runs the kernel).
+schedules keep the invariants the kernel's correctness rests on (no GPU: the
+instruction text is checked; tests/test_kernels_gpu.py runs the kernels).
 
-Invariants of schedule 2 (the shipped loop, avk_g4_mainloop2):
-  * every slice issues 64 MFMAs, 16 fragment reads and 8 LDS-DMA pieces;
+Invariants of every schedule, per 64-MFMA slice (sub-slice in schedule 4):
+  * 64 MFMAs, 16 fragment reads, 8 LDS-DMA pieces (schedule 3: 16 on even
+    slices, none on odd ones);
   * an A fragment register is re-read >= 3 MFMAs after its last use, and B
     reads only go to the other parity's set;
   * each piece's M0 write has >= 1 instruction between it and its load, and
     the next M0 write comes only after that load (M0 is read at issue);
-  * consecutive pieces are >= 8 MFMAs apart (closer spacing was measured to
-    corrupt the LDS image, variants 22/23 of round 4);
-  * at most one filler (DS read, M0 write, load) per MFMA gap;
-  * the slice ends with vmcnt(24) lgkmcnt(0) then s_barrier (3 slices of
-    8 pieces in flight).
+  * consecutive pieces are >= 4 MFMAs apart (back-to-back pieces were
+    measured to corrupt the LDS image: round 4's ablation variants 22/23);
+  * at most one filler (DS read, M0 write, load) per MFMA gap, but for the
+    early B pieces of schedule 4c (a DS read and an M0 write may share);
+  * the slice ends with the counted vmcnt, lgkmcnt(0), the exit test and the
+    s_barrier (schedule 4b/4c: odd sub-slices end with lgkmcnt(0) only).
+Schedule 4c (avk_g4_mainloop4c) is the shipped one (variant 28).
 """
 
 import importlib.util
@@ -34,7 +37,7 @@ def _gen():
 
 def test_checked_in_inc_is_the_generator_output():
     g = _gen()
-    assert INC.read_text() == g.render() + g.render2() + g.render3() + g.render4(), \
+    assert INC.read_text() == g.render_all(), \
         "run: python3 native/validator/gen_gemm4w_asm.py > " + str(INC)
 
 
@@ -166,3 +169,59 @@ def test_schedule4_ring_and_counts():
         prev = loaded - 5  # the unit that slot held
         if prev >= 0:
             assert last_read.get(prev, -1) < u, (u, prev)
+
+
+def _subslices(lines):
+    """Schedule 4: split after each exit test (every sub-slice has one)."""
+    out, cur, started = [], [], False
+    for ln in lines:
+        if ln.startswith("v_mfma"):
+            started = True
+        if not started:
+            continue
+        cur.append(ln)
+        if ln == "s_cbranch_scc1 3f":
+            out.append(cur)
+            cur = []
+    return out
+
+
+@pytest.mark.parametrize("variant", [{}, {"odd_barrier": False}, {"odd_barrier": False, "early_b": True}])
+def test_schedule4_subslice_invariants(variant):
+    g = _gen()
+    g.S4_OPTS.update({"odd_barrier": True, "early_b": False}, **variant)
+    try:
+        subs = _subslices(g.program4())
+    finally:
+        g.S4_OPTS.update(odd_barrier=True, early_b=False)
+    assert len(subs) == 11
+    for n, sl in enumerate(subs):
+        pos = 0 if n == 0 else n - 1
+        even = pos % 2 == 0
+        body = [ln for ln in sl if not ln.endswith(":") and ln != "s_barrier"]
+        mfma = [i for i, ln in enumerate(body) if ln.startswith("v_mfma")]
+        loads = [i for i, ln in enumerate(body) if ln.startswith("global_load_lds_dwordx4")]
+        m0 = [i for i, ln in enumerate(body) if ln.startswith("s_add_u32 m0")]
+        assert len(mfma) == 64 and len(loads) == 8 == len(m0)
+        assert sum(ln.startswith("ds_read_b128") for ln in body) == 16
+        for w, ld in zip(m0, loads):
+            assert 1 < ld - w and not any(ln.startswith("s_add_u32 m0") for ln in body[w + 1:ld])
+        at = [sum(1 for i in mfma if i < ld) for ld in loads]
+        assert all(b - a >= 4 for a, b in zip(at, at[1:]))
+        limit = 2 if variant.get("early_b") and not even else 1
+        for a, b in zip(mfma, mfma[1:]):
+            fill = [ln for ln in body[a + 1:b] if ln.startswith(("ds_read", "global_load", "s_add_u32 m0"))]
+            assert len(fill) <= limit, body[a:b + 1]
+        assert sl[-1] == "s_cbranch_scc1 3f"
+        if even or variant.get("odd_barrier", True):
+            assert f"s_waitcnt vmcnt({8 if even else 16}) lgkmcnt(0)" in sl[-3:]
+        else:
+            assert "s_waitcnt lgkmcnt(0)" in sl[-3:] and not any("vmcnt" in ln for ln in sl[-3:])
+    # barriers: 2 in the prologue, then after every even sub-slice (the peeled one and 5 in the
+    # body) and, in schedule 4, after the 5 odd ones too
+    g.S4_OPTS.update({"odd_barrier": True, "early_b": False}, **variant)
+    try:
+        prog = g.program4()
+    finally:
+        g.S4_OPTS.update(odd_barrier=True, early_b=False)
+    assert sum(ln == "s_barrier" for ln in prog) == 2 + 6 + (5 if variant.get("odd_barrier", True) else 0)

@@ -1,9 +1,9 @@
 """The shipped validator kernels carry the GEMMs the validator runs: the
-default 4-wave kernel with the generated main loop (variant 24, what the
+default 4-wave kernel with the generated main loop (variant 28, what the
 native validator and its AQL counter gate dispatch when K % 256 == 0, named
-in native/include/gemm_default.h), its other generated schedules (15, 25,
-26) and the 8-phase fallback for the other K (6).  The A/B kernels of rounds
-1-4 live in the tools build (``make -C native lab``) only."""
+in native/include/gemm_default.h) and the 8-phase fallback for the other K
+(6).  The other generated schedules and the A/B kernels of rounds 1-3 live
+in the tools build (``make -C native lab``) only."""
 
 import pathlib
 import re
@@ -21,22 +21,20 @@ def _gemm_kernels(path):
 
 
 def test_shipped_code_object_has_only_the_default_gemm():
-    assert (K.GEMM_DEFAULT_VARIANT, K.GEMM_FALLBACK_VARIANT) == (24, 6)
-    # <OUT_F32 = false / true, LOOP = 0 / 9 / 10 / 11: variants 15 / 24 / 25 / 26> and
-    # <OUT_F32, LOAD_IN_M = false, BAL = false, GROUP_M = 4>: variant 6
-    loops = (0, 9, 10, 11)
-    assert _gemm_kernels(native.artefact("validator_kernels.co")) == sorted(
-        [f"gemm_bf16_nt_4wa_kernelILb{f}ELi{lp}E" for f in (0, 1) for lp in loops]
-        + ["gemm_bf16_nt_8p_kernelILb0ELb0ELb0ELi4E", "gemm_bf16_nt_8p_kernelILb1ELb0ELb0ELi4E"])
+    assert (K.GEMM_DEFAULT_VARIANT, K.GEMM_FALLBACK_VARIANT) == (28, 6)
+    # <OUT_F32 = false / true, LOOP = 13>: variant 28; <OUT_F32, LOAD_IN_M = false, BAL = false, GROUP_M = 4>: 6
+    assert _gemm_kernels(native.artefact("validator_kernels.co")) == [
+        "gemm_bf16_nt_4wa_kernelILb0ELi13E", "gemm_bf16_nt_4wa_kernelILb1ELi13E",
+        "gemm_bf16_nt_8p_kernelILb0ELb0ELb0ELi4E", "gemm_bf16_nt_8p_kernelILb1ELb0ELb0ELi4E"]
 
 
 def test_the_gate_dispatches_the_default_kernel():
     """gemm_default.h's symbol (the AQL gate's prefix match) names exactly one
-    kernel of the code object: variant 24's bf16-out instance."""
+    kernel of the code object: variant 28's bf16-out instance."""
     hdr = (pathlib.Path(__file__).resolve().parents[1] / "native" / "include" / "gemm_default.h").read_text()
     sym = re.search(r'kGemmSymbol = "(\w+)"', hdr).group(1)
     assert [n for n in _gemm_kernels(native.artefact("validator_kernels.co")) if sym.startswith(n)] == \
-        ["gemm_bf16_nt_4wa_kernelILb0ELi9E"]
+        ["gemm_bf16_nt_4wa_kernelILb0ELi13E"]
     assert int(re.search(r"kGemmThreads = (\d+);", hdr).group(1)) == 64 * int(
         re.search(r"kGemmWavesPerTile = (\d+);", hdr).group(1)) == 256
 
