@@ -146,11 +146,11 @@ def vector_add_verify(a, b, c, stream=None) -> int:
     return int(bad.item())
 
 
-GEMM_DEFAULT_VARIANT = 28   # 4 waves x 128x128, generated main loop, schedule 4c (K a multiple of 256)
+GEMM_DEFAULT_VARIANT = 29   # 4 waves x 128x128, generated main loop (schedule 4c), 16-B bf16 stores (K % 256 == 0)
 GEMM_FALLBACK_VARIANT = 6   # 8-phase, 8 waves (K a multiple of 64)
 GEMM_DEFAULT_K_MULTIPLE = 256
 # variants in the shipped library; the rest need `make -C native lab`
-SHIPPED_GEMM_VARIANTS = (6, 28)
+SHIPPED_GEMM_VARIANTS = (6, 29)
 
 
 def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int | None = None):
@@ -161,8 +161,8 @@ def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int | No
     what the native validator runs: the 4-wave kernel (GEMM_DEFAULT_VARIANT)
     when K is a multiple of 256, else the 8-phase kernel
     (GEMM_FALLBACK_VARIANT).  The other generated schedules of the 4-wave
-    kernel (15, 24-27) and the A/B kernels of rounds 1-3 are served from the
-    tools build (``make -C native lab``).
+    kernel (15, 24-28, 30) and the A/B kernels of rounds 1-3 are served from
+    the tools build (``make -C native lab``).
     """
     import torch
 

@@ -421,6 +421,9 @@ def main():
             for i in range(n_steps):
                 pods = out is results and i == n_steps - 1 and not args.no_pod_workload
                 out.append(one_bring_up(args, n_gpus, launcher, workdir, fake_gpu, mode, pods))
+                # progress on stderr (a run that prints nothing for minutes looks hung to its caller)
+                print(f"bench: {'timed' if out is results else 'warm-up'} bring-up {i + 1}/{n_steps} done",
+                      file=sys.stderr, flush=True)
         except Exception as e:  # noqa: BLE001
             import traceback
 

@@ -9,10 +9,11 @@
 
 namespace avk {
 
-// gemm_bf16_nt_4wa_kernel<OUT_F32=false, LOOP=13> (variant 28): 256x256
-// tile, 4 waves of 128x128, the generated main loop of schedule 4c
-// (validator/gen_gemm4w_asm.py: 64-deep stages in 128-B LDS rows)
-constexpr const char* kGemmSymbol = "gemm_bf16_nt_4wa_kernelILb0ELi13EE";
+// gemm_bf16_nt_4wa_kernel<OUT_F32=false, LOOP=13, EPI=1> (variant 29):
+// 256x256 tile, 4 waves of 128x128, the generated main loop of schedule 4c
+// (validator/gen_gemm4w_asm.py: 64-deep stages in 128-B LDS rows), bf16
+// epilogue in 16-B stores
+constexpr const char* kGemmSymbol = "gemm_bf16_nt_4wa_kernelILb0ELi13ELi1EE";
 constexpr int kGemmThreads = 256;      // workgroup size
 constexpr int kGemmWavesPerTile = 4;   // kGemmThreads / 64
 constexpr int kGemmTile = 256;         // M and N multiple

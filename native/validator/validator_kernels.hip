@@ -1262,7 +1262,37 @@ __device__ __forceinline__ void g4_store_all(void* __restrict__ Cv, int N, int c
   (g4_store_tile<OUT_F32, T>(Cv, N, crow, ccol), ...);
 }
 
-template <bool OUT_F32, int LOOP = 0>
+// bf16 epilogue in 16-B stores: tiles (i, 2p) = X and (i, 2p + 1) = Y packed
+// to bf16 pairs, then v_permlane16_swap trades X's odd 16-lane rows for Y's
+// even ones, so lane-row q holds 8 consecutive columns of one output row:
+// q 0 / 2 -> X columns 0-7 / 8-15, q 1 / 3 -> Y columns 0-7 / 8-15; a store
+// instruction covers 16 rows x 64 B (the 8-B form: 16 rows x 32 B, twice the
+// instructions).
+template <int P, bool NT = false>
+__device__ __forceinline__ void g4_store_pair_bf16(__bf16* __restrict__ C, int N, int crow, int ccol16, int q) {
+  constexpr int i = P >> 2, jx = 2 * (P & 3);
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const f32x4 x = g4_acc<8 * i + jx>(), y = g4_acc<8 * i + jx + 1>();
+  const unsigned x0 = __builtin_bit_cast(unsigned, (bf16x2){(__bf16)x[0], (__bf16)x[1]});
+  const unsigned x1 = __builtin_bit_cast(unsigned, (bf16x2){(__bf16)x[2], (__bf16)x[3]});
+  const unsigned y0 = __builtin_bit_cast(unsigned, (bf16x2){(__bf16)y[0], (__bf16)y[1]});
+  const unsigned y1 = __builtin_bit_cast(unsigned, (bf16x2){(__bf16)y[2], (__bf16)y[3]});
+  const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
+  const size_t idx = (size_t)(crow + i * 16) * N + ccol16 + 16 * (jx + (q & 1)) + 8 * (q >> 1);
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(C + idx));
+  else *reinterpret_cast<u32x4*>(C + idx) = v;
+}
+
+template <bool NT, int... P>
+__device__ __forceinline__ void g4_store_pairs_bf16(__bf16* __restrict__ C, int N, int crow, int ccol16, int q,
+                                                    std::integer_sequence<int, P...>) {
+  (g4_store_pair_bf16<P, NT>(C, N, crow, ccol16, q), ...);
+}
+
+template <bool OUT_F32, int LOOP = 0, int EPI = 0>
 __global__ __launch_bounds__(g4::NTHR, 1) void gemm_bf16_nt_4wa_kernel(const __bf16* __restrict__ A,
                                                                       const __bf16* __restrict__ Bt,
                                                                       void* __restrict__ Cv, int M, int N, int K) {
@@ -1341,8 +1371,12 @@ __global__ __launch_bounds__(g4::NTHR, 1) void gemm_bf16_nt_4wa_kernel(const __b
 #undef AVK_G4_ARGS
 
   // D = Bfrag x Afrag: lane holds row (lane & 15), columns 4*(lane >> 4) + 0..3
-  g4_store_all<OUT_F32>(Cv, N, m0 + wm * 128 + fr, n0 + wn * 128 + (lane >> 4) * 4,
-                        std::make_integer_sequence<int, 64>{});
+  if constexpr (!OUT_F32 && EPI >= 1)
+    g4_store_pairs_bf16<EPI == 2>(reinterpret_cast<__bf16*>(Cv), N, m0 + wm * 128 + fr, n0 + wn * 128, lane >> 4,
+                                  std::make_integer_sequence<int, 32>{});
+  else
+    g4_store_all<OUT_F32>(Cv, N, m0 + wm * 128 + fr, n0 + wn * 128 + (lane >> 4) * 4,
+                          std::make_integer_sequence<int, 64>{});
 }
 
 // ------------------------------------------------- Freivalds check GEMVs ----
@@ -1649,10 +1683,12 @@ AVK_API int avk_vector_add_f32(const float* a, const float* b, float* c, int64_t
 //  25 schedule 3 (slice-pair loads)                         1387    1544    1454 / 1593
 //  26 schedule 4 (64-deep stages, 128-B rows)               1416    1574    same box
 //  27 schedule 4b (barrier after even sub-slices only)      1417    1577    1440 / 1595
-//  28 schedule 4c (4b, B units' pieces early) (DEFAULT)     1418    1578    same box
-//  (* BENCH_r03 / round 1 figures)  MFMA utilisation at 8192^3: schedule 4 0.83,
+//  28 schedule 4c (4b, B units' pieces early)               1418    1578    same box
+//  29 4c + bf16 epilogue in 16-B stores (DEFAULT)            1521    1654    1522 / 1654
+//  30 29 with non-temporal stores                            1516    1656    same box
+//  (* BENCH_r03 / round 1 figures)  MFMA utilisation at 8192^3: schedule 4c 0.84,
 //  schedule 2 0.75, hipBLASLt 0.87 (profiles/r4_gemm/pmc_summary_*).
-constexpr int kDefaultGemmVariant = 28;
+constexpr int kDefaultGemmVariant = 29;
 constexpr int kFallbackGemmVariant = 6;
 static_assert(avk::kGemmThreads == g4::NTHR && avk::kGemmWavesPerTile * 64 == g4::NTHR &&
                   avk::kGemmTile == g4::BM && avk::kGemmTile == g4::BN && avk::kGemmKMultiple == 256,
@@ -1712,8 +1748,18 @@ AVK_API int avk_gemm_bf16_nt_variant(const void* A, const void* Bt, void* C, int
       else gemm_bf16_nt_4wa_kernel<false, L><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);         \
       break;
     // 4 waves x 128x128 per 256x256 tile, 5-unit LDS ring (K: a multiple of 256)
-    AVK_G4A(28, 13)  // kDefaultGemmVariant: schedule 4c of the generated main loop
+    case 29:  // kDefaultGemmVariant: schedule 4c, the bf16 epilogue in 16-B stores (permlane16_swap pairs)
+      if (K % 256) return hipErrorInvalidValue;
+      if (out_f32) gemm_bf16_nt_4wa_kernel<true, 13><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+      else gemm_bf16_nt_4wa_kernel<false, 13, 1><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+      break;
 #if AVK_GEMM_LAB
+    AVK_G4A(28, 13)  // 4c with the 8-B bf16 epilogue
+    case 30:  // 29 with non-temporal stores (no difference: profiles/r4_gemm/kernel_bench_epilogue16_nt_vs_28.json)
+      if (K % 256) return hipErrorInvalidValue;
+      if (out_f32) gemm_bf16_nt_4wa_kernel<true, 13><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+      else gemm_bf16_nt_4wa_kernel<false, 13, 2><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+      break;
     // the other generated schedules (gen_gemm4w_asm.py; profiles/r4_gemm/)
     AVK_G4A(15, 0)   // 1: 32-deep slices in 64-B rows, rotating slot registers
     AVK_G4A(24, 9)   // 2: 10-slice unrolled body, constant addresses, one filler per MFMA gap

@@ -91,7 +91,8 @@ def test_failed_peer_and_orchestrator_abort(tmp_path):
     d.mkdir()
     p = _rank(d, 0, extra=["--peer-timeout", "60"])
     time.sleep(0.3)
-    (d / "abort").write_text("t rank 1 failed (rc 1)")
+    (d / "abort.tmp").write_text("t rank 1 failed (rc 1)")
+    os.replace(d / "abort.tmp", d / "abort")  # as validate.py writes it: never seen half-written
     rc, rep = _report(p, timeout=5)
     assert rc == 1 and rep["peer_state"] == "aborted" and "rank 1 failed" in rep["error"]
 

@@ -36,7 +36,7 @@ GEMM_VARIANTS = {6: "default_8phase", 0: "ring_pingpong", 1: "dbuf", 2: "ring", 
                  13: "8phase_lab_copy", 14: "4wave_builtin", 15: "4wave_asm",
                  16: "4wave_asm_no_glds", 17: "4wave_asm_no_barrier", 18: "4wave_asm_early_rotate",
                  19: "4wave_asm_no_dsread", 20: "4wave_asm_fixed_m0", 21: "4wave_asm_vgpr_loads",
-                 22: "4wave_asm_piece_pairs", 23: "4wave_asm_piece_burst", 24: "4wave_asm_sched2", 25: "4wave_asm_sched3", 26: "4wave_asm_sched4", 27: "4wave_asm_sched4b", 28: "4wave_asm_sched4c"}
+                 22: "4wave_asm_piece_pairs", 23: "4wave_asm_piece_burst", 24: "4wave_asm_sched2", 25: "4wave_asm_sched3", 26: "4wave_asm_sched4", 27: "4wave_asm_sched4b", 28: "4wave_asm_sched4c", 29: "4wave_asm_sched4c_epi16", 30: "4wave_asm_sched4c_epi16_nt"}
 
 
 def bench_gemm(n, rounds, iters, variants=None):
