@@ -19,7 +19,7 @@ extern "C" {
 // Counter names in the order of avk_aql_gate_result::values.
 const char* avk_aql_gate_counter_name(int i);
 
-// Dispatch gemm_bf16_nt_8p_kernel<false,false,false> (C = A * Bt^T, bf16 out)
+// Dispatch the default GEMM (gemm_default.h: C = A * Bt^T, bf16 out)
 // from the code object at `code_object` on the GPU at `pci_bus_id`
 // ("dddd:bb:dd.f", hipDeviceGetPCIBusId; `agent_ordinal` picks among the GPU
 // agents at that address - the compute partitions of one GPU share it, and HIP
