@@ -33,7 +33,10 @@ The interface keeps the pieces of grpcio's the operator used: handlers take
 wait_for_ready=)`` and :class:`RpcError` with ``code()`` / ``details()``.
 tests/test_rpc.py runs it against grpcio in both directions (grpcio client
 -> this server, this client -> grpcio server), which is the peer a kubelet's
-grpc-go stands in for.
+grpc-go stands in for; tests/test_rpc_grpcgo.py adds a frame-level stand-in
+for grpc-go's own wire habits (HPACK incremental indexing and eviction, BDP
+and graceful-stop pings, two-phase GOAWAY, Trailers-Only errors, multiplexed
+calls) in both directions, the kubelet side driving the production plugin.
 """
 
 from __future__ import annotations
