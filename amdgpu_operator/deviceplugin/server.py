@@ -338,7 +338,7 @@ class DevicePluginServer:
             if ident is None:
                 self._kubelet_ino = None  # socket gone: re-register when it returns
                 continue
-            if ident != self._kubelet_ino:
+            if ident != self._kubelet_ino and not self._stop.is_set():
                 try:
                     self.register()
                 except wire.RpcError as e:  # kubelet not ready yet: retry next tick
@@ -355,6 +355,9 @@ class DevicePluginServer:
         self._stop.set()
         with self._cv:
             self._cv.notify_all()
+        th = self._watch_thread
+        if th is not None and th is not threading.current_thread():
+            th.join(timeout=6.0)  # a re-registration in flight ends within its 5 s deadline
         if self._server is not None:
             self._server.stop(grace=0.5).wait()
             self._server = None
