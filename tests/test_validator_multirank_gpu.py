@@ -239,6 +239,17 @@ def test_xgmi_link_rate_matches_the_kfd_nominal_on_mi355x():
         ms = smi.collect()
     vals = ms[0].values
     nominal = [lk.max_bandwidth_mbps / 1000 for lk in topology.links("/") if lk.is_xgmi and lk.max_bandwidth_mbps]
+    if not nominal:  # a one-GPU slice of a hive: the peers' KFD nodes are listed, not enumerated as GPUs
+        import glob
+
+        for p in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/io_links/*/properties"):
+            try:
+                with open(p) as f:
+                    kv = dict(ln.split() for ln in f if len(ln.split()) == 2)
+            except OSError:  # other GPUs' nodes may be unreadable here
+                continue
+            if kv.get("type") == "11" and int(kv.get("max_bandwidth", 0)):  # CRAT_IOLINK_TYPE_XGMI
+                nominal.append(int(kv["max_bandwidth"]) / 1000)
     print(json.dumps({"speed": vals.get("xgmi_link_speed_gbps"), "width": vals.get("xgmi_link_width"),
                       "up": vals.get("xgmi_links_up"), "nominal": sorted(set(nominal))}))
     if not vals.get("xgmi_link_speed_gbps") or not vals.get("xgmi_link_width") or not nominal:
