@@ -63,6 +63,20 @@ class UpgradePolicy(_M):
     podDeletionForce: bool = False
 
 
+class RdmaSpec(_M):
+    """GPU memory for RDMA NICs (upstream ``driver.rdma``; off, as the
+    reference leaves it: README.md:101-110).  On MI355X: amdgpu's dma-buf
+    export imported by the RDMA core - no peer-memory module (discovery/rdma.py)."""
+
+    enabled: bool = False
+    # the host's MOFED / inbox RDMA stack loads the RDMA core; the driver
+    # container waits for it instead of loading ib_uverbs itself
+    useHostMofed: bool = False
+    # the device plugin also sets NCCL_IB_HCA to the allocation's nearest NICs
+    # (always: the amd.com/gpu.rdma-nics annotation)
+    hcaEnv: bool = False
+
+
 class DriverSpec(Operand):
     """amdgpu DKMS + ROCm userspace for gfx950 (README.md:104,212)."""
 
@@ -81,6 +95,7 @@ class DriverSpec(Operand):
     # per-node-pool drivers: one driver DaemonSet per AMDGPUDriver object
     # (api/driver_cr.py) instead of the single ClusterPolicy-wide one
     useDriverCRD: bool = False
+    rdma: RdmaSpec = Field(default_factory=RdmaSpec)
 
 
 class CDISpec(_M):

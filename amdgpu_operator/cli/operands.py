@@ -67,6 +67,8 @@ def build_parser() -> argparse.ArgumentParser:
     dp.add_argument("--device-list-strategy", default="envvar",
                     help="comma list of envvar, volume-mounts, cdi-annotations, cdi-cri")
     dp.add_argument("--no-device-specs", action="store_true", help="no DeviceSpecs in Allocate (CDI / hook inject)")
+    dp.add_argument("--rdma", action="store_true", help="driver.rdma: report each allocation's nearest RDMA NICs")
+    dp.add_argument("--rdma-hca-env", action="store_true", help="and set NCCL_IB_HCA to them")
     dp.add_argument("--config-file", default=None, help="device-plugin config file (flags + sharing)")
     dp.add_argument("--config-map", default=None, help="NAMESPACE/NAME of a ConfigMap of config files")
     dp.add_argument("--config-default", default="", help="ConfigMap key used when the node has no config label")
@@ -388,7 +390,8 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             key, dcfg = "", cli_config
         cfg = PluginConfig(resource_name=a.resource_name, socket_dir=env.device_plugin_dir, sysfs_root=env.sysfs_root(),
                            cdi_enabled=a.cdi, partition_strategy=a.partition_strategy, health_poll_ms=a.health_poll_ms,
-                           watch_interval_s=max(0.05, min(0.5, env.poll_s * 10)), device_config=dcfg)
+                           watch_interval_s=max(0.05, min(0.5, env.poll_s * 10)), device_config=dcfg,
+                           rdma=a.rdma, rdma_hca_env=a.rdma_hca_env)
         health = None
         if not a.no_health and not env.extra.get("no_health"):
             def health():  # amd-smi start-up on the health thread, overlapping registration

@@ -235,7 +235,9 @@ def state_driver(spec: ClusterPolicySpec, ns: str, owner, name: str = "amd-drive
            {"name": "AMDGPU_BLACKLIST_INBOX", "value": str(d.blacklistAmdgpuInbox).lower()},
            {"name": "AMDGPU_MODULE_PARAMS", "value": " ".join(f"{k}={v}" for k, v in sorted(d.kernelModuleParams.items()))},
            {"name": "AMDGPU_WAIT_SECONDS", "value": str(d.startupProbeTimeoutSeconds)},
-           {"name": "AMDGPU_UNLOAD_ON_EXIT", "value": str(d.unloadOnExit).lower()}
+           {"name": "AMDGPU_UNLOAD_ON_EXIT", "value": str(d.unloadOnExit).lower()},
+           {"name": "AMDGPU_RDMA_ENABLED", "value": str(d.rdma.enabled).lower()},
+           {"name": "AMDGPU_RDMA_USE_HOST_MOFED", "value": str(d.rdma.useHostMofed).lower()}
            ] + ([{"name": "AMDGPU_REPO_BASE", "value": d.packageRepository}] if d.packageRepository else []) + list(d.env)
     mounts = [_mount("run-amd", "/run/amd", propagation="Bidirectional"), _mount("host-root", "/host", ro=True,
                                                                                  propagation="HostToContainer"),
@@ -341,6 +343,8 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         wl_args += ["--rccl-single-gpu"]
     if w.rcclProcess == "separate":
         wl_args += ["--rccl-separate-process"]
+    if spec.driver.rdma.enabled:  # HBM exported as a dma-buf, what the RDMA NICs import
+        wl_args += ["--dmabuf"]
     inits = [_wait_init("driver-validation", image, v.imagePullPolicy, "driver")]
     # the plugin pods request what the device plugin advertises (its resource
     # name, and amd.com/gpu-<mode> for partitioned GPUs under "mixed")
@@ -395,6 +399,8 @@ def state_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         args.append("--cdi")
     if not p.passDeviceSpecs:
         args.append("--no-device-specs")
+    if spec.driver.rdma.enabled:  # nearest RDMA NICs of each allocation (discovery/rdma.py)
+        args += ["--rdma"] + (["--rdma-hca-env"] if spec.driver.rdma.hcaEnv else [])
     rbac = []
     if p.config.name:  # config-manager loop: reads the ConfigMap and this node's config label
         args += ["--config-map", f"{ns}/{p.config.name}", "--config-default", p.config.default]

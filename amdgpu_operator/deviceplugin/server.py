@@ -59,6 +59,8 @@ class PluginConfig:
     rocm_mount: str | None = None
     extra_env: dict = field(default_factory=dict)
     device_config: DevicePluginConfig | None = None  # config file: flags + sharing
+    rdma: bool = False  # driver.rdma: annotate allocations with their nearest RDMA NICs
+    rdma_hca_env: bool = False  # ... and set NCCL_IB_HCA to them
 
     @property
     def config(self) -> DevicePluginConfig:
@@ -137,6 +139,7 @@ class DevicePluginServer:
         self._stop = threading.Event()
         self._server: wire.Server | None = None
         self._watch_thread: threading.Thread | None = None
+        self._nics = None  # RDMA NICs (cfg.rdma), enumerated at the first allocation
         self._kubelet_ino = None
         self.registrations = 0
         self.allocations = 0
@@ -254,12 +257,35 @@ class DevicePluginServer:
         hives = sorted({str(d.hive_id) for d in devs if d.hive_id})
         if hives:
             r.annotations["amd.com/gpu.xgmi-hive"] = ",".join(hives)
+        if self.cfg.rdma:
+            nics = self._rdma_nics(devs)
+            if nics:
+                r.annotations["amd.com/gpu.rdma-nics"] = ",".join(nics)
+                if self.cfg.rdma_hca_env:
+                    r.envs["NCCL_IB_HCA"] = ",".join(nics)
         if self.cfg.rocm_mount:
             r.mounts.add(container_path=self.cfg.rocm_mount, host_path=self.cfg.rocm_mount, read_only=True)
         if "cdi-cri" in strategies:
             for d in devs:
                 r.cdi_devices.add(name=f"{self.cfg.cdi_kind}={d.index}")
         return r
+
+    def _rdma_nics(self, devs) -> list[str]:
+        """The allocation's nearest RDMA NICs (PCIe switch first), read once:
+        NICs do not come and go under a running plugin."""
+        if self._nics is None:
+            from ..discovery import rdma
+
+            try:
+                self._nics = rdma.enumerate_nics(self.cfg.sysfs_root)
+            except OSError as e:
+                log.warning("RDMA NICs not readable: %s", e)
+                self._nics = []
+        if not self._nics:
+            return []
+        from ..discovery import rdma
+
+        return rdma.allocation_nics(devs, self._nics, self.cfg.sysfs_root)
 
     def Allocate(self, request, context):
         out = api.pb["AllocateResponse"]()

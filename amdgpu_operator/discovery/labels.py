@@ -12,7 +12,9 @@ here both are implemented natively over the same sysfs view:
 * GFD: the MI355X capability set - product, CDNA4 family, gfx950 arch, device
   count, HBM per device, CUs/XCCs/LDS, MFMA data types (bf16, fp16, OCP fp8,
   fp6, fp4, f32, f64; no xf32 on gfx950), xGMI hive and link count, compute /
-  memory partition mode, driver and ROCm versions.
+  memory partition mode, driver and ROCm versions; with RDMA NICs on the
+  node, their count, link layer, rate and PCIe affinity to the GPUs
+  (discovery/rdma.py).
 """
 
 from __future__ import annotations
@@ -170,6 +172,9 @@ def gfd_labels(gpus: list[GpuDevice], root: str = "/", prefix: str = "amd.com") 
     rocm = rocm_version(root)
     if rocm:
         labels[f"{p}.rocm-version"] = label_value(rocm)
+    from .rdma import rdma_labels  # RDMA NICs beside the GPUs (none: no labels)
+
+    labels.update(rdma_labels(gpus, root, prefix))
     return labels
 
 

@@ -65,6 +65,11 @@ class HostModule:
         """Load the module the host provides (no installer in this image)."""
         subprocess.run(["modprobe", "amdgpu"], check=True, timeout=timeout, capture_output=True)
 
+    def load_rdma(self, env: NodeEnv, timeout: float = 120.0) -> None:
+        """The RDMA core for GPU peer memory (driver.rdma): ``ib_uverbs``
+        brings ``ib_core``; the NIC's own driver comes with the host stack."""
+        subprocess.run(["modprobe", "ib_uverbs"], check=True, timeout=timeout, capture_output=True)
+
     def unload(self, env: NodeEnv, timeout: float = 120.0, retry_s: float = 5.0) -> None:
         # a process that just exited may still be releasing its device files
         deadline = time.monotonic() + retry_s
@@ -184,6 +189,9 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
     cur = loaded_version(env)
     if ran_script and want and cur != want:
         raise RuntimeError(f"installed driver reports version {cur or 'none'}, requested {want}")
+    rdma = None
+    if cenv.get("AMDGPU_RDMA_ENABLED") == "true":
+        rdma = ensure_rdma(env, kmod, cenv.get("AMDGPU_RDMA_USE_HOST_MOFED") == "true", deadline, stop)
     # a restarted driver pod finds the module its predecessor installed: it stays ours
     prev = read_state(env)
     installed = ran_script or bool(prev.get("installed") and prev.get("version") == cur and live)
@@ -196,6 +204,8 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
     gpus = topology.enumerate_gpus(env.sysfs_root())
     out = {"ok": True, "message": msg, "gpus": len(gpus), "driver_version": cur, "installed": ran_script,
            "host_managed": host_managed, "seconds": time.perf_counter() - t0}
+    if rdma is not None:
+        out["rdma"] = rdma
     write_ready(env, "driver", out)  # the node's operands wait on this file, not on the annotation below
     try:  # for the upgrade controller (the loaded version / spec it compares with the policy)
         env.client.patch("v1", "Node", env.node_name, {"metadata": {"annotations": {
@@ -211,6 +221,39 @@ def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None =
         out["restarted"] = _restart_node_operands(env)
         log.info("driver back after a loss/unload; restarted %s", out["restarted"])
     return out
+
+
+def ensure_rdma(env: NodeEnv, kmod, host_stack: bool, deadline: float, stop: threading.Event | None = None) -> dict:
+    """driver.rdma: GPU memory reachable by the node's RDMA NICs before the
+    driver is declared ready (upstream: nvidia-peermem after MOFED).  On
+    MI355X the path is amdgpu's dma-buf export imported by the RDMA core, so
+    this needs the core loaded - by the host's MOFED / inbox stack
+    (``useHostMofed``: waited for) or here (``modprobe ib_uverbs``) - and a
+    kernel whose RDMA core imports dma-bufs.  NICs without an ACTIVE port are
+    reported, not waited for: a cable is not the driver's business.  The
+    validator's ``dmabuf`` step then exports HBM on the device itself."""
+    from ..discovery import rdma
+
+    st = rdma.readiness(env.sysfs_root())
+    if not st["dmabuf"]:
+        raise RuntimeError(f"driver.rdma: kernel {st['kernel']} cannot hand GPU memory to an RDMA NIC (needs >= 5.12)")
+    loaded = False
+    for delay in env.waits():
+        st = rdma.readiness(env.sysfs_root())
+        if all(st["modules"].values()):
+            break
+        if not host_stack and not loaded:
+            kmod.load_rdma(env)
+            loaded = True
+            continue
+        if time.monotonic() >= deadline:
+            raise RuntimeError("driver.rdma: RDMA core not loaded: " + "; ".join(st["problems"]))
+        if (stop.wait(delay) if stop is not None else (time.sleep(delay) or False)):
+            raise RuntimeError("stopped")
+    st["loaded_here"] = loaded
+    if st["problems"]:
+        log.warning("driver.rdma: %s", "; ".join(st["problems"]))
+    return st
 
 
 def _claim_lost_marker(env: NodeEnv) -> bool:

@@ -201,7 +201,7 @@ def _main(argv: list[str]) -> int:
                               "error": f"{expect} GPU(s) allocated to the pod, {seen} visible"}))
             return 1
     ndev = max(1, int(arg("--expect-devices", "1")))
-    per_device = ("vecadd", "gemm", "mfma", "hbm")
+    per_device = ("vecadd", "gemm", "mfma", "hbm", "dmabuf")
     recs = []
     for s in steps:
         for d in (range(ndev) if s in per_device and ndev > 1 else [None]):

@@ -58,11 +58,14 @@ class FakeGpu:
 
 def build_node(root: str, gpus: int = 8, compute_partition: str = "SPX", memory_partition: str = "NPS1",
                driver_loaded: bool = True, xgmi: bool = True, sockets: int = 2, hidden_peers: int = 0,
-               kernel: str = "6.8.0-45-generic") -> list[FakeGpu]:
+               kernel: str = "6.8.0-45-generic", pcie_tree: bool = False) -> list[FakeGpu]:
     """Write a fake node with ``gpus`` physical MI355X. Returns the GPU nodes.
 
     ``hidden_peers`` adds that many GPU nodes whose properties are unreadable
-    (what a container sees of the other GPUs of the host).
+    (what a container sees of the other GPUs of the host).  ``pcie_tree``
+    places each GPU behind its own PCIe switch (``sys/devices/pci…`` with
+    ``sys/bus/pci/devices/<bdf>`` a symlink into it, as on a real host), the
+    layout RDMA-NIC affinity reads (:func:`add_rdma_nics`).
     """
     split = PARTITION_SPLIT[compute_partition]
     os.makedirs(root, exist_ok=True)
@@ -169,7 +172,70 @@ def build_node(root: str, gpus: int = 8, compute_partition: str = "SPX", memory_
     _w(f"{root}/sys/bus/pci/devices/0000:00:01.0/vendor", "0x1022\n")
     _w(f"{root}/sys/bus/pci/devices/0000:00:01.0/class", "0x060000\n")
     _w(f"{root}/sys/bus/pci/devices/0000:00:01.0/device", "0x14a4\n")
+    if pcie_tree:
+        for bdf, numa in dict.fromkeys((g.bdf, g.numa) for g in out):
+            _into_tree(root, bdf, switch_path(bdf, numa) + (bdf,))
     return out
+
+
+def switch_path(gpu_bdf: str, numa: int) -> tuple[str, ...]:
+    """/sys/devices components of the fake PCIe switch above a GPU: host
+    bridge (one per socket), root port, switch upstream port, downstream port."""
+    bus = int(gpu_bdf.split(":")[1], 16)
+    hb = f"{0x00 if numa == 0 else 0x80:02x}"
+    return (f"pci0000:{hb}", f"0000:{hb}:{(bus >> 4) & 0x1f:02x}.1", f"0000:{bus - 2:02x}:00.0",
+            f"0000:{bus - 1:02x}:00.0")
+
+
+def _into_tree(root: str, bdf: str, parts: tuple[str, ...]) -> None:
+    """Move a flat ``sys/bus/pci/devices/<bdf>`` directory to
+    ``sys/devices/<parts>`` and leave the bus entry as a symlink to it; the
+    function's own relative symlinks (driver, iommu_group) become absolute so
+    they still resolve from the new depth."""
+    src = os.path.join(root, "sys/bus/pci/devices", bdf)
+    dst = os.path.join(root, "sys/devices", *parts)
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
+    if os.path.isdir(src) and not os.path.islink(src):
+        for name in os.listdir(src):
+            p = os.path.join(src, name)
+            if os.path.islink(p) and not os.path.isabs(os.readlink(p)):
+                target = os.path.normpath(os.path.join(src, os.readlink(p)))
+                os.unlink(p)
+                os.symlink(target, p)
+        shutil.move(src, dst)
+    else:
+        os.makedirs(dst, exist_ok=True)
+    _link(os.path.relpath(dst, os.path.dirname(src)), src)
+
+
+def add_rdma_nics(root: str, gpus: list[FakeGpu], link_layer: str = "Ethernet", rate_gbps: int = 400,
+                  active: bool = True, modules: bool = True, name: str = "ionic_{}") -> list[str]:
+    """One RDMA NIC per physical GPU, on the GPU's PCIe switch (build the
+    node with ``pcie_tree=True``): ``sys/class/infiniband/<name>`` with one
+    port, ``/dev/infiniband/uverbs<n>``, and the RDMA core modules."""
+    names = []
+    for i, (bdf, numa) in enumerate(dict.fromkeys((g.bdf, g.numa) for g in gpus)):
+        bus = int(bdf.split(":")[1], 16)
+        nic_bdf = f"0000:{bus + 1:02x}:00.0"
+        parts = switch_path(bdf, numa)[:-1] + (f"0000:{bus - 1:02x}:01.0", nic_bdf)
+        dev = os.path.join(root, "sys/devices", *parts)
+        _w(f"{dev}/vendor", "0x1dd8\n")
+        _w(f"{dev}/device", "0x1002\n")
+        _w(f"{dev}/class", "0x020000\n")
+        _w(f"{dev}/numa_node", f"{numa}\n")
+        _link(os.path.relpath(dev, f"{root}/sys/bus/pci/devices"), f"{root}/sys/bus/pci/devices/{nic_bdf}")
+        nm = name.format(i)
+        ib = f"{root}/sys/class/infiniband/{nm}"
+        _link(os.path.relpath(dev, ib), f"{ib}/device")
+        _w(f"{ib}/ports/1/state", "4: ACTIVE\n" if active else "1: DOWN\n")
+        _w(f"{ib}/ports/1/link_layer", f"{link_layer}\n")
+        _w(f"{ib}/ports/1/rate", f"{rate_gbps} Gb/sec (4X NDR)\n")
+        _w(f"{root}/dev/infiniband/uverbs{i}", "")
+        names.append(nm)
+    if modules:
+        for m in ("ib_core", "ib_uverbs"):
+            _w(f"{root}/sys/module/{m}/initstate", "live\n")
+    return names
 
 
 REAL_FIXTURE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
@@ -222,6 +288,12 @@ class SimModule:
             except FileNotFoundError:
                 pass
         self.log.append("unload")
+
+    def load_rdma(self, env=None, timeout: float = 0.0) -> None:
+        """``modprobe ib_uverbs`` (pulls in ib_core) on the fake node."""
+        for m in ("ib_core", "ib_uverbs"):
+            _w(f"{self.root}/sys/module/{m}/initstate", "live\n")
+        self.log.append("load-rdma")
 
     def install(self, env, cenv: dict, timeout: float) -> None:
         if self._live():

@@ -379,7 +379,9 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     (the throughput floors of :func:`fabric_floors`, passed to the binary as
     ``--min-rccl-busbw-gbps`` / ``--min-xgmi-read-gbps``),
     ``--max-gpu-processes N`` (the budget), ``--require-xgmi-links`` and
-    ``--min-xgmi-link-fraction F`` (:func:`check_fabric` on multi-GPU nodes)."""
+    ``--min-xgmi-link-fraction F`` (:func:`check_fabric` on multi-GPU nodes),
+    ``--dmabuf`` (driver.rdma: every device exports HBM as a dma-buf and
+    imports it back, the step an RDMA NIC's access rests on)."""
     from ..discovery import topology
 
     t0 = time.perf_counter()
@@ -404,11 +406,12 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     rccl_single = "--rccl-single-gpu" in args  # validate.py's own flags, not the binary's
     separate = "--rccl-separate-process" in args
     require_links = "--require-xgmi-links" in args
+    dmabuf = "--dmabuf" in args  # driver.rdma: HBM exported as a dma-buf on every device
     rccl_frac = float(_arg_value(args, "--rccl-busbw-link-fraction") or 0.0)
     xgmi_frac = float(_arg_value(args, "--xgmi-read-link-fraction") or 0.0)
     link_frac = float(_arg_value(args, "--min-xgmi-link-fraction") or 0.9)
     args = _drop_flag(args, "--rccl-single-gpu", "--rccl-shared-process", "--rccl-separate-process",
-                      "--require-xgmi-links")
+                      "--require-xgmi-links", "--dmabuf")
     args = _drop_value(args, "--rccl-busbw-link-fraction", "--xgmi-read-link-fraction", "--min-xgmi-link-fraction",
                        "--max-gpu-processes")
     steps = _steps_of(args)
@@ -423,7 +426,7 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
             args += ["--min-rccl-busbw-gbps", f"{floors['min_rccl_busbw_gbps']:g}"]
         if xgmi_frac > 0:
             args += ["--min-xgmi-read-gbps", f"{floors['min_xgmi_peer_read_gbps']:g}"]
-    kernel_steps = [s for s in steps if s not in ("xgmi", "rccl")]
+    kernel_steps = [s for s in steps if s not in ("xgmi", "rccl")] + ["dmabuf"] * (dmabuf and "dmabuf" not in steps)
     xgmi = "xgmi" in steps  # real peers at N >= 2, emulated peers on one device otherwise
     nproc, separate = workload_processes(world, run_rccl, separate, budget)
     jobs = []  # (rank, binary flags, run id, env)
@@ -558,7 +561,7 @@ def failure_summary(reports: list[dict], fabric: dict | None = None, problems: l
     return "; ".join(parts) or "no report"
 
 
-ALL_STEPS = ("hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl")
+ALL_STEPS = ("hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl")  # + "dmabuf" with driver.rdma
 
 
 def _steps_of(args: list[str]) -> list[str]:

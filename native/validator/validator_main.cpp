@@ -864,6 +864,98 @@ Step step_hbm(const Args& a, hipStream_t st, int cus) {
   return s;
 }
 
+// driver.rdma: device memory exported as a dma-buf - the handle an RDMA NIC
+// imports (ib_umem_dmabuf) to DMA straight to and from HBM, and what RCCL's
+// network path asks for.  The buffer is exported, the fd checked to be a
+// dma-buf of the buffer's size with amdgpu as its exporter, then imported
+// back through the external-memory path (hsa_amd_interop_map_buffer, the
+// importer side of the same fd): a checksum read through the imported view
+// must match the original, and a fill written through it must show in the
+// original - the two views are one allocation.
+Step step_dmabuf(hipStream_t st) {
+  auto t0 = Clock::now();
+  Step s{"dmabuf"};
+  const size_t bytes = 64ull << 20;
+  void* p = nullptr;
+  unsigned long long* cs = nullptr;
+  HIP_OK(hipMalloc(&p, bytes));
+  HIP_OK(hipMalloc(&cs, 16));
+  AVK_OK(avk_fill_uniform_f32((float*)p, bytes / 4, 47, -1, 1, st));
+  HIP_OK(hipStreamSynchronize(st));
+  int fd = -1;
+  const hipError_t xe = hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)p, bytes, hipMemRangeHandleTypeDmaBufFd, 0);
+  std::string err, exporter, link;
+  long long buf_size = -1;
+  bool read_ok = false, write_ok = false;
+  if (xe != hipSuccess || fd < 0) {
+    err = std::string("export: ") + hipGetErrorString(xe);
+  } else {
+    char lk[256] = {0};
+    const std::string fdp = "/proc/self/fd/" + std::to_string(fd);
+    if (readlink(fdp.c_str(), lk, sizeof(lk) - 1) > 0) link = lk;
+    std::ifstream info("/proc/self/fdinfo/" + std::to_string(fd));
+    for (std::string ln; std::getline(info, ln);) {
+      if (ln.rfind("size:", 0) == 0) buf_size = atoll(ln.c_str() + 5);
+      if (ln.rfind("exp_name:", 0) == 0) {
+        exporter = ln.substr(9);
+        exporter.erase(0, exporter.find_first_not_of(" \t"));
+      }
+    }
+    hipExternalMemoryHandleDesc desc;
+    memset(&desc, 0, sizeof(desc));
+    desc.type = hipExternalMemoryHandleTypeOpaqueFd;
+    desc.handle.fd = dup(fd);  // the import takes ownership of its fd
+    desc.size = bytes;
+    hipExternalMemory_t ext = nullptr;
+    const hipError_t ie = hipImportExternalMemory(&ext, &desc);
+    if (ie != hipSuccess) {
+      if (desc.handle.fd >= 0) close(desc.handle.fd);
+      err = std::string("import: ") + hipGetErrorString(ie);
+    } else {
+      hipExternalMemoryBufferDesc bd;
+      memset(&bd, 0, sizeof(bd));
+      bd.size = bytes;
+      void* q = nullptr;
+      const hipError_t me = hipExternalMemoryGetMappedBuffer(&q, ext, &bd);
+      if (me != hipSuccess) {
+        err = std::string("map: ") + hipGetErrorString(me);
+      } else {
+        unsigned long long h[2] = {0, 1};
+        AVK_OK(avk_checksum(p, bytes, cs, st));
+        AVK_OK(avk_checksum(q, bytes, cs + 1, st));
+        HIP_OK(hipMemcpyAsync(h, cs, 16, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        read_ok = h[0] == h[1];
+        AVK_OK(avk_fill_const(q, bytes / 4, 0, 3.0f, st));  // written through the imported view
+        AVK_OK(avk_checksum(p, bytes, cs, st));
+        AVK_OK(avk_fill_const(q, bytes / 4, 0, 5.0f, st));
+        AVK_OK(avk_checksum(p, bytes, cs + 1, st));
+        HIP_OK(hipMemcpyAsync(h, cs, 16, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        write_ok = h[0] != h[1] && h[1] != 0;  // the original changed with each write
+        (void)hipFree(q);
+      }
+      (void)hipDestroyExternalMemory(ext);
+    }
+    close(fd);
+  }
+  (void)hipFree(p);
+  (void)hipFree(cs);
+  const bool is_dmabuf = link.find("dmabuf") != std::string::npos;
+  s.ok = err.empty() && is_dmabuf && buf_size >= (long long)bytes && read_ok && write_ok;
+  if (err.empty() && !s.ok)
+    err = !is_dmabuf ? "exported fd is not a dma-buf (" + link + ")"
+                     : buf_size < (long long)bytes ? "dma-buf smaller than the buffer"
+                                                   : "imported view does not alias the buffer";
+  for (char& c : err)
+    if (c == '"' || c == '\\') c = '\'';
+  s.seconds = secs(t0);
+  s.detail = fmt("\"bytes\": %lld, \"dmabuf_bytes\": %lld, \"exporter\": \"%s\", \"read_match\": %s, "
+                 "\"write_through\": %s, \"error\": \"%s\"", (long long)bytes, buf_size, exporter.c_str(),
+                 read_ok ? "true" : "false", write_ok ? "true" : "false", err.c_str());
+  return s;
+}
+
 // K5: every CDNA4 matrix-core data type the GFD labels advertise, one exact tile each
 Step step_mfma(hipStream_t st) {
   auto t0 = Clock::now();
@@ -1319,6 +1411,7 @@ std::vector<Step> device_steps(Args ad, bool gate_last, bool with_hip) {
   if (!gate_last) run("gemm", [&] { return step_gemm(ad, sd, cus); });
   run("mfma", [&] { return step_mfma(sd); });
   run("hbm", [&] { return step_hbm(ad, sd, cus); });
+  run("dmabuf", [&] { return step_dmabuf(sd); });
   if (gate_last) run("gemm", [&] { return step_gemm(ad, sd, cus); });
   if (sd) (void)hipStreamDestroy(sd);
   return out;
@@ -1578,6 +1671,7 @@ int main(int argc, char** argv) {
       if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
       if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
+      if (ok && has_step(a, "dmabuf")) ok = (steps.push_back(step_dmabuf(st)), steps.back().ok);
     } else if (ok) {
       // several devices (a GPU's partitions, a pod's GPUs): all at once
       if (a.all_devices) steps.back().detail = fmt("\"device\": %d, ", devs[0].first) + steps.back().detail;

@@ -255,3 +255,38 @@ def test_xgmi_link_rate_matches_the_kfd_nominal_on_mi355x():
     if not vals.get("xgmi_link_speed_gbps") or not vals.get("xgmi_link_width") or not nominal:
         pytest.skip("amd-smi reports no xGMI rate/width here")
     assert vals["xgmi_link_speed_gbps"] * vals["xgmi_link_width"] / 8 >= 0.9 * min(nominal)
+
+
+def test_dmabuf_export_of_hbm_round_trips():
+    """driver.rdma's device step: HBM exported as a dma-buf (what an RDMA NIC
+    imports), the fd an amdgpu dma-buf of the buffer's size, and the buffer
+    imported back aliasing the original both ways (validator_main.cpp
+    step_dmabuf)."""
+    p = subprocess.run([VALIDATOR, "--steps", "hip,dmabuf"], capture_output=True, text=True, timeout=90)
+    rep = json.loads(p.stdout.strip().splitlines()[-1])
+    s = {x["name"]: x for x in rep["steps"]}["dmabuf"]
+    print(json.dumps(s))
+    assert p.returncode == 0 and rep["ok"] and s["ok"], (s, p.stderr[-2000:])
+    assert s["exporter"] in ("amdgpu", "drm") and s["dmabuf_bytes"] >= s["bytes"] == 64 << 20  # drm: PRIME
+    assert s["read_match"] and s["write_through"] and not s["error"]
+
+
+def test_rdma_discovery_on_the_real_host():
+    """discovery/rdma.py on the box's own sysfs: its RDMA NICs (if any) with
+    their PCIe paths, each GPU's nearest ones and the GFD labels."""
+    from amdgpu_operator.discovery import labels, rdma, topology
+
+    gpus = topology.enumerate_gpus("/")
+    nics = rdma.enumerate_nics("/")
+    out = {"readiness": rdma.readiness("/"),
+           "nics": [{"name": n.name, "bdf": n.bdf, "numa": n.numa_node, "path": list(n.pci_path),
+                     "ports": [list(p) for p in n.ports]} for n in nics],
+           "gpus": [{"bdf": g.bdf, "numa": g.numa_node, "path": list(rdma.pci_path("/", g.bdf))} for g in gpus],
+           "nearest": rdma.nearest_nics(gpus, nics), "labels": rdma.rdma_labels(gpus)}
+    print(json.dumps(out))
+    if not nics:
+        pytest.skip("no RDMA device on this host")
+    assert all(n.pci_path[0].startswith("pci") for n in nics)
+    assert all(rdma.pci_path("/", g.bdf)[0].startswith("pci") for g in gpus)
+    assert set(out["nearest"]) == {g.bdf for g in gpus} and all(out["nearest"].values())
+    assert labels.gfd_labels(gpus)["amd.com/gpu.rdma.nics"] == str(sum(1 for n in nics if n.active))
