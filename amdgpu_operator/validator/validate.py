@@ -113,6 +113,9 @@ def validate_driver(env: NodeEnv, timeout: float = 600.0, stop=None) -> dict:
         if ok:
             gpus = topology.enumerate_gpus(env.sysfs_root())
             out = {"ok": True, "message": msg, "gpus": len(gpus), "seconds": time.perf_counter() - t0}
+            prev = read_ready(env, "driver") or {}
+            if "rdma" in prev:  # the driver container's driver.rdma record (driver/manager.py ensure_rdma)
+                out["rdma"] = prev["rdma"]
             write_ready(env, "driver", out)
             return out
         if time.monotonic() >= deadline:

@@ -366,7 +366,10 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             "rank0_total_seconds": ranks[0].get("seconds") if ranks else None,
             "labels": {k: v for k, v in (nobj["metadata"].get("labels") or {}).items()
                        if k in ("amd.com/gpu.product", "amd.com/gpu.arch", "amd.com/gpu.family", "amd.com/gpu.memory",
-                                "amd.com/gpu.xgmi.links", "amd.com/gpu.count", "amd.com/gpu.validated")},
+                                "amd.com/gpu.xgmi.links", "amd.com/gpu.count", "amd.com/gpu.validated",
+                                "amd.com/gpu.rdma.capable", "amd.com/gpu.rdma.nics", "amd.com/gpu.rdma.affinity")},
+            "dmabuf": [s for s in steps.get("dmabuf", [])],  # driver.rdma (--set driver.rdma.enabled=true)
+            "driver_rdma": (read_ready(nd.env, "driver") or {}).get("rdma"),
         }
     finally:
         gc.enable()
