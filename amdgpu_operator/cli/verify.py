@@ -159,6 +159,12 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
         validated = labels.get("amd.com/gpu.validated") == "true"
         rep.add(f"validated[{name}]", validated, "amd.com/gpu.validated=true" if validated else "not validated",
                 "README.md:199")
+        if ((spec.get("driver") or {}).get("rdma") or {}).get("enabled"):
+            # driver.rdma: NICs that can reach GPU memory (discovery/rdma.py labels)
+            cap, nics, aff = (labels.get("amd.com/gpu.rdma.capable"), labels.get("amd.com/gpu.rdma.nics"),
+                              labels.get("amd.com/gpu.rdma.affinity"))
+            rep.add(f"rdma[{name}]", cap == "true", f"capable={cap} nics={nics} affinity={aff}",
+                    "driver.rdma (upstream GPUDirect RDMA; not set in README.md:101-110)")
         if (spec.get("driver") or {}).get("enabled", True):
             smi = (n["metadata"].get("annotations") or {}).get(DRIVER_SMI_ANN, "")
             rep.add(f"driver-smi[{name}]", smi.startswith("ok"), smi or "not reported by amd-driver-health",

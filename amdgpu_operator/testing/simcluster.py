@@ -60,6 +60,7 @@ class NodeSpec:
     memory_partition: str = "NPS1"
     sysfs_root: str | None = None     # None = synthetic tree; "/" = this machine
     kernel: str = "6.8.0-45-generic"  # the node's kernel release (synthetic tree)
+    rdma_nics: bool = False           # synthetic tree: one RDMA NIC per GPU on its PCIe switch
 
 
 @dataclass
@@ -314,7 +315,10 @@ class SimCluster:
         if ns.sysfs_root is None:
             root = os.path.join(d, "host")
             if ns.gpus > 0:
-                fakesys.build_node(root, ns.gpus, ns.compute_partition, ns.memory_partition, kernel=ns.kernel)
+                fake = fakesys.build_node(root, ns.gpus, ns.compute_partition, ns.memory_partition, kernel=ns.kernel,
+                                          pcie_tree=ns.rdma_nics)
+                if ns.rdma_nics:
+                    fakesys.add_rdma_nics(root, fake, modules=False)  # the driver container loads the RDMA core
             else:
                 os.makedirs(os.path.join(root, "sys/bus/pci/devices"), exist_ok=True)
                 fakesys._w(os.path.join(root, "sys/bus/pci/devices/0000:00:01.0/vendor"), "0x1022\n")

@@ -192,3 +192,30 @@ def test_tree_layout_keeps_driver_and_iommu_links(node):
     assert os.path.islink(dev) and os.path.basename(os.path.realpath(os.path.join(dev, "driver"))) == "amdgpu"
     assert os.path.isdir(os.path.join(dev, "iommu_group"))
     assert api.HEALTHY == "Healthy"
+
+
+def test_rdma_bring_up_on_the_simulated_cluster(tmp_path):
+    """driver.rdma end to end: the driver container loads the RDMA core on
+    the node, the validator's dmabuf step runs, GFD labels the NICs, the
+    config-5 pods' allocations name their nearest NICs, and verify checks it."""
+    from amdgpu_operator.cli.verify import verify
+    from amdgpu_operator.testing.podworkload import run_pod_workload
+    from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
+
+    c = SimCluster(str(tmp_path / "c"), [NodeSpec("gpu-1", 4, rdma_nics=True)], fake_gpu=True).start()
+    try:
+        c.install_operator(parse_set_flags(REFERENCE_SET_FLAGS + ["driver.rdma.enabled=true"]))
+        c.wait_ready(60, {"gpu-1": 4})
+        lab = c.client.get("v1", "Node", "gpu-1")["metadata"]["labels"]
+        assert lab["amd.com/gpu.rdma.capable"] == "true" and lab["amd.com/gpu.rdma.affinity"] == "PIX"
+        env = c.nodes["gpu-1"].env
+        drv = V.read_ready(env, "driver")["rdma"]
+        assert drv["ok"] and drv["loaded_here"] and drv["nics"] == [f"ionic_{i}" for i in range(4)]
+        wl = V.read_ready(env, "workload")
+        assert all(any(s["name"] == "dmabuf" and s["ok"] for s in r["steps"]) for r in wl["ranks"])
+        rep = verify(c.client, c.namespace, expect_gpus_per_node=4)
+        assert rep.ok and next(x for x in rep.checks if x.name == "rdma[gpu-1]").ok, rep.table()
+        out = run_pod_workload(c, "gpu-1", 4, gemm_n=256)
+        assert out["all_succeeded"] and out["single_gpu_pods_distinct_devices"]
+    finally:
+        c.stop()
