@@ -32,7 +32,7 @@ def build_file(package: str, filename: str, messages: dict[str, list[tuple]], se
     """Create message classes.
 
     ``messages``: ``{"Msg": [(field, number, type, label), ...]}`` where type is a
-    scalar name, another message name, or ``"map<string,string>"``; label is
+    scalar name, another message name, or ``"map<string,T>"`` (T a scalar or a message); label is
     ``"opt"`` or ``"rep"``.
     ``services``: ``{"Svc": [(method, input, output, server_streaming), ...]}``
     (recorded in the descriptor for completeness; gRPC wiring is done with
@@ -50,7 +50,12 @@ def build_file(package: str, filename: str, messages: dict[str, list[tuple]], se
                 entry = m.nested_type.add(name=_camel(fname) + "Entry")
                 entry.options.map_entry = True
                 entry.field.add(name="key", number=1, type=_SCALARS[kt.strip()], label=F.LABEL_OPTIONAL, json_name="key")
-                entry.field.add(name="value", number=2, type=_SCALARS[vt.strip()], label=F.LABEL_OPTIONAL, json_name="value")
+                vt = vt.strip()
+                if vt in _SCALARS:
+                    entry.field.add(name="value", number=2, type=_SCALARS[vt], label=F.LABEL_OPTIONAL, json_name="value")
+                else:  # map<string, Message>
+                    entry.field.add(name="value", number=2, type=F.TYPE_MESSAGE, type_name=f".{package}.{vt}",
+                                    label=F.LABEL_OPTIONAL, json_name="value")
                 f.label = F.LABEL_REPEATED
                 f.type = F.TYPE_MESSAGE
                 f.type_name = f".{package}.{mname}.{entry.name}"

@@ -57,6 +57,10 @@ _TYPES = [
     ResourceType("monitoring.coreos.com", "v1", "ServiceMonitor", "servicemonitors", True),
     ResourceType("amd.com", "v1", "ClusterPolicy", "clusterpolicies", False),
     ResourceType("amd.com", "v1", "AMDGPUDriver", "amdgpudrivers", False),
+    # Dynamic Resource Allocation, structured parameters (dra/)
+    ResourceType("resource.k8s.io", "v1beta1", "ResourceSlice", "resourceslices", False),
+    ResourceType("resource.k8s.io", "v1beta1", "DeviceClass", "deviceclasses", False),
+    ResourceType("resource.k8s.io", "v1beta1", "ResourceClaim", "resourceclaims", True),
 ]
 
 REGISTRY: dict[tuple[str, str], ResourceType] = {(t.api_version, t.kind): t for t in _TYPES}

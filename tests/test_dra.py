@@ -1,0 +1,161 @@
+"""DRA driver ``gpu.amd.com`` (dra/): ResourceSlice content, kubelet
+registration, NodePrepareResources / NodeUnprepareResources with CDI specs
+and a checkpoint, the structured-parameters allocator of the simulated
+scheduler, and the wire codec against google.protobuf."""
+
+import json
+import os
+
+import grpc
+import pytest
+
+from amdgpu_operator.dra import api
+from amdgpu_operator.dra.driver import DraDriver, device_class, resource_slice
+from amdgpu_operator.discovery import topology as T
+from amdgpu_operator.kube import resources as R
+from amdgpu_operator.kube.client import LocalClient
+from amdgpu_operator.kube.fakeapi import FakeApiServer
+from amdgpu_operator.nodeenv import NodeEnv
+from amdgpu_operator.testing import fakedra, fakesys
+
+RV1B1 = "resource.k8s.io/v1beta1"
+
+
+def _claim(name, count=1, selectors=(), constraints=(), mode=None, ns="default"):
+    req = {"name": "gpus", "deviceClassName": api.DRIVER_NAME, "count": count,
+           "selectors": [{"cel": {"expression": e}} for e in selectors]}
+    if mode:
+        req["allocationMode"] = mode
+        req.pop("count")
+    return {"apiVersion": RV1B1, "kind": "ResourceClaim", "metadata": {"name": name, "namespace": ns},
+            "spec": {"devices": {"requests": [req], "constraints": list(constraints)}}}
+
+
+@pytest.fixture
+def node(tmp_path):
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 8)
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Node", "n1"))
+    c.create(device_class())
+    env = NodeEnv("n1", c, host_root=root, validations_dir=str(tmp_path / "val"), poll_s=0.01,
+                  device_plugin_dir=str(tmp_path / "kubelet" / "device-plugins"), cdi_dir=str(tmp_path / "cdi"))
+    drv = DraDriver(env)
+    drv.publish()
+    drv.serve()
+    yield env, drv, str(tmp_path / "kubelet")
+    drv.stop()
+
+
+def test_slice_lists_every_device_with_its_attributes(tmp_path):
+    root = str(tmp_path / "cpx")
+    fakesys.build_node(root, 2, compute_partition="CPX")
+    gpus = T.enumerate_gpus(root)
+    s = resource_slice("n1", gpus, "uid-1", "6.12.12")
+    devs = s["spec"]["devices"]
+    assert s["spec"]["driver"] == "gpu.amd.com" and s["spec"]["pool"] == {"name": "n1", "generation": 1,
+                                                                           "resourceSliceCount": 1}
+    assert [d["name"] for d in devs] == [f"gpu-{i}" for i in range(16)]
+    a = devs[9]["basic"]["attributes"]
+    assert a["productName"] == {"string": "AMD-Instinct-MI355X"} and a["architecture"] == {"string": "gfx950"}
+    assert a["computePartition"] == {"string": "CPX"} and a["physicalIndex"] == {"int": 1}
+    assert a["partitionIndex"] == {"int": 1} and a["driverVersion"] == {"version": "6.12.12"}
+    assert devs[9]["basic"]["capacity"]["computeUnits"] == {"value": str(gpus[9].cu_count)}
+    assert s["metadata"]["ownerReferences"][0]["kind"] == "Node"
+
+
+def test_register_allocate_prepare_unprepare(node):
+    env, drv, kdir = node
+    k = fakedra.FakeDraKubelet(kdir)
+    assert k.discover() == {api.DRIVER_NAME: drv.endpoint} and drv.registered.is_set()
+    c = env.client
+    # 2 GPUs on one NUMA node with at least 200 GiB each
+    claim = c.create(_claim("job", 2, selectors=['device.capacity["gpu.amd.com"].memory.compareTo(quantity("200Gi")) >= 0',
+                                                 'device.attributes["gpu.amd.com"].productName == "AMD-Instinct-MI355X"'],
+                            constraints=[{"matchAttribute": "gpu.amd.com/numaNode"}]))
+    claim = fakedra.allocate(c, claim, "n1")
+    res = claim["status"]["allocation"]["devices"]["results"]
+    assert len(res) == 2 and {r["pool"] for r in res} == {"n1"}
+    gpus = {f"gpu-{g.index}": g for g in T.enumerate_gpus(env.sysfs_root())}
+    assert len({gpus[r["device"]].numa_node for r in res}) == 1
+    out = k.prepare(api.DRIVER_NAME, [claim])[claim["metadata"]["uid"]]
+    assert not out.error and [d.device_name for d in out.devices] == [r["device"] for r in res]
+    uid = claim["metadata"]["uid"]
+    assert out.devices[0].cdi_device_ids == [f"gpu.amd.com/claim={uid}-{res[0]['device']}"]
+    with open(drv.cdi_path(uid)) as f:
+        spec = json.load(f)
+    assert spec["kind"] == "gpu.amd.com/claim" and spec["containerEdits"]["deviceNodes"][0]["path"] == "/dev/kfd"
+    assert [d["containerEdits"]["deviceNodes"][0]["path"] for d in spec["devices"]] == \
+        [gpus[r["device"]].render_node for r in res]
+    # idempotent, and a restarted driver answers from its checkpoint
+    assert k.prepare(api.DRIVER_NAME, [claim])[uid].devices[0].device_name == res[0]["device"]
+    drv2 = DraDriver(env)
+    assert drv2.prepared[uid]["devices"] == drv.prepared[uid]["devices"]
+    # a second claim gets other devices; a claim asking for too many fails to allocate
+    other = fakedra.allocate(c, c.create(_claim("job2", 6)), "n1")
+    assert not ({r["device"] for r in res} & {r["device"] for r in other["status"]["allocation"]["devices"]["results"]})
+    with pytest.raises(ValueError, match="no fitting set"):
+        fakedra.allocate(c, c.create(_claim("job3", 1)), "n1")
+    assert not k.unprepare(api.DRIVER_NAME, [claim])[uid].error
+    assert not os.path.exists(drv.cdi_path(uid)) and uid not in drv.prepared
+    assert not k.unprepare(api.DRIVER_NAME, [claim])[uid].error  # again: still fine
+
+
+def test_prepare_errors_name_the_claim(node):
+    env, drv, kdir = node
+    k = fakedra.FakeDraKubelet(kdir)
+    k.discover()
+    c = env.client
+    claim = c.create(_claim("a", 1))
+    unalloc = k.prepare(api.DRIVER_NAME, [claim])[claim["metadata"]["uid"]]
+    assert "no gpu.amd.com device allocated on n1" in unalloc.error
+    fake = dict(claim, metadata=dict(claim["metadata"], uid="not-the-uid"))
+    assert "kubelet asked for not-the-uid" in k.prepare(api.DRIVER_NAME, [fake])["not-the-uid"].error
+    gone = dict(claim, metadata=dict(claim["metadata"], name="gone"))
+    assert "not found" in k.prepare(api.DRIVER_NAME, [gone])[claim["metadata"]["uid"]].error
+
+
+def test_allocation_modes_and_selectors(node):
+    env, _, _ = node
+    c = env.client
+    every = fakedra.allocate(c, c.create(_claim("all", mode="All")), "n1")
+    assert len(every["status"]["allocation"]["devices"]["results"]) == 8
+    c.delete(RV1B1, "ResourceClaim", "all", "default")
+    none = c.create(_claim("big", 1, selectors=['device.attributes["gpu.amd.com"].computePartition == "CPX"']))
+    with pytest.raises(ValueError):
+        fakedra.allocate(c, none, "n1")
+    with pytest.raises(ValueError, match="supported subset"):
+        fakedra.cel_match('device.attributes["gpu.amd.com"].productName.startsWith("AMD")', api.DRIVER_NAME, {})
+    assert fakedra.quantity("288Gi") == 288 << 30 and fakedra.quantity("1500M") == 1_500_000_000
+
+
+def test_grpcio_kubelet_calls_the_dra_endpoint(node):
+    """The DRA endpoint against grpcio as the kubelet-side client."""
+    env, drv, _ = node
+    claim = fakedra.allocate(env.client, env.client.create(_claim("g", 1)), "n1")
+    i, o, _ = api.DRA_METHODS["NodePrepareResources"]
+    ipb, opb = api.protobuf_classes()[0]["NodePrepareResourcesRequest"], \
+        api.protobuf_classes()[0]["NodePrepareResourcesResponse"]
+    req = ipb()
+    req.claims.add(namespace="default", uid=claim["metadata"]["uid"], name="g")
+    with grpc.insecure_channel("unix:" + drv.endpoint) as ch:
+        call = ch.unary_unary(api.method_path(api.DRA_SERVICE, "NodePrepareResources"),
+                              request_serializer=ipb.SerializeToString, response_deserializer=opb.FromString)
+        resp = call(req, timeout=5)
+    got = resp.claims[claim["metadata"]["uid"]]  # a real proto3 map on the google.protobuf side
+    assert not got.error and got.devices[0].pool_name == "n1" and got.devices[0].cdi_device_ids[0].startswith(
+        "gpu.amd.com/claim=")
+    assert i and o
+
+
+def test_codec_matches_google_protobuf_for_dra_messages():
+    d_pb, r_pb = api.protobuf_classes()
+    ours = api.dra["NodePrepareResourcesResponse"]()
+    r = api.dra["NodePrepareResourceResponse"](error="")
+    r.devices.add(request_names=["gpus"], pool_name="n1", device_name="gpu-3", cdi_device_ids=["gpu.amd.com/claim=u-gpu-3"])
+    ours.claims.add(key="u", value=r)
+    theirs = d_pb["NodePrepareResourcesResponse"].FromString(ours.SerializeToString())
+    assert theirs.claims["u"].devices[0].device_name == "gpu-3"
+    assert api.dra["NodePrepareResourcesResponse"].FromString(theirs.SerializeToString()).claims[0].key == "u"
+    info = api.reg["PluginInfo"](type="DRAPlugin", name="gpu.amd.com", endpoint="/x", supported_versions=["v1beta1.DRAPlugin"])
+    assert r_pb["PluginInfo"].FromString(info.SerializeToString()).supported_versions == ["v1beta1.DRAPlugin"]
