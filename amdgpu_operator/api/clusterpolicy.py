@@ -135,6 +135,18 @@ class DevicePluginConfigRef(_M):
     default: str = ""
 
 
+class DraDriverSpec(Operand):
+    """DRA driver ``gpu.amd.com`` (dra/): GPUs as ResourceSlice devices for
+    ResourceClaims (Kubernetes >= 1.32, resource.k8s.io/v1beta1) instead of
+    the amd.com/gpu extended resource.  Off by default - the reference's
+    cluster is v1.28 (README.md:45-46) and advertises through the device
+    plugin (README.md:106,211); a GPU is handed out by one of the two."""
+
+    enabled: bool = False
+    image: str = "amd-device-plugin"  # the operand image that carries the device plugin
+    deviceClass: str = "gpu.amd.com"  # the DeviceClass the operator creates
+
+
 class DevicePluginSpec(Operand):
     """kubelet device plugin for amd.com/gpu (README.md:106,211)."""
 
@@ -366,6 +378,7 @@ class ClusterPolicySpec(_M):
     driver: DriverSpec = Field(default_factory=DriverSpec)
     toolkit: ToolkitSpec = Field(default_factory=ToolkitSpec)
     devicePlugin: DevicePluginSpec = Field(default_factory=DevicePluginSpec)
+    draDriver: DraDriverSpec = Field(default_factory=DraDriverSpec)
     dcgmExporter: MetricsExporterSpec = Field(default_factory=MetricsExporterSpec, alias="metricsExporter")
     nodeStatusExporter: NodeStatusExporterSpec = Field(default_factory=NodeStatusExporterSpec)
     gfd: GFDSpec = Field(default_factory=GFDSpec)
@@ -390,6 +403,9 @@ class ClusterPolicySpec(_M):
 
     @model_validator(mode="after")
     def _consistency(self):
+        if self.draDriver.enabled and self.devicePlugin.enabled:
+            raise ValueError("draDriver.enabled needs devicePlugin.enabled=false: both would hand out the same GPUs "
+                             "(ResourceClaims and amd.com/gpu)")
         if self.devicePlugin.enabled and not self.driver.enabled and not self.toolkit.enabled:
             pass  # host-installed driver/toolkit is a supported setup
         if self.migManager.enabled and self.devicePlugin.partitionStrategy == "single":
@@ -407,6 +423,7 @@ STATES = [
     ("state-container-toolkit", "toolkit"),
     ("state-operator-validation", "validator"),
     ("state-device-plugin", "devicePlugin"),
+    ("state-dra-driver", "draDriver"),
     ("state-metrics-exporter", "dcgmExporter"),
     ("state-gpu-feature-discovery", "gfd"),
     ("state-partition-manager", "migManager"),
@@ -420,7 +437,7 @@ STATES = [
 SANDBOX_OPERANDS = ("vfioManager", "sandboxValidator", "sandboxDevicePlugin")
 # which operands a GPU node runs for its amd.com/gpu.workload.config
 WORKLOAD_OPERANDS = {
-    "container": ("driver", "toolkit", "validator", "devicePlugin", "dcgmExporter", "gfd", "migManager",
+    "container": ("driver", "toolkit", "validator", "devicePlugin", "draDriver", "dcgmExporter", "gfd", "migManager",
                   "nodeStatusExporter"),
     "vm-passthrough": SANDBOX_OPERANDS,
 }

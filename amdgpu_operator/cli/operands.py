@@ -108,6 +108,8 @@ def build_parser() -> argparse.ArgumentParser:
     vm.add_argument("--kfd-idle-timeout", type=float, default=300.0)
     vm.add_argument("--interval", type=float, default=30.0)
 
+    sub.add_parser("dra-driver", help="DRA driver gpu.amd.com: ResourceSlice + kubelet DRA plugin (dra/)")
+
     sdp = sub.add_parser("sandbox-device-plugin", help="kubelet device plugin for vfio-bound GPUs")
     sdp.add_argument("--resource-prefix", default="amd.com")
     sdp.add_argument("--health-poll-ms", type=int, default=1000)
@@ -494,6 +496,18 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         stop.wait()
         ex.stop()
         srv.stop()
+        return 0
+
+    if cmd == "dra-driver":
+        from ..dra.driver import DraDriver
+
+        drv = DraDriver(env)
+        drv.serve()
+        drv.publish()
+        log.info("DRA driver gpu.amd.com: %d device(s) published, endpoint %s", len(drv.gpus), drv.endpoint)
+        ready()
+        stop.wait()
+        drv.stop(withdraw=True)  # the driver leaves the node: its devices stop being allocatable
         return 0
 
     if cmd == "node-status-exporter":

@@ -415,6 +415,39 @@ def state_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     return [_sa(sa, ns, owner), *rbac, _daemonset(spec, ns, owner, name, "devicePlugin", sa, [ctr], inits, vols)]
 
 
+DRA_RULES = [
+    {"apiGroups": [""], "resources": ["nodes"], "verbs": ["get"]},
+    {"apiGroups": ["resource.k8s.io"], "resources": ["resourceslices"],
+     "verbs": ["get", "list", "watch", "create", "update", "delete"]},
+    {"apiGroups": ["resource.k8s.io"], "resources": ["resourceclaims"], "verbs": ["get"]},
+]
+
+
+def state_dra_driver(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
+    """DRA driver gpu.amd.com (dra/driver.py): publishes the node's
+    ResourceSlice, registers with the kubelet's plugin watcher and prepares
+    claims as CDI specs; plus the DeviceClass claims name."""
+    from ..dra.driver import device_class
+
+    d = spec.draDriver
+    name, sa = "amd-dra-driver", "amd-dra-driver"
+    image = d.ref("amd-device-plugin")
+    ctr = _container("amd-dra-driver", image, d.imagePullPolicy, ["dra-driver", *d.args],
+                     [_mount("kubelet-plugins", "/var/lib/kubelet/plugins"),
+                      _mount("kubelet-registry", "/var/lib/kubelet/plugins_registry"),
+                      _mount("cdi-dir", spec.toolkit.cdi.specDir), *_host_view()],
+                     list(d.env), True, d.resources.model_dump())
+    inits = _gate(spec, ctr, _wait_init("driver-validation", image, d.imagePullPolicy, "driver"), "driver")
+    vols = [_hostpath("kubelet-plugins", "/var/lib/kubelet/plugins"),
+            _hostpath("kubelet-registry", "/var/lib/kubelet/plugins_registry"),
+            _hostpath("cdi-dir", spec.toolkit.cdi.specDir), _hostpath("host-sys", "/sys", "Directory"),
+            _hostpath("run-amd-validations", VALIDATIONS_HOST_DIR)]
+    dc = device_class(d.deviceClass)
+    dc["metadata"]["ownerReferences"] = owner
+    return [_sa(sa, ns, owner), _cluster_role(sa, DRA_RULES, owner), _cluster_binding(sa, sa, ns, owner), dc,
+            _daemonset(spec, ns, owner, name, "draDriver", sa, [ctr], inits, vols)]
+
+
 def state_metrics_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     m = spec.dcgmExporter
     name, sa = "amd-metrics-exporter", "amd-metrics-exporter"
@@ -648,6 +681,7 @@ STATE_BUILDERS = {
     "state-container-toolkit": state_toolkit,
     "state-operator-validation": state_validator,
     "state-device-plugin": state_device_plugin,
+    "state-dra-driver": state_dra_driver,
     "state-metrics-exporter": state_metrics_exporter,
     "state-node-feature-discovery": state_nfd,
     "state-gpu-feature-discovery": state_gfd,

@@ -15,6 +15,7 @@ OPERAND_LABELS = {
     "toolkit": "container-toolkit",
     "validator": "operator-validator",
     "devicePlugin": "device-plugin",
+    "draDriver": "dra-driver",
     "dcgmExporter": "metrics-exporter",
     "gfd": "gpu-feature-discovery",
     "migManager": "partition-manager",

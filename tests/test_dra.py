@@ -32,7 +32,19 @@ def _claim(name, count=1, selectors=(), constraints=(), mode=None, ns="default")
 
 
 @pytest.fixture
-def node(tmp_path):
+def short_tmp():
+    """unix socket paths are limited to 107 bytes; xdist's tmp_path can exceed it"""
+    import shutil
+    import tempfile
+
+    d = tempfile.mkdtemp(prefix="dra", dir="/tmp")
+    yield __import__("pathlib").Path(d)
+    shutil.rmtree(d, ignore_errors=True)
+
+
+@pytest.fixture
+def node(short_tmp):
+    tmp_path = short_tmp
     root = str(tmp_path / "host")
     fakesys.build_node(root, 8)
     c = LocalClient(FakeApiServer())
@@ -159,3 +171,37 @@ def test_codec_matches_google_protobuf_for_dra_messages():
     assert api.dra["NodePrepareResourcesResponse"].FromString(theirs.SerializeToString()).claims[0].key == "u"
     info = api.reg["PluginInfo"](type="DRAPlugin", name="gpu.amd.com", endpoint="/x", supported_versions=["v1beta1.DRAPlugin"])
     assert r_pb["PluginInfo"].FromString(info.SerializeToString()).supported_versions == ["v1beta1.DRAPlugin"]
+
+
+def test_policy_deploys_the_dra_driver_on_the_simulated_cluster(short_tmp):
+    """draDriver.enabled (device plugin off): the operator creates the
+    DeviceClass and the driver DaemonSet; the node's ResourceSlice lists its
+    GPUs; a claim allocated from it is prepared through the kubelet's DRA
+    side into a CDI spec on the node; the policy refuses both advertisers."""
+    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, parse_set_flags, spec_from_values
+    from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
+
+    with pytest.raises(ValueError, match="devicePlugin.enabled=false"):
+        spec_from_values(parse_set_flags(REFERENCE_SET_FLAGS + ["draDriver.enabled=true"]))
+    flags = REFERENCE_SET_FLAGS + ["draDriver.enabled=true", "devicePlugin.enabled=false"]
+    c = SimCluster(str(short_tmp / "c"), [NodeSpec("gpu-1", 4)], fake_gpu=True).start()
+    try:
+        c.install_operator(parse_set_flags(flags))
+        c.wait_ready(60)
+        slices = c.client.list(RV1B1, "ResourceSlice")
+        assert len(slices) == 1 and len(slices[0]["spec"]["devices"]) == 4 and slices[0]["spec"]["nodeName"] == "gpu-1"
+        assert c.client.get(RV1B1, "DeviceClass", "gpu.amd.com")
+        env = c.nodes["gpu-1"].env
+        k = fakedra.FakeDraKubelet(os.path.dirname(env.device_plugin_dir.rstrip("/")))
+        import time
+
+        deadline = time.monotonic() + 10
+        while not k.discover() and time.monotonic() < deadline:
+            time.sleep(0.05)
+        claim = fakedra.allocate(c.client, c.client.create(_claim("train", 4, constraints=[
+            {"matchAttribute": "gpu.amd.com/xgmiHive"}])), "gpu-1")
+        out = k.prepare(api.DRIVER_NAME, [claim])[claim["metadata"]["uid"]]
+        assert not out.error and len(out.devices) == 4
+        assert os.path.exists(os.path.join(env.cdi_dir, f"gpu.amd.com-claim_{claim['metadata']['uid']}.json"))
+    finally:
+        c.stop()
