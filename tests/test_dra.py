@@ -205,3 +205,34 @@ def test_policy_deploys_the_dra_driver_on_the_simulated_cluster(short_tmp):
         assert os.path.exists(os.path.join(env.cdi_dir, f"gpu.amd.com-claim_{claim['metadata']['uid']}.json"))
     finally:
         c.stop()
+
+
+@pytest.mark.gpu
+def test_real_mi355x_slice_and_claim(short_tmp):
+    """On the MI355X box: the slice built from the real KFD topology, and a
+    claim for it prepared into a CDI spec naming the real render node."""
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Node", "box"))
+    c.create(device_class())
+    env = NodeEnv("box", c, host_root="/", validations_dir=str(short_tmp / "val"), poll_s=0.01,
+                  device_plugin_dir=str(short_tmp / "kubelet" / "device-plugins"), cdi_dir=str(short_tmp / "cdi"))
+    drv = DraDriver(env)
+    drv.serve()
+    try:
+        s = drv.publish()
+        dev = s["spec"]["devices"][0]
+        print(json.dumps(s["spec"]))
+        assert dev["basic"]["attributes"]["architecture"] == {"string": "gfx950"}
+        assert int(dev["basic"]["capacity"]["memory"]["value"][:-2]) > 250_000  # MiB of HBM3E
+        k = fakedra.FakeDraKubelet(str(short_tmp / "kubelet"))
+        assert k.discover() == {api.DRIVER_NAME: drv.endpoint}
+        claim = fakedra.allocate(c, c.create(_claim("one", 1, selectors=[
+            'device.attributes["gpu.amd.com"].family == "CDNA4"'])), "box")
+        out = k.prepare(api.DRIVER_NAME, [claim])[claim["metadata"]["uid"]]
+        assert not out.error
+        with open(drv.cdi_path(claim["metadata"]["uid"])) as f:
+            spec = json.load(f)
+        node = spec["devices"][0]["containerEdits"]["deviceNodes"][0]["path"]
+        assert node.startswith("/dev/dri/renderD") and os.path.exists(node)
+    finally:
+        drv.stop()
