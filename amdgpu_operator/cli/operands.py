@@ -506,7 +506,11 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         drv.publish()
         log.info("DRA driver gpu.amd.com: %d device(s) published, endpoint %s", len(drv.gpus), drv.endpoint)
         ready()
-        stop.wait()
+        while not stop.wait(max(1.0, env.poll_s * 30)):  # a partition change re-creates the devices
+            try:
+                drv.refresh()
+            except Exception as e:  # noqa: BLE001 - API or sysfs hiccup: next round
+                log.warning("DRA refresh: %s", e)
         drv.stop(withdraw=True)  # the driver leaves the node: its devices stop being allocatable
         return 0
 

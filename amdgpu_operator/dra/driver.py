@@ -131,6 +131,21 @@ class DraDriver:
         want["metadata"]["resourceVersion"] = cur["metadata"].get("resourceVersion")
         return c.update(want)
 
+    def refresh(self) -> bool:
+        """Re-read the node's devices (a partition change re-creates them) and
+        republish when the set changed; True when it did."""
+        from ..discovery import topology
+
+        gpus = topology.enumerate_gpus(self.env.sysfs_root())
+        if [(device_name(g), g.bdf, g.compute_partition) for g in gpus] == \
+                [(device_name(g), g.bdf, g.compute_partition) for g in self.gpus]:
+            return False
+        self.gpus = gpus
+        self.by_name = {device_name(g): g for g in gpus}
+        self.publish()
+        log.info("devices changed: %d now published", len(gpus))
+        return True
+
     def withdraw(self) -> None:
         from ..kube.errors import NotFound
 

@@ -236,3 +236,17 @@ def test_real_mi355x_slice_and_claim(short_tmp):
         assert node.startswith("/dev/dri/renderD") and os.path.exists(node)
     finally:
         drv.stop()
+
+
+def test_partition_change_republishes_with_a_new_generation(node):
+    env, drv, _ = node
+    assert not drv.refresh()
+    root = env.sysfs_root()
+    import shutil
+
+    shutil.rmtree(os.path.join(root, "sys/class/kfd/kfd/topology/nodes"))
+    fakesys.build_node(root, 8, compute_partition="DPX")
+    assert drv.refresh()
+    s = env.client.get(RV1B1, "ResourceSlice", f"n1-{api.DRIVER_NAME}")
+    assert len(s["spec"]["devices"]) == 16 and s["spec"]["pool"]["generation"] == 2
+    assert s["spec"]["devices"][1]["basic"]["attributes"]["computePartition"] == {"string": "DPX"}
