@@ -50,6 +50,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="plugin: what the validation pod runs on its GPUs (amdgpu-gpu-check / amdgpu-validator)")
     v.add_argument("--plugin-pods", default="perResource", choices=["perResource", "perDevice"],
                    help="plugin: one pod per resource holding all its devices, or one 1-device pod per device")
+    v.add_argument("--dra", action="store_true",
+                   help="gpu: the GPUs are advertised by the DRA driver: validate a ResourceClaim + pod instead")
     v.add_argument("--wait-toolkit", action="store_true",
                    help="gpu: plugin validation waits for the toolkit; the workload starts right away")
     v.add_argument("--with-driver", action="store_true",
@@ -177,6 +179,9 @@ def _validate(env, a, extra, stop, ready) -> int:
     elif a.step == "workload":
         if V.read_ready(env, "workload") is None:
             V.validate_workload(env, extra, a.timeout)
+    elif a.step == "plugin" and a.dra:
+        if V.read_ready(env, "plugin") is None:
+            V.validate_dra(env, a.timeout, stop)
     elif a.step == "plugin":
         if V.read_ready(env, "plugin") is None:
             pod_args = _plugin_pod_args(extra)
@@ -187,7 +192,7 @@ def _validate(env, a, extra, stop, ready) -> int:
         V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
                        wait_toolkit=a.wait_toolkit, with_driver=a.with_driver,
                        partition_strategy=a.partition_strategy, pod_check=a.pod_check,
-                       per_device=a.plugin_pods == "perDevice")
+                       per_device=a.plugin_pods == "perDevice", dra=a.dra)
         if a.complete:
             return _complete(env, stop, ready)
     elif a.step == "vfio":
@@ -247,7 +252,7 @@ def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
             known += args[i:i + 2]
             i += 2
             continue
-        if a in ("--wait-toolkit", "--with-driver", "--complete"):
+        if a in ("--wait-toolkit", "--with-driver", "--complete", "--dra"):
             known.append(a)
             i += 1
             continue

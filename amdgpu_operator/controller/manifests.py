@@ -351,13 +351,17 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     plugin_res = ["--resource", spec.devicePlugin.resourceName,
                   "--partition-strategy", spec.devicePlugin.partitionStrategy, "--pod-check", v.pluginPodCheck,
                   "--plugin-pods", v.pluginPods]
-    if v.pluginValidation and spec.devicePlugin.enabled and w.prespawn:
+    # the GPUs' advertiser: the device plugin, or the DRA driver (a claim and a pod through the scheduler)
+    advertiser = spec.devicePlugin.enabled or spec.draDriver.enabled
+    if spec.draDriver.enabled:
+        plugin_res.append("--dra")
+    if v.pluginValidation and advertiser and w.prespawn:
         # one init container validates the driver and, meanwhile, starts the
         # workload processes behind their start gate (validate.py validate_gpu)
         extra = [*plugin_res, "--with-driver"] + (["--wait-toolkit"] if spec.toolkit.enabled else [])
         inits = [_wait_init("gpu-validation", image, v.imagePullPolicy, "gpu", [*extra, *wl_args],
                             env=_workload_pod_env(v, image), mounts=[POD_RESOURCES_MOUNT, DEVICE_PLUGINS_MOUNT])]
-    elif v.pluginValidation and spec.devicePlugin.enabled:  # (validation pods: _workload_pod_env)
+    elif v.pluginValidation and advertiser:  # (validation pods: _workload_pod_env)
         # workload (all GPUs, RCCL over xGMI) and plugin (1-GPU pods through the
         # device plugin + OCI hook) validation run concurrently.  The workload
         # needs only the driver (its processes run in this pod, not through the
@@ -384,8 +388,17 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     if any(m["name"] == "pod-resources" for c in [*inits, ctr] for m in c["volumeMounts"]):
         vols += [_hostpath("pod-resources", "/var/lib/kubelet/pod-resources"),
                  _hostpath("device-plugin", "/var/lib/kubelet/device-plugins")]
-    return [_sa(sa, ns, owner), _cluster_role(sa, NODE_RW_RULES, owner), _cluster_binding(sa, sa, ns, owner),
+    rules = NODE_RW_RULES + (VALIDATOR_DRA_RULES if spec.draDriver.enabled else [])
+    return [_sa(sa, ns, owner), _cluster_role(sa, rules, owner), _cluster_binding(sa, sa, ns, owner),
             _daemonset(spec, ns, owner, name, "validator", sa, [ctr], inits, vols)]
+
+
+# validate.py validate_dra: the node's slice, and a claim it creates and deletes
+VALIDATOR_DRA_RULES = [
+    {"apiGroups": ["resource.k8s.io"], "resources": ["resourceslices"], "verbs": ["get", "list", "watch"]},
+    {"apiGroups": ["resource.k8s.io"], "resources": ["resourceclaims"],
+     "verbs": ["get", "list", "watch", "create", "delete"]},
+]
 
 
 def state_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:

@@ -387,6 +387,7 @@ class SimCluster:
                                 "status": {"capacity": {"cpu": "128"}, "allocatable": {"cpu": "128"},
                                            "conditions": [{"type": "Ready", "status": "True"}]}})
         self._spawn(self._ds_controller_loop, "sim-ds-controller")
+        self._spawn(self._scheduler_loop, "sim-scheduler")
         for node in self.nodes.values():
             self._spawn(lambda n=node: self._kubelet_loop(n), f"sim-kubelet-{node.spec.name}")
             self._spawn(lambda n=node: self._node_status_loop(n), f"sim-nodestatus-{node.spec.name}")
@@ -586,6 +587,90 @@ class SimCluster:
                 self.sync_daemonsets()
             except Exception as e:  # noqa: BLE001
                 log.warning("ds sync: %s", e)
+
+    # ------------------------------------------------------------ scheduler
+    def _scheduler_loop(self) -> None:
+        """Pods without ``nodeName`` (those with ResourceClaims must go through
+        the scheduler: it allocates the claims): bound to the node their
+        ``kubernetes.io/hostname`` selector names once their claims are
+        allocated there (testing/fakedra.py allocate, the structured-parameters
+        allocator)."""
+        while not self.stop_event.is_set():
+            try:
+                for etype, pod in self.client.watch("v1", "Pod", stop=self.stop_event):
+                    if etype != "DELETED" and not pod["spec"].get("nodeName") \
+                            and not pod["metadata"].get("deletionTimestamp"):
+                        self._schedule(pod)
+            except Exception as e:  # noqa: BLE001
+                log.debug("scheduler watch: %s", e)
+                self.stop_event.wait(0.1)
+
+    def _schedule(self, pod: dict) -> None:
+        from . import fakedra
+
+        md = pod["metadata"]
+        node = ((pod["spec"].get("nodeSelector") or {}).get("kubernetes.io/hostname"))
+        if node not in self.nodes:
+            return
+        ns = md.get("namespace", "default")
+        try:
+            for rc in pod["spec"].get("resourceClaims") or []:
+                claim = self.client.get("resource.k8s.io/v1beta1", "ResourceClaim", rc["resourceClaimName"], ns)
+                if not (claim.get("status") or {}).get("allocation"):
+                    fakedra.allocate(self.client, claim, node)
+            self.client.patch("v1", "Pod", md["name"], {"spec": {"nodeName": node}}, ns)
+            self.trace("pod-scheduled", md["name"])
+        except (ValueError, NotFound) as e:  # unschedulable for now: the next event tries again
+            try:
+                self.client.patch("v1", "Pod", md["name"], {"status": {"phase": "Pending", "conditions": [
+                    {"type": "PodScheduled", "status": "False", "reason": "Unschedulable", "message": str(e)}]}}, ns)
+            except NotFound:
+                pass
+
+    def _prepare_claims(self, run: _PodRun) -> tuple[list[int], dict[str, str], list[str]]:
+        """The kubelet's DRA manager for a pod's ResourceClaims: prepare them
+        through the node's DRA driver and apply the CDI specs it wrote (render
+        nodes -> the devices the container sees, env).  Returns (device
+        indices, env, prepared claim uids)."""
+        from ..dra import api as dra_api
+        from . import fakedra
+
+        node = run.node
+        k = fakedra.FakeDraKubelet(os.path.dirname(node.env.device_plugin_dir.rstrip("/")))
+        deadline = time.monotonic() + 30
+        while dra_api.DRIVER_NAME not in k.discover():
+            if time.monotonic() >= deadline:
+                raise AdmissionError(f"DRA driver {dra_api.DRIVER_NAME} not registered on {node.spec.name}")
+            time.sleep(0.05)
+        claims = [self.client.get("resource.k8s.io/v1beta1", "ResourceClaim", rc["resourceClaimName"], run.ns)
+                  for rc in run.pod["spec"].get("resourceClaims") or []]
+        out = k.prepare(dra_api.DRIVER_NAME, claims)
+        errors = [r.error for r in out.values() if r.error]
+        if errors:
+            raise AdmissionError("; ".join(errors))
+        from ..discovery import topology
+
+        by_minor = {f"/dev/dri/renderD{g.render_minor}": g.index for g in topology.enumerate_gpus(node.env.sysfs_root())}
+        devices, envs = [], {}
+        for uid, r in out.items():
+            with open(os.path.join(node.env.cdi_dir, f"{dra_api.DRIVER_NAME}-claim_{uid}.json")) as f:
+                spec = json.load(f)
+            edits = {d["name"]: d["containerEdits"] for d in spec["devices"]}
+            for dev in r.devices:
+                for cdi_id in dev.cdi_device_ids:
+                    for dn in edits[cdi_id.split("=", 1)[1]].get("deviceNodes", []):
+                        if dn["path"] in by_minor:
+                            devices.append(by_minor[dn["path"]])
+            envs.update(e.split("=", 1) for e in spec.get("containerEdits", {}).get("env", []))
+        return devices, envs, list(out)
+
+    def _unprepare_claims(self, run: _PodRun, uids: list[str]) -> None:
+        from ..dra import api as dra_api
+        from . import fakedra
+
+        k = fakedra.FakeDraKubelet(os.path.dirname(run.node.env.device_plugin_dir.rstrip("/")))
+        if k.discover(timeout=2.0).get(dra_api.DRIVER_NAME):
+            k.unprepare(dra_api.DRIVER_NAME, [{"metadata": {"namespace": run.ns, "name": "", "uid": u}} for u in uids])
 
     # -------------------------------------------------------------- kubelet
     def _kubelet_loop(self, node: SimNode) -> None:
@@ -861,7 +946,11 @@ class SimCluster:
         gpu_res = [(k, int(v)) for k, v in limits.items() if k.startswith(RESOURCE_NAME)]
         envs: dict[str, str] = {}
         devices: list[int] = []
-        if gpu_res:
+        if run.pod["spec"].get("resourceClaims") and not gpu_res:  # DRA: the claims' CDI devices
+            devices, envs, uids = self._prepare_claims(run)
+            self.trace("gpu-pod-allocated", run.name)
+            run.cleanups.append(lambda: self._unprepare_claims(run, uids))
+        elif gpu_res:
             res, n = gpu_res[0]
             if not node.kubelet.wait_registered(res, timeout=30):
                 raise AdmissionError(f"resource {res} not registered on {node.spec.name}")

@@ -878,6 +878,77 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
     return summary
 
 
+def validate_dra(env: NodeEnv, timeout: float = 600.0, stop=None, image: str | None = None,
+                 pull_policy: str = "IfNotPresent", pull_secrets: list[str] | None = None) -> dict:
+    """The DRA counterpart of :func:`validate_plugin` (``draDriver.enabled``,
+    device plugin off): once the node's ResourceSlice lists every device, a
+    ResourceClaim for all of them (``allocationMode: All``) and one pod that
+    uses it and runs the pod check with ``--expect-devices`` - the scheduler
+    allocates the claim, the kubelet has the DRA driver prepare it, the
+    runtime injects the claim's CDI devices.  The pod goes through the
+    scheduler (``kubernetes.io/hostname`` selector, no ``nodeName``): a pod
+    bound directly would skip the claim's allocation."""
+    from ..discovery import topology
+    from ..dra.api import DRIVER_NAME
+    from ..kube.client import wait_for
+
+    pod_image = env.extra.get("validator_image") or {}
+    image = image or pod_image.get("image") or "amd-operator-validator"
+    pull_policy = pod_image.get("pull_policy") or pull_policy
+    pull_secrets = list(pod_image.get("pull_secrets") or []) if pull_secrets is None else pull_secrets
+    t0 = time.perf_counter()
+    n = len(topology.enumerate_gpus(env.sysfs_root()))
+    deadline = time.monotonic() + timeout
+    slice_name = f"{env.node_name}-{DRIVER_NAME}"
+    _, ok = wait_for(env.client, "resource.k8s.io/v1beta1", "ResourceSlice",
+                     lambda objs: len(((objs.get(slice_name) or {}).get("spec") or {}).get("devices") or []) == n,
+                     name=slice_name, timeout=timeout, stop=stop, poll_s=env.poll_s)
+    if not ok:
+        raise StepFailed(f"ResourceSlice {slice_name} does not list the node's {n} device(s)")
+    marks = {"start": time.time() - (time.perf_counter() - t0), "devices_seen": time.time()}
+    run_id = os.urandom(4).hex()
+    name = f"amd-validator-dra-{run_id}"
+    claim = {"apiVersion": "resource.k8s.io/v1beta1", "kind": "ResourceClaim",
+             "metadata": {"name": name, "namespace": env.namespace, "labels": {WORKLOAD_POD_LABEL: run_id}},
+             "spec": {"devices": {"requests": [{"name": "gpus", "deviceClassName": DRIVER_NAME,
+                                                "allocationMode": "All"}]}}}
+    pod = {"apiVersion": "v1", "kind": "Pod",
+           "metadata": {"name": name, "namespace": env.namespace,
+                        "labels": {"app": "amd-validator-workload", WORKLOAD_POD_LABEL: run_id}},
+           "spec": {"nodeSelector": {"kubernetes.io/hostname": env.node_name}, "restartPolicy": "Never",
+                    "resourceClaims": [{"name": "gpus", "resourceClaimName": name}],
+                    "containers": [{"name": "workload", "image": image, "imagePullPolicy": pull_policy,
+                                    "command": ["amdgpu-gpu-check"], "args": ["--timeout", "30", "--expect-devices",
+                                                                              str(n)],
+                                    "env": PLUGIN_POD_ENV, "resources": {"claims": [{"name": "gpus"}]}}]}}
+    if pull_secrets:
+        pod["spec"]["imagePullSecrets"] = [{"name": x} for x in pull_secrets]
+    env.client.create(claim)
+    try:
+        env.client.create(pod)
+        marks["pods_created"] = time.time()
+        objs, ok = wait_for(env.client, "v1", "Pod", lambda o: (((o.get(name) or {}).get("status") or {}).get("phase")
+                                                                 in ("Succeeded", "Failed")),
+                            name=name, namespace=env.namespace, timeout=max(0.0, deadline - time.monotonic()),
+                            stop=stop, poll_s=env.poll_s)
+        st = (objs.get(name) or {}).get("status") or {}
+        if not ok or st.get("phase") != "Succeeded":
+            raise StepFailed(f"DRA validation pod {st.get('phase', 'Missing')}: {st.get('message', '')[-300:]}")
+        got = env.client.get("resource.k8s.io/v1beta1", "ResourceClaim", name, env.namespace)
+        devices = [r["device"] for r in (((got.get("status") or {}).get("allocation") or {}).get("devices") or {})
+                   .get("results", [])]
+    finally:
+        for kind, api_version in (("Pod", "v1"), ("ResourceClaim", "resource.k8s.io/v1beta1")):
+            try:
+                env.client.delete(api_version, kind, name, env.namespace)
+            except Exception:  # noqa: BLE001
+                pass
+    summary = {"ok": True, "pods": 1, "devices_validated": len(devices), "devices": devices, "pod_mode": "dra",
+               "claim": name, "marks": {k: round(v, 4) for k, v in marks.items()}, "seconds": time.perf_counter() - t0}
+    write_ready(env, "plugin", summary)
+    return summary
+
+
 START_GATE_PREFIX = ".start-gate-"
 
 
@@ -936,8 +1007,9 @@ def abort_start_gates(env: NodeEnv) -> list[str]:
 def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURCE_NAME,
                  pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                  wait_toolkit: bool = False, with_driver: bool = False, partition_strategy: str = "single",
-                 pod_check: str = "hsa", per_device: bool = False) -> dict:
+                 pod_check: str = "hsa", per_device: bool = False, dra: bool = False) -> dict:
     """Workload and plugin validation concurrently (each skipped if already done).
+    ``dra``: the plugin step validates the DRA driver instead (:func:`validate_dra`).
 
     Only the driver gates the workload: its processes run in this privileged
     pod, not through the container runtime, so they start while the toolkit
@@ -1009,7 +1081,9 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
                 wait_ready(env, "toolkit", timeout, stop)
             if os.environ.get("AMDGPU_EXPERIMENT_PLUGIN_AFTER_WORKLOAD"):  # start-up contention experiment
                 wait_ready(env, "workload", timeout, stop)
-            if read_ready(env, "plugin") is None:
+            if read_ready(env, "plugin") is None and dra:
+                results["plugin"] = validate_dra(env, timeout, stop)
+            elif read_ready(env, "plugin") is None:
                 results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop,
                                                     kubelet=kubelet, partition_strategy=partition_strategy,
                                                     pod_check=pod_check, per_device=per_device,

@@ -188,6 +188,13 @@ def test_policy_deploys_the_dra_driver_on_the_simulated_cluster(short_tmp):
     try:
         c.install_operator(parse_set_flags(flags))
         c.wait_ready(60)
+        env = c.nodes["gpu-1"].env
+        from amdgpu_operator.validator.validate import read_ready
+
+        plug = read_ready(env, "plugin")  # the validator proved the DRA path: a claim for all 4, one pod
+        assert plug["pod_mode"] == "dra" and plug["devices_validated"] == 4, plug
+        assert not c.client.list(RV1B1, "ResourceClaim")  # its claim is gone again
+        assert not os.listdir(env.cdi_dir) or not any(f.startswith("gpu.amd.com-claim_") for f in os.listdir(env.cdi_dir))
         slices = c.client.list(RV1B1, "ResourceSlice")
         assert len(slices) == 1 and len(slices[0]["spec"]["devices"]) == 4 and slices[0]["spec"]["nodeName"] == "gpu-1"
         assert c.client.get(RV1B1, "DeviceClass", "gpu.amd.com")
