@@ -289,7 +289,9 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
         gc_stats = gcm.stop()
         gc.enable()
         # the kubelet then publishes amd.com/gpu in Node.status on its own status tick
-        cluster.wait_ready(args.timeout, {"mi355x-node-0": n_gpus})
+        # (experiments with the DRA driver instead of the device plugin: no amd.com/gpu)
+        if (values.get("devicePlugin") or {}).get("enabled", True) is not False:
+            cluster.wait_ready(args.timeout, {"mi355x-node-0": n_gpus})
         alloc_visible = time.perf_counter() - t0
         t_total = time.perf_counter() - t0
         pod_workload = None
