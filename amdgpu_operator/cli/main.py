@@ -26,7 +26,7 @@ from .. import DEFAULT_NAMESPACE
 from ..utils import logs
 
 OPERAND_CMDS = {"driver", "toolkit", "validate", "device-plugin", "metrics-exporter", "node-status-exporter", "nfd",
-                "gfd", "partition-manager", "vfio-manager", "sandbox-device-plugin"}
+                "gfd", "partition-manager", "vfio-manager", "sandbox-device-plugin", "dra-driver"}
 
 
 def _client(args):

@@ -173,7 +173,8 @@ def test_codec_matches_google_protobuf_for_dra_messages():
     assert r_pb["PluginInfo"].FromString(info.SerializeToString()).supported_versions == ["v1beta1.DRAPlugin"]
 
 
-def test_policy_deploys_the_dra_driver_on_the_simulated_cluster(short_tmp):
+@pytest.mark.parametrize("processes", [False, True], ids=["threads", "processes"])
+def test_policy_deploys_the_dra_driver_on_the_simulated_cluster(short_tmp, processes):
     """draDriver.enabled (device plugin off): the operator creates the
     DeviceClass and the driver DaemonSet; the node's ResourceSlice lists its
     GPUs; a claim allocated from it is prepared through the kubelet's DRA
@@ -184,7 +185,8 @@ def test_policy_deploys_the_dra_driver_on_the_simulated_cluster(short_tmp):
     with pytest.raises(ValueError, match="devicePlugin.enabled=false"):
         spec_from_values(parse_set_flags(REFERENCE_SET_FLAGS + ["draDriver.enabled=true"]))
     flags = REFERENCE_SET_FLAGS + ["draDriver.enabled=true", "devicePlugin.enabled=false"]
-    c = SimCluster(str(short_tmp / "c"), [NodeSpec("gpu-1", 4)], fake_gpu=True).start()
+    c = SimCluster(str(short_tmp / "c"), [NodeSpec("gpu-1", 4)], fake_gpu=True,
+                   process_containers=processes).start()  # processes: the operand images' entry point
     try:
         c.install_operator(parse_set_flags(flags))
         c.wait_ready(60)
