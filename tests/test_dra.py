@@ -196,14 +196,17 @@ def test_policy_deploys_the_dra_driver_on_the_simulated_cluster(short_tmp, proce
         plug = read_ready(env, "plugin")  # the validator proved the DRA path: a claim for all 4, one pod
         assert plug["pod_mode"] == "dra" and plug["devices_validated"] == 4, plug
         assert not c.client.list(RV1B1, "ResourceClaim")  # its claim is gone again
-        assert not os.listdir(env.cdi_dir) or not any(f.startswith("gpu.amd.com-claim_") for f in os.listdir(env.cdi_dir))
+        import time
+
+        deadline = time.monotonic() + 10  # the kubelet unprepares the claim once the deleted pod has stopped
+        while any(f.startswith("gpu.amd.com-claim_") for f in os.listdir(env.cdi_dir)) and time.monotonic() < deadline:
+            time.sleep(0.05)
+        assert not any(f.startswith("gpu.amd.com-claim_") for f in os.listdir(env.cdi_dir))
         slices = c.client.list(RV1B1, "ResourceSlice")
         assert len(slices) == 1 and len(slices[0]["spec"]["devices"]) == 4 and slices[0]["spec"]["nodeName"] == "gpu-1"
         assert c.client.get(RV1B1, "DeviceClass", "gpu.amd.com")
         env = c.nodes["gpu-1"].env
         k = fakedra.FakeDraKubelet(os.path.dirname(env.device_plugin_dir.rstrip("/")))
-        import time
-
         deadline = time.monotonic() + 10
         while not k.discover() and time.monotonic() < deadline:
             time.sleep(0.05)
