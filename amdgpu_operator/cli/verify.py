@@ -33,12 +33,14 @@ EXPECTED_OPERANDS = {
     "amd-driver-daemonset": "driver",
     "amd-container-toolkit-daemonset": "toolkit",
     "amd-device-plugin-daemonset": "devicePlugin",
+    "amd-dra-driver": "draDriver",
     "amd-operator-validator": "validator",
     "gpu-feature-discovery": "gfd",
     "amd-metrics-exporter": "dcgmExporter",
     "amd-node-status-exporter": "nodeStatusExporter",
     "node-feature-discovery-worker": "nfd",
 }
+OFF_BY_DEFAULT = {"draDriver"}  # operands a policy without the key does not run
 # vm-passthrough nodes (sandboxWorkloads) run these instead of the container operands
 EXPECTED_SANDBOX_OPERANDS = {
     "amd-vfio-manager": "vfioManager",
@@ -104,6 +106,20 @@ def _pod_ok(p: dict) -> tuple[bool, str]:
     return ok, f"{phase} {ready}/{len(cs)} restarts={restarts}"
 
 
+def _allocatable_check(rep: "Report", name: str, labels: dict, allocs: dict, expect_gpus_per_node: int | None) -> None:
+    # amd.com/gpu, partition (-cpx ...) and time-sliced (.shared / renamed) resources all count;
+    # time-slicing multiplies the advertised devices by the replicas GFD publishes
+    count = _count(allocs, lambda k: k == RESOURCE_NAME or k.startswith((RESOURCE_NAME + "-", RESOURCE_NAME + ".")))
+    try:
+        replicas = max(1, int(labels.get("amd.com/gpu.replicas", "1")))
+    except ValueError:
+        replicas = 1
+    want = expect_gpus_per_node * replicas if expect_gpus_per_node else None
+    ok = count > 0 and (want is None or count == want)
+    rep.add(f"allocatable[{name}]", ok, f"{RESOURCE_NAME}*={count}" + (f" (expected {want})" if want else ""),
+            "README.md:122")
+
+
 def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> Report:
     rep = Report()
     nodes = client.list("v1", "Node")
@@ -137,17 +153,18 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
             rep.add(f"validated[{name}]", validated, "GPUs on vfio-pci" if validated else "not validated",
                     "README.md:199")
             continue
-        # amd.com/gpu, partition (-cpx ...) and time-sliced (.shared / renamed) resources all count;
-        # time-slicing multiplies the advertised devices by the replicas GFD publishes
-        count = _count(allocs, lambda k: k == RESOURCE_NAME or k.startswith((RESOURCE_NAME + "-", RESOURCE_NAME + ".")))
-        try:
-            replicas = max(1, int(labels.get("amd.com/gpu.replicas", "1")))
-        except ValueError:
-            replicas = 1
-        want = expect_gpus_per_node * replicas if expect_gpus_per_node else None
-        ok = count > 0 and (want is None or count == want)
-        rep.add(f"allocatable[{name}]", ok, f"{RESOURCE_NAME}*={count}" + (f" (expected {want})" if want else ""),
-                "README.md:122")
+        if (spec.get("draDriver") or {}).get("enabled"):
+            # DRA: the node's GPUs are devices of its ResourceSlice, not amd.com/gpu
+            try:
+                sl = client.get("resource.k8s.io/v1beta1", "ResourceSlice", f"{name}-gpu.amd.com")
+                count = len((sl.get("spec") or {}).get("devices") or [])
+            except Exception:  # noqa: BLE001 - no slice
+                count = 0
+            want = expect_gpus_per_node
+            rep.add(f"resourceslice[{name}]", count > 0 and (want is None or count == want),
+                    f"gpu.amd.com devices={count}" + (f" (expected {want})" if want else ""), "README.md:122 (DRA)")
+        else:
+            _allocatable_check(rep, name, labels, allocs, expect_gpus_per_node)
         # what the reference reads off `nvidia-smi` in the driver container
         # (README.md:152-166: product, memory, GPU count) comes from GFD labels
         prod, mem, arch = (labels.get("amd.com/gpu.product"), labels.get("amd.com/gpu.memory"),
@@ -195,7 +212,7 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
     if drv:  # per-kernel (usePrecompiled) and per-pool (AMDGPUDriver) driver DaemonSets count as the driver
         present.add("amd-driver-daemonset")
     missing = [ds for ds, key in EXPECTED_OPERANDS.items()
-               if (spec.get(key) or {}).get("enabled", True) and ds not in present
+               if (spec.get(key) or {}).get("enabled", key not in OFF_BY_DEFAULT) and ds not in present
                and (container_nodes if key != "nfd" else gpu_nodes)]
     missing += [ds for ds, key in EXPECTED_SANDBOX_OPERANDS.items()
                 if vm_nodes and (spec.get(key) or {}).get("enabled", True) and ds not in present]

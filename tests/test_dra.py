@@ -196,6 +196,10 @@ def test_policy_deploys_the_dra_driver_on_the_simulated_cluster(short_tmp, proce
         plug = read_ready(env, "plugin")  # the validator proved the DRA path: a claim for all 4, one pod
         assert plug["pod_mode"] == "dra" and plug["devices_validated"] == 4, plug
         assert not c.client.list(RV1B1, "ResourceClaim")  # its claim is gone again
+        from amdgpu_operator.cli.verify import verify
+
+        rep = verify(c.client, c.namespace, expect_gpus_per_node=4)
+        assert rep.ok and next(x for x in rep.checks if x.name == "resourceslice[gpu-1]").ok, rep.table()
         import time
 
         deadline = time.monotonic() + 10  # the kubelet unprepares the claim once the deleted pod has stopped
