@@ -11,7 +11,6 @@ import pytest
 
 from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, parse_set_flags, spec_from_values
 from amdgpu_operator.controller import manifests as M
-from amdgpu_operator.deviceplugin import api
 from amdgpu_operator.deviceplugin.server import DevicePluginServer, PluginConfig
 from amdgpu_operator.discovery import labels as L
 from amdgpu_operator.discovery import rdma
@@ -191,7 +190,6 @@ def test_tree_layout_keeps_driver_and_iommu_links(node):
     dev = os.path.join(root, "sys/bus/pci/devices/0000:72:00.0")
     assert os.path.islink(dev) and os.path.basename(os.path.realpath(os.path.join(dev, "driver"))) == "amdgpu"
     assert os.path.isdir(os.path.join(dev, "iommu_group"))
-    assert api.HEALTHY == "Healthy"
 
 
 def test_rdma_bring_up_on_the_simulated_cluster(tmp_path):
