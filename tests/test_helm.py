@@ -66,6 +66,24 @@ def test_overrides_reach_the_cluster_policy():
     assert s.validator.workload.gemmN == 8192 and s.migManager.enabled
 
 
+@pytest.mark.parametrize("flags", [
+    [],
+    ["sandboxWorkloads.enabled=true", "sandboxWorkloads.defaultWorkload=vm-passthrough", "vfioManager.enabled=true"],
+    ["draDriver.enabled=true", "devicePlugin.enabled=false", "driver.rdma.enabled=true", "psa.enabled=true"],
+])
+def test_every_spec_section_reaches_the_cluster_policy(flags):
+    """The chart's ClusterPolicy carries every section of the spec: what
+    `helm install --set ...` sets is what the operator reconciles (the
+    simulated cluster builds the CR from the values directly)."""
+    from amdgpu_operator.api.clusterpolicy import ClusterPolicySpec as S
+
+    docs = H.render_chart(set_flags=REFERENCE_SET_FLAGS + flags)
+    cp = next(d for d in docs if d["kind"] == "ClusterPolicy")
+    assert set(cp["spec"]) >= set(S.model_fields), set(S.model_fields) - set(cp["spec"])
+    rendered = S.model_validate(cp["spec"]).model_dump()
+    assert rendered == spec_from_values(parse_set_flags(REFERENCE_SET_FLAGS + flags)).model_dump()
+
+
 def test_crd_schema_accepts_rendered_spec_keys():
     crd = H.load_crd()
     props = crd["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]["spec"]["properties"]
