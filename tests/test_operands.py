@@ -642,3 +642,38 @@ def test_gfd_labels_describe_every_gpu_of_a_mixed_node(tmp_path):
     assert lab["amd.com/gpu.mfma.fp4"] == "false" and lab["amd.com/gpu.mfma.bf16"] == "true"
     for k, v in lab.items():
         assert len(k.split("/", 1)[1]) <= 63 and len(v) <= 63, (k, v)
+
+
+@pytest.mark.parametrize("flags", [[], ["draDriver.enabled=true", "devicePlugin.enabled=false", "driver.rdma.enabled=true",
+                                        "sandboxWorkloads.enabled=true", "migManager.enabled=true"]])
+def test_every_rendered_container_command_parses(flags):
+    """Every container the operator renders runs ``amdgpu-operator <cmd>``
+    with a command the entry point dispatches (cli/main.py OPERAND_CMDS or
+    its own sub-commands) and arguments its parser accepts - the image's
+    entry point, not only the in-process operand runner, must know them."""
+    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, parse_set_flags, spec_from_values
+    from amdgpu_operator.cli import main as M
+    from amdgpu_operator.cli.operands import _split_passthrough, build_parser
+    from amdgpu_operator.controller import manifests as MF
+
+    spec = spec_from_values(parse_set_flags(REFERENCE_SET_FLAGS + flags))
+    seen = set()
+    for builder in MF.STATE_BUILDERS.values():
+        for o in builder(spec, "ns", None):
+            if o.get("kind") not in ("DaemonSet", "Deployment", "Job"):
+                continue
+            tmpl = o["spec"]["template"]["spec"]
+            for c in tmpl.get("initContainers", []) + tmpl["containers"]:
+                if c.get("command") != ["amdgpu-operator"]:
+                    continue
+                args = list(c["args"])
+                assert args[0] in M.OPERAND_CMDS, (o["metadata"]["name"], args[0])
+                if args[0] == "validate":
+                    known, _ = _split_passthrough(args[1:])
+                    build_parser().parse_args(["validate", *known])
+                else:
+                    build_parser().parse_args(args)
+                seen.add(args[0])
+    assert {"driver", "validate"} <= seen
+    if flags:
+        assert "dra-driver" in seen
