@@ -75,6 +75,21 @@ class _Handler(BaseHTTPRequestHandler):
         try:
             t, ns, name, sub = _parse_path(u.path)
             api = self.api
+            authz = getattr(self.server, "authorizer", None)
+            if authz is not None:  # kube/rbac.py: the caller's ServiceAccount must be granted the request
+                from .rbac import verb_of
+
+                auth = self.headers.get("Authorization", "")
+                user = self.server.tokens.get(auth[7:] if auth.startswith("Bearer ") else "")
+                if user is None:
+                    raise ApiError(401, "Unauthorized", "no valid bearer token")
+                verb = verb_of(method, name, method == "GET" and q.get("watch") in ("1", "true"))
+                res = t.plural + (f"/{sub}" if sub else "")
+                if not authz.allowed(user, verb, t.group, res, ns, name):
+                    where = f' in the namespace "{ns}"' if ns else " at the cluster scope"
+                    self.server.denied.append((user, verb, t.group, res, ns, name))
+                    raise ApiError(403, "Forbidden", f'User "{user}" cannot {verb} resource "{res}" in API group '
+                                                     f'"{t.group}"{where}')
             if method == "GET" and name is None:
                 if q.get("watch") in ("1", "true"):
                     return self._watch(t, ns, q)
@@ -154,7 +169,26 @@ class HttpApiServer:
         self.httpd = _Server((host, port), handler)
         self.httpd.daemon_threads = True
         self.httpd.stopping = threading.Event()
+        self.httpd.authorizer = None  # enable_rbac()
+        self.httpd.tokens = {}  # bearer token -> user
+        self.httpd.denied = []  # (user, verb, group, resource, namespace, name) refused
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True, name="fake-apiserver-http")
+
+    def enable_rbac(self) -> None:
+        """Authorize every request against the RBAC objects in the API (kube/rbac.py)."""
+        from .rbac import Authorizer
+
+        self.httpd.authorizer = Authorizer(self.httpd.RequestHandlerClass.api)
+
+    def token_for(self, namespace: str, service_account: str) -> str:
+        """A bearer token that authenticates as ``namespace/service_account``."""
+        token = f"sa-{namespace}-{service_account}"
+        self.httpd.tokens[token] = f"system:serviceaccount:{namespace}:{service_account}"
+        return token
+
+    @property
+    def denied(self) -> list:
+        return self.httpd.denied
 
     @property
     def url(self) -> str:

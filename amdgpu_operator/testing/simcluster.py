@@ -225,7 +225,8 @@ class SimCluster:
                  fake_gpu: bool = True, poll_s: float = 0.01, launcher=None,
                  termination_s: float | None = None, agent_poll_s: float | None = None,
                  node_status_s: float | None = None, operator_resync_s: float = 1.0,
-                 operator_debounce_s: float = 0.005, http_api: bool = False, process_containers: bool = False):
+                 operator_debounce_s: float = 0.005, http_api: bool = False, process_containers: bool = False,
+                 rbac: bool = False):
         """``termination_s``: model graceful pod deletion - a deleted pod stays
         Terminating (listed, with ``deletionTimestamp``) for that many seconds
         (capped by its own grace period) before its kubelet removes it.
@@ -274,13 +275,16 @@ class SimCluster:
             self._http = HttpApiServer(self.api).start()
             self.agent_client = RestClient(self._http.url)
             if process_containers:  # what the operand processes read (main.py: KUBECONFIG)
-                self._kubeconfig = os.path.join(workdir, "kubeconfig")
                 os.makedirs(workdir, exist_ok=True)
-                with open(self._kubeconfig, "w") as f:
-                    json.dump({"apiVersion": "v1", "kind": "Config", "current-context": "sim",
-                               "clusters": [{"name": "sim", "cluster": {"server": self._http.url}}],
-                               "users": [{"name": "sim", "user": {}}],
-                               "contexts": [{"name": "sim", "context": {"cluster": "sim", "user": "sim"}}]}, f)
+                self._kubeconfig = self._write_kubeconfig(os.path.join(workdir, "kubeconfig"))
+            if rbac:
+                if not process_containers:
+                    raise ValueError("rbac=True needs process_containers=True (a ServiceAccount per process)")
+                # every request authorized against the ClusterRoles the chart
+                # and the operator create: the operator and each operand
+                # process run as their own ServiceAccount (kube/rbac.py)
+                self._http.enable_rbac()
+        self.rbac = rbac
         self.nodes: dict[str, SimNode] = {}
         self.stop_event = threading.Event()
         self._threads: list[threading.Thread] = []
@@ -376,8 +380,40 @@ class SimCluster:
             return self.launcher(argv, env, device, timeout)
         return run_local(argv, env, timeout)
 
+    def _write_kubeconfig(self, path: str, token: str | None = None) -> str:
+        with open(path, "w") as f:
+            json.dump({"apiVersion": "v1", "kind": "Config", "current-context": "sim",
+                       "clusters": [{"name": "sim", "cluster": {"server": self._http.url}}],
+                       "users": [{"name": "sim", "user": {"token": token} if token else {}}],
+                       "contexts": [{"name": "sim", "context": {"cluster": "sim", "user": "sim"}}]}, f)
+        return path
+
+    def _kubeconfig_for(self, namespace: str, service_account: str) -> str:
+        """rbac: the kubeconfig of a ServiceAccount (its token); else the shared one."""
+        if not self.rbac:
+            return self._kubeconfig
+        path = os.path.join(self.workdir, f"kubeconfig-{namespace}-{service_account}")
+        if not os.path.exists(path):
+            self._write_kubeconfig(path, self._http.token_for(namespace, service_account))
+        return path
+
+    def install_chart_rbac(self) -> None:
+        """The chart's own RBAC (the operator's ClusterRole and binding), as
+        ``helm install`` creates it, for ``rbac`` runs."""
+        from ..helm.render import render_chart
+
+        for d in render_chart(set_flags=["operator.cleanupCRD=false"], namespace=self.namespace):
+            if d.get("kind") in ("ClusterRole", "ClusterRoleBinding", "Role", "RoleBinding") \
+                    and d["metadata"]["name"] == "amd-gpu-operator":
+                try:
+                    self.client.create(d)
+                except Exception:  # noqa: BLE001 - already there
+                    pass
+
     def start(self) -> "SimCluster":
         self.client.create(R.new("v1", "Namespace", self.namespace))
+        if self.rbac:
+            self.install_chart_rbac()
         for ns in self._node_specs:
             node = self._make_node(ns)
             node.kubelet.start()
@@ -419,7 +455,8 @@ class SimCluster:
         penv.update({"AMDGPU_READY_FILE": ready, "PYTHONPATH": os.pathsep.join(
             [root] + [x for x in os.environ.get("PYTHONPATH", "").split(os.pathsep) if x])})
         penv.pop("KUBERNETES_SERVICE_HOST", None)
-        argv = [sys.executable, "-m", "amdgpu_operator", "operator", "--kubeconfig", self._kubeconfig,
+        argv = [sys.executable, "-m", "amdgpu_operator", "operator", "--kubeconfig",
+                self._kubeconfig_for(self.namespace, "amd-gpu-operator"),
                 "--namespace", self.namespace, "--resync", str(self.operator_resync_s),
                 "--debounce", str(self.operator_debounce_s), "--health-port", "0"]
         with open(os.path.join(d, "log"), "w") as log_f:
@@ -837,7 +874,8 @@ class SimCluster:
             "DEVICE_PLUGIN_DIR": env.device_plugin_dir, "POD_RESOURCES_SOCKET": env.pod_resources_socket,
             "CDI_SPEC_DIR": env.cdi_dir, "CONTAINERD_CONFIG": env.containerd_config,
             "CRIO_CONFIG_DIR": env.crio_config_dir, "DOCKER_CONFIG": env.docker_config, "INSTALL_DIR": env.install_dir,
-            "OPERATOR_NAMESPACE": env.namespace, "VALIDATION_POLL_S": str(env.poll_s), "KUBECONFIG": self._kubeconfig,
+            "OPERATOR_NAMESPACE": env.namespace, "VALIDATION_POLL_S": str(env.poll_s),
+            "KUBECONFIG": self._kubeconfig_for(run.ns, run.pod["spec"].get("serviceAccountName") or "default"),
             "AMDGPU_READY_FILE": ready_file, "AMDGPU_SIM_NODE": "1", "AMDGPU_STARTUP_TRACE": ready_file + ".trace",
             "PYTHONPATH": os.pathsep.join([root] + [x for x in os.environ.get("PYTHONPATH", "").split(os.pathsep) if x])})
         if "kmod" in env.extra:

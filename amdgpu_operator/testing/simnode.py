@@ -27,6 +27,13 @@ def adopt_sim_node_env(env: NodeEnv) -> None:
 
         env.extra["kmod"] = fakesys.SimModule(env.host_root)
         env.extra["pci_backend"] = fakesys.FakePciKernel(env.host_root)
+        if sys.argv[1:2] == ["partition-manager"]:  # partition switches act on the fake tree too
+            from ..discovery import topology
+            from ..partition import manager as PM
+
+            gpus = len({g.physical_index for g in topology.enumerate_gpus(env.host_root)})
+            env.extra["partition_backend"] = PM.SysfsBackend(
+                env.host_root, PM.sysfs_partition_rebuilder(env.host_root, gpus), env.validations_dir)
     if e.get("AMDGPU_SIM_METRICS_FIXTURE"):
         env.extra["metrics_fixture"] = e["AMDGPU_SIM_METRICS_FIXTURE"]
     env.extra["ephemeral_ports"] = True
