@@ -112,6 +112,7 @@ class FakeApiServer:
         self._blobs: dict[tuple, bytes] = {}
         self.request_count = 0
         self.hooks: list = []  # callables(event_type, obj) run synchronously after commit
+        self.validators: list = []  # callables(obj) -> [errors], before a create/update commits (kube/validation.py)
         # Pods on a node stay Terminating until a zero-grace delete (see delete())
         self.graceful_pod_deletion = False
 
@@ -141,6 +142,11 @@ class FakeApiServer:
         b = self._blobs.get(k)
         return pickle.loads(b) if b is not None else R.deep(o)
 
+    def _validate(self, obj: dict) -> None:
+        errs = [e for v in self.validators for e in v(obj)]
+        if errs:
+            raise ApiError(422, "Invalid", f"{obj.get('kind')} {R.name_of(obj)!r} is invalid: " + "; ".join(errs))
+
     def _key(self, t: R.ResourceType, namespace, name) -> tuple:
         return (t.api_version, t.kind, namespace if t.namespaced else None, name)
 
@@ -159,6 +165,7 @@ class FakeApiServer:
             md["namespace"] = "default"
         if not t.namespaced:
             md.pop("namespace", None)
+        self._validate(obj)
         with self._lock:
             k = self._key(t, md.get("namespace"), md["name"])
             if k in self._store:
@@ -225,6 +232,7 @@ class FakeApiServer:
                 new["status"] = obj.get("status", {})
             else:
                 new = obj
+                self._validate(new)
                 # the main endpoint never changes status (status subresource semantics)
                 if "status" in cur:
                     new["status"] = self._out(k, cur)["status"]

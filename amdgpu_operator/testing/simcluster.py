@@ -263,6 +263,9 @@ class SimCluster:
         self.operator_debounce_s = operator_debounce_s
         self.launcher = launcher
         self.api = FakeApiServer()
+        from ..kube import validation
+
+        validation.install(self.api)  # objects kube-apiserver would reject fail here too
         self.api.graceful_pod_deletion = termination_s is not None
         self.api.hooks.append(self._trace_api)
         self.client = LocalClient(self.api)  # the simulated kubelets / controllers

@@ -118,3 +118,51 @@ def test_template_engine_subset(tmp_path):
     text = out["a.yaml"]
     assert "a: dflt" in text and "b: other" in text and 'c: "q\\"x"' in text
     assert "d:\n  k:\n  - 1\n  - 2" in text and "- 7\n- 8" in text and "e: true" in text
+
+
+@pytest.mark.parametrize("flags", [
+    [],
+    ["draDriver.enabled=true", "devicePlugin.enabled=false", "driver.rdma.enabled=true", "migManager.enabled=true",
+     "sandboxWorkloads.enabled=true", "dcgmExporter.serviceMonitor.enabled=true", "psa.enabled=true"],
+    ["daemonsets.inContainerGates=false", "validator.workload.prespawn=false", "driver.usePrecompiled=true"],
+])
+def test_every_object_passes_apiserver_validation(flags):
+    """What kube-apiserver would reject (kube/validation.py): every object the
+    chart renders and every object each operator state builds."""
+    from amdgpu_operator.controller import manifests as M
+    from amdgpu_operator.kube.validation import validate
+
+    objs = H.render_chart(set_flags=REFERENCE_SET_FLAGS + flags)
+    spec = spec_from_values(parse_set_flags(REFERENCE_SET_FLAGS + flags))
+    for builder in M.STATE_BUILDERS.values():
+        objs += builder(spec, "gpu-operator-resources", None)
+    objs += M.state_driver(spec, "gpu-operator-resources", None, kernel="6.8.0-45-generic")
+    bad = {f"{o['kind']}/{o['metadata']['name']}": validate(o) for o in objs if validate(o)}
+    assert not bad, bad
+    assert len(objs) > 30
+
+
+def test_validation_catches_what_the_apiserver_rejects():
+    from amdgpu_operator.kube.fakeapi import ApiError, FakeApiServer
+    from amdgpu_operator.kube.validation import install, validate
+
+    ds = {"apiVersion": "apps/v1", "kind": "DaemonSet",
+          "metadata": {"name": "x", "namespace": "default", "labels": {"amd.com/gpu.xgmi.hive": "a" * 64}},
+          "spec": {"selector": {"matchLabels": {"app": "x"}},
+                   "template": {"metadata": {"labels": {"app": "y"}},
+                                "spec": {"containers": [{"name": "Main", "image": "i",
+                                                         "ports": [{"name": "metrics-exporter-port", "containerPort": 9400}],
+                                                         "volumeMounts": [{"name": "gone", "mountPath": "/x"}],
+                                                         "env": [{"name": "1BAD", "value": "v"}]}],
+                                         "volumes": [{"name": "h", "hostPath": {"path": "/h", "type": "Dir"}}],
+                                         "tolerations": [{"key": "k", "operator": "Exists", "value": "v"}]}}}}
+    errs = " | ".join(validate(ds))
+    for want in ("not a valid label value", "do not match spec.selector", "'Main': not a DNS-1123 label",
+                 "not a valid port name", "no volume of that name", "not a valid environment variable name",
+                 "hostPath.type 'Dir'", "operator Exists takes no value"):
+        assert want in errs, (want, errs)
+    api = FakeApiServer()
+    install(api)
+    with pytest.raises(ApiError) as e:
+        api.create(ds)
+    assert e.value.code == 422
