@@ -190,6 +190,43 @@ def validate(obj: dict) -> list[str]:
     return errs
 
 
+def schema_errors(value, schema: dict, path: str = "") -> list[str]:
+    """A CR against its CRD's structural openAPIV3Schema, as the apiserver
+    checks it: types, enums, required, nested properties and items; fields
+    the schema does not know are errors too (the apiserver would prune them
+    silently - the operator would never see the value it was given)."""
+    errs: list[str] = []
+    t = schema.get("type")
+    if value is None:
+        return [] if schema.get("nullable") else [f"{path or '.'}: null"]
+    ok = {"object": isinstance(value, dict), "array": isinstance(value, list), "string": isinstance(value, str),
+          "boolean": isinstance(value, bool), "integer": isinstance(value, int) and not isinstance(value, bool),
+          "number": isinstance(value, (int, float)) and not isinstance(value, bool)}.get(t, True)
+    if schema.get("x-kubernetes-int-or-string"):
+        ok = isinstance(value, (int, str)) and not isinstance(value, bool)
+    if not ok:
+        return [f"{path or '.'}: {type(value).__name__} where the schema has {t}"]
+    if "enum" in schema and value not in schema["enum"]:
+        errs.append(f"{path}: {value!r} not in {schema['enum']}")
+    if isinstance(value, dict) and not schema.get("x-kubernetes-preserve-unknown-fields"):
+        props = schema.get("properties")
+        addl = schema.get("additionalProperties")
+        for k in schema.get("required") or []:
+            if k not in value:
+                errs.append(f"{path}.{k}: required")
+        for k, v in value.items():
+            if props is not None and k in props:
+                errs += schema_errors(v, props[k], f"{path}.{k}")
+            elif isinstance(addl, dict):
+                errs += schema_errors(v, addl, f"{path}.{k}")
+            elif props is not None or addl is False:
+                errs.append(f"{path}.{k}: unknown field")
+    if isinstance(value, list) and isinstance(schema.get("items"), dict):
+        for i, v in enumerate(value):
+            errs += schema_errors(v, schema["items"], f"{path}[{i}]")
+    return errs
+
+
 def install(api) -> None:
     """Validate every create and update of ``api`` (a FakeApiServer)."""
     api.validators.append(validate)

@@ -166,3 +166,21 @@ def test_validation_catches_what_the_apiserver_rejects():
     with pytest.raises(ApiError) as e:
         api.create(ds)
     assert e.value.code == 422
+
+
+@pytest.mark.parametrize("flags", [
+    [],
+    ["draDriver.enabled=true", "devicePlugin.enabled=false", "driver.rdma.enabled=true", "migManager.enabled=true",
+     "sandboxWorkloads.enabled=true", "daemonsets.maxUnavailable=25%", "validator.workload.gemmN=8192"],
+])
+def test_rendered_cluster_policy_matches_the_crd_schema(flags):
+    """The CR `helm install` creates passes the CRD's structural schema
+    (types, enums, no field the schema would prune)."""
+    from amdgpu_operator.kube.validation import schema_errors
+
+    docs = H.render_chart(set_flags=REFERENCE_SET_FLAGS + flags)
+    cp = next(d for d in docs if d["kind"] == "ClusterPolicy")
+    crd = next(d for d in docs if d["kind"] == "CustomResourceDefinition" and d["spec"]["names"]["kind"] == "ClusterPolicy")
+    schema = crd["spec"]["versions"][0]["schema"]["openAPIV3Schema"]
+    assert not schema_errors({k: v for k, v in cp.items() if k in ("spec",)}, {
+        "type": "object", "properties": {"spec": schema["properties"]["spec"]}}), cp["spec"]
