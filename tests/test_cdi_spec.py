@@ -1,0 +1,103 @@
+"""CDI specs the operator writes, checked against the CDI specification's
+rules [EXT: cncf-tags/container-device-interface SPEC.md, v0.6.0] that
+containerd/CRI-O enforce when they load a spec directory: a spec that breaks
+them is skipped by the runtime and its devices cannot be injected.
+
+Producers: the toolkit's node-wide spec (``amd.com/gpu``, the native OCI
+hook's ``cdi`` mode, toolkit/install.py) and the DRA driver's per-claim specs
+(``gpu.amd.com/claim``, dra/driver.py)."""
+
+import json
+import os
+import re
+
+import pytest
+
+from amdgpu_operator.nodeenv import NodeEnv
+from amdgpu_operator.testing import fakesys
+
+_NAME = re.compile(r"[A-Za-z0-9][A-Za-z0-9_.-]*")
+_DEVICE = re.compile(r"[A-Za-z0-9][A-Za-z0-9_.:-]*")
+_SEMVER = re.compile(r"\d+\.\d+\.\d+")
+
+
+def cdi_errors(spec: dict) -> list[str]:
+    errs = []
+    if not _SEMVER.fullmatch(str(spec.get("cdiVersion", ""))):
+        errs.append(f"cdiVersion {spec.get('cdiVersion')!r}")
+    vendor, _, cls = str(spec.get("kind", "")).partition("/")
+    if not (vendor and cls and _NAME.fullmatch(vendor) and _NAME.fullmatch(cls)):
+        errs.append(f"kind {spec.get('kind')!r} is not vendor/class")
+    devices = spec.get("devices") or []
+    if not devices:
+        errs.append("no devices")
+    names = [d.get("name", "") for d in devices]
+    errs += [f"device name {n!r}" for n in names if not _DEVICE.fullmatch(n)]
+    if len(set(names)) != len(names):
+        errs.append("duplicate device names")
+
+    def edits(e, where):
+        for dn in e.get("deviceNodes") or []:
+            if not str(dn.get("path", "")).startswith("/"):
+                errs.append(f"{where}: device node path {dn.get('path')!r}")
+            if dn.get("type") not in (None, "b", "c", "u", "p"):
+                errs.append(f"{where}: device node type {dn.get('type')!r}")
+            if dn.get("permissions") is not None and not re.fullmatch(r"[rwm]+", dn["permissions"]):
+                errs.append(f"{where}: permissions {dn['permissions']!r}")
+        for env in e.get("env") or []:
+            if "=" not in env or env.startswith("="):
+                errs.append(f"{where}: env {env!r} is not KEY=VALUE")
+        for m in e.get("mounts") or []:
+            if not str(m.get("containerPath", "")).startswith("/") or not m.get("hostPath"):
+                errs.append(f"{where}: mount {m}")
+        for h in e.get("hooks") or []:
+            if h.get("hookName") not in ("prestart", "createRuntime", "createContainer", "startContainer",
+                                         "poststart", "poststop") or not h.get("path"):
+                errs.append(f"{where}: hook {h}")
+
+    edits(spec.get("containerEdits") or {}, "containerEdits")
+    for d in devices:
+        if not d.get("containerEdits"):
+            errs.append(f"device {d.get('name')!r}: containerEdits required")
+        edits(d.get("containerEdits") or {}, f"device {d.get('name')!r}")
+    return errs
+
+
+@pytest.mark.parametrize("partition", ["SPX", "CPX"])
+def test_toolkit_spec_is_valid_cdi(tmp_path, partition):
+    from amdgpu_operator.toolkit.install import generate_cdi
+
+    root = str(tmp_path / "h")
+    fakesys.build_node(root, 8, compute_partition=partition)
+    env = NodeEnv("n", None, host_root=root)
+    path = generate_cdi(env, str(tmp_path / "cdi" / "amd.com-gpu.json"))
+    with open(path) as f:
+        spec = json.load(f)
+    assert not cdi_errors(spec), cdi_errors(spec)
+    assert spec["kind"] == "amd.com/gpu" and len(spec["devices"]) >= (8 if partition == "SPX" else 64)
+
+
+def test_dra_claim_spec_is_valid_cdi(tmp_path):
+    from amdgpu_operator.dra.driver import DraDriver
+
+    root = str(tmp_path / "h")
+    fakesys.build_node(root, 4)
+    env = NodeEnv("n", None, host_root=root, cdi_dir=str(tmp_path / "cdi"),
+                  device_plugin_dir=str(tmp_path / "k" / "device-plugins"))
+    drv = DraDriver(env)
+    ids = drv._write_cdi("0b4f6a3e-59d1-4c1d-b8f1-1e2a3b4c5d6e", ["gpu-0", "gpu-3"])
+    with open(drv.cdi_path("0b4f6a3e-59d1-4c1d-b8f1-1e2a3b4c5d6e")) as f:
+        spec = json.load(f)
+    assert not cdi_errors(spec), cdi_errors(spec)
+    # the fully-qualified names the kubelet hands the runtime resolve to devices of the spec
+    assert all(i.split("=", 1)[0] == spec["kind"] and i.split("=", 1)[1] in {d["name"] for d in spec["devices"]}
+               for i in ids)
+    assert os.path.basename(drv.cdi_path("x")).endswith(".json")
+
+
+def test_checker_rejects_broken_specs():
+    bad = {"cdiVersion": "0.6", "kind": "amd.com", "devices": [{"name": "-x", "containerEdits": {
+        "deviceNodes": [{"path": "dev/kfd", "permissions": "rwx"}], "env": ["=1"]}}]}
+    errs = " | ".join(cdi_errors(bad))
+    for want in ("cdiVersion", "not vendor/class", "device name '-x'", "device node path", "permissions", "env"):
+        assert want in errs, (want, errs)
