@@ -101,3 +101,28 @@ def test_checker_rejects_broken_specs():
     errs = " | ".join(cdi_errors(bad))
     for want in ("cdiVersion", "not vendor/class", "device name '-x'", "device node path", "permissions", "env"):
         assert want in errs, (want, errs)
+
+
+def test_runtime_dropins_are_valid_toml_with_the_keys_the_runtimes_read():
+    """containerd (config version 2, the reference's `containerd config
+    default`, README.md:15-17) and CRI-O read these files as TOML; a syntax
+    error makes the runtime refuse to start."""
+    import tomli
+
+    from amdgpu_operator.toolkit import install as TK
+
+    for default in (False, True):
+        d = tomli.loads(TK.dropin_config("amd", "/usr/local/amd/amdgpu-oci-hook", "/var/run/cdi", ["--x"], default))
+        cri = d["plugins"]["io.containerd.grpc.v1.cri"]
+        assert d["version"] == 2 and cri["enable_cdi"] is True and "/var/run/cdi" in cri["cdi_spec_dirs"]
+        rt = cri["containerd"]["runtimes"]["amd"]
+        assert rt["runtime_type"] == "io.containerd.runc.v2" and rt["options"]["SystemdCgroup"] is True
+        assert (cri["containerd"].get("default_runtime_name") == "amd") == default
+    main = ('version = 2\n[plugins."io.containerd.grpc.v1.cri".containerd.runtimes.runc.options]\n'
+            "  SystemdCgroup = true\n")
+    patched = tomli.loads(TK.patch_containerd_config(main, "/etc/containerd/conf.d/99-amd.toml"))
+    assert patched["imports"] == ["/etc/containerd/conf.d/99-amd.toml"]
+    assert patched["plugins"]["io.containerd.grpc.v1.cri"]["containerd"]["runtimes"]["runc"]["options"]["SystemdCgroup"]
+    for hooks in (None, "/usr/local/amd/oci-hooks-prestart.d"):
+        c = tomli.loads(TK.crio_dropin("/var/run/cdi", hooks))["crio"]["runtime"]
+        assert "/var/run/cdi" in c["cdi_spec_dirs"] and (("hooks_dir" in c) == bool(hooks))
