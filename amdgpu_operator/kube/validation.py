@@ -133,6 +133,15 @@ def pod_spec(spec: dict, path: str, errs: list[str], in_template: bool = False, 
                     errs.append(f"{cp}.env[{j}].name {en!r}: not a valid environment variable name")
                 if "value" in e and "valueFrom" in e:
                     errs.append(f"{cp}.env[{j}]: value and valueFrom are exclusive")
+            res = c.get("resources") or {}
+            for rname, lim in (res.get("limits") or {}).items():
+                if "/" in rname and not rname.startswith(("kubernetes.io/", "requests.")):  # an extended resource
+                    req = (res.get("requests") or {}).get(rname, lim)
+                    if str(req) != str(lim):
+                        errs.append(f"{cp}.resources: extended resource {rname} must request what it limits "
+                                    f"({req} != {lim})")
+                    if not str(lim).isdigit():
+                        errs.append(f"{cp}.resources.limits[{rname}] {lim!r}: must be a whole number")
             for j, rc in enumerate(((c.get("resources") or {}).get("claims")) or []):
                 if rc.get("name") not in claims:
                     errs.append(f"{cp}.resources.claims[{j}] {rc.get('name')!r}: not in spec.resourceClaims")
@@ -177,6 +186,16 @@ def validate(obj: dict) -> list[str]:
                 errs.append("spec.selector: required")
             elif any(tl.get(k) != v for k, v in sel.items()):
                 errs.append(f"spec.template.metadata.labels: do not match spec.selector {sel}")
+    elif kind == "Service":
+        ports = spec.get("ports") or []
+        pnames = [p.get("name") for p in ports]
+        if len(ports) > 1 and (None in pnames or len(set(pnames)) != len(pnames)):
+            errs.append("spec.ports: several ports need distinct names")
+        for i, p in enumerate(ports):
+            if not 0 < int(p.get("port", 0)) < 65536:
+                errs.append(f"spec.ports[{i}].port {p.get('port')!r} out of range")
+            if p.get("name") and not _port_name(p["name"]) and not _dns_label(p["name"]):
+                errs.append(f"spec.ports[{i}].name {p['name']!r}")
     elif kind in ("ClusterRole", "Role"):
         for i, r in enumerate(obj.get("rules") or []):
             if not r.get("verbs"):
