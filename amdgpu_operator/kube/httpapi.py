@@ -66,10 +66,14 @@ class _Handler(BaseHTTPRequestHandler):
                             "message": e.message, "code": e.code})
 
     def _body(self) -> dict:
-        n = int(self.headers.get("Content-Length") or 0)
-        return json.loads(self.rfile.read(n) or b"{}")
+        return json.loads(self._raw or b"{}")
 
     def _dispatch(self, method: str) -> None:
+        # the body is read before anything can fail: an error answered with
+        # the body still unread would leave it in the kept-alive connection,
+        # where it becomes the next request's request line
+        n = int(self.headers.get("Content-Length") or 0)
+        self._raw = self.rfile.read(n) if n else b""
         u = urlparse(self.path)
         q = {k: v[-1] for k, v in parse_qs(u.query).items()}
         try:

@@ -71,7 +71,7 @@ def gemm_gate_passed(record: dict) -> bool:
 
 
 def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: bool = False,
-             real_gpu: bool = False, inject_noop: int = -1, processes: bool = False) -> bool:
+             real_gpu: bool = False, inject_noop: int = -1, processes: bool = False, rbac: bool = False) -> bool:
     rnd = random.Random(seed)
     d = tempfile.mkdtemp(prefix="chaos-")
     if real_gpu:  # one node, this machine's GPU(s): every validation runs on the real device
@@ -84,7 +84,7 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
         nodes, gpu_nodes = [NodeSpec("g0", 2), NodeSpec("g1", 2), NodeSpec("cpu", 0)], ["g0", "g1"]
     c = SimCluster(os.path.join(d, "c"), nodes, fake_gpu=not real_gpu,
                    poll_s=0.005, agent_poll_s=0.05, termination_s=0.0,  # kubelet-confirmed pod deletes
-                   http_api=http_api, process_containers=processes).start()
+                   http_api=http_api, process_containers=processes, rbac=rbac).start()
     mode = {n: "container" for n in gpu_nodes}
     cpx = {n: False for n in gpu_nodes}
     from amdgpu_operator.partition import manager as PM
@@ -208,6 +208,10 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
             reval = " ".join(f"{n} revalidated +{validation_record(c, n)['time'] - t_fault:.2f} s" for n in sorted(must))
             print(f"seed {seed} step {i} {fault} {node} {info}: ready {time.time() - t0:.2f} s after settling"
                   + (f"; {reval}" if reval else ""), flush=True)
+        if rbac and c._http.denied:  # a request the shipped roles do not grant (kube/rbac.py)
+            for d in sorted(set(c._http.denied)):
+                print(f"seed {seed}: RBAC denied {d}", flush=True)
+            return False
         return True
     finally:
         c.stop()
@@ -223,14 +227,15 @@ def main() -> int:
     ap.add_argument("--real-gpu", action="store_true", help="one node on this machine's GPUs (pod/kubelet/spec faults)")
     ap.add_argument("--processes", action="store_true",
                     help="the operator and every operand container as its own process (bench.py's headline mode)")
+    ap.add_argument("--rbac", action="store_true",
+                    help="with --processes: every request authorized against the shipped roles (kube/rbac.py)")
     ap.add_argument("--inject-noop", type=int, default=-1, metavar="STEP",
                     help="make step STEP a no-op fault that claims a revalidation (the harness must fail)")
     a = ap.parse_args()
-    if a.processes and not a.real_gpu:
-        # the fake cluster's partition and PCI backends live in this process (env.extra), out of an operand process's reach
-        ap.error("--processes needs --real-gpu")
+    if a.rbac and not a.processes:
+        ap.error("--rbac needs --processes (a ServiceAccount per operand process)")
     lo, _, hi = a.seeds.partition("-")
-    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api, a.real_gpu, a.inject_noop, a.processes)
+    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api, a.real_gpu, a.inject_noop, a.processes, a.rbac)
               for s in range(int(lo), int(hi or lo) + 1)])
     return 0 if ok else 1
 
