@@ -449,7 +449,8 @@ def state_dra_driver(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
                      [_mount("kubelet-plugins", "/var/lib/kubelet/plugins"),
                       _mount("kubelet-registry", "/var/lib/kubelet/plugins_registry"),
                       _mount("cdi-dir", spec.toolkit.cdi.specDir), *_host_view()],
-                     list(d.env), True, d.resources.model_dump())
+                     [{"name": "CDI_SPEC_DIR", "value": spec.toolkit.cdi.specDir}, *d.env], True,
+                     d.resources.model_dump())
     inits = _gate(spec, ctr, _wait_init("driver-validation", image, d.imagePullPolicy, "driver"), "driver")
     vols = [_hostpath("kubelet-plugins", "/var/lib/kubelet/plugins"),
             _hostpath("kubelet-registry", "/var/lib/kubelet/plugins_registry"),
