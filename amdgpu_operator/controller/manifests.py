@@ -451,7 +451,9 @@ def state_dra_driver(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
                       _mount("cdi-dir", spec.toolkit.cdi.specDir), *_host_view()],
                      [{"name": "CDI_SPEC_DIR", "value": spec.toolkit.cdi.specDir}, *d.env], True,
                      d.resources.model_dump())
-    inits = _gate(spec, ctr, _wait_init("driver-validation", image, d.imagePullPolicy, "driver"), "driver")
+    # claims are injected as CDI devices: the runtime must have CDI on (the toolkit) before devices are published
+    gate = "toolkit" if spec.toolkit.enabled else "driver"
+    inits = _gate(spec, ctr, _wait_init("toolkit-validation", image, d.imagePullPolicy, gate), gate)
     vols = [_hostpath("kubelet-plugins", "/var/lib/kubelet/plugins"),
             _hostpath("kubelet-registry", "/var/lib/kubelet/plugins_registry"),
             _hostpath("cdi-dir", spec.toolkit.cdi.specDir), _hostpath("host-sys", "/sys", "Directory"),

@@ -559,7 +559,7 @@ def test_in_container_gates_replace_the_init_containers():
                     gates[c["name"]] = env["VALIDATION_GATE"]
     assert gates == {"amd-container-toolkit-ctr": "driver", "amd-device-plugin": "toolkit",
                      "amd-metrics-exporter": "driver", "gpu-feature-discovery": "driver", "amd-partition-manager": "driver",
-                     "amd-dra-driver": "driver"}  # the DRA driver's DaemonSet is built whether or not it is enabled
+                     "amd-dra-driver": "toolkit"}  # the DRA driver's DaemonSet is built whether or not it is enabled
     drv = [o for o in M.state_driver(spec, "ns", None) if o["kind"] == "DaemonSet"][0]
     ctr = drv["spec"]["template"]["spec"]["containers"][0]
     assert ctr["args"][:3] == ["driver", "install", "--prepare-upgrade"]
