@@ -49,6 +49,10 @@ _DRA_SERVICES = {
 dra = build_file("k8s.io.kubelet.pkg.apis.dra.v1beta1", _DRA_MESSAGES)
 DRA_SERVICE = "k8s.io.kubelet.pkg.apis.dra.v1beta1.DRAPlugin"
 DRA_METHODS = {name: (dra[i], dra[o], s) for name, i, o, s in _DRA_SERVICES["DRAPlugin"]}
+# Kubernetes 1.31's kubelet speaks the same messages as service v1alpha4.Node;
+# the driver serves both and advertises both versions (the kubelet picks)
+DRA_SERVICE_V1ALPHA4 = "k8s.io.kubelet.pkg.apis.dra.v1alpha4.Node"
+DRA_VERSIONS = [DRA_VERSION, "v1alpha4.Node"]
 
 _REG_MESSAGES = {
     "InfoRequest": [],

@@ -247,7 +247,7 @@ class DraDriver:
 
     def GetInfo(self, request, context):
         return api.reg["PluginInfo"](type=api.PLUGIN_TYPE, name=api.DRIVER_NAME, endpoint=self.endpoint,
-                                     supported_versions=[api.DRA_VERSION])
+                                     supported_versions=list(api.DRA_VERSIONS))
 
     def NotifyRegistrationStatus(self, request, context):
         self.registration_error = request.error
@@ -261,13 +261,13 @@ class DraDriver:
     def serve(self) -> None:
         """DRA endpoint first, then the registration socket the kubelet's
         plugin watcher picks up (it dials the endpoint right after GetInfo)."""
-        for path, service, methods in ((self.endpoint, api.DRA_SERVICE, api.DRA_METHODS),
-                                       (self.registry_socket, api.REGISTRATION_SERVICE, api.REGISTRATION_METHODS)):
+        for path, services, methods in ((self.endpoint, (api.DRA_SERVICE, api.DRA_SERVICE_V1ALPHA4), api.DRA_METHODS),
+                                        (self.registry_socket, (api.REGISTRATION_SERVICE,), api.REGISTRATION_METHODS)):
             os.makedirs(os.path.dirname(path), exist_ok=True)
             wire.remove_socket(path)
-            srv = wire.Server({api.method_path(service, n): wire.MethodHandler(getattr(self, n), i.FromString,
-                                                                               o.SerializeToString, s)
-                               for n, (i, o, s) in methods.items()}, name="amdgpu-dra")
+            srv = wire.Server({api.method_path(svc, n): wire.MethodHandler(getattr(self, n), i.FromString,
+                                                                           o.SerializeToString, s)
+                               for svc in services for n, (i, o, s) in methods.items()}, name="amdgpu-dra")
             srv.add_unix(path)
             srv.start()
             self._servers.append(srv)

@@ -154,6 +154,9 @@ def test_grpcio_kubelet_calls_the_dra_endpoint(node):
         call = ch.unary_unary(api.method_path(api.DRA_SERVICE, "NodePrepareResources"),
                               request_serializer=ipb.SerializeToString, response_deserializer=opb.FromString)
         resp = call(req, timeout=5)
+        old = ch.unary_unary(api.method_path(api.DRA_SERVICE_V1ALPHA4, "NodePrepareResources"),
+                             request_serializer=ipb.SerializeToString, response_deserializer=opb.FromString)
+        assert not old(req, timeout=5).claims[claim["metadata"]["uid"]].error  # a 1.31 kubelet's service name
     got = resp.claims[claim["metadata"]["uid"]]  # a real proto3 map on the google.protobuf side
     assert not got.error and got.devices[0].pool_name == "n1" and got.devices[0].cdi_device_ids[0].startswith(
         "gpu.amd.com/claim=")
