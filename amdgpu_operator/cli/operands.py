@@ -539,7 +539,8 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             if cmd == "nfd":
                 from ..wellknown import NFD_SCANNED_ANN
 
-                L.sync_node_labels(env.client, env.node_name, L.nfd_labels(env.sysfs_root()), (L.NFD_PREFIX + "pci-",),
+                L.sync_node_labels(env.client, env.node_name, L.nfd_labels(env.sysfs_root()),
+                                   (L.NFD_PREFIX + "pci-", L.NFD_PREFIX + "rdma."),
                                    {NFD_SCANNED_ANN: "true"})
             else:
                 gpus = topology.enumerate_gpus(env.sysfs_root())

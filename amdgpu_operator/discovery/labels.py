@@ -84,6 +84,14 @@ def nfd_labels(root: str = "/") -> dict[str, str]:
             labels[f"{NFD_PREFIX}pci-{AMD_VENDOR}.present"] = "true"
     if _read(_root_join(root, "sys/module/amdgpu/initstate")) == "live":
         labels[f"{NFD_PREFIX}kernel-loadedmodule.amdgpu"] = "true"
+    # NFD's rdma feature: an RDMA device present / the user-space RDMA modules loaded
+    try:
+        if os.listdir(_root_join(root, "sys/class/infiniband")):
+            labels[f"{NFD_PREFIX}rdma.capable"] = "true"
+    except OSError:
+        pass
+    if all(os.path.isdir(_root_join(root, f"sys/module/{m}")) for m in ("ib_uverbs", "rdma_ucm")):
+        labels[f"{NFD_PREFIX}rdma.available"] = "true"
     # a container shares the node's kernel: its own uname is the node's
     ver = _read(_root_join(root, "proc/sys/kernel/osrelease")) or os.uname().release
     if ver:

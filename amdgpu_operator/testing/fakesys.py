@@ -233,7 +233,7 @@ def add_rdma_nics(root: str, gpus: list[FakeGpu], link_layer: str = "Ethernet", 
         _w(f"{root}/dev/infiniband/uverbs{i}", "")
         names.append(nm)
     if modules:
-        for m in ("ib_core", "ib_uverbs"):
+        for m in ("ib_core", "ib_uverbs", "rdma_ucm"):
             _w(f"{root}/sys/module/{m}/initstate", "live\n")
     return names
 

@@ -14,6 +14,7 @@
 //   feature.node.kubernetes.io/pci-1002.present              = true  (AMD display / accelerator)
 //   feature.node.kubernetes.io/kernel-loadedmodule.amdgpu    = true  (module live)
 //   feature.node.kubernetes.io/kernel-version.full           = <release>
+//   feature.node.kubernetes.io/rdma.capable / rdma.available  = true  (RDMA device / ib_uverbs + rdma_ucm)
 //
 // then GET the Node, and PATCH (merge patch) only what differs: new labels,
 // stale ones it owns (pci-*, the amdgpu module label) removed, and the
@@ -37,6 +38,7 @@
 #include <poll.h>
 #include <signal.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/utsname.h>
 #include <time.h>
 #include <unistd.h>
@@ -150,6 +152,18 @@ std::map<std::string, std::string> scan(const std::string& root) {
   std::string state;
   if (read_file(join(root, "sys/module/amdgpu/initstate"), &state) && trim(state) == "live")
     labels[std::string(kPrefix) + "kernel-loadedmodule.amdgpu"] = "true";
+  // NFD's rdma feature: an RDMA device present / the user-space RDMA modules loaded
+  if (DIR* d = opendir(join(root, "sys/class/infiniband").c_str())) {
+    bool any = false;
+    while (dirent* e = readdir(d))
+      if (e->d_name[0] != '.') any = true;
+    closedir(d);
+    if (any) labels[std::string(kPrefix) + "rdma.capable"] = "true";
+  }
+  struct stat st;
+  if (stat(join(root, "sys/module/ib_uverbs").c_str(), &st) == 0 && S_ISDIR(st.st_mode) &&
+      stat(join(root, "sys/module/rdma_ucm").c_str(), &st) == 0 && S_ISDIR(st.st_mode))
+    labels[std::string(kPrefix) + "rdma.available"] = "true";
   std::string rel;
   if (!read_file(join(root, "proc/sys/kernel/osrelease"), &rel) || trim(rel).empty()) {
     struct utsname u;  // a container shares the node's kernel
@@ -162,7 +176,7 @@ std::map<std::string, std::string> scan(const std::string& root) {
 
 bool owned(const std::string& key) {
   const std::string p(kPrefix);
-  return key.rfind(p + "pci-", 0) == 0 || key == p + "kernel-loadedmodule.amdgpu";
+  return key.rfind(p + "pci-", 0) == 0 || key == p + "kernel-loadedmodule.amdgpu" || key.rfind(p + "rdma.", 0) == 0;
 }
 
 // ---------------------------------------------------------------- API access

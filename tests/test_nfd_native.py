@@ -31,9 +31,12 @@ def _print(root):
     return json.loads(p.stdout)
 
 
-@pytest.mark.parametrize("kind", ["synthetic", "mi355x-capture"])
+@pytest.mark.parametrize("kind", ["synthetic", "mi355x-capture", "rdma"])
 def test_labels_match_the_python_worker(tmp_path, kind):
     root = str(tmp_path / "host")
+    if kind == "rdma":
+        fakesys.add_rdma_nics(root, fakesys.build_node(root, 4, pcie_tree=True))
+        assert L.nfd_labels(root)[P + "rdma.capable"] == L.nfd_labels(root)[P + "rdma.available"] == "true"
     if kind == "synthetic":
         fakesys.build_node(root, 4, kernel="6.8.0-45-generic")
     else:
