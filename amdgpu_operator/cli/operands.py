@@ -474,7 +474,13 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                 source = FixtureSource(fx)
         from ..exporter.metrics import parse_metrics_csv
 
-        attribution = PodAttribution(env.pod_resources_socket) if a.pod_attribution else None
+        attribution = None
+        if a.pod_attribution:
+            from ..dra.api import DRIVER_NAME
+            from ..exporter.metrics import dra_device_ids
+
+            attribution = PodAttribution(env.pod_resources_socket, dra_driver=DRIVER_NAME,
+                                         resolve=dra_device_ids(env.sysfs_root()))
         selection = None
         csv_text = None
         if a.metrics_config:

@@ -79,7 +79,17 @@ _PR_MESSAGES = {
     "PodResources": [("name", 1, "string", "opt"), ("namespace", 2, "string", "opt"),
                      ("containers", 3, "ContainerResources", "rep")],
     "ContainerResources": [("name", 1, "string", "opt"), ("devices", 2, "ContainerDevices", "rep"),
-                           ("cpu_ids", 3, "int64", "rep")],
+                           ("cpu_ids", 3, "int64", "rep"), ("memory", 4, "ContainerMemory", "rep"),
+                           ("dynamic_resources", 5, "DynamicResource", "rep")],
+    "ContainerMemory": [("memory_type", 1, "string", "opt"), ("size", 2, "uint64", "opt"),
+                        ("topology", 3, "TopologyInfo", "opt")],
+    # DRA claims prepared for the container (kubelet >= 1.27 behind the
+    # KubeletPodResourcesDynamicResources gate; driver/pool/device since 1.31)
+    "DynamicResource": [("class_name", 1, "string", "opt"), ("claim_name", 2, "string", "opt"),
+                        ("claim_namespace", 3, "string", "opt"), ("claim_resources", 4, "ClaimResource", "rep")],
+    "ClaimResource": [("cdi_devices", 1, "CDIDevice", "rep"), ("driver_name", 2, "string", "opt"),
+                      ("pool_name", 3, "string", "opt"), ("device_name", 4, "string", "opt")],
+    "CDIDevice": [("name", 1, "string", "opt")],
     "ContainerDevices": [("resource_name", 1, "string", "opt"), ("device_ids", 2, "string", "rep"),
                          ("topology", 3, "TopologyInfo", "opt")],
     "TopologyInfo": [("nodes", 1, "NUMANode", "rep")],

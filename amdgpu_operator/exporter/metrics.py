@@ -237,11 +237,19 @@ class SmiSource:
 
 
 class PodAttribution:
-    """Maps device IDs (PCI BDF[-pN]) to pods via the kubelet pod-resources API."""
+    """Maps device IDs (PCI BDF[-pN]) to pods via the kubelet pod-resources API.
 
-    def __init__(self, socket_path: str, resource_prefix: str = "amd.com/gpu"):
+    Device-plugin allocations arrive as ``devices`` (the plugin's IDs);
+    DRA allocations as ``dynamic_resources`` (claim -> driver/pool/device,
+    kubelet >= 1.31), whose device names (``gpu-<index>``, dra/driver.py)
+    ``resolve`` turns into the same BDF[-pN] IDs."""
+
+    def __init__(self, socket_path: str, resource_prefix: str = "amd.com/gpu", dra_driver: str = "",
+                 resolve=None):
         self.socket_path = socket_path
         self.prefix = resource_prefix
+        self.dra_driver = dra_driver
+        self.resolve = resolve  # DRA device name -> device ID (None: the name itself)
 
     def lookup(self) -> dict[str, dict]:
         from ..deviceplugin import api
@@ -257,12 +265,39 @@ class PodAttribution:
         m: dict[str, dict] = {}
         for pr in out.pod_resources:
             for c in pr.containers:
+                who = {"namespace": pr.namespace, "pod": pr.name, "container": c.name}
                 for d in c.devices:
                     if not d.resource_name.startswith(self.prefix):
                         continue
                     for dev in d.device_ids:
-                        m[dev] = {"namespace": pr.namespace, "pod": pr.name, "container": c.name}
+                        m[dev] = who
+                if not self.dra_driver:
+                    continue
+                for dr in c.dynamic_resources:
+                    for cr in dr.claim_resources:
+                        if cr.driver_name == self.dra_driver and cr.device_name:
+                            key = self.resolve(cr.device_name) if self.resolve else cr.device_name
+                            if key:
+                                m[key] = who
         return m
+
+
+def dra_device_ids(sysfs_root: str):
+    """``resolve`` for :class:`PodAttribution`: DRA device name -> BDF[-pN],
+    re-read from the KFD topology when a name is unknown (partitions
+    change the device set)."""
+    from ..discovery import topology
+    from ..dra.driver import device_name
+
+    cache: dict[str, str] = {}
+
+    def resolve(name: str) -> str | None:
+        if name not in cache:
+            cache.clear()
+            cache.update({device_name(g): g.device_id_str for g in topology.enumerate_gpus(sysfs_root)})
+        return cache.get(name)
+
+    return resolve
 
 
 class MetricsExporter:

@@ -51,6 +51,9 @@ class FakeKubelet:
         self.podres_sock = pod_resources_socket
         self.resources: dict[str, _Resource] = {}
         self.assignments: dict[tuple[str, str, str], tuple[str, list[str]]] = {}  # (ns,pod,ctr) -> (res, ids)
+        # (ns,pod,ctr) -> DRA claims the DRA manager prepared for it:
+        # [{"claim": (ns, name), "resources": [(driver, pool, device, [cdi ids])]}]
+        self.claims: dict[tuple[str, str, str], list[dict]] = {}
         self.register_calls = 0
         self.register_seconds: list[float] = []  # handler time per Register call
         self.register_walls: list[float] = []  # wall time each Register call arrived
@@ -166,13 +169,27 @@ class FakeKubelet:
         pods: dict[tuple[str, str], object] = {}
         with self._lock:
             items = list(self.assignments.items())
+            claims = dict(self.claims)
+        ctrs: dict[tuple[str, str, str], object] = {}
+
+        def container(ns, pod, ctr):
+            if (ns, pod, ctr) not in ctrs:
+                pr = pods.get((ns, pod))
+                if pr is None:
+                    pr = pods[(ns, pod)] = out.pod_resources.add(name=pod, namespace=ns)
+                ctrs[(ns, pod, ctr)] = pr.containers.add(name=ctr)
+            return ctrs[(ns, pod, ctr)]
+
         for (ns, pod, ctr), (res, ids) in items:
-            pr = pods.get((ns, pod))
-            if pr is None:
-                pr = out.pod_resources.add(name=pod, namespace=ns)
-                pods[(ns, pod)] = pr
-            c = pr.containers.add(name=ctr)
-            c.devices.add(resource_name=res, device_ids=ids)
+            container(ns, pod, ctr).devices.add(resource_name=res, device_ids=ids)
+        for (ns, pod, ctr), held in claims.items():
+            c = container(ns, pod, ctr)
+            for h in held:
+                dr = c.dynamic_resources.add(claim_namespace=h["claim"][0], claim_name=h["claim"][1])
+                for drv, pool, dev, cdi in h["resources"]:
+                    cr = dr.claim_resources.add(driver_name=drv, pool_name=pool, device_name=dev)
+                    for n in cdi:
+                        cr.cdi_devices.add(name=n)
         return out
 
     def _podres_allocatable(self, request, context):
@@ -291,3 +308,11 @@ class FakeKubelet:
         with self._lock:
             for k in [k for k in self.assignments if k[0] == namespace and k[1] == pod]:
                 del self.assignments[k]
+            for k in [k for k in self.claims if k[0] == namespace and k[1] == pod]:
+                del self.claims[k]
+
+    def record_claims(self, namespace: str, pod: str, container: str, held: list[dict]) -> None:
+        """The DRA manager prepared ``held`` for this container (what
+        pod-resources List reports as its dynamic_resources)."""
+        with self._lock:
+            self.claims[(namespace, pod, container)] = held

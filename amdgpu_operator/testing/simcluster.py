@@ -692,6 +692,15 @@ class SimCluster:
 
         by_minor = {f"/dev/dri/renderD{g.render_minor}": g.index for g in topology.enumerate_gpus(node.env.sysfs_root())}
         devices, envs = [], {}
+        # pod-resources: each container holds the claims its resources.claims names
+        held = {c["metadata"]["name"]: {"claim": (run.ns, c["metadata"]["name"]), "resources": [
+            (dra_api.DRIVER_NAME, d.pool_name, d.device_name, list(d.cdi_device_ids)) for d in out[c["metadata"]["uid"]].devices]}
+            for c in claims}
+        by_ref = {rc["name"]: rc["resourceClaimName"] for rc in run.pod["spec"].get("resourceClaims") or []}
+        for ctr in run.pod["spec"]["containers"]:
+            refs = [by_ref.get(x.get("name")) for x in (ctr.get("resources") or {}).get("claims") or []]
+            if any(r in held for r in refs):
+                node.kubelet.record_claims(run.ns, run.name, ctr["name"], [held[r] for r in refs if r in held])
         for uid, r in out.items():
             with open(os.path.join(node.env.cdi_dir, f"{dra_api.DRIVER_NAME}-claim_{uid}.json")) as f:
                 spec = json.load(f)

@@ -209,6 +209,7 @@ def test_policy_deploys_the_dra_driver_on_the_simulated_cluster(short_tmp, proce
         while any(f.startswith("gpu.amd.com-claim_") for f in os.listdir(env.cdi_dir)) and time.monotonic() < deadline:
             time.sleep(0.05)
         assert not any(f.startswith("gpu.amd.com-claim_") for f in os.listdir(env.cdi_dir))
+        assert not c.nodes["gpu-1"].kubelet.claims  # pod-resources no longer lists the stopped pod's claims
         slices = c.client.list(RV1B1, "ResourceSlice")
         assert len(slices) == 1 and len(slices[0]["spec"]["devices"]) == 4 and slices[0]["spec"]["nodeName"] == "gpu-1"
         assert c.client.get(RV1B1, "DeviceClass", "gpu.amd.com")
@@ -269,3 +270,39 @@ def test_partition_change_republishes_with_a_new_generation(node):
     s = env.client.get(RV1B1, "ResourceSlice", f"n1-{api.DRIVER_NAME}")
     assert len(s["spec"]["devices"]) == 16 and s["spec"]["pool"]["generation"] == 2
     assert s["spec"]["devices"][1]["basic"]["attributes"]["computePartition"] == {"string": "DPX"}
+
+
+def test_exporter_attributes_dra_claims_via_pod_resources(short_tmp):
+    """Pod attribution of GPU metrics with DRA: the kubelet's pod-resources
+    List reports a container's prepared claims as dynamic_resources
+    (driver/pool/device, kubelet >= 1.31); the exporter maps the DRA device
+    names (partitions too) back to the BDF[-pN] IDs its samples carry."""
+    from amdgpu_operator.exporter.metrics import PodAttribution, dra_device_ids
+    from amdgpu_operator.testing.fakekubelet import FakeKubelet
+
+    root = str(short_tmp / "cpx")
+    fakesys.build_node(root, 2, compute_partition="CPX")
+    gpus = T.enumerate_gpus(root)
+    sock = str(short_tmp / "podres" / "kubelet.sock")
+    k = FakeKubelet(str(short_tmp / "dp"), sock)
+    k.start()
+    try:
+        k.assignments[("ml", "legacy", "main")] = ("amd.com/gpu", [gpus[0].device_id_str])
+        k.record_claims("ml", "trainer", "main", [{"claim": ("ml", "train-gpus"), "resources": [
+            (api.DRIVER_NAME, "n1", "gpu-9", ["gpu.amd.com/claim=u-gpu-9"]),
+            (api.DRIVER_NAME, "n1", "gpu-10", ["gpu.amd.com/claim=u-gpu-10"])]}])
+        k.record_claims("ml", "other", "main", [{"claim": ("ml", "nic"), "resources": [
+            ("rdma.example.com", "n1", "gpu-3", [])]}])  # another driver's device of the same name
+        m = PodAttribution(sock, dra_driver=api.DRIVER_NAME, resolve=dra_device_ids(root)).lookup()
+        who = {"namespace": "ml", "pod": "trainer", "container": "main"}
+        assert m[gpus[9].device_id_str] == who and m[gpus[10].device_id_str] == who
+        assert gpus[9].device_id_str.endswith("-p1") and gpus[9].bdf == gpus[10].bdf != gpus[0].bdf
+        assert m[gpus[0].device_id_str]["pod"] == "legacy" and gpus[3].device_id_str not in m
+        assert not any(v["pod"] == "other" for v in m.values())
+        # without a DRA driver name only device-plugin allocations count
+        assert set(PodAttribution(sock).lookup()) == {gpus[0].device_id_str}
+        k.release("ml", "trainer")
+        assert gpus[9].device_id_str not in PodAttribution(sock, dra_driver=api.DRIVER_NAME,
+                                                            resolve=dra_device_ids(root)).lookup()
+    finally:
+        k.stop()

@@ -203,7 +203,7 @@ def test_event_recorder_aggregates_repeats(client):
 def test_bring_up_and_upgrade_leave_events(tmp_path):
     """kubectl describe parity (README.md:179): the ClusterPolicy reports Ready,
     the node reports its validation and each driver-upgrade step."""
-    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, deep_merge, parse_set_flags
+    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, parse_set_flags
     from amdgpu_operator.controller import upgrade as U
     from amdgpu_operator.kube.events import events_for
     from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster

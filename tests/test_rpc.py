@@ -39,6 +39,8 @@ def _value(ftype, depth, schema):
         return _i64
     if ftype == "int32":
         return _i32
+    if ftype == "uint64":
+        return hs.integers(0, (1 << 64) - 1)
     return _message_dict(ftype, schema, depth + 1)
 
 
