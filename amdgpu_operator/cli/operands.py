@@ -477,10 +477,10 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
         attribution = None
         if a.pod_attribution:
             from ..dra.api import DRIVER_NAME
-            from ..exporter.metrics import dra_device_ids
+            from ..exporter.metrics import device_id_resolver
 
             attribution = PodAttribution(env.pod_resources_socket, dra_driver=DRIVER_NAME,
-                                         resolve=dra_device_ids(env.sysfs_root()))
+                                         resolve=device_id_resolver(env.sysfs_root()))
         selection = None
         csv_text = None
         if a.metrics_config:

@@ -241,15 +241,16 @@ class PodAttribution:
 
     Device-plugin allocations arrive as ``devices`` (the plugin's IDs);
     DRA allocations as ``dynamic_resources`` (claim -> driver/pool/device,
-    kubelet >= 1.31), whose device names (``gpu-<index>``, dra/driver.py)
-    ``resolve`` turns into the same BDF[-pN] IDs."""
+    kubelet >= 1.31).  ``resolve`` turns DRA device names (``gpu-<index>``,
+    dra/driver.py) and the plugin's uuid/index IDs into the BDF[-pN] IDs the
+    samples carry (:func:`device_id_resolver`)."""
 
     def __init__(self, socket_path: str, resource_prefix: str = "amd.com/gpu", dra_driver: str = "",
                  resolve=None):
         self.socket_path = socket_path
         self.prefix = resource_prefix
         self.dra_driver = dra_driver
-        self.resolve = resolve  # DRA device name -> device ID (None: the name itself)
+        self.resolve = resolve  # allocation name -> BDF[-pN] (None: the name itself)
 
     def lookup(self) -> dict[str, dict]:
         from ..deviceplugin import api
@@ -270,7 +271,7 @@ class PodAttribution:
                     if not d.resource_name.startswith(self.prefix):
                         continue
                     for dev in d.device_ids:
-                        m[dev] = who
+                        m[(self.resolve(dev) if self.resolve else None) or dev] = who
                 if not self.dra_driver:
                     continue
                 for dr in c.dynamic_resources:
@@ -282,10 +283,14 @@ class PodAttribution:
         return m
 
 
-def dra_device_ids(sysfs_root: str):
-    """``resolve`` for :class:`PodAttribution`: DRA device name -> BDF[-pN],
-    re-read from the KFD topology when a name is unknown (partitions
-    change the device set)."""
+def device_id_resolver(sysfs_root: str):
+    """``resolve`` for :class:`PodAttribution`: any name the node's GPUs go
+    by in an allocation -> their BDF[-pN] ID.  DRA device names
+    (``gpu-<index>``) and the device plugin's ``uuid`` and ``index``
+    deviceIDStrategy IDs (deviceplugin/server.py base_id) all map to it; the
+    table is re-read from the KFD topology when a name is unknown
+    (partitions change the device set)."""
+    from ..deviceplugin.server import base_id
     from ..discovery import topology
     from ..dra.driver import device_name
 
@@ -294,7 +299,9 @@ def dra_device_ids(sysfs_root: str):
     def resolve(name: str) -> str | None:
         if name not in cache:
             cache.clear()
-            cache.update({device_name(g): g.device_id_str for g in topology.enumerate_gpus(sysfs_root)})
+            for g in topology.enumerate_gpus(sysfs_root):
+                for alias in (device_name(g), base_id(g, "uuid"), base_id(g, "index"), g.device_id_str):
+                    cache[alias] = g.device_id_str
         return cache.get(name)
 
     return resolve

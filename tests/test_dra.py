@@ -277,7 +277,7 @@ def test_exporter_attributes_dra_claims_via_pod_resources(short_tmp):
     List reports a container's prepared claims as dynamic_resources
     (driver/pool/device, kubelet >= 1.31); the exporter maps the DRA device
     names (partitions too) back to the BDF[-pN] IDs its samples carry."""
-    from amdgpu_operator.exporter.metrics import PodAttribution, dra_device_ids
+    from amdgpu_operator.exporter.metrics import PodAttribution, device_id_resolver
     from amdgpu_operator.testing.fakekubelet import FakeKubelet
 
     root = str(short_tmp / "cpx")
@@ -293,16 +293,24 @@ def test_exporter_attributes_dra_claims_via_pod_resources(short_tmp):
             (api.DRIVER_NAME, "n1", "gpu-10", ["gpu.amd.com/claim=u-gpu-10"])]}])
         k.record_claims("ml", "other", "main", [{"claim": ("ml", "nic"), "resources": [
             ("rdma.example.com", "n1", "gpu-3", [])]}])  # another driver's device of the same name
-        m = PodAttribution(sock, dra_driver=api.DRIVER_NAME, resolve=dra_device_ids(root)).lookup()
+        m = PodAttribution(sock, dra_driver=api.DRIVER_NAME, resolve=device_id_resolver(root)).lookup()
         who = {"namespace": "ml", "pod": "trainer", "container": "main"}
         assert m[gpus[9].device_id_str] == who and m[gpus[10].device_id_str] == who
         assert gpus[9].device_id_str.endswith("-p1") and gpus[9].bdf == gpus[10].bdf != gpus[0].bdf
         assert m[gpus[0].device_id_str]["pod"] == "legacy" and gpus[3].device_id_str not in m
         assert not any(v["pod"] == "other" for v in m.values())
+        # the plugin's uuid / index deviceIDStrategy IDs resolve to the same BDF[-pN]
+        from amdgpu_operator.deviceplugin.server import base_id
+
+        k.assignments[("ml", "by-uuid", "main")] = ("amd.com/gpu", [base_id(gpus[5], "uuid")])
+        k.assignments[("ml", "by-index", "main")] = ("amd.com/gpu", [base_id(gpus[12], "index")])
+        m = PodAttribution(sock, dra_driver=api.DRIVER_NAME, resolve=device_id_resolver(root)).lookup()
+        assert m[gpus[5].device_id_str]["pod"] == "by-uuid" and m[gpus[12].device_id_str]["pod"] == "by-index"
+        del k.assignments[("ml", "by-uuid", "main")], k.assignments[("ml", "by-index", "main")]
         # without a DRA driver name only device-plugin allocations count
         assert set(PodAttribution(sock).lookup()) == {gpus[0].device_id_str}
         k.release("ml", "trainer")
         assert gpus[9].device_id_str not in PodAttribution(sock, dra_driver=api.DRIVER_NAME,
-                                                            resolve=dra_device_ids(root)).lookup()
+                                                            resolve=device_id_resolver(root)).lookup()
     finally:
         k.stop()
