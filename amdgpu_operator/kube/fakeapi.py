@@ -68,14 +68,32 @@ class _Watch:
         self.q: queue.Queue = queue.Queue()
         self.closed = False
 
-    def offer(self, etype: str, obj: dict, blob: bytes | None = None) -> None:
+    def _passes(self, obj: dict) -> bool:
+        return R.matches(R.labels_of(obj), self.reqs) and _field_ok(obj, self.field_selector)
+
+    def offer(self, etype: str, obj: dict, blob: bytes | None = None, old: dict | None = None,
+              old_blob: bytes | None = None) -> None:
         """``blob``: the object pickled once by the server for every watcher;
-        each consumer unpickles its own copy (3x cheaper than a deep copy)."""
+        each consumer unpickles its own copy (3x cheaper than a deep copy).
+
+        A modification that moves an object into or out of this watch's
+        selectors arrives as ADDED or DELETED, as kube-apiserver's watch cache
+        sends it (the DELETED carrying the object as it last matched): a
+        kubelet watching ``spec.nodeName=<node>`` sees a pod the scheduler
+        binds as ADDED."""
         if self.closed or R.rtype_of(obj) != self.t:
             return
         if self.t.namespaced and self.namespace and R.ns_of(obj) != self.namespace:
             return
-        if not R.matches(R.labels_of(obj), self.reqs) or not _field_ok(obj, self.field_selector):
+        now = self._passes(obj)
+        if etype == "MODIFIED" and old is not None:
+            before = self._passes(old)
+            if now and not before:
+                etype = "ADDED"
+            elif before and not now:
+                self.q.put(("DELETED", old_blob if old_blob is not None else _pack(old)))
+                return
+        if not now:
             return
         self.q.put((etype, blob if blob is not None else _pack(obj)))
 
@@ -122,18 +140,19 @@ class FakeApiServer:
         self._last_rv = rv
         obj["metadata"]["resourceVersion"] = str(rv)
 
-    def _emit(self, etype: str, obj: dict) -> None:
+    def _emit(self, etype: str, obj: dict, old: dict | None = None) -> None:
         blob = _pack(obj)
         k = R.key_of(obj)
+        old_blob = self._blobs.get(k) if old is not None else None
         if etype == "DELETED":
             self._blobs.pop(k, None)
         else:
             self._blobs[k] = blob
-        self._history.append((int(obj["metadata"]["resourceVersion"]), etype, blob))
+        self._history.append((int(obj["metadata"]["resourceVersion"]), etype, blob, old_blob))
         if len(self._history) > 20000:
             del self._history[:5000]
         for w in list(self._watches):
-            w.offer(etype, obj, blob)
+            w.offer(etype, obj, blob, old, old_blob)
         for h in list(self.hooks):
             h(etype, pickle.loads(blob))
 
@@ -245,7 +264,7 @@ class FakeApiServer:
                     new["metadata"]["generation"] = cur["metadata"].get("generation", 1) + 1
             self._bump(new)
             self._store[k] = new
-            self._emit("MODIFIED", new)
+            self._emit("MODIFIED", new, cur)
             return self._out(k, new)
 
     def patch(self, api_version: str, kind: str, name: str, patch: dict, namespace: str | None = None,
@@ -315,9 +334,10 @@ class FakeApiServer:
         with self._lock:
             if resource_version not in (None, "", "0", 0):
                 rv = int(resource_version)
-                for erv, etype, blob in self._history:
+                for erv, etype, blob, old_blob in self._history:
                     if erv > rv:
-                        w.offer(etype, pickle.loads(blob), blob)
+                        w.offer(etype, pickle.loads(blob), blob,
+                                pickle.loads(old_blob) if old_blob is not None else None, old_blob)
             else:  # like kube-apiserver: the current state as synthetic ADDED events first
                 for k, obj in self._store.items():
                     w.offer("ADDED", obj, self._blobs.get(k))

@@ -18,6 +18,13 @@ every GPU it was given, Freivalds-checked, and ``--expect-devices`` so a GPU
 the runtime left out fails the pod.  The per-pod times come from the
 simulated kubelet's trace (pod created -> devices allocated -> spec hooked ->
 report out = kernel done).
+
+With the DRA driver instead of the device plugin (``dra=True``) the same
+batches are ResourceClaims: one claim per pod (``count: k``; the whole node
+as ``allocationMode: All``; the two halves with a ``matchAttribute`` on
+``gpu.amd.com/numaNode`` so each half is NUMA-local), allocated by the
+scheduler from the node's ResourceSlice, prepared by the node's DRA driver
+through the kubelet's DRA manager, and injected from the claim's CDI spec.
 """
 
 from __future__ import annotations
@@ -55,7 +62,31 @@ def _pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm_n: 
     }
 
 
-def _run_batch(cluster, node: str, namespace: str, shapes: list[int], gemm_n: int, timeout: float) -> list[dict]:
+def _dra_pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm_n: int, n_gpus: int) -> list[dict]:
+    """A ResourceClaim for ``count`` devices and the pod using it (scheduled
+    by the scheduler, which allocates the claim on ``node``)."""
+    from ..dra.api import DRIVER_NAME
+
+    req = {"name": "gpus", "deviceClassName": DRIVER_NAME}
+    if count == n_gpus:
+        req["allocationMode"] = "All"
+    else:
+        req["count"] = count
+    constraints = [{"requests": ["gpus"], "matchAttribute": f"{DRIVER_NAME}/numaNode"}] if 1 < count < n_gpus else []
+    claim = {"apiVersion": "resource.k8s.io/v1beta1", "kind": "ResourceClaim",
+             "metadata": {"name": name, "namespace": namespace, "labels": {POD_LABEL: run_id}},
+             "spec": {"devices": {"requests": [req], "constraints": constraints}}}
+    pod = _pod(name, node, namespace, run_id, count, gemm_n)
+    spec = pod["spec"]
+    del spec["nodeName"], spec["tolerations"]
+    spec["nodeSelector"] = {"kubernetes.io/hostname": node}
+    spec["resourceClaims"] = [{"name": "gpus", "resourceClaimName": name}]
+    spec["containers"][0]["resources"] = {"claims": [{"name": "gpus"}]}
+    return [claim, pod]
+
+
+def _run_batch(cluster, node: str, namespace: str, shapes: list[int], gemm_n: int, timeout: float,
+               dra: bool = False, n_gpus: int = 0) -> list[dict]:
     """Create one pod per entry of ``shapes`` (its GPU count) at once, wait for
     all, collect their record, delete them."""
     from ..kube.client import wait_for
@@ -65,7 +96,9 @@ def _run_batch(cluster, node: str, namespace: str, shapes: list[int], gemm_n: in
     created = {}
     for name, k in zip(names, shapes):
         created[name] = time.perf_counter()
-        cluster.client.create(_pod(name, node, namespace, run_id, k, gemm_n))
+        for obj in (_dra_pod(name, node, namespace, run_id, k, gemm_n, n_gpus) if dra
+                    else [_pod(name, node, namespace, run_id, k, gemm_n)]):
+            cluster.client.create(obj)
     objs, ok = wait_for(cluster.client, "v1", "Pod", lambda o: all(
         n in o and ((o[n].get("status") or {}).get("phase") in ("Succeeded", "Failed")) for n in names),
         namespace=namespace, label_selector=f"{POD_LABEL}={run_id}", timeout=timeout, poll_s=0.01)
@@ -73,21 +106,33 @@ def _run_batch(cluster, node: str, namespace: str, shapes: list[int], gemm_n: in
     for t, what, detail in list(cluster.events):
         if detail in created and what in ("gpu-pod-allocated", "gpu-pod-hooked", "gpu-pod-reported"):
             events.setdefault(detail, {}).setdefault(what, t)
-    topo = {}
+    topo, by_dra_name = {}, {}
     try:
         from ..discovery import topology
+        from ..dra.driver import device_name
 
         root = cluster.nodes[node].env.sysfs_root()
-        topo = {g.device_id_str: g for g in topology.enumerate_gpus(root)}
+        gpus = topology.enumerate_gpus(root)
+        topo = {g.device_id_str: g for g in gpus}
+        by_dra_name = {device_name(g): g.device_id_str for g in gpus}
     except Exception:  # noqa: BLE001 - record the device ids only
         pass
+    claims = {}
+    if dra:
+        claims = {c["metadata"]["name"]: c for c in cluster.client.list(
+            "resource.k8s.io/v1beta1", "ResourceClaim", namespace, label_selector=f"{POD_LABEL}={run_id}")}
     out = []
     for name, k in zip(names, shapes):
         o = objs.get(name) or {}
         ev = events.get(name, {})
         rec = {"pod": name, "gpus": k, "phase": (o.get("status") or {}).get("phase", "Missing")}
-        alloc = ((o.get("metadata") or {}).get("annotations") or {}).get("amd.com/gpu.allocated", "")
-        rec["devices"] = [d for d in alloc.split(",") if d]
+        if dra:
+            res = ((((claims.get(name) or {}).get("status") or {}).get("allocation") or {}).get("devices")
+                   or {}).get("results") or []
+            rec["devices"] = [by_dra_name.get(r["device"], r["device"]) for r in res]
+        else:
+            alloc = ((o.get("metadata") or {}).get("annotations") or {}).get("amd.com/gpu.allocated", "")
+            rec["devices"] = [d for d in alloc.split(",") if d]
         gs = [topo[d] for d in rec["devices"] if d in topo]
         if gs:
             rec["numa_nodes"] = sorted({g.numa_node for g in gs})
@@ -111,32 +156,49 @@ def _run_batch(cluster, node: str, namespace: str, shapes: list[int], gemm_n: in
             rec["simulated"] = bool(rep.get("simulated"))
         out.append(rec)
     for name in names:
-        try:
-            cluster.client.delete("v1", "Pod", name, namespace)
-        except Exception:  # noqa: BLE001
-            pass
+        for kind in (("v1", "Pod"),) + ((("resource.k8s.io/v1beta1", "ResourceClaim"),) if dra else ()):
+            try:
+                cluster.client.delete(*kind, name, namespace)
+            except Exception:  # noqa: BLE001
+                pass
     if not ok:
         raise TimeoutError(f"pod workload did not finish in {timeout} s: {[r['phase'] for r in out]}")
     # the next batch starts once the kubelet released these pods' devices
+    # (DRA: and the driver unprepared their claims, removing the CDI specs)
     kubelet = cluster.nodes[node].kubelet
+    cdi_dir = cluster.nodes[node].env.cdi_dir
+    uids = {c["metadata"].get("uid") for c in claims.values()}
+
+    def held():
+        if any(k[1] in names for k in list(kubelet.assignments) + list(kubelet.claims)):
+            return True
+        try:
+            return dra and any(f.split("claim_", 1)[-1][:-5] in uids for f in os.listdir(cdi_dir))
+        except OSError:
+            return False
+
     deadline = time.monotonic() + timeout
-    while time.monotonic() < deadline and any(k[1] in names for k in list(kubelet.assignments)):
+    while time.monotonic() < deadline and held():
         time.sleep(0.01)
     return out
 
 
 def run_pod_workload(cluster, node: str, n_gpus: int, gemm_n: int = 4096, timeout: float = 120.0,
-                     namespace: str = "default") -> dict:
+                     namespace: str = "default", dra: bool = False) -> dict:
     """Config 5 on a validated node; returns the ``pod_workload`` block."""
     t0 = time.perf_counter()
-    batches = {"single": _run_batch(cluster, node, namespace, [1] * n_gpus, gemm_n, timeout),
-               "whole_node": _run_batch(cluster, node, namespace, [n_gpus], gemm_n, timeout)}
+
+    def batch(shapes):
+        return _run_batch(cluster, node, namespace, shapes, gemm_n, timeout, dra=dra, n_gpus=n_gpus)
+
+    batches = {"single": batch([1] * n_gpus), "whole_node": batch([n_gpus])}
     if n_gpus == 8:
-        batches["two_halves"] = _run_batch(cluster, node, namespace, [4, 4], gemm_n, timeout)
+        batches["two_halves"] = batch([4, 4])
     pods = [p for b in batches.values() for p in b]
     single = batches["single"]
     done = [p["kernel_done_s"] for p in single if "kernel_done_s" in p]
     out = {
+        "allocation": "dra" if dra else "device-plugin",
         "pods": len(pods),
         "all_succeeded": all(p["phase"] == "Succeeded" for p in pods),
         "gemm_correct": all(p.get("gemm_ok") for p in pods),

@@ -71,6 +71,7 @@ class SimNode:
     kubelet: FakeKubelet
     pods: dict = field(default_factory=dict)  # pod name -> _PodRun
     terminating: set = field(default_factory=set)  # pods between graceful delete and removal
+    dra: object = None  # the kubelet's DRA side (fakedra.FakeDraKubelet), created on first use
 
 
 class AdmissionError(RuntimeError):
@@ -676,15 +677,15 @@ class SimCluster:
         from . import fakedra
 
         node = run.node
-        k = fakedra.FakeDraKubelet(os.path.dirname(node.env.device_plugin_dir.rstrip("/")))
-        deadline = time.monotonic() + 30
-        while dra_api.DRIVER_NAME not in k.discover():
-            if time.monotonic() >= deadline:
-                raise AdmissionError(f"DRA driver {dra_api.DRIVER_NAME} not registered on {node.spec.name}")
-            time.sleep(0.05)
         claims = [self.client.get("resource.k8s.io/v1beta1", "ResourceClaim", rc["resourceClaimName"], run.ns)
                   for rc in run.pod["spec"].get("resourceClaims") or []]
-        out = k.prepare(dra_api.DRIVER_NAME, claims)
+        try:
+            out = self._dra_kubelet(node).prepare(dra_api.DRIVER_NAME, claims)
+        except AdmissionError:
+            raise
+        except Exception:  # noqa: BLE001 - the driver restarted: the plugin watcher registers it again
+            node.dra = None
+            out = self._dra_kubelet(node).prepare(dra_api.DRIVER_NAME, claims)
         errors = [r.error for r in out.values() if r.error]
         if errors:
             raise AdmissionError("; ".join(errors))
@@ -713,13 +714,36 @@ class SimCluster:
             envs.update(e.split("=", 1) for e in spec.get("containerEdits", {}).get("env", []))
         return devices, envs, list(out)
 
-    def _unprepare_claims(self, run: _PodRun, uids: list[str]) -> None:
+    def _dra_kubelet(self, node: SimNode, timeout: float = 30.0):
+        """The node's kubelet plugin watcher + DRA manager: the driver is
+        registered once (GetInfo / NotifyRegistrationStatus) and its endpoint
+        reused for every pod, as on a real kubelet."""
         from ..dra import api as dra_api
         from . import fakedra
 
-        k = fakedra.FakeDraKubelet(os.path.dirname(run.node.env.device_plugin_dir.rstrip("/")))
-        if k.discover(timeout=2.0).get(dra_api.DRIVER_NAME):
-            k.unprepare(dra_api.DRIVER_NAME, [{"metadata": {"namespace": run.ns, "name": "", "uid": u}} for u in uids])
+        with self._lock:
+            if node.dra is None:
+                node.dra = fakedra.FakeDraKubelet(os.path.dirname(node.env.device_plugin_dir.rstrip("/")))
+            k = node.dra
+        deadline = time.monotonic() + timeout
+        while dra_api.DRIVER_NAME not in k.plugins and dra_api.DRIVER_NAME not in k.discover():
+            if time.monotonic() >= deadline:
+                raise AdmissionError(f"DRA driver {dra_api.DRIVER_NAME} not registered on {node.spec.name}")
+            time.sleep(0.05)
+        return k
+
+    def _unprepare_claims(self, run: _PodRun, uids: list[str]) -> None:
+        from ..dra import api as dra_api
+
+        claims = [{"metadata": {"namespace": run.ns, "name": "", "uid": u}} for u in uids]
+        try:
+            self._dra_kubelet(run.node, timeout=2.0).unprepare(dra_api.DRIVER_NAME, claims)
+        except Exception:  # noqa: BLE001 - once more through a fresh registration
+            run.node.dra = None
+            try:
+                self._dra_kubelet(run.node, timeout=2.0).unprepare(dra_api.DRIVER_NAME, claims)
+            except Exception as e:  # noqa: BLE001 - the driver is gone: its checkpoint keeps the claim
+                log.debug("unprepare %s: %s", uids, e)
 
     # -------------------------------------------------------------- kubelet
     def _kubelet_loop(self, node: SimNode) -> None:

@@ -302,7 +302,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             from amdgpu_operator.testing.podworkload import run_pod_workload
 
             pod_workload = run_pod_workload(cluster, "mi355x-node-0", n_gpus, gemm_n=args.pod_gemm,
-                                            timeout=args.timeout)
+                                            timeout=args.timeout,
+                                            dra=(values.get("draDriver") or {}).get("enabled") is True)
         cp = cluster.policy()
         nobj = cluster.client.get("v1", "Node", "mi355x-node-0")
         alloc = int(nobj["status"]["allocatable"].get("amd.com/gpu", "0"))

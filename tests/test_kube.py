@@ -98,6 +98,27 @@ def test_watch_from_resource_version():
     assert got == ["b"]
 
 
+def test_watch_selector_transitions_are_added_and_deleted():
+    """kube-apiserver's watch cache: a modification that moves an object into
+    a watch's label/field selector is ADDED, one that moves it out is DELETED
+    (with the object as it last matched) - how a kubelet watching
+    spec.nodeName sees the pod the scheduler just bound.  Also on a replay
+    from a resourceVersion."""
+    api = FakeApiServer()
+    c = LocalClient(api)
+    c.create(R.new("v1", "Namespace", "ns"))
+    rv = api.resource_version()
+    c.create(R.new("v1", "Pod", "p", "ns", spec={"containers": []}))
+    c.patch("v1", "Pod", "p", {"spec": {"nodeName": "n1"}}, "ns")
+    c.patch("v1", "Pod", "p", {"metadata": {"labels": {"x": "1"}}}, "ns")
+    c.patch("v1", "Pod", "p", {"spec": {"nodeName": "n2"}}, "ns")
+    got = [(et, o["spec"].get("nodeName")) for et, o in
+           c.watch("v1", "Pod", "ns", field_selector="spec.nodeName=n1", resource_version=rv, timeout=0.3)]
+    assert got == [("ADDED", "n1"), ("MODIFIED", "n1"), ("DELETED", "n1")]
+    got = [et for et, _ in c.watch("v1", "Pod", "ns", label_selector="x=1", resource_version=rv, timeout=0.3)]
+    assert got == ["ADDED", "MODIFIED"]
+
+
 def test_owner_reference_gc_and_namespace_delete(client):
     client.create(R.new("v1", "Namespace", "ns"))
     owner = client.create(R.new("amd.com/v1", "ClusterPolicy", "cp"))

@@ -439,6 +439,27 @@ def test_config5_pod_workload_on_an_8_gpu_hive(cluster_factory):
     assert all(p["phase"] == "Succeeded" for b in out["batches"].values() for p in b)
 
 
+def test_config5_pod_workload_over_dra_claims(cluster_factory):
+    """The same config-5 batches with the DRA driver instead of the device
+    plugin: one ResourceClaim per pod, allocated by the scheduler from the
+    node's ResourceSlice (the halves with a numaNode matchAttribute),
+    prepared by the DRA driver and injected from its CDI spec."""
+    from amdgpu_operator.discovery import topology
+    from amdgpu_operator.testing.podworkload import run_pod_workload
+
+    c = cluster_factory([NodeSpec("gpu-1", 8)])
+    c.install_operator(parse_set_flags(REFERENCE_SET_FLAGS + ["draDriver.enabled=true", "devicePlugin.enabled=false"]))
+    c.wait_ready(60, {})
+    out = run_pod_workload(c, "gpu-1", 8, dra=True)
+    assert out["allocation"] == "dra" and out["pods"] == 8 + 1 + 2 and out["all_succeeded"] and out["gemm_correct"]
+    assert out["single_gpu_pods_distinct_devices"] and out["two_halves_numa_local"] and out["two_halves_disjoint"]
+    assert len(out["batches"]["whole_node"][0]["devices"]) == 8
+    gpus = {g.bdf: g for g in topology.enumerate_gpus(c.nodes["gpu-1"].env.sysfs_root())}
+    assert all(d in gpus for b in out["batches"].values() for p in b for d in p["devices"])
+    assert not c.client.list("resource.k8s.io/v1beta1", "ResourceClaim")  # every claim deleted with its pod
+    assert not c.nodes["gpu-1"].kubelet.claims
+
+
 def test_per_device_plugin_validation_pods(cluster_factory):
     """validator.pluginPods=perDevice: 8 one-GPU pods, each its own
     allocation, on 8 distinct GPUs; past the GPU-process budget (2 x CPX = 16
