@@ -61,6 +61,7 @@ _TYPES = [
     ResourceType("resource.k8s.io", "v1beta1", "ResourceSlice", "resourceslices", False),
     ResourceType("resource.k8s.io", "v1beta1", "DeviceClass", "deviceclasses", False),
     ResourceType("resource.k8s.io", "v1beta1", "ResourceClaim", "resourceclaims", True),
+    ResourceType("resource.k8s.io", "v1beta1", "ResourceClaimTemplate", "resourceclaimtemplates", True),
 ]
 
 REGISTRY: dict[tuple[str, str], ResourceType] = {(t.api_version, t.kind): t for t in _TYPES}

@@ -95,7 +95,17 @@ def pod_spec(spec: dict, path: str, errs: list[str], in_template: bool = False, 
                 errs.append(f"{path}.volumes[{i}].hostPath.path must be absolute")
             if hp.get("type", "") not in HOSTPATH_TYPES:
                 errs.append(f"{path}.volumes[{i}].hostPath.type {hp.get('type')!r} not supported")
-    claims = {c.get("name") for c in spec.get("resourceClaims") or []}
+    claims = set()
+    for i, rc in enumerate(spec.get("resourceClaims") or []):
+        n = rc.get("name", "")
+        if not _dns_label(n):
+            errs.append(f"{path}.resourceClaims[{i}].name {n!r}")
+        elif n in claims:
+            errs.append(f"{path}.resourceClaims[{i}].name {n!r}: duplicate")
+        claims.add(n)
+        if bool(rc.get("resourceClaimName")) == bool(rc.get("resourceClaimTemplateName")):
+            errs.append(f"{path}.resourceClaims[{i}]: exactly one of resourceClaimName, "
+                        "resourceClaimTemplateName is required")
     names = set()
     for group in ("initContainers", "containers"):
         for i, c in enumerate(spec.get(group) or []):
@@ -165,6 +175,45 @@ def pod_spec(spec: dict, path: str, errs: list[str], in_template: bool = False, 
             errs.append(f"{path}.nodeSelector: {k}={v!r} is not a valid label")
 
 
+def claim_spec(spec: dict, path: str, errs: list[str]) -> None:
+    """resource.k8s.io/v1beta1 ResourceClaimSpec: named requests of one
+    DeviceClass, ExactCount (count >= 1) or All, CEL selectors, and
+    constraints whose matchAttribute is a fully qualified attribute
+    (``<domain>/<name>``) over requests that exist."""
+    devices = spec.get("devices") or {}
+    reqs = devices.get("requests") or []
+    names = set()
+    for i, r in enumerate(reqs):
+        rp = f"{path}.devices.requests[{i}]"
+        n = r.get("name", "")
+        if not _dns_label(n):
+            errs.append(f"{rp}.name {n!r}")
+        elif n in names:
+            errs.append(f"{rp}.name {n!r}: duplicate")
+        names.add(n)
+        if not r.get("deviceClassName"):
+            errs.append(f"{rp}.deviceClassName: required")
+        mode = r.get("allocationMode", "ExactCount")
+        if mode not in ("ExactCount", "All"):
+            errs.append(f"{rp}.allocationMode {mode!r}: ExactCount or All")
+        elif mode == "ExactCount" and int(r.get("count", 1)) < 1:
+            errs.append(f"{rp}.count {r.get('count')!r}: must be at least 1")
+        elif mode == "All" and "count" in r:
+            errs.append(f"{rp}.count: must not be set with allocationMode All")
+        for j, sel in enumerate(r.get("selectors") or []):
+            if not ((sel.get("cel") or {}).get("expression") or "").strip():
+                errs.append(f"{rp}.selectors[{j}].cel.expression: required")
+    for i, c in enumerate(devices.get("constraints") or []):
+        cp = f"{path}.devices.constraints[{i}]"
+        attr = c.get("matchAttribute", "")
+        dom, _, nm = str(attr).partition("/")
+        if not (dom and nm and _dns_subdomain(dom)):
+            errs.append(f"{cp}.matchAttribute {attr!r}: a fully qualified <domain>/<name>")
+        for rn in c.get("requests") or []:
+            if rn not in names:
+                errs.append(f"{cp}.requests: {rn!r} is not a request of this claim")
+
+
 def validate(obj: dict) -> list[str]:
     """The apiserver's ``Invalid`` causes for ``obj`` (empty: valid)."""
     errs: list[str] = []
@@ -186,6 +235,9 @@ def validate(obj: dict) -> list[str]:
                 errs.append("spec.selector: required")
             elif any(tl.get(k) != v for k, v in sel.items()):
                 errs.append(f"spec.template.metadata.labels: do not match spec.selector {sel}")
+    elif kind in ("ResourceClaim", "ResourceClaimTemplate"):
+        claim_spec(spec.get("spec") or {} if kind == "ResourceClaimTemplate" else spec,
+                   "spec.spec" if kind == "ResourceClaimTemplate" else "spec", errs)
     elif kind == "Service":
         ports = spec.get("ports") or []
         pnames = [p.get("name") for p in ports]

@@ -72,6 +72,9 @@ class SimNode:
     pods: dict = field(default_factory=dict)  # pod name -> _PodRun
     terminating: set = field(default_factory=set)  # pods between graceful delete and removal
     dra: object = None  # the kubelet's DRA side (fakedra.FakeDraKubelet), created on first use
+    # the DRA manager's claim cache lock: a shared claim's prepare, its pods'
+    # use counts and its unprepare are one critical section
+    dra_lock: threading.Lock = field(default_factory=threading.Lock)
 
 
 class AdmissionError(RuntimeError):
@@ -110,6 +113,7 @@ class _PodRun:
         self.ready: dict[str, bool] = {}
         self.thread = threading.Thread(target=self._run, daemon=True, name=f"pod-{self.name}")
         self.cleanups: list = []
+        self.dra_uids: list[str] = []  # ResourceClaims prepared for this pod
         self.restarts = 0
         self._status_lock = threading.Lock()
 
@@ -148,6 +152,10 @@ class _PodRun:
             cur = self.cluster.client.get("v1", "Pod", self.name, self.ns)
         except NotFound:
             return
+        # fields of the pod's status other writers own (the resourceclaim controller's claim names)
+        for k in ("resourceClaimStatuses",):
+            if k in (cur.get("status") or {}):
+                st[k] = cur["status"][k]
         if cur.get("status") == st:
             return
         cur["status"] = st
@@ -650,15 +658,36 @@ class SimCluster:
         from . import fakedra
 
         md = pod["metadata"]
-        node = ((pod["spec"].get("nodeSelector") or {}).get("kubernetes.io/hostname"))
-        if node not in self.nodes:
+        want = dict(pod["spec"].get("nodeSelector") or {})
+        host = want.pop("kubernetes.io/hostname", None)
+        if host is not None and host not in self.nodes:
             return
         ns = md.get("namespace", "default")
         try:
-            for rc in pod["spec"].get("resourceClaims") or []:
-                claim = self.client.get("resource.k8s.io/v1beta1", "ResourceClaim", rc["resourceClaimName"], ns)
-                if not (claim.get("status") or {}).get("allocation"):
-                    fakedra.allocate(self.client, claim, node)
+            claims = [self.client.get("resource.k8s.io/v1beta1", "ResourceClaim", n, ns)
+                      for n in self._pod_claims(pod).values()]
+            # the nodes the pod may land on: its hostname selector, else every
+            # GPU node whose labels match; a claim allocated earlier (shared by
+            # several pods) pins the node it was allocated on
+            pinned = {t["values"][0] for c in claims for term in ((((c.get("status") or {}).get("allocation") or {})
+                                                                   .get("nodeSelector") or {}).get("nodeSelectorTerms") or [])
+                      for t in term.get("matchFields") or [] if t.get("key") == "metadata.name"}
+            cands = [host] if host else [n for n, sn in self.nodes.items() if sn.spec.gpus > 0 and all(
+                (self.client.get("v1", "Node", n)["metadata"].get("labels") or {}).get(k) == v for k, v in want.items())]
+            cands = [n for n in cands if not pinned or n in pinned]
+            if not cands:
+                raise ValueError(f"no node matches (selector {want}, claims allocated on {sorted(pinned)})")
+            err: Exception | None = None
+            for node in cands:
+                try:
+                    for claim in claims:
+                        if not (claim.get("status") or {}).get("allocation"):
+                            fakedra.allocate(self.client, claim, node)
+                    break
+                except ValueError as e:  # this node cannot satisfy the claims: the next one
+                    err = e
+            else:
+                raise err or ValueError("unschedulable")
             self.client.patch("v1", "Pod", md["name"], {"spec": {"nodeName": node}}, ns)
             self.trace("pod-scheduled", md["name"])
         except (ValueError, NotFound) as e:  # unschedulable for now: the next event tries again
@@ -668,7 +697,50 @@ class SimCluster:
             except NotFound:
                 pass
 
+    def _pod_claims(self, pod: dict) -> dict[str, str]:
+        """The pod's resourceClaims entry name -> ResourceClaim name.  An entry
+        naming a ResourceClaimTemplate gets its own claim the way
+        kube-controller-manager's resourceclaim controller makes it: named
+        ``<pod>-<entry>-<suffix>``, owned by the pod (deleted with it),
+        annotated with the entry, and recorded in the pod's
+        ``status.resourceClaimStatuses``."""
+        md = pod["metadata"]
+        ns = md.get("namespace", "default")
+        done = {s["name"]: s.get("resourceClaimName") for s in (pod.get("status") or {}).get("resourceClaimStatuses") or []}
+        out, new = {}, []
+        for rc in pod["spec"].get("resourceClaims") or []:
+            if rc.get("resourceClaimName"):
+                out[rc["name"]] = rc["resourceClaimName"]
+            elif rc.get("resourceClaimTemplateName"):
+                if rc["name"] not in done:
+                    tmpl = self.client.get("resource.k8s.io/v1beta1", "ResourceClaimTemplate",
+                                           rc["resourceClaimTemplateName"], ns)
+                    t_spec = tmpl.get("spec") or {}
+                    name = f"{md['name']}-{rc['name']}-{os.urandom(3).hex()[:5]}"
+                    self.client.create({
+                        "apiVersion": "resource.k8s.io/v1beta1", "kind": "ResourceClaim",
+                        "metadata": {"name": name, "namespace": ns,
+                                     "labels": dict((t_spec.get("metadata") or {}).get("labels") or {}),
+                                     "annotations": {"resource.kubernetes.io/pod-claim-name": rc["name"]},
+                                     "ownerReferences": [{"apiVersion": "v1", "kind": "Pod", "name": md["name"],
+                                                          "uid": md.get("uid"), "controller": True,
+                                                          "blockOwnerDeletion": True}]},
+                        "spec": t_spec.get("spec") or {}})
+                    done[rc["name"]] = name
+                    new.append({"name": rc["name"], "resourceClaimName": name})
+                out[rc["name"]] = done[rc["name"]]
+        if new:
+            self.client.patch("v1", "Pod", md["name"], {"status": {"resourceClaimStatuses": [
+                {"name": k, "resourceClaimName": v} for k, v in done.items()]}}, ns, subresource="status")
+        return out
+
     def _prepare_claims(self, run: _PodRun) -> tuple[list[int], dict[str, str], list[str]]:
+        with run.node.dra_lock:
+            devices, envs, uids = self._prepare_claims_locked(run)
+            run.dra_uids = uids
+            return devices, envs, uids
+
+    def _prepare_claims_locked(self, run: _PodRun) -> tuple[list[int], dict[str, str], list[str]]:
         """The kubelet's DRA manager for a pod's ResourceClaims: prepare them
         through the node's DRA driver and apply the CDI specs it wrote (render
         nodes -> the devices the container sees, env).  Returns (device
@@ -677,8 +749,12 @@ class SimCluster:
         from . import fakedra
 
         node = run.node
-        claims = [self.client.get("resource.k8s.io/v1beta1", "ResourceClaim", rc["resourceClaimName"], run.ns)
-                  for rc in run.pod["spec"].get("resourceClaims") or []]
+        try:  # the scheduler recorded template claims in the pod's status after the kubelet's copy was taken
+            pod = self.client.get("v1", "Pod", run.name, run.ns)
+        except NotFound:
+            pod = run.pod
+        by_ref = self._pod_claims(pod)
+        claims = [self.client.get("resource.k8s.io/v1beta1", "ResourceClaim", n, run.ns) for n in by_ref.values()]
         try:
             out = self._dra_kubelet(node).prepare(dra_api.DRIVER_NAME, claims)
         except AdmissionError:
@@ -697,7 +773,6 @@ class SimCluster:
         held = {c["metadata"]["name"]: {"claim": (run.ns, c["metadata"]["name"]), "resources": [
             (dra_api.DRIVER_NAME, d.pool_name, d.device_name, list(d.cdi_device_ids)) for d in out[c["metadata"]["uid"]].devices]}
             for c in claims}
-        by_ref = {rc["name"]: rc["resourceClaimName"] for rc in run.pod["spec"].get("resourceClaims") or []}
         for ctr in run.pod["spec"]["containers"]:
             refs = [by_ref.get(x.get("name")) for x in (ctr.get("resources") or {}).get("claims") or []]
             if any(r in held for r in refs):
@@ -733,9 +808,20 @@ class SimCluster:
         return k
 
     def _unprepare_claims(self, run: _PodRun, uids: list[str]) -> None:
+        """NodeUnprepareResources for the claims no other pod on the node
+        still uses (the kubelet's DRA manager counts a shared claim's pods)."""
+        with run.node.dra_lock:
+            self._unprepare_claims_locked(run, uids)
+
+    def _unprepare_claims_locked(self, run: _PodRun, uids: list[str]) -> None:
         from ..dra import api as dra_api
 
-        claims = [{"metadata": {"namespace": run.ns, "name": "", "uid": u}} for u in uids]
+        with self._lock:
+            run.dra_uids = []  # this pod's containers are done with them
+            in_use = {u for r in run.node.pods.values() if r is not run for u in r.dra_uids}
+        claims = [{"metadata": {"namespace": run.ns, "name": "", "uid": u}} for u in uids if u not in in_use]
+        if not claims:
+            return
         try:
             self._dra_kubelet(run.node, timeout=2.0).unprepare(dra_api.DRIVER_NAME, claims)
         except Exception:  # noqa: BLE001 - once more through a fresh registration
