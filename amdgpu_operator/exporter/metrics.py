@@ -271,7 +271,8 @@ class PodAttribution:
                     if not d.resource_name.startswith(self.prefix):
                         continue
                     for dev in d.device_ids:
-                        m[(self.resolve(dev) if self.resolve else None) or dev] = who
+                        base = dev.split(api.REPLICA_SEP, 1)[0]  # a time-sliced replica: its GPU
+                        m[(self.resolve(base) if self.resolve else None) or base] = who
                 if not self.dra_driver:
                     continue
                 for dr in c.dynamic_resources:

@@ -304,9 +304,12 @@ def test_exporter_attributes_dra_claims_via_pod_resources(short_tmp):
 
         k.assignments[("ml", "by-uuid", "main")] = ("amd.com/gpu", [base_id(gpus[5], "uuid")])
         k.assignments[("ml", "by-index", "main")] = ("amd.com/gpu", [base_id(gpus[12], "index")])
+        k.assignments[("ml", "sliced", "main")] = ("amd.com/gpu", [gpus[14].device_id_str + "::3"])
         m = PodAttribution(sock, dra_driver=api.DRIVER_NAME, resolve=device_id_resolver(root)).lookup()
         assert m[gpus[5].device_id_str]["pod"] == "by-uuid" and m[gpus[12].device_id_str]["pod"] == "by-index"
-        del k.assignments[("ml", "by-uuid", "main")], k.assignments[("ml", "by-index", "main")]
+        assert m[gpus[14].device_id_str]["pod"] == "sliced"  # a time-sliced replica counts for its GPU
+        for pod in ("by-uuid", "by-index", "sliced"):
+            del k.assignments[("ml", pod, "main")]
         # without a DRA driver name only device-plugin allocations count
         assert set(PodAttribution(sock).lookup()) == {gpus[0].device_id_str}
         k.release("ml", "trainer")
