@@ -98,16 +98,15 @@ def test_watch_from_resource_version():
     assert got == ["b"]
 
 
-def test_watch_selector_transitions_are_added_and_deleted():
+def test_watch_selector_transitions_are_added_and_deleted(client):
     """kube-apiserver's watch cache: a modification that moves an object into
     a watch's label/field selector is ADDED, one that moves it out is DELETED
     (with the object as it last matched) - how a kubelet watching
     spec.nodeName sees the pod the scheduler just bound.  Also on a replay
     from a resourceVersion."""
-    api = FakeApiServer()
-    c = LocalClient(api)
+    c = client
     c.create(R.new("v1", "Namespace", "ns"))
-    rv = api.resource_version()
+    _, rv = c.list_rv("v1", "Namespace")
     c.create(R.new("v1", "Pod", "p", "ns", spec={"containers": []}))
     c.patch("v1", "Pod", "p", {"spec": {"nodeName": "n1"}}, "ns")
     c.patch("v1", "Pod", "p", {"metadata": {"labels": {"x": "1"}}}, "ns")
