@@ -230,7 +230,28 @@ class SmiSource:
         self.smi = Smi()
 
     def collect(self) -> list[Sample]:
-        return [Sample(m.index, m.bdf, m.uuid, m.market_name, m.values) for m in self.smi.collect()]
+        return [Sample(m.index, m.bdf, m.uuid, self._product(m.bdf, m.market_name), m.values)
+                for m in self.smi.collect()]
+
+    _names: dict = {}
+
+    @classmethod
+    def _product(cls, bdf: str, market_name: str) -> str:
+        """amd-smi's market name comes from libdrm's amdgpu.ids; where that
+        table is missing or does not know the part it says "AMD Radeon
+        Graphics" (seen on MI355X hosts).  The PCI device ID names it then,
+        as the node labels do (discovery/labels.py PRODUCTS)."""
+        if market_name and market_name != "AMD Radeon Graphics":
+            return market_name
+        if bdf not in cls._names:
+            from ..discovery.labels import PRODUCTS
+
+            try:
+                with open(f"/sys/bus/pci/devices/{bdf}/device") as f:
+                    cls._names[bdf] = PRODUCTS.get(int(f.read().strip(), 16), market_name)
+            except (OSError, ValueError):
+                cls._names[bdf] = market_name
+        return cls._names[bdf]
 
     def close(self):
         self.smi.close()

@@ -258,6 +258,51 @@ def test_real_mi355x_slice_and_claim(short_tmp):
         drv.stop()
 
 
+@pytest.mark.gpu
+def test_real_mi355x_exporter_attributes_the_claim_holder(short_tmp):
+    """On the MI355X box: a claim prepared by the DRA driver, reported by the
+    kubelet's pod-resources API as the container's dynamic_resources, labels
+    the live amd-smi series of exactly that GPU with the pod (the DRA device
+    name resolved to the BDF amd-smi reports)."""
+    from amdgpu_operator.exporter.metrics import MetricsExporter, PodAttribution, SmiSource, device_id_resolver
+    from amdgpu_operator.testing.fakekubelet import FakeKubelet
+
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Node", "box"))
+    c.create(device_class())
+    env = NodeEnv("box", c, host_root="/", validations_dir=str(short_tmp / "val"), poll_s=0.01,
+                  device_plugin_dir=str(short_tmp / "kubelet" / "device-plugins"), cdi_dir=str(short_tmp / "cdi"))
+    drv = DraDriver(env)
+    drv.serve()
+    sock = str(short_tmp / "podres" / "kubelet.sock")
+    kl = FakeKubelet(str(short_tmp / "dp"), sock)
+    kl.start()
+    src = SmiSource()
+    try:
+        drv.publish()
+        k = fakedra.FakeDraKubelet(str(short_tmp / "kubelet"))
+        k.discover()
+        claim = fakedra.allocate(c, c.create(_claim("train", 1)), "box")
+        out = k.prepare(api.DRIVER_NAME, [claim])[claim["metadata"]["uid"]]
+        assert not out.error
+        kl.record_claims("ml", "trainer", "main", [{"claim": ("default", "train"), "resources": [
+            (api.DRIVER_NAME, d.pool_name, d.device_name, list(d.cdi_device_ids)) for d in out.devices]}])
+        held = drv.by_name[out.devices[0].device_name]
+        ex = MetricsExporter(src, "box", attribution=PodAttribution(sock, dra_driver=api.DRIVER_NAME,
+                                                                     resolve=device_id_resolver("/")))
+        ex.collect_once()
+        assert ex.errors == 0
+        lines = [ln for ln in ex.render().splitlines() if ln.startswith("amd_gpu_power_watts{")]
+        print("\n".join(lines))
+        mine = [ln for ln in lines if f'bdf="{held.bdf}"' in ln]
+        assert mine and all('pod="trainer"' in ln and 'namespace="ml"' in ln for ln in mine), (held.bdf, lines)
+        assert not any('pod="trainer"' in ln for ln in lines if ln not in mine)
+    finally:
+        src.close()
+        kl.stop()
+        drv.stop()
+
+
 def test_partition_change_republishes_with_a_new_generation(node):
     env, drv, _ = node
     assert not drv.refresh()

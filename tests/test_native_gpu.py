@@ -224,6 +224,7 @@ def test_metrics_exporter_live():
         text = ex.render()
         assert "amd_gpu_vram_total_bytes{" in text and "amd_gpu_power_watts{" in text
         assert ex.errors == 0
+        assert 'product="AMD-Instinct-MI355X"' in text  # not libdrm's generic name
     finally:
         src.close()
 
