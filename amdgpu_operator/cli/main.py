@@ -171,6 +171,10 @@ def main(argv: list[str] | None = None) -> int:
     _common(ve)
     ve.add_argument("--json", action="store_true")
     ve.add_argument("--expect-gpus", type=int, default=None)
+    ve.add_argument("--run-pod", action="store_true",
+                    help="also run one 1-GPU pod per GPU node (device plugin or DRA claim) and require it to succeed")
+    ve.add_argument("--pod-image", default="amd-operator-validator")
+    ve.add_argument("--pod-timeout", type=float, default=120.0)
     rn = sub.add_parser("render", help="render the Helm chart (helm template)")
     rn.add_argument("--set", action="append", default=[])
     rn.add_argument("--namespace", default=DEFAULT_NAMESPACE)
@@ -263,7 +267,8 @@ def main(argv: list[str] | None = None) -> int:
     if args.cmd == "verify":
         from .verify import main_verify
 
-        return main_verify(_client(args), args.namespace, args.json, args.expect_gpus)
+        return main_verify(_client(args), args.namespace, args.json, args.expect_gpus, args.run_pod,
+                           args.pod_image, args.pod_timeout)
     if args.cmd == "render":
         import yaml
 

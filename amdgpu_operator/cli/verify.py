@@ -15,6 +15,10 @@ exec ... -c nvidia-driver-ctr -- nvidia-smi (:152)      amd-driver-ctr present, 
                                                         temperature for every GPU (the health
                                                         container's amd.com/gpu.driver-smi)
 (validator "Completed", :199)                           node labelled amd.com/gpu.validated
+(``--run-pod``: a user's first GPU pod)                 per GPU node, one pod asking for one GPU
+                                                        (amd.com/gpu, or a ResourceClaim with the
+                                                        DRA driver) runs a kernel on exactly the
+                                                        GPU it was given and Succeeds
 =====================================================  =====================================
 
 Output: one JSON document (``--json``) or a table; exit 0 only if all pass.
@@ -23,6 +27,8 @@ Output: one JSON document (``--json``) or a table; exit 0 only if all pass.
 from __future__ import annotations
 
 import json
+import os
+import time
 from dataclasses import asdict, dataclass, field
 
 from .. import LABEL_PRESENT, RESOURCE_NAME
@@ -120,7 +126,58 @@ def _allocatable_check(rep: "Report", name: str, labels: dict, allocs: dict, exp
             "README.md:122")
 
 
-def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> Report:
+def run_gpu_pod(client, node: str, namespace: str, dra: bool, image: str = "amd-operator-validator",
+                timeout: float = 120.0) -> tuple[bool, str]:
+    """One pod on ``node`` asking for one GPU - through the device plugin
+    (``amd.com/gpu: 1``) or, with the DRA driver, a ResourceClaim for one
+    ``gpu.amd.com`` device - running ``amdgpu-gpu-check --expect-devices 1``
+    from the validator image; (passed, detail).  Pod and claim are deleted
+    afterwards."""
+    from ..dra.api import DRIVER_NAME
+
+    name = f"amd-gpu-verify-{os.urandom(3).hex()}"
+    ctr = {"name": "check", "image": image, "command": ["amdgpu-gpu-check"],
+           "args": ["--timeout", "30", "--expect-devices", "1"]}
+    spec = {"restartPolicy": "Never", "containers": [ctr]}
+    objs = []
+    if dra:
+        objs.append({"apiVersion": "resource.k8s.io/v1beta1", "kind": "ResourceClaim",
+                     "metadata": {"name": name, "namespace": namespace},
+                     "spec": {"devices": {"requests": [{"name": "gpu", "deviceClassName": DRIVER_NAME}]}}})
+        spec["nodeSelector"] = {"kubernetes.io/hostname": node}
+        spec["resourceClaims"] = [{"name": "gpu", "resourceClaimName": name}]
+        ctr["resources"] = {"claims": [{"name": "gpu"}]}
+    else:
+        spec["nodeSelector"] = {"kubernetes.io/hostname": node}
+        spec["tolerations"] = [{"key": RESOURCE_NAME, "operator": "Exists", "effect": "NoSchedule"}]
+        ctr["resources"] = {"limits": {RESOURCE_NAME: "1"}}
+    objs.append({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": namespace,
+                                                                  "labels": {"app": "amd-gpu-verify"}}, "spec": spec})
+    t0 = time.monotonic()
+    try:
+        for o in objs:
+            client.create(o)
+        phase, st = "Pending", {}
+        while time.monotonic() - t0 < timeout:
+            st = client.get("v1", "Pod", name, namespace).get("status") or {}
+            phase = st.get("phase", "Pending")
+            if phase in ("Succeeded", "Failed"):
+                break
+            time.sleep(0.05)
+        detail = f"{'dra claim' if dra else RESOURCE_NAME + '=1'}: {phase} in {time.monotonic() - t0:.2f} s"
+        if phase != "Succeeded" and st.get("message"):
+            detail += f" ({st['message'][:300]})"
+        return phase == "Succeeded", detail
+    finally:
+        for o in reversed(objs):
+            try:
+                client.delete(o["apiVersion"], o["kind"], name, namespace)
+            except Exception:  # noqa: BLE001 - already gone
+                pass
+
+
+def verify(client, namespace: str, expect_gpus_per_node: int | None = None, run_pods: bool = False,
+           pod_image: str = "amd-operator-validator", pod_timeout: float = 120.0) -> Report:
     rep = Report()
     nodes = client.list("v1", "Node")
     not_ready = [n["metadata"]["name"] for n in nodes
@@ -186,6 +243,10 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
             smi = (n["metadata"].get("annotations") or {}).get(DRIVER_SMI_ANN, "")
             rep.add(f"driver-smi[{name}]", smi.startswith("ok"), smi or "not reported by amd-driver-health",
                     "README.md:152-167")
+        if run_pods:
+            ok, detail = run_gpu_pod(client, name, namespace, bool((spec.get("draDriver") or {}).get("enabled")),
+                                     pod_image, pod_timeout)
+            rep.add(f"gpu-pod[{name}]", ok, detail, "README.md:147-152 (a GPU workload runs)")
 
     pods = client.list("v1", "Pod", namespace)
     bad = []
@@ -222,7 +283,8 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None) -> R
     return rep
 
 
-def main_verify(client, namespace: str, as_json: bool, expect: int | None) -> int:
-    rep = verify(client, namespace, expect)
+def main_verify(client, namespace: str, as_json: bool, expect: int | None, run_pods: bool = False,
+                pod_image: str = "amd-operator-validator", pod_timeout: float = 120.0) -> int:
+    rep = verify(client, namespace, expect, run_pods, pod_image, pod_timeout)
     print(json.dumps(rep.as_dict(), indent=1) if as_json else rep.table())
     return 0 if rep.ok else 1

@@ -131,3 +131,28 @@ def test_dra_examples_run(short_tmp):
         c.client.delete(RV1B1, "ResourceClaim", "shared-mi355x", "default")
     finally:
         c.stop()
+
+
+@pytest.mark.parametrize("dra", [False, True], ids=["device-plugin", "dra"])
+def test_verify_run_pod(short_tmp, dra):
+    """``amdgpu-operator verify --run-pod``: per GPU node one 1-GPU pod (an
+    amd.com/gpu limit, or a ResourceClaim with the DRA driver) must succeed;
+    it leaves no pod or claim behind."""
+    from amdgpu_operator.cli.verify import verify
+    from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
+
+    flags = REFERENCE_SET_FLAGS + (["draDriver.enabled=true", "devicePlugin.enabled=false"] if dra else [])
+    c = SimCluster(str(short_tmp / "c"), [NodeSpec("gpu-1", 4), NodeSpec("gpu-2", 2)], fake_gpu=True).start()
+    try:
+        c.install_operator(parse_set_flags(flags))
+        c.wait_ready(60, {} if dra else {"gpu-1": 4, "gpu-2": 2})
+        rep = verify(c.client, c.namespace, run_pods=True, pod_timeout=30)
+        pods = [x for x in rep.checks if x.name.startswith("gpu-pod[")]
+        assert rep.ok and len(pods) == 2, rep.table()
+        assert all(("dra claim" if dra else "amd.com/gpu=1") in x.detail for x in pods), rep.table()
+        assert not [p for p in c.client.list("v1", "Pod", c.namespace)
+                    if p["metadata"]["name"].startswith("amd-gpu-verify-")
+                    and not p["metadata"].get("deletionTimestamp")]
+        assert not c.client.list(RV1B1, "ResourceClaim")
+    finally:
+        c.stop()
