@@ -251,6 +251,12 @@ def test_sim_cluster_on_real_gpu(mode):
         wl = read_ready(c.nodes["node-0"].env, "workload")
         gemm = [s for s in wl["ranks"][0]["steps"] if s["name"] == "gemm"][0]
         assert gemm["counter_gate"] == "pass"
+        if mode == "process":  # verify --run-pod: a user's 1-GPU pod runs its kernel on the MI355X
+            from amdgpu_operator.cli.verify import verify
+
+            rep = verify(c.client, c.namespace, run_pods=True, pod_timeout=60)
+            pod = next(x for x in rep.checks if x.name == "gpu-pod[node-0]")
+            assert pod.ok, rep.table()
     finally:
         c.stop()
 
