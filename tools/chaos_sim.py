@@ -16,6 +16,15 @@ Ready again with the allocatable each node's workload implies:
   noop        (--inject-noop only) claims to revalidate but does nothing: the
               harness must catch it
 
+With ``--dra`` the GPUs are advertised by the DRA driver instead of the
+device plugin (draDriver.enabled, devicePlugin.enabled=false): Ready means
+the node's ResourceSlice lists every device (2 or 16 per node), a kubelet
+restart makes the plugin watcher register the driver again, there is no
+vm-passthrough switch, and one more fault runs a user's workload:
+
+  claimpod    a ResourceClaim for one device and a pod using it (amdgpu-gpu-check
+              --expect-devices 1) must Succeed; both are deleted again
+
 Ready again is not enough to pass a step: a fault that must revalidate the
 node (validator pod deleted, driver loss, partition change, driver upgrade,
 workload switch) must leave a strictly newer validation record on it - the
@@ -33,6 +42,7 @@ diagnostics; exits 1 if any seed failed.
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import os
 import random
 import sys
@@ -52,6 +62,44 @@ REVALIDATE = ("driverloss", "partition", "partbusy", "upgrade", "switch", "noop"
 
 
 REAL_GPU_FAULTS = ("delpod", "delpod", "kubelet", "spec")  # no root on a GPU box: no module, PCI or partition changes
+DRA_FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "spec", "upgrade", "partition", "partbusy", "claimpod",
+              "claimpod")
+REAL_GPU_DRA_FAULTS = ("delpod", "delpod", "kubelet", "spec", "claimpod")
+RV1B1 = "resource.k8s.io/v1beta1"
+
+
+def slice_devices(c, node: str) -> int:
+    try:
+        return len((c.client.get(RV1B1, "ResourceSlice", f"{node}-gpu.amd.com").get("spec") or {}).get("devices") or [])
+    except Exception:  # noqa: BLE001 - not published (yet)
+        return 0
+
+
+def claim_pod(c, node: str, timeout: float) -> tuple[bool, str]:
+    """A user's one-GPU DRA workload on ``node``: claim + pod, Succeeded?"""
+    name = f"chaos-{os.urandom(3).hex()}"
+    c.client.create({"apiVersion": RV1B1, "kind": "ResourceClaim", "metadata": {"name": name, "namespace": "default"},
+                     "spec": {"devices": {"requests": [{"name": "gpu", "deviceClassName": "gpu.amd.com"}]}}})
+    c.client.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+                     "spec": {"restartPolicy": "Never", "nodeSelector": {"kubernetes.io/hostname": node},
+                              "resourceClaims": [{"name": "gpu", "resourceClaimName": name}],
+                              "containers": [{"name": "check", "image": "amd-operator-validator",
+                                              "command": ["amdgpu-gpu-check"],
+                                              "args": ["--timeout", "30", "--expect-devices", "1"],
+                                              "resources": {"claims": [{"name": "gpu"}]}}]}})
+    deadline = time.time() + timeout
+    st = {}
+    while time.time() < deadline:
+        st = c.client.get("v1", "Pod", name, "default").get("status") or {}
+        if st.get("phase") in ("Succeeded", "Failed"):
+            break
+        time.sleep(0.05)
+    for kind in (("v1", "Pod"), (RV1B1, "ResourceClaim")):
+        try:
+            c.client.delete(*kind, name, "default")
+        except Exception:  # noqa: BLE001
+            pass
+    return st.get("phase") == "Succeeded", f"{name} {st.get('phase')} {st.get('message', '')[:200]}"
 
 
 def validation_record(c, node: str) -> dict:
@@ -71,7 +119,8 @@ def gemm_gate_passed(record: dict) -> bool:
 
 
 def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: bool = False,
-             real_gpu: bool = False, inject_noop: int = -1, processes: bool = False, rbac: bool = False) -> bool:
+             real_gpu: bool = False, inject_noop: int = -1, processes: bool = False, rbac: bool = False,
+             dra: bool = False) -> bool:
     rnd = random.Random(seed)
     d = tempfile.mkdtemp(prefix="chaos-")
     if real_gpu:  # one node, this machine's GPU(s): every validation runs on the real device
@@ -96,17 +145,31 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
                                                              PM.sysfs_partition_rebuilder(env.host_root, 2),
                                                              validations_dir=env.validations_dir)
 
+    def devices(n):
+        return 8 * n_gpus if cpx[n] else n_gpus
+
     def expect():
-        return {n: ((8 * n_gpus if cpx[n] else n_gpus) if m == "container" else {"amd.com/MI355X": n_gpus})
-                for n, m in mode.items()}
+        if dra:  # no amd.com/gpu: the slice is checked instead (wait_ready below)
+            return {}
+        return {n: (devices(n) if m == "container" else {"amd.com/MI355X": n_gpus}) for n, m in mode.items()}
+
+    def wait_ready():
+        c.wait_ready(timeout, expect())
+        deadline = time.time() + timeout
+        while dra and any(slice_devices(c, n) != devices(n) for n in gpu_nodes):
+            if time.time() > deadline:
+                raise TimeoutError(f"ResourceSlices {[(n, slice_devices(c, n), devices(n)) for n in gpu_nodes]}")
+            time.sleep(0.05)
 
     try:
         extra = [] if real_gpu else ["migManager.enabled=true"]
+        extra += ["draDriver.enabled=true", "devicePlugin.enabled=false"] if dra else []
         c.install_operator(deep_merge(parse_set_flags(REFERENCE_SET_FLAGS + extra),
-                                      {} if real_gpu else {"sandboxWorkloads": {"enabled": True}}))
-        c.wait_ready(timeout, expect())
+                                      {} if real_gpu or dra else {"sandboxWorkloads": {"enabled": True}}))
+        wait_ready()
+        faults = (REAL_GPU_DRA_FAULTS if dra else REAL_GPU_FAULTS) if real_gpu else (DRA_FAULTS if dra else FAULTS)
         for i in range(steps):
-            fault, node = rnd.choice(REAL_GPU_FAULTS if real_gpu else FAULTS), rnd.choice(gpu_nodes)
+            fault, node = rnd.choice(faults), rnd.choice(gpu_nodes)
             if i == inject_noop:
                 fault = "noop"
             info = ""
@@ -125,10 +188,18 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
                 env = c.nodes[node].env
                 f = os.path.join(env.host_root, "sys/module/amdgpu/initstate")
                 os.rename(f, f + ".gone")
-                monitor_once(env)  # the driver container's health monitor notices
+                # the driver container's health monitor notices (run here with the harness's own
+                # client: under --rbac the node env's HTTP client carries no ServiceAccount token)
+                monitor_once(dataclasses.replace(env, client=c.client))
                 os.rename(f + ".gone", f)
             elif fault == "kubelet":
                 c.nodes[node].kubelet.restart()
+                c.nodes[node].dra = None  # the plugin watcher starts over and registers the DRA driver again
+            elif fault == "claimpod":
+                ok, info = claim_pod(c, node, timeout)
+                if not ok:
+                    print(f"seed {seed} step {i} claimpod {node}: the workload did not succeed: {info}", flush=True)
+                    return False
             elif fault == "switch":
                 mode[node] = "vm-passthrough" if mode[node] == "container" else "container"
                 c.client.patch("v1", "Node", node, {"metadata": {"labels": {WORKLOAD_CONFIG_LABEL: mode[node]}}})
@@ -181,13 +252,14 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
                             (c.client.get("v1", "Node", n)["metadata"].get("annotations") or {}).get(
                                 "amd.com/gpu-driver.version") == want for n, m in mode.items() if m == "container"):
                         time.sleep(0.05)
-                c.wait_ready(timeout, expect())
+                wait_ready()
                 # the fault must have landed: a fresh validation of every node it concerns
                 deadline = time.time() + timeout
                 while time.time() < deadline and any(validation_record(c, n)["time"] <= before[n] for n in must):
                     time.sleep(0.05)
-                    c.wait_ready(timeout, expect())
-                while fault == "kubelet" and time.time() < deadline and c.nodes[node].kubelet.register_calls <= regs_before:
+                    wait_ready()
+                while fault == "kubelet" and not dra and time.time() < deadline \
+                        and c.nodes[node].kubelet.register_calls <= regs_before:
                     time.sleep(0.05)  # the plugin sees the new kubelet.sock within its watch interval
             except TimeoutError as e:
                 print(f"seed {seed} step {i} {fault} {node} {info}: NOT READY after {timeout:.0f} s\n{e}", flush=True)
@@ -202,7 +274,10 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
             if real_gpu and must and not all(gemm_gate_passed(validation_record(c, n)) for n in must):
                 print(f"seed {seed} step {i} {fault} {node}: revalidated without a passing GEMM counter gate", flush=True)
                 return False
-            if fault == "kubelet" and c.nodes[node].kubelet.register_calls <= regs_before:
+            if fault == "kubelet" and dra and claim_pod(c, node, timeout)[0] is False:
+                print(f"seed {seed} step {i} kubelet {node}: no DRA workload after the restart", flush=True)
+                return False
+            if fault == "kubelet" and not dra and c.nodes[node].kubelet.register_calls <= regs_before:
                 print(f"seed {seed} step {i} kubelet {node}: the device plugin did not register again", flush=True)
                 return False
             reval = " ".join(f"{n} revalidated +{validation_record(c, n)['time'] - t_fault:.2f} s" for n in sorted(must))
@@ -229,13 +304,16 @@ def main() -> int:
                     help="the operator and every operand container as its own process (bench.py's headline mode)")
     ap.add_argument("--rbac", action="store_true",
                     help="with --processes: every request authorized against the shipped roles (kube/rbac.py)")
+    ap.add_argument("--dra", action="store_true",
+                    help="the DRA driver advertises the GPUs (device plugin off); adds the claimpod fault")
     ap.add_argument("--inject-noop", type=int, default=-1, metavar="STEP",
                     help="make step STEP a no-op fault that claims a revalidation (the harness must fail)")
     a = ap.parse_args()
     if a.rbac and not a.processes:
         ap.error("--rbac needs --processes (a ServiceAccount per operand process)")
     lo, _, hi = a.seeds.partition("-")
-    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api, a.real_gpu, a.inject_noop, a.processes, a.rbac)
+    ok = all([run_seed(s, a.steps, a.settle_s, a.timeout, a.http_api, a.real_gpu, a.inject_noop, a.processes, a.rbac,
+                        a.dra)
               for s in range(int(lo), int(hi or lo) + 1)])
     return 0 if ok else 1
 
