@@ -188,6 +188,7 @@ def main(argv: list[str] | None = None) -> int:
     sm.add_argument("--nodes", type=int, default=1, help="GPU nodes in the simulated cluster")
     sm.add_argument("--http-api", action="store_true",
                     help="operator and operands talk to the API server over HTTP (RestClient), as in a cluster")
+    sm.add_argument("--run-pod", action="store_true", help="verify --run-pod after the bring-up (a 1-GPU pod per node)")
     pf = sub.add_parser("preflight", help="check (and --fix) a node's prerequisites before kubeadm join")
     pf.add_argument("--root", default="/")
     pf.add_argument("--fix", action="store_true")
@@ -293,7 +294,7 @@ def main(argv: list[str] | None = None) -> int:
         try:
             c.install_operator(parse_set_flags(args.set))
             ttr = c.wait_ready(args.timeout)
-            rep = verify(c.agent_client, c.namespace)
+            rep = verify(c.agent_client, c.namespace, run_pods=args.run_pod)
             print(json.dumps({"time_to_ready_s": round(ttr, 4), "nodes": args.nodes, "http_api": args.http_api,
                               "verify": rep.as_dict()}, indent=1))
             return 0 if rep.ok else 1
