@@ -25,3 +25,12 @@ def test_a_fault_that_does_not_land_fails_the_harness():
     import chaos_sim
 
     assert not chaos_sim.run_seed(1, steps=2, settle_s=0.1, timeout=3.0, inject_noop=1)
+
+
+def test_dra_cluster_converges_after_each_fault():
+    """The same with the DRA driver advertising the GPUs: Ready includes each
+    node's ResourceSlice listing its devices (2 or 16 after a partition
+    change), and claimpod faults run a user's claim workload in between."""
+    import chaos_sim
+
+    assert chaos_sim.run_seed(51, steps=6, settle_s=0.3, timeout=60.0, dra=True)
