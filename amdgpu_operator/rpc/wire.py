@@ -587,9 +587,9 @@ class Server:
 
     def _on_end(self, conn: Connection, st: _Stream) -> None:
         th = threading.Thread(target=self._run_call, args=(conn, st), name=f"{self.name}-call", daemon=True)
-        with self._lock:
+        with self._lock:  # registered and started together: stop() never joins a thread not yet started
             self._calls.add(th)
-        th.start()
+            th.start()
 
     def _run_call(self, conn: Connection, st: _Stream) -> None:
         try:
