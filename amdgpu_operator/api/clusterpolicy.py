@@ -532,3 +532,27 @@ REFERENCE_SET_FLAGS = [
     "migManager.enabled=false",
     "operator.cleanupCRD=true",
 ]
+
+
+def policy_images(spec: ClusterPolicySpec | dict) -> dict[str, str]:
+    """Every image the policy can run, by spec path (``driver``,
+    ``validator``, ...): what a node pulls, what an air-gapped registry must
+    mirror, and what the simulated kubelet can pull (testing/simcluster.py)."""
+    if isinstance(spec, dict):
+        spec = ClusterPolicySpec.model_validate(spec)
+    out = {}
+    for name in type(spec).model_fields:
+        v = getattr(spec, name)
+        if isinstance(v, Image):
+            out[name] = v.ref(v.image)
+    return out
+
+
+def validator_pod_image(spec: ClusterPolicySpec | dict) -> dict:
+    """The image a GPU check pod runs (plugin validation, ``verify --run-pod``,
+    the example workloads): the validator's, with its pull policy and pull
+    secrets - the same resolution the operand DaemonSets use."""
+    if isinstance(spec, dict):
+        spec = ClusterPolicySpec.model_validate(spec)
+    v = spec.validator
+    return {"image": v.ref(v.image), "pull_policy": v.imagePullPolicy, "pull_secrets": list(v.imagePullSecrets)}

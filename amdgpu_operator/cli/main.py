@@ -173,7 +173,8 @@ def main(argv: list[str] | None = None) -> int:
     ve.add_argument("--expect-gpus", type=int, default=None)
     ve.add_argument("--run-pod", action="store_true",
                     help="also run one 1-GPU pod per GPU node (device plugin or DRA claim) and require it to succeed")
-    ve.add_argument("--pod-image", default="amd-operator-validator")
+    ve.add_argument("--pod-image", default=None,
+                    help="image of the --run-pod pod (default: the ClusterPolicy's validator image)")
     ve.add_argument("--pod-timeout", type=float, default=120.0)
     rn = sub.add_parser("render", help="render the Helm chart (helm template)")
     rn.add_argument("--set", action="append", default=[])

@@ -52,6 +52,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="plugin: one pod per resource holding all its devices, or one 1-device pod per device")
     v.add_argument("--dra", action="store_true",
                    help="gpu: the GPUs are advertised by the DRA driver: validate a ResourceClaim + pod instead")
+    v.add_argument("--dra-device-class", default=None,
+                   help="the DeviceClass the DRA validation claim asks for (draDriver.deviceClass)")
     v.add_argument("--wait-toolkit", action="store_true",
                    help="gpu: plugin validation waits for the toolkit; the workload starts right away")
     v.add_argument("--with-driver", action="store_true",
@@ -181,7 +183,7 @@ def _validate(env, a, extra, stop, ready) -> int:
             V.validate_workload(env, extra, a.timeout)
     elif a.step == "plugin" and a.dra:
         if V.read_ready(env, "plugin") is None:
-            V.validate_dra(env, a.timeout, stop)
+            V.validate_dra(env, a.timeout, stop, device_class=a.dra_device_class)
     elif a.step == "plugin":
         if V.read_ready(env, "plugin") is None:
             pod_args = _plugin_pod_args(extra)
@@ -192,7 +194,8 @@ def _validate(env, a, extra, stop, ready) -> int:
         V.validate_gpu(env, extra, a.resource, _plugin_pod_args(extra), a.timeout, stop,
                        wait_toolkit=a.wait_toolkit, with_driver=a.with_driver,
                        partition_strategy=a.partition_strategy, pod_check=a.pod_check,
-                       per_device=a.plugin_pods == "perDevice", dra=a.dra)
+                       per_device=a.plugin_pods == "perDevice", dra=a.dra, dra_device_class=a.dra_device_class)
+        V.clear_failure(env, "gpu")  # a previous attempt's record (the main container stays up below)
         if a.complete:
             return _complete(env, stop, ready)
     elif a.step == "vfio":
@@ -248,7 +251,8 @@ def _split_passthrough(args: list[str]) -> tuple[list[str], list[str]]:
     i = 0
     while i < len(args):
         a = args[i]
-        if a in ("--resource", "--timeout", "--partition-strategy", "--pod-check", "--plugin-pods"):
+        if a in ("--resource", "--timeout", "--partition-strategy", "--pod-check", "--plugin-pods",
+                 "--dra-device-class"):
             known += args[i:i + 2]
             i += 2
             continue
@@ -344,9 +348,12 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
                 "image": cenv["VALIDATOR_IMAGE"], "pull_policy": cenv.get("VALIDATOR_IMAGE_PULL_POLICY"),
                 "pull_secrets": [x for x in cenv.get("VALIDATOR_IMAGE_PULL_SECRETS", "").split(",") if x]}
         try:
-            return _validate(env, a, extra, stop, ready)
+            rc = _validate(env, a, extra, stop, ready)
+            V.clear_failure(env, a.step)
+            return rc
         except V.StepFailed as e:
             if not stop.is_set():  # a pod being deleted is not a failed validation
+                V.write_failure(env, a.step, {"message": str(e)[:2000]})
                 _node_event(env, "Warning", "ValidationFailed", f"{a.step} validation failed: {e}")
             raise
 

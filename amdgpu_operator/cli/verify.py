@@ -126,24 +126,50 @@ def _allocatable_check(rep: "Report", name: str, labels: dict, allocs: dict, exp
             "README.md:122")
 
 
-def run_gpu_pod(client, node: str, namespace: str, dra: bool, image: str = "amd-operator-validator",
-                timeout: float = 120.0) -> tuple[bool, str]:
+def pod_image_of(spec: dict, override: str | None = None) -> dict:
+    """The image a verification pod runs: the live ClusterPolicy's validator
+    image (``{repository}/{image}:{version}``, its pull policy and pull
+    secrets: api/clusterpolicy.py validator_pod_image, as the validator's own
+    plugin pods), or ``override`` (``--pod-image``) with the policy's pull
+    settings.  A bare name would be pulled from Docker Hub on a cluster."""
+    from ..api.clusterpolicy import ClusterPolicySpec, validator_pod_image
+
+    try:
+        img = validator_pod_image(ClusterPolicySpec.model_validate(spec or {}))
+    except Exception:  # noqa: BLE001 - a policy this version cannot parse: its validator block only
+        v = (spec or {}).get("validator") or {}
+        from ..api.clusterpolicy import DEFAULT_REPOSITORY, DEFAULT_VERSION
+
+        img = {"image": f"{v.get('repository', DEFAULT_REPOSITORY)}/{v.get('image') or 'amd-operator-validator'}:"
+                        f"{v.get('version', DEFAULT_VERSION)}",
+               "pull_policy": v.get("imagePullPolicy", "IfNotPresent"), "pull_secrets": v.get("imagePullSecrets") or []}
+    if override:
+        img["image"] = override
+    return img
+
+
+def run_gpu_pod(client, node: str, namespace: str, dra: bool, image: str | dict,
+                timeout: float = 120.0, device_class: str | None = None) -> tuple[bool, str]:
     """One pod on ``node`` asking for one GPU - through the device plugin
     (``amd.com/gpu: 1``) or, with the DRA driver, a ResourceClaim for one
-    ``gpu.amd.com`` device - running ``amdgpu-gpu-check --expect-devices 1``
-    from the validator image; (passed, detail).  Pod and claim are deleted
-    afterwards."""
+    device of the policy's DeviceClass - running ``amdgpu-gpu-check
+    --expect-devices 1`` from the validator image (:func:`pod_image_of`);
+    (passed, detail).  Pod and claim are deleted afterwards."""
     from ..dra.api import DRIVER_NAME
 
+    img = image if isinstance(image, dict) else {"image": image}
     name = f"amd-gpu-verify-{os.urandom(3).hex()}"
-    ctr = {"name": "check", "image": image, "command": ["amdgpu-gpu-check"],
-           "args": ["--timeout", "30", "--expect-devices", "1"]}
+    ctr = {"name": "check", "image": img["image"], "imagePullPolicy": img.get("pull_policy") or "IfNotPresent",
+           "command": ["amdgpu-gpu-check"], "args": ["--timeout", "30", "--expect-devices", "1"]}
     spec = {"restartPolicy": "Never", "containers": [ctr]}
+    if img.get("pull_secrets"):
+        spec["imagePullSecrets"] = [{"name": x} for x in img["pull_secrets"]]
     objs = []
     if dra:
         objs.append({"apiVersion": "resource.k8s.io/v1beta1", "kind": "ResourceClaim",
                      "metadata": {"name": name, "namespace": namespace},
-                     "spec": {"devices": {"requests": [{"name": "gpu", "deviceClassName": DRIVER_NAME}]}}})
+                     "spec": {"devices": {"requests": [{"name": "gpu",
+                                                        "deviceClassName": device_class or DRIVER_NAME}]}}})
         spec["nodeSelector"] = {"kubernetes.io/hostname": node}
         spec["resourceClaims"] = [{"name": "gpu", "resourceClaimName": name}]
         ctr["resources"] = {"claims": [{"name": "gpu"}]}
@@ -167,6 +193,10 @@ def run_gpu_pod(client, node: str, namespace: str, dra: bool, image: str = "amd-
         detail = f"{'dra claim' if dra else RESOURCE_NAME + '=1'}: {phase} in {time.monotonic() - t0:.2f} s"
         if phase != "Succeeded" and st.get("message"):
             detail += f" ({st['message'][:300]})"
+        waiting = [((c.get("state") or {}).get("waiting") or {}) for c in st.get("containerStatuses") or []]
+        if phase != "Succeeded" and any(w.get("reason") for w in waiting):  # ErrImagePull, ImagePullBackOff, ...
+            w = next(w for w in waiting if w.get("reason"))
+            detail += f" ({w['reason']}: {str(w.get('message', ''))[:300]}; image {img['image']})"
         return phase == "Succeeded", detail
     finally:
         for o in reversed(objs):
@@ -177,7 +207,7 @@ def run_gpu_pod(client, node: str, namespace: str, dra: bool, image: str = "amd-
 
 
 def verify(client, namespace: str, expect_gpus_per_node: int | None = None, run_pods: bool = False,
-           pod_image: str = "amd-operator-validator", pod_timeout: float = 120.0) -> Report:
+           pod_image: str | None = None, pod_timeout: float = 120.0) -> Report:
     rep = Report()
     nodes = client.list("v1", "Node")
     not_ready = [n["metadata"]["name"] for n in nodes
@@ -244,8 +274,9 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None, run_
             rep.add(f"driver-smi[{name}]", smi.startswith("ok"), smi or "not reported by amd-driver-health",
                     "README.md:152-167")
         if run_pods:
-            ok, detail = run_gpu_pod(client, name, namespace, bool((spec.get("draDriver") or {}).get("enabled")),
-                                     pod_image, pod_timeout)
+            dra = (spec.get("draDriver") or {})
+            ok, detail = run_gpu_pod(client, name, namespace, bool(dra.get("enabled")), pod_image_of(spec, pod_image),
+                                     pod_timeout, dra.get("deviceClass"))
             rep.add(f"gpu-pod[{name}]", ok, detail, "README.md:147-152 (a GPU workload runs)")
 
     pods = client.list("v1", "Pod", namespace)
@@ -284,7 +315,7 @@ def verify(client, namespace: str, expect_gpus_per_node: int | None = None, run_
 
 
 def main_verify(client, namespace: str, as_json: bool, expect: int | None, run_pods: bool = False,
-                pod_image: str = "amd-operator-validator", pod_timeout: float = 120.0) -> int:
+                pod_image: str | None = None, pod_timeout: float = 120.0) -> int:
     rep = verify(client, namespace, expect, run_pods, pod_image, pod_timeout)
     print(json.dumps(rep.as_dict(), indent=1) if as_json else rep.table())
     return 0 if rep.ok else 1

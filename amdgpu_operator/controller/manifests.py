@@ -354,7 +354,7 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     # the GPUs' advertiser: the device plugin, or the DRA driver (a claim and a pod through the scheduler)
     advertiser = spec.devicePlugin.enabled or spec.draDriver.enabled
     if spec.draDriver.enabled:
-        plugin_res.append("--dra")
+        plugin_res += ["--dra", "--dra-device-class", spec.draDriver.deviceClass]
     if v.pluginValidation and advertiser and w.prespawn:
         # one init container validates the driver and, meanwhile, starts the
         # workload processes behind their start gate (validate.py validate_gpu)

@@ -69,12 +69,13 @@ def driver_spec_hash(spec: ClusterPolicySpec) -> str:
     return hashlib.sha1(json.dumps(key, sort_keys=True).encode()).hexdigest()[:16]
 
 
-def _uses_gpu(pod: dict) -> bool:
-    for c in (pod.get("spec") or {}).get("containers", []):
-        lim = ((c.get("resources") or {}).get("limits") or {})
-        if any(k.startswith("amd.com/gpu") for k in lim):
-            return True
-    return False
+def _uses_gpu(pod: dict, client=None) -> bool:
+    """amd.com/gpu or a gpu.amd.com DRA claim (wellknown.uses_gpu): an amdgpu
+    unload finds the module busy while either kind runs."""
+    from ..wellknown import uses_gpu
+
+    get = (lambda ns, n: client.get("resource.k8s.io/v1beta1", "ResourceClaim", n, ns)) if client is not None else None
+    return uses_gpu(pod, get)
 
 
 class DriverUpgradeController:
@@ -111,7 +112,8 @@ class DriverUpgradeController:
                 self.events.record(node, NORMAL, "DriverUpgrade", f"driver upgrade: {state}")
 
     def _gpu_pods(self, node_name: str) -> list[dict]:
-        return [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={node_name}") if _uses_gpu(p)]
+        return [p for p in self.client.list("v1", "Pod", field_selector=f"spec.nodeName={node_name}")
+                if _uses_gpu(p, self.client)]
 
     def _delete_pod(self, pod: dict, grace: int | None = None) -> None:
         try:

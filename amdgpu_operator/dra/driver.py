@@ -15,8 +15,11 @@ Allocation (dra/api.py has the wire API):
 3. **Prepare** a claim the scheduler allocated on this node: read it from the
    API server (uid checked), take the results for this driver and pool, and
    write a CDI spec for the claim (``gpu.amd.com/claim=<uid>-<device>``: the
-   device's render node, ``/dev/kfd``, ``AMD_VISIBLE_DEVICES``), returned as
-   the claim's CDI device ids - the container runtime injects them.  Prepared
+   device's render node, ``/dev/kfd``), returned as the claim's CDI device
+   ids - the container runtime injects them.  The spec sets no environment
+   variable: a container holding two claims gets both specs' edits, and two
+   values of one variable would leave it one of them (toolkit/cdi.py); the
+   device nodes compose, and ROCm finds the GPUs by them.  Prepared
    claims are checkpointed, so a repeated call (kubelet restart) answers the
    same and a driver restart keeps them; **unprepare** removes the spec.
 
@@ -124,10 +127,15 @@ class DraDriver:
             cur = c.get("resource.k8s.io/v1beta1", "ResourceSlice", name)
         except NotFound:
             return c.create(want)
-        if cur.get("spec") == want["spec"]:
-            return cur
+        gen = int(((cur.get("spec") or {}).get("pool") or {}).get("generation", 1))
+
+        def content(spec):  # what is published, apart from the pool's generation counter
+            return {**spec, "pool": {k: v for k, v in (spec.get("pool") or {}).items() if k != "generation"}}
+
+        if content(cur.get("spec") or {}) == content(want["spec"]):
+            return cur  # unchanged (a driver restart): the generation stays
         # new devices (a partition change): a new pool generation
-        want["spec"]["pool"]["generation"] = int(((cur.get("spec") or {}).get("pool") or {}).get("generation", 1)) + 1
+        want["spec"]["pool"]["generation"] = gen + 1
         want["metadata"]["resourceVersion"] = cur["metadata"].get("resourceVersion")
         return c.update(want)
 
@@ -174,9 +182,7 @@ class DraDriver:
 
     def _write_cdi(self, uid: str, devices: list[str]) -> list[str]:
         spec = {"cdiVersion": "0.6.0", "kind": CDI_KIND,
-                "containerEdits": {"deviceNodes": [{"path": "/dev/kfd", "type": "c", "permissions": "rw"}],
-                                   "env": ["AMD_VISIBLE_DEVICES=" + ",".join(str(self.by_name[d].index)
-                                                                               for d in devices)]},
+                "containerEdits": {"deviceNodes": [{"path": "/dev/kfd", "type": "c", "permissions": "rw"}]},
                 "devices": [{"name": f"{uid}-{d}", "containerEdits": {"deviceNodes": [
                     {"path": self.by_name[d].render_node, "type": "c", "permissions": "rw"}]}} for d in devices]}
         os.makedirs(self.env.cdi_dir, exist_ok=True)

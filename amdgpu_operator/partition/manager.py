@@ -320,18 +320,19 @@ def reconcile_node(env: NodeEnv, backend, profiles: dict, default: Profile,
         resume_operands(env, paused)
 
 
-def _uses_gpu(pod: dict) -> bool:
-    for c in (pod.get("spec") or {}).get("containers", []):
-        lim = ((c.get("resources") or {}).get("limits") or {})
-        if any(k.startswith("amd.com/gpu") for k in lim):
-            return True
-    return False
+def _uses_gpu(pod: dict, client=None) -> bool:
+    """A pod holding the node's GPUs: amd.com/gpu, or a gpu.amd.com DRA claim
+    (wellknown.uses_gpu) - a partition switch re-creates the devices both hold."""
+    from ..wellknown import uses_gpu
+
+    get = (lambda ns, n: client.get("resource.k8s.io/v1beta1", "ResourceClaim", n, ns)) if client is not None else None
+    return uses_gpu(pod, get)
 
 
 def evict_gpu_pods(env: NodeEnv) -> list[str]:
     out = []
     for pod in env.client.list("v1", "Pod", field_selector=f"spec.nodeName={env.node_name}"):
-        if _uses_gpu(pod):
+        if _uses_gpu(pod, env.client):
             env.client.delete("v1", "Pod", pod["metadata"]["name"], pod["metadata"].get("namespace"))
             out.append(f"{pod['metadata'].get('namespace')}/{pod['metadata']['name']}")
     return out
@@ -342,7 +343,7 @@ def wait_gpu_pods_gone(env: NodeEnv, timeout: float) -> bool:
     (they hold ``/dev/kfd`` until their containers exit)."""
     from ..kube.client import wait_for
 
-    _, ok = wait_for(env.client, "v1", "Pod", lambda pods: not any(_uses_gpu(p) for p in pods.values()),
+    _, ok = wait_for(env.client, "v1", "Pod", lambda pods: not any(_uses_gpu(p, env.client) for p in pods.values()),
                      field_selector=f"spec.nodeName={env.node_name}", timeout=timeout, poll_s=env.poll_s)
     return ok
 

@@ -145,6 +145,72 @@ class Rendezvous:
                 time.sleep(0.002)
 
 
+# The stand-in's fabric: every peer link at ~60 % of the MI355X xGMI nominal
+# (76 GB/s per direction), collectives on the alpha-beta shape the floors use
+# (validate.py RCCL_HALF_BW_BYTES).  Only the shape matters to the CPU tests:
+# numbers that pass the default floors, and fail floors set far above them.
+SIM_LINK_GBPS = 45.0
+SIM_LATENCY_US = 12.0
+
+
+def sim_busbw(world: int, nbytes: int) -> float:
+    return SIM_LINK_GBPS * max(1, world - 1) * nbytes / (nbytes + (16 << 20))
+
+
+def simulated_detail(step: str, argv: list[str], rank: int, world: int) -> dict:
+    """Extra report fields of a simulated step: the measured-rate fields the
+    native binary reports, from the model above, and the floor verdicts the
+    binary applies to them (``--min-rccl-busbw-gbps``, ``--min-xgmi-read-gbps``)."""
+    def arg(name, default):
+        return argv[argv.index(name) + 1] if name in argv else default
+
+    if step == "rccl" and world > 1:
+        nbytes = 4 * int(arg("--rccl-elems", str(1 << 24)))
+        bus = sim_busbw(world, nbytes)
+        floor = float(arg("--min-rccl-busbw-gbps", "0"))
+        ok = floor <= 0 or bus >= floor
+        return {"ok": ok, "world": world, "bytes": nbytes, "busbw_gbps": round(bus, 1), "min_busbw_gbps": floor,
+                "perf_ok": ok, "comm_init_s": 0.0}
+    if step == "xgmi" and world > 1:
+        read = SIM_LINK_GBPS * (world - 1)
+        floor = float(arg("--min-xgmi-read-gbps", "0"))
+        ok = floor <= 0 or read >= floor
+        return {"ok": ok, "peers": world, "peer_read_gbps": round(read, 1), "min_peer_read_gbps": floor,
+                "perf_ok": ok}
+    if step == "xgmi_links" and world > 1:
+        return {"world": world, "links": [{"peer": (rank + k) % world, "read_gbps": SIM_LINK_GBPS, "intact": True}
+                                          for k in range(1, world)], "min_read_gbps": SIM_LINK_GBPS}
+    if step == "sweep":
+        lo, hi, f = int(arg("--sweep-min-bytes", "8")), int(arg("--sweep-max-bytes", str(1 << 30))), \
+            int(arg("--sweep-factor", "4"))
+        ops = arg("--sweep-ops", "allreduce,allgather,reducescatter").split(",")
+        rows = []
+        for op in ("allreduce", "allgather", "reducescatter"):
+            if op not in ops:
+                continue
+            b = lo
+            sizes = []
+            while b <= hi:
+                sizes.append(b)
+                b *= f
+            if not sizes or sizes[-1] != hi:
+                sizes.append(hi)
+            last = None
+            for nbytes in sizes:
+                n = max(world, (nbytes // 4) // world * world) * 4
+                if n == last:  # as the native step: sizes below `world` floats round up to one tensor
+                    continue
+                last = n
+                factor = (2.0 if op == "allreduce" else 1.0) * (world - 1) / world if world > 1 else 0.0
+                peak = SIM_LINK_GBPS * max(1, world - 1)  # alpha-beta: latency + bytes on the wire / link rate
+                us = SIM_LATENCY_US + (n * factor if world > 1 else n) / (peak * 1e3)
+                algbw = n / (us * 1e-6) / 1e9
+                rows.append({"op": op, "bytes": n, "iters": 1, "us": round(us, 2), "algbw_gbps": round(algbw, 2),
+                             "busbw_gbps": round(algbw * factor, 2), "mismatches": 0})
+        return {"world": world, "comm_init_s": 0.0, "mismatches": 0, "rows": rows}
+    return {}
+
+
 def _fault(run_id: str, rank: int) -> str | None:
     spec = os.environ.get("AMDGPU_FAKE_VALIDATOR_FAULT", "")
     for item in filter(None, spec.split(",")):
@@ -205,7 +271,9 @@ def _main(argv: list[str]) -> int:
     recs = []
     for s in steps:
         for d in (range(ndev) if s in per_device and ndev > 1 else [None]):
-            recs.append({"name": s, "ok": True, "seconds": 0.0, "simulated": True, **({"device": d} if d is not None else {})})
+            recs.append({"name": s, "ok": True, "seconds": 0.0, "simulated": True, **({"device": d} if d is not None else {}),
+                         **simulated_detail(s, argv, rank, world)})
+    below = [r["name"] for r in recs if r.get("ok") is False]
     rep = {"ok": True, "simulated": True, "rank": rank, "world": world, "device": int(arg("--device", "0")),
            "owner_rank_env": os.environ.get("RANK"), "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES"),
            "rocr_visible_devices": os.environ.get("ROCR_VISIBLE_DEVICES"), "local_bdf": arg("--local-bdf", None),
@@ -217,8 +285,10 @@ def _main(argv: list[str]) -> int:
             while True:  # ends only through the abort file (or a kill)
                 rv.watch(rank)
                 time.sleep(0.005)
-        if world > 1 and ("rccl" in steps or "xgmi" in steps or "peers" in steps):
+        if world > 1 and any(s in steps for s in ("rccl", "xgmi", "peers", "sweep", "xgmi_links")):
             rv.barrier("rccl" if "rccl" in steps else "xgmi")  # like the RCCL unique-id exchange
+        if below:  # a measured rate under its floor (the native binary's perf_ok)
+            raise RuntimeError(f"step {below[0]} failed")
     except PeerError as e:
         rep.update(ok=False, error=str(e), failed_peer=e.peer, peer_state=e.state)
     except RuntimeError as e:

@@ -34,9 +34,12 @@ import os
 import time
 
 from .. import RESOURCE_NAME
+from ..api.clusterpolicy import DEFAULT_REPOSITORY, DEFAULT_VERSION, validator_pod_image
 
 POD_LABEL = "amd.com/pod-workload"
 
+
+DEFAULT_IMAGE = f"{DEFAULT_REPOSITORY}/amd-operator-validator:{DEFAULT_VERSION}"
 
 def _pct(xs: list[float], q: float) -> float | None:
     if not xs:
@@ -46,14 +49,14 @@ def _pct(xs: list[float], q: float) -> float | None:
 
 
 def _pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm_n: int,
-         resource: str = RESOURCE_NAME) -> dict:
+         resource: str = RESOURCE_NAME, image: str = DEFAULT_IMAGE) -> dict:
     return {
         "apiVersion": "v1", "kind": "Pod",
         "metadata": {"name": name, "namespace": namespace, "labels": {"app": "gpu-job", POD_LABEL: run_id}},
         "spec": {
             "nodeName": node, "restartPolicy": "Never",
             "tolerations": [{"key": resource, "operator": "Exists", "effect": "NoSchedule"}],
-            "containers": [{"name": "gemm", "image": "amd-operator-validator",
+            "containers": [{"name": "gemm", "image": image,
                             "command": ["amdgpu-validator"],
                             "args": ["--all-devices", "--expect-devices", str(count), "--steps", "hip,gemm",
                                      "--gemm", str(gemm_n), "--gemm-iters", "1"],
@@ -62,7 +65,8 @@ def _pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm_n: 
     }
 
 
-def _dra_pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm_n: int, n_gpus: int) -> list[dict]:
+def _dra_pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm_n: int, n_gpus: int,
+             image: str = DEFAULT_IMAGE) -> list[dict]:
     """A ResourceClaim for ``count`` devices and the pod using it (scheduled
     by the scheduler, which allocates the claim on ``node``)."""
     from ..dra.api import DRIVER_NAME
@@ -76,7 +80,7 @@ def _dra_pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm
     claim = {"apiVersion": "resource.k8s.io/v1beta1", "kind": "ResourceClaim",
              "metadata": {"name": name, "namespace": namespace, "labels": {POD_LABEL: run_id}},
              "spec": {"devices": {"requests": [req], "constraints": constraints}}}
-    pod = _pod(name, node, namespace, run_id, count, gemm_n)
+    pod = _pod(name, node, namespace, run_id, count, gemm_n, image=image)
     spec = pod["spec"]
     del spec["nodeName"], spec["tolerations"]
     spec["nodeSelector"] = {"kubernetes.io/hostname": node}
@@ -86,7 +90,7 @@ def _dra_pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm
 
 
 def _run_batch(cluster, node: str, namespace: str, shapes: list[int], gemm_n: int, timeout: float,
-               dra: bool = False, n_gpus: int = 0) -> list[dict]:
+               dra: bool = False, n_gpus: int = 0, image: str = DEFAULT_IMAGE) -> list[dict]:
     """Create one pod per entry of ``shapes`` (its GPU count) at once, wait for
     all, collect their record, delete them."""
     from ..kube.client import wait_for
@@ -96,8 +100,8 @@ def _run_batch(cluster, node: str, namespace: str, shapes: list[int], gemm_n: in
     created = {}
     for name, k in zip(names, shapes):
         created[name] = time.perf_counter()
-        for obj in (_dra_pod(name, node, namespace, run_id, k, gemm_n, n_gpus) if dra
-                    else [_pod(name, node, namespace, run_id, k, gemm_n)]):
+        for obj in (_dra_pod(name, node, namespace, run_id, k, gemm_n, n_gpus, image=image) if dra
+                    else [_pod(name, node, namespace, run_id, k, gemm_n, image=image)]):
             cluster.client.create(obj)
     objs, ok = wait_for(cluster.client, "v1", "Pod", lambda o: all(
         n in o and ((o[n].get("status") or {}).get("phase") in ("Succeeded", "Failed")) for n in names),
@@ -187,9 +191,12 @@ def run_pod_workload(cluster, node: str, n_gpus: int, gemm_n: int = 4096, timeou
                      namespace: str = "default", dra: bool = False) -> dict:
     """Config 5 on a validated node; returns the ``pod_workload`` block."""
     t0 = time.perf_counter()
+    # the user's GEMM image: the validator image of the installed policy (a bare
+    # name would not be in the registry, SimCluster.known_images)
+    image = validator_pod_image(((cluster.policy() or {}).get("spec")) or {})["image"]
 
     def batch(shapes):
-        return _run_batch(cluster, node, namespace, shapes, gemm_n, timeout, dra=dra, n_gpus=n_gpus)
+        return _run_batch(cluster, node, namespace, shapes, gemm_n, timeout, dra=dra, n_gpus=n_gpus, image=image)
 
     batches = {"single": batch([1] * n_gpus), "whole_node": batch([n_gpus])}
     if n_gpus == 8:

@@ -84,7 +84,7 @@ class AdmissionError(RuntimeError):
 
 def fake_validator_result(argv: list[str], env: dict | None = None) -> ProcResult:
     """Synthetic ``amdgpu-validator`` output for CPU-only runs."""
-    from .fake_validator import visible_count
+    from .fake_validator import simulated_detail, visible_count
 
     def arg(name, default):
         return argv[argv.index(name) + 1] if name in argv else default
@@ -96,10 +96,15 @@ def fake_validator_result(argv: list[str], env: dict | None = None) -> ProcResul
                "steps": []}
         return ProcResult(1, json.dumps(rep) + "\n", "", 0.0)
     steps = arg("--steps", "hip,vecadd,gemm,mfma,hbm,xgmi,rccl").split(",")
-    rep = {"ok": True, "simulated": True, "rank": int(arg("--rank", "0")), "world": int(arg("--world", "1")),
-           "device": int(arg("--device", "0")), "seconds": 0.0,
-           "steps": [{"name": s, "ok": True, "seconds": 0.0, "simulated": True} for s in steps]}
-    return ProcResult(0, json.dumps(rep) + "\n", "", 0.0)
+    rank, world = int(arg("--rank", "0")), int(arg("--world", "1"))
+    recs = [{"name": s, "ok": True, "seconds": 0.0, "simulated": True, **simulated_detail(s, argv, rank, world)}
+            for s in steps]
+    ok = all(r["ok"] for r in recs)
+    rep = {"ok": ok, "simulated": True, "rank": rank, "world": world, "device": int(arg("--device", "0")),
+           "seconds": 0.0, "steps": recs, "rocr_visible_devices": (env or {}).get("ROCR_VISIBLE_DEVICES")}
+    if not ok:
+        rep["error"] = f"step {next(r['name'] for r in recs if not r['ok'])} failed"
+    return ProcResult(0 if ok else 1, json.dumps(rep) + "\n", "", 0.0)
 
 
 class _PodRun:
@@ -125,10 +130,16 @@ class _PodRun:
         with self._status_lock:
             self._status_locked(phase, init_done, reason, message)
 
-    def _status_locked(self, phase: str, init_done: bool, reason: str, message: str) -> None:
+    def _status_locked(self, phase: str, init_done: bool, reason: str, message: str,
+                       waiting: dict | None = None) -> None:
         spec = self.pod["spec"]
         ctrs = spec.get("containers", [])
         all_ready = init_done and bool(ctrs) and all(self.ready.get(c["name"]) for c in ctrs)
+
+        def state(c):
+            if waiting is not None:  # image pull failed: the kubelet's waiting state (ErrImagePull / ImagePullBackOff)
+                return {"waiting": waiting}
+            return {"running": {}} if phase == "Running" else {"terminated": {"reason": reason}}
         now = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
         st = {
             "phase": phase,
@@ -140,8 +151,7 @@ class _PodRun:
                 {"type": "Ready", "status": "True" if all_ready else "False", "lastTransitionTime": now},
             ],
             "containerStatuses": [{"name": c["name"], "ready": bool(self.ready.get(c["name"])),
-                                   "restartCount": self.restarts,
-                                   "state": {"running": {}} if phase == "Running" else {"terminated": {"reason": reason}}}
+                                   "restartCount": self.restarts, "image": c.get("image", ""), "state": state(c)}
                                   for c in ctrs],
         }
         if reason:
@@ -165,9 +175,35 @@ class _PodRun:
             pass
 
     # ----------------------------------------------------------- lifecycle
+    def _pull(self, attempt: int) -> bool:
+        """The kubelet pulls every container's image before it starts any: an
+        image the registry does not hold (SimCluster.known_images: the chart's
+        and the ClusterPolicies' images, plus pushed ones) leaves the pod
+        Pending with ``ErrImagePull``, then ``ImagePullBackOff`` - as a bare
+        name pulled from Docker Hub does on a cluster."""
+        spec = self.pod["spec"]
+        want = [c.get("image", "") for c in spec.get("initContainers", []) + spec.get("containers", [])]
+        known = self.cluster.known_images()
+        missing = [i for i in want if i not in known]
+        if not missing:
+            return True
+        msg = (f'Failed to pull image "{missing[0]}": rpc error: code = NotFound desc = failed to resolve reference '
+               f'"{missing[0]}": not found')
+        self.cluster.trace("image-pull-failed", f"{self.name} {missing[0]}")
+        with self._status_lock:
+            self._status_locked("Pending", False, "", "", waiting={
+                "reason": "ErrImagePull" if attempt == 0 else "ImagePullBackOff",
+                "message": msg if attempt == 0 else f'Back-off pulling image "{missing[0]}"'})
+        return False
+
     def _run(self) -> None:
         restart = self.pod["spec"].get("restartPolicy", "Always") != "Never"
         backoff = self.cluster.poll_s * 10
+        attempt = 0
+        while not self._pull(attempt):
+            attempt += 1
+            if self.stop.wait(min(2.0, 0.1 * 2 ** attempt)):
+                return
         while not self.stop.is_set():
             failed = self._run_once()
             if not failed or not restart:
@@ -311,6 +347,10 @@ class SimCluster:
         self._hashes: dict[tuple, str] = {}
         self.hook_drop_devices = 0  # fault injection: GPUs the runtime leaves out of a GPU container
         self.pod_reports: dict[str, dict] = {}  # GPU pod name -> its process's JSON report
+        self.container_reports: dict[tuple[str, str], dict] = {}  # (pod, container) -> the same, per container
+        # images "pushed" to the simulated registry besides the chart's and the policies' (known_images)
+        self.pushed_images: set[str] = set()
+        self._images_cache: tuple = (None, set())
 
     # -------------------------------------------------------------- setup
     # a unix socket path must fit sockaddr_un.sun_path (108 bytes); the node's
@@ -734,17 +774,20 @@ class SimCluster:
                 {"name": k, "resourceClaimName": v} for k, v in done.items()]}}, ns, subresource="status")
         return out
 
-    def _prepare_claims(self, run: _PodRun) -> tuple[list[int], dict[str, str], list[str]]:
+    def _prepare_claims(self, run: _PodRun, ctr: dict) -> tuple[list[int], dict[str, str], list[str]]:
         with run.node.dra_lock:
-            devices, envs, uids = self._prepare_claims_locked(run)
+            devices, envs, uids = self._prepare_claims_locked(run, ctr)
             run.dra_uids = uids
             return devices, envs, uids
 
-    def _prepare_claims_locked(self, run: _PodRun) -> tuple[list[int], dict[str, str], list[str]]:
-        """The kubelet's DRA manager for a pod's ResourceClaims: prepare them
-        through the node's DRA driver and apply the CDI specs it wrote (render
-        nodes -> the devices the container sees, env).  Returns (device
-        indices, env, prepared claim uids)."""
+    def _prepare_claims_locked(self, run: _PodRun, ctr: dict) -> tuple[list[int], dict[str, str], list[str]]:
+        """The kubelet's DRA manager for a pod's ResourceClaims: prepare all of
+        them through the node's DRA driver (idempotent: once per pod in
+        effect), then give container ``ctr`` the CDI devices of the claims -
+        and requests - its ``resources.claims`` names, and only those, composed
+        as a CDI runtime does (toolkit/cdi.py, strict: two claims setting one
+        variable differently fail the container).  Returns (device indices
+        the container sees, its env, the pod's prepared claim uids)."""
         from ..dra import api as dra_api
         from . import fakedra
 
@@ -768,25 +811,32 @@ class SimCluster:
         from ..discovery import topology
 
         by_minor = {f"/dev/dri/renderD{g.render_minor}": g.index for g in topology.enumerate_gpus(node.env.sysfs_root())}
-        devices, envs = [], {}
         # pod-resources: each container holds the claims its resources.claims names
         held = {c["metadata"]["name"]: {"claim": (run.ns, c["metadata"]["name"]), "resources": [
             (dra_api.DRIVER_NAME, d.pool_name, d.device_name, list(d.cdi_device_ids)) for d in out[c["metadata"]["uid"]].devices]}
             for c in claims}
-        for ctr in run.pod["spec"]["containers"]:
-            refs = [by_ref.get(x.get("name")) for x in (ctr.get("resources") or {}).get("claims") or []]
+        for other in run.pod["spec"]["containers"]:
+            refs = [by_ref.get(x.get("name")) for x in (other.get("resources") or {}).get("claims") or []]
             if any(r in held for r in refs):
-                node.kubelet.record_claims(run.ns, run.name, ctr["name"], [held[r] for r in refs if r in held])
-        for uid, r in out.items():
-            with open(os.path.join(node.env.cdi_dir, f"{dra_api.DRIVER_NAME}-claim_{uid}.json")) as f:
-                spec = json.load(f)
-            edits = {d["name"]: d["containerEdits"] for d in spec["devices"]}
-            for dev in r.devices:
-                for cdi_id in dev.cdi_device_ids:
-                    for dn in edits[cdi_id.split("=", 1)[1]].get("deviceNodes", []):
-                        if dn["path"] in by_minor:
-                            devices.append(by_minor[dn["path"]])
-            envs.update(e.split("=", 1) for e in spec.get("containerEdits", {}).get("env", []))
+                node.kubelet.record_claims(run.ns, run.name, other["name"], [held[r] for r in refs if r in held])
+        from ..toolkit import cdi
+
+        uid_of = {c["metadata"]["name"]: c["metadata"]["uid"] for c in claims}
+        ids: list[str] = []
+        for ref in (ctr.get("resources") or {}).get("claims") or []:
+            claim_name = by_ref.get(ref.get("name"))
+            if claim_name is None:
+                raise AdmissionError(f"container {ctr['name']}: claim {ref.get('name')!r} is not in spec.resourceClaims")
+            for dev in out[uid_of[claim_name]].devices:
+                if ref.get("request") and ref["request"] not in dev.request_names:
+                    continue  # a container may take one request of a shared claim
+                ids += [i for i in dev.cdi_device_ids if i not in ids]
+        try:
+            edits = cdi.resolve(node.env.cdi_dir, ids, strict=True)
+        except cdi.CDIError as e:
+            raise RuntimeError(f"container {ctr['name']}: {e}") from e
+        devices = [by_minor[dn["path"]] for dn in edits.device_nodes if dn.get("path") in by_minor]
+        envs = dict(edits.env)
         return devices, envs, list(out)
 
     def _dra_kubelet(self, node: SimNode, timeout: float = 30.0):
@@ -1107,7 +1157,7 @@ class SimCluster:
         envs: dict[str, str] = {}
         devices: list[int] = []
         if run.pod["spec"].get("resourceClaims") and not gpu_res:  # DRA: the claims' CDI devices
-            devices, envs, uids = self._prepare_claims(run)
+            devices, envs, uids = self._prepare_claims(run, c)
             self.trace("gpu-pod-allocated", run.name)
             run.cleanups.append(lambda: self._unprepare_claims(run, uids))
         elif gpu_res:
@@ -1156,17 +1206,57 @@ class SimCluster:
         dev = devices[0] if devices else None
         if devices:
             proc_env.update(container_device_env(node.env.sysfs_root(), devices))
+        if run.pod["spec"].get("resourceClaims") and not gpu_res:
+            proc_env.update(envs)  # the CDI edits' environment
+            if not devices:  # a container of a claim-holding pod that names no claim: no GPU in it
+                proc_env["ROCR_VISIBLE_DEVICES"] = ""
         res = node.env.launch(argv, proc_env, device=dev, timeout=600)
         self.trace("gpu-pod-reported", run.name)
         try:  # the process's own step times, for the bring-up breakdown
             rep = json.loads(res.stdout.strip().splitlines()[-1])
             self.pod_reports[run.name] = rep
+            self.container_reports[(run.name, c["name"])] = rep
             steps = " ".join(f"{x['name']}={x.get('seconds', 0):.4f}" for x in rep.get("steps", []))
             self.trace("gpu-pod-steps", f"{run.name} total={rep.get('seconds', 0):.4f} {steps}")
         except (ValueError, IndexError, KeyError, TypeError):
             pass
         if res.rc != 0:
             raise RuntimeError(f"workload failed rc={res.rc}: {res.stderr.strip()[-500:]} {res.stdout.strip()[-500:]}")
+
+    def known_images(self) -> set[str]:
+        """What the simulated registry holds: the chart's operator image, every
+        image of every ClusterPolicy (api/clusterpolicy.py policy_images) and
+        AMDGPUDriver, and :attr:`pushed_images`."""
+        from ..api.clusterpolicy import policy_images
+        from ..api.driver_cr import AMDGPUDriverSpec
+        from ..helm.values import default_values
+
+        try:
+            cps = self.client.list(CP_API, "ClusterPolicy")
+        except Exception:  # noqa: BLE001 - CRD not installed yet
+            cps = []
+        try:
+            drvs = self.client.list(CP_API, "AMDGPUDriver")
+        except Exception:  # noqa: BLE001
+            drvs = []
+        key = tuple((o["metadata"].get("name"), o["metadata"].get("resourceVersion")) for o in cps + drvs)
+        if self._images_cache[0] != key:
+            imgs = set()
+            op = default_values().get("operator") or {}
+            imgs.add(f"{op.get('repository')}/{op.get('image')}:{op.get('version')}")
+            for cp in cps:
+                try:
+                    imgs.update(policy_images(cp.get("spec") or {}).values())
+                except Exception:  # noqa: BLE001 - a spec the API would have rejected
+                    continue
+            for d in drvs:
+                try:
+                    spec = AMDGPUDriverSpec.model_validate(d.get("spec") or {})
+                    imgs.add(spec.ref(spec.image))
+                except Exception:  # noqa: BLE001
+                    continue
+            self._images_cache = (key, imgs)
+        return self._images_cache[1] | self.pushed_images
 
     # -------------------------------------------------------------- queries
     def policy(self) -> dict | None:

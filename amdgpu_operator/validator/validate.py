@@ -218,22 +218,51 @@ def _xgmi_link_gbps(env: NodeEnv, gpus: list) -> dict[tuple[int, int], float]:
     return out
 
 
+# The per-peer rate the floors assume where KFD reports no XGMI link
+# bandwidth between two GPUs of a multi-GPU node (PCIe-routed peers, or a
+# driver that reports max_bandwidth 0): the MI355X xGMI nominal.  Without it
+# such a node summed to 0 and its floors to "no floor"; with it the node is
+# held to the xGMI rate it should have and a PCIe-routed node fails, as the
+# ClusterPolicy's derivation says (api/clusterpolicy.py WorkloadSpec).
+NOMINAL_XGMI_LINK_GBPS = 76.0
+
+
+def rccl_busbw_floor(link_sum_gbps: float, fraction: float, nbytes: int) -> float:
+    """The all-reduce busBW floor at ``nbytes`` (the alpha-beta shape above)."""
+    if nbytes <= 0:
+        return 0.0
+    return fraction * link_sum_gbps * nbytes / (nbytes + RCCL_HALF_BW_BYTES)
+
+
 def fabric_floors(env: NodeEnv, plan: list[list], gpus: list, rccl_fraction: float, xgmi_fraction: float,
                   rccl_bytes: int) -> dict:
     """Throughput floors of the multi-GPU steps, from the KFD link model above:
     per rank the sum of the links from its first device to every peer GPU's
-    first device; the floors use the smallest such sum of the node."""
+    first device; the floors use the smallest such sum of the node.  A peer
+    pair with no KFD XGMI bandwidth counts at :data:`NOMINAL_XGMI_LINK_GBPS`
+    (``nominal_pairs`` says how many), so such a node is never left without a
+    floor."""
     links = _xgmi_link_gbps(env, gpus)
-    sums = []
+    sums, nominal = [], 0
     for r, devs in enumerate(plan):
         me = devs[0].index
-        sums.append(sum(links.get((me, p[0].index), links.get((p[0].index, me), 0.0))
-                        for q, p in enumerate(plan) if q != r))
+        total = 0.0
+        for q, p in enumerate(plan):
+            if q == r:
+                continue
+            bw = links.get((me, p[0].index)) or links.get((p[0].index, me)) or 0.0
+            if bw <= 0:
+                bw = NOMINAL_XGMI_LINK_GBPS
+                nominal += 1
+            total += bw
+        sums.append(total)
     link_sum = min(sums) if sums else 0.0
-    size = rccl_bytes / (rccl_bytes + RCCL_HALF_BW_BYTES) if rccl_bytes > 0 else 0.0
-    return {"link_gbps_per_rank": [round(x, 1) for x in sums],
-            "min_rccl_busbw_gbps": round(rccl_fraction * link_sum * size, 1),
-            "min_xgmi_peer_read_gbps": round(xgmi_fraction * link_sum, 1)}
+    out = {"link_gbps_per_rank": [round(x, 1) for x in sums],
+           "min_rccl_busbw_gbps": round(rccl_busbw_floor(link_sum, rccl_fraction, rccl_bytes), 1),
+           "min_xgmi_peer_read_gbps": round(xgmi_fraction * link_sum, 1)}
+    if nominal:
+        out["nominal_pairs"] = nominal  # peer pairs without KFD XGMI bandwidth, held to the xGMI nominal
+    return out
 
 
 def check_fabric(env: NodeEnv, gpus: list, smi_metrics: list | None = None, min_link_fraction: float = 0.9) -> dict:
@@ -524,9 +553,67 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         if not fabric["ok"]:
             ok = summary["ok"] = False
     if not ok:
-        raise StepFailed(f"workload validation failed: {failure_summary(reports, fabric, problems)}")
+        msg = f"workload validation failed: {failure_summary(reports, fabric, problems)}"
+        write_failure(env, "workload", failure_record(summary, msg))
+        raise StepFailed(msg)
+    clear_failure(env, "workload")
     write_ready(env, "workload", summary)
     return summary
+
+
+# A failed step leaves ``<step>-failed`` next to the ready files: what failed
+# and every rate the run measured against the floor it was held to, so a node
+# that will not validate can be diagnosed from the host (must-gather collects
+# the directory) and a harness can stop at the first failure instead of
+# waiting out its timeout (bench.py).  The next pass of the step clears it.
+FAILED_SUFFIX = "-failed"
+_RATE_KEYS = ("tflops", "min_tflops", "gbps", "min_gbps", "busbw_gbps", "min_busbw_gbps", "algbw_gbps", "bytes",
+              "peer_read_gbps", "min_peer_read_gbps", "perf_ok", "counter_gate", "mismatches", "max_abs_err",
+              "freivalds_rel_err", "comm_init_s", "world", "device", "error", "failed")
+
+
+def write_failure(env: NodeEnv, step: str, payload: dict) -> str:
+    os.makedirs(env.validations_dir, exist_ok=True)
+    path = env.validation_file(step + FAILED_SUFFIX)
+    tmp = f"{path}.tmp.{os.getpid()}.{threading.get_ident()}"
+    with open(tmp, "w") as f:
+        json.dump({"step": step, "node": env.node_name, "time": time.time(), **payload}, f)
+    os.replace(tmp, path)
+    return path
+
+
+def read_failure(env: NodeEnv, step: str) -> dict | None:
+    try:
+        with open(env.validation_file(step + FAILED_SUFFIX)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def clear_failure(env: NodeEnv, step: str) -> None:
+    try:
+        os.unlink(env.validation_file(step + FAILED_SUFFIX))
+    except OSError:
+        pass
+
+
+def failure_record(summary: dict, message: str) -> dict:
+    """The compact record of a failed workload run: per rank its error (or the
+    peer it found gone), and per step the measured rates next to the floors
+    (``min_*``), the fabric check's problems and the floors the node was held
+    to (:func:`fabric_floors`)."""
+    ranks = []
+    for i, r in enumerate(summary.get("ranks", [])):
+        steps = [{"name": s.get("name"), "ok": s.get("ok"), **{k: s[k] for k in _RATE_KEYS if k in s}}
+                 for s in r.get("steps", [])]
+        ranks.append({"rank": i, "ok": bool(r.get("ok")) and r.get("rc") == 0, "rc": r.get("rc"),
+                      **{k: r[k] for k in ("error", "failed_peer", "peer_state") if r.get(k) is not None},
+                      "steps": steps})
+    fabric = summary.get("fabric")
+    return {"message": message[:2000], "world": summary.get("world"), "floors": summary.get("floors"),
+            "fabric_problems": (fabric or {}).get("problems", []) if fabric else [],
+            "coverage_problems": summary.get("coverage_problems", []), "ranks": ranks,
+            "failed_ranks": [r["rank"] for r in ranks if not r["ok"]]}
 
 
 def device_coverage(plan: list[list], reports: list[dict]) -> list[str]:
@@ -879,7 +966,8 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
 
 
 def validate_dra(env: NodeEnv, timeout: float = 600.0, stop=None, image: str | None = None,
-                 pull_policy: str = "IfNotPresent", pull_secrets: list[str] | None = None) -> dict:
+                 pull_policy: str = "IfNotPresent", pull_secrets: list[str] | None = None,
+                 device_class: str | None = None) -> dict:
     """The DRA counterpart of :func:`validate_plugin` (``draDriver.enabled``,
     device plugin off): once the node's ResourceSlice lists every device, a
     ResourceClaim for all of them (``allocationMode: All``) and one pod that
@@ -910,7 +998,7 @@ def validate_dra(env: NodeEnv, timeout: float = 600.0, stop=None, image: str | N
     name = f"amd-validator-dra-{run_id}"
     claim = {"apiVersion": "resource.k8s.io/v1beta1", "kind": "ResourceClaim",
              "metadata": {"name": name, "namespace": env.namespace, "labels": {WORKLOAD_POD_LABEL: run_id}},
-             "spec": {"devices": {"requests": [{"name": "gpus", "deviceClassName": DRIVER_NAME,
+             "spec": {"devices": {"requests": [{"name": "gpus", "deviceClassName": device_class or DRIVER_NAME,
                                                 "allocationMode": "All"}]}}}
     pod = {"apiVersion": "v1", "kind": "Pod",
            "metadata": {"name": name, "namespace": env.namespace,
@@ -1007,7 +1095,8 @@ def abort_start_gates(env: NodeEnv) -> list[str]:
 def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURCE_NAME,
                  pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                  wait_toolkit: bool = False, with_driver: bool = False, partition_strategy: str = "single",
-                 pod_check: str = "hsa", per_device: bool = False, dra: bool = False) -> dict:
+                 pod_check: str = "hsa", per_device: bool = False, dra: bool = False,
+                 dra_device_class: str | None = None) -> dict:
     """Workload and plugin validation concurrently (each skipped if already done).
     ``dra``: the plugin step validates the DRA driver instead (:func:`validate_dra`).
 
@@ -1082,7 +1171,7 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
             if os.environ.get("AMDGPU_EXPERIMENT_PLUGIN_AFTER_WORKLOAD"):  # start-up contention experiment
                 wait_ready(env, "workload", timeout, stop)
             if read_ready(env, "plugin") is None and dra:
-                results["plugin"] = validate_dra(env, timeout, stop)
+                results["plugin"] = validate_dra(env, timeout, stop, device_class=dra_device_class)
             elif read_ready(env, "plugin") is None:
                 results["plugin"] = validate_plugin(env, resource, pod_args=pod_args, timeout=timeout, stop=stop,
                                                     kubelet=kubelet, partition_strategy=partition_strategy,

@@ -41,3 +41,42 @@ LOADED_VERSION_ANN = "amd.com/gpu-driver.version"
 # the driver health container's amd-smi status line (driver/manager.py publish_smi,
 # checked by `amdgpu-operator verify`)
 DRIVER_SMI_ANN = "amd.com/gpu.driver-smi"
+
+# the DRA driver's name (dra/api.py DRIVER_NAME): ResourceClaim results it allocated
+DRA_DRIVER = "gpu.amd.com"
+
+
+def uses_gpu(pod: dict, get_claim=None) -> bool:
+    """Does this pod hold GPUs of the node - through the device plugin
+    (``amd.com/gpu*`` limits or requests of any container) or through the DRA
+    driver (a ResourceClaim that one of its containers names)?  A partition
+    change, a driver upgrade and a drain must take both kinds off the node.
+    ``get_claim(namespace, name)``: the claim, to skip claims another DRA
+    driver (a NIC's) allocated; without it, or when a claim cannot be read or
+    is not allocated yet, any claim counts (the safe side: evict)."""
+    spec = pod.get("spec") or {}
+    ctrs = list(spec.get("containers") or []) + list(spec.get("initContainers") or [])
+    for c in ctrs:
+        res = c.get("resources") or {}
+        if any(k.startswith("amd.com/gpu") for part in ("limits", "requests") for k in (res.get(part) or {})):
+            return True
+    entries = spec.get("resourceClaims") or []
+    if not entries or not any((c.get("resources") or {}).get("claims") for c in ctrs):
+        return False
+    if get_claim is None:
+        return True
+    ns = (pod.get("metadata") or {}).get("namespace", "default")
+    generated = {s.get("name"): s.get("resourceClaimName")
+                 for s in (pod.get("status") or {}).get("resourceClaimStatuses") or []}
+    for e in entries:
+        name = e.get("resourceClaimName") or generated.get(e.get("name"))
+        if not name:
+            return True  # a template's claim not created yet
+        try:
+            claim = get_claim(ns, name)
+        except Exception:  # noqa: BLE001 - unreadable: count it
+            return True
+        results = ((((claim or {}).get("status") or {}).get("allocation") or {}).get("devices") or {}).get("results")
+        if not results or any(r.get("driver") == DRA_DRIVER for r in results):
+            return True
+    return False

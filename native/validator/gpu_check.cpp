@@ -268,8 +268,11 @@ int main(int argc, char** argv) {
   std::string error;
   bool ok = true;
   int ngpu = 0;
+  double hsa_init_s = -1;
   try {
+    const auto th = Clock::now();
     check(hsa_init(), "hsa_init");
+    hsa_init_s = secs(th);
     Agents ag;
     check(hsa_iterate_agents(find_agents, &ag), "iterate agents");
     ngpu = (int)ag.gpus.size();
@@ -320,7 +323,7 @@ int main(int argc, char** argv) {
   std::string out = "{\"ok\": " + std::string(ok ? "true" : "false") + ", \"devices\": " + std::to_string(ngpu);
   char b[96];
   // t_main: CLOCK_MONOTONIC at main (steady_clock), comparable with a parent's time.monotonic()
-  snprintf(b, sizeof b, ", \"seconds\": %.4f, \"t_main\": %.6f", secs(t0),
+  snprintf(b, sizeof b, ", \"seconds\": %.4f, \"hsa_init_s\": %.4f, \"t_main\": %.6f", secs(t0), hsa_init_s,
            std::chrono::duration<double>(t0.time_since_epoch()).count());
   out += b;
   if (!error.empty()) {

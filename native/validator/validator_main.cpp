@@ -30,6 +30,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -39,6 +40,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -267,6 +269,12 @@ struct Args {
   int agent_ordinal = 0;      // which HSA agent at the device's PCI address (set per device)
   bool rccl_destroy = false;  // ncclCommDestroy before exit (default: barrier + exit, see step_rccl)
   std::string ready_file;
+  // the sweep step (collective curve after Ready, bench.py): sizes min * factor^k up to max
+  long long sweep_min_bytes = 8;
+  long long sweep_max_bytes = 1ll << 30;
+  int sweep_factor = 4;
+  std::string sweep_ops = "allreduce,allgather,reducescatter";
+  long long link_bytes = 64ll << 20;  // the xgmi_links step: bytes read over each link
 };
 
 struct Step {
@@ -1221,23 +1229,32 @@ float time_collective(hipStream_t st, int iters, ncclComm_t comm, const Rendezvo
 // checked exactly (rank r contributes r+1) and timed; busBW uses the usual
 // ring factors (all-reduce 2(n-1)/n, gather/scatter (n-1)/n) so the numbers
 // compare with rccl-tests.  SURVEY.md §2.E call sites.
-Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread* init_thread, RcclInit* ri) {
-  auto t0 = Clock::now();
-  Step s{"rccl"};
-  try {
-    await_rccl_init(a, rv, init_thread, ri);
-  } catch (const PeerError& e) {
-    throw PeerError(e.peer, e.state, std::string("rccl init: ") + e.what());
-  } catch (const std::exception& e) {
-    throw std::runtime_error(std::string("rccl init: ") + e.what());
+// The communicator of this process, once its set-up thread is done (the rccl
+// and sweep steps share one; the second caller finds it ready).  Throws with
+// the failing peer named, as await_rccl_init.
+ncclComm_t rccl_comm(const Args& a, const Rendezvous& rv, std::thread* init_thread, RcclInit* ri) {
+  if (init_thread->joinable() || !ri->done.load()) {
+    try {
+      await_rccl_init(a, rv, init_thread, ri);
+    } catch (const PeerError& e) {
+      throw PeerError(e.peer, e.state, std::string("rccl init: ") + e.what());
+    } catch (const std::exception& e) {
+      throw std::runtime_error(std::string("rccl init: ") + e.what());
+    }
   }
-  const double wait_s = secs(t0);
   if (!ri->error.empty()) {
     if (ri->failed_peer >= 0 || !ri->peer_state.empty())
       throw PeerError(ri->failed_peer, ri->peer_state, "rccl init: " + ri->error);
     throw std::runtime_error("rccl init: " + ri->error);
   }
-  ncclComm_t comm = ri->comm;
+  return ri->comm;
+}
+
+Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread* init_thread, RcclInit* ri) {
+  auto t0 = Clock::now();
+  Step s{"rccl"};
+  ncclComm_t comm = rccl_comm(a, rv, init_thread, ri);
+  const double wait_s = secs(t0);
   // a non-blocking communicator may answer a collective with ncclInProgress
   auto call = [&](ncclResult_t r, const char* what) {
     if (r == ncclInProgress) nccl_settle(comm, rv, a.collective_timeout_s, what);
@@ -1342,6 +1359,194 @@ Step step_rccl(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread*
                  W, (long long)(n * 4), ri->load_s, ri->init_s, wait_s, first_s, checks_s, destroy_s, ar_ms, ar_algbw,
                  ar_busbw, (long long)total_bad) +
              detail + "}, \"library\": \"" + g_rccl.path + "\"";
+  return s;
+}
+
+// The message sizes of the collective sweep: min, min*factor, ... up to and
+// including max (8 B ... 1 GiB by 4x: 15 sizes).
+std::vector<int64_t> sweep_sizes(int64_t lo, int64_t hi, int factor) {
+  std::vector<int64_t> out;
+  for (int64_t b = lo; b <= hi; b *= factor) out.push_back(b);
+  if (out.empty() || out.back() != hi) out.push_back(hi);
+  return out;
+}
+
+// --steps ...,sweep: the collective curve of SURVEY.md §5.8 on this node's
+// communicator - all-reduce, all-gather and reduce-scatter (fp32 sum) at every
+// size of sweep_sizes, each checked exactly on the device (rank r contributes
+// r + 1) and then timed over back-to-back launches (HIP events on the
+// collectives' stream), out of place.  One row per (op, size): bytes of the full tensor,
+// us per launch, algBW = bytes / time, busBW with the rccl-tests factors
+// (all-reduce 2(n-1)/n, the others (n-1)/n).  The per-rank rows are merged by
+// validate.py collective_sweep (slowest rank per row).  Run after the node is
+// Ready (bench.py), not on the time-to-Ready path: its 2 x max bytes of
+// device memory and ~seconds do not belong in a bring-up.
+Step step_sweep(const Args& a, hipStream_t st, const Rendezvous& rv, std::thread* init_thread, RcclInit* ri) {
+  auto t0 = Clock::now();
+  Step s{"sweep"};
+  ncclComm_t comm = rccl_comm(a, rv, init_thread, ri);
+  const double wait_s = secs(t0);
+  auto call = [&](ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) nccl_settle(comm, rv, a.collective_timeout_s, what);
+    else if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + g_rccl.GetErrorString(r));
+  };
+  hipEvent_t done_ev;
+  HIP_OK(hipEventCreateWithFlags(&done_ev, hipEventDisableTiming));
+  const int W = a.world;
+  const auto sizes = sweep_sizes(a.sweep_min_bytes, a.sweep_max_bytes, a.sweep_factor);
+  const int64_t cap = ((a.sweep_max_bytes / 4 + W - 1) / W) * W;  // elements of the largest tensor
+  float *buf, *aux;
+  unsigned long long* bad_dev;
+  HIP_OK(hipMalloc(&buf, cap * 4));
+  HIP_OK(hipMalloc(&aux, cap * 4));
+  HIP_OK(hipMalloc(&bad_dev, sizeof(unsigned long long)));
+  const float mine = (float)(a.rank + 1), expect_sum = W * (W + 1) / 2.0f;
+  auto check = [&](const float* x, int64_t count, int64_t block, float base, float step) -> int64_t {
+    HIP_OK(hipEventRecord(done_ev, st));
+    wait_collective(done_ev, comm, rv, a.collective_timeout_s);
+    AVK_OK(avk_check_blocks(x, count, 0, block, base, step, bad_dev, st));
+    unsigned long long bad = 0;
+    HIP_OK(hipMemcpyAsync(&bad, bad_dev, sizeof(bad), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    return (int64_t)bad;
+  };
+  std::string rows;
+  int64_t total_bad = 0;
+  int nrows = 0;
+  const char* ops[] = {"allreduce", "allgather", "reducescatter"};
+  for (const char* op : ops) {
+    const std::string o = op;
+    if (a.sweep_ops.find(o) == std::string::npos) continue;
+    int64_t last_n = -1;
+    for (int64_t bytes : sizes) {
+      const int64_t n = std::max<int64_t>(W, ((bytes / 4) / W) * W);  // full tensor, a multiple of W elements
+      if (n == last_n) continue;  // sizes below W floats all round up to one tensor
+      last_n = n;
+      const int64_t per = n / W;
+      std::function<void()> launch;
+      int64_t bad = 0;
+      if (o == "allreduce") {
+        // out of place (rccl-tests' default): at world 1 an in-place
+        // all-reduce moves nothing, out of place it is a device copy
+        launch = [&] { call(g_rccl.AllReduce(buf, aux, n, ncclFloat32, ncclSum, comm, st), "ncclAllReduce"); };
+        AVK_OK(avk_fill_const(buf, n, 0, mine, st));
+        launch();
+        bad = check(aux, n, n, expect_sum, 0.0f);
+      } else if (o == "allgather") {
+        launch = [&] { call(g_rccl.AllGather(buf, aux, per, ncclFloat32, comm, st), "ncclAllGather"); };
+        AVK_OK(avk_fill_const(buf, per, 0, mine, st));
+        launch();
+        bad = check(aux, n, per, 1.0f, 1.0f);
+      } else {
+        launch = [&] { call(g_rccl.ReduceScatter(buf, aux, per, ncclFloat32, ncclSum, comm, st), "ncclReduceScatter"); };
+        AVK_OK(avk_fill_const(buf, n, 0, mine, st));
+        launch();
+        bad = check(aux, per, per, expect_sum, 0.0f);
+      }
+      // short messages: enough launches to average out the event resolution;
+      // large ones: a few (a 1 GiB all-reduce at 8 ranks is ~10 ms)
+      const int iters = bytes <= (1 << 20) ? 20 : bytes <= (64 << 20) ? 10 : 4;
+      launch();  // warm-up of this size's algorithm / protocol choice
+      const float ms = time_collective(st, iters, comm, rv, a.collective_timeout_s, launch);
+      const double busf = W > 1 ? (o == "allreduce" ? 2.0 * (W - 1) / W : (W - 1.0) / W) : 0.0;
+      const double algbw = n * 4.0 / (ms * 1e-3) / 1e9;
+      rows += fmt("%s{\"op\": \"%s\", \"bytes\": %lld, \"iters\": %d, \"us\": %.2f, \"algbw_gbps\": %.2f, "
+                  "\"busbw_gbps\": %.2f, \"mismatches\": %lld}",
+                  nrows++ ? ", " : "", op, (long long)(n * 4), iters, ms * 1e3, algbw, algbw * busf, (long long)bad);
+      total_bad += bad;
+    }
+  }
+  rv.barrier(a.run_id + "-sweep-done");  // no rank leaves while a peer's kernel may read its buffers
+  (void)hipFree(buf);
+  (void)hipFree(aux);
+  (void)hipFree(bad_dev);
+  (void)hipEventDestroy(done_ev);
+  s.ok = total_bad == 0;
+  s.seconds = secs(t0);
+  s.detail = fmt("\"world\": %d, \"comm_init_s\": %.4f, \"init_wait_s\": %.4f, \"mismatches\": %lld, \"rows\": [", W,
+                 ri->init_s, wait_s, (long long)total_bad) +
+             rows + "]";
+  return s;
+}
+
+// --steps ...,xgmi_links (world > 1): every xGMI link on its own.  Each rank
+// exports a buffer over IPC; in round k (1 .. W-1, lockstep barriers) rank r
+// copies peer (r + k) % W's buffer into local memory with the K4 kernel on one
+// peer pointer, so every link carries one reader per direction per round.
+// Reported per peer: GB/s read over that link (fastest of 3) and whether the
+// data arrived intact.  The K4 step's all-peers-at-once read (xgmi) bounds the
+// sum; this names the slow link.
+Step step_xgmi_links(const Args& a, hipStream_t st, const Rendezvous& rv) {
+  auto t0 = Clock::now();
+  Step s{"xgmi_links"};
+  const int W = a.world;
+  const int64_t n = a.link_bytes / 4;
+  float *in, *out, *expect;
+  unsigned int* md;
+  HIP_OK(hipMalloc(&in, n * 4));
+  HIP_OK(hipMalloc(&out, n * 4));
+  HIP_OK(hipMalloc(&expect, n * 4));
+  HIP_OK(hipMalloc(&md, 4));
+  AVK_OK(avk_fill_uniform_f32(in, n, 7000 + a.rank, -1, 1, st));
+  HIP_OK(hipStreamSynchronize(st));
+  hipIpcMemHandle_t mine;
+  HIP_OK(hipIpcGetMemHandle(&mine, in));
+  rv.publish(a.run_id + "-link-ipc-" + std::to_string(a.rank), &mine, sizeof(mine));
+  std::vector<const float*> peer(W, nullptr);
+  for (int r = 0; r < W; ++r) {
+    if (r == a.rank) continue;
+    auto buf = rv.fetch(a.run_id + "-link-ipc-" + std::to_string(r), sizeof(hipIpcMemHandle_t), r);
+    hipIpcMemHandle_t h;
+    memcpy(&h, buf.data(), sizeof(h));
+    void* p = nullptr;
+    HIP_OK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    peer[r] = (const float*)p;
+  }
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  std::string rows;
+  bool ok = true;
+  double min_gbps = 0;
+  for (int k = 1; k < W; ++k) {
+    rv.barrier(a.run_id + "-link-" + std::to_string(k));
+    const int p = (a.rank + k) % W;
+    const float* src[1] = {peer[p]};
+    AVK_OK(avk_allreduce_oneshot_f32(src, 1, out, n, st));  // first touch of the mapping
+    float best = 0;
+    for (int t = 0; t < 3; ++t) {
+      HIP_OK(hipEventRecord(e0, st));
+      AVK_OK(avk_allreduce_oneshot_f32(src, 1, out, n, st));
+      HIP_OK(hipEventRecord(e1, st));
+      HIP_OK(hipEventSynchronize(e1));
+      float tm = 0;
+      HIP_OK(hipEventElapsedTime(&tm, e0, e1));
+      if (t == 0 || tm < best) best = tm;
+    }
+    AVK_OK(avk_fill_uniform_f32(expect, n, 7000 + p, -1, 1, st));
+    AVK_OK(avk_max_abs_diff_f32(out, expect, n, md, st));
+    unsigned int bits = 0;
+    HIP_OK(hipMemcpyAsync(&bits, md, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    float err;
+    memcpy(&err, &bits, 4);
+    const double gbps = n * 4.0 / (best * 1e-3) / 1e9;
+    const bool intact = err == 0.0f;
+    ok = ok && intact;
+    min_gbps = (k == 1 || gbps < min_gbps) ? gbps : min_gbps;
+    rows += fmt("%s{\"peer\": %d, \"read_gbps\": %.1f, \"ms\": %.4f, \"intact\": %s}", k > 1 ? ", " : "", p, gbps, best,
+                intact ? "true" : "false");
+  }
+  rv.barrier(a.run_id + "-link-out");  // every peer finished reading our buffer
+  for (int r = 0; r < W; ++r)
+    if (peer[r]) (void)hipIpcCloseMemHandle((void*)peer[r]);
+  for (void* q : {(void*)in, (void*)out, (void*)expect, (void*)md}) (void)hipFree(q);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  s.ok = ok;
+  s.seconds = secs(t0);
+  s.detail = fmt("\"world\": %d, \"bytes\": %lld, \"min_read_gbps\": %.1f, \"links\": [", W, (long long)(n * 4),
+                 min_gbps) + rows + "]";
   return s;
 }
 
@@ -1502,6 +1707,7 @@ void usage(const char* p) {
           "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--rccl-destroy]\n"
           "          [--ready-file PATH] [--start-gate FILE] [--gate-mode aql|sdk] [--min-mfma-util U]\n"
           "          [--min-rccl-busbw-gbps X] [--min-xgmi-read-gbps X] [--peer-timeout S] [--collective-timeout S]\n"
+          "          [--sweep-min-bytes B] [--sweep-max-bytes B] [--sweep-factor F] [--sweep-ops a,b] [--link-bytes B]\n"
           "       %s --check-gate M,N,K,CUS,MOPS,BUSY,WAVES,GUI,GUI_SAMPLES [--min-mfma-util U]\n"
           "          (gate verdict on a counter tuple; no GPU access)\n",
           p, p);
@@ -1551,6 +1757,11 @@ int main(int argc, char** argv) {
     else if (k == "--counter-gate") a.counter_gate = true;
     else if (k == "--any-arch") a.any_arch = true;
     else if (k == "--rccl-destroy") a.rccl_destroy = true;
+    else if (k == "--sweep-min-bytes") a.sweep_min_bytes = atoll(v());
+    else if (k == "--sweep-max-bytes") a.sweep_max_bytes = atoll(v());
+    else if (k == "--sweep-factor") a.sweep_factor = atoi(v());
+    else if (k == "--sweep-ops") a.sweep_ops = v();
+    else if (k == "--link-bytes") a.link_bytes = atoll(v());
     else if (k == "--ready-file") a.ready_file = v();
     else if (k == "--start-gate") a.start_gate = v();
     else if (k == "--gate-mode") a.gate_mode = v();
@@ -1561,7 +1772,9 @@ int main(int argc, char** argv) {
   }
   if (a.world < 1 || a.rank < 0 || a.rank >= a.world || a.gemm_n <= 0 || a.gemm_n % 256 || a.hbm_bytes <= 0 ||
       a.hbm_bytes % 16 || a.rccl_elems <= 0 || a.xgmi_elems <= 0 || a.xgmi_elems % 4 || a.emulated_peers < 1 ||
-      a.emulated_peers > 8 || a.world > 64 || (a.world > 8 && has_step(a, "xgmi"))) {
+      a.emulated_peers > 8 || a.world > 64 || (a.world > 8 && has_step(a, "xgmi")) || a.sweep_min_bytes < 4 ||
+      a.sweep_max_bytes < a.sweep_min_bytes || a.sweep_max_bytes > (16ll << 30) || a.sweep_factor < 2 ||
+      a.link_bytes < 16 || a.link_bytes % 16) {
     fprintf(stderr, "amdgpu-validator: invalid arguments (gemm %% 256, sizes %% 16, world <= 64, xgmi needs world <= 8)\n");
     return 2;
   }
@@ -1569,8 +1782,9 @@ int main(int argc, char** argv) {
     fprintf(stderr, "amdgpu-validator: --all-devices and --local-bdf exclude each other\n");
     return 2;
   }
-  if (a.all_devices && (a.world > 1 || has_step(a, "rccl") || has_step(a, "xgmi"))) {
-    fprintf(stderr, "amdgpu-validator: --all-devices runs the single-GPU steps (world 1, no rccl / xgmi)\n");
+  if (a.all_devices && (a.world > 1 || has_step(a, "rccl") || has_step(a, "xgmi") || has_step(a, "sweep") ||
+                        has_step(a, "xgmi_links"))) {
+    fprintf(stderr, "amdgpu-validator: --all-devices runs the single-GPU steps (world 1, no rccl / xgmi / sweep)\n");
     return 2;
   }
   if (a.gate_mode != "aql" && a.gate_mode != "sdk") {
@@ -1603,7 +1817,8 @@ int main(int argc, char** argv) {
   memset(&prop, 0, sizeof(prop));
   std::thread rccl_thread;
   RcclInit rccl_state;
-  if (has_step(a, "rccl")) {  // before any HIP call: see the note at struct Rccl
+  const bool need_comm = has_step(a, "rccl") || has_step(a, "sweep");
+  if (need_comm) {  // before any HIP call: see the note at struct Rccl
     auto tl = Clock::now();
     std::string err;
     if (!g_rccl.load(Gate::exe_dir(), &err)) rccl_state.error = err;
@@ -1660,7 +1875,7 @@ int main(int argc, char** argv) {
     a.agent_ordinal = devs[0].second;
     steps.push_back(step_hip(a, &prop));
     ok = steps.back().ok;
-    if (ok && has_step(a, "rccl") && rccl_state.error.empty())
+    if (ok && need_comm && rccl_state.error.empty())
       rccl_thread = std::thread(rccl_init, std::cref(a), std::cref(rv), &rccl_state);
     const auto ts = Clock::now();
     if (!a.null_stream) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -1681,6 +1896,8 @@ int main(int argc, char** argv) {
     // the collective steps on the first local device (this rank's device)
     HIP_OK(hipSetDevice(a.device));
     if (ok && has_step(a, "xgmi")) ok = (steps.push_back(step_xgmi(a, st, rv)), steps.back().ok);
+    if (ok && has_step(a, "xgmi_links") && a.world > 1) ok = (steps.push_back(step_xgmi_links(a, st, rv)), steps.back().ok);
+    if (ok && has_step(a, "sweep")) ok = (steps.push_back(step_sweep(a, st, rv, &rccl_thread, &rccl_state)), steps.back().ok);
     if (ok && has_step(a, "rccl")) ok = (steps.push_back(step_rccl(a, st, rv, &rccl_thread, &rccl_state)), steps.back().ok);
   } catch (const PeerError& e) {
     ok = false;

@@ -32,6 +32,43 @@ def test_bench_json_line_contract():
     ops = cfg["operands"]
     assert ops["amd-device-plugin-daemonset/amd-device-plugin"]["ready_s"] > 0
     assert ops["amd-operator-validator/amd-operator-validator"]["ready_s"] > 0
+    # both halves of the metric (README.md:122), and every timed step's critical path
+    vis = cfg["allocatable_visible_s"]
+    assert cfg["allocatable_visible_mean_s"] == round(sum(vis) / 2, 3) and cfg["allocatable_visible_p95_s"] == max(vis)
+    cps = cfg["critical_path"]
+    assert len(cps) == 2 and all(c["ttr"] > 0 and "complete" in c["at"] and "ready_gap" in c for c in cps)
+    assert [c["ttr"] for c in cps] == cfg["time_to_ready_s"]
+    # the collective block after the last timed bring-up (world 1 here; the 8-rank run: test_launcher.py)
+    col = cfg["collectives"]
+    assert col["ok"] and col["world"] == 1 and set(col["ops"]) == {"allreduce", "allgather", "reducescatter"}
+    assert [r["bytes"] for r in col["ops"]["allreduce"]][-1] == 1 << 30
+
+
+def test_bench_floor_failure_prints_a_structured_line():
+    """A bring-up that fails its floors (here the RCCL busBW fraction set 250x
+    above the link model) ends at once with the JSON line: value null, the
+    failing step, ranks and floor vs measured, and the collective curve
+    measured after it; rc non-zero."""
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port=29617", "bench.py", "--gpus", "2", "--steps", "3",
+                        "--warmup", "0", "--fake-gpu-procs", "--compare", "0",
+                        "--set", "validator.workload.rcclBusbwLinkFraction=50"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode != 0
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:] + p.stderr[-2000:]
+    out = json.loads(lines[0])
+    assert KEYS <= set(out) and out["value"] is None and out["vs_baseline"] is None
+    e = out["error"]
+    assert e["phase"] == "timed" and e["bring_up"] == 1 and e["failed_steps"][0] in ("gpu", "workload")
+    assert e["world"] == 2 and e["failed_ranks"] == [0, 1]
+    assert e["floors"]["min_rccl_busbw_gbps"] == 3040.0  # 50 x 76 GB/s x 64/(64+16) MiB
+    for r in e["ranks"]:
+        rccl = next(s for s in r["steps"] if s["name"] == "rccl")
+        assert rccl["ok"] is False and rccl["perf_ok"] is False and rccl["busbw_gbps"] < rccl["min_busbw_gbps"]
+    col = out["config"]["collectives"]
+    assert col["ok"] and col["world"] == 2 and col["xgmi_links"]["min_read_gbps"] > 0
+    assert col["fabric_floors"]["rccl_busbw_link_fraction"] == 0.2  # the sweep reports against the default model
 
 
 @pytest.mark.gpu
@@ -63,3 +100,8 @@ def test_bench_harness_never_opens_the_gpu():
     assert line["config"]["harness_holds_kfd"] is False
     assert str(p.pid) not in seen
     assert seen - {str(os.getpid())}, "no GPU process seen at all: the KFD process list is not being read"
+    # the collective block on the device (world 1: RCCL's single-rank path, the curve's shape)
+    col = line["config"]["collectives"]
+    assert col["ok"] and col["world"] == 1 and not col["simulated"], col
+    assert len(col["ops"]["allreduce"]) >= 14 and all(r["ok"] and r["latency_us"] > 0 for r in col["ops"]["allreduce"])
+    assert col["ops"]["allreduce"][-1]["algbw_gbps"] > 100  # a 1 GiB single-rank all-reduce is an HBM copy

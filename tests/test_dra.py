@@ -315,6 +315,10 @@ def test_partition_change_republishes_with_a_new_generation(node):
     s = env.client.get(RV1B1, "ResourceSlice", f"n1-{api.DRIVER_NAME}")
     assert len(s["spec"]["devices"]) == 16 and s["spec"]["pool"]["generation"] == 2
     assert s["spec"]["devices"][1]["basic"]["attributes"]["computePartition"] == {"string": "DPX"}
+    # a restarted driver publishing the same devices leaves the slice (and its generation) alone
+    rv = s["metadata"]["resourceVersion"]
+    again = DraDriver(env).publish()
+    assert again["spec"]["pool"]["generation"] == 2 and again["metadata"]["resourceVersion"] == rv
 
 
 def test_exporter_attributes_dra_claims_via_pod_resources(short_tmp):
@@ -362,3 +366,90 @@ def test_exporter_attributes_dra_claims_via_pod_resources(short_tmp):
                                                             resolve=device_id_resolver(root)).lookup()
     finally:
         k.stop()
+
+
+def _check_ctr(name, claims, expect):
+    return {"name": name, "image": "registry.local/amd-gpu-operator/amd-operator-validator:0.1.0",
+            "command": ["amdgpu-gpu-check"], "args": ["--timeout", "30", "--expect-devices", str(expect)],
+            "resources": {"claims": [{"name": x} for x in claims]}}
+
+
+@pytest.mark.parametrize("processes", [False, True], ids=["threads", "processes"])
+def test_claims_apply_per_container(short_tmp, processes):
+    """A CDI runtime gives a container the devices of the claims its
+    ``resources.claims`` names, and composes their specs: one container
+    holding two claims sees both GPUs (the specs' edits compose: no
+    variable set twice), two containers of one pod holding one claim each
+    see one GPU each - different ones - and a container naming no claim
+    sees none."""
+    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, parse_set_flags
+    from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
+
+    flags = REFERENCE_SET_FLAGS + ["draDriver.enabled=true", "devicePlugin.enabled=false"]
+    c = SimCluster(str(short_tmp / "c"), [NodeSpec("gpu-1", 4)], fake_gpu=True, process_containers=processes).start()
+    try:
+        c.install_operator(parse_set_flags(flags))
+        c.wait_ready(60)
+        for n in ("a", "b", "x", "y"):
+            c.client.create(_claim(n, 1))
+
+        def pod(name, ctrs, claims):
+            return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
+                    "spec": {"restartPolicy": "Never", "nodeSelector": {"kubernetes.io/hostname": "gpu-1"},
+                             "resourceClaims": [{"name": x, "resourceClaimName": x} for x in claims],
+                             "containers": ctrs}}
+
+        c.client.create(pod("both", [_check_ctr("check", ["a", "b"], 2)], ["a", "b"]))
+        c.client.create(pod("split", [_check_ctr("left", ["x"], 1), _check_ctr("right", ["y"], 1),
+                                      _check_ctr("none", [], 0)], ["x", "y"]))
+        import time
+
+        def phase(n):
+            return (c.client.get("v1", "Pod", n, "default").get("status") or {}).get("phase")
+
+        deadline = time.monotonic() + 30
+        while time.monotonic() < deadline and not {phase("both"), phase("split")} <= {"Succeeded", "Failed"}:
+            time.sleep(0.05)
+        assert phase("both") == "Succeeded", c.client.get("v1", "Pod", "both", "default")["status"]
+        assert phase("split") == "Succeeded", c.client.get("v1", "Pod", "split", "default")["status"]
+        rep = c.container_reports
+        both = rep[("both", "check")]["rocr_visible_devices"].split(",")
+        left = rep[("split", "left")]["rocr_visible_devices"].split(",")
+        right = rep[("split", "right")]["rocr_visible_devices"].split(",")
+        assert len(both) == 2 and len(left) == len(right) == 1 and left != right
+        assert rep[("split", "none")]["rocr_visible_devices"] == ""
+        alloc = {n: c.client.get(RV1B1, "ResourceClaim", n, "default")["status"]["allocation"]["devices"]["results"][0]
+                 ["device"] for n in ("a", "b", "x", "y")}
+        assert len(set(alloc.values())) == 4  # four claims, four GPUs
+    finally:
+        c.stop()
+
+
+def test_cdi_specs_of_two_claims_compose(node):
+    """The driver's per-claim specs, resolved together as a runtime does
+    (toolkit/cdi.py, strict): /dev/kfd once, both render nodes, no variable
+    set twice.  A spec set that does set one twice fails in strict mode."""
+    from amdgpu_operator.toolkit import cdi
+
+    env, drv, kdir = node
+    k = fakedra.FakeDraKubelet(kdir)
+    k.discover()
+    ids = []
+    for n in ("p", "q"):
+        claim = fakedra.allocate(env.client, env.client.create(_claim(n, 1)), "n1")
+        ids += k.prepare(api.DRIVER_NAME, [claim])[claim["metadata"]["uid"]].devices[0].cdi_device_ids
+    e = cdi.resolve(env.cdi_dir, ids, strict=True)
+    paths = [d["path"] for d in e.device_nodes]
+    assert paths.count("/dev/kfd") == 1 and len([p for p in paths if "renderD" in p]) == 2 and not e.conflicts
+    with pytest.raises(cdi.CDIError, match="unresolvable"):
+        cdi.resolve(env.cdi_dir, ids + ["gpu.amd.com/claim=nope"])
+    # the round-4 spec shape (AMD_VISIBLE_DEVICES at spec level) collides when composed
+    for i, path in enumerate(sorted(f for f in os.listdir(env.cdi_dir) if f.startswith("gpu.amd.com-claim_"))):
+        with open(os.path.join(env.cdi_dir, path)) as f:
+            spec = json.load(f)
+        spec["containerEdits"]["env"] = [f"AMD_VISIBLE_DEVICES={i}"]
+        with open(os.path.join(env.cdi_dir, path), "w") as f:
+            json.dump(spec, f)
+    assert cdi.resolve(env.cdi_dir, ids).conflicts
+    with pytest.raises(cdi.CDIError, match="set a variable twice"):
+        cdi.resolve(env.cdi_dir, ids, strict=True)

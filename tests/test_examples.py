@@ -137,14 +137,25 @@ def test_dra_examples_run(short_tmp):
 def test_verify_run_pod(short_tmp, dra):
     """``amdgpu-operator verify --run-pod``: per GPU node one 1-GPU pod (an
     amd.com/gpu limit, or a ResourceClaim with the DRA driver) must succeed;
-    it leaves no pod or claim behind."""
+    it leaves no pod or claim behind.  The pod runs the ClusterPolicy's
+    validator image - here from a mirror registry (``validator.repository``),
+    with a pull secret - and, with the DRA driver, claims from the policy's
+    own DeviceClass (``draDriver.deviceClass``)."""
     from amdgpu_operator.cli.verify import verify
     from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
 
-    flags = REFERENCE_SET_FLAGS + (["draDriver.enabled=true", "devicePlugin.enabled=false"] if dra else [])
+    flags = REFERENCE_SET_FLAGS + ["validator.repository=mirror.example.com/gpu", "validator.version=7.2.0-r5"]
+    flags += ["draDriver.enabled=true", "devicePlugin.enabled=false", "draDriver.deviceClass=mi355x.example.com"] \
+        if dra else []
+    values = parse_set_flags(flags)
+    values["validator"]["imagePullSecrets"] = ["mirror-creds"]
     c = SimCluster(str(short_tmp / "c"), [NodeSpec("gpu-1", 4), NodeSpec("gpu-2", 2)], fake_gpu=True).start()
+    seen = []
+    c.api.hooks.append(lambda etype, obj: seen.append(obj) if etype == "ADDED"
+                       and obj.get("kind") in ("Pod", "ResourceClaim")
+                       and obj["metadata"].get("name", "").startswith("amd-gpu-verify-") else None)
     try:
-        c.install_operator(parse_set_flags(flags))
+        c.install_operator(values)
         c.wait_ready(60, {} if dra else {"gpu-1": 4, "gpu-2": 2})
         rep = verify(c.client, c.namespace, run_pods=True, pod_timeout=30)
         pods = [x for x in rep.checks if x.name.startswith("gpu-pod[")]
@@ -154,5 +165,45 @@ def test_verify_run_pod(short_tmp, dra):
                     if p["metadata"]["name"].startswith("amd-gpu-verify-")
                     and not p["metadata"].get("deletionTimestamp")]
         assert not c.client.list(RV1B1, "ResourceClaim")
+        created = [o for o in seen if o["kind"] == "Pod"]
+        assert len(created) == 2
+        for pod in created:
+            ctr = pod["spec"]["containers"][0]
+            assert ctr["image"] == "mirror.example.com/gpu/amd-operator-validator:7.2.0-r5"
+            assert pod["spec"]["imagePullSecrets"] == [{"name": "mirror-creds"}]
+        if dra:
+            assert all(o["spec"]["devices"]["requests"][0]["deviceClassName"] == "mi355x.example.com"
+                       for o in seen if o["kind"] == "ResourceClaim")
+    finally:
+        c.stop()
+
+
+def test_a_bare_image_name_does_not_pull(short_tmp):
+    """A real kubelet pulls ``amd-operator-validator`` from Docker Hub and the
+    pod ends in ImagePullBackOff; the simulated kubelet's registry holds only
+    the chart's and the ClusterPolicy's images, so it does the same - and
+    ``verify --run-pod --pod-image <bare>`` fails, naming the pull error."""
+    from amdgpu_operator.cli.verify import verify
+    from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster
+
+    c = SimCluster(str(short_tmp / "c"), [NodeSpec("gpu-1", 1)], fake_gpu=True).start()
+    try:
+        c.install_operator(parse_set_flags(REFERENCE_SET_FLAGS))
+        c.wait_ready(60, {"gpu-1": 1})
+        rep = verify(c.client, c.namespace, run_pods=True, pod_image="amd-operator-validator", pod_timeout=2)
+        (pod,) = [x for x in rep.checks if x.name.startswith("gpu-pod[")]
+        assert not pod.ok and "Pending" in pod.detail and "ImagePull" in pod.detail, pod.detail
+        docs = _docs("gpu-pod.yaml")
+        docs[0]["spec"]["nodeName"] = "gpu-1"
+        docs[0]["spec"]["containers"][0]["image"] = "amd-operator-validator"
+        _create_all(c, docs)
+        def reason():
+            st = c.client.get("v1", "Pod", "amd-gpu-check", "default").get("status") or {}
+            return (((st.get("containerStatuses") or [{}])[0].get("state") or {}).get("waiting") or {}).get("reason")
+
+        assert _wait(lambda: reason() == "ImagePullBackOff"), reason()
+        assert _phase(c, "amd-gpu-check") == "Pending"
+        # every pod the product itself created pulled: the operands and the validator's pods ran
+        assert all(p["status"]["phase"] in ("Running", "Succeeded") for p in c.client.list("v1", "Pod", c.namespace))
     finally:
         c.stop()

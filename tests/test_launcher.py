@@ -84,5 +84,19 @@ def test_bench_n8_stays_within_the_gpu_process_budget(tmp_path):
     assert pw["pods"] == 11 and pw["all_succeeded"] and pw["single_gpu_pods_distinct_devices"]
     assert pw["two_halves_numa_local"] and pw["two_halves_disjoint"]
     peak, roles = _peak_concurrency(log_dir)
-    assert roles == {"validator": 8, "pod": 1 + 11}, roles  # the plugin-validation pod + the workload's pods
+    # 8 validator processes per pass: the bring-up's, then the collective sweep's
+    assert roles == {"validator": 16, "pod": 1 + 11}, roles  # the plugin-validation pod + the workload's pods
     assert peak <= 16, peak
+    # the collective curve at world 8 after the timed bring-up
+    col = out["config"]["collectives"]
+    assert col["ok"] and col["world"] == 8
+    for op in ("allreduce", "allgather", "reducescatter"):
+        rows = col["ops"][op]
+        assert len(rows) == 14 and rows[0]["bytes"] == 32 and rows[-1]["bytes"] == 1 << 30  # 8 B rounds up to 8 floats
+        assert all(r["ok"] and r["latency_us"] > 0 and r["busbw_gbps"] >= 0 for r in rows)
+        assert rows[-1]["busbw_gbps"] > rows[0]["busbw_gbps"]
+    links = col["xgmi_links"]["read_gbps"]
+    assert len(links) == 8 and all(links[r][r] is None and all(links[r][p] for p in range(8) if p != r) for r in range(8))
+    ff = col["fabric_floors"]
+    assert ff["link_gbps_per_rank"] == [532.0] * 8 and ff["min_allreduce_ratio"] > 1 and ff["links_below_floor"] == []
+    assert len(out["config"]["critical_path"]) == 1

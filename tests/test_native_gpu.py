@@ -127,6 +127,37 @@ def test_validator_single_rank_rccl(tmp_path):
     assert all(c["mismatches"] == 0 and c["ms"] > 0 for c in r["collectives"].values())
 
 
+def test_validator_sweep_step_one_rank(tmp_path):
+    # the native sweep (validator_main.cpp step_sweep): every size checked on the
+    # device, then timed; 8 B ... 16 MiB here
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,sweep", "--sweep-max-bytes", str(16 << 20)])
+    assert rc == 0 and rep["ok"], rep
+    s = {x["name"]: x for x in rep["steps"]}["sweep"]
+    assert s["world"] == 1 and s["mismatches"] == 0 and s["comm_init_s"] > 0
+    rows = s["rows"]
+    for op in ("allreduce", "allgather", "reducescatter"):
+        mine = [r for r in rows if r["op"] == op]
+        assert [r["bytes"] for r in mine] == [8 * 4 ** k for k in range(12)] + [16 << 20]
+        assert all(r["mismatches"] == 0 and r["us"] > 0 and r["busbw_gbps"] == 0 for r in mine)  # world 1: no bus
+    assert max(r["algbw_gbps"] for r in rows) > 50
+
+
+def test_validator_xgmi_links_two_processes_one_gpu(tmp_path):
+    # two ranks on one GPU take the per-link path (IPC, lockstep rounds, data
+    # checked); on a node each round crosses a different xGMI link
+    procs = [subprocess.Popen([VALIDATOR, "--rank", str(r), "--world", "2", "--device", "0", "--rendezvous",
+                               str(tmp_path), "--run-id", "links", "--steps", "hip,xgmi_links",
+                               "--link-bytes", str(16 << 20)],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    for r, (p, (out, err)) in enumerate(zip(procs, outs)):
+        rep = json.loads(out.strip().splitlines()[-1])
+        assert p.returncode == 0 and rep["ok"], (rep, err[-2000:])
+        x = {s["name"]: s for s in rep["steps"]}["xgmi_links"]
+        assert x["links"] == [dict(x["links"][0], peer=1 - r)] and x["links"][0]["intact"]
+        assert x["min_read_gbps"] > 10
+
+
 def test_collectives_sweep_rccl_one_gpu():
     import sys
 

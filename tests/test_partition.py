@@ -246,3 +246,58 @@ def test_failed_unload_during_a_reload_restores_driver_ready(node, monkeypatch):
     ready = read_ready(node, "driver")
     assert ready and ready["time"] >= t0 and ready.get("recovered")
     assert not os.path.exists(node.validation_file(DM.LOST_MARKER))  # claimed by the recovery
+
+
+def _dra_pod(name, claim, with_ref=True):
+    ctr = {"name": "c", "image": "x", "resources": {"claims": [{"name": "g"}]} if with_ref else {}}
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": NS},
+            "spec": {"nodeName": "n1", "resourceClaims": [{"name": "g", "resourceClaimName": claim}],
+                     "containers": [ctr]}}
+
+
+def _alloc_claim(c, name, driver):
+    claim = c.create({"apiVersion": "resource.k8s.io/v1beta1", "kind": "ResourceClaim",
+                      "metadata": {"name": name, "namespace": NS},
+                      "spec": {"devices": {"requests": [{"name": "g", "deviceClassName": driver}]}}})
+    claim["status"] = {"allocation": {"devices": {"results": [
+        {"request": "g", "driver": driver, "pool": "n1", "device": "gpu-0"}]}}}
+    c.update_status(claim)
+
+
+def test_dra_claim_holders_are_gpu_pods(node):
+    """with the DRA driver the node's GPUs are held through
+    ResourceClaims, not amd.com/gpu limits.  A partition change evicts (and
+    waits for) those pods too; a pod whose claim another DRA driver (a NIC's)
+    allocated, or that names no claim in any container, stays."""
+    from amdgpu_operator.wellknown import uses_gpu
+
+    c = node.client
+    _alloc_claim(c, "gpu-claim", "gpu.amd.com")
+    _alloc_claim(c, "nic-claim", "rdma.example.com")
+    c.create(_dra_pod("dra-gpu", "gpu-claim"))
+    c.create(_dra_pod("dra-nic", "nic-claim"))
+    c.create(_dra_pod("dra-unreferenced", "gpu-claim", with_ref=False))
+    c.create(_dra_pod("dra-pending", "not-yet"))  # its claim is not there yet: counts (safe side)
+    assert uses_gpu(c.get("v1", "Pod", "dra-gpu", NS)) and uses_gpu(c.get("v1", "Pod", "dra-nic", NS))  # no lookup
+    evicted = PM.evict_gpu_pods(node)
+    assert sorted(evicted) == sorted(f"{NS}/{n}" for n in ("workload", "dra-gpu", "dra-pending")), evicted
+    left = {p["metadata"]["name"] for p in c.list("v1", "Pod", NS)}
+    assert {"dra-nic", "dra-unreferenced"} <= left and not {"dra-gpu", "workload"} & left
+    assert PM.wait_gpu_pods_gone(node, 1.0)
+
+
+def test_driver_upgrade_drains_dra_claim_holders():
+    """The driver upgrade's drain lists a gpu.amd.com claim holder as a GPU
+    pod (an amdgpu unload would find the module busy under it)."""
+    from amdgpu_operator.controller import upgrade as U
+
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Namespace", NS))
+    c.create(R.new("v1", "Node", "n1"))
+    _alloc_claim(c, "gpu-claim", "gpu.amd.com")
+    _alloc_claim(c, "nic-claim", "rdma.example.com")
+    c.create(_dra_pod("dra-gpu", "gpu-claim"))
+    c.create(_dra_pod("dra-nic", "nic-claim"))
+    c.create(_pod("plugin-pod", gpu=True))
+    ctl = U.DriverUpgradeController(c, NS)
+    assert sorted(p["metadata"]["name"] for p in ctl._gpu_pods("n1")) == ["dra-gpu", "plugin-pod"]

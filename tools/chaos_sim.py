@@ -52,7 +52,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, deep_merge, parse_set_flags  # noqa: E402
+from amdgpu_operator.api.clusterpolicy import (REFERENCE_SET_FLAGS, deep_merge, parse_set_flags,  # noqa: E402
+                                              validator_pod_image)
 from amdgpu_operator.driver.manager import monitor_once  # noqa: E402
 from amdgpu_operator.sandbox import WORKLOAD_CONFIG_LABEL  # noqa: E402
 from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster  # noqa: E402
@@ -83,7 +84,8 @@ def claim_pod(c, node: str, timeout: float) -> tuple[bool, str]:
     c.client.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "default"},
                      "spec": {"restartPolicy": "Never", "nodeSelector": {"kubernetes.io/hostname": node},
                               "resourceClaims": [{"name": "gpu", "resourceClaimName": name}],
-                              "containers": [{"name": "check", "image": "amd-operator-validator",
+                              "containers": [{"name": "check", "image": validator_pod_image(
+                                  (c.policy() or {}).get("spec") or {})["image"],
                                               "command": ["amdgpu-gpu-check"],
                                               "args": ["--timeout", "30", "--expect-devices", "1"],
                                               "resources": {"claims": [{"name": "gpu"}]}}]}})
