@@ -18,7 +18,7 @@ from ..utils.logs import get_logger
 from .manifests import DEPLOY_LABEL, OPERAND_LABELS
 
 log = get_logger("amdgpu.nodes")
-VALIDATED_LABELS = ("amd.com/gpu.validated", "amd.com/gpu.validated.mfma")
+VALIDATED_LABELS = ("amd.com/gpu.validated", "amd.com/gpu.validated.mfma", "amd.com/gpu.validated.mfma-rate")
 
 NFD_PCI_LABELS = (
     "feature.node.kubernetes.io/pci-1002.present",       # vendor only

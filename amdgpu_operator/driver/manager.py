@@ -273,7 +273,7 @@ def _withdraw_validation(env: NodeEnv, reason: str) -> None:
     """The node's validation no longer holds: remember why (the loss marker,
     :func:`_claim_lost_marker`), drop every ready file and the node's
     ``amd.com/gpu.validated`` labels."""
-    from ..validator.validate import MFMA_LABEL, VALIDATED_LABEL
+    from ..validator.validate import MFMA_LABEL, MFMA_RATE_LABEL, VALIDATED_LABEL
 
     os.makedirs(env.validations_dir, exist_ok=True)
     tmp = env.validation_file(f"{LOST_MARKER}.tmp.{os.getpid()}.{threading.get_ident()}")
@@ -283,8 +283,8 @@ def _withdraw_validation(env: NodeEnv, reason: str) -> None:
     clear_ready(env, ("driver", "toolkit", "workload", "plugin", "complete"))
     if env.client is not None:
         try:
-            env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": {VALIDATED_LABEL: None,
-                                                                                   MFMA_LABEL: None}}})
+            env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": {
+                VALIDATED_LABEL: None, MFMA_LABEL: None, MFMA_RATE_LABEL: None}}})
         except Exception as e:  # noqa: BLE001
             log.warning("could not withdraw %s: %s", VALIDATED_LABEL, e)
 

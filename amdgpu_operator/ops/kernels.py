@@ -48,6 +48,10 @@ def _lib(name: str = LIB_NAME) -> ctypes.CDLL:
         "avk_gemm_bf16_nt": ([P, P, P, I, I, I, I, S], I),
         "avk_gemm_bf16_nt_variant": ([P, P, P, I, I, I, I, I, S], I),
         "avk_gemv_rows": ([P, I, P, P, I, I, S], I),
+        "avk_gemm_fp8_nt": ([P, P, P, I, I, I, I, S], I),
+        "avk_fill_fp8": ([P, I64, U64, S], I),
+        "avk_gemv_rows_fp8": ([P, P, P, I, I, S], I),
+        "avk_gemv_cols_fp8": ([P, P, P, I, I, S], I),
         "avk_gemv_cols_bf16": ([P, P, P, I, I, S], I),
         "avk_hbm_copy": ([P, P, I64, I, I, S], I),
         "avk_checksum": ([P, I64, P, S], I),
@@ -185,6 +189,51 @@ def gemm_bf16_nt(a, bt, out=None, out_dtype=None, stream=None, variant: int | No
     rc = lib.avk_gemm_bf16_nt_variant(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
                                       M, N, K, variant, _stream(stream))
     _check(rc, "gemm_bf16_nt")
+    return out
+
+
+FP8_K_MULTIPLE = 256
+
+
+def _fp8_bytes(t, name: str):
+    """An OCP e4m3 operand as its bytes: ``torch.float8_e4m3fn`` or uint8."""
+    import torch
+
+    if t.dtype == torch.float8_e4m3fn:
+        t = t.view(torch.uint8)
+    _require(t, torch.uint8, name)
+    return t
+
+
+def fill_fp8_(t, seed: int, stream=None):
+    """Deterministic random finite e4m3 values (|x| <= 3.75) into a
+    ``float8_e4m3fn`` / uint8 tensor (the fp8 rate step's operands)."""
+    b = _fp8_bytes(t, "t")
+    _check(_lib().avk_fill_fp8(b.data_ptr(), b.numel(), seed & ((1 << 64) - 1), _stream(stream)), "fill_fp8")
+    return t
+
+
+def gemm_fp8_nt(a, bt, out=None, out_dtype=None, stream=None):
+    """K2b: ``out[M,N] = a[M,K] @ bt[N,K].T`` with OCP e4m3 operands
+    (``torch.float8_e4m3fn`` or their uint8 bytes) on
+    ``v_mfma_f32_16x16x128_f8f6f4``, fp32 accumulation, bf16 or fp32 out.
+    M and N multiples of 256, K of 256 (the kernel has no edge tiles)."""
+    import torch
+
+    ab, bb = _fp8_bytes(a, "a"), _fp8_bytes(bt, "bt")
+    if ab.dim() != 2 or bb.dim() != 2 or ab.shape[1] != bb.shape[1]:
+        raise ValueError(f"bad GEMM operands {tuple(ab.shape)} x {tuple(bb.shape)}^T")
+    M, K = ab.shape
+    N = bb.shape[0]
+    if M % GEMM_BM or N % GEMM_BN or K % FP8_K_MULTIPLE:
+        raise ValueError(f"fp8 GEMM shape {M}x{N}x{K} must be multiples of {GEMM_BM}x{GEMM_BN}x{FP8_K_MULTIPLE}")
+    if out is None:
+        out = torch.empty((M, N), device=ab.device, dtype=out_dtype or torch.bfloat16)
+    if out.shape != (M, N) or out.dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("bad GEMM output")
+    _require(out, out.dtype, "out")
+    _check(_lib().avk_gemm_fp8_nt(ab.data_ptr(), bb.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
+                                  M, N, K, _stream(stream)), "gemm_fp8_nt")
     return out
 
 

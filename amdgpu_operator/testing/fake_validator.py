@@ -151,6 +151,9 @@ class Rendezvous:
 # numbers that pass the default floors, and fail floors set far above them.
 SIM_LINK_GBPS = 45.0
 SIM_LATENCY_US = 12.0
+# GEMM rates of the simulated GPU (TF/s at 4096^3): above the default floors
+# (api/clusterpolicy.py WorkloadSpec), below floors set far above them
+SIM_GEMM_TFLOPS = {"gemm": 1300.0, "gemm_fp8": 2600.0}
 
 
 def sim_busbw(world: int, nbytes: int) -> float:
@@ -164,6 +167,14 @@ def simulated_detail(step: str, argv: list[str], rank: int, world: int) -> dict:
     def arg(name, default):
         return argv[argv.index(name) + 1] if name in argv else default
 
+    if step in SIM_GEMM_TFLOPS:  # the binary's floors apply from 4096^3 (validator_main.cpp gemm_floor)
+        size_flag, floor_flag = ("--gemm", "--min-gemm-tflops") if step == "gemm" else ("--fp8-gemm", "--min-fp8-tflops")
+        n = int(arg(size_flag, "4096"))
+        tf = SIM_GEMM_TFLOPS[step]
+        floor = float(arg(floor_flag, "0")) if n >= 4096 else 0.0
+        ok = floor <= 0 or tf >= floor
+        return {"ok": ok, "n": n, "tflops": tf, "min_tflops": floor, "perf_ok": ok,
+                "counter_gate": "pass" if "--counter-gate" in argv else "off"}
     if step == "rccl" and world > 1:
         nbytes = 4 * int(arg("--rccl-elems", str(1 << 24)))
         bus = sim_busbw(world, nbytes)
@@ -267,7 +278,7 @@ def _main(argv: list[str]) -> int:
                               "error": f"{expect} GPU(s) allocated to the pod, {seen} visible"}))
             return 1
     ndev = max(1, int(arg("--expect-devices", "1")))
-    per_device = ("vecadd", "gemm", "mfma", "hbm", "dmabuf")
+    per_device = ("vecadd", "gemm", "gemm_fp8", "mfma", "hbm", "dmabuf")
     recs = []
     for s in steps:
         for d in (range(ndev) if s in per_device and ndev > 1 else [None]):

@@ -50,6 +50,9 @@ READY_FILES = {
 }
 VALIDATED_LABEL = "amd.com/gpu.validated"
 MFMA_LABEL = "amd.com/gpu.validated.mfma"  # data types whose MFMA tile checked out on every GPU
+# data types whose GEMM held its TF/s floor (and counter gate) on every GPU:
+# bf16 (the gemm step), fp8 (gemm_fp8, e4m3 on the f8f6f4 MFMA)
+MFMA_RATE_LABEL = "amd.com/gpu.validated.mfma-rate"
 WORKLOAD_POD_LABEL = "amd.com/validator-workload"
 # take a validator process's result at its report, not at its exit (A/B: =0)
 REPORT_EARLY = os.environ.get("AMDGPU_VALIDATOR_REPORT_EARLY", "1") == "1"
@@ -375,8 +378,17 @@ def planned_workload_processes(env: NodeEnv, args: list[str], budget: int) -> in
     return workload_processes(world, run_rccl, "--rccl-separate-process" in args, budget)[0]
 
 
+# The workload validator processes stay until the plugin validation is done
+# (``--linger-until`` its ready file): their exit would tear down their KFD
+# processes right when the plugin pod starts its HSA runtime, which then waits
+# for that teardown (validator_main.cpp, end of main).  =0: exit at once (A/B).
+LINGER = os.environ.get("AMDGPU_VALIDATOR_LINGER", "1") == "1"
+LINGER_MAX_S = 3.0
+
+
 def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: float = 600.0,
-                      start_gate: str | None = None, budget: int | None = None) -> dict:
+                      start_gate: str | None = None, budget: int | None = None,
+                      linger_until: str | None = None) -> dict:
     """One native validator process per physical GPU, all in one RCCL
     communicator.
 
@@ -439,11 +451,13 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     separate = "--rccl-separate-process" in args
     require_links = "--require-xgmi-links" in args
     dmabuf = "--dmabuf" in args  # driver.rdma: HBM exported as a dma-buf on every device
+    if "--no-gemm-fp8" in args:  # validator.workload.fp8RateCheck off
+        args = _drop_step(args, "gemm_fp8")
     rccl_frac = float(_arg_value(args, "--rccl-busbw-link-fraction") or 0.0)
     xgmi_frac = float(_arg_value(args, "--xgmi-read-link-fraction") or 0.0)
     link_frac = float(_arg_value(args, "--min-xgmi-link-fraction") or 0.9)
     args = _drop_flag(args, "--rccl-single-gpu", "--rccl-shared-process", "--rccl-separate-process",
-                      "--require-xgmi-links", "--dmabuf")
+                      "--require-xgmi-links", "--dmabuf", "--no-gemm-fp8")
     args = _drop_value(args, "--rccl-busbw-link-fraction", "--xgmi-read-link-fraction", "--min-xgmi-link-fraction",
                        "--max-gpu-processes")
     steps = _steps_of(args)
@@ -492,6 +506,8 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         argv = workload_argv(jargs, rank, world, rdv, rid, 0)
         if start_gate:
             argv += ["--start-gate", start_gate]
+        if linger_until and LINGER:
+            argv += ["--linger-until", linger_until, "--linger-max-s", f"{LINGER_MAX_S:g}"]
         # the launcher runs the process on the rank that owns physical GPU `rank`
         res = env.launch(argv, jenv, device=rank, timeout=timeout)
         if world > 1 and failed(res):
@@ -651,7 +667,7 @@ def failure_summary(reports: list[dict], fabric: dict | None = None, problems: l
     return "; ".join(parts) or "no report"
 
 
-ALL_STEPS = ("hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl")  # + "dmabuf" with driver.rdma
+ALL_STEPS = ("hip", "vecadd", "gemm", "gemm_fp8", "mfma", "hbm", "xgmi", "rccl")  # + "dmabuf" with driver.rdma
 
 
 def _steps_of(args: list[str]) -> list[str]:
@@ -1150,7 +1166,10 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
                 if "driver" not in results:
                     return
             if read_ready(env, "workload") is None:
-                results["workload"] = validate_workload(env, workload_args, timeout, start_gate=gate, budget=budget - 1)
+                # the plugin validation runs beside it: the processes leave once it is done
+                linger = env.validation_file(READY_FILES["plugin"]) if read_ready(env, "plugin") is None else None
+                results["workload"] = validate_workload(env, workload_args, timeout, start_gate=gate, budget=budget - 1,
+                                                        linger_until=linger)
         except Exception as e:  # noqa: BLE001
             errors.append(f"workload: {e}")
 
@@ -1218,6 +1237,22 @@ def validated_mfma_dtypes(workload: dict | None) -> list[str]:
     return [d for d in sets[0] if d in common]
 
 
+RATE_STEPS = (("bf16", "gemm"), ("fp8", "gemm_fp8"))
+
+
+def validated_rate_dtypes(workload: dict | None) -> list[str]:
+    """Data types whose GEMM step passed on every device of every rank of the
+    workload report with a TF/s floor applied (``min_tflops`` > 0: a
+    report-only run proves no rate)."""
+    reports = (workload or {}).get("ranks") or []
+    out = []
+    for dtype, name in RATE_STEPS:
+        recs = [s for r in reports for s in r.get("steps", []) if s.get("name") == name]
+        if recs and all(s.get("ok") is True and (s.get("min_tflops") or 0) > 0 for s in recs):
+            out.append(dtype)
+    return out
+
+
 def complete(env: NodeEnv) -> dict:
     """Mark the node validated: label, the MFMA data types the probe confirmed
     (``amd.com/gpu.validated.mfma=f16.bf16.fp8...``, next to GFD's per-arch
@@ -1228,9 +1263,11 @@ def complete(env: NodeEnv) -> dict:
     dtypes = validated_mfma_dtypes(read_ready(env, "workload"))
     if dtypes:
         labels[MFMA_LABEL] = ".".join(dtypes)[:63]
+    rates = validated_rate_dtypes(read_ready(env, "workload"))
+    labels[MFMA_RATE_LABEL] = ".".join(rates) if rates else None  # a stale claim goes
     env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": labels, "annotations": ann}})
-    write_ready(env, "complete", {"steps": steps, "mfma_dtypes": dtypes})
-    return {"ok": True, "steps": steps, "mfma_dtypes": dtypes}
+    write_ready(env, "complete", {"steps": steps, "mfma_dtypes": dtypes, "mfma_rate_dtypes": rates})
+    return {"ok": True, "steps": steps, "mfma_dtypes": dtypes, "mfma_rate_dtypes": rates}
 
 
 # ------------------------------------------------------- sandbox workloads --

@@ -80,9 +80,12 @@ def parse():
                     help="skip the collective sweep (RCCL all-reduce / all-gather / reduce-scatter, 8 B ... "
                          "--sweep-max-bytes, and every xGMI link on its own) after the last timed bring-up")
     ap.add_argument("--sweep-max-bytes", type=int, default=1 << 30)
-    ap.add_argument("--settle-s", type=float, default=1.0,
+    ap.add_argument("--settle-s", type=float, default=0.0,
                     help="start each bring-up this long after the previous one's cluster stopped (its GPU processes' "
                          "teardown in the kernel; 0: back to back)")
+    ap.add_argument("--no-linger", action="store_true",
+                    help="A/B: the workload validator processes exit at their report instead of after the plugin "
+                         "validation (AMDGPU_VALIDATOR_LINGER=0)")
     ap.add_argument("--no-tool-watch", action="store_true",
                     help="do not watch for GPU tools of other parties (amd-smi, rocm-smi, ...) during the bring-ups")
     ap.add_argument("--timeout", type=float, default=120.0)
@@ -517,6 +520,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             "kubelet_first_list_at_s": {r: round(x - t0_wall, 4) for r, x in nd.kubelet.first_list_walls.items()},
             "gemm_tflops": [s.get("tflops") for s in steps.get("gemm", [])],
             "gemm_counter_gate": [s.get("counter_gate") for s in steps.get("gemm", [])],
+            "fp8_tflops": [s.get("tflops") for s in steps.get("gemm_fp8", [])],
+            "fp8_counter_gate": [s.get("counter_gate") for s in steps.get("gemm_fp8", [])],
             "hbm_gbps": [s.get("gbps") for s in steps.get("hbm", [])],
             "xgmi_read_gbps": [s.get("read_gbps") for s in steps.get("xgmi", [])],
             "rccl_busbw_gbps": [s.get("busbw_gbps") for s in steps.get("rccl", [])],
@@ -606,6 +611,8 @@ def failure_line(args, n_gpus: int, fake_gpu, err: dict, results: list, warm: li
 
 def main():
     args = parse()
+    if args.no_linger:  # read by the validator operand processes (validate.py LINGER)
+        os.environ["AMDGPU_VALIDATOR_LINGER"] = "0"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -785,6 +792,8 @@ def main():
                 "kubelet_node_status_s": args.kubelet_status_s,
                 "validation_poll_s": NodeEnv.poll_s if args.agent_poll_s is None else args.agent_poll_s,
                 "gemm_tflops_per_gpu": results[-1]["gemm_tflops"],
+                "fp8_gemm_tflops_per_gpu": results[-1]["fp8_tflops"],
+                "fp8_counter_gate": results[-1]["fp8_counter_gate"],
                 "hbm_gbps_per_gpu": results[-1]["hbm_gbps"],
                 "rccl_busbw_gbps": results[-1]["rccl_busbw_gbps"],
                 "rccl_comm_init_s": results[-1]["rccl_comm_init_s"],

@@ -6,9 +6,11 @@
 #include <cstdint>
 
 #define AVK_AQL_GATE_COUNTERS 4
+#define AVK_AQL_GATE_BF16 0  // gemm_default.h kGemmSymbol, SQ_INSTS_VALU_MFMA_MOPS_BF16
+#define AVK_AQL_GATE_FP8 1   // gemm_default.h kGemmFp8Symbol, SQ_INSTS_VALU_MFMA_MOPS_F8
 
 struct avk_aql_gate_result {
-  // SQ_INSTS_VALU_MFMA_MOPS_BF16, SQ_VALU_MFMA_BUSY_CYCLES, SQ_WAVES, GRBM_GUI_ACTIVE
+  // SQ_INSTS_VALU_MFMA_MOPS_{BF16|F8}, SQ_VALU_MFMA_BUSY_CYCLES, SQ_WAVES, GRBM_GUI_ACTIVE
   double values[AVK_AQL_GATE_COUNTERS];
   int samples[AVK_AQL_GATE_COUNTERS];  // per-instance samples summed into each value
   double setup_s;                      // aqlprofile load, queue, code object, buffers
@@ -18,6 +20,7 @@ struct avk_aql_gate_result {
 extern "C" {
 // Counter names in the order of avk_aql_gate_result::values.
 const char* avk_aql_gate_counter_name(int i);
+const char* avk_aql_gate_counter_name_dtype(int dtype, int i);
 
 // Dispatch the default GEMM (gemm_default.h: C = A * Bt^T, bf16 out)
 // from the code object at `code_object` on the GPU at `pci_bus_id`
@@ -27,8 +30,18 @@ const char* avk_aql_gate_counter_name(int i);
 // packets on a private queue, and sum every per-instance counter sample.  A,
 // Bt and C are device pointers (hipMalloc); M, N and K are multiples of 256
 // (the kernel's tile).  Waits at most timeout_s for the stop packet.  Returns
-// 0, or -1 with a message in err.
+// 0, or -1 with a message in err.  The HSA state of the gate (aqlprofile,
+// the loaded code object, a private queue, the counter buffers) is set up on
+// the first call for a GPU agent and kept for the process's life, so a
+// process's later gates (retries, the fp8 GEMM's) cost their dispatch only;
+// setup_s is ~0 on those.
 int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt, void* C, int M,
                       int N, int K, const char* code_object, double timeout_s, avk_aql_gate_result* out, char* err,
                       int errlen);
+
+// The same for the GEMM of `dtype` (AVK_AQL_GATE_BF16 or AVK_AQL_GATE_FP8:
+// gemm_fp8_nt_kernel, A and Bt e4m3 bytes, bf16 out, same grid and kernargs).
+int avk_aql_gate_gemm_dtype(int dtype, const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt,
+                            void* C, int M, int N, int K, const char* code_object, double timeout_s,
+                            avk_aql_gate_result* out, char* err, int errlen);
 }

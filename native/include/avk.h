@@ -18,6 +18,10 @@ int avk_vector_add_verify_f32(const float* a, const float* b, const float* c, in
                               hipStream_t s);
 int avk_gemm_bf16_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K, hipStream_t s);
 int avk_gemv_rows(const void* X, int x_is_bf16, const float* v, float* y, int R, int C, hipStream_t s);
+int avk_gemm_fp8_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K, hipStream_t s);
+int avk_fill_fp8(void* p, int64_t n, uint64_t seed, hipStream_t s);
+int avk_gemv_rows_fp8(const void* X, const float* v, float* y, int R, int C, hipStream_t s);
+int avk_gemv_cols_fp8(const void* X, const float* v, float* z, int R, int C, hipStream_t s);
 int avk_gemv_cols_bf16(const void* X, const float* v, float* z, int R, int C, hipStream_t s);
 int avk_hbm_copy(const void* src, void* dst, int64_t bytes, int num_cus, int variant, hipStream_t s);
 int avk_checksum(const void* p, int64_t bytes, unsigned long long* out_dev, hipStream_t s);

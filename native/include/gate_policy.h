@@ -32,7 +32,7 @@
 namespace avk {
 
 struct GateCounters {
-  double mops = 0;         // SQ_INSTS_VALU_MFMA_MOPS_BF16, summed over instances
+  double mops = 0;         // SQ_INSTS_VALU_MFMA_MOPS_<dtype>, summed over instances
   double busy = 0;         // SQ_VALU_MFMA_BUSY_CYCLES, summed over instances
   double waves = 0;        // SQ_WAVES, summed over instances
   double gui = 0;          // GRBM_GUI_ACTIVE, summed over instances (one per XCD)
@@ -49,11 +49,15 @@ struct GateVerdict {
   double util_floor = 0;   // the floor applied (min_util * occupancy)
 };
 
+// `mops_name` / `flop_per_mop`: the MOPS counter of the GEMM's data type
+// (SQ_INSTS_VALU_MFMA_MOPS_BF16 for the default GEMM, _F8 for the mfma-rate
+// step's e4m3 GEMM; profiles/r5_fp8 measured the same 512 FLOP per MOP).
 inline GateVerdict gate_verdict(long long m, long long n, long long k, int cus, const GateCounters& c,
-                                double min_util) {
+                                double min_util, const char* mops_name = "SQ_INSTS_VALU_MFMA_MOPS_BF16",
+                                double flop_per_mop = 512.0) {
   GateVerdict v;
   char buf[256];
-  v.expected_mops = 2.0 * (double)m * (double)n * (double)k / 512.0;
+  v.expected_mops = 2.0 * (double)m * (double)n * (double)k / flop_per_mop;
   const long long tiles = (m / 256) * (n / 256);
   v.expected_waves = (double)tiles * kGemmWavesPerTile;
   const double simds = 4.0 * (cus > 0 ? cus : 0);
@@ -68,7 +72,7 @@ inline GateVerdict gate_verdict(long long m, long long n, long long k, int cus, 
   } else if (!c.output_matches) {
     v.reason = "counted dispatch output differs from the HIP run";
   } else if (!(c.mops == v.expected_mops)) {
-    snprintf(buf, sizeof(buf), "SQ_INSTS_VALU_MFMA_MOPS_BF16 %.0f != 2MNK/512 = %.0f", c.mops, v.expected_mops);
+    snprintf(buf, sizeof(buf), "%s %.0f != 2MNK/%.0f = %.0f", mops_name, c.mops, flop_per_mop, v.expected_mops);
     v.reason = buf;
   } else if (!(c.waves == v.expected_waves)) {
     snprintf(buf, sizeof(buf), "SQ_WAVES %.0f != tiles*%d = %.0f", c.waves, kGemmWavesPerTile, v.expected_waves);

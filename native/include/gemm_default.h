@@ -19,4 +19,9 @@ constexpr int kGemmWavesPerTile = 4;   // kGemmThreads / 64
 constexpr int kGemmTile = 256;         // M and N multiple
 constexpr int kGemmKMultiple = 256;    // K multiple
 
+// gemm_fp8_nt_kernel<OUT_F32=false, EPI=1>: the e4m3 GEMM of the mfma-rate
+// step, same 256x256 tile and 4 waves, the generated main loop of schedule 8
+// (v_mfma_f32_16x16x128_f8f6f4, 128-deep stages)
+constexpr const char* kGemmFp8Symbol = "gemm_fp8_nt_kernelILb0ELi1EE";
+
 }  // namespace avk

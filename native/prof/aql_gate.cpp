@@ -35,7 +35,10 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <fstream>
+#include <map>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -46,15 +49,29 @@ using Clock = std::chrono::steady_clock;
 
 double secs(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
 
-const char* kNames[AVK_AQL_GATE_COUNTERS] = {"SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES",
-                                             "GRBM_GUI_ACTIVE"};
-const hsa_ven_amd_aqlprofile_event_t kEvents[AVK_AQL_GATE_COUNTERS] = {
-    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 52},
-    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 93},
-    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 4},
-    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, 2},
+// Per gated GEMM (AVK_AQL_GATE_BF16 / _FP8): the kernel and the MOPS counter
+// of its data type; the other three counters are the same.  Event ids of
+// ROCm 7.2's gfx950 counter definitions (rocprofiler-sdk counter_defs.yaml):
+// SQ_INSTS_VALU_MFMA_MOPS_BF16 52, SQ_INSTS_VALU_MFMA_MOPS_F8 56.
+struct GateSpec {
+  const char* symbol;
+  const char* names[AVK_AQL_GATE_COUNTERS];
+  hsa_ven_amd_aqlprofile_event_t events[AVK_AQL_GATE_COUNTERS];
 };
-using avk::kGemmSymbol;  // the default GEMM (gemm_default.h)
+const GateSpec kSpecs[2] = {
+    {avk::kGemmSymbol,
+     {"SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"},
+     {{HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 52},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 93},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 4},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, 2}}},
+    {avk::kGemmFp8Symbol,
+     {"SQ_INSTS_VALU_MFMA_MOPS_F8", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"},
+     {{HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 56},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 93},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 4},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, 2}}},
+};
 
 struct Api {
   decltype(&hsa_ven_amd_aqlprofile_validate_event) validate_event = nullptr;
@@ -131,6 +148,7 @@ hsa_status_t find_kernarg_pool(hsa_amd_memory_pool_t p, void* d) {
 }
 
 struct Kernel {
+  const char* symbol = nullptr;  // substring of the mangled name to find
   uint64_t object = 0;
   uint32_t kernarg_size = 0, group_size = 0, private_size = 0;
 };
@@ -145,7 +163,7 @@ hsa_status_t find_kernel(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t 
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_NAME_LENGTH, &len);
   std::string name(len, '\0');
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_NAME, name.data());
-  if (name.find(kGemmSymbol) == std::string::npos) return HSA_STATUS_SUCCESS;
+  if (name.find(k->symbol) == std::string::npos) return HSA_STATUS_SUCCESS;
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k->object);
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k->kernarg_size);
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k->group_size);
@@ -154,6 +172,7 @@ hsa_status_t find_kernel(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t 
 }
 
 struct Sums {
+  const hsa_ven_amd_aqlprofile_event_t* events = nullptr;
   double values[AVK_AQL_GATE_COUNTERS] = {};
   int samples[AVK_AQL_GATE_COUNTERS] = {};
 };
@@ -162,8 +181,8 @@ hsa_status_t collect(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlpro
   if (type != HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA) return HSA_STATUS_SUCCESS;
   auto* s = static_cast<Sums*>(d);
   for (int i = 0; i < AVK_AQL_GATE_COUNTERS; ++i) {
-    if (info->pmc_data.event.block_name == kEvents[i].block_name &&
-        info->pmc_data.event.counter_id == kEvents[i].counter_id) {
+    if (info->pmc_data.event.block_name == s->events[i].block_name &&
+        info->pmc_data.event.counter_id == s->events[i].counter_id) {
       s->values[i] += static_cast<double>(info->pmc_data.result);
       s->samples[i] += 1;
     }
@@ -221,49 +240,42 @@ void* pool_alloc(hsa_amd_memory_pool_t pool, hsa_agent_t gpu, size_t bytes) {
   return p;
 }
 
-}  // namespace
-
-extern "C" const char* avk_aql_gate_counter_name(int i) {
-  return (i >= 0 && i < AVK_AQL_GATE_COUNTERS) ? kNames[i] : "";
-}
-
-extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt, void* C,
-                                 int M, int N, int K, const char* code_object, double timeout_s,
-                                 avk_aql_gate_result* out, char* err, int errlen) {
-  const auto t0 = Clock::now();
-  memset(out, 0, sizeof(*out));
-  hsa_queue_t* queue = nullptr;
-  hsa_signal_t done{0};
+// One per GPU agent (and code object), kept for the life of the process:
+// aqlprofile, the agent lookup, the loaded executable with both gated GEMMs,
+// the private queue and the counter buffers.  The validator gates the bf16
+// GEMM, then the fp8 one (and retries a polluted count), so only the first
+// gate of a process pays the set-up (~5 ms); the rest cost their dispatch.
+// The queue is left to the process exit, like HIP's own.
+struct Session {
+  std::mutex m;
+  bool broken = false;  // a dispatch that never completed: the queue is not reused
+  Api api;
+  AgentSearch as;
+  hsa_amd_memory_pool_t kpool{0};
   hsa_executable_t exe{0};
   hsa_code_object_reader_t reader{0};
-  std::vector<void*> allocs;
-  int rc = -1;
-  try {
+  Kernel kern[2];
+  hsa_queue_t* queue = nullptr;
+  hsa_signal_t done{0};
+  char* karg = nullptr;
+  hsa_ven_amd_aqlprofile_profile_t prof[2]{};
+
+  void open(const char* pci_bus_id, int agent_ordinal, const char* code_object) {
     unsigned dom = 0, bus = 0, dev = 0, fn = 0;
     if (!pci_bus_id || sscanf(pci_bus_id, "%x:%x:%x.%x", &dom, &bus, &dev, &fn) != 4)
       throw Fail{std::string("bad PCI bus id '") + (pci_bus_id ? pci_bus_id : "") + "'"};
-    if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 256) throw Fail{"M, N, K must be multiples of 256"};
-    Api api;
     std::string e;
     if (!api.load(&e)) throw Fail{e};
     g_aql_error = api.error_string;
     check(hsa_init(), "hsa_init");  // reference-counted: HIP holds the runtime already
-    AgentSearch as;
     as.domain = dom;
     as.bdfid = (bus << 8) | (dev << 3) | fn;
     as.ordinal = agent_ordinal;
     check(hsa_iterate_agents(find_agents, &as), "iterate agents");
     if (!as.gpu_ok || !as.cpu_ok) throw Fail{std::string("no HSA agent for ") + pci_bus_id};
-    hsa_amd_memory_pool_t kpool{0};
     check(hsa_amd_agent_iterate_memory_pools(as.cpu, find_kernarg_pool, &kpool), "memory pools");
     if (!kpool.handle) throw Fail{"no kernarg memory pool"};
-    for (const auto& ev : kEvents) {
-      bool ok = false;
-      check(api.validate_event(as.gpu, &ev, &ok), "validate event");
-      if (!ok) throw Fail{"aqlprofile rejects a gate counter on this agent"};
-    }
-
-    // the GEMM kernel from the validator's device code object
+    // the GEMM kernels from the validator's device code object
     std::vector<char> co;
     if (!read_file(code_object, &co)) throw Fail{std::string("cannot read ") + code_object};
     check(hsa_code_object_reader_create_from_memory(co.data(), co.size(), &reader), "code object reader");
@@ -271,77 +283,146 @@ extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, cons
           "executable create");
     check(hsa_executable_load_agent_code_object(exe, as.gpu, reader, nullptr, nullptr), "load code object");
     check(hsa_executable_freeze(exe, nullptr), "executable freeze");
-    Kernel kern;
-    check(hsa_executable_iterate_agent_symbols(exe, as.gpu, find_kernel, &kern), "kernel symbols");
-    if (!kern.object) throw Fail{"GEMM kernel not in the code object"};
-    if (kern.kernarg_size < 36) throw Fail{"unexpected GEMM kernarg layout"};
+    uint32_t karg_size = 0;
+    for (int d = 0; d < 2; ++d) {
+      kern[d].symbol = kSpecs[d].symbol;
+      check(hsa_executable_iterate_agent_symbols(exe, as.gpu, find_kernel, &kern[d]), "kernel symbols");
+      if (!kern[d].object) throw Fail{std::string("GEMM kernel ") + kSpecs[d].symbol + " not in the code object"};
+      if (kern[d].kernarg_size < 36) throw Fail{"unexpected GEMM kernarg layout"};
+      karg_size = std::max(karg_size, kern[d].kernarg_size);
+    }
+    karg = static_cast<char*>(pool_alloc(kpool, as.gpu, karg_size));
+    check(hsa_queue_create(as.gpu, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &queue),
+          "queue create");
+    check(hsa_amd_profiling_set_profiler_enabled(queue, 1), "queue profiling");
+    check(hsa_signal_create(1, 0, nullptr, &done), "signal create");
+  }
 
-    // profile: command buffer (PM4 the CP executes) and output buffer (counter values)
-    hsa_ven_amd_aqlprofile_profile_t prof{};
-    prof.agent = as.gpu;
-    prof.type = HSA_VEN_AMD_AQLPROFILE_EVENT_TYPE_PMC;
-    prof.events = kEvents;
-    prof.event_count = AVK_AQL_GATE_COUNTERS;
+  // the counter profile of `d` (command and output buffers), on first use
+  hsa_ven_amd_aqlprofile_profile_t& profile(int d) {
+    auto& p = prof[d];
+    if (p.command_buffer.ptr) return p;
+    const auto* ev = kSpecs[d].events;
+    for (int i = 0; i < AVK_AQL_GATE_COUNTERS; ++i) {
+      bool ok = false;
+      check(api.validate_event(as.gpu, &ev[i], &ok), "validate event");
+      if (!ok) throw Fail{std::string("aqlprofile rejects ") + kSpecs[d].names[i] + " on this agent"};
+    }
+    p.agent = as.gpu;
+    p.type = HSA_VEN_AMD_AQLPROFILE_EVENT_TYPE_PMC;
+    p.events = ev;
+    p.event_count = AVK_AQL_GATE_COUNTERS;
     uint32_t cmd_size = 0, out_size = 0;
-    check(api.get_info(&prof, HSA_VEN_AMD_AQLPROFILE_INFO_COMMAND_BUFFER_SIZE, &cmd_size), "command buffer size");
-    check(api.get_info(&prof, HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA_SIZE, &out_size), "output buffer size");
+    check(api.get_info(&p, HSA_VEN_AMD_AQLPROFILE_INFO_COMMAND_BUFFER_SIZE, &cmd_size), "command buffer size");
+    check(api.get_info(&p, HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA_SIZE, &out_size), "output buffer size");
     // gfx950, ROCm 7.2: start() refuses the four-counter profile with the
     // sizes get_info reports (any one or two counters pass); 4x both is
     // accepted, and costs 56 KiB of host memory
     cmd_size *= 4;
     out_size *= 4;
-    prof.command_buffer.ptr = pool_alloc(kpool, as.gpu, cmd_size);
-    prof.command_buffer.size = cmd_size;
-    allocs.push_back(prof.command_buffer.ptr);
-    prof.output_buffer.ptr = pool_alloc(kpool, as.gpu, out_size);
-    prof.output_buffer.size = out_size;
-    allocs.push_back(prof.output_buffer.ptr);
-    hsa_ext_amd_aql_pm4_packet_t start{}, stop{}, rd{};
-    if (api.start(&prof, &start) != HSA_STATUS_SUCCESS) {
-      // name the counters aqlprofile refuses on this agent, one profile each
-      std::string bad;
-      for (int i = 0; i < AVK_AQL_GATE_COUNTERS; ++i) {
-        hsa_ven_amd_aqlprofile_profile_t one = prof;
-        one.events = &kEvents[i];
-        one.event_count = 1;
-        hsa_ext_amd_aql_pm4_packet_t pk{};
-        if (api.start(&one, &pk) != HSA_STATUS_SUCCESS) bad += std::string(bad.empty() ? "" : ",") + kNames[i];
-      }
-      std::string pairs;
-      for (int i = 0; i < AVK_AQL_GATE_COUNTERS; ++i)
-        for (int j = i + 1; j < AVK_AQL_GATE_COUNTERS; ++j) {
-          hsa_ven_amd_aqlprofile_event_t two[2] = {kEvents[i], kEvents[j]};
-          hsa_ven_amd_aqlprofile_profile_t p2 = prof;
-          p2.events = two;
-          p2.event_count = 2;
-          hsa_ext_amd_aql_pm4_packet_t pk{};
-          if (api.start(&p2, &pk) != HSA_STATUS_SUCCESS)
-            pairs += std::string(pairs.empty() ? "" : ",") + std::to_string(i) + "+" + std::to_string(j);
-        }
-      throw Fail{"aqlprofile start refused the profile; single-counter profiles refused: " +
-                 (bad.empty() ? std::string("none") : bad) + "; pairs refused: " + (pairs.empty() ? "none" : pairs) +
-                 " (cmd " + std::to_string(cmd_size) + " B, out " + std::to_string(out_size) + " B)"};
-    }
-    check(api.stop(&prof, &stop), "aqlprofile stop");
-    check(api.read(&prof, &rd), "aqlprofile read");
+    p.command_buffer.ptr = pool_alloc(kpool, as.gpu, cmd_size);
+    p.command_buffer.size = cmd_size;
+    p.output_buffer.ptr = pool_alloc(kpool, as.gpu, out_size);
+    p.output_buffer.size = out_size;
+    return p;
+  }
 
-    // kernel arguments: (const bf16* A, const bf16* Bt, void* C, int M, int N, int K)
-    char* karg = static_cast<char*>(pool_alloc(kpool, as.gpu, kern.kernarg_size));
-    allocs.push_back(karg);
+  // aqlprofile refused the profile: name the counters (and pairs) it refuses
+  std::string refused(int d, const hsa_ven_amd_aqlprofile_profile_t& p) {
+    const auto* ev = kSpecs[d].events;
+    std::string bad;
+    for (int i = 0; i < AVK_AQL_GATE_COUNTERS; ++i) {
+      hsa_ven_amd_aqlprofile_profile_t one = p;
+      one.events = &ev[i];
+      one.event_count = 1;
+      hsa_ext_amd_aql_pm4_packet_t pk{};
+      if (api.start(&one, &pk) != HSA_STATUS_SUCCESS) bad += std::string(bad.empty() ? "" : ",") + kSpecs[d].names[i];
+    }
+    std::string pairs;
+    for (int i = 0; i < AVK_AQL_GATE_COUNTERS; ++i)
+      for (int j = i + 1; j < AVK_AQL_GATE_COUNTERS; ++j) {
+        hsa_ven_amd_aqlprofile_event_t two[2] = {ev[i], ev[j]};
+        hsa_ven_amd_aqlprofile_profile_t p2 = p;
+        p2.events = two;
+        p2.event_count = 2;
+        hsa_ext_amd_aql_pm4_packet_t pk{};
+        if (api.start(&p2, &pk) != HSA_STATUS_SUCCESS)
+          pairs += std::string(pairs.empty() ? "" : ",") + std::to_string(i) + "+" + std::to_string(j);
+      }
+    return "aqlprofile start refused the profile; single-counter profiles refused: " +
+           (bad.empty() ? std::string("none") : bad) + "; pairs refused: " + (pairs.empty() ? "none" : pairs) +
+           " (cmd " + std::to_string(p.command_buffer.size) + " B, out " + std::to_string(p.output_buffer.size) + " B)";
+  }
+};
+
+std::mutex g_sessions_m;
+std::map<std::string, Session*> g_sessions;  // by "bus/ordinal/code object"; never freed (process lifetime)
+
+}  // namespace
+
+extern "C" const char* avk_aql_gate_counter_name(int i) {
+  return (i >= 0 && i < AVK_AQL_GATE_COUNTERS) ? kSpecs[0].names[i] : "";
+}
+
+extern "C" const char* avk_aql_gate_counter_name_dtype(int dtype, int i) {
+  return (dtype >= 0 && dtype < 2 && i >= 0 && i < AVK_AQL_GATE_COUNTERS) ? kSpecs[dtype].names[i] : "";
+}
+
+extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt, void* C,
+                                 int M, int N, int K, const char* code_object, double timeout_s,
+                                 avk_aql_gate_result* out, char* err, int errlen) {
+  return avk_aql_gate_gemm_dtype(AVK_AQL_GATE_BF16, pci_bus_id, agent_ordinal, A, Bt, C, M, N, K, code_object,
+                                 timeout_s, out, err, errlen);
+}
+
+extern "C" int avk_aql_gate_gemm_dtype(int dtype, const char* pci_bus_id, int agent_ordinal, const void* A,
+                                       const void* Bt, void* C, int M, int N, int K, const char* code_object,
+                                       double timeout_s, avk_aql_gate_result* out, char* err, int errlen) {
+  const int d = dtype == AVK_AQL_GATE_FP8 ? 1 : 0;
+  const auto t0 = Clock::now();
+  memset(out, 0, sizeof(*out));
+  try {
+    if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 256) throw Fail{"M, N, K must be multiples of 256"};
+    Session* ss = nullptr;
+    {
+      const std::string key = std::string(pci_bus_id ? pci_bus_id : "") + "/" + std::to_string(agent_ordinal) + "/" +
+                              (code_object ? code_object : "");
+      std::lock_guard<std::mutex> l(g_sessions_m);
+      auto it = g_sessions.find(key);
+      if (it != g_sessions.end() && it->second->broken) g_sessions.erase(it), it = g_sessions.end();
+      if (it == g_sessions.end()) {
+        auto* fresh = new Session;
+        try {
+          fresh->open(pci_bus_id, agent_ordinal, code_object);
+        } catch (...) {
+          delete fresh;  // a half-open session is not kept (its HSA objects go with the process)
+          throw;
+        }
+        it = g_sessions.emplace(key, fresh).first;
+      }
+      ss = it->second;
+    }
+    std::lock_guard<std::mutex> l(ss->m);
+    auto& prof = ss->profile(d);
+    memset(prof.output_buffer.ptr, 0, prof.output_buffer.size);
+    hsa_ext_amd_aql_pm4_packet_t start{}, stop{}, rd{};
+    if (ss->api.start(&prof, &start) != HSA_STATUS_SUCCESS) throw Fail{ss->refused(d, prof)};
+    check(ss->api.stop(&prof, &stop), "aqlprofile stop");
+    check(ss->api.read(&prof, &rd), "aqlprofile read");
+    const Kernel& kern = ss->kern[d];
+    // kernel arguments: (const T* A, const T* Bt, void* C, int M, int N, int K)
+    char* karg = ss->karg;
     memcpy(karg + 0, &A, 8);
     memcpy(karg + 8, &Bt, 8);
     memcpy(karg + 16, &C, 8);
     memcpy(karg + 24, &M, 4);
     memcpy(karg + 28, &N, 4);
     memcpy(karg + 32, &K, 4);
-
-    check(hsa_queue_create(as.gpu, 64, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &queue),
-          "queue create");
-    check(hsa_amd_profiling_set_profiler_enabled(queue, 1), "queue profiling");
-    check(hsa_signal_create(1, 0, nullptr, &done), "signal create");
+    hsa_queue_t* queue = ss->queue;
+    hsa_signal_store_relaxed(ss->done, 1);
     out->setup_s = secs(t0);
 
-    // [PM4 start] [GEMM] [PM4 stop -> done]: bodies first, headers last, in order
+    // [PM4 start] [GEMM] [PM4 stop] [PM4 read -> done]: bodies first, headers last, in order
     const uint64_t npk = 4;
     const uint64_t idx = hsa_queue_add_write_index_relaxed(queue, npk);
     auto slot = [&](uint64_t i) {
@@ -350,6 +431,7 @@ extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, cons
     auto* p0 = reinterpret_cast<hsa_ext_amd_aql_pm4_packet_t*>(slot(idx));
     auto* p1 = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(slot(idx + 1));
     auto* p2 = reinterpret_cast<hsa_ext_amd_aql_pm4_packet_t*>(slot(idx + 2));
+    auto* p3 = reinterpret_cast<hsa_ext_amd_aql_pm4_packet_t*>(slot(idx + 3));
     memcpy(reinterpret_cast<char*>(p0) + 4, reinterpret_cast<char*>(&start) + 4, 60);
     p0->completion_signal.handle = 0;
     memset(reinterpret_cast<char*>(p1) + 4, 0, 60);
@@ -367,37 +449,31 @@ extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, cons
     p1->completion_signal.handle = 0;
     memcpy(reinterpret_cast<char*>(p2) + 4, reinterpret_cast<char*>(&stop) + 4, 60);
     p2->completion_signal.handle = 0;
-    auto* p3 = reinterpret_cast<hsa_ext_amd_aql_pm4_packet_t*>(slot(idx + 3));
     memcpy(reinterpret_cast<char*>(p3) + 4, reinterpret_cast<char*>(&rd) + 4, 60);
-    p3->completion_signal = done;
+    p3->completion_signal = ss->done;
     const auto t1 = Clock::now();
     publish(p0, header(HSA_PACKET_TYPE_VENDOR_SPECIFIC), start.pm4_command[0]);
     publish(p1, header(HSA_PACKET_TYPE_KERNEL_DISPATCH), 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS);
     publish(p2, header(HSA_PACKET_TYPE_VENDOR_SPECIFIC), stop.pm4_command[0]);
     publish(p3, header(HSA_PACKET_TYPE_VENDOR_SPECIFIC), rd.pm4_command[0]);
     hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx + npk - 1));
-    hsa_signal_value_t v = 1;
-    while ((v = hsa_signal_wait_scacquire(done, HSA_SIGNAL_CONDITION_LT, 1, 1000000, HSA_WAIT_STATE_BLOCKED)) >= 1) {
-      if (secs(t1) > timeout_s) throw Fail{"counter gate: dispatch did not complete"};
+    while (hsa_signal_wait_scacquire(ss->done, HSA_SIGNAL_CONDITION_LT, 1, 1000000, HSA_WAIT_STATE_BLOCKED) >= 1) {
+      if (secs(t1) > timeout_s) {
+        ss->broken = true;  // its packets may still run: a later gate opens a new session
+        throw Fail{"counter gate: dispatch did not complete"};
+      }
     }
     out->dispatch_s = secs(t1);
     Sums sums;
-    check(api.iterate_data(&prof, collect, &sums), "iterate counter data");
+    sums.events = kSpecs[d].events;
+    check(ss->api.iterate_data(&prof, collect, &sums), "iterate counter data");
     for (int i = 0; i < AVK_AQL_GATE_COUNTERS; ++i) {
       out->values[i] = sums.values[i];
       out->samples[i] = sums.samples[i];
     }
-    rc = 0;
+    return 0;
   } catch (const Fail& f) {
     snprintf(err, errlen, "%s", f.msg.c_str());
   }
-  // a queue whose packets never completed is left to the process exit (the
-  // driver tears it down); everything else is released here
-  if (queue && rc == 0) hsa_queue_destroy(queue);
-  if (done.handle) hsa_signal_destroy(done);
-  if (exe.handle) hsa_executable_destroy(exe);
-  if (reader.handle) hsa_code_object_reader_destroy(reader);
-  if (rc == 0)
-    for (void* p : allocs) hsa_amd_memory_pool_free(p);
-  return rc;
+  return -1;
 }

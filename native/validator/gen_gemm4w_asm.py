@@ -598,9 +598,180 @@ def render4(suffix: str = "", **opts) -> str:
             f"               : \"memory\", \"scc\", {clob});\n"
             "}\n")
 
+# ------------------------------------------------------------ schedule 8 (fp8) --
+# The same ring, units, pieces and barriers as schedule 4b (every byte address
+# of the data movement is schedule 4's: a 128-B row is 64 bf16 or 128 fp8 k),
+# with v_mfma_f32_16x16x128_f8f6f4 (OCP e4m3 A and B: cbsz = blgp = 0) on the
+# stage's whole 128-B rows: twice the cycles of the bf16 16x16x32 at 4x its K,
+# so 2x its FLOP per cycle (MI355X_MICROARCH.md "FP8" row).  A stage is 64
+# MFMAs in two sub-slices of 32 (1,024 MFMA cycles each, as schedule 4's):
+# E(s) rows 0-3 and O(s) rows 4-7 of the wave's 8x8 tiles, both in B-major
+# order (MFMA m = 4j + i').  A fragment is 16 rows x 32 B: lane l holds row
+# l & 15, bytes 32 (l >> 4) .. +31 - two ds_read_b128 into 8 VGPRs.
+#
+# One register set per fragment (128 VGPRs), each read in place:
+#   E(s) reads B4-7(s) (first used at E m = 16: counted lgkmcnt waits) and
+#        A4-7(s) (used in O(s)); their registers were last read in O(s-1);
+#   O(s) reads B0-3(s+1) three MFMAs after each one's last use in O(s), and
+#        A0-3(s+1) (last used in E(s)) - stage s+1's units are visible after
+#        the barrier that ends E(s) (vmcnt(8) there, as in schedule 4).
+# 16 fragment reads per sub-slice either way.  The image swizzle differs from
+# schedule 4's: this read pattern (chunks 2g, 2g + 1 of 16 rows per lane
+# group) meets 16 distinct bank slots per ds_read_b128 lane group under
+# S8_SWZ (tests/test_gemm4w_asm.py), under S4_SWZ it conflicts.
+S8_SWZ = [((r >> 1) & 1) | (((r >> 2) & 1) << 2) for r in range(8)]
+# (operand, 16-B half t of the lane's 32 B) -> fragment base VGPR for slots 0/1, 2/3, 4
+S8_FBASE = {("A", 0): ("v128", "v130", "v132"), ("A", 1): ("v129", "v131", "v133"),
+            ("B", 0): ("v134", "v136", "v138"), ("B", 1): ("v135", "v137", "v139")}
+S8_VOFF = [f"v{140 + j}" for j in range(8)]
+S8_VGPRS = 148
+S8_M0_AT = {4 * q + 2: q for q in range(8)}
+S8_LOAD_AT = {4 * q + 3: q for q in range(8)}
+
+
+def a8(i: int) -> str:
+    return f"v[{8 * i}:{8 * i + 7}]"
+
+
+def b8(j: int) -> str:
+    return f"v[{64 + 8 * j}:{64 + 8 * j + 7}]"
+
+
+def s8_addr(op: str, t: int, slot: int, i: int) -> str:
+    base = S8_FBASE[(op, t)][slot // 2]
+    return f"{base} offset:{(slot % 2) * UNIT_BYTES + i * 2048}"
+
+
+def s8_reads(pos: int) -> dict[int, list[tuple[str, str]]]:
+    """MFMA index -> the fragment reads issued after it, (register, address)."""
+    stage = pos >> 1
+    out: dict[int, list[tuple[str, str]]] = {}
+    if pos % 2 == 0:  # E: this stage's B4-7 (in place), then A4-7
+        aslot, bslot = (2 * stage) % NSLOT, (2 * stage + 1) % NSLOT
+        for n, j in enumerate(range(4, 8)):
+            for t in (0, 1):
+                out.setdefault(2 * n + t, []).append((f"v[{64 + 8 * j + 4 * t}:{64 + 8 * j + 4 * t + 3}]",
+                                                      s8_addr("B", t, bslot, j)))
+        for n, i in enumerate(range(4, 8)):
+            for t in (0, 1):
+                out.setdefault(8 + 2 * n + t, []).append((f"v[{8 * i + 4 * t}:{8 * i + 4 * t + 3}]",
+                                                          s8_addr("A", t, aslot, i)))
+    else:  # O: the next stage's B0-3 after their last use here, and A0-3
+        aslot, bslot = (2 * stage + 2) % NSLOT, (2 * stage + 3) % NSLOT
+        for j in range(4):
+            for t in (0, 1):
+                out.setdefault(4 * j + 6 + t, []).append((f"v[{64 + 8 * j + 4 * t}:{64 + 8 * j + 4 * t + 3}]",
+                                                          s8_addr("B", t, bslot, j)))
+        for i in range(4):
+            for t in (0, 1):
+                out.setdefault(20 + 2 * i + t, []).append((f"v[{8 * i + 4 * t}:{8 * i + 4 * t + 3}]",
+                                                           s8_addr("A", t, aslot, i)))
+    return out
+
+
+def s8_slice(pos: int, first: bool = False, label: str | None = None) -> list[str]:
+    """Sub-slice at body position `pos` (u mod 10): E (even) or O (odd) of
+    stage pos >> 1 (mod 5); loads unit u + 4 like schedule 4b."""
+    even = pos % 2 == 0
+    rows = range(0, 4) if even else range(4, 8)
+    lslot = (pos + 4) % NSLOT
+    src = S4_SA if even else S4_SB
+    reads = s8_reads(pos)
+    issued: list[str] = []  # registers of the DS reads issued so far in this sub-slice, in order
+    lines = [f"{label}:"] if label else []
+    for m in range(32):
+        j, i = m >> 2, rows[m & 3]
+        if even and m % 4 == 0 and j >= 4:
+            # B_j of this stage was read in this sub-slice: wait until its two reads are back
+            # (LDS returns a wave's reads in order: later reads may stay outstanding)
+            last = max(k for k, r in enumerate(issued) if r.startswith(f"v[{64 + 8 * j + 4}:"))
+            lines.append(f"s_waitcnt lgkmcnt({len(issued) - 1 - last})")
+        c = "0" if first else acc(i, j)
+        lines.append(f"v_mfma_f32_16x16x128_f8f6f4 {acc(i, j)}, {b8(j)}, {a8(i)}, {c}")
+        for reg, addr in reads.get(m, []):
+            lines.append(f"ds_read_b128 {reg}, {addr}")
+            issued.append(reg)
+        if m in S8_M0_AT:
+            lines.append(s4_m0(lslot, S8_M0_AT[m]))
+        if m in S8_LOAD_AT:
+            lines.append(f"global_load_lds_dwordx4 {S8_VOFF[S8_LOAD_AT[m]]}, {src}")
+        if m == 20:
+            lines += [f"s_sub_u32 {S4_CNT}, {S4_CNT}, 1"]
+        if m == 21:  # the next unit of this operand exists: move its base one stage on
+            lines += [f"s_cmp_ge_u32 {S4_CNT}, {7 if even else 6}", f"s_cselect_b32 {S4_INC}, 0x80, 0"]
+    lo, hi = (S4_SA_LO, S4_SA_HI) if even else (S4_SB_LO, S4_SB_HI)
+    lines += [f"s_add_u32 {lo}, {lo}, {S4_INC}", f"s_addc_u32 {hi}, {hi}, 0"]
+    if even:
+        lines += ["s_waitcnt vmcnt(8) lgkmcnt(0)", f"s_cmp_eq_u32 {S4_CNT}, 0", "s_cbranch_scc1 3f", "s_barrier"]
+    else:
+        lines += ["s_waitcnt lgkmcnt(0)", f"s_cmp_eq_u32 {S4_CNT}, 0", "s_cbranch_scc1 3f"]
+    return lines
+
+
+def program8() -> list[str]:
+    lines = [f"s_mov_b32 {S4_KEEP}, m0",
+             f"s_mov_b32 {S4_SA_LO}, %[a_lo]", f"s_mov_b32 {S4_SA_HI}, %[a_hi]",
+             f"s_mov_b32 {S4_SB_LO}, %[b_lo]", f"s_mov_b32 {S4_SB_HI}, %[b_hi]",
+             f"s_mov_b32 {S4_WAVE}, %[wave_lds]", f"s_lshl_b32 {S4_CNT}, %[ns], 1",  # sub-slices left, this one included
+             f"s_mov_b32 {S4_ROW}, %[ps]",
+             "v_mov_b32 v128, %[la0]", "v_mov_b32 v129, %[la1]", "v_mov_b32 v134, %[lb0]", "v_mov_b32 v135, %[lb1]",
+             f"v_mov_b32 {S8_VOFF[0]}, %[g_off]"]
+    for op in ("A", "B"):
+        for t in (0, 1):
+            b0, b2, b4 = S8_FBASE[(op, t)]
+            lines += [f"v_add_u32 {b2}, {2 * UNIT_BYTES}, {b0}", f"v_add_u32 {b4}, {4 * UNIT_BYTES}, {b0}"]
+    for j in range(1, 8):
+        lines.append(f"v_add_u32 {S8_VOFF[j]}, {S4_ROW}, {S8_VOFF[j - 1]}")
+    for unit in range(4):  # A_0, B_0, A_1, B_1 into slots 0..3
+        lo, hi, src = (S4_SA_LO, S4_SA_HI, S4_SA) if unit % 2 == 0 else (S4_SB_LO, S4_SB_HI, S4_SB)
+        for j in range(8):
+            lines += [s4_m0(unit, j), "s_nop 0", f"global_load_lds_dwordx4 {S8_VOFF[j]}, {src}"]
+        lines += ["s_nop 4", f"s_add_u32 {lo}, {lo}, 0x80", f"s_addc_u32 {hi}, {hi}, 0"]
+    lines += ["s_waitcnt vmcnt(16)", "s_barrier"]  # A_0, B_0 landed and visible
+    for i in range(4):  # E(0)'s A0-3 and B0-3 (it reads its own B4-7 and O(0)'s A4-7)
+        for t in (0, 1):
+            lines.append(f"ds_read_b128 v[{8 * i + 4 * t}:{8 * i + 4 * t + 3}], {s8_addr('A', t, 0, i)}")
+    for j in range(4):
+        for t in (0, 1):
+            lines.append(f"ds_read_b128 v[{64 + 8 * j + 4 * t}:{64 + 8 * j + 4 * t + 3}], {s8_addr('B', t, 1, j)}")
+    lines += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+    lines += s8_slice(0, first=True)   # E(0), O(0): every accumulator starts from 0
+    lines += s8_slice(1, first=True)
+    lines += ["s_branch 2f"]
+    lines += ["1:"] + s8_slice(0) + s8_slice(1)
+    lines += s8_slice(2, label="2")
+    for pos in range(3, 10):
+        lines += s8_slice(pos)
+    lines += ["s_branch 1b", "3:",
+              "s_waitcnt vmcnt(0)", "s_nop 15", "s_nop 15", f"s_mov_b32 m0, {S4_KEEP}"]
+    return lines
+
+
+def render8() -> str:
+    body = "\\n\\t".join(program8())
+    clob = ", ".join([f'"v{r}"' for r in range(S8_VGPRS)] + [f'"s{r}"' for r in S4_SGPRS]
+                     + [f'"a{r}"' for r in range(256)])
+    return ("// Schedule 8 (OCP fp8 e4m3, v_mfma_f32_16x16x128_f8f6f4): schedule 4b's data movement.\n"
+            "// a_lo/a_hi, b_lo/b_hi: global byte address of this wave's first A / B row\n"
+            "// (rows wave*64..), stage 0; ps: 8 rows in bytes; wave_lds: LDS byte address of\n"
+            "// this wave's first piece (slot 0); ns = K / 128; la0/la1, lb0/lb1: per-lane LDS\n"
+            "// byte address of 16-B half 0 / 1 of fragment 0 of A / B, slot 0; g_off: per-lane\n"
+            "// byte offset in piece 0.\n"
+            "__device__ __forceinline__ void avk_g8_mainloop(unsigned a_lo, unsigned a_hi, unsigned b_lo, unsigned b_hi,\n"
+            "                                                unsigned ps, unsigned wave_lds, unsigned ns, unsigned la0,\n"
+            "                                                unsigned la1, unsigned lb0, unsigned lb1, unsigned g_off) {\n"
+            f'  asm volatile("{body}"\n'
+            "               :\n"
+            "               : [a_lo] \"s\"(a_lo), [a_hi] \"s\"(a_hi), [b_lo] \"s\"(b_lo), [b_hi] \"s\"(b_hi), [ps] \"s\"(ps),\n"
+            "                 [wave_lds] \"s\"(wave_lds), [ns] \"s\"(ns), [la0] \"v\"(la0), [la1] \"v\"(la1),\n"
+            "                 [lb0] \"v\"(lb0), [lb1] \"v\"(lb1), [g_off] \"v\"(g_off)\n"
+            f"               : \"memory\", \"scc\", {clob});\n"
+            "}\n")
+
+
 def render_all() -> str:
     return (render() + render2() + render3() + render4() + render4("b", odd_barrier=False)
-            + render4("c", odd_barrier=False, early_b=True))
+            + render4("c", odd_barrier=False, early_b=True) + render8())
 
 
 if __name__ == "__main__":

@@ -1379,6 +1379,110 @@ __global__ __launch_bounds__(g4::NTHR, 1) void gemm_bf16_nt_4wa_kernel(const __b
                           std::make_integer_sequence<int, 64>{});
 }
 
+// ------------------------------------------------ K2b fp8 (e4m3) GEMM ----
+// The MI355X's fp8 rate (2x bf16 per clock on the f8f6f4 MFMA, ~5 PF dense):
+// C = A . Bt^T with A [M][K], Bt [N][K] OCP e4m3 (row-major bytes), f32
+// accumulation, bf16 or f32 out.  The 4-wave 256x256 tile and schedule 4b's
+// data movement with schedule 8's main loop (gen_gemm4w_asm.py): 64
+// v_mfma_f32_16x16x128_f8f6f4 per 128-deep stage per wave, every fragment in
+// one register set, the image swizzled by g8_swz.  Same epilogues as the bf16
+// kernel (the 16x16 C/D layout does not depend on the data type).
+__device__ __forceinline__ int g8_swz(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 2); }
+
+template <bool OUT_F32, int EPI = 1>
+__global__ __launch_bounds__(g4::NTHR, 1) void gemm_fp8_nt_kernel(const uint8_t* __restrict__ A,
+                                                                 const uint8_t* __restrict__ Bt,
+                                                                 void* __restrict__ Cv, int M, int N, int K) {
+  using namespace g4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid % kNumXcd;
+  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
+  const int per_group = GROUP_M * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid % per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  // this wave's pieces: 8 rows x 128 B (128 k) each, rows wave*64 + 8j; lane
+  // l moves 16 B: row l >> 3, logical chunk (l & 7) ^ g8_swz(row)
+  const uint64_t a0 = reinterpret_cast<uint64_t>(A + (size_t)(m0 + wave * 64) * K);
+  const uint64_t b0 = reinterpret_cast<uint64_t>(Bt + (size_t)(n0 + wave * 64) * K);
+  const int pr = lane >> 3;
+  const unsigned g_off = (unsigned)(pr * K + ((lane & 7) ^ g8_swz(pr)) * 16);
+  const unsigned lds = (unsigned)(uintptr_t)smem;
+  // fragment i: rows 16i + (lane & 15) of the wave's 128, logical chunks
+  // 2 (lane >> 4) and 2 (lane >> 4) + 1 of the 128-B row (32 fp8 of k)
+  const int fr = lane & 15;
+  const unsigned c0 = (unsigned)(((2 * (lane >> 4)) ^ g8_swz(fr & 7)) * 16);
+  const unsigned c1 = (unsigned)(((2 * (lane >> 4) + 1) ^ g8_swz(fr & 7)) * 16);
+  const unsigned la = lds + (wm * 128 + fr) * 128, lb = lds + (wn * 128 + fr) * 128;
+  avk_g8_mainloop(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
+                  __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
+                  (unsigned)(8 * K), __builtin_amdgcn_readfirstlane(lds + wave * 8 * 1024), (unsigned)(K / 128),
+                  la + c0, la + c1, lb + c0, lb + c1, g_off);
+
+  if constexpr (!OUT_F32 && EPI >= 1)
+    g4_store_pairs_bf16<EPI == 2>(reinterpret_cast<__bf16*>(Cv), N, m0 + wm * 128 + fr, n0 + wn * 128, lane >> 4,
+                                  std::make_integer_sequence<int, 32>{});
+  else
+    g4_store_all<OUT_F32>(Cv, N, m0 + wm * 128 + fr, n0 + wn * 128 + (lane >> 4) * 4,
+                          std::make_integer_sequence<int, 64>{});
+}
+
+// OCP e4m3 (gfx950's fp8, not MI300's fnuz): 1 sign, 4 exponent (bias 7), 3
+// mantissa bits; exponent 0 is subnormal (m / 8 * 2^-6), S.1111.111 is NaN
+__device__ __forceinline__ float e4m3_to_f32(uint8_t b) {
+  const unsigned e = (b >> 3) & 15u, m = b & 7u;
+  float v = e ? __builtin_bit_cast(float, ((e + 120u) << 23) | (m << 20)) : (float)m * (1.0f / 512.0f);
+  if (e == 15u && m == 7u) v = __builtin_nanf("");
+  return (b & 0x80) ? -v : v;
+}
+
+struct e4m3 {
+  uint8_t b;
+  __device__ __forceinline__ operator float() const { return e4m3_to_f32(b); }
+};
+
+// random finite e4m3 bytes: sign, exponent field 0..8, any mantissa (|x| <= 3.75)
+__global__ __launch_bounds__(256) void fill_fp8_kernel(uint8_t* __restrict__ p, int64_t n, uint64_t seed) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull ^ seed * 0xD1B54A32D192ED03ull;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+    const unsigned mag = (unsigned)((h >> 8) % 72u);  // exponent 0..8 x mantissa 0..7
+    p[i] = (uint8_t)(((h & 1u) << 7) | ((mag >> 3) << 3) | (mag & 7u));
+  }
+}
+
+// z[c] += sum_{r in slice} X[r][c] * v[r]   (X e4m3 row-major), 8 cols per lane
+__global__ __launch_bounds__(256) void gemv_cols_fp8_kernel(const uint8_t* __restrict__ X, const float* __restrict__ v,
+                                                            float* __restrict__ z, int R, int C, int rows_per_slice) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c0 >= C) return;
+  const int r0 = blockIdx.y * rows_per_slice;
+  const int r1 = min(R, r0 + rows_per_slice);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < r1; ++r) {
+    const uint64_t x = *reinterpret_cast<const uint64_t*>(X + (size_t)r * C + c0);
+    const float vr = v[r];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += e4m3_to_f32((uint8_t)(x >> (8 * j))) * vr;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) atomicAdd(z + c0 + j, s[j]);
+}
+
 // ------------------------------------------------- Freivalds check GEMVs ----
 // y[r] = sum_c X[r][c] * v[c]   (X bf16 or f32, row-major, one wave per row)
 template <typename T>
@@ -1831,6 +1935,47 @@ AVK_API int avk_gemm_bf16_nt(const void* A, const void* Bt, void* C, int out_f32
                              hipStream_t s) {
   return avk_gemm_bf16_nt_variant(A, Bt, C, out_f32, M, N, K,
                                   K % avk::kGemmKMultiple == 0 ? kDefaultGemmVariant : kFallbackGemmVariant, s);
+}
+
+// C = A . Bt^T, OCP e4m3 operands (K a multiple of 256); the fp8 rate step and
+// its counter gate (gate_policy.h, SQ_INSTS_VALU_MFMA_MOPS_F8)
+AVK_API int avk_gemm_fp8_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K, hipStream_t s) {
+  if (!A || !Bt || !C || M <= 0 || N <= 0 || K <= 0) return hipErrorInvalidValue;
+  if (M % avk::kGemmTile || N % avk::kGemmTile || K % 256) return hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)Bt | (uintptr_t)C) % 16 != 0) return hipErrorInvalidValue;
+  const int nwg = (M / g4::BM) * (N / g4::BN);
+  const uint8_t* a = (const uint8_t*)A;
+  const uint8_t* b = (const uint8_t*)Bt;
+  if (out_f32) gemm_fp8_nt_kernel<true><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+  else gemm_fp8_nt_kernel<false, 1><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+  return hipGetLastError();
+}
+
+AVK_API int avk_fill_fp8(void* p, int64_t n, uint64_t seed, hipStream_t s) {
+  if (!p || n < 0) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  fill_fp8_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>((uint8_t*)p, n, seed);
+  return hipGetLastError();
+}
+
+// y = X v, X e4m3 [R][C] (C % 8 == 0)
+AVK_API int avk_gemv_rows_fp8(const void* X, const float* v, float* y, int R, int C, hipStream_t s) {
+  if (!X || !v || !y || R <= 0 || C <= 0 || C % 8) return hipErrorInvalidValue;
+  gemv_rows_kernel<e4m3><<<(R + 3) / 4, 256, 0, s>>>((const e4m3*)X, v, y, R, C);
+  return hipGetLastError();
+}
+
+// z = X^T v accumulated into z (caller zeroes z); X e4m3 [R][C], C % 8 == 0
+AVK_API int avk_gemv_cols_fp8(const void* X, const float* v, float* z, int R, int C, hipStream_t s) {
+  if (!X || !v || !z || R <= 0 || C <= 0 || C % 8 || ((uintptr_t)X % 8)) return hipErrorInvalidValue;
+  const int bx = (C / 8 + 255) / 256;
+  int slices = 256 / bx;
+  if (slices < 1) slices = 1;
+  if (slices > R) slices = R;
+  const int rows_per_slice = (R + slices - 1) / slices;
+  dim3 grid(bx, (R + rows_per_slice - 1) / rows_per_slice);
+  gemv_cols_fp8_kernel<<<grid, 256, 0, s>>>((const uint8_t*)X, v, z, R, C, rows_per_slice);
+  return hipGetLastError();
 }
 
 // y = X v ; X is [R][C] row-major (bf16 when x_is_bf16, else f32); C % 8 == 0

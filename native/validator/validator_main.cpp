@@ -250,6 +250,8 @@ struct Args {
   long long xgmi_elems = 1ll << 22;
   int emulated_peers = 8;
   double min_gemm_tflops = 0;      // for a whole MI355X (256 CUs); applied pro rata to a partition
+  int fp8_n = 4096;                // the gemm_fp8 step (mfma-rate): e4m3 GEMM size
+  double min_fp8_tflops = 0;       // its floor, like min_gemm_tflops
   double min_hbm_gbps = 0;         // idem
   double min_mfma_util = 0;        // counter-gate floor (gate_policy.h), scaled by the launch's occupancy
   double min_rccl_busbw_gbps = 0;  // fp32 all-reduce busBW floor at world > 1
@@ -275,6 +277,10 @@ struct Args {
   int sweep_factor = 4;
   std::string sweep_ops = "allreduce,allgather,reducescatter";
   long long link_bytes = 64ll << 20;  // the xgmi_links step: bytes read over each link
+  // after the report: stay (GPU state held) until this file exists, at most
+  // linger_max_s - see the note at the end of main
+  std::string linger_until;
+  double linger_max_s = 2.0;
 };
 
 struct Step {
@@ -586,7 +592,10 @@ constexpr int kGateAttempts = 3;
 // several GPUs): their gated dispatches take turns, and the first turn starts
 // only once every device has finished its other kernels (arrive() before its
 // gate, or drop() when it ends early), so no kernel of this process runs
-// beside a counted dispatch.
+// beside a counted dispatch.  A device holds its turn from its first gated
+// dispatch until its steps end (run_local_devices), so its later kernels -
+// gemm_fp8's timed dispatches between the bf16 and fp8 gates - never run
+// beside another device's counted dispatch either.
 struct GateTurns {
   std::mutex m;
   std::condition_variable cv;
@@ -610,25 +619,20 @@ struct GateTurns {
   }
 };
 GateTurns* g_gate_turns = nullptr;  // set while devices run concurrently (run_local_devices)
-thread_local bool t_gate_arrived = false;
+thread_local bool t_gate_arrived = false;  // this device holds (or held) its turn
 
+// `dtype`: AVK_AQL_GATE_BF16 (the gemm step's kernel) or AVK_AQL_GATE_FP8
+// (gemm_fp8's); the MOPS counter is that data type's.
 bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int cus, hipStream_t st,
-              std::string* json) {
+              std::string* json, int dtype = AVK_AQL_GATE_BF16) {
+  const char* mops_name = avk_aql_gate_counter_name_dtype(dtype, 0);
   const auto tg = Clock::now();
   unsigned long long* cs;
   HIP_OK(hipMalloc(&cs, 16));
   char bus[64] = {0};
   HIP_OK(hipDeviceGetPCIBusId(bus, sizeof(bus), a.device));
   const std::string co = Gate::exe_dir() + "validator_kernels.co";
-  struct Turn {
-    GateTurns* t;
-    explicit Turn(GateTurns* g) : t(g) {
-      if (t) t->acquire(), t_gate_arrived = true;
-    }
-    ~Turn() {
-      if (t) t->release();
-    }
-  } turn(g_gate_turns);
+  if (g_gate_turns && !t_gate_arrived) g_gate_turns->acquire(), t_gate_arrived = true;  // released by run_local_devices
   avk_aql_gate_result r;
   avk::GateVerdict v;
   bool same = false;
@@ -640,7 +644,8 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
     HIP_OK(hipMemsetAsync(C16, 0, (size_t)n * n * 2, st));
     HIP_OK(hipStreamSynchronize(st));
     char err[512] = {0};
-    const int rc = avk_aql_gate_gemm(bus, a.agent_ordinal, A, B, C16, n, n, n, co.c_str(), 5.0, &r, err, sizeof(err));
+    const int rc =
+        avk_aql_gate_gemm_dtype(dtype, bus, a.agent_ordinal, A, B, C16, n, n, n, co.c_str(), 5.0, &r, err, sizeof(err));
     unsigned long long sums[2] = {0, 0};
     if (rc == 0) {
       AVK_OK(avk_checksum(C16, (int64_t)n * n * 2, cs + 1, st));
@@ -662,7 +667,7 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
     c.gui = r.values[3];
     c.gui_samples = r.samples[3];
     c.output_matches = same;
-    v = avk::gate_verdict(n, n, n, cus, c, a.min_mfma_util);
+    v = avk::gate_verdict(n, n, n, cus, c, a.min_mfma_util, mops_name);
     if (v.ok || !same) break;  // a wrong result is never retried
     reasons += (reasons.empty() ? "" : "; ") + v.reason;
   }
@@ -671,11 +676,11 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
   const double mops = r.values[0], busy = r.values[1], waves = r.values[2], gui = r.values[3];
   const double flops = 2.0 * n * (double)n * n;
   *json = fmt("\"counter_gate\": \"%s\", \"gate_mode\": \"aql\", \"dispatches\": 1, \"gate_attempts\": %d, "
-              "\"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.0f, \"SQ_VALU_MFMA_BUSY_CYCLES\": %.0f, \"SQ_WAVES\": %.0f, "
+              "\"%s\": %.0f, \"SQ_VALU_MFMA_BUSY_CYCLES\": %.0f, \"SQ_WAVES\": %.0f, "
               "\"GRBM_GUI_ACTIVE\": %.0f, \"flop_per_mop\": %.6g, \"samples\": [%d, %d, %d, %d], "
               "\"gated_output_matches\": %s, \"mfma_util\": %.4f, \"mfma_util_floor\": %.4f, "
               "\"gate_seconds\": %.4f, \"gate_setup_seconds\": %.4f, \"gate_dispatch_seconds\": %.4f",
-              v.ok ? "pass" : "fail", attempt, mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0, r.samples[0],
+              v.ok ? "pass" : "fail", attempt, mops_name, mops, busy, waves, gui, mops > 0 ? flops / mops : 0.0, r.samples[0],
               r.samples[1], r.samples[2], r.samples[3], same ? "true" : "false", v.mfma_util, v.util_floor, secs(tg),
               r.setup_s, r.dispatch_s);
   if (!v.ok) *json += ", \"gate_reason\": \"" + v.reason + "\"";
@@ -817,6 +822,82 @@ Step step_gemm(const Args& a, hipStream_t st, int cus) {
   s.seconds = secs(t0);
   s.detail = fmt("\"n\": %d, \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, \"min_tflops\": %.1f, "
                  "\"perf_ok\": %s, ", n, rel, ms, tflops, floor, perf_ok ? "true" : "false") + gate_json;
+  return s;
+}
+
+// gemm_fp8 (label amd.com/gpu.validated.mfma-rate): the matrix cores at the
+// fp8 rate - an OCP e4m3 GEMM on v_mfma_f32_16x16x128_f8f6f4 (2x the bf16
+// FLOP per clock), checked like the gemm step: Freivalds on the fp32-out
+// product (the operands are exact e4m3 values, |x| <= 3.75), the fastest of
+// three trials of bf16-out dispatches against --min-fp8-tflops, and with the
+// counter gate one counted dispatch whose SQ_INSTS_VALU_MFMA_MOPS_F8 must
+// equal 2MNK/512 (aql mode; the sdk tool counts only the bf16 GEMM).
+double fp8_floor(const Args& a, int n, int cus) {
+  return n >= 4096 ? avk::scale_floor_by_cus(a.min_fp8_tflops, cus) : 0.0;
+}
+
+Step step_gemm_fp8(const Args& a, hipStream_t st, int cus) {
+  auto t0 = Clock::now();
+  Step s{"gemm_fp8"};
+  const int n = a.fp8_n;
+  void *A, *B, *C16;
+  float *C32, *x, *y1, *z, *y2;
+  HIP_OK(hipMalloc(&A, (size_t)n * n));
+  HIP_OK(hipMalloc(&B, (size_t)n * n));
+  HIP_OK(hipMalloc(&C16, (size_t)n * n * 2));
+  HIP_OK(hipMalloc(&C32, (size_t)n * n * 4));
+  HIP_OK(hipMalloc(&x, n * 4));
+  HIP_OK(hipMalloc(&y1, n * 4));
+  HIP_OK(hipMalloc(&y2, n * 4));
+  HIP_OK(hipMalloc(&z, n * 4));
+  AVK_OK(avk_fill_fp8(A, (int64_t)n * n, 41, st));
+  AVK_OK(avk_fill_fp8(B, (int64_t)n * n, 42, st));
+  AVK_OK(avk_fill_uniform_f32(x, n, 43, -1, 1, st));
+  AVK_OK(avk_gemm_fp8_nt(A, B, C32, 1, n, n, n, st));
+  AVK_OK(avk_gemv_rows(C32, 0, x, y1, n, n, st));
+  HIP_OK(hipMemsetAsync(z, 0, n * 4, st));
+  AVK_OK(avk_gemv_cols_fp8(B, x, z, n, n, st));
+  AVK_OK(avk_gemv_rows_fp8(A, z, y2, n, n, st));
+  std::vector<float> h1(n), h2(n);
+  HIP_OK(hipMemcpyAsync(h1.data(), y1, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(h2.data(), y2, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  double err = 0, scale = 1e-30;
+  for (int i = 0; i < n; ++i) {
+    err = std::max(err, (double)std::fabs(h1[i] - h2[i]));
+    scale = std::max(scale, (double)std::fabs(h2[i]));
+  }
+  const double rel = err / scale;
+  const bool numerics_ok = std::isfinite(rel) && rel <= 1e-3;
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  AVK_OK(avk_gemm_fp8_nt(A, B, C16, 0, n, n, n, st));  // warm
+  float best_ms = 0;
+  for (int t = 0; t < 3; ++t) {
+    HIP_OK(hipEventRecord(e0, st));
+    for (int i = 0; i < a.gemm_iters; ++i) AVK_OK(avk_gemm_fp8_nt(A, B, C16, 0, n, n, n, st));
+    HIP_OK(hipEventRecord(e1, st));
+    HIP_OK(hipEventSynchronize(e1));
+    float tm = 0;
+    HIP_OK(hipEventElapsedTime(&tm, e0, e1));
+    if (t == 0 || tm < best_ms) best_ms = tm;
+  }
+  std::string gate_json = "\"counter_gate\": \"off\"";
+  bool gate_ok = true;
+  if (a.counter_gate && a.gate_mode == "aql") gate_ok = aql_gate(a, A, B, C16, n, cus, st, &gate_json, AVK_AQL_GATE_FP8);
+  const float ms = best_ms / a.gemm_iters;
+  const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) (void)hipFree(p);
+  const double floor = fp8_floor(a, n, cus);
+  const bool perf_ok = floor <= 0 || tflops >= floor;
+  s.ok = numerics_ok && gate_ok && perf_ok;
+  s.seconds = secs(t0);
+  s.detail = fmt("\"n\": %d, \"dtype\": \"e4m3\", \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, "
+                 "\"min_tflops\": %.1f, \"perf_ok\": %s, ", n, rel, ms, tflops, floor, perf_ok ? "true" : "false") +
+             gate_json;
   return s;
 }
 
@@ -1614,10 +1695,12 @@ std::vector<Step> device_steps(Args ad, bool gate_last, bool with_hip) {
   };
   run("vecadd", [&] { return step_vecadd(ad, sd); });
   if (!gate_last) run("gemm", [&] { return step_gemm(ad, sd, cus); });
+  if (!gate_last) run("gemm_fp8", [&] { return step_gemm_fp8(ad, sd, cus); });
   run("mfma", [&] { return step_mfma(sd); });
   run("hbm", [&] { return step_hbm(ad, sd, cus); });
   run("dmabuf", [&] { return step_dmabuf(sd); });
   if (gate_last) run("gemm", [&] { return step_gemm(ad, sd, cus); });
+  if (gate_last) run("gemm_fp8", [&] { return step_gemm_fp8(ad, sd, cus); });
   if (sd) (void)hipStreamDestroy(sd);
   return out;
 }
@@ -1647,7 +1730,10 @@ std::vector<Step> run_local_devices(const Args& a, const std::vector<std::pair<i
         f.detail = "\"error\": \"" + esc + "\"";
         per[i].push_back(f);
       }
-      if (n > 1 && !t_gate_arrived) turns.drop();  // ended before its gate: the others must not wait for it
+      if (n > 1) {
+        if (t_gate_arrived) turns.release();
+        else turns.drop();  // ended before its gate: the others must not wait for it
+      }
     });
   for (auto& t : threads) t.join();
   g_gate_turns = nullptr;
@@ -1703,11 +1789,12 @@ void usage(const char* p) {
   fprintf(stderr,
           "usage: %s [--device N | --local-bdf BDF | --all-devices] [--expect-devices N]\n"
           "          [--rank R --world W --rendezvous DIR --run-id ID] [--steps a,b,...]\n"
-          "          [--gemm N] [--gemm-iters K] [--hbm-bytes B] [--vecadd-elems N] [--rccl-elems E] [--xgmi-elems E]\n"
+          "          [--gemm N] [--gemm-iters K] [--fp8-gemm N] [--min-fp8-tflops X] [--hbm-bytes B] [--vecadd-elems N] [--rccl-elems E] [--xgmi-elems E]\n"
           "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--rccl-destroy]\n"
           "          [--ready-file PATH] [--start-gate FILE] [--gate-mode aql|sdk] [--min-mfma-util U]\n"
           "          [--min-rccl-busbw-gbps X] [--min-xgmi-read-gbps X] [--peer-timeout S] [--collective-timeout S]\n"
           "          [--sweep-min-bytes B] [--sweep-max-bytes B] [--sweep-factor F] [--sweep-ops a,b] [--link-bytes B]\n"
+          "          [--linger-until FILE] [--linger-max-s S]\n"
           "       %s --check-gate M,N,K,CUS,MOPS,BUSY,WAVES,GUI,GUI_SAMPLES [--min-mfma-util U]\n"
           "          (gate verdict on a counter tuple; no GPU access)\n",
           p, p);
@@ -1747,6 +1834,8 @@ int main(int argc, char** argv) {
     else if (k == "--emulated-peers") a.emulated_peers = atoi(v());
     else if (k == "--min-gemm-tflops") a.min_gemm_tflops = atof(v());
     else if (k == "--min-hbm-gbps") a.min_hbm_gbps = atof(v());
+    else if (k == "--fp8-gemm") a.fp8_n = atoi(v());
+    else if (k == "--min-fp8-tflops") a.min_fp8_tflops = atof(v());
     else if (k == "--min-mfma-util") a.min_mfma_util = atof(v());
     else if (k == "--min-rccl-busbw-gbps") a.min_rccl_busbw_gbps = atof(v());
     else if (k == "--min-xgmi-read-gbps") a.min_xgmi_read_gbps = atof(v());
@@ -1762,6 +1851,8 @@ int main(int argc, char** argv) {
     else if (k == "--sweep-factor") a.sweep_factor = atoi(v());
     else if (k == "--sweep-ops") a.sweep_ops = v();
     else if (k == "--link-bytes") a.link_bytes = atoll(v());
+    else if (k == "--linger-until") a.linger_until = v();
+    else if (k == "--linger-max-s") a.linger_max_s = atof(v());
     else if (k == "--ready-file") a.ready_file = v();
     else if (k == "--start-gate") a.start_gate = v();
     else if (k == "--gate-mode") a.gate_mode = v();
@@ -1770,7 +1861,7 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
-  if (a.world < 1 || a.rank < 0 || a.rank >= a.world || a.gemm_n <= 0 || a.gemm_n % 256 || a.hbm_bytes <= 0 ||
+  if (a.world < 1 || a.rank < 0 || a.rank >= a.world || a.gemm_n <= 0 || a.gemm_n % 256 || a.fp8_n <= 0 || a.fp8_n % 256 || a.hbm_bytes <= 0 ||
       a.hbm_bytes % 16 || a.rccl_elems <= 0 || a.xgmi_elems <= 0 || a.xgmi_elems % 4 || a.emulated_peers < 1 ||
       a.emulated_peers > 8 || a.world > 64 || (a.world > 8 && has_step(a, "xgmi")) || a.sweep_min_bytes < 4 ||
       a.sweep_max_bytes < a.sweep_min_bytes || a.sweep_max_bytes > (16ll << 30) || a.sweep_factor < 2 ||
@@ -1884,6 +1975,8 @@ int main(int argc, char** argv) {
       // one device: the kernel steps in order on the main thread
       if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
       if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st, prop.multiProcessorCount)), steps.back().ok);
+      if (ok && has_step(a, "gemm_fp8"))
+        ok = (steps.push_back(step_gemm_fp8(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
       if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "dmabuf")) ok = (steps.push_back(step_dmabuf(st)), steps.back().ok);
@@ -1981,6 +2074,19 @@ int main(int argc, char** argv) {
     dup2(dn, 1);
     dup2(dn, 2);
     close(dn);
+  }
+  // --linger-until: the caller already has the report (EOF above); the
+  // process keeps its GPU state until the file appears.  Its exit makes the
+  // kernel tear down its KFD process in a workqueue, and another process
+  // opening /dev/kfd meanwhile waits for that work (~0.14 s measured,
+  // BASELINE.md "what a fresh HIP process costs"): the node's plugin-
+  // validation pod starts its HSA runtime right when this process finishes,
+  // and its slow start-ups were the long bring-ups of profiles/r5_ttr.  So
+  // the workload validator leaves once the plugin validation is done.
+  if (!a.linger_until.empty()) {
+    const auto tl = Clock::now();
+    struct stat sb;
+    while (stat(a.linger_until.c_str(), &sb) != 0 && secs(tl) < a.linger_max_s) usleep(1000);
   }
   _exit(ok ? 0 : 1);
 }

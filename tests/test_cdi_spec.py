@@ -126,3 +126,90 @@ def test_runtime_dropins_are_valid_toml_with_the_keys_the_runtimes_read():
     for hooks in (None, "/usr/local/amd/oci-hooks-prestart.d"):
         c = tomli.loads(TK.crio_dropin("/var/run/cdi", hooks))["crio"]["runtime"]
         assert "/var/run/cdi" in c["cdi_spec_dirs"] and (("hooks_dir" in c) == bool(hooks))
+
+
+# containerd 2.x's `containerd config default` (config version 3), trimmed to
+# the parts the operator reads or must leave alone
+CONTAINERD_V3_MAIN = """version = 3
+root = '/var/lib/containerd'
+state = '/run/containerd'
+
+[plugins]
+  [plugins.'io.containerd.cri.v1.images']
+    snapshotter = 'overlayfs'
+
+  [plugins.'io.containerd.cri.v1.runtime']
+    enable_selinux = false
+
+    [plugins.'io.containerd.cri.v1.runtime'.containerd]
+      default_runtime_name = 'runc'
+
+      [plugins.'io.containerd.cri.v1.runtime'.containerd.runtimes]
+        [plugins.'io.containerd.cri.v1.runtime'.containerd.runtimes.runc]
+          runtime_type = 'io.containerd.runc.v2'
+
+          [plugins.'io.containerd.cri.v1.runtime'.containerd.runtimes.runc.options]
+            SystemdCgroup = true
+"""
+
+
+def test_containerd_v2_and_v3_dropins_use_the_keys_each_version_reads():
+    """containerd 2.x (config version 3) split the CRI plugin: runtime
+    handlers, enable_cdi and cdi_spec_dirs moved to io.containerd.cri.v1.runtime.
+    The drop-in follows the main config's version; a version-3 file keeps
+    no key under the version-2 plugin name and the reverse."""
+    import tomli
+
+    from amdgpu_operator.toolkit import install as TK
+
+    assert TK.containerd_config_version(CONTAINERD_V3_MAIN) == 3
+    assert TK.containerd_config_version('version = 2\n[plugins]\n') == 2
+    assert TK.containerd_config_version("[plugins]\nversion = 3\n") == 2  # a key of a table, not the file's version
+    assert TK.containerd_config_version("") == TK.containerd_config_version(None) == 2
+    for version, plugin, other in ((2, "io.containerd.grpc.v1.cri", "io.containerd.cri.v1.runtime"),
+                                   (3, "io.containerd.cri.v1.runtime", "io.containerd.grpc.v1.cri")):
+        d = tomli.loads(TK.dropin_config("amd", "/usr/local/amd/amdgpu-oci-hook", "/var/run/cdi", [], True, version))
+        assert d["version"] == version and other not in d["plugins"]
+        cri = d["plugins"][plugin]
+        assert cri["enable_cdi"] is True and cri["cdi_spec_dirs"] == ["/var/run/cdi", "/etc/cdi"]
+        assert cri["containerd"]["default_runtime_name"] == "amd"
+        rt = cri["containerd"]["runtimes"]["amd"]
+        assert rt["runtime_type"] == "io.containerd.runc.v2" and rt["pod_annotations"] == ["cdi.k8s.io/*"]
+        assert rt["options"] == {"BinaryName": "runc", "SystemdCgroup": True}
+
+
+def test_containerd_v3_install_is_idempotent_and_uninstall_restores(tmp_path):
+    import tomli
+
+    from amdgpu_operator.nodeenv import NodeEnv
+    from amdgpu_operator.testing import fakesys
+    from amdgpu_operator.toolkit import install as TK
+
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 2)
+    cfg = tmp_path / "etc" / "containerd" / "config.toml"
+    cfg.parent.mkdir(parents=True)
+    cfg.write_text(CONTAINERD_V3_MAIN)
+    env = NodeEnv("n1", None, host_root=root, validations_dir=str(tmp_path / "v"), cdi_dir=str(tmp_path / "cdi"),
+                  containerd_config=str(cfg), install_dir=str(tmp_path / "amd"))
+    out = TK.install(env)
+    assert out["config_changed"]
+    dropin = cfg.parent / "conf.d" / TK.DROPIN_NAME
+    d = tomli.loads(dropin.read_text())
+    assert d["version"] == 3 and "io.containerd.cri.v1.runtime" in d["plugins"]
+    main = tomli.loads(cfg.read_text())
+    assert main["version"] == 3 and main["imports"] == [str(dropin)]
+    # the user's runc handler and images settings are untouched
+    assert main["plugins"]["io.containerd.cri.v1.runtime"]["containerd"]["runtimes"]["runc"]["options"]["SystemdCgroup"]
+    assert main["plugins"]["io.containerd.cri.v1.images"]["snapshotter"] == "overlayfs"
+    assert not TK.install(env)["config_changed"]  # idempotent
+    TK.uninstall(env)
+    assert cfg.read_text() == CONTAINERD_V3_MAIN and not dropin.exists()
+    # an upgrade from containerd 1.7 (v2 main config, v2 drop-in) to 2.x (v3 main): the drop-in follows
+    cfg.write_text('version = 2\n[plugins."io.containerd.grpc.v1.cri".containerd.runtimes.runc.options]\n'
+                   "  SystemdCgroup = true\n")
+    TK.install(env)
+    assert tomli.loads(dropin.read_text())["version"] == 2
+    TK.uninstall(env)
+    cfg.write_text(CONTAINERD_V3_MAIN)
+    assert TK.install(env)["config_changed"] and tomli.loads(dropin.read_text())["version"] == 3

@@ -20,6 +20,7 @@ Schedule 4c (avk_g4_mainloop4c) is the shipped one (variant 28).
 """
 
 import importlib.util
+import os
 import pathlib
 import re
 
@@ -225,3 +226,126 @@ def test_schedule4_subslice_invariants(variant):
     finally:
         g.S4_OPTS.update(odd_barrier=True, early_b=False)
     assert sum(ln == "s_barrier" for ln in prog) == 2 + 6 + (5 if variant.get("odd_barrier", True) else 0)
+
+
+# ------------------------------------------------------------ schedule 8 (fp8) --
+
+def test_schedule8_image_is_conflict_free_and_a_bijection():
+    """fp8 fragments read 32 B per lane (chunks 2g, 2g + 1 of the 128-B row,
+    g = lane >> 4) as two ds_read_b128: under S8_SWZ each of the two reads
+    meets 16 distinct bank slots per lane group (under S4_SWZ they collide),
+    and the LDS-DMA side still moves every logical chunk of every row once."""
+    g = _gen()
+    for swz, want_free in ((g.S8_SWZ, True), (g.S4_SWZ, False)):
+        free = True
+        for t in (0, 1):
+            for base in range(0, 256, 16):
+                for grp in _DS_GROUPS:
+                    slots = {(((base + (lane & 15)) * 128 + ((2 * (lane >> 4) + t) ^ swz[lane & 7]) * 16) % 256) // 16
+                             for lane in grp}
+                    free &= len(slots) == 16
+        assert free == want_free
+    got = {((lane >> 3), (lane & 7) ^ g.S8_SWZ[lane >> 3]) for lane in range(64)}
+    assert got == {(r, c) for r in range(8) for c in range(8)}
+    # the two 16-B halves of a lane's 32 B stay a pair of adjacent chunks
+    assert all(((2 * q) ^ s) ^ 1 == (2 * q + 1) ^ s for q in range(4) for s in g.S8_SWZ)
+
+
+def _s8_stream(g):
+    """Schedule 8 in execution order: prologue, the two peeled sub-slices,
+    body positions 2..9, then two full turns of the body."""
+    prog = g.program8()
+    i2 = prog.index("2:")
+    i1 = prog.index("1:")
+    peel_end = prog.index("s_branch 2f")
+    body = prog[i1 + 1:prog.index("s_branch 1b")]
+    body = [ln for ln in body if ln != "2:"]
+    return prog[:peel_end] + prog[i2 + 1:prog.index("s_branch 1b")] + body + body
+
+
+def test_schedule8_fragment_hazards_and_waits():
+    """Every fragment register is overwritten by a DS read only 3 or more MFMAs
+    after the last MFMA that read it, and every MFMA reads only registers
+    whose DS reads have returned (LDS returns a wave's reads in order:
+    ``lgkmcnt(k)`` leaves the last k outstanding)."""
+    import re
+
+    g = _gen()
+    pending: list[int] = []       # first VGPR of each outstanding DS read, in issue order
+    last_use: dict[int, int] = {}  # VGPR -> index of the last MFMA that read it
+    n_mfma = 0
+    for ln in _s8_stream(g):
+        if ln.startswith("s_waitcnt") and "lgkmcnt(" in ln:
+            k = int(re.search(r"lgkmcnt\((\d+)\)", ln).group(1))
+            pending = pending[len(pending) - k:] if k else []
+        elif ln.startswith("ds_read_b128"):
+            lo = int(re.match(r"ds_read_b128 v\[(\d+):", ln).group(1))
+            for r in range(lo, lo + 4):
+                assert n_mfma - last_use.get(r, -99) >= 3, (ln, n_mfma, last_use.get(r))
+            pending.append(lo)
+        elif ln.startswith("v_mfma"):
+            regs = re.findall(r"v\[(\d+):(\d+)\]", ln)
+            assert len(regs) == 2
+            for a, b in regs:
+                busy = [p for p in pending if int(a) <= p <= int(b)]
+                assert not busy, (ln, busy)
+                for r in range(int(a), int(b) + 1):
+                    last_use[r] = n_mfma
+            n_mfma += 1
+    assert n_mfma == 32 * (2 + 8 + 20)
+
+
+def test_schedule8_subslice_shape():
+    g = _gen()
+    for pos in range(10):
+        sl = g.s8_slice(pos)
+        assert sum(ln.startswith("v_mfma_f32_16x16x128_f8f6f4") for ln in sl) == 32
+        assert sum(ln.startswith("ds_read_b128") for ln in sl) == 16
+        assert sum(ln.startswith("global_load_lds_dwordx4") for ln in sl) == 8
+        m0 = [int(ln.rsplit(", ", 1)[1]) for ln in sl if ln.startswith("s_add_u32 m0")]
+        assert {x // g.UNIT_BYTES for x in m0} == {(pos + 4) % 5}  # unit u + 4, as schedule 4
+        assert ("s_barrier" in sl) == (pos % 2 == 0)  # only even sub-slices end with a barrier (schedule 4b)
+        # E reads this stage's units, O the next stage's (slot = base VGPR group x 2 + offset // unit)
+        groups = {b: n for key, bases in g.S8_FBASE.items() for n, b in enumerate(bases)}
+        read_slots = set()
+        for ln in sl:
+            if ln.startswith("ds_read_b128"):
+                base, off = re.search(r", (v\d+) offset:(\d+)", ln).groups()
+                read_slots.add(2 * groups[base] + int(off) // g.UNIT_BYTES)
+        stage = (pos >> 1) + (pos & 1)
+        assert read_slots == {(2 * stage) % 5, (2 * stage + 1) % 5}, (pos, read_slots)
+
+
+def test_agpr_accumulators_live_from_the_main_loop_to_the_epilogue():
+    """the epilogue reads the accumulators by AGPR name in asm
+    statements the compiler knows nothing of.  In the built code object no
+    instruction between a GEMM kernel's last MFMA (the end of the main-loop
+    statement) and its end writes an AGPR (no spill, copy or reuse), all 256
+    are read there, and nothing spills to scratch."""
+    import re
+    import shutil
+    import subprocess
+
+    from amdgpu_operator import native
+
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    assert shutil.which(objdump) or os.path.exists(objdump)
+    co = native.artefact("validator_kernels.co")
+    text = subprocess.run([objdump, "-d", "--no-show-raw-insn", str(co)], capture_output=True, text=True,
+                          check=True).stdout.splitlines()
+    starts = [i for i, ln in enumerate(text) if re.match(r"^[0-9a-f]+ <.*>:$", ln)]
+    checked = 0
+    for k, st in enumerate(starts):
+        name = text[st]
+        if not ("gemm_fp8_nt_kernel" in name or "gemm_bf16_nt_4wa_kernel" in name):
+            continue
+        end = starts[k + 1] if k + 1 < len(starts) else len(text)
+        body = [ln.strip() for ln in text[st + 1:end] if ln.strip() and not ln.strip().startswith(";")]
+        last = max(i for i, ln in enumerate(body) if ln.startswith("v_mfma"))
+        tail = body[last + 1:]
+        assert not [ln for ln in tail if ln.startswith(("v_accvgpr_write", "v_accvgpr_mov", "v_mfma"))], name
+        read = {int(m.group(1)) for ln in tail if (m := re.match(r"v_accvgpr_read_b32 v\d+, a(\d+)", ln))}
+        assert read == set(range(256)), (name, len(read))
+        assert not any("scratch_" in ln for ln in body), name
+        checked += 1
+    assert checked >= 4  # the shipped bf16 default (bf16 and f32 out) and the fp8 kernel (both outs)

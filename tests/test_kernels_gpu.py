@@ -280,3 +280,70 @@ def test_fill_const_and_block_check_match_torch(dtype):
     y[5] += 1
     y[n - 1] = float("nan")
     assert K.check_blocks(y, per, 1.0, 1.0) == 2
+
+
+# ---------------------------------------------------------- K2b fp8 GEMM ----
+_FP8_SHAPES = [(256, 256, 256), (512, 768, 512), (1024, 1024, 1024), (2048, 1024, 4096), (768, 512, 2304),
+               (256, 512, 768)]
+
+
+def _fp8_pair(M, N, Kd, seed):
+    a = torch.empty(M, Kd, device=DEV, dtype=torch.float8_e4m3fn)
+    bt = torch.empty(N, Kd, device=DEV, dtype=torch.float8_e4m3fn)
+    K.fill_fp8_(a, seed)
+    K.fill_fp8_(bt, seed + 1)
+    return a, bt
+
+
+def test_fp8_fill_is_finite_ocp_e4m3_and_deterministic():
+    a = torch.empty(1 << 16, device=DEV, dtype=torch.float8_e4m3fn)
+    K.fill_fp8_(a, 5)
+    x = a.float()
+    assert torch.isfinite(x).all() and x.abs().max().item() <= 3.75 and x.unique().numel() > 100
+    b = torch.empty_like(a)
+    K.fill_fp8_(b, 5)
+    assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", _FP8_SHAPES)
+def test_fp8_gemm_vs_fp32_reference(shape, out_dtype):
+    """The e4m3 GEMM against fp32 torch on the dequantized operands (every
+    e4m3 value is exact in fp32; the products of two are too)."""
+    M, N, Kd = shape
+    a, bt = _fp8_pair(M, N, Kd, M + N + Kd)
+    ref = a.float() @ bt.float().t()
+    out = K.gemm_fp8_nt(a, bt, out_dtype=out_dtype)
+    err = (out.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    tol = 1e-5 * scale if out_dtype == torch.float32 else 8e-3 * scale
+    assert err <= tol, (err, tol)
+
+
+@pytest.mark.parametrize("Kd", [256, 1024])
+def test_fp8_gemm_exact_integer_asymmetric(Kd):
+    """Small integers (exact in e4m3), asymmetric B: a transposed C-write,
+    a swapped fragment half or a wrong LDS swizzle changes the result; every
+    sum is exact in fp32."""
+    M, N = 512, 256
+    i = torch.arange(M, device=DEV).view(M, 1)
+    k = torch.arange(Kd, device=DEV).view(1, Kd)
+    a = ((i * 3 + k * 7) % 5 - 2).float().to(torch.float8_e4m3fn)
+    n = torch.arange(N, device=DEV).view(N, 1)
+    bt = ((n * 11 + k * 2 + (n > k).long()) % 7 - 3).float().to(torch.float8_e4m3fn)
+    ref = a.double() @ bt.double().t()
+    out = K.gemm_fp8_nt(a, bt, out_dtype=torch.float32)
+    assert torch.equal(out.double(), ref)
+    eye = torch.eye(256, device=DEV).to(torch.float8_e4m3fn)
+    bt2 = ((torch.arange(256 * Kd, device=DEV).view(256, Kd) % 9) - 4).float().to(torch.float8_e4m3fn)
+    assert torch.equal(K.gemm_fp8_nt(bt2, eye[:, :Kd] if Kd == 256 else torch.cat(
+        [eye, torch.zeros(256, Kd - 256, device=DEV).to(torch.float8_e4m3fn)], 1), out_dtype=torch.float32),
+        bt2.float()[:, :256])
+
+
+def test_fp8_gemm_rejects_bad_shapes():
+    a = torch.zeros(256, 128, device=DEV, dtype=torch.float8_e4m3fn)
+    with pytest.raises(ValueError):
+        K.gemm_fp8_nt(a, a)
+    with pytest.raises(ValueError):
+        K.gemm_fp8_nt(torch.zeros(256, 256, device=DEV, dtype=torch.bfloat16), a)

@@ -46,6 +46,32 @@ def test_validator_all_local_steps_with_counter_gate(tmp_path):
     assert steps["xgmi"]["emulated"] and steps["xgmi"]["max_abs_err"] <= 8e-5
 
 
+def test_validator_fp8_rate_step_with_counter_gate(tmp_path):
+    """mfma-rate: the e4m3 GEMM on the f8f6f4 MFMA, Freivalds-checked, over
+    its floor, and counted: SQ_INSTS_VALU_MFMA_MOPS_F8 == 2N^3/512 with the
+    default kernel's waves.  Its gate reuses the bf16 gate's HSA session
+    (setup ~0 the second time)."""
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm,gemm_fp8", "--counter-gate",
+                    "--min-fp8-tflops", "1200", "--min-gemm-tflops", "620"])
+    assert rc == 0 and rep["ok"], rep
+    steps = {s["name"]: s for s in rep["steps"]}
+    f = steps["gemm_fp8"]
+    assert f["dtype"] == "e4m3" and f["n"] == 4096 and f["freivalds_rel_err"] < 1e-4
+    assert f["counter_gate"] == "pass" and f["gated_output_matches"], f
+    assert f["SQ_INSTS_VALU_MFMA_MOPS_F8"] * 512 == 2 * 4096 ** 3 and f["flop_per_mop"] == 512
+    assert f["SQ_WAVES"] == (4096 // 256) ** 2 * _WPT
+    assert f["perf_ok"] and f["tflops"] >= 1200 and f["min_tflops"] == 1200
+    assert f["tflops"] > 1.3 * steps["gemm"]["tflops"]  # 2x the FLOP per clock of the bf16 MFMA
+    assert f["gate_setup_seconds"] < 0.002 < steps["gemm"]["gate_setup_seconds"]
+
+
+def test_validator_fp8_floor_fails_the_step(tmp_path):
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm_fp8", "--min-fp8-tflops", "100000"])
+    assert rc != 0 and not rep["ok"]
+    f = {s["name"]: s for s in rep["steps"]}["gemm_fp8"]
+    assert f["perf_ok"] is False and f["min_tflops"] == 100000 and f["freivalds_rel_err"] < 1e-4
+
+
 def test_validator_counter_gate_tool_library_from_env(tmp_path):
     # the operator's path: the tool library is named explicitly (validate.py)
     from amdgpu_operator.validator.validate import gate_env
@@ -137,7 +163,7 @@ def test_validator_sweep_step_one_rank(tmp_path):
     rows = s["rows"]
     for op in ("allreduce", "allgather", "reducescatter"):
         mine = [r for r in rows if r["op"] == op]
-        assert [r["bytes"] for r in mine] == [8 * 4 ** k for k in range(12)] + [16 << 20]
+        assert [r["bytes"] for r in mine] == [8 * 4 ** k for k in range(11)] + [16 << 20]
         assert all(r["mismatches"] == 0 and r["us"] > 0 and r["busbw_gbps"] == 0 for r in mine)  # world 1: no bus
     assert max(r["algbw_gbps"] for r in rows) > 50
 

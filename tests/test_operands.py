@@ -326,7 +326,7 @@ def test_workload_validation_launch_plan(env):
     # one process per GPU: its kernel checks, the xGMI IPC step and RCCL
     assert len(launched) == 2
     for argv, e, device in launched:
-        assert argv[argv.index("--steps") + 1] == "hip,vecadd,gemm,mfma,hbm,xgmi,rccl"
+        assert argv[argv.index("--steps") + 1] == "hip,vecadd,gemm,gemm_fp8,mfma,hbm,xgmi,rccl"
         assert argv[argv.index("--local-bdf") + 1] == gpus[device].bdf and "--counter-gate" in argv
         # it sees its own GPU first, then its peer (RCCL and IPC need the peer visible)
         assert e["ROCR_VISIBLE_DEVICES"].split(",")[0] == f"GPU-{gpus[device].unique_id:016x}"
@@ -336,7 +336,7 @@ def test_workload_validation_launch_plan(env):
         assert e.get("AMDGPU_VALIDATOR_COUNTERS") is None
     assert sorted(d for _, _, d in launched) == [0, 1]
     names = [s["name"] for s in out["ranks"][0]["steps"]]
-    assert names == ["hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl"]
+    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "mfma", "hbm", "xgmi", "rccl"]
     assert V.read_ready(env, "workload")["world"] == 2
 
     def reset():
@@ -361,7 +361,7 @@ def test_workload_validation_launch_plan(env):
     assert all(len(e["ROCR_VISIBLE_DEVICES"].split(",")) == 2 for _, e in rccl)
     assert all("--counter-gate" in a for a, _ in kernel) and not any("--counter-gate" in a for a, _ in rccl)
     names = [s["name"] for s in out["ranks"][0]["steps"]]
-    assert names == ["hip", "vecadd", "gemm", "mfma", "hbm", "xgmi", "rccl"]
+    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "mfma", "hbm", "xgmi", "rccl"]
 
 
 def test_workload_failure_is_reported(env):
@@ -383,7 +383,7 @@ def test_single_gpu_skips_rccl(tmp_path):
 
     env.launcher = launcher
     out = V.validate_workload(env, [])
-    assert seen == ["hip,vecadd,gemm,mfma,hbm,xgmi"]
+    assert seen == ["hip,vecadd,gemm,gemm_fp8,mfma,hbm,xgmi"]
     assert out["ranks"][0]["steps"][-1]["skipped"].startswith("single GPU")
 
 
@@ -407,6 +407,62 @@ def test_complete_publishes_mfma_types_confirmed_on_every_gpu(env):
     labels = env.client.get("v1", "Node", "n1")["metadata"]["labels"]
     assert labels[V.MFMA_LABEL] == "f16.bf16.f64"
     assert V.validated_mfma_dtypes({"ranks": [{"steps": [{"name": "hip"}]}]}) == []
+
+
+def test_complete_publishes_the_validated_mfma_rates(env):
+    """amd.com/gpu.validated.mfma-rate: the GEMM data types whose step held a
+    TF/s floor on every device of every rank; a report-only run (floor 0) or
+    one device short of its floor claims nothing, and a stale claim is taken
+    off the node."""
+    def rank(*gemms):
+        return {"steps": [{"name": "hip", "ok": True}, *gemms]}
+
+    bf16 = {"name": "gemm", "ok": True, "tflops": 1450.0, "min_tflops": 620.0}
+    fp8 = {"name": "gemm_fp8", "ok": True, "tflops": 2900.0, "min_tflops": 1200.0}
+    V.write_ready(env, "workload", {"ranks": [rank(bf16, fp8), rank(bf16, {**fp8, "device": 1})]})
+    assert V.complete(env)["mfma_rate_dtypes"] == ["bf16", "fp8"]
+    assert env.client.get("v1", "Node", "n1")["metadata"]["labels"][V.MFMA_RATE_LABEL] == "bf16.fp8"
+    V.write_ready(env, "workload", {"ranks": [rank(bf16, fp8), rank(bf16, {**fp8, "min_tflops": 0.0})]})
+    assert V.complete(env)["mfma_rate_dtypes"] == ["bf16"]
+    V.write_ready(env, "workload", {"ranks": [rank({**bf16, "ok": False}, fp8)]})
+    assert V.complete(env)["mfma_rate_dtypes"] == ["fp8"]
+    V.write_ready(env, "workload", {"ranks": [rank({**bf16, "min_tflops": 0.0})]})
+    assert V.complete(env)["mfma_rate_dtypes"] == []
+    assert V.MFMA_RATE_LABEL not in env.client.get("v1", "Node", "n1")["metadata"]["labels"]
+
+
+def test_fp8_rate_check_flags_reach_the_validator(tmp_path):
+    """validator.workload.fp8RateCheck / fp8GemmN / minFp8Tflops become the
+    binary's --fp8-gemm / --min-fp8-tflops; switched off, the gemm_fp8 step
+    is dropped from the run (and its floor is not passed)."""
+    from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, ClusterPolicySpec, deep_merge, parse_set_flags
+    from amdgpu_operator.controller import manifests as M
+
+    ref = parse_set_flags(REFERENCE_SET_FLAGS)
+
+    def args(values):
+        ds = [o for o in M.state_validator(ClusterPolicySpec.model_validate(values), "ns", None)
+              if o["kind"] == "DaemonSet"][0]
+        return ds["spec"]["template"]["spec"]["containers"][0]["args"]
+
+    on = args(ref)
+    assert on[on.index("--fp8-gemm") + 1] == "4096" and on[on.index("--min-fp8-tflops") + 1] == "1200"
+    off = args(deep_merge(ref, {"validator": {"workload": {"fp8RateCheck": False}}}))
+    assert "--no-gemm-fp8" in off and "--min-fp8-tflops" not in off and "--fp8-gemm" not in off
+
+    root = str(tmp_path / "h1")
+    fakesys.build_node(root, 1)
+    venv = NodeEnv("n1", None, host_root=root, validations_dir=str(tmp_path / "v"), poll_s=0.01)
+    seen = []
+
+    def launcher(argv, e, device, timeout):
+        seen.append(argv)
+        return ProcResult(0, json.dumps({"ok": True, "steps": []}), "", 0.0)
+
+    venv.launcher = launcher
+    V.validate_workload(venv, ["--no-gemm-fp8", "--fp8-gemm", "8192"])
+    assert seen[0][seen[0].index("--steps") + 1] == "hip,vecadd,gemm,mfma,hbm,xgmi"
+    assert "--no-gemm-fp8" not in seen[0]
 
 
 # ------------------------------------------------------------------ CLI

@@ -80,6 +80,50 @@ def bench_gemm(n, rounds, iters, variants=None):
     return out
 
 
+def bench_fp8(n, rounds, iters):
+    """K2b (OCP e4m3 on v_mfma_f32_16x16x128_f8f6f4, bf16 out) against
+    torch._scaled_mm (hipBLASLt's fp8 GEMM, unit scales, bf16 out) and the
+    bf16 kernel, interleaved on the same random operands; TF/s also against
+    the ~5 PF dense fp8 peak (MI355X_MICROARCH.md)."""
+    a = torch.empty(n, n, device="cuda", dtype=torch.float8_e4m3fn)
+    bt = torch.empty(n, n, device="cuda", dtype=torch.float8_e4m3fn)
+    K.fill_fp8_(a, 11)
+    K.fill_fp8_(bt, 12)
+    c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+    one = torch.ones((), device="cuda", dtype=torch.float32)
+    arms = {"ours_fp8": lambda: K.gemm_fp8_nt(a, bt, out=c)}
+    lib_err = None
+    try:
+        ref = torch._scaled_mm(a, bt.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
+        arms["scaled_mm_fp8"] = lambda: torch._scaled_mm(a, bt.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
+    except Exception as e:  # noqa: BLE001 - no fp8 GEMM in this torch build: report against the peak only
+        ref, lib_err = None, f"{type(e).__name__}: {e}"[:300]
+    ab, bb = a.to(torch.bfloat16), bt.to(torch.bfloat16)
+    c16 = torch.empty_like(c)
+    arms["ours_bf16_same_values"] = lambda: K.gemm_bf16_nt(ab, bb, out=c16)
+    for fn in arms.values():
+        fn()
+    samples = {k: [] for k in arms}
+    for _ in range(rounds):
+        for k, fn in arms.items():
+            samples[k].append(time_ms(fn, iters))
+    fl = 2.0 * n ** 3
+    out = {"n": n}
+    for k, v in samples.items():
+        out[k + "_tflops"] = fl / statistics.median(v) / 1e9
+        out[k + "_tflops_best"] = fl / min(v) / 1e9
+    out["ours_fp8_of_dense_peak"] = out["ours_fp8_tflops"] / 5000.0
+    K.gemm_fp8_nt(a, bt, out=c)
+    exact = a.float() @ bt.float().t()
+    out["ours_fp8_max_rel_err_vs_fp32"] = ((c.float() - exact).abs().max() / exact.abs().max()).item()
+    if ref is not None:
+        out["scaled_mm_max_rel_err_vs_fp32"] = ((ref.float() - exact).abs().max() / exact.abs().max()).item()
+        out["ours_over_scaled_mm"] = out["ours_fp8_tflops"] / out["scaled_mm_fp8_tflops"]
+    else:
+        out["scaled_mm_error"] = lib_err
+    return out
+
+
 def bench_hbm(nbytes, rounds, iters):
     src = torch.empty(nbytes // 4, device="cuda")
     dst = torch.empty_like(src)
@@ -128,10 +172,13 @@ def main():
     ap.add_argument("--gemm-variants", type=int, nargs="+", default=None,
                     help="GEMM A/B only: these variants (the first is reported as ours) vs hipBLASLt")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--fp8", action="store_true", help="the fp8 GEMM vs torch._scaled_mm only (4096^3, 8192^3)")
     args = ap.parse_args()
     t0 = time.time()
     out = {"device": torch.cuda.get_device_name(0)}
-    if args.gemm_variants:
+    if args.fp8:
+        out["fp8"] = [bench_fp8(n, args.rounds, 10) for n in (4096, 8192)]
+    elif args.gemm_variants:
         out["gemm"] = [bench_gemm(n, args.rounds, 10, args.gemm_variants) for n in (4096, 8192)]
     elif args.quick:
         out["gemm"] = [bench_gemm(4096, 2, 5)]
