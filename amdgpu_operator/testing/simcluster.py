@@ -1083,7 +1083,7 @@ class SimCluster:
 
             argv = [str(native.binary("amdgpu-nfd")), *cmd[1:]]
         else:
-            argv = [sys.executable, "-m", "amdgpu_operator", *cmd[1:]]
+            argv = [sys.executable, "-S", "-m", "amdgpu_operator", *cmd[1:]]  # as the images' entry point
         with open(os.path.join(d, "log"), "w") as log_f:
             p = subprocess.Popen(argv, env=penv, stdout=log_f, stderr=subprocess.STDOUT, start_new_session=True)
         self.process_stats.append(rec)

@@ -722,11 +722,16 @@ def program8() -> list[str]:
             lines += [f"v_add_u32 {b2}, {2 * UNIT_BYTES}, {b0}", f"v_add_u32 {b4}, {4 * UNIT_BYTES}, {b0}"]
     for j in range(1, 8):
         lines.append(f"v_add_u32 {S8_VOFF[j]}, {S4_ROW}, {S8_VOFF[j - 1]}")
+    # the step to stage 2 only when there is one (K = 256 has stages 0 and 1):
+    # the first sub-slices load the stage the pointers hold before their own
+    # INC check, so with ns = 2 they re-load stage 1 into the free ring unit
+    # instead of reading 128 B past the end of the last row of A / Bt
+    lines += [f"s_cmp_gt_u32 %[ns], 2", f"s_cselect_b32 {S4_INC}, 0x80, 0"]
     for unit in range(4):  # A_0, B_0, A_1, B_1 into slots 0..3
         lo, hi, src = (S4_SA_LO, S4_SA_HI, S4_SA) if unit % 2 == 0 else (S4_SB_LO, S4_SB_HI, S4_SB)
         for j in range(8):
             lines += [s4_m0(unit, j), "s_nop 0", f"global_load_lds_dwordx4 {S8_VOFF[j]}, {src}"]
-        lines += ["s_nop 4", f"s_add_u32 {lo}, {lo}, 0x80", f"s_addc_u32 {hi}, {hi}, 0"]
+        lines += ["s_nop 4", f"s_add_u32 {lo}, {lo}, {'0x80' if unit < 2 else S4_INC}", f"s_addc_u32 {hi}, {hi}, 0"]
     lines += ["s_waitcnt vmcnt(16)", "s_barrier"]  # A_0, B_0 landed and visible
     for i in range(4):  # E(0)'s A0-3 and B0-3 (it reads its own B4-7 and O(0)'s A4-7)
         for t in (0, 1):

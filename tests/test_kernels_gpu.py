@@ -308,16 +308,39 @@ def test_fp8_fill_is_finite_ocp_e4m3_and_deterministic():
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", _FP8_SHAPES)
 def test_fp8_gemm_vs_fp32_reference(shape, out_dtype):
-    """The e4m3 GEMM against fp32 torch on the dequantized operands (every
-    e4m3 value is exact in fp32; the products of two are too)."""
+    """The e4m3 GEMM against the fp64 product of the dequantized operands
+    and against hipBLASLt's fp8 GEMM (torch._scaled_mm, unit scales).  The
+    f8f6f4 MFMA does not keep a full fp32 sum inside one instruction: on
+    gfx950 both kernels land ~5e-5 of the output's scale from the exact
+    result (profiles/r5_fp8/diag.json), where an fp32 GEMM lands ~1e-6.  So
+    the check against the exact product is loose, and the one against
+    hipBLASLt, which runs the same instruction in another order, is tight."""
     M, N, Kd = shape
     a, bt = _fp8_pair(M, N, Kd, M + N + Kd)
-    ref = a.float() @ bt.float().t()
+    ref = a.double() @ bt.double().t()
     out = K.gemm_fp8_nt(a, bt, out_dtype=out_dtype)
-    err = (out.float() - ref).abs().max().item()
     scale = ref.abs().max().item()
-    tol = 1e-5 * scale if out_dtype == torch.float32 else 8e-3 * scale
-    assert err <= tol, (err, tol)
+    err = (out.double() - ref).abs().max().item()
+    assert err <= (2e-4 if out_dtype == torch.float32 else 8e-3) * scale, (err, scale)
+    one = torch.ones((), device=DEV)
+    lt = torch._scaled_mm(a, bt.t(), scale_a=one, scale_b=one, out_dtype=out_dtype)
+    err_lt = (out.double() - lt.double()).abs().max().item()
+    assert err_lt <= (1e-5 if out_dtype == torch.float32 else 8e-3) * scale, (err_lt, scale)
+
+
+def test_fp8_gemm_one_k_block_matches_hipblaslt():
+    """One MFMA's worth of K per output (A zero beyond k = 128): the rest of
+    the sum adds zeros, so the result is hipBLASLt's to within a rounding of
+    the order it adds its partial sums in (bit-equal at 1024 x 1024 x 4096 in
+    profiles/r5_fp8/diag.json)."""
+    a, bt = _fp8_pair(512, 256, 512, 77)
+    a = a.view(torch.uint8).clone()
+    a[:, 128:] = 0
+    a = a.view(torch.float8_e4m3fn)
+    one = torch.ones((), device=DEV)
+    lt = torch._scaled_mm(a, bt.t(), scale_a=one, scale_b=one, out_dtype=torch.float32)
+    out = K.gemm_fp8_nt(a, bt, out_dtype=torch.float32)
+    assert (out - lt).abs().max().item() <= 2e-6 * lt.abs().max().item()
 
 
 @pytest.mark.parametrize("Kd", [256, 1024])

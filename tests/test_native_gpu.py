@@ -56,7 +56,7 @@ def test_validator_fp8_rate_step_with_counter_gate(tmp_path):
     assert rc == 0 and rep["ok"], rep
     steps = {s["name"]: s for s in rep["steps"]}
     f = steps["gemm_fp8"]
-    assert f["dtype"] == "e4m3" and f["n"] == 4096 and f["freivalds_rel_err"] < 1e-4
+    assert f["dtype"] == "e4m3" and f["n"] == 4096 and f["freivalds_rel_err"] < 1e-3
     assert f["counter_gate"] == "pass" and f["gated_output_matches"], f
     assert f["SQ_INSTS_VALU_MFMA_MOPS_F8"] * 512 == 2 * 4096 ** 3 and f["flop_per_mop"] == 512
     assert f["SQ_WAVES"] == (4096 // 256) ** 2 * _WPT
@@ -69,7 +69,7 @@ def test_validator_fp8_floor_fails_the_step(tmp_path):
     rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm_fp8", "--min-fp8-tflops", "100000"])
     assert rc != 0 and not rep["ok"]
     f = {s["name"]: s for s in rep["steps"]}["gemm_fp8"]
-    assert f["perf_ok"] is False and f["min_tflops"] == 100000 and f["freivalds_rel_err"] < 1e-4
+    assert f["perf_ok"] is False and f["min_tflops"] == 100000 and f["freivalds_rel_err"] < 1e-3
 
 
 def test_validator_counter_gate_tool_library_from_env(tmp_path):
