@@ -995,8 +995,15 @@ class SimCluster:
         self.events.append((time.perf_counter(), what, detail))
 
     def _trace_api(self, etype: str, obj: dict) -> None:
-        if obj.get("kind") == "Pod" and etype in ("ADDED", "DELETED"):
+        kind = obj.get("kind")
+        if kind == "Pod" and etype in ("ADDED", "DELETED"):
             self.trace(f"pod-{etype.lower()}", obj["metadata"]["name"])
+        elif kind == "DaemonSet" and etype == "MODIFIED":  # the status the operator's states read
+            st = obj.get("status") or {}
+            if st.get("desiredNumberScheduled") and st.get("numberReady") == st.get("desiredNumberScheduled"):
+                self.trace("ds-ready", obj["metadata"]["name"])
+        elif kind == "ClusterPolicy" and etype == "MODIFIED":
+            self.trace("policy-status", (obj.get("status") or {}).get("state") or "")
 
     def trace_since(self, t0: float) -> list[tuple[float, str, str]]:
         """Events after ``t0`` (perf_counter), times relative to it."""

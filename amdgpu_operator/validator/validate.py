@@ -378,11 +378,12 @@ def planned_workload_processes(env: NodeEnv, args: list[str], budget: int) -> in
     return workload_processes(world, run_rccl, "--rccl-separate-process" in args, budget)[0]
 
 
-# The workload validator processes stay until the plugin validation is done
-# (``--linger-until`` its ready file): their exit would tear down their KFD
-# processes right when the plugin pod starts its HSA runtime, which then waits
-# for that teardown (validator_main.cpp, end of main).  =0: exit at once (A/B).
-LINGER = os.environ.get("AMDGPU_VALIDATOR_LINGER", "1") == "1"
+# AMDGPU_VALIDATOR_LINGER=1: the workload validator processes stay until the
+# plugin validation is done (``--linger-until`` its ready file), so their KFD
+# teardown cannot overlap the plugin pod's HSA start-up (validator_main.cpp,
+# end of main).  Off by default: interleaved A/B on the MI355X found no gain
+# (0.386 / 0.384 s with, 0.376 / 0.379 s without; profiles/r5_ttr/linger).
+LINGER = os.environ.get("AMDGPU_VALIDATOR_LINGER", "0") == "1"
 LINGER_MAX_S = 3.0
 
 

@@ -54,6 +54,8 @@ def parse():
                     help="CPU-only, but start stand-in validator processes through the rank launcher")
     ap.add_argument("--sysfs-root", default=None, help="default: / when a GPU is present, else synthetic")
     ap.add_argument("--quick-workload", action="store_true", help="small validator sizes (CI)")
+    ap.add_argument("--operator-debounce", type=float, default=0.02,
+                    help="the operator's reconcile debounce (s; the chart's default, cli/main.py --debounce)")
     ap.add_argument("--no-counter-gate", action="store_true", help="skip the rocprofiler counter gate (outer profiler)")
     ap.add_argument("--rccl-single-gpu", action="store_true",
                     help="rehearsal: run the RCCL validation process at N=1 too (multi-GPU critical path)")
@@ -83,9 +85,9 @@ def parse():
     ap.add_argument("--settle-s", type=float, default=0.0,
                     help="start each bring-up this long after the previous one's cluster stopped (its GPU processes' "
                          "teardown in the kernel; 0: back to back)")
-    ap.add_argument("--no-linger", action="store_true",
-                    help="A/B: the workload validator processes exit at their report instead of after the plugin "
-                         "validation (AMDGPU_VALIDATOR_LINGER=0)")
+    ap.add_argument("--linger", action="store_true",
+                    help="A/B: the workload validator processes stay until the plugin validation is done "
+                         "(AMDGPU_VALIDATOR_LINGER=1) instead of exiting at their report")
     ap.add_argument("--no-tool-watch", action="store_true",
                     help="do not watch for GPU tools of other parties (amd-smi, rocm-smi, ...) during the bring-ups")
     ap.add_argument("--timeout", type=float, default=120.0)
@@ -390,7 +392,7 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
     # termination_s=0: kubelet-confirmed pod deletes, as on a cluster
     cluster = SimCluster(d, [node], fake_gpu=fake_gpu, poll_s=0.005, launcher=launcher, agent_poll_s=agent_poll,
                          node_status_s=args.kubelet_status_s or None, termination_s=0.0,
-                         operator_resync_s=30.0, operator_debounce_s=0.02,  # cli/main.py defaults
+                         operator_resync_s=30.0, operator_debounce_s=args.operator_debounce,  # cli/main.py defaults
                          process_containers=(mode == "process")).start()
     import gc
 
@@ -482,7 +484,13 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
                 st = {}
                 for x in rep.get("steps", []):
                     st[x["name"]] = round(st.get(x["name"], 0.0) + x.get("seconds", 0.0), 4)
-                pod_reps.append({"proc": rep.get("seconds"), "hsa_init": rep.get("hsa_init_s"), **st})
+                main_at = None
+                if isinstance(rep.get("t_main"), (int, float)):  # CLOCK_MONOTONIC at the pod process's main
+                    main_at = round(rep["t_main"] - (time.monotonic() - time.perf_counter()) - t0, 4)
+                pod_reps.append({"proc": rep.get("seconds"), "hsa_init": rep.get("hsa_init_s"), **st,
+                                 "main_at": main_at,
+                                 "done_at": round(main_at + rep["seconds"], 4) if main_at is not None
+                                 and isinstance(rep.get("seconds"), (int, float)) else None})
         return {
             "mode": mode,
             "t0_wall": t0_wall,
@@ -611,8 +619,8 @@ def failure_line(args, n_gpus: int, fake_gpu, err: dict, results: list, warm: li
 
 def main():
     args = parse()
-    if args.no_linger:  # read by the validator operand processes (validate.py LINGER)
-        os.environ["AMDGPU_VALIDATOR_LINGER"] = "0"
+    if args.linger:  # read by the validator operand processes (validate.py LINGER)
+        os.environ["AMDGPU_VALIDATOR_LINGER"] = "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

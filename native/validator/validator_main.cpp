@@ -2075,14 +2075,12 @@ int main(int argc, char** argv) {
     dup2(dn, 2);
     close(dn);
   }
-  // --linger-until: the caller already has the report (EOF above); the
-  // process keeps its GPU state until the file appears.  Its exit makes the
-  // kernel tear down its KFD process in a workqueue, and another process
-  // opening /dev/kfd meanwhile waits for that work (~0.14 s measured,
-  // BASELINE.md "what a fresh HIP process costs"): the node's plugin-
-  // validation pod starts its HSA runtime right when this process finishes,
-  // and its slow start-ups were the long bring-ups of profiles/r5_ttr.  So
-  // the workload validator leaves once the plugin validation is done.
+  // --linger-until (opt-in, validate.py AMDGPU_VALIDATOR_LINGER=1): the
+  // caller already has the report (EOF above); the process keeps its GPU
+  // state until the file appears, so its KFD teardown cannot overlap the
+  // plugin-validation pod's HSA start-up.  The interleaved A/B on the
+  // MI355X found no gain from it (profiles/r5_ttr/linger), so the default
+  // is to exit here at once.
   if (!a.linger_until.empty()) {
     const auto tl = Clock::now();
     struct stat sb;

@@ -733,3 +733,31 @@ def test_every_rendered_container_command_parses(flags):
     assert {"driver", "validate"} <= seen
     if flags:
         assert "dra-driver" in seen
+
+
+def test_operands_start_without_site(tmp_path):
+    """Operand containers run `python3 -S -m amdgpu_operator` (the images'
+    entry script, the simulated kubelet): each operand's modules load from
+    the package alone - no site-packages module on the start-up path - and
+    the -S fallback still finds installed packages for the ones that want
+    them later (yaml for config files)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, runpy\n"
+            "import amdgpu_operator.cli.main, amdgpu_operator.cli.operands, amdgpu_operator.validator.validate\n"
+            "import amdgpu_operator.deviceplugin.server, amdgpu_operator.driver.manager, amdgpu_operator.toolkit.install\n"
+            "import amdgpu_operator.exporter.metrics\n"
+            "third = sorted({m.split('.')[0] for m in sys.modules} & {'yaml', 'pydantic', 'numpy', 'torch', 'grpc', "
+            "'requests', 'certifi', 'pydantic_core'})\n"
+            "print(third)\n")
+    p = subprocess.run([sys.executable, "-S", "-c", code], env={**os.environ, "PYTHONPATH": root},
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.strip() == "[]"
+    p = subprocess.run([sys.executable, "-S", "-m", "amdgpu_operator", "render", "--help"],
+                       env={**os.environ, "PYTHONPATH": root}, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    with open(os.path.join(root, "deploy", "images", "amd-device-plugin", "Dockerfile")) as f:
+        assert "exec python3 -S -m amdgpu_operator" in f.read()
