@@ -148,6 +148,7 @@ class ClusterPolicyReconciler:
         self.clock = clock
         self._ready_at: dict[str, dict[str, float]] = {}  # policy uid -> state -> seconds since creation
         self._created_at: dict[str, float] = {}
+        self._nodes_changed = False  # a Node event since this pass labelled the nodes (set by the watches)
         self._ttr: dict[str, float] = {}
         self.reconciles = 0
         self.metrics = ReconcileMetrics()
@@ -235,13 +236,24 @@ class ClusterPolicyReconciler:
 
         if spec.psa.enabled:
             self._label_namespace_psa()
+        self._nodes_changed = False
         gpu_nodes, patched, nfd_scanned, node_labels = label_nodes(self.client, spec)
         owner = owner_ref(cp)
         results: list[StateResult] = []
         driver_live = None
         pool_status = None
         ds_ready: dict[str, bool] = {}
+        midpass = not os.environ.get("AMDGPU_EXPERIMENT_NO_MIDPASS_LABELS")  # A/B switch (profiles/r5_ttr)
         for state, key in STATES:
+            if self._nodes_changed and midpass:
+                # a node changed during this pass (NFD's labels come in during
+                # the pass that created NFD, ~30 ms of creates on the box): its
+                # GPU-node labels go on now, so the DaemonSets created later in
+                # this pass, and those before it, get their pods without
+                # waiting for the next pass
+                self._nodes_changed = False
+                gpu_nodes, again, nfd_scanned, node_labels = label_nodes(self.client, spec)
+                patched = patched or again
             enabled = operand_enabled(spec, key)
             objs = STATE_BUILDERS[state](spec, self.namespace, owner)
             unlabelled: list[str] = []
@@ -458,14 +470,19 @@ class ClusterPolicyReconciler:
             # so the first pass does not wait for the initial lists; the
             # informers end with ``stop`` (e.g. leadership lost), and so does
             # this wrapping: a later run() builds fresh caches
-            self.client = CachedClient(server, self.cached_kinds(), stop, on_event=events.put)
+            def on_event(kind):
+                if kind == "Node":
+                    self._nodes_changed = True
+                events.put((kind, time.monotonic()))
+
+            self.client = CachedClient(server, self.cached_kinds(), stop, on_event=on_event)
         else:
             watches = [(CP_API, "ClusterPolicy", None), ("v1", "Node", None), ("apps/v1", "DaemonSet", self.namespace),
                        (CP_API, "AMDGPUDriver", None)]
             for av, kind, ns in watches:
                 threading.Thread(target=self._pump, args=(av, kind, ns, events, stop), daemon=True,
                                  name=f"operator-watch-{kind}").start()
-        events.put("start")
+        events.put(("start", time.monotonic()))
         try:
             self._loop(stop, events, resync_s, debounce_s, on_result)
         finally:
@@ -477,9 +494,9 @@ class ClusterPolicyReconciler:
         # triggering event and at the pass's start, its duration, the trigger)
         trace = os.environ.get("AMDGPU_RECONCILE_TRACE")
         while not stop.is_set():
-            trigger = "resync"
+            trigger, t_first = "resync", time.monotonic()
             try:
-                trigger = events.get(timeout=min(resync_s, 0.5))
+                trigger, t_first = events.get(timeout=min(resync_s, 0.5))
             except queue.Empty:
                 if time.monotonic() - last < resync_s:
                     continue
@@ -489,8 +506,12 @@ class ClusterPolicyReconciler:
             # event close behind a pass - usually the echo of that pass's own
             # writes - waits out the rest of the debounce window so a burst
             # costs one pass (the rest only: an operand that turns Ready just
-            # after a pass, e.g. the validator, is seen at most debounce_s later)
-            wait = debounce_s - (time.monotonic() - last)
+            # after a pass, e.g. the validator, is seen at most debounce_s
+            # later).  The window runs from the earlier of the pass's end and
+            # the event: an event that came in during a long pass (NFD's node
+            # labels during the pass that created NFD, ~30 ms over HTTP) has
+            # waited already and starts the next pass at once.
+            wait = debounce_s - (time.monotonic() - min(last, t_first))
             if wait > 0:
                 time.sleep(wait)
             while True:  # coalesce bursts
@@ -516,7 +537,9 @@ class ClusterPolicyReconciler:
         while not stop.is_set():
             try:
                 for _etype, _obj in self.client.watch(av, kind, namespace=ns, stop=stop):
-                    events.put(kind)
+                    if kind == "Node":
+                        self._nodes_changed = True
+                    events.put((kind, time.monotonic()))
             except Exception as e:  # noqa: BLE001 - re-establish the watch
                 log.debug("watch %s ended: %s", kind, e)
                 stop.wait(0.5)
