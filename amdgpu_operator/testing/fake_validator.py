@@ -308,6 +308,17 @@ def _main(argv: list[str]) -> int:
     if world > 1:
         rv.finish(rep["ok"], rep.get("error", ""))
     print(json.dumps(rep))
+    sys.stdout.flush()
+    # the report in a file as well, like the native checks: --result-file
+    # (amdgpu-gpu-check) always, --ready-file (amdgpu-validator) when ok
+    for flag, always in (("--result-file", True), ("--ready-file", False)):
+        path = arg(flag, None)
+        if path and (always or rep["ok"]):
+            with open(path + ".tmp", "w") as f:
+                f.write(json.dumps(rep))
+            os.replace(path + ".tmp", path)
+    if os.environ.get("AMDGPU_FAKE_POD_EXIT_S") and "--pod-check" in argv:  # the kernel's release of a GPU process
+        time.sleep(float(os.environ["AMDGPU_FAKE_POD_EXIT_S"]))
     return 0 if rep["ok"] else 1
 
 

@@ -94,6 +94,7 @@ def fake_validator_result(argv: list[str], env: dict | None = None) -> ProcResul
     if "--pod-check" in argv and expect >= 0 and seen is not None and seen != expect:
         rep = {"ok": False, "simulated": True, "error": f"{expect} GPU(s) allocated to the pod, {seen} visible",
                "steps": []}
+        _write_result(argv, rep)
         return ProcResult(1, json.dumps(rep) + "\n", "", 0.0)
     steps = arg("--steps", "hip,vecadd,gemm,mfma,hbm,xgmi,rccl").split(",")
     rank, world = int(arg("--rank", "0")), int(arg("--world", "1"))
@@ -104,7 +105,18 @@ def fake_validator_result(argv: list[str], env: dict | None = None) -> ProcResul
            "seconds": 0.0, "steps": recs, "rocr_visible_devices": (env or {}).get("ROCR_VISIBLE_DEVICES")}
     if not ok:
         rep["error"] = f"step {next(r['name'] for r in recs if not r['ok'])} failed"
+    _write_result(argv, rep)
     return ProcResult(0 if ok else 1, json.dumps(rep) + "\n", "", 0.0)
+
+
+def _write_result(argv: list[str], rep: dict) -> None:
+    """The native checks' report file (--result-file always, --ready-file when ok)."""
+    for flag, always in (("--result-file", True), ("--ready-file", False)):
+        if flag in argv and (always or rep.get("ok")):
+            path = argv[argv.index(flag) + 1]
+            with open(path + ".tmp", "w") as f:
+                f.write(json.dumps(rep))
+            os.replace(path + ".tmp", path)
 
 
 class _PodRun:
@@ -407,7 +419,8 @@ class SimCluster:
     def _launch(self, argv, env, device, timeout) -> ProcResult:
         if self.fake_gpu and argv and os.path.basename(argv[0]) == "amdgpu-gpu-check":
             expect = ["--expect-devices", argv[argv.index("--expect-devices") + 1]] if "--expect-devices" in argv else []
-            argv = [argv[0], "--steps", "hsa,vecadd", "--pod-check", *expect]  # the stand-in reports the check's steps
+            result = ["--result-file", argv[argv.index("--result-file") + 1]] if "--result-file" in argv else []
+            argv = [argv[0], "--steps", "hsa,vecadd", "--pod-check", *expect, *result]  # the stand-in reports the check's steps
             if self.fake_gpu != "procs":
                 return fake_validator_result(argv, env)
             import sys

@@ -819,6 +819,93 @@ def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, k
             w.close()
 
 
+POD_RESULTS = "pod-results"  # validations_dir/<this>: the plugin pods' reports (hostPath in the pods)
+
+
+def _pod_results_dir(env: NodeEnv) -> str:
+    d = os.path.join(env.validations_dir, POD_RESULTS)
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def _with_result_file(env: NodeEnv, pod: dict, flag: str) -> dict:
+    """The pod writes its report into the node's validation directory too
+    (``flag``: the check's option for it, published by rename): the
+    validator has the result as soon as the check is done, while the kernel
+    is still releasing the pod process's GPU state (~50 ms, BASELINE.md
+    pod_exit_probe), which the pod's Succeeded waits for.  The directory is
+    a hostPath on the node, at the same path in the pod as in the validator's
+    container."""
+    d = _pod_results_dir(env)
+    name = pod["metadata"]["name"]
+    ctr = pod["spec"]["containers"][0]
+    ctr["args"] = list(ctr.get("args") or []) + [flag, os.path.join(d, f"{name}.json")]
+    ctr.setdefault("volumeMounts", []).append({"name": "pod-results", "mountPath": d})
+    pod["spec"].setdefault("volumes", []).append({"name": "pod-results",
+                                                   "hostPath": {"path": d, "type": "DirectoryOrCreate"}})
+    return pod
+
+
+def _await_pods(env: NodeEnv, names, run_id: str, deadline: float, stop=None) -> tuple[dict, dict]:
+    """Wait for the pods ``names`` (label ``run_id``): -> (pods by name,
+    {name: report}) once every pod has written an ``ok`` report to its result
+    file, or once every pod has ended (Succeeded / Failed).  A pod that
+    reports a failure, or ends without a result file (not admitted, an image
+    without the option), is judged by its phase as before."""
+    from ..kube.client import wait_for
+    from ..utils.fswait import wait_for_file
+
+    halt = threading.Event()
+    box: dict = {}
+
+    def phases():
+        try:
+            box["live"], box["ended"] = wait_for(
+                env.client, "v1", "Pod", lambda objs: all(
+                    n in objs and ((objs[n].get("status") or {}).get("phase") in ("Succeeded", "Failed"))
+                    for n in names),
+                namespace=env.namespace, label_selector=f"{WORKLOAD_POD_LABEL}={run_id}",
+                timeout=max(0.0, deadline - time.monotonic()), stop=halt, poll_s=env.poll_s)
+        finally:
+            halt.set()
+
+    th = threading.Thread(target=phases, name="validate-pod-phases", daemon=True)
+    th.start()
+    d = _pod_results_dir(env)
+    stopped = (lambda: False) if stop is None else stop.is_set
+    reports: dict = {}
+    for n in names:
+        path = os.path.join(d, f"{n}.json")
+        if not wait_for_file(path, max(0.0, deadline - time.monotonic()), halt, 0.5,
+                             check=lambda p: os.path.exists(p) or stopped()) or stopped():
+            halt.set()  # a stop ends the phase wait too
+            break
+        try:
+            with open(path) as f:
+                reports[n] = json.loads(f.read())
+        except (OSError, ValueError):
+            break
+        if not reports[n].get("ok"):
+            break
+    for n in names:
+        try:
+            os.unlink(os.path.join(d, f"{n}.json"))
+        except OSError:
+            pass
+    if len(reports) == len(names) and all(r.get("ok") for r in reports.values()):
+        halt.set()
+        th.join()
+        live = {}
+        for n in names:  # the allocation the kubelet recorded; the pod may still be exiting
+            try:
+                live[n] = env.client.get("v1", "Pod", n, env.namespace)
+            except Exception:  # noqa: BLE001
+                live[n] = {}
+        return live, reports
+    th.join()
+    return box.get("live") or {}, {}
+
+
 def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | None = None,
                     pod_args: list[str] | None = None, timeout: float = 600.0, stop=None,
                     image: str | None = None, pull_policy: str = "IfNotPresent",
@@ -905,7 +992,7 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
         }
         if pull_secrets:
             pod["spec"]["imagePullSecrets"] = [{"name": x} for x in pull_secrets]
-        return pod
+        return _with_result_file(env, pod, "--result-file" if pod_check == "hsa" else "--ready-file")
 
     def phase(o):
         return (o.get("status") or {}).get("phase", "Pending")
@@ -941,16 +1028,15 @@ def validate_plugin(env: NodeEnv, resource: str = RESOURCE_NAME, expect: int | N
             env.client.create(make_pod(name, run_id, res, count))
             names[name] = (res, count)
         marks.setdefault("pods_created", time.time())
-        live, _ = wait_for(env.client, "v1", "Pod", lambda objs: all(
-            n in objs and phase(objs[n]) in ("Succeeded", "Failed") for n in names), namespace=env.namespace,
-            label_selector=f"{WORKLOAD_POD_LABEL}={run_id}", timeout=max(0.0, deadline - time.monotonic()),
-            stop=stop, poll_s=env.poll_s)
+        live, reports = _await_pods(env, list(names), run_id, deadline, stop)
+        if reports:
+            marks.setdefault("pods_reported", time.time())
         for n in names:
             try:
                 env.client.delete("v1", "Pod", n, env.namespace)
             except Exception:  # noqa: BLE001
                 pass
-        phases = {n: phase(live[n]) if n in live else "Missing" for n in names}
+        phases = {n: "Succeeded" if n in reports else phase(live[n]) if n in live else "Missing" for n in names}
         retry = [n for n in names if phases[n] == "Failed"
                  and (live[n].get("status") or {}).get("reason") == "UnexpectedAdmissionError"]
         hard = {n: p for n, p in phases.items() if p != "Succeeded" and n not in retry}
@@ -1028,16 +1114,17 @@ def validate_dra(env: NodeEnv, timeout: float = 600.0, stop=None, image: str | N
                                     "env": PLUGIN_POD_ENV, "resources": {"claims": [{"name": "gpus"}]}}]}}
     if pull_secrets:
         pod["spec"]["imagePullSecrets"] = [{"name": x} for x in pull_secrets]
+    pod = _with_result_file(env, pod, "--result-file")
     env.client.create(claim)
     try:
         env.client.create(pod)
         marks["pods_created"] = time.time()
-        objs, ok = wait_for(env.client, "v1", "Pod", lambda o: (((o.get(name) or {}).get("status") or {}).get("phase")
-                                                                 in ("Succeeded", "Failed")),
-                            name=name, namespace=env.namespace, timeout=max(0.0, deadline - time.monotonic()),
-                            stop=stop, poll_s=env.poll_s)
+        objs, reports = _await_pods(env, [name], run_id, deadline, stop)
         st = (objs.get(name) or {}).get("status") or {}
-        if not ok or st.get("phase") != "Succeeded":
+        if name in reports:
+            st = {"phase": "Succeeded"}
+            marks["pods_reported"] = time.time()
+        if st.get("phase") != "Succeeded":
             raise StepFailed(f"DRA validation pod {st.get('phase', 'Missing')}: {st.get('message', '')[-300:]}")
         got = env.client.get("resource.k8s.io/v1beta1", "ResourceClaim", name, env.namespace)
         devices = [r["device"] for r in (((got.get("status") or {}).get("allocation") or {}).get("devices") or {})

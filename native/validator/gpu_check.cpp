@@ -249,13 +249,16 @@ int main(int argc, char** argv) {
   double timeout_s = 10.0;
   int elems = 1 << 16;
   int expect = -1;  // --expect-devices: the GPUs the kubelet allocated to this pod
+  std::string result_file;  // --result-file: the report, also written here (validate.py reads it)
   for (int i = 1; i < argc; ++i) {
     std::string k = argv[i];
     if (k == "--timeout" && i + 1 < argc) timeout_s = atof(argv[++i]);
+    else if (k == "--result-file" && i + 1 < argc) result_file = argv[++i];
     else if (k == "--elems" && i + 1 < argc) elems = atoi(argv[++i]);
     else if (k == "--expect-devices" && i + 1 < argc) expect = atoi(argv[++i]);
     else if (k == "--help" || k == "-h") {
-      fprintf(stderr, "usage: amdgpu-gpu-check [--timeout S] [--elems N] [--expect-devices N]   (every visible GPU)\n");
+      fprintf(stderr, "usage: amdgpu-gpu-check [--timeout S] [--elems N] [--expect-devices N] [--result-file PATH]"
+                      "   (every visible GPU)\n");
       return 2;
     }
     // other flags (the validator's pod arguments) are accepted and ignored
@@ -336,6 +339,18 @@ int main(int argc, char** argv) {
   out += "]}";
   puts(out.c_str());
   fflush(stdout);
+  // --result-file: the same report in a file of the node's validation
+  // directory (a hostPath the validator watches), published by rename.  The
+  // pod's exit - the kernel releasing this process's GPU state, ~50 ms
+  // (pod_exit_probe) - is then no longer between the check and
+  // the validator seeing its result; the kubelet still reports the pod's end.
+  if (!result_file.empty()) {
+    const std::string tmp = result_file + ".tmp";
+    if (FILE* rf = fopen(tmp.c_str(), "w")) {
+      const bool wrote = fputs(out.c_str(), rf) >= 0;
+      if (fclose(rf) == 0 && wrote) rename(tmp.c_str(), result_file.c_str());
+    }
+  }
   // the report is the result: the runtime's teardown is left to the exit
   // (AMDGPU_GPU_CHECK_SHUTDOWN=1: hsa_shut_down first - tools/pod_exit_probe.py A/B)
   if (const char* e = getenv("AMDGPU_GPU_CHECK_SHUTDOWN"); e && e[0] == '1') hsa_shut_down();

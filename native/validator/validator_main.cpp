@@ -2049,11 +2049,11 @@ int main(int argc, char** argv) {
   trace("report");
   puts(out.c_str());
   fflush(stdout);
-  if (ok && !a.ready_file.empty()) {
-    FILE* f = fopen(a.ready_file.c_str(), "w");
-    if (f) {
-      fprintf(f, "%s\n", out.c_str());
-      fclose(f);
+  if (ok && !a.ready_file.empty()) {  // published by rename: a reader never sees half a report
+    const std::string tmp = a.ready_file + ".tmp";
+    if (FILE* f = fopen(tmp.c_str(), "w")) {
+      const bool wrote = fprintf(f, "%s\n", out.c_str()) > 0;
+      if (fclose(f) == 0 && wrote) rename(tmp.c_str(), a.ready_file.c_str());
     }
   }
   // Every stream is synchronised, every buffer and communicator released and

@@ -434,3 +434,66 @@ def test_kernel_suffix_is_a_dns_label():
     assert kernel_suffix("6.8.0-45-generic") == "6-8-0-45-generic"
     long = kernel_suffix("5.14.0-427.13.1.el9_4.x86_64+debug.with.a.very.long.local.suffix")
     assert len(long) <= 40 and long.replace("-", "").isalnum() and not long.startswith("-")
+
+
+def test_node_labelled_by_nfd_during_a_pass_gets_its_gpu_labels_in_that_pass():
+    """NFD labels the node while the first pass is still creating objects: the
+    pass puts the GPU-node labels on at its next state (a Node event sets
+    _nodes_changed), instead of leaving them to the next pass."""
+    c = LocalClient(FakeApiServer())
+    c.create(R.new("v1", "Namespace", NS))
+    c.create(R.new("v1", "Node", "gpu-b"))  # not yet labelled by NFD
+    rec = ClusterPolicyReconciler(c, NS)
+    c.create(cluster_policy(spec=spec_from_values(parse_set_flags(REFERENCE_SET_FLAGS))))
+    builders = dict(STATE_BUILDERS)
+
+    def nfd_then_label(spec, ns, owner):
+        objs = builders["state-node-feature-discovery"](spec, ns, owner)
+        c.patch("v1", "Node", "gpu-b", {"metadata": {"labels": GPU_LABEL}})  # the NFD worker, mid-pass
+        rec._nodes_changed = True  # what the operator's Node watch does
+        return objs
+
+    STATE_BUILDERS["state-node-feature-discovery"] = nfd_then_label
+    try:
+        res = rec.reconcile()
+    finally:
+        STATE_BUILDERS.update(builders)
+    assert res.gpu_nodes == 1
+    labels = c.get("v1", "Node", "gpu-b")["metadata"]["labels"]
+    assert labels["amd.com/gpu.present"] == "true" and labels["amd.com/gpu.deploy.driver"] == "true"
+
+
+def test_an_event_that_waited_through_a_long_pass_starts_the_next_at_once():
+    """Debounce: an event right behind a pass waits out the window (echoes of
+    the pass's own writes coalesce); an event that came in during a long pass
+    has waited already and the next pass starts at once."""
+    import queue
+    import threading
+    import time
+
+    rec = ClusterPolicyReconciler(None, NS)
+    events: queue.Queue = queue.Queue()
+    starts, stop = [], threading.Event()
+
+    class Res:
+        state = "notReady"
+
+    def fake_reconcile():
+        starts.append(time.monotonic())
+        if len(starts) == 1:
+            time.sleep(0.3)
+            events.put(("Node", time.monotonic() - 0.25))  # came in 0.25 s ago, mid-pass
+        elif len(starts) == 2:
+            events.put(("DaemonSet", time.monotonic() + 0.0))  # right behind this pass: an echo
+        else:
+            stop.set()
+        return Res()
+
+    rec.reconcile = fake_reconcile
+    events.put(("start", time.monotonic()))
+    t = threading.Thread(target=rec._loop, args=(stop, events, 30.0, 0.2, None))
+    t.start()
+    t.join(5)
+    assert len(starts) == 3
+    assert starts[1] - starts[0] < 0.3 + 0.1  # no debounce wait after the long pass
+    assert starts[2] - starts[1] >= 0.19  # the echo waited out the window

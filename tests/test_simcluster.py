@@ -476,3 +476,28 @@ def test_per_device_plugin_validation_pods(cluster_factory):
     p2 = read_ready(c.nodes["gpu-2"].env, "plugin")
     assert p2["pod_mode"] == "perResource" and p2["pods"] == 1 and "exceed" in p2["pod_mode_fallback"]
     assert p2["devices_validated"] == 16
+
+
+def test_plugin_validation_takes_the_pods_result_file_not_their_exit(tmp_path, monkeypatch):
+    """The plugin-validation pod writes its report to the node's validation
+    directory (hostPath): the validator has it when the check is done, not
+    when the kernel has released the pod process's GPU state (~50 ms on the
+    MI355X; here a stand-in check that takes 1.5 s to exit after its report).
+    A failing check is still judged from its report and the pod's phase."""
+    from amdgpu_operator.validator.validate import POD_RESULTS, read_ready
+
+    monkeypatch.setenv("AMDGPU_FAKE_POD_EXIT_S", "1.5")
+    c = SimCluster(str(tmp_path / "c"), [NodeSpec("gpu-1", 1)], fake_gpu="procs").start()
+    try:
+        c.install_operator(REF)
+        c.wait_ready(60, {"gpu-1": 1})
+        plugin = read_ready(c.nodes["gpu-1"].env, "plugin")
+        marks = plugin["marks"]
+        assert "pods_reported" in marks and marks["pods_reported"] - marks["pods_created"] < 1.5, marks
+        assert plugin["devices_validated"] == 1 and plugin["pods"] == 1
+        pods = [p for p in c.client.list("v1", "Pod") if p["metadata"]["name"].startswith("amd-validator-workload")]
+        assert not pods or all(p["metadata"].get("deletionTimestamp") for p in pods)
+        # the result files are consumed
+        assert os.listdir(os.path.join(c.nodes["gpu-1"].env.validations_dir, POD_RESULTS)) == []
+    finally:
+        c.stop()
