@@ -40,8 +40,10 @@ def visible_count(env: dict) -> int | None:
 
 def wait_start_gate(path: str | None, timeout: float = 120.0, abort_path: str | None = None) -> str:
     """The native validator's ``--start-gate``: block until the file has a
-    verdict; "go" releases the process (same protocol as validator_main.cpp).
-    An abort file in the run's rendezvous directory aborts the wait too."""
+    verdict; "go" releases the process (same protocol as validator_main.cpp,
+    where "init" already lets the runtime start: a stand-in has none, so it
+    waits on for the final verdict).  An abort file in the run's rendezvous
+    directory aborts the wait too."""
     if not path:
         return "go"
     deadline = time.time() + timeout
@@ -49,7 +51,7 @@ def wait_start_gate(path: str | None, timeout: float = 120.0, abort_path: str | 
         try:
             with open(path) as f:
                 text = f.read().strip()
-            if text:
+            if text and text != "init":
                 return text
         except FileNotFoundError:
             pass

@@ -404,8 +404,9 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     needs the peers visible, the runtime need not set up the rest.
 
     ``start_gate``: a file the processes wait on before their first HIP call
-    (``amdgpu-validator --start-gate``): "go" releases them, anything else
-    aborts them.  The caller spawns them before the driver is validated and
+    (``amdgpu-validator --start-gate``): "init" lets the runtime start (the
+    driver container has the module loaded), "go" releases the kernel steps,
+    anything else aborts them.  The caller spawns them before the driver is validated and
     writes the verdict afterwards (:func:`validate_gpu`).
 
     Bounded failure at N >= 2: every rank keeps a liveness record in the
@@ -1184,8 +1185,8 @@ def abort_start_gates(env: NodeEnv) -> list[str]:
         path = os.path.join(env.validations_dir, name)
         try:
             with open(path) as f:
-                if f.read().strip():
-                    continue  # verdict already given
+                if f.read().strip() not in ("", "init"):
+                    continue  # final verdict already given ("init": the runtime may be starting, abort it too)
         except FileNotFoundError:
             continue
         tmp = f"{path}.abort.tmp"
@@ -1232,19 +1233,25 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
         gate = os.path.join(env.validations_dir, f"{START_GATE_PREFIX}{os.urandom(6).hex()}")
         open(gate, "w").close()  # empty = no verdict yet (driver/manager.py may abort it)
 
+    def publish(verdict: str) -> None:
+        tmp = f"{gate}.tmp"
+        with open(tmp, "w") as f:
+            f.write(verdict)
+        os.replace(tmp, gate)
+
     def driver():
         verdict = "abort"
         try:
             wait_ready(env, "driver", timeout, stop)
+            if gate:  # the module is loaded: the runtime may start while the N1 check runs (validator_main.cpp)
+                publish("init")
             results["driver"] = validate_driver(env, timeout, stop)
             verdict = "go"
         except Exception as e:  # noqa: BLE001
             errors.append(f"driver: {e}")
         finally:
-            tmp = f"{gate}.tmp"
-            with open(tmp, "w") as f:
-                f.write(verdict)
-            os.replace(tmp, gate)
+            if gate:
+                publish(verdict)
             driver_done.set()
 
     def workload():

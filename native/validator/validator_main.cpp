@@ -1919,40 +1919,41 @@ int main(int argc, char** argv) {
   // its exec, dynamic linking and library constructors overlap that wait;
   // nothing here has touched the GPU yet (kfd_open_at_gate reports whether
   // the runtime opened /dev/kfd early, which would make the pre-spawn unsafe).
-  double gate_wait_s = -1;
+  // Two verdicts release it: "init" once the driver container has the module
+  // loaded (its ready file) - the HIP runtime may start, ~0.1 s, beside the
+  // validator's own check of the driver - and "go" once that check passed,
+  // which the kernel steps wait for.  Anything else aborts.
+  double gate_wait_s = -1, gate_go_wait_s = -1;
   double stream_create_s = -1;
   bool kfd_early = false;
-  if (!a.start_gate.empty()) {
-    auto tg = Clock::now();
-    kfd_early = fd_open_to("/dev/kfd");
-    std::string verdict;
+  auto wait_gate = [&](bool accept_init) -> std::string {
+    const auto tg = Clock::now();
     for (;;) {
       std::string text;
       if (read_small(a.start_gate, &text)) {
         while (!text.empty() && (text.back() == '\n' || text.back() == ' ')) text.pop_back();
-        if (!text.empty()) {
-          verdict = text;
-          break;
-        }
+        if (!text.empty() && (accept_init || text != "init")) return text;
       }
-      if (std::string why; a.world > 1 && rv.read_text("abort", &why)) {  // a sibling rank failed
-        verdict = "abort";
-        break;
-      }
-      if (secs(tg) > a.timeout_s) {
-        verdict = "timeout";
-        break;
-      }
+      if (std::string why; a.world > 1 && rv.read_text("abort", &why)) return "abort";  // a sibling rank failed
+      if (secs(tg) > a.timeout_s) return "timeout";
       usleep(250);
     }
+  };
+  auto gate_fail = [&](const std::string& verdict) {
+    if (a.world > 1) rv.finish(false, "start gate: " + std::string(verdict == "timeout" ? "timeout" : "aborted"));
+    printf("{\"ok\": false, \"rank\": %d, \"world\": %d, \"device\": %d, \"error\": \"start gate: %s\", "
+           "\"steps\": []}\n", a.rank, a.world, a.device, verdict == "timeout" ? "timeout" : "aborted");
+    fflush(stdout);
+    _exit(3);
+  };
+  bool await_go = false;
+  if (!a.start_gate.empty()) {
+    auto tg = Clock::now();
+    kfd_early = fd_open_to("/dev/kfd");
+    const std::string verdict = wait_gate(true);
     gate_wait_s = secs(tg);
-    if (verdict != "go") {
-      if (a.world > 1) rv.finish(false, "start gate: " + std::string(verdict == "timeout" ? "timeout" : "aborted"));
-      printf("{\"ok\": false, \"rank\": %d, \"world\": %d, \"device\": %d, \"error\": \"start gate: %s\", "
-             "\"steps\": []}\n", a.rank, a.world, a.device, verdict == "timeout" ? "timeout" : "aborted");
-      fflush(stdout);
-      _exit(3);
-    }
+    if (verdict != "go" && verdict != "init") gate_fail(verdict);
+    await_go = verdict == "init";
   }
   int failed_peer = -1;
   std::string peer_state;
@@ -1971,6 +1972,12 @@ int main(int argc, char** argv) {
     const auto ts = Clock::now();
     if (!a.null_stream) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     stream_create_s = secs(ts);
+    if (await_go) {  // the runtime is up; the kernels wait for the driver check
+      const auto tg = Clock::now();
+      const std::string verdict = wait_gate(false);
+      gate_go_wait_s = secs(tg);
+      if (verdict != "go") gate_fail(verdict);
+    }
     if (ok && devs.size() == 1 && !a.all_devices) {
       // one device: the kernel steps in order on the main thread
       if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
@@ -2030,8 +2037,8 @@ int main(int argc, char** argv) {
   }
   if (stream_create_s >= 0) out += fmt("\"stream_create_s\": %.4f, ", stream_create_s);
   if (gate_wait_s >= 0)
-    out += fmt("\"start_gate\": {\"wait_s\": %.4f, \"kfd_open_at_gate\": %s, \"steps_s\": %.4f}, ", gate_wait_s,
-               kfd_early ? "true" : "false", total - gate_wait_s);
+    out += fmt("\"start_gate\": {\"wait_s\": %.4f, \"go_wait_s\": %.4f, \"kfd_open_at_gate\": %s, \"steps_s\": %.4f}, ",
+               gate_wait_s, gate_go_wait_s, kfd_early ? "true" : "false", total - gate_wait_s);
   if (!error.empty()) {
     std::string esc;
     for (char c : error) esc += (c == '"' || c == '\\') ? '\'' : c;

@@ -72,6 +72,48 @@ def test_validator_fp8_floor_fails_the_step(tmp_path):
     assert f["perf_ok"] is False and f["min_tflops"] == 100000 and f["freivalds_rel_err"] < 1e-3
 
 
+def test_start_gate_init_starts_the_runtime_and_go_the_kernels(tmp_path):
+    """Two-phase start gate: "init" (the driver container has the module
+    loaded) lets the HIP runtime start; the kernel steps wait for "go" (the
+    validator's own driver check).  The second wait is reported."""
+    import threading
+    import time
+
+    gate = tmp_path / "gate"
+    gate.write_text("init")
+
+    def release():
+        time.sleep(0.5)
+        (tmp_path / "gate.tmp").write_text("go")
+        (tmp_path / "gate.tmp").replace(gate)
+
+    th = threading.Thread(target=release)
+    th.start()
+    rc, rep = _run(["--rendezvous", str(tmp_path / "rv"), "--steps", "hip,vecadd", "--start-gate", str(gate)])
+    th.join()
+    assert rc == 0 and rep["ok"], rep
+    sg = rep["start_gate"]
+    assert sg["wait_s"] < 0.1 and 0.2 < sg["go_wait_s"] < 1.0, sg  # the runtime started during the 0.5 s
+
+
+def test_start_gate_abort_after_init_exits_before_the_kernels(tmp_path):
+    import threading
+    import time
+
+    gate = tmp_path / "gate"
+    gate.write_text("init")
+
+    def release():
+        time.sleep(0.3)
+        gate.write_text("abort")
+
+    th = threading.Thread(target=release)
+    th.start()
+    rc, rep = _run(["--rendezvous", str(tmp_path / "rv"), "--steps", "hip,vecadd", "--start-gate", str(gate)])
+    th.join()
+    assert rc == 3 and rep["error"] == "start gate: aborted" and rep["steps"] == []
+
+
 def test_validator_counter_gate_tool_library_from_env(tmp_path):
     # the operator's path: the tool library is named explicitly (validate.py)
     from amdgpu_operator.validator.validate import gate_env

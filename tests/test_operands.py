@@ -650,13 +650,16 @@ def test_driver_change_aborts_waiting_start_gates(env):
     os.makedirs(env.validations_dir, exist_ok=True)
     waiting = os.path.join(env.validations_dir, V.START_GATE_PREFIX + "a")
     released = os.path.join(env.validations_dir, V.START_GATE_PREFIX + "b")
+    starting = os.path.join(env.validations_dir, V.START_GATE_PREFIX + "c")  # runtime starting, kernels waiting
     open(waiting, "w").close()
     with open(released, "w") as f:
         f.write("go")
+    with open(starting, "w") as f:
+        f.write("init")
     env.extra["kmod"] = fakesys.SimModule(env.sysfs_root())
     out = DM.prepare_upgrade(env, "9.9.9", drain_timeout=0.1)
     assert out["unloaded"]
-    assert open(waiting).read() == "abort" and open(released).read() == "go"
+    assert open(waiting).read() == "abort" and open(released).read() == "go" and open(starting).read() == "abort"
 
 
 def test_cli_simulate_two_nodes_over_http(capsys):
