@@ -50,6 +50,8 @@ def _lib(name: str = LIB_NAME) -> ctypes.CDLL:
         "avk_gemv_rows": ([P, I, P, P, I, I, S], I),
         "avk_gemm_fp8_nt": ([P, P, P, I, I, I, I, S], I),
         "avk_fill_fp8": ([P, I64, U64, S], I),
+        "avk_gemm_fp4_nt": ([P, P, P, I, I, I, I, S], I),
+        "avk_fill_fp4": ([P, I64, U64, S], I),
         "avk_gemv_rows_fp8": ([P, P, P, I, I, S], I),
         "avk_gemv_cols_fp8": ([P, P, P, I, I, S], I),
         "avk_gemv_cols_bf16": ([P, P, P, I, I, S], I),
@@ -234,6 +236,57 @@ def gemm_fp8_nt(a, bt, out=None, out_dtype=None, stream=None):
     _require(out, out.dtype, "out")
     _check(_lib().avk_gemm_fp8_nt(ab.data_ptr(), bb.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
                                   M, N, K, _stream(stream)), "gemm_fp8_nt")
+    return out
+
+
+FP4_K_MULTIPLE = 256
+FP4_K_MIN = 512
+# e2m1 code -> value (OCP FP4: 1 sign, 2 exponent (bias 1), 1 mantissa bit)
+FP4_VALUES = (0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0, -0.0, -0.5, -1.0, -1.5, -2.0, -3.0, -4.0, -6.0)
+
+
+def fp4_to_float(t):
+    """FP4 pairs (uint8 [..., K/2], element 2k in the low nibble) -> float32 [..., K]."""
+    import torch
+
+    lut = torch.tensor(FP4_VALUES, dtype=torch.float32, device=t.device)
+    b = t.view(torch.uint8).long()
+    return torch.stack((lut[b & 15], lut[b >> 4]), dim=-1).flatten(-2)
+
+
+def fill_fp4_(t, seed: int, stream=None):
+    """Deterministic random FP4 bytes (two e2m1 codes each, all finite) into
+    a uint8 tensor."""
+    import torch
+
+    _require(t, torch.uint8, "t")
+    _check(_lib().avk_fill_fp4(t.data_ptr(), t.numel(), seed & ((1 << 64) - 1), _stream(stream)), "fill_fp4")
+    return t
+
+
+def gemm_fp4_nt(a, bt, out=None, out_dtype=None, stream=None):
+    """K2c: ``out[M,N] = A[M,K] @ Bt[N,K].T`` with OCP FP4 operands (e2m1
+    pairs in uint8 ``[M, K/2]`` / ``[N, K/2]``, element 2k in the low nibble)
+    on ``v_mfma_f32_16x16x128_f8f6f4 cbsz:4 blgp:4``, fp32 accumulation, bf16
+    or fp32 out.  M, N multiples of 256; K a multiple of 256, at least 512."""
+    import torch
+
+    _require(a, torch.uint8, "a")
+    _require(bt, torch.uint8, "bt")
+    if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
+        raise ValueError(f"bad GEMM operands {tuple(a.shape)} x {tuple(bt.shape)}^T")
+    M, K = a.shape[0], 2 * a.shape[1]
+    N = bt.shape[0]
+    if M % GEMM_BM or N % GEMM_BN or K % FP4_K_MULTIPLE or K < FP4_K_MIN:
+        raise ValueError(f"fp4 GEMM shape {M}x{N}x{K} must be multiples of {GEMM_BM}x{GEMM_BN}x{FP4_K_MULTIPLE}, "
+                         f"K >= {FP4_K_MIN}")
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=out_dtype or torch.bfloat16)
+    if out.shape != (M, N) or out.dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("bad GEMM output")
+    _require(out, out.dtype, "out")
+    _check(_lib().avk_gemm_fp4_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
+                                  M, N, K, _stream(stream)), "gemm_fp4_nt")
     return out
 
 

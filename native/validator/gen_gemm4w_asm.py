@@ -774,9 +774,124 @@ def render8() -> str:
             "}\n")
 
 
+# ------------------------------------------------------------ schedule 9 (fp4) --
+# OCP FP4 (e2m1, two per byte, element 2k in the low nibble) on the same
+# instruction with cbsz = blgp = 4: a 16x16x128 step takes 16 B of K per lane
+# (4 VGPRs) at half the cycles of the fp8 one.  Schedule 8's data movement
+# unchanged: a 128-B row is 256 k, so a stage is two k-steps - the two
+# ds_read_b128 of a fragment are its k-step 0 (chunk g, g = lane >> 4) and
+# k-step 1 (chunk g + 4); the kernel's per-lane addresses pick them, under
+# S4_SWZ (conflict free for this pattern, tests/test_gemm4w_asm.py).  Each
+# tile gets two MFMAs per sub-slice: k-step 0 in schedule 8's order, k-step 1
+# S9_LAG tiles later (dependent accumulations never back to back), and every
+# fragment read that overwrites a register moves S9_LAG slots later with its
+# last use; the last S9_LAG k-step-1 MFMAs close the sub-slice.
+S9_SWZ = [((r & 2) << 1) | ((r & 4) >> 1) for r in range(8)]
+S9_LAG = 4
+
+
+def a9(i: int, t: int) -> str:
+    return f"v[{8 * i + 4 * t}:{8 * i + 4 * t + 3}]"
+
+
+def b9(j: int, t: int) -> str:
+    return f"v[{64 + 8 * j + 4 * t}:{64 + 8 * j + 4 * t + 3}]"
+
+
+def s9_reads(pos: int) -> dict[int, list[tuple[str, str]]]:
+    """Schedule 8's reads; those that overwrite a fragment used in this
+    sub-slice (O's next-stage B0-3 and A0-3) S9_LAG slots later."""
+    out = s8_reads(pos)
+    if pos % 2 == 1:
+        out = {m + S9_LAG: rd for m, rd in out.items()}
+    return out
+
+
+def s9_slice(pos: int, first: bool = False, label: str | None = None) -> list[str]:
+    even = pos % 2 == 0
+    rows = range(0, 4) if even else range(4, 8)
+    lslot = (pos + 4) % NSLOT
+    src = S4_SA if even else S4_SB
+    reads = s9_reads(pos)
+    issued: list[str] = []
+    lines = [f"{label}:"] if label else []
+
+    def mfma(m: int, t: int) -> str:
+        j, i = m >> 2, rows[m & 3]
+        c = "0" if first and t == 0 else acc(i, j)
+        return f"v_mfma_f32_16x16x128_f8f6f4 {acc(i, j)}, {b9(j, t)}, {a9(i, t)}, {c} cbsz:4 blgp:4"
+
+    for m in range(32 + S9_LAG):
+        j = m >> 2
+        if m < 32:
+            if even and m % 4 == 0 and j >= 4:
+                last = max(k for k, r in enumerate(issued) if r.startswith(f"v[{64 + 8 * j + 4}:"))
+                lines.append(f"s_waitcnt lgkmcnt({len(issued) - 1 - last})")
+            lines.append(mfma(m, 0))
+        if m >= S9_LAG:
+            lines.append(mfma(m - S9_LAG, 1))
+        for reg, addr in reads.get(m, []):
+            lines.append(f"ds_read_b128 {reg}, {addr}")
+            issued.append(reg)
+        if m in S8_M0_AT:
+            lines.append(s4_m0(lslot, S8_M0_AT[m]))
+        if m in S8_LOAD_AT:
+            lines.append(f"global_load_lds_dwordx4 {S8_VOFF[S8_LOAD_AT[m]]}, {src}")
+        if m == 20:
+            lines += [f"s_sub_u32 {S4_CNT}, {S4_CNT}, 1"]
+        if m == 21:
+            lines += [f"s_cmp_ge_u32 {S4_CNT}, {7 if even else 6}", f"s_cselect_b32 {S4_INC}, 0x80, 0"]
+    lo, hi = (S4_SA_LO, S4_SA_HI) if even else (S4_SB_LO, S4_SB_HI)
+    lines += [f"s_add_u32 {lo}, {lo}, {S4_INC}", f"s_addc_u32 {hi}, {hi}, 0"]
+    if even:
+        lines += ["s_waitcnt vmcnt(8) lgkmcnt(0)", f"s_cmp_eq_u32 {S4_CNT}, 0", "s_cbranch_scc1 3f", "s_barrier"]
+    else:
+        lines += ["s_waitcnt lgkmcnt(0)", f"s_cmp_eq_u32 {S4_CNT}, 0", "s_cbranch_scc1 3f"]
+    return lines
+
+
+def program9() -> list[str]:
+    """program8 with schedule 9's sub-slices (same prologue: the fragment
+    reads of stage 0 are layout-agnostic)."""
+    prog = program8()
+    head = prog[:prog.index("s_waitcnt lgkmcnt(0)") + 2]  # through the prologue's second barrier
+    assert head[-1] == "s_barrier"
+    lines = list(head)
+    lines += s9_slice(0, first=True)
+    lines += s9_slice(1, first=True)
+    lines += ["s_branch 2f"]
+    lines += ["1:"] + s9_slice(0) + s9_slice(1)
+    lines += s9_slice(2, label="2")
+    for pos in range(3, 10):
+        lines += s9_slice(pos)
+    lines += ["s_branch 1b", "3:",
+              "s_waitcnt vmcnt(0)", "s_nop 15", "s_nop 15", f"s_mov_b32 m0, {S4_KEEP}"]
+    return lines
+
+
+def render9() -> str:
+    body = "\\n\\t".join(program9())
+    clob = ", ".join([f'"v{r}"' for r in range(S8_VGPRS)] + [f'"s{r}"' for r in S4_SGPRS]
+                     + [f'"a{r}"' for r in range(256)])
+    return ("// Schedule 9 (OCP fp4 e2m1, v_mfma_f32_16x16x128_f8f6f4 cbsz:4 blgp:4): schedule 8's\n"
+            "// data movement, two k-steps per 128-B row.  Arguments as avk_g8_mainloop, with\n"
+            "// la0/la1, lb0/lb1 the per-lane LDS byte addresses of k-step 0 / 1 of fragment 0,\n"
+            "// slot 0, and ns = K / 256.\n"
+            "__device__ __forceinline__ void avk_g9_mainloop(unsigned a_lo, unsigned a_hi, unsigned b_lo, unsigned b_hi,\n"
+            "                                                unsigned ps, unsigned wave_lds, unsigned ns, unsigned la0,\n"
+            "                                                unsigned la1, unsigned lb0, unsigned lb1, unsigned g_off) {\n"
+            f'  asm volatile("{body}"\n'
+            "               :\n"
+            "               : [a_lo] \"s\"(a_lo), [a_hi] \"s\"(a_hi), [b_lo] \"s\"(b_lo), [b_hi] \"s\"(b_hi), [ps] \"s\"(ps),\n"
+            "                 [wave_lds] \"s\"(wave_lds), [ns] \"s\"(ns), [la0] \"v\"(la0), [la1] \"v\"(la1),\n"
+            "                 [lb0] \"v\"(lb0), [lb1] \"v\"(lb1), [g_off] \"v\"(g_off)\n"
+            f"               : \"memory\", \"scc\", {clob});\n"
+            "}\n")
+
+
 def render_all() -> str:
     return (render() + render2() + render3() + render4() + render4("b", odd_barrier=False)
-            + render4("c", odd_barrier=False, early_b=True) + render8())
+            + render4("c", odd_barrier=False, early_b=True) + render8() + render9())
 
 
 if __name__ == "__main__":

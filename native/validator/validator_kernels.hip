@@ -1439,6 +1439,61 @@ __global__ __launch_bounds__(g4::NTHR, 1) void gemm_fp8_nt_kernel(const uint8_t*
                           std::make_integer_sequence<int, 64>{});
 }
 
+// K2c: C[M][N] = A[M][K] * Bt[N][K]^T with OCP FP4 (e2m1, two per byte, element
+// 2k in the low nibble) operands, fp32 accumulation: the 4-wave tile of the
+// fp8 kernel with schedule 9's main loop (gen_gemm4w_asm.py: the same 128-B
+// LDS rows, here 256 k = two v_mfma_f32_16x16x128_f8f6f4 cbsz:4 blgp:4 steps
+// per row; lane group g reads chunk g for k-step 0 and g + 4 for k-step 1,
+// under the bf16 kernel's swizzle).  K % 256 == 0, K >= 512.
+__device__ __forceinline__ int g9_swz(int r) { return ((r & 2) << 1) | ((r & 4) >> 1); }
+
+template <bool OUT_F32, int EPI = 1>
+__global__ __launch_bounds__(g4::NTHR, 1) void gemm_fp4_nt_kernel(const uint8_t* __restrict__ A,
+                                                                 const uint8_t* __restrict__ Bt,
+                                                                 void* __restrict__ Cv, int M, int N, int K) {
+  using namespace g4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid % kNumXcd;
+  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
+  const int per_group = GROUP_M * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid % per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  const int kb = K / 2;  // bytes per row
+  const uint64_t a0 = reinterpret_cast<uint64_t>(A + (size_t)(m0 + wave * 64) * kb);
+  const uint64_t b0 = reinterpret_cast<uint64_t>(Bt + (size_t)(n0 + wave * 64) * kb);
+  const int pr = lane >> 3;
+  const unsigned g_off = (unsigned)(pr * kb + ((lane & 7) ^ g9_swz(pr)) * 16);
+  const unsigned lds = (unsigned)(uintptr_t)smem;
+  const int fr = lane & 15;
+  const unsigned c0 = (unsigned)(((lane >> 4) ^ g9_swz(fr & 7)) * 16);
+  const unsigned c1 = (unsigned)((((lane >> 4) + 4) ^ g9_swz(fr & 7)) * 16);
+  const unsigned la = lds + (wm * 128 + fr) * 128, lb = lds + (wn * 128 + fr) * 128;
+  avk_g9_mainloop(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
+                  __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
+                  (unsigned)(8 * kb), __builtin_amdgcn_readfirstlane(lds + wave * 8 * 1024), (unsigned)(K / 256),
+                  la + c0, la + c1, lb + c0, lb + c1, g_off);
+
+  if constexpr (!OUT_F32 && EPI >= 1)
+    g4_store_pairs_bf16<EPI == 2>(reinterpret_cast<__bf16*>(Cv), N, m0 + wm * 128 + fr, n0 + wn * 128, lane >> 4,
+                                  std::make_integer_sequence<int, 32>{});
+  else
+    g4_store_all<OUT_F32>(Cv, N, m0 + wm * 128 + fr, n0 + wn * 128 + (lane >> 4) * 4,
+                          std::make_integer_sequence<int, 64>{});
+}
+
 // OCP e4m3 (gfx950's fp8, not MI300's fnuz): 1 sign, 4 exponent (bias 7), 3
 // mantissa bits; exponent 0 is subnormal (m / 8 * 2^-6), S.1111.111 is NaN
 __device__ __forceinline__ float e4m3_to_f32(uint8_t b) {
@@ -1462,6 +1517,17 @@ __global__ __launch_bounds__(256) void fill_fp8_kernel(uint8_t* __restrict__ p, 
     h ^= h >> 29;
     const unsigned mag = (unsigned)((h >> 8) % 72u);  // exponent 0..8 x mantissa 0..7
     p[i] = (uint8_t)(((h & 1u) << 7) | ((mag >> 3) << 3) | (mag & 7u));
+  }
+}
+
+// random FP4 bytes: every e2m1 code is finite (+-{0, 0.5, 1, 1.5, 2, 3, 4, 6})
+__global__ __launch_bounds__(256) void fill_fp4_kernel(uint8_t* __restrict__ p, int64_t n, uint64_t seed) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull ^ seed * 0xD1B54A32D192ED03ull;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+    p[i] = (uint8_t)(h >> 24);
   }
 }
 
@@ -1955,6 +2021,26 @@ AVK_API int avk_fill_fp8(void* p, int64_t n, uint64_t seed, hipStream_t s) {
   if (!p || n < 0) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
   fill_fp8_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>((uint8_t*)p, n, seed);
+  return hipGetLastError();
+}
+
+// FP4 (e2m1 pairs): A [M][K/2], Bt [N][K/2] bytes; M, N % 256, K % 256, K >= 512
+AVK_API int avk_gemm_fp4_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K, hipStream_t s) {
+  if (!A || !Bt || !C || M <= 0 || N <= 0 || K < 512) return hipErrorInvalidValue;
+  if (M % avk::kGemmTile || N % avk::kGemmTile || K % 256) return hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)Bt | (uintptr_t)C) % 16 != 0) return hipErrorInvalidValue;
+  const int nwg = (M / g4::BM) * (N / g4::BN);
+  const uint8_t* a = (const uint8_t*)A;
+  const uint8_t* b = (const uint8_t*)Bt;
+  if (out_f32) gemm_fp4_nt_kernel<true><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+  else gemm_fp4_nt_kernel<false, 1><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+  return hipGetLastError();
+}
+
+AVK_API int avk_fill_fp4(void* p, int64_t nbytes, uint64_t seed, hipStream_t s) {
+  if (!p || nbytes < 0) return hipErrorInvalidValue;
+  if (nbytes == 0) return hipSuccess;
+  fill_fp4_kernel<<<grid_for(nbytes, 256, 8192), 256, 0, s>>>((uint8_t*)p, nbytes, seed);
   return hipGetLastError();
 }
 

@@ -370,3 +370,73 @@ def test_fp8_gemm_rejects_bad_shapes():
         K.gemm_fp8_nt(a, a)
     with pytest.raises(ValueError):
         K.gemm_fp8_nt(torch.zeros(256, 256, device=DEV, dtype=torch.bfloat16), a)
+
+
+# ---------------------------------------------------------- K2c fp4 GEMM ----
+_FP4_SHAPES = [(256, 256, 512), (512, 768, 1024), (1024, 1024, 2048), (768, 512, 768), (256, 512, 4096)]
+
+
+def _fp4_pair(M, N, Kd, seed):
+    a = torch.empty(M, Kd // 2, device=DEV, dtype=torch.uint8)
+    bt = torch.empty(N, Kd // 2, device=DEV, dtype=torch.uint8)
+    K.fill_fp4_(a, seed)
+    K.fill_fp4_(bt, seed + 1)
+    return a, bt
+
+
+def _to_fp4(x):
+    """float values in the e2m1 set -> packed uint8 pairs (element 2k low)."""
+    codes = {v: i for i, v in enumerate(K.FP4_VALUES) if not (v == 0 and i == 8)}
+    flat = x.flatten().tolist()
+    c = torch.tensor([codes[float(v)] for v in flat], dtype=torch.uint8).view(*x.shape[:-1], x.shape[-1] // 2, 2)
+    return (c[..., 0] | (c[..., 1] << 4)).to(DEV)
+
+
+def test_fp4_fill_is_deterministic_and_spans_the_codes():
+    a = torch.empty(1 << 16, device=DEV, dtype=torch.uint8)
+    K.fill_fp4_(a, 3)
+    b = torch.empty_like(a)
+    K.fill_fp4_(b, 3)
+    assert torch.equal(a, b) and K.fp4_to_float(a).unique().numel() == 15  # +0 and -0 compare equal
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", _FP4_SHAPES)
+def test_fp4_gemm_vs_exact_product(shape, out_dtype):
+    """Every e2m1 value and product is exact; the MFMA's own sum is held to
+    the fp8 instruction's measured accuracy (profiles/r5_fp8/diag.json)."""
+    M, N, Kd = shape
+    a, bt = _fp4_pair(M, N, Kd, M + N + Kd)
+    ref = K.fp4_to_float(a).double() @ K.fp4_to_float(bt).double().t()
+    out = K.gemm_fp4_nt(a, bt, out_dtype=out_dtype)
+    scale = ref.abs().max().item()
+    err = (out.double() - ref).abs().max().item()
+    assert err <= (2e-4 if out_dtype == torch.float32 else 8e-3) * scale, (err, scale)
+
+
+def test_fp4_gemm_exact_small_integers_and_identity():
+    """Values in {0, +-1, +-2, +-4} with an asymmetric B: sums are small
+    integers, exact; an identity B returns A.  A swapped k-step, nibble or
+    fragment half changes the result."""
+    M, N, Kd = 512, 256, 1024
+    i = torch.arange(M).view(M, 1)
+    k = torch.arange(Kd).view(1, Kd)
+    vals = torch.tensor([0.0, 1.0, -1.0, 2.0, -2.0, 4.0, -4.0])
+    a = vals[(i * 3 + k * 5) % 7]
+    n = torch.arange(N).view(N, 1)
+    b = vals[(n * 11 + k * 2 + (n > k).long()) % 7]
+    out = K.gemm_fp4_nt(_to_fp4(a), _to_fp4(b), out_dtype=torch.float32)
+    assert torch.equal(out.double().cpu(), a.double() @ b.double().t())
+    eye = torch.zeros(256, Kd)
+    eye[:, :256] = torch.eye(256)
+    out = K.gemm_fp4_nt(_to_fp4(a), _to_fp4(eye), out_dtype=torch.float32)
+    assert torch.equal(out.cpu(), a[:, :256])
+
+
+def test_fp4_gemm_rejects_bad_shapes():
+    a = torch.zeros(256, 128, device=DEV, dtype=torch.uint8)  # K = 256 < 512
+    with pytest.raises(ValueError):
+        K.gemm_fp4_nt(a, a)
+    with pytest.raises(ValueError):
+        K.gemm_fp4_nt(torch.zeros(256, 320, device=DEV, dtype=torch.uint8), torch.zeros(256, 320, device=DEV,
+                                                                                      dtype=torch.uint8))  # K = 640

@@ -91,7 +91,12 @@ def bench_fp8(n, rounds, iters):
     K.fill_fp8_(bt, 12)
     c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
     one = torch.ones((), device="cuda", dtype=torch.float32)
-    arms = {"ours_fp8": lambda: K.gemm_fp8_nt(a, bt, out=c)}
+    a4 = torch.empty(n, n // 2, device="cuda", dtype=torch.uint8)
+    b4 = torch.empty(n, n // 2, device="cuda", dtype=torch.uint8)
+    K.fill_fp4_(a4, 13)
+    K.fill_fp4_(b4, 14)
+    c4 = torch.empty_like(c)
+    arms = {"ours_fp8": lambda: K.gemm_fp8_nt(a, bt, out=c), "ours_fp4": lambda: K.gemm_fp4_nt(a4, b4, out=c4)}
     lib_err = None
     try:
         ref = torch._scaled_mm(a, bt.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
@@ -113,6 +118,7 @@ def bench_fp8(n, rounds, iters):
         out[k + "_tflops"] = fl / statistics.median(v) / 1e9
         out[k + "_tflops_best"] = fl / min(v) / 1e9
     out["ours_fp8_of_dense_peak"] = out["ours_fp8_tflops"] / 5000.0
+    out["ours_fp4_of_dense_peak"] = out["ours_fp4_tflops"] / 10000.0  # FP4/FP6: 2x the fp8 rate on gfx950
     K.gemm_fp8_nt(a, bt, out=c)
     exact = a.float() @ bt.float().t()
     out["ours_fp8_max_rel_err_vs_fp32"] = ((c.float() - exact).abs().max() / exact.abs().max()).item()
