@@ -266,13 +266,16 @@ class WorkloadSpec(_M):
     # launch-bound and report their rate only); 0 = report only.
     minGemmTflops: float = 620.0
     minHbmGbps: float = 3700.0
-    # the mfma-rate check (validator step gemm_fp8, label
-    # amd.com/gpu.validated.mfma-rate): an OCP e4m3 GEMM on the gfx950 f8f6f4
-    # MFMA at fp8GemmN^3, held to minFp8Tflops (whole MI355X; half the rate
-    # measured in profiles/r5_fp8) and counted by the gate (MOPS_F8)
-    fp8RateCheck: bool = True
-    fp8GemmN: int = 4096
+    # the mfma-rate check (validator steps gemm_fp8 and gemm_fp4, label
+    # amd.com/gpu.validated.mfma-rate): OCP e4m3 and FP4 (e2m1) GEMMs on the
+    # gfx950 f8f6f4 MFMA at mfmaRateGemmN^3, held to minFp8Tflops /
+    # minFp4Tflops (whole MI355X; ~45 % of the rates measured in
+    # profiles/r5_ttr/fp8_step and profiles/r5_fp4) and counted by the gate
+    # (SQ_INSTS_VALU_MFMA_MOPS_F8 / _F6F4)
+    mfmaRateCheck: bool = True
+    mfmaRateGemmN: int = 4096
     minFp8Tflops: float = 1200.0
+    minFp4Tflops: float = 1900.0
     # counter-gate floor on MFMA busy cycles per SIMD-cycle of the counted
     # GEMM (native/include/gate_policy.h): ~0.49 measured at 4096^3
     # (profiles/r2_gate/aql_v2.json), floor at 40 % of it

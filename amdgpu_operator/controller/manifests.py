@@ -328,12 +328,13 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     w = v.workload
     wl_args = ["--gemm", str(w.gemmN), "--gemm-iters", str(w.gemmIters), "--hbm-bytes", str(w.hbmBytes),
                "--rccl-elems", str(w.rcclElems), "--xgmi-elems", str(w.xgmiElems)]
-    if w.fp8RateCheck:
-        wl_args += ["--fp8-gemm", str(w.fp8GemmN)]
+    if w.mfmaRateCheck:
+        wl_args += ["--fp8-gemm", str(w.mfmaRateGemmN), "--fp4-gemm", str(w.mfmaRateGemmN)]
     else:
-        wl_args += ["--no-gemm-fp8"]
+        wl_args += ["--no-mfma-rate"]
     for flag, val in (("--min-gemm-tflops", w.minGemmTflops), ("--min-hbm-gbps", w.minHbmGbps),
-                      ("--min-fp8-tflops", w.minFp8Tflops if w.fp8RateCheck else 0),
+                      ("--min-fp8-tflops", w.minFp8Tflops if w.mfmaRateCheck else 0),
+                      ("--min-fp4-tflops", w.minFp4Tflops if w.mfmaRateCheck else 0),
                       ("--min-mfma-util", w.minMfmaUtil), ("--rccl-busbw-link-fraction", w.rcclBusbwLinkFraction),
                       ("--xgmi-read-link-fraction", w.xgmiReadLinkFraction)):
         if val:

@@ -155,7 +155,7 @@ SIM_LINK_GBPS = 45.0
 SIM_LATENCY_US = 12.0
 # GEMM rates of the simulated GPU (TF/s at 4096^3): above the default floors
 # (api/clusterpolicy.py WorkloadSpec), below floors set far above them
-SIM_GEMM_TFLOPS = {"gemm": 1300.0, "gemm_fp8": 2600.0}
+SIM_GEMM_TFLOPS = {"gemm": 1300.0, "gemm_fp8": 2600.0, "gemm_fp4": 4100.0}
 
 
 def sim_busbw(world: int, nbytes: int) -> float:
@@ -170,7 +170,8 @@ def simulated_detail(step: str, argv: list[str], rank: int, world: int) -> dict:
         return argv[argv.index(name) + 1] if name in argv else default
 
     if step in SIM_GEMM_TFLOPS:  # the binary's floors apply from 4096^3 (validator_main.cpp gemm_floor)
-        size_flag, floor_flag = ("--gemm", "--min-gemm-tflops") if step == "gemm" else ("--fp8-gemm", "--min-fp8-tflops")
+        size_flag, floor_flag = {"gemm": ("--gemm", "--min-gemm-tflops"), "gemm_fp8": ("--fp8-gemm", "--min-fp8-tflops"),
+                                 "gemm_fp4": ("--fp4-gemm", "--min-fp4-tflops")}[step]
         n = int(arg(size_flag, "4096"))
         tf = SIM_GEMM_TFLOPS[step]
         floor = float(arg(floor_flag, "0")) if n >= 4096 else 0.0
@@ -280,7 +281,7 @@ def _main(argv: list[str]) -> int:
                               "error": f"{expect} GPU(s) allocated to the pod, {seen} visible"}))
             return 1
     ndev = max(1, int(arg("--expect-devices", "1")))
-    per_device = ("vecadd", "gemm", "gemm_fp8", "mfma", "hbm", "dmabuf")
+    per_device = ("vecadd", "gemm", "gemm_fp8", "gemm_fp4", "mfma", "hbm", "dmabuf")
     recs = []
     for s in steps:
         for d in (range(ndev) if s in per_device and ndev > 1 else [None]):

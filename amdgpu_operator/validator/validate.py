@@ -51,7 +51,8 @@ READY_FILES = {
 VALIDATED_LABEL = "amd.com/gpu.validated"
 MFMA_LABEL = "amd.com/gpu.validated.mfma"  # data types whose MFMA tile checked out on every GPU
 # data types whose GEMM held its TF/s floor (and counter gate) on every GPU:
-# bf16 (the gemm step), fp8 (gemm_fp8, e4m3 on the f8f6f4 MFMA)
+# bf16 (the gemm step), fp8 (gemm_fp8, e4m3) and fp4 (gemm_fp4, e2m1) on the
+# f8f6f4 MFMA
 MFMA_RATE_LABEL = "amd.com/gpu.validated.mfma-rate"
 WORKLOAD_POD_LABEL = "amd.com/validator-workload"
 # take a validator process's result at its report, not at its exit (A/B: =0)
@@ -453,13 +454,13 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     separate = "--rccl-separate-process" in args
     require_links = "--require-xgmi-links" in args
     dmabuf = "--dmabuf" in args  # driver.rdma: HBM exported as a dma-buf on every device
-    if "--no-gemm-fp8" in args:  # validator.workload.fp8RateCheck off
-        args = _drop_step(args, "gemm_fp8")
+    if "--no-mfma-rate" in args:  # validator.workload.mfmaRateCheck off
+        args = _drop_step(_drop_step(args, "gemm_fp8"), "gemm_fp4")
     rccl_frac = float(_arg_value(args, "--rccl-busbw-link-fraction") or 0.0)
     xgmi_frac = float(_arg_value(args, "--xgmi-read-link-fraction") or 0.0)
     link_frac = float(_arg_value(args, "--min-xgmi-link-fraction") or 0.9)
     args = _drop_flag(args, "--rccl-single-gpu", "--rccl-shared-process", "--rccl-separate-process",
-                      "--require-xgmi-links", "--dmabuf", "--no-gemm-fp8")
+                      "--require-xgmi-links", "--dmabuf", "--no-mfma-rate")
     args = _drop_value(args, "--rccl-busbw-link-fraction", "--xgmi-read-link-fraction", "--min-xgmi-link-fraction",
                        "--max-gpu-processes")
     steps = _steps_of(args)
@@ -669,7 +670,7 @@ def failure_summary(reports: list[dict], fabric: dict | None = None, problems: l
     return "; ".join(parts) or "no report"
 
 
-ALL_STEPS = ("hip", "vecadd", "gemm", "gemm_fp8", "mfma", "hbm", "xgmi", "rccl")  # + "dmabuf" with driver.rdma
+ALL_STEPS = ("hip", "vecadd", "gemm", "gemm_fp8", "gemm_fp4", "mfma", "hbm", "xgmi", "rccl")  # + "dmabuf" with driver.rdma
 
 
 def _steps_of(args: list[str]) -> list[str]:
@@ -1332,7 +1333,7 @@ def validated_mfma_dtypes(workload: dict | None) -> list[str]:
     return [d for d in sets[0] if d in common]
 
 
-RATE_STEPS = (("bf16", "gemm"), ("fp8", "gemm_fp8"))
+RATE_STEPS = (("bf16", "gemm"), ("fp8", "gemm_fp8"), ("fp4", "gemm_fp4"))
 
 
 def validated_rate_dtypes(workload: dict | None) -> list[str]:

@@ -8,6 +8,8 @@
 #define AVK_AQL_GATE_COUNTERS 4
 #define AVK_AQL_GATE_BF16 0  // gemm_default.h kGemmSymbol, SQ_INSTS_VALU_MFMA_MOPS_BF16
 #define AVK_AQL_GATE_FP8 1   // gemm_default.h kGemmFp8Symbol, SQ_INSTS_VALU_MFMA_MOPS_F8
+#define AVK_AQL_GATE_FP4 2   // gemm_default.h kGemmFp4Symbol, SQ_INSTS_VALU_MFMA_MOPS_F6F4
+#define AVK_AQL_GATE_DTYPES 3
 
 struct avk_aql_gate_result {
   // SQ_INSTS_VALU_MFMA_MOPS_{BF16|F8}, SQ_VALU_MFMA_BUSY_CYCLES, SQ_WAVES, GRBM_GUI_ACTIVE
@@ -39,8 +41,9 @@ int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, const void* A, 
                       int N, int K, const char* code_object, double timeout_s, avk_aql_gate_result* out, char* err,
                       int errlen);
 
-// The same for the GEMM of `dtype` (AVK_AQL_GATE_BF16 or AVK_AQL_GATE_FP8:
-// gemm_fp8_nt_kernel, A and Bt e4m3 bytes, bf16 out, same grid and kernargs).
+// The same for the GEMM of `dtype` (AVK_AQL_GATE_BF16, _FP8: gemm_fp8_nt_kernel,
+// A and Bt e4m3 bytes, or _FP4: gemm_fp4_nt_kernel, A and Bt e2m1 pairs; bf16
+// out, same grid and kernargs).
 int avk_aql_gate_gemm_dtype(int dtype, const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt,
                             void* C, int M, int N, int K, const char* code_object, double timeout_s,
                             avk_aql_gate_result* out, char* err, int errlen);

@@ -24,4 +24,8 @@ constexpr int kGemmKMultiple = 256;    // K multiple
 // (v_mfma_f32_16x16x128_f8f6f4, 128-deep stages)
 constexpr const char* kGemmFp8Symbol = "gemm_fp8_nt_kernelILb0ELi1EE";
 
+// gemm_fp4_nt_kernel<OUT_F32=false, EPI=1>: the OCP FP4 GEMM of the
+// mfma-rate step (schedule 9: v_mfma_f32_16x16x128_f8f6f4 cbsz:4 blgp:4)
+constexpr const char* kGemmFp4Symbol = "gemm_fp4_nt_kernelILb0ELi1EE";
+
 }  // namespace avk

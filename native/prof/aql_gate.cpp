@@ -52,13 +52,13 @@ double secs(Clock::time_point t0) { return std::chrono::duration<double>(Clock::
 // Per gated GEMM (AVK_AQL_GATE_BF16 / _FP8): the kernel and the MOPS counter
 // of its data type; the other three counters are the same.  Event ids of
 // ROCm 7.2's gfx950 counter definitions (rocprofiler-sdk counter_defs.yaml):
-// SQ_INSTS_VALU_MFMA_MOPS_BF16 52, SQ_INSTS_VALU_MFMA_MOPS_F8 56.
+// SQ_INSTS_VALU_MFMA_MOPS_BF16 52, SQ_INSTS_VALU_MFMA_MOPS_F8 56, _F6F4 57.
 struct GateSpec {
   const char* symbol;
   const char* names[AVK_AQL_GATE_COUNTERS];
   hsa_ven_amd_aqlprofile_event_t events[AVK_AQL_GATE_COUNTERS];
 };
-const GateSpec kSpecs[2] = {
+const GateSpec kSpecs[AVK_AQL_GATE_DTYPES] = {
     {avk::kGemmSymbol,
      {"SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"},
      {{HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 52},
@@ -68,6 +68,12 @@ const GateSpec kSpecs[2] = {
     {avk::kGemmFp8Symbol,
      {"SQ_INSTS_VALU_MFMA_MOPS_F8", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"},
      {{HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 56},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 93},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 4},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, 2}}},
+    {avk::kGemmFp4Symbol,
+     {"SQ_INSTS_VALU_MFMA_MOPS_F6F4", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"},
+     {{HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 57},
       {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 93},
       {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 4},
       {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, 2}}},
@@ -254,11 +260,11 @@ struct Session {
   hsa_amd_memory_pool_t kpool{0};
   hsa_executable_t exe{0};
   hsa_code_object_reader_t reader{0};
-  Kernel kern[2];
+  Kernel kern[AVK_AQL_GATE_DTYPES];
   hsa_queue_t* queue = nullptr;
   hsa_signal_t done{0};
   char* karg = nullptr;
-  hsa_ven_amd_aqlprofile_profile_t prof[2]{};
+  hsa_ven_amd_aqlprofile_profile_t prof[AVK_AQL_GATE_DTYPES]{};
 
   void open(const char* pci_bus_id, int agent_ordinal, const char* code_object) {
     unsigned dom = 0, bus = 0, dev = 0, fn = 0;
@@ -284,7 +290,7 @@ struct Session {
     check(hsa_executable_load_agent_code_object(exe, as.gpu, reader, nullptr, nullptr), "load code object");
     check(hsa_executable_freeze(exe, nullptr), "executable freeze");
     uint32_t karg_size = 0;
-    for (int d = 0; d < 2; ++d) {
+    for (int d = 0; d < AVK_AQL_GATE_DTYPES; ++d) {
       kern[d].symbol = kSpecs[d].symbol;
       check(hsa_executable_iterate_agent_symbols(exe, as.gpu, find_kernel, &kern[d]), "kernel symbols");
       if (!kern[d].object) throw Fail{std::string("GEMM kernel ") + kSpecs[d].symbol + " not in the code object"};
@@ -365,7 +371,8 @@ extern "C" const char* avk_aql_gate_counter_name(int i) {
 }
 
 extern "C" const char* avk_aql_gate_counter_name_dtype(int dtype, int i) {
-  return (dtype >= 0 && dtype < 2 && i >= 0 && i < AVK_AQL_GATE_COUNTERS) ? kSpecs[dtype].names[i] : "";
+  return (dtype >= 0 && dtype < AVK_AQL_GATE_DTYPES && i >= 0 && i < AVK_AQL_GATE_COUNTERS) ? kSpecs[dtype].names[i]
+                                                                                            : "";
 }
 
 extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt, void* C,
@@ -378,7 +385,7 @@ extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, cons
 extern "C" int avk_aql_gate_gemm_dtype(int dtype, const char* pci_bus_id, int agent_ordinal, const void* A,
                                        const void* Bt, void* C, int M, int N, int K, const char* code_object,
                                        double timeout_s, avk_aql_gate_result* out, char* err, int errlen) {
-  const int d = dtype == AVK_AQL_GATE_FP8 ? 1 : 0;
+  const int d = dtype == AVK_AQL_GATE_FP8 ? 1 : dtype == AVK_AQL_GATE_FP4 ? 2 : 0;
   const auto t0 = Clock::now();
   memset(out, 0, sizeof(*out));
   try {

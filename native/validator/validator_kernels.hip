@@ -1549,6 +1549,49 @@ __global__ __launch_bounds__(256) void gemv_cols_fp8_kernel(const uint8_t* __res
   for (int j = 0; j < 8; ++j) atomicAdd(z + c0 + j, s[j]);
 }
 
+// OCP FP4 e2m1: 1 sign, 2 exponent (bias 1), 1 mantissa bit; every code finite
+__device__ __forceinline__ float e2m1_to_f32(unsigned c) {
+  const unsigned e = (c >> 1) & 3u, m = c & 1u;
+  const float v = e ? (float)(2u + m) * (float)(1u << e) * 0.25f : 0.5f * (float)m;
+  return (c & 8u) ? -v : v;
+}
+
+// y[r] = sum_c X[r][c] * v[c], X FP4 pairs [R][C/2] (one wave per row, 16 values per lane step)
+__global__ __launch_bounds__(256) void gemv_rows_fp4_kernel(const uint8_t* __restrict__ X, const float* __restrict__ v,
+                                                            float* __restrict__ y, int R, int C) {
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= R) return;
+  const uint8_t* row = X + (size_t)wave * (C / 2);
+  float s = 0.f;
+  for (int c = lane * 16; c < C; c += 64 * 16) {
+    const uint64_t x = *reinterpret_cast<const uint64_t*>(row + c / 2);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += e2m1_to_f32((unsigned)(x >> (4 * j)) & 15u) * v[c + j];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) y[wave] = s;
+}
+
+// z[c] += sum_{r in slice} X[r][c] * v[r], X FP4 pairs [R][C/2], 16 cols per lane
+__global__ __launch_bounds__(256) void gemv_cols_fp4_kernel(const uint8_t* __restrict__ X, const float* __restrict__ v,
+                                                            float* __restrict__ z, int R, int C, int rows_per_slice) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 16;
+  if (c0 >= C) return;
+  const int r0 = blockIdx.y * rows_per_slice;
+  const int r1 = min(R, r0 + rows_per_slice);
+  float s[16] = {};
+  for (int r = r0; r < r1; ++r) {
+    const uint64_t x = *reinterpret_cast<const uint64_t*>(X + (size_t)r * (C / 2) + c0 / 2);
+    const float vr = v[r];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s[j] += e2m1_to_f32((unsigned)(x >> (4 * j)) & 15u) * vr;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) atomicAdd(z + c0 + j, s[j]);
+}
+
 // ------------------------------------------------- Freivalds check GEMVs ----
 // y[r] = sum_c X[r][c] * v[c]   (X bf16 or f32, row-major, one wave per row)
 template <typename T>
@@ -2041,6 +2084,26 @@ AVK_API int avk_fill_fp4(void* p, int64_t nbytes, uint64_t seed, hipStream_t s) 
   if (!p || nbytes < 0) return hipErrorInvalidValue;
   if (nbytes == 0) return hipSuccess;
   fill_fp4_kernel<<<grid_for(nbytes, 256, 8192), 256, 0, s>>>((uint8_t*)p, nbytes, seed);
+  return hipGetLastError();
+}
+
+// y = X v, X FP4 pairs [R][C/2] (C % 16 == 0)
+AVK_API int avk_gemv_rows_fp4(const void* X, const float* v, float* y, int R, int C, hipStream_t s) {
+  if (!X || !v || !y || R <= 0 || C <= 0 || C % 16 || ((uintptr_t)X % 8)) return hipErrorInvalidValue;
+  gemv_rows_fp4_kernel<<<(R + 3) / 4, 256, 0, s>>>((const uint8_t*)X, v, y, R, C);
+  return hipGetLastError();
+}
+
+// z = X^T v accumulated into z (caller zeroes z); X FP4 pairs [R][C/2], C % 16 == 0
+AVK_API int avk_gemv_cols_fp4(const void* X, const float* v, float* z, int R, int C, hipStream_t s) {
+  if (!X || !v || !z || R <= 0 || C <= 0 || C % 16 || ((uintptr_t)X % 8)) return hipErrorInvalidValue;
+  const int bx = (C / 16 + 255) / 256;
+  int slices = 256 / bx;
+  if (slices < 1) slices = 1;
+  if (slices > R) slices = R;
+  const int rows_per_slice = (R + slices - 1) / slices;
+  dim3 grid(bx, (R + rows_per_slice - 1) / rows_per_slice);
+  gemv_cols_fp4_kernel<<<grid, 256, 0, s>>>((const uint8_t*)X, v, z, R, C, rows_per_slice);
   return hipGetLastError();
 }
 

@@ -252,6 +252,8 @@ struct Args {
   double min_gemm_tflops = 0;      // for a whole MI355X (256 CUs); applied pro rata to a partition
   int fp8_n = 4096;                // the gemm_fp8 step (mfma-rate): e4m3 GEMM size
   double min_fp8_tflops = 0;       // its floor, like min_gemm_tflops
+  int fp4_n = 4096;                // the gemm_fp4 step: e2m1 GEMM size
+  double min_fp4_tflops = 0;
   double min_hbm_gbps = 0;         // idem
   double min_mfma_util = 0;        // counter-gate floor (gate_policy.h), scaled by the launch's occupancy
   double min_rccl_busbw_gbps = 0;  // fp32 all-reduce busBW floor at world > 1
@@ -825,39 +827,58 @@ Step step_gemm(const Args& a, hipStream_t st, int cus) {
   return s;
 }
 
-// gemm_fp8 (label amd.com/gpu.validated.mfma-rate): the matrix cores at the
-// fp8 rate - an OCP e4m3 GEMM on v_mfma_f32_16x16x128_f8f6f4 (2x the bf16
-// FLOP per clock), checked like the gemm step: Freivalds on the fp32-out
-// product (the operands are exact e4m3 values, |x| <= 3.75), the fastest of
-// three trials of bf16-out dispatches against --min-fp8-tflops, and with the
-// counter gate one counted dispatch whose SQ_INSTS_VALU_MFMA_MOPS_F8 must
-// equal 2MNK/512 (aql mode; the sdk tool counts only the bf16 GEMM).
-double fp8_floor(const Args& a, int n, int cus) {
-  return n >= 4096 ? avk::scale_floor_by_cus(a.min_fp8_tflops, cus) : 0.0;
+// gemm_fp8 / gemm_fp4 (label amd.com/gpu.validated.mfma-rate): the matrix
+// cores at the low-precision rates - an OCP e4m3 GEMM on
+// v_mfma_f32_16x16x128_f8f6f4 (2x the bf16 FLOP per clock) and an OCP FP4
+// (e2m1) GEMM on the same instruction with cbsz = blgp = 4 (2x again),
+// checked like the gemm step: Freivalds on the fp32-out product (every
+// operand value is exact), the fastest of three trials of bf16-out
+// dispatches against its floor, and with the counter gate one counted
+// dispatch whose SQ_INSTS_VALU_MFMA_MOPS_F8 / _F6F4 must equal 2MNK/512 (aql
+// mode; the sdk tool counts only the bf16 GEMM).
+struct LowPrecision {
+  const char* step;
+  const char* dtype;
+  int gate_dtype;
+  int64_t (*bytes)(int64_t n_elems);
+  int (*fill)(void*, int64_t, uint64_t, hipStream_t);
+  int (*gemm)(const void*, const void*, void*, int, int, int, int, hipStream_t);
+  int (*gemv_rows)(const void*, const float*, float*, int, int, hipStream_t);
+  int (*gemv_cols)(const void*, const float*, float*, int, int, hipStream_t);
+};
+const LowPrecision kFp8{"gemm_fp8", "e4m3", AVK_AQL_GATE_FP8, [](int64_t n) { return n; }, avk_fill_fp8,
+                        avk_gemm_fp8_nt, avk_gemv_rows_fp8, avk_gemv_cols_fp8};
+const LowPrecision kFp4{"gemm_fp4", "e2m1", AVK_AQL_GATE_FP4, [](int64_t n) { return n / 2; }, avk_fill_fp4,
+                        avk_gemm_fp4_nt, avk_gemv_rows_fp4, avk_gemv_cols_fp4};
+
+double lowp_floor(double floor_full_gpu, int n, int cus) {
+  return n >= 4096 ? avk::scale_floor_by_cus(floor_full_gpu, cus) : 0.0;
 }
 
-Step step_gemm_fp8(const Args& a, hipStream_t st, int cus) {
+Step step_gemm_lowp(const Args& a, hipStream_t st, int cus, const LowPrecision& lp) {
   auto t0 = Clock::now();
-  Step s{"gemm_fp8"};
-  const int n = a.fp8_n;
+  Step s{lp.step};
+  const bool fp4 = lp.gate_dtype == AVK_AQL_GATE_FP4;
+  const int n = fp4 ? a.fp4_n : a.fp8_n;
+  const int64_t nb = lp.bytes((int64_t)n * n);
   void *A, *B, *C16;
   float *C32, *x, *y1, *z, *y2;
-  HIP_OK(hipMalloc(&A, (size_t)n * n));
-  HIP_OK(hipMalloc(&B, (size_t)n * n));
+  HIP_OK(hipMalloc(&A, nb));
+  HIP_OK(hipMalloc(&B, nb));
   HIP_OK(hipMalloc(&C16, (size_t)n * n * 2));
   HIP_OK(hipMalloc(&C32, (size_t)n * n * 4));
   HIP_OK(hipMalloc(&x, n * 4));
   HIP_OK(hipMalloc(&y1, n * 4));
   HIP_OK(hipMalloc(&y2, n * 4));
   HIP_OK(hipMalloc(&z, n * 4));
-  AVK_OK(avk_fill_fp8(A, (int64_t)n * n, 41, st));
-  AVK_OK(avk_fill_fp8(B, (int64_t)n * n, 42, st));
-  AVK_OK(avk_fill_uniform_f32(x, n, 43, -1, 1, st));
-  AVK_OK(avk_gemm_fp8_nt(A, B, C32, 1, n, n, n, st));
+  AVK_OK(lp.fill(A, nb, fp4 ? 51 : 41, st));
+  AVK_OK(lp.fill(B, nb, fp4 ? 52 : 42, st));
+  AVK_OK(avk_fill_uniform_f32(x, n, fp4 ? 53 : 43, -1, 1, st));
+  AVK_OK(lp.gemm(A, B, C32, 1, n, n, n, st));
   AVK_OK(avk_gemv_rows(C32, 0, x, y1, n, n, st));
   HIP_OK(hipMemsetAsync(z, 0, n * 4, st));
-  AVK_OK(avk_gemv_cols_fp8(B, x, z, n, n, st));
-  AVK_OK(avk_gemv_rows_fp8(A, z, y2, n, n, st));
+  AVK_OK(lp.gemv_cols(B, x, z, n, n, st));
+  AVK_OK(lp.gemv_rows(A, z, y2, n, n, st));
   std::vector<float> h1(n), h2(n);
   HIP_OK(hipMemcpyAsync(h1.data(), y1, n * 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(h2.data(), y2, n * 4, hipMemcpyDeviceToHost, st));
@@ -872,11 +893,11 @@ Step step_gemm_fp8(const Args& a, hipStream_t st, int cus) {
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
-  AVK_OK(avk_gemm_fp8_nt(A, B, C16, 0, n, n, n, st));  // warm
+  AVK_OK(lp.gemm(A, B, C16, 0, n, n, n, st));  // warm
   float best_ms = 0;
   for (int t = 0; t < 3; ++t) {
     HIP_OK(hipEventRecord(e0, st));
-    for (int i = 0; i < a.gemm_iters; ++i) AVK_OK(avk_gemm_fp8_nt(A, B, C16, 0, n, n, n, st));
+    for (int i = 0; i < a.gemm_iters; ++i) AVK_OK(lp.gemm(A, B, C16, 0, n, n, n, st));
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipEventSynchronize(e1));
     float tm = 0;
@@ -885,21 +906,25 @@ Step step_gemm_fp8(const Args& a, hipStream_t st, int cus) {
   }
   std::string gate_json = "\"counter_gate\": \"off\"";
   bool gate_ok = true;
-  if (a.counter_gate && a.gate_mode == "aql") gate_ok = aql_gate(a, A, B, C16, n, cus, st, &gate_json, AVK_AQL_GATE_FP8);
+  if (a.counter_gate && a.gate_mode == "aql") gate_ok = aql_gate(a, A, B, C16, n, cus, st, &gate_json, lp.gate_dtype);
   const float ms = best_ms / a.gemm_iters;
   const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) (void)hipFree(p);
-  const double floor = fp8_floor(a, n, cus);
+  const double floor = lowp_floor(fp4 ? a.min_fp4_tflops : a.min_fp8_tflops, n, cus);
   const bool perf_ok = floor <= 0 || tflops >= floor;
   s.ok = numerics_ok && gate_ok && perf_ok;
   s.seconds = secs(t0);
-  s.detail = fmt("\"n\": %d, \"dtype\": \"e4m3\", \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, "
-                 "\"min_tflops\": %.1f, \"perf_ok\": %s, ", n, rel, ms, tflops, floor, perf_ok ? "true" : "false") +
+  s.detail = fmt("\"n\": %d, \"dtype\": \"%s\", \"freivalds_rel_err\": %.3e, \"ms\": %.4f, \"tflops\": %.1f, "
+                 "\"min_tflops\": %.1f, \"perf_ok\": %s, ", n, lp.dtype, rel, ms, tflops, floor,
+                 perf_ok ? "true" : "false") +
              gate_json;
   return s;
 }
+
+Step step_gemm_fp8(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kFp8); }
+Step step_gemm_fp4(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kFp4); }
 
 Step step_hbm(const Args& a, hipStream_t st, int cus) {
   auto t0 = Clock::now();
@@ -1696,11 +1721,13 @@ std::vector<Step> device_steps(Args ad, bool gate_last, bool with_hip) {
   run("vecadd", [&] { return step_vecadd(ad, sd); });
   if (!gate_last) run("gemm", [&] { return step_gemm(ad, sd, cus); });
   if (!gate_last) run("gemm_fp8", [&] { return step_gemm_fp8(ad, sd, cus); });
+  if (!gate_last) run("gemm_fp4", [&] { return step_gemm_fp4(ad, sd, cus); });
   run("mfma", [&] { return step_mfma(sd); });
   run("hbm", [&] { return step_hbm(ad, sd, cus); });
   run("dmabuf", [&] { return step_dmabuf(sd); });
   if (gate_last) run("gemm", [&] { return step_gemm(ad, sd, cus); });
   if (gate_last) run("gemm_fp8", [&] { return step_gemm_fp8(ad, sd, cus); });
+  if (gate_last) run("gemm_fp4", [&] { return step_gemm_fp4(ad, sd, cus); });
   if (sd) (void)hipStreamDestroy(sd);
   return out;
 }
@@ -1789,7 +1816,7 @@ void usage(const char* p) {
   fprintf(stderr,
           "usage: %s [--device N | --local-bdf BDF | --all-devices] [--expect-devices N]\n"
           "          [--rank R --world W --rendezvous DIR --run-id ID] [--steps a,b,...]\n"
-          "          [--gemm N] [--gemm-iters K] [--fp8-gemm N] [--min-fp8-tflops X] [--hbm-bytes B] [--vecadd-elems N] [--rccl-elems E] [--xgmi-elems E]\n"
+          "          [--gemm N] [--gemm-iters K] [--fp8-gemm N] [--min-fp8-tflops X] [--fp4-gemm N] [--min-fp4-tflops X] [--hbm-bytes B] [--vecadd-elems N] [--rccl-elems E] [--xgmi-elems E]\n"
           "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--rccl-destroy]\n"
           "          [--ready-file PATH] [--start-gate FILE] [--gate-mode aql|sdk] [--min-mfma-util U]\n"
           "          [--min-rccl-busbw-gbps X] [--min-xgmi-read-gbps X] [--peer-timeout S] [--collective-timeout S]\n"
@@ -1836,6 +1863,8 @@ int main(int argc, char** argv) {
     else if (k == "--min-hbm-gbps") a.min_hbm_gbps = atof(v());
     else if (k == "--fp8-gemm") a.fp8_n = atoi(v());
     else if (k == "--min-fp8-tflops") a.min_fp8_tflops = atof(v());
+    else if (k == "--fp4-gemm") a.fp4_n = atoi(v());
+    else if (k == "--min-fp4-tflops") a.min_fp4_tflops = atof(v());
     else if (k == "--min-mfma-util") a.min_mfma_util = atof(v());
     else if (k == "--min-rccl-busbw-gbps") a.min_rccl_busbw_gbps = atof(v());
     else if (k == "--min-xgmi-read-gbps") a.min_xgmi_read_gbps = atof(v());
@@ -1861,7 +1890,7 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
-  if (a.world < 1 || a.rank < 0 || a.rank >= a.world || a.gemm_n <= 0 || a.gemm_n % 256 || a.fp8_n <= 0 || a.fp8_n % 256 || a.hbm_bytes <= 0 ||
+  if (a.world < 1 || a.rank < 0 || a.rank >= a.world || a.gemm_n <= 0 || a.gemm_n % 256 || a.fp8_n <= 0 || a.fp8_n % 256 || a.fp4_n < 512 || a.fp4_n % 256 || a.hbm_bytes <= 0 ||
       a.hbm_bytes % 16 || a.rccl_elems <= 0 || a.xgmi_elems <= 0 || a.xgmi_elems % 4 || a.emulated_peers < 1 ||
       a.emulated_peers > 8 || a.world > 64 || (a.world > 8 && has_step(a, "xgmi")) || a.sweep_min_bytes < 4 ||
       a.sweep_max_bytes < a.sweep_min_bytes || a.sweep_max_bytes > (16ll << 30) || a.sweep_factor < 2 ||
@@ -1984,6 +2013,8 @@ int main(int argc, char** argv) {
       if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "gemm_fp8"))
         ok = (steps.push_back(step_gemm_fp8(a, st, prop.multiProcessorCount)), steps.back().ok);
+      if (ok && has_step(a, "gemm_fp4"))
+        ok = (steps.push_back(step_gemm_fp4(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
       if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "dmabuf")) ok = (steps.push_back(step_dmabuf(st)), steps.back().ok);

@@ -51,8 +51,8 @@ def test_validator_fp8_rate_step_with_counter_gate(tmp_path):
     its floor, and counted: SQ_INSTS_VALU_MFMA_MOPS_F8 == 2N^3/512 with the
     default kernel's waves.  Its gate reuses the bf16 gate's HSA session
     (setup ~0 the second time)."""
-    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm,gemm_fp8", "--counter-gate",
-                    "--min-fp8-tflops", "1200", "--min-gemm-tflops", "620"])
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm,gemm_fp8,gemm_fp4", "--counter-gate",
+                    "--min-fp8-tflops", "1200", "--min-gemm-tflops", "620", "--min-fp4-tflops", "1900"])
     assert rc == 0 and rep["ok"], rep
     steps = {s["name"]: s for s in rep["steps"]}
     f = steps["gemm_fp8"]
@@ -63,6 +63,11 @@ def test_validator_fp8_rate_step_with_counter_gate(tmp_path):
     assert f["perf_ok"] and f["tflops"] >= 1200 and f["min_tflops"] == 1200
     assert f["tflops"] > 1.3 * steps["gemm"]["tflops"]  # 2x the FLOP per clock of the bf16 MFMA
     assert f["gate_setup_seconds"] < 0.002 < steps["gemm"]["gate_setup_seconds"]
+    # FP4 (e2m1) on the same instruction, cbsz = blgp = 4: SQ_INSTS_VALU_MFMA_MOPS_F6F4
+    q = steps["gemm_fp4"]
+    assert q["dtype"] == "e2m1" and q["freivalds_rel_err"] < 1e-3 and q["counter_gate"] == "pass", q
+    assert q["SQ_INSTS_VALU_MFMA_MOPS_F6F4"] * 512 == 2 * 4096 ** 3 and q["SQ_WAVES"] == (4096 // 256) ** 2 * _WPT
+    assert q["perf_ok"] and q["tflops"] > 1.3 * f["tflops"] and q["gate_setup_seconds"] < 0.002
 
 
 def test_validator_fp8_floor_fails_the_step(tmp_path):

@@ -326,7 +326,7 @@ def test_workload_validation_launch_plan(env):
     # one process per GPU: its kernel checks, the xGMI IPC step and RCCL
     assert len(launched) == 2
     for argv, e, device in launched:
-        assert argv[argv.index("--steps") + 1] == "hip,vecadd,gemm,gemm_fp8,mfma,hbm,xgmi,rccl"
+        assert argv[argv.index("--steps") + 1] == "hip,vecadd,gemm,gemm_fp8,gemm_fp4,mfma,hbm,xgmi,rccl"
         assert argv[argv.index("--local-bdf") + 1] == gpus[device].bdf and "--counter-gate" in argv
         # it sees its own GPU first, then its peer (RCCL and IPC need the peer visible)
         assert e["ROCR_VISIBLE_DEVICES"].split(",")[0] == f"GPU-{gpus[device].unique_id:016x}"
@@ -336,7 +336,7 @@ def test_workload_validation_launch_plan(env):
         assert e.get("AMDGPU_VALIDATOR_COUNTERS") is None
     assert sorted(d for _, _, d in launched) == [0, 1]
     names = [s["name"] for s in out["ranks"][0]["steps"]]
-    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "mfma", "hbm", "xgmi", "rccl"]
+    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "gemm_fp4", "mfma", "hbm", "xgmi", "rccl"]
     assert V.read_ready(env, "workload")["world"] == 2
 
     def reset():
@@ -361,7 +361,7 @@ def test_workload_validation_launch_plan(env):
     assert all(len(e["ROCR_VISIBLE_DEVICES"].split(",")) == 2 for _, e in rccl)
     assert all("--counter-gate" in a for a, _ in kernel) and not any("--counter-gate" in a for a, _ in rccl)
     names = [s["name"] for s in out["ranks"][0]["steps"]]
-    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "mfma", "hbm", "xgmi", "rccl"]
+    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "gemm_fp4", "mfma", "hbm", "xgmi", "rccl"]
 
 
 def test_workload_failure_is_reported(env):
@@ -383,7 +383,7 @@ def test_single_gpu_skips_rccl(tmp_path):
 
     env.launcher = launcher
     out = V.validate_workload(env, [])
-    assert seen == ["hip,vecadd,gemm,gemm_fp8,mfma,hbm,xgmi"]
+    assert seen == ["hip,vecadd,gemm,gemm_fp8,gemm_fp4,mfma,hbm,xgmi"]
     assert out["ranks"][0]["steps"][-1]["skipped"].startswith("single GPU")
 
 
@@ -419,22 +419,24 @@ def test_complete_publishes_the_validated_mfma_rates(env):
 
     bf16 = {"name": "gemm", "ok": True, "tflops": 1450.0, "min_tflops": 620.0}
     fp8 = {"name": "gemm_fp8", "ok": True, "tflops": 2900.0, "min_tflops": 1200.0}
-    V.write_ready(env, "workload", {"ranks": [rank(bf16, fp8), rank(bf16, {**fp8, "device": 1})]})
-    assert V.complete(env)["mfma_rate_dtypes"] == ["bf16", "fp8"]
-    assert env.client.get("v1", "Node", "n1")["metadata"]["labels"][V.MFMA_RATE_LABEL] == "bf16.fp8"
+    fp4 = {"name": "gemm_fp4", "ok": True, "tflops": 4200.0, "min_tflops": 1900.0}
+    V.write_ready(env, "workload", {"ranks": [rank(bf16, fp8, fp4), rank(bf16, {**fp8, "device": 1}, fp4)]})
+    assert V.complete(env)["mfma_rate_dtypes"] == ["bf16", "fp8", "fp4"]
+    assert env.client.get("v1", "Node", "n1")["metadata"]["labels"][V.MFMA_RATE_LABEL] == "bf16.fp8.fp4"
     V.write_ready(env, "workload", {"ranks": [rank(bf16, fp8), rank(bf16, {**fp8, "min_tflops": 0.0})]})
     assert V.complete(env)["mfma_rate_dtypes"] == ["bf16"]
-    V.write_ready(env, "workload", {"ranks": [rank({**bf16, "ok": False}, fp8)]})
+    V.write_ready(env, "workload", {"ranks": [rank({**bf16, "ok": False}, fp8, {**fp4, "ok": False})]})
     assert V.complete(env)["mfma_rate_dtypes"] == ["fp8"]
     V.write_ready(env, "workload", {"ranks": [rank({**bf16, "min_tflops": 0.0})]})
     assert V.complete(env)["mfma_rate_dtypes"] == []
     assert V.MFMA_RATE_LABEL not in env.client.get("v1", "Node", "n1")["metadata"]["labels"]
 
 
-def test_fp8_rate_check_flags_reach_the_validator(tmp_path):
-    """validator.workload.fp8RateCheck / fp8GemmN / minFp8Tflops become the
-    binary's --fp8-gemm / --min-fp8-tflops; switched off, the gemm_fp8 step
-    is dropped from the run (and its floor is not passed)."""
+def test_mfma_rate_check_flags_reach_the_validator(tmp_path):
+    """validator.workload.mfmaRateCheck / mfmaRateGemmN / minFp8Tflops /
+    minFp4Tflops become the binary's --fp8-gemm / --fp4-gemm / --min-fp8-tflops /
+    --min-fp4-tflops; switched off, the gemm_fp8 and gemm_fp4 steps are
+    dropped from the run (and their floors are not passed)."""
     from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, ClusterPolicySpec, deep_merge, parse_set_flags
     from amdgpu_operator.controller import manifests as M
 
@@ -446,9 +448,10 @@ def test_fp8_rate_check_flags_reach_the_validator(tmp_path):
         return ds["spec"]["template"]["spec"]["containers"][0]["args"]
 
     on = args(ref)
-    assert on[on.index("--fp8-gemm") + 1] == "4096" and on[on.index("--min-fp8-tflops") + 1] == "1200"
-    off = args(deep_merge(ref, {"validator": {"workload": {"fp8RateCheck": False}}}))
-    assert "--no-gemm-fp8" in off and "--min-fp8-tflops" not in off and "--fp8-gemm" not in off
+    assert on[on.index("--fp8-gemm") + 1] == on[on.index("--fp4-gemm") + 1] == "4096"
+    assert on[on.index("--min-fp8-tflops") + 1] == "1200" and on[on.index("--min-fp4-tflops") + 1] == "1900"
+    off = args(deep_merge(ref, {"validator": {"workload": {"mfmaRateCheck": False}}}))
+    assert "--no-mfma-rate" in off and not {"--min-fp8-tflops", "--min-fp4-tflops", "--fp8-gemm"} & set(off)
 
     root = str(tmp_path / "h1")
     fakesys.build_node(root, 1)
@@ -460,9 +463,9 @@ def test_fp8_rate_check_flags_reach_the_validator(tmp_path):
         return ProcResult(0, json.dumps({"ok": True, "steps": []}), "", 0.0)
 
     venv.launcher = launcher
-    V.validate_workload(venv, ["--no-gemm-fp8", "--fp8-gemm", "8192"])
+    V.validate_workload(venv, ["--no-mfma-rate", "--fp8-gemm", "8192"])
     assert seen[0][seen[0].index("--steps") + 1] == "hip,vecadd,gemm,mfma,hbm,xgmi"
-    assert "--no-gemm-fp8" not in seen[0]
+    assert "--no-mfma-rate" not in seen[0]
 
 
 # ------------------------------------------------------------------ CLI
