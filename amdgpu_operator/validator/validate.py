@@ -895,8 +895,10 @@ def _await_pods(env: NodeEnv, names, run_id: str, deadline: float, stop=None) ->
         except OSError:
             pass
     if len(reports) == len(names) and all(r.get("ok") for r in reports.values()):
+        # the phase wait notices ``halt`` at its next watch event (the pods'
+        # deletion below at the latest): not joined, it would hold the result
+        # until the pod processes have exited after all
         halt.set()
-        th.join()
         live = {}
         for n in names:  # the allocation the kubelet recorded; the pod may still be exiting
             try:

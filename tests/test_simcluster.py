@@ -487,7 +487,9 @@ def test_plugin_validation_takes_the_pods_result_file_not_their_exit(tmp_path, m
     from amdgpu_operator.validator.validate import POD_RESULTS, read_ready
 
     monkeypatch.setenv("AMDGPU_FAKE_POD_EXIT_S", "1.5")
-    c = SimCluster(str(tmp_path / "c"), [NodeSpec("gpu-1", 1)], fake_gpu="procs").start()
+    # operands as processes over HTTP, as in the bench: the validator's pod
+    # watch blocks in a socket read between events
+    c = SimCluster(str(tmp_path / "c"), [NodeSpec("gpu-1", 1)], fake_gpu="procs", process_containers=True).start()
     try:
         c.install_operator(REF)
         c.wait_ready(60, {"gpu-1": 1})
