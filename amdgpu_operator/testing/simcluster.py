@@ -703,9 +703,46 @@ class SimCluster:
                     if etype != "DELETED" and not pod["spec"].get("nodeName") \
                             and not pod["metadata"].get("deletionTimestamp"):
                         self._schedule(pod)
+                    elif etype == "DELETED" or (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+                        # devices a pod held are free again: the pods waiting for them get another try
+                        for waiting in self.client.list("v1", "Pod"):
+                            if not waiting["spec"].get("nodeName") and not waiting["metadata"].get("deletionTimestamp") \
+                                    and self._gpu_requests(waiting):
+                                self._schedule(waiting)
             except Exception as e:  # noqa: BLE001
                 log.debug("scheduler watch: %s", e)
                 self.stop_event.wait(0.1)
+
+    @staticmethod
+    def _gpu_requests(pod: dict) -> dict[str, int]:
+        """Extended-resource requests of the device plugin's resources (limits
+        stand for requests, as for extended resources)."""
+        out: dict[str, int] = {}
+        for c in pod["spec"].get("containers") or []:
+            for k, v in ((c.get("resources") or {}).get("limits") or {}).items():
+                if k.startswith(RESOURCE_NAME):
+                    out[k] = out.get(k, 0) + int(v)
+        return out
+
+    def _gpu_fits(self, pod: dict, node: str) -> str | None:
+        """kube-scheduler's resource fit for the device plugin's resources: the
+        requests of every pod bound to the node that has not finished -
+        terminating ones included, until they are gone - plus this one's, within
+        what the node's kubelet advertises.  None if it fits, else why not."""
+        want = self._gpu_requests(pod)
+        if not want:
+            return None
+        used: dict[str, int] = {}
+        for p in self.client.list("v1", "Pod"):
+            if p["spec"].get("nodeName") == node and (p.get("status") or {}).get("phase") not in ("Succeeded",
+                                                                                                    "Failed"):
+                for k, v in self._gpu_requests(p).items():
+                    used[k] = used.get(k, 0) + v
+        kubelet = self.nodes[node].kubelet
+        for k, v in want.items():
+            if used.get(k, 0) + v > kubelet.capacity(k):
+                return f"Insufficient {k} on {node} ({used.get(k, 0)} in use of {kubelet.capacity(k)})"
+        return None
 
     def _schedule(self, pod: dict) -> None:
         from . import fakedra
@@ -730,6 +767,10 @@ class SimCluster:
             cands = [n for n in cands if not pinned or n in pinned]
             if not cands:
                 raise ValueError(f"no node matches (selector {want}, claims allocated on {sorted(pinned)})")
+            unfit = {n: self._gpu_fits(pod, n) for n in cands}
+            cands = [n for n in cands if unfit[n] is None]
+            if not cands:
+                raise ValueError("; ".join(v for v in unfit.values() if v))
             err: Exception | None = None
             for node in cands:
                 try:

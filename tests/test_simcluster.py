@@ -501,5 +501,9 @@ def test_plugin_validation_takes_the_pods_result_file_not_their_exit(tmp_path, m
         assert not pods or all(p["metadata"].get("deletionTimestamp") for p in pods)
         # the result files are consumed
         assert os.listdir(os.path.join(c.nodes["gpu-1"].env.validations_dir, POD_RESULTS)) == []
+        # a pod asking for the GPU right after Ready waits in the scheduler while the
+        # validation pod is still exiting (its GPU counts until it is gone), then runs
+        rep = verify(c.client, c.namespace, run_pods=True, pod_timeout=30)
+        assert rep.ok, rep.table()
     finally:
         c.stop()
