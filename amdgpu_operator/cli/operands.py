@@ -343,6 +343,8 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
     if cmd == "validate":
         from ..validator import validate as V
 
+        V._startup_mark("validate_imported")
+
         if cenv.get("VALIDATOR_IMAGE"):
             env.extra["validator_image"] = {
                 "image": cenv["VALIDATOR_IMAGE"], "pull_policy": cenv.get("VALIDATOR_IMAGE_PULL_POLICY"),

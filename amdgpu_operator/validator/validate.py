@@ -507,6 +507,7 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
         if REPORT_EARLY:
             jenv = {**jenv, REPORT_EARLY_ENV: "1"}
         argv = workload_argv(jargs, rank, world, rdv, rid, 0)
+        _startup_mark(f"spawn{rank}")
         if start_gate:
             argv += ["--start-gate", start_gate]
         if linger_until and LINGER:
@@ -819,6 +820,16 @@ def _wait_kubelet_devices(env: NodeEnv, expected: dict, deadline: float, stop, k
         kd.close()
         if w is not None:
             w.close()
+
+
+def _startup_mark(what: str) -> None:
+    """AMDGPU_STARTUP_TRACE (the simulated kubelet's operand processes): the
+    wall time of a point on the validator's path, next to cli/main.py's
+    start-up phases (bench.py operand_breakdown)."""
+    trace = os.environ.get("AMDGPU_STARTUP_TRACE")
+    if trace:
+        with open(trace, "a") as f:
+            f.write(f"{what} {time.time():.4f}\n")
 
 
 POD_RESULTS = "pod-results"  # validations_dir/<this>: the plugin pods' reports (hostPath in the pods)
@@ -1242,12 +1253,15 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
             f.write(verdict)
         os.replace(tmp, gate)
 
+    _startup_mark("validate_gpu")
+
     def driver():
         verdict = "abort"
         try:
             wait_ready(env, "driver", timeout, stop)
             if gate:  # the module is loaded: the runtime may start while the N1 check runs (validator_main.cpp)
                 publish("init")
+                _startup_mark("gate_init")
             results["driver"] = validate_driver(env, timeout, stop)
             verdict = "go"
         except Exception as e:  # noqa: BLE001
