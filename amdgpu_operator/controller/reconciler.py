@@ -56,6 +56,16 @@ class StateResult:
     detail: str = ""
 
 
+# The order a pass applies the states in.  Reported in STATES order; applied
+# with the validator right after the driver: on a first pass the operands'
+# objects are created one HTTP request at a time (~30 ms on the MI355X box),
+# and the validator's pod starts the longest chain of the bring-up (its
+# Python start-up, then the HIP runtime behind the start gate), so its
+# DaemonSet goes in before the toolkit's, device plugin's and exporters'.
+APPLY_ORDER = sorted(STATES, key=lambda sk: {"pre-requisites": 0, "state-node-feature-discovery": 1,
+                                              "state-driver": 2, "state-operator-validation": 3}.get(sk[0], 4))
+
+
 @dataclass
 class ReconcileResult:
     policy: str | None
@@ -244,7 +254,7 @@ class ClusterPolicyReconciler:
         pool_status = None
         ds_ready: dict[str, bool] = {}
         midpass = not os.environ.get("AMDGPU_EXPERIMENT_NO_MIDPASS_LABELS")  # A/B switch (profiles/r5_ttr)
-        for state, key in STATES:
+        for state, key in APPLY_ORDER:
             if self._nodes_changed and midpass:
                 # a node changed during this pass (NFD's labels come in during
                 # the pass that created NFD, ~30 ms of creates on the box): its
@@ -308,6 +318,8 @@ class ClusterPolicyReconciler:
             if ready and (gpu_nodes == 0 or not patched):
                 self._ready_at.setdefault(uid, {}).setdefault(state, self.clock() - self._created_at[uid])
 
+        rank = {st: i for i, (st, _) in enumerate(STATES)}
+        results.sort(key=lambda r: rank[r.name])  # reported in the states' order
         upgrade = None
         if spec.driver.enabled and spec.driver.upgradePolicy.autoUpgrade and gpu_nodes and self._upgrade_pending(
                 driver_live):
