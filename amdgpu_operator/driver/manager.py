@@ -421,10 +421,18 @@ def monitor_once(env: NodeEnv) -> bool:
     afresh; until then the ClusterPolicy reports the node not validated."""
     from ..discovery import topology
 
+    t_probe = time.time()
     ok, msg = topology.probe(env.sysfs_root())
     path = env.validation_file(READY_FILES["driver"])
     marker = env.validation_file(LOST_MARKER)
-    if not ok and os.path.exists(path):
+    try:
+        fresh = os.stat(path).st_mtime >= t_probe
+    except FileNotFoundError:
+        fresh = False
+    if not ok and os.path.exists(path) and not fresh:
+        # (a driver-ready written since this probe began is a reload that
+        # finished meanwhile, not the loss the probe saw: withdrawing it would
+        # leave the node unvalidated on a live module)
         log.error("driver lost: %s", msg)
         _withdraw_validation(env, msg)
     elif ok and os.path.exists(marker) and not os.path.exists(path):
