@@ -497,3 +497,30 @@ def test_an_event_that_waited_through_a_long_pass_starts_the_next_at_once():
     assert len(starts) == 3
     assert starts[1] - starts[0] < 0.3 + 0.1  # no debounce wait after the long pass
     assert starts[2] - starts[1] >= 0.19  # the echo waited out the window
+
+
+def test_states_apply_validator_early_and_report_in_order(env):
+    """A pass applies the validator's objects right after the driver's (its
+    pod starts the bring-up's longest chain) and reports the states in the
+    ClusterPolicy's order."""
+    from amdgpu_operator.api.clusterpolicy import STATES
+    from amdgpu_operator.controller.reconciler import APPLY_ORDER
+
+    c, rec = env
+    order = [s for s, _ in APPLY_ORDER]
+    assert order[:4] == ["pre-requisites", "state-node-feature-discovery", "state-driver", "state-operator-validation"]
+    assert sorted(order) == sorted(s for s, _ in STATES)
+    created = []
+    orig = c.create
+
+    def record(obj):
+        if obj.get("kind") == "DaemonSet":
+            created.append(obj["metadata"]["name"])
+        return orig(obj)
+
+    c.create = record
+    c.create(cluster_policy(spec=spec_from_values(parse_set_flags(REFERENCE_SET_FLAGS))))
+    res = rec.reconcile()
+    assert [r.name for r in res.states] == [s for s, _ in STATES]
+    assert created.index("amd-operator-validator") < created.index("amd-container-toolkit-daemonset")
+    assert created.index("amd-driver-daemonset") < created.index("amd-operator-validator")
