@@ -11,7 +11,7 @@ queries behind ``nvidia-smi`` (/root/reference/README.md:152,158-167).
 from __future__ import annotations
 
 import ctypes
-from dataclasses import asdict, dataclass, field
+from ..utils.record import asdict, field, record
 
 from .. import native
 
@@ -160,7 +160,7 @@ def _s(b: bytes) -> str:
     return b.decode("utf-8", "replace")
 
 
-@dataclass(frozen=True)
+@record(frozen=True)
 class GpuDevice:
     """One schedulable GPU (a whole MI355X in SPX, one partition in DPX/QPX/CPX)."""
 
@@ -202,7 +202,7 @@ class GpuDevice:
         return asdict(self)
 
 
-@dataclass(frozen=True)
+@record(frozen=True)
 class GpuLink:
     src: int
     dst: int
@@ -292,7 +292,7 @@ def probe(root: str | None = None, expect_gpus: int = 0) -> tuple[bool, str]:
     return rc == 0, _s(buf.value)
 
 
-@dataclass
+@record
 class GpuMetrics:
     index: int
     bdf: str
@@ -379,7 +379,7 @@ class Smi:
         return self._lib.at_smi_set_memory_partition(index, mode.encode())
 
 
-@dataclass(frozen=True)
+@record(frozen=True)
 class HealthEvent:
     index: int
     kind: str

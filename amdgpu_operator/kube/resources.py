@@ -10,10 +10,10 @@ from __future__ import annotations
 
 import copy
 import json
-from dataclasses import dataclass
+from ..utils.record import record
 
 
-@dataclass(frozen=True)
+@record(frozen=True)
 class ResourceType:
     group: str
     version: str

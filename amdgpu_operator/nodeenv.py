@@ -14,13 +14,13 @@ import os
 import subprocess
 import threading
 import time
-from dataclasses import dataclass, field
+from .utils.record import field, record
 from typing import Callable
 
 from . import DEFAULT_NAMESPACE
 
 
-@dataclass
+@record
 class ProcResult:
     rc: int
     stdout: str
@@ -104,7 +104,7 @@ def run_local(argv: list[str], env: dict | None = None, timeout: float = 300.0) 
         return ProcResult(124, e.stdout or "", (e.stderr or "") + "\ntimeout", time.perf_counter() - t0)
 
 
-@dataclass
+@record
 class NodeEnv:
     node_name: str
     client: object

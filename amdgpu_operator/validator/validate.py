@@ -30,7 +30,6 @@ import os
 import shutil
 import threading
 import time
-from concurrent.futures import ThreadPoolExecutor
 
 from .. import RESOURCE_NAME, native
 from ..kube.client import wait_for
@@ -520,11 +519,16 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
 
     fabric = None
     try:
-        with ThreadPoolExecutor(max_workers=len(jobs) + 1) as ex:
-            fabric_f = (ex.submit(check_fabric, env, gpus, None, link_frac) if require_links and world > 1
-                        else None)
-            results = list(ex.map(one, jobs))
-            fabric = fabric_f.result() if fabric_f is not None else None
+        if len(jobs) == 1 and not (require_links and world > 1):
+            results = [one(jobs[0])]  # one GPU: no pool (its import is on the spawn's path)
+        else:
+            from concurrent.futures import ThreadPoolExecutor
+
+            with ThreadPoolExecutor(max_workers=len(jobs) + 1) as ex:
+                fabric_f = (ex.submit(check_fabric, env, gpus, None, link_frac) if require_links and world > 1
+                            else None)
+                results = list(ex.map(one, jobs))
+                fabric = fabric_f.result() if fabric_f is not None else None
     finally:
         shutil.rmtree(rdv, ignore_errors=True)
     reports = []

@@ -678,12 +678,12 @@ def test_gfd_labels_describe_every_gpu_of_a_mixed_node(tmp_path):
     all of them (round 2 labelled it from the first GPU only): shared values
     as before, differing ones `mixed`, sizes the minimum, and per-mode
     counts that match the device plugin's `mixed` resources."""
-    import dataclasses
+    from amdgpu_operator.utils import record
 
     fakesys.build_node(str(tmp_path / "a"), 1, "SPX", "NPS1")
     fakesys.build_node(str(tmp_path / "b"), 1, "CPX", "NPS2")
     spx, cpx = T.enumerate_gpus(str(tmp_path / "a")), T.enumerate_gpus(str(tmp_path / "b"))
-    cpx = [dataclasses.replace(g, physical_index=1) for g in cpx]
+    cpx = [record.replace(g, physical_index=1) for g in cpx]
     lab = L.gfd_labels(spx + cpx, str(tmp_path / "a"))
     assert lab["amd.com/gpu.count"] == str(1 + len(cpx)) and lab["amd.com/gpu.physical-count"] == "2"
     assert lab["amd.com/gpu.compute-partition"] == "mixed" and lab["amd.com/gpu.memory-partition"] == "mixed"
@@ -696,7 +696,7 @@ def test_gfd_labels_describe_every_gpu_of_a_mixed_node(tmp_path):
     res = {T.partition_resource(g, "amd.com/gpu", "mixed") for g in spx + cpx}
     assert res == {"amd.com/gpu", "amd.com/gpu-cpx"}
     # mixed SKUs: per-product counts, MFMA types only where all have them
-    mi300 = [dataclasses.replace(spx[0], device_id=0x74A1, arch="gfx942", physical_index=2)]
+    mi300 = [record.replace(spx[0], device_id=0x74A1, arch="gfx942", physical_index=2)]
     lab = L.gfd_labels(spx + mi300, str(tmp_path / "a"))
     assert lab["amd.com/gpu.product"] == "mixed" and lab["amd.com/gpu.family"] == "mixed"
     assert lab["amd.com/gpu.product.AMD-Instinct-MI355X.count"] == "1"

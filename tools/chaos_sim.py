@@ -42,7 +42,6 @@ diagnostics; exits 1 if any seed failed.
 from __future__ import annotations
 
 import argparse
-import dataclasses
 import os
 import random
 import sys
@@ -57,6 +56,7 @@ from amdgpu_operator.api.clusterpolicy import (REFERENCE_SET_FLAGS, deep_merge, 
 from amdgpu_operator.driver.manager import monitor_once  # noqa: E402
 from amdgpu_operator.sandbox import WORKLOAD_CONFIG_LABEL  # noqa: E402
 from amdgpu_operator.testing.simcluster import NodeSpec, SimCluster  # noqa: E402
+from amdgpu_operator.utils import record  # noqa: E402
 
 FAULTS = ("delpod", "delpod", "driverloss", "kubelet", "switch", "switch", "spec", "upgrade", "partition", "partbusy")
 REVALIDATE = ("driverloss", "partition", "partbusy", "upgrade", "switch", "noop")
@@ -192,7 +192,7 @@ def run_seed(seed: int, steps: int, settle_s: float, timeout: float, http_api: b
                 os.rename(f, f + ".gone")
                 # the driver container's health monitor notices (run here with the harness's own
                 # client: under --rbac the node env's HTTP client carries no ServiceAccount token)
-                monitor_once(dataclasses.replace(env, client=c.client))
+                monitor_once(record.replace(env, client=c.client))
                 os.rename(f + ".gone", f)
             elif fault == "kubelet":
                 c.nodes[node].kubelet.restart()
