@@ -157,8 +157,9 @@ def main(argv: list[str] | None = None) -> int:
     _common(op)
     op.add_argument("--health-port", type=int, default=8081)
     op.add_argument("--resync", type=float, default=30.0)
-    op.add_argument("--debounce", type=float, default=0.02,
-                    help="an event within this long after a pass waits out the rest of it (bursts cost one pass)")
+    op.add_argument("--debounce", type=float, default=0.003,
+                    help="an event within this long after a pass waits out the rest of it (bursts cost one pass; "
+                         "the echoes of the operator's own writes trigger no pass at all, kube/informer.py)")
     op.add_argument("--leader-elect", action="store_true",
                     help="run the controller only while holding the Lease (replicas > 1: warm standbys)")
     op.add_argument("--leader-election-id", default="amd-gpu-operator-leader")

@@ -44,7 +44,11 @@ class Informer:
     """List-then-watch cache of one kind (optionally one namespace)."""
 
     def __init__(self, client, api_version: str, kind: str, namespace: str | None = None, on_event=None,
-                 relist_wait_s: float = 1.0, watch_timeout_s: float = 300.0):
+                 relist_wait_s: float = 1.0, watch_timeout_s: float = 300.0, is_echo=None):
+        """``is_echo(obj)``: True for the watch event of a write the owner
+        made itself (its own resourceVersion): cached, but ``on_event`` is not
+        called for it."""
+        self.is_echo = is_echo
         self.client = client
         self.watch_timeout_s = watch_timeout_s
         self.api_version = api_version
@@ -154,7 +158,8 @@ class Informer:
                             self.put(obj)
                         else:
                             continue  # BOOKMARK: only the version moves
-                        if self.on_event is not None:
+                        if self.on_event is not None and not (etype != "DELETED" and self.is_echo is not None
+                                                              and self.is_echo(obj)):
                             self.on_event(self.kind)
                     if not events and time.monotonic() - began < 1.0:
                         stop.wait(self.relist_wait_s)  # closed at once: do not spin on a failing server
@@ -170,12 +175,26 @@ class CachedClient:
         is called for every change of a kind whose ``trigger`` is true."""
         self._client = client
         self._stop = stop
+        # resourceVersions of this client's own writes: their watch events are
+        # echoes, which update the caches but trigger nothing (bounded)
+        self._own: dict[tuple, bool] = {}
         self.informers: dict[tuple[str, str], Informer] = {}
         for spec in kinds:
             av, kind, ns = spec[:3]
             trigger = spec[3] if len(spec) > 3 else False
-            self.informers[(av, kind)] = Informer(client, av, kind, ns,
-                                                  on_event=on_event if trigger else None).start(stop)
+            self.informers[(av, kind)] = Informer(client, av, kind, ns, on_event=on_event if trigger else None,
+                                                  is_echo=self._is_echo).start(stop)
+
+    OWN_WRITES_KEPT = 4096
+
+    @staticmethod
+    def _ident(obj: dict) -> tuple:
+        md = obj.get("metadata") or {}
+        return (obj.get("apiVersion"), obj.get("kind"), md.get("namespace"), md.get("name"))
+
+    def _is_echo(self, obj: dict) -> bool:
+        rv = (obj.get("metadata") or {}).get("resourceVersion")
+        return rv is not None and (self._ident(obj), rv) in self._own
 
     def uncached(self):
         return self._client
@@ -229,6 +248,11 @@ class CachedClient:
         inf = self.informers.get((obj.get("apiVersion"), obj.get("kind")))
         if inf is not None and isinstance(obj, dict) and obj.get("metadata"):
             inf.put(obj)
+            rv = obj["metadata"].get("resourceVersion")
+            if rv is not None:  # every version this client wrote (a write's event may come after the next write)
+                if len(self._own) >= self.OWN_WRITES_KEPT:
+                    self._own.pop(next(iter(self._own)))
+                self._own[(self._ident(obj), rv)] = True
         return obj
 
     def create(self, obj):

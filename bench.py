@@ -54,7 +54,7 @@ def parse():
                     help="CPU-only, but start stand-in validator processes through the rank launcher")
     ap.add_argument("--sysfs-root", default=None, help="default: / when a GPU is present, else synthetic")
     ap.add_argument("--quick-workload", action="store_true", help="small validator sizes (CI)")
-    ap.add_argument("--operator-debounce", type=float, default=0.02,
+    ap.add_argument("--operator-debounce", type=float, default=0.003,
                     help="the operator's reconcile debounce (s; the chart's default, cli/main.py --debounce)")
     ap.add_argument("--no-counter-gate", action="store_true", help="skip the rocprofiler counter gate (outer profiler)")
     ap.add_argument("--rccl-single-gpu", action="store_true",

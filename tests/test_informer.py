@@ -215,3 +215,35 @@ def test_timed_out_watch_resumes_without_a_relist():
         assert len(lists) == 1
     finally:
         stop.set()
+
+
+def test_echoes_of_own_writes_trigger_nothing():
+    """A CachedClient's own writes come back on the watch: the cache takes
+    them, but the change callback (the operator's reconcile trigger) is not
+    called for them; another party's write to the same object is."""
+    import threading
+    import time
+
+    from amdgpu_operator.kube import resources as R
+    from amdgpu_operator.kube.client import LocalClient
+    from amdgpu_operator.kube.fakeapi import FakeApiServer
+    from amdgpu_operator.kube.informer import CachedClient
+
+    server = LocalClient(FakeApiServer())
+    seen, stop = [], threading.Event()
+    cc = CachedClient(server, [("v1", "Node", None, True)], stop, on_event=seen.append)
+    try:
+        assert cc.wait_synced(5)
+        time.sleep(0.05)
+        seen.clear()
+        cc.create(R.new("v1", "Node", "n1"))
+        cc.patch("v1", "Node", "n1", {"metadata": {"labels": {"a": "1"}}})
+        time.sleep(0.2)
+        assert seen == [] and cc.get("v1", "Node", "n1")["metadata"]["labels"] == {"a": "1"}
+        server.patch("v1", "Node", "n1", {"metadata": {"labels": {"b": "2"}}})  # someone else
+        deadline = time.time() + 2
+        while not seen and time.time() < deadline:
+            time.sleep(0.01)
+        assert seen == ["Node"]
+    finally:
+        stop.set()
