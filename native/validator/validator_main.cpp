@@ -2124,5 +2124,8 @@ int main(int argc, char** argv) {
     struct stat sb;
     while (stat(a.linger_until.c_str(), &sb) != 0 && secs(tl) < a.linger_max_s) usleep(1000);
   }
+  // AMDGPU_VALIDATOR_CLEAN_EXIT=1: a normal exit, with the runtime's and a
+  // profiler's exit handlers (rocprofv3 writes its traces there)
+  if (const char* e = getenv("AMDGPU_VALIDATOR_CLEAN_EXIT"); e && e[0] == '1') exit(ok ? 0 : 1);
   _exit(ok ? 0 : 1);
 }
