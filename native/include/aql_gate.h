@@ -47,4 +47,11 @@ int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, const void* A, 
 int avk_aql_gate_gemm_dtype(int dtype, const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt,
                             void* C, int M, int N, int K, const char* code_object, double timeout_s,
                             avk_aql_gate_result* out, char* err, int errlen);
+
+// Set up the gate's HSA state for a GPU agent ahead of its first gate: the
+// session above and the counter profiles of every dtype.  It dispatches
+// nothing, so it can run on another thread while the process's other kernels
+// run; a gate call meanwhile waits for it.  Returns 0, or -1 with a message in
+// err (the gate call then reports the failure itself).
+int avk_aql_gate_prepare(const char* pci_bus_id, int agent_ordinal, const char* code_object, char* err, int errlen);
 }

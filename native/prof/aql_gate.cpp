@@ -364,7 +364,42 @@ struct Session {
 std::mutex g_sessions_m;
 std::map<std::string, Session*> g_sessions;  // by "bus/ordinal/code object"; never freed (process lifetime)
 
+// The open session of an agent and code object, opened here on first use.
+// A caller that finds the session being opened (avk_aql_gate_prepare on
+// another thread) waits for it on the lock.
+Session* session_for(const char* pci_bus_id, int agent_ordinal, const char* code_object) {
+  const std::string key = std::string(pci_bus_id ? pci_bus_id : "") + "/" + std::to_string(agent_ordinal) + "/" +
+                          (code_object ? code_object : "");
+  std::lock_guard<std::mutex> l(g_sessions_m);
+  auto it = g_sessions.find(key);
+  if (it != g_sessions.end() && it->second->broken) g_sessions.erase(it), it = g_sessions.end();
+  if (it == g_sessions.end()) {
+    auto* fresh = new Session;
+    try {
+      fresh->open(pci_bus_id, agent_ordinal, code_object);
+    } catch (...) {
+      delete fresh;  // a half-open session is not kept (its HSA objects go with the process)
+      throw;
+    }
+    it = g_sessions.emplace(key, fresh).first;
+  }
+  return it->second;
+}
+
 }  // namespace
+
+extern "C" int avk_aql_gate_prepare(const char* pci_bus_id, int agent_ordinal, const char* code_object, char* err,
+                                    int errlen) {
+  try {
+    Session* ss = session_for(pci_bus_id, agent_ordinal, code_object);
+    std::lock_guard<std::mutex> l(ss->m);
+    for (int d = 0; d < AVK_AQL_GATE_DTYPES; ++d) ss->profile(d);
+    return 0;
+  } catch (const Fail& f) {
+    if (err && errlen > 0) snprintf(err, errlen, "%s", f.msg.c_str());
+  }
+  return -1;
+}
 
 extern "C" const char* avk_aql_gate_counter_name(int i) {
   return (i >= 0 && i < AVK_AQL_GATE_COUNTERS) ? kSpecs[0].names[i] : "";
@@ -390,25 +425,7 @@ extern "C" int avk_aql_gate_gemm_dtype(int dtype, const char* pci_bus_id, int ag
   memset(out, 0, sizeof(*out));
   try {
     if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 256) throw Fail{"M, N, K must be multiples of 256"};
-    Session* ss = nullptr;
-    {
-      const std::string key = std::string(pci_bus_id ? pci_bus_id : "") + "/" + std::to_string(agent_ordinal) + "/" +
-                              (code_object ? code_object : "");
-      std::lock_guard<std::mutex> l(g_sessions_m);
-      auto it = g_sessions.find(key);
-      if (it != g_sessions.end() && it->second->broken) g_sessions.erase(it), it = g_sessions.end();
-      if (it == g_sessions.end()) {
-        auto* fresh = new Session;
-        try {
-          fresh->open(pci_bus_id, agent_ordinal, code_object);
-        } catch (...) {
-          delete fresh;  // a half-open session is not kept (its HSA objects go with the process)
-          throw;
-        }
-        it = g_sessions.emplace(key, fresh).first;
-      }
-      ss = it->second;
-    }
+    Session* ss = session_for(pci_bus_id, agent_ordinal, code_object);
     std::lock_guard<std::mutex> l(ss->m);
     auto& prof = ss->profile(d);
     memset(prof.output_buffer.ptr, 0, prof.output_buffer.size);

@@ -554,11 +554,15 @@ Step step_vecadd(const Args& args, hipStream_t st) {
   AVK_OK(avk_fill_uniform_f32(a, n, 11, -1, 1, st));
   AVK_OK(avk_fill_uniform_f32(b, n, 12, -1, 1, st));
   AVK_OK(avk_vector_add_f32(a, b, c, n, st));
-  // full check on the device + an independent host check of a prefix
+  // full check on the device + an independent host check of a prefix.  The
+  // prefix is 16 KiB a copy: the runtime copies that much from device to
+  // pageable host memory with a blit kernel, while a larger copy takes the
+  // SDMA engine, whose first use in a process costs ~8 ms (the validator's
+  // other read-backs are this size too: profiles/r5_init)
   unsigned long long* bad_dev;
   HIP_OK(hipMalloc(&bad_dev, sizeof(unsigned long long)));
   AVK_OK(avk_vector_add_verify_f32(a, b, c, n, bad_dev, st));
-  const int64_t hn = 1 << 16;
+  const int64_t hn = 1 << 12;
   std::vector<float> ha(hn), hb(hn), hc(hn);
   unsigned long long dev_bad = 0;
   HIP_OK(hipMemcpyAsync(ha.data(), a, hn * 4, hipMemcpyDeviceToHost, st));
@@ -942,7 +946,7 @@ Step step_hbm(const Args& a, hipStream_t st, int cus) {
   HIP_OK(hipEventCreate(&e1));
   // the fastest of several short trials: another process's kernel or queue
   // set-up on the GPU stalls one trial, not all (the floor judges the device)
-  const int iters = 3, trials = 5;
+  const int iters = 2, trials = 3;
   float ms = 0;
   for (int t = 0; t < trials; ++t) {
     HIP_OK(hipEventRecord(e0, st));
@@ -1937,6 +1941,11 @@ int main(int argc, char** argv) {
   memset(&prop, 0, sizeof(prop));
   std::thread rccl_thread;
   RcclInit rccl_state;
+  struct {
+    double seconds = -1;
+    std::string error;
+  } gate_prep;
+  std::thread gate_prep_thread;
   const bool need_comm = has_step(a, "rccl") || has_step(a, "sweep");
   if (need_comm) {  // before any HIP call: see the note at struct Rccl
     auto tl = Clock::now();
@@ -1994,6 +2003,30 @@ int main(int argc, char** argv) {
     for (const auto& d : devs) local_ids.push_back(d.first);
     primary = a.device = devs[0].first;
     a.agent_ordinal = devs[0].second;
+    if (a.counter_gate && a.gate_mode == "aql" &&
+        (has_step(a, "gemm") || has_step(a, "gemm_fp8") || has_step(a, "gemm_fp4"))) {
+      // the counter gates' HSA set-up (a private queue, the code object, the
+      // counter profiles: ~6 ms) on a thread, beside the stream's creation
+      // and the first steps; it dispatches nothing.  The first gate waits for
+      // it if it is still running.
+      std::vector<std::pair<std::string, int>> agents;
+      for (const auto& d : devs) {
+        char bus[64] = {0};
+        HIP_OK(hipDeviceGetPCIBusId(bus, sizeof(bus), d.first));
+        agents.emplace_back(bus, d.second);
+      }
+      gate_prep_thread = std::thread([agents, &gate_prep] {
+        const auto tp = Clock::now();
+        const std::string co = Gate::exe_dir() + "validator_kernels.co";
+        for (const auto& ag : agents) {
+          char err[512] = {0};
+          if (avk_aql_gate_prepare(ag.first.c_str(), ag.second, co.c_str(), err, sizeof(err)) != 0 &&
+              gate_prep.error.empty())
+            gate_prep.error = err;
+        }
+        gate_prep.seconds = secs(tp);
+      });
+    }
     steps.push_back(step_hip(a, &prop));
     ok = steps.back().ok;
     if (ok && need_comm && rccl_state.error.empty())
@@ -2039,6 +2072,7 @@ int main(int argc, char** argv) {
     ok = false;
     error = e.what();
   }
+  if (gate_prep_thread.joinable()) gate_prep_thread.join();
   if (rccl_thread.joinable()) {
     if (rccl_state.abandoned) rccl_thread.detach();  // blocked in RCCL's bootstrap: ends with the process
     else rccl_thread.join();
@@ -2067,6 +2101,12 @@ int main(int argc, char** argv) {
     out += "], ";
   }
   if (stream_create_s >= 0) out += fmt("\"stream_create_s\": %.4f, ", stream_create_s);
+  if (gate_prep.seconds >= 0) {
+    std::string esc;
+    for (char c : gate_prep.error) esc += (c == '"' || c == '\\') ? '\'' : c;
+    out += fmt("\"gate_prepare\": {\"seconds\": %.4f%s}, ", gate_prep.seconds,
+               esc.empty() ? "" : (", \"error\": \"" + esc + "\"").c_str());
+  }
   if (gate_wait_s >= 0)
     out += fmt("\"start_gate\": {\"wait_s\": %.4f, \"go_wait_s\": %.4f, \"kfd_open_at_gate\": %s, \"steps_s\": %.4f}, ",
                gate_wait_s, gate_go_wait_s, kfd_early ? "true" : "false", total - gate_wait_s);
