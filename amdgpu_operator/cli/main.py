@@ -17,7 +17,6 @@ Sub-commands:
 
 from __future__ import annotations
 
-import argparse
 import json
 import sys
 import threading
@@ -150,6 +149,8 @@ def main(argv: list[str] | None = None) -> int:
         # the kubelet stops a container with SIGTERM: operands then run their
         # shutdown (toolkit cleanup, vfio unbind, plugin socket removal)
         return run_operand(env, argv, _stop_on_signals(), ready=_ready_signal(), container_env=dict(os.environ))
+
+    import argparse  # not on the operands' start-up path (cli/argspec.py)
 
     ap = argparse.ArgumentParser(prog="amdgpu-operator")
     sub = ap.add_subparsers(dest="cmd", required=True)

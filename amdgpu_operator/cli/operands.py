@@ -9,19 +9,21 @@ environment and the pod's stop event.
 
 from __future__ import annotations
 
-import argparse
 import os
 import threading
 import time
 
 from ..nodeenv import NodeEnv
+from ..utils import logs
 from ..utils.logs import get_logger
+from .argspec import Spec
 
 log = get_logger("amdgpu.operand")
 
 
-def build_parser() -> argparse.ArgumentParser:
-    p = argparse.ArgumentParser(prog="amdgpu-operator", description="MI355X GPU operator components")
+def operand_spec() -> Spec:
+    """The operands' command line (parsed without argparse: cli/argspec.py)."""
+    p = Spec(prog="amdgpu-operator", description="MI355X GPU operator components")
     sub = p.add_subparsers(dest="cmd", required=True)
 
     d = sub.add_parser("driver", help="driver DaemonSet containers")
@@ -118,6 +120,11 @@ def build_parser() -> argparse.ArgumentParser:
     sdp.add_argument("--resource-prefix", default="amd.com")
     sdp.add_argument("--health-poll-ms", type=int, default=1000)
     return p
+
+
+def build_parser():
+    """The operands' command line as an ``argparse.ArgumentParser`` (help text)."""
+    return operand_spec().argparse()
 
 
 def _pci(env: NodeEnv):
@@ -274,9 +281,9 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
     cenv = container_env or {}
     if argv and argv[0] == "validate":
         known, extra = _split_passthrough(argv[1:])
-        a = build_parser().parse_args(["validate", *known])
+        a = operand_spec().parse(["validate", *known])
     else:
-        a = build_parser().parse_args(argv)
+        a = operand_spec().parse(argv)
         extra = []
     cmd = a.cmd
     # the device plugin prepares (enumeration, sockets, amd-smi health
@@ -370,7 +377,7 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
             threading.Thread(target=importlib.import_module, args=("amdgpu_operator.deviceplugin.server",),
                              name="preload-plugin", daemon=True).start()
             try:
-                V.wait_ready(env, "driver", GATE_TIMEOUT_S, stop)
+                V.wait_ready(env, "driver", GATE_TIMEOUT_S, stop)  # loads logging while it waits
             except V.StepFailed:
                 if stop.is_set():
                     return 0

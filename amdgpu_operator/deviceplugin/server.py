@@ -28,7 +28,6 @@ import was ~0.1 s of the plugin's start-up, before its kubelet registration.
 
 from __future__ import annotations
 
-import logging
 import os
 import threading
 import time
@@ -40,8 +39,9 @@ from . import api
 from .allocator import from_topology, preferred
 from .config import REPLICA_SEP, DevicePluginConfig
 from ..rpc import wire
+from ..utils.logs import get_logger
 
-log = logging.getLogger("amdgpu.deviceplugin")
+log = get_logger("amdgpu.deviceplugin")
 
 
 @dataclass

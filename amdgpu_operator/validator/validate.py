@@ -93,8 +93,16 @@ def clear_ready(env: NodeEnv, steps=READY_FILES) -> None:
 
 
 def wait_ready(env: NodeEnv, step: str, timeout: float = 600.0, stop: threading.Event | None = None) -> dict:
+    from ..utils import logs
     from ..utils.fswait import wait_for_file
 
+    got = read_ready(env, step)
+    if got is not None:
+        return got
+    # logging loads during the wait, not at the first log call after it (and
+    # not when there is no wait: the import would hold the interpreter lock
+    # beside what follows)
+    logs.preload_async()
     path = env.validation_file(READY_FILES[step])
     if wait_for_file(path, timeout, stop, env.poll_s, check=lambda p: read_ready(env, step) is not None):
         return read_ready(env, step)
