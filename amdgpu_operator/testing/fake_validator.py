@@ -320,7 +320,12 @@ def _main(argv: list[str]) -> int:
             with open(path + ".tmp", "w") as f:
                 f.write(json.dumps(rep))
             os.replace(path + ".tmp", path)
-    if os.environ.get("AMDGPU_FAKE_POD_EXIT_S") and "--pod-check" in argv:  # the kernel's release of a GPU process
+    if os.environ.get("AMDGPU_FAKE_POD_EXIT_S") and "--pod-check" in argv:
+        # the kernel's release of a GPU process after its exit: a signal does
+        # not cut it short, so the kubelet's stop waits it out
+        import signal
+
+        signal.signal(signal.SIGTERM, signal.SIG_IGN)
         time.sleep(float(os.environ["AMDGPU_FAKE_POD_EXIT_S"]))
     return 0 if rep["ok"] else 1
 

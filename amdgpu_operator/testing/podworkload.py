@@ -54,7 +54,11 @@ def _pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm_n: 
         "apiVersion": "v1", "kind": "Pod",
         "metadata": {"name": name, "namespace": namespace, "labels": {"app": "gpu-job", POD_LABEL: run_id}},
         "spec": {
-            "nodeName": node, "restartPolicy": "Never",
+            # through the scheduler, as a user's pod goes: it counts the GPUs of
+            # pods still terminating on the node (the plugin-validation pod the
+            # validator deleted once it had its result) and binds once they are
+            # free, where a pod bound by nodeName would fail kubelet admission
+            "nodeSelector": {"kubernetes.io/hostname": node}, "restartPolicy": "Never",
             "tolerations": [{"key": resource, "operator": "Exists", "effect": "NoSchedule"}],
             "containers": [{"name": "gemm", "image": image,
                             "command": ["amdgpu-validator"],
@@ -82,8 +86,7 @@ def _dra_pod(name: str, node: str, namespace: str, run_id: str, count: int, gemm
              "spec": {"devices": {"requests": [req], "constraints": constraints}}}
     pod = _pod(name, node, namespace, run_id, count, gemm_n, image=image)
     spec = pod["spec"]
-    del spec["nodeName"], spec["tolerations"]
-    spec["nodeSelector"] = {"kubernetes.io/hostname": node}
+    del spec["tolerations"]
     spec["resourceClaims"] = [{"name": "gpus", "resourceClaimName": name}]
     spec["containers"][0]["resources"] = {"claims": [{"name": "gpus"}]}
     return [claim, pod]

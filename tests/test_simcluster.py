@@ -488,11 +488,20 @@ def test_plugin_validation_takes_the_pods_result_file_not_their_exit(tmp_path, m
 
     monkeypatch.setenv("AMDGPU_FAKE_POD_EXIT_S", "1.5")
     # operands as processes over HTTP, as in the bench: the validator's pod
-    # watch blocks in a socket read between events
-    c = SimCluster(str(tmp_path / "c"), [NodeSpec("gpu-1", 1)], fake_gpu="procs", process_containers=True).start()
+    # watch blocks in a socket read between events; kubelet-confirmed pod
+    # deletes (termination_s=0), as the bench runs them
+    c = SimCluster(str(tmp_path / "c"), [NodeSpec("gpu-1", 1)], fake_gpu="procs", process_containers=True,
+                   termination_s=0.0).start()
     try:
         c.install_operator(REF)
-        c.wait_ready(60, {"gpu-1": 1})
+        c.wait_ready(60)  # the policy's Ready, as the bench's clock stops
+        # a user's pods right away (the bench's config-5 pods): they go through
+        # the scheduler, which counts the validation pod's GPU while that pod
+        # is still exiting, and bind once it is free
+        from amdgpu_operator.testing.podworkload import run_pod_workload
+
+        out = run_pod_workload(c, "gpu-1", 1, gemm_n=256, timeout=30)
+        assert out["all_succeeded"] and out["gemm_correct"], out
         plugin = read_ready(c.nodes["gpu-1"].env, "plugin")
         marks = plugin["marks"]
         assert "pods_reported" in marks and marks["pods_reported"] - marks["pods_created"] < 1.5, marks
@@ -501,8 +510,8 @@ def test_plugin_validation_takes_the_pods_result_file_not_their_exit(tmp_path, m
         assert not pods or all(p["metadata"].get("deletionTimestamp") for p in pods)
         # the result files are consumed
         assert os.listdir(os.path.join(c.nodes["gpu-1"].env.validations_dir, POD_RESULTS)) == []
-        # a pod asking for the GPU right after Ready waits in the scheduler while the
-        # validation pod is still exiting (its GPU counts until it is gone), then runs
+        # verify's pod as well
+        c.wait_ready(60, {"gpu-1": 1})
         rep = verify(c.client, c.namespace, run_pods=True, pod_timeout=30)
         assert rep.ok, rep.table()
     finally:
