@@ -484,6 +484,9 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
                 st = {}
                 for x in rep.get("steps", []):
                     st[x["name"]] = round(st.get(x["name"], 0.0) + x.get("seconds", 0.0), 4)
+                    for k in ("co_load_s", "queue_s"):  # the HSA set-up's parts (gpu_check.cpp)
+                        if isinstance(x.get(k), (int, float)):
+                            st[k[:-2]] = round(st.get(k[:-2], 0.0) + x[k], 4)
                 main_at = None
                 if isinstance(rep.get("t_main"), (int, float)):  # CLOCK_MONOTONIC at the pod process's main
                     main_at = round(rep["t_main"] - (time.monotonic() - time.perf_counter()) - t0, 4)
