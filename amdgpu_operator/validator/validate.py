@@ -387,10 +387,11 @@ def planned_workload_processes(env: NodeEnv, args: list[str], budget: int) -> in
 
 
 # AMDGPU_VALIDATOR_LINGER=1: the workload validator processes stay until the
-# plugin validation is done (``--linger-until`` its ready file), so their KFD
-# teardown cannot overlap the plugin pod's HSA start-up (validator_main.cpp,
-# end of main).  Off by default: interleaved A/B on the MI355X found no gain
-# (0.386 / 0.384 s with, 0.376 / 0.379 s without; profiles/r5_ttr/linger).
+# plugin validation is done (``--linger-until`` its ready file, at most
+# LINGER_MAX_S), so their teardown cannot overlap the plugin pod's HSA
+# set-up (validator_main.cpp, end of main).  Off by default: interleaved A/B
+# on the MI355X found no gain, before (profiles/r5_ttr/linger) and after the
+# HBM step kept its buffers to the process's end (profiles/r5_init/wipe).
 LINGER = os.environ.get("AMDGPU_VALIDATOR_LINGER", "0") == "1"
 LINGER_MAX_S = 3.0
 

@@ -930,6 +930,21 @@ Step step_gemm_lowp(const Args& a, hipStream_t st, int cus, const LowPrecision& 
 Step step_gemm_fp8(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kFp8); }
 Step step_gemm_fp4(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kFp4); }
 
+// Device buffers released only when the process ends.  Freeing VRAM makes
+// the kernel driver wipe it (wipe-on-release, an SDMA fill at ~80 GB/s), and
+// the GPU's other page-table work waits behind that: a 2 GiB hipFree delays
+// an HSA queue creation right after it from 5 ms to 32 ms, in any process on
+// the GPU.  The plugin-validation pod's queue creation and code-object load,
+// which run while the validator ends, took 10-30 ms longer in about half the
+// bring-ups after the HBM step freed its 2 GiB; kept to the process's end,
+// in none of 32 (profiles/r5_init/wipe).
+std::mutex g_release_m;  // the devices of one process run their steps on threads of their own
+std::vector<void*> g_release_at_exit;
+void release_at_exit(void* p) {
+  std::lock_guard<std::mutex> l(g_release_m);
+  g_release_at_exit.push_back(p);
+}
+
 Step step_hbm(const Args& a, hipStream_t st, int cus) {
   auto t0 = Clock::now();
   Step s{"hbm"};
@@ -967,8 +982,8 @@ Step step_hbm(const Args& a, hipStream_t st, int cus) {
   HIP_OK(hipStreamSynchronize(st));
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
-  (void)hipFree(src);
-  (void)hipFree(dst);
+  release_at_exit(src);  // not hipFree: see g_release_at_exit
+  release_at_exit(dst);
   (void)hipFree(cs);
   const double gbps = 2.0 * bytes / (ms * 1e-3) / 1e9;
   // calibrated on a 1 GiB copy; smaller copies are launch-bound: report only
@@ -2155,10 +2170,10 @@ int main(int argc, char** argv) {
   }
   // --linger-until (opt-in, validate.py AMDGPU_VALIDATOR_LINGER=1): the
   // caller already has the report (EOF above); the process keeps its GPU
-  // state until the file appears, so its KFD teardown cannot overlap the
-  // plugin-validation pod's HSA start-up.  The interleaved A/B on the
-  // MI355X found no gain from it (profiles/r5_ttr/linger), so the default
-  // is to exit here at once.
+  // state until the file appears, so its teardown cannot overlap the
+  // plugin-validation pod's HSA set-up.  Interleaved A/Bs on the MI355X found
+  // no gain from it (profiles/r5_ttr/linger, profiles/r5_init/wipe), so the
+  // default is to exit here at once.
   if (!a.linger_until.empty()) {
     const auto tl = Clock::now();
     struct stat sb;
