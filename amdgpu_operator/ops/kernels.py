@@ -55,6 +55,8 @@ def _lib(name: str = LIB_NAME) -> ctypes.CDLL:
         "avk_gemv_rows_fp8": ([P, P, P, I, I, S], I),
         "avk_gemv_cols_fp8": ([P, P, P, I, I, S], I),
         "avk_gemv_cols_bf16": ([P, P, P, I, I, S], I),
+        "avk_gemv_rows_fp4": ([P, P, P, I, I, S], I),
+        "avk_gemv_cols_fp4": ([P, P, P, I, I, S], I),
         "avk_hbm_copy": ([P, P, I64, I, I, S], I),
         "avk_checksum": ([P, I64, P, S], I),
         "avk_max_abs_diff_f32": ([P, P, I64, P, S], I),
@@ -320,6 +322,52 @@ def gemv_cols_bf16(x, v, out=None, stream=None):
     else:
         out.zero_()
     _check(_lib().avk_gemv_cols_bf16(x.data_ptr(), v.data_ptr(), out.data_ptr(), R, C, _stream(stream)), "gemv_cols")
+    return out
+
+
+def gemv_fp4(x, v, transpose: bool = False, out=None, stream=None):
+    """The fp4 step's Freivalds GEMVs, x FP4 pairs uint8 ``[R, C/2]``:
+    ``out[r] = sum_c x[r, c] v[c]``, or with ``transpose`` ``out[c] = sum_r
+    x[r, c] v[r]`` (fp32).  C a multiple of 16."""
+    import torch
+
+    _require(x, torch.uint8, "x", 8)
+    _require(v, torch.float32, "v")
+    if x.dim() != 2:
+        raise ValueError("gemv_fp4 shape mismatch")
+    R, C = x.shape[0], 2 * x.shape[1]
+    if C % 16 or v.numel() != (R if transpose else C):
+        raise ValueError("gemv_fp4 shape mismatch")
+    n = C if transpose else R
+    if out is None:
+        out = torch.zeros(n, device=x.device, dtype=torch.float32)
+    elif transpose:
+        out.zero_()
+    fn = _lib().avk_gemv_cols_fp4 if transpose else _lib().avk_gemv_rows_fp4
+    _check(fn(x.data_ptr(), v.data_ptr(), out.data_ptr(), R, C, _stream(stream)), "gemv_fp4")
+    return out
+
+
+def gemv_fp8(x, v, transpose: bool = False, out=None, stream=None):
+    """The fp8 step's Freivalds GEMVs, x e4m3 bytes uint8 ``[R, C]``:
+    ``out[r] = sum_c x[r, c] v[c]``, or with ``transpose`` ``out[c] = sum_r
+    x[r, c] v[r]`` (fp32).  C a multiple of 8."""
+    import torch
+
+    _require(x, torch.uint8, "x", 8)
+    _require(v, torch.float32, "v")
+    if x.dim() != 2:
+        raise ValueError("gemv_fp8 shape mismatch")
+    R, C = x.shape
+    if C % 8 or v.numel() != (R if transpose else C):
+        raise ValueError("gemv_fp8 shape mismatch")
+    n = C if transpose else R
+    if out is None:
+        out = torch.zeros(n, device=x.device, dtype=torch.float32)
+    elif transpose:
+        out.zero_()
+    fn = _lib().avk_gemv_cols_fp8 if transpose else _lib().avk_gemv_rows_fp8
+    _check(fn(x.data_ptr(), v.data_ptr(), out.data_ptr(), R, C, _stream(stream)), "gemv_fp8")
     return out
 
 

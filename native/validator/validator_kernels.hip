@@ -1494,19 +1494,18 @@ __global__ __launch_bounds__(g4::NTHR, 1) void gemm_fp4_nt_kernel(const uint8_t*
                           std::make_integer_sequence<int, 64>{});
 }
 
-// OCP e4m3 (gfx950's fp8, not MI300's fnuz): 1 sign, 4 exponent (bias 7), 3
-// mantissa bits; exponent 0 is subnormal (m / 8 * 2^-6), S.1111.111 is NaN
-__device__ __forceinline__ float e4m3_to_f32(uint8_t b) {
-  const unsigned e = (b >> 3) & 15u, m = b & 7u;
-  float v = e ? __builtin_bit_cast(float, ((e + 120u) << 23) | (m << 20)) : (float)m * (1.0f / 512.0f);
-  if (e == 15u && m == 7u) v = __builtin_nanf("");
-  return (b & 0x80) ? -v : v;
+// four OCP e4m3 bytes (1 sign, 4 exponent bits with bias 7, 3 mantissa bits;
+// gfx950's fp8, not MI300's fnuz) -> floats on the conversion unit
+// (v_cvt_pk_f32_fp8): a tenth of the VALU work of a bit decode, which made the
+// column GEMV decode-bound (47 -> 23 us at 4096^2, profiles/r5_kernels)
+__device__ __forceinline__ void e4m3x4_to_f32(uint32_t x, float* out) {
+  const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)x, false);
+  const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)x, true);
+  out[0] = lo[0];
+  out[1] = lo[1];
+  out[2] = hi[0];
+  out[3] = hi[1];
 }
-
-struct e4m3 {
-  uint8_t b;
-  __device__ __forceinline__ operator float() const { return e4m3_to_f32(b); }
-};
 
 // random finite e4m3 bytes: sign, exponent field 0..8, any mantissa (|x| <= 3.75)
 __global__ __launch_bounds__(256) void fill_fp8_kernel(uint8_t* __restrict__ p, int64_t n, uint64_t seed) {
@@ -1531,29 +1530,22 @@ __global__ __launch_bounds__(256) void fill_fp4_kernel(uint8_t* __restrict__ p, 
   }
 }
 
-// z[c] += sum_{r in slice} X[r][c] * v[r]   (X e4m3 row-major), 8 cols per lane
-__global__ __launch_bounds__(256) void gemv_cols_fp8_kernel(const uint8_t* __restrict__ X, const float* __restrict__ v,
-                                                            float* __restrict__ z, int R, int C, int rows_per_slice) {
-  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
-  if (c0 >= C) return;
-  const int r0 = blockIdx.y * rows_per_slice;
-  const int r1 = min(R, r0 + rows_per_slice);
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r = r0; r < r1; ++r) {
-    const uint64_t x = *reinterpret_cast<const uint64_t*>(X + (size_t)r * C + c0);
-    const float vr = v[r];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += e4m3_to_f32((uint8_t)(x >> (8 * j))) * vr;
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) atomicAdd(z + c0 + j, s[j]);
-}
-
-// OCP FP4 e2m1: 1 sign, 2 exponent (bias 1), 1 mantissa bit; every code finite
-__device__ __forceinline__ float e2m1_to_f32(unsigned c) {
-  const unsigned e = (c >> 1) & 3u, m = c & 1u;
-  const float v = e ? (float)(2u + m) * (float)(1u << e) * 0.25f : 0.5f * (float)m;
-  return (c & 8u) ? -v : v;
+// eight OCP FP4 e2m1 codes (1 sign, 2 exponent bits with bias 1, 1 mantissa
+// bit; four bytes, element 2k in the low nibble) -> floats on gfx950's
+// conversion unit (v_cvt_scalef32_pk_f32_fp4, scale 1)
+__device__ __forceinline__ void e2m1x8_to_f32(uint32_t x, float* out) {
+  const auto p0 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(x, 1.0f, 0);
+  const auto p1 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(x, 1.0f, 1);
+  const auto p2 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(x, 1.0f, 2);
+  const auto p3 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(x, 1.0f, 3);
+  out[0] = p0[0];
+  out[1] = p0[1];
+  out[2] = p1[0];
+  out[3] = p1[1];
+  out[4] = p2[0];
+  out[5] = p2[1];
+  out[6] = p3[0];
+  out[7] = p3[1];
 }
 
 // y[r] = sum_c X[r][c] * v[c], X FP4 pairs [R][C/2] (one wave per row, 16 values per lane step)
@@ -1566,30 +1558,110 @@ __global__ __launch_bounds__(256) void gemv_rows_fp4_kernel(const uint8_t* __res
   float s = 0.f;
   for (int c = lane * 16; c < C; c += 64 * 16) {
     const uint64_t x = *reinterpret_cast<const uint64_t*>(row + c / 2);
+    float f[16];
+    e2m1x8_to_f32((uint32_t)x, f);
+    e2m1x8_to_f32((uint32_t)(x >> 32), f + 8);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) s += e2m1_to_f32((unsigned)(x >> (4 * j)) & 15u) * v[c + j];
+    for (int j = 0; j < 16; ++j) s += f[j] * v[c + j];
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   if (lane == 0) y[wave] = s;
 }
 
-// z[c] += sum_{r in slice} X[r][c] * v[r], X FP4 pairs [R][C/2], 16 cols per lane
-__global__ __launch_bounds__(256) void gemv_cols_fp4_kernel(const uint8_t* __restrict__ X, const float* __restrict__ v,
-                                                            float* __restrict__ z, int R, int C, int rows_per_slice) {
-  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 16;
-  if (c0 >= C) return;
+// Column GEMVs of the Freivalds checks: z[c] += sum_{r in slice} X[r][c] v[r],
+// X row-major.  A block covers 64 * Dec::kCols columns (one 8- or 16-byte load
+// per lane per row), its 4 waves take every 4th row of the slice (4 row
+// streams in flight per block), and their partial sums meet in LDS, so each
+// column gets one atomic per block.  (A wave per block-row with kCols atomics
+// per lane made the fp4 one 121 us at 4096^2: profiles/r5_kernels.)
+struct DecFp4 {  // FP4 pairs [R][C/2]: 16 columns in 8 bytes
+  static constexpr int kCols = 16;
+  __device__ static void load(const void* X, int r, int C, int c0, float* out) {
+    const uint64_t x = *reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(X) + (size_t)r * (C / 2) + c0 / 2);
+    e2m1x8_to_f32((uint32_t)x, out);
+    e2m1x8_to_f32((uint32_t)(x >> 32), out + 8);
+  }
+};
+struct DecFp8 {  // e4m3 [R][C]: 8 columns in 8 bytes
+  static constexpr int kCols = 8;
+  __device__ static void load(const void* X, int r, int C, int c0, float* out) {
+    const uint64_t x = *reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(X) + (size_t)r * C + c0);
+    e4m3x4_to_f32((uint32_t)x, out);
+    e4m3x4_to_f32((uint32_t)(x >> 32), out + 4);
+  }
+};
+struct DecBf16 {  // bf16 [R][C]: 8 columns in 16 bytes
+  static constexpr int kCols = 8;
+  __device__ static void load(const void* X, int r, int C, int c0, float* out) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(static_cast<const __bf16*>(X) + (size_t)r * C + c0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = (float)x[j];
+  }
+};
+
+template <typename Dec>
+__global__ __launch_bounds__(256) void gemv_cols_kernel(const void* __restrict__ X, const float* __restrict__ v,
+                                                        float* __restrict__ z, int R, int C, int rows_per_slice) {
+  constexpr int W = 64 * Dec::kCols;  // columns per block
+  __shared__ float red[4][W];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cb = blockIdx.x * W;
+  const int c0 = cb + lane * Dec::kCols;
   const int r0 = blockIdx.y * rows_per_slice;
   const int r1 = min(R, r0 + rows_per_slice);
-  float s[16] = {};
-  for (int r = r0; r < r1; ++r) {
-    const uint64_t x = *reinterpret_cast<const uint64_t*>(X + (size_t)r * (C / 2) + c0 / 2);
-    const float vr = v[r];
+  float s[Dec::kCols] = {};
+  if (c0 < C) {
+    for (int r = r0 + w; r < r1; r += 4) {
+      float x[Dec::kCols];
+      Dec::load(X, r, C, c0, x);
+      const float vr = v[r];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) s[j] += e2m1_to_f32((unsigned)(x >> (4 * j)) & 15u) * vr;
+      for (int j = 0; j < Dec::kCols; ++j) s[j] += x[j] * vr;
+    }
   }
 #pragma unroll
-  for (int j = 0; j < 16; ++j) atomicAdd(z + c0 + j, s[j]);
+  for (int j = 0; j < Dec::kCols; ++j) red[w][lane * Dec::kCols + j] = s[j];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < W / 256; ++k) {
+    const int col = k * 256 + threadIdx.x;
+    if (cb + col < C) atomicAdd(z + cb + col, red[0][col] + red[1][col] + red[2][col] + red[3][col]);
+  }
+}
+
+template <typename Dec>
+int launch_gemv_cols(const void* X, const float* v, float* z, int R, int C, hipStream_t s) {
+  constexpr int W = 64 * Dec::kCols;
+  const int bx = (C + W - 1) / W;
+  int slices = 512 / bx;  // ~2048 waves in all at 4096^2 (4 per block), each over a stream of rows
+  if (slices < 1) slices = 1;
+  if (slices > R) slices = R;
+  const int rows_per_slice = (R + slices - 1) / slices;
+  dim3 grid(bx, (R + rows_per_slice - 1) / rows_per_slice);
+  gemv_cols_kernel<Dec><<<grid, 256, 0, s>>>(X, v, z, R, C, rows_per_slice);
+  return hipGetLastError();
+}
+
+// y[r] = sum_c X[r][c] v[c], X e4m3 [R][C] (one wave per row, 8 bytes per lane step)
+__global__ __launch_bounds__(256) void gemv_rows_fp8_kernel(const uint8_t* __restrict__ X, const float* __restrict__ v,
+                                                            float* __restrict__ y, int R, int C) {
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= R) return;
+  const uint8_t* row = X + (size_t)wave * C;
+  float s = 0.f;
+  for (int c = lane * 8; c < C; c += 64 * 8) {
+    const uint64_t x = *reinterpret_cast<const uint64_t*>(row + c);
+    float f[8];
+    e4m3x4_to_f32((uint32_t)x, f);
+    e4m3x4_to_f32((uint32_t)(x >> 32), f + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += f[j] * v[c + j];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) y[wave] = s;
 }
 
 // ------------------------------------------------- Freivalds check GEMVs ----
@@ -1609,26 +1681,6 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const T* __restrict__ X,
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   if (lane == 0) y[wave] = s;
-}
-
-// z[c] += sum_{r in slice} X[r][c] * v[r]   (X bf16 row-major), 8 cols per lane
-__global__ __launch_bounds__(256) void gemv_cols_bf16_kernel(const __bf16* __restrict__ X,
-                                                             const float* __restrict__ v,
-                                                             float* __restrict__ z, int R, int C,
-                                                             int rows_per_slice) {
-  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
-  if (c0 >= C) return;
-  const int r0 = blockIdx.y * rows_per_slice;
-  const int r1 = min(R, r0 + rows_per_slice);
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r = r0; r < r1; ++r) {
-    bf16x8 x = *reinterpret_cast<const bf16x8*>(X + (size_t)r * C + c0);
-    const float vr = v[r];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += (float)x[j] * vr;
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) atomicAdd(z + c0 + j, s[j]);
 }
 
 // ------------------------------------------------------------ K3 HBM copy ----
@@ -2097,34 +2149,20 @@ AVK_API int avk_gemv_rows_fp4(const void* X, const float* v, float* y, int R, in
 // z = X^T v accumulated into z (caller zeroes z); X FP4 pairs [R][C/2], C % 16 == 0
 AVK_API int avk_gemv_cols_fp4(const void* X, const float* v, float* z, int R, int C, hipStream_t s) {
   if (!X || !v || !z || R <= 0 || C <= 0 || C % 16 || ((uintptr_t)X % 8)) return hipErrorInvalidValue;
-  const int bx = (C / 16 + 255) / 256;
-  int slices = 256 / bx;
-  if (slices < 1) slices = 1;
-  if (slices > R) slices = R;
-  const int rows_per_slice = (R + slices - 1) / slices;
-  dim3 grid(bx, (R + rows_per_slice - 1) / rows_per_slice);
-  gemv_cols_fp4_kernel<<<grid, 256, 0, s>>>((const uint8_t*)X, v, z, R, C, rows_per_slice);
-  return hipGetLastError();
+  return launch_gemv_cols<DecFp4>(X, v, z, R, C, s);
 }
 
 // y = X v, X e4m3 [R][C] (C % 8 == 0)
 AVK_API int avk_gemv_rows_fp8(const void* X, const float* v, float* y, int R, int C, hipStream_t s) {
-  if (!X || !v || !y || R <= 0 || C <= 0 || C % 8) return hipErrorInvalidValue;
-  gemv_rows_kernel<e4m3><<<(R + 3) / 4, 256, 0, s>>>((const e4m3*)X, v, y, R, C);
+  if (!X || !v || !y || R <= 0 || C <= 0 || C % 8 || ((uintptr_t)X % 8)) return hipErrorInvalidValue;
+  gemv_rows_fp8_kernel<<<(R + 3) / 4, 256, 0, s>>>((const uint8_t*)X, v, y, R, C);
   return hipGetLastError();
 }
 
 // z = X^T v accumulated into z (caller zeroes z); X e4m3 [R][C], C % 8 == 0
 AVK_API int avk_gemv_cols_fp8(const void* X, const float* v, float* z, int R, int C, hipStream_t s) {
   if (!X || !v || !z || R <= 0 || C <= 0 || C % 8 || ((uintptr_t)X % 8)) return hipErrorInvalidValue;
-  const int bx = (C / 8 + 255) / 256;
-  int slices = 256 / bx;
-  if (slices < 1) slices = 1;
-  if (slices > R) slices = R;
-  const int rows_per_slice = (R + slices - 1) / slices;
-  dim3 grid(bx, (R + rows_per_slice - 1) / rows_per_slice);
-  gemv_cols_fp8_kernel<<<grid, 256, 0, s>>>((const uint8_t*)X, v, z, R, C, rows_per_slice);
-  return hipGetLastError();
+  return launch_gemv_cols<DecFp8>(X, v, z, R, C, s);
 }
 
 // y = X v ; X is [R][C] row-major (bf16 when x_is_bf16, else f32); C % 8 == 0
@@ -2141,14 +2179,7 @@ AVK_API int avk_gemv_rows(const void* X, int x_is_bf16, const float* v, float* y
 // z = X^T v accumulated into z (caller zeroes z); X bf16 [R][C], C % 8 == 0
 AVK_API int avk_gemv_cols_bf16(const void* X, const float* v, float* z, int R, int C, hipStream_t s) {
   if (!X || !v || !z || R <= 0 || C <= 0 || C % 8 || ((uintptr_t)X % 16)) return hipErrorInvalidValue;
-  const int bx = (C / 8 + 255) / 256;
-  int slices = 256 / bx;
-  if (slices < 1) slices = 1;
-  if (slices > R) slices = R;
-  const int rows_per_slice = (R + slices - 1) / slices;
-  dim3 grid(bx, (R + rows_per_slice - 1) / rows_per_slice);
-  gemv_cols_bf16_kernel<<<grid, 256, 0, s>>>((const __bf16*)X, v, z, R, C, rows_per_slice);
-  return hipGetLastError();
+  return launch_gemv_cols<DecBf16>(X, v, z, R, C, s);
 }
 
 // variant: 0 = plain loads/stores, 1 = nontemporal

@@ -440,3 +440,45 @@ def test_fp4_gemm_rejects_bad_shapes():
     with pytest.raises(ValueError):
         K.gemm_fp4_nt(torch.zeros(256, 320, device=DEV, dtype=torch.uint8), torch.zeros(256, 320, device=DEV,
                                                                                       dtype=torch.uint8))  # K = 640
+
+
+@pytest.mark.parametrize("shape", [(4096, 4096), (512, 1024), (300, 1040), (7, 16)])
+def test_fp4_gemvs_vs_fp32(shape):
+    """The fp4 step's Freivalds GEMVs against fp32 torch on the dequantized
+    matrix: x v (one wave per row) and x^T v (column blocks of 1024, four row
+    streams per block meeting in LDS, one atomic per column per block)."""
+    R, C = shape
+    x = torch.empty(R, C // 2, device=DEV, dtype=torch.uint8)
+    K.fill_fp4_(x, R * 7 + C)
+    xf = K.fp4_to_float(x)
+    g = torch.Generator(device="cpu").manual_seed(R + C)
+    vr = torch.rand(R, generator=g).mul_(2).sub_(1).to(DEV)
+    vc = torch.rand(C, generator=g).mul_(2).sub_(1).to(DEV)
+    ref_cols = (xf.double().t() @ vr.double())
+    ref_rows = (xf.double() @ vc.double())
+    cols = K.gemv_fp4(x, vr, transpose=True)
+    rows = K.gemv_fp4(x, vc)
+    for got, ref in ((cols, ref_cols), (rows, ref_rows)):
+        scale = ref.abs().max().item()
+        assert (got.double() - ref).abs().max().item() <= 1e-5 * max(scale, 1.0) * (1 + (R + C) / 1024)
+    # accumulates into a given output only after zeroing it (the caller's z)
+    z = torch.full((C,), 123.0, device=DEV)
+    assert torch.allclose(K.gemv_fp4(x, vr, transpose=True, out=z).double(), ref_cols, atol=1e-3)
+
+
+@pytest.mark.parametrize("shape", [(4096, 4096), (512, 1024), (300, 1032), (5, 8)])
+def test_fp8_gemvs_vs_fp32(shape):
+    """The fp8 step's Freivalds GEMVs (8-byte loads per lane, column blocks
+    reduced in LDS) against fp32 torch on the dequantized e4m3 matrix."""
+    R, C = shape
+    x = torch.empty(R, C, device=DEV, dtype=torch.float8_e4m3fn)
+    K.fill_fp8_(x, R * 5 + C)
+    xf = x.float()
+    g = torch.Generator(device="cpu").manual_seed(R * C)
+    vr = torch.rand(R, generator=g).mul_(2).sub_(1).to(DEV)
+    vc = torch.rand(C, generator=g).mul_(2).sub_(1).to(DEV)
+    xb = x.view(torch.uint8)
+    for got, ref in ((K.gemv_fp8(xb, vr, transpose=True), xf.double().t() @ vr.double()),
+                     (K.gemv_fp8(xb, vc), xf.double() @ vc.double())):
+        scale = ref.abs().max().item()
+        assert (got.double() - ref).abs().max().item() <= 1e-5 * max(scale, 1.0) * (1 + (R + C) / 1024)
