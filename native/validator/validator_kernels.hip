@@ -1496,8 +1496,8 @@ __global__ __launch_bounds__(g4::NTHR, 1) void gemm_fp4_nt_kernel(const uint8_t*
 
 // four OCP e4m3 bytes (1 sign, 4 exponent bits with bias 7, 3 mantissa bits;
 // gfx950's fp8, not MI300's fnuz) -> floats on the conversion unit
-// (v_cvt_pk_f32_fp8): a tenth of the VALU work of a bit decode, which made the
-// column GEMV decode-bound (47 -> 23 us at 4096^2, profiles/r5_kernels)
+// (v_cvt_pk_f32_fp8): a tenth of the VALU work of a bit decode, which had
+// made the column GEMV decode-bound (profiles/r5_kernels)
 __device__ __forceinline__ void e4m3x4_to_f32(uint32_t x, float* out) {
   const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)x, false);
   const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)x, true);
