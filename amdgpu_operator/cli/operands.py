@@ -369,15 +369,18 @@ def run_operand(env: NodeEnv, argv: list[str], stop: threading.Event, ready=lamb
     if cmd == "device-plugin":
         gated = bool(cenv.get(GATE_ENV))
         if gated:  # devices are enumerated from the live driver's KFD topology
-            import importlib
-
             from ..validator import validate as V
 
-            # the plugin's modules (allocator, config, rpc) load while the driver gate is still closed
-            threading.Thread(target=importlib.import_module, args=("amdgpu_operator.deviceplugin.server",),
-                             name="preload-plugin", daemon=True).start()
+            # the plugin's modules (allocator, config, rpc) and logging load
+            # before the driver gate is waited for, in this thread: the plugin
+            # needs them the moment the gate opens, and an import still running
+            # on another thread then held the interpreter lock against it (the
+            # gate noticed ~20 ms late on the MI355X box, profiles/r5_startup)
+            from ..deviceplugin import server as _server  # noqa: F401
+
+            logs.load()
             try:
-                V.wait_ready(env, "driver", GATE_TIMEOUT_S, stop)  # loads logging while it waits
+                V.wait_ready(env, "driver", GATE_TIMEOUT_S, stop)
             except V.StepFailed:
                 if stop.is_set():
                     return 0

@@ -22,7 +22,7 @@ device order so the answer is deterministic (kubelet retries are stable).
 from __future__ import annotations
 
 import itertools
-from dataclasses import dataclass
+from ..utils.record import record as dataclass
 from math import comb
 
 SAME_GPU_COST = 0

@@ -38,7 +38,8 @@ any GPU is doubled up.
 from __future__ import annotations
 
 import json
-from dataclasses import asdict, dataclass, field, fields
+from ..utils.record import asdict, field
+from ..utils.record import record as dataclass
 
 from .. import RESOURCE_NAME
 from .api import REPLICA_SEP  # noqa: F401 - "<device id>::<replica>"
@@ -86,7 +87,7 @@ class Flags:
 
     @classmethod
     def from_dict(cls, data) -> "Flags":
-        d = _check_keys("flags", data, [f.name for f in fields(cls)])
+        d = _check_keys("flags", data, list(cls.__record_fields__))
         out = cls()
         if "partitionStrategy" in d:
             out.partitionStrategy = _choice("flags.partitionStrategy", d["partitionStrategy"], ("single", "mixed"))
@@ -113,7 +114,7 @@ class SharedResource:
 
     @classmethod
     def from_dict(cls, data) -> "SharedResource":
-        d = _check_keys("sharing.timeSlicing.resources[]", data, [f.name for f in fields(cls)])
+        d = _check_keys("sharing.timeSlicing.resources[]", data, list(cls.__record_fields__))
         r = d.get("replicas")
         if isinstance(r, bool) or not isinstance(r, int) or not 1 <= r <= 256:
             raise ValueError(f"replicas must be an integer in [1, 256], got {r!r}")
@@ -140,7 +141,7 @@ class TimeSlicing:
 
     @classmethod
     def from_dict(cls, data) -> "TimeSlicing":
-        d = _check_keys("sharing.timeSlicing", data, [f.name for f in fields(cls)])
+        d = _check_keys("sharing.timeSlicing", data, list(cls.__record_fields__))
         res = d.get("resources") or []
         if not isinstance(res, list):
             raise ValueError("sharing.timeSlicing.resources must be a list")

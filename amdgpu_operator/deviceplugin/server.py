@@ -31,7 +31,8 @@ from __future__ import annotations
 import os
 import threading
 import time
-from dataclasses import dataclass, field
+from ..utils.record import field
+from ..utils.record import record as dataclass
 from typing import Callable
 
 from .. import RESOURCE_NAME

@@ -32,6 +32,11 @@ def _logging():
     return logging
 
 
+def load() -> None:
+    """Import ``logging`` (and apply setup) now."""
+    _logging()
+
+
 def preload_async() -> None:
     """Import ``logging`` (and apply setup) on a daemon thread.  An operand
     calls this before it waits (for a gate, another operand's ready file),
