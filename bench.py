@@ -362,6 +362,57 @@ def critical_path(r: dict) -> dict:
     return cp
 
 
+# the parts of a bring-up's critical path a slow step is measured on: (name,
+# getter of the part's duration in s)
+_CP_PARTS = (
+    ("plugin pod HSA start-up (hsa_init)", lambda cp: (cp.get("pod") or {}).get("hsa_init")),
+    ("plugin pod HSA set-up (queue, code object)", lambda cp: (cp.get("pod") or {}).get("hsa")),
+    ("workload validator process", lambda cp: (cp.get("wl") or {}).get("proc")),
+    ("driver validated", lambda cp: (cp.get("at") or {}).get("driver")),
+    ("device plugin registered", lambda cp: (cp.get("at") or {}).get("registered")),
+    ("plugin pod start (created -> main)", lambda cp: (((cp.get("pod") or {}).get("main_at") or 0)
+                                                      - ((cp.get("at") or {}).get("pods_created") or 0)) or None),
+    ("validated -> policy Ready", lambda cp: cp.get("ready_gap")),
+    ("harness stall", lambda cp: (cp.get("stall_ms") or 0) / 1e3 or None),
+)
+
+
+def slow_steps(cps: list[dict], factor: float = 1.3) -> list[dict]:
+    """Every timed bring-up above ``factor`` x the median time-to-Ready, with
+    the critical-path part that grew the most against its own median (VERDICT
+    r4: the record names the cause of any step above 1.3 x median)."""
+    import statistics
+
+    if len(cps) < 3:
+        return []
+    med = statistics.median(cp["ttr"] for cp in cps)
+    meds = {}
+    for name, get in _CP_PARTS:
+        vals = [v for v in (get(cp) for cp in cps) if isinstance(v, (int, float))]
+        if vals:
+            meds[name] = statistics.median(vals)
+    out = []
+    for i, cp in enumerate(cps):
+        if cp["ttr"] <= factor * med:
+            continue
+        growth = []
+        for name, get in _CP_PARTS:
+            v = get(cp)
+            if isinstance(v, (int, float)) and name in meds:
+                growth.append((v - meds[name], name, v))
+        growth.sort(reverse=True)
+        rec = {"step": i, "ttr": cp["ttr"], "median_ttr": round(med, 4)}
+        if growth and growth[0][0] > 0:
+            d, name, v = growth[0]
+            rec["cause"] = name
+            rec["cause_s"] = round(v, 4)
+            rec["cause_median_s"] = round(meds[name], 4)
+            rec["also"] = [{"part": n, "s": round(x, 4), "median_s": round(meds[n], 4)}
+                           for dd, n, x in growth[1:3] if dd > 0.01]
+        out.append(rec)
+    return out
+
+
 def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode: str = "process",
                  pods: bool = False) -> dict:
     from amdgpu_operator.api.clusterpolicy import REFERENCE_SET_FLAGS, deep_merge, parse_set_flags
@@ -825,6 +876,8 @@ def main():
                 # process and plugin-pod steps; harness stall / GC / CPU throttling; GPU tools of
                 # other parties that overlapped it)
                 "critical_path": [critical_path(r) for r in results],
+                # the bring-ups above 1.3 x the median, each with the critical-path part that grew most
+                "slow_steps": slow_steps([critical_path(r) for r in results]),
                 f"{other}_mode_time_to_ready_s": [round(r["time_to_ready_s"], 4) for r in compare],
             },
         }

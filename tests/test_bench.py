@@ -38,6 +38,7 @@ def test_bench_json_line_contract():
     cps = cfg["critical_path"]
     assert len(cps) == 2 and all(c["ttr"] > 0 and "complete" in c["at"] and "ready_gap" in c for c in cps)
     assert [c["ttr"] for c in cps] == cfg["time_to_ready_s"]
+    assert isinstance(cfg["slow_steps"], list)  # fewer than 3 steps: nothing is judged slow
     # the collective block after the last timed bring-up (world 1 here; the 8-rank run: test_launcher.py)
     col = cfg["collectives"]
     assert col["ok"] and col["world"] == 1 and set(col["ops"]) == {"allreduce", "allgather", "reducescatter"}
@@ -105,3 +106,26 @@ def test_bench_harness_never_opens_the_gpu():
     assert col["ok"] and col["world"] == 1 and not col["simulated"], col
     assert len(col["ops"]["allreduce"]) >= 14 and all(r["ok"] and r["latency_us"] > 0 for r in col["ops"]["allreduce"])
     assert col["ops"]["allreduce"][-1]["algbw_gbps"] > 100  # a 1 GiB single-rank all-reduce is an HBM copy
+
+
+def test_slow_steps_name_the_part_that_grew():
+    """the record names the cause of any bring-up above 1.3 x the
+    median - the critical-path part that grew most against its own median."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+
+    def cp(ttr, hsa_init=0.06, proc=0.12):
+        return {"ttr": ttr, "at": {"driver": 0.09, "registered": 0.08, "pods_created": 0.11},
+                "wl": {"proc": proc}, "pod": {"hsa_init": hsa_init, "hsa": 0.011, "main_at": 0.14},
+                "ready_gap": 0.008, "stall_ms": 3.0}
+
+    cps = [cp(0.24), cp(0.23), cp(0.25), cp(0.42, hsa_init=0.25), cp(0.33, proc=0.22), cp(0.24)]
+    slow = b.slow_steps(cps)
+    assert [s["step"] for s in slow] == [3, 4]
+    assert slow[0]["cause"] == "plugin pod HSA start-up (hsa_init)" and slow[0]["cause_s"] == 0.25
+    assert slow[0]["cause_median_s"] == 0.06 and slow[0]["median_ttr"] == 0.245
+    assert slow[1]["cause"] == "workload validator process" and slow[1]["cause_s"] == 0.22
+    assert b.slow_steps(cps[:2]) == []
