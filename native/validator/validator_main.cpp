@@ -590,9 +590,13 @@ Step step_vecadd(const Args& args, hipStream_t st) {
 // GPU during the counted dispatch (a plugin-validation pod, a user workload
 // during a revalidation) adds its waves and MFMA ops, and the exact
 // invariants fail.  A failed verdict whose output still matched is therefore
-// counted again (kGateAttempts in all): a healthy GPU passes as soon as one
-// dispatch runs alone, a defective one fails every attempt.
-constexpr int kGateAttempts = 3;
+// counted again (kGateAttempts in all), after a pause that doubles each time
+// (2, 4, 8, 16, 32 ms: 62 ms at most): a healthy GPU passes as soon as one
+// dispatch runs alone, a defective one fails every attempt.  Back-to-back
+// retries all fell inside one plugin pod's HSA set-up (its code-object upload
+// and kernel, ~10-40 ms) in 1 of 75 bring-ups on a CPU-throttled box, and
+// failed the node's validation (profiles/r5_final/gate_retry).
+constexpr int kGateAttempts = 6;
 
 // Several devices in one process (the partitions of one GPU, a pod holding
 // several GPUs): their gated dispatches take turns, and the first turn starts
@@ -645,6 +649,7 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
   int attempt = 0;
   std::string reasons;
   for (attempt = 1; attempt <= kGateAttempts; ++attempt) {
+    if (attempt > 1) std::this_thread::sleep_for(std::chrono::milliseconds(1 << (attempt - 1)));
     HIP_OK(hipMemsetAsync(cs, 0, 16, st));
     AVK_OK(avk_checksum(C16, (int64_t)n * n * 2, cs, st));
     HIP_OK(hipMemsetAsync(C16, 0, (size_t)n * n * 2, st));
