@@ -274,6 +274,68 @@ def settle_gpu(settle_s: float) -> dict | None:
     return {"waited_s": round(waited, 3), "kfd_procs": kfd}
 
 
+def _proc_tree(root_pid: int) -> list[int]:
+    """Every descendant of ``root_pid`` (from /proc/<pid>/stat's ppid)."""
+    children: dict[int, list[int]] = {}
+    try:
+        pids = [int(p) for p in os.listdir("/proc") if p.isdigit()]
+    except OSError:
+        return []
+    for pid in pids:
+        try:
+            with open(f"/proc/{pid}/stat", "rb") as f:
+                st = f.read()
+            ppid = int(st[st.rindex(b")") + 2:].split()[1])
+        except (OSError, ValueError, IndexError):
+            continue
+        children.setdefault(ppid, []).append(pid)
+    out, todo = [], [root_pid]
+    while todo:
+        p = todo.pop()
+        for c in children.get(p, []):
+            out.append(c)
+            todo.append(c)
+    return out
+
+
+def tree_kfd_holders(root_pid: int | None = None) -> list[str]:
+    """The processes of the bring-up's own tree (the harness's descendants;
+    under torchrun the agent's, so every rank's children) holding /dev/kfd,
+    as ``<pid>:<what>``: an operand container's ``python -m amdgpu_operator
+    <operand>`` sub-command, or the executable's name (validator, pod check).
+    Reading /proc/<pid>/fd of our own children sidesteps the PID namespace of
+    the KFD process list in sysfs (it names host PIDs)."""
+    if root_pid is None:
+        root_pid = os.getppid() if int(os.environ.get("WORLD_SIZE", "1")) > 1 else os.getpid()
+    out = []
+    for pid in _proc_tree(root_pid):
+        try:
+            fds = os.listdir(f"/proc/{pid}/fd")
+        except OSError:
+            continue
+        held = False
+        for fd in fds:
+            try:
+                if os.readlink(f"/proc/{pid}/fd/{fd}") == "/dev/kfd":
+                    held = True
+                    break
+            except OSError:
+                continue
+        if not held:
+            continue
+        try:
+            with open(f"/proc/{pid}/cmdline", "rb") as f:
+                argv = [a.decode(errors="replace") for a in f.read().split(b"\0") if a]
+        except OSError:
+            argv = []
+        what = os.path.basename(argv[0]) if argv else "?"
+        if "amdgpu_operator" in argv:
+            i = argv.index("amdgpu_operator")
+            what = " ".join(argv[i + 1:i + 3]) or what
+        out.append(f"{pid}:{what[:40]}")
+    return out
+
+
 class BringUpFailed(RuntimeError):
     """A validation step of the bring-up failed: its host failure records
     (validate.py ``write_failure``) carry what failed and the rates measured
@@ -457,6 +519,7 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
         # keep their collectors.
         gc.collect()
         settle = settle_gpu(args.settle_s)
+        kfd_holders = {"start": tree_kfd_holders()}
         gc.disable()
         thr0 = cpu_throttle_stat()
         stall = StallMeter()
@@ -476,6 +539,8 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
         max_stall = stall.stop()
         gc_stats = gcm.stop()
         gc.enable()
+        # the operator's own GPU processes still open at Ready (operands' amd-smi sessions, ...)
+        kfd_holders["ready"] = tree_kfd_holders()
         # the kubelet then publishes amd.com/gpu in Node.status on its own status tick
         # (experiments with the DRA driver instead of the device plugin: no amd.com/gpu)
         if (values.get("devicePlugin") or {}).get("enabled", True) is not False:
@@ -584,6 +649,15 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             "gemm_counter_gate": [s.get("counter_gate") for s in steps.get("gemm", [])],
             "fp8_tflops": [s.get("tflops") for s in steps.get("gemm_fp8", [])],
             "fp8_counter_gate": [s.get("counter_gate") for s in steps.get("gemm_fp8", [])],
+            "fp4_tflops": [s.get("tflops") for s in steps.get("gemm_fp4", [])],
+            "fp4_counter_gate": [s.get("counter_gate") for s in steps.get("gemm_fp4", [])],
+            "fp6_tflops": [s.get("tflops") for s in steps.get("gemm_fp6", [])],
+            "fp6_counter_gate": [s.get("counter_gate") for s in steps.get("gemm_fp6", [])],
+            "mxfp4_tflops": [s.get("tflops") for s in steps.get("gemm_mxfp4", [])],
+            "mxfp4_counter_gate": [s.get("counter_gate") for s in steps.get("gemm_mxfp4", [])],
+            "gate_attempts": [s.get("gate_attempts") for k in ("gemm", "gemm_fp8", "gemm_fp4", "gemm_fp6",
+                                                                "gemm_mxfp4") for s in steps.get(k, [])],
+            "kfd_holders": kfd_holders,
             "hbm_gbps": [s.get("gbps") for s in steps.get("hbm", [])],
             "xgmi_read_gbps": [s.get("read_gbps") for s in steps.get("xgmi", [])],
             "rccl_busbw_gbps": [s.get("busbw_gbps") for s in steps.get("rccl", [])],
@@ -632,43 +706,341 @@ def standalone_sweep(args, launcher, fake_gpu, workdir: str) -> dict:
         shutil.rmtree(d, ignore_errors=True)
 
 
-def failure_line(args, n_gpus: int, fake_gpu, err: dict, results: list, warm: list, elapsed: float) -> dict:
-    """The JSON line of a run whose bring-up failed: ``value`` null, an
-    ``error`` object (which bring-up, which validation step, which ranks, the
-    floors against what was measured, the fabric's problems) and every
-    measurement the run got before and after it."""
+# The driver keeps a ~9 KB tail of the run's stdout + stderr and parses the JSON
+# line out of it (BENCH_r05: a 22 KB line with every step's critical path did
+# not parse).  The line carries the headline and summaries only; everything
+# per step, per rank, per size or per link goes to the detail file it names.
+LINE_BUDGET = 3000
+MODEL = "amd-gpu-operator ClusterPolicy bring-up (reference --set flags) + HIP/MFMA/RCCL validator"
+
+
+def default_detail_path(n_gpus: int) -> str:
+    """``gpurun_out/bench_detail_n<N>.json`` in the tree (merged back from a GPU
+    box), or the temp dir when the tree is read-only."""
+    d = os.path.join(ROOT, "gpurun_out")
+    try:
+        os.makedirs(d, exist_ok=True)
+        if os.access(d, os.W_OK):
+            return os.path.join(d, f"bench_detail_n{n_gpus}.json")
+    except OSError:
+        pass
+    return os.path.join(tempfile.gettempdir(), f"amdgpu_bench_detail_n{n_gpus}.json")
+
+
+def write_detail(path: str, obj: dict) -> str | None:
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        tmp = f"{path}.tmp.{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump(obj, f, indent=1, default=str)
+        os.replace(tmp, path)
+        return path
+    except OSError:
+        return None
+
+
+def _r(x, nd=4):
+    return round(x, nd) if isinstance(x, (int, float)) and not isinstance(x, bool) else x
+
+
+def dist_summary(xs: list, nd: int = 4) -> dict | None:
+    """min / median / p90 / max / mean of a list of numbers (nearest rank)."""
+    v = sorted(x for x in xs if isinstance(x, (int, float)) and not isinstance(x, bool))
+    if not v:
+        return None
+    n = len(v)
+
+    def q(p):
+        return v[min(n - 1, max(0, int(round(p * (n - 1)))))]
+
+    return {"min": round(v[0], nd), "med": round(q(0.5), nd), "p90": round(q(0.9), nd), "max": round(v[-1], nd),
+            "mean": round(sum(v) / n, nd)}
+
+
+def per_gpu_range(xs: list, nd: int = 1):
+    """A per-GPU list as [min, max] (one value at N = 1), None entries dropped."""
+    v = [x for x in (xs or []) if isinstance(x, (int, float)) and not isinstance(x, bool)]
+    if not v:
+        return None
+    return [round(min(v), nd)] if len(set(v)) == 1 or len(v) == 1 else [round(min(v), nd), round(max(v), nd)]
+
+
+def gate_verdict(xs: list):
+    """Per-GPU counter-gate verdicts, as one word when they agree."""
+    v = [x for x in (xs or []) if x is not None]
+    if not v:
+        return None
+    return v[0] if len(set(v)) == 1 else {k: v.count(k) for k in sorted(set(v))}
+
+
+def collectives_summary(col: dict | None) -> dict | None:
+    """The sweep (validator/sweep.py) as peak busBW, busBW at 1 MiB / 256 MiB,
+    the Ready gate's worst ratio and the slowest link; the rows stay in the
+    detail file."""
+    if not col:
+        return None
+    out = {k: col[k] for k in ("ok", "world", "sizes", "simulated", "seconds") if k in col}
+    if col.get("error"):
+        out["error"] = str(col["error"])[:200]
+    ar = (col.get("ops") or {}).get("allreduce") or []
+    if ar:
+        out["peak_busbw_gbps"] = max(r.get("busbw_gbps", 0.0) for r in ar)
+        out["peak_algbw_gbps"] = max(r.get("algbw_gbps", 0.0) for r in ar)
+        for label, b in (("1MiB", 1 << 20), ("256MiB", 256 << 20)):
+            row = min(ar, key=lambda r: abs(r["bytes"] - b))
+            if row["bytes"] == b or abs(row["bytes"] - b) <= b // 2:
+                out[f"busbw_{label}_gbps"] = row.get("busbw_gbps")
+        out["small_latency_us"] = ar[0].get("latency_us")
+    ff = col.get("fabric_floors") or {}
+    if ff:
+        out["min_allreduce_ratio"] = ff.get("min_allreduce_ratio")
+        below = ff.get("links_below_floor") or []
+        out["links_below_floor"] = len(below)
+        if below:
+            out["links_below_floor_first"] = below[:4]
+    lm = col.get("xgmi_links") or {}
+    if lm:
+        out["min_read_gbps"] = lm.get("min_read_gbps")
+        out["links_intact"] = lm.get("intact")
+    return out
+
+
+def pod_workload_summary(pw: dict | None) -> dict | None:
+    if not pw:
+        return None
+    out = {"ok": bool(pw.get("all_succeeded")) and pw.get("gemm_correct", True) is not False}
+    for k, name in (("pods", "pods"), ("allocation", "allocation"), ("admission_to_kernel_done_p50_s", "p50_s"),
+                    ("admission_to_kernel_done_p99_s", "p99_s"), ("single_gpu_pods_distinct_devices", "distinct"),
+                    ("error", "error")):
+        if k in pw:
+            out[name] = str(pw[k])[:200] if k == "error" else pw[k]
+    return out
+
+
+def slow_summary(slow: list[dict]) -> dict:
+    causes: dict[str, int] = {}
+    for s in slow:
+        if s.get("cause"):
+            causes[s["cause"]] = causes.get(s["cause"], 0) + 1
+    out: dict = {"count": len(slow), "factor": 1.3, "steps": [s["step"] for s in slow][:20]}
+    if causes:
+        top = max(causes.items(), key=lambda kv: kv[1])
+        out["top_cause"] = top[0]
+        out["top_cause_count"] = top[1]
+    return out
+
+
+def rates_summary(r: dict) -> dict:
+    """The last timed bring-up's per-GPU validator rates, as [min, max]."""
+    out = {}
+    for k, name in (("gemm_tflops", "bf16_tflops"), ("fp8_tflops", "fp8_tflops"), ("fp4_tflops", "fp4_tflops"),
+                    ("fp6_tflops", "fp6_tflops"), ("mxfp4_tflops", "mxfp4_tflops"), ("hbm_gbps", "hbm_gbps"),
+                    ("xgmi_read_gbps", "xgmi_read_gbps"), ("rccl_busbw_gbps", "rccl_busbw_gbps"),
+                    ("rccl_comm_init_s", "rccl_comm_init_s")):
+        v = per_gpu_range(r.get(k) or [], 4 if k.endswith("_s") else 1)
+        if v is not None:
+            out[name] = v
+    gates = {}
+    for k, name in (("gemm_counter_gate", "bf16"), ("fp8_counter_gate", "fp8"), ("fp4_counter_gate", "fp4"),
+                    ("fp6_counter_gate", "fp6"), ("mxfp4_counter_gate", "mxfp4")):
+        g = gate_verdict(r.get(k) or [])
+        if g is not None:
+            gates[name] = g
+    if gates:
+        out["counter_gate"] = gates
+    att = [a for a in (r.get("gate_attempts") or []) if isinstance(a, int)]
+    if att:
+        out["gate_attempts_max"] = max(att)
+    return out
+
+
+# the order optional summary fields leave the line if it is still over budget
+# (a safety net: the summaries are sized to fit well below it at N = 8)
+_SHED = ("warmup_time_to_ready_s", "other_mode_time_to_ready_s", "kfd_holders", "pod_workload", "rates",
+         "allocatable_visible_s", "collectives", "time_to_ready_s", "slow_steps", "settle")
+
+
+def fit_line(out: dict, budget: int = LINE_BUDGET) -> str:
+    """The JSON line, at most ``budget`` bytes: the headline fields first,
+    optional summaries shed (and named in ``config.shed``) if it is over."""
+    line = json.dumps(out, separators=(",", ":"))
+    cfg = out.get("config") or {}
+    shed = []
+    for k in _SHED:
+        if len(line) <= budget:
+            break
+        if k in cfg:
+            cfg.pop(k)
+            shed.append(k)
+            cfg["shed"] = shed
+            line = json.dumps(out, separators=(",", ":"))
+    if len(line) > budget and isinstance(out.get("error"), dict):
+        out["error"] = {k: out["error"][k] for k in ("phase", "bring_up", "type", "failed_steps") if k in out["error"]}
+        line = json.dumps(out, separators=(",", ":"))
+    return line
+
+
+def error_summary(err: dict) -> dict:
+    """A failed run's ``error`` object, <= ~1 KB: which bring-up, which
+    validation step, which ranks, the floors it was held to; the ranks'
+    steps, the messages in full and any traceback are in the detail file."""
     recs = err.get("records") or {}
-    e = {k: err[k] for k in ("phase", "bring_up", "type", "message", "elapsed_s") if k in err}
+    e = {k: err[k] for k in ("phase", "bring_up", "type", "elapsed_s") if k in err}
+    e["message"] = str(err.get("message", ""))[:300]
     e["failed_steps"] = sorted(recs)
     wl = recs.get("workload")
     if wl:
         e["world"] = wl.get("world")
-        e["failed_ranks"] = wl.get("failed_ranks")
-        e["floors"] = wl.get("floors")
-        e["fabric_problems"] = wl.get("fabric_problems")
-        e["coverage_problems"] = wl.get("coverage_problems")
-        e["ranks"] = wl.get("ranks")
-    for step, rec in recs.items():
-        if step != "workload":
-            e.setdefault("step_messages", {})[step] = str(rec.get("message", ""))[:600]
-    if err.get("harness"):
-        e["harness"] = err["harness"]
+        e["failed_ranks"] = (wl.get("failed_ranks") or [])[:16]
+        fl = wl.get("floors") or {}
+        mins = {k: v for k, v in fl.items() if k.startswith("min_") and isinstance(v, (int, float))}
+        if mins:
+            e["floors"] = mins
+        # the first failing step of the first failed rank, measured vs floor
+        for r in wl.get("ranks") or []:
+            bad = next((s for s in r.get("steps", []) if s.get("ok") is False), None)
+            if bad:
+                e["first_failed"] = {"rank": r.get("rank"), **{k: bad[k] for k in
+                                     ("name", "tflops", "min_tflops", "gbps", "min_gbps", "busbw_gbps",
+                                      "min_busbw_gbps", "peer_read_gbps", "min_peer_read_gbps", "counter_gate",
+                                      "error") if k in bad}}
+                if "error" in e["first_failed"]:
+                    e["first_failed"]["error"] = str(e["first_failed"]["error"])[:160]
+                break
+        fp = wl.get("fabric_problems") or []
+        if fp:
+            e["fabric_problems"] = len(fp)
+            e["fabric_problem_first"] = str(fp[0])[:160]
+        cp = wl.get("coverage_problems") or []
+        if cp:
+            e["coverage_problems"] = len(cp)
+    msgs = {step: str(rec.get("message", ""))[:120] for step, rec in recs.items() if step != "workload"}
+    if msgs:
+        e["step_messages"] = dict(list(msgs.items())[:3])
+    return e
+
+
+def failure_line(args, n_gpus: int, fake_gpu, err: dict, results: list, warm: list, elapsed: float,
+                 detail: str | None = None) -> dict:
+    """The JSON line of a run whose bring-up failed: ``value`` null, a compact
+    ``error`` object (:func:`error_summary`) and the summaries of what the run
+    measured before and after it; the records, the traceback and every step's
+    critical path are in the detail file."""
     ttr = [r["time_to_ready_s"] for r in results]
+    cps = [critical_path(r) for r in results]
+    cfg = {
+        "model": MODEL, "global_batch": n_gpus, "seq_len": 0, "parallelism": f"dp{n_gpus}",
+        "detail": detail,
+        "ttr_s": dist_summary(ttr),
+        "time_to_ready_s": [round(x, 3) for x in ttr][:40],
+        "warmup_time_to_ready_s": [round(r["time_to_ready_s"], 3) for r in warm][:10],
+        "slow_steps": slow_summary(slow_steps(cps)),
+        "collectives": collectives_summary(err.get("collectives")),
+    }
     return {
         "metric": METRIC, "value": None, "unit": "s", "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / max(1, len(results)) * 1000, 2) if results else None,
         "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic" + (" (simulated GPUs: no GPU present)" if fake_gpu else ""),
-        "error": e,
-        "config": {
-            "model": "amd-gpu-operator ClusterPolicy bring-up (reference --set flags) + HIP/MFMA/RCCL validator",
-            "global_batch": n_gpus, "seq_len": 0, "parallelism": f"dp{n_gpus}",
-            "time_to_ready_s": [round(x, 4) for x in ttr],
-            "warmup_time_to_ready_s": [round(r["time_to_ready_s"], 4) for r in warm],
-            "critical_path": [critical_path(r) for r in results],
-            "collectives": err.get("collectives"),
-        },
+        "error": error_summary(err),
+        "config": {k: v for k, v in cfg.items() if v is not None},
     }
+
+
+def success_line(args, n_gpus: int, fake_gpu, results: list, warm: list, compare: list, other: str,
+                 elapsed: float, kfd_held: bool, detail: str | None) -> dict:
+    """The headline JSON line (module docstring): value = mean time-to-Ready of
+    the timed bring-ups; config = summaries only (LINE_BUDGET)."""
+    from amdgpu_operator.nodeenv import NodeEnv
+
+    ttr = [r["time_to_ready_s"] for r in results]
+    mean_ttr = sum(ttr) / len(ttr)
+    vis = [r["allocatable_visible_s"] for r in results]
+    cps = [critical_path(r) for r in results]
+    last = results[-1]
+    holders = [r["kfd_holders"] for r in results if r.get("kfd_holders")]
+    cfg = {
+        "model": MODEL, "global_batch": n_gpus, "seq_len": 0, "parallelism": f"dp{n_gpus}",
+        "allocatable_amd_com_gpu": last["allocatable"],
+        "detail": detail,
+        # the validator's Ready (`value`) over the timed bring-ups
+        "ttr_s": dist_summary(ttr),
+        "time_to_ready_s": [round(x, 3) for x in ttr] if len(ttr) <= 40 else None,
+        # the other half of the metric: allocatable amd.com/gpu in Node.status
+        # (README.md:122), on the kubelet's status tick
+        "allocatable_visible_s": {"mean": round(sum(vis) / len(vis), 3),
+                                  "p95": round(sorted(vis)[min(len(vis) - 1, int(0.95 * len(vis)))], 3)},
+        "kubelet_node_status_s": args.kubelet_status_s,
+        "validation_poll_s": NodeEnv.poll_s if args.agent_poll_s is None else args.agent_poll_s,
+        "slow_steps": slow_summary(slow_steps(cps)),
+        # processes of the bring-up's own tree holding /dev/kfd at each timed step's start and at its
+        # Ready (max over steps; who they were: the detail file), and the host's KFD process count
+        "kfd_holders": {"start_max": max(len(h.get("start") or []) for h in holders),
+                        "ready_max": max(len(h.get("ready") or []) for h in holders),
+                        "host_procs_max": max((r.get("settle") or {}).get("kfd_procs") or 0 for r in results)}
+        if holders else None,
+        "rates": rates_summary(last),
+        "operand_mode": args.mode,
+        # the harness itself never held a GPU context (no /dev/kfd descriptor)
+        "harness_holds_kfd": kfd_held,
+        # BASELINE config 5 after the last timed bring-up (not part of `value`)
+        "pod_workload": pod_workload_summary(last.get("pod_workload")),
+        # SURVEY §5.8 after the last timed bring-up (not part of `value`)
+        "collectives": collectives_summary(last.get("collectives")),
+        "other_mode_time_to_ready_s": {"mode": other, "s": [round(r["time_to_ready_s"], 3) for r in compare]}
+        if compare else None,
+    }
+    return {
+        "metric": METRIC,
+        "value": round(mean_ttr, 4),
+        "unit": "s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1000, 2),
+        "higher_is_better": False,
+        "scaling": "weak",
+        "vs_baseline": round(mean_ttr / BASELINE_TTR_S, 6),
+        "dtype": "bf16",
+        "data": "synthetic" + (" (simulated GPUs: no GPU present)" if fake_gpu else ""),
+        "config": {k: v for k, v in cfg.items() if v is not None},
+    }
+
+
+def route_logs(detail_path: str, rank: int) -> str | None:
+    """The ``amdgpu`` loggers of this process (the simulated cluster's pod
+    failures with their operands' tracebacks, ...) into
+    ``<detail>.rank<r>.log``."""
+    import logging
+
+    path = f"{os.path.splitext(detail_path)[0]}.rank{rank}.log"
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        h = logging.FileHandler(path, mode="w")
+    except OSError:
+        return None
+    h.setFormatter(logging.Formatter("%(asctime)s %(levelname)s %(name)s %(message)s"))
+    root = logging.getLogger("amdgpu")
+    root.handlers[:] = [h]
+    root.setLevel(logging.INFO)
+    root.propagate = False
+    return path
+
+
+class Progress:
+    """A few stderr lines per run: one at each phase's end and at most one a
+    minute within a phase (the caller's silence watchdog), so the JSON line
+    stays inside the driver's tail."""
+
+    def __init__(self, every_s: float = 60.0):
+        self.every_s = every_s
+        self.last = time.monotonic()
+
+    def step(self, phase: str, i: int, n: int, force: bool = False) -> None:
+        now = time.monotonic()
+        if force or i == n or now - self.last >= self.every_s:
+            self.last = now
+            print(f"bench: {phase} {i}/{n}", file=sys.stderr, flush=True)
 
 
 def main():
@@ -680,6 +1052,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.gpus != world:
         args.gpus = world
+    # the operator's and the simulated cluster's log records go to a file next to
+    # the detail file: on stderr they would push the JSON line out of the driver's tail
+    detail_path = args.detail or default_detail_path(args.gpus)
+    log_path = route_logs(detail_path, rank)
+    os.environ.setdefault("TORCH_CPP_LOG_LEVEL", "ERROR")  # c10d's per-rank socket warnings
     has_gpu = gpu_available(args.sysfs_root or "/")
     fake_gpu = args.fake_gpu or args.fake_gpu_procs or not has_gpu
     if fake_gpu and args.fake_gpu_procs:
@@ -694,10 +1071,9 @@ def main():
         group = dist.group.WORLD
     del local_rank  # GPU d's processes run on rank d % world (launcher), children of the harness
 
-    from amdgpu_operator.nodeenv import NodeEnv
     from amdgpu_operator.parallel.launcher import DistributedLauncher
 
-    launcher = DistributedLauncher(rank, world, group) if world > 1 else None
+    launcher =DistributedLauncher(rank, world, group) if world > 1 else None
     n_gpus = args.gpus
     if not fake_gpu and rank == 0:
         from amdgpu_operator.discovery import topology
@@ -718,28 +1094,30 @@ def main():
 
         tools = ToolWatch(os.path.join(workdir, "gpu-tools.jsonl"))
 
+    progress = Progress()
+
     def driver_thread(n_steps: int, out: list, mode: str):
         import faulthandler
 
         faulthandler.dump_traceback_later(args.timeout + 60, exit=False)  # stacks if a step wedges
         i = 0
+        label = "timed" if out is results else "warm-up" if out is warm else "compare"
         try:
             for i in range(n_steps):
                 pods = out is results and i == n_steps - 1 and not args.no_pod_workload
                 out.append(one_bring_up(args, n_gpus, launcher, workdir, fake_gpu, mode, pods))
-                # progress on stderr (a run that prints nothing for minutes looks hung to its caller)
-                print(f"bench: {'timed' if out is results else 'warm-up'} bring-up {i + 1}/{n_steps} done",
-                      file=sys.stderr, flush=True)
+                # progress on stderr: a run that prints nothing for minutes looks hung to its
+                # caller, and every line also takes room from the JSON line in the driver's tail
+                progress.step(label, i + 1, n_steps)
         except Exception as e:  # noqa: BLE001
             import traceback
 
-            err = {"phase": "timed" if out is results else "warm-up" if out is warm else "compare",
-                   "bring_up": i + 1, "type": type(e).__name__, "message": str(e)[:2000]}
+            err = {"phase": label, "bring_up": i + 1, "type": type(e).__name__, "message": str(e)[:2000],
+                   "traceback": traceback.format_exc()[-6000:]}
             if isinstance(e, BringUpFailed):
                 err.update(records=e.records, elapsed_s=round(e.elapsed_s, 4), harness=getattr(e, "partial", None))
-            else:
-                err["traceback"] = traceback.format_exc()[-3000:]
-            print(f"bench: bring-up {i + 1} ({err['phase']}) failed: {e}", file=sys.stderr, flush=True)
+            print(f"bench: {label} bring-up {i + 1} failed: {type(e).__name__}: {str(e)[:200]}", file=sys.stderr,
+                  flush=True)
             if not args.no_sweep:
                 # what the fabric does, measured, next to the failure (the floors it failed are in the records)
                 try:
@@ -811,84 +1189,34 @@ def main():
         for r in results + warm:  # GPU tools of other parties alive during each timed bring-up
             r["foreign_gpu_tools"] = tools.overlapping(r["t0_wall"], r["t0_wall"] + r["time_to_ready_s"])
     rc = 1 if errors else 0  # every rank: the run failed
-    if rank == 0 and errors:
-        out = failure_line(args, n_gpus, fake_gpu, errors[0], results, warm, elapsed)
-        print(json.dumps(out))
-        print(errors[0].get("traceback") or errors[0]["message"], file=sys.stderr)
-        if args.detail:
-            with open(args.detail, "w") as f:
-                json.dump({"summary": out, "steps": results, "warmup": warm, "errors": errors}, f, indent=1,
-                          default=str)
-    elif rank == 0:
-        ttr = [r["time_to_ready_s"] for r in results]
-        mean_ttr = sum(ttr) / len(ttr)
-        alloc = results[-1]["allocatable"]
-        vis = sorted(r["allocatable_visible_s"] for r in results)
-        out = {
-            "metric": METRIC,
-            "value": round(mean_ttr, 4),
-            "unit": "s",
-            "n_gpus": n_gpus,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1000, 2),
-            "higher_is_better": False,
-            "scaling": "weak",
-            "vs_baseline": round(mean_ttr / BASELINE_TTR_S, 6),
-            "dtype": "bf16",
-            "data": "synthetic" + (" (simulated GPUs: no GPU present)" if fake_gpu else ""),
-            "config": {
-                "model": "amd-gpu-operator ClusterPolicy bring-up (reference --set flags) + HIP/MFMA/RCCL validator",
-                "global_batch": n_gpus,
-                "seq_len": 0,
-                "parallelism": f"dp{n_gpus}",
-                "allocatable_amd_com_gpu": alloc,
-                "time_to_ready_s": [round(x, 4) for x in ttr],
-                "time_to_ready_min_s": round(min(ttr), 4),
-                # both halves of the metric: the validator's Ready (`value`) and the
-                # allocatable GPUs in Node.status (README.md:122), on the kubelet's status tick
-                "allocatable_visible_mean_s": round(sum(vis) / len(vis), 3),
-                "allocatable_visible_p95_s": round(vis[min(len(vis) - 1, int(0.95 * len(vis)))], 3),
-                "allocatable_visible_s": [round(r["allocatable_visible_s"], 3) for r in results],
-                "time_to_ready_median_s": round(sorted(ttr)[len(ttr) // 2], 4),
-                "kubelet_node_status_s": args.kubelet_status_s,
-                "validation_poll_s": NodeEnv.poll_s if args.agent_poll_s is None else args.agent_poll_s,
-                "gemm_tflops_per_gpu": results[-1]["gemm_tflops"],
-                "fp8_gemm_tflops_per_gpu": results[-1]["fp8_tflops"],
-                "fp8_counter_gate": results[-1]["fp8_counter_gate"],
-                "hbm_gbps_per_gpu": results[-1]["hbm_gbps"],
-                "rccl_busbw_gbps": results[-1]["rccl_busbw_gbps"],
-                "rccl_comm_init_s": results[-1]["rccl_comm_init_s"],
-                "counter_gate": results[-1]["gemm_counter_gate"],
-                "operand_mode": args.mode,
-                # the harness itself never held a GPU context (no /dev/kfd descriptor)
-                "harness_holds_kfd": kfd_held,
-                # per operand container of the last timed bring-up (process mode)
-                "operands": results[-1].get("operands"),
-                # BASELINE config 5 after the last timed bring-up: N pods x 1 GPU, 1 pod x N (and 2 x 4 at N = 8),
-                # each a random-init bf16 GEMM on the hand-written kernel of its GPUs (not part of `value`)
-                "pod_workload": results[-1].get("pod_workload"),
-                # SURVEY §5.8 after the last timed bring-up: RCCL all-reduce / all-gather / reduce-scatter,
-                # 8 B ... 1 GiB (algBW, busBW, latency per size, slowest rank), every xGMI link read on its
-                # own, and the Ready gate's floors next to them (not part of `value`)
-                "collectives": results[-1].get("collectives"),
-                # every timed bring-up's critical path (s after ClusterPolicy creation; validator
-                # process and plugin-pod steps; harness stall / GC / CPU throttling; GPU tools of
-                # other parties that overlapped it)
-                "critical_path": [critical_path(r) for r in results],
-                # the bring-ups above 1.3 x the median, each with the critical-path part that grew most
-                "slow_steps": slow_steps([critical_path(r) for r in results]),
-                f"{other}_mode_time_to_ready_s": [round(r["time_to_ready_s"], 4) for r in compare],
-            },
-        }
-        print(json.dumps(out))
-        if args.detail:
-            with open(args.detail, "w") as f:
-                json.dump({"summary": out, "steps": results, "warmup": warm, "compare": compare}, f, indent=1)
+    if rank == 0:
+        # everything per step / rank / size / link goes to the detail file, the
+        # line names it; the line is the last thing this process prints
+        cps = [critical_path(r) for r in results]
+        if errors:
+            out = failure_line(args, n_gpus, fake_gpu, errors[0], results, warm, elapsed, detail_path)
+            detail = {"summary": out, "errors": errors, "critical_path": cps, "steps": results, "warmup": warm}
+        else:
+            out = success_line(args, n_gpus, fake_gpu, results, warm, compare, other, elapsed, kfd_held, detail_path)
+            detail = {"summary": out, "critical_path": cps, "slow_steps": slow_steps(cps),
+                      "collectives": results[-1].get("collectives"), "pod_workload": results[-1].get("pod_workload"),
+                      "operands": results[-1].get("operands"),
+                      "kfd_holders": [r.get("kfd_holders") for r in results],
+                      "steps": results, "warmup": warm, "compare": compare}
+        detail["log"] = log_path
+        if write_detail(detail_path, detail) is None:
+            out["config"]["detail"] = None
+        sys.stderr.flush()
+        print(fit_line(out), flush=True)
     shutil.rmtree(workdir, ignore_errors=True)
     if world > 1:
+        dist.barrier()  # rank 0 has printed the line
         dist.destroy_process_group()
-    if rc:
+    if rc and rank == 0:
+        # the other ranks exit 0 first: torchrun then reports one failed rank
+        # (not eight, nor SIGTERMs to the rest) after the line
+        if world > 1:
+            time.sleep(1.0)
         raise SystemExit(rc)
 
 

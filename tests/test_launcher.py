@@ -22,13 +22,13 @@ def test_processes_run_on_owner_rank(nproc, port):
 
 
 @pytest.mark.parametrize("nproc,warmup,port,mode", [(2, 0, 29613, "thread"), (8, 1, 29614, "process")])
-def test_bench_ranks_with_stand_in_validators(nproc, warmup, port, mode):
+def test_bench_ranks_with_stand_in_validators(nproc, warmup, port, mode, tmp_path):
     """The driver's scaling launch (torchrun, one rank per GPU) on CPU: 8 ranks,
     a warm-up phase and the other-mode comparison exercise the launcher
     hand-over between phases; thread mode routes every GPU process through
     the rank that owns the GPU, process mode runs the operands as processes."""
     p = _torchrun(nproc, "bench.py", "--gpus", str(nproc), "--steps", "1", "--warmup", str(warmup),
-                  "--fake-gpu-procs", "--mode", mode, "--compare", "1", port=port)
+                  "--fake-gpu-procs", "--mode", mode, "--compare", "1", "--detail", str(tmp_path / "detail.json"), port=port)
     assert p.returncode == 0, p.stderr[-3000:]
     import json
 
@@ -38,7 +38,9 @@ def test_bench_ranks_with_stand_in_validators(nproc, warmup, port, mode):
     assert out["n_gpus"] == nproc and out["config"]["allocatable_amd_com_gpu"] == nproc
     assert out["config"]["parallelism"] == f"dp{nproc}" and out["steps"] == 1 and out["warmup"] == warmup
     other = "thread" if mode == "process" else "process"
-    assert out["config"]["operand_mode"] == mode and len(out["config"][f"{other}_mode_time_to_ready_s"]) == 1
+    assert out["config"]["operand_mode"] == mode
+    assert out["config"]["other_mode_time_to_ready_s"]["mode"] == other
+    assert len(out["config"]["other_mode_time_to_ready_s"]["s"]) == 1
 
 
 def test_run_local_takes_the_report_before_the_exit():
@@ -75,12 +77,21 @@ def test_bench_n8_stays_within_the_gpu_process_budget(tmp_path):
     env = dict(os.environ, AMDGPU_FAKE_GPU_PROC_LOG=log_dir)
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
                         "--master-addr", "127.0.0.1", "--master-port=29615", "bench.py", "--gpus", "8", "--steps", "1",
-                        "--warmup", "0", "--fake-gpu-procs", "--mode", "process", "--compare", "0"],
+                        "--warmup", "0", "--fake-gpu-procs", "--mode", "process", "--compare", "0",
+                        "--detail", str(tmp_path / "detail.json")],
                        capture_output=True, text=True, timeout=240, cwd=os.path.dirname(HERE), env=env)
     assert p.returncode == 0, p.stderr[-3000:]
-    out = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0])
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][0]
+    # the driver's tail (~8.9 KB of stdout + stderr) holds the line at N = 8, with
+    # room for 40 steps' time-to-Ready list (7 bytes each) on top of this 1-step run
+    assert len(line) + 40 * 7 <= 3000, len(line)
+    assert len(p.stdout) + len(p.stderr) < 8000
+    out = json.loads(line)
     assert out["config"]["allocatable_amd_com_gpu"] == 8 and out["config"]["harness_holds_kfd"] is False
-    pw = out["config"]["pod_workload"]  # config 5 after Ready: 8 x 1 GPU, 1 x 8, 2 x 4
+    with open(out["config"]["detail"]) as f:
+        detail = json.load(f)
+    assert out["config"]["pod_workload"]["ok"] and out["config"]["pod_workload"]["pods"] == 11
+    pw = detail["pod_workload"]  # config 5 after Ready: 8 x 1 GPU, 1 x 8, 2 x 4
     assert pw["pods"] == 11 and pw["all_succeeded"] and pw["single_gpu_pods_distinct_devices"]
     assert pw["two_halves_numa_local"] and pw["two_halves_disjoint"]
     peak, roles = _peak_concurrency(log_dir)
@@ -88,7 +99,10 @@ def test_bench_n8_stays_within_the_gpu_process_budget(tmp_path):
     assert roles == {"validator": 16, "pod": 1 + 11}, roles  # the plugin-validation pod + the workload's pods
     assert peak <= 16, peak
     # the collective curve at world 8 after the timed bring-up
-    col = out["config"]["collectives"]
+    cs = out["config"]["collectives"]
+    assert cs["ok"] and cs["world"] == 8 and cs["links_below_floor"] == 0 and cs["min_allreduce_ratio"] > 1
+    assert cs["peak_busbw_gbps"] >= cs["busbw_256MiB_gbps"] > cs["busbw_1MiB_gbps"] > 0
+    col = detail["collectives"]
     assert col["ok"] and col["world"] == 8
     for op in ("allreduce", "allgather", "reducescatter"):
         rows = col["ops"][op]
@@ -99,4 +113,4 @@ def test_bench_n8_stays_within_the_gpu_process_budget(tmp_path):
     assert len(links) == 8 and all(links[r][r] is None and all(links[r][p] for p in range(8) if p != r) for r in range(8))
     ff = col["fabric_floors"]
     assert ff["link_gbps_per_rank"] == [532.0] * 8 and ff["min_allreduce_ratio"] > 1 and ff["links_below_floor"] == []
-    assert len(out["config"]["critical_path"]) == 1
+    assert len(detail["critical_path"]) == 1
