@@ -159,6 +159,8 @@ class DevicePluginSpec(Operand):
     passDeviceSpecs: bool = True
     cdiAnnotations: bool = False
     healthPollMs: int = 1000
+    # open the amd-smi health event client once the node is validated (not beside the validator)
+    healthStart: Literal["afterValidation", "immediate"] = "afterValidation"
     config: DevicePluginConfigRef = Field(default_factory=DevicePluginConfigRef)
 
 
@@ -184,6 +186,8 @@ class MetricsExporterSpec(Operand):
     intervalSeconds: float = 1.0
     podAttribution: bool = True
     dcgmNames: bool = False  # also emit DCGM_FI_DEV_* series for existing dashboards
+    # the XID-equivalent series (amd-smi reset / VM-fault / thermal events, ECC / xGMI deltas)
+    healthEvents: bool = True
     serviceMonitor: ServiceMonitor = Field(default_factory=ServiceMonitor)
     config: MetricsConfigRef = Field(default_factory=lambda: MetricsConfigRef())
 

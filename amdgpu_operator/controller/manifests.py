@@ -413,7 +413,8 @@ def state_device_plugin(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     image = p.ref("amd-device-plugin")
     args = ["device-plugin", "--resource-name", p.resourceName, "--partition-strategy", p.partitionStrategy,
             "--health-poll-ms", str(p.healthPollMs), "--device-id-strategy", p.deviceIDStrategy,
-            "--device-list-strategy", ",".join(p.deviceListStrategy)]
+            "--device-list-strategy", ",".join(p.deviceListStrategy),
+            "--health-start", "after-validation" if p.healthStart == "afterValidation" else "immediate"]
     if spec.toolkit.enabled and spec.toolkit.cdi.enabled and p.cdiAnnotations:
         args.append("--cdi")
     if not p.passDeviceSpecs:
@@ -479,6 +480,8 @@ def state_metrics_exporter(spec: ClusterPolicySpec, ns: str, owner) -> list[dict
         args.append("--pod-attribution")
     if m.dcgmNames:
         args.append("--dcgm-names")
+    if not m.healthEvents:
+        args.append("--no-health-events")
     rbac = []
     if m.config.name:
         args += ["--metrics-config-map", f"{ns}/{m.config.name}/{m.config.key}"]

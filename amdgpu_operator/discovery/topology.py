@@ -11,6 +11,7 @@ queries behind ``nvidia-smi`` (/root/reference/README.md:152,158-167).
 from __future__ import annotations
 
 import ctypes
+import threading
 from ..utils.record import asdict, field, record
 
 from .. import native
@@ -405,3 +406,105 @@ class HealthWatcher:
 
     def close(self) -> None:
         self._lib.at_health_stop()
+
+
+class HealthHub:
+    """One N6 event client per process, fanned out to every subscriber.
+
+    amd-smi delivers each event notification to one reader, and N6's counter
+    deltas are computed against one baseline, so two watchers in a process
+    (the device plugin's health loop and the exporter's XID-equivalent
+    series, both threads of one process in the simulated cluster's thread
+    mode) would split the stream between them.  The hub owns the only
+    :class:`HealthWatcher`, polls it on one thread, and queues every event
+    for each :class:`HealthSubscription`; the watcher closes when the last
+    subscription does.  ``factory`` builds the watcher (tests pass a fake)."""
+
+    _lock = threading.Lock()
+    _inst: "HealthHub | None" = None
+
+    def __init__(self, factory):
+        self._watcher = factory()
+        self._subs: list[HealthSubscription] = []
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="amdgpu-health-hub", daemon=True)
+        self._thread.start()
+
+    @classmethod
+    def subscribe(cls, factory=None) -> "HealthSubscription":
+        """A new subscription on the process's hub (started on first use;
+        raises what the watcher raises when amd-smi is unavailable)."""
+        with cls._lock:
+            if cls._inst is None:
+                cls._inst = HealthHub(factory or HealthWatcher)
+            sub = HealthSubscription(cls._inst)
+            cls._inst._subs.append(sub)
+            return sub
+
+    def _release(self, sub: "HealthSubscription") -> None:
+        with HealthHub._lock:
+            if sub in self._subs:
+                self._subs.remove(sub)
+            if self._subs or HealthHub._inst is not self:
+                return
+            HealthHub._inst = None
+        self._stop.set()
+        self._thread.join(timeout=5.0)
+        try:
+            self._watcher.close()
+        except Exception:  # noqa: BLE001 - closing a watcher of a vanished device
+            pass
+
+    def _run(self) -> None:
+        while not self._stop.is_set():
+            try:
+                events = self._watcher.poll(200)
+            except Exception as e:  # noqa: BLE001 - handed to every subscriber's poll
+                events = e
+            with HealthHub._lock:
+                subs = list(self._subs)
+            if isinstance(events, Exception):
+                for s in subs:
+                    s._q.put(events)
+                self._stop.wait(1.0)
+                continue
+            if events:
+                for s in subs:
+                    s._q.put(list(events))
+
+
+class HealthSubscription:
+    """A subscriber's view of the process's :class:`HealthHub`: ``poll``
+    has :meth:`HealthWatcher.poll`'s signature and returns every event since
+    the previous call (waiting up to ``timeout_ms`` for the first)."""
+
+    def __init__(self, hub: HealthHub):
+        import queue
+
+        self._hub = hub
+        self._q: "queue.Queue[list[HealthEvent] | Exception]" = queue.Queue()
+        self._closed = False
+
+    def poll(self, timeout_ms: int = 1000) -> list[HealthEvent]:
+        import queue
+
+        out: list[HealthEvent] = []
+        try:
+            item = self._q.get(timeout=max(0.0, timeout_ms / 1000.0))
+        except queue.Empty:
+            return out
+        while True:
+            if isinstance(item, Exception):
+                if out:
+                    return out
+                raise item
+            out.extend(item)
+            try:
+                item = self._q.get_nowait()
+            except queue.Empty:
+                return out
+
+    def close(self) -> None:
+        if not self._closed:
+            self._closed = True
+            self._hub._release(self)

@@ -28,6 +28,10 @@ amd_gpu_xgmi_{read,write}_bytes_total (NVLink traffic: per-GPU xGMI bytes)
 amd_gpu_pcie_replay_total             DCGM_FI_DEV_PCIE_REPLAY_COUNTER
 amd_gpu_pcie_link_width               DCGM_FI_DEV_PCIE_LINK_WIDTH
 amd_gpu_throttle_*_residency_total    (DCGM_FI_DEV_*_VIOLATION analogs)
+amd_gpu_last_critical_event_code      DCGM_FI_DEV_XID_ERRORS (last critical
+                                      N6 event; :class:`HealthCounters`)
+amd_gpu_reset_total, _vm_fault_total, (XID-class events, per GPU)
+_*_events_total, _health_critical
 ====================================  ==================================
 
 Metric selection (``--metrics-config`` / ``dcgmExporter.config``): the
@@ -103,10 +107,101 @@ FIELDS = [
     ("amd_gpu_throttle_status", "throttle_status", "gauge", "Throttle status bitmask", None, 1.0),
     ("amd_gpu_vram_max_bandwidth_gbps", "vram_max_bandwidth_gbps", "gauge", "HBM bandwidth at max memory clock (GB/s)",
      None, 1.0),
+    # the XID equivalent (:class:`HealthCounters`): N6 health events per GPU
+    ("amd_gpu_reset_total", "health_gpu_pre_reset", "counter", "GPU resets (amd-smi GPU pre-reset events)", None, 1.0),
+    ("amd_gpu_reset_recovered_total", "health_gpu_post_reset", "counter",
+     "GPU reset recoveries (amd-smi GPU post-reset events)", None, 1.0),
+    ("amd_gpu_vm_fault_total", "health_vm_fault", "counter", "GPU VM (page) faults (amd-smi events)", None, 1.0),
+    ("amd_gpu_thermal_throttle_events_total", "health_thermal_throttle", "counter",
+     "Thermal throttle events (amd-smi events)", None, 1.0),
+    ("amd_gpu_ecc_uncorrectable_events_total", "health_ecc_uncorrectable", "counter",
+     "Polls that found new uncorrectable ECC errors", None, 1.0),
+    ("amd_gpu_xgmi_link_error_events_total", "health_xgmi_link_error", "counter",
+     "Polls that found more xGMI links in error", None, 1.0),
+    ("amd_gpu_device_lost_events_total", "health_device_lost", "counter", "The GPU stopped answering amd-smi",
+     None, 1.0),
+    ("amd_gpu_bad_page_events_total", "health_bad_pages", "counter", "Polls that found newly retired HBM pages",
+     None, 1.0),
+    ("amd_gpu_health_critical", "health_critical", "gauge",
+     "A critical health event (reset, uncorrectable ECC, xGMI link error, device lost) and no recovery since",
+     None, 1.0),
+    ("amd_gpu_last_critical_event_code", "health_last_critical_code", "gauge",
+     "Code of the last critical health event (3 GPU reset, 100 uncorrectable ECC, 101 xGMI link error, "
+     "102 device lost; 0 none)", "DCGM_FI_DEV_XID_ERRORS", 1.0),
 ]
 # DCGM fields with no MI355X source: accepted in a metrics CSV, reported as unsupported
-DCGM_UNSUPPORTED = {"DCGM_FI_DEV_ENC_UTIL", "DCGM_FI_DEV_DEC_UTIL", "DCGM_FI_DEV_XID_ERRORS",
+DCGM_UNSUPPORTED = {"DCGM_FI_DEV_ENC_UTIL", "DCGM_FI_DEV_DEC_UTIL",
                     "DCGM_FI_DEV_VGPU_LICENSE_STATUS", "DCGM_FI_DEV_NVLINK_BANDWIDTH_TOTAL"}
+HEALTH_KINDS = ("gpu_pre_reset", "gpu_post_reset", "vm_fault", "thermal_throttle", "ecc_uncorrectable",
+                "xgmi_link_error", "device_lost", "bad_pages")
+# N6 event kinds (native/include/amdgpu_topo.h AT_EV_*), the code the XID alias carries
+HEALTH_CODES = {"vm_fault": 1, "thermal_throttle": 2, "gpu_pre_reset": 3, "gpu_post_reset": 4,
+                "ecc_uncorrectable": 100, "xgmi_link_error": 101, "device_lost": 102, "bad_pages": 103}
+
+
+class HealthCounters:
+    """The exporter's XID-equivalent series: N6's health events
+    (native/topology/health.cpp - amd-smi GPU reset, VM-fault and thermal
+    notifications, and the ECC / xGMI / bad-page / device-lost deltas of its
+    polls) counted per GPU, a ``health_critical`` gauge that a critical event
+    raises and a reset recovery (post-reset) clears, and the last critical
+    event's code, which the ``DCGM_FI_DEV_XID_ERRORS`` alias carries as the
+    dcgm-exporter's XID gauge carries the last XID.  The reference's exporter
+    "collects GPU metrics for monitoring" (/root/reference/README.md:204,213);
+    GPU alerting keys on the XID series.
+
+    ``poll`` is a :class:`~amdgpu_operator.discovery.topology.HealthSubscription`
+    poll (the process's one amd-smi event client, shared with the device
+    plugin's health loop when both run in one process)."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._by_gpu: dict[int, dict] = {}
+        self.unattributed = 0
+        self.live = False
+        self.events = 0
+
+    def ingest(self, events) -> None:
+        with self._lock:
+            for ev in events:
+                self.events += 1
+                if ev.index is None or ev.index < 0:
+                    self.unattributed += 1
+                    continue
+                g = self._by_gpu.setdefault(ev.index, {})
+                if ev.kind in HEALTH_KINDS:
+                    g[f"health_{ev.kind}"] = g.get(f"health_{ev.kind}", 0) + 1
+                if ev.critical:
+                    g["health_critical"] = 1
+                    g["health_last_critical_code"] = HEALTH_CODES.get(ev.kind, 0)
+                    g["health_last_message"] = str(ev.message)[:200]
+                elif ev.kind == "gpu_post_reset":
+                    g["health_critical"] = 0
+
+    def values(self, index: int) -> dict:
+        """Every health field of one GPU (0 where nothing happened)."""
+        with self._lock:
+            g = dict(self._by_gpu.get(index, {}))
+        out = {f"health_{k}": float(g.get(f"health_{k}", 0)) for k in HEALTH_KINDS}
+        out["health_critical"] = float(g.get("health_critical", 0))
+        out["health_last_critical_code"] = float(g.get("health_last_critical_code", 0))
+        return out
+
+    def run(self, poll, stop: threading.Event, timeout_ms: int = 500) -> None:
+        """Feed from ``poll`` until ``stop``."""
+        self.live = True
+        try:
+            while not stop.is_set():
+                try:
+                    evs = poll(timeout_ms)
+                except Exception as e:  # noqa: BLE001 - keep serving the counts so far
+                    log.warning("health events: %s", e)
+                    stop.wait(1.0)
+                    continue
+                if evs:
+                    self.ingest(evs)
+        finally:
+            self.live = False
 
 
 @dataclass(frozen=True)
@@ -331,8 +426,10 @@ def device_id_resolver(sysfs_root: str):
 
 class MetricsExporter:
     def __init__(self, source, node_name: str = "", interval_s: float = 1.0, attribution: PodAttribution | None = None,
-                 dcgm_names: bool = False, selection: list[Series] | None = None):
+                 dcgm_names: bool = False, selection: list[Series] | None = None,
+                 health: HealthCounters | None = None):
         self.source = source
+        self.health = health  # the XID-equivalent series (None: not exported)
         self.selection = selection  # None = every field (plus DCGM aliases with dcgm_names)
         self.node = node_name
         self.interval = interval_s
@@ -385,6 +482,9 @@ class MetricsExporter:
     def render(self) -> str:
         with self._lock:
             snap, pods = list(self._snapshot), dict(self._pods)
+        if self.health is not None:
+            snap = [Sample(s.index, s.bdf, s.uuid, s.product, {**s.values, **self.health.values(s.index)})
+                    for s in snap]
         lines = []
         for ser in self._series():
             rows = [s for s in snap if ser.field in s.values]
@@ -411,6 +511,15 @@ class MetricsExporter:
             "# TYPE amd_gpu_exporter_errors_total counter",
             f"amd_gpu_exporter_errors_total {self.errors}",
         ]
+        if self.health is not None:
+            lines += [
+                "# HELP amd_gpu_exporter_health_events_live The amd-smi health event stream is being read",
+                "# TYPE amd_gpu_exporter_health_events_live gauge",
+                f"amd_gpu_exporter_health_events_live {int(self.health.live)}",
+                "# HELP amd_gpu_health_unattributed_events_total Health events naming no known GPU",
+                "# TYPE amd_gpu_health_unattributed_events_total counter",
+                f"amd_gpu_health_unattributed_events_total {self.health.unattributed}",
+            ]
         return "\n".join(lines) + "\n"
 
 

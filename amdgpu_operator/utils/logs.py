@@ -67,10 +67,27 @@ def _json_formatter(logging):
     return JsonFormatter()
 
 
+def _stderr_handler(logging):
+    """A StreamHandler on whatever ``sys.stderr`` is at each record (like
+    logging's last-resort handler), not on the stream it was created with: a
+    replaced stderr (a test's capture, a daemon's redirect) that was since
+    closed would otherwise fail every later record of a long-lived thread."""
+
+    class StderrHandler(logging.StreamHandler):
+        def __init__(self):
+            logging.Handler.__init__(self)
+
+        @property
+        def stream(self):
+            return sys.stderr
+
+    return StderrHandler()
+
+
 def _apply(logging, level: str | None, json_logs: bool | None) -> None:
     level = (level or os.environ.get("LOG_LEVEL", "info")).upper()
     json_logs = json_logs if json_logs is not None else os.environ.get("LOG_FORMAT", "json") == "json"
-    h = logging.StreamHandler(sys.stderr)
+    h = _stderr_handler(logging)
     h.setFormatter(_json_formatter(logging) if json_logs
                    else logging.Formatter("%(asctime)s %(levelname)s %(name)s %(message)s"))
     root = logging.getLogger("amdgpu")

@@ -35,3 +35,34 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+# threads of a gRPC server (rpc/wire.py ``<name>-accept``) or of a device
+# plugin's kubelet watch that a test started must be gone when it ends: a
+# leaked plugin re-registers with whatever kubelet socket appears later (and
+# logs into a closed stream), and under -n N it can reach another test's
+# kubelet through a shared temp dir
+_SERVER_THREADS = ("amdgpu-dp-watch", "amdgpu-dp-health", "amdgpu-health-hub")
+
+
+def _server_threads():
+    import threading
+
+    return {t for t in threading.enumerate()
+            if t.is_alive() and (t.name in _SERVER_THREADS or t.name.endswith("-accept"))}
+
+
+@pytest.fixture(autouse=True)
+def no_leaked_servers(request):
+    import time
+
+    before = _server_threads()
+    yield
+    deadline = time.monotonic() + 3.0
+    left = _server_threads() - before
+    while left and time.monotonic() < deadline:
+        time.sleep(0.02)
+        left = {t for t in left if t.is_alive()}
+    if left:
+        pytest.fail(f"{request.node.nodeid} left server threads running: {sorted(t.name for t in left)}",
+                    pytrace=False)

@@ -337,6 +337,44 @@ def test_metrics_exporter_live():
         src.close()
 
 
+def test_metrics_exporter_health_series_live():
+    """The XID-equivalent series on the MI355X: the exporter's amd-smi event
+    client (the process's one HealthHub watcher) initialises, every series
+    exists at 0 per GPU, and the stream reads as live."""
+    import threading
+    import time
+
+    from amdgpu_operator.discovery.topology import HealthHub
+    from amdgpu_operator.exporter.metrics import HealthCounters, MetricsExporter, SmiSource
+
+    src = SmiSource()
+    stop = threading.Event()
+    sub = HealthHub.subscribe()
+    sub2 = HealthHub.subscribe()  # a second consumer in the process shares the watcher
+    try:
+        assert sub._hub is sub2._hub
+        hc = HealthCounters()
+        th = threading.Thread(target=hc.run, args=(sub.poll, stop, 100), daemon=True)
+        th.start()
+        ex = MetricsExporter(src, "box", health=hc, dcgm_names=True)
+        ex.collect_once()
+        deadline = time.monotonic() + 5
+        while not hc.live and time.monotonic() < deadline:
+            time.sleep(0.01)
+        text = ex.render()
+        assert "amd_gpu_exporter_health_events_live 1" in text
+        for name in ("amd_gpu_reset_total", "amd_gpu_vm_fault_total", "amd_gpu_thermal_throttle_events_total",
+                     "amd_gpu_ecc_uncorrectable_events_total", "amd_gpu_health_critical", "DCGM_FI_DEV_XID_ERRORS"):
+            rows = [ln for ln in text.splitlines() if ln.startswith(name + "{")]
+            assert rows and all(ln.endswith(" 0") for ln in rows), (name, rows)
+    finally:
+        stop.set()
+        sub.close()
+        sub2.close()
+        src.close()
+    assert HealthHub._inst is None  # the last subscription closed the watcher
+
+
 @pytest.mark.parametrize("mode", ["local", "http", "process"])
 def test_sim_cluster_on_real_gpu(mode):
     """Bring-up on the MI355X; with ``http`` the operator and the operands
