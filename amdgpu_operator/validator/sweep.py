@@ -47,7 +47,10 @@ BUS_FACTOR = {"allreduce": lambda n: 2.0 * (n - 1) / n, "allgather": lambda n: (
 
 
 def sizes(min_bytes: int = 8, max_bytes: int = 1 << 30, factor: int = 4) -> list[int]:
-    """The message sizes (validator_main.cpp ``sweep_sizes``)."""
+    """The message sizes (validator_main.cpp ``sweep_sizes``, which accepts
+    factors 2 ... 1024)."""
+    if not 2 <= factor <= 1024 or min_bytes < 1:
+        raise ValueError(f"sweep factor must be in [2, 1024] (got {factor}) and min_bytes >= 1")
     out, b = [], min_bytes
     while b <= max_bytes:
         out.append(b)

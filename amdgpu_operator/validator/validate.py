@@ -457,7 +457,7 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     # the gated kernel processes (the binary does not link the SDK)
     # (the default AQL-packet gate needs no tool library: only --gate-mode sdk)
     sdk_gate = "--counter-gate" in args and _arg_value(args, "--gate-mode") == "sdk"
-    counter_env = gate_env() if sdk_gate else {}
+    counter_env = {**(gate_env() if sdk_gate else {}), **gate_lock_env(env)}
     rccl_single = "--rccl-single-gpu" in args  # validate.py's own flags, not the binary's
     separate = "--rccl-separate-process" in args
     require_links = "--require-xgmi-links" in args
@@ -495,7 +495,8 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
                          {**counter_env, **topology.visible_devices_env(devs, gpus)}))
             jobs.append((r, _with_steps(_drop_flag(args, "--counter-gate"), ["hip"] + ["xgmi"] * xgmi + ["rccl"])
                          + local + ["--expect-devices", "1"], run_id + "-rccl",
-                         {**thp_malloc_env(), **topology.visible_devices_env([devs[0], *others], gpus)}))
+                         {**thp_malloc_env(), **gate_lock_env(env),
+                          **topology.visible_devices_env([devs[0], *others], gpus)}))
             continue
         jenv = dict(counter_env)
         if run_rccl:
@@ -854,6 +855,19 @@ def _pod_results_dir(env: NodeEnv) -> str:
     return d
 
 
+# The counter gate's per-GPU lock files (native/include/gate_lock.h): the
+# validator holds a GPU's lock exclusively around each counted dispatch, and
+# the operator's other GPU work on it - the plugin-validation pod's check, the
+# validator's RCCL processes - holds it shared, so none of it lands in a
+# counted window.  They live in the pod-results hostPath, which the
+# plugin-validation pods already mount.
+GATE_LOCK_ENV = "AMDGPU_GATE_LOCK_DIR"
+
+
+def gate_lock_env(env: NodeEnv) -> dict:
+    return {GATE_LOCK_ENV: _pod_results_dir(env)}
+
+
 def _with_result_file(env: NodeEnv, pod: dict, flag: str) -> dict:
     """The pod writes its report into the node's validation directory too
     (``flag``: the check's option for it, published by rename): the
@@ -866,6 +880,7 @@ def _with_result_file(env: NodeEnv, pod: dict, flag: str) -> dict:
     name = pod["metadata"]["name"]
     ctr = pod["spec"]["containers"][0]
     ctr["args"] = list(ctr.get("args") or []) + [flag, os.path.join(d, f"{name}.json")]
+    ctr.setdefault("env", []).append({"name": GATE_LOCK_ENV, "value": d})  # the gate locks (gate_lock_env)
     ctr.setdefault("volumeMounts", []).append({"name": "pod-results", "mountPath": d})
     pod["spec"].setdefault("volumes", []).append({"name": "pod-results",
                                                    "hostPath": {"path": d, "type": "DirectoryOrCreate"}})

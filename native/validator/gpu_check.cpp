@@ -30,6 +30,8 @@
 #include <hsa/hsa_ext_amd.h>
 #include <unistd.h>
 
+#include "gate_lock.h"
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -141,10 +143,26 @@ std::string fmt_step(const char* name, int dev, bool ok, double s, const std::st
   return std::string(b) + (detail.empty() ? "" : ", " + detail) + "}";
 }
 
-// one device: queue, dispatch, verify; appends its step records
+// the agent's PCI address, as the validator names it (hipDeviceGetPCIBusId)
+std::string agent_bdf(hsa_agent_t gpu) {
+  uint32_t bdf = 0, domain = 0;
+  hsa_agent_get_info(gpu, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+  hsa_agent_get_info(gpu, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &domain);
+  char b[32];
+  snprintf(b, sizeof b, "%04x:%02x:%02x.%x", domain & 0xffff, (bdf >> 8) & 0xff, (bdf >> 3) & 0x1f, bdf & 0x7);
+  return b;
+}
+
+// one device: queue, dispatch, verify; appends its step records.  The GPU's
+// gate lock (gate_lock.h) is held shared from the code-object load to the
+// kernel's completion: a counter gate of the validator on this GPU never
+// counts this pod's upload or kernel.  `loop_s` > 0 (tests): keep
+// dispatching the kernel for that long, the lock taken per dispatch.
 bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std::vector<char>& co, int n,
-                  double timeout_s, std::vector<std::string>* steps, std::string* error) {
+                  double timeout_s, std::vector<std::string>* steps, std::string* error, double loop_s = 0) {
   const auto t0 = Clock::now();
+  const std::string bdf = agent_bdf(gpu);
+  avk::GateLock lock(bdf, avk::GateLock::kShared, 2.0);
   hsa_code_object_reader_t reader{0};
   hsa_executable_t exe{0};
   hsa_queue_t* queue = nullptr;
@@ -184,44 +202,58 @@ bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std:
     memcpy(karg + 8, &b, 8);
     memcpy(karg + 16, &c, 8);
     memcpy(karg + 24, &n, 4);
-    char tdet[96];
-    snprintf(tdet, sizeof tdet, "\"co_load_s\": %.4f, \"queue_s\": %.4f, ", co_load_s, queue_s);
-    steps->push_back(fmt_step("hsa", d, true, secs(t0), std::string(tdet) + "\"agent\": \"" + agent_name + "\""));
+    char tdet[160];
+    snprintf(tdet, sizeof tdet, "\"co_load_s\": %.4f, \"queue_s\": %.4f, \"gate_lock\": \"%s\", \"gate_lock_wait_s\": %.4f, ",
+             co_load_s, queue_s, lock.state(), lock.wait_s());
+    steps->push_back(fmt_step("hsa", d, true, secs(t0), std::string(tdet) + "\"bdf\": \"" + bdf + "\", \"agent\": \"" +
+                                                            agent_name + "\""));
 
     const auto t1 = Clock::now();
-    const uint64_t idx = hsa_queue_add_write_index_relaxed(queue, 1);
-    auto* p = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(static_cast<char*>(queue->base_address) +
-                                                              (idx & (queue->size - 1)) * 64);
-    memset(reinterpret_cast<char*>(p) + 4, 0, 60);
-    p->workgroup_size_x = 256;
-    p->workgroup_size_y = 1;
-    p->workgroup_size_z = 1;
-    p->grid_size_x = static_cast<uint32_t>((n + 255) / 256) * 256u;
-    p->grid_size_y = 1;
-    p->grid_size_z = 1;
-    p->private_segment_size = k.private_size;
-    p->group_segment_size = k.group_size;
-    p->kernel_object = k.object;
-    p->kernarg_address = karg;
-    p->completion_signal = done;
-    const uint16_t hdr = static_cast<uint16_t>((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                                               (1 << HSA_PACKET_HEADER_BARRIER) |
-                                               (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                                               (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
-    __atomic_store_n(reinterpret_cast<uint32_t*>(p),
-                     static_cast<uint32_t>(hdr) | (static_cast<uint32_t>(1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS) << 16),
-                     __ATOMIC_RELEASE);
-    hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
-    dispatched = true;
-    while (hsa_signal_wait_scacquire(done, HSA_SIGNAL_CONDITION_LT, 1, 1000000, HSA_WAIT_STATE_BLOCKED) >= 1)
-      if (secs(t1) > timeout_s) throw Fail{"dispatch did not complete within the timeout"};
+    int dispatches = 0;
+    for (;;) {
+      ++dispatches;
+      const uint64_t idx = hsa_queue_add_write_index_relaxed(queue, 1);
+      auto* p = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(static_cast<char*>(queue->base_address) +
+                                                                (idx & (queue->size - 1)) * 64);
+      memset(reinterpret_cast<char*>(p) + 4, 0, 60);
+      p->workgroup_size_x = 256;
+      p->workgroup_size_y = 1;
+      p->workgroup_size_z = 1;
+      p->grid_size_x = static_cast<uint32_t>((n + 255) / 256) * 256u;
+      p->grid_size_y = 1;
+      p->grid_size_z = 1;
+      p->private_segment_size = k.private_size;
+      p->group_segment_size = k.group_size;
+      p->kernel_object = k.object;
+      p->kernarg_address = karg;
+      p->completion_signal = done;
+      const uint16_t hdr = static_cast<uint16_t>((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                                 (1 << HSA_PACKET_HEADER_BARRIER) |
+                                                 (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                                 (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+      __atomic_store_n(reinterpret_cast<uint32_t*>(p),
+                       static_cast<uint32_t>(hdr) |
+                           (static_cast<uint32_t>(1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS) << 16),
+                       __ATOMIC_RELEASE);
+      hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
+      dispatched = true;
+      while (hsa_signal_wait_scacquire(done, HSA_SIGNAL_CONDITION_LT, 1, 1000000, HSA_WAIT_STATE_BLOCKED) >= 1)
+        if (secs(t1) > timeout_s + loop_s) throw Fail{"dispatch did not complete within the timeout"};
+      if (secs(t1) >= loop_s) break;
+      // --loop-seconds: the lock is released between dispatches, so a gate waits one kernel at most
+      lock.release();
+      std::this_thread::sleep_for(std::chrono::microseconds(500));
+      lock = avk::GateLock(bdf, avk::GateLock::kShared, 2.0);
+      hsa_signal_store_relaxed(done, 1);
+    }
+    lock.release();
     finished = true;
     int bad = 0;
     for (int i = 0; i < n; ++i)
       if (c[i] != a[i] + b[i]) ++bad;
     ok = bad == 0;
     char det[96];
-    snprintf(det, sizeof det, "\"elems\": %d, \"mismatches\": %d", n, bad);
+    snprintf(det, sizeof det, "\"elems\": %d, \"mismatches\": %d, \"dispatches\": %d", n, bad, dispatches);
     steps->push_back(fmt_step("vecadd", d, ok, secs(t1), det));
     if (!ok) *error = "device " + std::to_string(d) + ": " + std::to_string(bad) + " wrong elements";
   } catch (const Fail& f) {
@@ -250,21 +282,23 @@ int main(int argc, char** argv) {
   int elems = 1 << 16;
   int expect = -1;  // --expect-devices: the GPUs the kubelet allocated to this pod
   std::string result_file;  // --result-file: the report, also written here (validate.py reads it)
+  double loop_s = 0;  // --loop-seconds (tests): dispatch continuously for this long
   for (int i = 1; i < argc; ++i) {
     std::string k = argv[i];
     if (k == "--timeout" && i + 1 < argc) timeout_s = atof(argv[++i]);
     else if (k == "--result-file" && i + 1 < argc) result_file = argv[++i];
     else if (k == "--elems" && i + 1 < argc) elems = atoi(argv[++i]);
     else if (k == "--expect-devices" && i + 1 < argc) expect = atoi(argv[++i]);
+    else if (k == "--loop-seconds" && i + 1 < argc) loop_s = atof(argv[++i]);
     else if (k == "--help" || k == "-h") {
       fprintf(stderr, "usage: amdgpu-gpu-check [--timeout S] [--elems N] [--expect-devices N] [--result-file PATH]"
-                      "   (every visible GPU)\n");
+                      " [--loop-seconds S]   (every visible GPU; gate locks in $AMDGPU_GATE_LOCK_DIR)\n");
       return 2;
     }
     // other flags (the validator's pod arguments) are accepted and ignored
   }
-  if (elems < 256 || elems > (1 << 24)) {
-    fprintf(stderr, "amdgpu-gpu-check: --elems must be in [256, 2^24]\n");
+  if (elems < 256 || elems > (1 << 24) || loop_s < 0 || loop_s > 600) {
+    fprintf(stderr, "amdgpu-gpu-check: --elems must be in [256, 2^24], --loop-seconds in [0, 600]\n");
     return 2;
   }
   std::vector<std::string> steps;
@@ -304,7 +338,7 @@ int main(int argc, char** argv) {
     for (int d = 0; d < ngpu; ++d)
       threads.emplace_back([&, d] {
         try {  // nothing may leave a thread (std::terminate): an unexpected error fails this device only
-          dev_ok[d] = check_device(d, ag.gpus[d], pool, co, elems, timeout_s, &dev_steps[d], &dev_error[d]);
+          dev_ok[d] = check_device(d, ag.gpus[d], pool, co, elems, timeout_s, &dev_steps[d], &dev_error[d], loop_s);
         } catch (const std::exception& e) {
           dev_error[d] = "device " + std::to_string(d) + ": " + e.what();
         } catch (...) {

@@ -72,6 +72,57 @@ def test_validator_fp8_rate_step_with_counter_gate(tmp_path):
     assert q["perf_ok"] and q["tflops"] > 1.3 * f["tflops"] and q["gate_setup_seconds"] < 0.002
 
 
+def test_counter_gates_pass_first_time_beside_a_process_dispatching_continuously(tmp_path):
+    """VERDICT r5 task 3: a second process (the plugin-validation pod's check,
+    here looping its kernel for seconds) dispatches on the GPU the whole time
+    the validator's three counter gates run.  It holds the GPU's gate lock
+    shared per dispatch and the gates hold it exclusively around their counted
+    dispatch (gate_lock.h), so every gate passes on its first attempt."""
+    import time
+
+    locks = tmp_path / "locks"
+    locks.mkdir()
+    env = {"AMDGPU_GATE_LOCK_DIR": str(locks)}
+    bg = subprocess.Popen([str(native.binary("amdgpu-gpu-check")), "--loop-seconds", "6", "--elems", str(1 << 22),
+                           "--timeout", "30"], env={**os.environ, **env}, stdout=subprocess.PIPE, text=True)
+    try:
+        deadline = time.monotonic() + 20
+        while not list(locks.glob("gate-*.lock")) and time.monotonic() < deadline:
+            time.sleep(0.01)  # the loop's first lock: it is dispatching
+        assert list(locks.glob("gate-*.lock")), "the background check never took its lock"
+        rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm,gemm_fp8,gemm_fp4", "--counter-gate"],
+                       env=env)
+        assert bg.poll() is None, "the background dispatcher ended before the gates"
+    finally:
+        out = bg.communicate(timeout=60)[0]
+    assert rc == 0 and rep["ok"], rep
+    for name in ("gemm", "gemm_fp8", "gemm_fp4"):
+        st = next(x for x in rep["steps"] if x["name"] == name)
+        assert st["counter_gate"] == "pass" and st["gate_attempts"] == 1, st
+        assert st["gate_lock"] == "held" and st["gate_lock_wait_s"] < 0.5, st
+    bgrep = json.loads(out.strip().splitlines()[-1])
+    vec = next(x for x in bgrep["steps"] if x["name"] == "vecadd")
+    assert bgrep["ok"] and vec["dispatches"] > 10, bgrep  # it kept the GPU busy throughout
+    hsa = next(x for x in bgrep["steps"] if x["name"] == "hsa")
+    assert hsa["gate_lock"] == "held"
+    # the pod (HSA agent BDF) and the gates (hipDeviceGetPCIBusId) named the same lock file
+    assert [p.name for p in locks.glob("gate-*.lock")] == ["gate-" + hsa["bdf"].replace(":", "-").replace(".", "-")
+                                                           + ".lock"]
+
+
+def test_counter_gate_fails_closed_on_a_truncated_gemm(tmp_path):
+    """The counted dispatch runs half the K loop (AMDGPU_GATE_TEST_TRUNCATE_K):
+    its MFMA op count misses 2MNK/512 and its output differs, so the gate
+    fails on its first attempt and is not retried."""
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--counter-gate"],
+                   env={"AMDGPU_GATE_TEST_TRUNCATE_K": "1"})
+    assert rc != 0 and not rep["ok"]
+    g = next(x for x in rep["steps"] if x["name"] == "gemm")
+    assert g["counter_gate"] == "fail" and g["gate_attempts"] == 1, g
+    assert g["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 == 4096 ** 3  # half of 2 * 4096^3
+    assert g["gated_output_matches"] is False and g["freivalds_rel_err"] < 1e-4  # the HIP GEMM itself was right
+
+
 def test_validator_fp8_floor_fails_the_step(tmp_path):
     rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm_fp8", "--min-fp8-tflops", "100000"])
     assert rc != 0 and not rep["ok"]
