@@ -277,7 +277,8 @@ class WorkloadSpec(_M):
     # profiles/r5_ttr/fp8_step and profiles/r5_fp4) and counted by the gate
     # (SQ_INSTS_VALU_MFMA_MOPS_F8 / _F6F4)
     mfmaRateCheck: bool = True
-    mfmaRateGemmN: int = 4096
+    # the validator takes multiples of 256 (its 256 x 256 tiles), and >= 512 for fp4
+    mfmaRateGemmN: int = Field(default=4096, ge=512, multiple_of=256)
     minFp8Tflops: float = 1200.0
     minFp4Tflops: float = 1900.0
     # counter-gate floor on MFMA busy cycles per SIMD-cycle of the counted

@@ -335,6 +335,8 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
     for flag, val in (("--min-gemm-tflops", w.minGemmTflops), ("--min-hbm-gbps", w.minHbmGbps),
                       ("--min-fp8-tflops", w.minFp8Tflops if w.mfmaRateCheck else 0),
                       ("--min-fp4-tflops", w.minFp4Tflops if w.mfmaRateCheck else 0),
+                      ("--min-fp6-tflops", w.minFp6Tflops if w.mfmaRateCheck else 0),
+                      ("--min-mxfp4-tflops", w.minMxfp4Tflops if w.mfmaRateCheck else 0),
                       ("--min-mfma-util", w.minMfmaUtil), ("--rccl-busbw-link-fraction", w.rcclBusbwLinkFraction),
                       ("--xgmi-read-link-fraction", w.xgmiReadLinkFraction)):
         if val:

@@ -132,15 +132,66 @@ def outdated(env: NodeEnv, desired_version: str, spec_hash: str = "") -> str:
     return ""
 
 
-def _release_gated_validators(env: NodeEnv) -> None:
+def _release_gated_validators(env: NodeEnv, timeout: float = 5.0) -> list[str]:
     """Validator processes waiting at their start gate may hold /dev/kfd
-    (validator/validate.py prespawn_safe): abort them before the module goes."""
+    (validator/validate.py prespawn_safe; with an "init" verdict their HIP
+    runtime is starting): abort them before the module goes, and wait until
+    they are gone - each holds ``<gate>.held`` locked for its lifetime (the
+    native validator, validator_main.cpp) - and until the kernel has torn
+    down their GPU state (:func:`wait_kfd_settled`).  Returns the gates that
+    were aborted."""
     from ..validator.validate import abort_start_gates
 
     aborted = abort_start_gates(env)
-    if aborted:
-        log.info("aborted %d validator start gate(s) before the driver change", len(aborted))
-        time.sleep(0.2)  # they poll their gate every 0.25 ms and exit at once
+    if not aborted:
+        return aborted
+    t0 = time.monotonic()
+    deadline = t0 + timeout
+    left = [g for g in aborted if not _wait_unlocked(env.validation_file(g) + ".held", deadline)]
+    settled = wait_kfd_settled(env, deadline)
+    log.info("aborted %d validator start gate(s) before the driver change: gone after %.3f s%s%s", len(aborted),
+             time.monotonic() - t0, f", {len(left)} still running" if left else "",
+             "" if settled else ", KFD teardown still under way")
+    return aborted
+
+
+def _wait_unlocked(path: str, deadline: float) -> bool:
+    """Until nobody holds ``path`` flock-ed (its holder exited) or ``deadline``
+    (monotonic); a missing file has no holder."""
+    import fcntl
+
+    try:
+        fd = os.open(path, os.O_RDONLY | os.O_CLOEXEC)
+    except FileNotFoundError:
+        return True
+    try:
+        while True:
+            try:
+                fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
+                fcntl.flock(fd, fcntl.LOCK_UN)
+                return True
+            except BlockingIOError:
+                if time.monotonic() >= deadline:
+                    return False
+                time.sleep(0.001)
+    finally:
+        os.close(fd)
+
+
+def wait_kfd_settled(env: NodeEnv, deadline: float) -> bool:
+    """Until no exited process still has KFD state (a ``kfd/proc/<pid>`` entry
+    whose PID is gone from /proc: the kernel's teardown of it is under way,
+    and the module counts it as a user) or ``deadline``.  The driver
+    container runs in the host PID namespace, where both lists name the same
+    PIDs."""
+    proc = os.path.join(env.sysfs_root(), "proc")
+    while True:
+        stale = [p for p in kfd_users(env) if not os.path.exists(os.path.join(proc, p))]
+        if not stale:
+            return True
+        if time.monotonic() >= deadline:
+            return False
+        time.sleep(0.002)
 
 
 def install(env: NodeEnv, timeout: float = 600.0, stop: threading.Event | None = None,

@@ -57,6 +57,14 @@ def _lib(name: str = LIB_NAME) -> ctypes.CDLL:
         "avk_gemv_cols_bf16": ([P, P, P, I, I, S], I),
         "avk_gemv_rows_fp4": ([P, P, P, I, I, S], I),
         "avk_gemv_cols_fp4": ([P, P, P, I, I, S], I),
+        "avk_gemm_fp6_nt": ([P, P, P, I, I, I, I, S], I),
+        "avk_fill_fp6": ([P, I64, U64, S], I),
+        "avk_gemv_rows_fp6": ([P, P, P, I, I, S], I),
+        "avk_gemv_cols_fp6": ([P, P, P, I, I, S], I),
+        "avk_gemm_mxfp4_nt": ([P, P, P, P, P, I, I, I, I, S], I),
+        "avk_fill_e8m0": ([P, I64, U64, I, I, S], I),
+        "avk_gemv_rows_mxfp4": ([P, P, P, P, I, I, S], I),
+        "avk_gemv_cols_mxfp4": ([P, P, P, P, I, I, S], I),
         "avk_hbm_copy": ([P, P, I64, I, I, S], I),
         "avk_checksum": ([P, I64, P, S], I),
         "avk_max_abs_diff_f32": ([P, P, I64, P, S], I),
@@ -289,6 +297,185 @@ def gemm_fp4_nt(a, bt, out=None, out_dtype=None, stream=None):
     _require(out, out.dtype, "out")
     _check(_lib().avk_gemm_fp4_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
                                   M, N, K, _stream(stream)), "gemm_fp4_nt")
+    return out
+
+
+# ----------------------------------------------------------------- fp6 (e2m3)
+# The validator's fp6 storage: each 32-element k-block of a row is a 32-B slot
+# with the 32 six-bit codes packed little-endian in its first 24 B (element j
+# at bits 6j .. 6j+5, the f8f6f4 MFMA's operand order) and 8 B of zeros, so a
+# row of K fp6 is K bytes (validator_kernels.hip gemm_fp6_nt_kernel).
+FP6_K_MULTIPLE = 256
+
+
+def e2m3_values():
+    """code (0..63) -> value of OCP FP6 e2m3 (1 sign, 2 exponent bits with
+    bias 1, 3 mantissa bits)."""
+    out = []
+    for c in range(64):
+        e, m = (c >> 3) & 3, c & 7
+        mag = m / 8 if e == 0 else (1 + m / 8) * 2.0 ** (e - 1)
+        out.append(-mag if c & 0x20 else mag)
+    return tuple(out)
+
+
+FP6_VALUES = e2m3_values()
+
+
+def fp6_to_float(t):
+    """fp6 storage (uint8 [..., K], K a multiple of 32) -> float32 [..., K]."""
+    import torch
+
+    lut = torch.tensor(FP6_VALUES, dtype=torch.float32, device=t.device)
+    slots = t.view(torch.uint8).reshape(*t.shape[:-1], t.shape[-1] // 32, 32)[..., :24].long()
+    bits = torch.stack([(slots >> b) & 1 for b in range(8)], dim=-1).flatten(-2)  # [..., slots, 192] little-endian
+    w = torch.tensor([1 << b for b in range(6)], device=t.device)
+    codes = (bits.view(*bits.shape[:-1], 32, 6) * w).sum(-1)
+    return lut[codes].flatten(-2)
+
+
+def float_to_fp6(x):
+    """float values in the e2m3 set [..., K] -> fp6 storage uint8 [..., K]."""
+    import torch
+
+    table = {v: i for i, v in enumerate(FP6_VALUES) if not (v == 0 and i == 32)}
+    codes = torch.tensor([table[float(v)] for v in x.flatten().tolist()], dtype=torch.long)
+    codes = codes.view(*x.shape[:-1], x.shape[-1] // 32, 32)
+    bits = torch.stack([(codes >> b) & 1 for b in range(6)], dim=-1).flatten(-2)  # [..., slots, 192]
+    byte = (bits.view(*bits.shape[:-1], 24, 8) * torch.tensor([1 << b for b in range(8)])).sum(-1)
+    out = torch.zeros(*codes.shape[:-1], 32, dtype=torch.uint8)
+    out[..., :24] = byte.to(torch.uint8)
+    return out.flatten(-2)
+
+
+def fill_fp6_(t, seed: int, stream=None):
+    """Deterministic random fp6 storage (every e2m3 code, slots padded) into a
+    uint8 tensor whose size is a multiple of 32."""
+    import torch
+
+    _require(t, torch.uint8, "t")
+    _check(_lib().avk_fill_fp6(t.data_ptr(), t.numel(), seed & ((1 << 64) - 1), _stream(stream)), "fill_fp6")
+    return t
+
+
+def gemm_fp6_nt(a, bt, out=None, out_dtype=None, stream=None):
+    """K2d: ``out[M,N] = A[M,K] @ Bt[N,K].T`` with OCP FP6 e2m3 operands in the
+    fp6 storage (uint8 ``[M, K]`` / ``[N, K]``) on ``v_mfma_f32_16x16x128_f8f6f4
+    cbsz:2 blgp:2``, fp32 accumulation, bf16 or fp32 out.  M, N multiples of
+    256, K of 256."""
+    import torch
+
+    _require(a, torch.uint8, "a")
+    _require(bt, torch.uint8, "bt")
+    if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
+        raise ValueError(f"bad GEMM operands {tuple(a.shape)} x {tuple(bt.shape)}^T")
+    M, K = a.shape
+    N = bt.shape[0]
+    if M % GEMM_BM or N % GEMM_BN or K % FP6_K_MULTIPLE:
+        raise ValueError(f"fp6 GEMM shape {M}x{N}x{K} must be multiples of {GEMM_BM}x{GEMM_BN}x{FP6_K_MULTIPLE}")
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=out_dtype or torch.bfloat16)
+    if out.shape != (M, N) or out.dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("bad GEMM output")
+    _require(out, out.dtype, "out")
+    _check(_lib().avk_gemm_fp6_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), int(out.dtype == torch.float32),
+                                  M, N, K, _stream(stream)), "gemm_fp6_nt")
+    return out
+
+
+def gemv_fp6(x, v, transpose: bool = False, out=None, stream=None):
+    """The fp6 step's Freivalds GEMVs on fp6 storage ``[R, C]``."""
+    import torch
+
+    _require(x, torch.uint8, "x", 16)
+    _require(v, torch.float32, "v")
+    R, C = x.shape
+    if v.numel() != (R if transpose else C) or C % 32:
+        raise ValueError("gemv_fp6 shape mismatch")
+    if transpose:
+        out = torch.zeros(C, device=x.device, dtype=torch.float32) if out is None else out.zero_()
+        _check(_lib().avk_gemv_cols_fp6(x.data_ptr(), v.data_ptr(), out.data_ptr(), R, C, _stream(stream)), "gemv")
+    else:
+        out = torch.empty(R, device=x.device, dtype=torch.float32) if out is None else out
+        _check(_lib().avk_gemv_rows_fp6(x.data_ptr(), v.data_ptr(), out.data_ptr(), R, C, _stream(stream)), "gemv")
+    return out
+
+
+# ------------------------------------------------------------ MXFP4 (scaled)
+# Block-scaled OCP MXFP4: e2m1 pairs as gemm_fp4_nt's with one E8M0 scale
+# (2^(s - 127)) per row and 32-element k-block, periodic in k with 8 blocks:
+# scales uint8 [rows, 8], block b of row r scaled by S[r, b % 8].
+MX_SCALE_PERIOD = 8
+
+
+def fill_e8m0_(t, seed: int, lo: int = 124, hi: int = 130, stream=None):
+    """Random E8M0 scales in [lo, hi] (default 2^-3 .. 2^3) into a uint8 tensor."""
+    import torch
+
+    _require(t, torch.uint8, "t", 1)
+    _check(_lib().avk_fill_e8m0(t.data_ptr(), t.numel(), seed & ((1 << 64) - 1), lo, hi, _stream(stream)), "fill_e8m0")
+    return t
+
+
+def mxfp4_to_float(x, scales):
+    """MXFP4 operand (pairs uint8 [R, K/2], scales uint8 [R, 8]) -> the
+    dequantized float64 [R, K]."""
+    import torch
+
+    v = fp4_to_float(x).double()
+    R, K = v.shape
+    blk = (torch.arange(K, device=x.device) // 32) % MX_SCALE_PERIOD
+    sc = torch.pow(2.0, scales.long().double() - 127.0)[:, blk]
+    return v * sc
+
+
+def gemm_mxfp4_nt(a, bt, sa, sb, out=None, out_dtype=None, stream=None):
+    """K2e: ``out = (2^(SA-127) A) @ (2^(SB-127) Bt).T`` on
+    ``v_mfma_scale_f32_16x16x128_f8f6f4 cbsz:4 blgp:4`` (MXFP4 with E8M0 block
+    scales ``sa`` [M, 8] / ``sb`` [N, 8] uint8, see MX_SCALE_PERIOD)."""
+    import torch
+
+    for t, n in ((a, "a"), (bt, "bt")):
+        _require(t, torch.uint8, n)
+    for t, n in ((sa, "sa"), (sb, "sb")):
+        _require(t, torch.uint8, n, 1)
+    if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
+        raise ValueError(f"bad GEMM operands {tuple(a.shape)} x {tuple(bt.shape)}^T")
+    M, K = a.shape[0], 2 * a.shape[1]
+    N = bt.shape[0]
+    if tuple(sa.shape) != (M, MX_SCALE_PERIOD) or tuple(sb.shape) != (N, MX_SCALE_PERIOD):
+        raise ValueError("MX scales must be [rows, 8] uint8")
+    if M % GEMM_BM or N % GEMM_BN or K % FP4_K_MULTIPLE or K < FP4_K_MIN:
+        raise ValueError(f"mxfp4 GEMM shape {M}x{N}x{K} must be multiples of {GEMM_BM}x{GEMM_BN}x{FP4_K_MULTIPLE}, "
+                         f"K >= {FP4_K_MIN}")
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=out_dtype or torch.bfloat16)
+    if out.shape != (M, N) or out.dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("bad GEMM output")
+    _require(out, out.dtype, "out")
+    _check(_lib().avk_gemm_mxfp4_nt(a.data_ptr(), bt.data_ptr(), sa.data_ptr(), sb.data_ptr(), out.data_ptr(),
+                                    int(out.dtype == torch.float32), M, N, K, _stream(stream)), "gemm_mxfp4_nt")
+    return out
+
+
+def gemv_mxfp4(x, scales, v, transpose: bool = False, out=None, stream=None):
+    """The MXFP4 step's Freivalds GEMVs on the dequantized operand."""
+    import torch
+
+    _require(x, torch.uint8, "x", 8)
+    _require(scales, torch.uint8, "scales", 1)
+    _require(v, torch.float32, "v")
+    R, C = x.shape[0], 2 * x.shape[1]
+    if v.numel() != (R if transpose else C) or C % 16:
+        raise ValueError("gemv_mxfp4 shape mismatch")
+    if transpose:
+        out = torch.zeros(C, device=x.device, dtype=torch.float32) if out is None else out.zero_()
+        _check(_lib().avk_gemv_cols_mxfp4(x.data_ptr(), scales.data_ptr(), v.data_ptr(), out.data_ptr(), R, C,
+                                          _stream(stream)), "gemv")
+    else:
+        out = torch.empty(R, device=x.device, dtype=torch.float32) if out is None else out
+        _check(_lib().avk_gemv_rows_mxfp4(x.data_ptr(), scales.data_ptr(), v.data_ptr(), out.data_ptr(), R, C,
+                                          _stream(stream)), "gemv")
     return out
 
 

@@ -38,6 +38,22 @@ def visible_count(env: dict) -> int | None:
     return None
 
 
+_HELD: list = []
+
+
+def _hold_for_life(path: str) -> None:
+    """``<gate>.held`` locked until the process exits, as the native validator
+    does (driver/manager.py _release_gated_validators waits on it)."""
+    import fcntl
+
+    try:
+        f = open(path, "a")
+        fcntl.flock(f, fcntl.LOCK_EX | fcntl.LOCK_NB)
+        _HELD.append(f)
+    except OSError:
+        pass
+
+
 def wait_start_gate(path: str | None, timeout: float = 120.0, abort_path: str | None = None) -> str:
     """The native validator's ``--start-gate``: block until the file has a
     verdict; "go" releases the process (same protocol as validator_main.cpp,
@@ -46,6 +62,7 @@ def wait_start_gate(path: str | None, timeout: float = 120.0, abort_path: str | 
     directory aborts the wait too."""
     if not path:
         return "go"
+    _hold_for_life(path + ".held")
     deadline = time.time() + timeout
     while time.time() < deadline:
         try:
@@ -155,7 +172,7 @@ SIM_LINK_GBPS = 45.0
 SIM_LATENCY_US = 12.0
 # GEMM rates of the simulated GPU (TF/s at 4096^3): above the default floors
 # (api/clusterpolicy.py WorkloadSpec), below floors set far above them
-SIM_GEMM_TFLOPS = {"gemm": 1300.0, "gemm_fp8": 2600.0, "gemm_fp4": 4100.0}
+SIM_GEMM_TFLOPS = {"gemm": 1300.0, "gemm_fp8": 2600.0, "gemm_fp4": 4100.0, "gemm_fp6": 3600.0, "gemm_mxfp4": 4000.0}
 
 
 def sim_busbw(world: int, nbytes: int) -> float:
@@ -171,7 +188,9 @@ def simulated_detail(step: str, argv: list[str], rank: int, world: int) -> dict:
 
     if step in SIM_GEMM_TFLOPS:  # the binary's floors apply from 4096^3 (validator_main.cpp gemm_floor)
         size_flag, floor_flag = {"gemm": ("--gemm", "--min-gemm-tflops"), "gemm_fp8": ("--fp8-gemm", "--min-fp8-tflops"),
-                                 "gemm_fp4": ("--fp4-gemm", "--min-fp4-tflops")}[step]
+                                 "gemm_fp4": ("--fp4-gemm", "--min-fp4-tflops"),
+                                 "gemm_fp6": ("--fp8-gemm", "--min-fp6-tflops"),
+                                 "gemm_mxfp4": ("--fp4-gemm", "--min-mxfp4-tflops")}[step]
         n = int(arg(size_flag, "4096"))
         tf = SIM_GEMM_TFLOPS[step]
         floor = float(arg(floor_flag, "0")) if n >= 4096 else 0.0
@@ -281,7 +300,7 @@ def _main(argv: list[str]) -> int:
                               "error": f"{expect} GPU(s) allocated to the pod, {seen} visible"}))
             return 1
     ndev = max(1, int(arg("--expect-devices", "1")))
-    per_device = ("vecadd", "gemm", "gemm_fp8", "gemm_fp4", "mfma", "hbm", "dmabuf")
+    per_device = ("vecadd", "gemm", "gemm_fp8", "gemm_fp4", "gemm_fp6", "gemm_mxfp4", "mfma", "hbm", "dmabuf")
     recs = []
     for s in steps:
         for d in (range(ndev) if s in per_device and ndev > 1 else [None]):

@@ -50,8 +50,9 @@ READY_FILES = {
 VALIDATED_LABEL = "amd.com/gpu.validated"
 MFMA_LABEL = "amd.com/gpu.validated.mfma"  # data types whose MFMA tile checked out on every GPU
 # data types whose GEMM held its TF/s floor (and counter gate) on every GPU:
-# bf16 (the gemm step), fp8 (gemm_fp8, e4m3) and fp4 (gemm_fp4, e2m1) on the
-# f8f6f4 MFMA
+# bf16 (the gemm step), fp8 (gemm_fp8, e4m3), fp4 (gemm_fp4, e2m1), fp6
+# (gemm_fp6, e2m3) and block-scaled mxfp4 (gemm_mxfp4, E8M0 scales) on the
+# f8f6f4 MFMA, e.g. "bf16.fp8.fp4.fp6.mxfp4"
 MFMA_RATE_LABEL = "amd.com/gpu.validated.mfma-rate"
 WORKLOAD_POD_LABEL = "amd.com/validator-workload"
 # take a validator process's result at its report, not at its exit (A/B: =0)
@@ -463,7 +464,8 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     require_links = "--require-xgmi-links" in args
     dmabuf = "--dmabuf" in args  # driver.rdma: HBM exported as a dma-buf on every device
     if "--no-mfma-rate" in args:  # validator.workload.mfmaRateCheck off
-        args = _drop_step(_drop_step(args, "gemm_fp8"), "gemm_fp4")
+        for st in ("gemm_fp8", "gemm_fp4", "gemm_fp6", "gemm_mxfp4"):
+            args = _drop_step(args, st)
     rccl_frac = float(_arg_value(args, "--rccl-busbw-link-fraction") or 0.0)
     xgmi_frac = float(_arg_value(args, "--xgmi-read-link-fraction") or 0.0)
     link_frac = float(_arg_value(args, "--min-xgmi-link-fraction") or 0.9)
@@ -685,7 +687,7 @@ def failure_summary(reports: list[dict], fabric: dict | None = None, problems: l
     return "; ".join(parts) or "no report"
 
 
-ALL_STEPS = ("hip", "vecadd", "gemm", "gemm_fp8", "gemm_fp4", "mfma", "hbm", "xgmi", "rccl")  # + "dmabuf" with driver.rdma
+ALL_STEPS = ("hip", "vecadd", "gemm", "gemm_fp8", "gemm_fp4", "gemm_fp6", "gemm_mxfp4", "mfma", "hbm", "xgmi", "rccl")  # + "dmabuf" with driver.rdma
 
 
 def _steps_of(args: list[str]) -> list[str]:
@@ -1222,7 +1224,7 @@ def abort_start_gates(env: NodeEnv) -> list[str]:
     except FileNotFoundError:
         return out
     for name in names:
-        if not name.startswith(START_GATE_PREFIX) or name.endswith(".tmp"):
+        if not name.startswith(START_GATE_PREFIX) or name.endswith((".tmp", ".held")):
             continue
         path = os.path.join(env.validations_dir, name)
         try:
@@ -1352,10 +1354,11 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
             th.join()
     finally:
         if gate:
-            try:
-                os.unlink(gate)
-            except FileNotFoundError:
-                pass
+            for path in (gate, gate + ".held"):  # .held: the processes' lifetime lock (driver/manager.py)
+                try:
+                    os.unlink(path)
+                except FileNotFoundError:
+                    pass
     if errors:
         raise StepFailed("; ".join(errors))
     return {"ok": True, "seconds": time.perf_counter() - t0, **results}
@@ -1377,18 +1380,22 @@ def validated_mfma_dtypes(workload: dict | None) -> list[str]:
     return [d for d in sets[0] if d in common]
 
 
-RATE_STEPS = (("bf16", "gemm"), ("fp8", "gemm_fp8"), ("fp4", "gemm_fp4"))
+RATE_STEPS = (("bf16", "gemm"), ("fp8", "gemm_fp8"), ("fp4", "gemm_fp4"), ("fp6", "gemm_fp6"),
+              ("mxfp4", "gemm_mxfp4"))
 
 
 def validated_rate_dtypes(workload: dict | None) -> list[str]:
     """Data types whose GEMM step passed on every device of every rank of the
     workload report with a TF/s floor applied (``min_tflops`` > 0: a
-    report-only run proves no rate)."""
+    report-only run proves no rate) and, where the counter gate was asked
+    for, counted by it (``counter_gate`` "pass"; "not_counted": the sdk-mode
+    gate counts only the bf16 GEMM, so that rate is not claimed)."""
     reports = (workload or {}).get("ranks") or []
     out = []
     for dtype, name in RATE_STEPS:
         recs = [s for r in reports for s in r.get("steps", []) if s.get("name") == name]
-        if recs and all(s.get("ok") is True and (s.get("min_tflops") or 0) > 0 for s in recs):
+        if recs and all(s.get("ok") is True and (s.get("min_tflops") or 0) > 0
+                        and s.get("counter_gate", "off") in ("pass", "off") for s in recs):
             out.append(dtype)
     return out
 

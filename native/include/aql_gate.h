@@ -9,7 +9,9 @@
 #define AVK_AQL_GATE_BF16 0  // gemm_default.h kGemmSymbol, SQ_INSTS_VALU_MFMA_MOPS_BF16
 #define AVK_AQL_GATE_FP8 1   // gemm_default.h kGemmFp8Symbol, SQ_INSTS_VALU_MFMA_MOPS_F8
 #define AVK_AQL_GATE_FP4 2   // gemm_default.h kGemmFp4Symbol, SQ_INSTS_VALU_MFMA_MOPS_F6F4
-#define AVK_AQL_GATE_DTYPES 3
+#define AVK_AQL_GATE_FP6 3   // gemm_default.h kGemmFp6Symbol, SQ_INSTS_VALU_MFMA_MOPS_F6F4
+#define AVK_AQL_GATE_MXFP4 4 // gemm_default.h kGemmMxFp4Symbol (E8M0 scales), SQ_INSTS_VALU_MFMA_MOPS_F6F4
+#define AVK_AQL_GATE_DTYPES 5
 
 struct avk_aql_gate_result {
   // SQ_INSTS_VALU_MFMA_MOPS_{BF16|F8}, SQ_VALU_MFMA_BUSY_CYCLES, SQ_WAVES, GRBM_GUI_ACTIVE
@@ -47,6 +49,13 @@ int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, const void* A, 
 int avk_aql_gate_gemm_dtype(int dtype, const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt,
                             void* C, int M, int N, int K, const char* code_object, double timeout_s,
                             avk_aql_gate_result* out, char* err, int errlen);
+
+// The same for a block-scaled GEMM (AVK_AQL_GATE_MXFP4: kernargs A, Bt, C, M,
+// N, K, then the E8M0 scale arrays SA [M][8] and SB [N][8]); SA / SB are
+// ignored (may be null) for the other dtypes.
+int avk_aql_gate_gemm_scaled(int dtype, const char* pci_bus_id, int agent_ordinal, const void* A, const void* Bt,
+                             void* C, int M, int N, int K, const void* SA, const void* SB, const char* code_object,
+                             double timeout_s, avk_aql_gate_result* out, char* err, int errlen);
 
 // Set up the gate's HSA state for a GPU agent ahead of its first gate: the
 // session above and the counter profiles of every dtype.  It dispatches

@@ -24,6 +24,15 @@ int avk_gemm_fp4_nt(const void* A, const void* Bt, void* C, int out_f32, int M, 
 int avk_fill_fp4(void* p, int64_t nbytes, uint64_t seed, hipStream_t s);
 int avk_gemv_rows_fp4(const void* X, const float* v, float* y, int R, int C, hipStream_t s);
 int avk_gemv_cols_fp4(const void* X, const float* v, float* z, int R, int C, hipStream_t s);
+int avk_gemm_fp6_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K, hipStream_t s);
+int avk_fill_fp6(void* p, int64_t nbytes, uint64_t seed, hipStream_t s);
+int avk_gemv_rows_fp6(const void* X, const float* v, float* y, int R, int C, hipStream_t s);
+int avk_gemv_cols_fp6(const void* X, const float* v, float* z, int R, int C, hipStream_t s);
+int avk_gemm_mxfp4_nt(const void* A, const void* Bt, const void* SA, const void* SB, void* C, int out_f32, int M,
+                      int N, int K, hipStream_t s);
+int avk_fill_e8m0(void* p, int64_t n, uint64_t seed, int lo, int hi, hipStream_t s);
+int avk_gemv_rows_mxfp4(const void* X, const void* S, const float* v, float* y, int R, int C, hipStream_t s);
+int avk_gemv_cols_mxfp4(const void* X, const void* S, const float* v, float* z, int R, int C, hipStream_t s);
 int avk_gemv_rows_fp8(const void* X, const float* v, float* y, int R, int C, hipStream_t s);
 int avk_gemv_cols_fp8(const void* X, const float* v, float* z, int R, int C, hipStream_t s);
 int avk_gemv_cols_bf16(const void* X, const float* v, float* z, int R, int C, hipStream_t s);

@@ -28,4 +28,12 @@ constexpr const char* kGemmFp8Symbol = "gemm_fp8_nt_kernelILb0ELi1EE";
 // mfma-rate step (schedule 9: v_mfma_f32_16x16x128_f8f6f4 cbsz:4 blgp:4)
 constexpr const char* kGemmFp4Symbol = "gemm_fp4_nt_kernelILb0ELi1EE";
 
+// gemm_fp6_nt_kernel<false, 1>: the OCP FP6 (e2m3) GEMM of the mfma-rate step
+// (schedule 10: cbsz:2 blgp:2, fp6 in 32-B slots per 32 elements)
+constexpr const char* kGemmFp6Symbol = "gemm_fp6_nt_kernelILb0ELi1EE";
+
+// gemm_mxfp4_nt_kernel<false, 1>: block-scaled MXFP4 (schedule 11:
+// v_mfma_scale_f32_16x16x128_f8f6f4, E8M0 scales per row and k-block)
+constexpr const char* kGemmMxFp4Symbol = "gemm_mxfp4_nt_kernelILb0ELi1EE";
+
 }  // namespace avk

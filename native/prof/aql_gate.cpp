@@ -37,6 +37,7 @@
 #include <cstring>
 #include <algorithm>
 #include <fstream>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -72,6 +73,18 @@ const GateSpec kSpecs[AVK_AQL_GATE_DTYPES] = {
       {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 4},
       {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, 2}}},
     {avk::kGemmFp4Symbol,
+     {"SQ_INSTS_VALU_MFMA_MOPS_F6F4", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"},
+     {{HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 57},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 93},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 4},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, 2}}},
+    {avk::kGemmFp6Symbol,
+     {"SQ_INSTS_VALU_MFMA_MOPS_F6F4", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"},
+     {{HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 57},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 93},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 4},
+      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, 2}}},
+    {avk::kGemmMxFp4Symbol,
      {"SQ_INSTS_VALU_MFMA_MOPS_F6F4", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"},
      {{HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 57},
       {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 0, 93},
@@ -254,7 +267,9 @@ void* pool_alloc(hsa_amd_memory_pool_t pool, hsa_agent_t gpu, size_t bytes) {
 // The queue is left to the process exit, like HIP's own.
 struct Session {
   std::mutex m;
-  bool broken = false;  // a dispatch that never completed: the queue is not reused
+  // a dispatch that never completed: the queue is not reused.  Written under
+  // the session's lock, read under g_sessions_m by session_for: atomic
+  std::atomic<bool> broken{false};
   Api api;
   AgentSearch as;
   hsa_amd_memory_pool_t kpool{0};
@@ -420,7 +435,15 @@ extern "C" int avk_aql_gate_gemm(const char* pci_bus_id, int agent_ordinal, cons
 extern "C" int avk_aql_gate_gemm_dtype(int dtype, const char* pci_bus_id, int agent_ordinal, const void* A,
                                        const void* Bt, void* C, int M, int N, int K, const char* code_object,
                                        double timeout_s, avk_aql_gate_result* out, char* err, int errlen) {
-  const int d = dtype == AVK_AQL_GATE_FP8 ? 1 : dtype == AVK_AQL_GATE_FP4 ? 2 : 0;
+  return avk_aql_gate_gemm_scaled(dtype, pci_bus_id, agent_ordinal, A, Bt, C, M, N, K, nullptr, nullptr, code_object,
+                                  timeout_s, out, err, errlen);
+}
+
+extern "C" int avk_aql_gate_gemm_scaled(int dtype, const char* pci_bus_id, int agent_ordinal, const void* A,
+                                        const void* Bt, void* C, int M, int N, int K, const void* SA, const void* SB,
+                                        const char* code_object, double timeout_s, avk_aql_gate_result* out,
+                                        char* err, int errlen) {
+  const int d = dtype >= 0 && dtype < AVK_AQL_GATE_DTYPES ? dtype : 0;
   const auto t0 = Clock::now();
   memset(out, 0, sizeof(*out));
   try {
@@ -442,6 +465,11 @@ extern "C" int avk_aql_gate_gemm_dtype(int dtype, const char* pci_bus_id, int ag
     memcpy(karg + 24, &M, 4);
     memcpy(karg + 28, &N, 4);
     memcpy(karg + 32, &K, 4);
+    if (d == AVK_AQL_GATE_MXFP4) {  // (..., int K, const uint8_t* SA, const uint8_t* SB)
+      if (!SA || !SB || kern.kernarg_size < 56) throw Fail{"MX gate: scale arrays or kernarg layout missing"};
+      memcpy(karg + 40, &SA, 8);
+      memcpy(karg + 48, &SB, 8);
+    }
     hsa_queue_t* queue = ss->queue;
     hsa_signal_store_relaxed(ss->done, 1);
     out->setup_s = secs(t0);

@@ -46,6 +46,7 @@ nothing).
 from __future__ import annotations
 
 import os
+import re
 import sys
 
 SLICE_BYTES = 32 * 1024          # one ring slot: A 256x32 + B 256x32 bf16
@@ -889,9 +890,138 @@ def render9() -> str:
             "}\n")
 
 
+# ------------------------------------------------------------ schedule 10 (fp6) --
+# OCP FP6 (e2m3: cbsz = blgp = 2) on schedule 8 unchanged: a lane's fragment
+# of 32 fp6 is 24 B packed + 8 B of padding, so a 32-element block takes a
+# 32-B slot and a row of K fp6 the K bytes of an fp8 row (the validator's
+# storage layout for its synthetic fp6 operands, gemm_fp6_nt_kernel).  The
+# instruction reads the first six VGPRs of each eight-VGPR fragment, at the
+# fp4 rate: half the cycles of the fp8 step on the same bytes.
+S10_FMT = {"e2m3": 2, "e3m2": 3}
+
+
+def s10_slice(pos: int, first: bool = False, label: str | None = None, fmt: int = 2) -> list[str]:
+    out = []
+    for ln in s8_slice(pos, first, label):
+        if ln.startswith("v_mfma_f32_16x16x128_f8f6f4 "):
+            dst, b, a, c = [x.strip() for x in ln.split(" ", 1)[1].split(",")]
+            six = [re.sub(r"\[(\d+):(\d+)\]", lambda mm: f"[{mm.group(1)}:{int(mm.group(1)) + 5}]", r) for r in (b, a)]
+            ln = f"v_mfma_f32_16x16x128_f8f6f4 {dst}, {six[0]}, {six[1]}, {c} cbsz:{fmt} blgp:{fmt}"
+        out.append(ln)
+    return out
+
+
+def program10(fmt: int = 2) -> list[str]:
+    prog = program8()
+    head = prog[:prog.index("s_waitcnt lgkmcnt(0)") + 2]
+    assert head[-1] == "s_barrier"
+    lines = list(head)
+    lines += s10_slice(0, first=True, fmt=fmt)
+    lines += s10_slice(1, first=True, fmt=fmt)
+    lines += ["s_branch 2f"]
+    lines += ["1:"] + s10_slice(0, fmt=fmt) + s10_slice(1, fmt=fmt)
+    lines += s10_slice(2, label="2", fmt=fmt)
+    for pos in range(3, 10):
+        lines += s10_slice(pos, fmt=fmt)
+    lines += ["s_branch 1b", "3:",
+              "s_waitcnt vmcnt(0)", "s_nop 15", "s_nop 15", f"s_mov_b32 m0, {S4_KEEP}"]
+    return lines
+
+
+_MAINLOOP_ARGS = ("(unsigned a_lo, unsigned a_hi, unsigned b_lo, unsigned b_hi,\n"
+                  "                                                 unsigned ps, unsigned wave_lds, unsigned ns, unsigned la0,\n"
+                  "                                                 unsigned la1, unsigned lb0, unsigned lb1, unsigned g_off")
+_MAINLOOP_IN = ("               : [a_lo] \"s\"(a_lo), [a_hi] \"s\"(a_hi), [b_lo] \"s\"(b_lo), [b_hi] \"s\"(b_hi), [ps] \"s\"(ps),\n"
+                "                 [wave_lds] \"s\"(wave_lds), [ns] \"s\"(ns), [la0] \"v\"(la0), [la1] \"v\"(la1),\n"
+                "                 [lb0] \"v\"(lb0), [lb1] \"v\"(lb1), [g_off] \"v\"(g_off)")
+
+
+def render10() -> str:
+    body = "\\n\\t".join(program10(S10_FMT["e2m3"]))
+    clob = ", ".join([f'"v{r}"' for r in range(S8_VGPRS)] + [f'"s{r}"' for r in S4_SGPRS]
+                     + [f'"a{r}"' for r in range(256)])
+    return ("// Schedule 10 (OCP fp6 e2m3 in 32-B slots per 32 elements, v_mfma_f32_16x16x128_f8f6f4\n"
+            "// cbsz:2 blgp:2): schedule 8's data movement and arguments (ns = K / 128).\n"
+            "__device__ __forceinline__ void avk_g10_mainloop" + _MAINLOOP_ARGS + ") {\n"
+            f'  asm volatile("{body}"\n'
+            "               :\n" + _MAINLOOP_IN + "\n"
+            f"               : \"memory\", \"scc\", {clob});\n"
+            "}\n")
+
+
+# ------------------------------------------------- schedule 11 (MX-scaled fp4) --
+# Block-scaled OCP MXFP4 on schedule 9: v_mfma_scale_f32_16x16x128_f8f6f4 with
+# one E8M0 scale per operand per lane per MFMA - the scale of the lane's
+# 32-element k-block (a 16-B chunk of the 128-B row).  The validator's MX
+# operands carry a scale per (row, k-block mod 8): a lane's scales are then
+# the same in every stage, 16 bytes per operand (fragment i or j, k-step t ->
+# byte 2i + t), loaded by the kernel into four VGPRs per operand before the
+# loop and picked per MFMA by op_sel / op_sel_hi (byte = op_sel + 2 op_sel_hi).
+# The instruction's first source is the B fragment (the product is computed
+# transposed, as in every schedule here), so its scale is B's.
+def s11_scale(op: str, idx: int, t: int) -> tuple[str, int]:
+    byte = 2 * idx + t
+    return f"%[s{op.lower()}{byte // 4}]", byte % 4
+
+
+def s11_slice(pos: int, first: bool = False, label: str | None = None) -> list[str]:
+    even = pos % 2 == 0
+    rows = range(0, 4) if even else range(4, 8)
+    out = []
+    for ln in s9_slice(pos, first, label):
+        if ln.startswith("v_mfma_f32_16x16x128_f8f6f4 "):
+            ops = [x.strip() for x in ln.split(" ", 1)[1].split(" cbsz")[0].split(",")]
+            dst, b, a, c = ops
+            j = (int(re.match(r"v\[(\d+):", b).group(1)) - 64) // 8
+            t = ((int(re.match(r"v\[(\d+):", b).group(1)) - 64) % 8) // 4
+            i = int(re.match(r"v\[(\d+):", a).group(1)) // 8
+            assert i in rows and t == (int(re.match(r"v\[(\d+):", a).group(1)) % 8) // 4
+            sb, bb = s11_scale("B", j, t)
+            sa, ba = s11_scale("A", i, t)
+            ln = (f"v_mfma_scale_f32_16x16x128_f8f6f4 {dst}, {b}, {a}, {c}, {sb}, {sa} "
+                  f"op_sel:[{bb & 1},{ba & 1},0] op_sel_hi:[{bb >> 1},{ba >> 1},0] cbsz:4 blgp:4")
+        out.append(ln)
+    return out
+
+
+def program11() -> list[str]:
+    prog = program8()
+    head = prog[:prog.index("s_waitcnt lgkmcnt(0)") + 2]
+    assert head[-1] == "s_barrier"
+    lines = list(head)
+    lines += s11_slice(0, first=True)
+    lines += s11_slice(1, first=True)
+    lines += ["s_branch 2f"]
+    lines += ["1:"] + s11_slice(0) + s11_slice(1)
+    lines += s11_slice(2, label="2")
+    for pos in range(3, 10):
+        lines += s11_slice(pos)
+    lines += ["s_branch 1b", "3:",
+              "s_waitcnt vmcnt(0)", "s_nop 15", "s_nop 15", f"s_mov_b32 m0, {S4_KEEP}"]
+    return lines
+
+
+def render11() -> str:
+    body = "\\n\\t".join(program11())
+    clob = ", ".join([f'"v{r}"' for r in range(S8_VGPRS)] + [f'"s{r}"' for r in S4_SGPRS]
+                     + [f'"a{r}"' for r in range(256)])
+    scales = ", ".join(f"unsigned s{op}{q}" for op in "ab" for q in range(4))
+    scale_in = ", ".join(f'[s{op}{q}] "v"(s{op}{q})' for op in "ab" for q in range(4))
+    return ("// Schedule 11 (MXFP4: v_mfma_scale_f32_16x16x128_f8f6f4 cbsz:4 blgp:4 with E8M0 block\n"
+            "// scales): schedule 9's data movement and arguments (ns = K / 256), plus the lane's\n"
+            "// scale bytes of A (sa0..sa3: fragment i, k-step t at byte 2i + t) and of B (sb0..sb3).\n"
+            "__device__ __forceinline__ void avk_g11_mainloop" + _MAINLOOP_ARGS + ",\n"
+            "                                                 " + scales + ") {\n"
+            f'  asm volatile("{body}"\n'
+            "               :\n" + _MAINLOOP_IN + ",\n"
+            "                 " + scale_in + "\n"
+            f"               : \"memory\", \"scc\", {clob});\n"
+            "}\n")
+
+
 def render_all() -> str:
     return (render() + render2() + render3() + render4() + render4("b", odd_barrier=False)
-            + render4("c", odd_barrier=False, early_b=True) + render8() + render9())
+            + render4("c", odd_barrier=False, early_b=True) + render8() + render9() + render10() + render11())
 
 
 if __name__ == "__main__":

@@ -1494,6 +1494,127 @@ __global__ __launch_bounds__(g4::NTHR, 1) void gemm_fp4_nt_kernel(const uint8_t*
                           std::make_integer_sequence<int, 64>{});
 }
 
+// K2d: C = A . Bt^T with OCP FP6 (e2m3) operands in the validator's fp6
+// storage: each 32-element k-block of a row is a 32-B slot holding the 32
+// 6-bit codes packed little-endian (element j at bits 6j .. 6j + 5 of the
+// slot, the f8f6f4 MFMA's operand order) in its first 24 B and 8 B of zeros,
+// so a row of K fp6 is K bytes - the fp8 kernel's data movement unchanged,
+// with schedule 10's main loop (v_mfma_f32_16x16x128_f8f6f4 cbsz:2 blgp:2,
+// which reads the first six VGPRs of each fragment: the fp4 rate per clock).
+template <bool OUT_F32, int EPI = 1>
+__global__ __launch_bounds__(g4::NTHR, 1) void gemm_fp6_nt_kernel(const uint8_t* __restrict__ A,
+                                                                 const uint8_t* __restrict__ Bt,
+                                                                 void* __restrict__ Cv, int M, int N, int K) {
+  using namespace g4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid % kNumXcd;
+  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
+  const int per_group = GROUP_M * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid % per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  const uint64_t a0 = reinterpret_cast<uint64_t>(A + (size_t)(m0 + wave * 64) * K);
+  const uint64_t b0 = reinterpret_cast<uint64_t>(Bt + (size_t)(n0 + wave * 64) * K);
+  const int pr = lane >> 3;
+  const unsigned g_off = (unsigned)(pr * K + ((lane & 7) ^ g8_swz(pr)) * 16);
+  const unsigned lds = (unsigned)(uintptr_t)smem;
+  const int fr = lane & 15;
+  const unsigned c0 = (unsigned)(((2 * (lane >> 4)) ^ g8_swz(fr & 7)) * 16);
+  const unsigned c1 = (unsigned)(((2 * (lane >> 4) + 1) ^ g8_swz(fr & 7)) * 16);
+  const unsigned la = lds + (wm * 128 + fr) * 128, lb = lds + (wn * 128 + fr) * 128;
+  avk_g10_mainloop(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
+                   __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
+                   (unsigned)(8 * K), __builtin_amdgcn_readfirstlane(lds + wave * 8 * 1024), (unsigned)(K / 128),
+                   la + c0, la + c1, lb + c0, lb + c1, g_off);
+
+  if constexpr (!OUT_F32 && EPI >= 1)
+    g4_store_pairs_bf16<EPI == 2>(reinterpret_cast<__bf16*>(Cv), N, m0 + wm * 128 + fr, n0 + wn * 128, lane >> 4,
+                                  std::make_integer_sequence<int, 32>{});
+  else
+    g4_store_all<OUT_F32>(Cv, N, m0 + wm * 128 + fr, n0 + wn * 128 + (lane >> 4) * 4,
+                          std::make_integer_sequence<int, 64>{});
+}
+
+// K2e: block-scaled MXFP4.  C = (2^(SA - 127) . A) (2^(SB - 127) . Bt)^T with A,
+// Bt OCP FP4 pairs as gemm_fp4_nt_kernel's and one E8M0 scale per row and
+// 32-element k-block, periodic in k with 8 blocks (SA[M][8], SB[N][8]: block
+// b of row r has scale S[r][b % 8] - every block of a 256-deep stage its own
+// scale, the same in every stage).  Schedule 11's main loop
+// (v_mfma_scale_f32_16x16x128_f8f6f4): a lane's scales are one byte per
+// fragment and k-step, loaded here before the loop into four VGPRs per
+// operand (fragment i, k-step t at byte 2i + t; k-step t of lane group g
+// reads k-block g + 4t of the stage, gemm_fp4_nt_kernel).
+template <bool OUT_F32, int EPI = 1>
+__global__ __launch_bounds__(g4::NTHR, 1) void gemm_mxfp4_nt_kernel(const uint8_t* __restrict__ A,
+                                                                   const uint8_t* __restrict__ Bt,
+                                                                   void* __restrict__ Cv, int M, int N, int K,
+                                                                   const uint8_t* __restrict__ SA,
+                                                                   const uint8_t* __restrict__ SB) {
+  using namespace g4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid % kNumXcd;
+  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
+  const int per_group = GROUP_M * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid % per_group;
+  const int m0 = (first_m + in_group % gsize) * BM;
+  const int n0 = (in_group / gsize) * BN;
+
+  const int fr = lane & 15, g = lane >> 4;
+  unsigned sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int byte = 2 * i + t;
+      sa[byte >> 2] |= (unsigned)SA[(size_t)(m0 + wm * 128 + 16 * i + fr) * 8 + g + 4 * t] << (8 * (byte & 3));
+      sb[byte >> 2] |= (unsigned)SB[(size_t)(n0 + wn * 128 + 16 * i + fr) * 8 + g + 4 * t] << (8 * (byte & 3));
+    }
+
+  const int kb = K / 2;
+  const uint64_t a0 = reinterpret_cast<uint64_t>(A + (size_t)(m0 + wave * 64) * kb);
+  const uint64_t b0 = reinterpret_cast<uint64_t>(Bt + (size_t)(n0 + wave * 64) * kb);
+  const int pr = lane >> 3;
+  const unsigned g_off = (unsigned)(pr * kb + ((lane & 7) ^ g9_swz(pr)) * 16);
+  const unsigned lds = (unsigned)(uintptr_t)smem;
+  const unsigned c0 = (unsigned)((g ^ g9_swz(fr & 7)) * 16);
+  const unsigned c1 = (unsigned)(((g + 4) ^ g9_swz(fr & 7)) * 16);
+  const unsigned la = lds + (wm * 128 + fr) * 128, lb = lds + (wn * 128 + fr) * 128;
+  avk_g11_mainloop(__builtin_amdgcn_readfirstlane((unsigned)a0), __builtin_amdgcn_readfirstlane((unsigned)(a0 >> 32)),
+                   __builtin_amdgcn_readfirstlane((unsigned)b0), __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32)),
+                   (unsigned)(8 * kb), __builtin_amdgcn_readfirstlane(lds + wave * 8 * 1024), (unsigned)(K / 256),
+                   la + c0, la + c1, lb + c0, lb + c1, g_off, sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]);
+
+  if constexpr (!OUT_F32 && EPI >= 1)
+    g4_store_pairs_bf16<EPI == 2>(reinterpret_cast<__bf16*>(Cv), N, m0 + wm * 128 + fr, n0 + wn * 128, lane >> 4,
+                                  std::make_integer_sequence<int, 32>{});
+  else
+    g4_store_all<OUT_F32>(Cv, N, m0 + wm * 128 + fr, n0 + wn * 128 + (lane >> 4) * 4,
+                          std::make_integer_sequence<int, 64>{});
+}
+
 // four OCP e4m3 bytes (1 sign, 4 exponent bits with bias 7, 3 mantissa bits;
 // gfx950's fp8, not MI300's fnuz) -> floats on the conversion unit
 // (v_cvt_pk_f32_fp8): a tenth of the VALU work of a bit decode, which had
@@ -1548,6 +1669,109 @@ __device__ __forceinline__ void e2m1x8_to_f32(uint32_t x, float* out) {
   out[7] = p3[1];
 }
 
+// OCP FP6 e2m3 (1 sign, 2 exponent bits with bias 1, 3 mantissa bits; every
+// code finite, |x| <= 7.5) -> float
+__device__ __forceinline__ float e2m3_to_f32(unsigned c) {
+  const unsigned e = (c >> 3) & 3u, m = c & 7u;
+  const float mag = e == 0 ? (float)m * 0.125f : (float)(8u + m) * 0.125f * (float)(1u << (e - 1));
+  return (c & 0x20u) ? -mag : mag;
+}
+
+// one 32-B fp6 slot (32 codes in its first 24 B) -> 32 floats
+__device__ __forceinline__ void fp6_slot_to_f32(const uint8_t* slot, float* out) {
+  const uint4 lo = *reinterpret_cast<const uint4*>(slot);
+  const uint2 hi = *reinterpret_cast<const uint2*>(slot + 16);
+  const uint32_t w[6] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y};
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const int bit = 6 * j, wi = bit >> 5, sh = bit & 31;
+    unsigned c = w[wi] >> sh;
+    if (sh > 26) c |= w[wi + 1] << (32 - sh);
+    out[j] = e2m3_to_f32(c & 0x3Fu);
+  }
+}
+
+// random fp6 storage: per 32-B slot 32 random e2m3 codes, packed, 8 B of zeros
+__global__ __launch_bounds__(256) void fill_fp6_kernel(uint8_t* __restrict__ p, int64_t slots, uint64_t seed) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < slots; i += (int64_t)gridDim.x * 256) {
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull ^ seed * 0xD1B54A32D192ED03ull;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      if ((j & 7) == 0) {
+        h ^= h >> 31;
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 29;
+      }
+      const unsigned c = (unsigned)(h >> (6 * (j & 7) + 8)) & 0x3Fu;
+      const int bit = 6 * j, wi = bit >> 5, sh = bit & 31;
+      w[wi] |= c << sh;
+      if (sh > 26) w[wi + 1] |= c >> (32 - sh);
+    }
+    uint4* d = reinterpret_cast<uint4*>(p + i * 32);
+    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d[1] = make_uint4(w[4], w[5], 0u, 0u);
+  }
+}
+
+// random E8M0 scales in [lo, hi] (2^(lo - 127) .. 2^(hi - 127))
+__global__ __launch_bounds__(256) void fill_e8m0_kernel(uint8_t* __restrict__ p, int64_t n, uint64_t seed, int lo,
+                                                        int span) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull ^ seed * 0xD1B54A32D192ED03ull;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+    p[i] = (uint8_t)(lo + (int)((h >> 16) % (uint64_t)span));
+  }
+}
+
+__device__ __forceinline__ float e8m0_to_f32(uint8_t s) { return __uint_as_float((unsigned)s << 23); }
+
+// y[r] = sum_c X[r][c] v[c], X fp6 storage [R][C] bytes (a wave per row, a slot per lane step)
+__global__ __launch_bounds__(256) void gemv_rows_fp6_kernel(const uint8_t* __restrict__ X, const float* __restrict__ v,
+                                                            float* __restrict__ y, int R, int C) {
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= R) return;
+  const uint8_t* row = X + (size_t)wave * C;
+  float s = 0.f;
+  for (int c = lane * 32; c < C; c += 64 * 32) {
+    float f[32];
+    fp6_slot_to_f32(row + c, f);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) s += f[j] * v[c + j];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) y[wave] = s;
+}
+
+// y[r] = sum_c 2^(S[r][(c / 32) % 8] - 127) X[r][c] v[c], X FP4 pairs [R][C/2]
+__global__ __launch_bounds__(256) void gemv_rows_mxfp4_kernel(const uint8_t* __restrict__ X,
+                                                              const uint8_t* __restrict__ S,
+                                                              const float* __restrict__ v, float* __restrict__ y,
+                                                              int R, int C) {
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= R) return;
+  const uint8_t* row = X + (size_t)wave * (C / 2);
+  float s = 0.f;
+  for (int c = lane * 16; c < C; c += 64 * 16) {
+    const uint64_t x = *reinterpret_cast<const uint64_t*>(row + c / 2);
+    float f[16];
+    e2m1x8_to_f32((uint32_t)x, f);
+    e2m1x8_to_f32((uint32_t)(x >> 32), f + 8);
+    float p = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) p += f[j] * v[c + j];
+    s += p * e8m0_to_f32(S[(size_t)wave * 8 + ((c >> 5) & 7)]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) y[wave] = s;
+}
+
 // y[r] = sum_c X[r][c] * v[c], X FP4 pairs [R][C/2] (one wave per row, 16 values per lane step)
 __global__ __launch_bounds__(256) void gemv_rows_fp4_kernel(const uint8_t* __restrict__ X, const float* __restrict__ v,
                                                             float* __restrict__ y, int R, int C) {
@@ -1577,7 +1801,7 @@ __global__ __launch_bounds__(256) void gemv_rows_fp4_kernel(const uint8_t* __res
 // per lane made the fp4 one 121 us at 4096^2: profiles/r5_kernels.)
 struct DecFp4 {  // FP4 pairs [R][C/2]: 16 columns in 8 bytes
   static constexpr int kCols = 16;
-  __device__ static void load(const void* X, int r, int C, int c0, float* out) {
+  __device__ static void load(const void* X, const void*, int r, int C, int c0, float* out) {
     const uint64_t x = *reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(X) + (size_t)r * (C / 2) + c0 / 2);
     e2m1x8_to_f32((uint32_t)x, out);
     e2m1x8_to_f32((uint32_t)(x >> 32), out + 8);
@@ -1585,7 +1809,7 @@ struct DecFp4 {  // FP4 pairs [R][C/2]: 16 columns in 8 bytes
 };
 struct DecFp8 {  // e4m3 [R][C]: 8 columns in 8 bytes
   static constexpr int kCols = 8;
-  __device__ static void load(const void* X, int r, int C, int c0, float* out) {
+  __device__ static void load(const void* X, const void*, int r, int C, int c0, float* out) {
     const uint64_t x = *reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(X) + (size_t)r * C + c0);
     e4m3x4_to_f32((uint32_t)x, out);
     e4m3x4_to_f32((uint32_t)(x >> 32), out + 4);
@@ -1593,16 +1817,33 @@ struct DecFp8 {  // e4m3 [R][C]: 8 columns in 8 bytes
 };
 struct DecBf16 {  // bf16 [R][C]: 8 columns in 16 bytes
   static constexpr int kCols = 8;
-  __device__ static void load(const void* X, int r, int C, int c0, float* out) {
+  __device__ static void load(const void* X, const void*, int r, int C, int c0, float* out) {
     const bf16x8 x = *reinterpret_cast<const bf16x8*>(static_cast<const __bf16*>(X) + (size_t)r * C + c0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) out[j] = (float)x[j];
   }
 };
 
+struct DecFp6 {  // fp6 storage [R][C] bytes: 32 columns in one 32-B slot
+  static constexpr int kCols = 32;
+  __device__ static void load(const void* X, const void*, int r, int C, int c0, float* out) {
+    fp6_slot_to_f32(static_cast<const uint8_t*>(X) + (size_t)r * C + c0, out);
+  }
+};
+struct DecMxFp4 {  // FP4 pairs [R][C/2] with E8M0 scales S[R][8] (block c / 32 mod 8): 16 columns in 8 bytes
+  static constexpr int kCols = 16;
+  __device__ static void load(const void* X, const void* S, int r, int C, int c0, float* out) {
+    DecFp4::load(X, nullptr, r, C, c0, out);
+    const float sc = e8m0_to_f32(static_cast<const uint8_t*>(S)[(size_t)r * 8 + ((c0 >> 5) & 7)]);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) out[j] *= sc;
+  }
+};
+
 template <typename Dec>
 __global__ __launch_bounds__(256) void gemv_cols_kernel(const void* __restrict__ X, const float* __restrict__ v,
-                                                        float* __restrict__ z, int R, int C, int rows_per_slice) {
+                                                        float* __restrict__ z, int R, int C, int rows_per_slice,
+                                                        const void* __restrict__ aux) {
   constexpr int W = 64 * Dec::kCols;  // columns per block
   __shared__ float red[4][W];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1614,7 +1855,7 @@ __global__ __launch_bounds__(256) void gemv_cols_kernel(const void* __restrict__
   if (c0 < C) {
     for (int r = r0 + w; r < r1; r += 4) {
       float x[Dec::kCols];
-      Dec::load(X, r, C, c0, x);
+      Dec::load(X, aux, r, C, c0, x);
       const float vr = v[r];
 #pragma unroll
       for (int j = 0; j < Dec::kCols; ++j) s[j] += x[j] * vr;
@@ -1631,7 +1872,8 @@ __global__ __launch_bounds__(256) void gemv_cols_kernel(const void* __restrict__
 }
 
 template <typename Dec>
-int launch_gemv_cols(const void* X, const float* v, float* z, int R, int C, hipStream_t s) {
+int launch_gemv_cols(const void* X, const float* v, float* z, int R, int C, hipStream_t s,
+                     const void* aux = nullptr) {
   constexpr int W = 64 * Dec::kCols;
   const int bx = (C + W - 1) / W;
   int slices = 512 / bx;  // ~2048 waves in all at 4096^2 (4 per block), each over a stream of rows
@@ -1639,7 +1881,7 @@ int launch_gemv_cols(const void* X, const float* v, float* z, int R, int C, hipS
   if (slices > R) slices = R;
   const int rows_per_slice = (R + slices - 1) / slices;
   dim3 grid(bx, (R + rows_per_slice - 1) / rows_per_slice);
-  gemv_cols_kernel<Dec><<<grid, 256, 0, s>>>(X, v, z, R, C, rows_per_slice);
+  gemv_cols_kernel<Dec><<<grid, 256, 0, s>>>(X, v, z, R, C, rows_per_slice, aux);
   return hipGetLastError();
 }
 
@@ -2130,6 +2372,74 @@ AVK_API int avk_gemm_fp4_nt(const void* A, const void* Bt, void* C, int out_f32,
   if (out_f32) gemm_fp4_nt_kernel<true><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
   else gemm_fp4_nt_kernel<false, 1><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
   return hipGetLastError();
+}
+
+// C = A . Bt^T with fp6 (e2m3) operands in the validator's fp6 storage (32-B
+// slot per 32 elements: K bytes per row); K a multiple of 256
+AVK_API int avk_gemm_fp6_nt(const void* A, const void* Bt, void* C, int out_f32, int M, int N, int K, hipStream_t s) {
+  if (!A || !Bt || !C || M <= 0 || N <= 0 || K <= 0) return hipErrorInvalidValue;
+  if (M % avk::kGemmTile || N % avk::kGemmTile || K % 256) return hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)Bt | (uintptr_t)C) % 16 != 0) return hipErrorInvalidValue;
+  const int nwg = (M / g4::BM) * (N / g4::BN);
+  const uint8_t* a = (const uint8_t*)A;
+  const uint8_t* b = (const uint8_t*)Bt;
+  if (out_f32) gemm_fp6_nt_kernel<true><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+  else gemm_fp6_nt_kernel<false, 1><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K);
+  return hipGetLastError();
+}
+
+// nbytes: a multiple of 32 (one slot per 32 elements)
+AVK_API int avk_fill_fp6(void* p, int64_t nbytes, uint64_t seed, hipStream_t s) {
+  if (!p || nbytes <= 0 || nbytes % 32) return hipErrorInvalidValue;
+  fill_fp6_kernel<<<grid_for(nbytes / 32, 256, 8192), 256, 0, s>>>((uint8_t*)p, nbytes / 32, seed);
+  return hipGetLastError();
+}
+
+AVK_API int avk_gemv_rows_fp6(const void* X, const float* v, float* y, int R, int C, hipStream_t s) {
+  if (!X || !v || !y || R <= 0 || C <= 0 || C % 32) return hipErrorInvalidValue;
+  gemv_rows_fp6_kernel<<<(R + 3) / 4, 256, 0, s>>>((const uint8_t*)X, v, y, R, C);
+  return hipGetLastError();
+}
+
+AVK_API int avk_gemv_cols_fp6(const void* X, const float* v, float* z, int R, int C, hipStream_t s) {
+  if (!X || !v || !z || R <= 0 || C <= 0 || C % 32) return hipErrorInvalidValue;
+  return launch_gemv_cols<DecFp6>(X, v, z, R, C, s);
+}
+
+// block-scaled MXFP4: C = (2^(SA-127) A)(2^(SB-127) Bt)^T, A / Bt FP4 pairs,
+// SA [M][8] / SB [N][8] E8M0 (scale of row r, k-block b: S[r][b % 8]); K a
+// multiple of 256, >= 512
+AVK_API int avk_gemm_mxfp4_nt(const void* A, const void* Bt, const void* SA, const void* SB, void* C, int out_f32,
+                              int M, int N, int K, hipStream_t s) {
+  if (!A || !Bt || !SA || !SB || !C || M <= 0 || N <= 0 || K < 512) return hipErrorInvalidValue;
+  if (M % avk::kGemmTile || N % avk::kGemmTile || K % 256) return hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)Bt | (uintptr_t)C) % 16 != 0) return hipErrorInvalidValue;
+  const int nwg = (M / g4::BM) * (N / g4::BN);
+  const uint8_t* a = (const uint8_t*)A;
+  const uint8_t* b = (const uint8_t*)Bt;
+  const uint8_t* sa = (const uint8_t*)SA;
+  const uint8_t* sb = (const uint8_t*)SB;
+  if (out_f32) gemm_mxfp4_nt_kernel<true><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K, sa, sb);
+  else gemm_mxfp4_nt_kernel<false, 1><<<nwg, g4::NTHR, 0, s>>>(a, b, C, M, N, K, sa, sb);
+  return hipGetLastError();
+}
+
+// n random E8M0 scales in [lo, hi]
+AVK_API int avk_fill_e8m0(void* p, int64_t n, uint64_t seed, int lo, int hi, hipStream_t s) {
+  if (!p || n <= 0 || lo < 1 || hi > 254 || hi < lo) return hipErrorInvalidValue;
+  fill_e8m0_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>((uint8_t*)p, n, seed, lo, hi - lo + 1);
+  return hipGetLastError();
+}
+
+AVK_API int avk_gemv_rows_mxfp4(const void* X, const void* S, const float* v, float* y, int R, int C, hipStream_t s) {
+  if (!X || !S || !v || !y || R <= 0 || C <= 0 || C % 16) return hipErrorInvalidValue;
+  gemv_rows_mxfp4_kernel<<<(R + 3) / 4, 256, 0, s>>>((const uint8_t*)X, (const uint8_t*)S, v, y, R, C);
+  return hipGetLastError();
+}
+
+AVK_API int avk_gemv_cols_mxfp4(const void* X, const void* S, const float* v, float* z, int R, int C, hipStream_t s) {
+  if (!X || !S || !v || !z || R <= 0 || C <= 0 || C % 16) return hipErrorInvalidValue;
+  return launch_gemv_cols<DecMxFp4>(X, v, z, R, C, s, S);
 }
 
 AVK_API int avk_fill_fp4(void* p, int64_t nbytes, uint64_t seed, hipStream_t s) {

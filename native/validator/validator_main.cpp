@@ -253,8 +253,10 @@ struct Args {
   double min_gemm_tflops = 0;      // for a whole MI355X (256 CUs); applied pro rata to a partition
   int fp8_n = 4096;                // the gemm_fp8 step (mfma-rate): e4m3 GEMM size
   double min_fp8_tflops = 0;       // its floor, like min_gemm_tflops
-  int fp4_n = 4096;                // the gemm_fp4 step: e2m1 GEMM size
+  int fp4_n = 4096;                // the gemm_fp4 / gemm_mxfp4 steps: e2m1 GEMM size
   double min_fp4_tflops = 0;
+  double min_fp6_tflops = 0;       // gemm_fp6 (size fp8_n)
+  double min_mxfp4_tflops = 0;     // gemm_mxfp4 (size fp4_n)
   double min_hbm_gbps = 0;         // idem
   double min_mfma_util = 0;        // counter-gate floor (gate_policy.h), scaled by the launch's occupancy
   double min_rccl_busbw_gbps = 0;  // fp32 all-reduce busBW floor at world > 1
@@ -642,7 +644,7 @@ thread_local bool t_gate_arrived = false;  // this device holds (or held) its tu
 // `dtype`: AVK_AQL_GATE_BF16 (the gemm step's kernel) or AVK_AQL_GATE_FP8
 // (gemm_fp8's); the MOPS counter is that data type's.
 bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int cus, hipStream_t st,
-              std::string* json, int dtype = AVK_AQL_GATE_BF16) {
+              std::string* json, int dtype = AVK_AQL_GATE_BF16, const void* SA = nullptr, const void* SB = nullptr) {
   const char* mops_name = avk_aql_gate_counter_name_dtype(dtype, 0);
   const auto tg = Clock::now();
   unsigned long long* cs;
@@ -672,8 +674,8 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
     avk::GateLock lock(bus, avk::GateLock::kExclusive, 2.0);  // the counted window only
     lock_wait_s += lock.wait_s();
     lock_state = lock.state();
-    const int rc = avk_aql_gate_gemm_dtype(dtype, bus, a.agent_ordinal, A, B, C16, n, n, k_counted, co.c_str(), 5.0,
-                                           &r, err, sizeof(err));
+    const int rc = avk_aql_gate_gemm_scaled(dtype, bus, a.agent_ordinal, A, B, C16, n, n, k_counted, SA, SB,
+                                            co.c_str(), 5.0, &r, err, sizeof(err));
     lock.release();
     unsigned long long sums[2] = {0, 0};
     if (rc == 0) {
@@ -864,20 +866,65 @@ Step step_gemm(const Args& a, hipStream_t st, int cus) {
 // dispatches against its floor, and with the counter gate one counted
 // dispatch whose SQ_INSTS_VALU_MFMA_MOPS_F8 / _F6F4 must equal 2MNK/512 (aql
 // mode; the sdk tool counts only the bf16 GEMM).
+//
+// gemm_fp6 and gemm_mxfp4 (SURVEY C6's .mfma.{bf16,fp8,fp6,fp4}; MX is the
+// format MI355X inference runs): OCP FP6 e2m3 on cbsz = blgp = 2 (the fp4
+// rate per clock; the validator's fp6 storage keeps a 32-element block in a
+// 32-B slot, so its bytes move like fp8's), and block-scaled MXFP4 on
+// v_mfma_scale_f32_16x16x128_f8f6f4 with E8M0 scales of 2^-3 .. 2^3 per row
+// and k-block (periodic in k with 8 blocks, validator_kernels.hip
+// gemm_mxfp4_nt_kernel).  Both are checked and counted like the others
+// (SQ_INSTS_VALU_MFMA_MOPS_F6F4); the MX Freivalds GEMVs apply the scales.
 struct LowPrecision {
   const char* step;
   const char* dtype;
   int gate_dtype;
   int64_t (*bytes)(int64_t n_elems);
   int (*fill)(void*, int64_t, uint64_t, hipStream_t);
-  int (*gemm)(const void*, const void*, void*, int, int, int, int, hipStream_t);
-  int (*gemv_rows)(const void*, const float*, float*, int, int, hipStream_t);
-  int (*gemv_cols)(const void*, const float*, float*, int, int, hipStream_t);
+  // scales: E8M0 [rows][8] of A / Bt (MX), nullptr otherwise
+  int (*gemm)(const void*, const void*, const void*, const void*, void*, int, int, int, int, hipStream_t);
+  int (*gemv_rows)(const void*, const void*, const float*, float*, int, int, hipStream_t);
+  int (*gemv_cols)(const void*, const void*, const float*, float*, int, int, hipStream_t);
+  bool scaled;
 };
-const LowPrecision kFp8{"gemm_fp8", "e4m3", AVK_AQL_GATE_FP8, [](int64_t n) { return n; }, avk_fill_fp8,
-                        avk_gemm_fp8_nt, avk_gemv_rows_fp8, avk_gemv_cols_fp8};
-const LowPrecision kFp4{"gemm_fp4", "e2m1", AVK_AQL_GATE_FP4, [](int64_t n) { return n / 2; }, avk_fill_fp4,
-                        avk_gemm_fp4_nt, avk_gemv_rows_fp4, avk_gemv_cols_fp4};
+const LowPrecision kFp8{
+    "gemm_fp8", "e4m3", AVK_AQL_GATE_FP8, [](int64_t n) { return n; }, avk_fill_fp8,
+    [](const void* A, const void* B, const void*, const void*, void* C, int f, int m, int n, int k, hipStream_t s) {
+      return avk_gemm_fp8_nt(A, B, C, f, m, n, k, s);
+    },
+    [](const void* X, const void*, const float* v, float* y, int r, int c, hipStream_t s) {
+      return avk_gemv_rows_fp8(X, v, y, r, c, s);
+    },
+    [](const void* X, const void*, const float* v, float* z, int r, int c, hipStream_t s) {
+      return avk_gemv_cols_fp8(X, v, z, r, c, s);
+    },
+    false};
+const LowPrecision kFp4{
+    "gemm_fp4", "e2m1", AVK_AQL_GATE_FP4, [](int64_t n) { return n / 2; }, avk_fill_fp4,
+    [](const void* A, const void* B, const void*, const void*, void* C, int f, int m, int n, int k, hipStream_t s) {
+      return avk_gemm_fp4_nt(A, B, C, f, m, n, k, s);
+    },
+    [](const void* X, const void*, const float* v, float* y, int r, int c, hipStream_t s) {
+      return avk_gemv_rows_fp4(X, v, y, r, c, s);
+    },
+    [](const void* X, const void*, const float* v, float* z, int r, int c, hipStream_t s) {
+      return avk_gemv_cols_fp4(X, v, z, r, c, s);
+    },
+    false};
+const LowPrecision kFp6{
+    "gemm_fp6", "e2m3", AVK_AQL_GATE_FP6, [](int64_t n) { return n; }, avk_fill_fp6,
+    [](const void* A, const void* B, const void*, const void*, void* C, int f, int m, int n, int k, hipStream_t s) {
+      return avk_gemm_fp6_nt(A, B, C, f, m, n, k, s);
+    },
+    [](const void* X, const void*, const float* v, float* y, int r, int c, hipStream_t s) {
+      return avk_gemv_rows_fp6(X, v, y, r, c, s);
+    },
+    [](const void* X, const void*, const float* v, float* z, int r, int c, hipStream_t s) {
+      return avk_gemv_cols_fp6(X, v, z, r, c, s);
+    },
+    false};
+const LowPrecision kMxFp4{"gemm_mxfp4", "mxfp4", AVK_AQL_GATE_MXFP4, [](int64_t n) { return n / 2; }, avk_fill_fp4,
+                          avk_gemm_mxfp4_nt, avk_gemv_rows_mxfp4, avk_gemv_cols_mxfp4, true};
 
 double lowp_floor(double floor_full_gpu, int n, int cus) {
   return n >= 4096 ? avk::scale_floor_by_cus(floor_full_gpu, cus) : 0.0;
@@ -886,10 +933,12 @@ double lowp_floor(double floor_full_gpu, int n, int cus) {
 Step step_gemm_lowp(const Args& a, hipStream_t st, int cus, const LowPrecision& lp) {
   auto t0 = Clock::now();
   Step s{lp.step};
-  const bool fp4 = lp.gate_dtype == AVK_AQL_GATE_FP4;
+  const int dt = lp.gate_dtype;
+  const bool fp4 = dt == AVK_AQL_GATE_FP4 || dt == AVK_AQL_GATE_MXFP4;
   const int n = fp4 ? a.fp4_n : a.fp8_n;
   const int64_t nb = lp.bytes((int64_t)n * n);
-  void *A, *B, *C16;
+  const uint64_t seed = 41 + 10 * (uint64_t)dt;
+  void *A, *B, *C16, *SA = nullptr, *SB = nullptr;
   float *C32, *x, *y1, *z, *y2;
   HIP_OK(hipMalloc(&A, nb));
   HIP_OK(hipMalloc(&B, nb));
@@ -899,14 +948,20 @@ Step step_gemm_lowp(const Args& a, hipStream_t st, int cus, const LowPrecision& 
   HIP_OK(hipMalloc(&y1, n * 4));
   HIP_OK(hipMalloc(&y2, n * 4));
   HIP_OK(hipMalloc(&z, n * 4));
-  AVK_OK(lp.fill(A, nb, fp4 ? 51 : 41, st));
-  AVK_OK(lp.fill(B, nb, fp4 ? 52 : 42, st));
-  AVK_OK(avk_fill_uniform_f32(x, n, fp4 ? 53 : 43, -1, 1, st));
-  AVK_OK(lp.gemm(A, B, C32, 1, n, n, n, st));
+  AVK_OK(lp.fill(A, nb, seed, st));
+  AVK_OK(lp.fill(B, nb, seed + 1, st));
+  if (lp.scaled) {  // E8M0 2^-3 .. 2^3 per row and k-block (mod 8)
+    HIP_OK(hipMalloc(&SA, (size_t)n * 8));
+    HIP_OK(hipMalloc(&SB, (size_t)n * 8));
+    AVK_OK(avk_fill_e8m0(SA, (int64_t)n * 8, seed + 3, 124, 130, st));
+    AVK_OK(avk_fill_e8m0(SB, (int64_t)n * 8, seed + 4, 124, 130, st));
+  }
+  AVK_OK(avk_fill_uniform_f32(x, n, seed + 2, -1, 1, st));
+  AVK_OK(lp.gemm(A, B, SA, SB, C32, 1, n, n, n, st));
   AVK_OK(avk_gemv_rows(C32, 0, x, y1, n, n, st));
   HIP_OK(hipMemsetAsync(z, 0, n * 4, st));
-  AVK_OK(lp.gemv_cols(B, x, z, n, n, st));
-  AVK_OK(lp.gemv_rows(A, z, y2, n, n, st));
+  AVK_OK(lp.gemv_cols(B, SB, x, z, n, n, st));
+  AVK_OK(lp.gemv_rows(A, SA, z, y2, n, n, st));
   std::vector<float> h1(n), h2(n);
   HIP_OK(hipMemcpyAsync(h1.data(), y1, n * 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(h2.data(), y2, n * 4, hipMemcpyDeviceToHost, st));
@@ -921,26 +976,36 @@ Step step_gemm_lowp(const Args& a, hipStream_t st, int cus, const LowPrecision& 
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
-  AVK_OK(lp.gemm(A, B, C16, 0, n, n, n, st));  // warm
+  AVK_OK(lp.gemm(A, B, SA, SB, C16, 0, n, n, n, st));  // warm
   float best_ms = 0;
   for (int t = 0; t < 3; ++t) {
     HIP_OK(hipEventRecord(e0, st));
-    for (int i = 0; i < a.gemm_iters; ++i) AVK_OK(lp.gemm(A, B, C16, 0, n, n, n, st));
+    for (int i = 0; i < a.gemm_iters; ++i) AVK_OK(lp.gemm(A, B, SA, SB, C16, 0, n, n, n, st));
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipEventSynchronize(e1));
     float tm = 0;
     HIP_OK(hipEventElapsedTime(&tm, e0, e1));
     if (t == 0 || tm < best_ms) best_ms = tm;
   }
-  std::string gate_json = "\"counter_gate\": \"off\"";
+  // the sdk tool counts the bf16 GEMM only: with the gate asked for in sdk
+  // mode this rate is measured but not counted, and validate.py
+  // validated_rate_dtypes does not claim it on the mfma-rate label
+  std::string gate_json = a.counter_gate ? "\"counter_gate\": \"not_counted\", \"gate_mode\": \"sdk\""
+                                         : "\"counter_gate\": \"off\"";
   bool gate_ok = true;
-  if (a.counter_gate && a.gate_mode == "aql") gate_ok = aql_gate(a, A, B, C16, n, cus, st, &gate_json, lp.gate_dtype);
+  if (a.counter_gate && a.gate_mode == "aql")
+    gate_ok = aql_gate(a, A, B, C16, n, cus, st, &gate_json, lp.gate_dtype, SA, SB);
   const float ms = best_ms / a.gemm_iters;
   const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
-  for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) (void)hipFree(p);
-  const double floor = lowp_floor(fp4 ? a.min_fp4_tflops : a.min_fp8_tflops, n, cus);
+  for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z, SA, SB})
+    if (p) (void)hipFree(p);
+  const double floor_full = dt == AVK_AQL_GATE_FP4     ? a.min_fp4_tflops
+                            : dt == AVK_AQL_GATE_FP6   ? a.min_fp6_tflops
+                            : dt == AVK_AQL_GATE_MXFP4 ? a.min_mxfp4_tflops
+                                                       : a.min_fp8_tflops;
+  const double floor = lowp_floor(floor_full, n, cus);
   const bool perf_ok = floor <= 0 || tflops >= floor;
   s.ok = numerics_ok && gate_ok && perf_ok;
   s.seconds = secs(t0);
@@ -953,6 +1018,8 @@ Step step_gemm_lowp(const Args& a, hipStream_t st, int cus, const LowPrecision& 
 
 Step step_gemm_fp8(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kFp8); }
 Step step_gemm_fp4(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kFp4); }
+Step step_gemm_fp6(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kFp6); }
+Step step_gemm_mxfp4(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kMxFp4); }
 
 // Device buffers released only when the process ends.  Freeing VRAM makes
 // the kernel driver wipe it (wipe-on-release, an SDMA fill at ~80 GB/s), and
@@ -1771,12 +1838,16 @@ std::vector<Step> device_steps(Args ad, bool gate_last, bool with_hip) {
   if (!gate_last) run("gemm", [&] { return step_gemm(ad, sd, cus); });
   if (!gate_last) run("gemm_fp8", [&] { return step_gemm_fp8(ad, sd, cus); });
   if (!gate_last) run("gemm_fp4", [&] { return step_gemm_fp4(ad, sd, cus); });
+  if (!gate_last) run("gemm_fp6", [&] { return step_gemm_fp6(ad, sd, cus); });
+  if (!gate_last) run("gemm_mxfp4", [&] { return step_gemm_mxfp4(ad, sd, cus); });
   run("mfma", [&] { return step_mfma(sd); });
   run("hbm", [&] { return step_hbm(ad, sd, cus); });
   run("dmabuf", [&] { return step_dmabuf(sd); });
   if (gate_last) run("gemm", [&] { return step_gemm(ad, sd, cus); });
   if (gate_last) run("gemm_fp8", [&] { return step_gemm_fp8(ad, sd, cus); });
   if (gate_last) run("gemm_fp4", [&] { return step_gemm_fp4(ad, sd, cus); });
+  if (gate_last) run("gemm_fp6", [&] { return step_gemm_fp6(ad, sd, cus); });
+  if (gate_last) run("gemm_mxfp4", [&] { return step_gemm_mxfp4(ad, sd, cus); });
   if (sd) (void)hipStreamDestroy(sd);
   return out;
 }
@@ -1934,6 +2005,8 @@ int main(int argc, char** argv) {
     else if (k == "--min-fp8-tflops") a.min_fp8_tflops = atof(v());
     else if (k == "--fp4-gemm") a.fp4_n = atoi(v());
     else if (k == "--min-fp4-tflops") a.min_fp4_tflops = atof(v());
+    else if (k == "--min-fp6-tflops") a.min_fp6_tflops = atof(v());
+    else if (k == "--min-mxfp4-tflops") a.min_mxfp4_tflops = atof(v());
     else if (k == "--min-mfma-util") a.min_mfma_util = atof(v());
     else if (k == "--min-rccl-busbw-gbps") a.min_rccl_busbw_gbps = atof(v());
     else if (k == "--min-xgmi-read-gbps") a.min_xgmi_read_gbps = atof(v());
@@ -2052,13 +2125,37 @@ int main(int argc, char** argv) {
     _exit(3);
   };
   bool await_go = false;
+  // "init" lets the HIP runtime start before the driver check has passed; an
+  // "abort" (a driver reload or unload, driver/manager.py) can come during
+  // that start.  A watcher thread reads the gate meanwhile and ends the
+  // process at once, so the module's users are gone within ~1 ms of the
+  // abort instead of after the runtime's start-up.  The process holds
+  // <gate>.held (flock) for its lifetime: the driver container takes that lock
+  // to know an aborted validator has exited (_release_gated_validators).
+  std::atomic<bool> go_seen{false};
+  std::thread gate_watch;
   if (!a.start_gate.empty()) {
+    const int held_fd = ::open((a.start_gate + ".held").c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+    if (held_fd >= 0) (void)::flock(held_fd, LOCK_EX | LOCK_NB);  // released by the exit
     auto tg = Clock::now();
     kfd_early = fd_open_to("/dev/kfd");
     const std::string verdict = wait_gate(true);
     gate_wait_s = secs(tg);
     if (verdict != "go" && verdict != "init") gate_fail(verdict);
     await_go = verdict == "init";
+    if (await_go)
+      gate_watch = std::thread([&] {
+        for (;;) {
+          if (go_seen.load()) return;
+          std::string text;
+          if (read_small(a.start_gate, &text)) {
+            while (!text.empty() && (text.back() == '\n' || text.back() == ' ')) text.pop_back();
+            if (text == "go") return;
+            if (!text.empty() && text != "init") gate_fail(text == "timeout" ? "timeout" : "abort");
+          }
+          usleep(250);
+        }
+      });
   }
   int failed_peer = -1;
   std::string peer_state;
@@ -2071,7 +2168,8 @@ int main(int argc, char** argv) {
     primary = a.device = devs[0].first;
     a.agent_ordinal = devs[0].second;
     if (a.counter_gate && a.gate_mode == "aql" &&
-        (has_step(a, "gemm") || has_step(a, "gemm_fp8") || has_step(a, "gemm_fp4"))) {
+        (has_step(a, "gemm") || has_step(a, "gemm_fp8") || has_step(a, "gemm_fp4") || has_step(a, "gemm_fp6") ||
+         has_step(a, "gemm_mxfp4"))) {
       // the counter gates' HSA set-up (a private queue, the code object, the
       // counter profiles: ~6 ms) on a thread, beside the stream's creation
       // and the first steps; it dispatches nothing.  The first gate waits for
@@ -2106,6 +2204,8 @@ int main(int argc, char** argv) {
       const std::string verdict = wait_gate(false);
       gate_go_wait_s = secs(tg);
       if (verdict != "go") gate_fail(verdict);
+      go_seen = true;
+      if (gate_watch.joinable()) gate_watch.join();
     }
     if (ok && devs.size() == 1 && !a.all_devices) {
       // one device: the kernel steps in order on the main thread
@@ -2115,6 +2215,10 @@ int main(int argc, char** argv) {
         ok = (steps.push_back(step_gemm_fp8(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "gemm_fp4"))
         ok = (steps.push_back(step_gemm_fp4(a, st, prop.multiProcessorCount)), steps.back().ok);
+      if (ok && has_step(a, "gemm_fp6"))
+        ok = (steps.push_back(step_gemm_fp6(a, st, prop.multiProcessorCount)), steps.back().ok);
+      if (ok && has_step(a, "gemm_mxfp4"))
+        ok = (steps.push_back(step_gemm_mxfp4(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
       if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "dmabuf")) ok = (steps.push_back(step_dmabuf(st)), steps.back().ok);
@@ -2139,6 +2243,8 @@ int main(int argc, char** argv) {
     ok = false;
     error = e.what();
   }
+  go_seen = true;  // a step failed before "go": the gate watcher ends too
+  if (gate_watch.joinable()) gate_watch.join();
   if (gate_prep_thread.joinable()) gate_prep_thread.join();
   if (rccl_thread.joinable()) {
     if (rccl_state.abandoned) rccl_thread.detach();  // blocked in RCCL's bootstrap: ends with the process

@@ -482,3 +482,135 @@ def test_fp8_gemvs_vs_fp32(shape):
                      (K.gemv_fp8(xb, vc), xf.double() @ vc.double())):
         scale = ref.abs().max().item()
         assert (got.double() - ref).abs().max().item() <= 1e-5 * max(scale, 1.0) * (1 + (R + C) / 1024)
+
+
+# ----------------------------------------------- fp6 (e2m3) and MXFP4 (scaled)
+_FP6_SHAPES = [(256, 256, 256), (512, 768, 1024), (1024, 1024, 2048), (256, 512, 4096)]
+
+
+def _fp6_pair(M, N, Kd, seed):
+    a = torch.empty(M, Kd, device=DEV, dtype=torch.uint8)
+    bt = torch.empty(N, Kd, device=DEV, dtype=torch.uint8)
+    K.fill_fp6_(a, seed)
+    K.fill_fp6_(bt, seed + 1)
+    return a, bt
+
+
+def test_fp6_fill_spans_the_codes_and_pads_its_slots():
+    a = torch.empty(1 << 16, device=DEV, dtype=torch.uint8)
+    K.fill_fp6_(a, 5)
+    b = torch.empty_like(a)
+    K.fill_fp6_(b, 5)
+    assert torch.equal(a, b)
+    assert K.fp6_to_float(a).unique().numel() == 63  # 64 codes, +0 and -0 compare equal
+    assert int(a.view(-1, 32)[:, 24:].abs().sum()) == 0  # the 8 B of padding per slot
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", _FP6_SHAPES)
+def test_fp6_gemm_vs_exact_product(shape, out_dtype):
+    """e2m3 values (|x| <= 7.5) and their products are exact; the sum is the
+    MFMA's fp32 accumulation, checked against the fp64 product of the decoded
+    operands."""
+    M, N, Kd = shape
+    a, bt = _fp6_pair(M, N, Kd, M + 2 * N + Kd)
+    ref = K.fp6_to_float(a).double() @ K.fp6_to_float(bt).double().t()
+    out = K.gemm_fp6_nt(a, bt, out_dtype=out_dtype)
+    scale = ref.abs().max().item()
+    err = (out.double() - ref).abs().max().item()
+    assert err <= (2e-4 if out_dtype == torch.float32 else 8e-3) * scale, (err, scale)
+
+
+def test_fp6_gemm_exact_small_integers_and_identity():
+    """Values in {0, +-1, +-2, +-4} with an asymmetric B: exact integer sums;
+    an identity B returns A.  A swapped 6-bit field, slot or fragment half
+    changes the result."""
+    M, N, Kd = 512, 256, 512
+    i = torch.arange(M).view(M, 1)
+    k = torch.arange(Kd).view(1, Kd)
+    vals = torch.tensor([0.0, 1.0, -1.0, 2.0, -2.0, 4.0, -4.0, 0.5])
+    a = vals[(i * 3 + k * 5) % 8]
+    n = torch.arange(N).view(N, 1)
+    b = vals[(n * 11 + k * 2 + (n > k).long()) % 8]
+    out = K.gemm_fp6_nt(K.float_to_fp6(a).to(DEV), K.float_to_fp6(b).to(DEV), out_dtype=torch.float32)
+    assert torch.equal(out.double().cpu(), a.double() @ b.double().t())
+    eye = torch.zeros(256, Kd)
+    eye[:, :256] = torch.eye(256)
+    out = K.gemm_fp6_nt(K.float_to_fp6(a).to(DEV), K.float_to_fp6(eye).to(DEV), out_dtype=torch.float32)
+    assert torch.equal(out.cpu(), a[:, :256])
+
+
+@pytest.mark.parametrize("shape", [(4096, 4096), (512, 1024), (300, 1056), (7, 32)])
+def test_fp6_gemvs_vs_fp32(shape):
+    R, C = shape
+    x = torch.empty(R, C, device=DEV, dtype=torch.uint8)
+    K.fill_fp6_(x, R * 5 + C)
+    xf = K.fp6_to_float(x).double()
+    g = torch.Generator(device="cpu").manual_seed(R + C)
+    vr = torch.rand(R, generator=g).mul_(2).sub_(1).to(DEV)
+    vc = torch.rand(C, generator=g).mul_(2).sub_(1).to(DEV)
+    for got, ref in ((K.gemv_fp6(x, vr, transpose=True), xf.t() @ vr.double()), (K.gemv_fp6(x, vc), xf @ vc.double())):
+        scale = ref.abs().max().item()
+        assert (got.double() - ref).abs().max().item() <= 1e-5 * max(scale, 1.0) * (1 + (R + C) / 1024)
+
+
+def _mx_operands(M, N, Kd, seed, lo=124, hi=130):
+    a = torch.empty(M, Kd // 2, device=DEV, dtype=torch.uint8)
+    bt = torch.empty(N, Kd // 2, device=DEV, dtype=torch.uint8)
+    sa = torch.empty(M, 8, device=DEV, dtype=torch.uint8)
+    sb = torch.empty(N, 8, device=DEV, dtype=torch.uint8)
+    K.fill_fp4_(a, seed)
+    K.fill_fp4_(bt, seed + 1)
+    K.fill_e8m0_(sa, seed + 2, lo, hi)
+    K.fill_e8m0_(sb, seed + 3, lo, hi)
+    return a, bt, sa, sb
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", _FP4_SHAPES)
+def test_mxfp4_gemm_vs_exact_product_with_non_unit_scales(shape, out_dtype):
+    """Block-scaled MXFP4 with E8M0 scales 2^-3 .. 2^3 per row and k-block:
+    against the fp64 product of the dequantized, scaled operands."""
+    M, N, Kd = shape
+    a, bt, sa, sb = _mx_operands(M, N, Kd, 3 * M + N + Kd)
+    assert sa.unique().numel() == 7 and sb.unique().numel() == 7
+    ref = K.mxfp4_to_float(a, sa) @ K.mxfp4_to_float(bt, sb).t()
+    out = K.gemm_mxfp4_nt(a, bt, sa, sb, out_dtype=out_dtype)
+    scale = ref.abs().max().item()
+    err = (out.double() - ref).abs().max().item()
+    assert err <= (2e-4 if out_dtype == torch.float32 else 8e-3) * scale, (err, scale)
+
+
+def test_mxfp4_scales_are_per_row_and_block():
+    """Unit scales give the plain fp4 GEMM bit for bit; doubling one row's
+    scale of one k-block changes exactly that block's contribution (a scale
+    taken from the wrong lane, fragment or byte fails this)."""
+    M, N, Kd = 256, 256, 512
+    a, bt, sa, sb = _mx_operands(M, N, Kd, 77, 127, 127)
+    plain = K.gemm_fp4_nt(a, bt, out_dtype=torch.float32)
+    assert torch.equal(K.gemm_mxfp4_nt(a, bt, sa, sb, out_dtype=torch.float32), plain)
+    for r, blk in ((0, 0), (37, 5), (200, 7), (129, 3)):
+        sa2 = sa.clone()
+        sa2[r, blk] = 128  # x2 for row r, k-blocks blk, blk + 8, ...
+        sb2 = sb.clone()
+        sb2[(r * 7) % N, (blk + 1) % 8] = 125  # x1/4 for one B row, another block
+        ref = K.mxfp4_to_float(a, sa2) @ K.mxfp4_to_float(bt, sb2).t()
+        out = K.gemm_mxfp4_nt(a, bt, sa2, sb2, out_dtype=torch.float32)
+        assert (out.double() - ref).abs().max().item() <= 2e-4 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("shape", [(4096, 4096), (512, 1024), (300, 1040), (7, 16)])
+def test_mxfp4_gemvs_vs_fp32(shape):
+    R, C = shape
+    x = torch.empty(R, C // 2, device=DEV, dtype=torch.uint8)
+    s = torch.empty(R, 8, device=DEV, dtype=torch.uint8)
+    K.fill_fp4_(x, R + 3 * C)
+    K.fill_e8m0_(s, R + C)
+    xf = K.mxfp4_to_float(x, s)
+    g = torch.Generator(device="cpu").manual_seed(R * C)
+    vr = torch.rand(R, generator=g).mul_(2).sub_(1).to(DEV)
+    vc = torch.rand(C, generator=g).mul_(2).sub_(1).to(DEV)
+    for got, ref in ((K.gemv_mxfp4(x, s, vr, transpose=True), xf.t() @ vr.double()),
+                     (K.gemv_mxfp4(x, s, vc), xf @ vc.double())):
+        scale = ref.abs().max().item()
+        assert (got.double() - ref).abs().max().item() <= 1e-5 * max(scale, 1.0) * (1 + (R + C) / 1024)

@@ -174,6 +174,35 @@ def test_start_gate_abort_after_init_exits_before_the_kernels(tmp_path):
     assert rc == 3 and rep["error"] == "start gate: aborted" and rep["steps"] == []
 
 
+def test_start_gate_abort_during_the_runtime_start_ends_the_process_at_once(tmp_path):
+    """"abort" while the HIP runtime is still starting after "init"
+    - the gate watcher thread ends the process within milliseconds, not after
+    the runtime's start-up, and its ``.held`` lock is free once it is gone
+    (what the driver container waits on before a reload)."""
+    import fcntl
+    import time
+
+    gate = tmp_path / "gate"
+    gate.write_text("init")
+    p = subprocess.Popen([VALIDATOR, "--rendezvous", str(tmp_path / "rv"), "--steps", "hip,vecadd", "--start-gate",
+                          str(gate)], stdout=subprocess.PIPE, text=True)
+    held = tmp_path / "gate.held"
+    deadline = time.monotonic() + 10
+    while not held.exists() and time.monotonic() < deadline:
+        time.sleep(0.0005)
+    time.sleep(0.01)  # inside the runtime's start (~0.1 s)
+    t0 = time.monotonic()
+    gate.write_text("abort")
+    line = p.stdout.readline()  # printed right before _exit
+    answered = time.monotonic() - t0
+    p.wait(timeout=30)
+    rep = json.loads(line)
+    assert p.returncode == 3 and rep["error"] == "start gate: aborted", rep
+    assert answered < 0.05, answered
+    with open(held) as f:
+        fcntl.flock(f, fcntl.LOCK_EX | fcntl.LOCK_NB)  # released with the process
+
+
 def test_validator_counter_gate_tool_library_from_env(tmp_path):
     # the operator's path: the tool library is named explicitly (validate.py)
     from amdgpu_operator.validator.validate import gate_env

@@ -783,6 +783,56 @@ def test_driver_change_aborts_waiting_start_gates(env):
     assert open(waiting).read() == "abort" and open(released).read() == "go" and open(starting).read() == "abort"
 
 
+def test_driver_change_waits_for_aborted_validators_to_exit(env):
+    """an aborted validator may be in its HIP start ("init") when
+    the driver reloads; the driver container waits until the process has
+    exited (its ``<gate>.held`` lock is free) instead of a fixed pause."""
+    import subprocess
+    import sys
+    import time
+
+    from amdgpu_operator.driver import manager as DM
+
+    os.makedirs(env.validations_dir, exist_ok=True)
+    gate = os.path.join(env.validations_dir, V.START_GATE_PREFIX + "slow")
+    with open(gate, "w") as f:
+        f.write("init")
+    # a process in its "runtime start": holds the lock, reacts to the abort only after 0.6 s
+    child = ("import fcntl,sys,time\nf=open(sys.argv[1]+'.held','a');fcntl.flock(f,fcntl.LOCK_EX)\n"
+             "print('up',flush=True)\nwhile open(sys.argv[1]).read().strip()!='abort': time.sleep(0.001)\n"
+             "time.sleep(0.6)\n")
+    p = subprocess.Popen([sys.executable, "-c", child, gate], stdout=subprocess.PIPE, text=True)
+    assert p.stdout.readline().strip() == "up"
+    t0 = time.monotonic()
+    aborted = DM._release_gated_validators(env)
+    waited = time.monotonic() - t0
+    assert aborted == [V.START_GATE_PREFIX + "slow"] and 0.55 < waited < 4.0
+    assert p.wait(timeout=5) == 0
+    # nothing to abort: no wait at all
+    t0 = time.monotonic()
+    assert DM._release_gated_validators(env) == [] and time.monotonic() - t0 < 0.05
+
+
+def test_kfd_settled_waits_out_exited_processes(env):
+    """A KFD process entry whose PID is gone is a teardown under way: the
+    module still counts it; the wait ends when the entry goes."""
+    import threading
+    import time
+
+    from amdgpu_operator.driver import manager as DM
+
+    kp = os.path.join(env.sysfs_root(), "sys/class/kfd/kfd/proc")
+    os.makedirs(kp, exist_ok=True)
+    os.makedirs(os.path.join(env.sysfs_root(), "proc", "4242"), exist_ok=True)
+    os.makedirs(os.path.join(kp, "4242"))  # alive
+    os.makedirs(os.path.join(kp, "999999"))  # exited, being torn down
+    threading.Timer(0.2, lambda: os.rmdir(os.path.join(kp, "999999"))).start()
+    t0 = time.monotonic()
+    assert DM.wait_kfd_settled(env, time.monotonic() + 3) and 0.15 < time.monotonic() - t0 < 2
+    os.makedirs(os.path.join(kp, "999998"))
+    assert not DM.wait_kfd_settled(env, time.monotonic() + 0.05)
+
+
 def test_cli_simulate_two_nodes_over_http(capsys):
     from amdgpu_operator.cli.main import main
 
