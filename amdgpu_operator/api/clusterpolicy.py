@@ -262,29 +262,36 @@ class WorkloadSpec(_M):
     rcclElems: int = 1 << 24
     xgmiElems: int = 1 << 22
     # Ready-gate floors, for a whole MI355X (256 CUs; a compute partition is
-    # held to its share of the CUs).  Calibrated from the round-2 driver bench
-    # on MI355X (BENCH_r02.json: GEMM 1,238.5 TF/s at 4096^3, HBM copy
-    # 6,235.9 GB/s at 1 GiB): half the GEMM rate, 60 % of the copy rate.  A GPU
-    # held at low clocks, a slow HBM stack or fenced-off CUs fails the node.
-    # The floors apply at gemmN >= 4096 / hbmBytes >= 1 GiB (smaller runs are
-    # launch-bound and report their rate only); 0 = report only.
-    minGemmTflops: float = 620.0
-    minHbmGbps: float = 3700.0
-    # the mfma-rate check (validator steps gemm_fp8 and gemm_fp4, label
-    # amd.com/gpu.validated.mfma-rate): OCP e4m3 and FP4 (e2m1) GEMMs on the
-    # gfx950 f8f6f4 MFMA at mfmaRateGemmN^3, held to minFp8Tflops /
-    # minFp4Tflops (whole MI355X; ~45 % of the rates measured in
-    # profiles/r5_ttr/fp8_step and profiles/r5_fp4) and counted by the gate
+    # held to its share of the CUs).  Derived (tools/floor_calibration.py,
+    # profiles/r6_floors, table in BASELINE.md) from 60 validator runs on an
+    # MI355X at the shipped kernels and sizes: floor = min(0.72 x median,
+    # 0.90 x the slowest healthy run), i.e. ~72 % of the typical rate with a
+    # 10 % margin under the slowest run for clocks and temperature.  A GPU
+    # held at low clocks or a capped power limit, a slow HBM stack or fenced-off
+    # CUs fails the node.  The floors apply at gemmN >= 4096 / hbmBytes >=
+    # 1 GiB (smaller runs are launch-bound and report their rate only); 0 =
+    # report only.
+    minGemmTflops: float = 1080.0   # bf16: median 1,505.5 TF/s
+    minHbmGbps: float = 4270.0      # 1 GiB copy: median 5,944 GB/s
+    # the mfma-rate check (validator steps gemm_fp8, gemm_fp4, gemm_fp6 and
+    # gemm_mxfp4, label amd.com/gpu.validated.mfma-rate): OCP e4m3, FP4 (e2m1),
+    # FP6 (e2m3) and block-scaled MXFP4 GEMMs on the gfx950 f8f6f4 MFMA at
+    # mfmaRateGemmN^3, held to these floors and counted by the gate
     # (SQ_INSTS_VALU_MFMA_MOPS_F8 / _F6F4)
     mfmaRateCheck: bool = True
     # the validator takes multiples of 256 (its 256 x 256 tiles), and >= 512 for fp4
     mfmaRateGemmN: int = Field(default=4096, ge=512, multiple_of=256)
-    minFp8Tflops: float = 1200.0
-    minFp4Tflops: float = 1900.0
+    minFp8Tflops: float = 1940.0    # median 2,706 TF/s
+    minFp4Tflops: float = 3100.0    # median 4,313 TF/s
+    minFp6Tflops: float = 2540.0    # median 3,534 TF/s
+    minMxfp4Tflops: float = 2830.0  # median 3,939 TF/s
     # counter-gate floor on MFMA busy cycles per SIMD-cycle of the counted
-    # GEMM (native/include/gate_policy.h): ~0.49 measured at 4096^3
-    # (profiles/r2_gate/aql_v2.json), floor at 40 % of it
-    minMfmaUtil: float = 0.2
+    # bf16 GEMM (native/include/gate_policy.h): median 0.62 at 4096^3
+    minMfmaUtil: float = 0.44
+    # the same per low-precision data type (their 4096^3 GEMMs keep the MFMA
+    # pipes busy a smaller share of the time: medians 0.46 / 0.30 / 0.29 / 0.29)
+    minMfmaUtilByDtype: dict[str, float] = Field(
+        default_factory=lambda: {"fp8": 0.33, "fp4": 0.21, "fp6": 0.20, "mxfp4": 0.20})
     # N >= 2 throughput floors from the xGMI link model (validator/validate.py
     # fabric_floors): a rank's links to its N-1 peers carry 76 GB/s each per
     # direction on MI355X (KFD io_links), 532 GB/s at N = 8.  RCCL fp32

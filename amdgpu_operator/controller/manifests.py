@@ -341,6 +341,9 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
                       ("--xgmi-read-link-fraction", w.xgmiReadLinkFraction)):
         if val:
             wl_args += [flag, f"{val:g}"]
+    util = {k: v for k, v in w.minMfmaUtilByDtype.items() if w.mfmaRateCheck or k == "bf16"}
+    if util:
+        wl_args += ["--min-mfma-util-by-dtype", ",".join(f"{k}={v:g}" for k, v in sorted(util.items()))]
     wl_args += ["--peer-timeout", f"{w.peerTimeoutSeconds:g}", "--collective-timeout", f"{w.collectiveTimeoutSeconds:g}",
                 "--max-gpu-processes", str(w.maxGpuProcesses)]
     if w.requireXgmiLinks:

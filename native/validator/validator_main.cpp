@@ -259,6 +259,10 @@ struct Args {
   double min_mxfp4_tflops = 0;     // gemm_mxfp4 (size fp4_n)
   double min_hbm_gbps = 0;         // idem
   double min_mfma_util = 0;        // counter-gate floor (gate_policy.h), scaled by the launch's occupancy
+  // per gated data type (AVK_AQL_GATE_*; --min-mfma-util-by-dtype fp8=0.3,...): the
+  // low-precision GEMMs keep their MFMA pipes busy a smaller share of the time
+  // at 4096^3 than the bf16 one; < 0: min_mfma_util
+  double min_util_dtype[AVK_AQL_GATE_DTYPES] = {-1, -1, -1, -1, -1};
   double min_rccl_busbw_gbps = 0;  // fp32 all-reduce busBW floor at world > 1
   double min_xgmi_read_gbps = 0;   // K4 one-shot: peer-read floor at world > 1 (all peers together)
   double timeout_s = 120;
@@ -698,7 +702,10 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
     c.gui = r.values[3];
     c.gui_samples = r.samples[3];
     c.output_matches = same;
-    v = avk::gate_verdict(n, n, n, cus, c, a.min_mfma_util, mops_name);
+    const double util_floor = (dtype >= 0 && dtype < AVK_AQL_GATE_DTYPES && a.min_util_dtype[dtype] >= 0)
+                                  ? a.min_util_dtype[dtype]
+                                  : a.min_mfma_util;
+    v = avk::gate_verdict(n, n, n, cus, c, util_floor, mops_name);
     if (v.ok || !same) break;  // a wrong result is never retried
     reasons += (reasons.empty() ? "" : "; ") + v.reason;
   }
@@ -2008,6 +2015,23 @@ int main(int argc, char** argv) {
     else if (k == "--min-fp6-tflops") a.min_fp6_tflops = atof(v());
     else if (k == "--min-mxfp4-tflops") a.min_mxfp4_tflops = atof(v());
     else if (k == "--min-mfma-util") a.min_mfma_util = atof(v());
+    else if (k == "--min-mfma-util-by-dtype") {
+      // bf16=.., fp8=.., fp4=.., fp6=.., mxfp4=..
+      std::stringstream ss(v());
+      std::string kv;
+      while (std::getline(ss, kv, ',')) {
+        const auto eq = kv.find('=');
+        const std::string name = kv.substr(0, eq);
+        const int d = name == "bf16" ? AVK_AQL_GATE_BF16 : name == "fp8" ? AVK_AQL_GATE_FP8
+                      : name == "fp4" ? AVK_AQL_GATE_FP4 : name == "fp6" ? AVK_AQL_GATE_FP6
+                      : name == "mxfp4" ? AVK_AQL_GATE_MXFP4 : -1;
+        if (d < 0 || eq == std::string::npos) {
+          fprintf(stderr, "amdgpu-validator: --min-mfma-util-by-dtype takes bf16|fp8|fp4|fp6|mxfp4=FLOOR,...\n");
+          return 2;
+        }
+        a.min_util_dtype[d] = atof(kv.c_str() + eq + 1);
+      }
+    }
     else if (k == "--min-rccl-busbw-gbps") a.min_rccl_busbw_gbps = atof(v());
     else if (k == "--min-xgmi-read-gbps") a.min_xgmi_read_gbps = atof(v());
     else if (k == "--peer-timeout") a.peer_timeout_s = atof(v());

@@ -72,6 +72,55 @@ def test_validator_fp8_rate_step_with_counter_gate(tmp_path):
     assert q["perf_ok"] and q["tflops"] > 1.3 * f["tflops"] and q["gate_setup_seconds"] < 0.002
 
 
+def test_validator_fp6_and_mxfp4_rate_steps_with_counter_gate(tmp_path):
+    """VERDICT r5 task 6: the fp6 (e2m3) and block-scaled MXFP4 GEMMs at
+    4096^3 - Freivalds-checked against the decoded (and, for MX, scaled)
+    operands, over a floor, and counted: SQ_INSTS_VALU_MFMA_MOPS_F6F4 ==
+    2N^3/512 with the default kernel's waves."""
+    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm_fp4,gemm_fp6,gemm_mxfp4", "--counter-gate",
+                    "--min-fp6-tflops", "1000", "--min-mxfp4-tflops", "1000", "--min-fp4-tflops", "1000"])
+    assert rc == 0 and rep["ok"], rep
+    steps = {s["name"]: s for s in rep["steps"]}
+    for name, dtype in (("gemm_fp6", "e2m3"), ("gemm_mxfp4", "mxfp4")):
+        g = steps[name]
+        assert g["dtype"] == dtype and g["n"] == 4096 and g["freivalds_rel_err"] < 1e-3, g
+        assert g["counter_gate"] == "pass" and g["gate_attempts"] == 1 and g["gated_output_matches"], g
+        assert g["SQ_INSTS_VALU_MFMA_MOPS_F6F4"] * 512 == 2 * 4096 ** 3 and g["SQ_WAVES"] == (4096 // 256) ** 2 * _WPT
+        assert g["perf_ok"] and g["tflops"] >= 1000 and g["min_tflops"] == 1000
+    # fp6 moves fp8's bytes at the fp4 MFMA rate: well above the fp8 step's rate class
+    assert steps["gemm_fp6"]["tflops"] > 0.6 * steps["gemm_fp4"]["tflops"]
+    assert steps["gemm_mxfp4"]["tflops"] > 0.8 * steps["gemm_fp4"]["tflops"]  # the scales cost little
+
+
+def test_shipped_floors_pass_and_a_floor_above_the_measured_rate_fails(tmp_path):
+    """VERDICT r5 task 5: the Ready gate's shipped floors (WorkloadSpec) pass
+    on a healthy MI355X; the same floors at 1.05 x what this GPU just
+    measured fail the step - so the floors sit near the rate, not at 40 %."""
+    from amdgpu_operator.api.clusterpolicy import WorkloadSpec
+
+    w = WorkloadSpec()
+    floors = ["--min-gemm-tflops", str(w.minGemmTflops), "--min-fp8-tflops", str(w.minFp8Tflops),
+              "--min-fp4-tflops", str(w.minFp4Tflops), "--min-fp6-tflops", str(w.minFp6Tflops),
+              "--min-mxfp4-tflops", str(w.minMxfp4Tflops), "--min-hbm-gbps", str(w.minHbmGbps),
+              "--min-mfma-util", str(w.minMfmaUtil),
+              "--min-mfma-util-by-dtype", ",".join(f"{k}={v}" for k, v in w.minMfmaUtilByDtype.items())]
+    steps = "hip,gemm,gemm_fp8,gemm_fp4,gemm_fp6,gemm_mxfp4,hbm"
+    rc, rep = _run(["--rendezvous", str(tmp_path / "a"), "--steps", steps, "--counter-gate", *floors])
+    assert rc == 0 and rep["ok"], rep
+    got = {s["name"]: s for s in rep["steps"]}
+    for name, floor in (("gemm", w.minGemmTflops), ("gemm_fp8", w.minFp8Tflops), ("gemm_fp4", w.minFp4Tflops),
+                        ("gemm_fp6", w.minFp6Tflops), ("gemm_mxfp4", w.minMxfp4Tflops)):
+        assert got[name]["min_tflops"] == floor and got[name]["tflops"] < floor / 0.60, (name, got[name]["tflops"])
+    assert got["hbm"]["gbps"] < w.minHbmGbps / 0.60
+    over = {"gemm": "--min-gemm-tflops", "gemm_fp8": "--min-fp8-tflops", "gemm_fp4": "--min-fp4-tflops",
+            "gemm_fp6": "--min-fp6-tflops", "gemm_mxfp4": "--min-mxfp4-tflops"}
+    for name, flag in over.items():
+        rc, rep = _run(["--rendezvous", str(tmp_path / name), "--steps", f"hip,{name}",
+                        flag, f"{1.05 * got[name]['tflops']:.1f}"])
+        st = next(s for s in rep["steps"] if s["name"] == name)
+        assert rc != 0 and st["perf_ok"] is False, st
+
+
 def test_counter_gates_pass_first_time_beside_a_process_dispatching_continuously(tmp_path):
     """VERDICT r5 task 3: a second process (the plugin-validation pod's check,
     here looping its kernel for seconds) dispatches on the GPU the whole time

@@ -444,7 +444,8 @@ def test_workload_validation_launch_plan(env):
     # one process per GPU: its kernel checks, the xGMI IPC step and RCCL
     assert len(launched) == 2
     for argv, e, device in launched:
-        assert argv[argv.index("--steps") + 1] == "hip,vecadd,gemm,gemm_fp8,gemm_fp4,mfma,hbm,xgmi,rccl"
+        assert argv[argv.index("--steps") + 1] == ("hip,vecadd,gemm,gemm_fp8,gemm_fp4,gemm_fp6,gemm_mxfp4,mfma,hbm,"
+                                                   "xgmi,rccl")
         assert argv[argv.index("--local-bdf") + 1] == gpus[device].bdf and "--counter-gate" in argv
         # it sees its own GPU first, then its peer (RCCL and IPC need the peer visible)
         assert e["ROCR_VISIBLE_DEVICES"].split(",")[0] == f"GPU-{gpus[device].unique_id:016x}"
@@ -454,7 +455,8 @@ def test_workload_validation_launch_plan(env):
         assert e.get("AMDGPU_VALIDATOR_COUNTERS") is None
     assert sorted(d for _, _, d in launched) == [0, 1]
     names = [s["name"] for s in out["ranks"][0]["steps"]]
-    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "gemm_fp4", "mfma", "hbm", "xgmi", "rccl"]
+    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "gemm_fp4", "gemm_fp6", "gemm_mxfp4", "mfma", "hbm", "xgmi",
+                     "rccl"]
     assert V.read_ready(env, "workload")["world"] == 2
 
     def reset():
@@ -479,7 +481,8 @@ def test_workload_validation_launch_plan(env):
     assert all(len(e["ROCR_VISIBLE_DEVICES"].split(",")) == 2 for _, e in rccl)
     assert all("--counter-gate" in a for a, _ in kernel) and not any("--counter-gate" in a for a, _ in rccl)
     names = [s["name"] for s in out["ranks"][0]["steps"]]
-    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "gemm_fp4", "mfma", "hbm", "xgmi", "rccl"]
+    assert names == ["hip", "vecadd", "gemm", "gemm_fp8", "gemm_fp4", "gemm_fp6", "gemm_mxfp4", "mfma", "hbm", "xgmi",
+                     "rccl"]
 
 
 def test_workload_failure_is_reported(env):
@@ -501,7 +504,7 @@ def test_single_gpu_skips_rccl(tmp_path):
 
     env.launcher = launcher
     out = V.validate_workload(env, [])
-    assert seen == ["hip,vecadd,gemm,gemm_fp8,gemm_fp4,mfma,hbm,xgmi"]
+    assert seen == ["hip,vecadd,gemm,gemm_fp8,gemm_fp4,gemm_fp6,gemm_mxfp4,mfma,hbm,xgmi"]
     assert out["ranks"][0]["steps"][-1]["skipped"].startswith("single GPU")
 
 
@@ -567,9 +570,13 @@ def test_mfma_rate_check_flags_reach_the_validator(tmp_path):
 
     on = args(ref)
     assert on[on.index("--fp8-gemm") + 1] == on[on.index("--fp4-gemm") + 1] == "4096"
-    assert on[on.index("--min-fp8-tflops") + 1] == "1200" and on[on.index("--min-fp4-tflops") + 1] == "1900"
+    assert on[on.index("--min-fp8-tflops") + 1] == "1940" and on[on.index("--min-fp4-tflops") + 1] == "3100"
+    assert on[on.index("--min-fp6-tflops") + 1] == "2540" and on[on.index("--min-mxfp4-tflops") + 1] == "2830"
+    assert on[on.index("--min-mfma-util") + 1] == "0.44"
+    assert on[on.index("--min-mfma-util-by-dtype") + 1] == "fp4=0.21,fp6=0.2,fp8=0.33,mxfp4=0.2"
     off = args(deep_merge(ref, {"validator": {"workload": {"mfmaRateCheck": False}}}))
-    assert "--no-mfma-rate" in off and not {"--min-fp8-tflops", "--min-fp4-tflops", "--fp8-gemm"} & set(off)
+    assert "--no-mfma-rate" in off and not {"--min-fp8-tflops", "--min-fp4-tflops", "--fp8-gemm", "--min-fp6-tflops",
+                                            "--min-mxfp4-tflops", "--min-mfma-util-by-dtype"} & set(off)
 
     root = str(tmp_path / "h1")
     fakesys.build_node(root, 1)

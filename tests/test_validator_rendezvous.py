@@ -204,7 +204,8 @@ def test_validate_flags_translate_to_the_binary(env8, monkeypatch):
         assert a[a.index("--min-rccl-busbw-gbps") + 1] == "12.2"
         assert a[a.index("--min-xgmi-read-gbps") + 1] == "19"
         assert a[a.index("--min-mfma-util") + 1] == "0.2"
-        assert a[a.index("--steps") + 1] == "hip,vecadd,gemm,gemm_fp8,gemm_fp4,mfma,hbm,xgmi,rccl"  # one process per GPU
+        # one process per GPU
+        assert a[a.index("--steps") + 1] == "hip,vecadd,gemm,gemm_fp8,gemm_fp4,gemm_fp6,gemm_mxfp4,mfma,hbm,xgmi,rccl"
 
 
 # ------------------------------------------- process layout and budget ----
