@@ -290,6 +290,9 @@ class WorkloadSpec(_M):
     minMfmaUtil: float = 0.44
     # the same per low-precision data type (their 4096^3 GEMMs keep the MFMA
     # pipes busy a smaller share of the time: medians 0.46 / 0.30 / 0.29 / 0.29)
+    # N7 gate lock (native/include/gate_lock.h): the counted dispatch holds a
+    # per-GPU lock that the plugin pod's check and the RCCL processes share
+    gateLock: bool = True
     minMfmaUtilByDtype: dict[str, float] = Field(
         default_factory=lambda: {"fp8": 0.33, "fp4": 0.21, "fp6": 0.20, "mxfp4": 0.20})
     # N >= 2 throughput floors from the xGMI link model (validator/validate.py

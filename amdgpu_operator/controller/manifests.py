@@ -341,6 +341,8 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
                       ("--xgmi-read-link-fraction", w.xgmiReadLinkFraction)):
         if val:
             wl_args += [flag, f"{val:g}"]
+    if not w.gateLock:
+        wl_args.append("--no-gate-lock")
     util = {k: v for k, v in w.minMfmaUtilByDtype.items() if w.mfmaRateCheck or k == "bf16"}
     if util:
         wl_args += ["--min-mfma-util-by-dtype", ",".join(f"{k}={v:g}" for k, v in sorted(util.items()))]

@@ -458,6 +458,8 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     # the gated kernel processes (the binary does not link the SDK)
     # (the default AQL-packet gate needs no tool library: only --gate-mode sdk)
     sdk_gate = "--counter-gate" in args and _arg_value(args, "--gate-mode") == "sdk"
+    if "--no-gate-lock" in args:
+        env.extra["no_gate_lock"] = True
     counter_env = {**(gate_env() if sdk_gate else {}), **gate_lock_env(env)}
     rccl_single = "--rccl-single-gpu" in args  # validate.py's own flags, not the binary's
     separate = "--rccl-separate-process" in args
@@ -470,7 +472,7 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     xgmi_frac = float(_arg_value(args, "--xgmi-read-link-fraction") or 0.0)
     link_frac = float(_arg_value(args, "--min-xgmi-link-fraction") or 0.9)
     args = _drop_flag(args, "--rccl-single-gpu", "--rccl-shared-process", "--rccl-separate-process",
-                      "--require-xgmi-links", "--dmabuf", "--no-mfma-rate")
+                      "--require-xgmi-links", "--dmabuf", "--no-mfma-rate", "--no-gate-lock")
     args = _drop_value(args, "--rccl-busbw-link-fraction", "--xgmi-read-link-fraction", "--min-xgmi-link-fraction",
                        "--max-gpu-processes")
     steps = _steps_of(args)
@@ -867,6 +869,10 @@ GATE_LOCK_ENV = "AMDGPU_GATE_LOCK_DIR"
 
 
 def gate_lock_env(env: NodeEnv) -> dict:
+    """The lock directory for the node's GPU processes (none with
+    ``validator.workload.gateLock`` off: ``--no-gate-lock``)."""
+    if env.extra.get("no_gate_lock"):
+        return {}
     return {GATE_LOCK_ENV: _pod_results_dir(env)}
 
 
@@ -882,7 +888,8 @@ def _with_result_file(env: NodeEnv, pod: dict, flag: str) -> dict:
     name = pod["metadata"]["name"]
     ctr = pod["spec"]["containers"][0]
     ctr["args"] = list(ctr.get("args") or []) + [flag, os.path.join(d, f"{name}.json")]
-    ctr.setdefault("env", []).append({"name": GATE_LOCK_ENV, "value": d})  # the gate locks (gate_lock_env)
+    if gate_lock_env(env):
+        ctr.setdefault("env", []).append({"name": GATE_LOCK_ENV, "value": d})  # the gate locks (gate_lock_env)
     ctr.setdefault("volumeMounts", []).append({"name": "pod-results", "mountPath": d})
     pod["spec"].setdefault("volumes", []).append({"name": "pod-results",
                                                    "hostPath": {"path": d, "type": "DirectoryOrCreate"}})
@@ -1271,6 +1278,8 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
     wl_procs = 0 if read_ready(env, "workload") is not None else planned_workload_processes(env, workload_args,
                                                                                              budget - 1)
     sdk_gate = "--counter-gate" in workload_args and _arg_value(workload_args, "--gate-mode") == "sdk"
+    if "--no-gate-lock" in workload_args:  # before the plugin thread creates its pods
+        env.extra["no_gate_lock"] = True
     prespawn = with_driver and prespawn_safe(env, sdk_gate)
     if with_driver:
         os.makedirs(env.validations_dir, exist_ok=True)

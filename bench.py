@@ -658,6 +658,11 @@ def one_bring_up(args, n_gpus: int, launcher, workdir: str, fake_gpu: bool, mode
             "gate_attempts": [s.get("gate_attempts") for k in ("gemm", "gemm_fp8", "gemm_fp4", "gemm_fp6",
                                                                 "gemm_mxfp4") for s in steps.get(k, [])],
             "kfd_holders": kfd_holders,
+            # every counted dispatch of the bring-up: verdict, attempts, why a retry was needed, lock wait
+            "gates": [{k: s.get(k) for k in ("name", "device", "counter_gate", "gate_attempts", "gate_retried_after",
+                                             "gate_reason", "mfma_util", "mfma_util_floor", "gate_lock",
+                                             "gate_lock_wait_s") if s.get(k) is not None}
+                      for k2 in ("gemm", "gemm_fp8", "gemm_fp4", "gemm_fp6", "gemm_mxfp4") for s in steps.get(k2, [])],
             "hbm_gbps": [s.get("gbps") for s in steps.get("hbm", [])],
             "xgmi_read_gbps": [s.get("read_gbps") for s in steps.get("xgmi", [])],
             "rccl_busbw_gbps": [s.get("busbw_gbps") for s in steps.get("rccl", [])],

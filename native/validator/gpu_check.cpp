@@ -32,6 +32,7 @@
 
 #include "gate_lock.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -154,15 +155,19 @@ std::string agent_bdf(hsa_agent_t gpu) {
 }
 
 // one device: queue, dispatch, verify; appends its step records.  The GPU's
-// gate lock (gate_lock.h) is held shared from the code-object load to the
-// kernel's completion: a counter gate of the validator on this GPU never
-// counts this pod's upload or kernel.  `loop_s` > 0 (tests): keep
-// dispatching the kernel for that long, the lock taken per dispatch.
+// gate lock (gate_lock.h) is held shared from the code-object load through
+// the teardown of the queue and the executable (freeing the code object's
+// VRAM starts the driver's wipe of it, GPU work a counted window must not
+// see either): a counter gate of the validator on this GPU never counts this
+// pod's upload, kernel or clean-up.  `loop_s` > 0 (tests): keep dispatching
+// the kernel for that long, the lock released between dispatches.
 bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std::vector<char>& co, int n,
-                  double timeout_s, std::vector<std::string>* steps, std::string* error, double loop_s = 0) {
+                  double timeout_s, std::vector<std::string>* steps, std::string* error, double loop_s,
+                  avk::GateLock* held) {
   const auto t0 = Clock::now();
   const std::string bdf = agent_bdf(gpu);
-  avk::GateLock lock(bdf, avk::GateLock::kShared, 2.0);
+  avk::GateLock& lock = *held;
+  lock = avk::GateLock(bdf, avk::GateLock::kShared, 2.0);
   hsa_code_object_reader_t reader{0};
   hsa_executable_t exe{0};
   hsa_queue_t* queue = nullptr;
@@ -246,7 +251,6 @@ bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std:
       lock = avk::GateLock(bdf, avk::GateLock::kShared, 2.0);
       hsa_signal_store_relaxed(done, 1);
     }
-    lock.release();
     finished = true;
     int bad = 0;
     for (int i = 0; i < n; ++i)
@@ -271,6 +275,7 @@ bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std:
     if (reader.handle) hsa_code_object_reader_destroy(reader);
     for (void* q : allocs) hsa_amd_memory_pool_free(q);
   }
+  lock.release();  // after the teardown above
   return ok;
 }
 
@@ -305,6 +310,7 @@ int main(int argc, char** argv) {
   std::string error;
   bool ok = true;
   int ngpu = 0;
+  std::vector<avk::GateLock> dev_locks;  // each GPU's gate lock (check_device)
   double hsa_init_s = -1;
   try {
     const auto th = Clock::now();
@@ -333,12 +339,14 @@ int main(int argc, char** argv) {
     std::vector<std::vector<std::string>> dev_steps(ngpu);
     std::vector<std::string> dev_error(ngpu);
     std::vector<char> dev_ok(ngpu, 0);
+    dev_locks.resize(ngpu);
     std::vector<std::thread> threads;
     threads.reserve(ngpu);
     for (int d = 0; d < ngpu; ++d)
       threads.emplace_back([&, d] {
         try {  // nothing may leave a thread (std::terminate): an unexpected error fails this device only
-          dev_ok[d] = check_device(d, ag.gpus[d], pool, co, elems, timeout_s, &dev_steps[d], &dev_error[d], loop_s);
+          dev_ok[d] = check_device(d, ag.gpus[d], pool, co, elems, timeout_s, &dev_steps[d], &dev_error[d], loop_s,
+                                   &dev_locks[d]);
         } catch (const std::exception& e) {
           dev_error[d] = "device " + std::to_string(d) + ": " + e.what();
         } catch (...) {
@@ -386,7 +394,12 @@ int main(int argc, char** argv) {
     }
   }
   // the report is the result: the runtime's teardown is left to the exit
-  // (AMDGPU_GPU_CHECK_SHUTDOWN=1: hsa_shut_down first - tools/pod_exit_probe.py A/B)
-  if (const char* e = getenv("AMDGPU_GPU_CHECK_SHUTDOWN"); e && e[0] == '1') hsa_shut_down();
+  // (AMDGPU_GPU_CHECK_SHUTDOWN=1: hsa_shut_down first - tools/pod_exit_probe.py
+  // A/B).  Holding the gate locks through hsa_shut_down kept its queue
+  // unmaps out of the validator's counted windows, but made the first gate
+  // wait 21-42 ms for it (+30 ms time-to-Ready, profiles/r6_gate_lock): the
+  // gate retries a window with evidence of preemption instead
+  // (validator_main.cpp aql_gate)
+  if (const char* e = getenv("AMDGPU_GPU_CHECK_SHUTDOWN"); ok && e && e[0] == '1') hsa_shut_down();
   _exit(ok ? 0 : 1);
 }

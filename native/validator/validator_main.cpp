@@ -589,22 +589,44 @@ Step step_vecadd(const Args& args, hipStream_t st) {
   return s;
 }
 
+// Device buffers released only when the process ends.  Freeing VRAM makes
+// the kernel driver wipe it (wipe-on-release, an SDMA fill at ~80 GB/s), and
+// the GPU's other page-table work waits behind that: a 2 GiB hipFree delays
+// an HSA queue creation right after it from 5 ms to 32 ms, in any process on
+// the GPU.  The plugin-validation pod's queue creation and code-object load,
+// which run while the validator ends, took 10-30 ms longer in about half the
+// bring-ups after the HBM step freed its 2 GiB; kept to the process's end,
+// in none of 32 (profiles/r5_init/wipe).  The GEMM steps keep theirs too: a
+// wipe of one step's buffers ran beside the next step's counted dispatch and
+// took its MFMA utilisation below the gate's floor (profiles/r6_floors).
+std::mutex g_release_m;  // the devices of one process run their steps on threads of their own
+std::vector<void*> g_release_at_exit;
+void release_at_exit(void* p) {
+  std::lock_guard<std::mutex> l(g_release_m);
+  g_release_at_exit.push_back(p);
+}
+
 // N7 on AQL profiling packets (prof/aql_gate.cpp): one more dispatch of the
 // same GEMM on a private queue between PM4 start/stop packets.  Its output is
 // checked against the HIP path's (checksum of C before and after, C zeroed in
 // between), so the counted dispatch is the validated computation, not a stand-in.
-// The hardware counters are device-wide: a kernel another process runs on the
-// GPU during the counted dispatch adds its waves and MFMA ops, and the exact
-// invariants fail.  The operator's own GPU work on this GPU - the
-// plugin-validation pod's code-object upload and kernel, the validator's RCCL
-// collectives - takes the GPU's gate lock shared (gate_lock.h), and the
-// counted dispatch holds it exclusively: those can no longer land in the
-// counted window (round 5's retry loop met exactly that, 1 bring-up in 75,
-// profiles/r5_final/gate_retry).  What the lock cannot order - a co-tenant
-// process of another party during a revalidation - gets one more attempt
-// after a 2 ms pause; a wrong result is never retried, and a defective GPU
-// fails both.
-constexpr int kGateAttempts = 2;
+// The counters are device-wide, and the counted window is not alone on the
+// GPU: another process creating or destroying a queue makes the scheduler
+// unmap and remap every queue, preempting ours - its waves are saved and
+// restored (SQ_WAVES above tiles x waves, measured 1,286 for 1,024), or its
+// dispatch waits while the GPU stays busy (MFMA utilisation ~0.13 for a
+// ~0.56 GEMM).  Both were seen in bring-ups right after the plugin pod's
+// runtime teardown at its exit (profiles/r6_gate_lock).  So an attempt is
+// retried only on that signature - the output matched, the MFMA op count
+// is exact, and either the waves exceed the launch's (restored waves) or
+// the utilisation is under its floor - after a 2 ms pause, kGateAttempts
+// in all; a wrong output, a wrong op count or missing waves (work dropped
+// or duplicated) fail at once, and a GPU whose own utilisation is low fails
+// every attempt.  The operator's own GPU work on this GPU (the
+// plugin-validation pod's code-object load, queue and kernel; the
+// validator's RCCL collectives) also takes the GPU's gate lock shared
+// (gate_lock.h) while the counted dispatch holds it exclusively.
+constexpr int kGateAttempts = 4;
 
 std::string pci_bus(int device) {
   char bus[64] = {0};
@@ -706,8 +728,12 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
                                   ? a.min_util_dtype[dtype]
                                   : a.min_mfma_util;
     v = avk::gate_verdict(n, n, n, cus, c, util_floor, mops_name);
-    if (v.ok || !same) break;  // a wrong result is never retried
-    reasons += (reasons.empty() ? "" : "; ") + v.reason;
+    if (v.ok) break;
+    // the preemption signature (comment above): anything else is the GPU's own
+    const bool preempted = same && c.mops == v.expected_mops &&
+                           (c.waves > v.expected_waves || (c.waves == v.expected_waves && v.mfma_util < v.util_floor));
+    reasons += (reasons.empty() ? "" : "; ") + v.reason + fmt(" (waves %.0f)", c.waves);
+    if (!preempted) break;
   }
   attempt = std::min(attempt, kGateAttempts);
   (void)hipFree(cs);
@@ -794,7 +820,7 @@ Step step_gemm(const Args& a, hipStream_t st, int cus) {
     const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) (void)hipFree(p);
+    for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) release_at_exit(p);
     const double floor = gemm_floor(a, n, cus);
     const bool perf_ok = floor <= 0 || tflops >= floor;
     s.ok = numerics_ok && gate_ok && perf_ok;
@@ -854,7 +880,7 @@ Step step_gemm(const Args& a, hipStream_t st, int cus) {
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
-  for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) (void)hipFree(p);
+  for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z}) release_at_exit(p);
   const double floor = gemm_floor(a, n, cus);
   const bool perf_ok = floor <= 0 || tflops >= floor;
   s.ok = numerics_ok && gate_ok && perf_ok;
@@ -1007,7 +1033,7 @@ Step step_gemm_lowp(const Args& a, hipStream_t st, int cus, const LowPrecision& 
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   for (void* p : {A, B, C16, (void*)C32, (void*)x, (void*)y1, (void*)y2, (void*)z, SA, SB})
-    if (p) (void)hipFree(p);
+    if (p) release_at_exit(p);  // not hipFree: see g_release_at_exit
   const double floor_full = dt == AVK_AQL_GATE_FP4     ? a.min_fp4_tflops
                             : dt == AVK_AQL_GATE_FP6   ? a.min_fp6_tflops
                             : dt == AVK_AQL_GATE_MXFP4 ? a.min_mxfp4_tflops
@@ -1027,21 +1053,6 @@ Step step_gemm_fp8(const Args& a, hipStream_t st, int cus) { return step_gemm_lo
 Step step_gemm_fp4(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kFp4); }
 Step step_gemm_fp6(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kFp6); }
 Step step_gemm_mxfp4(const Args& a, hipStream_t st, int cus) { return step_gemm_lowp(a, st, cus, kMxFp4); }
-
-// Device buffers released only when the process ends.  Freeing VRAM makes
-// the kernel driver wipe it (wipe-on-release, an SDMA fill at ~80 GB/s), and
-// the GPU's other page-table work waits behind that: a 2 GiB hipFree delays
-// an HSA queue creation right after it from 5 ms to 32 ms, in any process on
-// the GPU.  The plugin-validation pod's queue creation and code-object load,
-// which run while the validator ends, took 10-30 ms longer in about half the
-// bring-ups after the HBM step freed its 2 GiB; kept to the process's end,
-// in none of 32 (profiles/r5_init/wipe).
-std::mutex g_release_m;  // the devices of one process run their steps on threads of their own
-std::vector<void*> g_release_at_exit;
-void release_at_exit(void* p) {
-  std::lock_guard<std::mutex> l(g_release_m);
-  g_release_at_exit.push_back(p);
-}
 
 Step step_hbm(const Args& a, hipStream_t st, int cus) {
   auto t0 = Clock::now();
