@@ -607,7 +607,8 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
 FAILED_SUFFIX = "-failed"
 _RATE_KEYS = ("tflops", "min_tflops", "gbps", "min_gbps", "busbw_gbps", "min_busbw_gbps", "algbw_gbps", "bytes",
               "peer_read_gbps", "min_peer_read_gbps", "perf_ok", "counter_gate", "mismatches", "max_abs_err",
-              "freivalds_rel_err", "comm_init_s", "world", "device", "error", "failed")
+              "freivalds_rel_err", "comm_init_s", "world", "device", "error", "failed", "gate_reason",
+              "gate_retried_after", "gate_attempts", "mfma_util", "mfma_util_floor", "n")
 
 
 def write_failure(env: NodeEnv, step: str, payload: dict) -> str:

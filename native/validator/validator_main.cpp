@@ -628,6 +628,16 @@ void release_at_exit(void* p) {
 // (gate_lock.h) while the counted dispatch holds it exclusively.
 constexpr int kGateAttempts = 4;
 
+// The MFMA-utilisation floor of a counted GEMM of size n and gated data type:
+// calibrated at 4096^3 (profiles/r6_floors) and applied from there on, like
+// the TF/s floors (gemm_floor); a smaller GEMM is launch-bound (1024^3 keeps
+// the pipes ~2.6 % busy) and its gate checks the exact invariants only.
+double gate_util_floor(const Args& a, int n, int dtype) {
+  if (n < 4096) return 0.0;
+  return (dtype >= 0 && dtype < AVK_AQL_GATE_DTYPES && a.min_util_dtype[dtype] >= 0) ? a.min_util_dtype[dtype]
+                                                                                      : a.min_mfma_util;
+}
+
 std::string pci_bus(int device) {
   char bus[64] = {0};
   HIP_OK(hipDeviceGetPCIBusId(bus, sizeof(bus), device));
@@ -724,9 +734,7 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
     c.gui = r.values[3];
     c.gui_samples = r.samples[3];
     c.output_matches = same;
-    const double util_floor = (dtype >= 0 && dtype < AVK_AQL_GATE_DTYPES && a.min_util_dtype[dtype] >= 0)
-                                  ? a.min_util_dtype[dtype]
-                                  : a.min_mfma_util;
+    const double util_floor = gate_util_floor(a, n, dtype);
     v = avk::gate_verdict(n, n, n, cus, c, util_floor, mops_name);
     if (v.ok) break;
     // the preemption signature (comment above): anything else is the GPU's own
@@ -866,7 +874,7 @@ Step step_gemm(const Args& a, hipStream_t st, int cus) {
       c.waves = waves;
       c.gui = gui;
       c.gui_samples = std::max(1, cus / 32);
-      const avk::GateVerdict v = avk::gate_verdict(n, n, n, cus, c, a.min_mfma_util);
+      const avk::GateVerdict v = avk::gate_verdict(n, n, n, cus, c, gate_util_floor(a, n, AVK_AQL_GATE_BF16));
       gate_ok = disp == 1 && v.ok;
       gate_json = fmt("\"counter_gate\": \"%s\", \"gate_mode\": \"sdk\", \"dispatches\": %d, "
                       "\"SQ_INSTS_VALU_MFMA_MOPS_BF16\": %.0f, "
