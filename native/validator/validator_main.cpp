@@ -619,8 +619,9 @@ void release_at_exit(void* p) {
 // runtime teardown at its exit (profiles/r6_gate_lock).  So an attempt is
 // retried only on that signature - the output matched, the MFMA op count
 // is exact, and either the waves exceed the launch's (restored waves) or
-// the utilisation is under its floor - after a 2 ms pause, kGateAttempts
-// in all; a wrong output, a wrong op count or missing waves (work dropped
+// the utilisation is under its floor - after a pause (2, 4, 8 ms: queue
+// creations come in bursts when many GPU processes start), kGateAttempts in
+// all; a wrong output, a wrong op count or missing waves (work dropped
 // or duplicated) fail at once, and a GPU whose own utilisation is low fails
 // every attempt.  The operator's own GPU work on this GPU (the
 // plugin-validation pod's code-object load, queue and kernel; the
@@ -701,7 +702,7 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
   const char* trunc = getenv("AMDGPU_GATE_TEST_TRUNCATE_K");
   const int k_counted = (trunc && trunc[0] == '1' && n >= 512) ? n / 2 : n;
   for (attempt = 1; attempt <= kGateAttempts; ++attempt) {
-    if (attempt > 1) std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    if (attempt > 1) std::this_thread::sleep_for(std::chrono::milliseconds(1 << (attempt - 1)));  // 2, 4, 8 ms
     HIP_OK(hipMemsetAsync(cs, 0, 16, st));
     AVK_OK(avk_checksum(C16, (int64_t)n * n * 2, cs, st));
     HIP_OK(hipMemsetAsync(C16, 0, (size_t)n * n * 2, st));
