@@ -215,264 +215,7 @@ __device__ unsigned long long g_stamps[kStampBlocks * 8 * kStampSlices * kStampP
 #endif
 
 #if AVK_GEMM_LAB
-// Round-1/2 GEMM experiments (variants 0-5, 7-9 of avk_gemm_bf16_nt_variant):
-// built only into the tools library (make -C native lab ->
-// _native/lab/libamdgpu_validator_lab.so) for A/B runs (tools/kernel_bench.py).
-// The shipped library carries the default kernel (variant 6, the 8-phase one below).
-__device__ __forceinline__ void gemm_stage(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                                           int K, int m0, int n0, int k0, char* stage_base, int wave,
-                                           int lane) {
-  using namespace gemm;
-  const int rsub = lane >> 3;
-  const int pc = lane & 7;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = wave * 4 + i;  // 1 KiB piece, 0..31
-    const int r = p * 8 + rsub;  // tile row 0..255
-    const int lc = pc ^ ((r >> 1) & 7);
-    const __bf16* srcA = A + (size_t)(m0 + r) * K + k0 + lc * 8;
-    const __bf16* srcB = Bt + (size_t)(n0 + r) * K + k0 + lc * 8;
-    __builtin_amdgcn_global_load_lds(srcA, (lds_void_ptr)(stage_base + p * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(srcB, (lds_void_ptr)(stage_base + TILE_BYTES + p * 1024), 16, 0, 0);
-  }
-}
-
-template <bool OUT_F32>
-__global__ __launch_bounds__(gemm::NTHR, 2) void gemm_bf16_nt_kernel(const __bf16* __restrict__ A,
-                                                                     const __bf16* __restrict__ Bt,
-                                                                     void* __restrict__ Cv, int M, int N,
-                                                                     int K) {
-  using namespace gemm;
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2;  // 0..1
-  const int wn = wave & 3;   // 0..3
-
-  // XCD-aware, bijective block remap: blocks b and b+8 share an XCD under the
-  // observed round-robin dispatch; give each XCD a contiguous run of tiles.
-  const int tiles_m = M / BM, tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int xcd = bid % kNumXcd;
-  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
-  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
-  // grouped ordering: GROUP_M tile rows swept column by column
-  const int per_group = GROUP_M * tiles_n;
-  const int group = wgid / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
-  const int in_group = wgid % per_group;
-  const int tm = first_m + in_group % gsize;
-  const int tn = in_group / gsize;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK;
-  gemm_stage(A, Bt, K, m0, n0, 0, smem, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // per-lane fragment offsets (row = lane&15 inside a 16-row tile; swizzle
-  // term (row>>1)&7 only depends on lane because tile rows are multiples of 16)
-  const int frow = lane & 15;
-  const int fsw = (frow >> 1) & 7;
-  const int fq = lane >> 4;  // which 8-element k group
-  const int a_row_base = (wm * 128 + frow) * 128;
-  const int b_row_base = (wn * 64 + frow) * 128;
-
-  for (int t = 0; t < nk; ++t) {
-    char* cur = smem + (t & 1) * STAGE_BYTES;
-    if (t + 1 < nk) gemm_stage(A, Bt, K, m0, n0, (t + 1) * BK, smem + ((t + 1) & 1) * STAGE_BYTES, wave, lane);
-    const char* As = cur;
-    const char* Bs = cur + TILE_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int pcol = ((s * 4 + fq) ^ fsw) * 16;
-      bf16x8 a[8], b[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + b_row_base + j * 16 * 128 + pcol);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + a_row_base + i * 16 * 128 + pcol);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // epilogue: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + reg
-  const int crow0 = m0 + wm * 128 + fq * 4;
-  const int ccol0 = n0 + wn * 64 + frow;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const size_t idx = (size_t)(crow0 + i * 16 + r) * N + ccol0 + j * 16;
-        if constexpr (OUT_F32)
-          reinterpret_cast<float*>(Cv)[idx] = acc[i][j][r];
-        else
-          reinterpret_cast<__bf16*>(Cv)[idx] = (__bf16)acc[i][j][r];
-      }
-}
-
-// ------------------------------------------ K2 GEMM, 4-slot LDS-DMA ring ----
-//
-// Same 256x256 block tile, 8 waves (2M x 4N, 128x64 per wave, 16x16x32 bf16
-// MFMA) as above, but the K loop is a 4-slot ring of 32-deep slices
-// (32 KiB per slot: A 256x32 + B 256x32, 128 KiB total).  Loads for slice
-// t+3 are issued right after the barrier of slice t, so every slice has ~3
-// compute periods to land; each iteration waits only for its own slice with
-// a COUNTED vmcnt (never 0 in the steady state) and passes ONE raw s_barrier
-// - no __syncthreads(), whose fence would drain every LDS-DMA in flight
-// (cdna_hip_programming.md §5 "Pipelining across barriers").
-//   RAW: slice t is read after every wave's vmcnt for it + the barrier.
-//   WAR: slot (t+3)%4 == (t-1)%4 was last read in iteration t-1; every wave
-//        consumed those ds_reads (its MFMAs used them) before the barrier.
-// 64-B LDS rows: the bank swizzle is physical 16-B chunk = chunk ^ (3*((row>>3)&1)),
-// applied to the glds SOURCE address and to the ds_read_b128 address; it puts
-// each 16-lane ds_read_b128 group on 16 distinct slots (conflict-free).
-namespace gring {
-constexpr int BM = 256, BN = 256, BK = 32, NTHR = 512, SLOTS = 4;
-constexpr int OP_BYTES = BM * BK * 2;          // 16 KiB
-constexpr int SLOT_BYTES = 2 * OP_BYTES;       // 32 KiB
-constexpr int LDS_BYTES = SLOTS * SLOT_BYTES;  // 128 KiB
-constexpr int GROUP_M = 4;
-}  // namespace gring
-
-__device__ __forceinline__ void ring_stage(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, int K,
-                                           int m0, int n0, int k0, char* slot, int wave, int lane) {
-  using namespace gring;
-  const int rsub = lane >> 2;  // 16 rows of 64 B per 1 KiB piece
-  const int pc = lane & 3;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int p = wave * 2 + i;  // piece 0..15
-    const int r = p * 16 + rsub;
-    const int lc = pc ^ (((r >> 3) & 1) * 3);
-    __builtin_amdgcn_global_load_lds(A + (size_t)(m0 + r) * K + k0 + lc * 8, (lds_void_ptr)(slot + p * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(Bt + (size_t)(n0 + r) * K + k0 + lc * 8,
-                                     (lds_void_ptr)(slot + OP_BYTES + p * 1024), 16, 0, 0);
-  }
-}
-
-template <bool OUT_F32>
-__global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_ring_kernel(const __bf16* __restrict__ A,
-                                                                          const __bf16* __restrict__ Bt,
-                                                                          void* __restrict__ Cv, int M, int N,
-                                                                          int K) {
-  using namespace gring;
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-
-  const int tiles_m = M / BM, tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int xcd = bid % kNumXcd;
-  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
-  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
-  const int per_group = GROUP_M * tiles_n;
-  const int first_m = (wgid / per_group) * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
-  const int in_group = wgid % per_group;
-  const int m0 = (first_m + in_group % gsize) * BM;
-  const int n0 = (in_group / gsize) * BN;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK;
-#pragma unroll
-  for (int s = 0; s < 3; ++s)
-    if (s < nk) ring_stage(A, Bt, K, m0, n0, s * BK, smem + s * SLOT_BYTES, wave, lane);
-
-  const int frow = lane & 15;
-  const int pcol = ((lane >> 4) ^ (((frow >> 3) & 1) * 3)) * 16;
-  const int a_off = (wm * 128 + frow) * 64 + pcol;
-  const int b_off = OP_BYTES + (wn * 64 + frow) * 64 + pcol;
-
-  for (int t = 0; t < nk; ++t) {
-    const int ahead = min(2, nk - 1 - t);  // slices issued after t (wave-uniform)
-    if (ahead == 2)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (t + 3 < nk) ring_stage(A, Bt, K, m0, n0, (t + 3) * BK, smem + ((t + 3) & 3) * SLOT_BYTES, wave, lane);
-    const char* slot = smem + (t & 3) * SLOT_BYTES;
-    bf16x8 a[8], b[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(slot + b_off + j * 1024);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(slot + a_off + i * 1024);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-
-  const int crow0 = m0 + wm * 128 + (lane >> 4) * 4;
-  const int ccol0 = n0 + wn * 64 + frow;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const size_t idx = (size_t)(crow0 + i * 16 + r) * N + ccol0 + j * 16;
-        if constexpr (OUT_F32)
-          reinterpret_cast<float*>(Cv)[idx] = acc[i][j][r];
-        else
-          reinterpret_cast<__bf16*>(Cv)[idx] = (__bf16)acc[i][j][r];
-      }
-}
-
-// ---------------------------- K2 GEMM, 4-slot ring + two-group ping-pong ----
-//
-// The ring above keeps both waves of a SIMD in lockstep: one barrier per slice
-// realigns them, so both burst their LDS reads at the same time and then both
-// run MFMAs - the SIMD's matrix pipe idles through every read burst.  Here the
-// 8 waves form two groups (waves 0-3 = rows 0..127, waves 4-7 = rows 128..255;
-// one wave of each group per SIMD) and every slice is two barrier-separated
-// segments, R (issue the slice t+3 LDS-DMA, 12 ds_read_b128, lgkmcnt(0)) and
-// M (32 MFMAs).  Group 1 passes one extra barrier up front, so it runs exactly
-// one segment behind: in every segment one wave of each SIMD computes while
-// its partner reads (MI355X_MICROARCH.md "Two waves per SIMD").
-//
-// Segment s lies between workgroup barriers s and s+1.  Group 0 runs R(t) in
-// segment 2t and M(t) in 2t+1; group 1 runs R(t) in 2t+1 and M(t) in 2t+2.
-//   RAW  slice t+1 is first read in segment 2t+2; every wave waits for its own
-//        share with a counted vmcnt before barrier 2t+2 (group 0 after M(t),
-//        group 1 after R(t), both after issuing slice t+3).
-//   WAR  slot (t+3)%4 held slice t-1, whose last reads (group 1, segment
-//        2t-1) completed (lgkmcnt(0)) before barrier 2t; slice t+3 is issued
-//        in segments 2t / 2t+1.
-// Both groups pass 2*nk+1 barriers.  Operands are swapped in the MFMA
-// (D = B-frag x A-frag = C^T), so each lane ends up with 4 consecutive
-// COLUMNS of one output row: one 16-B (fp32) / 8-B (bf16) store per fragment.
+#include "gemm_lab_1.inc"
 #endif  // AVK_GEMM_LAB
 
 __device__ __forceinline__ void wg_barrier() {
@@ -484,316 +227,7 @@ __device__ __forceinline__ void wg_barrier() {
 }
 
 #if AVK_GEMM_LAB
-__device__ __forceinline__ void wait_slice_vmcnt(int ahead) {
-  if (ahead >= 2)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (ahead == 1)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// LOAD_IN_M moves the slice t+3 LDS-DMA out of R(t) into M(t), one piece
-// after every two MFMA rows: a piece costs ~60 issue cycles among bare MFMAs
-// but 100-185 inside a read burst (MI355X_MICROARCH.md constants table), and
-// R is the segment the partner's MFMAs wait for.  The refill is then issued
-// in segments 2t+1 (group 0) / 2t+2 (group 1), still after barrier 2t, and is
-// never skipped (past the last slice it re-reads slice nk-1 into a slot no one
-// reads again), so the waits are constant: group 0 after M(t) has slices t+2,
-// t+3 newer than t+1 in flight -> vmcnt(8); group 1 after R(t) has issued only
-// up to t+2 -> vmcnt(4).
-//
-// NSLOT = 5 (LOAD_IN_M only) deepens the ring to the full 160 KiB of LDS:
-// slice t+4 is refilled in M(t) and every wait allows one more slice in flight.
-template <bool OUT_F32, bool LOAD_IN_M, int NSLOT = 4>
-__global__ __launch_bounds__(gring::NTHR, 2) void gemm_bf16_nt_pp_kernel(const __bf16* __restrict__ A,
-                                                                        const __bf16* __restrict__ Bt,
-                                                                        void* __restrict__ Cv, int M, int N,
-                                                                        int K) {
-  using namespace gring;
-  static_assert(NSLOT == 4 || (NSLOT == 5 && LOAD_IN_M), "ring depth");
-  constexpr int AHEAD = NSLOT - 1;  // slices in flight beyond the one being read
-  __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const bool lag = wm == 1;  // wave-uniform
-
-  const int tiles_m = M / BM, tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int xcd = bid % kNumXcd;
-  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
-  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
-  const int per_group = GROUP_M * tiles_n;
-  const int first_m = (wgid / per_group) * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
-  const int in_group = wgid % per_group;
-  const int m0 = (first_m + in_group % gsize) * BM;
-  const int n0 = (in_group / gsize) * BN;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK;
-  if constexpr (LOAD_IN_M) {
-#pragma unroll
-    for (int s = 0; s < AHEAD; ++s)
-      ring_stage(A, Bt, K, m0, n0, min(s, nk - 1) * BK, smem + s * SLOT_BYTES, wave, lane);
-    if constexpr (AHEAD == 4)
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  } else {
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-      if (s < nk) ring_stage(A, Bt, K, m0, n0, s * BK, smem + s * SLOT_BYTES, wave, lane);
-    wait_slice_vmcnt(min(2, nk - 1));
-  }
-  wg_barrier();
-  if (lag) wg_barrier();
-
-  const int frow = lane & 15;
-  const int pcol = ((lane >> 4) ^ (((frow >> 3) & 1) * 3)) * 16;
-  const int a_off = (wm * 128 + frow) * 64 + pcol;
-  const int b_off = OP_BYTES + (wn * 64 + frow) * 64 + pcol;
-  const int rsub = lane >> 2, pc = lane & 3;
-
-  for (int t = 0; t < nk; ++t) {
-    AVK_STAMP(t, 0);
-    // ---- R(t)
-    if (!LOAD_IN_M && t + 3 < nk)
-      ring_stage(A, Bt, K, m0, n0, (t + 3) * BK, smem + ((t + 3) & 3) * SLOT_BYTES, wave, lane);
-    const char* slot = smem + (t % NSLOT) * SLOT_BYTES;
-    bf16x8 a[8], b[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(slot + b_off + j * 1024);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(slot + a_off + i * 1024);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    AVK_STAMP(t, 1);
-    if (lag) {
-      if constexpr (LOAD_IN_M && AHEAD == 4)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if constexpr (LOAD_IN_M)
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else
-        wait_slice_vmcnt(min(2, nk - 2 - t));
-    }
-    AVK_STAMP(t, 2);
-    wg_barrier();
-    AVK_STAMP(t, 3);
-    // ---- M(t)
-    char* sslot = smem + ((t + AHEAD) % NSLOT) * SLOT_BYTES;
-    const int kload = min(t + AHEAD, nk - 1) * BK;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-      if (LOAD_IN_M && (i & 1)) {  // piece k = i>>1: operand k>>1, rows ((wave*2 + (k&1))*16 + rsub)
-        const int k = i >> 1;
-        const int p = wave * 2 + (k & 1);
-        const int r = p * 16 + rsub;
-        const int lc = pc ^ (((r >> 3) & 1) * 3);
-        const __bf16* src = (k < 2 ? A + (size_t)(m0 + r) * K : Bt + (size_t)(n0 + r) * K) + kload + lc * 8;
-        __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)(sslot + (k < 2 ? 0 : OP_BYTES) + p * 1024), 16, 0, 0);
-      }
-    }
-    if constexpr (LOAD_IN_M) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);  // two MFMA rows
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one LDS-DMA piece
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    AVK_STAMP(t, 4);
-    if (!lag) {
-      if constexpr (LOAD_IN_M && AHEAD == 4)
-        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else if constexpr (LOAD_IN_M)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else
-        wait_slice_vmcnt(min(2, nk - 2 - t));
-    }
-    AVK_STAMP(t, 5);
-    if (!(lag && t == nk - 1)) wg_barrier();
-  }
-  if constexpr (LOAD_IN_M) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy refills drained
-
-  // acc[i][j] = C^T fragment: lane holds C[i*16 + (lane&15)][j*16 + (lane>>4)*4 + 0..3]
-  const int crow = m0 + wm * 128 + frow;
-  const int ccol = n0 + wn * 64 + (lane >> 4) * 4;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const size_t idx = (size_t)(crow + i * 16) * N + ccol + j * 16;
-      if constexpr (OUT_F32) {
-        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + idx) = acc[i][j];
-      } else {
-        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        bf16x4 v = {(__bf16)acc[i][j][0], (__bf16)acc[i][j][1], (__bf16)acc[i][j][2], (__bf16)acc[i][j][3]};
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(Cv) + idx) = v;
-      }
-    }
-}
-
-// ------------------- K2 GEMM, 4 waves x 128x128, one wave per SIMD --------
-//
-// Counters on the 8-wave kernels (profiles/r1_gemm) show the LDS read stream
-// as the cost: a 128x64 wave tile re-reads 12 KiB per 32 MFMAs.  A 128x128 wave
-// tile halves that (16 ds_read_b128 per 64 MFMAs), at the price of 256
-// accumulator registers - so one wave per SIMD (4 per workgroup), which then
-// has no partner to hide its reads behind: it software-pipelines them itself,
-// reading slice t+1's fragments into a second register set while its MFMAs
-// consume slice t's.  Same 4-slot ring (BK = 32) and source-side swizzle as
-// above; one counted vmcnt + one barrier per slice:
-//   top of iteration j: own share of slice j+1 landed (vmcnt), barrier ->
-//   every share landed AND every wave's reads of slice j-1 (issued in
-//   iteration j-2, consumed by iteration j-1's MFMAs) retired, so slot
-//   (j+3)%4 == (j-1)%4 may be refilled.
-namespace gw4 {
-constexpr int BM = 256, BN = 256, BK = 32, NTHR = 256, SLOTS = 4;
-constexpr int OP_BYTES = BM * BK * 2;          // 16 KiB
-constexpr int SLOT_BYTES = 2 * OP_BYTES;       // 32 KiB
-constexpr int LDS_BYTES = SLOTS * SLOT_BYTES;  // 128 KiB
-constexpr int GROUP_M = 4;
-}  // namespace gw4
-
-__device__ __forceinline__ void w4_stage(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, int K,
-                                         int m0, int n0, int k0, char* slot, int wave, int lane) {
-  using namespace gw4;
-  const int rsub = lane >> 2;
-  const int pc = lane & 3;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = wave * 4 + i;  // piece 0..15, 16 rows x 64 B
-    const int r = p * 16 + rsub;
-    const int lc = pc ^ (((r >> 3) & 1) * 3);
-    __builtin_amdgcn_global_load_lds(A + (size_t)(m0 + r) * K + k0 + lc * 8, (lds_void_ptr)(slot + p * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(Bt + (size_t)(n0 + r) * K + k0 + lc * 8,
-                                     (lds_void_ptr)(slot + OP_BYTES + p * 1024), 16, 0, 0);
-  }
-}
-
-struct W4Frags {
-  bf16x8 a[8], b[8];
-};
-
-__device__ __forceinline__ void w4_read(W4Frags& f, const char* slot, int a_off, int b_off) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) f.a[i] = *reinterpret_cast<const bf16x8*>(slot + a_off + i * 1024);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f.b[j] = *reinterpret_cast<const bf16x8*>(slot + b_off + j * 1024);
-}
-
-// One slice: refill slot (j+3)%4, MFMAs on the fragments of slice j, read
-// slice j+1's fragments in place.  Column-major MFMA order frees each fragment
-// register early (b[c] after column c, a[r] after MFMA (r, 7)), so ONE
-// fragment set (64 VGPRs) carries the read-ahead next to the 256 accumulators
-// (which take all 256 AGPRs: anything that makes the allocator want one more
-// AGPR - explicit sched_group_barrier interleaves, a peeled tail with its own
-// copy of the body - turns into hundreds of v_accvgpr moves per slice).  The
-// body is therefore branch-free: past the last slice the refill re-reads slice
-// nk-1 into a slot nobody reads again and the read-ahead reads a stale slot,
-// which keeps every vmcnt count constant.  hipcc schedules it as
-//   [LDS-DMA piece] [8 MFMA] [ds_read b[c]]  x 8 columns.
-__device__ __forceinline__ void w4_iter(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, int K, int m0,
-                                        int n0, char* smem, int wave, int lane, int a_off, int b_off, int j, int nk,
-                                        f32x4 (&acc)[8][8], W4Frags& f) {
-  using namespace gw4;
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // own share of slice j+1 landed
-  wg_barrier();
-  const char* nslot = smem + ((j + 1) & 3) * SLOT_BYTES;
-  char* sslot = smem + ((j + 3) & 3) * SLOT_BYTES;
-  const int kload = min(j + 3, nk - 1) * BK;
-  const int rsub = lane >> 2, pc = lane & 3;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    {  // piece c: operand c>>2, rows ((wave*4 + (c&3))*16 + rsub)
-      const int p = wave * 4 + (c & 3);
-      const int r = p * 16 + rsub;
-      const int lc = pc ^ (((r >> 3) & 1) * 3);
-      const __bf16* src = (c < 4 ? A + (size_t)(m0 + r) * K : Bt + (size_t)(n0 + r) * K) + kload + lc * 8;
-      __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)(sslot + (c < 4 ? 0 : OP_BYTES) + p * 1024), 16, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b[c], f.a[r], acc[r][c], 0, 0, 0);
-      if (c == 7) f.a[r] = *reinterpret_cast<const bf16x8*>(nslot + a_off + r * 1024);
-    }
-    f.b[c] = *reinterpret_cast<const bf16x8*>(nslot + b_off + c * 1024);
-  }
-}
-
-template <bool OUT_F32>
-__global__ __launch_bounds__(gw4::NTHR, 1) void gemm_bf16_nt_w4_kernel(const __bf16* __restrict__ A,
-                                                                      const __bf16* __restrict__ Bt,
-                                                                      void* __restrict__ Cv, int M, int N, int K) {
-  using namespace gw4;
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-
-  const int tiles_m = M / BM, tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int xcd = bid % kNumXcd;
-  const int q = nwg / kNumXcd, rr = nwg % kNumXcd;
-  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / kNumXcd;
-  const int per_group = GROUP_M * tiles_n;
-  const int first_m = (wgid / per_group) * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
-  const int in_group = wgid % per_group;
-  const int m0 = (first_m + in_group % gsize) * BM;
-  const int n0 = (in_group / gsize) * BN;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int frow = lane & 15;
-  const int pcol = ((lane >> 4) ^ (((frow >> 3) & 1) * 3)) * 16;
-  const int a_off = (wm * 128 + frow) * 64 + pcol;
-  const int b_off = OP_BYTES + (wn * 128 + frow) * 64 + pcol;
-
-  const int nk = K / BK;
-#pragma unroll
-  for (int s = 0; s < 3; ++s) w4_stage(A, Bt, K, m0, n0, min(s, nk - 1) * BK, smem + s * SLOT_BYTES, wave, lane);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  wg_barrier();
-  W4Frags f;
-  w4_read(f, smem, a_off, b_off);
-  for (int j = 0; j < nk; ++j) w4_iter(A, Bt, K, m0, n0, smem, wave, lane, a_off, b_off, j, nk, acc, f);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
-
-  const int crow = m0 + wm * 128 + frow;
-  const int ccol = n0 + wn * 128 + (lane >> 4) * 4;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const size_t idx = (size_t)(crow + i * 16) * N + ccol + jj * 16;
-      if constexpr (OUT_F32) {
-        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + idx) = acc[i][jj];
-      } else {
-        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        bf16x4 v = {(__bf16)acc[i][jj][0], (__bf16)acc[i][jj][1], (__bf16)acc[i][jj][2], (__bf16)acc[i][jj][3]};
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(Cv) + idx) = v;
-      }
-    }
-}
-
+#include "gemm_lab_2.inc"
 #endif  // AVK_GEMM_LAB
 
 // ------------------- K2 GEMM, 8-phase quadrant pipeline (BK = 64, 2 buffers) ----
