@@ -551,6 +551,16 @@ def test_complete_publishes_the_validated_mfma_rates(env):
     V.write_ready(env, "workload", {"ranks": [rank({**bf16, "min_tflops": 0.0})]})
     assert V.complete(env)["mfma_rate_dtypes"] == []
     assert V.MFMA_RATE_LABEL not in env.client.get("v1", "Node", "n1")["metadata"]["labels"]
+    # round 6: fp6 and block-scaled MXFP4; a rate the gate was asked to count but did not
+    # (the sdk-mode gate counts bf16 only: "not_counted") is not claimed
+    fp6 = {"name": "gemm_fp6", "ok": True, "tflops": 3500.0, "min_tflops": 2540.0, "counter_gate": "pass"}
+    mx = {"name": "gemm_mxfp4", "ok": True, "tflops": 3900.0, "min_tflops": 2830.0, "counter_gate": "pass"}
+    V.write_ready(env, "workload", {"ranks": [rank(bf16, fp8, fp4, fp6, mx)]})
+    assert V.complete(env)["mfma_rate_dtypes"] == ["bf16", "fp8", "fp4", "fp6", "mxfp4"]
+    assert env.client.get("v1", "Node", "n1")["metadata"]["labels"][V.MFMA_RATE_LABEL] == "bf16.fp8.fp4.fp6.mxfp4"
+    V.write_ready(env, "workload", {"ranks": [rank({**bf16, "counter_gate": "pass"},
+                                                   {**fp8, "counter_gate": "not_counted"}, fp6)]})
+    assert V.complete(env)["mfma_rate_dtypes"] == ["bf16", "fp6"]
 
 
 def test_mfma_rate_check_flags_reach_the_validator(tmp_path):
