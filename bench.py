@@ -1087,7 +1087,7 @@ def main():
         if present > n_gpus:
             os.environ["AMDGPU_VISIBLE_GPUS"] = ",".join(str(i) for i in range(n_gpus))
         elif present < n_gpus:
-            raise SystemExit(f"requested {n_gpus} GPUs, node exposes {present}")
+            raise RuntimeError(f"requested {n_gpus} GPUs, node exposes {present}")
 
     workdir = tempfile.mkdtemp(prefix="amdgpu-bench-")
     results: list[dict] = []
@@ -1225,5 +1225,28 @@ def main():
         raise SystemExit(rc)
 
 
+def setup_failure_line(e: BaseException) -> dict:
+    """The line of a run that failed before its first bring-up (the node has
+    fewer GPUs than asked for, the ranks' rendezvous, an import): the same
+    shape as :func:`failure_line`, phase ``setup``."""
+    import traceback
+
+    try:
+        args = parse()
+    except BaseException:  # noqa: BLE001 - the arguments themselves: the contract's defaults
+        args = argparse.Namespace(steps=None, warmup=None, gpus=int(os.environ.get("WORLD_SIZE", "1")))
+    n = int(os.environ.get("WORLD_SIZE", "0")) or args.gpus
+    err = {"phase": "setup", "type": type(e).__name__, "message": str(e)[:2000],
+           "traceback": traceback.format_exc()[-6000:]}
+    return failure_line(args, n, False, err, [], [], 0.0, None)
+
+
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except (SystemExit, KeyboardInterrupt):
+        raise
+    except BaseException as exc:  # noqa: BLE001 - one parseable line, then the failure
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(fit_line(setup_failure_line(exc)), flush=True)
+        raise SystemExit(1) from exc

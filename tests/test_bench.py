@@ -109,6 +109,29 @@ def test_bench_floor_failure_prints_a_structured_line(tmp_path):
     assert "Traceback" in d["errors"][0]["traceback"]
 
 
+def test_bench_setup_failure_prints_a_structured_line(tmp_path):
+    """A run that fails before its first bring-up (here: two GPUs asked of a
+    node whose KFD topology has one) still ends with one parseable line,
+    value null and phase "setup", and a non-zero exit."""
+    from amdgpu_operator.testing import fakesys
+
+    root = str(tmp_path / "host")
+    fakesys.build_node(root, 1)
+    os.makedirs(os.path.join(root, "dev"), exist_ok=True)
+    open(os.path.join(root, "dev", "kfd"), "w").close()
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--sysfs-root", root, "--detail", str(tmp_path / "d.json")],
+                       cwd=ROOT, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1, p.stderr[-2000:]
+    line = _line(p.stdout)
+    assert len(line) <= LINE_BUDGET
+    out = json.loads(line)
+    assert out["value"] is None and out["n_gpus"] == 2 and out["steps"] == 1
+    assert out["error"]["phase"] == "setup"
+    assert "node exposes 1" in out["error"]["message"]
+    assert list(out)[:len(HEAD)] == HEAD
+
+
 def test_fit_line_sheds_optional_fields_to_the_budget():
     b = _bench()
     out = {"metric": "m", "value": 1.0, "config": {"model": "x", "time_to_ready_s": [0.25] * 400,
