@@ -90,6 +90,34 @@ inline GateVerdict gate_verdict(long long m, long long n, long long k, int cus, 
   return v;
 }
 
+// Whether a failed verdict may be counted again (validator_main.cpp aql_gate,
+// at most kGateAttempts in all).  The counters are device-wide, so a window
+// that overlapped someone else's work is not evidence against this GPU:
+//   "preempted"    - output and op count exact, waves above the launch's
+//                    (a queue remap saved and restored ours) or exact waves
+//                    with the utilisation under its floor (our dispatch
+//                    waited while the GPU stayed busy);
+//   "foreign_mfma" - output exact, op count above 2MNK, waves not below the
+//                    launch's: another process's MFMA kernel of the same data
+//                    type ran in the window.  Its waves count only if they
+//                    started inside it: a co-tenant's GEMM whose waves were
+//                    already resident added 2.08x our ops with our waves
+//                    exact (tests/test_native_gpu.py, a PyTorch bf16 loop).
+// Everything else is the GPU's own: a wrong output, an op count short of
+// 2MNK (other work only adds), missing waves.  A retry never passes by
+// itself - a pass needs every equality exact on one attempt - so a truncated
+// dispatch hidden under foreign work, or a kernel that itself issues extra
+// MFMAs, is counted again and fails after the last attempt, not accepted.
+// Returns "" when the failure is final.
+inline const char* gate_retry_kind(const GateCounters& c, const GateVerdict& v) {
+  if (v.ok || !c.output_matches) return "";
+  if (c.mops == v.expected_mops &&
+      (c.waves > v.expected_waves || (c.waves == v.expected_waves && v.mfma_util < v.util_floor)))
+    return "preempted";
+  if (c.mops > v.expected_mops && c.waves >= v.expected_waves) return "foreign_mfma";
+  return "";
+}
+
 // Floors given for a whole MI355X (256 CUs) apply pro rata to a compute
 // partition (DPX 128, QPX 64, CPX 32 CUs).
 inline double scale_floor_by_cus(double floor_full_gpu, int cus) {

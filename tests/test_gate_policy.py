@@ -78,6 +78,24 @@ def test_floor_scales_with_occupancy():
     assert v["mfma_util_floor"] == pytest.approx(0.2)
 
 
+@pytest.mark.parametrize("kw,kind", [
+    ({"waves": WAVES + 262}, "preempted"),                         # a queue remap restored our waves
+    ({"gui": GUI * 4}, "preempted"),                               # our dispatch waited, the GPU stayed busy
+    ({"mops": MOPS + 4096, "waves": WAVES + 64}, "foreign_mfma"),  # another process's MFMA kernel in the window
+    ({"mops": MOPS // 2 + 8192, "waves": WAVES + 64}, ""),         # short of 2MNK even with foreign work: final
+    ({"mops": MOPS * 2 + 22176832}, "foreign_mfma"),               # a resident co-tenant GEMM: our waves exact
+    ({"mops": MOPS - 512}, ""),                                    # dropped work: final
+    ({"waves": WAVES - 4}, ""),                                    # missing waves: final
+])
+def test_retry_only_on_other_parties_signatures(kw, kind):
+    """Which failed windows aql_gate counts again (gate_policy.h
+    gate_retry_kind): only those another process's work explains.  None of
+    them passes - a pass needs the exact equalities on one attempt."""
+    v = verdict(**kw)
+    assert not v["ok"]
+    assert v["retry"] == kind
+
+
 def test_floor_zero_reports_only_but_equalities_still_hold():
     assert verdict(gui=GUI * 50, min_util=0)["ok"]
     assert not verdict(waves=WAVES - 1, min_util=0)["ok"]

@@ -159,6 +159,54 @@ def test_counter_gates_pass_first_time_beside_a_process_dispatching_continuously
                                                            + ".lock"]
 
 
+def test_counter_gate_beside_another_partys_mfma_kernels(tmp_path):
+    """A co-tenant that takes no gate lock (a PyTorch process running bf16
+    GEMMs back to back) shares the device-wide counters with the counted
+    window.  The gate never accepts such a window: it passes only with every
+    equality exact on one attempt, and a window the other party's work
+    explains (its waves, and for the bf16 gate its MFMA ops too) is counted
+    again - up to 4 attempts - never failed outright on the first."""
+    import sys
+    import time
+
+    code = ("import sys, time, torch\n"
+            "a = torch.randn(4096, 4096, device='cuda', dtype=torch.bfloat16)\n"
+            "b = torch.randn(4096, 4096, device='cuda', dtype=torch.bfloat16)\n"
+            "(a @ b).sum().item()\n"
+            "print('ready', flush=True)\n"
+            "t = time.monotonic()\n"
+            "while time.monotonic() - t < float(sys.argv[1]):\n"
+            "    for _ in range(8):\n"
+            "        c = a @ b\n"
+            "    torch.cuda.synchronize()\n")
+    bg = subprocess.Popen([sys.executable, "-c", code, "8"], stdout=subprocess.PIPE, text=True)
+    try:
+        assert bg.stdout.readline().strip() == "ready"
+        t0 = time.monotonic()
+        rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm,gemm_fp8", "--counter-gate"],
+                       timeout=60)
+        busy_throughout = bg.poll() is None
+        took = time.monotonic() - t0
+    finally:
+        bg.communicate(timeout=60)
+    assert busy_throughout, "the co-tenant ended before the gates"
+    got = {x["name"]: x for x in rep["steps"]}
+    assert "gemm" in got, rep  # gemm_fp8 runs only if the bf16 step passed
+    for name, mops in (("gemm", "SQ_INSTS_VALU_MFMA_MOPS_BF16"), ("gemm_fp8", "SQ_INSTS_VALU_MFMA_MOPS_F8")):
+        st = got.get(name)
+        if st is None:
+            continue
+        assert st["freivalds_rel_err"] < 1e-3, st  # the computation itself was right
+        if st["counter_gate"] == "pass":
+            assert st[mops] * 512 == 2 * 4096 ** 3 and st["SQ_WAVES"] == (4096 // 256) ** 2 * _WPT, st
+        else:
+            assert st["counter_gate"] == "fail" and st["gate_attempts"] == 4, st
+        tries = [r for r in st.get("gate_retried_after", "").split("; ") if r]
+        assert len(tries) == st["gate_attempts"] - (st["counter_gate"] == "pass"), st
+        assert all(r.endswith(", preempted)") or r.endswith(", foreign_mfma)") for r in tries), st
+    assert took < 30
+
+
 def test_counter_gate_fails_closed_on_a_truncated_gemm(tmp_path):
     """The counted dispatch runs half the K loop (AMDGPU_GATE_TEST_TRUNCATE_K):
     its MFMA op count misses 2MNK/512 and its output differs, so the gate
