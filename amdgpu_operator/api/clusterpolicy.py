@@ -293,6 +293,12 @@ class WorkloadSpec(_M):
     # N7 gate lock (native/include/gate_lock.h): the counted dispatch holds a
     # per-GPU lock that the plugin pod's check and the RCCL processes share
     gateLock: bool = True
+    # count the GEMMs after the kernel steps (validator_main.cpp PendingGate)
+    # instead of inside each step: the first counted window rarely waits for
+    # the plugin pod's hold on the gate lock (-2.5 ms median time-to-Ready),
+    # but back-to-back GEMM trials read fp6 / MXFP4 3-9 % lower
+    # (profiles/r6_defer), so off by default
+    deferGates: bool = False
     minMfmaUtilByDtype: dict[str, float] = Field(
         default_factory=lambda: {"fp8": 0.33, "fp4": 0.21, "fp6": 0.20, "mxfp4": 0.20})
     # N >= 2 throughput floors from the xGMI link model (validator/validate.py

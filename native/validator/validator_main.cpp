@@ -269,6 +269,7 @@ struct Args {
   double peer_timeout_s = 30;       // a rank not alive by then is missing; bound on communicator set-up
   double collective_timeout_s = 30;  // bound on any one collective (or batch of timed collectives)
   bool counter_gate = false;
+  bool defer_gates = false;  // count the GEMMs after the kernel steps (PendingGate)
   bool any_arch = false;
   bool null_stream = false;   // run the steps on the legacy null stream instead of a created one
   bool all_devices = false;   // every visible device (a plugin-validation pod holding N GPUs)
@@ -764,6 +765,77 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
   return v.ok;
 }
 
+// Counted dispatches after the kernel steps (--defer-gates, one device per
+// process): each GEMM step measures, checks and times its kernel at once but
+// queues its counter gate here, and finish_deferred_gates counts them in step
+// order once the other kernel steps are done.  The counted window needs the
+// GPU's gate lock exclusively, and the plugin-validation pod holds it shared
+// from its code-object load through its teardown; the first inline gate
+// waits 3-17 ms for it in most bring-ups (profiles/r6_final/head2).
+// Deferred, that wait mostly goes (the workload chain -6 ms, time-to-Ready
+// median -2.5 ms over 40 interleaved pairs), but the GEMM steps' timed
+// trials then run back to back and the later ones read lower and wider
+// (fp6 -3 %, MXFP4 -9 %: profiles/r6_defer), so the default stays inline.
+// The buffers stay allocated to the process's end anyway (release_at_exit),
+// and C16 still holds the step's own output for the gate's comparison.
+struct PendingGate {
+  std::string step;
+  const void* A;
+  const void* B;
+  void* C16;
+  int n;
+  int cus;
+  int dtype;
+  const void* SA;
+  const void* SB;
+};
+std::vector<PendingGate>* g_deferred_gates = nullptr;  // set by main's one-device path
+
+// Queue (deferred) or run the step's gate: returns false when it ran and failed.
+bool gate_or_defer(const Args& a, const char* step, const void* A, const void* B, void* C16, int n, int cus,
+                   hipStream_t st, std::string* json, int dtype, const void* SA = nullptr, const void* SB = nullptr) {
+  if (g_deferred_gates) {
+    g_deferred_gates->push_back({step, A, B, C16, n, cus, dtype, SA, SB});
+    json->clear();
+    return true;
+  }
+  return aql_gate(a, A, B, C16, n, cus, st, json, dtype, SA, SB);
+}
+
+void append_gate_json(Step* s, const std::string& json) {
+  std::string& d = s->detail;
+  while (!d.empty() && (d.back() == ' ' || d.back() == ',')) d.pop_back();  // the step left room for it
+  d += (d.empty() ? "" : ", ") + json;
+}
+
+// The queued gates, in step order; a failed gate fails its step (and the
+// run: the step's ok turns false and the report names the gate's reason).
+// With `run` false (an earlier step failed, or a step threw) the queued gates
+// are reported as not run - the run has failed already.
+void finish_deferred_gates(const Args& a, hipStream_t st, std::vector<Step>* steps, bool run) {
+  if (!g_deferred_gates) return;
+  std::vector<PendingGate> todo;
+  todo.swap(*g_deferred_gates);
+  g_deferred_gates = nullptr;
+  for (const auto& p : todo) {
+    const auto tg = Clock::now();
+    std::string json = "\"counter_gate\": \"not_run\", \"gate_mode\": \"aql\"";
+    bool ok = false;
+    if (run) {
+      ok = aql_gate(a, p.A, p.B, p.C16, p.n, p.cus, st, &json, p.dtype, p.SA, p.SB);
+      json += ", \"gate_deferred\": true";
+    }
+    for (auto& s : *steps)
+      if (s.name == p.step) {
+        s.ok = s.ok && ok;
+        s.seconds += secs(tg);
+        append_gate_json(&s, json);
+        break;
+      }
+    run = run && ok;  // after a failed gate the rest are not counted
+  }
+}
+
 // The TF/s floor is calibrated at 4096^3 (BENCH_r02: 1,238 TF/s) and holds
 // for larger problems; a smaller GEMM is launch- and tail-bound (1024^3 runs
 // ~70 TF/s on a healthy MI355X), so below 4096 the rate is reported only.
@@ -826,7 +898,7 @@ Step step_gemm(const Args& a, hipStream_t st, int cus) {
   // dispatches, so it must not overlap the timed ones
   if (a.counter_gate && a.gate_mode == "aql") {
     std::string gate_json;
-    const bool gate_ok = aql_gate(a, A, B, C16, n, cus, st, &gate_json);
+    const bool gate_ok = gate_or_defer(a, "gemm", A, B, C16, n, cus, st, &gate_json, AVK_AQL_GATE_BF16);
     const float ms = best_ms / a.gemm_iters;
     const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
     (void)hipEventDestroy(e0);
@@ -1038,7 +1110,7 @@ Step step_gemm_lowp(const Args& a, hipStream_t st, int cus, const LowPrecision& 
                                          : "\"counter_gate\": \"off\"";
   bool gate_ok = true;
   if (a.counter_gate && a.gate_mode == "aql")
-    gate_ok = aql_gate(a, A, B, C16, n, cus, st, &gate_json, lp.gate_dtype, SA, SB);
+    gate_ok = gate_or_defer(a, lp.step, A, B, C16, n, cus, st, &gate_json, lp.gate_dtype, SA, SB);
   const float ms = best_ms / a.gemm_iters;
   const double tflops = 2.0 * n * (double)n * n / (ms * 1e-3) / 1e12;
   (void)hipEventDestroy(e0);
@@ -1968,7 +2040,7 @@ void usage(const char* p) {
           "          [--rank R --world W --rendezvous DIR --run-id ID] [--steps a,b,...]\n"
           "          [--gemm N] [--gemm-iters K] [--fp8-gemm N] [--min-fp8-tflops X] [--fp4-gemm N] [--min-fp4-tflops X] [--hbm-bytes B] [--vecadd-elems N] [--rccl-elems E] [--xgmi-elems E]\n"
           "          [--min-gemm-tflops X] [--min-hbm-gbps Y] [--counter-gate] [--any-arch] [--rccl-destroy]\n"
-          "          [--ready-file PATH] [--start-gate FILE] [--gate-mode aql|sdk] [--min-mfma-util U]\n"
+          "          [--ready-file PATH] [--start-gate FILE] [--gate-mode aql|sdk] [--defer-gates] [--min-mfma-util U]\n"
           "          [--min-rccl-busbw-gbps X] [--min-xgmi-read-gbps X] [--peer-timeout S] [--collective-timeout S]\n"
           "          [--sweep-min-bytes B] [--sweep-max-bytes B] [--sweep-factor F] [--sweep-ops a,b] [--link-bytes B]\n"
           "          [--linger-until FILE] [--linger-max-s S]\n"
@@ -2063,6 +2135,7 @@ int main(int argc, char** argv) {
     else if (k == "--gate-lock-probe") lock_probe = v();
     else if (k == "--timeout") a.timeout_s = atof(v());
     else if (k == "--counter-gate") a.counter_gate = true;
+    else if (k == "--defer-gates") a.defer_gates = true;
     else if (k == "--any-arch") a.any_arch = true;
     else if (k == "--rccl-destroy") a.rccl_destroy = true;
     else if (k == "--sweep-min-bytes") a.sweep_min_bytes = atoll(v());
@@ -2121,6 +2194,7 @@ int main(int argc, char** argv) {
     }
   }
   std::vector<Step> steps;
+  std::vector<PendingGate> deferred_gates;
   bool ok = true;
   std::string error;
   hipStream_t st = nullptr;
@@ -2255,7 +2329,9 @@ int main(int argc, char** argv) {
       if (gate_watch.joinable()) gate_watch.join();
     }
     if (ok && devs.size() == 1 && !a.all_devices) {
-      // one device: the kernel steps in order on the main thread
+      // one device: the kernel steps in order on the main thread, the
+      // counted dispatches after them (PendingGate)
+      if (a.counter_gate && a.gate_mode == "aql" && a.defer_gates) g_deferred_gates = &deferred_gates;
       if (ok && has_step(a, "vecadd")) ok = (steps.push_back(step_vecadd(a, st)), steps.back().ok);
       if (ok && has_step(a, "gemm")) ok = (steps.push_back(step_gemm(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "gemm_fp8"))
@@ -2269,6 +2345,9 @@ int main(int argc, char** argv) {
       if (ok && has_step(a, "mfma")) ok = (steps.push_back(step_mfma(st)), steps.back().ok);
       if (ok && has_step(a, "hbm")) ok = (steps.push_back(step_hbm(a, st, prop.multiProcessorCount)), steps.back().ok);
       if (ok && has_step(a, "dmabuf")) ok = (steps.push_back(step_dmabuf(st)), steps.back().ok);
+      const bool run_gates = ok;
+      finish_deferred_gates(a, st, &steps, run_gates);
+      for (const auto& s : steps) ok = ok && s.ok;
     } else if (ok) {
       // several devices (a GPU's partitions, a pod's GPUs): all at once
       if (a.all_devices) steps.back().detail = fmt("\"device\": %d, ", devs[0].first) + steps.back().detail;
@@ -2291,6 +2370,7 @@ int main(int argc, char** argv) {
     error = e.what();
   }
   go_seen = true;  // a step failed before "go": the gate watcher ends too
+  finish_deferred_gates(a, st, &steps, false);  // a step threw: the queued gates did not run
   if (gate_watch.joinable()) gate_watch.join();
   if (gate_prep_thread.joinable()) gate_prep_thread.join();
   if (rccl_thread.joinable()) {

@@ -112,13 +112,17 @@ def test_shipped_floors_pass_and_a_floor_above_the_measured_rate_fails(tmp_path)
                         ("gemm_fp6", w.minFp6Tflops), ("gemm_mxfp4", w.minMxfp4Tflops)):
         assert got[name]["min_tflops"] == floor and got[name]["tflops"] < floor / 0.60, (name, got[name]["tflops"])
     assert got["hbm"]["gbps"] < w.minHbmGbps / 0.60
+    # 1.05 x the rate: this run's, or the calibration median where this run
+    # read lower (one best-of-3 reading spreads ~+-8 % for fp8 between
+    # processes, profiles/r6_defer; the 60-run medians of profiles/r6_floors)
+    medians = {"gemm": 1505.5, "gemm_fp8": 2706.2, "gemm_fp4": 4313.0, "gemm_fp6": 3533.7, "gemm_mxfp4": 3938.8}
     over = {"gemm": "--min-gemm-tflops", "gemm_fp8": "--min-fp8-tflops", "gemm_fp4": "--min-fp4-tflops",
             "gemm_fp6": "--min-fp6-tflops", "gemm_mxfp4": "--min-mxfp4-tflops"}
     for name, flag in over.items():
-        rc, rep = _run(["--rendezvous", str(tmp_path / name), "--steps", f"hip,{name}",
-                        flag, f"{1.05 * got[name]['tflops']:.1f}"])
+        rate = max(got[name]["tflops"], medians[name])
+        rc, rep = _run(["--rendezvous", str(tmp_path / name), "--steps", f"hip,{name}", flag, f"{1.05 * rate:.1f}"])
         st = next(s for s in rep["steps"] if s["name"] == name)
-        assert rc != 0 and st["perf_ok"] is False, st
+        assert rc != 0 and st["perf_ok"] is False and st["tflops"] < st["min_tflops"], st
 
 
 def test_counter_gates_pass_first_time_beside_a_process_dispatching_continuously(tmp_path):
@@ -191,10 +195,10 @@ def test_counter_gate_beside_another_partys_mfma_kernels(tmp_path):
         bg.communicate(timeout=60)
     assert busy_throughout, "the co-tenant ended before the gates"
     got = {x["name"]: x for x in rep["steps"]}
-    assert "gemm" in got, rep  # gemm_fp8 runs only if the bf16 step passed
+    assert got["gemm"]["counter_gate"] in ("pass", "fail"), rep
     for name, mops in (("gemm", "SQ_INSTS_VALU_MFMA_MOPS_BF16"), ("gemm_fp8", "SQ_INSTS_VALU_MFMA_MOPS_F8")):
         st = got.get(name)
-        if st is None:
+        if st is None or st["counter_gate"] == "not_run":  # counted only while the earlier gates pass
             continue
         assert st["freivalds_rel_err"] < 1e-3, st  # the computation itself was right
         if st["counter_gate"] == "pass":
@@ -211,13 +215,37 @@ def test_counter_gate_fails_closed_on_a_truncated_gemm(tmp_path):
     """The counted dispatch runs half the K loop (AMDGPU_GATE_TEST_TRUNCATE_K):
     its MFMA op count misses 2MNK/512 and its output differs, so the gate
     fails on its first attempt and is not retried."""
-    rc, rep = _run(["--rendezvous", str(tmp_path), "--steps", "hip,gemm", "--counter-gate"],
-                   env={"AMDGPU_GATE_TEST_TRUNCATE_K": "1"})
-    assert rc != 0 and not rep["ok"]
-    g = next(x for x in rep["steps"] if x["name"] == "gemm")
-    assert g["counter_gate"] == "fail" and g["gate_attempts"] == 1, g
-    assert g["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 == 4096 ** 3  # half of 2 * 4096^3
-    assert g["gated_output_matches"] is False and g["freivalds_rel_err"] < 1e-4  # the HIP GEMM itself was right
+    for mode in ([], ["--defer-gates"]):
+        rc, rep = _run(["--rendezvous", str(tmp_path / str(len(mode))), "--steps", "hip,gemm,gemm_fp8",
+                        "--counter-gate", *mode], env={"AMDGPU_GATE_TEST_TRUNCATE_K": "1"})
+        assert rc != 0 and not rep["ok"]
+        g = next(x for x in rep["steps"] if x["name"] == "gemm")
+        assert g["counter_gate"] == "fail" and g["gate_attempts"] == 1 and not g["ok"], g
+        assert g["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 == 4096 ** 3  # half of 2 * 4096^3
+        assert g["gated_output_matches"] is False and g["freivalds_rel_err"] < 1e-4  # the HIP GEMM itself was right
+        f = next((x for x in rep["steps"] if x["name"] == "gemm_fp8"), None)
+        if mode:  # deferred: the fp8 step ran, and after the failed gate its own is not counted
+            assert g["gate_deferred"] and f["counter_gate"] == "not_run" and not f["ok"], f
+        else:  # inline: the run stops at the failed step
+            assert f is None
+
+
+def test_counter_gates_run_after_the_kernel_steps(tmp_path):
+    """PendingGate (--defer-gates, validator.workload.deferGates): each GEMM
+    step is measured and checked in place, its counted dispatch runs once the
+    kernel steps are done - after the HBM step here - and lands in the step's
+    own record; by default the gate runs inside the step."""
+    steps = "hip,gemm,gemm_fp8,hbm"
+    rc, rep = _run(["--rendezvous", str(tmp_path / "d"), "--steps", steps, "--counter-gate", "--defer-gates"])
+    assert rc == 0 and rep["ok"], rep
+    got = {x["name"]: x for x in rep["steps"]}
+    for name in ("gemm", "gemm_fp8"):
+        assert got[name]["counter_gate"] == "pass" and got[name]["gate_deferred"] is True, got[name]
+        assert got[name]["seconds"] >= got[name]["gate_seconds"]
+    rc, rep = _run(["--rendezvous", str(tmp_path / "n"), "--steps", steps, "--counter-gate"])
+    assert rc == 0 and rep["ok"], rep
+    got = {x["name"]: x for x in rep["steps"]}
+    assert got["gemm"]["counter_gate"] == "pass" and "gate_deferred" not in got["gemm"]
 
 
 def test_validator_fp8_floor_fails_the_step(tmp_path):
