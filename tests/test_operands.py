@@ -587,6 +587,9 @@ def test_mfma_rate_check_flags_reach_the_validator(tmp_path):
     off = args(deep_merge(ref, {"validator": {"workload": {"mfmaRateCheck": False}}}))
     assert "--no-mfma-rate" in off and not {"--min-fp8-tflops", "--min-fp4-tflops", "--fp8-gemm", "--min-fp6-tflops",
                                             "--min-mxfp4-tflops", "--min-mfma-util-by-dtype"} & set(off)
+    # counted dispatches inline by default; deferGates queues them after the kernel steps
+    assert "--defer-gates" not in on
+    assert "--defer-gates" in args(deep_merge(ref, {"validator": {"workload": {"deferGates": True}}}))
 
     root = str(tmp_path / "h1")
     fakesys.build_node(root, 1)
