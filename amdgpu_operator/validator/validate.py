@@ -1414,6 +1414,7 @@ def complete(env: NodeEnv) -> dict:
     """Mark the node validated: label, the MFMA data types the probe confirmed
     (``amd.com/gpu.validated.mfma=f16.bf16.fp8...``, next to GFD's per-arch
     ``amd.com/gpu.mfma.*`` claims) and an annotation with the step durations."""
+    drv_time = (read_ready(env, "driver") or {}).get("time")
     steps = {s: (read_ready(env, s) or {}).get("seconds") for s in ("driver", "workload", "plugin")}
     ann = {"amd.com/gpu.validation": json.dumps({k: round(v, 4) for k, v in steps.items() if v is not None})}
     labels = {VALIDATED_LABEL: "true"}
@@ -1424,6 +1425,26 @@ def complete(env: NodeEnv) -> dict:
     labels[MFMA_RATE_LABEL] = ".".join(rates) if rates else None  # a stale claim goes
     env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": labels, "annotations": ann}})
     write_ready(env, "complete", {"steps": steps, "mfma_dtypes": dtypes, "mfma_rate_dtypes": rates})
+    # The driver can go while this runs: the driver container's health
+    # monitor then leaves its loss marker, removes every ready file and these
+    # labels (driver/manager.py _withdraw_validation).  Had that happened
+    # between the label patch and the file above, the node would stay
+    # marked validated on a driver that is gone; so, with a marker newer
+    # than the driver validation this completes, or with no driver
+    # validation left (the marker stays until the driver is back and the
+    # validator restarted; an older one is a loss that a later driver
+    # validation already followed), the node's validation goes again.
+    from ..driver.manager import LOST_MARKER
+
+    try:
+        lost_at = os.stat(env.validation_file(LOST_MARKER)).st_mtime
+    except FileNotFoundError:
+        lost_at = None
+    if lost_at is not None and (drv_time is None or lost_at >= drv_time):
+        clear_ready(env, ("complete",))
+        env.client.patch("v1", "Node", env.node_name, {"metadata": {"labels": {
+            VALIDATED_LABEL: None, MFMA_LABEL: None, MFMA_RATE_LABEL: None}}})
+        return {"ok": False, "reason": "driver withdrawn during completion", "steps": steps}
     return {"ok": True, "steps": steps, "mfma_dtypes": dtypes, "mfma_rate_dtypes": rates}
 
 

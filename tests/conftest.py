@@ -58,7 +58,7 @@ def no_leaked_servers(request):
 
     before = _server_threads()
     yield
-    deadline = time.monotonic() + 3.0
+    deadline = time.monotonic() + 10.0  # a loaded CI box (pytest -n 8) can take seconds to end a watch thread
     left = _server_threads() - before
     while left and time.monotonic() < deadline:
         time.sleep(0.02)
