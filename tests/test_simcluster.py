@@ -121,6 +121,10 @@ def test_driver_loss_triggers_revalidation(cluster_factory):
     c.install_operator(REF)
     c.wait_ready(60, {"gpu-1": 2})
     env = c.nodes["gpu-1"].env
+    # the policy turns Ready on the node label; the validator writes its file right after
+    deadline = time.monotonic() + 10
+    while not os.path.exists(env.validation_file("validated")) and time.monotonic() < deadline:
+        time.sleep(0.01)
     initstate = os.path.join(env.host_root, "sys/module/amdgpu/initstate")
     os.rename(initstate, initstate + ".gone")  # driver unloaded behind our back
     from amdgpu_operator.driver.manager import monitor_once
