@@ -154,26 +154,59 @@ std::string agent_bdf(hsa_agent_t gpu) {
   return b;
 }
 
-// one device: queue, dispatch, verify; appends its step records.  The GPU's
-// gate lock (gate_lock.h) is held shared from the code-object load through
-// the teardown of the queue and the executable (freeing the code object's
-// VRAM starts the driver's wipe of it, GPU work a counted window must not
-// see either): a counter gate of the validator on this GPU never counts this
-// pod's upload, kernel or clean-up.  `loop_s` > 0 (tests): keep dispatching
-// the kernel for that long, the lock released between dispatches.
-bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std::vector<char>& co, int n,
-                  double timeout_s, std::vector<std::string>* steps, std::string* error, double loop_s,
-                  avk::GateLock* held) {
-  const auto t0 = Clock::now();
-  const std::string bdf = agent_bdf(gpu);
-  avk::GateLock& lock = *held;
-  lock = avk::GateLock(bdf, avk::GateLock::kShared, 2.0);
+// What one device's check holds until its teardown (DeviceRes::release),
+// which runs after the report is out: the queue, the executable and the
+// buffers, and the GPU's gate lock (gate_lock.h) taken before the code-object
+// load.  The lock stays held through the teardown (freeing the code object's
+// VRAM starts the driver's wipe of it, and the queue's destruction unmaps it:
+// GPU work a counted window must not see), so a counter gate of the validator
+// on this GPU never counts this pod's upload, kernel or clean-up.
+struct DeviceRes {
+  avk::GateLock lock;
   hsa_code_object_reader_t reader{0};
   hsa_executable_t exe{0};
   hsa_queue_t* queue = nullptr;
   hsa_signal_t done{0};
   std::vector<void*> allocs;
-  bool ok = false, dispatched = false, finished = false;
+  bool dispatched = false, finished = false;
+
+  // A dispatch that did not finish may still be running (slow, not dead): its
+  // queue, completion signal, code object and buffers all stay until the
+  // process exit, so the kernel never runs from freed code or signals freed
+  // memory.  (A failure before the dispatch left nothing in flight.)
+  void release() {
+    if (!(dispatched && !finished)) {
+      if (queue) hsa_queue_destroy(queue);
+      if (done.handle) hsa_signal_destroy(done);
+      if (exe.handle) hsa_executable_destroy(exe);
+      if (reader.handle) hsa_code_object_reader_destroy(reader);
+      for (void* q : allocs) hsa_amd_memory_pool_free(q);
+    }
+    queue = nullptr;
+    done.handle = exe.handle = reader.handle = 0;
+    allocs.clear();
+    lock.release();  // after the teardown above
+  }
+};
+
+// one device: queue, dispatch, verify; appends its step records and leaves
+// what it holds in `res` for DeviceRes::release.  `loop_s` > 0 (tests): keep
+// dispatching the kernel for that long, the lock released between dispatches.
+bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std::vector<char>& co, int n,
+                  double timeout_s, std::vector<std::string>* steps, std::string* error, double loop_s,
+                  DeviceRes* res) {
+  const auto t0 = Clock::now();
+  const std::string bdf = agent_bdf(gpu);
+  avk::GateLock& lock = res->lock;
+  lock = avk::GateLock(bdf, avk::GateLock::kShared, 2.0);
+  hsa_code_object_reader_t& reader = res->reader;
+  hsa_executable_t& exe = res->exe;
+  hsa_queue_t*& queue = res->queue;
+  hsa_signal_t& done = res->done;
+  std::vector<void*>& allocs = res->allocs;
+  bool& dispatched = res->dispatched;
+  bool& finished = res->finished;
+  bool ok = false;
   char agent_name[64] = {0};
   try {
     hsa_agent_get_info(gpu, HSA_AGENT_INFO_NAME, agent_name);
@@ -264,18 +297,6 @@ bool check_device(int d, hsa_agent_t gpu, hsa_amd_memory_pool_t pool, const std:
     *error = "device " + std::to_string(d) + ": " + f.msg;
     steps->push_back(fmt_step("vecadd", d, false, secs(t0), ""));
   }
-  // A dispatch that did not finish may still be running (slow, not dead): its
-  // queue, completion signal, code object and buffers all stay until the
-  // process exit, so the kernel never runs from freed code or signals freed
-  // memory.  (A failure before the dispatch left nothing in flight.)
-  if (!(dispatched && !finished)) {
-    if (queue) hsa_queue_destroy(queue);
-    if (done.handle) hsa_signal_destroy(done);
-    if (exe.handle) hsa_executable_destroy(exe);
-    if (reader.handle) hsa_code_object_reader_destroy(reader);
-    for (void* q : allocs) hsa_amd_memory_pool_free(q);
-  }
-  lock.release();  // after the teardown above
   return ok;
 }
 
@@ -310,7 +331,7 @@ int main(int argc, char** argv) {
   std::string error;
   bool ok = true;
   int ngpu = 0;
-  std::vector<avk::GateLock> dev_locks;  // each GPU's gate lock (check_device)
+  std::vector<DeviceRes> dev_res;  // each GPU's queue, executable, buffers and gate lock (check_device)
   double hsa_init_s = -1;
   try {
     const auto th = Clock::now();
@@ -339,14 +360,14 @@ int main(int argc, char** argv) {
     std::vector<std::vector<std::string>> dev_steps(ngpu);
     std::vector<std::string> dev_error(ngpu);
     std::vector<char> dev_ok(ngpu, 0);
-    dev_locks.resize(ngpu);
+    dev_res.resize(ngpu);
     std::vector<std::thread> threads;
     threads.reserve(ngpu);
     for (int d = 0; d < ngpu; ++d)
       threads.emplace_back([&, d] {
         try {  // nothing may leave a thread (std::terminate): an unexpected error fails this device only
           dev_ok[d] = check_device(d, ag.gpus[d], pool, co, elems, timeout_s, &dev_steps[d], &dev_error[d], loop_s,
-                                   &dev_locks[d]);
+                                   &dev_res[d]);
         } catch (const std::exception& e) {
           dev_error[d] = "device " + std::to_string(d) + ": " + e.what();
         } catch (...) {
@@ -392,6 +413,15 @@ int main(int argc, char** argv) {
       const bool wrote = fputs(out.c_str(), rf) >= 0;
       if (fclose(rf) == 0 && wrote) rename(tmp.c_str(), result_file.c_str());
     }
+  }
+  // The report is out: now each device's queue, executable and buffers go,
+  // under its gate lock (DeviceRes::release; ~7.5 ms a device, which the
+  // report no longer waits for).  Devices in parallel, as their checks ran.
+  {
+    std::vector<std::thread> rel;
+    rel.reserve(dev_res.size());
+    for (auto& r : dev_res) rel.emplace_back([&r] { r.release(); });
+    for (auto& t : rel) t.join();
   }
   // the report is the result: the runtime's teardown is left to the exit
   // (AMDGPU_GPU_CHECK_SHUTDOWN=1: hsa_shut_down first - tools/pod_exit_probe.py

@@ -88,12 +88,21 @@ def main() -> int:
     ap.add_argument("--period-ms", type=float, default=1.0)
     ap.add_argument("--kubelet-status-s", type=float, default=0.5)
     ap.add_argument("--out", default="gpurun_out/kfd_churn.json")
+    ap.add_argument("--idle-s", type=float, default=0.0,
+                    help="first sample this long with no bring-up running: the host's own KFD churn")
     a = ap.parse_args()
     sys.argv = [sys.argv[0], "--kubelet-status-s", str(a.kubelet_status_s), "--no-sweep", "--no-pod-workload"]
     args = bench.parse()
     fake = not bench.gpu_available("/")
     workdir = tempfile.mkdtemp(prefix="kfd-churn-")
     sampler = Sampler(a.period_ms / 1000.0).start()
+    idle = None
+    if a.idle_s > 0:
+        t_idle = time.time()
+        time.sleep(a.idle_s)
+        ev = sampler.window(t_idle, 0.0, a.idle_s)
+        idle = {"seconds": a.idle_s, "appeared": sum(1 for e in ev if e[1] == "+"),
+                "exited": sum(1 for e in ev if e[1] == "-"), "events": ev}
     rows = []
     t_print = time.monotonic()
     try:
@@ -116,7 +125,7 @@ def main() -> int:
         sampler.stop()
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
-        json.dump(rows, f, indent=1)
+        json.dump({"idle": idle, "steps": rows} if idle is not None else rows, f, indent=1)
     hsa = [r["pod_hsa_init"] for r in rows if isinstance(r["pod_hsa_init"], (int, float))]
     med = statistics.median(hsa) if hsa else 0.0
 
@@ -137,6 +146,8 @@ def main() -> int:
             [sum(1 for e in r["events"] if e[1] == "-" and e[0] >= 0) for r in rows]) if rows else None,
         "ttr": bench.dist_summary([r["ttr"] for r in rows]),
     }
+    if idle is not None:
+        summary["idle"] = {k: idle[k] for k in ("seconds", "appeared", "exited")}
     print(json.dumps(summary))
     return 0
 
