@@ -299,13 +299,6 @@ class WorkloadSpec(_M):
     # but back-to-back GEMM trials read fp6 / MXFP4 3-9 % lower
     # (profiles/r6_defer), so off by default
     deferGates: bool = False
-    # when the validator processes' HIP runtime may start: once the driver
-    # container reports the module loaded (driverReady), or as soon as the
-    # module is live and no driver upgrade is under way on the node
-    # (moduleLive; a driver container that replaces the module after all
-    # aborts them first).  The kernel steps wait for the driver validation
-    # either way.
-    runtimeStart: Literal["driverReady", "moduleLive"] = "driverReady"
     minMfmaUtilByDtype: dict[str, float] = Field(
         default_factory=lambda: {"fp8": 0.33, "fp4": 0.21, "fp6": 0.20, "mxfp4": 0.20})
     # N >= 2 throughput floors from the xGMI link model (validator/validate.py

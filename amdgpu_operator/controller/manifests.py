@@ -345,8 +345,6 @@ def state_validator(spec: ClusterPolicySpec, ns: str, owner) -> list[dict]:
         wl_args.append("--no-gate-lock")
     if w.deferGates:
         wl_args.append("--defer-gates")
-    if w.runtimeStart == "moduleLive":
-        wl_args.append("--runtime-start-module-live")
     util = {k: v for k, v in w.minMfmaUtilByDtype.items() if w.mfmaRateCheck or k == "bf16"}
     if util:
         wl_args += ["--min-mfma-util-by-dtype", ",".join(f"{k}={v:g}" for k, v in sorted(util.items()))]

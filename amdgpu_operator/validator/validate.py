@@ -472,8 +472,7 @@ def validate_workload(env: NodeEnv, args: list[str] | None = None, timeout: floa
     xgmi_frac = float(_arg_value(args, "--xgmi-read-link-fraction") or 0.0)
     link_frac = float(_arg_value(args, "--min-xgmi-link-fraction") or 0.9)
     args = _drop_flag(args, "--rccl-single-gpu", "--rccl-shared-process", "--rccl-separate-process",
-                      "--require-xgmi-links", "--dmabuf", "--no-mfma-rate", "--no-gate-lock",
-                      "--runtime-start-module-live")
+                      "--require-xgmi-links", "--dmabuf", "--no-mfma-rate", "--no-gate-lock")
     args = _drop_value(args, "--rccl-busbw-link-fraction", "--xgmi-read-link-fraction", "--min-xgmi-link-fraction",
                        "--max-gpu-processes")
     steps = _steps_of(args)
@@ -1198,26 +1197,6 @@ def validate_dra(env: NodeEnv, timeout: float = 600.0, stop=None, image: str | N
 START_GATE_PREFIX = ".start-gate-"
 
 
-def module_live_and_settled(env: NodeEnv) -> bool:
-    """amdgpu is live (N1 probe) and no driver upgrade is under way on the
-    node (its upgrade-state label): a live module the driver container is
-    about to keep, so the validator processes' HIP runtime may start before
-    the driver container says so (``validator.workload.runtimeStart``:
-    moduleLive).  Should the driver container replace the module after all,
-    it aborts the start gates first and waits for those processes to exit
-    (driver/manager.py _release_gated_validators)."""
-    from ..wellknown import ACTIVE, UPGRADE_STATE_LABEL as STATE_LABEL
-    from ..discovery import topology
-
-    if not topology.probe(env.sysfs_root())[0]:
-        return False
-    try:
-        node = env.client.get("v1", "Node", env.node_name)
-    except Exception:  # noqa: BLE001 - no API answer: take the safe path
-        return False
-    return (node["metadata"].get("labels") or {}).get(STATE_LABEL) not in ACTIVE
-
-
 def prespawn_safe(env: NodeEnv, sdk_gate: bool = False) -> bool:
     """May validator processes start before the driver validation?
 
@@ -1230,7 +1209,18 @@ def prespawn_safe(env: NodeEnv, sdk_gate: bool = False) -> bool:
     driver manager aborts pending gates before it unloads a module
     (driver/manager.py), so an early process never holds the device against
     a driver replacement."""
-    return True if not sdk_gate else module_live_and_settled(env)
+    from ..wellknown import ACTIVE, UPGRADE_STATE_LABEL as STATE_LABEL
+    from ..discovery import topology
+
+    if not sdk_gate:
+        return True
+    if not topology.probe(env.sysfs_root())[0]:
+        return False
+    try:
+        node = env.client.get("v1", "Node", env.node_name)
+    except Exception:  # noqa: BLE001 - no API answer: take the safe path
+        return False
+    return (node["metadata"].get("labels") or {}).get(STATE_LABEL) not in ACTIVE
 
 
 def abort_start_gates(env: NodeEnv) -> list[str]:
@@ -1305,20 +1295,11 @@ def validate_gpu(env: NodeEnv, workload_args: list[str], resource: str = RESOURC
 
     _startup_mark("validate_gpu")
 
-    early_init = gate is not None and prespawn and "--runtime-start-module-live" in workload_args
-
     def driver():
         verdict = "abort"
-        init = False
         try:
-            if early_init and module_live_and_settled(env):
-                # runtimeStart moduleLive: the runtime starts on the live module,
-                # before the driver container's verdict (module_live_and_settled)
-                publish("init")
-                init = True
-                _startup_mark("gate_init")
             wait_ready(env, "driver", timeout, stop)
-            if gate and not init:  # the module is loaded: the runtime may start while the N1 check runs
+            if gate:  # the module is loaded: the runtime may start while the N1 check runs (validator_main.cpp)
                 publish("init")
                 _startup_mark("gate_init")
             results["driver"] = validate_driver(env, timeout, stop)

@@ -590,10 +590,6 @@ def test_mfma_rate_check_flags_reach_the_validator(tmp_path):
     # counted dispatches inline by default; deferGates queues them after the kernel steps
     assert "--defer-gates" not in on
     assert "--defer-gates" in args(deep_merge(ref, {"validator": {"workload": {"deferGates": True}}}))
-    # the runtime starts on the driver container's verdict by default, on a live module with moduleLive
-    assert "--runtime-start-module-live" not in on
-    assert "--runtime-start-module-live" in args(deep_merge(ref, {"validator": {"workload": {
-        "runtimeStart": "moduleLive"}}}))
 
     root = str(tmp_path / "h1")
     fakesys.build_node(root, 1)

@@ -116,22 +116,6 @@ def test_unhealthy_gpu_drops_allocatable(cluster_factory):
     assert before >= 1
 
 
-def test_runtime_start_on_a_live_module_validates(cluster_factory):
-    """validator.workload.runtimeStart=moduleLive: with amdgpu already live
-    and no upgrade under way, the start gate says "init" before the driver
-    container's ready file; the node validates as before."""
-    c = cluster_factory([NodeSpec("gpu-1", 2)])
-    c.install_operator(parse_set_flags(REFERENCE_SET_FLAGS + ["validator.workload.runtimeStart=moduleLive"]))
-    c.wait_ready(60, {"gpu-1": 2})
-    from amdgpu_operator.validator import validate as V
-
-    env = c.nodes["gpu-1"].env
-    assert V.read_ready(env, "workload")["ranks"] and V.module_live_and_settled(env)
-    ds = next(d for d in c.client.list("apps/v1", "DaemonSet", c.namespace)
-              if d["metadata"]["name"] == "amd-operator-validator")
-    assert "--runtime-start-module-live" in ds["spec"]["template"]["spec"]["containers"][0]["args"]
-
-
 def test_driver_loss_triggers_revalidation(cluster_factory):
     c = cluster_factory([NodeSpec("gpu-1", 2)])
     c.install_operator(REF)
