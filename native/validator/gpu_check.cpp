@@ -157,10 +157,16 @@ std::string agent_bdf(hsa_agent_t gpu) {
 // What one device's check holds until its teardown (DeviceRes::release),
 // which runs after the report is out: the queue, the executable and the
 // buffers, and the GPU's gate lock (gate_lock.h) taken before the code-object
-// load.  The lock stays held through the teardown (freeing the code object's
-// VRAM starts the driver's wipe of it, and the queue's destruction unmaps it:
-// GPU work a counted window must not see), so a counter gate of the validator
-// on this GPU never counts this pod's upload, kernel or clean-up.
+// load.  The lock covers the upload, the queue creation and the kernel - the
+// pod's GPU work a counted window of the validator must not see - and is let
+// go before the teardown: a queue destruction in a counted window shows as
+// the preemption signature and that attempt is counted again
+// (validator_main.cpp aql_gate), which costs less than every first gate
+// waiting out the teardown (interleaved A/B, 40 pairs: time-to-Ready median
+// 0.2415 against 0.2517 s, the validator process 0.140 against 0.153 s, gate
+// retries 18 against 9 of 200, none past a second attempt:
+// profiles/r6_unlock).  AMDGPU_GPU_CHECK_LOCK_TEARDOWN=1 keeps the lock
+// through the teardown (the A/B's other arm).
 struct DeviceRes {
   avk::GateLock lock;
   hsa_code_object_reader_t reader{0};
@@ -174,7 +180,8 @@ struct DeviceRes {
   // queue, completion signal, code object and buffers all stay until the
   // process exit, so the kernel never runs from freed code or signals freed
   // memory.  (A failure before the dispatch left nothing in flight.)
-  void release() {
+  void release(bool unlock_first) {
+    if (unlock_first) lock.release();
     if (!(dispatched && !finished)) {
       if (queue) hsa_queue_destroy(queue);
       if (done.handle) hsa_signal_destroy(done);
@@ -185,7 +192,7 @@ struct DeviceRes {
     queue = nullptr;
     done.handle = exe.handle = reader.handle = 0;
     allocs.clear();
-    lock.release();  // after the teardown above
+    lock.release();  // (a no-op once let go above)
   }
 };
 
@@ -414,13 +421,15 @@ int main(int argc, char** argv) {
       if (fclose(rf) == 0 && wrote) rename(tmp.c_str(), result_file.c_str());
     }
   }
-  // The report is out: now each device's queue, executable and buffers go,
-  // under its gate lock (DeviceRes::release; ~7.5 ms a device, which the
-  // report no longer waits for).  Devices in parallel, as their checks ran.
+  // The report is out: now each device's queue, executable and buffers go
+  // (DeviceRes::release; ~7.5 ms a device, which the report no longer waits
+  // for), the gate lock let go first.  Devices in parallel, as their checks ran.
   {
     std::vector<std::thread> rel;
     rel.reserve(dev_res.size());
-    for (auto& r : dev_res) rel.emplace_back([&r] { r.release(); });
+    const char* lt = getenv("AMDGPU_GPU_CHECK_LOCK_TEARDOWN");
+    const bool unlock_first = !(lt && lt[0] == '1');
+    for (auto& r : dev_res) rel.emplace_back([&r, unlock_first] { r.release(unlock_first); });
     for (auto& t : rel) t.join();
   }
   // the report is the result: the runtime's teardown is left to the exit

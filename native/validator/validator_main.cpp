@@ -769,9 +769,10 @@ bool aql_gate(const Args& a, const void* A, const void* B, void* C16, int n, int
 // process): each GEMM step measures, checks and times its kernel at once but
 // queues its counter gate here, and finish_deferred_gates counts them in step
 // order once the other kernel steps are done.  The counted window needs the
-// GPU's gate lock exclusively, and the plugin-validation pod holds it shared
+// GPU's gate lock exclusively, and the plugin-validation pod held it shared
 // from its code-object load through its teardown; the first inline gate
-// waits 3-17 ms for it in most bring-ups (profiles/r6_final/head2).
+// waited 3-17 ms for it in most bring-ups (profiles/r6_final/head2; the pod
+// now lets go before its teardown, profiles/r6_unlock).
 // Deferred, that wait mostly goes (the workload chain -6 ms, time-to-Ready
 // median -2.5 ms over 40 interleaved pairs), but the GEMM steps' timed
 // trials then run back to back and the later ones read lower and wider

@@ -33,7 +33,8 @@ def main() -> int:
     ap.add_argument("--pairs", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--arm", action="append", required=True,
-                    help="NAME=SET[,SET...] (Helm --set flags of this arm; empty: the defaults)")
+                    help="NAME=SET[,SET...] (Helm --set flags of this arm, or env:VAR=VALUE for the environment "
+                         "its processes inherit; empty: the defaults)")
     ap.add_argument("--kubelet-status-s", type=float, default=0.5,
                     help="the simulated kubelet's status tick (time-to-Ready does not wait for it)")
     ap.add_argument("--out", default="gpurun_out/ttr_ab.json")
@@ -49,10 +50,23 @@ def main() -> int:
     steps: dict[str, list[dict]] = {n: [] for n, _ in arms}
 
     def one(name, sets):
-        args.extra_set = list(sets)
-        r = bench.one_bring_up(args, 1, None, workdir, fake, "process", False)
+        # "env:NAME=VALUE" entries set the environment the bring-up's processes inherit
+        envs = dict(x[4:].split("=", 1) for x in sets if x.startswith("env:"))
+        args.extra_set = [x for x in sets if not x.startswith("env:")]
+        saved = {k: os.environ.get(k) for k in envs}
+        os.environ.update(envs)
+        try:
+            r = bench.one_bring_up(args, 1, None, workdir, fake, "process", False)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         cp = bench.critical_path(r)
         cp["kfd_holders"] = r.get("kfd_holders")
+        cp["gates"] = [{k: g.get(k) for k in ("name", "gate_attempts", "gate_lock_wait_s", "gate_retried_after")}
+                       for g in (r.get("gates") or [])]
         return cp
 
     for i in range(a.warmup):
@@ -82,7 +96,10 @@ def main() -> int:
         print(json.dumps({"arm": name, "set": sets, "n": len(ttr), "ttr": bench.dist_summary(ttr),
                           "p90_over_median": round(sorted(ttr)[int(0.9 * (len(ttr) - 1))] / med, 3),
                           "above_1.3x_median": len(slow), "slow": bench.slow_summary(slow),
-                          "part_medians": parts}))
+                          "part_medians": parts,
+                          "gate_retries": sum(max(0, (g.get("gate_attempts") or 1) - 1) for c in cps for g in c["gates"]),
+                          "first_gate_lock_wait_median_s": statistics.median(
+                              [c["gates"][0]["gate_lock_wait_s"] or 0.0 for c in cps if c["gates"]] or [0.0])}))
     return 0
 
 
