@@ -195,8 +195,9 @@ def simulated_detail(step: str, argv: list[str], rank: int, world: int) -> dict:
         tf = SIM_GEMM_TFLOPS[step]
         floor = float(arg(floor_flag, "0")) if n >= 4096 else 0.0
         ok = floor <= 0 or tf >= floor
+        gated = "--counter-gate" in argv
         return {"ok": ok, "n": n, "tflops": tf, "min_tflops": floor, "perf_ok": ok,
-                "counter_gate": "pass" if "--counter-gate" in argv else "off"}
+                "counter_gate": "pass" if gated else "off", **({"gate_attempts": 1} if gated else {})}
     if step == "rccl" and world > 1:
         nbytes = 4 * int(arg("--rccl-elems", str(1 << 24)))
         bus = sim_busbw(world, nbytes)

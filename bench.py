@@ -859,9 +859,19 @@ def rates_summary(r: dict) -> dict:
     return out
 
 
+def gate_retry_summary(results: list) -> dict | None:
+    """Every timed bring-up's counted dispatches: how many were counted again
+    (another process's work in the window, gate_policy.h gate_retry_kind)
+    and the most attempts any took."""
+    att = [a for r in results for a in (r.get("gate_attempts") or []) if isinstance(a, int)]
+    if not att:
+        return None
+    return {"gates": len(att), "retried": sum(1 for a in att if a > 1), "max_attempts": max(att)}
+
+
 # the order optional summary fields leave the line if it is still over budget
 # (a safety net: the summaries are sized to fit well below it at N = 8)
-_SHED = ("warmup_time_to_ready_s", "other_mode_time_to_ready_s", "kfd_holders", "pod_workload", "rates",
+_SHED = ("warmup_time_to_ready_s", "other_mode_time_to_ready_s", "gate_retries", "kfd_holders", "pod_workload", "rates",
          "allocatable_visible_s", "collectives", "time_to_ready_s", "slow_steps", "settle")
 
 
@@ -985,6 +995,7 @@ def success_line(args, n_gpus: int, fake_gpu, results: list, warm: list, compare
                         "host_procs_max": max((r.get("settle") or {}).get("kfd_procs") or 0 for r in results)}
         if holders else None,
         "rates": rates_summary(last),
+        "gate_retries": gate_retry_summary(results),
         "operand_mode": args.mode,
         # the harness itself never held a GPU context (no /dev/kfd descriptor)
         "harness_holds_kfd": kfd_held,

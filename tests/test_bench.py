@@ -55,6 +55,8 @@ def test_bench_json_line_contract(tmp_path):
     assert 0 < cfg["allocatable_visible_s"]["mean"] <= cfg["allocatable_visible_s"]["p95"]
     assert cfg["slow_steps"]["count"] == 0  # fewer than 3 steps: nothing is judged slow
     assert cfg["rates"]["counter_gate"]["bf16"] == "pass" and cfg["kfd_holders"]["ready_max"] == 0
+    gr = cfg["gate_retries"]  # every timed bring-up's counted dispatches
+    assert gr["gates"] >= 2 and 0 <= gr["retried"] <= gr["gates"] and gr["max_attempts"] >= 1
     col = cfg["collectives"]
     assert col["ok"] and col["world"] == 1 and col["sizes"] == 15
     assert cfg["pod_workload"]["ok"] and cfg["detail"] == detail
