@@ -349,6 +349,7 @@ class SimCluster:
         self.stop_event = threading.Event()
         self._threads: list[threading.Thread] = []
         self._lock = threading.RLock()
+        self._ds_seq: dict[str, int] = {}  # DaemonSet uid -> the order its ADDED event came in
         self.reconciler: ClusterPolicyReconciler | None = None
         self._operator_proc = None  # process_containers: the operator as its own process (its Deployment's pod)
         # bring-up trace: (perf_counter, what, detail) - pods created/deleted,
@@ -614,7 +615,11 @@ class SimCluster:
                 for r in p["metadata"].get("ownerReferences") or []:
                     if r.get("kind") == "DaemonSet":
                         all_pods.setdefault((p["metadata"].get("namespace"), r.get("uid")), []).append(p)
-            for ds in self.client.list("apps/v1", "DaemonSet"):
+            # in the order the DaemonSets were created, as the real controller's
+            # work queue takes their ADDED events (the list is in name order)
+            seq = {} if os.environ.get("AMDGPU_SIM_DS_NAME_ORDER") == "1" else self._ds_seq  # A/B: name order
+            for ds in sorted(self.client.list("apps/v1", "DaemonSet"),
+                             key=lambda d: (seq.get(d["metadata"]["uid"], float("inf")), d["metadata"]["name"])):
                 ns = ds["metadata"]["namespace"]
                 name = ds["metadata"]["name"]
                 h = self._template_hash(ds)
@@ -671,7 +676,9 @@ class SimCluster:
         def pump(av, kind):
             while not self.stop_event.is_set():
                 try:
-                    for _ in self.client.watch(av, kind, stop=self.stop_event):
+                    for etype, obj in self.client.watch(av, kind, stop=self.stop_event):
+                        if kind == "DaemonSet" and etype == "ADDED":
+                            self._ds_seq.setdefault(obj["metadata"]["uid"], len(self._ds_seq))
                         q.put(kind)
                 except Exception:  # noqa: BLE001
                     self.stop_event.wait(0.1)
