@@ -1278,6 +1278,7 @@ class SimCluster:
             proc_env.update(envs)  # the CDI edits' environment
             if not devices:  # a container of a claim-holding pod that names no claim: no GPU in it
                 proc_env["ROCR_VISIBLE_DEVICES"] = ""
+        self.trace("gpu-pod-launch", run.name)
         res = node.env.launch(argv, proc_env, device=dev, timeout=600)
         self.trace("gpu-pod-reported", run.name)
         try:  # the process's own step times, for the bring-up breakdown
